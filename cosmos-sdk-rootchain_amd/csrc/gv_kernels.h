@@ -1,0 +1,37 @@
+// gv_kernels.h -- internal interface between the C-ABI runtime (gv_runtime.cpp)
+// and the HIP kernels (gv_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GV_GTAB_N 128           // multiples 1..128 of G (signed 8-bit windows)
+#define GV_QTAB_WORDS 192       // per-lane Q table words: 8 entries x (x, y, z-ratio)
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// One device batch of C lanes (C % 256 == 0, n <= C live items).  All pointers
+// are device pointers.  Either dig32 (digest path) or msg_* (message path).
+typedef struct gvk_batch {
+  uint32_t n, C;
+  const uint8_t* pub33;
+  const uint8_t* sig64;
+  const uint8_t* dig32;
+  const uint8_t* msg_blob;
+  const uint64_t* msg_off;
+  const uint32_t* msg_len;
+  const uint32_t* gtab;
+  uint32_t *in_x, *in_pfx, *in_r, *in_s, *in_e;
+  uint32_t *q_xy, *scal, *flags, *qtab;
+  uint64_t* bits;               // C/64 words, bit (i%64) of word i/64
+  hipEvent_t ev[3];             // optional: after unpack/sha, after prep, after ecmult
+} gvk_batch;
+
+hipError_t gvk_gen_gtable(uint32_t* gtab, hipStream_t st);
+hipError_t gvk_verify(const gvk_batch* b, hipStream_t st);
+hipError_t gvk_debug(int op, uint32_t n, const uint32_t* in, uint32_t* out, hipStream_t st);
+
+#ifdef __cplusplus
+}
+#endif

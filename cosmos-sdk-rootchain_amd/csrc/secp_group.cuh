@@ -1,0 +1,96 @@
+// secp_group.cuh -- secp256k1 group law in Jacobian coordinates, one point per
+// lane.  Restates the complete group law of btcec KoblitzCurve.Add /
+// addJacobian / doubleJacobian (btcd v0.20.1-beta btcec/btcec.go): P == Q
+// doubles, P == -Q gives the point at infinity, infinity is the identity.
+// The fast formulas below are incomplete; the exceptional cases are detected
+// (H == 0 mod p) and routed to doubling / infinity, so results are identical.
+//
+// Infinity is carried as a per-lane bool next to the Jacobian point.
+#pragma once
+#include "secp_field.cuh"
+
+namespace gv {
+
+struct gej { fe x, y, z; };
+
+// r = 2a (a finite; secp256k1 has no point of order 2 so the result is finite).
+// dbl-2009-l for a = 0: 2M + 5S.  r may alias a.
+GV_DEV void gej_double(gej& r, const gej& a) {
+  fe A, B, C, D, E, t;
+  fe_sqr(A, a.x);
+  fe_sqr(B, a.y);
+  fe_mul(t, a.y, a.z);
+  fe_dbl(r.z, t);                 // Z3 = 2*Y*Z   (a.y, a.z dead from here)
+  fe_sqr(C, B);
+  fe_add(t, a.x, B);
+  fe_sqr(t, t);
+  fe_sub(t, t, A);
+  fe_sub(t, t, C);
+  fe_dbl(D, t);                   // D = 2((X+B)^2 - A - C)
+  fe_dbl(E, A);
+  fe_add(E, E, A);                // E = 3A
+  fe_sqr(t, E);                   // F = E^2
+  fe_sub(t, t, D);
+  fe_sub(r.x, t, D);              // X3 = F - 2D
+  fe_sub(t, D, r.x);
+  fe_mul(t, E, t);
+  fe_dbl(C, C);
+  fe_dbl(C, C);
+  fe_dbl(C, C);
+  fe_sub(r.y, t, C);              // Y3 = E(D - X3) - 8C
+}
+
+// Shared tail of the mixed additions: given U2, S2 (the affine point scaled to
+// a's Z), finish a + b.  zmul is the factor the output Z gets multiplied with
+// (a.z for a plain mixed add).  Handles the exceptional cases.
+GV_DEV void gej_add_tail(gej& a, bool& inf, const fe& u2, const fe& s2) {
+  fe h, rr;
+  fe_sub(h, u2, a.x);
+  fe_sub(rr, s2, a.y);
+  if (fe_is_zero(h)) {
+    if (fe_is_zero(rr)) {
+      gej_double(a, a);           // a == b
+    } else {
+      inf = true;                 // a == -b
+    }
+    return;
+  }
+  fe h2, h3, v, t;
+  fe_sqr(h2, h);
+  fe_mul(h3, h2, h);
+  fe_mul(v, a.x, h2);             // V = X1*H^2
+  fe_mul(a.z, a.z, h);            // Z3 = Z1*H
+  fe_sqr(t, rr);
+  fe_sub(t, t, h3);
+  fe_sub(t, t, v);
+  fe_sub(a.x, t, v);              // X3 = R^2 - H^3 - 2V
+  fe_sub(t, v, a.x);
+  fe_mul(t, rr, t);
+  fe_mul(h3, a.y, h3);
+  fe_sub(a.y, t, h3);             // Y3 = R(V - X3) - Y1*H^3
+}
+
+// a += (x2, y2) affine (same curve as a).  a finite.
+GV_DEV void gej_add_ge(gej& a, bool& inf, const fe& x2, const fe& y2) {
+  fe z2, u2, s2;
+  fe_sqr(z2, a.z);
+  fe_mul(u2, x2, z2);
+  fe_mul(z2, z2, a.z);
+  fe_mul(s2, y2, z2);
+  gej_add_tail(a, inf, u2, s2);
+}
+
+// a += b where b is the Jacobian point (x2, y2, 1/zinv) -- i.e. an affine point
+// of the real curve added to an accumulator that lives on the isomorphic curve
+// scaled by zinv (effective-affine table trick).  a finite.
+GV_DEV void gej_add_zinv(gej& a, bool& inf, const fe& x2, const fe& y2, const fe& zinv) {
+  fe az, z2, u2, s2;
+  fe_mul(az, a.z, zinv);
+  fe_sqr(z2, az);
+  fe_mul(u2, x2, z2);
+  fe_mul(z2, z2, az);
+  fe_mul(s2, y2, z2);
+  gej_add_tail(a, inf, u2, s2);
+}
+
+}  // namespace gv

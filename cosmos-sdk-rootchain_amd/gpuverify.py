@@ -1,0 +1,270 @@
+"""gpuverify.py -- ctypes binding of libgpuverify.so (include/gpuverify.h).
+
+Host-side mirror of the reference's verification interface for tests and the
+benchmark (the reference's own host language, Go, has no toolchain in this
+image; INTEGRATION.md carries the cgo binding).  Names follow the reference:
+
+  PubKeySecp256k1(pub33).verify_bytes(msg, sig)   tendermint VerifyBytes
+                                                  (x/auth/ante/sigverify.go:210)
+  Verifier.verify_batch_msgs / verify_batch_digests   batched VerifyBytes
+                                                  (crypto/gpuverify in INTEGRATION.md)
+
+This module never falls back to a CPU implementation: if libgpuverify.so is
+missing or no HIP device is present it raises GpuVerifyError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libgpuverify.so")
+
+GV_OK, GV_EINVAL, GV_ENODEV, GV_EHIP, GV_ENOMEM, GV_EFAULT = 0, -1, -2, -3, -4, -5
+
+# every symbol include/gpuverify.h declares
+EXPORTED_SYMBOLS = (
+    "gv_open", "gv_close", "gv_num_devices", "gv_verify_msgs", "gv_verify_digests",
+    "gv_verify_digests_bits", "gv_verify_msgs_bits", "gv_dev_verify_digests", "gv_dev_verify_msgs",
+    "gv_set_option", "gv_last_stage_ms", "gv_strerror", "gv_debug_op", "gv_dev_alloc", "gv_dev_free",
+    "gv_dev_copy", "gv_dev_sync", "gv_stage_stats",
+)
+
+
+class GpuVerifyError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        msg = _strerror(code) if _lib is not None else str(code)
+        super().__init__(f"{what}: {msg} ({code})" if what else f"{msg} ({code})")
+
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def load(path: str = LIB_PATH):
+    """Load libgpuverify.so and declare argtypes.  Does not touch the GPU."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise GpuVerifyError(GV_ENODEV, f"{path} not built (run make -C {HERE})")
+    L = ctypes.CDLL(path)
+    vp, sz, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    L.gv_open.argtypes = [ctypes.POINTER(i32), i32, ctypes.POINTER(vp)]
+    L.gv_open.restype = i32
+    L.gv_close.argtypes = [vp]
+    L.gv_close.restype = None
+    L.gv_num_devices.argtypes = [vp]
+    L.gv_num_devices.restype = i32
+    L.gv_verify_msgs.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp]
+    L.gv_verify_msgs.restype = i32
+    L.gv_verify_digests.argtypes = [vp, sz, vp, vp, vp, vp]
+    L.gv_verify_digests.restype = i32
+    L.gv_verify_digests_bits.argtypes = [vp, sz, vp, vp, vp, vp]
+    L.gv_verify_digests_bits.restype = i32
+    L.gv_verify_msgs_bits.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp]
+    L.gv_verify_msgs_bits.restype = i32
+    L.gv_dev_verify_digests.argtypes = [vp, i32, sz, vp, vp, vp, vp, vp]
+    L.gv_dev_verify_digests.restype = i32
+    L.gv_dev_verify_msgs.argtypes = [vp, i32, sz, vp, vp, vp, vp, vp, vp, vp]
+    L.gv_dev_verify_msgs.restype = i32
+    L.gv_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_longlong]
+    L.gv_set_option.restype = i32
+    L.gv_last_stage_ms.argtypes = [vp, i32] + [ctypes.POINTER(ctypes.c_float)] * 3
+    L.gv_last_stage_ms.restype = i32
+    L.gv_strerror.argtypes = [i32]
+    L.gv_strerror.restype = ctypes.c_char_p
+    L.gv_debug_op.argtypes = [vp, i32, i32, sz, vp, vp]
+    L.gv_debug_op.restype = i32
+    L.gv_dev_alloc.argtypes = [vp, i32, sz, ctypes.POINTER(vp)]
+    L.gv_dev_alloc.restype = i32
+    L.gv_dev_free.argtypes = [vp, i32, vp]
+    L.gv_dev_free.restype = i32
+    L.gv_dev_copy.argtypes = [vp, i32, vp, vp, sz, i32]
+    L.gv_dev_copy.restype = i32
+    L.gv_dev_sync.argtypes = [vp, i32]
+    L.gv_dev_sync.restype = i32
+    L.gv_stage_stats.argtypes = [vp, i32, ctypes.POINTER(i32)] + [ctypes.POINTER(ctypes.c_double)] * 3
+    L.gv_stage_stats.restype = i32
+    _lib = L
+    return L
+
+
+def _strerror(code: int) -> str:
+    return _lib.gv_strerror(code).decode()
+
+
+def _ptr(a: np.ndarray):
+    assert a.flags["C_CONTIGUOUS"]
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _check(rc: int, what: str):
+    if rc != GV_OK:
+        raise GpuVerifyError(rc, what)
+
+
+def pack_msgs(msgs):
+    """list[bytes] -> (blob u8, off u64, len u32)"""
+    lens = np.fromiter((len(m) for m in msgs), dtype=np.uint32, count=len(msgs))
+    off = np.zeros(len(msgs), dtype=np.uint64)
+    if len(msgs) > 1:
+        off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    blob = np.frombuffer(b"".join(msgs) or b"\0", dtype=np.uint8).copy()
+    return blob, off, lens
+
+
+class Verifier:
+    """Batched VerifyBytes on one or more MI355X devices (gv_ctx)."""
+
+    def __init__(self, devices=None):
+        L = load()
+        ctx = ctypes.c_void_p()
+        if devices:
+            ids = (ctypes.c_int * len(devices))(*devices)
+            rc = L.gv_open(ids, len(devices), ctypes.byref(ctx))
+        else:
+            rc = L.gv_open(None, 0, ctypes.byref(ctx))
+        _check(rc, "gv_open")
+        self._ctx = ctx
+        self._L = L
+
+    def close(self):
+        if self._ctx:
+            self._L.gv_close(self._ctx)
+            self._ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def num_devices(self) -> int:
+        return self._L.gv_num_devices(self._ctx)
+
+    def set_option(self, key: str, val: int):
+        _check(self._L.gv_set_option(self._ctx, key.encode(), int(val)), f"gv_set_option({key})")
+
+    def verify_batch_digests(self, pub33: np.ndarray, sig64: np.ndarray, dig32: np.ndarray) -> np.ndarray:
+        pub33, sig64, dig32 = (np.ascontiguousarray(a, dtype=np.uint8) for a in (pub33, sig64, dig32))
+        n = pub33.shape[0]
+        assert pub33.shape == (n, 33) and sig64.shape == (n, 64) and dig32.shape == (n, 32)
+        out = np.zeros(n, dtype=np.uint8)
+        if n:
+            _check(self._L.gv_verify_digests(self._ctx, n, _ptr(pub33), _ptr(sig64), _ptr(dig32), _ptr(out)),
+                   "gv_verify_digests")
+        return out
+
+    def verify_batch_digests_bits(self, pub33, sig64, dig32) -> np.ndarray:
+        n = pub33.shape[0]
+        out = np.zeros((n + 63) // 64, dtype=np.uint64)
+        if n:
+            _check(self._L.gv_verify_digests_bits(self._ctx, n, _ptr(pub33), _ptr(sig64), _ptr(dig32),
+                                                  _ptr(out)), "gv_verify_digests_bits")
+        return out
+
+    def verify_batch_msgs(self, pub33: np.ndarray, sig64: np.ndarray, msgs) -> np.ndarray:
+        """msgs: list[bytes] or a (blob, off, len) triple."""
+        pub33, sig64 = (np.ascontiguousarray(a, dtype=np.uint8) for a in (pub33, sig64))
+        blob, off, ln = pack_msgs(msgs) if isinstance(msgs, (list, tuple)) and (
+            len(msgs) == 0 or isinstance(msgs[0], (bytes, bytearray))) else msgs
+        n = pub33.shape[0]
+        out = np.zeros(n, dtype=np.uint8)
+        if n:
+            _check(self._L.gv_verify_msgs(self._ctx, n, _ptr(pub33), _ptr(sig64), _ptr(blob), _ptr(off),
+                                          _ptr(ln), _ptr(out)), "gv_verify_msgs")
+        return out
+
+    def dev_verify_digests(self, slot: int, n: int, d_pub, d_sig, d_dig, d_bits, stream=None):
+        """Device-resident path: d_* are device addresses (ints); stream a hipStream_t int."""
+        _check(self._L.gv_dev_verify_digests(self._ctx, slot, n, ctypes.c_void_p(d_pub), ctypes.c_void_p(d_sig),
+                                             ctypes.c_void_p(d_dig), ctypes.c_void_p(d_bits),
+                                             ctypes.c_void_p(stream or 0)), "gv_dev_verify_digests")
+
+    def dev_verify_msgs(self, slot: int, n: int, d_pub, d_sig, d_blob, d_off, d_len, d_bits, stream=None):
+        _check(self._L.gv_dev_verify_msgs(self._ctx, slot, n, ctypes.c_void_p(d_pub), ctypes.c_void_p(d_sig),
+                                          ctypes.c_void_p(d_blob), ctypes.c_void_p(d_off), ctypes.c_void_p(d_len),
+                                          ctypes.c_void_p(d_bits), ctypes.c_void_p(stream or 0)),
+               "gv_dev_verify_msgs")
+
+    def last_stage_ms(self, slot: int = 0):
+        a, b, c = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
+        _check(self._L.gv_last_stage_ms(self._ctx, slot, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+               "gv_last_stage_ms")
+        return a.value, b.value, c.value
+
+    # ---- device memory helpers (no torch/HIP runtime needed on the caller side)
+    def dev_alloc(self, nbytes: int, slot: int = 0) -> int:
+        p = ctypes.c_void_p()
+        _check(self._L.gv_dev_alloc(self._ctx, slot, nbytes, ctypes.byref(p)), "gv_dev_alloc")
+        return p.value
+
+    def dev_free(self, ptr: int, slot: int = 0):
+        _check(self._L.gv_dev_free(self._ctx, slot, ctypes.c_void_p(ptr)), "gv_dev_free")
+
+    def dev_upload(self, ptr: int, arr: np.ndarray, slot: int = 0):
+        arr = np.ascontiguousarray(arr)
+        _check(self._L.gv_dev_copy(self._ctx, slot, ctypes.c_void_p(ptr), _ptr(arr), arr.nbytes, 1), "gv_dev_copy")
+
+    def dev_download(self, arr: np.ndarray, ptr: int, slot: int = 0):
+        assert arr.flags["C_CONTIGUOUS"]
+        _check(self._L.gv_dev_copy(self._ctx, slot, _ptr(arr), ctypes.c_void_p(ptr), arr.nbytes, 2), "gv_dev_copy")
+
+    def dev_sync(self, slot: int = 0):
+        _check(self._L.gv_dev_sync(self._ctx, slot), "gv_dev_sync")
+
+    def stage_stats(self, slot: int = 0):
+        c = ctypes.c_int()
+        a, b, d = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        _check(self._L.gv_stage_stats(self._ctx, slot, ctypes.byref(c), ctypes.byref(a), ctypes.byref(b),
+                                      ctypes.byref(d)), "gv_stage_stats")
+        return c.value, a.value, b.value, d.value
+
+    def debug_op(self, op: int, words: np.ndarray, slot: int = 0) -> np.ndarray:
+        words = np.ascontiguousarray(words, dtype=np.uint32)
+        n = words.shape[0]
+        assert words.shape == (n, 16)
+        out = np.zeros((n, 16), dtype=np.uint32)
+        _check(self._L.gv_debug_op(self._ctx, slot, op, n, _ptr(words), _ptr(out)), "gv_debug_op")
+        return out
+
+
+class PubKeySecp256k1:
+    """Mirror of tendermint crypto/secp256k1.PubKeySecp256k1 ([33]byte) whose
+    VerifyBytes runs on the GPU (batch of one).  Same argument meaning and
+    result: bool, never an exception for a cryptographic rejection."""
+
+    _shared = None
+
+    def __init__(self, pub33: bytes):
+        assert len(pub33) == 33
+        self.key = bytes(pub33)
+
+    @classmethod
+    def _verifier(cls):
+        if cls._shared is None:
+            cls._shared = Verifier()
+        return cls._shared
+
+    def verify_bytes(self, msg: bytes, sig: bytes) -> bool:
+        if len(sig) != 64:          # VerifyBytes' first check, decided on the host
+            return False
+        pub = np.frombuffer(self.key, dtype=np.uint8).reshape(1, 33)
+        s = np.frombuffer(bytes(sig), dtype=np.uint8).reshape(1, 64)
+        return bool(self._verifier().verify_batch_msgs(pub, s, [bytes(msg)])[0])

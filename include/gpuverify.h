@@ -1,0 +1,125 @@
+/*
+ * gpuverify.h -- C ABI of libgpuverify.so, the MI355X (gfx950) batched
+ * secp256k1 transaction-signature verifier.
+ *
+ * Drop-in boundary.  Every entry point below replaces, for a
+ * whole batch at once, the reference's per-signature call
+ *
+ *     pubKey.VerifyBytes(signBytes, sig)            x/auth/ante/sigverify.go:210
+ *
+ * i.e. tendermint v0.33.4 crypto/secp256k1 PubKeySecp256k1.VerifyBytes
+ * (secp256k1_nocgo.go), reached through SigVerificationDecorator.AnteHandle
+ * (x/auth/ante/sigverify.go:170-216) and, for multisig leaves, through
+ * multisig.PubKeyMultisigThreshold.VerifyBytes (the type switch at
+ * x/auth/ante/sigverify.go:303-321 names both key types).  out_ok[i] is
+ * exactly VerifyBytes(msg_i, sig_i) for pubkey pub33_i: 1 = true, 0 = false.
+ * Cryptographic rejection is never an error code.
+ *
+ * Plain pointers and sizes only (cgo / ctypes / JNI friendly).  The caller owns
+ * every buffer; the library copies inputs into its own device memory and keeps
+ * no caller pointer after a call returns.  Calls are synchronous and a gv_ctx
+ * may be shared by concurrent threads (calls on one device serialise).
+ * INTEGRATION.md shows the Go (cgo) binding a maintainer adds as
+ * crypto/gpuverify and the BatchSigVerificationDecorator built on it.
+ */
+#ifndef GPUVERIFY_H
+#define GPUVERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Return codes: 0 = OK, negative = infrastructure error.  On any nonzero
+ * return the caller must not use out_ok and should re-verify on the CPU
+ * (fail-closed; SURVEY.md §5 "Failure detection"). */
+#define GV_OK        0
+#define GV_EINVAL   -1   /* bad argument (null pointer, misaligned device ptr, ...) */
+#define GV_ENODEV   -2   /* no usable HIP device / bad device id */
+#define GV_EHIP     -3   /* HIP runtime or kernel error */
+#define GV_ENOMEM   -4   /* device or host allocation failed */
+#define GV_EFAULT   -5   /* injected fault (option "fault_inject") */
+
+typedef struct gv_ctx gv_ctx;
+
+/* Open a context on dev_ids[0..n_dev) (HIP ordinals); n_dev == 0 -> every
+ * visible device.  Builds the per-device G table.  Replaces nothing in the
+ * reference (which has no device state); the Go shim calls it once at app
+ * construction (simapp/app.go:335-339 wiring site). */
+int gv_open(const int* dev_ids, int n_dev, gv_ctx** out);
+void gv_close(gv_ctx* ctx);
+int gv_num_devices(const gv_ctx* ctx);
+
+/* Batch VerifyBytes over messages.  Item i: pubkey pub33 + 33*i (SEC1
+ * compressed, as stored by secp256k1.PubKeySecp256k1 [33]byte), signature
+ * sig64 + 64*i (R||S big-endian, tendermint's 64-byte format), message
+ * msg_blob[msg_off[i] .. msg_off[i] + msg_len[i]) (StdSignBytes,
+ * x/auth/types/stdtx.go:248-259).  Signatures whose length is not 64 are
+ * decided (false) by the caller before the call, exactly like VerifyBytes'
+ * first check.  Replaces the loop body at x/auth/ante/sigverify.go:194-213. */
+int gv_verify_msgs(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64,
+                   const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len,
+                   uint8_t* out_ok);
+
+/* Same with the messages already hashed: dig32 + 32*i = SHA256(msg_i)
+ * (tendermint crypto.Sha256).  This is VerifyBytes minus its hashing step
+ * (btcec Signature.Verify(hash, pub) preceded by the tendermint checks). */
+int gv_verify_digests(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64,
+                      const uint8_t* dig32, uint8_t* out_ok);
+
+/* Packed-bitmap variants: bit (i % 64) of out_bits[i / 64] is item i's
+ * verdict; ceil(n/64) words are written (unused high bits 0). */
+int gv_verify_digests_bits(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64,
+                           const uint8_t* dig32, uint64_t* out_bits);
+int gv_verify_msgs_bits(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64,
+                        const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len,
+                        uint64_t* out_bits);
+
+/* Device-resident entry points for callers whose batch already lives in HBM
+ * (benchmarks, a node that stages blocks on the GPU).  dev_slot indexes the
+ * context's devices; d_* are device pointers on that device (4-byte aligned);
+ * d_bits receives ceil(n/64) words; stream is a hipStream_t (NULL = the
+ * context's stream).  Asynchronous: results are ready when the stream is. */
+int gv_dev_verify_digests(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub33,
+                          const void* d_sig64, const void* d_dig32, void* d_bits, void* stream);
+int gv_dev_verify_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub33,
+                       const void* d_sig64, const void* d_msg_blob, const void* d_msg_off,
+                       const void* d_msg_len, void* d_bits, void* stream);
+
+/* Device memory and stream helpers for callers of the gv_dev_* entry points
+ * that have no HIP runtime of their own (bench.py, tests).  kind: 1 = host to
+ * device, 2 = device to host, 3 = device to device; copies are ordered on the
+ * context stream of dev_slot and synchronous. */
+int gv_dev_alloc(gv_ctx* ctx, int dev_slot, size_t bytes, void** d_ptr);
+int gv_dev_free(gv_ctx* ctx, int dev_slot, void* d_ptr);
+int gv_dev_copy(gv_ctx* ctx, int dev_slot, void* dst, const void* src, size_t bytes, int kind);
+int gv_dev_sync(gv_ctx* ctx, int dev_slot);
+
+/* Options: "max_batch" (lanes per device launch, default 1<<20),
+ * "time_kernels" (0/1: record HIP events around each kernel stage),
+ * "fault_inject" (0/1: every verify call fails with GV_EFAULT; test hook). */
+int gv_set_option(gv_ctx* ctx, const char* key, long long val);
+
+/* With "time_kernels" on: milliseconds of the last launch's stages on dev_slot
+ * (unpack+sha, prep, ecmult), measured with HIP events on the launch stream. */
+int gv_last_stage_ms(gv_ctx* ctx, int dev_slot, float* unpack_ms, float* prep_ms, float* ecmult_ms);
+
+/* With "time_kernels" on: average stage milliseconds over every launch on
+ * dev_slot since the previous call (at most the last 256 launches); *count
+ * receives the number of launches averaged.  Synchronises dev_slot. */
+int gv_stage_stats(gv_ctx* ctx, int dev_slot, int* count, double* unpack_ms, double* prep_ms,
+                   double* ecmult_ms);
+
+const char* gv_strerror(int code);
+
+/* Test hook: run one arithmetic building block per item on dev_slot
+ * (op codes in gv_kernels.hip k_debug; in/out = n x 16 little-endian u32
+ * host arrays).  Used by the GPU unit tests only. */
+int gv_debug_op(gv_ctx* ctx, int dev_slot, int op, size_t n, const uint32_t* in, uint32_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPUVERIFY_H */

@@ -1,0 +1,270 @@
+"""GPU parity tests: libgpuverify (HIP, gfx950) vs the oracle, through the C-ABI.
+
+Bit-exact bar: every accept/reject verdict must equal the oracle's
+(oracle/secp256k1_oracle.c, pinned in tests/test_oracle.py), which restates
+tendermint VerifyBytes / btcec / crypto/ecdsa (x/auth/ante/sigverify.go:210).
+"""
+import random
+
+import numpy as np
+import pytest
+
+import gpuverify as gvm
+from golden_io import load_digest_vectors, load_msg_vectors
+from oracle import oracle as O
+from oracle import secp_ref as R
+
+pytestmark = pytest.mark.gpu
+
+P, N = R.P, R.N
+BETA = R.BETA
+
+
+@pytest.fixture(scope="module")
+def ver():
+    v = gvm.Verifier([0])
+    yield v
+    v.close()
+
+
+def to_words(a: int, b: int):
+    return [(a >> (32 * i)) & 0xFFFFFFFF for i in range(8)] + [(b >> (32 * i)) & 0xFFFFFFFF for i in range(8)]
+
+
+def from_words(ws, lo=0, n=8):
+    return sum(int(ws[lo + i]) << (32 * i) for i in range(n))
+
+
+EDGE = [0, 1, 2, 977, 2**32, 2**32 + 977, P - 1, P, P + 1, 2**256 - 1, 2**256 - 2**32 - 978,
+        2**255, 2**224 - 1, N, N - 1, BETA, (1 << 128) - 1]
+
+
+def operand_pairs(rng, count):
+    vals = EDGE + [rng.randrange(2**256) for _ in range(count)]
+    pairs = [(a, b) for a in EDGE for b in EDGE]
+    pairs += [(rng.choice(vals), rng.choice(vals)) for _ in range(count)]
+    return pairs
+
+
+def run_op(ver, op, pairs):
+    w = np.array([to_words(a, b) for a, b in pairs], dtype=np.uint32)
+    return ver.debug_op(op, w)
+
+
+@pytest.mark.parametrize("op,fn", [
+    (0, lambda a, b: a * b % P),
+    (1, lambda a, b: a * a % P),
+    (2, lambda a, b: (a + b) % P),
+    (3, lambda a, b: (a - b) % P),
+    (6, lambda a, b: a % P),
+])
+def test_field_ops(ver, op, fn):
+    rng = random.Random(op)
+    pairs = operand_pairs(rng, 3000)
+    out = run_op(ver, op, pairs)
+    for (a, b), o in zip(pairs, out):
+        assert from_words(o) == fn(a, b), (op, hex(a), hex(b))
+
+
+def test_mul512(ver):
+    rng = random.Random(7)
+    pairs = operand_pairs(rng, 3000)
+    out = run_op(ver, 7, pairs)
+    for (a, b), o in zip(pairs, out):
+        assert from_words(o, 0, 16) == a * b, (hex(a), hex(b))
+
+
+def test_field_inv_and_sqrt(ver):
+    rng = random.Random(11)
+    xs = [1, 2, P - 1, 7, BETA] + [rng.randrange(1, P) for _ in range(500)]
+    out = run_op(ver, 4, [(x, 0) for x in xs])
+    for x, o in zip(xs, out):
+        assert from_words(o) == pow(x, P - 2, P)
+    out = run_op(ver, 5, [(x, 0) for x in xs])
+    for x, o in zip(xs, out):
+        assert from_words(o) == pow(x, (P + 1) // 4, P)
+
+
+def test_scalar_montmul(ver):
+    rng = random.Random(13)
+    Rinv = pow(2**256, -1, N)
+    pairs = [(a, b) for a in (0, 1, N - 1, 2) for b in (0, 1, N - 1, 3)]
+    pairs += [(rng.randrange(N), rng.randrange(N)) for _ in range(3000)]
+    out = run_op(ver, 8, pairs)
+    for (a, b), o in zip(pairs, out):
+        assert from_words(o) == a * b * Rinv % N
+
+
+def test_glv_split(ver):
+    rng = random.Random(17)
+    ks = [0, 1, 2, N - 1, N - 2, N // 2, R.LAMBDA, 2**128, 2**128 - 1] + [rng.randrange(N) for _ in range(4000)]
+    out = run_op(ver, 9, [(k, 0) for k in ks])
+    for k, o in zip(ks, out):
+        k1 = from_words(o, 0, 4) * (-1 if o[8] else 1)
+        k2 = from_words(o, 4, 4) * (-1 if o[9] else 1)
+        assert (k1 + k2 * R.LAMBDA - k) % N == 0, hex(k)
+        assert abs(k1) < 2**128 and abs(k2) < 2**128
+
+
+def test_batch_inversion_across_wave(ver):
+    rng = random.Random(19)
+    xs = [rng.randrange(1, N) for _ in range(1000)] + [1, N - 1]
+    out = run_op(ver, 10, [(x, 0) for x in xs])
+    for x, o in zip(xs, out):
+        assert from_words(o) == pow(x, N - 2, N)
+
+
+def test_point_double(ver):
+    pts = [R.point_mul(k, R.G) for k in (1, 2, 3, 12345, N - 1, R.LAMBDA)]
+    out = run_op(ver, 11, [(p[0], p[1]) for p in pts])
+    for p, o in zip(pts, out):
+        q = R.point_add(p, p)
+        assert from_words(o, 0) == q[0] and from_words(o, 8) == q[1]
+
+
+# ------------------------------------------------------------ full verification
+def test_golden_digest_vectors(ver):
+    pub, sig, dig, ok, cats = load_digest_vectors()
+    got = ver.verify_batch_digests(pub, sig, dig)
+    bad = [(i, cats[i], int(ok[i])) for i in range(len(ok)) if got[i] != ok[i]]
+    assert not bad, bad[:20]
+
+
+def test_golden_message_vectors(ver):
+    pub, sig, msgs, ok, cats = load_msg_vectors()
+    got = ver.verify_batch_msgs(pub, sig, msgs)
+    bad = [(i, cats[i], int(ok[i])) for i in range(len(ok)) if got[i] != ok[i]]
+    assert not bad, bad[:20]
+
+
+def make_random_batch(n, seed, adversarial=0.25, nkeys=257):
+    rng = np.random.default_rng(seed)
+    privs = rng.integers(0, 256, size=(nkeys, 32), dtype=np.uint8)
+    privs[:, 0] &= 0x7F
+    privs[:, 31] |= 1
+    pubs = O.pubkey_batch(privs, threads=8)
+    kidx = np.arange(n) % nkeys
+    dig = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    sig = O.sign_batch(np.ascontiguousarray(privs[kidx]), dig, threads=8)
+    pub = np.ascontiguousarray(pubs[kidx])
+    m = rng.random(n) < adversarial
+    kinds = rng.integers(0, 6, size=n)
+    for i in np.nonzero(m)[0]:
+        k = kinds[i]
+        if k == 0:        # high-S
+            s = int.from_bytes(bytes(sig[i, 32:]), "big")
+            sig[i, 32:] = np.frombuffer((N - s).to_bytes(32, "big"), np.uint8)
+        elif k == 1:      # r out of range
+            sig[i, :32] = np.frombuffer((N + int(rng.integers(0, 1000))).to_bytes(32, "big"), np.uint8)
+        elif k == 2:      # s zero / huge
+            sig[i, 32:] = 0 if rng.random() < 0.5 else 0xFF
+        elif k == 3:      # off-curve / random x
+            pub[i, 1:] = rng.integers(0, 256, size=32, dtype=np.uint8)
+        elif k == 4:      # malformed prefix
+            pub[i, 0] = rng.choice([0, 1, 4, 5, 6, 7, 0xFF])
+        else:             # wrong message
+            dig[i, int(rng.integers(0, 32))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    return pub, sig, dig
+
+
+def test_random_adversarial_batch_vs_oracle(ver):
+    pub, sig, dig = make_random_batch(20000, seed=0xC3)
+    want = O.verify_digests(pub, sig, dig, threads=16)
+    got = ver.verify_batch_digests(pub, sig, dig)
+    assert 0.6 < want.mean() < 0.9
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, bad[:20]
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 256, 257, 1000])
+def test_ragged_sizes_and_bitmap(ver, n):
+    pub, sig, dig = make_random_batch(n, seed=n, adversarial=0.3, nkeys=7)
+    want = O.verify_digests(pub, sig, dig, threads=8)
+    assert np.array_equal(ver.verify_batch_digests(pub, sig, dig), want)
+    bits = ver.verify_batch_digests_bits(pub, sig, dig)
+    unpacked = np.array([(int(bits[i // 64]) >> (i % 64)) & 1 for i in range(n)], dtype=np.uint8)
+    assert np.array_equal(unpacked, want)
+    tail = int(bits[-1]) >> (n % 64) if n % 64 else 0
+    assert tail == 0
+
+
+def test_empty_batch(ver):
+    z = np.zeros((0, 33), np.uint8)
+    assert ver.verify_batch_digests(z, np.zeros((0, 64), np.uint8), np.zeros((0, 32), np.uint8)).size == 0
+
+
+def test_chunked_batches(ver):
+    pub, sig, dig = make_random_batch(3000, seed=5, adversarial=0.2, nkeys=11)
+    want = O.verify_digests(pub, sig, dig, threads=8)
+    ver.set_option("max_batch", 512)
+    try:
+        assert np.array_equal(ver.verify_batch_digests(pub, sig, dig), want)
+    finally:
+        ver.set_option("max_batch", 1 << 20)
+
+
+def test_message_path_random(ver):
+    rng = random.Random(23)
+    msgs, pubs, sigs, want = [], [], [], []
+    for i in range(600):
+        d = rng.randrange(1, N)
+        msg = rng.randbytes(rng.randrange(0, 700))
+        sig = bytearray(R.sign(d, msg)) if i < 40 else None
+        if sig is None:
+            priv = d.to_bytes(32, "big")
+            sig = bytearray(O.sign(priv, O.sha256(msg)))
+        if i % 5 == 0:
+            msg = msg + b"!"
+        pub = O.pubkey(d.to_bytes(32, "big"))
+        msgs.append(msg)
+        pubs.append(np.frombuffer(pub, np.uint8))
+        sigs.append(np.frombuffer(bytes(sig), np.uint8))
+        want.append(O.verify_bytes(pub, msg, bytes(sig)))
+    got = ver.verify_batch_msgs(np.array(pubs), np.array(sigs), msgs)
+    assert np.array_equal(got, np.array(want, dtype=np.uint8))
+
+
+def test_fault_injection_fails_closed(ver):
+    pub, sig, dig = make_random_batch(8, seed=1, nkeys=2)
+    ver.set_option("fault_inject", 1)
+    try:
+        with pytest.raises(gvm.GpuVerifyError) as ei:
+            ver.verify_batch_digests(pub, sig, dig)
+        assert ei.value.code == gvm.GV_EFAULT
+    finally:
+        ver.set_option("fault_inject", 0)
+
+
+def test_device_resident_path(ver):
+    pub, sig, dig = make_random_batch(5000, seed=9, adversarial=0.25, nkeys=31)
+    want = O.verify_digests(pub, sig, dig, threads=16)
+    n = 5000
+    bufs = {k: ver.dev_alloc(a.nbytes) for k, a in (("pub", pub), ("sig", sig), ("dig", dig))}
+    d_bits = ver.dev_alloc(((n + 63) // 64) * 8)
+    try:
+        ver.dev_upload(bufs["pub"], pub)
+        ver.dev_upload(bufs["sig"], sig)
+        ver.dev_upload(bufs["dig"], dig)
+        ver.set_option("time_kernels", 1)
+        for _ in range(3):
+            ver.dev_verify_digests(0, n, bufs["pub"], bufs["sig"], bufs["dig"], d_bits)
+        cnt, a, b, c = ver.stage_stats()
+        assert cnt == 3 and c > 0 and b > 0
+        bits = np.zeros((n + 63) // 64, dtype=np.uint64)
+        ver.dev_download(bits, d_bits)
+    finally:
+        ver.set_option("time_kernels", 0)
+        for p in list(bufs.values()) + [d_bits]:
+            ver.dev_free(p)
+    got = np.array([(int(bits[i // 64]) >> (i % 64)) & 1 for i in range(n)], dtype=np.uint8)
+    assert np.array_equal(got, want)
+
+
+def test_pubkey_class_mirror():
+    d = 0xC0FFEE
+    msg = b'{"account_number":"1"}'
+    sig = R.sign(d, msg)
+    pk = gvm.PubKeySecp256k1(R.pubkey(d))
+    assert pk.verify_bytes(msg, sig) is True
+    assert pk.verify_bytes(msg + b" ", sig) is False
+    assert pk.verify_bytes(msg, sig[:63]) is False

@@ -1,0 +1,234 @@
+/*
+ * gv_workload.c -- synthetic signed-transaction workload generator for
+ * bench.py.  NOT the oracle: signatures are made
+ * with OpenSSL 3 libcrypto (ECDSA_do_sign on NID_secp256k1, then tendermint's
+ * low-S normalisation), keys follow tendermint GenPrivKeySecp256k1
+ * ((SHA256(secret) mod (n-1)) + 1).  Expected verdicts are known by
+ * construction: untouched items are valid, mutated (adversarial) items are
+ * invalid.
+ *
+ * C1 sign bytes: StdSignBytes of a simapp bank MsgSend
+ * (x/auth/types/stdtx.go:292-312, x/bank/types/msgs.go:43-45) with
+ * from = addr_i, to = addr_{i+1}, amount 10foocoin, fee 0stake / gas 1000000,
+ * memo "", chain-id "gv-bench", account number i, sequence 0.
+ */
+#include <openssl/bn.h>
+#include <openssl/ec.h>
+#include <openssl/ecdsa.h>
+#include <openssl/obj_mac.h>
+#include <openssl/sha.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+static uint64_t splitmix(uint64_t* s) {
+  uint64_t z = (*s += 0x9E3779B97F4A7C15ULL);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+static const char* N_HEX = "FFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141";
+
+/* ----------------------------------------------------------- RIPEMD-160 */
+static uint32_t rol(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+static const int RL[80] = {0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,7,4,13,1,10,6,15,3,12,0,9,5,2,14,11,8,
+  3,10,14,4,9,15,8,1,2,7,0,6,13,11,5,12,1,9,11,10,0,8,12,4,13,3,7,15,14,5,6,2,4,0,5,9,7,12,2,10,14,1,3,8,11,6,15,13};
+static const int RR[80] = {5,14,7,0,9,2,11,4,13,6,15,8,1,10,3,12,6,11,3,7,0,13,5,10,14,15,8,12,4,9,1,2,
+  15,5,1,3,7,14,6,9,11,8,12,2,10,0,4,13,8,6,4,1,3,11,15,0,5,12,2,13,9,7,10,14,12,15,10,4,1,5,8,7,6,2,13,14,0,3,9,11};
+static const int SL[80] = {11,14,15,12,5,8,7,9,11,13,14,15,6,7,9,8,7,6,8,13,11,9,7,15,7,12,15,9,11,7,13,12,
+  11,13,6,7,14,9,13,15,14,8,13,6,5,12,7,5,11,12,14,15,14,15,9,8,9,14,5,6,8,6,5,12,9,15,5,11,6,8,13,12,5,12,13,14,11,8,5,6};
+static const int SR[80] = {8,9,9,11,13,15,15,5,7,7,8,11,14,14,12,6,9,13,15,7,12,8,9,11,7,7,12,7,6,15,13,11,
+  9,7,15,11,8,6,6,14,12,13,5,14,13,13,7,5,15,5,8,11,14,14,6,14,6,9,12,9,12,5,15,8,8,5,12,9,12,5,14,6,8,13,6,5,15,13,11,11};
+static uint32_t rf(int j, uint32_t x, uint32_t y, uint32_t z) {
+  switch (j) { case 0: return x ^ y ^ z; case 1: return (x & y) | (~x & z); case 2: return (x | ~y) ^ z;
+               case 3: return (x & z) | (y & ~z); default: return x ^ (y | ~z); }
+}
+static void ripemd160_32(const uint8_t in[32], uint8_t out[20]) {
+  static const uint32_t KL[5] = {0, 0x5A827999, 0x6ED9EBA1, 0x8F1BBCDC, 0xA953FD4E};
+  static const uint32_t KR[5] = {0x50A28BE6, 0x5C4DD124, 0x6D703EF3, 0x7A6D76E9, 0};
+  uint8_t blk[64] = {0}; memcpy(blk, in, 32); blk[32] = 0x80; blk[56] = 0x00; blk[57] = 0x01; /* 256 bits LE */
+  uint32_t X[16]; for (int i = 0; i < 16; ++i) X[i] = blk[4*i] | blk[4*i+1] << 8 | blk[4*i+2] << 16 | (uint32_t)blk[4*i+3] << 24;
+  uint32_t h[5] = {0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0};
+  uint32_t al = h[0], bl = h[1], cl = h[2], dl = h[3], el = h[4], ar = al, br = bl, cr = cl, dr = dl, er = el;
+  for (int i = 0; i < 80; ++i) {
+    int j = i / 16;
+    uint32_t t = rol(al + rf(j, bl, cl, dl) + X[RL[i]] + KL[j], SL[i]) + el;
+    al = el; el = dl; dl = rol(cl, 10); cl = bl; bl = t;
+    t = rol(ar + rf(4 - j, br, cr, dr) + X[RR[i]] + KR[j], SR[i]) + er;
+    ar = er; er = dr; dr = rol(cr, 10); cr = br; br = t;
+  }
+  uint32_t t = h[1] + cl + dr; h[1] = h[2] + dl + er; h[2] = h[3] + el + ar; h[3] = h[4] + al + br; h[4] = h[0] + bl + cr; h[0] = t;
+  for (int i = 0; i < 5; ++i) for (int k = 0; k < 4; ++k) out[4*i+k] = (uint8_t)(h[i] >> (8*k));
+}
+
+/* ----------------------------------------------------------------- bech32 */
+static uint32_t polymod(const uint8_t* v, size_t n) {
+  static const uint32_t GEN[5] = {0x3b6a57b2, 0x26508e6d, 0x1ea119fa, 0x3d4233dd, 0x2a1462b3};
+  uint32_t chk = 1;
+  for (size_t i = 0; i < n; ++i) {
+    uint32_t b = chk >> 25; chk = ((chk & 0x1ffffff) << 5) ^ v[i];
+    for (int k = 0; k < 5; ++k) if ((b >> k) & 1) chk ^= GEN[k];
+  }
+  return chk;
+}
+static int bech32_cosmos(const uint8_t addr[20], char* out) {
+  static const char* CS = "qpzry9x8gf2tvdw0s3jn54khce6mua7l";
+  uint8_t v[64]; size_t nv = 0;
+  const char* hrp = "cosmos";
+  for (const char* p = hrp; *p; ++p) v[nv++] = (uint8_t)(*p >> 5);
+  v[nv++] = 0;
+  for (const char* p = hrp; *p; ++p) v[nv++] = (uint8_t)(*p & 31);
+  size_t d0 = nv; uint32_t acc = 0; int bits = 0;
+  for (int i = 0; i < 20; ++i) { acc = (acc << 8) | addr[i]; bits += 8; while (bits >= 5) { bits -= 5; v[nv++] = (acc >> bits) & 31; } }
+  if (bits) v[nv++] = (acc << (5 - bits)) & 31;
+  size_t dlen = nv - d0;
+  for (int i = 0; i < 6; ++i) v[nv + i] = 0;
+  uint32_t pm = polymod(v, nv + 6) ^ 1;
+  int o = sprintf(out, "%s1", hrp);
+  for (size_t i = 0; i < dlen; ++i) out[o++] = CS[v[d0 + i]];
+  for (int i = 0; i < 6; ++i) out[o++] = CS[(pm >> (5 * (5 - i))) & 31];
+  out[o] = 0;
+  return o;
+}
+
+/* ------------------------------------------------------------------ keys */
+typedef struct { size_t lo, hi; uint64_t seed; uint8_t *priv, *pub; } keyjob;
+static void* key_worker(void* a) {
+  keyjob* j = (keyjob*)a;
+  EC_GROUP* grp = EC_GROUP_new_by_curve_name(NID_secp256k1);
+  BN_CTX* ctx = BN_CTX_new();
+  BIGNUM *n = NULL, *nm1 = BN_new(), *fe = BN_new();
+  BN_hex2bn(&n, N_HEX); BN_copy(nm1, n); BN_sub_word(nm1, 1);
+  EC_POINT* pt = EC_POINT_new(grp);
+  for (size_t i = j->lo; i < j->hi; ++i) {
+    uint8_t secret[22]; memcpy(secret, "gv-c2-", 6);
+    for (int k = 0; k < 8; ++k) { secret[6 + k] = (uint8_t)(j->seed >> (8 * k)); secret[14 + k] = (uint8_t)((uint64_t)i >> (8 * k)); }
+    uint8_t h[32]; SHA256(secret, sizeof secret, h);
+    BN_bin2bn(h, 32, fe); BN_mod(fe, fe, nm1, ctx); BN_add_word(fe, 1);
+    BN_bn2binpad(fe, j->priv + 32 * i, 32);
+    EC_POINT_mul(grp, pt, fe, NULL, NULL, ctx);
+    EC_POINT_point2oct(grp, pt, POINT_CONVERSION_COMPRESSED, j->pub + 33 * i, 33, ctx);
+  }
+  EC_POINT_free(pt); BN_free(n); BN_free(nm1); BN_free(fe); BN_CTX_free(ctx); EC_GROUP_free(grp);
+  return NULL;
+}
+
+/* Derive nkeys (priv32, pub33) pairs. */
+int gvw_keys(size_t nkeys, uint64_t seed, uint8_t* priv32, uint8_t* pub33, int threads) {
+  if (threads < 1) threads = 1;
+  pthread_t th[256]; keyjob js[256]; if (threads > 256) threads = 256;
+  for (int t = 0; t < threads; ++t) {
+    js[t].lo = nkeys * t / threads; js[t].hi = nkeys * (t + 1) / threads; js[t].seed = seed; js[t].priv = priv32; js[t].pub = pub33;
+    pthread_create(&th[t], NULL, key_worker, &js[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  return 0;
+}
+
+/* ------------------------------------------------------- sign + mutate */
+typedef struct {
+  size_t lo, hi, nkeys; uint64_t seed; double adv;
+  const uint8_t *priv, *pub; const uint32_t* kidx; const uint8_t* msgdig;
+  uint8_t *opub, *osig, *odig, *expect;
+} signjob;
+
+static void* sign_worker(void* a) {
+  signjob* j = (signjob*)a;
+  EC_GROUP* grp = EC_GROUP_new_by_curve_name(NID_secp256k1);
+  BIGNUM *n = NULL, *half = BN_new(), *d = BN_new();
+  BN_hex2bn(&n, N_HEX); BN_rshift1(half, n);
+  EC_KEY* key = EC_KEY_new_by_curve_name(NID_secp256k1);
+  const BIGNUM *r, *s;
+  BIGNUM* s2 = BN_new();
+  for (size_t i = j->lo; i < j->hi; ++i) {
+    size_t k = j->kidx ? j->kidx[i] : i % j->nkeys;
+    uint8_t* dig = j->odig + 32 * i;
+    if (j->msgdig) memcpy(dig, j->msgdig + 32 * i, 32);
+    else {
+      uint8_t m[24]; memcpy(m, "gv-dig", 6);
+      for (int q = 0; q < 8; ++q) { m[6 + q] = (uint8_t)(j->seed >> (8 * q)); m[14 + q] = (uint8_t)((uint64_t)i >> (8 * q)); }
+      m[22] = m[23] = 0;
+      SHA256(m, sizeof m, dig);
+    }
+    BN_bin2bn(j->priv + 32 * k, 32, d);
+    EC_KEY_set_private_key(key, d);
+    ECDSA_SIG* sg = ECDSA_do_sign(dig, 32, key);
+    ECDSA_SIG_get0(sg, &r, &s);
+    if (BN_cmp(s, half) > 0) { BN_sub(s2, n, s); } else { BN_copy(s2, s); }
+    uint8_t* sig = j->osig + 64 * i;
+    BN_bn2binpad(r, sig, 32); BN_bn2binpad(s2, sig + 32, 32);
+    ECDSA_SIG_free(sg);
+    memcpy(j->opub + 33 * i, j->pub + 33 * k, 33);
+    j->expect[i] = 1;
+    /* adversarial mutation (C3): split evenly over six rejection classes */
+    uint64_t st = j->seed ^ (0xA5A5A5A5ULL * (i + 1));
+    uint64_t u = splitmix(&st);
+    if ((double)(u >> 11) * (1.0 / 9007199254740992.0) < j->adv) {
+      uint64_t v = splitmix(&st);
+      j->expect[i] = 0;
+      switch (v % 6) {
+        case 0: { /* high-S */ BIGNUM* t = BN_new(); BN_bin2bn(sig + 32, 32, t); BN_sub(t, n, t); BN_bn2binpad(t, sig + 32, 32); BN_free(t); break; }
+        case 1: { /* r >= n */ BIGNUM* t = BN_new(); BN_copy(t, n); BN_add_word(t, (unsigned)(v >> 40) & 0xFFFF); BN_bn2binpad(t, sig, 32); BN_free(t); break; }
+        case 2: /* s == 0 or huge */ memset(sig + 32, (v >> 8) & 1 ? 0xFF : 0x00, 32); break;
+        case 3: /* random x (off-curve or wrong key) */ for (int q = 1; q < 33; ++q) j->opub[33 * i + q] = (uint8_t)splitmix(&st); break;
+        case 4: { static const uint8_t bad[7] = {0, 1, 4, 5, 6, 7, 0xFF}; j->opub[33 * i] = bad[(v >> 8) % 7]; break; }
+        default: /* wrong message */ dig[(v >> 8) & 31] ^= (uint8_t)(1u << ((v >> 16) & 7)); break;
+      }
+    }
+  }
+  BN_free(s2); EC_KEY_free(key); BN_free(n); BN_free(half); BN_free(d); EC_GROUP_free(grp);
+  return NULL;
+}
+
+/* n signed items over digests.  Item i uses key kidx[i] (or i % nkeys when
+ * kidx is NULL); digest = SHA256("gv-dig"||seed||i) unless msgdig (n x 32) is
+ * given (message path: the caller hashed the sign bytes).  adv in [0,1): the
+ * fraction of items mutated into invalid ones.  expect[i] = 1 valid, 0 invalid. */
+int gvw_sign(size_t n, uint64_t seed, size_t nkeys, const uint8_t* priv32, const uint8_t* pub33,
+             const uint32_t* kidx, const uint8_t* msgdig, double adv, uint8_t* out_pub33,
+             uint8_t* out_sig64, uint8_t* out_dig32, uint8_t* expect, int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t th[256]; signjob js[256];
+  for (int t = 0; t < threads; ++t) {
+    signjob j = {n * t / threads, n * (t + 1) / threads, nkeys, seed, adv, priv32, pub33, kidx, msgdig,
+                 out_pub33, out_sig64, out_dig32, expect};
+    js[t] = j;
+    pthread_create(&th[t], NULL, sign_worker, &js[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  return 0;
+}
+
+/* C1/C4 sign bytes: StdSignBytes(MsgSend) for account i (from key i to key
+ * (i+1) % nkeys), accnum = i, sequence = seq.  Writes into blob (capacity
+ * blob_cap) with off/len per item; returns total bytes or -1 on overflow. */
+long long gvw_msgsend_signbytes(size_t n, const uint8_t* pub33, size_t nkeys, uint64_t seq,
+                                uint8_t* blob, size_t blob_cap, uint64_t* off, uint32_t* len) {
+  size_t pos = 0;
+  char from[64], to[64];
+  for (size_t i = 0; i < n; ++i) {
+    uint8_t h[32], a1[20], a2[20];
+    SHA256(pub33 + 33 * (i % nkeys), 33, h); ripemd160_32(h, a1);
+    SHA256(pub33 + 33 * ((i + 1) % nkeys), 33, h); ripemd160_32(h, a2);
+    bech32_cosmos(a1, from); bech32_cosmos(a2, to);
+    char buf[1024];
+    int m = snprintf(buf, sizeof buf,
+      "{\"account_number\":\"%zu\",\"chain_id\":\"gv-bench\",\"fee\":{\"amount\":[{\"amount\":\"0\",\"denom\":\"stake\"}],"
+      "\"gas\":\"1000000\"},\"memo\":\"\",\"msgs\":[{\"type\":\"cosmos-sdk/MsgSend\",\"value\":{\"amount\":"
+      "[{\"amount\":\"10\",\"denom\":\"foocoin\"}],\"from_address\":\"%s\",\"to_address\":\"%s\"}}],\"sequence\":\"%llu\"}",
+      i % nkeys, from, to, (unsigned long long)seq);
+    if (pos + (size_t)m > blob_cap) return -1;
+    memcpy(blob + pos, buf, (size_t)m);
+    off[i] = pos; len[i] = (uint32_t)m; pos += (size_t)m;
+  }
+  return (long long)pos;
+}
+
+/* sha256 of every message (used to feed gvw_sign on the message path) */
+void gvw_sha256_msgs(size_t n, const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint8_t* out32) {
+  for (size_t i = 0; i < n; ++i) SHA256(blob + off[i], len[i], out32 + 32 * i);
+}
