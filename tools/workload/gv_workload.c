@@ -100,6 +100,7 @@ static void* key_worker(void* a) {
   keyjob* j = (keyjob*)a;
   EC_GROUP* grp = EC_GROUP_new_by_curve_name(NID_secp256k1);
   BN_CTX* ctx = BN_CTX_new();
+  EC_GROUP_precompute_mult(grp, ctx);
   BIGNUM *n = NULL, *nm1 = BN_new(), *fe = BN_new();
   BN_hex2bn(&n, N_HEX); BN_copy(nm1, n); BN_sub_word(nm1, 1);
   EC_POINT* pt = EC_POINT_new(grp);
@@ -140,7 +141,11 @@ static void* sign_worker(void* a) {
   EC_GROUP* grp = EC_GROUP_new_by_curve_name(NID_secp256k1);
   BIGNUM *n = NULL, *half = BN_new(), *d = BN_new();
   BN_hex2bn(&n, N_HEX); BN_rshift1(half, n);
-  EC_KEY* key = EC_KEY_new_by_curve_name(NID_secp256k1);
+  /* fixed-base precomputation makes OpenSSL's k*G several times faster */
+  BN_CTX* bctx = BN_CTX_new();
+  EC_GROUP_precompute_mult(grp, bctx);
+  EC_KEY* key = EC_KEY_new();
+  EC_KEY_set_group(key, grp);
   const BIGNUM *r, *s;
   BIGNUM* s2 = BN_new();
   for (size_t i = j->lo; i < j->hi; ++i) {
@@ -179,7 +184,7 @@ static void* sign_worker(void* a) {
       }
     }
   }
-  BN_free(s2); EC_KEY_free(key); BN_free(n); BN_free(half); BN_free(d); EC_GROUP_free(grp);
+  BN_free(s2); EC_KEY_free(key); BN_free(n); BN_free(half); BN_free(d); BN_CTX_free(bctx); EC_GROUP_free(grp);
   return NULL;
 }
 
