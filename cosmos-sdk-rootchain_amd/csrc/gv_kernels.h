@@ -6,6 +6,7 @@
 
 #define GV_GTAB_N 128           // multiples 1..128 of G (signed 8-bit windows)
 #define GV_QTAB_WORDS 192       // per-lane Q table words: 8 entries x (x, y, z-ratio)
+#define GV_INV_M 16             // signatures folded per lane by k_scalar_inv
 
 #ifdef __cplusplus
 extern "C" {
@@ -23,7 +24,8 @@ typedef struct gvk_batch {
   const uint32_t* msg_len;
   const uint32_t* gtab;
   uint32_t *in_x, *in_pfx, *in_r, *in_s, *in_e;
-  uint32_t *q_xy, *scal, *flags, *qtab;
+  uint32_t *digits;             // 33 rows: packed Booth digits per window (16 rows reused as scratch)
+  uint32_t *zq, *flags, *qtab;  // shared Z of the Q table (8 rows), flags, Q table (192 rows)
   uint64_t* bits;               // C/64 words, bit (i%64) of word i/64
   hipEvent_t ev[3];             // optional: after unpack/sha, after prep, after ecmult
 } gvk_batch;

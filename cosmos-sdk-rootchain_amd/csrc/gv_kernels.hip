@@ -154,95 +154,7 @@ __global__ __launch_bounds__(256) void k_sha256(const uint8_t* blob, const uint6
   for (int i = 0; i < 8; ++i) e[(size_t)i * C + g] = h[7 - i];
 }
 
-// -------------------------------------------------------------------- k_prep
-// flags bits: 1 = passes every check before the curve arithmetic,
-//             2 = r < p - n (so R.x == r + n is also an accept)
-__global__ __launch_bounds__(256) void k_prep(u32 C, const u32* in_x, const u32* in_pfx,
-                                               const u32* in_r, const u32* in_s, const u32* in_e,
-                                               u32* q_xy, u32* scal, u32* flags) {
-  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;   // C % 256 == 0: all lanes live
-  bool ok = true;
-
-  // ---- btcec.ParsePubKey (compressed): prefix, decompressPoint, range, IsOnCurve
-  const u32 pre = in_pfx[g];
-  ok &= (pre & 0xFEu) == 0x02u;
-  fe x;
-  load_fe(x, in_x, C, g);
-  // x < p  (btcec: "pubkey X parameter is >= to P")
-  {
-    u32 br = 0, d;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) d = __builtin_subc(x.v[i], kP[i], br, &br);
-    (void)d;
-    ok &= (br != 0);
-  }
-  fe c, y, y2, seven;
-  fe_sqr(c, x);
-  fe_mul(c, c, x);
-  fe_set_u32(seven, 7);
-  fe_add(c, c, seven);                      // c = x^3 + 7
-  fe_sqrt_candidate(y, c);                  // y = c^((p+1)/4)
-  fe_sqr(y2, y);
-  ok &= fe_equal(y2, c);                    // "invalid square root"
-  fe_normalize(y);
-  if ((y.v[0] & 1u) != (pre & 1u)) fe_neg(y, y);   // choose parity (y != 0 always)
-  fe_normalize(y);
-  // (IsOnCurve and Y < P hold by construction once the square-root check passed)
-
-  // ---- tendermint low-S + crypto/ecdsa range checks
-  u32 r[8], s[8], e[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    r[i] = in_r[(size_t)i * C + g];
-    s[i] = in_s[(size_t)i * C + g];
-    e[i] = in_e[(size_t)i * C + g];
-  }
-  ok &= !u256_is_zero(r);
-  ok &= !u256_geq(r, kN);
-  ok &= !u256_is_zero(s);
-  ok &= u256_geq(kHalfN, s);                // s <= N/2  (tendermint rejects s > halfN)
-  // r < p - n ?
-  const bool r_small = !u256_geq(r, kPminusN);
-  sc_reduce_once(e);                        // e mod n (hashToInt keeps all 256 bits)
-
-  // invalid lanes: harmless stand-ins so the whole wave stays on one path
-  if (!ok) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { s[i] = (i == 0) ? 1u : 0u; e[i] = 0u; r[i] = 0u; }
-    fe_from_const(x, kGx);
-    fe_from_const(y, kGy);
-  }
-
-  // ---- w = s^-1 mod n, batched across the wavefront
-  u32 sm[8], wm[8], u1[8], u2[8];
-  sc_to_mont(sm, s);
-  sc_batch_inv_wave(wm, sm);
-  sc_montmul(u1, e, wm);                    // e*w  (plain form)
-  sc_montmul(u2, r, wm);                    // r*w
-
-  // ---- GLV split
-  u32 k1g[4], k2g[4], k1q[4], k2q[4], n1g, n2g, n1q, n2q;
-  glv_split(k1g, n1g, k2g, n2g, u1);
-  glv_split(k1q, n1q, k2q, n2q, u2);
-  if (!ok) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { k1g[i] = k2g[i] = k1q[i] = k2q[i] = 0u; }
-  }
-
-  store_fe(q_xy, C, g, x);
-  store_fe(q_xy + 8 * (size_t)C, C, g, y);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    scal[(size_t)(0 + i) * C + g] = k1q[i];
-    scal[(size_t)(4 + i) * C + g] = k2q[i];
-    scal[(size_t)(8 + i) * C + g] = k1g[i];
-    scal[(size_t)(12 + i) * C + g] = k2g[i];
-  }
-  scal[(size_t)16 * C + g] = n1q | (n2q << 1) | (n1g << 2) | (n2g << 3);
-  flags[g] = (ok ? 1u : 0u) | (r_small ? 2u : 0u);
-}
-
-// ------------------------------------------------------------------ k_ecmult
+// ------------------------------------------------------------ ladder helpers
 // Signed fixed-window (Booth) digit of a 128-bit magnitude k at window `win`
 // of width W: d = (bits [W*win-1 .. W*win+W-1]) recoded into [-2^(W-1), 2^(W-1)].
 template <int W>
@@ -324,25 +236,197 @@ GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx, const fe& qy, fe&
   }
 }
 
-__global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, const u32* q_xy,
-                                                 const u32* scal, const u32* flags,
-                                                 const u32* in_r, u32* qt, uint64_t* bits) {
+// ------------------------------------------------------------- k_scalar_inv
+// w = s^-1 mod n for every lane, Montgomery form, by Montgomery's trick:
+// each lane folds GV_INV_M signatures (element (wave*M + j)*64 + lane, so each
+// step j is a coalesced wave access), the lane totals are combined across the
+// wavefront by prefix/suffix scans, and ONE Fermat inversion serves the wave's
+// 64*M signatures -- ~3 Montgomery products per signature + 394/M amortised,
+// instead of ~380 (a per-lane inversion costs the same SIMT time whether one
+// lane or all 64 run it).  s outside [1, n) is replaced by 1 (those lanes are
+// rejected in k_prep).  pre/sm use the scratch rows given by the caller.
+GV_DEV void load_sc(u32 a[8], const u32* base, u32 C, u32 g) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = base[(size_t)i * C + g];
+}
+GV_DEV void store_sc(u32* base, u32 C, u32 g, const u32 a[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) base[(size_t)i * C + g] = a[i];
+}
+
+__global__ __launch_bounds__(256) void k_scalar_inv(u32 C, const u32* in_s, u32* w, u32* pre) {
+  const u32 lane = threadIdx.x & 63u;
+  const u32 wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const u32 one_m[8] = {0x2FC9BEBFu, 0x402DA173u, 0x50B75FC4u, 0x45512319u, 1u, 0u, 0u, 0u};
+  u32 acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = one_m[i];
+  for (int j = 0; j < GV_INV_M; ++j) {
+    const u32 e = (wave * GV_INV_M + j) * 64u + lane;
+    if (e >= C) break;                       // wave-uniform (C % 64 == 0)
+    u32 s[8], sm[8];
+    load_sc(s, in_s, C, e);
+    const bool ok = !u256_is_zero(s) && !u256_geq(s, kN);
+    if (!ok) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] = (i == 0) ? 1u : 0u;
+    }
+    sc_to_mont(sm, s);
+    store_sc(pre, C, e, acc);                // exclusive prefix within the lane
+    store_sc(w, C, e, sm);
+    sc_montmul(acc, acc, sm);
+  }
+  u32 inv_lane[8];
+  sc_batch_inv_wave(inv_lane, acc);          // (lane total)^-1, one Fermat chain per wave
+  for (int j = GV_INV_M - 1; j >= 0; --j) {
+    const u32 e = (wave * GV_INV_M + j) * 64u + lane;
+    if (e >= C) continue;
+    u32 p[8], sm[8], inv[8];
+    load_sc(p, pre, C, e);
+    load_sc(sm, w, C, e);
+    sc_montmul(inv, inv_lane, p);            // s_j^-1 = (s_0..s_j)^-1 * (s_0..s_{j-1})
+    sc_montmul(inv_lane, inv_lane, sm);      // drop s_j from the running inverse
+    store_sc(w, C, e, inv);
+  }
+}
+
+// -------------------------------------------------------------------- k_prep
+// flags bits: 1 = passes every check before the curve arithmetic,
+//             2 = r < p - n (so R.x == r + n is also an accept)
+__global__ __launch_bounds__(256) void k_prep(u32 C, const u32* in_x, const u32* in_pfx,
+                                               const u32* in_r, const u32* in_s, const u32* in_e,
+                                               const u32* in_w, u32* digits, u32* qt, u32* zq_out,
+                                               u32* flags) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;   // C % 256 == 0: all lanes live
+  bool ok = true;
+
+  // ---- btcec.ParsePubKey (compressed): prefix, decompressPoint, range, IsOnCurve
+  const u32 pre = in_pfx[g];
+  ok &= (pre & 0xFEu) == 0x02u;
+  fe x;
+  load_fe(x, in_x, C, g);
+  // x < p  (btcec: "pubkey X parameter is >= to P")
+  {
+    u32 br = 0, d;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d = __builtin_subc(x.v[i], kP[i], br, &br);
+    (void)d;
+    ok &= (br != 0);
+  }
+  fe c, y, y2, seven;
+  fe_sqr(c, x);
+  fe_mul(c, c, x);
+  fe_set_u32(seven, 7);
+  fe_add(c, c, seven);                      // c = x^3 + 7
+  fe_sqrt_candidate(y, c);                  // y = c^((p+1)/4)
+  fe_sqr(y2, y);
+  ok &= fe_equal(y2, c);                    // "invalid square root"
+  fe_normalize(y);
+  if ((y.v[0] & 1u) != (pre & 1u)) fe_neg(y, y);   // choose parity (y != 0 always)
+  fe_normalize(y);
+  // (IsOnCurve and Y < P hold by construction once the square-root check passed)
+
+  // ---- tendermint low-S + crypto/ecdsa range checks
+  u32 r[8], s[8], e[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    r[i] = in_r[(size_t)i * C + g];
+    s[i] = in_s[(size_t)i * C + g];
+    e[i] = in_e[(size_t)i * C + g];
+  }
+  ok &= !u256_is_zero(r);
+  ok &= !u256_geq(r, kN);
+  ok &= !u256_is_zero(s);
+  ok &= u256_geq(kHalfN, s);                // s <= N/2  (tendermint rejects s > halfN)
+  // r < p - n ?
+  const bool r_small = !u256_geq(r, kPminusN);
+  sc_reduce_once(e);                        // e mod n (hashToInt keeps all 256 bits)
+
+  // invalid lanes: harmless stand-ins so the whole wave stays on one path
+  if (!ok) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { s[i] = (i == 0) ? 1u : 0u; e[i] = 0u; r[i] = 0u; }
+    fe_from_const(x, kGx);
+    fe_from_const(y, kGy);
+  }
+
+  // ---- w = s^-1 mod n (Montgomery form, from k_scalar_inv)
+  u32 wm[8], u1[8], u2[8];
+  load_sc(wm, in_w, C, g);
+  sc_montmul(u1, e, wm);                    // e*w  (plain form)
+  sc_montmul(u2, r, wm);                    // r*w
+
+  // ---- GLV split
+  u32 k1g[4], k2g[4], k1q[4], k2q[4], n1g, n2g, n1q, n2q;
+  glv_split(k1g, n1g, k2g, n2g, u1);
+  glv_split(k1q, n1q, k2q, n2q, u2);
+  if (!ok) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { k1g[i] = k2g[i] = k1q[i] = k2q[i] = 0u; }
+  }
+
+  // ---- signed fixed-window (Booth) recoding, scalar signs folded in.
+  // digits[win*C + g] packs four two's-complement fields: dQ1 bits 0..4,
+  // dQ2 bits 5..9 (4-bit windows: digits in [-8, 8]), dG1 bits 10..18, dG2
+  // bits 19..27 (8-bit windows, only on even win: digits in [-128, 128] --
+  // +128 does not fit an int8, hence 9-bit fields).
+#pragma unroll
+  for (int win = 0; win <= 32; ++win) {
+    int d0 = booth_digit<4>(k1q, win), d1 = booth_digit<4>(k2q, win), d2 = 0, d3 = 0;
+    if ((win & 1) == 0) { d2 = booth_digit<8>(k1g, win >> 1); d3 = booth_digit<8>(k2g, win >> 1); }
+    if (n1q) d0 = -d0;
+    if (n2q) d1 = -d1;
+    if (n1g) d2 = -d2;
+    if (n2g) d3 = -d3;
+    digits[(size_t)win * C + g] = ((u32)d0 & 0x1Fu) | (((u32)d1 & 0x1Fu) << 5) | (((u32)d2 & 0x1FFu) << 10) |
+                                  (((u32)d3 & 0x1FFu) << 19);
+  }
+  flags[g] = (ok ? 1u : 0u) | (r_small ? 2u : 0u);
+
+  // ---- per-lane table of Q multiples (shared Z, isomorphic-curve affine)
+  fe zq;
+  build_q_table(qt, C, g, x, y, zq);
+  store_fe(zq_out, C, g, zq);
+}
+
+// ------------------------------------------------------------------ k_ecmult
+// acc <- acc + (x, y) where (x, y) is affine on the accumulator's curve
+// (zinv == nullptr: Q-table entry) or an affine point of the real curve to be
+// lifted by zinv (G-table entry).  An infinite accumulator takes the point.
+GV_DEV void add_entry(gej& acc, bool& inf, const fe& x, const fe& y, const fe* zinv) {
+  fe az;
+  if (zinv) {                                   // wave-uniform
+    if (inf) az = *zinv;
+    else fe_mul(az, acc.z, *zinv);
+  } else {
+    if (inf) fe_set_u32(az, 1);
+    else az = acc.z;
+  }
+  fe z2, u2, s2;
+  fe_sqr(z2, az);
+  fe_mul(u2, x, z2);
+  fe_mul(z2, z2, az);
+  fe_mul(s2, y, z2);
+  if (inf) {
+    acc.x = u2;
+    acc.y = s2;
+    fe_set_u32(acc.z, 1);
+    inf = false;
+    return;
+  }
+  gej_add_tail(acc, inf, u2, s2);
+}
+
+__global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, const u32* digits,
+                                                 const u32* qt, const u32* zq_in, const u32* flags,
+                                                 const u32* in_r, uint64_t* bits) {
   __shared__ u32 gt[GV_GTAB_N * 16];
   for (u32 i = threadIdx.x; i < GV_GTAB_N * 16; i += blockDim.x) gt[i] = gtab[i];
   __syncthreads();
 
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
-  fe qx, qy, zq;
-  load_fe(qx, q_xy, C, g);
-  load_fe(qy, q_xy + 8 * (size_t)C, C, g);
-  build_q_table(qt, C, g, qx, qy, zq);
-
-  u32 k[4][4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) k[s][i] = scal[(size_t)(4 * s + i) * C + g];
-  const u32 sgn = scal[(size_t)16 * C + g];
+  fe zq;
+  load_fe(zq, zq_in, C, g);
 
   gej acc;
   fe_set_zero(acc.x); fe_set_zero(acc.y); fe_set_zero(acc.z);
@@ -354,18 +438,16 @@ __global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, c
 #pragma unroll 1
       for (int d = 0; d < 4; ++d) gej_double(acc, acc);
     }
-    int dig[4];
-    dig[0] = booth_digit<4>(k[0], win);
-    dig[1] = booth_digit<4>(k[1], win);
-    const bool gwin = (win & 1) == 0;
-    dig[2] = gwin ? booth_digit<8>(k[2], win >> 1) : 0;
-    dig[3] = gwin ? booth_digit<8>(k[3], win >> 1) : 0;
-    const int nslots = gwin ? 4 : 2;
+    const u32 dw = digits[(size_t)win * C + g];
+    const int nslots = (win & 1) ? 2 : 4;
 #pragma unroll 1
     for (int slot = 0; slot < nslots; ++slot) {
-      const int d = slot == 0 ? dig[0] : slot == 1 ? dig[1] : slot == 2 ? dig[2] : dig[3];
+      // sign-extend field `slot` (see the packing in k_prep)
+      const int d = slot == 0 ? ((int)(dw << 27) >> 27)
+                  : slot == 1 ? ((int)(dw << 22) >> 27)
+                  : slot == 2 ? ((int)(dw << 13) >> 23)
+                              : ((int)(dw << 4) >> 23);
       if (d == 0) continue;
-      const bool neg = (d < 0) != (((sgn >> slot) & 1u) != 0u);
       const u32 e = (u32)((d < 0 ? -d : d) - 1);
       fe x, y;
       if (slot < 2) {
@@ -376,33 +458,17 @@ __global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, c
 #pragma unroll
         for (int i = 0; i < 8; ++i) { x.v[i] = gt[e * 16 + i]; y.v[i] = gt[e * 16 + 8 + i]; }
       }
-      if (slot & 1) {                       // lambda * P = (beta * x, y)
+      if (slot & 1) {                            // lambda * P = (beta * x, y)
         fe beta;
         fe_from_const(beta, kBeta);
         fe_mul(x, x, beta);
       }
-      if (neg) fe_neg(y, y);
-      if (inf) {
-        if (slot < 2) {
-          acc.x = x; acc.y = y;
-        } else {                             // real-curve point onto the iso curve
-          fe z2, z3;
-          fe_sqr(z2, zq);
-          fe_mul(z3, z2, zq);
-          fe_mul(acc.x, x, z2);
-          fe_mul(acc.y, y, z3);
-        }
-        fe_set_u32(acc.z, 1);
-        inf = false;
-      } else if (slot < 2) {
-        gej_add_ge(acc, inf, x, y);
-      } else {
-        gej_add_zinv(acc, inf, x, y, zq);
-      }
+      if (d < 0) fe_neg(y, y);
+      add_entry(acc, inf, x, y, slot < 2 ? nullptr : &zq);
     }
   }
 
-  // ---- final check: R = (X, Y, Z*zq) on the real curve
+  // ---- final check: R = (X, Y, Z*zq) on the real curve; x(R) mod n == r
   const u32 fl = flags[g];
   bool ok = (fl & 1u) && !inf;
   fe zr, zz, rf, t, X;
@@ -506,11 +572,19 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
     hipLaunchKernelGGL(gv::k_sha256, grd, blk, 0, st, b->msg_blob, b->msg_off, b->msg_len, b->n, C,
                        b->in_e);
   if (b->ev[0]) hipEventRecord(b->ev[0], st);
-  hipLaunchKernelGGL(gv::k_prep, grd, blk, 0, st, C, b->in_x, b->in_pfx, b->in_r, b->in_s, b->in_e,
-                     b->q_xy, b->scal, b->flags);
+  {
+    const uint32_t waves = (C / 64 + GV_INV_M - 1) / GV_INV_M;
+    // scratch for w and the prefix products: the digit rows.  k_prep reads
+    // its lane's w before writing that lane's digits (same lane, same rows).
+    uint32_t* w = b->digits;                   // rows 0..7
+    uint32_t* pre = b->digits + (size_t)8 * C; // rows 8..15
+    hipLaunchKernelGGL(gv::k_scalar_inv, dim3((waves + 3) / 4), blk, 0, st, C, b->in_s, w, pre);
+    hipLaunchKernelGGL(gv::k_prep, grd, blk, 0, st, C, b->in_x, b->in_pfx, b->in_r, b->in_s, b->in_e,
+                       (const uint32_t*)w, b->digits, b->qtab, b->zq, b->flags);
+  }
   if (b->ev[1]) hipEventRecord(b->ev[1], st);
-  hipLaunchKernelGGL(gv::k_ecmult, grd, blk, 0, st, b->gtab, b->n, C, b->q_xy, b->scal, b->flags,
-                     b->in_r, b->qtab, b->bits);
+  hipLaunchKernelGGL(gv::k_ecmult, grd, blk, 0, st, b->gtab, b->n, C, b->digits, b->qtab, b->zq, b->flags,
+                     b->in_r, b->bits);
   if (b->ev[2]) hipEventRecord(b->ev[2], st);
   return hipGetLastError();
 }

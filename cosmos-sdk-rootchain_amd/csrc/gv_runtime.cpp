@@ -26,7 +26,7 @@ namespace {
     if (e_ != hipSuccess) return GV_EHIP;         \
   } while (0)
 
-constexpr size_t kLaneWords = 8 + 1 + 8 + 8 + 8 + 16 + 17 + 1 + GV_QTAB_WORDS;
+constexpr size_t kLaneWords = 8 + 1 + 8 + 8 + 8 + 33 + 8 + 1 + GV_QTAB_WORDS;
 
 struct Dev {
   int id = 0;
@@ -35,7 +35,7 @@ struct Dev {
   size_t cap = 0;               // lanes of scratch (multiple of 256)
   uint8_t* scratch = nullptr;   // one allocation, carved below
   uint8_t *d_pub = nullptr, *d_sig = nullptr, *d_dig = nullptr;
-  uint32_t *in_x, *in_pfx, *in_r, *in_s, *in_e, *q_xy, *scal, *flags, *qtab;
+  uint32_t *in_x, *in_pfx, *in_r, *in_s, *in_e, *digits, *zq, *flags, *qtab;
   uint64_t* bits = nullptr;
   uint8_t* d_blob = nullptr;
   size_t blob_cap = 0;
@@ -69,8 +69,8 @@ int ensure_cap(Dev* d, size_t C) {
   d->in_r = (uint32_t*)take(C * 8 * 4);
   d->in_s = (uint32_t*)take(C * 8 * 4);
   d->in_e = (uint32_t*)take(C * 8 * 4);
-  d->q_xy = (uint32_t*)take(C * 16 * 4);
-  d->scal = (uint32_t*)take(C * 17 * 4);
+  d->digits = (uint32_t*)take(C * 33 * 4);
+  d->zq = (uint32_t*)take(C * 8 * 4);
   d->flags = (uint32_t*)take(C * 4);
   d->qtab = (uint32_t*)take(C * GV_QTAB_WORDS * 4);
   d->bits = (uint64_t*)take((C / 64) * 8);
@@ -129,7 +129,7 @@ int launch(gv_ctx* ctx, Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig
   b.msg_blob = blob; b.msg_off = off; b.msg_len = len;
   b.gtab = d->gtab;
   b.in_x = d->in_x; b.in_pfx = d->in_pfx; b.in_r = d->in_r; b.in_s = d->in_s; b.in_e = d->in_e;
-  b.q_xy = d->q_xy; b.scal = d->scal; b.flags = d->flags; b.qtab = d->qtab;
+  b.digits = d->digits; b.zq = d->zq; b.flags = d->flags; b.qtab = d->qtab;
   b.bits = bits_out;
   hipEvent_t* rs = nullptr;
   if (ctx->time_kernels) {

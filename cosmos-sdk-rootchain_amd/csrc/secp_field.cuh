@@ -5,13 +5,12 @@
 // congruent to the intended residue (i.e. in [0, 2^256)); fe_normalize() gives
 // the canonical representative when a comparison needs it.
 //
-// The 256x256 product is one hand-scheduled inline-asm block: product scanning
-// (column by column) with v_mad_u64_u32 accumulating into a 64-bit register
-// pair and its carry-out (VCC) counted by v_addc_co_u32 into the high word of
-// the *next* column's pair -- 2 VALU ops per 32x32 product, no compiler
-// s_nop between products.  Measured on MI355X, v_mad_u64_u32 issues at ~the
-// same chip rate as plain 32-bit VALU ops (tools/microbench/alu_rate.hip), so
-// instruction count, not multiply count, is what this layer minimises.
+// Multiply, square, reduction, add and sub are hand-scheduled inline-asm
+// blocks (see below).  Measured on MI355X, v_mad_u64_u32 issues at ~the same
+// chip rate as plain 32-bit VALU ops (tools/microbench/alu_rate.hip), so
+// instruction count, not multiply count, is what this layer minimises; every
+// carry chain is kept back-to-back because hipcc pads a VCC read that is one
+// instruction away from its writer with an s_nop.
 //
 // Reference semantics being accelerated: btcec/field.go (btcd v0.20.1-beta)
 // via crypto/ecdsa.Verify; see SURVEY.md §2 "External: btcec".
@@ -39,48 +38,38 @@ GV_DEV void fe_set_zero(fe& r) {
 GV_DEV void fe_set_u32(fe& r, u32 x) { fe_set_zero(r); r.v[0] = x; }
 
 // ---------------------------------------------------------------------------
-// 512-bit product t = a * b.  Scratch: v[0:3] and VCC (declared clobbered).
-// Column k accumulates in pair P_k (alternating v[0:1] / v[2:3]); the carry
-// out of each mad increments P_{k+1}.hi, which becomes the high word of the
-// next column's accumulator; P_{k+1}.lo <- P_k.hi at the column boundary.
-// Generated by tools/gen_mul_asm.py (kept in-tree so the schedule is reviewable).
-#include "secp_mul_asm.inc"
+// Hand-scheduled sequences (tools/gen_field_asm.py; validated on the CPU by an
+// instruction-level model in tests/test_field_asm_model.py).  Scratch: v0..v3
+// and VCC, declared clobbered.
+//   mul: product scanning -- column k accumulates in a 64-bit pair with
+//        v_mad_u64_u32; each mad's carry-out (VCC) is counted by v_addc_co_u32
+//        into the high word of the next column's pair: 2 VALU ops per product.
+//   sqr: the 28 cross products the same way, then one pass of v_alignbit
+//        doubling and one carry chain adding the 8 diagonal squares.
+//   reduce: t = L + H*2^256 == L + 977*H + (H << 32) as three back-to-back
+//        carry chains, then two folds of the (at most 34-bit) top word.
+#include "secp_field_asm.inc"
 
 GV_DEV void mul_256x256(u32 t[16], const u32 a[8], const u32 b[8]) {
   GV_MUL512_ASM(t, a, b);
 }
 
-// ---------------------------------------------------------------------------
+GV_DEV void sqr_256(u32 t[16], const u32 a[8]) {
+  u32 c[16];
+  u64 sq[8];
+  GV_SQRX_ASM(c, a);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sq[i] = (u64)a[i] * a[i];
+  GV_SQRF_ASM(t, c, sq);
+}
+
 // Reduce a 512-bit value modulo p to a weakly reduced 256-bit value.
-// t = L + H * 2^256,  2^256 == 2^32 + 977 (mod p).
 GV_DEV void fe_reduce512(fe& r, const u32 t[16]) {
-  // pass 1: s = L + 977*H + (H << 32)  -> 8 limbs + 34-bit top
-  u32 s[8];
-  u64 acc = 0;
+  u64 m[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    acc += (u64)t[8 + i] * 977u + t[i];
-    if (i) acc += t[7 + i];
-    s[i] = (u32)acc;
-    acc >>= 32;
-  }
-  u64 top = acc + t[15];                 // < 2^33 + 2^10
-  // pass 2: r = s + top*977 + (top << 32)
-  u32 top_lo = (u32)top, top_hi = (u32)(top >> 32);   // top_hi in {0,1,2}
-  u64 x = (u64)top_lo * 977u + s[0];
-  r.v[0] = (u32)x;
-  x = (x >> 32) + (u64)s[1] + top_lo + (u64)top_hi * 977u;
-  r.v[1] = (u32)x;
-  x = (x >> 32) + (u64)s[2] + top_hi;
-  r.v[2] = (u32)x;
-  u32 c = (u32)(x >> 32);
-#pragma unroll
-  for (int i = 3; i < 8; ++i) r.v[i] = __builtin_addc(s[i], 0u, c, &c);
-  // pass 3 (rare): a wrap past 2^256 leaves a value < 2^67; add 2^32+977 once.
-  u32 c2;
-  r.v[0] = __builtin_addc(r.v[0], c * 977u, 0u, &c2);
-  r.v[1] = __builtin_addc(r.v[1], c, c2, &c2);
-  r.v[2] = __builtin_addc(r.v[2], 0u, c2, &c2);
+  for (int i = 0; i < 8; ++i) m[i] = (u64)t[8 + i] * 977u;
+  u32 top, top2;
+  GV_REDUCE_ASM(r.v, t, m, top, top2);
 }
 
 GV_DEV void fe_mul(fe& r, const fe& a, const fe& b) {
@@ -90,43 +79,17 @@ GV_DEV void fe_mul(fe& r, const fe& a, const fe& b) {
 }
 GV_DEV void fe_sqr(fe& r, const fe& a) {
   u32 t[16];
-  mul_256x256(t, a.v, a.v);
+  sqr_256(t, a.v);
   fe_reduce512(r, t);
 }
 
-// r = a + b (mod p), weakly reduced.
-GV_DEV void fe_add(fe& r, const fe& a, const fe& b) {
-  u32 c = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
-  // fold the carry: + c*(2^32 + 977)
-  u32 c2;
-  r.v[0] = __builtin_addc(r.v[0], c * 977u, 0u, &c2);
-  r.v[1] = __builtin_addc(r.v[1], c, c2, &c2);
-#pragma unroll
-  for (int i = 2; i < 8; ++i) r.v[i] = __builtin_addc(r.v[i], 0u, c2, &c2);
-  // a second wrap leaves a value < 2^33+977: limbs 0..1 absorb one more fold
-  u32 c3;
-  r.v[0] = __builtin_addc(r.v[0], c2 * 977u, 0u, &c3);
-  r.v[1] = __builtin_addc(r.v[1], c2, c3, &c3);
-}
+// r = a + b (mod p), weakly reduced: carry chain, then two folds of the carry
+// (c * (2^32 + 977)); the second fold can only touch limbs 0..1.
+GV_DEV void fe_add(fe& r, const fe& a, const fe& b) { GV_ADD_ASM(r.v, a.v, b.v); }
 
-// r = a - b (mod p), weakly reduced.
-GV_DEV void fe_sub(fe& r, const fe& a, const fe& b) {
-  u32 br = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
-  // borrow: value wrapped to a-b+2^256; want a-b+p = (a-b+2^256) - (2^32+977)
-  u32 b2;
-  r.v[0] = __builtin_subc(r.v[0], br * 977u, 0u, &b2);
-  r.v[1] = __builtin_subc(r.v[1], br, b2, &b2);
-#pragma unroll
-  for (int i = 2; i < 8; ++i) r.v[i] = __builtin_subc(r.v[i], 0u, b2, &b2);
-  // a second borrow (only when a-b < -p) leaves a value >= 2^256 - 2^33: fold again
-  u32 b3;
-  r.v[0] = __builtin_subc(r.v[0], b2 * 977u, 0u, &b3);
-  r.v[1] = __builtin_subc(r.v[1], b2, b3, &b3);
-}
+// r = a - b (mod p), weakly reduced: a borrow means the result wrapped to
+// a - b + 2^256, so subtract 2^32 + 977 (== 2^256 - p), at most twice.
+GV_DEV void fe_sub(fe& r, const fe& a, const fe& b) { GV_SUB_ASM(r.v, a.v, b.v); }
 
 GV_DEV void fe_neg(fe& r, const fe& a) { fe z; fe_set_zero(z); fe_sub(r, z, a); }
 GV_DEV void fe_dbl(fe& r, const fe& a) { fe_add(r, a, a); }

@@ -40,34 +40,38 @@ GV_DEV void gej_double(gej& r, const gej& a) {
   fe_sub(r.y, t, C);              // Y3 = E(D - X3) - 8C
 }
 
-// Shared tail of the mixed additions: given U2, S2 (the affine point scaled to
-// a's Z), finish a + b.  zmul is the factor the output Z gets multiplied with
-// (a.z for a plain mixed add).  Handles the exceptional cases.
+// Shared tail of the mixed additions: given U2, S2 (the added point scaled to
+// a's Z), finish a + b.  Exceptional cases: H == 0 and R == 0 (a == b) ->
+// doubling; H == 0 and R != 0 (a == -b) -> infinity.  The doubling is done
+// AFTER the regular formula's region (which is masked off for those lanes) so
+// its temporaries never overlap the addition's live values: with exec-masked
+// SIMT branches an inline doubling inside the add would hold both register
+// sets at once.
 GV_DEV void gej_add_tail(gej& a, bool& inf, const fe& u2, const fe& s2) {
   fe h, rr;
   fe_sub(h, u2, a.x);
   fe_sub(rr, s2, a.y);
-  if (fe_is_zero(h)) {
-    if (fe_is_zero(rr)) {
-      gej_double(a, a);           // a == b
-    } else {
-      inf = true;                 // a == -b
-    }
-    return;
+  const bool exc = fe_is_zero(h);
+  bool dbl = false;
+  if (exc) {
+    dbl = fe_is_zero(rr);
+    if (!dbl) inf = true;         // a == -b
+  } else {
+    fe h2, h3, v, t;
+    fe_sqr(h2, h);
+    fe_mul(h3, h2, h);
+    fe_mul(v, a.x, h2);             // V = X1*H^2
+    fe_mul(a.z, a.z, h);            // Z3 = Z1*H
+    fe_sqr(t, rr);
+    fe_sub(t, t, h3);
+    fe_sub(t, t, v);
+    fe_sub(a.x, t, v);              // X3 = R^2 - H^3 - 2V
+    fe_sub(t, v, a.x);
+    fe_mul(t, rr, t);
+    fe_mul(h3, a.y, h3);
+    fe_sub(a.y, t, h3);             // Y3 = R(V - X3) - Y1*H^3
   }
-  fe h2, h3, v, t;
-  fe_sqr(h2, h);
-  fe_mul(h3, h2, h);
-  fe_mul(v, a.x, h2);             // V = X1*H^2
-  fe_mul(a.z, a.z, h);            // Z3 = Z1*H
-  fe_sqr(t, rr);
-  fe_sub(t, t, h3);
-  fe_sub(t, t, v);
-  fe_sub(a.x, t, v);              // X3 = R^2 - H^3 - 2V
-  fe_sub(t, v, a.x);
-  fe_mul(t, rr, t);
-  fe_mul(h3, a.y, h3);
-  fe_sub(a.y, t, h3);             // Y3 = R(V - X3) - Y1*H^3
+  if (dbl) gej_double(a, a);        // a == b: a + b = 2a (a untouched above)
 }
 
 // a += (x2, y2) affine (same curve as a).  a finite.

@@ -181,7 +181,10 @@ def main():
             forced.append((a, b, N - 1))
     for (a, b, dq) in [(1, 1, 2), (2, 1, 3), (lam, 1, 1), (1, lam, 1), (lam, lam, 1), (N - 1, 2, 1),
                        (2**128 - 1, 2**128 - 1, 1), (2**128, 1, 1), (1, 2**128, 1), (N - 2**128, 1, 1),
-                       (16, 1, 240), (1, 1, N - 2), (3, 5, 7), (2**127, 2**127, 1)]:
+                       (16, 1, 240), (1, 1, N - 2), (3, 5, 7), (2**127, 2**127, 1),
+                       # Booth extremes: +128 in an 8-bit G window, +8 in a 4-bit Q window
+                       (0x7F80, 3, 1), (0x7F807F80, 0x78, 5), (0x7F80 << 64, 0x7878, 1),
+                       (N - 0x7F80, 0x78 << 100, 9), (0x7F80 << 112, 2**127 + 0x78, 1)]:
         forced.append((a, b, dq))
     for (u1, u2, dq) in forced:
         Q = R.point_mul(dq, G)
