@@ -4,8 +4,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define GV_GTAB_N 128           // multiples 1..128 of G (signed 8-bit windows)
-#define GV_QTAB_WORDS 192       // per-lane Q table words: 8 entries x (x, y, z-ratio)
+#define GV_GW 10                // G / lambda*G signed window width (bits)
+#define GV_QW 5                 // Q / lambda*Q signed window width (bits)
+#define GV_GTAB_N 512           // multiples 1..2^(GV_GW-1) of G (LDS table, 32 KiB)
+#define GV_QTAB_N 16            // multiples 1..2^(GV_QW-1) of Q per lane
+#define GV_QTAB_WORDS (GV_QTAB_N * 24)   // per entry: x, y, z-ratio scratch (8 words each)
+#define GV_QWIN 26              // Q windows over a 128-bit GLV half: positions 0,5,..,125
+#define GV_GWIN 13              // G windows: positions 0,10,..,120 (= even Q windows)
+#define GV_DIGIT_ROWS (GV_QWIN + GV_GWIN)
 #define GV_INV_M 16             // signatures folded per lane by k_scalar_inv
 
 #ifdef __cplusplus

@@ -174,13 +174,15 @@ GV_DEV int booth_digit(const u32 k[4], int win) {
   return mag - (int)((v >> W) << (W - 1));
 }
 
-// One lane's Q table: (j+1)*Q for j = 0..7 in the isomorphic-curve affine
-// representation with a shared Z (returned in zq).  qt layout:
+// One lane's Q table: (j+1)*Q for j = 0..GV_QTAB_N-1 in the isomorphic-curve
+// affine representation with a shared Z (returned in zq).  qt layout:
 // qt[(j*24 + c) * C + g], c = 0..7 x, 8..15 y, 16..23 z-ratio scratch.
+// Built as P1 = Q, P2 = 2Q, P_{k+1} = P_k + Q (mixed adds; no exceptional case:
+// (k)Q == +-Q would need (k-1)Q or (k+1)Q == O for k+1 <= 16 < n), then every
+// entry is scaled to the last entry's Z by back-propagating the Z ratios.
 GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx, const fe& qy, fe& zq) {
   gej p;
   p.x = qx; p.y = qy; fe_set_u32(p.z, 1);
-  // entry 0: Q itself with Z = 1 ; ratio Z2/Z1 = 2*qy
   store_fe(qt + 0 * C, C, g, p.x);
   store_fe(qt + 8 * (size_t)C, C, g, p.y);
   gej_double(p, p);                                   // 2Q, Z2 = 2*qy
@@ -188,13 +190,11 @@ GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx, const fe& qy, fe&
     fe ratio; fe_dbl(ratio, qy);
     store_fe(qt + 16 * (size_t)C, C, g, ratio);
   }
-  for (int j = 1; j < 8; ++j) {
+  for (int j = 1; j < GV_QTAB_N; ++j) {
     u32* ent = qt + (size_t)j * 24 * C;
     store_fe(ent, C, g, p.x);
     store_fe(ent + 8 * (size_t)C, C, g, p.y);
-    if (j == 7) break;
-    // P_{j+2} = P_{j+1} + Q ; Z ratio = H (Z3 = Z1*H); no exceptional case:
-    // (j+1)Q == +-Q would need jQ or (j+2)Q == O for j+2 <= 8 < n.
+    if (j == GV_QTAB_N - 1) break;
     fe z2, u2, s2, h, rr, h2, h3, v, t;
     fe_sqr(z2, p.z);
     fe_mul(u2, qx, z2);
@@ -202,7 +202,7 @@ GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx, const fe& qy, fe&
     fe_mul(s2, qy, z2);
     fe_sub(h, u2, p.x);
     fe_sub(rr, s2, p.y);
-    store_fe(ent + 16 * (size_t)C, C, g, h);
+    store_fe(ent + 16 * (size_t)C, C, g, h);          // Z_{j+2} / Z_{j+1} = H
     fe_sqr(h2, h);
     fe_mul(h3, h2, h);
     fe_mul(v, p.x, h2);
@@ -216,15 +216,14 @@ GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx, const fe& qy, fe&
     fe_mul(h3, p.y, h3);
     fe_sub(p.y, t, h3);
   }
-  zq = p.z;                                           // Z8 = shared Z
-  // back-propagate: entry j gets scaled by (Z8/Z_{j+1})^2, ^3
+  zq = p.z;                                           // shared Z
   fe acc;
   fe_set_u32(acc, 1);
-  for (int j = 6; j >= 0; --j) {
+  for (int j = GV_QTAB_N - 2; j >= 0; --j) {
     u32* ent = qt + (size_t)j * 24 * C;
     fe ratio, x, y, a2, a3;
     load_fe(ratio, ent + 16 * (size_t)C, C, g);
-    fe_mul(acc, acc, ratio);
+    fe_mul(acc, acc, ratio);                          // acc = Z_last / Z_{j+1}
     fe_sqr(a2, acc);
     fe_mul(a3, a2, acc);
     load_fe(x, ent, C, g);
@@ -366,20 +365,22 @@ __global__ __launch_bounds__(256) void k_prep(u32 C, const u32* in_x, const u32*
   }
 
   // ---- signed fixed-window (Booth) recoding, scalar signs folded in.
-  // digits[win*C + g] packs four two's-complement fields: dQ1 bits 0..4,
-  // dQ2 bits 5..9 (4-bit windows: digits in [-8, 8]), dG1 bits 10..18, dG2
-  // bits 19..27 (8-bit windows, only on even win: digits in [-128, 128] --
-  // +128 does not fit an int8, hence 9-bit fields).
+  // Q digits (5-bit windows, [-16, 16]): digits[win*C + g] = dQ1 | dQ2 << 16
+  // (int16 halves), win = 0..GV_QWIN-1.  G digits (10-bit windows, [-512,
+  // 512]): digits[(GV_QWIN + j)*C + g] = dG1 | dG2 << 16, j = 0..GV_GWIN-1.
 #pragma unroll
-  for (int win = 0; win <= 32; ++win) {
-    int d0 = booth_digit<4>(k1q, win), d1 = booth_digit<4>(k2q, win), d2 = 0, d3 = 0;
-    if ((win & 1) == 0) { d2 = booth_digit<8>(k1g, win >> 1); d3 = booth_digit<8>(k2g, win >> 1); }
+  for (int win = 0; win < GV_QWIN; ++win) {
+    int d0 = booth_digit<GV_QW>(k1q, win), d1 = booth_digit<GV_QW>(k2q, win);
     if (n1q) d0 = -d0;
     if (n2q) d1 = -d1;
+    digits[(size_t)win * C + g] = ((u32)d0 & 0xFFFFu) | ((u32)d1 << 16);
+  }
+#pragma unroll
+  for (int j = 0; j < GV_GWIN; ++j) {
+    int d2 = booth_digit<GV_GW>(k1g, j), d3 = booth_digit<GV_GW>(k2g, j);
     if (n1g) d2 = -d2;
     if (n2g) d3 = -d3;
-    digits[(size_t)win * C + g] = ((u32)d0 & 0x1Fu) | (((u32)d1 & 0x1Fu) << 5) | (((u32)d2 & 0x1FFu) << 10) |
-                                  (((u32)d3 & 0x1FFu) << 19);
+    digits[(size_t)(GV_QWIN + j) * C + g] = ((u32)d2 & 0xFFFFu) | ((u32)d3 << 16);
   }
   flags[g] = (ok ? 1u : 0u) | (r_small ? 2u : 0u);
 
@@ -420,7 +421,7 @@ GV_DEV void add_entry(gej& acc, bool& inf, const fe& x, const fe& y, const fe* z
 __global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, const u32* digits,
                                                  const u32* qt, const u32* zq_in, const u32* flags,
                                                  const u32* in_r, uint64_t* bits) {
-  __shared__ u32 gt[GV_GTAB_N * 16];
+  __shared__ u32 gt[GV_GTAB_N * 16];          // 32 KiB: (e+1)*G, e = 0..511
   for (u32 i = threadIdx.x; i < GV_GTAB_N * 16; i += blockDim.x) gt[i] = gtab[i];
   __syncthreads();
 
@@ -432,21 +433,21 @@ __global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, c
   fe_set_zero(acc.x); fe_set_zero(acc.y); fe_set_zero(acc.z);
   bool inf = true;
 
+  // Strauss ladder: Q windows at bit 5*win, G windows at bit 10*j = 5*(2j).
 #pragma unroll 1
-  for (int win = 32; win >= 0; --win) {
-    if (win != 32) {
+  for (int win = GV_QWIN - 1; win >= 0; --win) {
+    if (win != GV_QWIN - 1) {
 #pragma unroll 1
-      for (int d = 0; d < 4; ++d) gej_double(acc, acc);
+      for (int d = 0; d < GV_QW; ++d) gej_double(acc, acc);
     }
-    const u32 dw = digits[(size_t)win * C + g];
-    const int nslots = (win & 1) ? 2 : 4;
+    const bool gwin = (win & 1) == 0;
+    const u32 dq = digits[(size_t)win * C + g];
+    const u32 dg = gwin ? digits[(size_t)(GV_QWIN + (win >> 1)) * C + g] : 0u;
+    const int nslots = gwin ? 4 : 2;
 #pragma unroll 1
     for (int slot = 0; slot < nslots; ++slot) {
-      // sign-extend field `slot` (see the packing in k_prep)
-      const int d = slot == 0 ? ((int)(dw << 27) >> 27)
-                  : slot == 1 ? ((int)(dw << 22) >> 27)
-                  : slot == 2 ? ((int)(dw << 13) >> 23)
-                              : ((int)(dw << 4) >> 23);
+      const u32 dw = slot < 2 ? dq : dg;
+      const int d = (slot & 1) ? ((int)dw >> 16) : ((int)(dw << 16) >> 16);
       if (d == 0) continue;
       const u32 e = (u32)((d < 0 ? -d : d) - 1);
       fe x, y;

@@ -26,7 +26,7 @@ namespace {
     if (e_ != hipSuccess) return GV_EHIP;         \
   } while (0)
 
-constexpr size_t kLaneWords = 8 + 1 + 8 + 8 + 8 + 33 + 8 + 1 + GV_QTAB_WORDS;
+constexpr size_t kLaneWords = 8 + 1 + 8 + 8 + 8 + GV_DIGIT_ROWS + 8 + 1 + GV_QTAB_WORDS;
 
 struct Dev {
   int id = 0;
@@ -69,7 +69,7 @@ int ensure_cap(Dev* d, size_t C) {
   d->in_r = (uint32_t*)take(C * 8 * 4);
   d->in_s = (uint32_t*)take(C * 8 * 4);
   d->in_e = (uint32_t*)take(C * 8 * 4);
-  d->digits = (uint32_t*)take(C * 33 * 4);
+  d->digits = (uint32_t*)take(C * GV_DIGIT_ROWS * 4);
   d->zq = (uint32_t*)take(C * 8 * 4);
   d->flags = (uint32_t*)take(C * 4);
   d->qtab = (uint32_t*)take(C * GV_QTAB_WORDS * 4);

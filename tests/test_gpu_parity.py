@@ -268,3 +268,15 @@ def test_pubkey_class_mirror():
     assert pk.verify_bytes(msg, sig) is True
     assert pk.verify_bytes(msg + b" ", sig) is False
     assert pk.verify_bytes(msg, sig[:63]) is False
+
+
+def test_multi_device_split_and_gather():
+    """gv_open with two device slots (here: the same GPU twice) exercises the
+    host-side slicing, per-device worker threads and bitmap gather."""
+    pub, sig, dig = make_random_batch(3001, seed=77, adversarial=0.25, nkeys=13)
+    want = O.verify_digests(pub, sig, dig, threads=16)
+    with gvm.Verifier([0, 0]) as v2:
+        assert v2.num_devices == 2
+        assert np.array_equal(v2.verify_batch_digests(pub, sig, dig), want)
+        bits = v2.verify_batch_digests_bits(pub, sig, dig)
+        assert np.array_equal(np.unpackbits(bits.view(np.uint8), bitorder="little")[:3001], want)
