@@ -1,0 +1,143 @@
+"""gvhost.py -- ctypes binding of libgvhost.so (host/gvhost.h), the C++ mirror
+of the reference's signature-verification ante decorators over libgpuverify.
+
+  HostApp.ante(tx)        SetPubKey -> ValidateSigCount -> SigGasConsume ->
+                          BatchSigVerification -> IncrementSequence
+                          (x/auth/ante/ante.go:13-31, sigverify.go)
+  HostApp.preverify(txs)  block pre-verification hook
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import gpuverify as gvm
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libgvhost.so")
+
+GVH_OK, GVH_EINVAL, GVH_EDEVICE, GVH_ENOVERIFIER = 0, -1, -2, -3
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_uint32), ("codespace", ctypes.c_char * 16), ("log", ctypes.c_char * 512),
+                ("gas_used", ctypes.c_uint64), ("gpu_leaves", ctypes.c_uint32), ("cache_hits", ctypes.c_uint32)]
+
+    def as_dict(self):
+        return {"code": self.code, "codespace": self.codespace.decode(), "log": self.log.decode(),
+                "gas_used": self.gas_used, "gpu_leaves": self.gpu_leaves, "cache_hits": self.cache_hits}
+
+
+_L = None
+
+
+def lib():
+    global _L
+    if _L is None:
+        gvm.load()                       # libgvhost links libgpuverify
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u64, sz = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t
+        L.gvh_app_new.restype = vp
+        L.gvh_app_new.argtypes = [vp]
+        L.gvh_app_free.argtypes = [vp]
+        L.gvh_set_params.argtypes = [vp, u64, u64, u64]
+        L.gvh_set_context.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int, u64]
+        L.gvh_set_account.argtypes = [vp, ctypes.c_char_p, u64, u64, ctypes.c_char_p, sz]
+        L.gvh_get_account.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(u64), ctypes.POINTER(u64), vp,
+                                      ctypes.POINTER(sz)]
+        L.gvh_ante.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_int, ctypes.POINTER(Result)]
+        L.gvh_preverify.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), ctypes.POINTER(sz)]
+        L.gvh_consume_sig_gas.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p, sz, u64, ctypes.POINTER(Result)]
+        L.gvh_cache_clear.argtypes = [vp]
+        L.gvh_cache_size.argtypes = [vp]
+        L.gvh_cache_size.restype = sz
+        L.gvh_std_sign_bytes.argtypes = [ctypes.c_char_p, u64, u64, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p),
+                                         sz, ctypes.c_char_p, vp, sz]
+        L.gvh_std_sign_bytes.restype = sz
+        L.gvh_pubkey_address.argtypes = [ctypes.c_char_p, sz, vp]
+        L.gvh_bech32_address.argtypes = [ctypes.c_char_p, vp, sz]
+        L.gvh_bech32_address.restype = sz
+        _L = L
+    return _L
+
+
+def pubkey_address(pub_amino: bytes) -> bytes:
+    out = ctypes.create_string_buffer(20)
+    if lib().gvh_pubkey_address(pub_amino, len(pub_amino), out) != 0:
+        raise ValueError("malformed amino pubkey")
+    return out.raw
+
+
+def bech32_address(addr20: bytes) -> str:
+    out = ctypes.create_string_buffer(128)
+    lib().gvh_bech32_address(addr20, out, 128)
+    return out.value.decode()
+
+
+def std_sign_bytes(chain_id: str, accnum: int, seq: int, fee_json: str, msgs_json, memo: str) -> bytes:
+    arr = (ctypes.c_char_p * max(1, len(msgs_json)))(*[m.encode() for m in msgs_json])
+    n = lib().gvh_std_sign_bytes(chain_id.encode(), accnum, seq, fee_json.encode(), arr, len(msgs_json),
+                                 memo.encode(), None, 0)
+    buf = ctypes.create_string_buffer(n)
+    lib().gvh_std_sign_bytes(chain_id.encode(), accnum, seq, fee_json.encode(), arr, len(msgs_json), memo.encode(),
+                             buf, n)
+    return buf.raw
+
+
+class HostApp:
+    def __init__(self, verifier: gvm.Verifier | None = None, chain_id: str = "gv-test", height: int = 1):
+        self._L = lib()
+        self._v = verifier
+        self._app = self._L.gvh_app_new(verifier._ctx if verifier is not None else None)
+        self.set_context(chain_id, height)
+
+    def close(self):
+        if self._app:
+            self._L.gvh_app_free(self._app)
+            self._app = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_params(self, tx_sig_limit=7, cost_secp=1000, cost_ed=590):
+        self._L.gvh_set_params(self._app, tx_sig_limit, cost_secp, cost_ed)
+
+    def set_context(self, chain_id: str, height: int = 1, recheck: bool = False, gas_limit: int = 0):
+        self._L.gvh_set_context(self._app, chain_id.encode(), height, int(recheck), gas_limit)
+
+    def set_account(self, addr20: bytes, number: int, sequence: int, pub_amino: bytes = b""):
+        self._L.gvh_set_account(self._app, addr20, number, sequence, pub_amino or None, len(pub_amino))
+
+    def get_account(self, addr20: bytes):
+        num, seq, ln = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_size_t()
+        buf = ctypes.create_string_buffer(512)
+        if not self._L.gvh_get_account(self._app, addr20, ctypes.byref(num), ctypes.byref(seq), buf, ctypes.byref(ln)):
+            return None
+        return {"number": num.value, "sequence": seq.value, "pub": buf.raw[:ln.value]}
+
+    def ante(self, tx: bytes, simulate: bool = False):
+        r = Result()
+        rc = self._L.gvh_ante(self._app, tx, len(tx), int(simulate), ctypes.byref(r))
+        return rc, r.as_dict()
+
+    def preverify(self, txs):
+        arr = (ctypes.c_char_p * len(txs))(*txs)
+        lens = (ctypes.c_size_t * len(txs))(*[len(t) for t in txs])
+        n = ctypes.c_size_t()
+        rc = self._L.gvh_preverify(self._app, len(txs), arr, lens, ctypes.byref(n))
+        return rc, n.value
+
+    def consume_sig_gas(self, sig: bytes, pub_amino: bytes | None, gas_limit: int = 0):
+        r = Result()
+        self._L.gvh_consume_sig_gas(self._app, sig, len(sig), pub_amino, len(pub_amino or b""), gas_limit,
+                                    ctypes.byref(r))
+        return r.as_dict()
+
+    def cache_size(self) -> int:
+        return self._L.gvh_cache_size(self._app)
+
+    def cache_clear(self):
+        self._L.gvh_cache_clear(self._app)

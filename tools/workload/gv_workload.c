@@ -237,3 +237,35 @@ long long gvw_msgsend_signbytes(size_t n, const uint8_t* pub33, size_t nkeys, ui
 void gvw_sha256_msgs(size_t n, const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint8_t* out32) {
   for (size_t i = 0; i < n; ++i) SHA256(blob + off[i], len[i], out32 + 32 * i);
 }
+
+/* single-item helpers for the client-side tx kit (cosmos-sdk-rootchain_amd/txkit.py) */
+int gvw_pubkey(const uint8_t priv32[32], uint8_t pub33[33]) {
+  EC_GROUP* grp = EC_GROUP_new_by_curve_name(NID_secp256k1);
+  BN_CTX* ctx = BN_CTX_new();
+  BIGNUM* d = BN_bin2bn(priv32, 32, NULL);
+  EC_POINT* pt = EC_POINT_new(grp);
+  int ok = EC_POINT_mul(grp, pt, d, NULL, NULL, ctx) == 1 &&
+           EC_POINT_point2oct(grp, pt, POINT_CONVERSION_COMPRESSED, pub33, 33, ctx) == 33;
+  EC_POINT_free(pt); BN_free(d); BN_CTX_free(ctx); EC_GROUP_free(grp);
+  return ok ? 0 : -1;
+}
+
+/* ECDSA over a 32-byte digest, low-S normalised (tendermint Sign): R||S */
+int gvw_sign_digest(const uint8_t priv32[32], const uint8_t dig32[32], uint8_t sig64[64]) {
+  EC_KEY* key = EC_KEY_new_by_curve_name(NID_secp256k1);
+  BIGNUM *d = BN_bin2bn(priv32, 32, NULL), *n = NULL, *half = BN_new(), *s2 = BN_new();
+  BN_hex2bn(&n, N_HEX); BN_rshift1(half, n);
+  EC_KEY_set_private_key(key, d);
+  ECDSA_SIG* sg = ECDSA_do_sign(dig32, 32, key);
+  int rc = -1;
+  if (sg) {
+    const BIGNUM *r, *s;
+    ECDSA_SIG_get0(sg, &r, &s);
+    if (BN_cmp(s, half) > 0) BN_sub(s2, n, s); else BN_copy(s2, s);
+    BN_bn2binpad(r, sig64, 32); BN_bn2binpad(s2, sig64 + 32, 32);
+    ECDSA_SIG_free(sg);
+    rc = 0;
+  }
+  BN_free(d); BN_free(n); BN_free(half); BN_free(s2); EC_KEY_free(key);
+  return rc;
+}
