@@ -115,6 +115,22 @@ def checktx_latency(ver, pub, sig, dig, sizes=(1, 16, 32, 64, 128, 256), reps=20
     return out
 
 
+PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_latest.json")
+
+
+def load_pmc(kernel):
+    """Per-item HBM bytes / VALU counters of `kernel` from the committed PMC summary
+    (tools/pmc_summary.py over tools/pmc_round.sh); None if absent."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+        e = dict(d["kernels"][kernel])
+        e["source"] = d["source"]
+        return e
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -196,6 +212,8 @@ def main():
     ms_per_step = elapsed_max / args.steps * 1e3
 
     achieved = n * W_ECMULT / (ecmult_ms * 1e-3) if ecmult_ms > 0 else 0.0
+    pmc = load_pmc("k_ecmult")
+    traffic = round(pmc["hbm_bytes_per_item"] * n) if pmc else None
     result = {
         "metric": "secp256k1 verifies/sec at 1/2/4/8 MI355X; p50 latency @64-tx CheckTx batch",
         "value": round(value, 1),
@@ -220,12 +238,18 @@ def main():
             "peak": round(P_MUL / 1e12, 3),
             "unit": "Tmul32/s",
             "frac": round(achieved / P_MUL, 4) if achieved else None,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes per launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE, scaled per item)",
+            "traffic_source": pmc["source"] if pmc else None,
+            "hbm_gbps_at_traffic": round(traffic / (ecmult_ms * 1e-3) / 1e9, 1) if (pmc and ecmult_ms > 0) else None,
+            "valu_insts_per_verify": round(pmc["valu_insts_per_item"]) if pmc else None,
+            "valu_busy_frac": round(pmc["valu_busy_frac"], 3) if pmc else None,
             "work_per_verify": W_ECMULT,
             "kernel_ms": round(ecmult_ms, 3),
             "launches_averaged": cnt,
             "note": "achieved = items x W_ecmult products / avg k_ecmult duration (HIP events on the launch "
-                    "stream); peak = measured v_mad_u64_u32 chip rate; HBM is not the bound (<200 B/verify)",
+                    "stream); peak = measured v_mad_u64_u32 chip rate; traffic / VALU counters from the committed "
+                    "rocprofv3 --pmc passes of this bench command (tools/pmc_round.sh)",
         },
         "pipeline": {"unpack_ms": round(unpack_ms, 3), "prep_ms": round(prep_ms, 3), "ecmult_ms": round(ecmult_ms, 3),
                      "whole_verify_roofline_frac": round(value / world * W_MUL / P_MUL, 4)},

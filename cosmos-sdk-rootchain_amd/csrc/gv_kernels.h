@@ -4,15 +4,19 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define GV_GW 10                // G / lambda*G signed window width (bits)
+#define GV_GW 15                // G / lambda*G signed window width (bits)
 #define GV_QW 5                 // Q / lambda*Q signed window width (bits)
-#define GV_GTAB_N 512           // multiples 1..2^(GV_GW-1) of G (LDS table, 32 KiB)
+#define GV_GTAB_N (1 << (GV_GW - 1))   // multiples 1..2^(GV_GW-1) per table: 16384 x 64 B = 1 MiB
+#define GV_GSTEP (GV_GW / GV_QW)       // Q windows per G window
 #define GV_QTAB_N 16            // multiples 1..2^(GV_QW-1) of Q per lane
-#define GV_QTAB_WORDS (GV_QTAB_N * 24)   // per entry: x, y, z-ratio scratch (8 words each)
+#define GV_QTAB_WORDS (GV_QTAB_N * 16 + (GV_QTAB_N - 1) * 8)  // per lane: entries x,y (AoS) + Z-ratio rows (SoA)
 #define GV_QWIN 26              // Q windows over a 128-bit GLV half: positions 0,5,..,125
-#define GV_GWIN 13              // G windows: positions 0,10,..,120 (= even Q windows)
+#define GV_GWIN 9               // G windows: positions 0,15,..,120 (every GV_GSTEP-th Q window)
 #define GV_DIGIT_ROWS (GV_QWIN + GV_GWIN)
 #define GV_INV_M 16             // signatures folded per lane by k_scalar_inv
+
+static_assert(GV_GW % GV_QW == 0, "G windows must sit on Q window positions");
+static_assert(GV_GW * GV_GWIN >= 130 && GV_GW * (GV_GWIN - 1) <= GV_QW * (GV_QWIN - 1), "G window count");
 
 #ifdef __cplusplus
 extern "C" {
@@ -28,9 +32,9 @@ typedef struct gvk_batch {
   const uint8_t* msg_blob;
   const uint64_t* msg_off;
   const uint32_t* msg_len;
-  const uint32_t* gtab;
+  const uint32_t* gtab;         // 2 tables (G, lambda*G) x GV_GTAB_N entries x 16 words, AoS
   uint32_t *in_x, *in_pfx, *in_r, *in_s, *in_e;
-  uint32_t *digits;             // 33 rows: packed Booth digits per window (16 rows reused as scratch)
+  uint32_t *digits;             // GV_DIGIT_ROWS rows: packed Booth digits per window (16 rows reused as scratch)
   uint32_t *zq, *flags, *qtab;  // shared Z of the Q table (8 rows), flags, Q table (192 rows)
   uint64_t* bits;               // C/64 words, bit (i%64) of word i/64
   hipEvent_t ev[3];             // optional: after unpack/sha, after prep, after ecmult

@@ -9,14 +9,16 @@
 // Pipeline for a batch of C lanes (C = capacity rounded up to 256):
 //   k_unpack      AoS bytes (pub33, sig64, dig32) -> SoA 32-bit limbs, via LDS
 //   k_sha256      (message path) one StdSignBytes message per lane -> e limbs
+//   k_scalar_inv  s^-1 mod n by Montgomery batch inversion (16 per lane + wave scan)
 //   k_prep        pubkey decompression (sqrt), r/s/low-S range checks,
-//                 s^-1 by Montgomery batch inversion across the wavefront,
-//                 u1 = e*w, u2 = r*w, GLV split of u1 and u2 (4 x 128-bit)
-//   k_ecmult      per-lane table of Q multiples (effective affine, shared Z),
-//                 Strauss double-scalar multiplication with signed (Booth)
-//                 fixed windows: 4-bit for Q/lambda*Q, 8-bit for G/lambda*G from
-//                 an LDS-resident table; final x-coordinate check without
-//                 inversion (X == r*Z^2 or (r+n)*Z^2); accept bitmap by ballot.
+//                 u1 = e*w, u2 = r*w, GLV split of u1 and u2 (4 x 128-bit),
+//                 signed (Booth) window digits, per-lane table of Q multiples
+//                 (effective affine, shared Z)
+//   k_ecmult      Strauss double-scalar multiplication: 5-bit windows for
+//                 Q/lambda*Q from the lane's table, 15-bit windows for G and
+//                 lambda*G from two 1 MiB global (L2-resident) tables; final
+//                 x-coordinate check without inversion (X == r*Z^2 or
+//                 (r+n)*Z^2); accept bitmap by ballot.
 //
 // SoA layout: limb i of item g lives at base[i*C + g] -> every per-limb access
 // of a wave is one coalesced 256-byte transaction.
@@ -54,7 +56,8 @@ GV_DEV void fe_from_const(fe& r, const u32* c) {
 
 // ---------------------------------------------------------------- k_gen_gtable
 // gtab[e*16 + c]: e = 0..GV_GTAB_N-1 holds (e+1)*G affine, canonical; c = 0..7 x
-// limbs, 8..15 y limbs.  Run once per context.
+// limbs, 8..15 y limbs; gtab[(GV_GTAB_N + e)*16 + c] holds (e+1)*lambda*G =
+// (beta*x, y).  Run once per context.
 __global__ void k_gen_gtable(u32* gtab) {
   const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= GV_GTAB_N) return;
@@ -78,8 +81,14 @@ __global__ void k_gen_gtable(u32* gtab) {
   fe_mul(y, acc.y, zi3);
   fe_normalize(x);
   fe_normalize(y);
+  fe beta, lx;
+  fe_from_const(beta, kBeta);
+  fe_mul(lx, x, beta);
+  fe_normalize(lx);
+  u32* t0 = gtab + (size_t)e * 16;
+  u32* t1 = gtab + ((size_t)GV_GTAB_N + e) * 16;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { gtab[e * 16 + i] = x.v[i]; gtab[e * 16 + 8 + i] = y.v[i]; }
+  for (int i = 0; i < 8; ++i) { t0[i] = x.v[i]; t0[8 + i] = y.v[i]; t1[i] = lx.v[i]; t1[8 + i] = y.v[i]; }
 }
 
 // ------------------------------------------------------------------ k_unpack
@@ -175,25 +184,43 @@ GV_DEV int booth_digit(const u32 k[4], int win) {
 }
 
 // One lane's Q table: (j+1)*Q for j = 0..GV_QTAB_N-1 in the isomorphic-curve
-// affine representation with a shared Z (returned in zq).  qt layout:
-// qt[(j*24 + c) * C + g], c = 0..7 x, 8..15 y, 16..23 z-ratio scratch.
+// affine representation with a shared Z (returned in zq).  qt layout: the
+// first C*16*16 words hold the entries lane-major (AoS): lane g, entry j at
+// qt[(g*16 + j)*16 ..], x then y, 64 contiguous bytes, so k_ecmult's per-lane
+// gather of entry d is four 16-byte loads of whole cache-line halves instead of
+// sixteen 4-byte loads spread over sixteen lines.  The Z-ratio scratch follows
+// as SoA rows: qr[(j*8 + c) * C + g].
 // Built as P1 = Q, P2 = 2Q, P_{k+1} = P_k + Q (mixed adds; no exceptional case:
 // (k)Q == +-Q would need (k-1)Q or (k+1)Q == O for k+1 <= 16 < n), then every
 // entry is scaled to the last entry's Z by back-propagating the Z ratios.
+GV_DEV void store_qent(u32* qt, u32 g, int j, const fe& x, const fe& y) {
+  uint4* p = (uint4*)(qt + ((size_t)g * GV_QTAB_N + j) * 16);
+  p[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+  p[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+  p[2] = make_uint4(y.v[0], y.v[1], y.v[2], y.v[3]);
+  p[3] = make_uint4(y.v[4], y.v[5], y.v[6], y.v[7]);
+}
+GV_DEV void load_qent(fe& x, fe& y, const u32* qt, u32 g, u32 j) {
+  const uint4* p = (const uint4*)(qt + ((size_t)g * GV_QTAB_N + j) * 16);
+  uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+  x.v[0] = a.x; x.v[1] = a.y; x.v[2] = a.z; x.v[3] = a.w;
+  x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
+  y.v[0] = c.x; y.v[1] = c.y; y.v[2] = c.z; y.v[3] = c.w;
+  y.v[4] = d.x; y.v[5] = d.y; y.v[6] = d.z; y.v[7] = d.w;
+}
+
 GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx, const fe& qy, fe& zq) {
+  u32* qr = qt + (size_t)C * GV_QTAB_N * 16;         // Z-ratio rows
   gej p;
   p.x = qx; p.y = qy; fe_set_u32(p.z, 1);
-  store_fe(qt + 0 * C, C, g, p.x);
-  store_fe(qt + 8 * (size_t)C, C, g, p.y);
+  store_qent(qt, g, 0, p.x, p.y);
   gej_double(p, p);                                   // 2Q, Z2 = 2*qy
   {
     fe ratio; fe_dbl(ratio, qy);
-    store_fe(qt + 16 * (size_t)C, C, g, ratio);
+    store_fe(qr, C, g, ratio);
   }
   for (int j = 1; j < GV_QTAB_N; ++j) {
-    u32* ent = qt + (size_t)j * 24 * C;
-    store_fe(ent, C, g, p.x);
-    store_fe(ent + 8 * (size_t)C, C, g, p.y);
+    store_qent(qt, g, j, p.x, p.y);
     if (j == GV_QTAB_N - 1) break;
     fe z2, u2, s2, h, rr, h2, h3, v, t;
     fe_sqr(z2, p.z);
@@ -202,7 +229,7 @@ GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx, const fe& qy, fe&
     fe_mul(s2, qy, z2);
     fe_sub(h, u2, p.x);
     fe_sub(rr, s2, p.y);
-    store_fe(ent + 16 * (size_t)C, C, g, h);          // Z_{j+2} / Z_{j+1} = H
+    store_fe(qr + (size_t)j * 8 * C, C, g, h);        // Z_{j+2} / Z_{j+1} = H
     fe_sqr(h2, h);
     fe_mul(h3, h2, h);
     fe_mul(v, p.x, h2);
@@ -220,18 +247,15 @@ GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx, const fe& qy, fe&
   fe acc;
   fe_set_u32(acc, 1);
   for (int j = GV_QTAB_N - 2; j >= 0; --j) {
-    u32* ent = qt + (size_t)j * 24 * C;
     fe ratio, x, y, a2, a3;
-    load_fe(ratio, ent + 16 * (size_t)C, C, g);
+    load_fe(ratio, qr + (size_t)j * 8 * C, C, g);
     fe_mul(acc, acc, ratio);                          // acc = Z_last / Z_{j+1}
     fe_sqr(a2, acc);
     fe_mul(a3, a2, acc);
-    load_fe(x, ent, C, g);
-    load_fe(y, ent + 8 * (size_t)C, C, g);
+    load_qent(x, y, qt, g, j);
     fe_mul(x, x, a2);
     fe_mul(y, y, a3);
-    store_fe(ent, C, g, x);
-    store_fe(ent + 8 * (size_t)C, C, g, y);
+    store_qent(qt, g, j, x, y);
   }
 }
 
@@ -366,8 +390,8 @@ __global__ __launch_bounds__(256) void k_prep(u32 C, const u32* in_x, const u32*
 
   // ---- signed fixed-window (Booth) recoding, scalar signs folded in.
   // Q digits (5-bit windows, [-16, 16]): digits[win*C + g] = dQ1 | dQ2 << 16
-  // (int16 halves), win = 0..GV_QWIN-1.  G digits (10-bit windows, [-512,
-  // 512]): digits[(GV_QWIN + j)*C + g] = dG1 | dG2 << 16, j = 0..GV_GWIN-1.
+  // (int16 halves), win = 0..GV_QWIN-1.  G digits (15-bit windows, [-2^14,
+  // 2^14]): digits[(GV_QWIN + j)*C + g] = dG1 | dG2 << 16, j = 0..GV_GWIN-1.
 #pragma unroll
   for (int win = 0; win < GV_QWIN; ++win) {
     int d0 = booth_digit<GV_QW>(k1q, win), d1 = booth_digit<GV_QW>(k2q, win);
@@ -421,10 +445,6 @@ GV_DEV void add_entry(gej& acc, bool& inf, const fe& x, const fe& y, const fe* z
 __global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, const u32* digits,
                                                  const u32* qt, const u32* zq_in, const u32* flags,
                                                  const u32* in_r, uint64_t* bits) {
-  __shared__ u32 gt[GV_GTAB_N * 16];          // 32 KiB: (e+1)*G, e = 0..511
-  for (u32 i = threadIdx.x; i < GV_GTAB_N * 16; i += blockDim.x) gt[i] = gtab[i];
-  __syncthreads();
-
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   fe zq;
   load_fe(zq, zq_in, C, g);
@@ -433,16 +453,18 @@ __global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, c
   fe_set_zero(acc.x); fe_set_zero(acc.y); fe_set_zero(acc.z);
   bool inf = true;
 
-  // Strauss ladder: Q windows at bit 5*win, G windows at bit 10*j = 5*(2j).
+  // Strauss ladder: Q windows at bit 5*win, G windows at bit 15*j = 5*(3j).
+  // Slots per window: 0 = Q, 1 = lambda*Q (beta*x of the Q entry), and on G
+  // windows 2 = G, 3 = lambda*G (second table).
 #pragma unroll 1
   for (int win = GV_QWIN - 1; win >= 0; --win) {
     if (win != GV_QWIN - 1) {
 #pragma unroll 1
       for (int d = 0; d < GV_QW; ++d) gej_double(acc, acc);
     }
-    const bool gwin = (win & 1) == 0;
+    const bool gwin = (win % GV_GSTEP) == 0;
     const u32 dq = digits[(size_t)win * C + g];
-    const u32 dg = gwin ? digits[(size_t)(GV_QWIN + (win >> 1)) * C + g] : 0u;
+    const u32 dg = gwin ? digits[(size_t)(GV_QWIN + win / GV_GSTEP) * C + g] : 0u;
     const int nslots = gwin ? 4 : 2;
 #pragma unroll 1
     for (int slot = 0; slot < nslots; ++slot) {
@@ -452,17 +474,14 @@ __global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, c
       const u32 e = (u32)((d < 0 ? -d : d) - 1);
       fe x, y;
       if (slot < 2) {
-        const u32* ent = qt + (size_t)e * 24 * C;
-        load_fe(x, ent, C, g);
-        load_fe(y, ent + 8 * (size_t)C, C, g);
+        load_qent(x, y, qt, g, e);
+        if (slot == 1) {                           // lambda * P = (beta * x, y)
+          fe beta;
+          fe_from_const(beta, kBeta);
+          fe_mul(x, x, beta);
+        }
       } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) { x.v[i] = gt[e * 16 + i]; y.v[i] = gt[e * 16 + 8 + i]; }
-      }
-      if (slot & 1) {                            // lambda * P = (beta * x, y)
-        fe beta;
-        fe_from_const(beta, kBeta);
-        fe_mul(x, x, beta);
+        load_qent(x, y, gtab + (slot == 3 ? (size_t)GV_GTAB_N * 16 : 0), 0, e);
       }
       if (d < 0) fe_neg(y, y);
       add_entry(acc, inf, x, y, slot < 2 ? nullptr : &zq);
@@ -572,7 +591,7 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   if (b->msg_blob)
     hipLaunchKernelGGL(gv::k_sha256, grd, blk, 0, st, b->msg_blob, b->msg_off, b->msg_len, b->n, C,
                        b->in_e);
-  if (b->ev[0]) hipEventRecord(b->ev[0], st);
+  if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
   {
     const uint32_t waves = (C / 64 + GV_INV_M - 1) / GV_INV_M;
     // scratch for w and the prefix products: the digit rows.  k_prep reads
@@ -583,10 +602,10 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
     hipLaunchKernelGGL(gv::k_prep, grd, blk, 0, st, C, b->in_x, b->in_pfx, b->in_r, b->in_s, b->in_e,
                        (const uint32_t*)w, b->digits, b->qtab, b->zq, b->flags);
   }
-  if (b->ev[1]) hipEventRecord(b->ev[1], st);
+  if (b->ev[1]) (void)hipEventRecord(b->ev[1], st);
   hipLaunchKernelGGL(gv::k_ecmult, grd, blk, 0, st, b->gtab, b->n, C, b->digits, b->qtab, b->zq, b->flags,
                      b->in_r, b->bits);
-  if (b->ev[2]) hipEventRecord(b->ev[2], st);
+  if (b->ev[2]) (void)hipEventRecord(b->ev[2], st);
   return hipGetLastError();
 }
 

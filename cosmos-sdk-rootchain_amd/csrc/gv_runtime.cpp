@@ -254,7 +254,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
     ctx->devs.push_back(d);
     if (hipSetDevice(id) != hipSuccess ||
         hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&d->gtab, GV_GTAB_N * 16 * 4) != hipSuccess ||
+        hipMalloc(&d->gtab, (size_t)2 * GV_GTAB_N * 16 * 4) != hipSuccess ||
         gvk_gen_gtable(d->gtab, d->st) != hipSuccess ||
         hipStreamSynchronize(d->st) != hipSuccess) {
       gv_close(ctx);

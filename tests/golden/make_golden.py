@@ -173,6 +173,7 @@ def main():
             dv.append(rec("small_q", Q, R.sign_digest(d, dig), dig))
 
     # forced (u1, u2, Q): accumulator meets +-table entry inside the Strauss ladder
+    ALT15 = sum((0x4000 if j % 2 == 0 else 0x3FFF) << (15 * j) for j in range(8))
     forced = []
     small = [1, 2, 3, 5, 8, 9, 16, 17, 127, 128, 129, 256]
     for a in small:
@@ -184,7 +185,11 @@ def main():
                        (16, 1, 240), (1, 1, N - 2), (3, 5, 7), (2**127, 2**127, 1),
                        # Booth extremes: +128 in an 8-bit G window, +8 in a 4-bit Q window
                        (0x7F80, 3, 1), (0x7F807F80, 0x78, 5), (0x7F80 << 64, 0x7878, 1),
-                       (N - 0x7F80, 0x78 << 100, 9), (0x7F80 << 112, 2**127 + 0x78, 1)]:
+                       (N - 0x7F80, 0x78 << 100, 9), (0x7F80 << 112, 2**127 + 0x78, 1),
+                       # Booth extremes of 15-bit G windows: alternating -2^14 / +2^14 digits
+                       (ALT15, 3, 1), ((lam * ALT15) % N, 5, 1), (ALT15 | 2**127, 2, 3),
+                       (ALT15 + (lam * (ALT15 >> 15)) % N, 9, 1), (0x1FFFC000, 1, 7),
+                       ((lam * 0x1FFFC000) % N, 0x78, 1)]:
         forced.append((a, b, dq))
     for (u1, u2, dq) in forced:
         Q = R.point_mul(dq, G)

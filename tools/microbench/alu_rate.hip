@@ -158,6 +158,91 @@ __global__ void k_clock(uint64_t* out, uint32_t seed) {
   if ((x0 ^ x1 ^ x2 ^ x3) == 0x123456789ull) out[0] = 0;
 }
 
+
+// Generic: 8 independent 32-bit ops per iteration, "OP dst, src, dst" shapes.
+#define K8_32(NAME, OPFMT)                                                             \
+__global__ void NAME(uint64_t* out, uint32_t seed) {                                   \
+  uint32_t a = threadIdx.x ^ seed, b = blockIdx.x * 2654435761u + seed;                \
+  uint32_t r0 = a, r1 = b, r2 = a ^ 1, r3 = b ^ 3, r4 = a + 7, r5 = b + 9, r6 = a * 3, r7 = b * 5; \
+  for (int i = 0; i < ITERS; ++i) {                                                    \
+    asm volatile(OPFMT(0) OPFMT(1) OPFMT(2) OPFMT(3) OPFMT(4) OPFMT(5) OPFMT(6) OPFMT(7) \
+      : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(b), "v"(a)); \
+  }                                                                                    \
+  out[blockIdx.x * blockDim.x + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7;  \
+}
+#define F_AND(k) "v_and_b32 %" #k ", %8, %" #k "\n\t"
+#define F_ALIGN(k) "v_alignbit_b32 %" #k ", %8, %" #k ", 26\n\t"
+#define F_LSHR(k) "v_lshrrev_b32 %" #k ", 26, %" #k "\n\t"
+#define F_ADD3(k) "v_add3_u32 %" #k ", %8, %9, %" #k "\n\t"
+#define F_MAD24(k) "v_mad_u32_u24 %" #k ", %8, %9, %" #k "\n\t"
+#define F_MULLO(k) "v_mul_lo_u32 %" #k ", %8, %" #k "\n\t"
+#define F_LSHLADD(k) "v_lshl_add_u32 %" #k ", %8, 3, %" #k "\n\t"
+#define F_BFE(k) "v_bfe_u32 %" #k ", %" #k ", 3, 26\n\t"
+K8_32(k_and, F_AND)
+K8_32(k_align, F_ALIGN)
+K8_32(k_lshr, F_LSHR)
+K8_32(k_add3, F_ADD3)
+K8_32(k_mad24, F_MAD24)
+K8_32(k_mullo, F_MULLO)
+K8_32(k_lshladd, F_LSHLADD)
+K8_32(k_bfe, F_BFE)
+
+// independent add-with-carry-out into distinct SGPR pairs (no VCC chain)
+__global__ void k_addco_ind(uint64_t* out, uint32_t seed) {
+  uint32_t a = threadIdx.x ^ seed, b = blockIdx.x * 2654435761u + seed;
+  uint32_t r0 = a, r1 = b, r2 = a ^ 1, r3 = b ^ 3, r4 = a + 7, r5 = b + 9, r6 = a * 3, r7 = b * 5;
+  uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+  for (int i = 0; i < ITERS; ++i) {
+    asm volatile(
+      "v_add_co_u32 %0, %8, %12, %0\n\t" "v_add_co_u32 %1, %9, %12, %1\n\t"
+      "v_add_co_u32 %2, %10, %12, %2\n\t" "v_add_co_u32 %3, %11, %12, %3\n\t"
+      "v_add_co_u32 %4, %8, %12, %4\n\t" "v_add_co_u32 %5, %9, %12, %5\n\t"
+      "v_add_co_u32 %6, %10, %12, %6\n\t" "v_add_co_u32 %7, %11, %12, %7\n\t"
+      : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7),
+        "+s"(c0), "+s"(c1), "+s"(c2), "+s"(c3) : "v"(b));
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7 ^ c0 ^ c1 ^ c2 ^ c3;
+}
+
+// 64-bit ops: v_lshrrev_b64 and v_lshl_add_u64 (gfx940+), 8 independent
+__global__ void k_lshr64(uint64_t* out, uint32_t seed) {
+  uint64_t a = threadIdx.x ^ seed, b = blockIdx.x * 2654435761ull + seed;
+  uint64_t r0 = a, r1 = b, r2 = a ^ 1, r3 = b ^ 3, r4 = a + 7, r5 = b + 9, r6 = a * 3, r7 = b * 5;
+  for (int i = 0; i < ITERS; ++i) {
+    asm volatile(
+      "v_lshrrev_b64 %0, 1, %0\n\t" "v_lshrrev_b64 %1, 1, %1\n\t" "v_lshrrev_b64 %2, 1, %2\n\t" "v_lshrrev_b64 %3, 1, %3\n\t"
+      "v_lshrrev_b64 %4, 1, %4\n\t" "v_lshrrev_b64 %5, 1, %5\n\t" "v_lshrrev_b64 %6, 1, %6\n\t" "v_lshrrev_b64 %7, 1, %7\n\t"
+      : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7));
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7;
+}
+__global__ void k_lshladd64(uint64_t* out, uint32_t seed) {
+  uint64_t a = threadIdx.x ^ seed, b = blockIdx.x * 2654435761ull + seed;
+  uint64_t r0 = a, r1 = b, r2 = a ^ 1, r3 = b ^ 3, r4 = a + 7, r5 = b + 9, r6 = a * 3, r7 = b * 5;
+  for (int i = 0; i < ITERS; ++i) {
+    asm volatile(
+      "v_lshl_add_u64 %0, %8, 2, %0\n\t" "v_lshl_add_u64 %1, %8, 2, %1\n\t" "v_lshl_add_u64 %2, %8, 2, %2\n\t" "v_lshl_add_u64 %3, %8, 2, %3\n\t"
+      "v_lshl_add_u64 %4, %8, 2, %4\n\t" "v_lshl_add_u64 %5, %8, 2, %5\n\t" "v_lshl_add_u64 %6, %8, 2, %6\n\t" "v_lshl_add_u64 %7, %8, 2, %7\n\t"
+      : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(b));
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7;
+}
+// mad chain with 4 waves/SIMD and ILP 4 (the field-mul regime), 32-bit x 32-bit + 64
+__global__ void k_mad_ilp4(uint64_t* out, uint32_t seed) {
+  uint32_t a = threadIdx.x ^ seed, b = blockIdx.x * 2654435761u + seed;
+  uint64_t r0 = a, r1 = b, r2 = a ^ 1, r3 = b ^ 3;
+  uint64_t cc = 0;
+  for (int i = 0; i < ITERS; ++i) {
+    asm volatile(
+      "v_mad_u64_u32 %0, %4, %5, %6, %0\n\t" "v_mad_u64_u32 %1, %4, %5, %6, %1\n\t"
+      "v_mad_u64_u32 %2, %4, %5, %6, %2\n\t" "v_mad_u64_u32 %3, %4, %5, %6, %3\n\t"
+      "v_mad_u64_u32 %0, %4, %5, %6, %0\n\t" "v_mad_u64_u32 %1, %4, %5, %6, %1\n\t"
+      "v_mad_u64_u32 %2, %4, %5, %6, %2\n\t" "v_mad_u64_u32 %3, %4, %5, %6, %3\n\t"
+      : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+s"(cc) : "v"(a), "v"(b));
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ cc;
+}
+
 typedef void (*kfn)(uint64_t*, uint32_t);
 
 static int run(const char* name, kfn f, int blocks, int threads, uint64_t* d, double per_iter = 8.0) {
@@ -195,6 +280,18 @@ int main() {
   if (run("mad+addc dep-pair 8w/SIMD (products)", k_madc_dep, blocks, threads, d, 4.0)) return 1;
   if (run("mad+addc dep-pair 2w/SIMD (products)", k_madc_dep, 256 * 2, threads, d, 4.0)) return 1;
   if (run("v_mad_u64_u32 ILP8 2w/SIMD", k_mad, 256 * 2, threads, d)) return 1;
+  if (run("v_and_b32", k_and, blocks, threads, d)) return 1;
+  if (run("v_alignbit_b32", k_align, blocks, threads, d)) return 1;
+  if (run("v_lshrrev_b32", k_lshr, blocks, threads, d)) return 1;
+  if (run("v_add3_u32", k_add3, blocks, threads, d)) return 1;
+  if (run("v_mad_u32_u24", k_mad24, blocks, threads, d)) return 1;
+  if (run("v_mul_lo_u32", k_mullo, blocks, threads, d)) return 1;
+  if (run("v_lshl_add_u32", k_lshladd, blocks, threads, d)) return 1;
+  if (run("v_bfe_u32", k_bfe, blocks, threads, d)) return 1;
+  if (run("v_add_co_u32 independent (sgpr carries)", k_addco_ind, blocks, threads, d)) return 1;
+  if (run("v_lshrrev_b64", k_lshr64, blocks, threads, d)) return 1;
+  if (run("v_lshl_add_u64", k_lshladd64, blocks, threads, d)) return 1;
+  if (run("v_mad_u64_u32 ILP4 4w/SIMD", k_mad_ilp4, 256 * 4, threads, d)) return 1;
   {
     int nb = 256 * 8;
     hipLaunchKernelGGL(k_clock, dim3(nb), dim3(256), 0, 0, d, 3u);
