@@ -4,15 +4,17 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define GV_GW 15                // G / lambda*G signed window width (bits)
+#ifndef GV_GW
+#define GV_GW 20                // G / lambda*G signed window width (bits); multiple of GV_QW
+#endif
 #define GV_QW 5                 // Q / lambda*Q signed window width (bits)
-#define GV_GTAB_N (1 << (GV_GW - 1))   // multiples 1..2^(GV_GW-1) per table: 16384 x 64 B = 1 MiB
+#define GV_GTAB_N (1 << (GV_GW - 1))   // multiples 1..2^(GV_GW-1) per table (64 B each)
 #define GV_GSTEP (GV_GW / GV_QW)       // Q windows per G window
 #define GV_QTAB_N 16            // multiples 1..2^(GV_QW-1) of Q per lane
 #define GV_QTAB_WORDS (GV_QTAB_N * 16 + (GV_QTAB_N - 1) * 8)  // per lane: entries x,y (AoS) + Z-ratio rows (SoA)
 #define GV_QWIN 26              // Q windows over a 128-bit GLV half: positions 0,5,..,125
-#define GV_GWIN 9               // G windows: positions 0,15,..,120 (every GV_GSTEP-th Q window)
-#define GV_DIGIT_ROWS (GV_QWIN + GV_GWIN)
+#define GV_GWIN ((GV_QWIN - 1) / GV_GSTEP + 1)   // G windows at positions 0, GV_GW, ..
+#define GV_DIGIT_ROWS (GV_QWIN + 2 * GV_GWIN)    // Q: packed int16 pair per window; G: int32 per digit
 #define GV_INV_M 16             // signatures folded per lane by k_scalar_inv
 
 static_assert(GV_GW % GV_QW == 0, "G windows must sit on Q window positions");

@@ -15,8 +15,8 @@
 //                 signed (Booth) window digits, per-lane table of Q multiples
 //                 (effective affine, shared Z)
 //   k_ecmult      Strauss double-scalar multiplication: 5-bit windows for
-//                 Q/lambda*Q from the lane's table, 15-bit windows for G and
-//                 lambda*G from two 1 MiB global (L2-resident) tables; final
+//                 Q/lambda*Q from the lane's table, GV_GW-bit windows for G and
+//                 lambda*G from two global tables (GV_GW=20: 32 MiB each); final
 //                 x-coordinate check without inversion (X == r*Z^2 or
 //                 (r+n)*Z^2); accept bitmap by ballot.
 //
@@ -183,16 +183,21 @@ GV_DEV int booth_digit(const u32 k[4], int win) {
   return mag - (int)((v >> W) << (W - 1));
 }
 
-// One lane's Q table: (j+1)*Q for j = 0..GV_QTAB_N-1 in the isomorphic-curve
-// affine representation with a shared Z (returned in zq).  qt layout: the
-// first C*16*16 words hold the entries lane-major (AoS): lane g, entry j at
-// qt[(g*16 + j)*16 ..], x then y, 64 contiguous bytes, so k_ecmult's per-lane
-// gather of entry d is four 16-byte loads of whole cache-line halves instead of
-// sixteen 4-byte loads spread over sixteen lines.  The Z-ratio scratch follows
-// as SoA rows: qr[(j*8 + c) * C + g].
-// Built as P1 = Q, P2 = 2Q, P_{k+1} = P_k + Q (mixed adds; no exceptional case:
-// (k)Q == +-Q would need (k-1)Q or (k+1)Q == O for k+1 <= 16 < n), then every
-// entry is scaled to the last entry's Z by back-propagating the Z ratios.
+// One lane's Q table: m*Q for m = 1..GV_QTAB_N in the isomorphic-curve affine
+// representation with a shared Z (returned in zq).  qt layout: the first
+// C*16*16 words hold the entries lane-major (AoS): lane g, entry m at
+// qt[(g*16 + m-1)*16 ..], x then y, 64 contiguous bytes, so k_ecmult's
+// per-lane gather of an entry is four 16-byte loads instead of sixteen 4-byte
+// loads spread over sixteen lines.  The Z-ratio scratch follows as SoA rows:
+// qr[(i*8 + c) * C + g].
+//
+// Built with co-Z arithmetic (Meloni's ZADDU): a co-Z doubling gives 2Q and
+// Q' (Q on the same Z); then each step adds the co-Z pair (Q', mQ) into
+// (m+1)Q and re-expresses Q' on the new Z, for 4M + 2S per step (the new Z,
+// Z*(X1-X2), is never formed: only the ratio X1-X2 is stored).  No exceptional
+// case: X(Q') == X(mQ) would need mQ == +-Q, i.e. n | m -+ 1, for 2 <= m <= 15.
+// Every entry is then scaled to the last entry's Z by back-propagating the
+// ratios, and zq = 2y * prod(ratios) is that Z.
 GV_DEV void store_qent(u32* qt, u32 g, int j, const fe& x, const fe& y) {
   uint4* p = (uint4*)(qt + ((size_t)g * GV_QTAB_N + j) * 16);
   p[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
@@ -211,52 +216,73 @@ GV_DEV void load_qent(fe& x, fe& y, const u32* qt, u32 g, u32 j) {
 
 GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx, const fe& qy, fe& zq) {
   u32* qr = qt + (size_t)C * GV_QTAB_N * 16;         // Z-ratio rows
-  gej p;
-  p.x = qx; p.y = qy; fe_set_u32(p.z, 1);
-  store_qent(qt, g, 0, p.x, p.y);
-  gej_double(p, p);                                   // 2Q, Z2 = 2*qy
+  fe X1, Y1, X2, Y2, t;
   {
-    fe ratio; fe_dbl(ratio, qy);
-    store_fe(qr, C, g, ratio);
+    // co-Z doubling of the affine Q: Z1 = 2y, 2Q = (M^2 - 2S, M(S - X) - 8y^4),
+    // Q' = (S, 8y^4) with S = 4xy^2, M = 3x^2.
+    fe B, E, L, M;
+    fe_sqr(B, qx);
+    fe_sqr(E, qy);
+    fe_sqr(L, E);
+    fe_add(t, qx, E);
+    fe_sqr(t, t);
+    fe_sub(t, t, B);
+    fe_sub(t, t, L);
+    fe_dbl(X1, t);                                    // S
+    fe_dbl(M, B);
+    fe_add(M, M, B);
+    fe_sqr(t, M);
+    fe_sub(t, t, X1);
+    fe_sub(X2, t, X1);
+    fe_dbl(L, L);
+    fe_dbl(L, L);
+    fe_dbl(Y1, L);                                    // 8y^4
+    fe_sub(t, X1, X2);
+    fe_mul(t, M, t);
+    fe_sub(Y2, t, Y1);
   }
-  for (int j = 1; j < GV_QTAB_N; ++j) {
-    store_qent(qt, g, j, p.x, p.y);
-    if (j == GV_QTAB_N - 1) break;
-    fe z2, u2, s2, h, rr, h2, h3, v, t;
-    fe_sqr(z2, p.z);
-    fe_mul(u2, qx, z2);
-    fe_mul(z2, z2, p.z);
-    fe_mul(s2, qy, z2);
-    fe_sub(h, u2, p.x);
-    fe_sub(rr, s2, p.y);
-    store_fe(qr + (size_t)j * 8 * C, C, g, h);        // Z_{j+2} / Z_{j+1} = H
-    fe_sqr(h2, h);
-    fe_mul(h3, h2, h);
-    fe_mul(v, p.x, h2);
-    fe_mul(p.z, p.z, h);
-    fe_sqr(t, rr);
-    fe_sub(t, t, h3);
-    fe_sub(t, t, v);
-    fe_sub(p.x, t, v);
-    fe_sub(t, v, p.x);
+  store_qent(qt, g, 0, X1, Y1);                       // 1*Q on Z1
+  store_qent(qt, g, 1, X2, Y2);                       // 2*Q on Z1
+  for (int m = 2; m < GV_QTAB_N; ++m) {               // (Q', mQ) -> ((m+1)Q, Q'')
+    fe h, rr, c, w1, w2, d, a1;
+    fe_sub(h, X1, X2);
+    store_fe(qr + (size_t)(m - 2) * 8 * C, C, g, h);  // Z_m / Z_{m-1}
+    fe_sub(rr, Y1, Y2);
+    fe_sqr(c, h);
+    fe_mul(w1, X1, c);
+    fe_mul(w2, X2, c);
+    fe_sqr(d, rr);
+    fe_sub(t, w1, w2);
+    fe_mul(a1, Y1, t);
+    fe_sub(t, d, w1);
+    fe_sub(X2, t, w2);                                // X3 = D - W1 - W2
+    fe_sub(t, w1, X2);
     fe_mul(t, rr, t);
-    fe_mul(h3, p.y, h3);
-    fe_sub(p.y, t, h3);
+    fe_sub(Y2, t, a1);                                // Y3 = (Y1-Y2)(W1-X3) - A1
+    X1 = w1;                                          // Q' on the new Z
+    Y1 = a1;
+    store_qent(qt, g, m, X2, Y2);                     // (m+1)*Q
   }
-  zq = p.z;                                           // shared Z
+  // entry m (index m-1) lives on Z_{m-1} (m >= 2; entry 1 on Z_1); the last
+  // entry on Z_15.  acc = Z_15 / Z(entry m) accumulates the stored ratios.
   fe acc;
-  fe_set_u32(acc, 1);
-  for (int j = GV_QTAB_N - 2; j >= 0; --j) {
-    fe ratio, x, y, a2, a3;
-    load_fe(ratio, qr + (size_t)j * 8 * C, C, g);
-    fe_mul(acc, acc, ratio);                          // acc = Z_last / Z_{j+1}
+  for (int m = GV_QTAB_N - 1; m >= 1; --m) {
+    if (m >= 2) {
+      fe ratio;
+      load_fe(ratio, qr + (size_t)(m - 2) * 8 * C, C, g);
+      if (m == GV_QTAB_N - 1) acc = ratio;
+      else fe_mul(acc, acc, ratio);
+    }
+    fe x, y, a2, a3;
     fe_sqr(a2, acc);
     fe_mul(a3, a2, acc);
-    load_qent(x, y, qt, g, j);
+    load_qent(x, y, qt, g, m - 1);
     fe_mul(x, x, a2);
     fe_mul(y, y, a3);
-    store_qent(qt, g, j, x, y);
+    store_qent(qt, g, m - 1, x, y);
   }
+  fe_dbl(t, qy);
+  fe_mul(zq, t, acc);                                 // Z_15 = 2y * prod(ratios)
 }
 
 // ------------------------------------------------------------- k_scalar_inv
@@ -390,8 +416,9 @@ __global__ __launch_bounds__(256) void k_prep(u32 C, const u32* in_x, const u32*
 
   // ---- signed fixed-window (Booth) recoding, scalar signs folded in.
   // Q digits (5-bit windows, [-16, 16]): digits[win*C + g] = dQ1 | dQ2 << 16
-  // (int16 halves), win = 0..GV_QWIN-1.  G digits (15-bit windows, [-2^14,
-  // 2^14]): digits[(GV_QWIN + j)*C + g] = dG1 | dG2 << 16, j = 0..GV_GWIN-1.
+  // (int16 halves), win = 0..GV_QWIN-1.  G digits (GV_GW-bit windows,
+  // [-2^(GV_GW-1), 2^(GV_GW-1)]) as int32: digits[(GV_QWIN + 2j)*C + g] = dG1,
+  // digits[(GV_QWIN + 2j + 1)*C + g] = dG2, j = 0..GV_GWIN-1.
 #pragma unroll
   for (int win = 0; win < GV_QWIN; ++win) {
     int d0 = booth_digit<GV_QW>(k1q, win), d1 = booth_digit<GV_QW>(k2q, win);
@@ -404,7 +431,8 @@ __global__ __launch_bounds__(256) void k_prep(u32 C, const u32* in_x, const u32*
     int d2 = booth_digit<GV_GW>(k1g, j), d3 = booth_digit<GV_GW>(k2g, j);
     if (n1g) d2 = -d2;
     if (n2g) d3 = -d3;
-    digits[(size_t)(GV_QWIN + j) * C + g] = ((u32)d2 & 0xFFFFu) | ((u32)d3 << 16);
+    digits[(size_t)(GV_QWIN + 2 * j) * C + g] = (u32)d2;
+    digits[(size_t)(GV_QWIN + 2 * j + 1) * C + g] = (u32)d3;
   }
   flags[g] = (ok ? 1u : 0u) | (r_small ? 2u : 0u);
 
@@ -453,7 +481,7 @@ __global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, c
   fe_set_zero(acc.x); fe_set_zero(acc.y); fe_set_zero(acc.z);
   bool inf = true;
 
-  // Strauss ladder: Q windows at bit 5*win, G windows at bit 15*j = 5*(3j).
+  // Strauss ladder: Q windows at bit 5*win, G windows at bit GV_GW*j = 5*(GV_GSTEP*j).
   // Slots per window: 0 = Q, 1 = lambda*Q (beta*x of the Q entry), and on G
   // windows 2 = G, 3 = lambda*G (second table).
 #pragma unroll 1
@@ -464,12 +492,13 @@ __global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, c
     }
     const bool gwin = (win % GV_GSTEP) == 0;
     const u32 dq = digits[(size_t)win * C + g];
-    const u32 dg = gwin ? digits[(size_t)(GV_QWIN + win / GV_GSTEP) * C + g] : 0u;
+    const u32* grow = digits + (size_t)(GV_QWIN + 2 * (win / GV_GSTEP)) * C + g;
+    const u32 dg0 = gwin ? grow[0] : 0u, dg1 = gwin ? grow[C] : 0u;
     const int nslots = gwin ? 4 : 2;
 #pragma unroll 1
     for (int slot = 0; slot < nslots; ++slot) {
-      const u32 dw = slot < 2 ? dq : dg;
-      const int d = (slot & 1) ? ((int)dw >> 16) : ((int)(dw << 16) >> 16);
+      const int d = slot == 0 ? ((int)(dq << 16) >> 16) : slot == 1 ? ((int)dq >> 16)
+                  : slot == 2 ? (int)dg0 : (int)dg1;
       if (d == 0) continue;
       const u32 e = (u32)((d < 0 ? -d : d) - 1);
       fe x, y;

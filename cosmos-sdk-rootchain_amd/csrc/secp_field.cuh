@@ -92,7 +92,25 @@ GV_DEV void fe_add(fe& r, const fe& a, const fe& b) { GV_ADD_ASM(r.v, a.v, b.v);
 GV_DEV void fe_sub(fe& r, const fe& a, const fe& b) { GV_SUB_ASM(r.v, a.v, b.v); }
 
 GV_DEV void fe_neg(fe& r, const fe& a) { fe z; fe_set_zero(z); fe_sub(r, z, a); }
-GV_DEV void fe_dbl(fe& r, const fe& a) { fe_add(r, a, a); }
+GV_DEV void fe_dbl(fe& r, const fe& a) { GV_SHL1_ASM(r.v, a.v); }
+
+// r = a * 2^S and r = a - b * 2^S (S = 1..3), r = 3a: limb shifts by
+// v_alignbit and a single fold of the bits above 2^256 -- one sequence instead
+// of S chained additions.  r must not alias the inputs' storage only as far as
+// the asm's early-clobber outputs already guarantee (aliasing is fine in C).
+template <int S> GV_DEV void fe_shl(fe& r, const fe& a) {
+  static_assert(S >= 1 && S <= 3, "shift");
+  if (S == 1) GV_SHL1_ASM(r.v, a.v);
+  else if (S == 2) GV_SHL2_ASM(r.v, a.v);
+  else GV_SHL3_ASM(r.v, a.v);
+}
+template <int S> GV_DEV void fe_sub_shl(fe& r, const fe& a, const fe& b) {
+  static_assert(S >= 1 && S <= 3, "shift");
+  if (S == 1) GV_SUBSHL1_ASM(r.v, a.v, b.v);
+  else if (S == 2) GV_SUBSHL2_ASM(r.v, a.v, b.v);
+  else GV_SUBSHL3_ASM(r.v, a.v, b.v);
+}
+GV_DEV void fe_mul3(fe& r, const fe& a) { GV_MUL3_ASM(r.v, a.v); }
 
 // canonical representative in [0, p)
 GV_DEV void fe_normalize(fe& r) {

@@ -14,30 +14,27 @@ namespace gv {
 struct gej { fe x, y, z; };
 
 // r = 2a (a finite; secp256k1 has no point of order 2 so the result is finite).
-// dbl-2009-l for a = 0: 2M + 5S.  r may alias a.
+// For a = 0 with D = X*B in place of the (X+B)^2 - A - C trick: 3M + 4S, but
+// only six linear steps (x3, x2, x4, one subtraction, two fused
+// "minus 8 times") instead of fourteen chained additions/subtractions:
+//   A = X^2, B = Y^2, C = B^2, D = X*B, E = 3A, F = E^2,
+//   X3 = F - 8D, Y3 = E*(4D - X3) - 8C, Z3 = 2*Y*Z.
+// r may alias a.
 GV_DEV void gej_double(gej& r, const gej& a) {
   fe A, B, C, D, E, t;
   fe_sqr(A, a.x);
   fe_sqr(B, a.y);
   fe_mul(t, a.y, a.z);
-  fe_dbl(r.z, t);                 // Z3 = 2*Y*Z   (a.y, a.z dead from here)
+  fe_shl<1>(r.z, t);              // Z3 = 2*Y*Z   (a.y, a.z dead from here)
   fe_sqr(C, B);
-  fe_add(t, a.x, B);
-  fe_sqr(t, t);
-  fe_sub(t, t, A);
-  fe_sub(t, t, C);
-  fe_dbl(D, t);                   // D = 2((X+B)^2 - A - C)
-  fe_dbl(E, A);
-  fe_add(E, E, A);                // E = 3A
-  fe_sqr(t, E);                   // F = E^2
-  fe_sub(t, t, D);
-  fe_sub(r.x, t, D);              // X3 = F - 2D
+  fe_mul(D, a.x, B);              // (a.x dead from here)
+  fe_mul3(E, A);
+  fe_sqr(t, E);
+  fe_sub_shl<3>(r.x, t, D);       // X3 = F - 8D
+  fe_shl<2>(D, D);
   fe_sub(t, D, r.x);
   fe_mul(t, E, t);
-  fe_dbl(C, C);
-  fe_dbl(C, C);
-  fe_dbl(C, C);
-  fe_sub(r.y, t, C);              // Y3 = E(D - X3) - 8C
+  fe_sub_shl<3>(r.y, t, C);       // Y3 = E*(4D - X3) - 8C
 }
 
 // Shared tail of the mixed additions: given U2, S2 (the added point scaled to
@@ -64,8 +61,7 @@ GV_DEV void gej_add_tail(gej& a, bool& inf, const fe& u2, const fe& s2) {
     fe_mul(a.z, a.z, h);            // Z3 = Z1*H
     fe_sqr(t, rr);
     fe_sub(t, t, h3);
-    fe_sub(t, t, v);
-    fe_sub(a.x, t, v);              // X3 = R^2 - H^3 - 2V
+    fe_sub_shl<1>(a.x, t, v);       // X3 = R^2 - H^3 - 2V
     fe_sub(t, v, a.x);
     fe_mul(t, rr, t);
     fe_mul(h3, a.y, h3);

@@ -174,6 +174,7 @@ def main():
 
     # forced (u1, u2, Q): accumulator meets +-table entry inside the Strauss ladder
     ALT15 = sum((0x4000 if j % 2 == 0 else 0x3FFF) << (15 * j) for j in range(8))
+    ALT20 = sum((0x80000 if j % 2 == 0 else 0x7FFFF) << (20 * j) for j in range(6))
     forced = []
     small = [1, 2, 3, 5, 8, 9, 16, 17, 127, 128, 129, 256]
     for a in small:
@@ -189,7 +190,10 @@ def main():
                        # Booth extremes of 15-bit G windows: alternating -2^14 / +2^14 digits
                        (ALT15, 3, 1), ((lam * ALT15) % N, 5, 1), (ALT15 | 2**127, 2, 3),
                        (ALT15 + (lam * (ALT15 >> 15)) % N, 9, 1), (0x1FFFC000, 1, 7),
-                       ((lam * 0x1FFFC000) % N, 0x78, 1)]:
+                       ((lam * 0x1FFFC000) % N, 0x78, 1),
+                       # ... and of 20-bit G windows: alternating -2^19 / +2^19 digits
+                       (ALT20, 3, 1), ((lam * ALT20) % N, 5, 1), (ALT20 | 2**127, 2, 3),
+                       (ALT20 + (lam * (ALT20 >> 20)) % N, 9, 1), ((0x7FFFF << 20) | (1 << 19), 1, 7)]:
         forced.append((a, b, dq))
     for (u1, u2, dq) in forced:
         Q = R.point_mul(dq, G)

@@ -26,8 +26,11 @@ def test_generated_include_is_current():
 
 
 def test_no_carry_hazards():
-    for g in (G.gen_mul512, G.gen_sqr_cross, G.gen_sqr_finish, G.gen_reduce, G.gen_add, G.gen_sub):
+    for g in (G.gen_mul512, G.gen_sqr_cross, G.gen_sqr_finish, G.gen_reduce, G.gen_add, G.gen_sub, G.gen_mul3):
         assert G.hazard_check(g()) is None, g.__name__
+    for s in (1, 2, 3):
+        assert G.hazard_check(G.gen_shl(s)) is None
+        assert G.hazard_check(G.gen_sub_shl(s)) is None
 
 
 def test_sequences_match_integer_arithmetic():
@@ -44,3 +47,17 @@ def test_sequences_match_integer_arithmetic():
     for t in [0, 2**512 - 1, (2**256 - 1) ** 2, P * P, (P - 1) ** 2] + [rng.randrange(2**512) for _ in range(1500)]:
         r = G.emu_reduce(t)
         assert r < 2**256 and r % P == t % P
+
+
+def test_shift_and_small_multiple_sequences():
+    rng = random.Random(0x5A)
+    vals = EDGE + [rng.randrange(2**256) for _ in range(800)]
+    for a in vals:
+        r = G.emu_mul3(a)
+        assert r < 2**256 and r % P == 3 * a % P
+        for s in (1, 2, 3):
+            r = G.emu_shl(a, s)
+            assert r < 2**256 and r % P == (a << s) % P
+            for b in [rng.choice(vals)] + EDGE[-6:]:
+                r = G.emu_sub_shl(a, b, s)
+                assert r < 2**256 and r % P == (a - (b << s)) % P

@@ -191,6 +191,74 @@ def gen_sub():
     return p
 
 
+def _fold_add(p):
+    """r += v1 * (2^32 + 977) (v1 small), then one more fold of the carry-out."""
+    p("mul24", "v0", "0x3d1", "v1")
+    p("add_co", "%[r0]", "vcc", "%[r0]", "v0")
+    p("addc", "%[r1]", "vcc", "%[r1]", "v1", "vcc")
+    for i in range(2, 8):
+        p("addc", f"%[r{i}]", "vcc", f"%[r{i}]", "0", "vcc")
+    p("addc", "v1", "vcc", "0", "0", "vcc")                     # carry-out (0/1)
+    p("mul24", "v0", "0x3d1", "v1")                             # wrapped: r < 2^(s+34), no further carry
+    p("add_co", "%[r0]", "vcc", "%[r0]", "v0")
+    p("addc", "%[r1]", "vcc", "%[r1]", "v1", "vcc")
+
+
+def gen_shl(s):
+    """r = a * 2^s mod p (weak), 1 <= s <= 8: limb shifts by v_alignbit, one fold."""
+    p = Prog()
+    p("lshr", "v1", str(32 - s), "%[a7]")                       # bits >= 256 (< 2^s)
+    for i in range(7, 0, -1):
+        p("alignbit", f"%[r{i}]", f"%[a{i}]", f"%[a{i - 1}]", str(32 - s))
+    p("lshl", "%[r0]", str(s), "%[a0]")
+    _fold_add(p)
+    return p
+
+
+def gen_mul3():
+    """r = 3a mod p (weak): 2a by v_alignbit, + a in one chain, one fold."""
+    p = Prog()
+    p("lshr", "v1", "31", "%[a7]")
+    for i in range(7, 0, -1):
+        p("alignbit", f"%[r{i}]", f"%[a{i}]", f"%[a{i - 1}]", "31")
+    p("lshl", "%[r0]", "1", "%[a0]")
+    p("add_co", "%[r0]", "vcc", "%[r0]", "%[a0]")
+    for i in range(1, 8):
+        p("addc", f"%[r{i}]", "vcc", f"%[r{i}]", f"%[a{i}]", "vcc")
+    p("addc", "v1", "vcc", "v1", "0", "vcc")                    # bits >= 256: 0..2
+    _fold_add(p)
+    return p
+
+
+def gen_sub_shl(s):
+    """r = a - b * 2^s mod p (weak), 1 <= s <= 8.
+
+    The low 256 bits of b<<s are formed in r and subtracted from a in one borrow
+    chain; top bits and the borrow both stand for multiples of 2^256 == 2^32 + 977,
+    so k = top + borrow copies of (2^32 + 977) are subtracted, and a final borrow
+    is folded once more (the wrapped value is then >= 2^256 - 2^42: no further
+    borrow)."""
+    p = Prog()
+    p("lshr", "v1", str(32 - s), "%[b7]")
+    for i in range(7, 0, -1):
+        p("alignbit", f"%[r{i}]", f"%[b{i}]", f"%[b{i - 1}]", str(32 - s))
+    p("lshl", "%[r0]", str(s), "%[b0]")
+    p("sub_co", "%[r0]", "vcc", "%[a0]", "%[r0]")
+    for i in range(1, 8):
+        p("subb", f"%[r{i}]", "vcc", f"%[a{i}]", f"%[r{i}]", "vcc")
+    p("addc", "v0", "vcc", "v1", "0", "vcc")                    # k = top + borrow
+    p("mul24", "v1", "0x3d1", "v0")
+    p("sub_co", "%[r0]", "vcc", "%[r0]", "v1")
+    p("subb", "%[r1]", "vcc", "%[r1]", "v0", "vcc")
+    for i in range(2, 8):
+        p("subb", f"%[r{i}]", "vcc", f"%[r{i}]", "0", "vcc")
+    p("addc", "v0", "vcc", "0", "0", "vcc")                     # borrow-out (0/1)
+    p("mul24", "v1", "0x3d1", "v0")
+    p("sub_co", "%[r0]", "vcc", "%[r0]", "v1")
+    p("subb", "%[r1]", "vcc", "%[r1]", "v0", "vcc")
+    return p
+
+
 # -------------------------------------------------------------- text output
 def fmt(ins):
     op = ins[0]
@@ -213,6 +281,10 @@ def fmt(ins):
         return f"v_lshlrev_b32 {a[0]}, 1, {a[1]}"
     if op == "lshr31":
         return f"v_lshrrev_b32 {a[0]}, 31, {a[1]}"
+    if op == "lshl":
+        return f"v_lshlrev_b32 {a[0]}, {a[1]}, {a[2]}"
+    if op == "lshr":
+        return f"v_lshrrev_b32 {a[0]}, {a[1]}, {a[2]}"
     if op == "mul24":
         return f"v_mul_u32_u24_e32 {a[0]}, {a[1]}, {a[2]}"
     if op == "add":
@@ -263,6 +335,14 @@ def generate():
                        [f'[r{i}] "=&v"((R)[{i}])' for i in range(8)],
                        [f'[a{i}] "v"((A)[{i}])' for i in range(8)] + [f'[b{i}] "v"((B)[{i}])' for i in range(8)],
                        ['"v0"', '"v1"', '"vcc"']))
+    R8 = [f'[r{i}] "=&v"((R)[{i}])' for i in range(8)]
+    A8 = [f'[a{i}] "v"((A)[{i}])' for i in range(8)]
+    B8 = [f'[b{i}] "v"((B)[{i}])' for i in range(8)]
+    for sh in (1, 2, 3):
+        parts.append(macro(f"GV_SHL{sh}_ASM", ["R", "A"], gen_shl(sh), R8, A8, ['"v0"', '"v1"', '"vcc"']))
+        parts.append(macro(f"GV_SUBSHL{sh}_ASM", ["R", "A", "B"], gen_sub_shl(sh), R8, A8 + B8,
+                           ['"v0"', '"v1"', '"vcc"']))
+    parts.append(macro("GV_MUL3_ASM", ["R", "A"], gen_mul3(), R8, A8, ['"v0"', '"v1"', '"vcc"']))
     return "\n".join(parts)
 
 
@@ -330,6 +410,10 @@ class Machine:
                 self.setv(a[0], self.val(a[1]) << 1)
             elif op == "lshr31":
                 self.setv(a[0], self.val(a[1]) >> 31)
+            elif op == "lshl":
+                self.setv(a[0], self.val(a[2]) << int(a[1]))
+            elif op == "lshr":
+                self.setv(a[0], self.val(a[2]) >> int(a[1]))
             elif op == "mul24":
                 self.setv(a[0], (self.val(a[1]) & 0xFFFFFF) * (self.val(a[2]) & 0xFFFFFF))
             elif op == "add":
@@ -408,6 +492,25 @@ def emu_sub(a, b):
     env = {f"a{i}": v for i, v in enumerate(limbs(a, 8))}
     env.update({f"b{i}": v for i, v in enumerate(limbs(b, 8))})
     m = Machine(env).run(gen_sub())
+    return join([m.r[f"r{i}"] for i in range(8)])
+
+
+def emu_shl(a, sh):
+    env = {f"a{i}": v for i, v in enumerate(limbs(a, 8))}
+    m = Machine(env).run(gen_shl(sh))
+    return join([m.r[f"r{i}"] for i in range(8)])
+
+
+def emu_mul3(a):
+    env = {f"a{i}": v for i, v in enumerate(limbs(a, 8))}
+    m = Machine(env).run(gen_mul3())
+    return join([m.r[f"r{i}"] for i in range(8)])
+
+
+def emu_sub_shl(a, b, sh):
+    env = {f"a{i}": v for i, v in enumerate(limbs(a, 8))}
+    env.update({f"b{i}": v for i, v in enumerate(limbs(b, 8))})
+    m = Machine(env).run(gen_sub_shl(sh))
     return join([m.r[f"r{i}"] for i in range(8)])
 
 

@@ -243,6 +243,56 @@ __global__ void k_mad_ilp4(uint64_t* out, uint32_t seed) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ cc;
 }
 
+// Mixed streams: does a v_mov_b32 next to a 4-cycle op cost its own slot?
+__global__ void k_mad_mov(uint64_t* out, uint32_t seed) {
+  uint32_t a = threadIdx.x ^ seed, b = blockIdx.x * 2654435761u + seed;
+  uint64_t r0 = a, r1 = b, r2 = a ^ 1, r3 = b ^ 3;
+  uint32_t m0 = a, m1 = b, m2 = a + 1, m3 = b + 1;
+  uint64_t cc = 0;
+  for (int i = 0; i < ITERS; ++i) {
+    asm volatile(
+      "v_mad_u64_u32 %0, %8, %9, %10, %0\n\tv_mov_b32 %4, %9\n\t"
+      "v_mad_u64_u32 %1, %8, %9, %10, %1\n\tv_mov_b32 %5, %10\n\t"
+      "v_mad_u64_u32 %2, %8, %9, %10, %2\n\tv_mov_b32 %6, %9\n\t"
+      "v_mad_u64_u32 %3, %8, %9, %10, %3\n\tv_mov_b32 %7, %10\n\t"
+      "v_mad_u64_u32 %0, %8, %9, %10, %0\n\tv_mov_b32 %4, %10\n\t"
+      "v_mad_u64_u32 %1, %8, %9, %10, %1\n\tv_mov_b32 %5, %9\n\t"
+      "v_mad_u64_u32 %2, %8, %9, %10, %2\n\tv_mov_b32 %6, %10\n\t"
+      "v_mad_u64_u32 %3, %8, %9, %10, %3\n\tv_mov_b32 %7, %9\n\t"
+      : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(m0), "+v"(m1), "+v"(m2), "+v"(m3), "+s"(cc)
+      : "v"(a), "v"(b));
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ cc ^ m0 ^ m1 ^ m2 ^ m3;
+}
+__global__ void k_addc_mov(uint64_t* out, uint32_t seed) {
+  uint32_t a = threadIdx.x ^ seed, b = blockIdx.x * 2654435761u + seed;
+  uint32_t r0 = a, r1 = b, r2 = a ^ 1, r3 = b ^ 3, m0 = a, m1 = b, m2 = a + 1, m3 = b + 1;
+  for (int i = 0; i < ITERS; ++i) {
+    asm volatile(
+      "v_add_co_u32 %0, vcc, %8, %0\n\tv_mov_b32 %4, %8\n\t"
+      "v_addc_co_u32 %1, vcc, %8, %1, vcc\n\tv_mov_b32 %5, %0\n\t"
+      "v_addc_co_u32 %2, vcc, %8, %2, vcc\n\tv_mov_b32 %6, %1\n\t"
+      "v_addc_co_u32 %3, vcc, %8, %3, vcc\n\tv_mov_b32 %7, %2\n\t"
+      "v_addc_co_u32 %0, vcc, %8, %0, vcc\n\tv_mov_b32 %4, %3\n\t"
+      "v_addc_co_u32 %1, vcc, %8, %1, vcc\n\tv_mov_b32 %5, %8\n\t"
+      "v_addc_co_u32 %2, vcc, %8, %2, vcc\n\tv_mov_b32 %6, %8\n\t"
+      "v_addc_co_u32 %3, vcc, %8, %3, vcc\n\tv_mov_b32 %7, %0\n\t"
+      : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(m0), "+v"(m1), "+v"(m2), "+v"(m3) : "v"(b) : "vcc");
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ m0 ^ m1 ^ m2 ^ m3;
+}
+__global__ void k_mov(uint64_t* out, uint32_t seed) {
+  uint32_t a = threadIdx.x ^ seed, b = blockIdx.x * 2654435761u + seed;
+  uint32_t r0 = a, r1 = b, r2 = a ^ 1, r3 = b ^ 3, r4 = a + 7, r5 = b + 9, r6 = a * 3, r7 = b * 5;
+  for (int i = 0; i < ITERS; ++i) {
+    asm volatile(
+      "v_mov_b32 %0, %1\n\t" "v_mov_b32 %1, %2\n\t" "v_mov_b32 %2, %3\n\t" "v_mov_b32 %3, %4\n\t"
+      "v_mov_b32 %4, %5\n\t" "v_mov_b32 %5, %6\n\t" "v_mov_b32 %6, %7\n\t" "v_mov_b32 %7, %8\n\t"
+      : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(b));
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7;
+}
+
 typedef void (*kfn)(uint64_t*, uint32_t);
 
 static int run(const char* name, kfn f, int blocks, int threads, uint64_t* d, double per_iter = 8.0) {
@@ -292,6 +342,11 @@ int main() {
   if (run("v_lshrrev_b64", k_lshr64, blocks, threads, d)) return 1;
   if (run("v_lshl_add_u64", k_lshladd64, blocks, threads, d)) return 1;
   if (run("v_mad_u64_u32 ILP4 4w/SIMD", k_mad_ilp4, 256 * 4, threads, d)) return 1;
+  if (run("v_mov_b32", k_mov, blocks, threads, d)) return 1;
+  // pairs counted as 2 ops: a rate equal to the mad-only rate x2 means the mov is free
+  if (run("mad+mov pairs (ops) 4w/SIMD", k_mad_mov, 256 * 4, threads, d, 16.0)) return 1;
+  if (run("addc+mov pairs (ops) 4w/SIMD", k_addc_mov, 256 * 4, threads, d, 16.0)) return 1;
+  if (run("v_addc_co_u32 chain 4w/SIMD", k_addc, 256 * 4, threads, d)) return 1;
   {
     int nb = 256 * 8;
     hipLaunchKernelGGL(k_clock, dim3(nb), dim3(256), 0, 0, d, 3u);
