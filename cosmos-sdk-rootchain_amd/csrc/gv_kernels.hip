@@ -590,6 +590,13 @@ __global__ void k_debug(int op, u32 n, const u32* in, u32* out) {
 #pragma unroll
               for (int i = 0; i < 8; ++i) o[8 + i] = p.y.v[i];
               break; }
+    case 12: fe_shl<1>(r, a); fe_normalize(r); break;
+    case 13: fe_shl<2>(r, a); fe_normalize(r); break;
+    case 14: fe_shl<3>(r, a); fe_normalize(r); break;
+    case 15: fe_mul3(r, a); fe_normalize(r); break;
+    case 16: fe_sub_shl<1>(r, a, b); fe_normalize(r); break;
+    case 17: fe_sub_shl<2>(r, a, b); fe_normalize(r); break;
+    case 18: fe_sub_shl<3>(r, a, b); fe_normalize(r); break;
     default: r = a; break;
   }
   if (op != 7 && op != 9) {

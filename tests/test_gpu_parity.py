@@ -57,6 +57,13 @@ def run_op(ver, op, pairs):
     (2, lambda a, b: (a + b) % P),
     (3, lambda a, b: (a - b) % P),
     (6, lambda a, b: a % P),
+    (12, lambda a, b: 2 * a % P),
+    (13, lambda a, b: 4 * a % P),
+    (14, lambda a, b: 8 * a % P),
+    (15, lambda a, b: 3 * a % P),
+    (16, lambda a, b: (a - 2 * b) % P),
+    (17, lambda a, b: (a - 4 * b) % P),
+    (18, lambda a, b: (a - 8 * b) % P),
 ])
 def test_field_ops(ver, op, fn):
     rng = random.Random(op)
