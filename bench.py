@@ -131,18 +131,21 @@ def load_pmc(kernel):
         return None
 
 
-def main():
+def main(argv=None, verifier_factory=None, workload_fn=None):
+    """verifier_factory(local_rank) / workload_fn(n, seed, keys, adv, threads) are
+    injection points for tests/test_bench_dist.py (gloo, CPU, fake verifier)."""
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1_000_000, help="signatures per rank")
+    ap.add_argument("--items", "--n", dest="n", type=int, default=1_000_000, help="signatures per rank")
     ap.add_argument("--adversarial", type=float, default=0.0, help="C3: fraction of invalid signatures")
     ap.add_argument("--keys", type=int, default=65536)
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
-    args = ap.parse_args()
+    ap.add_argument("--no-extras", action="store_true", help="skip the C3 / message-path / C1 ante lines")
+    args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -167,10 +170,11 @@ def main():
 
     n = args.n
     t0 = time.perf_counter()
-    pub, sig, dig, exp = make_digest_workload(n, 0xC2 + 7919 * rank, args.keys, args.adversarial, args.threads)
+    pub, sig, dig, exp = (workload_fn or make_digest_workload)(n, 0xC2 + 7919 * rank, args.keys, args.adversarial,
+                                                               args.threads)
     log(f"[rank {rank}] workload {n} items in {time.perf_counter() - t0:.1f}s; valid {exp.mean():.3f}")
 
-    ver = gvm.Verifier([local_rank])
+    ver = verifier_factory(local_rank) if verifier_factory else gvm.Verifier([local_rank])
     d_pub = ver.dev_alloc(pub.nbytes)
     d_sig = ver.dev_alloc(sig.nbytes)
     d_dig = ver.dev_alloc(dig.nbytes)
@@ -268,6 +272,16 @@ def main():
 
     for p in (d_pub, d_sig, d_dig, d_bits):
         ver.dev_free(p)
+    if rank == 0 and world == 1 and not args.no_extras:
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        import bench_extras as X
+        ex = {}
+        t = time.perf_counter()
+        ex["c3_adversarial"] = X.c3_adversarial(ver, make_digest_workload, n, args.threads)
+        ex["msg_path"] = X.msg_path(ver, workload_lib(), min(n, 500_000), args.threads)
+        ex["c1_ante"] = X.c1_ante(ver)
+        log(f"extras in {time.perf_counter() - t:.1f}s")
+        result["extras"] = ex
     ver.close()
     if rank == 0:
         print(json.dumps(result), flush=True)

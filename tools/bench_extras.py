@@ -1,0 +1,166 @@
+"""Secondary measurements reported inside bench.py's JSON line (rank 0, N=1).
+
+  c3_adversarial  BASELINE.json configs[2]: 1M signatures, 25 % invalid (high-S,
+                  r >= n, s = 0 / 2^256-1, random x, malformed prefix, wrong
+                  message), device-resident, bitmap checked against the verdicts
+                  known by construction.
+  msg_path        the full VerifyBytes path on MsgSend StdSignBytes (C1 message
+                  shape, ~350-byte messages: SHA-256 on the GPU, one message per
+                  lane) through gv_dev_verify_msgs, device-resident.
+  c1_ante         BASELINE.json configs[0] shape: 10k single-signer MsgSend txs
+                  through the host mirror of the ante chain (libgvhost) --
+                  block path (PreVerifyTxs: one GPU batch, then the decorators
+                  with verdict-cache hits) and the per-tx CheckTx path (one GPU
+                  call per tx), host buffers / PCIe included.
+
+Nothing here touches oracle/: verdicts come from construction (the workload
+signs valid items with OpenSSL and mutates the invalid ones).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "cosmos-sdk-rootchain_amd"))
+
+
+def _unpack_bits(bits: np.ndarray, n: int) -> np.ndarray:
+    return np.unpackbits(bits.view(np.uint8), bitorder="little")[:n]
+
+
+def _timed_device_runs(ver, run, steps: int, warmup: int = 1):
+    for _ in range(warmup):
+        run()
+    ver.dev_sync()
+    ver.set_option("time_kernels", 1)
+    ver.stage_stats()
+    t = time.perf_counter()
+    for _ in range(steps):
+        run()
+    ver.dev_sync()
+    el = time.perf_counter() - t
+    cnt, unpack_ms, prep_ms, ecmult_ms = ver.stage_stats()
+    ver.set_option("time_kernels", 0)
+    return el, {"unpack_or_sha_ms": round(unpack_ms, 3), "prep_ms": round(prep_ms, 3), "ecmult_ms": round(ecmult_ms, 3)}
+
+
+def c3_adversarial(ver, make_workload, n: int, threads: int, steps: int = 3):
+    pub, sig, dig, exp = make_workload(n, 0xC3, 65536, 0.25, threads)
+    d = [ver.dev_alloc(a.nbytes) for a in (pub, sig, dig)]
+    for p, a in zip(d, (pub, sig, dig)):
+        ver.dev_upload(p, a)
+    nw = (n + 63) // 64
+    d_bits = ver.dev_alloc(nw * 8)
+    el, stages = _timed_device_runs(ver, lambda: ver.dev_verify_digests(0, n, d[0], d[1], d[2], d_bits), steps)
+    bits = np.zeros(nw, np.uint64)
+    ver.dev_download(bits, d_bits)
+    got = _unpack_bits(bits, n)
+    out = {"items": n, "invalid_fraction": round(1 - float(exp.mean()), 4),
+           "value": round(n * steps / el, 1), "unit": "verifies/s",
+           "mismatches": int(np.count_nonzero(got != exp)), "accepted": int(got.sum()),
+           "expected_accepted": int(exp.sum()), "stages": stages}
+    for p in d + [d_bits]:
+        ver.dev_free(p)
+    return out
+
+
+def msg_path(ver, wl, n: int, threads: int, nkeys: int = 10000, steps: int = 3):
+    """wl: tools/workload/libgvwork.so handle (bench.workload_lib())."""
+    priv = np.zeros((nkeys, 32), np.uint8)
+    pubk = np.zeros((nkeys, 33), np.uint8)
+    wl.gvw_keys(nkeys, 0xC1, priv.ctypes.data, pubk.ctypes.data, threads)
+    cap = n * 512
+    blob = np.zeros(cap, np.uint8)
+    off = np.zeros(n, np.uint64)
+    ln = np.zeros(n, np.uint32)
+    wl.gvw_msgsend_signbytes.restype = ctypes.c_longlong
+    wl.gvw_msgsend_signbytes.argtypes = [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
+                                         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+    wl.gvw_sha256_msgs.argtypes = [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_void_p]
+    total = wl.gvw_msgsend_signbytes(n, pubk.ctypes.data, nkeys, 0, blob.ctypes.data, cap, off.ctypes.data,
+                                     ln.ctypes.data)
+    assert total > 0
+    blob = blob[:total].copy()
+    mdig = np.zeros((n, 32), np.uint8)
+    wl.gvw_sha256_msgs(n, blob.ctypes.data, off.ctypes.data, ln.ctypes.data, mdig.ctypes.data)
+    pub = np.zeros((n, 33), np.uint8)
+    sig = np.zeros((n, 64), np.uint8)
+    dig = np.zeros((n, 32), np.uint8)
+    exp = np.zeros(n, np.uint8)
+    wl.gvw_sign(n, 0xC1, nkeys, priv.ctypes.data, pubk.ctypes.data, None, mdig.ctypes.data, 0.0,
+                pub.ctypes.data, sig.ctypes.data, dig.ctypes.data, exp.ctypes.data, threads)
+    arrs = (pub, sig, blob, off, ln)
+    d = [ver.dev_alloc(a.nbytes) for a in arrs]
+    for p, a in zip(d, arrs):
+        ver.dev_upload(p, a)
+    nw = (n + 63) // 64
+    d_bits = ver.dev_alloc(nw * 8)
+    el, stages = _timed_device_runs(
+        ver, lambda: ver.dev_verify_msgs(0, n, d[0], d[1], d[2], d[3], d[4], d_bits), steps)
+    bits = np.zeros(nw, np.uint64)
+    ver.dev_download(bits, d_bits)
+    got = _unpack_bits(bits, n)
+    out = {"items": n, "mean_msg_bytes": round(float(ln.mean()), 1), "value": round(n * steps / el, 1),
+           "unit": "verifies/s (SHA-256 of StdSignBytes + ECDSA)", "mismatches": int(np.count_nonzero(got != exp)),
+           "stages": stages}
+    for p in d + [d_bits]:
+        ver.dev_free(p)
+    return out
+
+
+def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500):
+    import gvhost
+    import txkit as T
+    keys = []
+    for i in range(ntx + 1):
+        priv = T.privkey_from_secret(b"gv-c1-" + struct.pack("<Q", i))
+        pub33 = T.secp_pubkey(priv)
+        amino = T.amino_secp(pub33)
+        keys.append((priv, amino, T.address(amino)))
+    fee = T.fee_json([(0, "stake")], 1000000)
+    txs = []
+    for i in range(ntx):
+        priv, amino, addr = keys[i]
+        msg = T.msg_send_json(addr, keys[i + 1][2], [(10, "foocoin")])
+        sb = T.std_sign_bytes("gv-bench", i, 0, fee, [msg], "")
+        txs.append(T.flat_tx([msg], fee, "", [addr], [(amino, T.secp_sign(priv, sb))]))
+
+    def fresh_app():
+        app = gvhost.HostApp(ver, chain_id="gv-bench", height=1)
+        for i in range(ntx):
+            app.set_account(keys[i][2], i, 0)
+        return app
+
+    # block path: PreVerifyTxs (one GPU batch) + the ante chain per tx
+    app = fresh_app()
+    t = time.perf_counter()
+    rc, leaves = app.preverify(txs)
+    t_pre = time.perf_counter() - t
+    ok = 0
+    hits = 0
+    for tx in txs:
+        _, r = app.ante(tx)
+        ok += r["code"] == 0
+        hits += r["cache_hits"]
+    t_block = time.perf_counter() - t
+    app.close()
+    # per-tx path (CheckTx without batching): one GPU call per tx
+    app = fresh_app()
+    m = min(per_tx_sample, ntx)
+    t = time.perf_counter()
+    ok2 = sum(app.ante(tx)[1]["code"] == 0 for tx in txs[:m])
+    t_single = time.perf_counter() - t
+    app.close()
+    return {"txs": ntx, "block_path": {"txs_per_s": round(ntx / t_block, 1), "total_ms": round(t_block * 1e3, 2),
+                                       "preverify_ms": round(t_pre * 1e3, 2), "accepted": ok, "cache_hits": hits,
+                                       "gpu_leaves": leaves},
+            "per_tx_path": {"txs": m, "txs_per_s": round(m / t_single, 1), "accepted": ok2},
+            "note": "host mirror (libgvhost) of SetPubKey/ValidateSigCount/SigGasConsume/BatchSigVerification/"
+                    "IncrementSequence over libgpuverify; sign bytes rebuilt per tx in C++; host buffers"}

@@ -137,20 +137,20 @@ def gen_reduce():
         p("addc", f"%[r{i}]", "vcc", f"%[r{i}]", f"%[t{7 + i}]", "vcc")
     p("addc", "%[top]", "vcc", "%[top]", "%[t15]", "vcc")
     p("addc", "%[top2]", "vcc", "0", "0", "vcc")
-    # fold 1: value = r + (top + top2*2^32) * (2^32 + 977)
+    # fold 1: value = r + T * (2^32 + 977), T = top + top2*2^32 (< 2^33):
+    # T*(2^32+977) = s0 + s1*2^32 + s2*2^64 with s0:s1' = top*977 (+ top2*977
+    # in s1'), s1 = s1' + top, s2 = top2 + carry -- one chain adds all three.
     p("mad", pair(0), "vcc", "%[top]", "%[k977]", "0")          # v0:v1 = top*977
     p("mul24", "v2", "0x3d1", "%[top2]")                        # top2*977 (top2 <= 1)
     p("add", "v1", "v1", "v2")                                  # < 2^11, no carry
+    p("add_co", "v1", "vcc", "v1", "%[top]")                    # s1
+    p("addc", "v2", "vcc", "%[top2]", "0", "vcc")               # s2 <= 2
     p("add_co", "%[r0]", "vcc", "%[r0]", "v0")
     p("addc", "%[r1]", "vcc", "%[r1]", "v1", "vcc")
-    p("addc", "%[r2]", "vcc", "%[r2]", "%[top2]", "vcc")
+    p("addc", "%[r2]", "vcc", "%[r2]", "v2", "vcc")
     for i in range(3, 8):
         p("addc", f"%[r{i}]", "vcc", f"%[r{i}]", "0", "vcc")
-    p("addc", "v3", "vcc", "0", "0", "vcc")                     # carry c3
-    p("add_co", "%[r1]", "vcc", "%[r1]", "%[top]")               # + top * 2^32
-    for i in range(2, 8):
-        p("addc", f"%[r{i}]", "vcc", f"%[r{i}]", "0", "vcc")
-    p("addc", "v3", "vcc", "v3", "0", "vcc")                    # c3 in {0,1}
+    p("addc", "v3", "vcc", "0", "0", "vcc")                     # carry c3 in {0,1}
     # fold 2: a wrap leaves r < 2^77; add c3*(2^32+977) into limbs 0..2
     p("mul24", "v2", "0x3d1", "v3")
     p("add_co", "%[r0]", "vcc", "%[r0]", "v2")
