@@ -144,7 +144,7 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the C3 / message-path / C1 ante lines")
+    ap.add_argument("--no-extras", action="store_true", help="skip the C3 / message-path / C1 / C4 lines")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -280,6 +280,7 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
         ex["c3_adversarial"] = X.c3_adversarial(ver, make_digest_workload, n, args.threads)
         ex["msg_path"] = X.msg_path(ver, workload_lib(), min(n, 500_000), args.threads)
         ex["c1_ante"] = X.c1_ante(ver)
+        ex["c4_multisig"] = X.c4_multisig(ver, workload_lib(), threads=args.threads)
         log(f"extras in {time.perf_counter() - t:.1f}s")
         result["extras"] = ex
     ver.close()

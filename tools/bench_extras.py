@@ -146,8 +146,8 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500):
     ok = 0
     hits = 0
     for tx in txs:
-        _, r = app.ante(tx)
-        ok += r["code"] == 0
+        rc_a, r = app.ante(tx)
+        ok += rc_a == 0 and r["code"] == 0
         hits += r["cache_hits"]
     t_block = time.perf_counter() - t
     app.close()
@@ -155,7 +155,10 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500):
     app = fresh_app()
     m = min(per_tx_sample, ntx)
     t = time.perf_counter()
-    ok2 = sum(app.ante(tx)[1]["code"] == 0 for tx in txs[:m])
+    ok2 = 0
+    for tx in txs[:m]:
+        rc_a, r = app.ante(tx)
+        ok2 += rc_a == 0 and r["code"] == 0
     t_single = time.perf_counter() - t
     app.close()
     return {"txs": ntx, "block_path": {"txs_per_s": round(ntx / t_block, 1), "total_ms": round(t_block * 1e3, 2),
@@ -164,3 +167,77 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500):
             "per_tx_path": {"txs": m, "txs_per_s": round(m / t_single, 1), "accepted": ok2},
             "note": "host mirror (libgvhost) of SetPubKey/ValidateSigCount/SigGasConsume/BatchSigVerification/"
                     "IncrementSequence over libgpuverify; sign bytes rebuilt per tx in C++; host buffers"}
+
+
+def c4_multisig(ver, wl=None, ntx: int = 30000, block: int = 10000, naccounts: int = 96, threads: int = 16):
+    """BASELINE.json configs[3] shape on one GPU: k-of-n threshold multisig
+    MsgSend txs (2-of-3, 3-of-5, 4-of-7 in equal shares), replayed in blocks of
+    `block` txs: gvh_preverify (every secp256k1 leaf of the block in one GPU
+    batch, sequences predicted per signer) then the ante chain per tx.
+    wl: tools/workload/libgvwork.so handle (batch signing with OpenSSL)."""
+    import hashlib
+    import gvhost
+    import txkit as T
+    shapes = [(2, 3), (3, 5), (4, 7)]
+    privs, accts = [], []
+    for a in range(naccounts):
+        k, nsub = shapes[a % 3]
+        base = len(privs)
+        amino = []
+        for j in range(nsub):
+            priv = T.privkey_from_secret(b"gv-c4-" + struct.pack("<QQ", a, j))
+            privs.append(priv)
+            amino.append(T.amino_secp(T.secp_pubkey(priv)))
+        mk = T.amino_multisig(k, amino)
+        accts.append((k, nsub, base, mk, T.address(mk)))
+    sink = T.address(T.amino_secp(T.secp_pubkey(T.privkey_from_secret(b"gv-c4-sink"))))
+    fee = T.fee_json([(0, "stake")], 1000000)
+    msgs, kidx, digs = [], [], []
+    for i in range(ntx):
+        a = i % naccounts
+        k, nsub, base, mk, addr = accts[a]
+        msg = T.msg_send_json(addr, sink, [(1, "foocoin")])
+        sb = T.std_sign_bytes("gv-bench", a, i // naccounts, fee, [msg], "")
+        msgs.append(msg)
+        d = hashlib.sha256(sb).digest()
+        for j in range(k):
+            kidx.append(base + j)
+            digs.append(d)
+    L = len(kidx)
+    priv_arr = np.frombuffer(b"".join(privs), np.uint8).reshape(-1, 32).copy()
+    pub_arr = np.zeros((len(privs), 33), np.uint8)          # unused by gvw_sign's signing
+    kid = np.array(kidx, np.uint32)
+    dig = np.frombuffer(b"".join(digs), np.uint8).reshape(L, 32).copy()
+    o_pub = np.zeros((L, 33), np.uint8)
+    o_sig = np.zeros((L, 64), np.uint8)
+    o_dig = np.zeros((L, 32), np.uint8)
+    exp = np.zeros(L, np.uint8)
+    wl.gvw_sign(L, 0xC4, len(privs), priv_arr.ctypes.data, pub_arr.ctypes.data, kid.ctypes.data, dig.ctypes.data,
+                0.0, o_pub.ctypes.data, o_sig.ctypes.data, o_dig.ctypes.data, exp.ctypes.data, threads)
+    txs, pos = [], 0
+    for i in range(ntx):
+        k, nsub, base, mk, addr = accts[i % naccounts]
+        sigs = [o_sig[pos + j].tobytes() for j in range(k)]
+        pos += k
+        bits = [j < k for j in range(nsub)]
+        txs.append(T.flat_tx([msgs[i]], fee, "", [addr], [(mk, T.multisignature(bits, sigs))]))
+    app = gvhost.HostApp(ver, chain_id="gv-bench", height=1)
+    for a, acct in enumerate(accts):
+        app.set_account(acct[4], a, 0)
+    ok = 0
+    t_pre = 0.0
+    t = time.perf_counter()
+    for b0 in range(0, ntx, block):
+        blk = txs[b0:b0 + block]
+        tp = time.perf_counter()
+        app.preverify(blk)
+        t_pre += time.perf_counter() - tp
+        for tx in blk:
+            rc_a, r = app.ante(tx)
+            ok += rc_a == 0 and r["code"] == 0
+    el = time.perf_counter() - t
+    app.close()
+    return {"txs": ntx, "leaves": L, "block_txs": block, "accepted": ok,
+            "leaves_per_s": round(L / el, 1), "txs_per_s": round(ntx / el, 1),
+            "preverify_ms_per_block": round(t_pre * 1e3 / ((ntx + block - 1) // block), 2),
+            "note": "2-of-3 / 3-of-5 / 4-of-7 threshold accounts, all k bits set; host mirror path with host buffers"}
