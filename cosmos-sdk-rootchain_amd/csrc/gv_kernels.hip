@@ -27,6 +27,7 @@
 #include "secp_field.cuh"
 #include "secp_scalar.cuh"
 #include "secp_group.cuh"
+#include "secp_group29.cuh"
 #include "secp_sha256.cuh"
 #include "gv_kernels.h"
 
@@ -49,6 +50,28 @@ GV_DEV void store_fe(u32* base, u32 C, u32 g, const fe& a) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) base[(size_t)i * C + g] = a.v[i];
 }
+// 9 x 29 field elements cross memory as 8 x 32 words (value < 2^256,
+// canonical when written here): the SoA rows and the 64-byte table entries
+// keep one layout for both field layers.
+GV_DEV void load_f29(fe29& r, const u32* base, u32 C, u32 g) {
+  u32 w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = base[(size_t)i * C + g];
+  f29_from_words(r, w);
+}
+GV_DEV void store_f29(u32* base, u32 C, u32 g, const fe29& a) {
+  u32 w[8];
+  f29_to_words(w, a);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) base[(size_t)i * C + g] = w[i];
+}
+GV_DEV void f29_from_const(fe29& r, const u32* c) {
+  u32 w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = c[i];
+  f29_from_words(r, w);
+}
+
 GV_DEV void fe_from_const(fe& r, const u32* c) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) r.v[i] = c[i];
@@ -214,75 +237,90 @@ GV_DEV void load_qent(fe& x, fe& y, const u32* qt, u32 g, u32 j) {
   y.v[4] = d.x; y.v[5] = d.y; y.v[6] = d.z; y.v[7] = d.w;
 }
 
-GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx, const fe& qy, fe& zq) {
+GV_DEV void store_qent29(u32* qt, u32 g, int j, const fe29& x29, const fe29& y29) {
+  fe x, y;
+  f29_to_words(x.v, x29);
+  f29_to_words(y.v, y29);
+  store_qent(qt, g, j, x, y);
+}
+GV_DEV void load_qent29(fe29& x29, fe29& y29, const u32* qt, u32 g, u32 j) {
+  fe x, y;
+  load_qent(x, y, qt, g, j);
+  f29_from_words(x29, x.v);
+  f29_from_words(y29, y.v);
+}
+
+// Magnitudes (9 x 29 layer) annotated per step; every stored value is
+// canonical words.
+GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx8, const fe& qy8, fe& zq8) {
   u32* qr = qt + (size_t)C * GV_QTAB_N * 16;         // Z-ratio rows
-  fe X1, Y1, X2, Y2, t;
+  fe29 qx, qy, X1, Y1, X2, Y2, t, u;
+  f29_from_words(qx, qx8.v);
+  f29_from_words(qy, qy8.v);
   {
     // co-Z doubling of the affine Q: Z1 = 2y, 2Q = (M^2 - 2S, M(S - X) - 8y^4),
     // Q' = (S, 8y^4) with S = 4xy^2, M = 3x^2.
-    fe B, E, L, M;
-    fe_sqr(B, qx);
-    fe_sqr(E, qy);
-    fe_sqr(L, E);
-    fe_add(t, qx, E);
-    fe_sqr(t, t);
-    fe_sub(t, t, B);
-    fe_sub(t, t, L);
-    fe_dbl(X1, t);                                    // S
-    fe_dbl(M, B);
-    fe_add(M, M, B);
-    fe_sqr(t, M);
-    fe_sub(t, t, X1);
-    fe_sub(X2, t, X1);
-    fe_dbl(L, L);
-    fe_dbl(L, L);
-    fe_dbl(Y1, L);                                    // 8y^4
-    fe_sub(t, X1, X2);
-    fe_mul(t, M, t);
-    fe_sub(Y2, t, Y1);
+    fe29 B, E, L, M;
+    f29_sqr(B, qx);                                   // 1
+    f29_sqr(E, qy);                                   // 1
+    f29_sqr(L, E);                                    // y^4: 1
+    f29_add(t, qx, E);                                // 2
+    f29_sqr(t, t);                                    // 1
+    f29_sub<1>(t, t, B);                              // 3
+    f29_sub_norm<1>(t, t, L);                         // (x + y^2)^2 - x^2 - y^4 = 2xy^2: 1
+    f29_shl_norm<1>(X1, t);                           // S = 4xy^2: 1
+    f29_mul3_norm(M, B);                              // 1
+    f29_sqr(t, M);                                    // 1
+    f29_add(u, X1, X1);                               // 2
+    f29_sub_norm<2>(X2, t, u);                        // M^2 - 2S: 1
+    f29_shl_norm<3>(Y1, L);                           // 8y^4: 1
+    f29_sub<1>(t, X1, X2);                            // 3
+    f29_mul(t, M, t);                                 // 1
+    f29_sub_norm<1>(Y2, t, Y1);                       // 1
   }
-  store_qent(qt, g, 0, X1, Y1);                       // 1*Q on Z1
-  store_qent(qt, g, 1, X2, Y2);                       // 2*Q on Z1
+  store_qent29(qt, g, 0, X1, Y1);                     // 1*Q on Z1
+  store_qent29(qt, g, 1, X2, Y2);                     // 2*Q on Z1
   for (int m = 2; m < GV_QTAB_N; ++m) {               // (Q', mQ) -> ((m+1)Q, Q'')
-    fe h, rr, c, w1, w2, d, a1;
-    fe_sub(h, X1, X2);
-    store_fe(qr + (size_t)(m - 2) * 8 * C, C, g, h);  // Z_m / Z_{m-1}
-    fe_sub(rr, Y1, Y2);
-    fe_sqr(c, h);
-    fe_mul(w1, X1, c);
-    fe_mul(w2, X2, c);
-    fe_sqr(d, rr);
-    fe_sub(t, w1, w2);
-    fe_mul(a1, Y1, t);
-    fe_sub(t, d, w1);
-    fe_sub(X2, t, w2);                                // X3 = D - W1 - W2
-    fe_sub(t, w1, X2);
-    fe_mul(t, rr, t);
-    fe_sub(Y2, t, a1);                                // Y3 = (Y1-Y2)(W1-X3) - A1
+    fe29 h, rr, c, w1, w2, d, a1;
+    f29_sub_norm<1>(h, X1, X2);                       // 1
+    store_f29(qr + (size_t)(m - 2) * 8 * C, C, g, h); // Z_m / Z_{m-1}
+    f29_sub_norm<1>(rr, Y1, Y2);                      // 1
+    f29_sqr(c, h);
+    f29_mul(w1, X1, c);
+    f29_mul(w2, X2, c);
+    f29_sqr(d, rr);
+    f29_sub<1>(t, w1, w2);                            // 3
+    f29_mul(a1, Y1, t);                               // 1
+    f29_add(u, w1, w2);                               // 2
+    f29_sub_norm<2>(X2, d, u);                        // X3 = D - W1 - W2: 1
+    f29_sub<1>(t, w1, X2);                            // 3
+    f29_mul(t, rr, t);                                // 1
+    f29_sub_norm<1>(Y2, t, a1);                       // Y3 = (Y1-Y2)(W1-X3) - A1: 1
     X1 = w1;                                          // Q' on the new Z
     Y1 = a1;
-    store_qent(qt, g, m, X2, Y2);                     // (m+1)*Q
+    store_qent29(qt, g, m, X2, Y2);                   // (m+1)*Q
   }
   // entry m (index m-1) lives on Z_{m-1} (m >= 2; entry 1 on Z_1); the last
   // entry on Z_15.  acc = Z_15 / Z(entry m) accumulates the stored ratios.
-  fe acc;
+  fe29 acc;
   for (int m = GV_QTAB_N - 1; m >= 1; --m) {
     if (m >= 2) {
-      fe ratio;
-      load_fe(ratio, qr + (size_t)(m - 2) * 8 * C, C, g);
+      fe29 ratio;
+      load_f29(ratio, qr + (size_t)(m - 2) * 8 * C, C, g);
       if (m == GV_QTAB_N - 1) acc = ratio;
-      else fe_mul(acc, acc, ratio);
+      else f29_mul(acc, acc, ratio);
     }
-    fe x, y, a2, a3;
-    fe_sqr(a2, acc);
-    fe_mul(a3, a2, acc);
-    load_qent(x, y, qt, g, m - 1);
-    fe_mul(x, x, a2);
-    fe_mul(y, y, a3);
-    store_qent(qt, g, m - 1, x, y);
+    fe29 x, y, a2, a3;
+    f29_sqr(a2, acc);
+    f29_mul(a3, a2, acc);
+    load_qent29(x, y, qt, g, m - 1);
+    f29_mul(x, x, a2);
+    f29_mul(y, y, a3);
+    store_qent29(qt, g, m - 1, x, y);
   }
-  fe_dbl(t, qy);
-  fe_mul(zq, t, acc);                                 // Z_15 = 2y * prod(ratios)
+  f29_add(t, qy, qy);                                 // 2
+  f29_mul(t, t, acc);                                 // Z_15 = 2y * prod(ratios)
+  f29_to_words(zq8.v, t);
 }
 
 // ------------------------------------------------------------- k_scalar_inv
@@ -362,15 +400,19 @@ __global__ __launch_bounds__(256) void k_prep(u32 C, const u32* in_x, const u32*
     (void)d;
     ok &= (br != 0);
   }
-  fe c, y, y2, seven;
-  fe_sqr(c, x);
-  fe_mul(c, c, x);
-  fe_set_u32(seven, 7);
-  fe_add(c, c, seven);                      // c = x^3 + 7
-  fe_sqrt_candidate(y, c);                  // y = c^((p+1)/4)
-  fe_sqr(y2, y);
-  ok &= fe_equal(y2, c);                    // "invalid square root"
-  fe_normalize(y);
+  fe y;
+  {
+    fe29 x29, c, y29, y2, seven;
+    f29_from_words(x29, x.v);
+    f29_sqr(c, x29);
+    f29_mul(c, c, x29);
+    f29_set_u32(seven, 7);
+    f29_add(c, c, seven);                   // c = x^3 + 7 (magnitude 2)
+    f29_sqrt_candidate(y29, c);             // y = c^((p+1)/4)
+    f29_sqr(y2, y29);
+    ok &= f29_equal(y2, c);                 // "invalid square root"
+    f29_to_words(y.v, y29);                 // canonical
+  }
   if ((y.v[0] & 1u) != (pre & 1u)) fe_neg(y, y);   // choose parity (y != 0 always)
   fe_normalize(y);
   // (IsOnCurve and Y < P hold by construction once the square-root check passed)
@@ -446,39 +488,40 @@ __global__ __launch_bounds__(256) void k_prep(u32 C, const u32* in_x, const u32*
 // acc <- acc + (x, y) where (x, y) is affine on the accumulator's curve
 // (zinv == nullptr: Q-table entry) or an affine point of the real curve to be
 // lifted by zinv (G-table entry).  An infinite accumulator takes the point.
-GV_DEV void add_entry(gej& acc, bool& inf, const fe& x, const fe& y, const fe* zinv) {
-  fe az;
+// x magnitude 1, y magnitude <= 2 (a negated entry), zinv magnitude 1.
+GV_DEV void add_entry(gej29& acc, bool& inf, const fe29& x, const fe29& y, const fe29* zinv) {
+  fe29 az;
   if (zinv) {                                   // wave-uniform
     if (inf) az = *zinv;
-    else fe_mul(az, acc.z, *zinv);
+    else f29_mul(az, acc.z, *zinv);             // 1
   } else {
-    if (inf) fe_set_u32(az, 1);
-    else az = acc.z;
+    if (inf) f29_set_u32(az, 1);
+    else az = acc.z;                            // <= 2
   }
-  fe z2, u2, s2;
-  fe_sqr(z2, az);
-  fe_mul(u2, x, z2);
-  fe_mul(z2, z2, az);
-  fe_mul(s2, y, z2);
+  fe29 z2, u2, s2;
+  f29_sqr(z2, az);
+  f29_mul(u2, x, z2);
+  f29_mul(z2, z2, az);
+  f29_mul(s2, y, z2);                           // 2 x 1
   if (inf) {
     acc.x = u2;
     acc.y = s2;
-    fe_set_u32(acc.z, 1);
+    f29_set_u32(acc.z, 1);
     inf = false;
     return;
   }
-  gej_add_tail(acc, inf, u2, s2);
+  gej29_add_tail(acc, inf, u2, s2);
 }
 
 __global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, const u32* digits,
                                                  const u32* qt, const u32* zq_in, const u32* flags,
                                                  const u32* in_r, uint64_t* bits) {
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
-  fe zq;
-  load_fe(zq, zq_in, C, g);
+  fe29 zq;
+  load_f29(zq, zq_in, C, g);
 
-  gej acc;
-  fe_set_zero(acc.x); fe_set_zero(acc.y); fe_set_zero(acc.z);
+  gej29 acc;
+  f29_set_zero(acc.x); f29_set_zero(acc.y); f29_set_zero(acc.z);
   bool inf = true;
 
   // Strauss ladder: Q windows at bit 5*win, G windows at bit GV_GW*j = 5*(GV_GSTEP*j).
@@ -488,7 +531,7 @@ __global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, c
   for (int win = GV_QWIN - 1; win >= 0; --win) {
     if (win != GV_QWIN - 1) {
 #pragma unroll 1
-      for (int d = 0; d < GV_QW; ++d) gej_double(acc, acc);
+      for (int d = 0; d < GV_QW; ++d) gej29_double(acc, acc);
     }
     const bool gwin = (win % GV_GSTEP) == 0;
     const u32 dq = digits[(size_t)win * C + g];
@@ -501,18 +544,18 @@ __global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, c
                   : slot == 2 ? (int)dg0 : (int)dg1;
       if (d == 0) continue;
       const u32 e = (u32)((d < 0 ? -d : d) - 1);
-      fe x, y;
+      fe29 x, y;
       if (slot < 2) {
-        load_qent(x, y, qt, g, e);
+        load_qent29(x, y, qt, g, e);
         if (slot == 1) {                           // lambda * P = (beta * x, y)
-          fe beta;
-          fe_from_const(beta, kBeta);
-          fe_mul(x, x, beta);
+          fe29 beta;
+          f29_from_const(beta, kBeta);
+          f29_mul(x, x, beta);
         }
       } else {
-        load_qent(x, y, gtab + (slot == 3 ? (size_t)GV_GTAB_N * 16 : 0), 0, e);
+        load_qent29(x, y, gtab + (slot == 3 ? (size_t)GV_GTAB_N * 16 : 0), 0, e);
       }
-      if (d < 0) fe_neg(y, y);
+      if (d < 0) f29_neg<1>(y, y);                 // 2
       add_entry(acc, inf, x, y, slot < 2 ? nullptr : &zq);
     }
   }
@@ -520,27 +563,30 @@ __global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, c
   // ---- final check: R = (X, Y, Z*zq) on the real curve; x(R) mod n == r
   const u32 fl = flags[g];
   bool ok = (fl & 1u) && !inf;
-  fe zr, zz, rf, t, X;
-  fe_mul(zr, acc.z, zq);
-  fe_sqr(zz, zr);
-  load_fe(rf, in_r, C, g);
-  fe_mul(t, rf, zz);
-  X = acc.x;
-  fe_normalize(X);
-  fe_normalize(t);
+  fe29 zr, zz, rf, t;
+  f29_mul(zr, acc.z, zq);
+  f29_sqr(zz, zr);
+  u32 rw[8], X[8], tw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rw[i] = in_r[(size_t)i * C + g];
+  f29_from_words(rf, rw);
+  f29_mul(t, rf, zz);
+  f29_to_words(X, acc.x);
+  f29_to_words(tw, t);
   bool eq = true;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) eq &= (X.v[i] == t.v[i]);
+  for (int i = 0; i < 8; ++i) eq &= (X[i] == tw[i]);
   if (!eq && (fl & 2u)) {                   // R.x in [n, p): x mod n == r  <=>  x == r + n
-    fe rn;
+    u32 rn[8];
     u32 c = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) rn.v[i] = __builtin_addc(rf.v[i], kN[i], c, &c);
-    fe_mul(t, rn, zz);
-    fe_normalize(t);
+    for (int i = 0; i < 8; ++i) rn[i] = __builtin_addc(rw[i], kN[i], c, &c);
+    f29_from_words(rf, rn);
+    f29_mul(t, rf, zz);
+    f29_to_words(tw, t);
     eq = true;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) eq &= (X.v[i] == t.v[i]);
+    for (int i = 0; i < 8; ++i) eq &= (X[i] == tw[i]);
   }
   ok &= eq;
   const uint64_t mask = __ballot(ok);
