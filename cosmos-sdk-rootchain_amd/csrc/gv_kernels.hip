@@ -28,6 +28,7 @@
 #include "secp_scalar.cuh"
 #include "secp_group.cuh"
 #include "secp_group29.cuh"
+#include "secp_sc29.cuh"
 #include "secp_sha256.cuh"
 #include "gv_kernels.h"
 
@@ -324,56 +325,102 @@ GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx8, const fe& qy8, f
 }
 
 // ------------------------------------------------------------- k_scalar_inv
-// w = s^-1 mod n for every lane, Montgomery form, by Montgomery's trick:
-// each lane folds GV_INV_M signatures (element (wave*M + j)*64 + lane, so each
-// step j is a coalesced wave access), the lane totals are combined across the
-// wavefront by prefix/suffix scans, and ONE Fermat inversion serves the wave's
-// 64*M signatures -- ~3 Montgomery products per signature + 394/M amortised,
-// instead of ~380 (a per-lane inversion costs the same SIMT time whether one
-// lane or all 64 run it).  s outside [1, n) is replaced by 1 (those lanes are
-// rejected in k_prep).  pre/sm use the scratch rows given by the caller.
+// w = s^-1 mod n for every lane, Montgomery form (radix 2^29, R = 2^261,
+// secp_sc29.cuh), by Montgomery's trick: each lane folds GV_INV_M signatures
+// (element (wave*M + j)*64 + lane, so each step j is a coalesced wave access),
+// the lane totals are combined across the wavefront by prefix/suffix scans,
+// and ONE Fermat inversion serves the wave's 64*M signatures -- ~3 Montgomery
+// products per signature + ~330/M amortised, instead of ~330 (a per-lane
+// inversion costs the same SIMT time whether one lane or all 64 run it).  s
+// outside [1, n) is replaced by 1 (those lanes are rejected in k_prep).
+// w and the prefix products use 9 scratch rows each (limb i of lane e at
+// row[i*C + e]); the caller gives the row bases.
 GV_DEV void load_sc(u32 a[8], const u32* base, u32 C, u32 g) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) a[i] = base[(size_t)i * C + g];
 }
-GV_DEV void store_sc(u32* base, u32 C, u32 g, const u32 a[8]) {
+GV_DEV void load_sc29(sc29& a, const u32* base, u32 C, u32 g) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) base[(size_t)i * C + g] = a[i];
+  for (int i = 0; i < 9; ++i) a.n[i] = base[(size_t)i * C + g];
+}
+GV_DEV void store_sc29(u32* base, u32 C, u32 g, const sc29& a) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) base[(size_t)i * C + g] = a.n[i];
+}
+GV_DEV void sc29_mont_one(sc29& r) {          // R mod n = 2^261 mod n
+  const u32 t[9] = {0x1937D7E0u, 0x0DA1732Fu, 0x1AFE2201u, 0x08C6542Du, 0x00028AA2u, 0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.n[i] = t[i];
+}
+GV_DEV sc29 sc29_shfl(const sc29& a, int mode, int d) {
+  sc29 r;
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+    r.n[i] = mode == 0 ? shfl_up_u32(a.n[i], d) : mode == 1 ? shfl_down_u32(a.n[i], d) : shfl_idx_u32(a.n[i], d);
+  return r;
+}
+
+// Batch inversion across the wavefront: every lane holds a nonzero x
+// (Montgomery form); returns x^-1 (Montgomery form).  All 64 lanes active.
+// Prefix/suffix products by Hillis-Steele scans (6 steps each) + one Fermat
+// inversion shared by the wave.
+GV_DEV void sc29_batch_inv_wave(sc29& inv, const sc29& x) {
+  const u32 lane = lane_id();
+  sc29 pre = x, suf = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    sc29 t = sc29_shfl(pre, 0, d), m;
+    sc29_mul(m, pre, t);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) pre.n[i] = (lane >= (u32)d) ? m.n[i] : pre.n[i];
+    t = sc29_shfl(suf, 1, d);
+    sc29_mul(m, suf, t);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) suf.n[i] = (lane + (u32)d < 64u) ? m.n[i] : suf.n[i];
+  }
+  sc29 tot = sc29_shfl(pre, 2, 63), tinv, one;
+  sc29_inv(tinv, tot);
+  sc29_mont_one(one);
+  sc29 pe = sc29_shfl(pre, 0, 1), se = sc29_shfl(suf, 1, 1), m;
+  if (lane == 0) pe = one;
+  if (lane == 63) se = one;
+  sc29_mul(m, pe, se);
+  sc29_mul(inv, m, tinv);
 }
 
 __global__ __launch_bounds__(256) void k_scalar_inv(u32 C, const u32* in_s, u32* w, u32* pre) {
   const u32 lane = threadIdx.x & 63u;
   const u32 wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const u32 one_m[8] = {0x2FC9BEBFu, 0x402DA173u, 0x50B75FC4u, 0x45512319u, 1u, 0u, 0u, 0u};
-  u32 acc[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] = one_m[i];
+  sc29 acc;
+  sc29_mont_one(acc);
   for (int j = 0; j < GV_INV_M; ++j) {
     const u32 e = (wave * GV_INV_M + j) * 64u + lane;
     if (e >= C) break;                       // wave-uniform (C % 64 == 0)
-    u32 s[8], sm[8];
+    u32 s[8];
     load_sc(s, in_s, C, e);
     const bool ok = !u256_is_zero(s) && !u256_geq(s, kN);
     if (!ok) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) s[i] = (i == 0) ? 1u : 0u;
     }
-    sc_to_mont(sm, s);
-    store_sc(pre, C, e, acc);                // exclusive prefix within the lane
-    store_sc(w, C, e, sm);
-    sc_montmul(acc, acc, sm);
+    sc29 s29, sm;
+    sc29_from_words(s29, s);
+    sc29_to_mont(sm, s29);
+    store_sc29(pre, C, e, acc);              // exclusive prefix within the lane
+    store_sc29(w, C, e, sm);
+    sc29_mul(acc, acc, sm);
   }
-  u32 inv_lane[8];
-  sc_batch_inv_wave(inv_lane, acc);          // (lane total)^-1, one Fermat chain per wave
+  sc29 inv_lane;
+  sc29_batch_inv_wave(inv_lane, acc);        // (lane total)^-1, one Fermat chain per wave
   for (int j = GV_INV_M - 1; j >= 0; --j) {
     const u32 e = (wave * GV_INV_M + j) * 64u + lane;
     if (e >= C) continue;
-    u32 p[8], sm[8], inv[8];
-    load_sc(p, pre, C, e);
-    load_sc(sm, w, C, e);
-    sc_montmul(inv, inv_lane, p);            // s_j^-1 = (s_0..s_j)^-1 * (s_0..s_{j-1})
-    sc_montmul(inv_lane, inv_lane, sm);      // drop s_j from the running inverse
-    store_sc(w, C, e, inv);
+    sc29 p, sm, inv;
+    load_sc29(p, pre, C, e);
+    load_sc29(sm, w, C, e);
+    sc29_mul(inv, inv_lane, p);              // s_j^-1 = (s_0..s_j)^-1 * (s_0..s_{j-1})
+    sc29_mul(inv_lane, inv_lane, sm);        // drop s_j from the running inverse
+    store_sc29(w, C, e, inv);
   }
 }
 
@@ -442,10 +489,17 @@ __global__ __launch_bounds__(256) void k_prep(u32 C, const u32* in_x, const u32*
   }
 
   // ---- w = s^-1 mod n (Montgomery form, from k_scalar_inv)
-  u32 wm[8], u1[8], u2[8];
-  load_sc(wm, in_w, C, g);
-  sc_montmul(u1, e, wm);                    // e*w  (plain form)
-  sc_montmul(u2, r, wm);                    // r*w
+  u32 u1[8], u2[8];
+  {
+    sc29 w29, e29, r29, t;
+    load_sc29(w29, in_w, C, g);
+    sc29_from_words(e29, e);
+    sc29_from_words(r29, r);
+    sc29_mul(t, e29, w29);                  // e*w  (plain form)
+    sc29_to_words(u1, t);
+    sc29_mul(t, r29, w29);                  // r*w
+    sc29_to_words(u2, t);
+  }
 
   // ---- GLV split
   u32 k1g[4], k2g[4], k1q[4], k2q[4], n1g, n2g, n1q, n2q;
@@ -626,9 +680,15 @@ __global__ void k_debug(int op, u32 n, const u32* in, u32* out) {
               for (int i = 0; i < 4; ++i) { o[i] = k1[i]; o[4 + i] = k2[i]; }
               o[8] = n1; o[9] = n2; r = a; break; }
     case 10: { // batch inversion of a (plain form, nonzero) across the wave -> plain inverse
-              u32 am[8], im[8], one[8] = {1u, 0, 0, 0, 0, 0, 0, 0};
+               // (the production path: radix-2^29 Montgomery, secp_sc29.cuh)
+              u32 one[8] = {1u, 0, 0, 0, 0, 0, 0, 0};
               if (!live || u256_is_zero(a.v)) { for (int i = 0; i < 8; ++i) a.v[i] = one[i]; }
-              sc_to_mont(am, a.v); sc_batch_inv_wave(im, am); sc_montmul(r.v, im, one); break; }
+              sc29 x, xm, im, o1, pl;
+              sc29_from_words(x, a.v); sc29_to_mont(xm, x); sc29_batch_inv_wave(im, xm);
+              sc29_from_words(o1, one); sc29_mul(pl, im, o1); sc29_to_words(r.v, pl); break; }
+    case 26: { // radix-2^29 Montgomery product a * b * 2^-261 mod n, canonical
+              sc29 x, y, z; sc29_from_words(x, a.v); sc29_from_words(y, b.v); sc29_mul(z, x, y);
+              sc29_to_words(r.v, z); break; }
     case 11: { // Jacobian double of affine (a, b), returned affine
               gej p; p.x = a; p.y = b; fe_set_u32(p.z, 1); gej_double(p, p);
               fe zi, z2, z3; fe_inv(zi, p.z); fe_sqr(z2, zi); fe_mul(z3, z2, zi);
@@ -643,6 +703,34 @@ __global__ void k_debug(int op, u32 n, const u32* in, u32* out) {
     case 16: fe_sub_shl<1>(r, a, b); fe_normalize(r); break;
     case 17: fe_sub_shl<2>(r, a, b); fe_normalize(r); break;
     case 18: fe_sub_shl<3>(r, a, b); fe_normalize(r); break;
+    // 9 x 29 layer (secp_fe29.cuh / secp_group29.cuh): words in, canonical words out
+    case 19: case 20: case 21: case 22: case 23: case 25: {
+      fe29 x, y, z;
+      f29_from_words(x, a.v);
+      f29_from_words(y, b.v);
+      if (op == 19) f29_mul(z, x, y);
+      else if (op == 20) f29_sqr(z, x);
+      else if (op == 21) f29_sub_norm<1>(z, x, y);
+      else if (op == 22) f29_inv(z, x);
+      else if (op == 23) f29_sqrt_candidate(z, x);
+      else { f29_sub_norm<1>(z, x, y); f29_set_u32(z, f29_is_zero_fast(z) ? 1u : 0u); }
+      f29_to_words(r.v, z);
+      break;
+    }
+    case 24: {  // Jacobian double of affine (a, b) on the 9 x 29 layer, returned affine
+      gej29 q;
+      f29_from_words(q.x, a.v); f29_from_words(q.y, b.v); f29_set_u32(q.z, 1);
+      gej29_double(q, q);
+      fe29 zi, z2, z3;
+      f29_inv(zi, q.z); f29_sqr(z2, zi); f29_mul(z3, z2, zi);
+      f29_mul(q.x, q.x, z2); f29_mul(q.y, q.y, z3);
+      f29_to_words(r.v, q.x);
+      u32 yw[8];
+      f29_to_words(yw, q.y);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[8 + i] = yw[i];
+      break;
+    }
     default: r = a; break;
   }
   if (op != 7 && op != 9) {
@@ -678,8 +766,8 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
     const uint32_t waves = (C / 64 + GV_INV_M - 1) / GV_INV_M;
     // scratch for w and the prefix products: the digit rows.  k_prep reads
     // its lane's w before writing that lane's digits (same lane, same rows).
-    uint32_t* w = b->digits;                   // rows 0..7
-    uint32_t* pre = b->digits + (size_t)8 * C; // rows 8..15
+    uint32_t* w = b->digits;                   // rows 0..8
+    uint32_t* pre = b->digits + (size_t)9 * C; // rows 9..17
     hipLaunchKernelGGL(gv::k_scalar_inv, dim3((waves + 3) / 4), blk, 0, st, C, b->in_s, w, pre);
     hipLaunchKernelGGL(gv::k_prep, grd, blk, 0, st, C, b->in_x, b->in_pfx, b->in_r, b->in_s, b->in_e,
                        (const uint32_t*)w, b->digits, b->qtab, b->zq, b->flags);

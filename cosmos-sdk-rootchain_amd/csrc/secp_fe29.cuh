@@ -91,7 +91,11 @@ GV_DEV u32 f29_add32(u32 a, u32 b) {
 template <bool SQR>
 GV_DEV int f29_col_hi(int k) { return SQR ? (k >> 1) : (k < 9 ? k : 8); }
 
-template <bool SQR>
+// NCH = 1: one chain per column (throughput kernels).  NCH = 2: even and odd
+// terms on two interleaved chains joined by one 64-bit add per column -- more
+// instructions, but a single wave on a SIMD (the small-batch latency kernels)
+// no longer waits on every mad's predecessor.
+template <bool SQR, int NCH>
 GV_DEV void f29_mulsqr(fe29& r, const fe29& a, const fe29& b) {
   u32 kr0 = F29_R0, kr1 = F29_R1;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -102,12 +106,21 @@ GV_DEV void f29_mulsqr(fe29& r, const fe29& a, const fe29& b) {
   for (int i = 0; i < 9; ++i) d[i] = SQR ? (a.n[i] << 1) : 0u;
 #define F29_X(i, j) (SQR ? ((i) == (j) ? a.n[i] : d[i]) : a.n[i])
 #define F29_Y(i, j) (SQR ? a.n[j] : b.n[j])
+#define F29_TERM(x, y)                                   \
+  do {                                                   \
+    if (NCH == 2 && (idx & 1)) cb = f29_mad(x, y, cb);    \
+    else ca = f29_mad(x, y, ca);                          \
+    ++idx;                                               \
+  } while (0)
   u32 t[9];
   u64 acc = 0;
 #pragma unroll
   for (int k = 9; k <= 16; ++k) {             // high columns, carry chained
+    u64 ca = acc, cb = 0;
+    int idx = 0;
 #pragma unroll
-    for (int i = k - 8; i <= f29_col_hi<SQR>(k); ++i) acc = f29_mad(F29_X(i, k - i), F29_Y(i, k - i), acc);
+    for (int i = k - 8; i <= f29_col_hi<SQR>(k); ++i) F29_TERM(F29_X(i, k - i), F29_Y(i, k - i));
+    acc = (NCH == 2 && idx > 1) ? ca + cb : ca;
     t[k - 9] = (u32)acc & F29_M;
     acc >>= 29;
   }
@@ -117,13 +130,17 @@ GV_DEV void f29_mulsqr(fe29& r, const fe29& a, const fe29& b) {
   acc = 0;                                    // the carry out of column 8 into 9 is
 #pragma unroll                                // NOT added above: it re-enters below
   for (int j = 0; j <= 8; ++j) {              // as part of the 2^261 fold
+    u64 ca = acc, cb = 0;
+    int idx = 0;
 #pragma unroll
-    for (int i = 0; i <= f29_col_hi<SQR>(j); ++i) acc = f29_mad(F29_X(i, j - i), F29_Y(i, j - i), acc);
-    acc = f29_mad(t[j], kr0, acc);
-    if (j >= 1) acc = f29_mad(t[j - 1], kr1, acc);
+    for (int i = 0; i <= f29_col_hi<SQR>(j); ++i) F29_TERM(F29_X(i, j - i), F29_Y(i, j - i));
+    F29_TERM(t[j], kr0);
+    if (j >= 1) F29_TERM(t[j - 1], kr1);
+    acc = (NCH == 2 && idx > 1) ? ca + cb : ca;
     o.n[j] = (u32)acc & F29_M;
     acc >>= 29;
   }
+#undef F29_TERM
 #undef F29_X
 #undef F29_Y
   acc = f29_mad(t[8], kr1, acc);              // 256 * limb 17 -> weight 2^261
@@ -138,10 +155,13 @@ GV_DEV void f29_mulsqr(fe29& r, const fe29& a, const fe29& b) {
   r = o;
 }
 
+#ifndef F29_NCH
+#define F29_NCH 1
+#endif
 // r = a * b mod p (magnitude 1).  mag(a) * mag(b) <= 6.  r may alias a or b.
-GV_DEV void f29_mul(fe29& r, const fe29& a, const fe29& b) { f29_mulsqr<false>(r, a, b); }
+GV_DEV void f29_mul(fe29& r, const fe29& a, const fe29& b) { f29_mulsqr<false, F29_NCH>(r, a, b); }
 // r = a^2 mod p (magnitude 1).  mag(a) <= 2.  r may alias a.
-GV_DEV void f29_sqr(fe29& r, const fe29& a) { f29_mulsqr<true>(r, a, a); }
+GV_DEV void f29_sqr(fe29& r, const fe29& a) { f29_mulsqr<true, F29_NCH>(r, a, a); }
 
 // ------------------------------------------------------------ linear ops
 GV_DEV void f29_set_u32(fe29& r, u32 x) {

@@ -23,11 +23,13 @@ M29 = 2**29 - 1
 PL = [(P >> (29 * i)) & M29 for i in range(9)]
 
 
-@pytest.fixture(scope="module")
-def lib():
+@pytest.fixture(scope="module", params=[1, 2], ids=["one-chain", "two-chain"])
+def lib(request):
+    """Both product engines (F29_NCH = 1: throughput kernels, 2: latency kernels)."""
     d = tempfile.mkdtemp()
-    so = os.path.join(d, "f29.so")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", so, SRC], check=True)
+    so = os.path.join(d, f"f29_{request.param}.so")
+    subprocess.run(["g++", "-O2", "-std=c++17", f"-DF29_NCH={request.param}", "-shared", "-fPIC",
+                    "-o", so, SRC], check=True)
     return ctypes.CDLL(so)
 
 

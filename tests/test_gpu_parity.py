@@ -73,6 +73,42 @@ def test_field_ops(ver, op, fn):
         assert from_words(o) == fn(a, b), (op, hex(a), hex(b))
 
 
+@pytest.mark.parametrize("op,fn", [
+    (19, lambda a, b: a * b % P),
+    (20, lambda a, b: a * a % P),
+    (21, lambda a, b: (a - b) % P),
+    (25, lambda a, b: int((a - b) % P == 0)),
+])
+def test_field29_ops(ver, op, fn):
+    """The 9 x 29 reduced-radix layer (csrc/secp_fe29.cuh) on the device: words
+    in (any value < 2^256), canonical words out, incl. the fast zero test."""
+    rng = random.Random(100 + op)
+    pairs = operand_pairs(rng, 3000)
+    if op == 25:
+        pairs += [(b + k * P, b) for b in (0, 1, 5, 2**200, P - 1) for k in (0, 1) if b + k * P < 2**256]
+        pairs += [(a, a) for a in EDGE]
+    out = run_op(ver, op, pairs)
+    for (a, b), o in zip(pairs, out):
+        assert from_words(o) == fn(a, b), (op, hex(a), hex(b))
+
+
+def test_field29_inv_sqrt_double(ver):
+    rng = random.Random(23)
+    xs = [1, 2, P - 1, 7, BETA] + [rng.randrange(1, P) for _ in range(500)]
+    out = run_op(ver, 22, [(x, 0) for x in xs])
+    for x, o in zip(xs, out):
+        assert from_words(o) == pow(x, P - 2, P)
+    out = run_op(ver, 23, [(x, 0) for x in xs])
+    for x, o in zip(xs, out):
+        assert from_words(o) == pow(x, (P + 1) // 4, P)
+    pts = [R.point_mul(k, R.G) for k in (1, 2, 3, 12345, N - 1, R.LAMBDA)]
+    pts += [R.point_mul(rng.randrange(1, N), R.G) for _ in range(64)]
+    out = run_op(ver, 24, [(p[0], p[1]) for p in pts])
+    for p, o in zip(pts, out):
+        q = R.point_add(p, p)
+        assert from_words(o, 0) == q[0] and from_words(o, 8) == q[1]
+
+
 def test_mul512(ver):
     rng = random.Random(7)
     pairs = operand_pairs(rng, 3000)
@@ -98,6 +134,17 @@ def test_scalar_montmul(ver):
     pairs = [(a, b) for a in (0, 1, N - 1, 2) for b in (0, 1, N - 1, 3)]
     pairs += [(rng.randrange(N), rng.randrange(N)) for _ in range(3000)]
     out = run_op(ver, 8, pairs)
+    for (a, b), o in zip(pairs, out):
+        assert from_words(o) == a * b * Rinv % N
+
+
+def test_scalar29_montmul(ver):
+    """Radix-2^29 Montgomery product mod n (csrc/secp_sc29.cuh), R = 2^261."""
+    rng = random.Random(29)
+    Rinv = pow(2**261, -1, N)
+    pairs = [(a, b) for a in (0, 1, N - 1, 2, 2**256 - 1) for b in (0, 1, N - 1, 3, 2**256 - 1)]
+    pairs += [(rng.randrange(2**256), rng.randrange(2**256)) for _ in range(3000)]
+    out = run_op(ver, 26, pairs)
     for (a, b), o in zip(pairs, out):
         assert from_words(o) == a * b * Rinv % N
 

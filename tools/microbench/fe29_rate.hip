@@ -37,6 +37,14 @@ __global__ __launch_bounds__(256) void k_mul29(u32* out, u32 s) {
   for (int i = 0; i < ITERS; ++i) { f29_mul(a, a, b); f29_mul(b, b, a); }
   u32 w[8]; f29_to_words(w, a); put(out, 0, g, w);
 }
+__global__ __launch_bounds__(256) void k_mul29x2(u32* out, u32 s) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  fe a0, b0; seed_fe(a0, g, s); seed_fe(b0, g, s + 1);
+  fe29 a, b; f29_from_words(a, a0.v); f29_from_words(b, b0.v);
+#pragma unroll 1
+  for (int i = 0; i < ITERS; ++i) { f29_mulsqr<false, 2>(a, a, b); f29_mulsqr<false, 2>(b, b, a); }
+  u32 w[8]; f29_to_words(w, a); put(out, 0, g, w);
+}
 __global__ __launch_bounds__(256) void k_sqr32(u32* out, u32 s) {
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   fe a, b; seed_fe(a, g, s); seed_fe(b, g, s + 1);
@@ -123,7 +131,20 @@ static int cmp(const char* what, u32* d0, u32* d1, size_t words) {
   return 0;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  if (argc > 1) {   // latency mode: one wave per SIMD, ns per dependent operation
+    const int blocks = 256;
+    u32* d; CHK(hipMalloc(&d, (size_t)blocks * 256 * 24 * 4));
+    printf("{\"mode\": \"latency, 1 wave/SIMD, ms for %d dependent ops per lane\"}\n", 2 * ITERS);
+    if (run("lat fe_mul 8x32", k_mul32, blocks, d, 2.0 * ITERS)) return 1;
+    if (run("lat fe_mul 9x29 one-chain", k_mul29, blocks, d, 2.0 * ITERS)) return 1;
+    if (run("lat fe_mul 9x29 two-chain", k_mul29x2, blocks, d, 2.0 * ITERS)) return 1;
+    if (run("lat fe_sqr 8x32", k_sqr32, blocks, d, 2.0 * ITERS)) return 1;
+    if (run("lat fe_sqr 9x29", k_sqr29, blocks, d, 2.0 * ITERS)) return 1;
+    if (run("lat gej_double 8x32", k_dbl32, blocks, d, ITERS)) return 1;
+    if (run("lat gej_double 9x29", k_dbl29, blocks, d, ITERS)) return 1;
+    return 0;
+  }
   const int blocks = 256 * 8;
   const size_t lanes = (size_t)blocks * 256;
   u32 *d0, *d1;
@@ -131,6 +152,8 @@ int main() {
   if (run("fe_mul 8x32", k_mul32, blocks, d0, 2.0 * ITERS)) return 1;
   if (run("fe_mul 9x29", k_mul29, blocks, d1, 2.0 * ITERS)) return 1;
   if (cmp("mul", d0, d1, lanes * 8)) return 1;
+  if (run("fe_mul 9x29 two-chain", k_mul29x2, blocks, d1, 2.0 * ITERS)) return 1;
+  if (cmp("mul2", d0, d1, lanes * 8)) return 1;
   if (run("fe_sqr 8x32", k_sqr32, blocks, d0, 2.0 * ITERS)) return 1;
   if (run("fe_sqr 9x29", k_sqr29, blocks, d1, 2.0 * ITERS)) return 1;
   if (cmp("sqr", d0, d1, lanes * 8)) return 1;
