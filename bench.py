@@ -99,19 +99,46 @@ def cpu_baseline(pub, sig, dig, threads: int):
             "serial_value": round(serial, 1)}
 
 
-def checktx_latency(ver, pub, sig, dig, sizes=(1, 16, 32, 64, 128, 256), reps=200):
-    """C5: host-path latency (pack -> H2D -> kernels -> D2H) per batch size."""
+def _pct(ts):
+    ts = np.array(ts) * 1e3
+    return round(float(np.percentile(ts, 50)), 3), round(float(np.percentile(ts, 99)), 3)
+
+
+def checktx_latency(ver, pub, sig, dig, threads, sizes=(1, 16, 32, 64, 128, 256, 1024, 4096), reps=200):
+    """C5: host-path latency (pack -> H2D -> kernel(s) -> D2H -> verdicts) per
+    batch size.  p50/p99 are the default GPU path (the fused latency kernel,
+    gv_lat.hip, up to the "lat_max" option); next to it the throughput pipeline
+    forced for the same batches, and the CPU oracle (oracle/secp256k1_oracle.c,
+    the reference algorithm restated in C) serial and on `threads` cores."""
+    from oracle import oracle as O
+    O.lib()
     out = {}
     for b in sizes:
-        ts = []
-        for r in range(reps + 5):
-            o = (r * b) % (len(pub) - b)
-            t = time.perf_counter()
-            ver.verify_batch_digests(pub[o:o + b], sig[o:o + b], dig[o:o + b])
-            ts.append(time.perf_counter() - t)
-        ts = np.array(ts[5:]) * 1e3
-        out[str(b)] = {"p50_ms": round(float(np.percentile(ts, 50)), 3),
-                       "p99_ms": round(float(np.percentile(ts, 99)), 3)}
+        def run_gpu(rr):
+            ts = []
+            for r in range(rr + 5):
+                o = (r * b) % (len(pub) - b)
+                t = time.perf_counter()
+                ver.verify_batch_digests(pub[o:o + b], sig[o:o + b], dig[o:o + b])
+                ts.append(time.perf_counter() - t)
+            return ts[5:]
+        p50, p99 = _pct(run_gpu(reps))
+        ver.set_option("lat_max", 0)
+        tp50, _ = _pct(run_gpu(max(20, reps // 4)))
+        ver.set_option("lat_max", 4096)
+        cpu = {}
+        for label, th in (("cpu_serial_p50_ms", 1), ("cpu_allcore_p50_ms", threads)):
+            ts = []
+            budget = time.perf_counter() + 1.0
+            for r in range(50):
+                o = (r * b) % (len(pub) - b)
+                t = time.perf_counter()
+                O.verify_digests(pub[o:o + b], sig[o:o + b], dig[o:o + b], threads=th)
+                ts.append(time.perf_counter() - t)
+                if time.perf_counter() > budget and len(ts) >= 3:
+                    break
+            cpu[label] = _pct(ts)[0]
+        out[str(b)] = {"p50_ms": p50, "p99_ms": p99, "throughput_path_p50_ms": tp50, **cpu}
     return out
 
 
@@ -262,7 +289,7 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
     }
 
     if rank == 0 and world == 1 and not args.no_latency:
-        lat = checktx_latency(ver, pub, sig, dig)
+        lat = checktx_latency(ver, pub, sig, dig, args.threads)
         result["checktx_latency_ms"] = lat
         result["checktx_p50_ms_64"] = lat["64"]["p50_ms"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -42,7 +42,29 @@ typedef struct gvk_batch {
   hipEvent_t ev[3];             // optional: after unpack/sha, after prep, after ecmult
 } gvk_batch;
 
+// Small-batch latency path (gv_lat.hip): GV_LAT_SIGS signatures per block of
+// 128 threads, one fused kernel (after k_sha256 on the message path).  bits
+// receives ceil(n / GV_LAT_SIGS) 16-bit words (the caller zeroes the tail of
+// the last 64-bit word).
+#define GV_LAT_SIGS 16
+typedef struct gvk_lat {
+  uint32_t n, C;                // C: stride of e_soa rows (>= n)
+  const uint8_t* pub33;
+  const uint8_t* sig64;
+  const uint8_t* dig32;
+  const uint8_t* msg_blob;
+  const uint64_t* msg_off;
+  const uint32_t* msg_len;
+  const uint32_t* gtab;
+  uint32_t* e_soa;              // message path: 8 rows of C words
+  uint64_t* bits;
+  hipEvent_t ev[1];             // optional: after the SHA stage
+} gvk_lat;
+
 hipError_t gvk_gen_gtable(uint32_t* gtab, hipStream_t st);
+hipError_t gvk_verify_lat(const gvk_lat* b, hipStream_t st);
+hipError_t gvk_sha256(const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint32_t n, uint32_t C,
+                      uint32_t* e, hipStream_t st);
 hipError_t gvk_verify(const gvk_batch* b, hipStream_t st);
 hipError_t gvk_debug(int op, uint32_t n, const uint32_t* in, uint32_t* out, hipStream_t st);
 

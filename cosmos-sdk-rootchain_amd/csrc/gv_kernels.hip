@@ -188,25 +188,6 @@ __global__ __launch_bounds__(256) void k_sha256(const uint8_t* blob, const uint6
 }
 
 // ------------------------------------------------------------ ladder helpers
-// Signed fixed-window (Booth) digit of a 128-bit magnitude k at window `win`
-// of width W: d = (bits [W*win-1 .. W*win+W-1]) recoded into [-2^(W-1), 2^(W-1)].
-template <int W>
-GV_DEV int booth_digit(const u32 k[4], int win) {
-  const int p = W * win - 1;          // lowest bit position used (borrow bit)
-  u32 v;
-  if (p < 0) {
-    v = (k[0] << 1) & ((1u << (W + 1)) - 1u);
-  } else {
-    const int limb = p >> 5, sh = p & 31;
-    u32 lo = limb == 0 ? k[0] : limb == 1 ? k[1] : limb == 2 ? k[2] : limb == 3 ? k[3] : 0u;
-    u32 hi = limb == 0 ? k[1] : limb == 1 ? k[2] : limb == 2 ? k[3] : 0u;
-    u32 w = (u32)((((u64)hi << 32) | lo) >> sh);
-    v = w & ((1u << (W + 1)) - 1u);
-  }
-  const int mag = (int)((v >> 1) & ((1u << (W - 1)) - 1u)) + (int)(v & 1u);
-  return mag - (int)((v >> W) << (W - 1));
-}
-
 // One lane's Q table: m*Q for m = 1..GV_QTAB_N in the isomorphic-curve affine
 // representation with a shared Z (returned in zq).  qt layout: the first
 // C*16*16 words hold the entries lane-major (AoS): lane g, entry m at
@@ -776,6 +757,12 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   hipLaunchKernelGGL(gv::k_ecmult, grd, blk, 0, st, b->gtab, b->n, C, b->digits, b->qtab, b->zq, b->flags,
                      b->in_r, b->bits);
   if (b->ev[2]) (void)hipEventRecord(b->ev[2], st);
+  return hipGetLastError();
+}
+
+hipError_t gvk_sha256(const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint32_t n, uint32_t C,
+                      uint32_t* e, hipStream_t st) {
+  hipLaunchKernelGGL(gv::k_sha256, dim3(C / 256), dim3(256), 0, st, blob, off, len, n, C, e);
   return hipGetLastError();
 }
 

@@ -1,0 +1,429 @@
+// gv_lat.hip -- the small-batch (CheckTx mempool) latency
+// path of the secp256k1 verifier: one fused kernel, the work of each
+// signature spread over several lanes and two waves.
+//
+// Same verdict as the throughput pipeline (gv_kernels.hip) and the reference
+// (x/auth/ante/sigverify.go:210 -> tendermint VerifyBytes -> btcec /
+// crypto/ecdsa.Verify): identical checks, identical group law; only the
+// schedule differs.  A throughput launch gives each signature one lane and
+// runs the stages back to back, so a batch of 64 costs the full serial chain
+// of one lane (~1 ms).  Here a block of 128 threads takes LAT_SIGS = 16
+// signatures:
+//   wave 0, lanes 4s..4s+3 (signature s): pubkey decompression (sqrt chain),
+//           then the Q and lambda*Q tables in LDS;
+//   wave 1, lane s:  range / low-S checks, s^-1 (Fermat, radix-2^29
+//           Montgomery), u1 = e w, u2 = r w, GLV split, Booth digits -> LDS.
+//   The two chains run concurrently; one barrier.
+//   wave 0 ladder: lane 4s + k accumulates ONE of the four partial sums
+//           k1q*Q, k2q*(lambda Q), k1g*G, k2g*(lambda G) (125 doublings and
+//           <= 26 additions instead of 125 and 66 on one lane), then two
+//           cross-lane rounds of complete Jacobian additions combine them and
+//           lane 4s runs the final x(R) == r check.
+// The field layer is compiled with F29_NCH = 2 (two interleaved mad chains
+// per column): a single wave per SIMD waits on every dependent mad, and the
+// second chain fills those slots (tools/microbench/fe29_rate.hip, latency
+// mode).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "secp_field.cuh"
+#include "secp_scalar.cuh"
+#include "secp_group29.cuh"
+#include "secp_sc29.cuh"
+#include "gv_kernels.h"
+
+static_assert(F29_NCH == 2, "gv_lat.hip is built with -DF29_NCH=2");
+
+namespace gv {
+
+static __constant__ const u32 kLBeta[8] = {0x719501EEu, 0xC1396C28u, 0x12F58995u, 0x9CF04975u,
+                                           0xAC3434E9u, 0x6E64479Eu, 0x657C0710u, 0x7AE96A2Bu};
+static __constant__ const u32 kLP[8] = {0xFFFFFC2Fu, 0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu,
+                                        0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+
+struct LatShared {
+  u32 qtab[GV_LAT_SIGS][2][GV_QTAB_N][16];  // Q, lambda*Q entries: x words, y words (effective affine)
+  u32 ratio[64][GV_QTAB_N - 1][8];          // per-lane Z-ratio scratch of the table build
+  u32 dq[GV_LAT_SIGS][GV_QWIN];             // packed int16 Q / lambda*Q digits per window
+  int dg[GV_LAT_SIGS][GV_GWIN][2];          // G / lambda*G digits
+  u32 zq[GV_LAT_SIGS][8];
+  u32 r[GV_LAT_SIGS][8];
+  u32 okp[GV_LAT_SIGS];                     // pubkey checks passed (wave 0)
+  u32 oks[GV_LAT_SIGS];                     // bit 0: scalar checks passed, bit 1: r < p - n (wave 1)
+};
+
+GV_DEV u32 be32(const uint8_t* p) {
+  return ((u32)p[0] << 24) | ((u32)p[1] << 16) | ((u32)p[2] << 8) | (u32)p[3];
+}
+
+GV_DEV void lds_put_ent(u32* e, const fe29& x, const fe29& y) {
+  u32 w[8];
+  f29_to_words(w, x);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) e[i] = w[i];
+  f29_to_words(w, y);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) e[8 + i] = w[i];
+}
+GV_DEV void lds_get_ent(fe29& x, fe29& y, const u32* e) {
+  u32 w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = e[i];
+  f29_from_words(x, w);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = e[8 + i];
+  f29_from_words(y, w);
+}
+
+// Wave 0 prep for one signature (all four lanes of it compute; slot 0 stores).
+// Table build as build_q_table in gv_kernels.hip (co-Z chain + one
+// back-propagation of the Z ratios), into LDS; the back-propagation also
+// writes the lambda*Q entry (beta*x, y).
+GV_DEV void lat_pubkey_and_tables(LatShared& sh, int sig, int slot, bool live, const uint8_t* pub33) {
+  const uint8_t* p = pub33;
+  u32 pre = live ? p[0] : 0u;
+  fe x8;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x8.v[i] = live ? be32(p + 1 + 4 * (7 - i)) : 0u;
+  bool ok = live && (pre & 0xFEu) == 0x02u;
+  {
+    u32 br = 0, d;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d = __builtin_subc(x8.v[i], kLP[i], br, &br);
+    (void)d;
+    ok &= (br != 0);                                    // x < p
+  }
+  fe y8;
+  {
+    fe29 x29, c, y29, y2, seven;
+    f29_from_words(x29, x8.v);
+    f29_sqr(c, x29);
+    f29_mul(c, c, x29);
+    f29_set_u32(seven, 7);
+    f29_add(c, c, seven);                               // x^3 + 7
+    f29_sqrt_candidate(y29, c);
+    f29_sqr(y2, y29);
+    ok &= f29_equal(y2, c);                             // "invalid square root"
+    f29_to_words(y8.v, y29);
+  }
+  if ((y8.v[0] & 1u) != (pre & 1u)) fe_neg(y8, y8);
+  fe_normalize(y8);
+  if (!ok) {                                          // harmless stand-in point: G
+    const u32 gx[8] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu,
+                       0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu};
+    const u32 gy[8] = {0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
+                       0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { x8.v[i] = gx[i]; y8.v[i] = gy[i]; }
+  }
+  const bool st = slot == 0;
+  u32 (*qt)[16] = sh.qtab[sig][0];
+  u32 (*lt)[16] = sh.qtab[sig][1];
+  u32 (*qr)[8] = sh.ratio[sig * 4 + slot];
+  fe29 qx, qy, X1, Y1, X2, Y2, t, u;
+  f29_from_words(qx, x8.v);
+  f29_from_words(qy, y8.v);
+  {
+    fe29 B, E, L, M;
+    f29_sqr(B, qx);
+    f29_sqr(E, qy);
+    f29_sqr(L, E);
+    f29_add(t, qx, E);
+    f29_sqr(t, t);
+    f29_sub<1>(t, t, B);
+    f29_sub_norm<1>(t, t, L);
+    f29_shl_norm<1>(X1, t);                           // S = 4xy^2
+    f29_mul3_norm(M, B);
+    f29_sqr(t, M);
+    f29_add(u, X1, X1);
+    f29_sub_norm<2>(X2, t, u);                        // 2Q.x
+    f29_shl_norm<3>(Y1, L);                           // 8y^4
+    f29_sub<1>(t, X1, X2);
+    f29_mul(t, M, t);
+    f29_sub_norm<1>(Y2, t, Y1);                       // 2Q.y
+  }
+  if (st) { lds_put_ent(qt[0], X1, Y1); lds_put_ent(qt[1], X2, Y2); }
+  for (int m = 2; m < GV_QTAB_N; ++m) {
+    fe29 h, rr, c, w1, w2, d, a1;
+    f29_sub_norm<1>(h, X1, X2);
+    {
+      u32 w[8];
+      f29_to_words(w, h);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) qr[m - 2][i] = w[i];  // lane-private
+    }
+    f29_sub_norm<1>(rr, Y1, Y2);
+    f29_sqr(c, h);
+    f29_mul(w1, X1, c);
+    f29_mul(w2, X2, c);
+    f29_sqr(d, rr);
+    f29_sub<1>(t, w1, w2);
+    f29_mul(a1, Y1, t);
+    f29_add(u, w1, w2);
+    f29_sub_norm<2>(X2, d, u);
+    f29_sub<1>(t, w1, X2);
+    f29_mul(t, rr, t);
+    f29_sub_norm<1>(Y2, t, a1);
+    X1 = w1;
+    Y1 = a1;
+    if (st) lds_put_ent(qt[m], X2, Y2);
+  }
+  // Back-propagation: entry m-1 scaled to the last entry's Z (as in
+  // build_q_table: entry index j lives on Z_max(j,1), ratio[k] = Z_(k+2) /
+  // Z_(k+1)).  Every lane reads the entries its signature's slot-0 lane stored
+  // above (same wave, earlier instructions: LDS executes one wave's operations
+  // in order); the lambda*Q entry (beta*x, y) is written alongside.
+  fe29 acc, beta;
+  {
+    u32 w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = kLBeta[i];
+    f29_from_words(beta, w);
+  }
+  for (int m = GV_QTAB_N; m >= 1; --m) {
+    fe29 x, y;
+    lds_get_ent(x, y, qt[m - 1]);
+    if (m < GV_QTAB_N) {
+      if (m >= 2) {
+        u32 w[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = qr[m - 2][i];
+        fe29 ratio;
+        f29_from_words(ratio, w);                     // Z_m / Z_(m-1)
+        if (m == GV_QTAB_N - 1) acc = ratio;
+        else f29_mul(acc, acc, ratio);
+      }
+      fe29 a2, a3;
+      f29_sqr(a2, acc);
+      f29_mul(a3, a2, acc);
+      f29_mul(x, x, a2);
+      f29_mul(y, y, a3);
+      if (st) lds_put_ent(qt[m - 1], x, y);
+    }
+    f29_mul(t, x, beta);
+    if (st) lds_put_ent(lt[m - 1], t, y);
+  }
+  f29_add(t, qy, qy);
+  f29_mul(t, t, acc);                                 // Z_15 = 2y * prod(ratios)
+  if (st) {
+    u32 w[8];
+    f29_to_words(w, t);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sh.zq[sig][i] = w[i];
+    sh.okp[sig] = ok ? 1u : 0u;
+  }
+}
+
+
+// Wave 1: the scalar chain of one signature (lane sig < GV_LAT_SIGS).
+GV_DEV void lat_scalars(LatShared& sh, int sig, bool live, const uint8_t* sig64, const uint8_t* dig32,
+                        const u32* e_soa, u32 C, u32 gi) {
+  u32 r[8], s[8], e[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    r[i] = live ? be32(sig64 + 4 * (7 - i)) : 0u;
+    s[i] = live ? be32(sig64 + 32 + 4 * (7 - i)) : 0u;
+    e[i] = !live ? 0u : dig32 ? be32(dig32 + 4 * (7 - i)) : e_soa[(size_t)i * C + gi];
+  }
+  bool ok = live;
+  ok &= !u256_is_zero(r);
+  ok &= !u256_geq(r, kN);
+  ok &= !u256_is_zero(s);
+  ok &= u256_geq(kHalfN, s);                // tendermint low-S: s <= N/2
+  const bool r_small = !u256_geq(r, kPminusN);
+  sc_reduce_once(e);                        // e mod n
+  if (!ok) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { s[i] = (i == 0) ? 1u : 0u; e[i] = 0u; r[i] = 0u; }
+  }
+  u32 u1[8], u2[8];
+  {
+    sc29 s29, sm, w, e29, r29, t;
+    sc29_from_words(s29, s);
+    sc29_to_mont(sm, s29);
+    sc29_inv(w, sm);                        // s^-1 (Montgomery form)
+    sc29_from_words(e29, e);
+    sc29_from_words(r29, r);
+    sc29_mul(t, e29, w);
+    sc29_to_words(u1, t);                   // e * s^-1
+    sc29_mul(t, r29, w);
+    sc29_to_words(u2, t);                   // r * s^-1
+  }
+  u32 k1g[4], k2g[4], k1q[4], k2q[4], n1g, n2g, n1q, n2q;
+  glv_split(k1g, n1g, k2g, n2g, u1);
+  glv_split(k1q, n1q, k2q, n2q, u2);
+  if (!ok) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { k1g[i] = k2g[i] = k1q[i] = k2q[i] = 0u; }
+  }
+#pragma unroll
+  for (int win = 0; win < GV_QWIN; ++win) {
+    int d0 = booth_digit<GV_QW>(k1q, win), d1 = booth_digit<GV_QW>(k2q, win);
+    if (n1q) d0 = -d0;
+    if (n2q) d1 = -d1;
+    sh.dq[sig][win] = ((u32)d0 & 0xFFFFu) | ((u32)d1 << 16);
+  }
+#pragma unroll
+  for (int j = 0; j < GV_GWIN; ++j) {
+    int d2 = booth_digit<GV_GW>(k1g, j), d3 = booth_digit<GV_GW>(k2g, j);
+    if (n1g) d2 = -d2;
+    if (n2g) d3 = -d3;
+    sh.dg[sig][j][0] = d2;
+    sh.dg[sig][j][1] = d3;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sh.r[sig][i] = r[i];
+  sh.oks[sig] = (ok ? 1u : 0u) | (r_small ? 2u : 0u);
+}
+
+GV_DEV void shfl_xor_gej(gej29& o, bool& oinf, const gej29& a, bool ainf, int m) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    o.x.n[i] = (u32)__shfl_xor((int)a.x.n[i], m, 64);
+    o.y.n[i] = (u32)__shfl_xor((int)a.y.n[i], m, 64);
+    o.z.n[i] = (u32)__shfl_xor((int)a.z.n[i], m, 64);
+  }
+  oinf = __shfl_xor((int)ainf, m, 64) != 0;
+}
+
+// One block = GV_LAT_SIGS signatures, 128 threads.  Inputs: AoS bytes as in
+// gv_verify_digests; e from dig32 (digest path) or from the SoA rows e_soa
+// written by k_sha256 (message path, stride C).  Output: 16 verdict bits per
+// block, bits16[block] (the u64 bitmap viewed as u16 words).
+__global__ __launch_bounds__(128) void k_verify_lat(const u32* gtab, const uint8_t* pub33,
+                                                     const uint8_t* sig64, const uint8_t* dig32,
+                                                     const u32* e_soa, u32 C, u32 n, uint16_t* bits16) {
+  __shared__ LatShared sh;
+  const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  if (wave == 0) {
+    const int sig = lane >> 2, slot = lane & 3;
+    const u32 gi = blockIdx.x * GV_LAT_SIGS + sig;
+    const bool live = gi < n;
+    lat_pubkey_and_tables(sh, sig, slot, live, pub33 + (size_t)(live ? gi : 0) * 33u);
+  } else if (lane < GV_LAT_SIGS) {
+    const u32 gi = blockIdx.x * GV_LAT_SIGS + lane;
+    const bool live = gi < n;
+    const u32 gs = live ? gi : 0u;
+    lat_scalars(sh, lane, live, sig64 + (size_t)gs * 64u, dig32 ? dig32 + (size_t)gs * 32u : nullptr,
+                e_soa, C, gs);
+  }
+  __syncthreads();
+  if (wave != 0) return;
+
+  // ---- ladder: lane 4s + slot accumulates one of the four partial sums
+  const int sig = lane >> 2, slot = lane & 3;
+  gej29 acc;
+  f29_set_zero(acc.x); f29_set_zero(acc.y); f29_set_zero(acc.z);
+  bool inf = true;
+#pragma unroll 1
+  for (int win = GV_QWIN - 1; win >= 0; --win) {
+    if (win != GV_QWIN - 1) {
+#pragma unroll 1
+      for (int d = 0; d < GV_QW; ++d) gej29_double(acc, acc);
+    }
+    const bool gwin = (win % GV_GSTEP) == 0;          // block-uniform
+    const u32 dq = sh.dq[sig][win];
+    int d;
+    if (slot < 2) d = slot == 0 ? ((int)(dq << 16) >> 16) : ((int)dq >> 16);
+    else d = gwin ? sh.dg[sig][win / GV_GSTEP][slot - 2] : 0;
+    if (d != 0) {
+      const u32 e = (u32)((d < 0 ? -d : d) - 1);
+      fe29 x, y;
+      if (slot < 2) {
+        lds_get_ent(x, y, sh.qtab[sig][slot][e]);
+      } else {
+        const uint4* p = (const uint4*)(gtab + ((size_t)(slot == 3 ? GV_GTAB_N : 0) + e) * 16);
+        uint4 a = p[0], b = p[1], c = p[2], dd = p[3];
+        u32 wx[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        u32 wy[8] = {c.x, c.y, c.z, c.w, dd.x, dd.y, dd.z, dd.w};
+        f29_from_words(x, wx);
+        f29_from_words(y, wy);
+      }
+      if (d < 0) f29_neg<1>(y, y);
+      // Q slots live on the isomorphic curve of the shared table Z, G slots on
+      // the real curve: either way the entry is affine on the lane's curve.
+      fe29 az, z2, u2, s2;
+      if (inf) f29_set_u32(az, 1);
+      else az = acc.z;
+      f29_sqr(z2, az);
+      f29_mul(u2, x, z2);
+      f29_mul(z2, z2, az);
+      f29_mul(s2, y, z2);
+      if (inf) {
+        acc.x = u2; acc.y = s2; f29_set_u32(acc.z, 1); inf = false;
+      } else {
+        gej29_add_tail(acc, inf, u2, s2);
+      }
+    }
+  }
+
+  // ---- combine: Q-slot points back to the real curve (Z *= zq), then two
+  // rounds of complete additions across the signature's four lanes.
+  {
+    u32 w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = sh.zq[sig][i];
+    fe29 zq;
+    f29_from_words(zq, w);
+    if (slot >= 2) f29_set_u32(zq, 1);
+    f29_mul(acc.z, acc.z, zq);
+  }
+  gej29 other;
+  bool oinf;
+  shfl_xor_gej(other, oinf, acc, inf, 1);
+  gej29_add_gej(acc, inf, acc, inf, other, oinf);
+  shfl_xor_gej(other, oinf, acc, inf, 2);
+  gej29_add_gej(acc, inf, acc, inf, other, oinf);
+
+  // ---- final check (as k_ecmult): x(R) mod n == r, without inversion
+  const u32 fl = sh.oks[sig];
+  bool ok = (fl & 1u) && sh.okp[sig] && !inf;
+  fe29 zz, rf, t;
+  f29_sqr(zz, acc.z);
+  u32 rw[8], X[8], tw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rw[i] = sh.r[sig][i];
+  f29_from_words(rf, rw);
+  f29_mul(t, rf, zz);
+  f29_to_words(X, acc.x);
+  f29_to_words(tw, t);
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) eq &= (X[i] == tw[i]);
+  if (!eq && (fl & 2u)) {
+    u32 rn[8], c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rn[i] = __builtin_addc(rw[i], kN[i], c, &c);
+    f29_from_words(rf, rn);
+    f29_mul(t, rf, zz);
+    f29_to_words(tw, t);
+    eq = true;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) eq &= (X[i] == tw[i]);
+  }
+  ok &= eq;
+  const uint64_t m = __ballot(ok && slot == 0);
+  if (lane == 0) {
+    u32 b16 = 0;
+#pragma unroll
+    for (int s2 = 0; s2 < GV_LAT_SIGS; ++s2) b16 |= (u32)((m >> (4 * s2)) & 1u) << s2;
+    bits16[blockIdx.x] = (uint16_t)b16;
+    if (blockIdx.x == gridDim.x - 1) {           // zero the rest of the last 64-bit word
+      for (u32 k = blockIdx.x + 1; (k & 3u) != 0u; ++k) bits16[k] = 0;
+    }
+  }
+}
+
+}  // namespace gv
+
+extern "C" hipError_t gvk_verify_lat(const gvk_lat* b, hipStream_t st) {
+  const uint32_t blocks = (b->n + GV_LAT_SIGS - 1) / GV_LAT_SIGS;
+  if (b->msg_blob) {
+    hipError_t e = gvk_sha256(b->msg_blob, b->msg_off, b->msg_len, b->n, b->C, b->e_soa, st);
+    if (e != hipSuccess) return e;
+  }
+  if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
+  hipLaunchKernelGGL(gv::k_verify_lat, dim3(blocks), dim3(128), 0, st, b->gtab, b->pub33, b->sig64,
+                     b->msg_blob ? nullptr : b->dig32, b->msg_blob ? (const uint32_t*)b->e_soa : nullptr,
+                     b->C, b->n, (uint16_t*)b->bits);
+  return hipGetLastError();
+}

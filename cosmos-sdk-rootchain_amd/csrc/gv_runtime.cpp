@@ -109,6 +109,7 @@ int ensure_hbits(Dev* d, size_t words) {
 struct gv_ctx {
   std::vector<Dev*> devs;
   size_t max_batch = size_t(1) << 20;
+  size_t lat_max = 4096;        // batches up to this size take the fused latency kernel (gv_lat.hip)
   bool time_kernels = false;
   bool fault_inject = false;
 };
@@ -139,7 +140,23 @@ int launch(gv_ctx* ctx, Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig
     CK(hipEventRecord(rs[3], st));
     b.ev[0] = rs[0]; b.ev[1] = rs[1]; b.ev[2] = rs[2];
   }
-  CK(gvk_verify(&b, st));
+  if (n <= ctx->lat_max) {
+    // small batch: one fused kernel, several lanes per signature (gv_lat.hip)
+    gvk_lat lb;
+    memset(&lb, 0, sizeof lb);
+    lb.n = (uint32_t)n; lb.C = (uint32_t)C;
+    lb.pub33 = pub; lb.sig64 = sig; lb.dig32 = dig;
+    lb.msg_blob = blob; lb.msg_off = off; lb.msg_len = len;
+    lb.gtab = d->gtab; lb.e_soa = d->in_e; lb.bits = bits_out;
+    lb.ev[0] = b.ev[0];
+    CK(gvk_verify_lat(&lb, st));
+    if (rs) {                                   // stages: SHA | fused kernel | (none)
+      CK(hipEventRecord(rs[1], st));
+      CK(hipEventRecord(rs[2], st));
+    }
+  } else {
+    CK(gvk_verify(&b, st));
+  }
   if (rs) {
     // mirror the last launch into ev[] for gv_last_stage_ms
     d->last = d->ring_next;
@@ -356,7 +373,10 @@ int gv_dev_verify_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub33,
 
 int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   if (!ctx || !key) return GV_EINVAL;
-  if (!strcmp(key, "max_batch")) {
+  if (!strcmp(key, "lat_max")) {
+    if (val < 0) return GV_EINVAL;
+    ctx->lat_max = (size_t)val;
+  } else if (!strcmp(key, "max_batch")) {
     if (val < 256) return GV_EINVAL;
     ctx->max_batch = round_up((size_t)val, 256);
   } else if (!strcmp(key, "time_kernels")) {

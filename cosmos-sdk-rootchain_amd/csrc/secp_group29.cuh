@@ -105,6 +105,57 @@ GV_DEV void gej29_add_ge(gej29& a, bool& inf, const fe29& x2, const fe29& y2) {
   gej29_add_tail(a, inf, u2, s2);
 }
 
+// r = a + b for two Jacobian points of the same curve (12M + 4S), complete:
+// either infinite -> the other; a == b -> 2a; a == -b -> infinity.  In: point
+// invariant; out: X, Y, Z magnitude 1.  r may alias a or b.
+GV_DEV void gej29_add_gej(gej29& r, bool& rinf, const gej29& a, bool ainf, const gej29& b, bool binf) {
+  if (ainf || binf) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {        // per-limb selects: no address-taken struct
+      r.x.n[i] = ainf ? b.x.n[i] : a.x.n[i];
+      r.y.n[i] = ainf ? b.y.n[i] : a.y.n[i];
+      r.z.n[i] = ainf ? b.z.n[i] : a.z.n[i];
+    }
+    rinf = ainf && binf;
+    return;
+  }
+  fe29 z1z1, z2z2, u1, u2, s1, s2, t, h, rr;
+  f29_sqr(z1z1, a.z);
+  f29_sqr(z2z2, b.z);
+  f29_mul(u1, a.x, z2z2);
+  f29_mul(u2, b.x, z1z1);
+  f29_mul(t, b.z, z2z2);             // 2 x 1
+  f29_mul(s1, a.y, t);
+  f29_mul(t, a.z, z1z1);
+  f29_mul(s2, b.y, t);
+  f29_sub_norm<1>(h, u2, u1);        // 1
+  f29_sub_norm<1>(rr, s2, s1);       // 1
+  bool inf = false, dbl = false;
+  gej29 o;
+  if (f29_is_zero_fast(h)) {
+    dbl = f29_is_zero(rr);
+    inf = !dbl;
+  } else {
+    fe29 h2, h3, v, w;
+    f29_sqr(h2, h);
+    f29_mul(h3, h2, h);
+    f29_mul(v, u1, h2);
+    f29_mul(t, a.z, b.z);            // <= 2 x 2
+    f29_mul(o.z, t, h);
+    f29_sqr(t, rr);
+    f29_add(w, v, v);                // 2
+    f29_add(w, w, h3);               // 3
+    f29_sub_norm<3>(o.x, t, w);      // X3 = R^2 - H^3 - 2V: 1
+    f29_sub<1>(t, v, o.x);           // 3
+    f29_mul(t, rr, t);
+    f29_mul(h3, s1, h3);
+    f29_sub_norm<1>(o.y, t, h3);     // Y3 = R(V - X3) - S1*H^3: 1
+  }
+  if (dbl) gej29_double(o, a);
+  r = o;
+  rinf = inf;
+}
+
 // ---------------------------------------------------- exponentiation chains
 GV_DEV void f29_sqr_n(fe29& r, const fe29& a, int k) {
   r = a;

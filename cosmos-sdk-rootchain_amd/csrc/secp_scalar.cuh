@@ -235,4 +235,23 @@ GV_DEV void glv_split(u32 k1[4], u32& k1neg, u32 k2[4], u32& k2neg, const u32 k[
   to_sign_mag128(k2, k2neg, v2);
 }
 
+// Signed fixed-window (Booth) digit of a 128-bit magnitude k at window `win`
+// of width W: d = (bits [W*win-1 .. W*win+W-1]) recoded into [-2^(W-1), 2^(W-1)].
+template <int W>
+GV_DEV int booth_digit(const u32 k[4], int win) {
+  const int p = W * win - 1;          // lowest bit position used (borrow bit)
+  u32 v;
+  if (p < 0) {
+    v = (k[0] << 1) & ((1u << (W + 1)) - 1u);
+  } else {
+    const int limb = p >> 5, sh = p & 31;
+    u32 lo = limb == 0 ? k[0] : limb == 1 ? k[1] : limb == 2 ? k[2] : limb == 3 ? k[3] : 0u;
+    u32 hi = limb == 0 ? k[1] : limb == 1 ? k[2] : limb == 2 ? k[3] : 0u;
+    u32 w = (u32)((((u64)hi << 32) | lo) >> sh);
+    v = w & ((1u << (W + 1)) - 1u);
+  }
+  const int mag = (int)((v >> 1) & ((1u << (W - 1)) - 1u)) + (int)(v & 1u);
+  return mag - (int)((v >> W) << (W - 1));
+}
+
 }  // namespace gv

@@ -98,6 +98,8 @@ int gv_dev_copy(gv_ctx* ctx, int dev_slot, void* dst, const void* src, size_t by
 int gv_dev_sync(gv_ctx* ctx, int dev_slot);
 
 /* Options: "max_batch" (lanes per device launch, default 1<<20),
+ * "lat_max" (batches of at most this many items -- per device slice -- take
+ * the fused small-batch latency kernel, default 4096; 0 = never),
  * "time_kernels" (0/1: record HIP events around each kernel stage),
  * "fault_inject" (0/1: every verify call fails with GV_EFAULT; test hook). */
 int gv_set_option(gv_ctx* ctx, const char* key, long long val);

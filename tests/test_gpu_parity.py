@@ -177,14 +177,27 @@ def test_point_double(ver):
 
 
 # ------------------------------------------------------------ full verification
-def test_golden_digest_vectors(ver):
+# Two schedules compute every verdict: the throughput pipeline (gv_kernels.hip,
+# one lane per signature) and the fused small-batch latency kernel
+# (gv_lat.hip, four lanes per signature); "lat_max" picks one per call.
+PATHS = {"throughput": 0, "latency": 1 << 30}
+
+
+@pytest.fixture(params=sorted(PATHS))
+def path(request, ver):
+    ver.set_option("lat_max", PATHS[request.param])
+    yield request.param
+    ver.set_option("lat_max", 4096)
+
+
+def test_golden_digest_vectors(ver, path):
     pub, sig, dig, ok, cats = load_digest_vectors()
     got = ver.verify_batch_digests(pub, sig, dig)
     bad = [(i, cats[i], int(ok[i])) for i in range(len(ok)) if got[i] != ok[i]]
     assert not bad, bad[:20]
 
 
-def test_golden_message_vectors(ver):
+def test_golden_message_vectors(ver, path):
     pub, sig, msgs, ok, cats = load_msg_vectors()
     got = ver.verify_batch_msgs(pub, sig, msgs)
     bad = [(i, cats[i], int(ok[i])) for i in range(len(ok)) if got[i] != ok[i]]
@@ -221,7 +234,7 @@ def make_random_batch(n, seed, adversarial=0.25, nkeys=257):
     return pub, sig, dig
 
 
-def test_random_adversarial_batch_vs_oracle(ver):
+def test_random_adversarial_batch_vs_oracle(ver, path):
     pub, sig, dig = make_random_batch(20000, seed=0xC3)
     want = O.verify_digests(pub, sig, dig, threads=16)
     got = ver.verify_batch_digests(pub, sig, dig)
@@ -230,8 +243,8 @@ def test_random_adversarial_batch_vs_oracle(ver):
     assert bad.size == 0, bad[:20]
 
 
-@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 256, 257, 1000])
-def test_ragged_sizes_and_bitmap(ver, n):
+@pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 63, 64, 65, 255, 256, 257, 1000])
+def test_ragged_sizes_and_bitmap(ver, n, path):
     pub, sig, dig = make_random_batch(n, seed=n, adversarial=0.3, nkeys=7)
     want = O.verify_digests(pub, sig, dig, threads=8)
     assert np.array_equal(ver.verify_batch_digests(pub, sig, dig), want)
