@@ -11,7 +11,8 @@
 #define GV_GTAB_N (1 << (GV_GW - 1))   // multiples 1..2^(GV_GW-1) per table (64 B each)
 #define GV_GSTEP (GV_GW / GV_QW)       // Q windows per G window
 #define GV_QTAB_N 16            // multiples 1..2^(GV_QW-1) of Q per lane
-#define GV_QTAB_WORDS (GV_QTAB_N * 16 + (GV_QTAB_N - 1) * 8)  // per lane: entries x,y (AoS) + Z-ratio rows (SoA)
+#define GV_QENT_WORDS 20        // Q-table entry: x[9], y[9] raw 29-bit limbs + 2 pad words (80 B)
+#define GV_QTAB_WORDS (GV_QTAB_N * GV_QENT_WORDS + (GV_QTAB_N - 1) * 9)  // per lane: entries (AoS) + Z-ratio rows (SoA)
 #define GV_QWIN 26              // Q windows over a 128-bit GLV half: positions 0,5,..,125
 #define GV_GWIN ((GV_QWIN - 1) / GV_GSTEP + 1)   // G windows at positions 0, GV_GW, ..
 #define GV_DIGIT_ROWS (GV_QWIN + 2 * GV_GWIN)    // Q: packed int16 pair per window; G: int32 per digit

@@ -219,23 +219,46 @@ GV_DEV void load_qent(fe& x, fe& y, const u32* qt, u32 g, u32 j) {
   y.v[4] = d.x; y.v[5] = d.y; y.v[6] = d.z; y.v[7] = d.w;
 }
 
-GV_DEV void store_qent29(u32* qt, u32 g, int j, const fe29& x29, const fe29& y29) {
-  fe x, y;
-  f29_to_words(x.v, x29);
-  f29_to_words(y.v, y29);
-  store_qent(qt, g, j, x, y);
+// Q-table entries (built and read on the 9 x 29 layer) are stored as raw
+// limbs: x[9], y[9], 2 pad words = 80 bytes, five 16-byte accesses per lane;
+// no word conversion on either side.  G-table entries stay 8 x 32 words.
+GV_DEV void store_qent29(u32* qt, u32 g, int j, const fe29& x, const fe29& y) {
+  uint4* p = (uint4*)(qt + ((size_t)g * GV_QTAB_N + j) * GV_QENT_WORDS);
+  p[0] = make_uint4(x.n[0], x.n[1], x.n[2], x.n[3]);
+  p[1] = make_uint4(x.n[4], x.n[5], x.n[6], x.n[7]);
+  p[2] = make_uint4(x.n[8], y.n[0], y.n[1], y.n[2]);
+  p[3] = make_uint4(y.n[3], y.n[4], y.n[5], y.n[6]);
+  p[4] = make_uint4(y.n[7], y.n[8], 0u, 0u);
 }
-GV_DEV void load_qent29(fe29& x29, fe29& y29, const u32* qt, u32 g, u32 j) {
+GV_DEV void load_qent29(fe29& x, fe29& y, const u32* qt, u32 g, u32 j) {
+  const uint4* p = (const uint4*)(qt + ((size_t)g * GV_QTAB_N + j) * GV_QENT_WORDS);
+  const uint4 a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
+  x.n[0] = a.x; x.n[1] = a.y; x.n[2] = a.z; x.n[3] = a.w;
+  x.n[4] = b.x; x.n[5] = b.y; x.n[6] = b.z; x.n[7] = b.w;
+  x.n[8] = c.x; y.n[0] = c.y; y.n[1] = c.z; y.n[2] = c.w;
+  y.n[3] = d.x; y.n[4] = d.y; y.n[5] = d.z; y.n[6] = d.w;
+  y.n[7] = e.x; y.n[8] = e.y;
+}
+GV_DEV void load_gent29(fe29& x29, fe29& y29, const u32* gt, u32 j) {
   fe x, y;
-  load_qent(x, y, qt, g, j);
+  load_qent(x, y, gt, 0, j);
   f29_from_words(x29, x.v);
   f29_from_words(y29, y.v);
+}
+// Z-ratio scratch: 9 raw-limb SoA rows per ratio after the entries.
+GV_DEV void store_ratio29(u32* qr, u32 C, u32 g, int k, const fe29& a) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) qr[((size_t)k * 9 + i) * C + g] = a.n[i];
+}
+GV_DEV void load_ratio29(fe29& a, const u32* qr, u32 C, u32 g, int k) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) a.n[i] = qr[((size_t)k * 9 + i) * C + g];
 }
 
 // Magnitudes (9 x 29 layer) annotated per step; every stored value is
 // canonical words.
 GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx8, const fe& qy8, fe& zq8) {
-  u32* qr = qt + (size_t)C * GV_QTAB_N * 16;         // Z-ratio rows
+  u32* qr = qt + (size_t)C * GV_QTAB_N * GV_QENT_WORDS;  // Z-ratio rows
   fe29 qx, qy, X1, Y1, X2, Y2, t, u;
   f29_from_words(qx, qx8.v);
   f29_from_words(qy, qy8.v);
@@ -265,7 +288,7 @@ GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx8, const fe& qy8, f
   for (int m = 2; m < GV_QTAB_N; ++m) {               // (Q', mQ) -> ((m+1)Q, Q'')
     fe29 h, rr, c, w1, w2, d, a1;
     f29_sub_norm<1>(h, X1, X2);                       // 1
-    store_f29(qr + (size_t)(m - 2) * 8 * C, C, g, h); // Z_m / Z_{m-1}
+    store_ratio29(qr, C, g, m - 2, h);                // Z_m / Z_{m-1}
     f29_sub_norm<1>(rr, Y1, Y2);                      // 1
     f29_sqr(c, h);
     f29_mul(w1, X1, c);
@@ -288,7 +311,7 @@ GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx8, const fe& qy8, f
   for (int m = GV_QTAB_N - 1; m >= 1; --m) {
     if (m >= 2) {
       fe29 ratio;
-      load_f29(ratio, qr + (size_t)(m - 2) * 8 * C, C, g);
+      load_ratio29(ratio, qr, C, g, m - 2);
       if (m == GV_QTAB_N - 1) acc = ratio;
       else f29_mul(acc, acc, ratio);
     }
@@ -588,7 +611,7 @@ __global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, c
           f29_mul(x, x, beta);
         }
       } else {
-        load_qent29(x, y, gtab + (slot == 3 ? (size_t)GV_GTAB_N * 16 : 0), 0, e);
+        load_gent29(x, y, gtab + (slot == 3 ? (size_t)GV_GTAB_N * 16 : 0), e);
       }
       if (d < 0) f29_neg<1>(y, y);                 // 2
       add_entry(acc, inf, x, y, slot < 2 ? nullptr : &zq);

@@ -41,8 +41,8 @@ static __constant__ const u32 kLP[8] = {0xFFFFFC2Fu, 0xFFFFFFFEu, 0xFFFFFFFFu, 0
                                         0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
 
 struct LatShared {
-  u32 qtab[GV_LAT_SIGS][2][GV_QTAB_N][16];  // Q, lambda*Q entries: x words, y words (effective affine)
-  u32 ratio[64][GV_QTAB_N - 1][8];          // per-lane Z-ratio scratch of the table build
+  u32 qtab[GV_LAT_SIGS][2][GV_QTAB_N][18];  // Q, lambda*Q entries: x, y raw 29-bit limbs (effective affine)
+  u32 ratio[64][GV_QTAB_N - 1][9];          // per-lane Z-ratio scratch of the table build (raw limbs)
   u32 dq[GV_LAT_SIGS][GV_QWIN];             // packed int16 Q / lambda*Q digits per window
   int dg[GV_LAT_SIGS][GV_GWIN][2];          // G / lambda*G digits
   u32 zq[GV_LAT_SIGS][8];
@@ -56,22 +56,12 @@ GV_DEV u32 be32(const uint8_t* p) {
 }
 
 GV_DEV void lds_put_ent(u32* e, const fe29& x, const fe29& y) {
-  u32 w[8];
-  f29_to_words(w, x);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) e[i] = w[i];
-  f29_to_words(w, y);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) e[8 + i] = w[i];
+  for (int i = 0; i < 9; ++i) { e[i] = x.n[i]; e[9 + i] = y.n[i]; }
 }
 GV_DEV void lds_get_ent(fe29& x, fe29& y, const u32* e) {
-  u32 w[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) w[i] = e[i];
-  f29_from_words(x, w);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) w[i] = e[8 + i];
-  f29_from_words(y, w);
+  for (int i = 0; i < 9; ++i) { x.n[i] = e[i]; y.n[i] = e[9 + i]; }
 }
 
 // Wave 0 prep for one signature (all four lanes of it compute; slot 0 stores).
@@ -116,9 +106,9 @@ GV_DEV void lat_pubkey_and_tables(LatShared& sh, int sig, int slot, bool live, c
     for (int i = 0; i < 8; ++i) { x8.v[i] = gx[i]; y8.v[i] = gy[i]; }
   }
   const bool st = slot == 0;
-  u32 (*qt)[16] = sh.qtab[sig][0];
-  u32 (*lt)[16] = sh.qtab[sig][1];
-  u32 (*qr)[8] = sh.ratio[sig * 4 + slot];
+  u32 (*qt)[18] = sh.qtab[sig][0];
+  u32 (*lt)[18] = sh.qtab[sig][1];
+  u32 (*qr)[9] = sh.ratio[sig * 4 + slot];
   fe29 qx, qy, X1, Y1, X2, Y2, t, u;
   f29_from_words(qx, x8.v);
   f29_from_words(qy, y8.v);
@@ -145,12 +135,8 @@ GV_DEV void lat_pubkey_and_tables(LatShared& sh, int sig, int slot, bool live, c
   for (int m = 2; m < GV_QTAB_N; ++m) {
     fe29 h, rr, c, w1, w2, d, a1;
     f29_sub_norm<1>(h, X1, X2);
-    {
-      u32 w[8];
-      f29_to_words(w, h);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) qr[m - 2][i] = w[i];  // lane-private
-    }
+    for (int i = 0; i < 9; ++i) qr[m - 2][i] = h.n[i];  // lane-private
     f29_sub_norm<1>(rr, Y1, Y2);
     f29_sqr(c, h);
     f29_mul(w1, X1, c);
@@ -184,11 +170,9 @@ GV_DEV void lat_pubkey_and_tables(LatShared& sh, int sig, int slot, bool live, c
     lds_get_ent(x, y, qt[m - 1]);
     if (m < GV_QTAB_N) {
       if (m >= 2) {
-        u32 w[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) w[i] = qr[m - 2][i];
         fe29 ratio;
-        f29_from_words(ratio, w);                     // Z_m / Z_(m-1)
+#pragma unroll
+        for (int i = 0; i < 9; ++i) ratio.n[i] = qr[m - 2][i];   // Z_m / Z_(m-1)
         if (m == GV_QTAB_N - 1) acc = ratio;
         else f29_mul(acc, acc, ratio);
       }
