@@ -558,8 +558,17 @@ GV_DEV void add_entry(gej29& acc, bool& inf, const fe29& x, const fe29& y, const
   }
   fe29 z2, u2, s2;
   f29_sqr(z2, az);
+#if GV_ILP
+  {
+    fe29 o[2];
+    const fe29 xa[2] = {x, z2}, ya[2] = {z2, az};
+    f29_multi<false, false>(o, xa, ya);
+    u2 = o[0]; z2 = o[1];
+  }
+#else
   f29_mul(u2, x, z2);
   f29_mul(z2, z2, az);
+#endif
   f29_mul(s2, y, z2);                           // 2 x 1
   if (inf) {
     acc.x = u2;

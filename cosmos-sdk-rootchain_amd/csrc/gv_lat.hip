@@ -329,8 +329,12 @@ __global__ __launch_bounds__(128) void k_verify_lat(const u32* gtab, const uint8
       if (inf) f29_set_u32(az, 1);
       else az = acc.z;
       f29_sqr(z2, az);
-      f29_mul(u2, x, z2);
-      f29_mul(z2, z2, az);
+      {
+        fe29 o[2];
+        const fe29 xa[2] = {x, z2}, ya[2] = {z2, az};
+        f29_multi<false, false>(o, xa, ya);
+        u2 = o[0]; z2 = o[1];
+      }
       f29_mul(s2, y, z2);
       if (inf) {
         acc.x = u2; acc.y = s2; f29_set_u32(acc.z, 1); inf = false;

@@ -163,6 +163,104 @@ GV_DEV void f29_mul(fe29& r, const fe29& a, const fe29& b) { f29_mulsqr<false, F
 // r = a^2 mod p (magnitude 1).  mag(a) <= 2.  r may alias a.
 GV_DEV void f29_sqr(fe29& r, const fe29& a) { f29_mulsqr<true, F29_NCH>(r, a, a); }
 
+// S independent products in lockstep (stream s: SQ[s] ? a[s]^2 : a[s]*b[s]),
+// each stream exactly the column engine above (one chain per column), with
+// the streams' terms interleaved: a wave running alone on a SIMD (the latency
+// kernel) always has S independent mad chains in flight, while the
+// throughput kernels issue the same instructions as S separate calls.
+// r may alias a or b (outputs are written last).
+#define F29M_X(s, i, j) (sq[s] ? ((i) == (j) ? a[s].n[i] : d[s][i]) : a[s].n[i])
+#define F29M_Y(s, i, j) (sq[s] ? a[s].n[j] : b[s].n[j])
+template <bool... SQ>
+GV_DEV void f29_multi(fe29* r, const fe29* a, const fe29* b) {
+  constexpr int S = sizeof...(SQ);
+  constexpr bool sq[S] = {SQ...};
+  u32 kr0 = F29_R0, kr1 = F29_R1;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(kr0), "+v"(kr1));
+#endif
+  u32 d[S][9];
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) d[s][i] = sq[s] ? (a[s].n[i] << 1) : 0u;
+  u32 t[S][9];
+  u64 acc[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) acc[s] = 0;
+#pragma unroll
+  for (int k = 9; k <= 16; ++k) {
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int i = k - 8 + q;
+        if (i <= (sq[s] ? (k >> 1) : 8)) acc[s] = f29_mad(F29M_X(s, i, k - i), F29M_Y(s, i, k - i), acc[s]);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      t[s][k - 9] = (u32)acc[s] & F29_M;
+      acc[s] >>= 29;
+    }
+  }
+  fe29 o[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    F29_TRAP((acc[s] >> 32) != 0, "multi t17");
+    t[s][8] = (u32)acc[s];
+    acc[s] = 0;
+  }
+#pragma unroll
+  for (int j = 0; j <= 8; ++j) {
+#pragma unroll
+    for (int q = 0; q <= 8; ++q) {
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        if (q <= (sq[s] ? (j >> 1) : j)) acc[s] = f29_mad(F29M_X(s, q, j - q), F29M_Y(s, q, j - q), acc[s]);
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) acc[s] = f29_mad(t[s][j], kr0, acc[s]);
+    if (j >= 1) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) acc[s] = f29_mad(t[s][j - 1], kr1, acc[s]);
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      o[s].n[j] = (u32)acc[s] & F29_M;
+      acc[s] >>= 29;
+    }
+  }
+  u32 clo[S], chi[S];
+  u64 x[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    acc[s] = f29_mad(t[s][8], kr1, acc[s]);
+    clo[s] = (u32)acc[s];
+    chi[s] = (u32)(acc[s] >> 32);
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) x[s] = f29_mad(clo[s], kr0, (u64)o[s].n[0]);
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    o[s].n[0] = (u32)x[s] & F29_M;
+    x[s] = (x[s] >> 29) + o[s].n[1];
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) x[s] = f29_mad(clo[s], kr1, x[s]);
+#pragma unroll
+  for (int s = 0; s < S; ++s) x[s] = f29_mad(chi[s], F29_RH1, x[s]);
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    o[s].n[1] = (u32)x[s] & F29_M;
+    o[s].n[2] = f29_add32(o[s].n[2], f29_add32((u32)(x[s] >> 29), chi[s] * F29_RH2));
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) r[s] = o[s];
+}
+#undef F29M_X
+#undef F29M_Y
+
 // ------------------------------------------------------------ linear ops
 GV_DEV void f29_set_u32(fe29& r, u32 x) {
   r.n[0] = x & F29_M;

@@ -16,6 +16,12 @@ namespace gv {
 
 struct gej29 { fe29 x, y, z; };
 
+// GV_ILP: issue the independent field products of a formula in lockstep
+// (f29_multi); same instruction count, more independent chains per wave.
+#ifndef GV_ILP
+#define GV_ILP 1
+#endif
+
 // a == 0 (mod p), any magnitude <= 7.  V = sum n_i 2^(29 i) < 2^264 is a
 // multiple k*p (k < 256) only if V mod 2^29 = (-977 k) mod 2^29, i.e. the low
 // limb (mod 2^29) is 0 or >= 2^29 - 977*256: every other lane answers "no"
@@ -44,7 +50,23 @@ GV_DEV bool f29_equal(const fe29& a, const fe29& b) {
 //   X3 = F - 8D, Y3 = E*(4D - X3) - 8C, Z3 = 2*Y*Z.
 // In: X 1, Y 1, Z <= 2.  Out: X 1, Y 1, Z 2.  r may alias a.
 GV_DEV void gej29_double(gej29& r, const gej29& a) {
-  fe29 A, B, C, D, E, t, u;
+  fe29 A, B, C, D, E, F, t, u;
+#if GV_ILP
+  {                                  // {A, B, YZ} and {C, F, D}: independent triples in lockstep
+    fe29 o[3];
+    const fe29 x[3] = {a.x, a.y, a.y}, y[3] = {a.x, a.y, a.z};
+    f29_multi<true, true, false>(o, x, y);
+    A = o[0]; B = o[1]; t = o[2];    // 1, 1, 1 (1 x 2)
+  }
+  f29_add(r.z, t, t);                // Z3 = 2YZ: 2      (a.y, a.z dead)
+  f29_mul3_norm(E, A);               // E = 3A: 1
+  {
+    fe29 o[3];
+    const fe29 x[3] = {B, E, a.x}, y[3] = {B, E, B};
+    f29_multi<true, true, false>(o, x, y);
+    C = o[0]; F = o[1]; D = o[2];    // B^2, E^2, X*B: 1  (a.x dead)
+  }
+#else
   f29_sqr(A, a.x);                   // 1
   f29_sqr(B, a.y);                   // 1
   f29_mul(t, a.y, a.z);              // 1   (1 x 2)
@@ -52,10 +74,11 @@ GV_DEV void gej29_double(gej29& r, const gej29& a) {
   f29_sqr(C, B);                     // 1
   f29_mul(D, a.x, B);                // 1                (a.x dead)
   f29_mul3_norm(E, A);               // E = 3A: 1
-  f29_sqr(t, E);                     // F: 1
+  f29_sqr(F, E);                     // 1
+#endif
   f29_shl_norm<2>(D, D);             // 4D: 1
   f29_add(u, D, D);                  // 8D: 2
-  f29_sub_norm<2>(r.x, t, u);        // X3 = F - 8D: 1   (in 1 + 2 + 1)
+  f29_sub_norm<2>(r.x, F, u);        // X3 = F - 8D: 1   (in 1 + 2 + 1)
   f29_sub<1>(t, D, r.x);             // 4D - X3: 3
   f29_mul(t, E, t);                  // 1   (1 x 3)
   f29_shl_norm<3>(u, C);             // 8C: 1
@@ -78,17 +101,41 @@ GV_DEV void gej29_add_tail(gej29& a, bool& inf, const fe29& u2, const fe29& s2) 
     if (!dbl) inf = true;            // a == -b
   } else {
     fe29 h2, h3, v, t, w;
+#if GV_ILP
+    {
+      fe29 o[2];
+      const fe29 x[2] = {h, rr};
+      f29_multi<true, true>(o, x, x);
+      h2 = o[0]; t = o[1];           // H^2, R^2: 1
+    }
+    {
+      fe29 o[3];
+      const fe29 x[3] = {h2, a.x, a.z}, y[3] = {h, h2, h};
+      f29_multi<false, false, false>(o, x, y);
+      h3 = o[0]; v = o[1]; a.z = o[2];   // H^3, V = X1*H^2, Z3 = Z1*H (2 x 1): 1
+    }
+#else
     f29_sqr(h2, h);                  // 1
     f29_mul(h3, h2, h);              // 1
     f29_mul(v, a.x, h2);             // V = X1*H^2: 1
     f29_mul(a.z, a.z, h);            // Z3 = Z1*H: 1    (2 x 1)
     f29_sqr(t, rr);                  // R^2: 1
+#endif
     f29_add(w, v, v);                // 2V: 2
     f29_add(w, w, h3);               // H^3 + 2V: 3
     f29_sub_norm<3>(a.x, t, w);      // X3 = R^2 - H^3 - 2V: 1   (in 1 + 3 + 1)
     f29_sub<1>(t, v, a.x);           // V - X3: 3
+#if GV_ILP
+    {
+      fe29 o[2];
+      const fe29 x[2] = {rr, a.y}, y[2] = {t, h3};
+      f29_multi<false, false>(o, x, y);
+      t = o[0]; h3 = o[1];           // R(V - X3) (1 x 3), Y1*H^3: 1
+    }
+#else
     f29_mul(t, rr, t);               // 1   (1 x 3)
     f29_mul(h3, a.y, h3);            // Y1*H^3: 1
+#endif
     f29_sub_norm<1>(a.y, t, h3);     // Y3 = R(V - X3) - Y1*H^3: 1
   }
   if (dbl) gej29_double(a, a);       // a == b: a + b = 2a (a untouched above)

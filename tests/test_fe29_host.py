@@ -126,3 +126,19 @@ def test_words_roundtrip_and_zero(lib):
         z = [x * k for x in PL]
         assert lib.f29h_is_zero(arr(z)) == 1
     assert lib.f29h_is_zero(arr([1] + [0] * 8)) == 0
+
+
+@pytest.mark.parametrize("m", [1, 2])
+def test_multi_stream_products(lib, m):
+    """f29_multi: independent squares / products in lockstep == separate calls."""
+    rng = random.Random(40 + m)
+    for it in range(800):
+        xs = [rand_mag(rng, m, rng.choice(STYLES)) for _ in range(3)]
+        ys = [rand_mag(rng, m, rng.choice(STYLES)) for _ in range(3)]
+        r = (ctypes.c_uint32 * 27)()
+        lib.f29h_multi(arr(sum(xs, [])), arr(sum(ys, [])), r)
+        r = list(r)
+        want = [val(xs[0]) ** 2 % P, val(xs[1]) ** 2 % P, val(xs[2]) * val(ys[2]) % P]
+        for s in range(3):
+            limbs = r[9 * s:9 * s + 9]
+            assert val(limbs) % P == want[s] and is_mag(limbs, 1)

@@ -44,3 +44,12 @@ void f29h_to_words(const u32* a, u32* w) { fe29 x; ld(x, a); f29_to_words(w, x);
 void f29h_from_words(const u32* w, u32* r) { fe29 x; f29_from_words(x, w); st(r, x); }
 int f29h_is_zero(const u32* a) { fe29 x; ld(x, a); return f29_is_zero(x); }
 }
+extern "C" {
+// three independent products in lockstep: (a0^2, a1^2, a2*b2) -> r (27 words)
+void f29h_multi(const u32* a, const u32* b, u32* r) {
+  fe29 x[3], y[3], o[3];
+  for (int s = 0; s < 3; ++s) { ld(x[s], a + 9 * s); ld(y[s], b + 9 * s); }
+  f29_multi<true, true, false>(o, x, y);
+  for (int s = 0; s < 3; ++s) st(r + 9 * s, o[s]);
+}
+}
