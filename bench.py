@@ -60,6 +60,7 @@ def workload_lib():
     L.gvw_sign.argtypes = [ctypes.c_size_t, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    L.gvw_openssl_verify.argtypes = [ctypes.c_size_t] + [ctypes.c_void_p] * 7 + [ctypes.c_int]
     return L
 
 
@@ -81,22 +82,70 @@ def unpack_bits(bits: np.ndarray, n: int) -> np.ndarray:
     return np.unpackbits(bits.view(np.uint8), bitorder="little")[:n]
 
 
-def cpu_baseline(pub, sig, dig, threads: int):
-    """The oracle (plain-C restatement of the reference path) on this host."""
+def openssl_verify(pub, sig, dig=None, msgs=None, threads: int = 1):
+    """tools/workload gvw_openssl_verify: VerifyBytes semantics on OpenSSL."""
+    L = workload_lib()
+    n = len(pub)
+    out = np.zeros(n, np.uint8)
+    if dig is not None:
+        L.gvw_openssl_verify(n, pub.ctypes.data, sig.ctypes.data, dig.ctypes.data, None, None, None,
+                             out.ctypes.data, threads)
+    else:
+        blob, off, ln = msgs
+        L.gvw_openssl_verify(n, pub.ctypes.data, sig.ctypes.data, None, blob.ctypes.data, off.ctypes.data,
+                             ln.ctypes.data, out.ctypes.data, threads)
+    return out
+
+
+def _rate(fn, n):
+    t = time.perf_counter()
+    fn()
+    return round(n / (time.perf_counter() - t), 1)
+
+
+def cpu_baseline(pub, sig, dig, threads: int, ver=None):
+    """CPU timing beside the GPU: (ii) the oracle port
+    (oracle/secp256k1_oracle.c, the reference algorithm restated in C) and
+    (iii) OpenSSL (ECDSA_do_verify + the low-S rule), each serial and on
+    `threads` cores, on bounded samples of C2 (digests) and of the C1 item set
+    (10k MsgSend StdSignBytes messages: SHA-256 + verify).  (i), the Go
+    reference, needs a Go toolchain the box does not have.  `value` is the
+    oracle port on C2, all cores.  The C1 line also times the GPU host path
+    (gv_verify_msgs, PCIe included) on the same 10k items."""
     from oracle import oracle as O
     O.lib()
     s1 = 4096
-    t = time.perf_counter()
-    O.verify_digests(pub[:s1], sig[:s1], dig[:s1], threads=1)
-    serial = s1 / (time.perf_counter() - t)
     s2 = min(len(pub), 6144 * threads)
-    t = time.perf_counter()
-    O.verify_digests(pub[:s2], sig[:s2], dig[:s2], threads=threads)
-    par = s2 / (time.perf_counter() - t)
-    return {"value": round(par, 1), "unit": "verifies/s", "cores": threads, "kind": "port",
+    c2 = {
+        "port_serial": _rate(lambda: O.verify_digests(pub[:s1], sig[:s1], dig[:s1], threads=1), s1),
+        "port_allcore": _rate(lambda: O.verify_digests(pub[:s2], sig[:s2], dig[:s2], threads=threads), s2),
+        "openssl_serial": _rate(lambda: openssl_verify(pub[:s1], sig[:s1], dig[:s1], threads=1), s1),
+        "openssl_allcore": _rate(lambda: openssl_verify(pub[:s2], sig[:s2], dig[:s2], threads=threads), s2),
+    }
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import bench_extras as X
+    n1 = 10000
+    cpub, csig, cmsgs, cexp = X.c1_items(workload_lib(), n1, threads)
+    blob, off, ln = cmsgs
+    c1 = {
+        "items": n1, "mean_msg_bytes": round(float(ln.mean()), 1),
+        "port_serial": _rate(lambda: O.verify_msgs(cpub[:s1], csig[:s1], blob, off[:s1], ln[:s1], threads=1), s1),
+        "port_allcore": _rate(lambda: O.verify_msgs(cpub, csig, blob, off, ln, threads=threads), n1),
+        "openssl_serial": _rate(lambda: openssl_verify(cpub[:s1], csig[:s1], msgs=(blob, off[:s1], ln[:s1]),
+                                                       threads=1), s1),
+        "openssl_allcore": _rate(lambda: openssl_verify(cpub, csig, msgs=cmsgs, threads=threads), n1),
+    }
+    if ver is not None:
+        ver.verify_batch_msgs(cpub, csig, cmsgs)                # warm the message-path buffers
+        t = time.perf_counter()
+        got = ver.verify_batch_msgs(cpub, csig, cmsgs)
+        c1["gpu_hostpath"] = round(n1 / (time.perf_counter() - t), 1)
+        c1["gpu_mismatches"] = int(np.count_nonzero(got != cexp))
+    return {"value": c2["port_allcore"], "unit": "verifies/s", "cores": threads, "kind": "port",
             "sample": f"first {s2} items of the same C2 batch, {threads} threads (oracle/secp256k1_oracle.c); "
-                      f"serial 1-thread on the first {s1}: {serial:.1f} verifies/s",
-            "serial_value": round(serial, 1)}
+                      f"serial 1-thread on the first {s1}; OpenSSL and the C1 message set beside it "
+                      f"(SURVEY.md §8d lines ii and iii)",
+            "serial_value": c2["port_serial"], "c2": c2, "c1": c1}
 
 
 def _pct(ts):
@@ -293,9 +342,10 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
         result["checktx_latency_ms"] = lat
         result["checktx_p50_ms_64"] = lat["64"]["p50_ms"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(pub, sig, dig, args.threads)
+        cb = cpu_baseline(pub, sig, dig, args.threads, ver)
         result["cpu_baseline"] = cb
         result["gpu_over_cpu"] = round(value / cb["value"], 1)
+        result["gpu_over_openssl_allcore"] = round(value / cb["c2"]["openssl_allcore"], 1)
 
     for p in (d_pub, d_sig, d_dig, d_bits):
         ver.dev_free(p)

@@ -70,8 +70,11 @@ def c3_adversarial(ver, make_workload, n: int, threads: int, steps: int = 3):
     return out
 
 
-def msg_path(ver, wl, n: int, threads: int, nkeys: int = 10000, steps: int = 3):
-    """wl: tools/workload/libgvwork.so handle (bench.workload_lib())."""
+def c1_items(wl, n: int, threads: int, nkeys: int = 10000):
+    """C1 item set: n MsgSend StdSignBytes messages for nkeys
+    accounts (key i = GenPrivKeySecp256k1 over a C1 secret, account number i,
+    sequence 0), signed with OpenSSL.  Returns pub, sig, (blob, off, len), and
+    the expected verdicts (all valid)."""
     priv = np.zeros((nkeys, 32), np.uint8)
     pubk = np.zeros((nkeys, 33), np.uint8)
     wl.gvw_keys(nkeys, 0xC1, priv.ctypes.data, pubk.ctypes.data, threads)
@@ -96,6 +99,12 @@ def msg_path(ver, wl, n: int, threads: int, nkeys: int = 10000, steps: int = 3):
     exp = np.zeros(n, np.uint8)
     wl.gvw_sign(n, 0xC1, nkeys, priv.ctypes.data, pubk.ctypes.data, None, mdig.ctypes.data, 0.0,
                 pub.ctypes.data, sig.ctypes.data, dig.ctypes.data, exp.ctypes.data, threads)
+    return pub, sig, (blob, off, ln), exp
+
+
+def msg_path(ver, wl, n: int, threads: int, nkeys: int = 10000, steps: int = 3):
+    """wl: tools/workload/libgvwork.so handle (bench.workload_lib())."""
+    pub, sig, (blob, off, ln), exp = c1_items(wl, n, threads, nkeys)
     arrs = (pub, sig, blob, off, ln)
     d = [ver.dev_alloc(a.nbytes) for a in arrs]
     for p, a in zip(d, arrs):

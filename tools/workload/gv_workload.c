@@ -238,6 +238,68 @@ void gvw_sha256_msgs(size_t n, const uint8_t* blob, const uint64_t* off, const u
   for (size_t i = 0; i < n; ++i) SHA256(blob + off[i], len[i], out32 + 32 * i);
 }
 
+/* ----------------------------------------------- OpenSSL CPU baseline (iii)
+ * SURVEY.md §8d "CPU timing beside it" (iii): tendermint VerifyBytes semantics
+ * on OpenSSL 3 libcrypto -- the third CPU line next to the oracle port.  Per
+ * item: btcec.ParsePubKey of the 33-byte SEC1 key (EC_POINT_oct2point: prefix
+ * 02/03, x < p, square root exists), tendermint's low-S rule (s <= n/2,
+ * secp256k1_nocgo.go), then ECDSA_do_verify (0 < r, s < n; x(u1*G + u2*Q)
+ * mod n == r).  dig32 != NULL: items are digests; otherwise SHA-256 of
+ * blob[off[i] .. off[i] + len[i]) is taken first (the full VerifyBytes).
+ * ok[i] = 1 / 0.  Timed by bench.py; not the oracle, not the product. */
+typedef struct {
+  size_t lo, hi;
+  const uint8_t *pub, *sig, *dig, *blob; const uint64_t* off; const uint32_t* len;
+  uint8_t* ok;
+} verjob;
+
+static void* verify_worker(void* a) {
+  verjob* j = (verjob*)a;
+  EC_GROUP* grp = EC_GROUP_new_by_curve_name(NID_secp256k1);
+  BN_CTX* bctx = BN_CTX_new();
+  EC_GROUP_precompute_mult(grp, bctx);
+  BIGNUM *n = NULL, *half = BN_new();
+  BN_hex2bn(&n, N_HEX); BN_rshift1(half, n);
+  EC_KEY* key = EC_KEY_new();
+  EC_KEY_set_group(key, grp);
+  EC_POINT* pt = EC_POINT_new(grp);
+  for (size_t i = j->lo; i < j->hi; ++i) {
+    uint8_t h[32];
+    const uint8_t* e = j->dig ? j->dig + 32 * i : h;
+    if (!j->dig) SHA256(j->blob + j->off[i], j->len[i], h);
+    int ok = 0;
+    if (EC_POINT_oct2point(grp, pt, j->pub + 33 * i, 33, bctx) == 1 && EC_KEY_set_public_key(key, pt) == 1) {
+      BIGNUM* r = BN_bin2bn(j->sig + 64 * i, 32, NULL);
+      BIGNUM* s = BN_bin2bn(j->sig + 64 * i + 32, 32, NULL);
+      if (BN_cmp(s, half) <= 0) {
+        ECDSA_SIG* sg = ECDSA_SIG_new();
+        ECDSA_SIG_set0(sg, r, s);            /* takes ownership */
+        ok = ECDSA_do_verify(e, 32, sg, key) == 1;
+        ECDSA_SIG_free(sg);
+      } else {
+        BN_free(r); BN_free(s);
+      }
+    }
+    j->ok[i] = (uint8_t)ok;
+  }
+  EC_POINT_free(pt); EC_KEY_free(key); BN_free(n); BN_free(half); BN_CTX_free(bctx); EC_GROUP_free(grp);
+  return NULL;
+}
+
+int gvw_openssl_verify(size_t n, const uint8_t* pub33, const uint8_t* sig64, const uint8_t* dig32,
+                       const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint8_t* ok, int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t th[256]; verjob js[256];
+  for (int t = 0; t < threads; ++t) {
+    verjob j = {n * t / threads, n * (t + 1) / threads, pub33, sig64, dig32, blob, off, len, ok};
+    js[t] = j;
+    pthread_create(&th[t], NULL, verify_worker, &js[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  return 0;
+}
+
 /* single-item helpers for the client-side tx kit (cosmos-sdk-rootchain_amd/txkit.py) */
 int gvw_pubkey(const uint8_t priv32[32], uint8_t pub33[33]) {
   EC_GROUP* grp = EC_GROUP_new_by_curve_name(NID_secp256k1);
