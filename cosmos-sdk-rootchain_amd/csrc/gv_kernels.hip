@@ -580,7 +580,17 @@ GV_DEV void add_entry(gej29& acc, bool& inf, const fe29& x, const fe29& y, const
   gej29_add_tail(acc, inf, u2, s2);
 }
 
-__global__ __launch_bounds__(256) void k_ecmult(const u32* gtab, u32 n, u32 C, const u32* digits,
+// GV_ECMULT_WAVES: minimum waves per SIMD the register allocator must allow
+// (0 = compiler's choice).
+#ifndef GV_ECMULT_WAVES
+#define GV_ECMULT_WAVES 0
+#endif
+#if GV_ECMULT_WAVES
+#define GV_ECMULT_ATTR __attribute__((amdgpu_waves_per_eu(GV_ECMULT_WAVES)))
+#else
+#define GV_ECMULT_ATTR
+#endif
+__global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult(const u32* gtab, u32 n, u32 C, const u32* digits,
                                                  const u32* qt, const u32* zq_in, const u32* flags,
                                                  const u32* in_r, uint64_t* bits) {
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;

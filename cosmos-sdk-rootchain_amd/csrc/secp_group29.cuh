@@ -48,10 +48,35 @@ GV_DEV bool f29_equal(const fe29& a, const fe29& b) {
 // r = 2a (a finite; secp256k1 has no point of order 2).  3M + 4S:
 //   A = X^2, B = Y^2, C = B^2, D = X*B, E = 3A, F = E^2,
 //   X3 = F - 8D, Y3 = E*(4D - X3) - 8C, Z3 = 2*Y*Z.
+// GV_DBL25: 2M + 5S, the product X*B taken as ((X + B)^2 - A - C) / 2
+// (a square is 45 + 9 multiplies against 81 for a product, for two extra
+// linear steps).
 // In: X 1, Y 1, Z <= 2.  Out: X 1, Y 1, Z 2.  r may alias a.
+#ifndef GV_DBL25
+#define GV_DBL25 0
+#endif
 GV_DEV void gej29_double(gej29& r, const gej29& a) {
   fe29 A, B, C, D, E, F, t, u;
-#if GV_ILP
+#if GV_DBL25
+  {
+    fe29 o[3];
+    const fe29 x[3] = {a.x, a.y, a.y}, y[3] = {a.x, a.y, a.z};
+    f29_multi<true, true, false>(o, x, y);
+    A = o[0]; B = o[1]; t = o[2];    // 1, 1, 1 (1 x 2)
+  }
+  f29_add(r.z, t, t);                // Z3 = 2YZ: 2      (a.y, a.z dead)
+  f29_mul3_norm(E, A);               // E = 3A: 1
+  f29_add(u, a.x, B);                // X + B: 2         (a.x dead)
+  {
+    fe29 o[3];
+    const fe29 x[3] = {B, E, u};
+    f29_multi<true, true, true>(o, x, x);
+    C = o[0]; F = o[1]; D = o[2];    // B^2, E^2, (X + B)^2: 1
+  }
+  f29_sub<1>(D, D, A);               // 3
+  f29_sub_norm<1>(D, D, C);          // 2XB: 1           (in 3 + 1 + 1)
+  f29_shl_norm<1>(D, D);             // 4D: 1
+#elif GV_ILP
   {                                  // {A, B, YZ} and {C, F, D}: independent triples in lockstep
     fe29 o[3];
     const fe29 x[3] = {a.x, a.y, a.y}, y[3] = {a.x, a.y, a.z};
@@ -76,7 +101,9 @@ GV_DEV void gej29_double(gej29& r, const gej29& a) {
   f29_mul3_norm(E, A);               // E = 3A: 1
   f29_sqr(F, E);                     // 1
 #endif
+#if !GV_DBL25
   f29_shl_norm<2>(D, D);             // 4D: 1
+#endif
   f29_add(u, D, D);                  // 8D: 2
   f29_sub_norm<2>(r.x, F, u);        // X3 = F - 8D: 1   (in 1 + 2 + 1)
   f29_sub<1>(t, D, r.x);             // 4D - X3: 3

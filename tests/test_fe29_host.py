@@ -128,6 +128,58 @@ def test_words_roundtrip_and_zero(lib):
     assert lib.f29h_is_zero(arr([1] + [0] * 8)) == 0
 
 
+@pytest.mark.parametrize("dbl25,ilp", [(0, 0), (0, 1), (1, 1)], ids=["3M4S", "3M4S-ilp", "2M5S"])
+def test_jacobian_double_variants(dbl25, ilp):
+    """gej29_double (csrc/secp_group29.cuh) in each formula variant, host build
+    with overflow traps, at the point invariant's extreme magnitudes (X, Y
+    magnitude 1, Z <= 2): same point as affine doubling, output invariant kept."""
+    d = tempfile.mkdtemp()
+    so = os.path.join(d, "g29.so")
+    subprocess.run(["g++", "-O2", "-std=c++17", f"-DGV_DBL25={dbl25}", f"-DGV_ILP={ilp}", "-shared", "-fPIC",
+                    "-o", so, os.path.join(REPO, "tools", "fe29", "g29_host.cpp")], check=True)
+    L = ctypes.CDLL(so)
+    rng = random.Random(dbl25 * 10 + ilp)
+    Gx = 0x79BE667EF9DCBBAC55A06295CE870B07029BFCDB2DCE28D959F2815B16F81798
+    Gy = 0x483ADA7726A3C4655DA4FBFC0E1108A8FD17B448A68554199C47D08FFB10D4B8
+    for it in range(250):
+        k = rng.randrange(1, 2**64)
+        # a random multiple of G in affine form via Python double-and-add
+        x, y = Gx, Gy
+        ax = ay = None
+        for bit in bin(k)[2:]:
+            if ax is not None:
+                lam = 3 * ax * ax * pow(2 * ay, P - 2, P) % P
+                nx = (lam * lam - 2 * ax) % P
+                ay = (lam * (ax - nx) - ay) % P
+                ax = nx
+            if bit == "1":
+                if ax is None:
+                    ax, ay = x, y
+                else:
+                    lam = (ay - y) * pow(ax - x, P - 2, P) % P
+                    nx = (lam * lam - ax - x) % P
+                    ay = (lam * (x - nx) - y) % P
+                    ax = nx
+        z = rng.randrange(1, P)
+        X, Y = ax * z * z % P, ay * z * z * z % P
+
+        def limbs(v, m):            # v + k*p limb-wise, k < m: magnitude m at most
+            k = rng.randrange(0, m)
+            return [((v >> (29 * i)) & M29) + k * PL[i] for i in range(9)]
+        inp = limbs(X, 1) + limbs(Y, 1) + limbs(z, 2)
+        assert val(inp[:9]) % P == X and val(inp[9:18]) % P == Y and val(inp[18:]) % P == z
+        r = (ctypes.c_uint32 * 27)()
+        L.g29h_double(arr(inp), r)
+        r = list(r)
+        X3, Y3, Z3 = val(r[:9]) % P, val(r[9:18]) % P, val(r[18:]) % P
+        assert is_mag(r[:9], 1) and is_mag(r[9:18], 1) and is_mag(r[18:], 2)
+        lam = 3 * ax * ax * pow(2 * ay, P - 2, P) % P
+        ex = (lam * lam - 2 * ax) % P
+        ey = (lam * (ax - ex) - ay) % P
+        zi = pow(Z3, P - 2, P)
+        assert X3 * zi * zi % P == ex and Y3 * zi * zi * zi % P == ey
+
+
 @pytest.mark.parametrize("m", [1, 2])
 def test_multi_stream_products(lib, m):
     """f29_multi: independent squares / products in lockstep == separate calls."""
