@@ -354,6 +354,7 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
         import bench_extras as X
         ex = {}
         t = time.perf_counter()
+        ex["c2_key_cache"] = X.c2_key_cache(ver, pub, sig, dig, exp, min(args.keys, n))
         ex["c3_adversarial"] = X.c3_adversarial(ver, make_digest_workload, n, args.threads)
         ex["msg_path"] = X.msg_path(ver, workload_lib(), min(n, 500_000), args.threads)
         ex["c1_ante"] = X.c1_ante(ver)

@@ -41,7 +41,17 @@ typedef struct gvk_batch {
   uint32_t *zq, *flags, *qtab;  // shared Z of the Q table (8 rows), flags, Q table (192 rows)
   uint64_t* bits;               // C/64 words, bit (i%64) of word i/64
   hipEvent_t ev[3];             // optional: after unpack/sha, after prep, after ecmult
+  // keyed batch (kslot != NULL, pub33 unused): item i's key is arena slot kslot[i]
+  const uint32_t* kslot;        // n slots (device)
+  const uint32_t* kqt;          // arena Q tables, row per slot (GV_QTAB_N x GV_QENT_WORDS words)
+  const uint32_t* kzq;          // arena table Z: 8 rows of stride kC
+  const uint32_t* kok;          // arena ParsePubKey verdicts
+  uint32_t kC, kcount;          // arena capacity (row stride) and slots in use
 } gvk_batch;
+
+// Key arena row of one slot: Q table entries only (the Z-ratio scratch of the
+// build lives in the batch scratch).
+#define GV_KEY_WORDS (GV_QTAB_N * GV_QENT_WORDS)
 
 // Small-batch latency path (gv_lat.hip): GV_LAT_SIGS signatures per block of
 // 128 threads, one fused kernel (after k_sha256 on the message path).  bits
@@ -67,6 +77,12 @@ hipError_t gvk_verify_lat(const gvk_lat* b, hipStream_t st);
 hipError_t gvk_sha256(const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint32_t n, uint32_t C,
                       uint32_t* e, hipStream_t st);
 hipError_t gvk_verify(const gvk_batch* b, hipStream_t st);
+// Parse n keys (device pub33) into arena slots base..base+n-1.  Scratch: the
+// batch rows in_x, in_pfx (and r, s, e as k_unpack targets) of stride C and
+// qr (GV_QTAB_N - 1) * 9 rows of stride C.
+hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
+                          uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t base,
+                          uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, hipStream_t st);
 hipError_t gvk_debug(int op, uint32_t n, const uint32_t* in, uint32_t* out, hipStream_t st);
 
 #ifdef __cplusplus

@@ -128,7 +128,8 @@ GV_DEV u32 lds_be32(const uint8_t* p) {
   return ((u32)p[0] << 24) | ((u32)p[1] << 16) | ((u32)p[2] << 8) | (u32)p[3];
 }
 
-// pub33/sig64/dig32: device AoS inputs (dig32 may be null: message path).
+// pub33/sig64/dig32: device AoS inputs (dig32 may be null: message path;
+// pub33 null: keyed batch; sig64 null: key load).
 // Outputs (SoA, C lanes): x[8], pfx[1], r[8], s[8], e[8].  Lanes >= n get
 // prefix 0 (rejected) and s = 1.
 __global__ __launch_bounds__(256) void k_unpack(const uint8_t* pub33, const uint8_t* sig64,
@@ -141,19 +142,19 @@ __global__ __launch_bounds__(256) void k_unpack(const uint8_t* pub33, const uint
   const bool live = threadIdx.x < nv;
   const uint8_t* l8 = (const uint8_t*)lds;
 
-  stage_bytes(lds, pub33 + (size_t)row0 * 33u, nv * 33u);
-  __syncthreads();
-  {
+  if (pub33) {                    // null: keyed batch (cached keys) or signature-less key load
+    stage_bytes(lds, pub33 + (size_t)row0 * 33u, nv * 33u);
+    __syncthreads();
     const uint8_t* p = l8 + threadIdx.x * 33u;
     u32 pre = live ? p[0] : 0u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) x[(size_t)i * C + g] = live ? lds_be32(p + 1 + 4 * (7 - i)) : 0u;
     pfx[g] = pre;
   }
-  __syncthreads();
-  stage_bytes(lds, sig64 + (size_t)row0 * 64u, nv * 64u);
-  __syncthreads();
-  {
+  if (sig64) {
+    __syncthreads();
+    stage_bytes(lds, sig64 + (size_t)row0 * 64u, nv * 64u);
+    __syncthreads();
     const uint8_t* p = l8 + threadIdx.x * 64u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -257,8 +258,9 @@ GV_DEV void load_ratio29(fe29& a, const u32* qr, u32 C, u32 g, int k) {
 
 // Magnitudes (9 x 29 layer) annotated per step; every stored value is
 // canonical words.
-GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx8, const fe& qy8, fe& zq8) {
-  u32* qr = qt + (size_t)C * GV_QTAB_N * GV_QENT_WORDS;  // Z-ratio rows
+// qt: entries of table row qi (lane-major AoS); qr: Z-ratio scratch rows of
+// stride C, column g.
+GV_DEV void build_q_table(u32* qt, u32 qi, u32* qr, u32 C, u32 g, const fe& qx8, const fe& qy8, fe& zq8) {
   fe29 qx, qy, X1, Y1, X2, Y2, t, u;
   f29_from_words(qx, qx8.v);
   f29_from_words(qy, qy8.v);
@@ -283,8 +285,8 @@ GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx8, const fe& qy8, f
     f29_mul(t, M, t);                                 // 1
     f29_sub_norm<1>(Y2, t, Y1);                       // 1
   }
-  store_qent29(qt, g, 0, X1, Y1);                     // 1*Q on Z1
-  store_qent29(qt, g, 1, X2, Y2);                     // 2*Q on Z1
+  store_qent29(qt, qi, 0, X1, Y1);                     // 1*Q on Z1
+  store_qent29(qt, qi, 1, X2, Y2);                     // 2*Q on Z1
   for (int m = 2; m < GV_QTAB_N; ++m) {               // (Q', mQ) -> ((m+1)Q, Q'')
     fe29 h, rr, c, w1, w2, d, a1;
     f29_sub_norm<1>(h, X1, X2);                       // 1
@@ -303,7 +305,7 @@ GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx8, const fe& qy8, f
     f29_sub_norm<1>(Y2, t, a1);                       // Y3 = (Y1-Y2)(W1-X3) - A1: 1
     X1 = w1;                                          // Q' on the new Z
     Y1 = a1;
-    store_qent29(qt, g, m, X2, Y2);                   // (m+1)*Q
+    store_qent29(qt, qi, m, X2, Y2);                   // (m+1)*Q
   }
   // entry m (index m-1) lives on Z_{m-1} (m >= 2; entry 1 on Z_1); the last
   // entry on Z_15.  acc = Z_15 / Z(entry m) accumulates the stored ratios.
@@ -318,10 +320,10 @@ GV_DEV void build_q_table(u32* qt, u32 C, u32 g, const fe& qx8, const fe& qy8, f
     fe29 x, y, a2, a3;
     f29_sqr(a2, acc);
     f29_mul(a3, a2, acc);
-    load_qent29(x, y, qt, g, m - 1);
+    load_qent29(x, y, qt, qi, m - 1);
     f29_mul(x, x, a2);
     f29_mul(y, y, a3);
-    store_qent29(qt, g, m - 1, x, y);
+    store_qent29(qt, qi, m - 1, x, y);
   }
   f29_add(t, qy, qy);                                 // 2
   f29_mul(t, t, acc);                                 // Z_15 = 2y * prod(ratios)
@@ -429,29 +431,18 @@ __global__ __launch_bounds__(256) void k_scalar_inv(u32 C, const u32* in_s, u32*
 }
 
 // -------------------------------------------------------------------- k_prep
-// flags bits: 1 = passes every check before the curve arithmetic,
-//             2 = r < p - n (so R.x == r + n is also an accept)
-__global__ __launch_bounds__(256) void k_prep(u32 C, const u32* in_x, const u32* in_pfx,
-                                               const u32* in_r, const u32* in_s, const u32* in_e,
-                                               const u32* in_w, u32* digits, u32* qt, u32* zq_out,
-                                               u32* flags) {
-  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;   // C % 256 == 0: all lanes live
-  bool ok = true;
-
-  // ---- btcec.ParsePubKey (compressed): prefix, decompressPoint, range, IsOnCurve
-  const u32 pre = in_pfx[g];
-  ok &= (pre & 0xFEu) == 0x02u;
-  fe x;
-  load_fe(x, in_x, C, g);
-  // x < p  (btcec: "pubkey X parameter is >= to P")
-  {
+// btcec.ParsePubKey for a compressed key (prefix 02/03, x < p, decompressPoint:
+// y = sqrt(x^3 + 7) with the prefix's parity; IsOnCurve and y < p then hold by
+// construction).  Returns false for a rejected key (x, y then undefined).
+GV_DEV bool parse_pubkey(u32 pre, const fe& x, fe& y) {
+  bool ok = (pre & 0xFEu) == 0x02u;
+  {                                         // x < p  (btcec: "pubkey X parameter is >= to P")
     u32 br = 0, d;
 #pragma unroll
     for (int i = 0; i < 8; ++i) d = __builtin_subc(x.v[i], kP[i], br, &br);
     (void)d;
     ok &= (br != 0);
   }
-  fe y;
   {
     fe29 x29, c, y29, y2, seven;
     f29_from_words(x29, x.v);
@@ -466,7 +457,35 @@ __global__ __launch_bounds__(256) void k_prep(u32 C, const u32* in_x, const u32*
   }
   if ((y.v[0] & 1u) != (pre & 1u)) fe_neg(y, y);   // choose parity (y != 0 always)
   fe_normalize(y);
-  // (IsOnCurve and Y < P hold by construction once the square-root check passed)
+  return ok;
+}
+
+// flags bits: 1 = passes every check before the curve arithmetic,
+//             2 = r < p - n (so R.x == r + n is also an accept)
+// KEYED = false: the lane's pubkey (in_x, in_pfx) is parsed here and its Q
+// table built into qt row g (zq_out column g).
+// KEYED = true: the item's key is slot kslot[g] of the key arena (gv_keys_load:
+// parsed once, table resident); an out-of-range slot or a rejected key makes
+// the item false.  qidx[g] receives the (clamped) slot for k_ecmult.
+template <bool KEYED>
+__global__ __launch_bounds__(256) void k_prep(u32 C, u32 n, const u32* in_x, const u32* in_pfx,
+                                               const u32* in_r, const u32* in_s, const u32* in_e,
+                                               const u32* in_w, u32* digits, u32* qt, u32* zq_out,
+                                               u32* flags, const u32* kslot, const u32* kok, u32 kcount,
+                                               u32* qidx) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;   // C % 256 == 0: all lanes live
+  bool ok = true;
+  fe x, y;
+  if (KEYED) {
+    u32 sl = g < n ? kslot[g] : 0xFFFFFFFFu;
+    const bool in_range = sl < kcount;
+    if (!in_range) sl = 0;                  // the arena always holds slot 0's memory
+    ok = in_range && kok[sl] != 0u;
+    qidx[g] = sl;
+  } else {
+    load_fe(x, in_x, C, g);
+    ok = parse_pubkey(in_pfx[g], x, y);
+  }
 
   // ---- tendermint low-S + crypto/ecdsa range checks
   u32 r[8], s[8], e[8];
@@ -488,8 +507,10 @@ __global__ __launch_bounds__(256) void k_prep(u32 C, const u32* in_x, const u32*
   if (!ok) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s[i] = (i == 0) ? 1u : 0u; e[i] = 0u; r[i] = 0u; }
-    fe_from_const(x, kGx);
-    fe_from_const(y, kGy);
+    if (!KEYED) {
+      fe_from_const(x, kGx);
+      fe_from_const(y, kGy);
+    }
   }
 
   // ---- w = s^-1 mod n (Montgomery form, from k_scalar_inv)
@@ -537,9 +558,33 @@ __global__ __launch_bounds__(256) void k_prep(u32 C, const u32* in_x, const u32*
   flags[g] = (ok ? 1u : 0u) | (r_small ? 2u : 0u);
 
   // ---- per-lane table of Q multiples (shared Z, isomorphic-curve affine)
-  fe zq;
-  build_q_table(qt, C, g, x, y, zq);
-  store_fe(zq_out, C, g, zq);
+  if (!KEYED) {
+    fe zq;
+    build_q_table(qt, g, qt + (size_t)C * GV_QTAB_N * GV_QENT_WORDS, C, g, x, y, zq);
+    store_fe(zq_out, C, g, zq);
+  }
+}
+
+// ------------------------------------------------------------ k_keys_build
+// Key arena (gv_keys_load): lane g parses key g of the load batch once and
+// writes its Q table to arena row base + g, the table's Z to kzq (8 rows of
+// stride kC) and the ParsePubKey verdict to kok.  A rejected key gets G's
+// table (never used: every item against it is false).  qr: Z-ratio scratch
+// rows of stride C.
+__global__ __launch_bounds__(256) void k_keys_build(u32 n, u32 C, const u32* in_x, const u32* in_pfx, u32 base,
+                                                     u32* kqt, u32* kzq, u32 kC, u32* kok, u32* qr) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;                       // no cross-lane work below
+  fe x, y, zq;
+  load_fe(x, in_x, C, g);
+  const bool ok = parse_pubkey(in_pfx[g], x, y);
+  if (!ok) {
+    fe_from_const(x, kGx);
+    fe_from_const(y, kGy);
+  }
+  build_q_table(kqt, base + g, qr, C, g, x, y, zq);
+  store_fe(kzq, kC, base + g, zq);
+  kok[base + g] = ok ? 1u : 0u;
 }
 
 // ------------------------------------------------------------------ k_ecmult
@@ -590,12 +635,16 @@ GV_DEV void add_entry(gej29& acc, bool& inf, const fe29& x, const fe29& y, const
 #else
 #define GV_ECMULT_ATTR
 #endif
+// KEYED: the Q table and its Z come from key-arena row qidx[g] (zq rows of
+// stride zC) instead of the lane's own row g (stride C).
+template <bool KEYED>
 __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult(const u32* gtab, u32 n, u32 C, const u32* digits,
                                                  const u32* qt, const u32* zq_in, const u32* flags,
-                                                 const u32* in_r, uint64_t* bits) {
+                                                 const u32* in_r, uint64_t* bits, const u32* qidx, u32 zC) {
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 qi = KEYED ? qidx[g] : g;
   fe29 zq;
-  load_f29(zq, zq_in, C, g);
+  load_f29(zq, zq_in, KEYED ? zC : C, qi);
 
   gej29 acc;
   f29_set_zero(acc.x); f29_set_zero(acc.y); f29_set_zero(acc.z);
@@ -623,7 +672,7 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult(const u32* gtab, 
       const u32 e = (u32)((d < 0 ? -d : d) - 1);
       fe29 x, y;
       if (slot < 2) {
-        load_qent29(x, y, qt, g, e);
+        load_qent29(x, y, qt, qi, e);
         if (slot == 1) {                           // lambda * P = (beta * x, y)
           fe29 beta;
           f29_from_const(beta, kBeta);
@@ -792,13 +841,35 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
     uint32_t* w = b->digits;                   // rows 0..8
     uint32_t* pre = b->digits + (size_t)9 * C; // rows 9..17
     hipLaunchKernelGGL(gv::k_scalar_inv, dim3((waves + 3) / 4), blk, 0, st, C, b->in_s, w, pre);
-    hipLaunchKernelGGL(gv::k_prep, grd, blk, 0, st, C, b->in_x, b->in_pfx, b->in_r, b->in_s, b->in_e,
-                       (const uint32_t*)w, b->digits, b->qtab, b->zq, b->flags);
+    if (b->kslot)   // keyed: in_pfx doubles as the clamped-slot row for k_ecmult
+      hipLaunchKernelGGL(gv::k_prep<true>, grd, blk, 0, st, C, b->n, (const uint32_t*)nullptr,
+                         (const uint32_t*)nullptr, b->in_r, b->in_s, b->in_e, (const uint32_t*)w, b->digits,
+                         (uint32_t*)nullptr, (uint32_t*)nullptr, b->flags, b->kslot, b->kok, b->kcount, b->in_pfx);
+    else
+      hipLaunchKernelGGL(gv::k_prep<false>, grd, blk, 0, st, C, b->n, b->in_x, b->in_pfx, b->in_r, b->in_s,
+                         b->in_e, (const uint32_t*)w, b->digits, b->qtab, b->zq, b->flags,
+                         (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr);
   }
   if (b->ev[1]) (void)hipEventRecord(b->ev[1], st);
-  hipLaunchKernelGGL(gv::k_ecmult, grd, blk, 0, st, b->gtab, b->n, C, b->digits, b->qtab, b->zq, b->flags,
-                     b->in_r, b->bits);
+  if (b->kslot)
+    hipLaunchKernelGGL(gv::k_ecmult<true>, grd, blk, 0, st, b->gtab, b->n, C, b->digits, b->kqt, b->kzq,
+                       b->flags, b->in_r, b->bits, (const uint32_t*)b->in_pfx, b->kC);
+  else
+    hipLaunchKernelGGL(gv::k_ecmult<false>, grd, blk, 0, st, b->gtab, b->n, C, b->digits,
+                       (const uint32_t*)b->qtab, (const uint32_t*)b->zq, b->flags, b->in_r, b->bits,
+                       (const uint32_t*)nullptr, 0u);
   if (b->ev[2]) (void)hipEventRecord(b->ev[2], st);
+  return hipGetLastError();
+}
+
+hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
+                          uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t base,
+                          uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, hipStream_t st) {
+  const dim3 blk(256), grd(C / 256);
+  hipLaunchKernelGGL(gv::k_unpack, grd, blk, 0, st, pub33, (const uint8_t*)nullptr, (const uint8_t*)nullptr, n, C,
+                     in_x, in_pfx, in_r, in_s, in_e);
+  hipLaunchKernelGGL(gv::k_keys_build, grd, blk, 0, st, n, C, (const uint32_t*)in_x, (const uint32_t*)in_pfx, base,
+                     kqt, kzq, kC, kok, qr);
   return hipGetLastError();
 }
 

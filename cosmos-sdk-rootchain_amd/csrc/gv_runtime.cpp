@@ -44,6 +44,10 @@ struct Dev {
   size_t msg_cap = 0;
   uint64_t* h_bits = nullptr;   // pinned
   size_t h_bits_cap = 0;
+  uint32_t* d_slot = nullptr;   // keyed host batches: slot column (part of scratch)
+  // key arena (gv_keys_load): Q table rows, table Z (8 rows of stride kcap), verdicts
+  uint32_t *kqt = nullptr, *kzq = nullptr, *kok = nullptr;
+  size_t kcap = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   // ring of per-launch stage events for gv_stage_stats
   static constexpr int kRing = 256;
@@ -57,7 +61,7 @@ size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 int ensure_cap(Dev* d, size_t C) {
   if (C <= d->cap) return GV_OK;
   if (d->scratch) { (void)hipFree(d->scratch); d->scratch = nullptr; d->cap = 0; }
-  const size_t bytes = C * (33 + 64 + 32) + C * kLaneWords * 4 + (C / 64) * 8 + 4096;
+  const size_t bytes = C * (33 + 64 + 32) + C * kLaneWords * 4 + (C / 64) * 8 + C * 4 + 4096;
   if (hipMalloc(&d->scratch, bytes) != hipSuccess) return GV_ENOMEM;
   uint8_t* p = d->scratch;
   auto take = [&](size_t nbytes) { uint8_t* r = p; p += round_up(nbytes, 256); return r; };
@@ -74,6 +78,7 @@ int ensure_cap(Dev* d, size_t C) {
   d->flags = (uint32_t*)take(C * 4);
   d->qtab = (uint32_t*)take(C * GV_QTAB_WORDS * 4);
   d->bits = (uint64_t*)take((C / 64) * 8);
+  d->d_slot = (uint32_t*)take(C * 4);
   d->cap = C;
   return GV_OK;
 }
@@ -95,6 +100,29 @@ int ensure_msg(Dev* d, size_t blob_bytes, size_t C) {
   return GV_OK;
 }
 
+// Grow the key arena to hold `need` slots, keeping the first `used` (row
+// stride of kzq changes with the capacity).
+int ensure_keys(Dev* d, size_t need, size_t used, hipStream_t st) {
+  if (need <= d->kcap) return GV_OK;
+  const size_t cap = round_up(std::max<size_t>({need, 2 * d->kcap, 4096}), 256);
+  uint32_t *qt = nullptr, *zq = nullptr, *ok = nullptr;
+  if (hipMalloc(&qt, cap * GV_KEY_WORDS * 4) != hipSuccess) return GV_ENOMEM;
+  if (hipMalloc(&zq, cap * 8 * 4) != hipSuccess) { (void)hipFree(qt); return GV_ENOMEM; }
+  if (hipMalloc(&ok, cap * 4) != hipSuccess) { (void)hipFree(qt); (void)hipFree(zq); return GV_ENOMEM; }
+  if (used) {
+    CK(hipMemcpyAsync(qt, d->kqt, used * GV_KEY_WORDS * 4, hipMemcpyDeviceToDevice, st));
+    for (int r = 0; r < 8; ++r)
+      CK(hipMemcpyAsync(zq + r * cap, d->kzq + r * d->kcap, used * 4, hipMemcpyDeviceToDevice, st));
+    CK(hipMemcpyAsync(ok, d->kok, used * 4, hipMemcpyDeviceToDevice, st));
+    CK(hipStreamSynchronize(st));
+  }
+  if (d->kqt) (void)hipFree(d->kqt);
+  if (d->kzq) (void)hipFree(d->kzq);
+  if (d->kok) (void)hipFree(d->kok);
+  d->kqt = qt; d->kzq = zq; d->kok = ok; d->kcap = cap;
+  return GV_OK;
+}
+
 int ensure_hbits(Dev* d, size_t words) {
   if (words <= d->h_bits_cap) return GV_OK;
   if (d->h_bits) (void)hipHostFree(d->h_bits);
@@ -112,6 +140,8 @@ struct gv_ctx {
   size_t lat_max = 4096;        // batches up to this size take the fused latency kernel (gv_lat.hip)
   bool time_kernels = false;
   bool fault_inject = false;
+  size_t keys = 0;              // key-arena slots in use (same on every device)
+  std::mutex keys_mu;
 };
 
 namespace {
@@ -119,10 +149,14 @@ namespace {
 // Launch the pipeline for n items whose inputs already sit on the device.
 int launch(gv_ctx* ctx, Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig, const uint8_t* dig,
            const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint64_t* bits_out,
-           hipStream_t st) {
+           hipStream_t st, const uint32_t* kslot = nullptr) {
   const size_t C = round_up(std::max<size_t>(n, 1), 256);
   int rc = ensure_cap(d, C);
   if (rc) return rc;
+  if (kslot) {                                  // the arena always exists for a keyed batch
+    rc = ensure_keys(d, 1, ctx->keys, st);
+    if (rc) return rc;
+  }
   gvk_batch b;
   memset(&b, 0, sizeof b);
   b.n = (uint32_t)n; b.C = (uint32_t)C;
@@ -132,6 +166,11 @@ int launch(gv_ctx* ctx, Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig
   b.in_x = d->in_x; b.in_pfx = d->in_pfx; b.in_r = d->in_r; b.in_s = d->in_s; b.in_e = d->in_e;
   b.digits = d->digits; b.zq = d->zq; b.flags = d->flags; b.qtab = d->qtab;
   b.bits = bits_out;
+  if (kslot) {
+    b.pub33 = nullptr;
+    b.kslot = kslot; b.kqt = d->kqt; b.kzq = d->kzq; b.kok = d->kok;
+    b.kC = (uint32_t)d->kcap; b.kcount = (uint32_t)ctx->keys;
+  }
   hipEvent_t* rs = nullptr;
   if (ctx->time_kernels) {
     rs = d->ring[d->ring_next];
@@ -140,7 +179,7 @@ int launch(gv_ctx* ctx, Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig
     CK(hipEventRecord(rs[3], st));
     b.ev[0] = rs[0]; b.ev[1] = rs[1]; b.ev[2] = rs[2];
   }
-  if (n <= ctx->lat_max) {
+  if (n <= ctx->lat_max && !kslot) {
     // small batch: one fused kernel, several lanes per signature (gv_lat.hip)
     gvk_lat lb;
     memset(&lb, 0, sizeof lb);
@@ -169,7 +208,7 @@ int launch(gv_ctx* ctx, Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig
 // Verify items [lo, hi) of a host batch on one device.  out_ok or out_bits.
 int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const uint8_t* pub33, const uint8_t* sig64,
               const uint8_t* dig32, const uint8_t* blob, const uint64_t* off, const uint32_t* len,
-              uint8_t* out_ok, uint64_t* out_bits) {
+              uint8_t* out_ok, uint64_t* out_bits, const uint32_t* slots) {
   std::lock_guard<std::mutex> lk(d->mu);
   CK(hipSetDevice(d->id));
   const size_t chunk = ctx->max_batch;
@@ -181,7 +220,8 @@ int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const uint8_t* pub33, c
     if (rc) return rc;
     rc = ensure_hbits(d, C / 64);
     if (rc) return rc;
-    CK(hipMemcpyAsync(d->d_pub, pub33 + c0 * 33, cn * 33, hipMemcpyHostToDevice, d->st));
+    if (slots) CK(hipMemcpyAsync(d->d_slot, slots + c0, cn * 4, hipMemcpyHostToDevice, d->st));
+    else CK(hipMemcpyAsync(d->d_pub, pub33 + c0 * 33, cn * 33, hipMemcpyHostToDevice, d->st));
     CK(hipMemcpyAsync(d->d_sig, sig64 + c0 * 64, cn * 64, hipMemcpyHostToDevice, d->st));
     const uint8_t* ddig = nullptr;
     const uint8_t* dblob = nullptr;
@@ -205,7 +245,7 @@ int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const uint8_t* pub33, c
       dblob = d->d_blob;
     }
     rc = launch(ctx, d, cn, d->d_pub, d->d_sig, ddig, dblob, dblob ? d->d_off : nullptr,
-                dblob ? d->d_len : nullptr, d->bits, d->st);
+                dblob ? d->d_len : nullptr, d->bits, d->st, slots ? d->d_slot : nullptr);
     if (rc) return rc;
     const size_t words = (cn + 63) / 64;
     CK(hipMemcpyAsync(d->h_bits, d->bits, words * 8, hipMemcpyDeviceToHost, d->st));
@@ -222,11 +262,11 @@ int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const uint8_t* pub33, c
 
 int run_host(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64, const uint8_t* dig32,
              const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint8_t* out_ok,
-             uint64_t* out_bits) {
+             uint64_t* out_bits, const uint32_t* slots = nullptr) {
   if (!ctx) return GV_EINVAL;
   if (ctx->fault_inject) return GV_EFAULT;
   if (n == 0) return GV_OK;
-  if (!pub33 || !sig64 || (!out_ok && !out_bits)) return GV_EINVAL;
+  if ((!pub33 && !slots) || !sig64 || (!out_ok && !out_bits)) return GV_EINVAL;
   if (!dig32 && (!blob || !off || !len)) return GV_EINVAL;
   const size_t nd = ctx->devs.size();
   const size_t per = round_up((n + nd - 1) / nd, 256);
@@ -236,7 +276,7 @@ int run_host(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64, 
     const size_t lo = std::min(n, k * per), hi = std::min(n, (k + 1) * per);
     if (lo >= hi) continue;
     auto job = [=, &rcs]() {
-      rcs[k] = run_slice(ctx, ctx->devs[k], lo, hi, pub33, sig64, dig32, blob, off, len, out_ok, out_bits);
+      rcs[k] = run_slice(ctx, ctx->devs[k], lo, hi, pub33, sig64, dig32, blob, off, len, out_ok, out_bits, slots);
     };
     if (nd == 1) job(); else th.emplace_back(job);
   }
@@ -295,6 +335,9 @@ void gv_close(gv_ctx* ctx) {
     if (d->d_off) (void)hipFree(d->d_off);
     if (d->d_len) (void)hipFree(d->d_len);
     if (d->h_bits) (void)hipHostFree(d->h_bits);
+    if (d->kqt) (void)hipFree(d->kqt);
+    if (d->kzq) (void)hipFree(d->kzq);
+    if (d->kok) (void)hipFree(d->kok);
     for (auto e : d->ev) if (e) (void)hipEventDestroy(e);
     for (auto& rs : d->ring)
       for (auto e : rs) if (e) (void)hipEventDestroy(e);
@@ -369,6 +412,71 @@ int gv_dev_verify_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub33,
   return launch(ctx, d, n, (const uint8_t*)d_pub33, (const uint8_t*)d_sig64, nullptr,
                 (const uint8_t*)d_msg_blob, (const uint64_t*)d_msg_off, (const uint32_t*)d_msg_len,
                 (uint64_t*)d_bits, st);
+}
+
+// ---- key arena
+int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out) {
+  if (!ctx) return GV_EINVAL;
+  if (n == 0) return GV_OK;
+  if (!pub33 || !slot_out) return GV_EINVAL;
+  std::lock_guard<std::mutex> kl(ctx->keys_mu);
+  const size_t base = ctx->keys;
+  if (base + n > 0xFFFFFF00ull) return GV_EINVAL;
+  for (Dev* d : ctx->devs) {                    // every device holds every key
+    std::lock_guard<std::mutex> lk(d->mu);
+    CK(hipSetDevice(d->id));
+    int rc = ensure_keys(d, base + n, base, d->st);
+    if (rc) return rc;
+    for (size_t c0 = 0; c0 < n; c0 += ctx->max_batch) {
+      const size_t cn = std::min(ctx->max_batch, n - c0);
+      const size_t C = round_up(cn, 256);
+      rc = ensure_cap(d, C);
+      if (rc) return rc;
+      CK(hipMemcpyAsync(d->d_pub, pub33 + c0 * 33, cn * 33, hipMemcpyHostToDevice, d->st));
+      CK(gvk_keys_build(d->d_pub, (uint32_t)cn, (uint32_t)C, d->in_x, d->in_pfx, d->in_r, d->in_s, d->in_e,
+                        d->qtab + C * GV_QTAB_N * GV_QENT_WORDS, (uint32_t)(base + c0), d->kqt, d->kzq,
+                        (uint32_t)d->kcap, d->kok, d->st));
+    }
+    CK(hipStreamSynchronize(d->st));
+  }
+  ctx->keys = base + n;
+  for (size_t i = 0; i < n; ++i) slot_out[i] = (uint32_t)(base + i);
+  return GV_OK;
+}
+
+int gv_keys_reset(gv_ctx* ctx) {
+  if (!ctx) return GV_EINVAL;
+  std::lock_guard<std::mutex> kl(ctx->keys_mu);
+  ctx->keys = 0;
+  return GV_OK;
+}
+
+size_t gv_keys_count(const gv_ctx* ctx) { return ctx ? ctx->keys : 0; }
+
+int gv_verify_digests_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64,
+                            const uint8_t* dig32, uint8_t* out_ok) {
+  if (n && (!slot || !dig32)) return GV_EINVAL;
+  return run_host(ctx, n, nullptr, sig64, dig32, nullptr, nullptr, nullptr, out_ok, nullptr, slot);
+}
+
+int gv_verify_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64,
+                         const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len,
+                         uint8_t* out_ok) {
+  if (n && !slot) return GV_EINVAL;
+  return run_host(ctx, n, nullptr, sig64, nullptr, msg_blob, msg_off, msg_len, out_ok, nullptr, slot);
+}
+
+int gv_dev_verify_digests_keyed(gv_ctx* ctx, int dev_slot, size_t n, const void* d_slot, const void* d_sig64,
+                                const void* d_dig32, void* d_bits, void* stream) {
+  Dev* d = nullptr;
+  int rc = dev_common(ctx, dev_slot, n, d_slot, d_sig64, d_bits, &d);
+  if (rc || n == 0) return rc;
+  if (!d_dig32 || ((uintptr_t)d_dig32 & 3)) return GV_EINVAL;
+  std::lock_guard<std::mutex> lk(d->mu);
+  CK(hipSetDevice(d->id));
+  hipStream_t st = stream ? (hipStream_t)stream : d->st;
+  return launch(ctx, d, n, nullptr, (const uint8_t*)d_sig64, (const uint8_t*)d_dig32, nullptr, nullptr, nullptr,
+                (uint64_t*)d_bits, st, (const uint32_t*)d_slot);
 }
 
 int gv_set_option(gv_ctx* ctx, const char* key, long long val) {

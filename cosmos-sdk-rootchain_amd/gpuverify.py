@@ -32,7 +32,8 @@ EXPORTED_SYMBOLS = (
     "gv_open", "gv_close", "gv_num_devices", "gv_verify_msgs", "gv_verify_digests",
     "gv_verify_digests_bits", "gv_verify_msgs_bits", "gv_dev_verify_digests", "gv_dev_verify_msgs",
     "gv_set_option", "gv_last_stage_ms", "gv_strerror", "gv_debug_op", "gv_dev_alloc", "gv_dev_free",
-    "gv_dev_copy", "gv_dev_sync", "gv_stage_stats",
+    "gv_dev_copy", "gv_dev_sync", "gv_stage_stats", "gv_keys_load", "gv_keys_reset", "gv_keys_count",
+    "gv_verify_digests_keyed", "gv_verify_msgs_keyed", "gv_dev_verify_digests_keyed",
 )
 
 
@@ -96,6 +97,18 @@ def load(path: str = LIB_PATH):
     L.gv_dev_sync.restype = i32
     L.gv_stage_stats.argtypes = [vp, i32, ctypes.POINTER(i32)] + [ctypes.POINTER(ctypes.c_double)] * 3
     L.gv_stage_stats.restype = i32
+    L.gv_keys_load.argtypes = [vp, sz, vp, vp]
+    L.gv_keys_load.restype = i32
+    L.gv_keys_reset.argtypes = [vp]
+    L.gv_keys_reset.restype = i32
+    L.gv_keys_count.argtypes = [vp]
+    L.gv_keys_count.restype = sz
+    L.gv_verify_digests_keyed.argtypes = [vp, sz, vp, vp, vp, vp]
+    L.gv_verify_digests_keyed.restype = i32
+    L.gv_verify_msgs_keyed.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp]
+    L.gv_verify_msgs_keyed.restype = i32
+    L.gv_dev_verify_digests_keyed.argtypes = [vp, i32, sz, vp, vp, vp, vp, vp]
+    L.gv_dev_verify_digests_keyed.restype = i32
     _lib = L
     return L
 
@@ -192,6 +205,53 @@ class Verifier:
             _check(self._L.gv_verify_msgs(self._ctx, n, _ptr(pub33), _ptr(sig64), _ptr(blob), _ptr(off),
                                           _ptr(ln), _ptr(out)), "gv_verify_msgs")
         return out
+
+    # ---- account pubkey cache (gv_keys_*)
+    def keys_load(self, pub33: np.ndarray) -> np.ndarray:
+        """Parse and keep n keys resident; returns their slots (u32)."""
+        pub33 = np.ascontiguousarray(pub33, dtype=np.uint8)
+        n = pub33.shape[0]
+        assert pub33.shape == (n, 33)
+        slots = np.zeros(n, dtype=np.uint32)
+        if n:
+            _check(self._L.gv_keys_load(self._ctx, n, _ptr(pub33), _ptr(slots)), "gv_keys_load")
+        return slots
+
+    def keys_reset(self):
+        _check(self._L.gv_keys_reset(self._ctx), "gv_keys_reset")
+
+    @property
+    def keys_count(self) -> int:
+        return self._L.gv_keys_count(self._ctx)
+
+    def verify_batch_digests_keyed(self, slots: np.ndarray, sig64: np.ndarray, dig32: np.ndarray) -> np.ndarray:
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        sig64, dig32 = (np.ascontiguousarray(a, dtype=np.uint8) for a in (sig64, dig32))
+        n = slots.shape[0]
+        assert sig64.shape == (n, 64) and dig32.shape == (n, 32)
+        out = np.zeros(n, dtype=np.uint8)
+        if n:
+            _check(self._L.gv_verify_digests_keyed(self._ctx, n, _ptr(slots), _ptr(sig64), _ptr(dig32), _ptr(out)),
+                   "gv_verify_digests_keyed")
+        return out
+
+    def verify_batch_msgs_keyed(self, slots: np.ndarray, sig64: np.ndarray, msgs) -> np.ndarray:
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        sig64 = np.ascontiguousarray(sig64, dtype=np.uint8)
+        blob, off, ln = pack_msgs(msgs) if isinstance(msgs, (list, tuple)) and (
+            len(msgs) == 0 or isinstance(msgs[0], (bytes, bytearray))) else msgs
+        n = slots.shape[0]
+        out = np.zeros(n, dtype=np.uint8)
+        if n:
+            _check(self._L.gv_verify_msgs_keyed(self._ctx, n, _ptr(slots), _ptr(sig64), _ptr(blob), _ptr(off),
+                                                _ptr(ln), _ptr(out)), "gv_verify_msgs_keyed")
+        return out
+
+    def dev_verify_digests_keyed(self, slot: int, n: int, d_slots, d_sig, d_dig, d_bits, stream=None):
+        _check(self._L.gv_dev_verify_digests_keyed(self._ctx, slot, n, ctypes.c_void_p(d_slots),
+                                                   ctypes.c_void_p(d_sig), ctypes.c_void_p(d_dig),
+                                                   ctypes.c_void_p(d_bits), ctypes.c_void_p(stream or 0)),
+               "gv_dev_verify_digests_keyed")
 
     def dev_verify_digests(self, slot: int, n: int, d_pub, d_sig, d_dig, d_bits, stream=None):
         """Device-resident path: d_* are device addresses (ints); stream a hipStream_t int."""

@@ -97,6 +97,34 @@ int gv_dev_free(gv_ctx* ctx, int dev_slot, void* d_ptr);
 int gv_dev_copy(gv_ctx* ctx, int dev_slot, void* dst, const void* src, size_t bytes, int kind);
 int gv_dev_sync(gv_ctx* ctx, int dev_slot);
 
+/* Account pubkey cache.  The reference amino-decodes and
+ * btcec-parses an account's pubkey on every VerifyBytes
+ * (x/auth/types/account.go:65-72 -> secp256k1_nocgo.go ParsePubKey), and a
+ * node verifies the same accounts block after block.  gv_keys_load parses n
+ * SEC1 keys once (prefix, x < p, square root) and keeps each key's table of
+ * 16 multiples resident in HBM on every device of the context (1,280 B per
+ * key: 1M accounts = 1.3 GB of the 288 GB); slot_out[i] receives key i's slot.
+ * A key that ParsePubKey rejects gets a slot too, and every verify against it
+ * is false.  Slots are assigned in load order and stay valid until
+ * gv_keys_reset.  Loading must not race keyed verifies of the same context. */
+int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out);
+int gv_keys_reset(gv_ctx* ctx);
+size_t gv_keys_count(const gv_ctx* ctx);
+
+/* VerifyBytes with the key given by slot: out_ok[i] is exactly what
+ * gv_verify_digests / gv_verify_msgs return with pub33 = the key loaded into
+ * slot[i]; a slot >= gv_keys_count() gives false.  Same batching, errors and
+ * multi-device split as the pub33 entry points (the fused small-batch kernel
+ * is not used for keyed batches). */
+int gv_verify_digests_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64,
+                            const uint8_t* dig32, uint8_t* out_ok);
+int gv_verify_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64,
+                         const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len,
+                         uint8_t* out_ok);
+/* Device-resident keyed digests: d_slot = n u32 slots on dev_slot. */
+int gv_dev_verify_digests_keyed(gv_ctx* ctx, int dev_slot, size_t n, const void* d_slot, const void* d_sig64,
+                                const void* d_dig32, void* d_bits, void* stream);
+
 /* Options: "max_batch" (lanes per device launch, default 1<<20),
  * "lat_max" (batches of at most this many items -- per device slice -- take
  * the fused small-batch latency kernel, default 4096; 0 = never),
