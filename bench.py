@@ -153,15 +153,19 @@ def _pct(ts):
     return round(float(np.percentile(ts, 50)), 3), round(float(np.percentile(ts, 99)), 3)
 
 
-def checktx_latency(ver, pub, sig, dig, threads, sizes=(1, 16, 32, 64, 128, 256, 1024, 4096), reps=200):
+def checktx_latency(ver, pub, sig, dig, threads, sizes=(1, 16, 32, 64, 128, 256, 1024, 4096), reps=1000):
     """C5: host-path latency (pack -> H2D -> kernel(s) -> D2H -> verdicts) per
     batch size.  p50/p99 are the default GPU path (the fused latency kernel,
     gv_lat.hip, up to the "lat_max" option); next to it the throughput pipeline
-    forced for the same batches, and the CPU oracle (oracle/secp256k1_oracle.c,
+    forced for the same batches, the keyed path (account keys in the HBM key
+    arena, gv_verify_digests_keyed), and the CPU oracle (oracle/secp256k1_oracle.c,
     the reference algorithm restated in C) serial and on `threads` cores."""
     from oracle import oracle as O
     O.lib()
     out = {}
+    nkeys = 65536                                   # the C2 workload's keys, item i uses key i % nkeys
+    ver.keys_reset()
+    slots = ver.keys_load(pub[:nkeys])[np.arange(len(pub)) % nkeys]
     for b in sizes:
         def run_gpu(rr):
             ts = []
@@ -172,6 +176,13 @@ def checktx_latency(ver, pub, sig, dig, threads, sizes=(1, 16, 32, 64, 128, 256,
                 ts.append(time.perf_counter() - t)
             return ts[5:]
         p50, p99 = _pct(run_gpu(reps))
+        ts = []
+        for r in range(reps // 2 + 5):
+            o = (r * b) % (len(pub) - b)
+            t = time.perf_counter()
+            ver.verify_batch_digests_keyed(slots[o:o + b], sig[o:o + b], dig[o:o + b])
+            ts.append(time.perf_counter() - t)
+        keyed50, _ = _pct(ts[5:])
         ver.set_option("lat_max", 0)
         tp50, _ = _pct(run_gpu(max(20, reps // 4)))
         ver.set_option("lat_max", 4096)
@@ -187,7 +198,8 @@ def checktx_latency(ver, pub, sig, dig, threads, sizes=(1, 16, 32, 64, 128, 256,
                 if time.perf_counter() > budget and len(ts) >= 3:
                     break
             cpu[label] = _pct(ts)[0]
-        out[str(b)] = {"p50_ms": p50, "p99_ms": p99, "throughput_path_p50_ms": tp50, **cpu}
+        out[str(b)] = {"p50_ms": p50, "p99_ms": p99, "throughput_path_p50_ms": tp50, "keyed_p50_ms": keyed50, **cpu}
+    ver.keys_reset()
     return out
 
 
@@ -355,6 +367,7 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
         ex = {}
         t = time.perf_counter()
         ex["c2_key_cache"] = X.c2_key_cache(ver, pub, sig, dig, exp, min(args.keys, n))
+        ex["c2_unique_keys"] = X.c2_unique_keys(ver, make_digest_workload, n, args.threads)
         ex["c3_adversarial"] = X.c3_adversarial(ver, make_digest_workload, n, args.threads)
         ex["msg_path"] = X.msg_path(ver, workload_lib(), min(n, 500_000), args.threads)
         ex["c1_ante"] = X.c1_ante(ver)

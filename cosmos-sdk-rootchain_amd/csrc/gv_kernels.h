@@ -70,6 +70,12 @@ typedef struct gvk_lat {
   uint32_t* e_soa;              // message path: 8 rows of C words
   uint64_t* bits;
   hipEvent_t ev[1];             // optional: after the SHA stage
+  // keyed batch (kslot != NULL, pub33 unused): tables from the key arena
+  const uint32_t* kslot;
+  const uint32_t* kqt;
+  const uint32_t* kzq;
+  const uint32_t* kok;
+  uint32_t kC, kcount;
 } gvk_lat;
 
 hipError_t gvk_gen_gtable(uint32_t* gtab, hipStream_t st);

@@ -35,6 +35,20 @@ static_assert(F29_NCH == 2, "gv_lat.hip is built with -DF29_NCH=2");
 
 namespace gv {
 
+// GV_LAT_TRACE (A/B builds only): per block, wall-clock stamps (100 MHz) of
+// the phases -- start, wave 0 prep done, wave 1 scalars done, after the
+// barrier, ladder done, combine done, end -- read back with
+// gv_debug_lat_trace.  Off in the product build.
+#ifndef GV_LAT_TRACE
+#define GV_LAT_TRACE 0
+#endif
+#if GV_LAT_TRACE
+__device__ uint64_t g_lat_trace[256][8];
+#define LAT_STAMP(k) do { if ((threadIdx.x & 63u) == 0 && blockIdx.x < 256) g_lat_trace[blockIdx.x][k] = wall_clock64(); } while (0)
+#else
+#define LAT_STAMP(k) do { } while (0)
+#endif
+
 static __constant__ const u32 kLBeta[8] = {0x719501EEu, 0xC1396C28u, 0x12F58995u, 0x9CF04975u,
                                            0xAC3434E9u, 0x6E64479Eu, 0x657C0710u, 0x7AE96A2Bu};
 static __constant__ const u32 kLP[8] = {0xFFFFFC2Fu, 0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu,
@@ -198,6 +212,44 @@ GV_DEV void lat_pubkey_and_tables(LatShared& sh, int sig, int slot, bool live, c
 }
 
 
+// Wave 0 prep for a keyed signature (gv_keys_load): the Q table comes from the
+// key arena row (built once per key by k_keys_build, same effective-affine
+// form and Z), so no square root and no table build.  Lane 4s + k copies
+// entries k, k+4, k+8, k+12 and forms their lambda*Q entries (beta*x, y).
+GV_DEV void lat_keyed_tables(LatShared& sh, int sig, int slot, bool live, u32 kslot, const u32* kqt,
+                             const u32* kzq, const u32* kok, u32 kC, u32 kcount) {
+  u32 sl = live ? kslot : 0xFFFFFFFFu;
+  bool ok = sl < kcount;
+  if (!ok) sl = 0;                                    // the arena always holds slot 0's memory
+  ok = ok && kok[sl] != 0u;
+  fe29 beta;
+  {
+    u32 w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = kLBeta[i];
+    f29_from_words(beta, w);
+  }
+#pragma unroll 1
+  for (int m = slot; m < GV_QTAB_N; m += 4) {
+    const uint4* p = (const uint4*)(kqt + ((size_t)sl * GV_QTAB_N + m) * GV_QENT_WORDS);
+    const uint4 a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
+    fe29 x, y, t;
+    x.n[0] = a.x; x.n[1] = a.y; x.n[2] = a.z; x.n[3] = a.w;
+    x.n[4] = b.x; x.n[5] = b.y; x.n[6] = b.z; x.n[7] = b.w;
+    x.n[8] = c.x; y.n[0] = c.y; y.n[1] = c.z; y.n[2] = c.w;
+    y.n[3] = d.x; y.n[4] = d.y; y.n[5] = d.z; y.n[6] = d.w;
+    y.n[7] = e.x; y.n[8] = e.y;
+    lds_put_ent(sh.qtab[sig][0][m], x, y);
+    f29_mul(t, x, beta);
+    lds_put_ent(sh.qtab[sig][1][m], t, y);
+  }
+  if (slot == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sh.zq[sig][i] = kzq[(size_t)i * kC + sl];
+    sh.okp[sig] = ok ? 1u : 0u;
+  }
+}
+
 // Wave 1: the scalar chain of one signature (lane sig < GV_LAT_SIGS).
 GV_DEV void lat_scalars(LatShared& sh, int sig, bool live, const uint8_t* sig64, const uint8_t* dig32,
                         const u32* e_soa, u32 C, u32 gi) {
@@ -275,14 +327,20 @@ GV_DEV void shfl_xor_gej(gej29& o, bool& oinf, const gej29& a, bool ainf, int m)
 // block, bits16[block] (the u64 bitmap viewed as u16 words).
 __global__ __launch_bounds__(128) void k_verify_lat(const u32* gtab, const uint8_t* pub33,
                                                      const uint8_t* sig64, const uint8_t* dig32,
-                                                     const u32* e_soa, u32 C, u32 n, uint16_t* bits16) {
+                                                     const u32* e_soa, u32 C, u32 n, uint16_t* bits16,
+                                                     const u32* kslot, const u32* kqt, const u32* kzq,
+                                                     const u32* kok, u32 kC, u32 kcount) {
   __shared__ LatShared sh;
   const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  if (wave == 0) LAT_STAMP(0);
   if (wave == 0) {
     const int sig = lane >> 2, slot = lane & 3;
     const u32 gi = blockIdx.x * GV_LAT_SIGS + sig;
     const bool live = gi < n;
-    lat_pubkey_and_tables(sh, sig, slot, live, pub33 + (size_t)(live ? gi : 0) * 33u);
+    if (kslot)                                        // keyed batch: tables from the key arena
+      lat_keyed_tables(sh, sig, slot, live, live ? kslot[gi] : 0u, kqt, kzq, kok, kC, kcount);
+    else
+      lat_pubkey_and_tables(sh, sig, slot, live, pub33 + (size_t)(live ? gi : 0) * 33u);
   } else if (lane < GV_LAT_SIGS) {
     const u32 gi = blockIdx.x * GV_LAT_SIGS + lane;
     const bool live = gi < n;
@@ -290,8 +348,10 @@ __global__ __launch_bounds__(128) void k_verify_lat(const u32* gtab, const uint8
     lat_scalars(sh, lane, live, sig64 + (size_t)gs * 64u, dig32 ? dig32 + (size_t)gs * 32u : nullptr,
                 e_soa, C, gs);
   }
+  if (wave == 0) LAT_STAMP(1); else LAT_STAMP(2);
   __syncthreads();
   if (wave != 0) return;
+  LAT_STAMP(3);
 
   // ---- ladder: lane 4s + slot accumulates one of the four partial sums
   const int sig = lane >> 2, slot = lane & 3;
@@ -344,6 +404,7 @@ __global__ __launch_bounds__(128) void k_verify_lat(const u32* gtab, const uint8
     }
   }
 
+  LAT_STAMP(4);
   // ---- combine: Q-slot points back to the real curve (Z *= zq), then two
   // rounds of complete additions across the signature's four lanes.
   {
@@ -362,6 +423,7 @@ __global__ __launch_bounds__(128) void k_verify_lat(const u32* gtab, const uint8
   shfl_xor_gej(other, oinf, acc, inf, 2);
   gej29_add_gej(acc, inf, acc, inf, other, oinf);
 
+  LAT_STAMP(5);
   // ---- final check (as k_ecmult): x(R) mod n == r, without inversion
   const u32 fl = sh.oks[sig];
   bool ok = (fl & 1u) && sh.okp[sig] && !inf;
@@ -395,6 +457,7 @@ __global__ __launch_bounds__(128) void k_verify_lat(const u32* gtab, const uint8
 #pragma unroll
     for (int s2 = 0; s2 < GV_LAT_SIGS; ++s2) b16 |= (u32)((m >> (4 * s2)) & 1u) << s2;
     bits16[blockIdx.x] = (uint16_t)b16;
+    LAT_STAMP(6);
     if (blockIdx.x == gridDim.x - 1) {           // zero the rest of the last 64-bit word
       for (u32 k = blockIdx.x + 1; (k & 3u) != 0u; ++k) bits16[k] = 0;
     }
@@ -412,6 +475,13 @@ extern "C" hipError_t gvk_verify_lat(const gvk_lat* b, hipStream_t st) {
   if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
   hipLaunchKernelGGL(gv::k_verify_lat, dim3(blocks), dim3(128), 0, st, b->gtab, b->pub33, b->sig64,
                      b->msg_blob ? nullptr : b->dig32, b->msg_blob ? (const uint32_t*)b->e_soa : nullptr,
-                     b->C, b->n, (uint16_t*)b->bits);
+                     b->C, b->n, (uint16_t*)b->bits, b->kslot, b->kqt, b->kzq, b->kok, b->kC, b->kcount);
   return hipGetLastError();
 }
+
+#if GV_LAT_TRACE
+extern "C" int gv_debug_lat_trace(uint64_t* out, int blocks) {
+  if (blocks > 256) blocks = 256;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gv::g_lat_trace), (size_t)blocks * 8 * 8) == hipSuccess ? 0 : -3;
+}
+#endif

@@ -179,7 +179,7 @@ int launch(gv_ctx* ctx, Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig
     CK(hipEventRecord(rs[3], st));
     b.ev[0] = rs[0]; b.ev[1] = rs[1]; b.ev[2] = rs[2];
   }
-  if (n <= ctx->lat_max && !kslot) {
+  if (n <= ctx->lat_max) {
     // small batch: one fused kernel, several lanes per signature (gv_lat.hip)
     gvk_lat lb;
     memset(&lb, 0, sizeof lb);
@@ -188,6 +188,10 @@ int launch(gv_ctx* ctx, Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig
     lb.msg_blob = blob; lb.msg_off = off; lb.msg_len = len;
     lb.gtab = d->gtab; lb.e_soa = d->in_e; lb.bits = bits_out;
     lb.ev[0] = b.ev[0];
+    if (kslot) {
+      lb.pub33 = nullptr;
+      lb.kslot = kslot; lb.kqt = b.kqt; lb.kzq = b.kzq; lb.kok = b.kok; lb.kC = b.kC; lb.kcount = b.kcount;
+    }
     CK(gvk_verify_lat(&lb, st));
     if (rs) {                                   // stages: SHA | fused kernel | (none)
       CK(hipEventRecord(rs[1], st));

@@ -49,6 +49,7 @@ def lib():
         L.gvh_preverify.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), ctypes.POINTER(sz)]
         L.gvh_consume_sig_gas.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p, sz, u64, ctypes.POINTER(Result)]
         L.gvh_cache_clear.argtypes = [vp]
+        L.gvh_set_threads.argtypes = [vp, ctypes.c_int]
         L.gvh_cache_size.argtypes = [vp]
         L.gvh_cache_size.restype = sz
         L.gvh_std_sign_bytes.argtypes = [ctypes.c_char_p, u64, u64, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p),
@@ -135,6 +136,9 @@ class HostApp:
         self._L.gvh_consume_sig_gas(self._app, sig, len(sig), pub_amino, len(pub_amino or b""), gas_limit,
                                     ctypes.byref(r))
         return r.as_dict()
+
+    def set_threads(self, n: int):
+        self._L.gvh_set_threads(self._app, n)
 
     def cache_size(self) -> int:
         return self._L.gvh_cache_size(self._app)

@@ -8,7 +8,10 @@
 #include <openssl/ripemd.h>
 #include <openssl/sha.h>
 
+#include <algorithm>
 #include <array>
+#include <chrono>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -16,6 +19,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -61,9 +65,15 @@ struct OutOfGas {
 };
 
 // ---------------------------------------------------------------- hashing
+// The one-shot SHA256() of OpenSSL 3 fetches the digest through the provider
+// store on every call (a global lock: no scaling across PreVerifyTxs threads);
+// the context API hashes with no shared state.
 std::array<uint8_t, 32> sha256(const uint8_t* p, size_t n) {
   std::array<uint8_t, 32> o;
-  SHA256(p, n, o.data());
+  SHA256_CTX c;
+  SHA256_Init(&c);
+  SHA256_Update(&c, p, n);
+  SHA256_Final(o.data(), &c);
   return o;
 }
 
@@ -292,7 +302,10 @@ std::array<uint8_t, 20> pubkey_address(const PubKey& pk) {
   std::array<uint8_t, 20> a{};
   if (pk.kind == PubKey::Secp256k1) {
     auto h = sha256(pk.secp.data(), 33);
-    RIPEMD160(h.data(), 32, a.data());
+    RIPEMD160_CTX c;                                  // context API: no provider fetch per call
+    RIPEMD160_Init(&c);
+    RIPEMD160_Update(&c, h.data(), 32);
+    RIPEMD160_Final(a.data(), &c);
   } else if (pk.kind == PubKey::Ed25519) {
     auto h = sha256(pk.ed.data(), 32);
     memcpy(a.data(), h.data(), 20);
@@ -408,6 +421,10 @@ struct gvh_app {
   std::unordered_map<std::array<uint8_t, 20>, Account, AddrHash> accounts;
   std::unordered_map<std::string, bool> cache;   // pub33 || sig64 || sha256(msg)
   std::mutex mu;
+  // PreVerifyTxs host threads: measured on the MI355X box host (tools/host_probe.py,
+  // 10k MsgSend txs) 1 thread 11-12 ms, 4 threads 9.4 ms, 16 threads 11.4 ms --
+  // the stages are allocation-heavy and stop scaling past a few threads.
+  int threads = std::max(1, std::min(4, (int)std::thread::hardware_concurrency()));
 };
 
 namespace {
@@ -678,6 +695,26 @@ int run_ante(gvh_app* app, const FlatTx& tx, bool simulate, gvh_result* out) {
   return GVH_OK;
 }
 
+// Run fn(i) for i in [0, n) on up to `threads` threads (dynamic chunks).
+template <class F>
+void parallel_for(size_t n, int threads, F fn) {
+  const size_t chunk = 64;
+  if (threads <= 1 || n <= chunk) {
+    for (size_t i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (size_t lo; (lo = next.fetch_add(chunk)) < n;)
+      for (size_t i = lo; i < std::min(n, lo + chunk); ++i) fn(i);
+  };
+  const int nt = (int)std::min<size_t>(threads, (n + chunk - 1) / chunk);
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+}
+
 }  // namespace
 
 extern "C" {
@@ -740,41 +777,76 @@ int gvh_ante(gvh_app* app, const uint8_t* tx, size_t tx_len, int simulate, gvh_r
   return run_ante(app, t, simulate != 0, out);
 }
 
+// PreVerifyTxs: (1) decode every tx in parallel, (2) predict each signer's
+// sequence in block order (serial: it is a prefix count per signer), (3) build
+// sign bytes, SHA-256 and the leaves of every (tx, signer) in parallel (the
+// host sign-bytes pipeline of SURVEY.md §8f-3), (4) one GPU batch for the
+// cache misses.
 int gvh_preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, size_t* n_leaves) {
   if (!app || (ntx && (!txs || !lens))) return GVH_EINVAL;
   std::lock_guard<std::mutex> lk(app->mu);
-  std::vector<Leaf> leaves;
-  std::map<std::array<uint8_t, 20>, uint64_t> seq_bump;     // sequence prediction
-  for (size_t t = 0; t < ntx; ++t) {
-    FlatTx tx;
+  auto T0 = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) { if (getenv("GVH_PROFILE")) { auto t = std::chrono::steady_clock::now(); fprintf(stderr, "%s %.3f ms\n", what, std::chrono::duration<double, std::milli>(t - T0).count()); T0 = t; } };
+  std::vector<FlatTx> parsed(ntx);
+  std::vector<uint8_t> good(ntx, 0);
+  parallel_for(ntx, app->threads, [&](size_t t) {
     try {
-      tx = parse_flat(txs[t], lens[t]);
+      parsed[t] = parse_flat(txs[t], lens[t]);
+      good[t] = 1;
     } catch (const std::exception&) {
-      continue;
     }
+  });
+  lap("parse");
+  struct Job {
+    const FlatTx* tx;
+    size_t signer;
+    const Bytes* pub;     // account pubkey, else the tx-supplied one (stable: accounts not modified here)
+    uint64_t accnum, seq;
+  };
+  std::vector<Job> jobs;
+  std::unordered_map<std::array<uint8_t, 20>, uint64_t, AddrHash> seq_bump;   // sequence prediction
+  seq_bump.reserve(ntx * 2);
+  jobs.reserve(ntx);
+  for (size_t t = 0; t < ntx; ++t) {
+    if (!good[t]) continue;
+    const FlatTx& tx = parsed[t];
     for (size_t i = 0; i < tx.sigs.size() && i < tx.signers.size(); ++i) {
       auto it = app->accounts.find(tx.signers[i]);
       if (it == app->accounts.end()) continue;
       const Account& acc = it->second;
-      Bytes pubb = !acc.pub.empty() ? acc.pub : (i < tx.sig_pubs.size() ? tx.sig_pubs[i] : Bytes());
-      if (pubb.empty()) continue;
-      try {
-        PubKey pk = decode_pubkey(pubb.data(), pubb.size());
-        const uint64_t seq = acc.sequence + seq_bump[tx.signers[i]];
-        std::string sb = std_sign_bytes(app->chain_id, app->height == 0 ? 0 : acc.number, seq, tx.fee, tx.msgs, tx.memo);
-        Bytes msg(sb.begin(), sb.end());
-        auto dig = sha256(msg.data(), msg.size());
-        build_node(pk, msg, dig, tx.sigs[i], leaves);
-      } catch (const Panic&) {
-        continue;   // malformed: the ante chain will report it; nothing to cache
-      }
+      const Bytes* pubb = !acc.pub.empty() ? &acc.pub : (i < tx.sig_pubs.size() ? &tx.sig_pubs[i] : nullptr);
+      if (!pubb || pubb->empty()) continue;
+      jobs.push_back(Job{&tx, i, pubb, app->height == 0 ? 0 : acc.number, acc.sequence + seq_bump[tx.signers[i]]});
     }
     for (auto& a : tx.signers) seq_bump[a] += 1;
   }
+  lap("jobs");
+  std::vector<std::vector<Leaf>> job_leaves(jobs.size());
+  parallel_for(jobs.size(), app->threads, [&](size_t j) {
+    const Job& jb = jobs[j];
+    try {
+      PubKey pk = decode_pubkey(jb.pub->data(), jb.pub->size());
+      std::string sb = std_sign_bytes(app->chain_id, jb.accnum, jb.seq, jb.tx->fee, jb.tx->msgs, jb.tx->memo);
+      Bytes msg(sb.begin(), sb.end());
+      auto dig = sha256(msg.data(), msg.size());
+      build_node(pk, msg, dig, jb.tx->sigs[jb.signer], job_leaves[j]);
+    } catch (const Panic&) {
+      job_leaves[j].clear();   // malformed: the ante chain will report it; nothing to cache
+    }
+  });
+  lap("signbytes");
+  std::vector<Leaf> leaves;
+  for (auto& v : job_leaves) leaves.insert(leaves.end(), v.begin(), v.end());
+  lap("concat");
   uint32_t gpu_leaves = 0, hits = 0;
   int rc = leaves.empty() ? GVH_OK : resolve_leaves(app, leaves, &gpu_leaves, &hits);
+  lap("resolve");
   if (n_leaves) *n_leaves = gpu_leaves;
   return rc;
+}
+
+void gvh_set_threads(gvh_app* app, int threads) {
+  if (app) app->threads = std::max(1, std::min(256, threads));
 }
 
 int gvh_consume_sig_gas(gvh_app* app, const uint8_t* sig, size_t sig_len, const uint8_t* pub_amino, size_t pub_len,

@@ -90,6 +90,9 @@ int gvh_preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const siz
 int gvh_consume_sig_gas(gvh_app* app, const uint8_t* sig, size_t sig_len, const uint8_t* pub_amino, size_t pub_len,
                         uint64_t gas_limit, gvh_result* out);
 void gvh_cache_clear(gvh_app* app);
+/* Host threads for PreVerifyTxs' decode / sign-bytes / SHA-256 stages
+ * (default min(4, hardware threads)). */
+void gvh_set_threads(gvh_app* app, int threads);
 size_t gvh_cache_size(gvh_app* app);
 
 /* StdSignBytes (x/auth/types/stdtx.go:292-312): canonical JSON.  Returns the

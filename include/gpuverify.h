@@ -114,8 +114,8 @@ size_t gv_keys_count(const gv_ctx* ctx);
 /* VerifyBytes with the key given by slot: out_ok[i] is exactly what
  * gv_verify_digests / gv_verify_msgs return with pub33 = the key loaded into
  * slot[i]; a slot >= gv_keys_count() gives false.  Same batching, errors and
- * multi-device split as the pub33 entry points (the fused small-batch kernel
- * is not used for keyed batches). */
+ * multi-device split as the pub33 entry points; batches up to "lat_max" take
+ * the fused small-batch kernel with the key's table read from the arena. */
 int gv_verify_digests_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64,
                             const uint8_t* dig32, uint8_t* out_ok);
 int gv_verify_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64,

@@ -295,3 +295,43 @@ def test_preverify_block_fills_cache(ver):
     app2.set_account(KEYS[7].addr, 7, 3)
     rc, r = app2.ante(tx)
     assert r["code"] == 0 and r["cache_hits"] == 0 and r["gpu_leaves"] == 1
+
+
+@pytest.mark.gpu
+def test_parallel_preverify_matches_serial_and_plain_ante(ver):
+    """PreVerifyTxs' parallel decode / sign-bytes / SHA stages (threads=8) fill
+    the same cache as one thread, and the ante verdicts with the cache equal
+    the verdicts without it -- over a block with repeat signers (predicted
+    sequences), a wrong-sequence tx, a bad signature and a malformed tx."""
+    def block():
+        txs, seqs = [], {k.addr: 0 for k in KEYS[:8]}
+        for t in range(400):
+            k = KEYS[t % 8]
+            s = seqs[k.addr] + (5 if t == 101 else 0)          # t=101: signed for a wrong sequence
+            tx = make_tx("gv-test", [k], [KEYS.index(k)], [s])
+            if t == 202:                                       # bad signature
+                tx = make_tx("gv-test", [k], [KEYS.index(k)], [s], sign_keys=[KEYS[9]])
+            txs.append(tx)
+            if t not in (101, 202):                            # a rejected tx leaves the sequence
+                seqs[k.addr] += 1
+        txs.insert(150, b"\x01\x02")                           # malformed flat tx
+        return txs
+
+    txs = block()
+    results = []
+    for threads, pre in ((1, True), (8, True), (8, False)):
+        app = new_app(ver)
+        app.set_threads(threads)
+        if pre:
+            rc, n = app.preverify(txs)
+            assert rc == 0 and n == 400
+        out = []
+        for tx in txs:
+            rc, r = app.ante(tx)
+            out.append((rc, r["code"], r["log"]) if rc == 0 else (rc,))
+        results.append((out, app.cache_size()))
+        app.close()
+    assert results[0] == results[1]
+    assert results[0][0] == results[2][0]
+    codes = [o[1] for o in results[0][0] if len(o) > 1]
+    assert codes.count(0) == 398 and codes.count(4) == 2

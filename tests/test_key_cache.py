@@ -8,7 +8,7 @@ import pytest
 import gpuverify as gvm
 from golden_io import load_digest_vectors, load_msg_vectors
 from oracle import oracle as O
-from test_gpu_parity import make_random_batch
+from test_gpu_parity import PATHS, make_random_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -18,6 +18,15 @@ def ver():
     v = gvm.Verifier([0])
     yield v
     v.close()
+
+
+@pytest.fixture(params=sorted(PATHS))
+def path(request, ver):
+    """Keyed batches take the fused small-batch kernel up to lat_max, the
+    throughput pipeline above it: both schedules are checked."""
+    ver.set_option("lat_max", PATHS[request.param])
+    yield request.param
+    ver.set_option("lat_max", 4096)
 
 
 def keyed_inputs(ver, pub):
@@ -30,7 +39,7 @@ def keyed_inputs(ver, pub):
     return slots[rank[inv.reshape(-1)]]
 
 
-def test_golden_vectors_keyed(ver):
+def test_golden_vectors_keyed(ver, path):
     ver.keys_reset()
     pub, sig, dig, ok, cats = load_digest_vectors()
     got = ver.verify_batch_digests_keyed(keyed_inputs(ver, pub), sig, dig)
@@ -42,7 +51,7 @@ def test_golden_vectors_keyed(ver):
     assert not bad, bad[:20]
 
 
-def test_adversarial_keyed_equals_oracle_and_pub_path(ver):
+def test_adversarial_keyed_equals_oracle_and_pub_path(ver, path):
     ver.keys_reset()
     pub, sig, dig = make_random_batch(20000, seed=0xCA, adversarial=0.25, nkeys=301)
     want = O.verify_digests(pub, sig, dig, threads=16)
@@ -53,7 +62,7 @@ def test_adversarial_keyed_equals_oracle_and_pub_path(ver):
 
 
 @pytest.mark.parametrize("n", [1, 17, 255, 256, 257, 3000])
-def test_ragged_keyed_and_unloaded_slots(ver, n):
+def test_ragged_keyed_and_unloaded_slots(ver, n, path):
     ver.keys_reset()
     pub, sig, dig = make_random_batch(n, seed=1000 + n, adversarial=0.3, nkeys=5)
     want = O.verify_digests(pub, sig, dig, threads=8)

@@ -1,5 +1,8 @@
 """Secondary measurements reported inside bench.py's JSON line (rank 0, N=1).
 
+  c2_key_cache    the C2 batch verified by account-key slot (gv_keys_load once,
+                  then gv_dev_verify_digests_keyed): SURVEY.md §8f-2.
+  c2_unique_keys  the C2 variant with one distinct key per item.
   c3_adversarial  BASELINE.json configs[2]: 1M signatures, 25 % invalid (high-S,
                   r >= n, s = 0 / 2^256-1, random x, malformed prefix, wrong
                   message), device-resident, bitmap checked against the verdicts
@@ -12,6 +15,8 @@
                   block path (PreVerifyTxs: one GPU batch, then the decorators
                   with verdict-cache hits) and the per-tx CheckTx path (one GPU
                   call per tx), host buffers / PCIe included.
+  c4_multisig     BASELINE.json configs[3] shape on one GPU: k-of-n multisig
+                  MsgSend txs replayed in blocks through PreVerifyTxs + ante.
 
 Nothing here touches oracle/: verdicts come from construction (the workload
 signs valid items with OpenSSL and mutates the invalid ones).
@@ -48,6 +53,25 @@ def _timed_device_runs(ver, run, steps: int, warmup: int = 1):
     cnt, unpack_ms, prep_ms, ecmult_ms = ver.stage_stats()
     ver.set_option("time_kernels", 0)
     return el, {"unpack_or_sha_ms": round(unpack_ms, 3), "prep_ms": round(prep_ms, 3), "ecmult_ms": round(ecmult_ms, 3)}
+
+
+def c2_unique_keys(ver, make_workload, n: int, threads: int, steps: int = 3):
+    """SURVEY.md §8d C2 variant: one distinct key per item (no key reuse at
+    all), device-resident, bitmap checked against construction."""
+    pub, sig, dig, exp = make_workload(n, 0xC2 ^ 0x5A5A, n, 0.0, threads)
+    d = [ver.dev_alloc(a.nbytes) for a in (pub, sig, dig)]
+    for p, a in zip(d, (pub, sig, dig)):
+        ver.dev_upload(p, a)
+    nw = (n + 63) // 64
+    d_bits = ver.dev_alloc(nw * 8)
+    el, stages = _timed_device_runs(ver, lambda: ver.dev_verify_digests(0, n, d[0], d[1], d[2], d_bits), steps)
+    bits = np.zeros(nw, np.uint64)
+    ver.dev_download(bits, d_bits)
+    got = _unpack_bits(bits, n)
+    for p in d + [d_bits]:
+        ver.dev_free(p)
+    return {"items": n, "keys": n, "value": round(n * steps / el, 1), "unit": "verifies/s",
+            "mismatches": int(np.count_nonzero(got != exp)), "stages": stages}
 
 
 def c3_adversarial(ver, make_workload, n: int, threads: int, steps: int = 3):

@@ -22,7 +22,8 @@ def load(d, name):
         return {}
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(p)):
-        k = r["Kernel_Name"].split("(")[0].replace("gv::", "")
+        # "void gv::k_ecmult<false>(...)" -> "k_ecmult" (the bench runs one instance of each)
+        k = r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "").replace("gv::", "").strip()
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in agg.items()}
 
