@@ -29,6 +29,7 @@
 #include "secp_group.cuh"
 #include "secp_group29.cuh"
 #include "secp_sc29.cuh"
+#include "secp_modinv.cuh"
 #include "secp_sha256.cuh"
 #include "gv_kernels.h"
 
@@ -758,6 +759,8 @@ __global__ void k_debug(int op, u32 n, const u32* in, u32* out) {
               sc29 x, xm, im, o1, pl;
               sc29_from_words(x, a.v); sc29_to_mont(xm, x); sc29_batch_inv_wave(im, xm);
               sc29_from_words(o1, one); sc29_mul(pl, im, o1); sc29_to_words(r.v, pl); break; }
+    case 27: { // a^-1 mod n by divsteps (secp_modinv.cuh; the latency kernel's s^-1)
+              s30_modinv(r.v, a.v, [](bool done) { return __all(done) != 0; }); break; }
     case 26: { // radix-2^29 Montgomery product a * b * 2^-261 mod n, canonical
               sc29 x, y, z; sc29_from_words(x, a.v); sc29_from_words(y, b.v); sc29_mul(z, x, y);
               sc29_to_words(r.v, z); break; }

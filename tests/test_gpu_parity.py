@@ -149,6 +149,16 @@ def test_scalar29_montmul(ver):
         assert from_words(o) == a * b * Rinv % N
 
 
+def test_scalar_inverse_divsteps(ver):
+    """op 27: s^-1 mod n by divsteps (the latency kernel's inverse) == pow(s, -1, n)."""
+    rng = random.Random(27)
+    xs = [1, 2, N - 1, N - 2, (N - 1) // 2, 2**255, 2**128 + 1] + [rng.randrange(1, N) for _ in range(4000)]
+    ws = np.array([to_words(x, 0) for x in xs], dtype=np.uint32)
+    out = ver.debug_op(27, ws)
+    for i, x in enumerate(xs):
+        assert from_words(out[i]) == pow(x, -1, N), hex(x)
+
+
 def test_glv_split(ver):
     rng = random.Random(17)
     ks = [0, 1, 2, N - 1, N - 2, N // 2, R.LAMBDA, 2**128, 2**128 - 1] + [rng.randrange(N) for _ in range(4000)]
