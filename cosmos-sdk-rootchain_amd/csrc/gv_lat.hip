@@ -43,6 +43,11 @@ namespace gv {
 #ifndef GV_LAT_TRACE
 #define GV_LAT_TRACE 0
 #endif
+// GV_LAT_SPLITBP: the table's Z back-propagation spread over the signature's
+// four lanes (suffix products once, entry scaling in lockstep).
+#ifndef GV_LAT_SPLITBP
+#define GV_LAT_SPLITBP 1
+#endif
 // GV_LAT_DIVSTEPS: s^-1 by divsteps (secp_modinv.cuh) instead of the Fermat chain.
 #ifndef GV_LAT_DIVSTEPS
 #define GV_LAT_DIVSTEPS 1
@@ -116,6 +121,7 @@ GV_DEV void lat_pubkey_and_tables(LatShared& sh, int sig, int slot, bool live, c
   }
   if ((y8.v[0] & 1u) != (pre & 1u)) fe_neg(y8, y8);
   fe_normalize(y8);
+  LAT_STAMP(7);
   if (!ok) {                                          // harmless stand-in point: G
     const u32 gx[8] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu,
                        0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu};
@@ -184,6 +190,52 @@ GV_DEV void lat_pubkey_and_tables(LatShared& sh, int sig, int slot, bool live, c
     for (int i = 0; i < 8; ++i) w[i] = kLBeta[i];
     f29_from_words(beta, w);
   }
+#if GV_LAT_SPLITBP
+  // (1) the suffix products acc_m = prod_{k=m..15} ratio_k, m = 15..2, on every
+  // lane alike; slot 0 overwrites its ratio scratch with them (read back by the
+  // other lanes of the signature: same wave, program order).
+  {
+    u32 (*qr0)[9] = sh.ratio[sig * 4];
+#pragma unroll 1
+    for (int m = GV_QTAB_N - 1; m >= 2; --m) {
+      fe29 ratio;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) ratio.n[i] = qr[m - 2][i];     // Z_m / Z_(m-1)
+      if (m == GV_QTAB_N - 1) acc = ratio;
+      else f29_mul(acc, acc, ratio);
+      if (st) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) qr0[m - 2][i] = acc.n[i];
+      }
+    }
+    // (2) lane 4s + k scales entries k, k+4, k+8, k+12 in lockstep: entry e
+    // (on Z_max(e,1)) times acc_(e+1)^2, acc_(e+1)^3 (entry 0 uses acc_2, the
+    // last entry is already on Z_15), and writes its lambda*Q entry.
+#pragma unroll 1
+    for (int j = 0; j < GV_QTAB_N / 4; ++j) {
+      const int e = 4 * j + slot;
+      fe29 x, y, a, a2, a3;
+      lds_get_ent(x, y, qt[e]);
+      if (e == GV_QTAB_N - 1) f29_set_u32(a, 1);
+      else if (e == 0) a = acc;
+      else {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) a.n[i] = qr0[e - 1][i];    // acc_(e+1)
+      }
+      f29_sqr(a2, a);
+      {
+        fe29 o[2];
+        const fe29 xa[2] = {a2, x}, ya[2] = {a, a2};
+        f29_multi<false, false>(o, xa, ya);
+        a3 = o[0]; x = o[1];
+      }
+      f29_mul(y, y, a3);
+      f29_mul(t, x, beta);
+      lds_put_ent(qt[e], x, y);
+      lds_put_ent(lt[e], t, y);
+    }
+  }
+#else
   for (int m = GV_QTAB_N; m >= 1; --m) {
     fe29 x, y;
     lds_get_ent(x, y, qt[m - 1]);
@@ -205,6 +257,7 @@ GV_DEV void lat_pubkey_and_tables(LatShared& sh, int sig, int slot, bool live, c
     f29_mul(t, x, beta);
     if (st) lds_put_ent(lt[m - 1], t, y);
   }
+#endif
   f29_add(t, qy, qy);
   f29_mul(t, t, acc);                                 // Z_15 = 2y * prod(ratios)
   if (st) {
