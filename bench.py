@@ -36,13 +36,25 @@ sys.path.insert(0, REPO)
 
 import gpuverify as gvm  # noqa: E402
 
-# Algorithmic work: 32x32->64-bit multiply products per verify.
-W_MUL = 1.2e5                 # whole verify (decompression + scalar stage + ecmult)
-W_PREP = 255 * 44 + 14 * 72 + 10 * 136 + 1700   # decompression 255S+14M, ~10 mod-n mults, GLV split
-W_ECMULT = W_MUL - W_PREP     # the k_ecmult share (~1.04e5)
-# Peak: measured v_mad_u64_u32 issue rate on MI355X (tools/microbench/alu_rate.hip,
-# profiles/alu_rate_r01.json): lane-products per second, whole chip.
-P_MUL = 3.3885e13
+# Algorithmic work per verify, in 32x32->64-bit multiply
+# products (field mul = 64 + 8 = 72, field square = 36 + 8 = 44, mod-n
+# Montgomery product = 136), attributed to the kernel that does it:
+FM, FS, NM = 72, 44, 136
+W_DECOMP = 255 * FS + 14 * FM              # sqrt chain (btcec decompressPoint)      12,228
+W_QTAB = 107 * FM + 44 * FS                # Q table: 1 dbl + 7 adds + affine conv.   9,640
+W_LADDER = 129 * (2 * FM + 5 * FS) + 72 * (7 * FM + 4 * FS) + (2 * FM + FS)   # dbl + adds + final 96,104
+W_INV = 4 * NM                             # s^-1 by batch inversion (~3 products/item + the shared chain)
+W_SCALAR = 6 * NM + 1700                   # u1, u2, Montgomery conversions, GLV split
+W_KERNEL = {"k_scalar_inv": W_INV,
+            "k_prep": W_DECOMP + W_QTAB + W_SCALAR,
+            "k_ecmult": W_LADDER}
+W_MUL = sum(W_KERNEL.values())             # 121,032 ~ the survey's 1.2e5
+# Peak: the highest v_mad_u64_u32 issue rate measured on MI355X
+# (tools/microbench/alu_rate.hip; profiles/r01/alu_rate_v3.jsonl, dependent
+# chains at 8 waves/SIMD), lane-products per second, whole chip.  bench.py
+# also re-measures it live and uses the larger of the two.
+P_MUL_COMMITTED = 3.7469e13
+ALU_BENCH = os.path.join(REPO, "tools", "microbench", "alu_rate")
 
 WORKLOAD_SO = os.path.join(REPO, "tools", "workload", "libgvwork.so")
 
@@ -115,7 +127,12 @@ def cpu_baseline(pub, sig, dig, threads: int, ver=None):
     from oracle import oracle as O
     O.lib()
     s1 = 4096
-    s2 = min(len(pub), 6144 * threads)
+    # all-core sample sized for ~6 s from a short calibration run
+    cal = min(len(pub), 512 * threads)
+    t = time.perf_counter()
+    O.verify_digests(pub[:cal], sig[:cal], dig[:cal], threads=threads)
+    est = cal / (time.perf_counter() - t)
+    s2 = int(min(len(pub), max(cal, est * 6)))
     c2 = {
         "port_serial": _rate(lambda: O.verify_digests(pub[:s1], sig[:s1], dig[:s1], threads=1), s1),
         "port_allcore": _rate(lambda: O.verify_digests(pub[:s2], sig[:s2], dig[:s2], threads=threads), s2),
@@ -142,10 +159,47 @@ def cpu_baseline(pub, sig, dig, threads: int, ver=None):
         c1["gpu_hostpath"] = round(n1 / (time.perf_counter() - t), 1)
         c1["gpu_mismatches"] = int(np.count_nonzero(got != cexp))
     return {"value": c2["port_allcore"], "unit": "verifies/s", "cores": threads, "kind": "port",
-            "sample": f"first {s2} items of the same C2 batch, {threads} threads (oracle/secp256k1_oracle.c); "
-                      f"serial 1-thread on the first {s1}; OpenSSL and the C1 message set beside it "
-                      f"(SURVEY.md §8d lines ii and iii)",
+            "host": host_cores(),
+            "sample": f"first {s2} items of the same C2 batch, {threads} threads = every CPU this process may run on "
+                      f"(affinity mask, capped by the cgroup quota; see host) (oracle/secp256k1_oracle.c: a clarity-first 4x64-limb port of the reference "
+                      f"algorithm, no GLV); serial 1-thread on the first {s1}; OpenSSL and the C1 message set "
+                      f"beside it (SURVEY.md §8d lines ii and iii)",
             "serial_value": c2["port_serial"], "c2": c2, "c1": c1}
+
+
+def live_mad_peak():
+    """Max v_mad_u64_u32 lane-products/s measured now by tools/microbench/alu_rate (None if unavailable)."""
+    import subprocess
+    if not os.path.exists(ALU_BENCH):
+        return None
+    try:
+        out = subprocess.run([ALU_BENCH], capture_output=True, text=True, timeout=120).stdout
+    except (OSError, subprocess.SubprocessError):
+        return None
+    best = None
+    for line in out.splitlines():
+        try:
+            d = json.loads(line)
+        except ValueError:
+            continue
+        if str(d.get("inst", "")).startswith("v_mad_u64_u32"):
+            best = max(best or 0.0, float(d["lane_ops_per_s"]))
+    return best
+
+
+def host_cores():
+    """CPU counts of this host: os.cpu_count(), the affinity mask, and the cgroup
+    CPU quota (cpu.max) when one is set."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    eff = aff if quota is None else max(1, min(aff, int(quota + 0.999)))
+    return {"cpu_count": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota, "effective": eff}
 
 
 def _pct(ts):
@@ -229,7 +283,9 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
     ap.add_argument("--items", "--n", dest="n", type=int, default=1_000_000, help="signatures per rank")
     ap.add_argument("--adversarial", type=float, default=0.0, help="C3: fraction of invalid signatures")
     ap.add_argument("--keys", type=int, default=65536)
-    ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--threads", type=int, default=host_cores()["effective"] or 1,
+                    help="CPU baseline / workload threads (default: every CPU this process may run on: the "
+                         "affinity mask, capped by the cgroup CPU quota when one is set)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the C3 / message-path / C1 / C4 lines")
@@ -285,8 +341,30 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
     got = unpack_bits(bits, n)
     mismatches = int(np.count_nonzero(got != exp))
 
+    # parity on an adversarial copy of the same batch (a kernel that accepted
+    # everything would pass the all-valid check above): 1/8 of the items get a
+    # malformed pubkey prefix (ParsePubKey rejects), 1/8 a flipped digest bit
+    # (ECDSA rejects); expected verdicts by construction
+    rng = np.random.default_rng(0xADF + rank)
+    sel = rng.random(n)
+    bad_pfx, bad_dig = sel < 0.125, (sel >= 0.125) & (sel < 0.25)
+    apub, adig = pub.copy(), dig.copy()
+    apub[bad_pfx, 0] = 0x05
+    adig[bad_dig, 31] ^= 1
+    aexp = exp & ~(bad_pfx | bad_dig)
+    ver.dev_upload(d_pub, apub)
+    ver.dev_upload(d_dig, adig)
+    step()
+    ver.dev_sync()
+    ver.dev_download(bits, d_bits)
+    adv_mismatches = int(np.count_nonzero(unpack_bits(bits, n) != aexp))
+    adv_rejected = int(n - aexp.sum())
+    ver.dev_upload(d_pub, pub)
+    ver.dev_upload(d_dig, dig)
+    del apub, adig
+
     ver.set_option("time_kernels", 1)
-    ver.stage_stats()                     # reset the event ring
+    ver.stage_stats4()                    # reset the event ring
     barrier()
     ver.dev_sync()
     t_start = time.perf_counter()
@@ -295,15 +373,24 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
     ver.dev_sync()
     barrier()
     elapsed = time.perf_counter() - t_start
-    cnt, unpack_ms, prep_ms, ecmult_ms = ver.stage_stats()
+    cnt, (unpack_ms, inv_ms, prep_ms, ecmult_ms) = ver.stage_stats4()
     ver.set_option("time_kernels", 0)
     elapsed_max = allmax(elapsed)
     total_mismatch = int(allmax(float(mismatches)))
+    total_adv_mismatch = int(allmax(float(adv_mismatches)))
 
     value = world * n * args.steps / elapsed_max
     ms_per_step = elapsed_max / args.steps * 1e3
 
-    achieved = n * W_ECMULT / (ecmult_ms * 1e-3) if ecmult_ms > 0 else 0.0
+    peak_live = live_mad_peak() if rank == 0 else None
+    P_MUL = max(P_MUL_COMMITTED, peak_live or 0.0)
+    kms = {"k_scalar_inv": inv_ms, "k_prep": prep_ms, "k_ecmult": ecmult_ms}
+    kernels = {}
+    for k, ms in kms.items():
+        a = n * W_KERNEL[k] / (ms * 1e-3) if ms > 0 else 0.0
+        kernels[k] = {"ms": round(ms, 4), "work_per_verify": W_KERNEL[k], "achieved_T": round(a / 1e12, 3),
+                      "frac": round(a / P_MUL, 4) if a else None}
+    achieved = n * W_KERNEL["k_ecmult"] / (ecmult_ms * 1e-3) if ecmult_ms > 0 else 0.0
     pmc = load_pmc("k_ecmult")
     traffic = round(pmc["hbm_bytes_per_item"] * n) if pmc else None
     result = {
@@ -336,17 +423,25 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
             "hbm_gbps_at_traffic": round(traffic / (ecmult_ms * 1e-3) / 1e9, 1) if (pmc and ecmult_ms > 0) else None,
             "valu_insts_per_verify": round(pmc["valu_insts_per_item"]) if pmc else None,
             "valu_busy_frac": round(pmc["valu_busy_frac"], 3) if pmc else None,
-            "work_per_verify": W_ECMULT,
-            "kernel_ms": round(ecmult_ms, 3),
+            "work_per_verify": W_KERNEL["k_ecmult"],
+            "kernel_ms": round(ecmult_ms, 4),
             "launches_averaged": cnt,
-            "note": "achieved = items x W_ecmult products / avg k_ecmult duration (HIP events on the launch "
-                    "stream); peak = measured v_mad_u64_u32 chip rate; traffic / VALU counters from the committed "
-                    "rocprofv3 --pmc passes of this bench command (tools/pmc_round.sh)",
+            "peak_committed": round(P_MUL_COMMITTED / 1e12, 3),
+            "peak_live": round(peak_live / 1e12, 3) if peak_live else None,
+            "kernels": kernels,
+            "note": "achieved = items x W (32x32 products per verify, SURVEY §8d, attributed per kernel: the Q-table "
+                    "build belongs to k_prep) / avg kernel duration (HIP events on the launch stream); peak = the "
+                    "max of the committed and live-measured v_mad_u64_u32 chip rates; traffic / VALU counters from "
+                    "the committed rocprofv3 --pmc passes of this bench command (tools/pmc_round.sh)",
         },
-        "pipeline": {"unpack_ms": round(unpack_ms, 3), "prep_ms": round(prep_ms, 3), "ecmult_ms": round(ecmult_ms, 3),
+        "pipeline": {"unpack_ms": round(unpack_ms, 3), "scalar_inv_ms": round(inv_ms, 3),
+                     "prep_ms": round(prep_ms, 3), "ecmult_ms": round(ecmult_ms, 3),
                      "whole_verify_roofline_frac": round(value / world * W_MUL / P_MUL, 4)},
         "parity": {"checked": n * world, "mismatches": total_mismatch,
-                   "reference": "verdicts known by construction (valid signatures; mutated ones invalid)"},
+                   "adversarial_checked": n * world, "adversarial_rejects_expected": adv_rejected * world,
+                   "adversarial_mismatches": total_adv_mismatch,
+                   "reference": "verdicts known by construction: the timed batch (valid signatures) and an "
+                                "adversarial copy (1/8 malformed prefix, 1/8 flipped digest bit -> rejected)"},
     }
 
     if rank == 0 and world == 1 and not args.no_latency:

@@ -40,7 +40,7 @@ typedef struct gvk_batch {
   uint32_t *digits;             // GV_DIGIT_ROWS rows: packed Booth digits per window (16 rows reused as scratch)
   uint32_t *zq, *flags, *qtab;  // shared Z of the Q table (8 rows), flags, Q table (192 rows)
   uint64_t* bits;               // C/64 words, bit (i%64) of word i/64
-  hipEvent_t ev[3];             // optional: after unpack/sha, after prep, after ecmult
+  hipEvent_t ev[4];             // optional: after unpack/sha, after scalar_inv, after prep, after ecmult
   // keyed batch (kslot != NULL, pub33 unused): item i's key is arena slot kslot[i]
   const uint32_t* kslot;        // n slots (device)
   const uint32_t* kqt;          // arena Q tables, row per slot (GV_QTAB_N x GV_QENT_WORDS words)
@@ -89,6 +89,8 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st);
 hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
                           uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t base,
                           uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, hipStream_t st);
+hipError_t gvk_keys_point(uint32_t n, const uint32_t* slots, const uint32_t* kqt, const uint32_t* kzq, uint32_t kC,
+                          const uint32_t* kok, uint32_t kcount, uint8_t* out_xy, uint8_t* out_ok, hipStream_t st);
 hipError_t gvk_debug(int op, uint32_t n, const uint32_t* in, uint32_t* out, hipStream_t st);
 
 #ifdef __cplusplus

@@ -588,6 +588,41 @@ __global__ __launch_bounds__(256) void k_keys_build(u32 n, u32 C, const u32* in_
   kok[base + g] = ok ? 1u : 0u;
 }
 
+// ------------------------------------------------------------ k_keys_point
+// Key-arena readback (gv_keys_point): the affine point 1*Q of slot slots[g]
+// from its table entry and shared Z (x = X / Z^2, y = Y / Z^3), as 64 bytes
+// x || y big-endian, and the slot's ParsePubKey verdict.
+__global__ __launch_bounds__(256) void k_keys_point(u32 n, const u32* slots, const u32* kqt, const u32* kzq,
+                                                     u32 kC, const u32* kok, u32 kcount, uint8_t* out_xy,
+                                                     uint8_t* out_ok) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  const u32 sl = slots[g];
+  uint8_t* o = out_xy + (size_t)g * 64;
+  if (sl >= kcount) {
+    for (int i = 0; i < 64; ++i) o[i] = 0;
+    out_ok[g] = 0;
+    return;
+  }
+  fe29 x, y, z, zi, z2, z3;
+  load_qent29(x, y, kqt, sl, 0);
+  load_f29(z, kzq, kC, sl);
+  f29_inv(zi, z);
+  f29_sqr(z2, zi);
+  f29_mul(z3, z2, zi);
+  f29_mul(x, x, z2);
+  f29_mul(y, y, z3);
+  u32 wx[8], wy[8];
+  f29_to_words(wx, x);
+  f29_to_words(wy, y);
+  for (int i = 0; i < 8; ++i)
+    for (int b = 0; b < 4; ++b) {
+      o[4 * (7 - i) + b] = (uint8_t)(wx[i] >> (24 - 8 * b));
+      o[32 + 4 * (7 - i) + b] = (uint8_t)(wy[i] >> (24 - 8 * b));
+    }
+  out_ok[g] = kok[sl] ? 1 : 0;
+}
+
 // ------------------------------------------------------------------ k_ecmult
 // acc <- acc + (x, y) where (x, y) is affine on the accumulator's curve
 // (zinv == nullptr: Q-table entry) or an affine point of the real curve to be
@@ -844,6 +879,7 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
     uint32_t* w = b->digits;                   // rows 0..8
     uint32_t* pre = b->digits + (size_t)9 * C; // rows 9..17
     hipLaunchKernelGGL(gv::k_scalar_inv, dim3((waves + 3) / 4), blk, 0, st, C, b->in_s, w, pre);
+    if (b->ev[1]) (void)hipEventRecord(b->ev[1], st);
     if (b->kslot)   // keyed: in_pfx doubles as the clamped-slot row for k_ecmult
       hipLaunchKernelGGL(gv::k_prep<true>, grd, blk, 0, st, C, b->n, (const uint32_t*)nullptr,
                          (const uint32_t*)nullptr, b->in_r, b->in_s, b->in_e, (const uint32_t*)w, b->digits,
@@ -853,7 +889,7 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
                          b->in_e, (const uint32_t*)w, b->digits, b->qtab, b->zq, b->flags,
                          (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr);
   }
-  if (b->ev[1]) (void)hipEventRecord(b->ev[1], st);
+  if (b->ev[2]) (void)hipEventRecord(b->ev[2], st);
   if (b->kslot)
     hipLaunchKernelGGL(gv::k_ecmult<true>, grd, blk, 0, st, b->gtab, b->n, C, b->digits, b->kqt, b->kzq,
                        b->flags, b->in_r, b->bits, (const uint32_t*)b->in_pfx, b->kC);
@@ -861,7 +897,7 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
     hipLaunchKernelGGL(gv::k_ecmult<false>, grd, blk, 0, st, b->gtab, b->n, C, b->digits,
                        (const uint32_t*)b->qtab, (const uint32_t*)b->zq, b->flags, b->in_r, b->bits,
                        (const uint32_t*)nullptr, 0u);
-  if (b->ev[2]) (void)hipEventRecord(b->ev[2], st);
+  if (b->ev[3]) (void)hipEventRecord(b->ev[3], st);
   return hipGetLastError();
 }
 
@@ -873,6 +909,13 @@ hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t
                      in_x, in_pfx, in_r, in_s, in_e);
   hipLaunchKernelGGL(gv::k_keys_build, grd, blk, 0, st, n, C, (const uint32_t*)in_x, (const uint32_t*)in_pfx, base,
                      kqt, kzq, kC, kok, qr);
+  return hipGetLastError();
+}
+
+hipError_t gvk_keys_point(uint32_t n, const uint32_t* slots, const uint32_t* kqt, const uint32_t* kzq, uint32_t kC,
+                          const uint32_t* kok, uint32_t kcount, uint8_t* out_xy, uint8_t* out_ok, hipStream_t st) {
+  hipLaunchKernelGGL(gv::k_keys_point, dim3((n + 255) / 256), dim3(256), 0, st, n, slots, kqt, kzq, kC, kok, kcount,
+                     out_xy, out_ok);
   return hipGetLastError();
 }
 

@@ -33,6 +33,9 @@
 #include "gv_kernels.h"
 
 static_assert(F29_NCH == 2, "gv_lat.hip is built with -DF29_NCH=2");
+#if defined(__HIP_DEVICE_COMPILE__) && defined(__AMDGCN_WAVEFRONT_SIZE) && __AMDGCN_WAVEFRONT_SIZE != 64
+#error "gv_lat.hip passes table entries between lanes of one wave64"
+#endif
 
 namespace gv {
 
@@ -74,6 +77,16 @@ struct LatShared {
   u32 okp[GV_LAT_SIGS];                     // pubkey checks passed (wave 0)
   u32 oks[GV_LAT_SIGS];                     // bit 0: scalar checks passed, bit 1: r < p - n (wave 1)
 };
+
+// The lanes of one signature hand table entries to each other through LDS
+// inside one wave64.  The hardware executes a wave's LDS operations in order;
+// the fence + wave barrier make that ordering part of the program (no compiler
+// reordering of the LDS stores and loads across this point).
+GV_DEV void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 GV_DEV u32 be32(const uint8_t* p) {
   return ((u32)p[0] << 24) | ((u32)p[1] << 16) | ((u32)p[2] << 8) | (u32)p[3];
@@ -178,6 +191,7 @@ GV_DEV void lat_pubkey_and_tables(LatShared& sh, int sig, int slot, bool live, c
     Y1 = a1;
     if (st) lds_put_ent(qt[m], X2, Y2);
   }
+  wave_lds_sync();                                    // slot 0's entries -> the other lanes
   // Back-propagation: entry m-1 scaled to the last entry's Z (as in
   // build_q_table: entry index j lives on Z_max(j,1), ratio[k] = Z_(k+2) /
   // Z_(k+1)).  Every lane reads the entries its signature's slot-0 lane stored
@@ -208,6 +222,7 @@ GV_DEV void lat_pubkey_and_tables(LatShared& sh, int sig, int slot, bool live, c
         for (int i = 0; i < 9; ++i) qr0[m - 2][i] = acc.n[i];
       }
     }
+    wave_lds_sync();                                  // slot 0's suffix products -> the other lanes
     // (2) lane 4s + k scales entries k, k+4, k+8, k+12 in lockstep: entry e
     // (on Z_max(e,1)) times acc_(e+1)^2, acc_(e+1)^3 (entry 0 uses acc_2, the
     // last entry is already on Z_15), and writes its lambda*Q entry.

@@ -1,16 +1,27 @@
 // gv_runtime.cpp -- the C-ABI runtime of libgpuverify.so (include/gpuverify.h).
 //
-// Owns per-device state (stream, LDS-source G table, scratch buffers sized for
-// the largest batch seen), splits host batches across the context's devices
-// (contiguous slices, one host thread per device, no collective -- SURVEY.md
-// §8e), streams each slice through the HIP pipeline in max_batch chunks and
-// gathers the accept bitmaps.  Fail-closed: any HIP error returns GV_EHIP and
-// the caller re-verifies on the CPU.
+// Per device: two pipeline "sets" (device scratch for one batch chunk, a HIP
+// stream, pinned host staging), a persistent worker thread and a small pool of
+// staging threads.  A host batch is split into contiguous slices, one per
+// device (no collective -- SURVEY.md §8e); each slice is cut into chunks that
+// alternate between the two sets, so the staging memcpy + H2D copy of chunk
+// c+1 overlaps the kernels of chunk c (§8e "one host thread + 2 HIP streams
+// per GPU, double-buffered pinned staging").  Only the packed accept bitmap
+// comes back.  Fail-closed: any HIP error returns GV_EHIP and the caller
+// re-verifies on the CPU.
+//
+// Ordering: every use of a set's device scratch, on whichever stream, first
+// waits for the previous use of that set (its `last` event) and then records
+// `last` again -- so a gv_dev_* call on a caller stream and a later host-path
+// or gv_dev_* call on another stream can never overwrite the inputs of kernels
+// still in flight.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -26,77 +37,244 @@ namespace {
     if (e_ != hipSuccess) return GV_EHIP;         \
   } while (0)
 
+constexpr size_t kMaxItems = 0xFFFFFF00ull;       // per launch (u32 lane indices)
 constexpr size_t kLaneWords = 8 + 1 + 8 + 8 + 8 + GV_DIGIT_ROWS + 8 + 1 + GV_QTAB_WORDS;
-
-struct Dev {
-  int id = 0;
-  hipStream_t st = nullptr;
-  uint32_t* gtab = nullptr;
-  size_t cap = 0;               // lanes of scratch (multiple of 256)
-  uint8_t* scratch = nullptr;   // one allocation, carved below
-  uint8_t *d_pub = nullptr, *d_sig = nullptr, *d_dig = nullptr;
-  uint32_t *in_x, *in_pfx, *in_r, *in_s, *in_e, *digits, *zq, *flags, *qtab;
-  uint64_t* bits = nullptr;
-  uint8_t* d_blob = nullptr;
-  size_t blob_cap = 0;
-  uint64_t* d_off = nullptr;
-  uint32_t* d_len = nullptr;
-  size_t msg_cap = 0;
-  uint64_t* h_bits = nullptr;   // pinned
-  size_t h_bits_cap = 0;
-  uint32_t* d_slot = nullptr;   // keyed host batches: slot column (part of scratch)
-  // key arena (gv_keys_load): Q table rows, table Z (8 rows of stride kcap), verdicts
-  uint32_t *kqt = nullptr, *kzq = nullptr, *kok = nullptr;
-  size_t kcap = 0;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  // ring of per-launch stage events for gv_stage_stats
-  static constexpr int kRing = 256;
-  hipEvent_t ring[kRing][4] = {};
-  int ring_next = 0, ring_count = 0, last = -1;
-  std::mutex mu;
-};
 
 size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 
-int ensure_cap(Dev* d, size_t C) {
-  if (C <= d->cap) return GV_OK;
-  if (d->scratch) { (void)hipFree(d->scratch); d->scratch = nullptr; d->cap = 0; }
-  const size_t bytes = C * (33 + 64 + 32) + C * kLaneWords * 4 + (C / 64) * 8 + C * 4 + 4096;
-  if (hipMalloc(&d->scratch, bytes) != hipSuccess) return GV_ENOMEM;
-  uint8_t* p = d->scratch;
+// ------------------------------------------------------------ thread helpers
+// Runs fn(part) for part in [0, parts): part 0 on the caller, the rest on the
+// pool's persistent threads.
+class Pool {
+ public:
+  explicit Pool(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this, i] { loop(i + 1); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      quit_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return (int)th_.size() + 1; }
+  void run(int parts, const std::function<void(int)>& fn) {
+    parts = std::max(1, std::min(parts, size()));
+    if (parts == 1) { fn(0); return; }
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      fn_ = &fn;
+      parts_ = parts;
+      pending_ = parts - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0);
+    std::unique_lock<std::mutex> lk(m_);
+    done_cv_.wait(lk, [this] { return pending_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* fn;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+        if (quit_) return;
+        seen = gen_;
+        if (id >= parts_) continue;
+        fn = fn_;
+      }
+      (*fn)(id);
+      std::lock_guard<std::mutex> lk(m_);
+      if (--pending_ == 0) done_cv_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int parts_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool quit_ = false;
+};
+
+// memcpy split over the pool (large copies only: one core streams ~10 GB/s)
+void par_copy(Pool* pool, void* dst, const void* src, size_t bytes) {
+  constexpr size_t kMin = size_t(4) << 20;
+  if (!pool || bytes < kMin) { if (bytes) memcpy(dst, src, bytes); return; }
+  const int parts = (int)std::min<size_t>(pool->size(), bytes / (kMin / 2));
+  const size_t per = round_up((bytes + parts - 1) / parts, 4096);
+  pool->run(parts, [&](int p) {
+    const size_t lo = std::min(bytes, p * per), hi = std::min(bytes, lo + per);
+    if (hi > lo) memcpy((uint8_t*)dst + lo, (const uint8_t*)src + lo, hi - lo);
+  });
+}
+
+// One persistent thread per extra device: runs the device's slice of a host batch.
+class Worker {
+ public:
+  Worker() : th_([this] { loop(); }) {}
+  ~Worker() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      quit_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void post(std::function<int()> job) {
+    std::lock_guard<std::mutex> lk(m_);
+    job_ = std::move(job);
+    has_ = true;
+    done_ = false;
+    cv_.notify_all();
+  }
+  int wait() {
+    std::unique_lock<std::mutex> lk(m_);
+    cv_.wait(lk, [this] { return done_; });
+    return rc_;
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<int()> job;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [this] { return quit_ || has_; });
+        if (quit_) return;
+        job = std::move(job_);
+        has_ = false;
+      }
+      const int rc = job();
+      std::lock_guard<std::mutex> lk(m_);
+      rc_ = rc;
+      done_ = true;
+      cv_.notify_all();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::function<int()> job_;
+  bool has_ = false, done_ = true, quit_ = false;
+  int rc_ = GV_OK;
+  std::thread th_;
+};
+
+// ------------------------------------------------------------ device state
+// Device scratch of one batch chunk of C lanes (C % 256 == 0): the staged
+// inputs (one contiguous region so a host chunk is ONE H2D copy), the SoA
+// working rows of the kernels, the accept bitmap.
+struct Set {
+  size_t cap = 0;
+  uint8_t* scratch = nullptr;
+  uint8_t* d_in = nullptr;                        // staged inputs, layout of in_layout()
+  uint32_t *in_x = nullptr, *in_pfx = nullptr, *in_r = nullptr, *in_s = nullptr, *in_e = nullptr;
+  uint32_t *digits = nullptr, *zq = nullptr, *flags = nullptr, *qtab = nullptr;
+  uint64_t* bits = nullptr;
+  uint8_t* d_blob = nullptr;                      // message path blob
+  size_t blob_cap = 0;
+  hipStream_t st = nullptr;                       // the set's own stream (host path)
+  hipEvent_t last = nullptr;                      // end of the last work using this set
+  hipStream_t last_st = nullptr;
+  hipEvent_t done = nullptr;                      // host path: chunk finished (bits on host)
+  // pinned host staging
+  uint8_t* h_in = nullptr;
+  size_t h_in_cap = 0;
+  uint8_t* h_blob = nullptr;
+  size_t h_blob_cap = 0;
+  uint64_t* h_bits = nullptr;
+  size_t h_bits_cap = 0;
+  // chunk waiting to be harvested
+  bool busy = false;
+  size_t c0 = 0, cn = 0;
+};
+
+// Input region layout of a chunk of C lanes: [pub33 (or u32 slot)] [sig64]
+// [dig32 | u64 off + u32 len], each part 256-byte aligned.
+struct InLayout {
+  size_t sig, third, len, total;
+};
+InLayout in_layout(size_t C, bool keyed, bool msgs) {
+  InLayout L;
+  L.sig = round_up(C * (keyed ? 4 : 33), 256);
+  L.third = L.sig + C * 64;
+  L.len = L.third + C * 8;                        // msgs only
+  L.total = msgs ? L.len + C * 4 : L.third + C * 32;
+  return L;
+}
+
+struct Dev {
+  int id = 0;
+  uint32_t* gtab = nullptr;
+  Set set[2];
+  // key arena (gv_keys_load): Q table rows, table Z (8 rows of stride kcap), verdicts
+  uint32_t *kqt = nullptr, *kzq = nullptr, *kok = nullptr;
+  size_t kcap = 0;
+  // ring of per-launch stage events for gv_stage_stats: start + 4 stage ends
+  static constexpr int kRing = 256;
+  hipEvent_t ring[kRing][5] = {};
+  int ring_next = 0, ring_count = 0, last = -1;
+  std::mutex mu;
+  Pool* pool = nullptr;                           // staging memcpy threads
+  Worker* worker = nullptr;                       // slice runner (devices 1..n-1 of a context)
+};
+
+int ensure_cap(Set* s, size_t C) {
+  if (C <= s->cap) return GV_OK;
+  if (s->scratch) { (void)hipFree(s->scratch); s->scratch = nullptr; s->cap = 0; }
+  const size_t in_bytes = in_layout(C, false, true).total + C * 32;
+  const size_t bytes = in_bytes + C * kLaneWords * 4 + (C / 64) * 8 + 16 * 256;
+  if (hipMalloc(&s->scratch, bytes) != hipSuccess) return GV_ENOMEM;
+  uint8_t* p = s->scratch;
   auto take = [&](size_t nbytes) { uint8_t* r = p; p += round_up(nbytes, 256); return r; };
-  d->d_pub = take(C * 33);
-  d->d_sig = take(C * 64);
-  d->d_dig = take(C * 32);
-  d->in_x = (uint32_t*)take(C * 8 * 4);
-  d->in_pfx = (uint32_t*)take(C * 4);
-  d->in_r = (uint32_t*)take(C * 8 * 4);
-  d->in_s = (uint32_t*)take(C * 8 * 4);
-  d->in_e = (uint32_t*)take(C * 8 * 4);
-  d->digits = (uint32_t*)take(C * GV_DIGIT_ROWS * 4);
-  d->zq = (uint32_t*)take(C * 8 * 4);
-  d->flags = (uint32_t*)take(C * 4);
-  d->qtab = (uint32_t*)take(C * GV_QTAB_WORDS * 4);
-  d->bits = (uint64_t*)take((C / 64) * 8);
-  d->d_slot = (uint32_t*)take(C * 4);
-  d->cap = C;
+  s->d_in = take(in_bytes);
+  s->in_x = (uint32_t*)take(C * 8 * 4);
+  s->in_pfx = (uint32_t*)take(C * 4);
+  s->in_r = (uint32_t*)take(C * 8 * 4);
+  s->in_s = (uint32_t*)take(C * 8 * 4);
+  s->in_e = (uint32_t*)take(C * 8 * 4);
+  s->digits = (uint32_t*)take(C * GV_DIGIT_ROWS * 4);
+  s->zq = (uint32_t*)take(C * 8 * 4);
+  s->flags = (uint32_t*)take(C * 4);
+  s->qtab = (uint32_t*)take(C * GV_QTAB_WORDS * 4);
+  s->bits = (uint64_t*)take((C / 64) * 8);
+  s->cap = C;
   return GV_OK;
 }
 
-int ensure_msg(Dev* d, size_t blob_bytes, size_t C) {
-  if (blob_bytes > d->blob_cap) {
-    if (d->d_blob) (void)hipFree(d->d_blob);
-    d->blob_cap = round_up(std::max<size_t>(blob_bytes, 1), 1 << 20);
-    if (hipMalloc(&d->d_blob, d->blob_cap) != hipSuccess) { d->blob_cap = 0; d->d_blob = nullptr; return GV_ENOMEM; }
-  }
-  if (C > d->msg_cap) {
-    if (d->d_off) (void)hipFree(d->d_off);
-    if (d->d_len) (void)hipFree(d->d_len);
-    d->d_off = nullptr; d->d_len = nullptr; d->msg_cap = 0;
-    if (hipMalloc(&d->d_off, C * 8) != hipSuccess) return GV_ENOMEM;
-    if (hipMalloc(&d->d_len, C * 4) != hipSuccess) return GV_ENOMEM;
-    d->msg_cap = C;
-  }
+int ensure_blob(Set* s, size_t bytes) {
+  if (bytes <= s->blob_cap) return GV_OK;
+  if (s->d_blob) (void)hipFree(s->d_blob);
+  s->blob_cap = round_up(std::max<size_t>(bytes, 1), 1 << 20);
+  if (hipMalloc(&s->d_blob, s->blob_cap) != hipSuccess) { s->blob_cap = 0; s->d_blob = nullptr; return GV_ENOMEM; }
+  return GV_OK;
+}
+
+int ensure_pinned(uint8_t** p, size_t* cap, size_t bytes) {
+  if (bytes <= *cap) return GV_OK;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  const size_t want = round_up(std::max<size_t>(bytes, 4096), 1 << 20);
+  if (hipHostMalloc((void**)p, want, hipHostMallocDefault) != hipSuccess) { *p = nullptr; return GV_ENOMEM; }
+  *cap = want;
+  return GV_OK;
+}
+
+// Order work on stream st after the previous use of set s (any stream).
+int set_acquire(Set* s, hipStream_t st) {
+  if (s->last_st && s->last_st != st) CK(hipStreamWaitEvent(st, s->last, 0));
+  return GV_OK;
+}
+int set_release(Set* s, hipStream_t st) {
+  CK(hipEventRecord(s->last, st));
+  s->last_st = st;
   return GV_OK;
 }
 
@@ -123,21 +301,14 @@ int ensure_keys(Dev* d, size_t need, size_t used, hipStream_t st) {
   return GV_OK;
 }
 
-int ensure_hbits(Dev* d, size_t words) {
-  if (words <= d->h_bits_cap) return GV_OK;
-  if (d->h_bits) (void)hipHostFree(d->h_bits);
-  d->h_bits = nullptr;
-  if (hipHostMalloc(&d->h_bits, words * 8, hipHostMallocDefault) != hipSuccess) { d->h_bits_cap = 0; return GV_ENOMEM; }
-  d->h_bits_cap = words;
-  return GV_OK;
-}
-
 }  // namespace
 
 struct gv_ctx {
   std::vector<Dev*> devs;
   size_t max_batch = size_t(1) << 20;
   size_t lat_max = 4096;        // batches up to this size take the fused latency kernel (gv_lat.hip)
+  size_t pipe_chunk = 262144;   // host path: chunk size of the two-set copy/compute pipeline (0 = max_batch)
+  int stage_threads = 4;        // host path: staging memcpy threads per device
   bool time_kernels = false;
   bool fault_inject = false;
   size_t keys = 0;              // key-arena slots in use (same on every device)
@@ -146,25 +317,29 @@ struct gv_ctx {
 
 namespace {
 
-// Launch the pipeline for n items whose inputs already sit on the device.
-int launch(gv_ctx* ctx, Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig, const uint8_t* dig,
+// Launch the pipeline for n items whose inputs already sit on the device, on
+// set s's scratch, stream st.  The caller holds d->mu.
+int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint8_t* sig, const uint8_t* dig,
            const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint64_t* bits_out,
            hipStream_t st, const uint32_t* kslot = nullptr) {
-  const size_t C = round_up(std::max<size_t>(n, 1), 256);
-  int rc = ensure_cap(d, C);
+  if (n == 0 || n > kMaxItems) return GV_EINVAL;
+  const size_t C = round_up(n, 256);
+  int rc = ensure_cap(s, C);
   if (rc) return rc;
   if (kslot) {                                  // the arena always exists for a keyed batch
     rc = ensure_keys(d, 1, ctx->keys, st);
     if (rc) return rc;
   }
+  rc = set_acquire(s, st);
+  if (rc) return rc;
   gvk_batch b;
   memset(&b, 0, sizeof b);
   b.n = (uint32_t)n; b.C = (uint32_t)C;
   b.pub33 = pub; b.sig64 = sig; b.dig32 = dig;
   b.msg_blob = blob; b.msg_off = off; b.msg_len = len;
   b.gtab = d->gtab;
-  b.in_x = d->in_x; b.in_pfx = d->in_pfx; b.in_r = d->in_r; b.in_s = d->in_s; b.in_e = d->in_e;
-  b.digits = d->digits; b.zq = d->zq; b.flags = d->flags; b.qtab = d->qtab;
+  b.in_x = s->in_x; b.in_pfx = s->in_pfx; b.in_r = s->in_r; b.in_s = s->in_s; b.in_e = s->in_e;
+  b.digits = s->digits; b.zq = s->zq; b.flags = s->flags; b.qtab = s->qtab;
   b.bits = bits_out;
   if (kslot) {
     b.pub33 = nullptr;
@@ -174,10 +349,10 @@ int launch(gv_ctx* ctx, Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig
   hipEvent_t* rs = nullptr;
   if (ctx->time_kernels) {
     rs = d->ring[d->ring_next];
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 5; ++i)
       if (!rs[i]) CK(hipEventCreate(&rs[i]));
-    CK(hipEventRecord(rs[3], st));
-    b.ev[0] = rs[0]; b.ev[1] = rs[1]; b.ev[2] = rs[2];
+    CK(hipEventRecord(rs[0], st));
+    for (int i = 0; i < 4; ++i) b.ev[i] = rs[i + 1];
   }
   if (n <= ctx->lat_max) {
     // small batch: one fused kernel, several lanes per signature (gv_lat.hip)
@@ -186,107 +361,181 @@ int launch(gv_ctx* ctx, Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig
     lb.n = (uint32_t)n; lb.C = (uint32_t)C;
     lb.pub33 = pub; lb.sig64 = sig; lb.dig32 = dig;
     lb.msg_blob = blob; lb.msg_off = off; lb.msg_len = len;
-    lb.gtab = d->gtab; lb.e_soa = d->in_e; lb.bits = bits_out;
+    lb.gtab = d->gtab; lb.e_soa = s->in_e; lb.bits = bits_out;
     lb.ev[0] = b.ev[0];
     if (kslot) {
       lb.pub33 = nullptr;
       lb.kslot = kslot; lb.kqt = b.kqt; lb.kzq = b.kzq; lb.kok = b.kok; lb.kC = b.kC; lb.kcount = b.kcount;
     }
     CK(gvk_verify_lat(&lb, st));
-    if (rs) {                                   // stages: SHA | fused kernel | (none)
-      CK(hipEventRecord(rs[1], st));
+    if (rs) {                                   // stages: SHA | (none) | (none) | fused kernel
       CK(hipEventRecord(rs[2], st));
+      CK(hipEventRecord(rs[3], st));
+      CK(hipEventRecord(rs[4], st));
     }
   } else {
     CK(gvk_verify(&b, st));
   }
   if (rs) {
-    // mirror the last launch into ev[] for gv_last_stage_ms
     d->last = d->ring_next;
     d->ring_next = (d->ring_next + 1) % Dev::kRing;
     d->ring_count = std::min(d->ring_count + 1, Dev::kRing);
   }
+  return set_release(s, st);
+}
+
+struct HostBatch {
+  const uint8_t *pub33, *sig64, *dig32, *blob;
+  const uint64_t* off;
+  const uint32_t* len;
+  const uint32_t* slots;
+  uint8_t* out_ok;
+  uint64_t* out_bits;
+};
+
+// Harvest a finished chunk of set s into the caller's outputs.
+int harvest(Dev* d, Set* s, const HostBatch& hb) {
+  CK(hipEventSynchronize(s->done));
+  const size_t c0 = s->c0, cn = s->cn, words = (cn + 63) / 64;
+  if (hb.out_ok) {
+    uint8_t* o = hb.out_ok + c0;
+    const uint64_t* w = s->h_bits;
+    auto unpack = [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) o[i] = (uint8_t)((w[i >> 6] >> (i & 63)) & 1u);
+    };
+    if (cn < (size_t(1) << 18)) unpack(0, cn);
+    else {
+      const int parts = d->pool->size();
+      const size_t per = round_up((cn + parts - 1) / parts, 64);
+      d->pool->run(parts, [&](int p) { unpack(std::min(cn, p * per), std::min(cn, (p + 1) * per)); });
+    }
+  } else {
+    memcpy(hb.out_bits + c0 / 64, s->h_bits, words * 8);   // c0 % 64 == 0 (chunks are 256-aligned)
+  }
+  s->busy = false;
   return GV_OK;
 }
 
-// Verify items [lo, hi) of a host batch on one device.  out_ok or out_bits.
-int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const uint8_t* pub33, const uint8_t* sig64,
-              const uint8_t* dig32, const uint8_t* blob, const uint64_t* off, const uint32_t* len,
-              uint8_t* out_ok, uint64_t* out_bits, const uint32_t* slots) {
+// Stage chunk [c0, c0 + cn) of a host batch into set s and enqueue H2D ->
+// kernels -> D2H of the bitmap on the set's stream.
+int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& hb) {
+  const size_t C = round_up(cn, 256);
+  const bool keyed = hb.slots != nullptr, msgs = hb.dig32 == nullptr;
+  int rc = ensure_cap(s, C);
+  if (rc) return rc;
+  const InLayout L = in_layout(C, keyed, msgs);
+  if ((rc = ensure_pinned(&s->h_in, &s->h_in_cap, L.total))) return rc;
+  size_t hb_bytes = 0;
+  if ((rc = ensure_pinned((uint8_t**)&s->h_bits, &s->h_bits_cap, (C / 64) * 8))) return rc;
+  uint8_t* h = s->h_in;
+  if (keyed) par_copy(d->pool, h, hb.slots + c0, cn * 4);
+  else par_copy(d->pool, h, hb.pub33 + c0 * 33, cn * 33);
+  par_copy(d->pool, h + L.sig, hb.sig64 + c0 * 64, cn * 64);
+  uint64_t bmin = 0;
+  if (!msgs) {
+    par_copy(d->pool, h + L.third, hb.dig32 + c0 * 32, cn * 32);
+  } else {
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (size_t i = c0; i < c0 + cn; ++i) {
+      lo = std::min<uint64_t>(lo, hb.off[i]);
+      hi = std::max<uint64_t>(hi, hb.off[i] + hb.len[i]);
+    }
+    if (lo > hi) lo = hi = 0;
+    bmin = lo;
+    hb_bytes = hi - lo;
+    uint64_t* ro = (uint64_t*)(h + L.third);
+    for (size_t i = 0; i < cn; ++i) ro[i] = hb.off[c0 + i] - bmin;
+    memcpy(h + L.len, hb.len + c0, cn * 4);
+    if ((rc = ensure_pinned(&s->h_blob, &s->h_blob_cap, hb_bytes))) return rc;
+    if ((rc = ensure_blob(s, hb_bytes))) return rc;
+    par_copy(d->pool, s->h_blob, hb.blob + bmin, hb_bytes);
+  }
+  if ((rc = set_acquire(s, s->st))) return rc;
+  CK(hipMemcpyAsync(s->d_in, h, msgs ? L.total : L.third + cn * 32, hipMemcpyHostToDevice, s->st));
+  if (msgs && hb_bytes) CK(hipMemcpyAsync(s->d_blob, s->h_blob, hb_bytes, hipMemcpyHostToDevice, s->st));
+  const uint8_t* din = s->d_in;
+  rc = launch(ctx, d, s, cn, keyed ? nullptr : din, din + L.sig, msgs ? nullptr : din + L.third,
+              msgs ? s->d_blob : nullptr, msgs ? (const uint64_t*)(din + L.third) : nullptr,
+              msgs ? (const uint32_t*)(din + L.len) : nullptr, s->bits, s->st,
+              keyed ? (const uint32_t*)din : nullptr);
+  if (rc) return rc;
+  CK(hipMemcpyAsync(s->h_bits, s->bits, ((cn + 63) / 64) * 8, hipMemcpyDeviceToHost, s->st));
+  CK(hipEventRecord(s->done, s->st));
+  if ((rc = set_release(s, s->st))) return rc;
+  s->busy = true;
+  s->c0 = c0;
+  s->cn = cn;
+  return GV_OK;
+}
+
+// Verify items [lo, hi) of a host batch on one device: chunks alternate
+// between the two sets so staging + H2D of one overlaps the kernels of the other.
+int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const HostBatch& hb) {
   std::lock_guard<std::mutex> lk(d->mu);
   CK(hipSetDevice(d->id));
-  const size_t chunk = ctx->max_batch;
-  std::vector<uint64_t> roff;
-  for (size_t c0 = lo; c0 < hi; c0 += chunk) {
-    const size_t cn = std::min(chunk, hi - c0);
-    const size_t C = round_up(cn, 256);
-    int rc = ensure_cap(d, C);
-    if (rc) return rc;
-    rc = ensure_hbits(d, C / 64);
-    if (rc) return rc;
-    if (slots) CK(hipMemcpyAsync(d->d_slot, slots + c0, cn * 4, hipMemcpyHostToDevice, d->st));
-    else CK(hipMemcpyAsync(d->d_pub, pub33 + c0 * 33, cn * 33, hipMemcpyHostToDevice, d->st));
-    CK(hipMemcpyAsync(d->d_sig, sig64 + c0 * 64, cn * 64, hipMemcpyHostToDevice, d->st));
-    const uint8_t* ddig = nullptr;
-    const uint8_t* dblob = nullptr;
-    if (dig32) {
-      CK(hipMemcpyAsync(d->d_dig, dig32 + c0 * 32, cn * 32, hipMemcpyHostToDevice, d->st));
-      ddig = d->d_dig;
-    } else {
-      uint64_t bmin = UINT64_MAX, bmax = 0;
-      for (size_t i = c0; i < c0 + cn; ++i) {
-        bmin = std::min<uint64_t>(bmin, off[i]);
-        bmax = std::max<uint64_t>(bmax, off[i] + len[i]);
-      }
-      if (cn == 0 || bmin > bmax) bmin = bmax = 0;
-      rc = ensure_msg(d, bmax - bmin, C);
-      if (rc) return rc;
-      roff.resize(cn);
-      for (size_t i = 0; i < cn; ++i) roff[i] = off[c0 + i] - bmin;
-      if (bmax > bmin) CK(hipMemcpyAsync(d->d_blob, blob + bmin, bmax - bmin, hipMemcpyHostToDevice, d->st));
-      CK(hipMemcpyAsync(d->d_off, roff.data(), cn * 8, hipMemcpyHostToDevice, d->st));
-      CK(hipMemcpyAsync(d->d_len, len + c0, cn * 4, hipMemcpyHostToDevice, d->st));
-      dblob = d->d_blob;
-    }
-    rc = launch(ctx, d, cn, d->d_pub, d->d_sig, ddig, dblob, dblob ? d->d_off : nullptr,
-                dblob ? d->d_len : nullptr, d->bits, d->st, slots ? d->d_slot : nullptr);
-    if (rc) return rc;
-    const size_t words = (cn + 63) / 64;
-    CK(hipMemcpyAsync(d->h_bits, d->bits, words * 8, hipMemcpyDeviceToHost, d->st));
-    CK(hipStreamSynchronize(d->st));
-    if (out_ok) {
-      for (size_t i = 0; i < cn; ++i) out_ok[c0 + i] = (uint8_t)((d->h_bits[i >> 6] >> (i & 63)) & 1u);
-    } else {
-      // c0 is a multiple of 64 (slices and chunks are multiples of 256)
-      memcpy(out_bits + c0 / 64, d->h_bits, words * 8);
-    }
+  const size_t n = hi - lo;
+  size_t nch = (n + ctx->max_batch - 1) / ctx->max_batch;
+  if (n > ctx->lat_max && ctx->pipe_chunk) nch = std::max(nch, (n + ctx->pipe_chunk - 1) / ctx->pipe_chunk);
+  const size_t chunk = std::min(ctx->max_batch, round_up((n + nch - 1) / nch, 256));
+  int rc = GV_OK;
+  int k = 0;
+  for (size_t c0 = lo; c0 < hi && rc == GV_OK; c0 += chunk, k ^= 1) {
+    Set* s = &d->set[k];
+    if (s->busy && (rc = harvest(d, s, hb))) break;
+    rc = submit(ctx, d, s, c0, std::min(chunk, hi - c0), hb);
   }
-  return GV_OK;
+  for (Set& s : d->set)                          // drain (also after an error)
+    if (s.busy) {
+      const int r2 = harvest(d, &s, hb);
+      if (rc == GV_OK) rc = r2;
+      s.busy = false;
+    }
+  return rc;
 }
 
-int run_host(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64, const uint8_t* dig32,
-             const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint8_t* out_ok,
-             uint64_t* out_bits, const uint32_t* slots = nullptr) {
+int run_host(gv_ctx* ctx, size_t n, const HostBatch& hb) {
   if (!ctx) return GV_EINVAL;
   if (ctx->fault_inject) return GV_EFAULT;
   if (n == 0) return GV_OK;
-  if ((!pub33 && !slots) || !sig64 || (!out_ok && !out_bits)) return GV_EINVAL;
-  if (!dig32 && (!blob || !off || !len)) return GV_EINVAL;
+  if ((!hb.pub33 && !hb.slots) || !hb.sig64 || (!hb.out_ok && !hb.out_bits)) return GV_EINVAL;
+  if (!hb.dig32 && (!hb.blob || !hb.off || !hb.len)) return GV_EINVAL;
   const size_t nd = ctx->devs.size();
   const size_t per = round_up((n + nd - 1) / nd, 256);
   std::vector<int> rcs(nd, GV_OK);
-  std::vector<std::thread> th;
-  for (size_t k = 0; k < nd; ++k) {
+  std::vector<bool> posted(nd, false);
+  for (size_t k = 1; k < nd; ++k) {             // devices 1.. on their persistent workers
     const size_t lo = std::min(n, k * per), hi = std::min(n, (k + 1) * per);
     if (lo >= hi) continue;
-    auto job = [=, &rcs]() {
-      rcs[k] = run_slice(ctx, ctx->devs[k], lo, hi, pub33, sig64, dig32, blob, off, len, out_ok, out_bits, slots);
-    };
-    if (nd == 1) job(); else th.emplace_back(job);
+    Dev* d = ctx->devs[k];
+    d->worker->post([=, &hb]() { return run_slice(ctx, d, lo, hi, hb); });
+    posted[k] = true;
   }
-  for (auto& t : th) t.join();
+  rcs[0] = run_slice(ctx, ctx->devs[0], 0, std::min(n, per), hb);   // device 0 on the caller
+  for (size_t k = 1; k < nd; ++k)
+    if (posted[k]) rcs[k] = ctx->devs[k]->worker->wait();
   for (int rc : rcs) if (rc) return rc;
   return GV_OK;
+}
+
+void free_set(Set& s) {
+  if (s.st) (void)hipStreamSynchronize(s.st);
+  if (s.scratch) (void)hipFree(s.scratch);
+  if (s.d_blob) (void)hipFree(s.d_blob);
+  if (s.h_in) (void)hipHostFree(s.h_in);
+  if (s.h_blob) (void)hipHostFree(s.h_blob);
+  if (s.h_bits) (void)hipHostFree(s.h_bits);
+  if (s.last) (void)hipEventDestroy(s.last);
+  if (s.done) (void)hipEventDestroy(s.done);
+  if (s.st) (void)hipStreamDestroy(s.st);
+}
+
+bool parse_size_env(const char* name, size_t* out) {
+  const char* v = getenv(name);
+  if (!v) return false;
+  const long long x = atoll(v);
+  if (x < 256 || (unsigned long long)x > kMaxItems) return false;
+  *out = round_up((size_t)x, 256);
+  return true;
 }
 
 }  // namespace
@@ -304,25 +553,26 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
     if (dev_ids[i] < 0 || dev_ids[i] >= count) return GV_ENODEV;
     ids.push_back(dev_ids[i]);
   }
-  gv_ctx* ctx = new gv_ctx();
-  if (const char* mb = getenv("GV_MAX_BATCH")) {
-    long long v = atoll(mb);
-    if (v >= 256) ctx->max_batch = round_up((size_t)v, 256);
+  for (int id : ids) {                          // the kernels are written for wave64
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, id) != hipSuccess || prop.warpSize != 64) return GV_ENODEV;
   }
-  for (int id : ids) {
+  gv_ctx* ctx = new gv_ctx();
+  parse_size_env("GV_MAX_BATCH", &ctx->max_batch);
+  for (size_t k = 0; k < ids.size(); ++k) {
     Dev* d = new Dev();
-    d->id = id;
+    d->id = ids[k];
     ctx->devs.push_back(d);
-    if (hipSetDevice(id) != hipSuccess ||
-        hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&d->gtab, (size_t)2 * GV_GTAB_N * 16 * 4) != hipSuccess ||
-        gvk_gen_gtable(d->gtab, d->st) != hipSuccess ||
-        hipStreamSynchronize(d->st) != hipSuccess) {
-      gv_close(ctx);
-      return GV_EHIP;
-    }
-    for (auto& e : d->ev)
-      if (hipEventCreate(&e) != hipSuccess) { gv_close(ctx); return GV_EHIP; }
+    d->pool = new Pool(ctx->stage_threads - 1);
+    if (k > 0) d->worker = new Worker();
+    bool ok = hipSetDevice(d->id) == hipSuccess;
+    for (Set& s : d->set)
+      ok = ok && hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) == hipSuccess &&
+           hipEventCreateWithFlags(&s.last, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipMalloc(&d->gtab, (size_t)2 * GV_GTAB_N * 16 * 4) == hipSuccess &&
+         gvk_gen_gtable(d->gtab, d->set[0].st) == hipSuccess && hipStreamSynchronize(d->set[0].st) == hipSuccess;
+    if (!ok) { gv_close(ctx); return GV_EHIP; }
   }
   *out = ctx;
   return GV_OK;
@@ -331,21 +581,16 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
 void gv_close(gv_ctx* ctx) {
   if (!ctx) return;
   for (Dev* d : ctx->devs) {
+    delete d->worker;
     (void)hipSetDevice(d->id);
-    if (d->st) (void)hipStreamSynchronize(d->st);
-    if (d->scratch) (void)hipFree(d->scratch);
+    for (Set& s : d->set) free_set(s);
     if (d->gtab) (void)hipFree(d->gtab);
-    if (d->d_blob) (void)hipFree(d->d_blob);
-    if (d->d_off) (void)hipFree(d->d_off);
-    if (d->d_len) (void)hipFree(d->d_len);
-    if (d->h_bits) (void)hipHostFree(d->h_bits);
     if (d->kqt) (void)hipFree(d->kqt);
     if (d->kzq) (void)hipFree(d->kzq);
     if (d->kok) (void)hipFree(d->kok);
-    for (auto e : d->ev) if (e) (void)hipEventDestroy(e);
     for (auto& rs : d->ring)
       for (auto e : rs) if (e) (void)hipEventDestroy(e);
-    if (d->st) (void)hipStreamDestroy(d->st);
+    delete d->pool;
     delete d;
   }
   delete ctx;
@@ -356,25 +601,25 @@ int gv_num_devices(const gv_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; 
 int gv_verify_msgs(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64,
                    const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len,
                    uint8_t* out_ok) {
-  return run_host(ctx, n, pub33, sig64, nullptr, msg_blob, msg_off, msg_len, out_ok, nullptr);
+  return run_host(ctx, n, HostBatch{pub33, sig64, nullptr, msg_blob, msg_off, msg_len, nullptr, out_ok, nullptr});
 }
 
 int gv_verify_digests(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64,
                       const uint8_t* dig32, uint8_t* out_ok) {
   if (!dig32 && n) return GV_EINVAL;
-  return run_host(ctx, n, pub33, sig64, dig32, nullptr, nullptr, nullptr, out_ok, nullptr);
+  return run_host(ctx, n, HostBatch{pub33, sig64, dig32, nullptr, nullptr, nullptr, nullptr, out_ok, nullptr});
 }
 
 int gv_verify_digests_bits(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64,
                            const uint8_t* dig32, uint64_t* out_bits) {
   if (!dig32 && n) return GV_EINVAL;
-  return run_host(ctx, n, pub33, sig64, dig32, nullptr, nullptr, nullptr, nullptr, out_bits);
+  return run_host(ctx, n, HostBatch{pub33, sig64, dig32, nullptr, nullptr, nullptr, nullptr, nullptr, out_bits});
 }
 
 int gv_verify_msgs_bits(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64,
                         const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len,
                         uint64_t* out_bits) {
-  return run_host(ctx, n, pub33, sig64, nullptr, msg_blob, msg_off, msg_len, nullptr, out_bits);
+  return run_host(ctx, n, HostBatch{pub33, sig64, nullptr, msg_blob, msg_off, msg_len, nullptr, nullptr, out_bits});
 }
 
 static int dev_common(gv_ctx* ctx, int slot, size_t n, const void* pub, const void* sig, void* bits,
@@ -385,7 +630,7 @@ static int dev_common(gv_ctx* ctx, int slot, size_t n, const void* pub, const vo
   if (n == 0) return GV_OK;
   if (!pub || !sig || !bits) return GV_EINVAL;
   if (((uintptr_t)pub & 3) || ((uintptr_t)sig & 3)) return GV_EINVAL;
-  if (n > 0xFFFFFF00ull) return GV_EINVAL;
+  if (n > kMaxItems) return GV_EINVAL;
   *dout = ctx->devs[slot];
   return GV_OK;
 }
@@ -398,8 +643,8 @@ int gv_dev_verify_digests(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub
   if (!d_dig32 || ((uintptr_t)d_dig32 & 3)) return GV_EINVAL;
   std::lock_guard<std::mutex> lk(d->mu);
   CK(hipSetDevice(d->id));
-  hipStream_t st = stream ? (hipStream_t)stream : d->st;
-  return launch(ctx, d, n, (const uint8_t*)d_pub33, (const uint8_t*)d_sig64, (const uint8_t*)d_dig32,
+  hipStream_t st = stream ? (hipStream_t)stream : d->set[0].st;
+  return launch(ctx, d, &d->set[0], n, (const uint8_t*)d_pub33, (const uint8_t*)d_sig64, (const uint8_t*)d_dig32,
                 nullptr, nullptr, nullptr, (uint64_t*)d_bits, st);
 }
 
@@ -412,8 +657,8 @@ int gv_dev_verify_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub33,
   if (!d_msg_blob || !d_msg_off || !d_msg_len) return GV_EINVAL;
   std::lock_guard<std::mutex> lk(d->mu);
   CK(hipSetDevice(d->id));
-  hipStream_t st = stream ? (hipStream_t)stream : d->st;
-  return launch(ctx, d, n, (const uint8_t*)d_pub33, (const uint8_t*)d_sig64, nullptr,
+  hipStream_t st = stream ? (hipStream_t)stream : d->set[0].st;
+  return launch(ctx, d, &d->set[0], n, (const uint8_t*)d_pub33, (const uint8_t*)d_sig64, nullptr,
                 (const uint8_t*)d_msg_blob, (const uint64_t*)d_msg_off, (const uint32_t*)d_msg_len,
                 (uint64_t*)d_bits, st);
 }
@@ -425,23 +670,26 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
   if (!pub33 || !slot_out) return GV_EINVAL;
   std::lock_guard<std::mutex> kl(ctx->keys_mu);
   const size_t base = ctx->keys;
-  if (base + n > 0xFFFFFF00ull) return GV_EINVAL;
+  if (base + n > kMaxItems) return GV_EINVAL;
   for (Dev* d : ctx->devs) {                    // every device holds every key
     std::lock_guard<std::mutex> lk(d->mu);
     CK(hipSetDevice(d->id));
-    int rc = ensure_keys(d, base + n, base, d->st);
+    Set* s = &d->set[0];
+    hipStream_t st = s->st;
+    int rc = ensure_keys(d, base + n, base, st);
     if (rc) return rc;
     for (size_t c0 = 0; c0 < n; c0 += ctx->max_batch) {
       const size_t cn = std::min(ctx->max_batch, n - c0);
       const size_t C = round_up(cn, 256);
-      rc = ensure_cap(d, C);
-      if (rc) return rc;
-      CK(hipMemcpyAsync(d->d_pub, pub33 + c0 * 33, cn * 33, hipMemcpyHostToDevice, d->st));
-      CK(gvk_keys_build(d->d_pub, (uint32_t)cn, (uint32_t)C, d->in_x, d->in_pfx, d->in_r, d->in_s, d->in_e,
-                        d->qtab + C * GV_QTAB_N * GV_QENT_WORDS, (uint32_t)(base + c0), d->kqt, d->kzq,
-                        (uint32_t)d->kcap, d->kok, d->st));
+      if ((rc = ensure_cap(s, C))) return rc;
+      if ((rc = set_acquire(s, st))) return rc;
+      CK(hipMemcpyAsync(s->d_in, pub33 + c0 * 33, cn * 33, hipMemcpyHostToDevice, st));
+      CK(gvk_keys_build(s->d_in, (uint32_t)cn, (uint32_t)C, s->in_x, s->in_pfx, s->in_r, s->in_s, s->in_e,
+                        s->qtab + C * GV_QTAB_N * GV_QENT_WORDS, (uint32_t)(base + c0), d->kqt, d->kzq,
+                        (uint32_t)d->kcap, d->kok, st));
+      if ((rc = set_release(s, st))) return rc;
+      CK(hipStreamSynchronize(st));            // the caller's pub33 chunk is read by then
     }
-    CK(hipStreamSynchronize(d->st));
   }
   ctx->keys = base + n;
   for (size_t i = 0; i < n; ++i) slot_out[i] = (uint32_t)(base + i);
@@ -457,17 +705,41 @@ int gv_keys_reset(gv_ctx* ctx) {
 
 size_t gv_keys_count(const gv_ctx* ctx) { return ctx ? ctx->keys : 0; }
 
+int gv_keys_point(gv_ctx* ctx, size_t n, const uint32_t* slots, uint8_t* out_xy64, uint8_t* out_ok) {
+  if (!ctx) return GV_EINVAL;
+  if (n == 0) return GV_OK;
+  if (!slots || !out_xy64 || !out_ok || n > kMaxItems) return GV_EINVAL;
+  Dev* d = ctx->devs[0];
+  std::lock_guard<std::mutex> lk(d->mu);
+  CK(hipSetDevice(d->id));
+  hipStream_t st = d->set[0].st;
+  int rc = ensure_keys(d, 1, ctx->keys, st);
+  if (rc) return rc;
+  uint8_t* buf = nullptr;
+  const size_t sb = round_up(n * 4, 256), xb = round_up(n * 64, 256);
+  if (hipMalloc(&buf, sb + xb + n) != hipSuccess) return GV_ENOMEM;
+  if (hipMemcpyAsync(buf, slots, n * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+      gvk_keys_point((uint32_t)n, (const uint32_t*)buf, d->kqt, d->kzq, (uint32_t)d->kcap, d->kok,
+                     (uint32_t)ctx->keys, buf + sb, buf + sb + xb, st) != hipSuccess ||
+      hipMemcpyAsync(out_xy64, buf + sb, n * 64, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(out_ok, buf + sb + xb, n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    rc = GV_EHIP;
+  (void)hipFree(buf);
+  return rc;
+}
+
 int gv_verify_digests_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64,
                             const uint8_t* dig32, uint8_t* out_ok) {
   if (n && (!slot || !dig32)) return GV_EINVAL;
-  return run_host(ctx, n, nullptr, sig64, dig32, nullptr, nullptr, nullptr, out_ok, nullptr, slot);
+  return run_host(ctx, n, HostBatch{nullptr, sig64, dig32, nullptr, nullptr, nullptr, slot, out_ok, nullptr});
 }
 
 int gv_verify_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64,
                          const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len,
                          uint8_t* out_ok) {
   if (n && !slot) return GV_EINVAL;
-  return run_host(ctx, n, nullptr, sig64, nullptr, msg_blob, msg_off, msg_len, out_ok, nullptr, slot);
+  return run_host(ctx, n, HostBatch{nullptr, sig64, nullptr, msg_blob, msg_off, msg_len, slot, out_ok, nullptr});
 }
 
 int gv_dev_verify_digests_keyed(gv_ctx* ctx, int dev_slot, size_t n, const void* d_slot, const void* d_sig64,
@@ -478,19 +750,22 @@ int gv_dev_verify_digests_keyed(gv_ctx* ctx, int dev_slot, size_t n, const void*
   if (!d_dig32 || ((uintptr_t)d_dig32 & 3)) return GV_EINVAL;
   std::lock_guard<std::mutex> lk(d->mu);
   CK(hipSetDevice(d->id));
-  hipStream_t st = stream ? (hipStream_t)stream : d->st;
-  return launch(ctx, d, n, nullptr, (const uint8_t*)d_sig64, (const uint8_t*)d_dig32, nullptr, nullptr, nullptr,
-                (uint64_t*)d_bits, st, (const uint32_t*)d_slot);
+  hipStream_t st = stream ? (hipStream_t)stream : d->set[0].st;
+  return launch(ctx, d, &d->set[0], n, nullptr, (const uint8_t*)d_sig64, (const uint8_t*)d_dig32, nullptr, nullptr,
+                nullptr, (uint64_t*)d_bits, st, (const uint32_t*)d_slot);
 }
 
 int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   if (!ctx || !key) return GV_EINVAL;
   if (!strcmp(key, "lat_max")) {
-    if (val < 0) return GV_EINVAL;
+    if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
     ctx->lat_max = (size_t)val;
   } else if (!strcmp(key, "max_batch")) {
-    if (val < 256) return GV_EINVAL;
+    if (val < 256 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
     ctx->max_batch = round_up((size_t)val, 256);
+  } else if (!strcmp(key, "pipe_chunk")) {
+    if (val != 0 && (val < 256 || (unsigned long long)val > kMaxItems)) return GV_EINVAL;
+    ctx->pipe_chunk = val ? round_up((size_t)val, 256) : 0;
   } else if (!strcmp(key, "time_kernels")) {
     ctx->time_kernels = val != 0;
   } else if (!strcmp(key, "fault_inject")) {
@@ -501,46 +776,54 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   return GV_OK;
 }
 
+static int stage_ms(hipEvent_t* e, float ms[4]) {
+  CK(hipEventSynchronize(e[4]));
+  for (int i = 0; i < 4; ++i) CK(hipEventElapsedTime(&ms[i], e[i], e[i + 1]));
+  return GV_OK;
+}
+
 int gv_last_stage_ms(gv_ctx* ctx, int dev_slot, float* unpack_ms, float* prep_ms, float* ecmult_ms) {
   if (!ctx || dev_slot < 0 || dev_slot >= (int)ctx->devs.size()) return GV_EINVAL;
   if (!ctx->time_kernels) return GV_EINVAL;
   Dev* d = ctx->devs[dev_slot];
   if (d->last < 0) return GV_EINVAL;
   CK(hipSetDevice(d->id));
-  hipEvent_t* e = d->ring[d->last];
-  CK(hipEventSynchronize(e[2]));
-  float a = 0, b = 0, c = 0;
-  CK(hipEventElapsedTime(&a, e[3], e[0]));
-  CK(hipEventElapsedTime(&b, e[0], e[1]));
-  CK(hipEventElapsedTime(&c, e[1], e[2]));
-  if (unpack_ms) *unpack_ms = a;
-  if (prep_ms) *prep_ms = b;
-  if (ecmult_ms) *ecmult_ms = c;
+  float ms[4];
+  int rc = stage_ms(d->ring[d->last], ms);
+  if (rc) return rc;
+  if (unpack_ms) *unpack_ms = ms[0];
+  if (prep_ms) *prep_ms = ms[1] + ms[2];
+  if (ecmult_ms) *ecmult_ms = ms[3];
+  return GV_OK;
+}
+
+int gv_stage_stats4(gv_ctx* ctx, int dev_slot, int* count, double ms_out[4]) {
+  if (!ctx || dev_slot < 0 || dev_slot >= (int)ctx->devs.size() || !ms_out) return GV_EINVAL;
+  Dev* d = ctx->devs[dev_slot];
+  std::lock_guard<std::mutex> lk(d->mu);
+  CK(hipSetDevice(d->id));
+  double sum[4] = {0, 0, 0, 0};
+  const int cnt = d->ring_count;
+  for (int k = 0; k < cnt; ++k) {
+    float ms[4];
+    int rc = stage_ms(d->ring[(d->ring_next - 1 - k + Dev::kRing) % Dev::kRing], ms);
+    if (rc) return rc;
+    for (int i = 0; i < 4; ++i) sum[i] += ms[i];
+  }
+  d->ring_count = 0;
+  if (count) *count = cnt;
+  for (int i = 0; i < 4; ++i) ms_out[i] = cnt ? sum[i] / cnt : 0.0;
   return GV_OK;
 }
 
 int gv_stage_stats(gv_ctx* ctx, int dev_slot, int* count, double* unpack_ms, double* prep_ms,
                    double* ecmult_ms) {
-  if (!ctx || dev_slot < 0 || dev_slot >= (int)ctx->devs.size()) return GV_EINVAL;
-  Dev* d = ctx->devs[dev_slot];
-  std::lock_guard<std::mutex> lk(d->mu);
-  CK(hipSetDevice(d->id));
-  double sa = 0, sb = 0, sc = 0;
-  const int cnt = d->ring_count;
-  for (int k = 0; k < cnt; ++k) {
-    hipEvent_t* e = d->ring[(d->ring_next - 1 - k + Dev::kRing) % Dev::kRing];
-    CK(hipEventSynchronize(e[2]));
-    float a = 0, b = 0, c = 0;
-    CK(hipEventElapsedTime(&a, e[3], e[0]));
-    CK(hipEventElapsedTime(&b, e[0], e[1]));
-    CK(hipEventElapsedTime(&c, e[1], e[2]));
-    sa += a; sb += b; sc += c;
-  }
-  d->ring_count = 0;
-  if (count) *count = cnt;
-  if (unpack_ms) *unpack_ms = cnt ? sa / cnt : 0.0;
-  if (prep_ms) *prep_ms = cnt ? sb / cnt : 0.0;
-  if (ecmult_ms) *ecmult_ms = cnt ? sc / cnt : 0.0;
+  double ms[4];
+  int rc = gv_stage_stats4(ctx, dev_slot, count, ms);
+  if (rc) return rc;
+  if (unpack_ms) *unpack_ms = ms[0];
+  if (prep_ms) *prep_ms = ms[1] + ms[2];
+  if (ecmult_ms) *ecmult_ms = ms[3];
   return GV_OK;
 }
 
@@ -572,8 +855,9 @@ int gv_dev_copy(gv_ctx* ctx, int dev_slot, void* dst, const void* src, size_t by
   }
   Dev* d = ctx->devs[dev_slot];
   CK(hipSetDevice(d->id));
-  CK(hipMemcpyAsync(dst, src, bytes, k, d->st));
-  CK(hipStreamSynchronize(d->st));
+  hipStream_t st = d->set[0].st;
+  CK(hipMemcpyAsync(dst, src, bytes, k, st));
+  CK(hipStreamSynchronize(st));
   return GV_OK;
 }
 
@@ -581,7 +865,7 @@ int gv_dev_sync(gv_ctx* ctx, int dev_slot) {
   if (!ctx || dev_slot < 0 || dev_slot >= (int)ctx->devs.size()) return GV_EINVAL;
   Dev* d = ctx->devs[dev_slot];
   CK(hipSetDevice(d->id));
-  CK(hipStreamSynchronize(d->st));
+  for (Set& s : d->set) CK(hipStreamSynchronize(s.st));
   return GV_OK;
 }
 
@@ -600,19 +884,21 @@ const char* gv_strerror(int code) {
 int gv_debug_op(gv_ctx* ctx, int dev_slot, int op, size_t n, const uint32_t* in, uint32_t* out) {
   if (!ctx || dev_slot < 0 || dev_slot >= (int)ctx->devs.size() || !in || !out) return GV_EINVAL;
   if (n == 0) return GV_OK;
+  if (n > kMaxItems) return GV_EINVAL;
   Dev* d = ctx->devs[dev_slot];
   std::lock_guard<std::mutex> lk(d->mu);
   CK(hipSetDevice(d->id));
+  hipStream_t st = d->set[0].st;
   const size_t npad = round_up(n, 256);
   uint32_t *din = nullptr, *dout = nullptr;
   CK(hipMalloc(&din, npad * 64));
   if (hipMalloc(&dout, npad * 64) != hipSuccess) { (void)hipFree(din); return GV_ENOMEM; }
   int rc = GV_OK;
-  if (hipMemsetAsync(din, 0, npad * 64, d->st) != hipSuccess ||
-      hipMemcpyAsync(din, in, n * 64, hipMemcpyHostToDevice, d->st) != hipSuccess ||
-      gvk_debug(op, (uint32_t)n, din, dout, d->st) != hipSuccess ||
-      hipMemcpyAsync(out, dout, n * 64, hipMemcpyDeviceToHost, d->st) != hipSuccess ||
-      hipStreamSynchronize(d->st) != hipSuccess)
+  if (hipMemsetAsync(din, 0, npad * 64, st) != hipSuccess ||
+      hipMemcpyAsync(din, in, n * 64, hipMemcpyHostToDevice, st) != hipSuccess ||
+      gvk_debug(op, (uint32_t)n, din, dout, st) != hipSuccess ||
+      hipMemcpyAsync(out, dout, n * 64, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
     rc = GV_EHIP;
   (void)hipFree(din);
   (void)hipFree(dout);

@@ -33,7 +33,8 @@ EXPORTED_SYMBOLS = (
     "gv_verify_digests_bits", "gv_verify_msgs_bits", "gv_dev_verify_digests", "gv_dev_verify_msgs",
     "gv_set_option", "gv_last_stage_ms", "gv_strerror", "gv_debug_op", "gv_dev_alloc", "gv_dev_free",
     "gv_dev_copy", "gv_dev_sync", "gv_stage_stats", "gv_keys_load", "gv_keys_reset", "gv_keys_count",
-    "gv_verify_digests_keyed", "gv_verify_msgs_keyed", "gv_dev_verify_digests_keyed",
+    "gv_verify_digests_keyed", "gv_verify_msgs_keyed", "gv_dev_verify_digests_keyed", "gv_stage_stats4",
+    "gv_keys_point",
 )
 
 
@@ -97,12 +98,16 @@ def load(path: str = LIB_PATH):
     L.gv_dev_sync.restype = i32
     L.gv_stage_stats.argtypes = [vp, i32, ctypes.POINTER(i32)] + [ctypes.POINTER(ctypes.c_double)] * 3
     L.gv_stage_stats.restype = i32
+    L.gv_stage_stats4.argtypes = [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double)]
+    L.gv_stage_stats4.restype = i32
     L.gv_keys_load.argtypes = [vp, sz, vp, vp]
     L.gv_keys_load.restype = i32
     L.gv_keys_reset.argtypes = [vp]
     L.gv_keys_reset.restype = i32
     L.gv_keys_count.argtypes = [vp]
     L.gv_keys_count.restype = sz
+    L.gv_keys_point.argtypes = [vp, sz, vp, vp, vp]
+    L.gv_keys_point.restype = i32
     L.gv_verify_digests_keyed.argtypes = [vp, sz, vp, vp, vp, vp]
     L.gv_verify_digests_keyed.restype = i32
     L.gv_verify_msgs_keyed.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp]
@@ -217,6 +222,16 @@ class Verifier:
             _check(self._L.gv_keys_load(self._ctx, n, _ptr(pub33), _ptr(slots)), "gv_keys_load")
         return slots
 
+    def keys_point(self, slots: np.ndarray):
+        """Affine points (n x 64 bytes x||y) and ParsePubKey verdicts the key arena holds for `slots`."""
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        n = slots.shape[0]
+        xy = np.zeros((n, 64), dtype=np.uint8)
+        ok = np.zeros(n, dtype=np.uint8)
+        if n:
+            _check(self._L.gv_keys_point(self._ctx, n, _ptr(slots), _ptr(xy), _ptr(ok)), "gv_keys_point")
+        return xy, ok
+
     def keys_reset(self):
         _check(self._L.gv_keys_reset(self._ctx), "gv_keys_reset")
 
@@ -297,6 +312,13 @@ class Verifier:
         _check(self._L.gv_stage_stats(self._ctx, slot, ctypes.byref(c), ctypes.byref(a), ctypes.byref(b),
                                       ctypes.byref(d)), "gv_stage_stats")
         return c.value, a.value, b.value, d.value
+
+    def stage_stats4(self, slot: int = 0):
+        """(count, [unpack/sha, scalar_inv, prep, ecmult] ms averaged over the launches since the last call)."""
+        c = ctypes.c_int()
+        ms = (ctypes.c_double * 4)()
+        _check(self._L.gv_stage_stats4(self._ctx, slot, ctypes.byref(c), ms), "gv_stage_stats4")
+        return c.value, list(ms)
 
     def debug_op(self, op: int, words: np.ndarray, slot: int = 0) -> np.ndarray:
         words = np.ascontiguousarray(words, dtype=np.uint32)

@@ -17,8 +17,11 @@
  *
  * Plain pointers and sizes only (cgo / ctypes / JNI friendly).  The caller owns
  * every buffer; the library copies inputs into its own device memory and keeps
- * no caller pointer after a call returns.  Calls are synchronous and a gv_ctx
- * may be shared by concurrent threads (calls on one device serialise).
+ * no caller pointer after a call returns.  Host-buffer calls are synchronous
+ * and a gv_ctx may be shared by concurrent threads (calls on one device
+ * serialise; every use of a device's scratch, on any stream, is ordered after
+ * the previous one, so gv_dev_* calls on different caller streams never
+ * overwrite each other's in-flight inputs).
  * INTEGRATION.md shows the Go (cgo) binding a maintainer adds as
  * crypto/gpuverify and the BatchSigVerificationDecorator built on it.
  */
@@ -111,6 +114,12 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
 int gv_keys_reset(gv_ctx* ctx);
 size_t gv_keys_count(const gv_ctx* ctx);
 
+/* Key-arena readback (tests, tools): for each slot, the affine point the
+ * arena holds for it, out_xy64 + 64*i = x || y (32 bytes each, big-endian),
+ * and out_ok[i] = its ParsePubKey verdict (a slot >= gv_keys_count(): zeros
+ * and 0).  Reads the first device's arena. */
+int gv_keys_point(gv_ctx* ctx, size_t n, const uint32_t* slots, uint8_t* out_xy64, uint8_t* out_ok);
+
 /* VerifyBytes with the key given by slot: out_ok[i] is exactly what
  * gv_verify_digests / gv_verify_msgs return with pub33 = the key loaded into
  * slot[i]; a slot >= gv_keys_count() gives false.  Same batching, errors and
@@ -125,9 +134,12 @@ int gv_verify_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint
 int gv_dev_verify_digests_keyed(gv_ctx* ctx, int dev_slot, size_t n, const void* d_slot, const void* d_sig64,
                                 const void* d_dig32, void* d_bits, void* stream);
 
-/* Options: "max_batch" (lanes per device launch, default 1<<20),
+/* Options: "max_batch" (lanes per device launch, default 1<<20, at most
+ * 0xFFFFFF00),
  * "lat_max" (batches of at most this many items -- per device slice -- take
  * the fused small-batch latency kernel, default 4096; 0 = never),
+ * "pipe_chunk" (host-buffer calls: chunk size of the two-stream copy/compute
+ * pipeline per device, default 262144; 0 = one chunk per max_batch),
  * "time_kernels" (0/1: record HIP events around each kernel stage),
  * "fault_inject" (0/1: every verify call fails with GV_EFAULT; test hook). */
 int gv_set_option(gv_ctx* ctx, const char* key, long long val);
@@ -141,6 +153,10 @@ int gv_last_stage_ms(gv_ctx* ctx, int dev_slot, float* unpack_ms, float* prep_ms
  * receives the number of launches averaged.  Synchronises dev_slot. */
 int gv_stage_stats(gv_ctx* ctx, int dev_slot, int* count, double* unpack_ms, double* prep_ms,
                    double* ecmult_ms);
+
+/* Same, per stage: ms[0] unpack (+ SHA-256 on the message path), ms[1]
+ * k_scalar_inv, ms[2] k_prep, ms[3] k_ecmult (fused latency kernel: ms[3]). */
+int gv_stage_stats4(gv_ctx* ctx, int dev_slot, int* count, double ms[4]);
 
 const char* gv_strerror(int code);
 

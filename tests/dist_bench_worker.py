@@ -14,7 +14,8 @@ import bench  # noqa: E402
 
 class FakeVerifier:
     """Device-memory and verify calls of gpuverify.Verifier, on host numpy arrays.
-    A signature is 'valid' iff its pubkey prefix byte is 0x02; rank r sleeps
+    A signature is 'valid' iff its pubkey prefix byte is 0x02 and bit 0 of its
+    digest's last byte is clear (the workload keeps it clear); rank r sleeps
     (r+1)*10 ms per batch so max-over-ranks is observable."""
 
     def __init__(self, rank):
@@ -38,7 +39,8 @@ class FakeVerifier:
         arr.reshape(-1).view(np.uint8)[:] = self.mem[p][:arr.nbytes]
 
     def dev_verify_digests(self, slot, n, d_pub, d_sig, d_dig, d_bits, stream=None):
-        ok = (self.mem[d_pub].reshape(-1, 33)[:n, 0] == 2).astype(np.uint8)
+        ok = ((self.mem[d_pub].reshape(-1, 33)[:n, 0] == 2) &
+              ((self.mem[d_dig].reshape(-1, 32)[:n, 31] & 1) == 0)).astype(np.uint8)
         packed = np.packbits(ok, bitorder="little")
         self.mem[d_bits][:] = 0
         self.mem[d_bits][:packed.size] = packed
@@ -53,6 +55,9 @@ class FakeVerifier:
     def stage_stats(self, slot=0):
         return 1, 0.1, 0.2, 0.3
 
+    def stage_stats4(self, slot=0):
+        return 1, [0.1, 0.05, 0.15, 0.3]
+
     def close(self):
         pass
 
@@ -63,6 +68,7 @@ def workload(n, seed, keys, adv, threads):
     pub[:, 0] = np.where(rng.random(n) < 0.75, 2, 4)
     sig = rng.integers(0, 256, (n, 64), dtype=np.uint8)
     dig = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    dig[:, 31] &= 0xFE
     exp = (pub[:, 0] == 2).astype(np.uint8)
     return pub, sig, dig, exp
 

@@ -37,5 +37,8 @@ def test_two_rank_bench_aggregation():
     # rank 1 sleeps 20 ms per step: the reported step time is the slower rank's
     assert out["ms_per_step"] >= 20.0
     assert abs(out["value"] - 2 * n / (out["ms_per_step"] * 1e-3)) / out["value"] < 0.01
-    assert out["parity"] == {"checked": 2 * n, "mismatches": 0,
-                             "reference": out["parity"]["reference"]}
+    par = out["parity"]
+    assert par["checked"] == 2 * n and par["mismatches"] == 0
+    assert par["adversarial_checked"] == 2 * n and par["adversarial_mismatches"] == 0
+    assert 0.2 * 2 * n < par["adversarial_rejects_expected"] < 0.5 * 2 * n
+    assert set(out["roofline"]["kernels"]) == {"k_scalar_inv", "k_prep", "k_ecmult"}

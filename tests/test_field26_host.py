@@ -1,6 +1,6 @@
 """Reduced-radix (10 x 26) field layer, host build, against Python integers.
 
-csrc/secp_field26.cuh is plain C++ apart from its qualifiers, so the exact
+tools/field26/secp_field26.cuh (a 10 x 26 prototype kept outside the product tree) is plain C++ apart from its qualifiers, so the exact
 source the kernels use is compiled with g++ here and driven through ctypes:
 random and extreme limb patterns at the maximum magnitudes the group formulas
 are allowed to feed in (mul/sqr inputs <= 16, normalize/is_zero <= 32).

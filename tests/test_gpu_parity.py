@@ -357,3 +357,67 @@ def test_multi_device_split_and_gather():
         assert np.array_equal(v2.verify_batch_digests(pub, sig, dig), want)
         bits = v2.verify_batch_digests_bits(pub, sig, dig)
         assert np.array_equal(np.unpackbits(bits.view(np.uint8), bitorder="little")[:3001], want)
+
+
+def test_overlapping_device_calls_on_separate_streams(ver):
+    """gv_dev_* calls on two caller streams, then a host-buffer call, issued
+    back to back with no host sync: every use of the device scratch is ordered
+    after the previous one (gv_runtime.cpp set_acquire/set_release), so no call
+    overwrites the inputs of kernels still in flight."""
+    torch = pytest.importorskip("torch")
+    s1, s2 = torch.cuda.Stream(device=0), torch.cuda.Stream(device=0)
+    batches = [make_random_batch(60000, seed=300 + k, adversarial=0.3, nkeys=97) for k in range(2)]
+    wants = [O.verify_digests(*b, threads=16) for b in batches]
+    bufs = []
+    for pub, sig, dig in batches:
+        d = [ver.dev_alloc(a.nbytes) for a in (pub, sig, dig)]
+        for p, a in zip(d, (pub, sig, dig)):
+            ver.dev_upload(p, a)
+        bufs.append(d + [ver.dev_alloc(((len(pub) + 63) // 64) * 8)])
+    try:
+        for (pub, _, _), d, st in zip(batches, bufs, (s1, s2)):
+            ver.dev_verify_digests(0, len(pub), d[0], d[1], d[2], d[3], stream=st.cuda_stream)
+        pub3, sig3, dig3 = make_random_batch(3000, seed=399, adversarial=0.3, nkeys=5)
+        got3 = ver.verify_batch_digests(pub3, sig3, dig3)
+        s1.synchronize()
+        s2.synchronize()
+        assert np.array_equal(got3, O.verify_digests(pub3, sig3, dig3, threads=8))
+        for (pub, _, _), d, want in zip(batches, bufs, wants):
+            bits = np.zeros((len(pub) + 63) // 64, dtype=np.uint64)
+            ver.dev_download(bits, d[3])
+            assert np.array_equal(np.unpackbits(bits.view(np.uint8), bitorder="little")[:len(pub)], want)
+    finally:
+        for d in bufs:
+            for p in d:
+                ver.dev_free(p)
+
+
+@pytest.mark.parametrize("chunk", [256, 4096, 0])
+def test_host_pipeline_chunking(ver, chunk):
+    """The two-stream host pipeline (pinned staging, chunks alternating between
+    two scratch sets) over ragged chunk boundaries, digests and messages."""
+    pub, sig, dig = make_random_batch(10007, seed=chunk + 1, adversarial=0.25, nkeys=29)
+    want = O.verify_digests(pub, sig, dig, threads=16)
+    ver.set_option("pipe_chunk", chunk)
+    try:
+        assert np.array_equal(ver.verify_batch_digests(pub, sig, dig), want)
+        bits = ver.verify_batch_digests_bits(pub, sig, dig)
+        assert np.array_equal(np.unpackbits(bits.view(np.uint8), bitorder="little")[:len(want)], want)
+        rng = random.Random(chunk)
+        msgs = [rng.randbytes(rng.randrange(0, 300)) for _ in range(5000)]
+        mdig = np.array([np.frombuffer(O.sha256(m), np.uint8) for m in msgs])
+        privs = np.array([np.frombuffer(rng.randrange(1, N).to_bytes(32, "big"), np.uint8) for _ in range(5000)])
+        mpub = O.pubkey_batch(privs, threads=8)
+        msig = O.sign_batch(privs, mdig, threads=8)
+        msgs = [m + b"x" if i % 7 == 0 else m for i, m in enumerate(msgs)]
+        mwant = np.array([i % 7 != 0 for i in range(5000)], np.uint8)
+        assert np.array_equal(ver.verify_batch_msgs(mpub, msig, msgs), mwant)
+    finally:
+        ver.set_option("pipe_chunk", 262144)
+
+
+def test_option_bounds(ver):
+    for key, val in (("max_batch", 1 << 32), ("max_batch", 255), ("lat_max", -1), ("lat_max", 1 << 33),
+                     ("pipe_chunk", 100), ("no_such_option", 1)):
+        with pytest.raises(gvm.GpuVerifyError):
+            ver.set_option(key, val)

@@ -1,5 +1,5 @@
-// Host build of csrc/secp_field26.cuh for tests/test_field26_host.py (ctypes).
-#include "../../cosmos-sdk-rootchain_amd/csrc/secp_field26.cuh"
+// Host build of tools/field26/secp_field26.cuh (the 10 x 26 prototype, not in the product tree) for tests/test_field26_host.py (ctypes).
+#include "secp_field26.cuh"
 #include <string.h>
 using namespace gv;
 static void ld(fe26& r, const u32* a) { memcpy(r.n, a, 40); }

@@ -4,7 +4,7 @@
 // (occupancy set by the kernel's VGPRs, as in k_ecmult).  Results of the two
 // representations are cross-checked (mismatch count printed).
 #include "../../cosmos-sdk-rootchain_amd/csrc/secp_group.cuh"
-#include "../../cosmos-sdk-rootchain_amd/csrc/secp_field26.cuh"
+#include "../field26/secp_field26.cuh"
 #include <stdio.h>
 
 using namespace gv;
