@@ -466,7 +466,7 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
         ex["c3_adversarial"] = X.c3_adversarial(ver, make_digest_workload, n, args.threads)
         ex["msg_path"] = X.msg_path(ver, workload_lib(), min(n, 500_000), args.threads)
         ex["c1_ante"] = X.c1_ante(ver)
-        ex["c4_multisig"] = X.c4_multisig(ver, workload_lib(), threads=args.threads)
+        ex["c4_multisig"] = X.c4_multisig(ver, workload_lib(), threads=min(args.threads, 16))
         log(f"extras in {time.perf_counter() - t:.1f}s")
         result["extras"] = ex
     ver.close()

@@ -861,6 +861,30 @@ int gv_dev_copy(gv_ctx* ctx, int dev_slot, void* dst, const void* src, size_t by
   return GV_OK;
 }
 
+int gv_dev_stream_create(gv_ctx* ctx, int dev_slot, void** stream_out) {
+  if (!ctx || !stream_out || dev_slot < 0 || dev_slot >= (int)ctx->devs.size()) return GV_EINVAL;
+  *stream_out = nullptr;
+  CK(hipSetDevice(ctx->devs[dev_slot]->id));
+  hipStream_t st = nullptr;
+  CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  *stream_out = (void*)st;
+  return GV_OK;
+}
+
+int gv_dev_stream_sync(gv_ctx* ctx, int dev_slot, void* stream) {
+  if (!ctx || !stream || dev_slot < 0 || dev_slot >= (int)ctx->devs.size()) return GV_EINVAL;
+  CK(hipSetDevice(ctx->devs[dev_slot]->id));
+  CK(hipStreamSynchronize((hipStream_t)stream));
+  return GV_OK;
+}
+
+int gv_dev_stream_destroy(gv_ctx* ctx, int dev_slot, void* stream) {
+  if (!ctx || !stream || dev_slot < 0 || dev_slot >= (int)ctx->devs.size()) return GV_EINVAL;
+  CK(hipSetDevice(ctx->devs[dev_slot]->id));
+  CK(hipStreamDestroy((hipStream_t)stream));
+  return GV_OK;
+}
+
 int gv_dev_sync(gv_ctx* ctx, int dev_slot) {
   if (!ctx || dev_slot < 0 || dev_slot >= (int)ctx->devs.size()) return GV_EINVAL;
   Dev* d = ctx->devs[dev_slot];

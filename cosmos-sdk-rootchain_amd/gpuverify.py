@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "gv_set_option", "gv_last_stage_ms", "gv_strerror", "gv_debug_op", "gv_dev_alloc", "gv_dev_free",
     "gv_dev_copy", "gv_dev_sync", "gv_stage_stats", "gv_keys_load", "gv_keys_reset", "gv_keys_count",
     "gv_verify_digests_keyed", "gv_verify_msgs_keyed", "gv_dev_verify_digests_keyed", "gv_stage_stats4",
-    "gv_keys_point",
+    "gv_keys_point", "gv_dev_stream_create", "gv_dev_stream_sync", "gv_dev_stream_destroy",
 )
 
 
@@ -96,6 +96,12 @@ def load(path: str = LIB_PATH):
     L.gv_dev_copy.restype = i32
     L.gv_dev_sync.argtypes = [vp, i32]
     L.gv_dev_sync.restype = i32
+    L.gv_dev_stream_create.argtypes = [vp, i32, ctypes.POINTER(vp)]
+    L.gv_dev_stream_create.restype = i32
+    L.gv_dev_stream_sync.argtypes = [vp, i32, vp]
+    L.gv_dev_stream_sync.restype = i32
+    L.gv_dev_stream_destroy.argtypes = [vp, i32, vp]
+    L.gv_dev_stream_destroy.restype = i32
     L.gv_stage_stats.argtypes = [vp, i32, ctypes.POINTER(i32)] + [ctypes.POINTER(ctypes.c_double)] * 3
     L.gv_stage_stats.restype = i32
     L.gv_stage_stats4.argtypes = [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double)]
@@ -305,6 +311,17 @@ class Verifier:
 
     def dev_sync(self, slot: int = 0):
         _check(self._L.gv_dev_sync(self._ctx, slot), "gv_dev_sync")
+
+    def stream_create(self, slot: int = 0) -> int:
+        p = ctypes.c_void_p()
+        _check(self._L.gv_dev_stream_create(self._ctx, slot, ctypes.byref(p)), "gv_dev_stream_create")
+        return p.value
+
+    def stream_sync(self, stream: int, slot: int = 0):
+        _check(self._L.gv_dev_stream_sync(self._ctx, slot, ctypes.c_void_p(stream)), "gv_dev_stream_sync")
+
+    def stream_destroy(self, stream: int, slot: int = 0):
+        _check(self._L.gv_dev_stream_destroy(self._ctx, slot, ctypes.c_void_p(stream)), "gv_dev_stream_destroy")
 
     def stage_stats(self, slot: int = 0):
         c = ctypes.c_int()

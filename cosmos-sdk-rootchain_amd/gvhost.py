@@ -3,8 +3,11 @@ of the reference's signature-verification ante decorators over libgpuverify.
 
   HostApp.ante(tx)        SetPubKey -> ValidateSigCount -> SigGasConsume ->
                           BatchSigVerification -> IncrementSequence
-                          (x/auth/ante/ante.go:13-31, sigverify.go)
+                          (x/auth/ante/ante.go:13-31, sigverify.go) on an amino StdTx
   HostApp.preverify(txs)  block pre-verification hook
+  HostApp.deliver_block   PreVerifyTxs + the DeliverTx ante loop (baseapp/abci.go:203-221)
+  HostApp.deliver_gentxs  genutil.DeliverGenTxs (x/genutil/gentx.go:96-114)
+  HostApp.checktx(tx)     CheckTx through the accumulation window (thread-safe)
 """
 from __future__ import annotations
 
@@ -21,11 +24,19 @@ GVH_OK, GVH_EINVAL, GVH_EDEVICE, GVH_ENOVERIFIER = 0, -1, -2, -3
 
 class Result(ctypes.Structure):
     _fields_ = [("code", ctypes.c_uint32), ("codespace", ctypes.c_char * 16), ("log", ctypes.c_char * 512),
-                ("gas_used", ctypes.c_uint64), ("gpu_leaves", ctypes.c_uint32), ("cache_hits", ctypes.c_uint32)]
+                ("gas_used", ctypes.c_uint64), ("gpu_leaves", ctypes.c_uint32), ("cache_hits", ctypes.c_uint32),
+                ("gas_wanted", ctypes.c_uint64)]
 
     def as_dict(self):
         return {"code": self.code, "codespace": self.codespace.decode(), "log": self.log.decode(),
-                "gas_used": self.gas_used, "gpu_leaves": self.gpu_leaves, "cache_hits": self.cache_hits}
+                "gas_used": self.gas_used, "gpu_leaves": self.gpu_leaves, "cache_hits": self.cache_hits,
+                "gas_wanted": self.gas_wanted}
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_uint64) for k in ("gpu_calls", "gpu_leaves", "cache_hits", "cache_misses", "memo_hits",
+                                               "windows", "window_txs", "cache_entries", "cache_capacity",
+                                               "preverify_ns", "gpu_ns", "deliver_loop_ns")]
 
 
 _L = None
@@ -58,6 +69,15 @@ def lib():
         L.gvh_pubkey_address.argtypes = [ctypes.c_char_p, sz, vp]
         L.gvh_bech32_address.argtypes = [ctypes.c_char_p, vp, sz]
         L.gvh_bech32_address.restype = sz
+        cpp = ctypes.POINTER(ctypes.c_char_p)
+        L.gvh_deliver_block.argtypes = [vp, sz, cpp, ctypes.POINTER(sz), ctypes.POINTER(Result)]
+        L.gvh_deliver_gentxs.argtypes = [vp, sz, cpp, ctypes.POINTER(sz), ctypes.POINTER(Result), ctypes.POINTER(sz)]
+        L.gvh_checktx.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(Result)]
+        L.gvh_set_window.argtypes = [vp, sz, ctypes.c_int64]
+        L.gvh_set_cache_capacity.argtypes = [vp, sz]
+        L.gvh_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+        L.gvh_tx_sign_bytes.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, u64, u64, vp, sz, vp, sz]
+        L.gvh_tx_sign_bytes.restype = sz
         _L = L
     return _L
 
@@ -83,6 +103,23 @@ def std_sign_bytes(chain_id: str, accnum: int, seq: int, fee_json: str, msgs_jso
     lib().gvh_std_sign_bytes(chain_id.encode(), accnum, seq, fee_json.encode(), arr, len(msgs_json), memo.encode(),
                              buf, n)
     return buf.raw
+
+
+def tx_sign_bytes(tx: bytes, chain_id: str, accnum: int, seq: int) -> bytes:
+    """DefaultTxDecoder + StdTx.GetSignBytes; raises ValueError(decode error) if the tx does not decode."""
+    cap = 1 << 16
+    out = ctypes.create_string_buffer(cap)
+    err = ctypes.create_string_buffer(512)
+    n = lib().gvh_tx_sign_bytes(tx, len(tx), chain_id.encode(), accnum, seq, out, cap, err, 512)
+    if n == 0:
+        raise ValueError(err.value.decode())
+    return out.raw[:n]
+
+
+def _arrays(txs):
+    arr = (ctypes.c_char_p * max(1, len(txs)))(*txs)
+    lens = (ctypes.c_size_t * max(1, len(txs)))(*[len(t) for t in txs])
+    return arr, lens
 
 
 class HostApp:
@@ -125,11 +162,64 @@ class HostApp:
         return rc, r.as_dict()
 
     def preverify(self, txs):
-        arr = (ctypes.c_char_p * len(txs))(*txs)
-        lens = (ctypes.c_size_t * len(txs))(*[len(t) for t in txs])
+        arr, lens = _arrays(txs)
         n = ctypes.c_size_t()
         rc = self._L.gvh_preverify(self._app, len(txs), arr, lens, ctypes.byref(n))
         return rc, n.value
+
+    def deliver_block(self, txs):
+        """(rc, [result dict per tx])"""
+        arr, lens = _arrays(txs)
+        res = (Result * max(1, len(txs)))()
+        rc = self._L.gvh_deliver_block(self._app, len(txs), arr, lens, res)
+        return rc, [res[i].as_dict() for i in range(len(txs))]
+
+    def deliver_block_codes(self, txs):
+        """Same, returning only (rc, numpy array of codes) -- cheap for large blocks."""
+        import numpy as np
+        arr, lens = _arrays(txs)
+        res = (Result * max(1, len(txs)))()
+        rc = self._L.gvh_deliver_block(self._app, len(txs), arr, lens, res)
+        codes = np.frombuffer(res, dtype=np.dtype([("code", "<u4"), ("rest", "V%d" % (ctypes.sizeof(Result) - 4))]),
+                              count=len(txs))["code"].copy()
+        return rc, codes
+
+    def deliver_block_blob(self, blob, offs, lens):
+        """A block held in one contiguous buffer (numpy u8 blob, u64 offsets, u64
+        lengths): no per-tx Python objects.  Returns (rc, codes u32 array)."""
+        import numpy as np
+        n = len(offs)
+        ptrs = (np.uint64(blob.ctypes.data) + offs.astype(np.uint64)).astype(np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        res = (Result * max(1, n))()
+        rc = self._L.gvh_deliver_block(self._app, n, ptrs.ctypes.data_as(ctypes.POINTER(ctypes.c_char_p)),
+                                       lens.ctypes.data_as(ctypes.POINTER(ctypes.c_size_t)), res)
+        codes = np.frombuffer(res, dtype=np.dtype([("code", "<u4"), ("rest", "V%d" % (ctypes.sizeof(Result) - 4))]),
+                              count=n)["code"].copy()
+        return rc, codes
+
+    def deliver_gentxs(self, txs):
+        arr, lens = _arrays(txs)
+        res = (Result * max(1, len(txs)))()
+        first = ctypes.c_size_t()
+        rc = self._L.gvh_deliver_gentxs(self._app, len(txs), arr, lens, res, ctypes.byref(first))
+        return rc, [res[i].as_dict() for i in range(len(txs))], first.value
+
+    def checktx(self, tx: bytes):
+        r = Result()
+        rc = self._L.gvh_checktx(self._app, tx, len(tx), ctypes.byref(r))
+        return rc, r.as_dict()
+
+    def set_window(self, max_txs: int, max_wait_us: int):
+        self._L.gvh_set_window(self._app, max_txs, max_wait_us)
+
+    def set_cache_capacity(self, entries: int):
+        self._L.gvh_set_cache_capacity(self._app, entries)
+
+    def stats(self):
+        st = Stats()
+        self._L.gvh_get_stats(self._app, ctypes.byref(st))
+        return {k: getattr(st, k) for k, _ in Stats._fields_}
 
     def consume_sig_gas(self, sig: bytes, pub_amino: bytes | None, gas_limit: int = 0):
         r = Result()

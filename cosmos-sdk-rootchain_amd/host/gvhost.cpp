@@ -1,7 +1,16 @@
 // gvhost.cpp -- host-side mirror of the reference's signature-verification
-// ante path (see gvhost.h for the file:line map), batching every secp256k1
-// leaf of a transaction (or of a whole block via gvh_preverify) into one
-// libgpuverify call.
+// ante path and the baseapp batching hooks around it (see gvhost.h for the
+// file:line map).  Every secp256k1 leaf of a transaction, a block or a CheckTx
+// window is answered from a bounded verdict cache or verified in one
+// libgpuverify batch.
+//
+// Block path (PreVerifyTxs / DeliverBlock): txs are decoded and every
+// signer's sign bytes predicted in parallel (sequence = state + earlier txs of
+// the same signer in the block), the verdict-cache misses go to the GPU in one
+// call with no app lock held, and the decode + per-signer plans are memoised
+// so the serial DeliverTx loop only checks each prediction against the state
+// and reads the cache.  A wrong prediction is a cache miss, never a different
+// verdict: the ante run rebuilds the sign bytes from the actual state.
 #include "gvhost.h"
 
 #include <openssl/evp.h>
@@ -10,13 +19,14 @@
 
 #include <algorithm>
 #include <array>
-#include <chrono>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
-#include <map>
 #include <memory>
 #include <mutex>
+#include <random>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -26,6 +36,8 @@
 namespace {
 
 using Bytes = std::vector<uint8_t>;
+using Addr = std::array<uint8_t, 20>;
+using H32 = std::array<uint8_t, 32>;
 
 // ------------------------------------------------------------------ errors
 // sdkerrors codes (types/errors/errors.go)
@@ -33,7 +45,7 @@ constexpr uint32_t kErrTxDecode = 2, kErrUnauthorized = 4, kErrInvalidPubKey = 8
                    kErrOutOfGas = 11, kErrTooManySignatures = 14, kErrPanic = 111222;
 
 struct SdkError {
-  uint32_t code;
+  uint32_t code = 0;
   std::string codespace;
   std::string log;
 };
@@ -55,26 +67,37 @@ SdkError wrap(uint32_t code, const std::string& msg) {
   return SdkError{code, code == kErrPanic ? "undefined" : "sdk", msg + ": " + err_desc(code)};
 }
 
-// Thrown where the reference panics (amino MustUnmarshal, index out of range);
-// runTx recovers it into ErrPanic (baseapp/baseapp.go:490-512).
+// Thrown where the reference panics (amino MustUnmarshal, index out of range,
+// nil interface); runTx recovers it into ErrPanic (baseapp/baseapp.go:490-512).
 struct Panic : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 struct OutOfGas {
   std::string descriptor;
 };
+// go-amino decode error (DefaultTxDecoder wraps it into ErrTxDecode)
+struct AminoErr : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
 
 // ---------------------------------------------------------------- hashing
-// The one-shot SHA256() of OpenSSL 3 fetches the digest through the provider
-// store on every call (a global lock: no scaling across PreVerifyTxs threads);
-// the context API hashes with no shared state.
-std::array<uint8_t, 32> sha256(const uint8_t* p, size_t n) {
-  std::array<uint8_t, 32> o;
+// OpenSSL's one-shot SHA256() fetches the digest from the provider store on
+// every call (a global lock); the context API hashes with no shared state.
+struct Sha256 {
   SHA256_CTX c;
-  SHA256_Init(&c);
-  SHA256_Update(&c, p, n);
-  SHA256_Final(o.data(), &c);
-  return o;
+  Sha256() { SHA256_Init(&c); }
+  void up(const void* p, size_t n) { SHA256_Update(&c, p, n); }
+  void up(const std::string& s) { SHA256_Update(&c, s.data(), s.size()); }
+  H32 fin() {
+    H32 o;
+    SHA256_Final(o.data(), &c);
+    return o;
+  }
+};
+H32 sha256(const uint8_t* p, size_t n) {
+  Sha256 h;
+  h.up(p, n);
+  return h.fin();
 }
 
 // ------------------------------------------------------------------ bech32
@@ -112,17 +135,19 @@ std::string bech32(const std::string& hrp, const uint8_t* data, size_t n) {
   for (int i = 0; i < 6; ++i) out += CS[(pm >> (5 * (5 - i))) & 31];
   return out;
 }
-std::string acc_string(const std::array<uint8_t, 20>& a) { return bech32("cosmos", a.data(), 20); }
+// sdk.AccAddress.String(): "" for an empty address (types/address.go:222-234)
+std::string acc_string(const uint8_t* a, size_t n) { return n ? bech32("cosmos", a, n) : std::string(); }
+std::string acc_string(const Bytes& a) { return acc_string(a.data(), a.size()); }
 
 // --------------------------------------------------- Go encoding/json strings
 // json.Marshal(string): escapes '"', '\\', control chars, HTML <>&, U+2028/9;
 // invalid UTF-8 becomes U+FFFD.
-std::string go_json_string(const std::string& s) {
-  std::string o = "\"";
+void go_json_string(std::string& o, const uint8_t* s, size_t n) {
   static const char* hex = "0123456789abcdef";
+  o += '"';
   size_t i = 0;
-  while (i < s.size()) {
-    unsigned char c = (unsigned char)s[i];
+  while (i < n) {
+    unsigned char c = s[i];
     if (c < 0x80) {
       if (c == '"' || c == '\\') { o += '\\'; o += (char)c; }
       else if (c == '\n') o += "\\n";
@@ -134,14 +159,13 @@ std::string go_json_string(const std::string& s) {
       ++i;
       continue;
     }
-    // decode one UTF-8 sequence
     int len = (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
     uint32_t cp = 0;
-    bool ok = len && i + len <= s.size();
+    bool ok = len && i + len <= n;
     if (ok) {
       cp = c & (0x7F >> len);
       for (int k = 1; k < len; ++k) {
-        unsigned char cc = (unsigned char)s[i + k];
+        unsigned char cc = s[i + k];
         if ((cc & 0xC0) != 0x80) { ok = false; break; }
         cp = (cp << 6) | (cc & 0x3F);
       }
@@ -150,145 +174,471 @@ std::string go_json_string(const std::string& s) {
         ok = false;
     }
     if (!ok) { o += "\xEF\xBF\xBD"; ++i; continue; }
-    if (cp == 0x2028 || cp == 0x2029) { o += cp == 0x2028 ? "\\u2028" : "\\u2029"; }
-    else o.append(s, i, len);
+    if (cp == 0x2028 || cp == 0x2029) o += cp == 0x2028 ? "\\u2028" : "\\u2029";
+    else o.append((const char*)s + i, len);
     i += len;
   }
-  return o + "\"";
+  o += '"';
+}
+void go_json_string(std::string& o, const std::string& s) { go_json_string(o, (const uint8_t*)s.data(), s.size()); }
+std::string go_json_string(const std::string& s) {
+  std::string o;
+  go_json_string(o, s);
+  return o;
 }
 
 // ------------------------------------------------------------------- amino
-// Registered prefixes (crypto/encode_test.go:51-60, tendermint crypto codec).
-const uint8_t kPrefixSecp[4] = {0xEB, 0x5A, 0xE9, 0x87};
-const uint8_t kPrefixEd[4] = {0x16, 0x24, 0xDE, 0x64};
-const uint8_t kPrefixMulti[4] = {0x22, 0xC1, 0xF7, 0xE2};
+// go-amino v0.15.1 (go.mod:30) binary decoding, restated: uvarint keys
+// (field << 3 | typ3), fields in increasing order, repeated (unpacked list)
+// fields as consecutive entries, unknown fields only after the known ones,
+// registered concrete types behind a 4-byte prefix (optionally preceded by
+// 0x00 + 3 disambiguation bytes).
+struct Span {
+  const uint8_t* p = nullptr;
+  size_t n = 0;
+};
 
 struct Reader {
   const uint8_t* p;
   size_t n, i = 0;
-  Reader(const uint8_t* p_, size_t n_) : p(p_), n(n_) {}
+  Reader(Span s) : p(s.p), n(s.n) {}
   bool done() const { return i >= n; }
-  uint64_t uvarint() {
-    uint64_t v = 0;
-    for (int s = 0; s < 64; s += 7) {
-      if (i >= n) throw Panic("EOF reading uvarint");
-      uint8_t b = p[i++];
-      v |= (uint64_t)(b & 0x7F) << s;
-      if (!(b & 0x80)) return v;
+  uint64_t uvarint() {                        // encoding/binary.Uvarint
+    uint64_t x = 0;
+    unsigned s = 0;
+    for (int k = 0; k < 10; ++k) {
+      if (i >= n) throw AminoErr("EOF decoding uvarint");
+      const uint8_t b = p[i++];
+      if (b < 0x80) {
+        if (k == 9 && b > 1) throw AminoErr("EOF decoding uvarint");
+        return x | (uint64_t)b << s;
+      }
+      x |= (uint64_t)(b & 0x7F) << s;
+      s += 7;
     }
-    throw Panic("uvarint overflow");
+    throw AminoErr("EOF decoding uvarint");
   }
-  Bytes bytes() {
-    uint64_t len = uvarint();
-    if (len > n - i) throw Panic("byte slice length out of range");
-    Bytes b(p + i, p + i + len);
-    i += len;
-    return b;
+  void key(uint32_t& f, int& t) {
+    const uint64_t v = uvarint();
+    t = (int)(v & 7);
+    if ((v >> 3) > (1u << 29) - 1) throw AminoErr("invalid field num");
+    f = (uint32_t)(v >> 3);
+  }
+  Span bytes() {
+    const uint64_t l = uvarint();
+    if (l > n - i) throw AminoErr("insufficient bytes decoding byteslice");
+    Span s{p + i, (size_t)l};
+    i += (size_t)l;
+    return s;
+  }
+  void skip(int t) {
+    switch (t) {
+      case 0: uvarint(); break;
+      case 1: if (n - i < 8) throw AminoErr("EOF decoding 8 bytes"); i += 8; break;
+      case 2: bytes(); break;
+      case 5: if (n - i < 4) throw AminoErr("EOF decoding 4 bytes"); i += 4; break;
+      default: throw AminoErr("invalid typ3 byte");
+    }
   }
 };
 
+struct FSpec {
+  uint32_t num;
+  int typ;
+  bool rep;
+};
+// Walk the fields of one amino struct encoding; fn(field, reader) consumes the value.
+template <size_t K, class F>
+void for_fields(Span s, const FSpec (&spec)[K], F&& fn) {
+  Reader r(s);
+  uint32_t last = 0, maxk = 0;
+  for (const FSpec& f : spec) maxk = std::max(maxk, f.num);
+  while (!r.done()) {
+    uint32_t f;
+    int t;
+    r.key(f, t);
+    const FSpec* fs = nullptr;
+    for (const FSpec& x : spec)
+      if (x.num == f) fs = &x;
+    if (!(fs && fs->rep && f == last) && f <= last)
+      throw AminoErr("encountered fieldNum: " + std::to_string(f) + ", but we have already seen fnum: " +
+                     std::to_string(last));
+    last = f;
+    if (!fs) {
+      if (f < maxk) throw AminoErr("expected field # of struct, got " + std::to_string(f));
+      r.skip(t);
+      continue;
+    }
+    if (t != fs->typ) throw AminoErr("expected field type for # " + std::to_string(f));
+    fn(f, r);
+  }
+}
+
+// amino name -> (disambiguation, prefix): SHA256(name), skip zero bytes, 3
+// disambiguation bytes, skip zero bytes, 4 prefix bytes.  Reproduces the
+// pinned prefixes of crypto/encode_test.go:58-59.
+struct Disfix {
+  uint8_t d[3], p[4];
+};
+Disfix disfix(const char* name) {
+  const H32 h = sha256((const uint8_t*)name, strlen(name));
+  size_t i = 0;
+  while (h[i] == 0) ++i;
+  Disfix r;
+  memcpy(r.d, &h[i], 3);
+  i += 3;
+  while (h[i] == 0) ++i;
+  memcpy(r.p, &h[i], 4);
+  return r;
+}
+const Disfix kSecp = disfix("tendermint/PubKeySecp256k1"), kEd = disfix("tendermint/PubKeyEd25519"),
+             kMulti = disfix("tendermint/PubKeyMultisigThreshold"), kStdTx = disfix("cosmos-sdk/StdTx"),
+             kMsgSend = disfix("cosmos-sdk/MsgSend"), kMsgMultiSend = disfix("cosmos-sdk/MsgMultiSend");
+
+// Interface value: consumes the disambiguation/prefix bytes; returns the
+// registered type among `types` (index) and leaves r at the concrete body.
+int interface_type(Span s, Span* body, std::initializer_list<const Disfix*> types) {
+  size_t off;
+  const uint8_t* pre;
+  const uint8_t* dis = nullptr;
+  if (s.n >= 8 && s.p[0] == 0x00) { dis = s.p + 1; pre = s.p + 4; off = 8; }
+  else if (s.n >= 4) { pre = s.p; off = 4; }
+  else throw AminoErr("EOF reading prefix bytes");
+  int k = 0;
+  for (const Disfix* t : types) {
+    if (!memcmp(pre, t->p, 4) && (!dis || !memcmp(dis, t->d, 3))) {
+      *body = Span{s.p + off, s.n - off};
+      return k;
+    }
+    ++k;
+  }
+  throw AminoErr("unrecognized prefix bytes");
+}
+
+// ---------------------------------------------------------------- sdk.Int
+// Int.Unmarshal (types/int.go:385-405): big.Int.UnmarshalText (Go
+// SetString base 0: sign, 0b/0o/0x/0 prefixes, '_' separators) and at most 255
+// bits; the sign-bytes JSON then prints the canonical decimal
+// (marshalJSON, types/int.go:332-339).  nil (no bytes) prints "0".
+std::string int_text_canonical(Span s) {
+  if (s.n == 0) return "0";
+  const uint8_t* p = s.p;
+  size_t i = 0, n = s.n;
+  bool neg = false;
+  if (p[i] == '+' || p[i] == '-') { neg = p[i] == '-'; ++i; }
+  unsigned base = 10;
+  char prefix = 0;
+  char prev = '.';
+  size_t count = 0;
+  if (i < n && p[i] == '0') {
+    prev = '0';
+    count = 1;
+    ++i;
+    if (i < n) {
+      switch (p[i]) {
+        case 'b': case 'B': base = 2; prefix = 'b'; break;
+        case 'o': case 'O': base = 8; prefix = 'o'; break;
+        case 'x': case 'X': base = 16; prefix = 'x'; break;
+        default: base = 8; prefix = '0'; break;
+      }
+      count = 0;
+      if (prefix != '0') ++i;
+    }
+  }
+  uint64_t w[5] = {0, 0, 0, 0, 0};                 // magnitude, little-endian 64-bit limbs (320 bits)
+  bool inval_sep = false;
+  for (; i < n; ++i) {
+    const uint8_t ch = p[i];
+    if (ch == '_') {
+      if (prev != '0') inval_sep = true;
+      prev = '_';
+      continue;
+    }
+    unsigned d = 99;
+    if (ch >= '0' && ch <= '9') d = ch - '0';
+    else if (ch >= 'a' && ch <= 'z') d = ch - 'a' + 10;
+    else if (ch >= 'A' && ch <= 'Z') d = ch - 'A' + 10;
+    if (d >= base) break;
+    prev = '0';
+    ++count;
+    unsigned __int128 c = d;
+    for (auto& x : w) {
+      c += (unsigned __int128)x * base;
+      x = (uint64_t)c;
+      c >>= 64;
+    }
+    if (c || w[4] >> 32) throw AminoErr("integer out of range");
+  }
+  if (count == 0 && prefix != '0') throw AminoErr("math/big: cannot unmarshal into a *big.Int");
+  if (i != n) throw AminoErr("math/big: cannot unmarshal into a *big.Int");
+  if (inval_sep || prev == '_') throw AminoErr("math/big: cannot unmarshal into a *big.Int");
+  if (w[4] || (w[3] >> 63)) throw AminoErr("integer out of range");   // BitLen > 255
+  std::string dec;
+  uint64_t t[4] = {w[0], w[1], w[2], w[3]};
+  for (;;) {
+    bool zero = !(t[0] | t[1] | t[2] | t[3]);
+    if (zero) break;
+    unsigned __int128 rem = 0;
+    for (int k = 3; k >= 0; --k) {
+      unsigned __int128 cur = (rem << 64) | t[k];
+      t[k] = (uint64_t)(cur / 10);
+      rem = cur % 10;
+    }
+    dec += (char)('0' + (int)rem);
+  }
+  if (dec.empty()) return "0";
+  if (neg) dec += '-';
+  std::reverse(dec.begin(), dec.end());
+  return dec;
+}
+
+// ------------------------------------------------------------ msgs, StdTx
+// sdk.Coin amino (types/types.pb.go:33-36: Denom field 1, Amount field 2);
+// JSON {"amount":"N","denom":"d"} with denom omitempty.
+void coin_json(std::string& o, Span s) {
+  std::string denom, amount = "0";
+  bool has_denom = false;
+  static const FSpec spec[] = {{1, 2, false}, {2, 2, false}};
+  for_fields(s, spec, [&](uint32_t f, Reader& r) {
+    Span b = r.bytes();
+    if (f == 1) { denom.assign((const char*)b.p, b.n); has_denom = b.n > 0; }
+    else amount = int_text_canonical(b);
+  });
+  o += "{\"amount\":\"";
+  o += amount;
+  o += '"';
+  if (has_denom) { o += ",\"denom\":"; go_json_string(o, denom); }
+  o += '}';
+}
+// sdk.Coins (repeated Coin) as JSON: null when absent (amino encodes a nil slice as null)
+struct CoinsJson {
+  std::string s;
+  bool any = false;
+  void add(Span c) {
+    s += any ? "," : "[";
+    any = true;
+    coin_json(s, c);
+  }
+  std::string done() const { return any ? s + "]" : "null"; }
+};
+
+struct Msg {
+  std::string json;                 // Msg.GetSignBytes(): MustSortJSON(amino JSON)
+  std::vector<Bytes> signers;       // Msg.GetSigners()
+};
+
+// x/bank MsgSend (types.pb.go:30-34): from field 1, to field 2, amount field 3;
+// GetSignBytes / GetSigners at x/bank/types/msgs.go:43-50.
+Msg decode_msg_send(Span body) {
+  Msg m;
+  Bytes from, to;
+  CoinsJson coins;
+  static const FSpec spec[] = {{1, 2, false}, {2, 2, false}, {3, 2, true}};
+  for_fields(body, spec, [&](uint32_t f, Reader& r) {
+    Span b = r.bytes();
+    if (f == 1) from.assign(b.p, b.p + b.n);
+    else if (f == 2) to.assign(b.p, b.p + b.n);
+    else coins.add(b);
+  });
+  std::string& o = m.json;
+  o = "{\"type\":\"cosmos-sdk/MsgSend\",\"value\":{\"amount\":" + coins.done();
+  if (!from.empty()) { o += ",\"from_address\":\"" + acc_string(from) + "\""; }
+  if (!to.empty()) { o += ",\"to_address\":\"" + acc_string(to) + "\""; }
+  o += "}}";
+  m.signers.push_back(std::move(from));
+  return m;
+}
+// x/bank MsgMultiSend: inputs field 1, outputs field 2; Input/Output {address 1, coins 2}
+// (types.pb.go:91-94,144-147); GetSigners = input addresses (msgs.go:86-90).
+Msg decode_msg_multisend(Span body) {
+  Msg m;
+  std::string ins, outs;
+  bool any_in = false, any_out = false;
+  static const FSpec spec[] = {{1, 2, true}, {2, 2, true}};
+  for_fields(body, spec, [&](uint32_t f, Reader& r) {
+    Span io = r.bytes();
+    Bytes addr;
+    CoinsJson coins;
+    static const FSpec ispec[] = {{1, 2, false}, {2, 2, true}};
+    for_fields(io, ispec, [&](uint32_t g, Reader& r2) {
+      Span b = r2.bytes();
+      if (g == 1) addr.assign(b.p, b.p + b.n);
+      else coins.add(b);
+    });
+    std::string& o = f == 1 ? ins : outs;
+    bool& any = f == 1 ? any_in : any_out;
+    o += any ? "," : "[";
+    any = true;
+    o += "{";
+    if (!addr.empty()) o += "\"address\":\"" + acc_string(addr) + "\",";
+    o += "\"coins\":" + coins.done() + "}";
+    if (f == 1) m.signers.push_back(std::move(addr));
+  });
+  m.json = "{\"type\":\"cosmos-sdk/MsgMultiSend\",\"value\":{\"inputs\":" + (any_in ? ins + "]" : std::string("null")) +
+           ",\"outputs\":" + (any_out ? outs + "]" : std::string("null")) + "}}";
+  return m;
+}
+
+// auth.StdTx (x/auth/types/stdtx.go:147-152): Msgs field 1 (interface list),
+// Fee field 2 {Amount 1, Gas 2}, Signatures field 3 {PubKey 1, Signature 2},
+// Memo field 4.  Owns its bytes; spans point into them.
+struct Tx {
+  Bytes raw;
+  std::vector<Msg> msgs;
+  bool nil_msg = false;
+  std::string fee_json;
+  uint64_t gas = 0;
+  std::string memo;
+  struct Sig {
+    Span pub, sig;
+  };
+  std::vector<Sig> sigs;
+  std::vector<Bytes> signers;       // StdTx.GetSigners(): msg signers, deduplicated in order
+  std::string sb_tail;              // sign bytes after chain_id: ,"fee":..,"memo":..,"msgs":[..],"sequence":"
+  Tx() = default;
+  Tx(const Tx&) = delete;
+  Tx& operator=(const Tx&) = delete;
+};
+
+// DefaultTxDecoder (stdtx.go:321-338): cdc.UnmarshalBinaryBare(txBytes, &StdTx{}).
+std::shared_ptr<Tx> decode_tx(const uint8_t* p, size_t n) {
+  auto tx = std::make_shared<Tx>();
+  if (n == 0) throw AminoErr("tx bytes are empty");
+  tx->raw.assign(p, p + n);
+  if (n < 4 || memcmp(p, kStdTx.p, 4))
+    throw AminoErr("UnmarshalBinaryBare expected to read prefix bytes (since it is registered concrete)");
+  CoinsJson fee;
+  bool has_fee = false;
+  static const FSpec spec[] = {{1, 2, true}, {2, 2, false}, {3, 2, true}, {4, 2, false}};
+  for_fields(Span{tx->raw.data() + 4, n - 4}, spec, [&](uint32_t f, Reader& r) {
+    Span b = r.bytes();
+    if (f == 1) {
+      if (b.n == 0) { tx->nil_msg = true; tx->msgs.emplace_back(); return; }
+      Span body;
+      const int k = interface_type(b, &body, {&kMsgSend, &kMsgMultiSend});
+      tx->msgs.push_back(k == 0 ? decode_msg_send(body) : decode_msg_multisend(body));
+    } else if (f == 2) {
+      has_fee = true;
+      static const FSpec fspec[] = {{1, 2, true}, {2, 0, false}};
+      for_fields(b, fspec, [&](uint32_t g, Reader& r2) {
+        if (g == 1) fee.add(r2.bytes());
+        else tx->gas = r2.uvarint();
+      });
+    } else if (f == 3) {
+      Tx::Sig sg;
+      static const FSpec sspec[] = {{1, 2, false}, {2, 2, false}};
+      for_fields(b, sspec, [&](uint32_t g, Reader& r2) {
+        if (g == 1) sg.pub = r2.bytes();
+        else sg.sig = r2.bytes();
+      });
+      tx->sigs.push_back(sg);
+    } else {
+      tx->memo.assign((const char*)b.p, b.n);
+    }
+  });
+  (void)has_fee;
+  // StdFee.Bytes() (stdtx.go:47-58): an empty amount is normalised to [] (not null)
+  tx->fee_json = "{\"amount\":" + (fee.any ? fee.s + "]" : std::string("[]")) + ",\"gas\":\"" +
+                 std::to_string(tx->gas) + "\"}";
+  if (!tx->nil_msg) {
+    for (const Msg& m : tx->msgs)
+      for (const Bytes& a : m.signers) {
+        bool seen = false;
+        for (const Bytes& s : tx->signers) seen = seen || s == a;
+        if (!seen) tx->signers.push_back(a);
+      }
+  }
+  // StdSignBytes (stdtx.go:292-312): the StdSignDoc keys are in sorted order and
+  // every embedded JSON is canonical, so composing the pieces equals
+  // MustSortJSON(amino.MarshalJSON(StdSignDoc{...})).
+  std::string& t = tx->sb_tail;
+  t = ",\"fee\":" + tx->fee_json + ",\"memo\":";
+  go_json_string(t, tx->memo);
+  t += ",\"msgs\":[";
+  for (size_t i = 0; i < tx->msgs.size(); ++i) {
+    if (i) t += ",";
+    t += tx->msgs[i].json;
+  }
+  t += "],\"sequence\":\"";
+  return tx;
+}
+
+// ------------------------------------------------------------- pubkeys
 struct PubKey {
-  enum Kind { Secp256k1, Ed25519, Multisig } kind;
+  enum Kind { Nil, Secp256k1, Ed25519, Multisig } kind = Nil;
   std::array<uint8_t, 33> secp{};
   std::array<uint8_t, 32> ed{};
   uint64_t k = 0;
   std::vector<PubKey> subs;
-  Bytes amino;   // the exact bytes (multisig address)
 };
 
-PubKey decode_pubkey(const uint8_t* p, size_t n, int depth = 0) {
-  if (depth > 8) throw Panic("multisig nesting too deep");
-  if (n < 4) throw Panic("amino: prefix too short");
+// crypto.PubKey amino interface (tendermint crypto codec; prefixes pinned by
+// crypto/encode_test.go:51-60): secp256k1 [33]byte, ed25519 [32]byte,
+// PubKeyMultisigThreshold {K uint field 1, PubKeys []PubKey field 2}.
+PubKey decode_pubkey_body(Span s, int depth) {
+  if (depth > 16) throw AminoErr("multisig nesting too deep");
   PubKey pk;
-  pk.amino.assign(p, p + n);
-  Reader r(p + 4, n - 4);
-  if (!memcmp(p, kPrefixSecp, 4)) {
-    pk.kind = PubKey::Secp256k1;
-    Bytes b = r.bytes();
-    if (b.size() != 33 || !r.done()) throw Panic("amino: bad secp256k1 pubkey");
-    memcpy(pk.secp.data(), b.data(), 33);
-  } else if (!memcmp(p, kPrefixEd, 4)) {
-    pk.kind = PubKey::Ed25519;
-    Bytes b = r.bytes();
-    if (b.size() != 32 || !r.done()) throw Panic("amino: bad ed25519 pubkey");
-    memcpy(pk.ed.data(), b.data(), 32);
-  } else if (!memcmp(p, kPrefixMulti, 4)) {
-    pk.kind = PubKey::Multisig;
-    int last_field = 0;
-    while (!r.done()) {
-      uint64_t key = r.uvarint();
-      int field = (int)(key >> 3), typ = (int)(key & 7);
-      if (field < last_field || (field == last_field && field != 2)) throw Panic("amino: field order");
-      last_field = field;
-      if (field == 1 && typ == 0) pk.k = r.uvarint();
-      else if (field == 2 && typ == 2) {
-        Bytes b = r.bytes();
-        pk.subs.push_back(decode_pubkey(b.data(), b.size(), depth + 1));
-      } else throw Panic("amino: unexpected field in PubKeyMultisigThreshold");
-    }
-  } else {
-    throw Panic("amino: unregistered concrete type prefix");
+  if (s.n == 0) return pk;                          // nil interface (an empty list element)
+  Span body;
+  const int k = interface_type(s, &body, {&kSecp, &kEd, &kMulti});
+  Reader r(body);
+  if (k == 0 || k == 1) {
+    const size_t want = k == 0 ? 33 : 32;
+    Span b = r.bytes();
+    if (b.n != want || !r.done()) throw AminoErr("mismatched byte array length");
+    if (k == 0) { pk.kind = PubKey::Secp256k1; memcpy(pk.secp.data(), b.p, 33); }
+    else { pk.kind = PubKey::Ed25519; memcpy(pk.ed.data(), b.p, 32); }
+    return pk;
   }
+  pk.kind = PubKey::Multisig;
+  static const FSpec spec[] = {{1, 0, false}, {2, 2, true}};
+  for_fields(body, spec, [&](uint32_t f, Reader& r2) {
+    if (f == 1) pk.k = r2.uvarint();
+    else pk.subs.push_back(decode_pubkey_body(r2.bytes(), depth + 1));
+  });
   return pk;
 }
+// amino.MustUnmarshalBinaryBare(bytes, &pk): a decode error panics (stdtx.go:91, account.go:70)
+PubKey decode_pubkey(const uint8_t* p, size_t n) {
+  try {
+    return decode_pubkey_body(Span{p, n}, 0);
+  } catch (const AminoErr& e) {
+    throw Panic(e.what());
+  }
+}
 
-// tendermint libs/bits CompactBitArray
-struct CompactBitArray {
-  bool present = false;
-  uint8_t extra = 0;
-  Bytes elems;
-  int size() const {
-    if (!present) return 0;
-    if (extra == 0) return (int)elems.size() * 8;
-    return ((int)elems.size() - 1) * 8 + extra;
-  }
-  bool get(int i) const {
-    if (i < 0 || i >= size()) return false;
-    return (elems[i >> 3] & (uint8_t)(1u << (7 - (i % 8)))) != 0;
-  }
-  int true_bits_before(int idx) const {
-    int c = 0;
-    for (int i = 0; i < idx && i < size(); ++i) c += get(i);
-    return c;
-  }
-};
-struct Multisignature {
-  CompactBitArray bits;
-  std::vector<Bytes> sigs;
-};
-Multisignature decode_multisig(const Bytes& b) {
-  Multisignature m;
-  Reader r(b.data(), b.size());
-  int last_field = 0;
-  while (!r.done()) {
-    uint64_t key = r.uvarint();
-    int field = (int)(key >> 3), typ = (int)(key & 7);
-    if (field < last_field || (field == last_field && field != 2)) throw Panic("amino: field order");
-    last_field = field;
-    if (field == 1 && typ == 2) {
-      Bytes cb = r.bytes();
-      Reader rc(cb.data(), cb.size());
-      m.bits.present = true;
-      int lf = 0;
-      while (!rc.done()) {
-        uint64_t k2 = rc.uvarint();
-        int f2 = (int)(k2 >> 3), t2 = (int)(k2 & 7);
-        if (f2 <= lf) throw Panic("amino: field order");
-        lf = f2;
-        if (f2 == 1 && t2 == 0) {
-          uint64_t v = rc.uvarint();
-          if (v > 255) throw Panic("amino: byte overflow");
-          m.bits.extra = (uint8_t)v;
-        } else if (f2 == 2 && t2 == 2) {
-          m.bits.elems = rc.bytes();
-        } else throw Panic("amino: unexpected field in CompactBitArray");
+void put_uvarint(Bytes& o, uint64_t v) {
+  while (v >= 0x80) { o.push_back((uint8_t)(v | 0x80)); v >>= 7; }
+  o.push_back((uint8_t)v);
+}
+// pk.Bytes() = cdc.MustMarshalBinaryBare(pk): the canonical encoding
+// (SetPubKey stores it, account.go:75-83; multisig Address hashes it).
+void encode_pubkey(Bytes& o, const PubKey& pk) {
+  switch (pk.kind) {
+    case PubKey::Nil: return;
+    case PubKey::Secp256k1:
+      o.insert(o.end(), kSecp.p, kSecp.p + 4); o.push_back(33); o.insert(o.end(), pk.secp.begin(), pk.secp.end());
+      return;
+    case PubKey::Ed25519:
+      o.insert(o.end(), kEd.p, kEd.p + 4); o.push_back(32); o.insert(o.end(), pk.ed.begin(), pk.ed.end());
+      return;
+    case PubKey::Multisig:
+      o.insert(o.end(), kMulti.p, kMulti.p + 4);
+      if (pk.k) { o.push_back(0x08); put_uvarint(o, pk.k); }
+      for (const PubKey& s : pk.subs) {
+        Bytes b;
+        encode_pubkey(b, s);
+        o.push_back(0x12);
+        put_uvarint(o, b.size());
+        o.insert(o.end(), b.begin(), b.end());
       }
-      if (m.bits.extra >= 8 || (m.bits.extra && m.bits.elems.empty())) throw Panic("amino: invalid CompactBitArray");
-    } else if (field == 2 && typ == 2) {
-      m.sigs.push_back(r.bytes());
-    } else throw Panic("amino: unexpected field in Multisignature");
+      return;
   }
-  return m;
+}
+Bytes pubkey_bytes(const PubKey& pk) {
+  Bytes b;
+  encode_pubkey(b, pk);
+  return b;
 }
 
 int count_subkeys(const PubKey& pk) {  // types.CountSubKeys (stdtx.go:125-137)
@@ -298,8 +648,8 @@ int count_subkeys(const PubKey& pk) {  // types.CountSubKeys (stdtx.go:125-137)
   return c;
 }
 
-std::array<uint8_t, 20> pubkey_address(const PubKey& pk) {
-  std::array<uint8_t, 20> a{};
+Addr pubkey_address(const PubKey& pk) {
+  Addr a{};
   if (pk.kind == PubKey::Secp256k1) {
     auto h = sha256(pk.secp.data(), 33);
     RIPEMD160_CTX c;                                  // context API: no provider fetch per call
@@ -309,151 +659,175 @@ std::array<uint8_t, 20> pubkey_address(const PubKey& pk) {
   } else if (pk.kind == PubKey::Ed25519) {
     auto h = sha256(pk.ed.data(), 32);
     memcpy(a.data(), h.data(), 20);
-  } else {
-    auto h = sha256(pk.amino.data(), pk.amino.size());
+  } else if (pk.kind == PubKey::Multisig) {
+    Bytes b = pubkey_bytes(pk);
+    auto h = sha256(b.data(), b.size());
     memcpy(a.data(), h.data(), 20);
+  } else {
+    throw Panic("runtime error: invalid memory address or nil pointer dereference");
   }
   return a;
 }
 
-bool ed25519_verify(const std::array<uint8_t, 32>& pub, const Bytes& msg, const Bytes& sig) {
-  if (sig.size() != 64) return false;
+bool ed25519_verify(const std::array<uint8_t, 32>& pub, const uint8_t* msg, size_t msg_len, Span sig) {
+  if (sig.n != 64) return false;
   EVP_PKEY* k = EVP_PKEY_new_raw_public_key(EVP_PKEY_ED25519, nullptr, pub.data(), 32);
   if (!k) return false;
   EVP_MD_CTX* c = EVP_MD_CTX_new();
   bool ok = c && EVP_DigestVerifyInit(c, nullptr, nullptr, nullptr, k) == 1 &&
-            EVP_DigestVerify(c, sig.data(), sig.size(), msg.data(), msg.size()) == 1;
+            EVP_DigestVerify(c, sig.p, sig.n, msg, msg_len) == 1;
   EVP_MD_CTX_free(c);
   EVP_PKEY_free(k);
   return ok;
 }
 
-// --------------------------------------------------------------- flat tx
-struct FlatTx {
-  std::vector<std::string> msgs;
-  std::string fee, memo;
-  std::vector<std::array<uint8_t, 20>> signers;
-  std::vector<Bytes> sig_pubs, sigs;
-};
-struct FlatReader {
-  const uint8_t* p;
-  size_t n, i = 0;
-  uint32_t u32() {
-    if (i + 4 > n) throw std::invalid_argument("truncated tx");
-    uint32_t v = p[i] | (p[i + 1] << 8) | (p[i + 2] << 16) | ((uint32_t)p[i + 3] << 24);
-    i += 4;
-    return v;
+// tendermint libs/bits CompactBitArray + crypto/multisig Multisignature
+struct CompactBitArray {
+  bool present = false;
+  uint8_t extra = 0;
+  Span elems;
+  int size() const {
+    if (!present) return 0;
+    if (extra == 0) return (int)elems.n * 8;
+    return ((int)elems.n - 1) * 8 + extra;
   }
-  Bytes bytes() {
-    uint32_t l = u32();
-    if (l > n - i) throw std::invalid_argument("truncated tx");
-    Bytes b(p + i, p + i + l);
-    i += l;
-    return b;
+  // GetIndex (libs/bits): indexing Elems past its end panics
+  bool get(int i) const {
+    if (i < 0 || i >= size()) return false;
+    if ((size_t)(i >> 3) >= elems.n) throw Panic("runtime error: index out of range");
+    return (elems.p[i >> 3] & (uint8_t)(1u << (7 - (i % 8)))) != 0;
+  }
+  int true_bits_before(int idx) const {
+    int c = 0;
+    for (int i = 0; i < idx && i < size(); ++i) c += get(i);
+    return c;
   }
 };
-FlatTx parse_flat(const uint8_t* p, size_t n) {
-  FlatReader r{p, n};
-  FlatTx t;
-  uint32_t nm = r.u32();
-  for (uint32_t k = 0; k < nm; ++k) { Bytes b = r.bytes(); t.msgs.emplace_back(b.begin(), b.end()); }
-  { Bytes b = r.bytes(); t.fee.assign(b.begin(), b.end()); }
-  { Bytes b = r.bytes(); t.memo.assign(b.begin(), b.end()); }
-  uint32_t ns = r.u32();
-  for (uint32_t k = 0; k < ns; ++k) {
-    if (r.i + 20 > n) throw std::invalid_argument("truncated tx");
-    std::array<uint8_t, 20> a;
-    memcpy(a.data(), p + r.i, 20);
-    r.i += 20;
-    t.signers.push_back(a);
-  }
-  uint32_t nsig = r.u32();
-  for (uint32_t k = 0; k < nsig; ++k) {
-    t.sig_pubs.push_back(r.bytes());
-    t.sigs.push_back(r.bytes());
-  }
-  if (r.i != n) throw std::invalid_argument("trailing bytes in tx");
-  return t;
+struct Multisignature {
+  CompactBitArray bits;
+  std::vector<Span> sigs;
+};
+Multisignature decode_multisig(Span s) {
+  Multisignature m;
+  static const FSpec spec[] = {{1, 2, false}, {2, 2, true}};
+  for_fields(s, spec, [&](uint32_t f, Reader& r) {
+    Span b = r.bytes();
+    if (f == 1) {
+      m.bits.present = true;
+      static const FSpec bspec[] = {{1, 0, false}, {2, 2, false}};
+      for_fields(b, bspec, [&](uint32_t g, Reader& r2) {
+        if (g == 1) {
+          const uint64_t v = r2.uvarint();
+          if (v > 255) throw AminoErr("byte overflow");
+          m.bits.extra = (uint8_t)v;
+        } else {
+          m.bits.elems = r2.bytes();
+        }
+      });
+    } else {
+      m.sigs.push_back(b);
+    }
+  });
+  return m;
 }
 
-std::string std_sign_bytes(const std::string& chain, uint64_t accnum, uint64_t seq, const std::string& fee,
-                           const std::vector<std::string>& msgs, const std::string& memo) {
-  // StdSignDoc keys are already in sorted order and every embedded JSON is
-  // canonical (MustSortJSON output), so composing canonical pieces equals
-  // MustSortJSON(amino.MarshalJSON(StdSignDoc{...})).
-  std::string o = "{\"account_number\":\"" + std::to_string(accnum) + "\",\"chain_id\":" + go_json_string(chain) +
-                  ",\"fee\":" + fee + ",\"memo\":" + go_json_string(memo) + ",\"msgs\":[";
-  for (size_t i = 0; i < msgs.size(); ++i) {
-    if (i) o += ",";
-    o += msgs[i];
+// ------------------------------------------------------------- verdict cache
+// Bounded verdict cache: key SHA256(kind || pub || sig || SHA256(signBytes))
+// (VerifyBytes depends on the message only through its SHA-256 for
+// secp256k1, so a cached verdict is exactly the reference's), 8-way buckets
+// with CLOCK (second chance) eviction, lock-striped.
+class VerdictCache {
+ public:
+  explicit VerdictCache(size_t entries) { resize(entries); }
+  void resize(size_t entries) {
+    std::lock_guard<std::mutex> g(resize_mu_);
+    size_t nb = 64;
+    while (nb * kWays < entries) nb <<= 1;
+    std::vector<Bucket> b(nb);
+    for (auto& l : locks_) l.lock();
+    buckets_.swap(b);
+    mask_ = nb - 1;
+    count_ = 0;
+    for (auto& l : locks_) l.unlock();
   }
-  o += "],\"sequence\":\"" + std::to_string(seq) + "\"}";
-  return o;
-}
+  void clear() { resize(capacity()); }
+  size_t capacity() const { return buckets_.size() * kWays; }
+  size_t size() const { return count_.load(); }
+  // 1/0 verdict, -1 miss
+  int get(const H32& k) {
+    const uint64_t h = hash(k);
+    std::lock_guard<std::mutex> g(locks_[h & (kLocks - 1)]);
+    Bucket& b = buckets_[h & mask_];
+    for (int w = 0; w < kWays; ++w) {
+      Entry& e = b.e[w];
+      if (e.state && !memcmp(e.key.data(), k.data(), 32)) {
+        e.state = (uint8_t)(2 | (e.state & 1) | 4);    // referenced
+        return e.state & 1;
+      }
+    }
+    return -1;
+  }
+  void put(const H32& k, bool v) {
+    const uint64_t h = hash(k);
+    std::lock_guard<std::mutex> g(locks_[h & (kLocks - 1)]);
+    Bucket& b = buckets_[h & mask_];
+    for (int w = 0; w < kWays; ++w)
+      if (b.e[w].state && !memcmp(b.e[w].key.data(), k.data(), 32)) { b.e[w].state = (uint8_t)(2 | 4 | v); return; }
+    for (int w = 0; w < kWays; ++w)
+      if (!b.e[w].state) { b.e[w] = Entry{k, (uint8_t)(2 | 4 | v)}; ++count_; return; }
+    for (;;) {                                          // CLOCK: clear referenced bits until a victim
+      Entry& e = b.e[b.hand];
+      b.hand = (uint8_t)((b.hand + 1) % kWays);
+      if (e.state & 4) e.state &= (uint8_t)~4;
+      else { e = Entry{k, (uint8_t)(2 | 4 | v)}; return; }
+    }
+  }
 
-// ----------------------------------------------------------- app / state
-// simSecp256k1Pubkey (x/auth/ante/sigverify.go:27-31), amino-encoded
-const Bytes kSimSecp256k1Pubkey = {0xEB, 0x5A, 0xE9, 0x87, 0x21, 0x03, 0x5A, 0xD6, 0x81, 0x0A, 0x47, 0xF0, 0x73, 0x55,
-                                   0x3F, 0xF3, 0x0D, 0x2F, 0xCC, 0x7E, 0x0D, 0x3B, 0x1C, 0x0B, 0x74, 0xB6, 0x1A, 0x1A,
-                                   0xAA, 0x25, 0x82, 0x34, 0x40, 0x37, 0x15, 0x1E, 0x14, 0x3A};
-
-struct Account {
-  uint64_t number = 0, sequence = 0;
-  Bytes pub;   // amino, empty = not set
-};
-struct AddrHash {
-  size_t operator()(const std::array<uint8_t, 20>& a) const {
-    size_t h;
-    memcpy(&h, a.data(), sizeof h);
+ private:
+  static constexpr int kWays = 8;
+  static constexpr size_t kLocks = 1024;
+  struct Entry {
+    H32 key;
+    uint8_t state;     // bit 1 occupied, bit 0 verdict, bit 2 referenced
+  };
+  struct Bucket {
+    Entry e[kWays] = {};
+    uint8_t hand = 0;
+  };
+  static uint64_t hash(const H32& k) {
+    uint64_t h;
+    memcpy(&h, k.data(), 8);                          // the key is a SHA-256 output
     return h;
   }
+  std::vector<Bucket> buckets_;
+  size_t mask_ = 0;
+  std::mutex locks_[kLocks];
+  std::mutex resize_mu_;
+  std::atomic<size_t> count_{0};
 };
 
-}  // namespace
-
-struct gvh_app {
-  gv_ctx* gpu = nullptr;
-  uint64_t sig_limit = 7, cost_secp = 1000, cost_ed = 590;
-  std::string chain_id = "";
-  int64_t height = 1;
-  bool recheck = false;
-  uint64_t gas_limit = 0;
-  std::unordered_map<std::array<uint8_t, 20>, Account, AddrHash> accounts;
-  std::unordered_map<std::string, bool> cache;   // pub33 || sig64 || sha256(msg)
-  std::mutex mu;
-  // PreVerifyTxs host threads: measured on the MI355X box host (tools/host_probe.py,
-  // 10k MsgSend txs) 1 thread 11-12 ms, 4 threads 9.4 ms, 16 threads 11.4 ms --
-  // the stages are allocation-heavy and stop scaling past a few threads.
-  int threads = std::max(1, std::min(4, (int)std::thread::hardware_concurrency()));
-};
-
-namespace {
-
-struct GasMeter {
-  uint64_t limit, used = 0;
-  void consume(uint64_t amount, const char* desc) {
-    used += amount;
-    if (limit && used > limit) throw OutOfGas{desc};
-  }
-};
-
-// One secp256k1 leaf: VerifyBytes(msg, sig) for pub33.
+// ------------------------------------------------------------ verification
+// One leaf: VerifyBytes of a secp256k1 (GPU) or ed25519 (CPU) key.
 struct Leaf {
-  std::array<uint8_t, 33> pub;
-  Bytes sig;
-  std::array<uint8_t, 32> dig;
-  int verdict = -1;    // -1 unknown, 0/1
-  std::string key() const {
-    std::string k((const char*)pub.data(), 33);
-    k.append((const char*)sig.data(), sig.size());
-    k.append((const char*)dig.data(), 32);
-    return k;
-  }
+  uint8_t kind = 0;                       // 0 secp256k1, 1 ed25519
+  std::array<uint8_t, 33> pub{};          // secp: 33 bytes; ed: first 32
+  std::array<uint8_t, 64> sig{};
+  H32 dig{};                              // SHA256(signBytes)
+  H32 key{};                              // verdict-cache key
+  int verdict = -1;
 };
+void leaf_key(Leaf& L) {
+  Sha256 h;
+  h.up(&L.kind, 1);
+  h.up(L.pub.data(), L.kind ? 32 : 33);
+  h.up(L.sig.data(), 64);
+  h.up(L.dig.data(), 32);
+  L.key = h.fin();
+}
 
 // Verification expression for one signer: tendermint VerifyBytes semantics.
 struct Node {
-  enum Op { Const, SecpLeaf, And } op = Const;
+  enum Op { Const, LeafRef, And, PanicNode } op = Const;
   bool value = false;
   int leaf = -1;
   std::vector<Node> kids;
@@ -462,25 +836,32 @@ struct Node {
 // Build the node for pk.VerifyBytes(msg, sig) (secp256k1_nocgo.go / ed25519 /
 // multisig threshold_pubkey.go).  Multisig leaves are AND-ed in bit order; since
 // every leaf is a pure function, the AND equals the reference's short-circuit.
-Node build_node(const PubKey& pk, const Bytes& msg, const std::array<uint8_t, 32>& dig, const Bytes& sig,
-                std::vector<Leaf>& leaves) {
+Node build_node(const PubKey& pk, const H32& dig, Span sig, std::vector<Leaf>& leaves) {
   Node n;
   switch (pk.kind) {
+    case PubKey::Nil:
+      n.op = Node::PanicNode;                         // method call on a nil interface
+      return n;
     case PubKey::Secp256k1:
-      if (sig.size() != 64) { n.op = Node::Const; n.value = false; return n; }
-      n.op = Node::SecpLeaf;
+    case PubKey::Ed25519: {
+      if (sig.n != 64) { n.op = Node::Const; n.value = false; return n; }
+      Leaf L;
+      L.kind = pk.kind == PubKey::Ed25519;
+      if (L.kind) memcpy(L.pub.data(), pk.ed.data(), 32);
+      else L.pub = pk.secp;
+      memcpy(L.sig.data(), sig.p, 64);
+      L.dig = dig;
+      leaf_key(L);
+      n.op = Node::LeafRef;
       n.leaf = (int)leaves.size();
-      leaves.push_back(Leaf{pk.secp, sig, dig, -1});
+      leaves.push_back(L);
       return n;
-    case PubKey::Ed25519:
-      n.op = Node::Const;
-      n.value = ed25519_verify(pk.ed, msg, sig);
-      return n;
+    }
     case PubKey::Multisig: {
       Multisignature ms;
       try {
         ms = decode_multisig(sig);
-      } catch (const Panic&) {
+      } catch (const AminoErr&) {
         n.op = Node::Const; n.value = false;     // UnmarshalBinaryBare error -> false
         return n;
       }
@@ -495,7 +876,7 @@ Node build_node(const PubKey& pk, const Bytes& msg, const std::array<uint8_t, 32
       for (int i = 0; i < size; ++i) {
         if (!ms.bits.get(i)) continue;
         if (si >= ms.sigs.size()) throw Panic("runtime error: index out of range");
-        n.kids.push_back(build_node(pk.subs[i], msg, dig, ms.sigs[si], leaves));
+        n.kids.push_back(build_node(pk.subs[i], dig, ms.sigs[si], leaves));
         ++si;
       }
       return n;
@@ -507,7 +888,8 @@ Node build_node(const PubKey& pk, const Bytes& msg, const std::array<uint8_t, 32
 bool eval(const Node& n, const std::vector<Leaf>& leaves) {
   switch (n.op) {
     case Node::Const: return n.value;
-    case Node::SecpLeaf: return leaves[n.leaf].verdict == 1;
+    case Node::LeafRef: return leaves[n.leaf].verdict == 1;
+    case Node::PanicNode: throw Panic("runtime error: invalid memory address or nil pointer dereference");
     case Node::And:
       for (auto& k : n.kids)
         if (!eval(k, leaves)) return false;
@@ -516,10 +898,207 @@ bool eval(const Node& n, const std::vector<Leaf>& leaves) {
   return false;
 }
 
+}  // namespace
+
+// ----------------------------------------------------------------- the app
+namespace {
+
+// store/types/gas.go basicGasMeter (limit) / infiniteGasMeter
+struct GasMeter {
+  bool infinite;
+  uint64_t limit;
+  uint64_t used = 0;
+  void consume(uint64_t amount, const char* desc) {
+    used += amount;
+    if (!infinite && used > limit) throw OutOfGas{desc};
+  }
+  bool fits(uint64_t amount) const { return infinite || used + amount <= limit; }
+};
+
+// 64-bit hash of a byte string for in-process tables (entries are always
+// confirmed by a full comparison, so collisions cost time, never results).
+uint64_t fast_hash(const uint8_t* p, size_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xC2B2AE3D27D4EB4Full);
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    memcpy(&w, p + i, 8);
+    h = (h ^ (w * 0x87C37B91114253D5ull)) * 0x4CF5AD432745937Full;
+    h ^= h >> 31;
+  }
+  uint64_t w = 0;
+  memcpy(&w, p + i, n - i);
+  h = (h ^ (w * 0x87C37B91114253D5ull)) * 0x4CF5AD432745937Full;
+  return h ^ (h >> 29);
+}
+
+// A decoded amino pubkey with its canonical bytes (pk.Bytes()), address and
+// CountSubKeys -- pure functions of the amino bytes, shared by every tx and
+// account that carries the same key.
+struct PubInfo {
+  Bytes raw;                    // the amino bytes it was decoded from
+  PubKey pk;
+  Bytes canon;
+  Addr addr{};
+  int subkeys = 1;
+};
+class PubCache {
+ public:
+  // throws Panic if the bytes do not decode (MustUnmarshalBinaryBare)
+  std::shared_ptr<const PubInfo> get(const uint8_t* p, size_t n) {
+    const uint64_t h = fast_hash(p, n);
+    Shard& s = shards_[h & (kShards - 1)];
+    {
+      std::lock_guard<std::mutex> g(s.mu);
+      auto it = s.map.find(h);
+      if (it != s.map.end())
+        for (auto& e : it->second)
+          if (e->raw.size() == n && !memcmp(e->raw.data(), p, n)) return e;
+    }
+    auto info = std::make_shared<PubInfo>();
+    info->raw.assign(p, p + n);
+    info->pk = decode_pubkey(p, n);
+    info->canon = pubkey_bytes(info->pk);
+    if (info->pk.kind != PubKey::Nil) info->addr = pubkey_address(info->pk);
+    info->subkeys = count_subkeys(info->pk);
+    std::lock_guard<std::mutex> g(s.mu);
+    if (s.count >= kPerShard) { s.map.clear(); s.count = 0; }
+    s.map[h].push_back(info);
+    ++s.count;
+    return info;
+  }
+
+ private:
+  static constexpr size_t kShards = 64, kPerShard = 8192;
+  struct Shard {
+    std::mutex mu;
+    std::unordered_map<uint64_t, std::vector<std::shared_ptr<const PubInfo>>> map;
+    size_t count = 0;
+  };
+  Shard shards_[kShards];
+};
+
+struct Account {
+  uint64_t number = 0, sequence = 0;
+  Bytes pub;                                  // amino (canonical), empty = not set
+  std::shared_ptr<const PubInfo> info;        // GetPubKey() of pub (decoded once)
+};
+struct AddrHash {
+  size_t operator()(const Bytes& a) const { return (size_t)fast_hash(a.data(), a.size()); }
+};
+
+// One signer's prepared verification: the sign bytes were built for
+// (accnum, seq) with the account pubkey `pub` (its canonical bytes), the gas
+// consumer's charge for that key and these signature bytes, and the leaves
+// (verdicts filled by PreVerifyTxs' GPU batch).
+struct SignerPlan {
+  bool ok = false;                  // plan built (else: recompute in ante)
+  uint64_t accnum = 0, seq = 0;
+  std::shared_ptr<const PubInfo> pub;
+  uint64_t gas = 0;
+  uint8_t gas_status = 0;           // 0 charged without error, 1 top-level error, 2 panic
+  bool resolved = false;            // every leaf has its verdict
+  Node node;
+  std::vector<Leaf> leaves;
+};
+// PreVerifyTxs' work on one tx, reused by its ante run.
+struct Memo {
+  std::shared_ptr<const Tx> tx;
+  std::string decode_err;                            // non-empty: the tx did not decode
+  std::vector<std::shared_ptr<const PubInfo>> tx_pk; // GetPubKeys(): per StdSignature (null: none)
+  int pk_panic = -1;                                 // first tx-supplied key that does not decode
+  std::string pk_panic_msg;
+  std::vector<SignerPlan> plans;
+};
+
+// Memo table (CheckTx window and separate PreVerifyTxs / ante calls): tx
+// bytes -> Memo with full-byte comparison, two generations.
+class MemoTable {
+ public:
+  std::shared_ptr<Memo> find(const uint8_t* p, size_t n) {
+    const uint64_t h = fast_hash(p, n);
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto* m : {&cur_, &old_}) {
+      auto it = m->find(h);
+      if (it != m->end())
+        for (auto e = it->second.rbegin(); e != it->second.rend(); ++e)     // newest first
+          if ((*e)->tx->raw.size() == n && !memcmp((*e)->tx->raw.data(), p, n)) return *e;
+    }
+    return nullptr;
+  }
+  void put(std::shared_ptr<Memo> m) {
+    if (!m->tx) return;
+    const uint64_t h = fast_hash(m->tx->raw.data(), m->tx->raw.size());
+    std::lock_guard<std::mutex> g(mu_);
+    if (count_ >= limit_) {
+      old_.swap(cur_);
+      cur_.clear();
+      count_ = 0;
+    }
+    auto& v = cur_[h];
+    for (auto& e : v)
+      if (e->tx->raw == m->tx->raw) { e = std::move(m); return; }
+    v.push_back(std::move(m));
+    ++count_;
+  }
+  void clear() {
+    std::lock_guard<std::mutex> g(mu_);
+    cur_.clear();
+    old_.clear();
+    count_ = 0;
+  }
+
+ private:
+  std::mutex mu_;
+  std::unordered_map<uint64_t, std::vector<std::shared_ptr<Memo>>> cur_, old_;
+  size_t count_ = 0, limit_ = 1 << 16;
+};
+
+struct Window {
+  std::mutex m;
+  std::condition_variable cv;
+  size_t max_txs = 64;
+  int64_t max_wait_us = 200;
+  struct Batch {
+    std::vector<std::pair<const uint8_t*, size_t>> items;
+    std::chrono::steady_clock::time_point deadline;
+    bool flushing = false, done = false;
+  };
+  std::shared_ptr<Batch> open;
+};
+
+// simSecp256k1Pubkey (x/auth/ante/sigverify.go:27-31), amino
+const Bytes kSimPub = {0xEB, 0x5A, 0xE9, 0x87, 0x21, 0x03, 0x5A, 0xD6, 0x81, 0x0A, 0x47, 0xF0, 0x73,
+                       0x55, 0x3F, 0xF3, 0x0D, 0x2F, 0xCC, 0x7E, 0x0D, 0x3B, 0x1C, 0x0B, 0x74, 0xB6,
+                       0x1A, 0x1A, 0xAA, 0x25, 0x82, 0x34, 0x40, 0x37, 0x15, 0x1E, 0x14, 0x3A};
+
+}  // namespace
+
+struct gvh_app {
+  gv_ctx* gpu = nullptr;
+  uint64_t sig_limit = 7, cost_secp = 1000, cost_ed = 590;
+  std::string chain_id = "", chain_json = "\"\"";
+  int64_t height = 1;
+  bool recheck = false;
+  uint64_t gas_limit = 0;
+  std::unordered_map<Bytes, Account, AddrHash> accounts;
+  std::mutex mu;                               // accounts + context
+  VerdictCache cache{size_t(1) << 20};
+  MemoTable memo;
+  PubCache pubs;
+  Window window;
+  std::mutex gpu_mu;                           // one GPU batch at a time per app
+  int threads = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+  std::atomic<uint64_t> st_gpu_calls{0}, st_gpu_leaves{0}, st_hits{0}, st_misses{0}, st_memo{0}, st_windows{0},
+      st_window_txs{0}, st_pre_ns{0}, st_gpu_ns{0}, st_loop_ns{0};
+};
+
+namespace {
+
 // DefaultSigVerificationGasConsumer (sigverify.go:299-322) incl. the multisig
 // recursion (ConsumeMultisignatureVerificationGas :325-338, whose nested errors
-// are ignored).  Returns an error for the top level only.
-bool consume_sig_gas(GasMeter& gm, const Bytes& sig, const PubKey& pk, const gvh_app* app, SdkError* err) {
+// are ignored).  Returns false + err for the top level only.
+bool consume_sig_gas(GasMeter& gm, Span sig, const PubKey& pk, const gvh_app* app, SdkError* err) {
   switch (pk.kind) {
     case PubKey::Ed25519:
       gm.consume(app->cost_ed, "ante verify: ed25519");
@@ -529,7 +1108,12 @@ bool consume_sig_gas(GasMeter& gm, const Bytes& sig, const PubKey& pk, const gvh
       gm.consume(app->cost_secp, "ante verify: secp256k1");
       return true;
     case PubKey::Multisig: {
-      Multisignature ms = decode_multisig(sig);      // MustUnmarshalBinaryBare: panics on error
+      Multisignature ms;
+      try {
+        ms = decode_multisig(sig);                   // MustUnmarshalBinaryBare: panics on error
+      } catch (const AminoErr& e) {
+        throw Panic(e.what());
+      }
       const int size = ms.bits.size();
       size_t si = 0;
       for (int i = 0; i < size; ++i) {
@@ -540,12 +1124,18 @@ bool consume_sig_gas(GasMeter& gm, const Bytes& sig, const PubKey& pk, const gvh
       }
       return true;
     }
+    case PubKey::Nil:
+      if (err) *err = wrap(kErrInvalidPubKey, "unrecognized public key type: <nil>");
+      return false;
   }
   return true;
 }
 
-void copy_result(gvh_result* out, const SdkError* e, uint64_t gas, uint32_t gpu_leaves, uint32_t hits) {
-  memset(out, 0, sizeof *out);
+void copy_result(gvh_result* out, const SdkError* e, uint64_t gas, uint32_t gpu_leaves, uint32_t hits,
+                 uint64_t wanted) {
+  out->code = 0;
+  out->codespace[0] = 0;
+  out->log[0] = 0;
   if (e) {
     out->code = e->code;
     snprintf(out->codespace, sizeof out->codespace, "%s", e->codespace.c_str());
@@ -554,151 +1144,109 @@ void copy_result(gvh_result* out, const SdkError* e, uint64_t gas, uint32_t gpu_
   out->gas_used = gas;
   out->gpu_leaves = gpu_leaves;
   out->cache_hits = hits;
+  out->gas_wanted = wanted;
 }
 
-// Resolve every leaf: cache first, misses in ONE gv_verify_digests batch.
-int resolve_leaves(gvh_app* app, std::vector<Leaf>& leaves, uint32_t* gpu_leaves, uint32_t* hits) {
-  std::vector<size_t> miss;
-  for (size_t i = 0; i < leaves.size(); ++i) {
-    auto it = app->cache.find(leaves[i].key());
-    if (it != app->cache.end()) { leaves[i].verdict = it->second; ++*hits; }
-    else miss.push_back(i);
+std::shared_ptr<const PubInfo> account_info(gvh_app* app, Account& acc) {
+  if (acc.pub.empty()) return nullptr;
+  if (!acc.info) acc.info = app->pubs.get(acc.pub.data(), acc.pub.size());
+  return acc.info;
+}
+
+// Sign-bytes digest of tx for (accnum, seq) on chain_json.
+H32 sign_digest(const Tx& tx, const std::string& chain_json, uint64_t accnum, uint64_t seq) {
+  char a[24], s[24];
+  const int na = snprintf(a, sizeof a, "%llu", (unsigned long long)accnum);
+  const int ns = snprintf(s, sizeof s, "%llu", (unsigned long long)seq);
+  Sha256 h;
+  h.up("{\"account_number\":\"", 19);
+  h.up(a, na);
+  h.up("\",\"chain_id\":", 13);
+  h.up(chain_json);
+  h.up(tx.sb_tail);
+  h.up(s, ns);
+  h.up("\"}", 2);
+  return h.fin();
+}
+std::string sign_bytes(const Tx& tx, const std::string& chain_json, uint64_t accnum, uint64_t seq) {
+  return "{\"account_number\":\"" + std::to_string(accnum) + "\",\"chain_id\":" + chain_json + tx.sb_tail +
+         std::to_string(seq) + "\"}";
+}
+
+// Build a signer's plan: gas charge, sign bytes digest, leaves + keys.
+// ed25519 leaves need the sign bytes themselves (SHA-512 over them): verified
+// here on the CPU (OpenSSL), their verdict cached like the secp256k1 ones.
+void make_plan(SignerPlan& p, gvh_app* app, const Tx& tx, size_t signer, std::shared_ptr<const PubInfo> pub,
+               uint64_t accnum, uint64_t seq, const std::string& chain_json) {
+  p.accnum = accnum;
+  p.seq = seq;
+  p.pub = std::move(pub);
+  p.leaves.clear();
+  p.resolved = false;
+  try {
+    GasMeter g{true, 0};
+    p.gas_status = consume_sig_gas(g, tx.sigs[signer].sig, p.pub->pk, app, nullptr) ? 0 : 1;
+    p.gas = g.used;
+  } catch (const Panic&) {
+    p.gas_status = 2;
   }
+  const H32 dig = sign_digest(tx, chain_json, accnum, seq);
+  p.node = build_node(p.pub->pk, dig, tx.sigs[signer].sig, p.leaves);
+  bool has_ed = false;
+  for (const Leaf& L : p.leaves) has_ed = has_ed || L.kind;
+  if (has_ed) {
+    const std::string sb = sign_bytes(tx, chain_json, accnum, seq);
+    for (Leaf& L : p.leaves) {
+      if (!L.kind) continue;
+      const int v = app->cache.get(L.key);
+      if (v >= 0) { L.verdict = v; continue; }
+      std::array<uint8_t, 32> ed;
+      memcpy(ed.data(), L.pub.data(), 32);
+      L.verdict = ed25519_verify(ed, (const uint8_t*)sb.data(), sb.size(), Span{L.sig.data(), 64}) ? 1 : 0;
+      app->cache.put(L.key, L.verdict == 1);
+    }
+  }
+  p.ok = true;
+}
+
+// Resolve leaves: cache first, the secp256k1 misses in ONE GPU batch.
+int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint32_t* hits) {
+  std::vector<Leaf*> miss;
+  for (Leaf* L : leaves) {
+    if (L->verdict >= 0) { if (hits) ++*hits; continue; }   // ed25519 leaves were decided in make_plan
+    const int v = app->cache.get(L->key);
+    if (v >= 0) { L->verdict = v; if (hits) ++*hits; }
+    else miss.push_back(L);
+  }
+  app->st_hits += leaves.size() - miss.size();
+  app->st_misses += miss.size();
   if (miss.empty()) return GVH_OK;
   if (!app->gpu) return GVH_ENOVERIFIER;
   const size_t m = miss.size();
   std::vector<uint8_t> pub(m * 33), sig(m * 64), dig(m * 32), ok(m);
   for (size_t k = 0; k < m; ++k) {
-    const Leaf& L = leaves[miss[k]];
-    memcpy(&pub[k * 33], L.pub.data(), 33);
-    memcpy(&sig[k * 64], L.sig.data(), 64);
-    memcpy(&dig[k * 32], L.dig.data(), 32);
+    memcpy(&pub[k * 33], miss[k]->pub.data(), 33);
+    memcpy(&sig[k * 64], miss[k]->sig.data(), 64);
+    memcpy(&dig[k * 32], miss[k]->dig.data(), 32);
   }
-  if (gv_verify_digests(app->gpu, m, pub.data(), sig.data(), dig.data(), ok.data()) != GV_OK) return GVH_EDEVICE;
+  {
+    std::lock_guard<std::mutex> g(app->gpu_mu);
+    if (gv_verify_digests(app->gpu, m, pub.data(), sig.data(), dig.data(), ok.data()) != GV_OK) return GVH_EDEVICE;
+  }
+  app->st_gpu_calls += 1;
+  app->st_gpu_leaves += m;
   for (size_t k = 0; k < m; ++k) {
-    leaves[miss[k]].verdict = ok[k];
-    app->cache[leaves[miss[k]].key()] = ok[k] != 0;
+    miss[k]->verdict = ok[k];
+    app->cache.put(miss[k]->key, ok[k] != 0);
   }
-  *gpu_leaves += (uint32_t)m;
-  return GVH_OK;
-}
-
-int run_ante(gvh_app* app, const FlatTx& tx, bool simulate, gvh_result* out) {
-  GasMeter gm{app->gas_limit};
-  uint32_t gpu_leaves = 0, hits = 0;
-  auto fail = [&](const SdkError& e) { copy_result(out, &e, gm.used, gpu_leaves, hits); return GVH_OK; };
-  try {
-    // GetPubKeys(): amino-decode every tx-supplied pubkey (MustUnmarshal -> panic)
-    std::vector<std::unique_ptr<PubKey>> tx_pks(tx.sig_pubs.size());
-    for (size_t i = 0; i < tx.sig_pubs.size(); ++i)
-      if (!tx.sig_pubs[i].empty()) tx_pks[i].reset(new PubKey(decode_pubkey(tx.sig_pubs[i].data(), tx.sig_pubs[i].size())));
-
-    // ---- SetPubKeyDecorator (sigverify.go:60-99)
-    for (size_t i = 0; i < tx_pks.size(); ++i) {
-      const Bytes* pkb = tx_pks[i] ? &tx.sig_pubs[i] : nullptr;
-      if (!pkb) {
-        if (!simulate) continue;           // pubkey already set on the account
-        pkb = &kSimSecp256k1Pubkey;        // simSecp256k1Pubkey (sigverify.go:19-31)
-      }
-      if (i >= tx.signers.size()) throw Panic("runtime error: index out of range");
-      if (!simulate && pubkey_address(*tx_pks[i]) != tx.signers[i])
-        return fail(wrap(kErrInvalidPubKey, "pubKey does not match signer address " + acc_string(tx.signers[i]) +
-                                                " with signer index: " + std::to_string(i)));
-      auto it = app->accounts.find(tx.signers[i]);
-      if (it == app->accounts.end())
-        return fail(wrap(kErrUnknownAddress, "account " + acc_string(tx.signers[i]) + " does not exist"));
-      if (it->second.pub.empty()) it->second.pub = *pkb;
-    }
-    // ---- ValidateSigCountDecorator (sigverify.go:275-294)
-    {
-      uint64_t count = 0;
-      for (auto& pk : tx_pks) {
-        count += pk ? (uint64_t)count_subkeys(*pk) : 1;   // CountSubKeys(nil) -> 1
-        if (count > app->sig_limit)
-          return fail(wrap(kErrTooManySignatures,
-                           "signatures: " + std::to_string(count) + ", limit: " + std::to_string(app->sig_limit)));
-      }
-    }
-    // ---- SigGasConsumeDecorator (sigverify.go:117-153)
-    for (size_t i = 0; i < tx.sigs.size(); ++i) {
-      if (i >= tx.signers.size()) throw Panic("runtime error: index out of range");
-      auto it = app->accounts.find(tx.signers[i]);
-      if (it == app->accounts.end())
-        return fail(wrap(kErrUnknownAddress, "account " + acc_string(tx.signers[i]) + " does not exist"));
-      PubKey pk;
-      if (it->second.pub.empty()) {
-        if (!simulate) {
-          // a nil pubkey reaches the gas consumer's type switch: "unrecognized public key type: <nil>"
-          return fail(wrap(kErrInvalidPubKey, "unrecognized public key type: <nil>"));
-        }
-        pk.kind = PubKey::Secp256k1;   // simSecp256k1Pubkey
-      } else {
-        pk = decode_pubkey(it->second.pub.data(), it->second.pub.size());
-      }
-      SdkError e;
-      if (!consume_sig_gas(gm, tx.sigs[i], pk, app, &e)) return fail(e);
-    }
-    // ---- BatchSigVerificationDecorator (replaces sigverify.go:170-216)
-    if (!app->recheck) {
-      if (tx.sigs.size() != tx.signers.size())
-        return fail(wrap(kErrUnauthorized, "invalid number of signer;  expected: " + std::to_string(tx.signers.size()) +
-                                               ", got " + std::to_string(tx.sigs.size())));
-      std::vector<Leaf> leaves;
-      std::vector<Node> nodes;
-      SdkError first_err;
-      bool have_err = false;
-      for (size_t i = 0; i < tx.sigs.size(); ++i) {
-        auto it = app->accounts.find(tx.signers[i]);
-        if (it == app->accounts.end()) {
-          first_err = wrap(kErrUnknownAddress, "account " + acc_string(tx.signers[i]) + " does not exist");
-          have_err = true;
-          break;
-        }
-        const Account& acc = it->second;
-        std::string sb = std_sign_bytes(app->chain_id, app->height == 0 ? 0 : acc.number, acc.sequence, tx.fee,
-                                        tx.msgs, tx.memo);
-        if (!simulate && acc.pub.empty()) {
-          first_err = wrap(kErrInvalidPubKey, "pubkey on account is not set");
-          have_err = true;
-          break;
-        }
-        if (simulate) continue;
-        PubKey pk = decode_pubkey(acc.pub.data(), acc.pub.size());
-        Bytes msg(sb.begin(), sb.end());
-        auto dig = sha256(msg.data(), msg.size());
-        nodes.push_back(build_node(pk, msg, dig, tx.sigs[i], leaves));
-      }
-      if (!leaves.empty()) {
-        int rc = resolve_leaves(app, leaves, &gpu_leaves, &hits);
-        if (rc != GVH_OK) return rc;
-      }
-      for (auto& n : nodes)   // report the FIRST failing signer, as the reference loop does
-        if (!eval(n, leaves))
-          return fail(wrap(kErrUnauthorized, "signature verification failed; verify correct account sequence and chain-id"));
-      if (have_err) return fail(first_err);
-    }
-    // ---- IncrementSequenceDecorator (sigverify.go:237-259)
-    if (!app->recheck || simulate) {
-      for (auto& a : tx.signers) {
-        auto it = app->accounts.find(a);
-        if (it == app->accounts.end()) throw Panic("account not found");
-        it->second.sequence += 1;
-      }
-    }
-  } catch (const Panic& p) {
-    return fail(wrap(kErrPanic, p.what()));
-  } catch (const OutOfGas& o) {
-    return fail(wrap(kErrOutOfGas, std::string("out of gas in location: ") + o.descriptor + "; gasWanted: " +
-                                       std::to_string(app->gas_limit) + ", gasUsed: " + std::to_string(gm.used)));
-  }
-  copy_result(out, nullptr, gm.used, gpu_leaves, hits);
+  if (gpu_leaves) *gpu_leaves += (uint32_t)m;
   return GVH_OK;
 }
 
 // Run fn(i) for i in [0, n) on up to `threads` threads (dynamic chunks).
 template <class F>
 void parallel_for(size_t n, int threads, F fn) {
-  const size_t chunk = 64;
+  const size_t chunk = 32;
   if (threads <= 1 || n <= chunk) {
     for (size_t i = 0; i < n; ++i) fn(i);
     return;
@@ -715,6 +1263,333 @@ void parallel_for(size_t n, int threads, F fn) {
   for (auto& t : th) t.join();
 }
 
+// The ante chain on one decoded tx (app->mu held by the caller).  memo: the
+// PreVerifyTxs work for these bytes, or null.  Every memoised value is used
+// only after checking that the state it was computed from is the state now.
+int run_ante(gvh_app* app, const Tx& tx, Memo* memo, bool simulate, gvh_result* out) {
+  const uint64_t wanted = tx.gas;
+  // SetGasMeter (setup.go:67-76): infinite when simulating or at height 0
+  GasMeter gm{!app->gas_limit && (simulate || app->height == 0), app->gas_limit ? app->gas_limit : tx.gas};
+  uint32_t gpu_leaves = 0, hits = 0;
+  // runTx runs the ante handler on a cache-wrapped context and writes it only
+  // on success (baseapp/baseapp.go:553-578): a failed chain leaves no state.
+  Account* set_pub[8];
+  int n_set = 0;
+  std::vector<Account*> set_pub_more;
+  auto rollback = [&]() {
+    for (int k = 0; k < n_set; ++k) { set_pub[k]->pub.clear(); set_pub[k]->info = nullptr; }
+    for (Account* a : set_pub_more) { a->pub.clear(); a->info = nullptr; }
+  };
+  auto fail = [&](const SdkError& e) {
+    rollback();
+    copy_result(out, &e, gm.used, gpu_leaves, hits, wanted);
+    return GVH_OK;
+  };
+  try {
+    if (tx.nil_msg) throw Panic("runtime error: invalid memory address or nil pointer dereference");
+    const auto& signers = tx.signers;
+    const size_t ns = tx.sigs.size();
+    // GetPubKeys(): amino-decode every tx-supplied pubkey (MustUnmarshal -> panic)
+    std::vector<std::shared_ptr<const PubInfo>> local;
+    const std::vector<std::shared_ptr<const PubInfo>>* tx_pk = nullptr;
+    if (memo && memo->tx_pk.size() == ns) {
+      if (memo->pk_panic >= 0) throw Panic(memo->pk_panic_msg);
+      tx_pk = &memo->tx_pk;
+    } else {
+      local.resize(ns);
+      for (size_t i = 0; i < ns; ++i)
+        if (tx.sigs[i].pub.n) local[i] = app->pubs.get(tx.sigs[i].pub.p, tx.sigs[i].pub.n);
+      tx_pk = &local;
+    }
+    // signer accounts, looked up once
+    std::vector<Account*> accs(signers.size(), nullptr);
+    auto acc_of = [&](size_t i) -> Account* {
+      if (!accs[i]) {
+        auto it = app->accounts.find(signers[i]);
+        if (it != app->accounts.end()) accs[i] = &it->second;
+      }
+      return accs[i];
+    };
+    static const std::shared_ptr<const PubInfo> kSim = [] {
+      auto p = std::make_shared<PubInfo>();
+      p->raw = kSimPub;
+      p->pk = decode_pubkey(kSimPub.data(), kSimPub.size());
+      p->canon = kSimPub;
+      p->addr = pubkey_address(p->pk);
+      return std::shared_ptr<const PubInfo>(p);
+    }();
+
+    // ---- SetPubKeyDecorator (sigverify.go:60-99)
+    for (size_t i = 0; i < ns; ++i) {
+      const PubInfo* pk = (*tx_pk)[i].get();
+      if (!pk && !simulate) continue;                 // pubkey already set on the account
+      if (i >= signers.size()) throw Panic("runtime error: index out of range");
+      if (!simulate) {
+        if (pk->pk.kind == PubKey::Nil) throw Panic("runtime error: invalid memory address or nil pointer dereference");
+        if (!(signers[i].size() == 20 && !memcmp(pk->addr.data(), signers[i].data(), 20)))
+          return fail(wrap(kErrInvalidPubKey, "pubKey does not match signer address " + acc_string(signers[i]) +
+                                                  " with signer index: " + std::to_string(i)));
+      }
+      Account* acc = acc_of(i);
+      if (!acc) return fail(wrap(kErrUnknownAddress, "account " + acc_string(signers[i]) + " does not exist"));
+      if (acc->pub.empty()) {
+        const auto& info = pk ? (*tx_pk)[i] : kSim;
+        acc->pub = info->canon;
+        acc->info = info->canon == info->raw ? info : nullptr;
+        if (n_set < 8) set_pub[n_set++] = acc;
+        else set_pub_more.push_back(acc);
+      }
+    }
+    // ---- ValidateSigCountDecorator (sigverify.go:275-294)
+    {
+      uint64_t count = 0;
+      for (size_t i = 0; i < ns; ++i) {
+        count += (*tx_pk)[i] ? (uint64_t)(*tx_pk)[i]->subkeys : 1;   // CountSubKeys(nil) -> 1
+        if (count > app->sig_limit)
+          return fail(wrap(kErrTooManySignatures,
+                           "signatures: " + std::to_string(count) + ", limit: " + std::to_string(app->sig_limit)));
+      }
+    }
+    // ---- SigGasConsumeDecorator (sigverify.go:117-153)
+    for (size_t i = 0; i < ns; ++i) {
+      if (i >= signers.size()) throw Panic("runtime error: index out of range");
+      Account* acc = acc_of(i);
+      if (!acc) return fail(wrap(kErrUnknownAddress, "account " + acc_string(signers[i]) + " does not exist"));
+      std::shared_ptr<const PubInfo> pk = account_info(app, *acc);
+      if (!pk) {
+        if (!simulate) return fail(wrap(kErrInvalidPubKey, "unrecognized public key type: <nil>"));
+        pk = kSim;
+      }
+      if (memo && i < memo->plans.size()) {
+        const SignerPlan& mp = memo->plans[i];
+        if (mp.ok && mp.gas_status == 0 && (mp.pub == pk || mp.pub->canon == acc->pub) && gm.fits(mp.gas)) {
+          gm.used += mp.gas;                          // the same charge, computed in PreVerifyTxs
+          continue;
+        }
+      }
+      SdkError e;
+      if (!consume_sig_gas(gm, tx.sigs[i].sig, pk->pk, app, &e)) return fail(e);
+    }
+    // ---- BatchSigVerificationDecorator (replaces sigverify.go:170-216)
+    if (!app->recheck) {
+      if (ns != signers.size())
+        return fail(wrap(kErrUnauthorized, "invalid number of signer;  expected: " + std::to_string(signers.size()) +
+                                               ", got " + std::to_string(ns)));
+      std::vector<SignerPlan> fresh;
+      SignerPlan* plans_small[8];
+      std::vector<SignerPlan*> plans_big;
+      size_t np = 0;
+      fresh.reserve(ns);
+      SdkError first_err;
+      bool have_err = false;
+      for (size_t i = 0; i < ns; ++i) {
+        Account* acc = acc_of(i);
+        if (!acc) {
+          first_err = wrap(kErrUnknownAddress, "account " + acc_string(signers[i]) + " does not exist");
+          have_err = true;
+          break;
+        }
+        const uint64_t accnum = app->height == 0 ? 0 : acc->number;
+        if (!simulate && acc->pub.empty()) {
+          first_err = wrap(kErrInvalidPubKey, "pubkey on account is not set");
+          have_err = true;
+          break;
+        }
+        if (simulate) continue;
+        SignerPlan* p = nullptr;
+        if (memo && i < memo->plans.size()) {
+          SignerPlan& mp = memo->plans[i];
+          if (mp.ok && mp.accnum == accnum && mp.seq == acc->sequence &&
+              (mp.pub == acc->info || mp.pub->canon == acc->pub)) {
+            p = &mp;
+            app->st_memo += 1;
+          }
+        }
+        if (!p) {
+          fresh.emplace_back();
+          p = &fresh.back();
+          make_plan(*p, app, tx, i, account_info(app, *acc), accnum, acc->sequence, app->chain_json);
+        }
+        if (np < 8) plans_small[np] = p;
+        else plans_big.push_back(p);
+        ++np;
+      }
+      auto plan_at = [&](size_t k) { return k < 8 ? plans_small[k] : plans_big[k - 8]; };
+      bool all_resolved = true;
+      for (size_t k = 0; k < np; ++k) all_resolved = all_resolved && plan_at(k)->resolved;
+      if (all_resolved) {
+        for (size_t k = 0; k < np; ++k) hits += (uint32_t)plan_at(k)->leaves.size();
+      } else {
+        std::vector<Leaf*> leaves;
+        for (size_t k = 0; k < np; ++k)
+          for (Leaf& L : plan_at(k)->leaves) leaves.push_back(&L);
+        if (!leaves.empty()) {
+          const int rc = resolve(app, leaves, &gpu_leaves, &hits);
+          if (rc != GVH_OK) { rollback(); return rc; }
+        }
+      }
+      for (size_t k = 0; k < np; ++k)   // report the FIRST failing signer, as the reference loop does
+        if (!eval(plan_at(k)->node, plan_at(k)->leaves))
+          return fail(wrap(kErrUnauthorized, "signature verification failed; verify correct account sequence and chain-id"));
+      if (have_err) return fail(first_err);
+    }
+    // ---- IncrementSequenceDecorator (sigverify.go:237-259)
+    if (!app->recheck || simulate) {
+      for (size_t i = 0; i < signers.size(); ++i) {
+        Account* acc = acc_of(i);
+        if (!acc) throw Panic("account not found");
+        acc->sequence += 1;
+      }
+    }
+  } catch (const Panic& p) {
+    return fail(wrap(kErrPanic, p.what()));
+  } catch (const OutOfGas& o) {
+    return fail(wrap(kErrOutOfGas, std::string("out of gas in location: ") + o.descriptor + "; gasWanted: " +
+                                       std::to_string(wanted) + ", gasUsed: " + std::to_string(gm.used)));
+  }
+  copy_result(out, nullptr, gm.used, gpu_leaves, hits, wanted);
+  return GVH_OK;
+}
+
+int ante_memo(gvh_app* app, Memo* m, bool simulate, gvh_result* out) {
+  if (!m->tx) {
+    SdkError err = wrap(kErrTxDecode, m->decode_err);
+    copy_result(out, &err, 0, 0, 0, 0);
+    return GVH_OK;
+  }
+  std::lock_guard<std::mutex> lk(app->mu);
+  return run_ante(app, *m->tx, m, simulate, out);
+}
+
+// ante on raw bytes: decode (or reuse the memo), then the chain.
+int ante_bytes(gvh_app* app, const uint8_t* p, size_t n, bool simulate, gvh_result* out) {
+  std::shared_ptr<Memo> m = app->memo.find(p, n);
+  if (m) return ante_memo(app, m.get(), simulate, out);
+  std::shared_ptr<const Tx> tx;
+  try {
+    tx = decode_tx(p, n);
+  } catch (const AminoErr& e) {
+    SdkError err = wrap(kErrTxDecode, e.what());
+    copy_result(out, &err, 0, 0, 0, 0);
+    return GVH_OK;
+  }
+  std::lock_guard<std::mutex> lk(app->mu);
+  return run_ante(app, *tx, nullptr, simulate, out);
+}
+
+// PreVerifyTxs.  Returns the memos (one per tx, in order).
+int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, size_t* n_leaves,
+              std::vector<std::shared_ptr<Memo>>* memos_out, bool keep) {
+  auto T0 = std::chrono::steady_clock::now();
+  const bool prof = getenv("GVH_PROFILE") != nullptr;
+  auto lap = [&](const char* what) {
+    if (!prof) return;
+    auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "preverify %s %.3f ms\n", what, std::chrono::duration<double, std::milli>(t - T0).count());
+    T0 = t;
+  };
+  // (1) parallel: decode (sharing an earlier decode of the same bytes) and
+  // GetPubKeys' tx-supplied keys with their address checks
+  std::vector<std::shared_ptr<Memo>> memos(ntx);
+  parallel_for(ntx, app->threads, [&](size_t t) {
+    // a fresh Memo every time (an earlier one may be in use by an ante run)
+    auto m = std::make_shared<Memo>();
+    auto old = keep ? app->memo.find(txs[t], lens[t]) : nullptr;
+    if (old) m->tx = old->tx;
+    else {
+      try {
+        m->tx = decode_tx(txs[t], lens[t]);
+      } catch (const AminoErr& e) {
+        m->decode_err = e.what();
+      }
+    }
+    if (m->tx) {
+      const Tx& tx = *m->tx;
+      m->tx_pk.resize(tx.sigs.size());
+      for (size_t i = 0; i < tx.sigs.size(); ++i) {
+        if (!tx.sigs[i].pub.n) continue;
+        try {
+          m->tx_pk[i] = app->pubs.get(tx.sigs[i].pub.p, tx.sigs[i].pub.n);
+        } catch (const Panic& e) {
+          m->pk_panic = (int)i;
+          m->pk_panic_msg = e.what();
+          break;
+        }
+      }
+      m->plans.resize(tx.sigs.size());
+    }
+    memos[t] = std::move(m);
+  });
+  lap("decode");
+  // (2) serial: the state the plans depend on, predicting sequences
+  struct Job {
+    size_t t, signer;
+    uint64_t accnum, seq;
+    std::shared_ptr<const PubInfo> pub;       // the account's key after SetPubKey
+  };
+  std::vector<Job> jobs;
+  std::string chain_json;
+  {
+    std::lock_guard<std::mutex> lk(app->mu);
+    chain_json = app->chain_json;
+    std::unordered_map<Bytes, uint64_t, AddrHash> bump;
+    bump.reserve(ntx * 2);
+    jobs.reserve(ntx);
+    for (size_t t = 0; t < ntx; ++t) {
+      Memo& m = *memos[t];
+      if (!m.tx || m.tx->nil_msg || m.pk_panic >= 0) continue;
+      const Tx& tx = *m.tx;
+      for (size_t i = 0; i < tx.sigs.size() && i < tx.signers.size(); ++i) {
+        auto it = app->accounts.find(tx.signers[i]);
+        if (it == app->accounts.end()) continue;
+        Account& acc = it->second;
+        std::shared_ptr<const PubInfo> pub;
+        try {
+          pub = account_info(app, acc);
+        } catch (const Panic&) {
+          continue;
+        }
+        if (!pub) pub = m.tx_pk[i];          // SetPubKey will store the tx-supplied key
+        if (!pub) continue;
+        uint64_t& b = bump[tx.signers[i]];
+        jobs.push_back(Job{t, i, app->height == 0 ? 0 : acc.number, acc.sequence + b, std::move(pub)});
+      }
+      for (auto& a : tx.signers) bump[a] += 1;
+    }
+  }
+  lap("jobs");
+  // (3) parallel: gas charge, sign bytes, leaves, cache keys
+  parallel_for(jobs.size(), app->threads, [&](size_t k) {
+    Job& j = jobs[k];
+    Memo& m = *memos[j.t];
+    try {
+      make_plan(m.plans[j.signer], app, *m.tx, j.signer, j.pub, j.accnum, j.seq, chain_json);
+    } catch (const Panic&) {
+      m.plans[j.signer].ok = false;                    // malformed: the ante chain will report it
+    }
+  });
+  lap("plans");
+  // (4) one GPU batch for the misses, no app lock held
+  std::vector<Leaf*> leaves;
+  for (auto& m : memos)
+    for (auto& p : m->plans)
+      if (p.ok)
+        for (Leaf& L : p.leaves) leaves.push_back(&L);
+  uint32_t gpu_leaves = 0;
+  const auto tg = std::chrono::steady_clock::now();
+  const int rc = leaves.empty() ? GVH_OK : resolve(app, leaves, &gpu_leaves, nullptr);
+  app->st_gpu_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tg).count();
+  if (rc == GVH_OK)
+    for (auto& m : memos)
+      for (auto& p : m->plans) p.resolved = p.ok;
+  lap("resolve");
+  if (keep)
+    for (auto& m : memos) app->memo.put(m);
+  if (n_leaves) *n_leaves = gpu_leaves;
+  if (memos_out) *memos_out = std::move(memos);
+  return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -727,12 +1602,15 @@ gvh_app* gvh_app_new(gv_ctx* gpu) {
 void gvh_app_free(gvh_app* app) { delete app; }
 
 void gvh_set_params(gvh_app* app, uint64_t lim, uint64_t cs, uint64_t ce) {
+  std::lock_guard<std::mutex> lk(app->mu);
   app->sig_limit = lim;
   app->cost_secp = cs;
   app->cost_ed = ce;
 }
 void gvh_set_context(gvh_app* app, const char* chain_id, int64_t height, int recheck, uint64_t gas_limit) {
+  std::lock_guard<std::mutex> lk(app->mu);
   app->chain_id = chain_id ? chain_id : "";
+  app->chain_json = go_json_string(app->chain_id);
   app->height = height;
   app->recheck = recheck != 0;
   app->gas_limit = gas_limit;
@@ -741,20 +1619,18 @@ void gvh_set_context(gvh_app* app, const char* chain_id, int64_t height, int rec
 int gvh_set_account(gvh_app* app, const uint8_t addr20[20], uint64_t num, uint64_t seq, const uint8_t* pub,
                     size_t pub_len) {
   if (!app || !addr20) return GVH_EINVAL;
-  std::array<uint8_t, 20> a;
-  memcpy(a.data(), addr20, 20);
+  Bytes a(addr20, addr20 + 20);
   Account acc;
   acc.number = num;
   acc.sequence = seq;
-  if (pub && pub_len) acc.pub.assign(pub, pub + pub_len);
+  if (pub && pub_len) acc.pub.assign(pub, pub + pub_len);      // info decoded on first use
   std::lock_guard<std::mutex> lk(app->mu);
   app->accounts[a] = acc;
   return GVH_OK;
 }
 int gvh_get_account(gvh_app* app, const uint8_t addr20[20], uint64_t* num, uint64_t* seq, uint8_t* pub_out,
                     size_t* pub_len) {
-  std::array<uint8_t, 20> a;
-  memcpy(a.data(), addr20, 20);
+  Bytes a(addr20, addr20 + 20);
   std::lock_guard<std::mutex> lk(app->mu);
   auto it = app->accounts.find(a);
   if (it == app->accounts.end()) return 0;
@@ -766,130 +1642,181 @@ int gvh_get_account(gvh_app* app, const uint8_t addr20[20], uint64_t* num, uint6
 }
 
 int gvh_ante(gvh_app* app, const uint8_t* tx, size_t tx_len, int simulate, gvh_result* out) {
-  if (!app || !tx || !out) return GVH_EINVAL;
-  FlatTx t;
-  try {
-    t = parse_flat(tx, tx_len);
-  } catch (const std::exception&) {
-    return GVH_EINVAL;
-  }
-  std::lock_guard<std::mutex> lk(app->mu);
-  return run_ante(app, t, simulate != 0, out);
+  if (!app || (!tx && tx_len) || !out) return GVH_EINVAL;
+  return ante_bytes(app, tx, tx_len, simulate != 0, out);
 }
 
-// PreVerifyTxs: (1) decode every tx in parallel, (2) predict each signer's
-// sequence in block order (serial: it is a prefix count per signer), (3) build
-// sign bytes, SHA-256 and the leaves of every (tx, signer) in parallel (the
-// host sign-bytes pipeline of SURVEY.md §8f-3), (4) one GPU batch for the
-// cache misses.
 int gvh_preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, size_t* n_leaves) {
   if (!app || (ntx && (!txs || !lens))) return GVH_EINVAL;
-  std::lock_guard<std::mutex> lk(app->mu);
-  auto T0 = std::chrono::steady_clock::now();
-  auto lap = [&](const char* what) { if (getenv("GVH_PROFILE")) { auto t = std::chrono::steady_clock::now(); fprintf(stderr, "%s %.3f ms\n", what, std::chrono::duration<double, std::milli>(t - T0).count()); T0 = t; } };
-  std::vector<FlatTx> parsed(ntx);
-  std::vector<uint8_t> good(ntx, 0);
-  parallel_for(ntx, app->threads, [&](size_t t) {
-    try {
-      parsed[t] = parse_flat(txs[t], lens[t]);
-      good[t] = 1;
-    } catch (const std::exception&) {
-    }
-  });
-  lap("parse");
-  struct Job {
-    const FlatTx* tx;
-    size_t signer;
-    const Bytes* pub;     // account pubkey, else the tx-supplied one (stable: accounts not modified here)
-    uint64_t accnum, seq;
-  };
-  std::vector<Job> jobs;
-  std::unordered_map<std::array<uint8_t, 20>, uint64_t, AddrHash> seq_bump;   // sequence prediction
-  seq_bump.reserve(ntx * 2);
-  jobs.reserve(ntx);
-  for (size_t t = 0; t < ntx; ++t) {
-    if (!good[t]) continue;
-    const FlatTx& tx = parsed[t];
-    for (size_t i = 0; i < tx.sigs.size() && i < tx.signers.size(); ++i) {
-      auto it = app->accounts.find(tx.signers[i]);
-      if (it == app->accounts.end()) continue;
-      const Account& acc = it->second;
-      const Bytes* pubb = !acc.pub.empty() ? &acc.pub : (i < tx.sig_pubs.size() ? &tx.sig_pubs[i] : nullptr);
-      if (!pubb || pubb->empty()) continue;
-      jobs.push_back(Job{&tx, i, pubb, app->height == 0 ? 0 : acc.number, acc.sequence + seq_bump[tx.signers[i]]});
-    }
-    for (auto& a : tx.signers) seq_bump[a] += 1;
+  return preverify(app, ntx, txs, lens, n_leaves, nullptr, true);
+}
+
+int gvh_deliver_block(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, gvh_result* out) {
+  if (!app || (ntx && (!txs || !lens || !out))) return GVH_EINVAL;
+  std::vector<std::shared_ptr<Memo>> memos;
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = preverify(app, ntx, txs, lens, nullptr, &memos, false);
+  const auto t1 = std::chrono::steady_clock::now();
+  app->st_pre_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+  if (rc != GVH_OK) return rc;
+  for (size_t t = 0; t < ntx; ++t) {                 // the DeliverTx loop, in block order
+    rc = ante_memo(app, memos[t].get(), false, &out[t]);
+    if (rc != GVH_OK) return rc;
   }
-  lap("jobs");
-  std::vector<std::vector<Leaf>> job_leaves(jobs.size());
-  parallel_for(jobs.size(), app->threads, [&](size_t j) {
-    const Job& jb = jobs[j];
-    try {
-      PubKey pk = decode_pubkey(jb.pub->data(), jb.pub->size());
-      std::string sb = std_sign_bytes(app->chain_id, jb.accnum, jb.seq, jb.tx->fee, jb.tx->msgs, jb.tx->memo);
-      Bytes msg(sb.begin(), sb.end());
-      auto dig = sha256(msg.data(), msg.size());
-      build_node(pk, msg, dig, jb.tx->sigs[jb.signer], job_leaves[j]);
-    } catch (const Panic&) {
-      job_leaves[j].clear();   // malformed: the ante chain will report it; nothing to cache
-    }
-  });
-  lap("signbytes");
-  std::vector<Leaf> leaves;
-  for (auto& v : job_leaves) leaves.insert(leaves.end(), v.begin(), v.end());
-  lap("concat");
-  uint32_t gpu_leaves = 0, hits = 0;
-  int rc = leaves.empty() ? GVH_OK : resolve_leaves(app, leaves, &gpu_leaves, &hits);
-  lap("resolve");
-  if (n_leaves) *n_leaves = gpu_leaves;
+  app->st_loop_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
+  return GVH_OK;
+}
+
+int gvh_deliver_gentxs(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, gvh_result* out,
+                       size_t* first_failed) {
+  if (!app) return GVH_EINVAL;
+  int64_t h;
+  uint64_t gl;
+  {
+    std::lock_guard<std::mutex> lk(app->mu);
+    h = app->height;
+    gl = app->gas_limit;
+    app->height = 0;                                  // InitChain context: genesis height, infinite gas
+    app->gas_limit = 0;
+  }
+  const int rc = gvh_deliver_block(app, ntx, txs, lens, out);
+  {
+    std::lock_guard<std::mutex> lk(app->mu);
+    app->height = h;
+    app->gas_limit = gl;
+  }
+  if (first_failed) {
+    *first_failed = ntx;
+    if (rc == GVH_OK)
+      for (size_t t = 0; t < ntx; ++t)
+        if (out[t].code) { *first_failed = t; break; }
+  }
   return rc;
 }
 
-void gvh_set_threads(gvh_app* app, int threads) {
-  if (app) app->threads = std::max(1, std::min(256, threads));
+void gvh_set_window(gvh_app* app, size_t max_txs, int64_t max_wait_us) {
+  std::lock_guard<std::mutex> lk(app->window.m);
+  app->window.max_txs = std::max<size_t>(1, max_txs);
+  app->window.max_wait_us = std::max<int64_t>(0, max_wait_us);
+}
+
+int gvh_checktx(gvh_app* app, const uint8_t* tx, size_t tx_len, gvh_result* out) {
+  if (!app || (!tx && tx_len) || !out) return GVH_EINVAL;
+  Window& w = app->window;
+  int rc = GVH_OK;
+  {
+    std::unique_lock<std::mutex> lk(w.m);
+    if (!w.open) {
+      w.open = std::make_shared<Window::Batch>();
+      w.open->deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(w.max_wait_us);
+    }
+    auto b = w.open;
+    b->items.emplace_back(tx, tx_len);
+    auto flush = [&]() {                              // this caller verifies the window's batch
+      w.open = nullptr;
+      b->flushing = true;
+      lk.unlock();
+      std::vector<const uint8_t*> ptrs;
+      std::vector<size_t> ls;
+      for (auto& it : b->items) { ptrs.push_back(it.first); ls.push_back(it.second); }
+      const int r = preverify(app, ptrs.size(), ptrs.data(), ls.data(), nullptr, nullptr, true);
+      app->st_windows += 1;
+      app->st_window_txs += ptrs.size();
+      lk.lock();
+      b->done = true;
+      w.cv.notify_all();
+      return r;
+    };
+    if (b->items.size() >= w.max_txs) rc = flush();
+    else
+      while (!b->done) {
+        if (b->flushing) { w.cv.wait(lk); continue; }
+        if (w.cv.wait_until(lk, b->deadline) == std::cv_status::timeout && !b->done && !b->flushing && w.open == b)
+          rc = flush();
+      }
+  }
+  if (rc == GVH_EDEVICE) return rc;                  // the GPU failed: the caller falls back
+  return ante_bytes(app, tx, tx_len, false, out);
 }
 
 int gvh_consume_sig_gas(gvh_app* app, const uint8_t* sig, size_t sig_len, const uint8_t* pub_amino, size_t pub_len,
                         uint64_t gas_limit, gvh_result* out) {
   if (!app || !out) return GVH_EINVAL;
-  GasMeter gm{gas_limit};
-  Bytes sg(sig, sig + (sig ? sig_len : 0));
+  GasMeter gm{gas_limit == 0, gas_limit};
+  Span sg{sig, sig ? sig_len : 0};
   try {
     if (!pub_amino || !pub_len) {
       SdkError e = wrap(kErrInvalidPubKey, "unrecognized public key type: <nil>");
-      copy_result(out, &e, gm.used, 0, 0);
+      copy_result(out, &e, gm.used, 0, 0, 0);
       return GVH_OK;
     }
     PubKey pk = decode_pubkey(pub_amino, pub_len);
     SdkError e;
-    if (!consume_sig_gas(gm, sg, pk, app, &e)) copy_result(out, &e, gm.used, 0, 0);
-    else copy_result(out, nullptr, gm.used, 0, 0);
+    if (!consume_sig_gas(gm, sg, pk, app, &e)) copy_result(out, &e, gm.used, 0, 0, 0);
+    else copy_result(out, nullptr, gm.used, 0, 0, 0);
   } catch (const Panic& p) {
     SdkError e = wrap(kErrPanic, p.what());
-    copy_result(out, &e, gm.used, 0, 0);
+    copy_result(out, &e, gm.used, 0, 0, 0);
   } catch (const OutOfGas& o) {
     SdkError e = wrap(kErrOutOfGas, std::string("out of gas in location: ") + o.descriptor);
-    copy_result(out, &e, gm.used, 0, 0);
+    copy_result(out, &e, gm.used, 0, 0, 0);
   }
   return GVH_OK;
 }
 
 void gvh_cache_clear(gvh_app* app) {
-  std::lock_guard<std::mutex> lk(app->mu);
   app->cache.clear();
+  app->memo.clear();
 }
-size_t gvh_cache_size(gvh_app* app) {
-  std::lock_guard<std::mutex> lk(app->mu);
-  return app->cache.size();
+size_t gvh_cache_size(gvh_app* app) { return app->cache.size(); }
+void gvh_set_cache_capacity(gvh_app* app, size_t entries) { app->cache.resize(std::max<size_t>(entries, 512)); }
+
+void gvh_set_threads(gvh_app* app, int threads) {
+  if (app) app->threads = std::max(1, std::min(256, threads));
+}
+
+void gvh_get_stats(gvh_app* app, gvh_stats* o) {
+  memset(o, 0, sizeof *o);
+  o->gpu_calls = app->st_gpu_calls;
+  o->gpu_leaves = app->st_gpu_leaves;
+  o->cache_hits = app->st_hits;
+  o->cache_misses = app->st_misses;
+  o->memo_hits = app->st_memo;
+  o->windows = app->st_windows;
+  o->window_txs = app->st_window_txs;
+  o->cache_entries = app->cache.size();
+  o->cache_capacity = app->cache.capacity();
+  o->preverify_ns = app->st_pre_ns;
+  o->gpu_ns = app->st_gpu_ns;
+  o->deliver_loop_ns = app->st_loop_ns;
 }
 
 size_t gvh_std_sign_bytes(const char* chain_id, uint64_t accnum, uint64_t seq, const char* fee_json,
                           const char* const* msgs_json, size_t n_msgs, const char* memo, uint8_t* out, size_t cap) {
-  std::vector<std::string> msgs;
-  for (size_t i = 0; i < n_msgs; ++i) msgs.emplace_back(msgs_json[i]);
-  std::string s = std_sign_bytes(chain_id ? chain_id : "", accnum, seq, fee_json ? fee_json : "", msgs, memo ? memo : "");
+  std::string s = "{\"account_number\":\"" + std::to_string(accnum) + "\",\"chain_id\":" +
+                  go_json_string(chain_id ? chain_id : "") + ",\"fee\":" + (fee_json ? fee_json : "") + ",\"memo\":" +
+                  go_json_string(memo ? memo : "") + ",\"msgs\":[";
+  for (size_t i = 0; i < n_msgs; ++i) {
+    if (i) s += ",";
+    s += msgs_json[i];
+  }
+  s += "],\"sequence\":\"" + std::to_string(seq) + "\"}";
   if (out) memcpy(out, s.data(), std::min(cap, s.size()));
   return s.size();
+}
+
+size_t gvh_tx_sign_bytes(const uint8_t* tx, size_t tx_len, const char* chain_id, uint64_t accnum, uint64_t seq,
+                         uint8_t* out, size_t cap, char* err, size_t err_cap) {
+  try {
+    auto t = decode_tx(tx, tx_len);
+    const std::string s = sign_bytes(*t, go_json_string(chain_id ? chain_id : ""), accnum, seq);
+    if (out) memcpy(out, s.data(), std::min(cap, s.size()));
+    if (err && err_cap) err[0] = 0;
+    return s.size();
+  } catch (const AminoErr& e) {
+    if (err && err_cap) snprintf(err, err_cap, "%s", e.what());
+    return 0;
+  }
 }
 
 int gvh_pubkey_address(const uint8_t* pub, size_t len, uint8_t out20[20]) {
@@ -904,9 +1831,7 @@ int gvh_pubkey_address(const uint8_t* pub, size_t len, uint8_t out20[20]) {
 }
 
 size_t gvh_bech32_address(const uint8_t addr20[20], char* out, size_t cap) {
-  std::array<uint8_t, 20> a;
-  memcpy(a.data(), addr20, 20);
-  std::string s = acc_string(a);
+  std::string s = acc_string(addr20, 20);
   if (out && cap) snprintf(out, cap, "%s", s.c_str());
   return s.size();
 }

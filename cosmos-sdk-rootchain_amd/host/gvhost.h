@@ -1,37 +1,39 @@
 /*
  * gvhost.h -- C ABI of libgvhost.so: the host-side mirror (C++) of the
- * reference's signature-verification ante path, built on libgpuverify.
+ * reference's signature-verification ante path and of the baseapp batching
+ * hooks around it, built on libgpuverify.
  *
  * The reference is Go (no toolchain in this image), so the layer above the
- * GPU C-ABI is written in C++ and mirrors the reference's decorators with the
- * same names, argument meaning, gas accounting and error (codespace, code,
- * log) results:
+ * GPU C-ABI is written in C++ and mirrors the reference with the same names,
+ * argument meaning, gas accounting and error (codespace, code, log) results:
  *
+ *   DefaultTxDecoder            x/auth/types/stdtx.go:321-338 (amino binary StdTx; bank MsgSend /
+ *                               MsgMultiSend are the registered msgs, x/bank/types/codec.go:26-27)
  *   SetPubKeyDecorator          x/auth/ante/sigverify.go:50-99
  *   ValidateSigCountDecorator   x/auth/ante/sigverify.go:265-294 (+ CountSubKeys stdtx.go:125-137)
  *   SigGasConsumeDecorator      x/auth/ante/sigverify.go:101-153, DefaultSigVerificationGasConsumer :299-322,
  *                               ConsumeMultisignatureVerificationGas :325-338
  *   BatchSigVerificationDecorator  replaces SigVerificationDecorator (sigverify.go:160-216): all leaves of
  *                               a tx (multisig fanned out, tendermint multisig.VerifyBytes semantics) are
- *                               verified in ONE libgpuverify batch; failures are reported in signer order
+ *                               answered from the verdict cache or verified in ONE libgpuverify batch;
+ *                               failures are reported in signer order
  *   IncrementSequenceDecorator  x/auth/ante/sigverify.go:218-259
+ *   SetGasMeter                 x/auth/ante/setup.go:67-76 (limit = the tx's fee gas; infinite at height 0)
  *   PreVerifyTxs                baseapp batching hook: one GPU batch for a block of txs,
  *                               sign bytes predicted with per-signer sequence prediction, verdicts cached
- *                               under (pub33 || sig64 || SHA256(signBytes))
+ *                               under SHA256(pub || sig || SHA256(signBytes)) in a bounded table
+ *   DeliverBlock                the DeliverTx loop of a block (baseapp/abci.go:203-221) after PreVerifyTxs
+ *   CheckTx window              CheckTx (baseapp/abci.go:165-196) through an accumulation window: calls
+ *                               arriving within max_wait_us (or until max_txs) share one GPU batch
+ *   DeliverGenTxs               x/genutil/gentx.go:96-114 (height 0: account number 0, infinite gas)
  *
- * Transactions are passed in a flat encoding (the decoded StdTx the Go shim
- * would hold -- amino tx decoding is out of scope, SURVEY.md §2 "Codec"):
- *   u32 n_msgs, { u32 len, msg sign-bytes JSON (canonical, Msg.GetSignBytes) }
- *   u32 len, fee JSON (StdFee.Bytes(), canonical)
- *   u32 len, memo (UTF-8)
- *   u32 n_signers, { 20-byte address }            (tx.GetSigners() order)
- *   u32 n_sigs,    { u32 len, amino pubkey bytes; u32 len, signature bytes }
- * All integers little-endian.
+ * Transactions are the amino binary StdTx bytes a node receives (DeliverTx /
+ * CheckTx req.Tx).  A tx that does not decode gets code 2 (ErrTxDecode).
  *
  * No CPU fallback for secp256k1: if the GPU batch fails the decorator
  * returns GVH_EDEVICE and the caller (the Go shim) re-verifies with the
- * reference VerifyBytes.  ed25519 multisig leaves are verified on the CPU
- * (OpenSSL), as in the reference.
+ * reference VerifyBytes (fail closed).  ed25519 multisig leaves are verified
+ * on the CPU, as in the reference.
  */
 #ifndef GVHOST_H
 #define GVHOST_H
@@ -51,13 +53,27 @@ extern "C" {
 typedef struct gvh_app gvh_app;
 
 typedef struct gvh_result {
-  uint32_t code;          /* 0 = OK, else the sdk error code (4 unauthorized, 8 invalid pubkey, ...) */
+  uint32_t code;          /* 0 = OK, else the sdk error code (2 tx decode, 4 unauthorized, 8 invalid pubkey, ...) */
   char codespace[16];     /* "sdk" or "undefined" (panic) */
   char log[512];          /* sdkerrors.Wrap(...).Error() text */
   uint64_t gas_used;      /* gas consumed by the decorators that ran */
   uint32_t gpu_leaves;    /* secp256k1 leaves sent to the GPU for this tx */
   uint32_t cache_hits;    /* leaves answered by the verdict cache */
+  uint64_t gas_wanted;    /* the tx's fee gas (0 if it did not decode) */
 } gvh_result;
+
+typedef struct gvh_stats {
+  uint64_t gpu_calls;     /* libgpuverify batches issued */
+  uint64_t gpu_leaves;    /* secp256k1 leaves verified on the GPU */
+  uint64_t cache_hits, cache_misses;
+  uint64_t memo_hits;     /* ante runs that reused PreVerifyTxs' decode + sign bytes */
+  uint64_t windows;       /* CheckTx windows flushed */
+  uint64_t window_txs;    /* txs that went through a window */
+  uint64_t cache_entries, cache_capacity;
+  uint64_t preverify_ns;  /* DeliverBlock: time in PreVerifyTxs (decode + plans + GPU) */
+  uint64_t gpu_ns;        /* time in the GPU batches of PreVerifyTxs */
+  uint64_t deliver_loop_ns; /* DeliverBlock: time in the serial ante loop */
+} gvh_stats;
 
 /* gpu may be NULL (then secp256k1 verification returns GVH_ENOVERIFIER). */
 gvh_app* gvh_app_new(gv_ctx* gpu);
@@ -66,7 +82,8 @@ void gvh_app_free(gvh_app* app);
 /* x/auth params (params.go:16-20 defaults: 7, 1000, 590). */
 void gvh_set_params(gvh_app* app, uint64_t tx_sig_limit, uint64_t sig_cost_secp256k1, uint64_t sig_cost_ed25519);
 /* sdk.Context pieces the decorators read: chain id, block height (0 = genesis:
- * account number 0 in sign bytes), ReCheckTx flag, gas limit (0 = infinite). */
+ * account number 0 in sign bytes, infinite gas), ReCheckTx flag.  gas_limit
+ * 0 = SetGasMeter semantics (the tx's fee gas); nonzero overrides it. */
 void gvh_set_context(gvh_app* app, const char* chain_id, int64_t height, int recheck, uint64_t gas_limit);
 
 /* In-memory AccountKeeper.  pub_amino may be NULL/0 (pubkey not set). */
@@ -76,30 +93,59 @@ int gvh_set_account(gvh_app* app, const uint8_t addr20[20], uint64_t account_num
 int gvh_get_account(gvh_app* app, const uint8_t addr20[20], uint64_t* account_number, uint64_t* sequence,
                     uint8_t* pub_amino_out, size_t* pub_len);
 
-/* SetPubKey -> ValidateSigCount -> SigGasConsume -> BatchSigVerification ->
- * IncrementSequence on one tx.  Returns GVH_OK when the chain ran (the tx
- * verdict is in out->code), or a negative GVH_E* infrastructure error. */
+/* SetUpContext (gas meter) -> SetPubKey -> ValidateSigCount -> SigGasConsume ->
+ * BatchSigVerification -> IncrementSequence on one amino StdTx.  Returns
+ * GVH_OK when the chain ran (the tx verdict is in out->code), or a negative
+ * GVH_E* infrastructure error. */
 int gvh_ante(gvh_app* app, const uint8_t* tx, size_t tx_len, int simulate, gvh_result* out);
 
-/* Pre-verify a block of txs in one GPU batch and fill the verdict cache.
- * Sequences are predicted as state sequence + earlier txs of the same signer
- * in this call.  *n_leaves = secp256k1 leaves verified. */
+/* PreVerifyTxs: decode a block of txs, predict every signer's sign bytes
+ * (sequence = state + earlier txs of the same signer here), verify the cache
+ * misses in ONE GPU batch and fill the verdict cache; the decode and sign
+ * bytes are memoised for the ante runs that follow.  No app lock is held
+ * during the GPU call.  *n_leaves = secp256k1 leaves verified on the GPU. */
 int gvh_preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, size_t* n_leaves);
+/* A block: PreVerifyTxs, then the ante chain of every tx in order (the
+ * DeliverTx loop); out[i] is tx i's result. */
+int gvh_deliver_block(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, gvh_result* out);
+/* genutil.DeliverGenTxs: the block path at height 0 (account number 0,
+ * infinite gas); *first_failed = index of the first tx whose result is not OK
+ * (the reference panics on it), or ntx if all passed. */
+int gvh_deliver_gentxs(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, gvh_result* out,
+                       size_t* first_failed);
+
+/* CheckTx through the accumulation window: thread-safe and blocking; calls
+ * arriving while a window is open share ONE PreVerifyTxs batch, flushed when
+ * it holds max_txs txs or max_wait_us after its first tx; then each call runs
+ * its own ante chain on the cached verdicts.  Defaults: 64 txs, 200 us. */
+int gvh_checktx(gvh_app* app, const uint8_t* tx, size_t tx_len, gvh_result* out);
+void gvh_set_window(gvh_app* app, size_t max_txs, int64_t max_wait_us);
+
 /* DefaultSigVerificationGasConsumer (x/auth/ante/sigverify.go:299-322) on its
  * own: pub_amino NULL/0 = nil pubkey. */
 int gvh_consume_sig_gas(gvh_app* app, const uint8_t* sig, size_t sig_len, const uint8_t* pub_amino, size_t pub_len,
                         uint64_t gas_limit, gvh_result* out);
+
+/* Verdict cache: bounded (CLOCK eviction in 8-way buckets), default 1<<20 entries. */
 void gvh_cache_clear(gvh_app* app);
-/* Host threads for PreVerifyTxs' decode / sign-bytes / SHA-256 stages
- * (default min(4, hardware threads)). */
-void gvh_set_threads(gvh_app* app, int threads);
 size_t gvh_cache_size(gvh_app* app);
+void gvh_set_cache_capacity(gvh_app* app, size_t entries);
+/* Host threads for PreVerifyTxs' decode / sign-bytes / SHA-256 stages
+ * (default min(16, hardware threads)). */
+void gvh_set_threads(gvh_app* app, int threads);
+void gvh_get_stats(gvh_app* app, gvh_stats* out);
 
 /* StdSignBytes (x/auth/types/stdtx.go:292-312): canonical JSON.  Returns the
  * length; writes at most cap bytes. */
 size_t gvh_std_sign_bytes(const char* chain_id, uint64_t account_number, uint64_t sequence,
                           const char* fee_json, const char* const* msgs_json, size_t n_msgs,
                           const char* memo, uint8_t* out, size_t cap);
+/* DefaultTxDecoder + StdTx.GetSignBytes for one amino StdTx: writes the sign
+ * bytes (at most cap) and returns their length; a tx that does not decode
+ * returns 0 and writes the decode error text (NUL-terminated, at most
+ * err_cap bytes) into err. */
+size_t gvh_tx_sign_bytes(const uint8_t* tx, size_t tx_len, const char* chain_id, uint64_t account_number,
+                         uint64_t sequence, uint8_t* out, size_t cap, char* err, size_t err_cap);
 /* crypto.PubKey.Address() of an amino pubkey: secp256k1 RIPEMD160(SHA256(pub33)),
  * multisig SHA256(amino bytes)[:20], ed25519 SHA256(pub32)[:20]. 0 = ok. */
 int gvh_pubkey_address(const uint8_t* pub_amino, size_t len, uint8_t out20[20]);

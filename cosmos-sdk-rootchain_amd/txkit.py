@@ -1,10 +1,14 @@
 """txkit.py -- client-side transaction kit for the host mirror and benchmarks.
 
 Builds what a Cosmos SDK client produces (the reference's client/keyring side,
-out of the GPU path): amino pubkey / multisig encodings, MsgSend sign bytes,
-StdFee JSON, signatures, and the flat decoded-tx encoding that libgvhost
-accepts (host/gvhost.h).  Signing uses OpenSSL via tools/workload/libgvwork.so
-(secp256k1, low-S) and libcrypto EVP (ed25519); nothing here is the oracle.
+out of the GPU path): amino pubkey / multisig encodings, bank MsgSend /
+MsgMultiSend (amino binary + sign-bytes JSON), StdFee, signatures, and the
+amino binary StdTx a node receives (DefaultTxEncoder, x/auth/types/stdtx.go),
+which libgvhost decodes (host/gvhost.h).  An independent Python restatement of
+the go-amino v0.15 binary encoding (registered-name prefixes, field keys,
+unpacked lists, zero values omitted).  Signing uses OpenSSL via
+tools/workload/libgvwork.so (secp256k1, low-S) and libcrypto EVP (ed25519);
+nothing here is the oracle.
 
 Formats (reference pins): amino prefixes crypto/encode_test.go:51-60
 (secp256k1 EB5AE987/0x21, multisig 22C1F7E2); MsgSend sign bytes
@@ -123,6 +127,102 @@ def amino_bytes_field(field: int, b: bytes) -> bytes:
     return uvarint((field << 3) | 2) + uvarint(len(b)) + b
 
 
+def amino_prefix(name: str) -> bytes:
+    """go-amino registered-concrete prefix: SHA256(name), skip zero bytes, 3
+    disambiguation bytes, skip zero bytes, next 4 bytes."""
+    bz = hashlib.sha256(name.encode()).digest()
+    while bz[0] == 0:
+        bz = bz[1:]
+    bz = bz[3:]
+    while bz[0] == 0:
+        bz = bz[1:]
+    return bz[:4]
+
+
+PREFIX_STDTX = amino_prefix("cosmos-sdk/StdTx")
+PREFIX_MSGSEND = amino_prefix("cosmos-sdk/MsgSend")
+PREFIX_MULTISEND = amino_prefix("cosmos-sdk/MsgMultiSend")
+assert amino_prefix("tendermint/PubKeySecp256k1") == PREFIX_SECP    # crypto/encode_test.go:58
+
+
+def _opt_bytes(field: int, b: bytes) -> bytes:
+    return amino_bytes_field(field, b) if b else b""
+
+
+def coins_amino(field: int, coins) -> bytes:
+    """sdk.Coins as an unpacked list of Coin{Denom 1, Amount 2 (sdk.Int text)}."""
+    return b"".join(amino_bytes_field(field, _opt_bytes(1, d.encode()) + _opt_bytes(2, str(a).encode()))
+                    for a, d in coins)
+
+
+class MsgSend:
+    """x/bank MsgSend (types.pb.go:30-34, amino name cosmos-sdk/MsgSend)."""
+
+    def __init__(self, frm: bytes, to: bytes, coins):
+        self.frm, self.to, self.coins = frm, to, list(coins)
+
+    def json(self) -> str:
+        return msg_send_json(self.frm, self.to, self.coins)
+
+    def amino(self) -> bytes:
+        return PREFIX_MSGSEND + _opt_bytes(1, self.frm) + _opt_bytes(2, self.to) + coins_amino(3, self.coins)
+
+    def signers(self):
+        return [self.frm]
+
+
+class MsgMultiSend:
+    """x/bank MsgMultiSend: inputs / outputs of (address, coins)."""
+
+    def __init__(self, inputs, outputs):
+        self.inputs, self.outputs = list(inputs), list(outputs)
+
+    def json(self) -> str:
+        io = lambda xs: [{"address": bech32("cosmos", a), "coins": [{"amount": str(x), "denom": d} for x, d in c]}
+                         for a, c in xs]
+        return sort_json({"type": "cosmos-sdk/MsgMultiSend", "value": {"inputs": io(self.inputs),
+                                                                         "outputs": io(self.outputs)}})
+
+    def amino(self) -> bytes:
+        io = lambda f, xs: b"".join(amino_bytes_field(f, _opt_bytes(1, a) + coins_amino(2, c)) for a, c in xs)
+        return PREFIX_MULTISEND + io(1, self.inputs) + io(2, self.outputs)
+
+    def signers(self):
+        return [a for a, _ in self.inputs]
+
+
+class Fee:
+    def __init__(self, coins, gas: int):
+        self.coins, self.gas = list(coins), gas
+
+    def json(self) -> str:
+        return fee_json(self.coins, self.gas)
+
+    def amino(self) -> bytes:
+        return coins_amino(1, self.coins) + (uvarint(2 << 3) + uvarint(self.gas) if self.gas else b"")
+
+
+def std_tx(msgs, fee: Fee, memo: str, sigs) -> bytes:
+    """Amino binary StdTx (DefaultTxEncoder): prefix, Msgs 1 (interfaces), Fee 2,
+    Signatures 3 {PubKey 1, Signature 2}, Memo 4.  sigs: (pub_amino or b'', sig)."""
+    out = PREFIX_STDTX
+    out += b"".join(amino_bytes_field(1, m.amino()) for m in msgs)
+    out += amino_bytes_field(2, fee.amino())
+    out += b"".join(amino_bytes_field(3, _opt_bytes(1, p) + _opt_bytes(2, s)) for p, s in sigs)
+    out += _opt_bytes(4, memo.encode())
+    return out
+
+
+def tx_signers(msgs):
+    """StdTx.GetSigners(): msg signers in order, duplicates dropped."""
+    out = []
+    for m in msgs:
+        for a in m.signers():
+            if a not in out:
+                out.append(a)
+    return out
+
+
 def amino_secp(pub33: bytes) -> bytes:
     return PREFIX_SECP + uvarint(33) + pub33
 
@@ -199,19 +299,10 @@ def fee_json(coins, gas: int) -> str:
     return sort_json({"amount": [{"amount": str(a), "denom": d} for a, d in coins], "gas": str(gas)})
 
 
-def std_sign_bytes(chain_id: str, accnum: int, seq: int, fee: str, msgs, memo: str) -> bytes:
+def std_sign_bytes(chain_id: str, accnum: int, seq: int, fee, msgs, memo: str) -> bytes:
+    """fee: JSON str or Fee; msgs: JSON strs or Msg objects."""
+    fee = fee.json() if isinstance(fee, Fee) else fee
+    msgs = [m if isinstance(m, str) else m.json() for m in msgs]
     doc = {"account_number": str(accnum), "chain_id": chain_id, "fee": json.loads(fee), "memo": memo,
            "msgs": [json.loads(m) for m in msgs], "sequence": str(seq)}
     return sort_json(doc).encode()
-
-
-# --------------------------------------------------------------- flat tx
-def flat_tx(msgs, fee: str, memo: str, signers, sigs) -> bytes:
-    """sigs: list of (pub_amino or b'', signature bytes)."""
-    def blob(b: bytes) -> bytes:
-        return struct.pack("<I", len(b)) + b
-    out = struct.pack("<I", len(msgs)) + b"".join(blob(m.encode()) for m in msgs)
-    out += blob(fee.encode()) + blob(memo.encode())
-    out += struct.pack("<I", len(signers)) + b"".join(signers)
-    out += struct.pack("<I", len(sigs)) + b"".join(blob(p) + blob(s) for p, s in sigs)
-    return out

@@ -99,6 +99,12 @@ int gv_dev_alloc(gv_ctx* ctx, int dev_slot, size_t bytes, void** d_ptr);
 int gv_dev_free(gv_ctx* ctx, int dev_slot, void* d_ptr);
 int gv_dev_copy(gv_ctx* ctx, int dev_slot, void* dst, const void* src, size_t bytes, int kind);
 int gv_dev_sync(gv_ctx* ctx, int dev_slot);
+/* A non-blocking HIP stream on dev_slot for the gv_dev_* calls' `stream`
+ * argument (callers without a HIP runtime of their own), its synchronisation
+ * and destruction. */
+int gv_dev_stream_create(gv_ctx* ctx, int dev_slot, void** stream_out);
+int gv_dev_stream_sync(gv_ctx* ctx, int dev_slot, void* stream);
+int gv_dev_stream_destroy(gv_ctx* ctx, int dev_slot, void* stream);
 
 /* Account pubkey cache.  The reference amino-decodes and
  * btcec-parses an account's pubkey on every VerifyBytes

@@ -22,7 +22,7 @@ import gpuverify as gvm
 import txkit as T
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FEE = T.fee_json([(150, "atom")], 200000)
+FEE = T.Fee([(150, "atom")], 200000)
 UNAUTH = "signature verification failed; verify correct account sequence and chain-id: unauthorized"
 
 
@@ -41,14 +41,14 @@ KEYS = [Key(i) for i in range(10)]
 
 
 def make_tx(app_chain, signers, accnums, seqs, msgs=None, fee=FEE, memo="", with_pub=True, sign_keys=None):
-    """A MsgSend tx signed by `signers` (Key objects) over their sign bytes."""
-    msgs = msgs or [T.msg_send_json(s.addr, KEYS[9].addr, [(10, "atom")]) for s in signers]
+    """An amino StdTx of MsgSends signed by `signers` (Key objects) over their sign bytes."""
+    msgs = msgs or [T.MsgSend(s.addr, KEYS[9].addr, [(10, "atom")]) for s in signers]
     sign_keys = sign_keys or signers
     sigs = []
     for k, s, an, sq in zip(sign_keys, signers, accnums, seqs):
         sb = T.std_sign_bytes(app_chain, an, sq, fee, msgs, memo)
         sigs.append((s.pub if with_pub else b"", k.sign(sb)))
-    return T.flat_tx(msgs, fee, memo, [s.addr for s in signers], sigs)
+    return T.std_tx(msgs, fee, memo, sigs)
 
 
 def new_app(verifier=None, chain="gv-test", height=1):
@@ -74,7 +74,7 @@ def test_sign_bytes_and_address_goldens():
 
 def test_go_json_escaping_in_sign_bytes():
     memo = 'a<b>&"\\\n é'
-    got = gvhost.std_sign_bytes("c", 1, 2, FEE, [], memo)
+    got = gvhost.std_sign_bytes("c", 1, 2, FEE.json(), [], memo)
     assert got == T.std_sign_bytes("c", 1, 2, FEE, [], memo)
     assert b"\\u003c" in got and b"\\u2028" in got
 
@@ -112,8 +112,8 @@ def test_count_subkeys_and_sig_limit():
     mk = T.amino_multisig(2, [k.pub for k in KEYS[:8]])
     maddr = T.address(mk)
     app.set_account(maddr, 20, 0)
-    tx = T.flat_tx([T.msg_send_json(maddr, KEYS[9].addr, [(1, "atom")])], FEE, "", [maddr],
-                   [(mk, T.multisignature([True, True] + [False] * 6, [b"\x00" * 64, b"\x00" * 64]))])
+    tx = T.std_tx([T.MsgSend(maddr, KEYS[9].addr, [(1, "atom")])], FEE, "",
+                  [(mk, T.multisignature([True, True] + [False] * 6, [b"\x00" * 64, b"\x00" * 64]))])
     rc, r = app.ante(tx)
     assert rc == 0 and r["code"] == 14 and r["log"] == "signatures: 8, limit: 7: maximum number of signatures exceeded"
     app.set_params(tx_sig_limit=8)
@@ -125,14 +125,12 @@ def test_pubkey_mismatch_and_unknown_account():
     app = new_app()
     tx = make_tx(app_chain="gv-test", signers=[KEYS[0]], accnums=[0], seqs=[0])
     # wrong signer: tx claims KEYS[0]'s address but carries KEYS[1]'s pubkey (ante_test.go:535-540)
-    bad = T.flat_tx([T.msg_send_json(KEYS[0].addr, KEYS[9].addr, [(10, "atom")])], FEE, "", [KEYS[0].addr],
-                    [(KEYS[1].pub, b"\x00" * 64)])
+    bad = T.std_tx([T.MsgSend(KEYS[0].addr, KEYS[9].addr, [(10, "atom")])], FEE, "", [(KEYS[1].pub, b"\x00" * 64)])
     rc, r = app.ante(bad)
     assert r["code"] == 8 and r["log"].startswith("pubKey does not match signer address " +
                                                   gvhost.bech32_address(KEYS[0].addr) + " with signer index: 0")
     stranger = Key(200)
-    tx = T.flat_tx([T.msg_send_json(stranger.addr, KEYS[9].addr, [(1, "atom")])], FEE, "", [stranger.addr],
-                   [(stranger.pub, b"\x00" * 64)])
+    tx = T.std_tx([T.MsgSend(stranger.addr, KEYS[9].addr, [(1, "atom")])], FEE, "", [(stranger.pub, b"\x00" * 64)])
     rc, r = app.ante(tx)
     assert r["code"] == 9 and r["log"] == f"account {gvhost.bech32_address(stranger.addr)} does not exist: unknown address"
 
@@ -145,8 +143,7 @@ def test_recheck_and_simulate_skip_verification():
     assert rc == 0 and r["code"] == 0 and r["gpu_leaves"] == 0 and r["gas_used"] == 1000
     assert app.get_account(KEYS[0].addr)["sequence"] == 0          # no increment on ReCheck
     app.set_context("gv-test", 1)
-    sim = T.flat_tx([T.msg_send_json(KEYS[1].addr, KEYS[9].addr, [(1, "atom")])], FEE, "", [KEYS[1].addr],
-                    [(b"", b"")])
+    sim = T.std_tx([T.MsgSend(KEYS[1].addr, KEYS[9].addr, [(1, "atom")])], FEE, "", [(b"", b"")])
     rc, r = app.ante(sim, simulate=True)        # Simulate: sim pubkey for gas, no verification
     assert rc == 0 and r["code"] == 0 and r["gas_used"] == 1000
     assert app.get_account(KEYS[1].addr)["sequence"] == 1
@@ -154,9 +151,9 @@ def test_recheck_and_simulate_skip_verification():
 
 def test_wrong_number_of_signatures():
     app = new_app()
-    msgs = [T.msg_send_json(KEYS[0].addr, KEYS[9].addr, [(1, "atom")]), T.msg_send_json(KEYS[1].addr, KEYS[9].addr, [(1, "atom")])]
+    msgs = [T.MsgSend(KEYS[0].addr, KEYS[9].addr, [(1, "atom")]), T.MsgSend(KEYS[1].addr, KEYS[9].addr, [(1, "atom")])]
     app.set_account(KEYS[0].addr, 0, 0, KEYS[0].pub)
-    tx = T.flat_tx(msgs, FEE, "", [KEYS[0].addr, KEYS[1].addr], [(KEYS[0].pub, b"\x00" * 64)])
+    tx = T.std_tx(msgs, FEE, "", [(KEYS[0].pub, b"\x00" * 64)])
     rc, r = app.ante(tx)
     assert r["code"] == 4 and r["log"] == "invalid number of signer;  expected: 2, got 1: unauthorized"
 
@@ -166,10 +163,10 @@ def test_multisig_structural_rejects_need_no_gpu():
     mk = T.amino_multisig(2, [k.pub for k in KEYS[:3]])
     maddr = T.address(mk)
     app.set_account(maddr, 30, 0)
-    msg = [T.msg_send_json(maddr, KEYS[9].addr, [(1, "atom")])]
+    msg = [T.MsgSend(maddr, KEYS[9].addr, [(1, "atom")])]
     for bits, nsig in (([True, False, False], 1),          # fewer than K signatures
                        ([True, True, False, False], 2)):    # bit array size != number of keys
-        tx = T.flat_tx(msg, FEE, "", [maddr], [(mk, T.multisignature(bits, [b"\x00" * 64] * nsig))])
+        tx = T.std_tx(msg, FEE, "", [(mk, T.multisignature(bits, [b"\x00" * 64] * nsig))])
         rc, r = app.ante(tx)
         assert rc == 0 and r["code"] == 4 and r["log"] == UNAUTH and r["gpu_leaves"] == 0
 
@@ -220,17 +217,16 @@ def test_multi_signer_and_first_failure_order(ver):
     assert r["code"] == 0 and r["gpu_leaves"] == 3 and r["gas_used"] == 3000
     # signer 1 signs with the wrong key; signer 2 has no pubkey anywhere
     app2 = new_app(ver)
-    msgs = [T.msg_send_json(k.addr, KEYS[9].addr, [(10, "atom")]) for k in KEYS[:3]]
+    msgs = [T.MsgSend(k.addr, KEYS[9].addr, [(10, "atom")]) for k in KEYS[:3]]
     sb = [T.std_sign_bytes("gv-test", i, 0, FEE, msgs, "") for i in range(3)]
-    tx = T.flat_tx(msgs, FEE, "", [k.addr for k in KEYS[:3]],
-                   [(KEYS[0].pub, KEYS[0].sign(sb[0])), (KEYS[1].pub, KEYS[5].sign(sb[1])), (b"", b"\x00" * 64)])
+    tx = T.std_tx(msgs, FEE, "", [(KEYS[0].pub, KEYS[0].sign(sb[0])), (KEYS[1].pub, KEYS[5].sign(sb[1])),
+                                  (b"", b"\x00" * 64)])
     rc, r = app2.ante(tx)
     assert r["code"] == 8 and "unrecognized public key type" in r["log"]   # gas stage sees the nil pubkey first
     app3 = new_app(ver)
     app3.set_account(KEYS[2].addr, 2, 0, KEYS[2].pub)
-    tx = T.flat_tx(msgs, FEE, "", [k.addr for k in KEYS[:3]],
-                   [(KEYS[0].pub, KEYS[0].sign(sb[0])), (KEYS[1].pub, KEYS[5].sign(sb[1])),
-                    (KEYS[2].pub, KEYS[2].sign(sb[2]))])
+    tx = T.std_tx(msgs, FEE, "", [(KEYS[0].pub, KEYS[0].sign(sb[0])), (KEYS[1].pub, KEYS[5].sign(sb[1])),
+                                  (KEYS[2].pub, KEYS[2].sign(sb[2]))])
     rc, r = app3.ante(tx)
     assert r["code"] == 4 and r["log"] == UNAUTH and r["gpu_leaves"] == 3
     assert app3.get_account(KEYS[0].addr)["sequence"] == 0        # failed tx: no increment
@@ -246,26 +242,26 @@ def test_multisig_k_of_n(ver):
     mk = T.amino_multisig(3, pubs)
     maddr = T.address(mk)
     app.set_account(maddr, 40, 0)
-    msgs = [T.msg_send_json(maddr, KEYS[9].addr, [(5, "atom")])]
+    msgs = [T.MsgSend(maddr, KEYS[9].addr, [(5, "atom")])]
     sb = T.std_sign_bytes("gv-test", 40, 0, FEE, msgs, "")
     bits = [True, False, True, False, True, True]
     sigs = [subs[0].sign(sb), subs[2].sign(sb), subs[4].sign(sb), T.ed25519_sign(ed_seed, sb)]
-    tx = T.flat_tx(msgs, FEE, "", [maddr], [(mk, T.multisignature(bits, sigs))])
+    tx = T.std_tx(msgs, FEE, "", [(mk, T.multisignature(bits, sigs))])
     rc, r = app.ante(tx)
     assert rc == 0 and r["code"] == 0 and r["gpu_leaves"] == 3 and r["gas_used"] == 3 * 1000 + 590
     # one bad secp256k1 leaf -> whole multisig false
     sb1 = T.std_sign_bytes("gv-test", 40, 1, FEE, msgs, "")
     bad = [subs[0].sign(sb1), subs[1].sign(sb1), subs[4].sign(sb1), T.ed25519_sign(ed_seed, sb1)]
-    tx = T.flat_tx(msgs, FEE, "", [maddr], [(b"", T.multisignature(bits, bad))])
+    tx = T.std_tx(msgs, FEE, "", [(b"", T.multisignature(bits, bad))])
     rc, r = app.ante(tx)
     assert r["code"] == 4 and r["log"] == UNAUTH
     # bad ed25519 leaf
     ok = [subs[0].sign(sb1), subs[2].sign(sb1), subs[4].sign(sb1), T.ed25519_sign(ed_seed, sb1 + b"x")]
-    tx = T.flat_tx(msgs, FEE, "", [maddr], [(b"", T.multisignature(bits, ok))])
+    tx = T.std_tx(msgs, FEE, "", [(b"", T.multisignature(bits, ok))])
     rc, r = app.ante(tx)
     assert r["code"] == 4
     ok[3] = T.ed25519_sign(ed_seed, sb1)
-    tx = T.flat_tx(msgs, FEE, "", [maddr], [(b"", T.multisignature(bits, ok))])
+    tx = T.std_tx(msgs, FEE, "", [(b"", T.multisignature(bits, ok))])
     rc, r = app.ante(tx)
     assert r["code"] == 0
 
@@ -314,7 +310,7 @@ def test_parallel_preverify_matches_serial_and_plain_ante(ver):
             txs.append(tx)
             if t not in (101, 202):                            # a rejected tx leaves the sequence
                 seqs[k.addr] += 1
-        txs.insert(150, b"\x01\x02")                           # malformed flat tx
+        txs.insert(150, b"\x01\x02")                           # undecodable bytes
         return txs
 
     txs = block()
@@ -334,4 +330,4 @@ def test_parallel_preverify_matches_serial_and_plain_ante(ver):
     assert results[0] == results[1]
     assert results[0][0] == results[2][0]
     codes = [o[1] for o in results[0][0] if len(o) > 1]
-    assert codes.count(0) == 398 and codes.count(4) == 2
+    assert codes.count(0) == 398 and codes.count(4) == 2 and codes.count(2) == 1   # 2: ErrTxDecode

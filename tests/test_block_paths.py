@@ -1,0 +1,310 @@
+"""Block-level paths of the host mirror on the GPU.
+
+* C4 multisig block replay: 2-of-3, 3-of-5 and 4-of-7 PubKeyMultisigThreshold
+  accounts (x/auth/ante/sigverify.go:312-338; ante_test.go:416-464 for the
+  multi-signer shape) with bad leaves, short bit arrays, too few signatures,
+  wrong sequences and ed25519 leaves, replayed through DeliverBlock
+  (PreVerifyTxs + the ante loop).  Every tx's code, log and gas is compared
+  with an expectation computed here from the oracle (secp256k1 leaves:
+  oracle.verify_bytes over the sign bytes of the state's sequence) and a
+  Python restatement of tendermint multisig.VerifyBytes + the gas consumer.
+* DeliverBlock == the per-tx ante without pre-verification, tx by tx.
+* CheckTx accumulation window: concurrent calls share GPU batches and get the
+  verdicts of the serial path.
+* DeliverGenTxs (x/genutil/gentx.go:96-114): height 0, account number 0.
+* The bounded verdict cache stays within its capacity and never changes a verdict.
+"""
+import hashlib
+import random
+import struct
+import threading
+
+import numpy as np
+import pytest
+
+import gpuverify as gvm
+import gvhost
+import txkit as T
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CHAIN = "gv-c4"
+FEE = T.Fee([(0, "stake")], 1000000)
+UNAUTH = "signature verification failed; verify correct account sequence and chain-id: unauthorized"
+
+
+@pytest.fixture(scope="module")
+def ver():
+    v = gvm.Verifier([0])
+    yield v
+    v.close()
+
+
+class SecpKey:
+    def __init__(self, tag: bytes):
+        self.priv = T.privkey_from_secret(b"c4-" + tag)
+        self.pub33 = T.secp_pubkey(self.priv)
+        self.amino = T.amino_secp(self.pub33)
+        self.ed = False
+
+    def sign(self, msg):
+        return T.secp_sign(self.priv, msg)
+
+
+class EdKey:
+    def __init__(self, tag: bytes):
+        self.seed, self.pub32 = T.ed25519_keypair(hashlib.sha256(b"ed-" + tag).digest())
+        self.amino = T.amino_ed25519(self.pub32)
+        self.ed = True
+
+    def sign(self, msg):
+        return T.ed25519_sign(self.seed, msg)
+
+
+class MultiAcct:
+    def __init__(self, idx, k, n, with_ed=False):
+        self.k, self.n = k, n
+        self.subs = [SecpKey(struct.pack("<QQ", idx, j)) for j in range(n)]
+        if with_ed:
+            self.subs[-1] = EdKey(struct.pack("<QQ", idx, n))
+        self.amino = T.amino_multisig(k, [s.amino for s in self.subs])
+        self.addr = T.address(self.amino)
+        self.number = 100 + idx
+
+
+def leaf_ok(key, msg, sig):
+    if len(sig) != 64:
+        return False
+    if key.ed:
+        return sig == key.sign(msg)                    # ed25519 signatures are deterministic
+    return O.verify_bytes(key.pub33, msg, sig)
+
+
+def expect(acct, seq_state, tx_parts):
+    """(code, log, gas) of the ante chain for one multisig tx, restating
+    DefaultSigVerificationGasConsumer + multisig.VerifyBytes; leaves by the oracle."""
+    msgs, bits, sigs, claimed = tx_parts
+    gas = 0
+    si = 0
+    for i, b in enumerate(bits):                       # gas consumer: per set bit (sigverify.go:325-338)
+        if b:
+            gas += 590 if acct.subs[i].ed else 1000
+            si += 1
+    msg = T.std_sign_bytes(CHAIN, acct.number, seq_state, FEE, msgs, "")
+    ok = len(bits) == acct.n and acct.k <= len(sigs) <= len(bits) and sum(bits) >= acct.k
+    if ok:
+        j = 0
+        for i, b in enumerate(bits):
+            if b:
+                ok = ok and leaf_ok(acct.subs[i], msg, sigs[j])
+                j += 1
+                if not ok:
+                    break
+    return (0, "", gas) if ok else (4, UNAUTH, gas)
+
+
+def build_block(accts, seqs, rng, ntx, sink):
+    """Txs with their parts.  Each tx is signed for the sequence its signer
+    expects (the state plus the earlier well-formed txs of the block); some
+    are malformed on purpose, and some claim a wrong sequence."""
+    seqs = dict(seqs)
+    txs, parts = [], []
+    for t in range(ntx):
+        a = accts[t % len(accts)]
+        wrong_seq = rng.random() < 0.04
+        claimed = seqs[a.addr] + (3 if wrong_seq else 0)
+        msgs = [T.MsgSend(a.addr, sink, [(1 + t % 7, "foocoin")])]
+        sb = T.std_sign_bytes(CHAIN, a.number, claimed, FEE, msgs, "")
+        chosen = sorted(rng.sample(range(a.n), a.k))
+        bits = [i in chosen for i in range(a.n)]
+        sigs = [a.subs[i].sign(sb) for i in chosen]
+        kind = rng.random()
+        if kind < 0.05:                                  # bad leaf: signed by another key
+            j = rng.randrange(len(sigs))
+            sigs[j] = (EdKey(b"intruder") if a.subs[chosen[j]].ed else SecpKey(b"intruder")).sign(sb)
+        elif kind < 0.08:                                # corrupted leaf bytes
+            j = rng.randrange(len(sigs))
+            sigs[j] = sigs[j][:10] + bytes([sigs[j][10] ^ 1]) + sigs[j][11:]
+        elif kind < 0.11:                                # too few signatures
+            bits[chosen[-1]] = False
+            sigs = sigs[:-1]
+        elif kind < 0.14:                                # short bit array
+            bits = bits[:-1]
+            sigs = sigs[:sum(bits)]
+        elif kind < 0.16:                                # short signature (VerifyBytes' length check)
+            sigs[0] = sigs[0][:63]
+        elif not wrong_seq:
+            seqs[a.addr] += 1
+        txs.append(T.std_tx(msgs, FEE, "", [(a.amino, T.multisignature(bits, sigs))]))
+        parts.append((a, (msgs, bits, sigs, claimed)))
+    return txs, parts
+
+
+def check_block(results, parts, state_seq):
+    for r, (a, p) in zip(results, parts):
+        code, log, gas = expect(a, state_seq[a.addr], p)
+        assert (r["code"], r["log"]) == (code, log), (p[1], p[3], state_seq[a.addr])
+        assert r["gas_used"] == gas
+        if code == 0:
+            state_seq[a.addr] += 1
+
+
+def test_c4_multisig_block_replay(ver):
+    rng = random.Random(0xC4)
+    shapes = [(2, 3, False), (3, 5, False), (4, 7, False), (2, 3, True), (3, 5, True)]
+    accts = [MultiAcct(i, *shapes[i % len(shapes)]) for i in range(15)]
+    sink = SecpKey(b"sink")
+    sink_addr = T.address(sink.amino)
+    app = gvhost.HostApp(ver, chain_id=CHAIN, height=5)
+    for a in accts:
+        app.set_account(a.addr, a.number, 0)
+    seqs = {a.addr: 0 for a in accts}
+    total_gpu = 0
+    for blk in range(3):
+        txs, parts = build_block(accts, seqs, rng, 300, sink_addr)
+        rc, res = app.deliver_block(txs)
+        assert rc == 0
+        check_block(res, parts, seqs)
+        total_gpu += sum(r["gpu_leaves"] for r in res)
+    codes = [r["code"] for r in res]
+    assert set(codes) == {0, 4} and codes.count(0) > 200
+    st = app.stats()
+    assert st["gpu_calls"] >= 3 and st["memo_hits"] > 0
+    app.close()
+
+
+def test_deliver_block_equals_plain_ante(ver):
+    """Same block through DeliverBlock (pre-verified, memoised) and through the
+    per-tx ante with no pre-verification: identical results tx by tx."""
+    rng = random.Random(11)
+    accts = [MultiAcct(50 + i, 2, 3, with_ed=(i % 2 == 1)) for i in range(6)]
+    singles = [SecpKey(b"single-%d" % i) for i in range(8)]
+    sink = T.address(SecpKey(b"sink2").amino)
+    txs = []
+    seqs = {a.addr: 0 for a in accts}
+    sseq = [0] * len(singles)
+    for t in range(240):
+        if t % 2:
+            a = accts[t % len(accts)]
+            msgs = [T.MsgSend(a.addr, sink, [(1, "x")])]
+            sb = T.std_sign_bytes(CHAIN, a.number, seqs[a.addr], FEE, msgs, "")
+            sigs = [a.subs[0].sign(sb), a.subs[1].sign(sb)]
+            if t % 17 == 0:
+                sigs[1] = sigs[0]
+            txs.append(T.std_tx(msgs, FEE, "", [(a.amino, T.multisignature([True, True, False], sigs))]))
+            seqs[a.addr] += t % 17 != 0
+        else:
+            i = t % len(singles)
+            k = singles[i]
+            addr = T.address(k.amino)
+            msgs = [T.MsgSend(addr, sink, [(2, "y")])]
+            sb = T.std_sign_bytes(CHAIN, 7 + i, sseq[i], FEE, msgs, "memo")
+            txs.append(T.std_tx(msgs, FEE, "memo", [(k.amino, k.sign(sb))]))
+            sseq[i] += 1
+    txs.insert(77, b"\x00garbage")
+
+    def fresh():
+        app = gvhost.HostApp(ver, chain_id=CHAIN, height=9)
+        for a in accts:
+            app.set_account(a.addr, a.number, 0)
+        for i, k in enumerate(singles):
+            app.set_account(T.address(k.amino), 7 + i, 0)
+        return app
+
+    app = fresh()
+    rc, blk = app.deliver_block(txs)
+    assert rc == 0
+    app.close()
+    app = fresh()
+    plain = []
+    for tx in txs:
+        rc, r = app.ante(tx)
+        assert rc == 0
+        plain.append(r)
+    app.close()
+    strip = lambda r: (r["code"], r["log"], r["gas_used"], r["gas_wanted"])
+    assert [strip(r) for r in blk] == [strip(r) for r in plain]
+    codes = [r["code"] for r in blk]
+    assert codes.count(2) == 1 and codes.count(4) >= 5 and codes.count(0) > 200
+
+
+def test_checktx_window_batches_concurrent_calls(ver):
+    keys = [SecpKey(b"ck-%d" % i) for i in range(96)]
+    sink = T.address(SecpKey(b"ck-sink").amino)
+    txs = []
+    for i, k in enumerate(keys):
+        addr = T.address(k.amino)
+        msgs = [T.MsgSend(addr, sink, [(3, "z")])]
+        sb = T.std_sign_bytes(CHAIN, i, 0, FEE, msgs, "")
+        sig = k.sign(sb) if i % 9 else SecpKey(b"other").sign(sb)
+        txs.append(T.std_tx(msgs, FEE, "", [(k.amino, sig)]))
+    app = gvhost.HostApp(ver, chain_id=CHAIN, height=3)
+    for i, k in enumerate(keys):
+        app.set_account(T.address(k.amino), i, 0)
+    app.set_window(32, 20000)
+    out = [None] * len(txs)
+    start = threading.Barrier(len(txs))
+
+    def worker(i):
+        start.wait()
+        out[i] = app.checktx(txs[i])
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(len(txs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    st = app.stats()
+    assert st["window_txs"] == len(txs) and st["windows"] <= len(txs) // 8
+    for i, (rc, r) in enumerate(out):
+        assert rc == 0 and r["code"] == (4 if i % 9 == 0 else 0), (i, r)
+        assert r["cache_hits"] == 1 and r["gpu_leaves"] == 0
+    app.close()
+
+
+def test_deliver_gentxs_height_zero(ver):
+    """genutil.DeliverGenTxs: sign bytes with account number 0, infinite gas;
+    the first failing gentx is reported (the reference panics on it)."""
+    keys = [SecpKey(b"gen-%d" % i) for i in range(5)]
+    txs = []
+    for i, k in enumerate(keys):
+        addr = T.address(k.amino)
+        msgs = [T.MsgSend(addr, addr, [(1, "stake")])]
+        fee = T.Fee([], 0)                                   # gas 0: infinite meter at height 0
+        sb = T.std_sign_bytes(CHAIN, 0, 0, fee, msgs, "")   # account number 0 at genesis
+        if i == 3:
+            sb = T.std_sign_bytes(CHAIN, 40 + i, 0, fee, msgs, "")   # signed with the real number: rejected
+        txs.append(T.std_tx(msgs, fee, "", [(k.amino, k.sign(sb))]))
+    app = gvhost.HostApp(ver, chain_id=CHAIN, height=12)
+    for i, k in enumerate(keys):
+        app.set_account(T.address(k.amino), 40 + i, 0)
+    rc, res, first = app.deliver_gentxs(txs)
+    assert rc == 0 and first == 3
+    assert [r["code"] for r in res] == [0, 0, 0, 4, 0]
+    assert all(r["gas_used"] == 1000 for r in res)
+    app.close()
+
+
+def test_bounded_verdict_cache(ver):
+    keys = [SecpKey(b"cap-%d" % i) for i in range(40)]
+    sink = T.address(SecpKey(b"cap-sink").amino)
+    app = gvhost.HostApp(ver, chain_id=CHAIN, height=2)
+    app.set_cache_capacity(512)
+    for i, k in enumerate(keys):
+        app.set_account(T.address(k.amino), i, 0)
+    for blk in range(3):
+        txs = []
+        for r in range(25):
+            for i, k in enumerate(keys):
+                addr = T.address(k.amino)
+                msgs = [T.MsgSend(addr, sink, [(1, "c")])]
+                seq = blk * 25 + r
+                sb = T.std_sign_bytes(CHAIN, i, seq, FEE, msgs, "")
+                txs.append(T.std_tx(msgs, FEE, "", [(k.amino if seq == 0 else b"", k.sign(sb))]))
+        rc, codes = app.deliver_block_codes(txs)
+        assert rc == 0 and (codes == 0).all()
+        assert app.cache_size() <= 512
+    st = app.stats()
+    assert st["cache_capacity"] == 512 and st["cache_entries"] <= 512
+    app.close()

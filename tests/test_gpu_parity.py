@@ -364,8 +364,7 @@ def test_overlapping_device_calls_on_separate_streams(ver):
     back to back with no host sync: every use of the device scratch is ordered
     after the previous one (gv_runtime.cpp set_acquire/set_release), so no call
     overwrites the inputs of kernels still in flight."""
-    torch = pytest.importorskip("torch")
-    s1, s2 = torch.cuda.Stream(device=0), torch.cuda.Stream(device=0)
+    s1, s2 = ver.stream_create(), ver.stream_create()
     batches = [make_random_batch(60000, seed=300 + k, adversarial=0.3, nkeys=97) for k in range(2)]
     wants = [O.verify_digests(*b, threads=16) for b in batches]
     bufs = []
@@ -376,11 +375,11 @@ def test_overlapping_device_calls_on_separate_streams(ver):
         bufs.append(d + [ver.dev_alloc(((len(pub) + 63) // 64) * 8)])
     try:
         for (pub, _, _), d, st in zip(batches, bufs, (s1, s2)):
-            ver.dev_verify_digests(0, len(pub), d[0], d[1], d[2], d[3], stream=st.cuda_stream)
+            ver.dev_verify_digests(0, len(pub), d[0], d[1], d[2], d[3], stream=st)
         pub3, sig3, dig3 = make_random_batch(3000, seed=399, adversarial=0.3, nkeys=5)
         got3 = ver.verify_batch_digests(pub3, sig3, dig3)
-        s1.synchronize()
-        s2.synchronize()
+        ver.stream_sync(s1)
+        ver.stream_sync(s2)
         assert np.array_equal(got3, O.verify_digests(pub3, sig3, dig3, threads=8))
         for (pub, _, _), d, want in zip(batches, bufs, wants):
             bits = np.zeros((len(pub) + 63) // 64, dtype=np.uint64)
@@ -390,6 +389,8 @@ def test_overlapping_device_calls_on_separate_streams(ver):
         for d in bufs:
             for p in d:
                 ver.dev_free(p)
+        ver.stream_destroy(s1)
+        ver.stream_destroy(s2)
 
 
 @pytest.mark.parametrize("chunk", [256, 4096, 0])

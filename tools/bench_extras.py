@@ -178,22 +178,27 @@ def msg_path(ver, wl, n: int, threads: int, nkeys: int = 10000, steps: int = 3):
     return out
 
 
-def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500):
+def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: int = 64):
+    """BASELINE.json configs[0] shape: 10k single-signer bank MsgSend txs (amino
+    StdTx) through the host mirror: the block path (DeliverBlock = PreVerifyTxs,
+    one GPU batch, then the DeliverTx ante loop), the per-tx path with no
+    batching (one GPU call per tx) and the CheckTx accumulation window (txs
+    submitted from concurrent threads)."""
+    import threading
     import gvhost
     import txkit as T
     keys = []
     for i in range(ntx + 1):
         priv = T.privkey_from_secret(b"gv-c1-" + struct.pack("<Q", i))
-        pub33 = T.secp_pubkey(priv)
-        amino = T.amino_secp(pub33)
+        amino = T.amino_secp(T.secp_pubkey(priv))
         keys.append((priv, amino, T.address(amino)))
-    fee = T.fee_json([(0, "stake")], 1000000)
+    fee = T.Fee([(0, "stake")], 1000000)
     txs = []
     for i in range(ntx):
         priv, amino, addr = keys[i]
-        msg = T.msg_send_json(addr, keys[i + 1][2], [(10, "foocoin")])
-        sb = T.std_sign_bytes("gv-bench", i, 0, fee, [msg], "")
-        txs.append(T.flat_tx([msg], fee, "", [addr], [(amino, T.secp_sign(priv, sb))]))
+        msgs = [T.MsgSend(addr, keys[i + 1][2], [(10, "foocoin")])]
+        sb = T.std_sign_bytes("gv-bench", i, 0, fee, msgs, "")
+        txs.append(T.std_tx(msgs, fee, "", [(amino, T.secp_sign(priv, sb))]))
 
     def fresh_app():
         app = gvhost.HostApp(ver, chain_id="gv-bench", height=1)
@@ -201,19 +206,16 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500):
             app.set_account(keys[i][2], i, 0)
         return app
 
-    # block path: PreVerifyTxs (one GPU batch) + the ante chain per tx
+    app = fresh_app()                                 # warm-up (buffers, threads)
+    app.deliver_block(txs[:512])
+    app.close()
     app = fresh_app()
     t = time.perf_counter()
-    rc, leaves = app.preverify(txs)
-    t_pre = time.perf_counter() - t
-    ok = 0
-    hits = 0
-    for tx in txs:
-        rc_a, r = app.ante(tx)
-        ok += rc_a == 0 and r["code"] == 0
-        hits += r["cache_hits"]
+    rc, codes = app.deliver_block_codes(txs)
     t_block = time.perf_counter() - t
+    st = app.stats()
     app.close()
+    assert rc == 0
     # per-tx path (CheckTx without batching): one GPU call per tx
     app = fresh_app()
     m = min(per_tx_sample, ntx)
@@ -224,83 +226,135 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500):
         ok2 += rc_a == 0 and r["code"] == 0
     t_single = time.perf_counter() - t
     app.close()
-    return {"txs": ntx, "block_path": {"txs_per_s": round(ntx / t_block, 1), "total_ms": round(t_block * 1e3, 2),
-                                       "preverify_ms": round(t_pre * 1e3, 2), "accepted": ok, "cache_hits": hits,
-                                       "gpu_leaves": leaves},
+    # CheckTx window: the txs submitted by concurrent callers
+    app = fresh_app()
+    app.set_window(256, 500)
+    nw = min(ntx, 4096)
+    res = [None] * nw
+    it = iter(range(nw))
+    lock = threading.Lock()
+
+    def worker():
+        while True:
+            with lock:
+                i = next(it, None)
+            if i is None:
+                return
+            res[i] = app.checktx(txs[i])
+
+    th = [threading.Thread(target=worker) for _ in range(checktx_threads)]
+    t = time.perf_counter()
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    t_win = time.perf_counter() - t
+    wst = app.stats()
+    app.close()
+    okw = sum(1 for rc_a, r in res if rc_a == 0 and r["code"] == 0)
+    return {"txs": ntx,
+            "block_path": {"txs_per_s": round(ntx / t_block, 1), "total_ms": round(t_block * 1e3, 2),
+                           "preverify_ms": round(st["preverify_ns"] / 1e6, 2), "gpu_ms": round(st["gpu_ns"] / 1e6, 2),
+                           "ante_loop_ms": round(st["deliver_loop_ns"] / 1e6, 2),
+                           "accepted": int((codes == 0).sum()), "gpu_leaves": st["gpu_leaves"],
+                           "memo_hits": st["memo_hits"]},
             "per_tx_path": {"txs": m, "txs_per_s": round(m / t_single, 1), "accepted": ok2},
-            "note": "host mirror (libgvhost) of SetPubKey/ValidateSigCount/SigGasConsume/BatchSigVerification/"
-                    "IncrementSequence over libgpuverify; sign bytes rebuilt per tx in C++; host buffers"}
+            "checktx_window": {"txs": nw, "callers": checktx_threads, "txs_per_s": round(nw / t_win, 1),
+                               "windows": wst["windows"], "accepted": okw, "max_txs": 256, "max_wait_us": 500},
+            "note": "host mirror (libgvhost) of DefaultTxDecoder + SetPubKey/ValidateSigCount/SigGasConsume/"
+                    "BatchSigVerification/IncrementSequence over libgpuverify; amino StdTx bytes in, host buffers"}
 
 
-def c4_multisig(ver, wl=None, ntx: int = 30000, block: int = 10000, naccounts: int = 96, threads: int = 16):
-    """BASELINE.json configs[3] shape on one GPU: k-of-n threshold multisig
-    MsgSend txs (2-of-3, 3-of-5, 4-of-7 in equal shares), replayed in blocks of
-    `block` txs: gvh_preverify (every secp256k1 leaf of the block in one GPU
-    batch, sequences predicted per signer) then the ante chain per tx.
-    wl: tools/workload/libgvwork.so handle (batch signing with OpenSSL)."""
+def c4_workload(wl, n_accounts: int = 30000, txs_per_account: int = 89, threads: int = 16, chain: str = "gv-bench"):
+    """BASELINE.json configs[3]: k-of-n multisig MsgSend txs (2-of-3, 3-of-5,
+    4-of-7 accounts in equal shares, the first k bits set), amino StdTx bytes in
+    one buffer.  Tx t is account t % n_accounts at sequence t // n_accounts.
+    Returns (blob, offsets, lengths, accounts [(addr, accnum)], leaves)."""
     import hashlib
-    import gvhost
     import txkit as T
     shapes = [(2, 3), (3, 5), (4, 7)]
-    privs, accts = [], []
-    for a in range(naccounts):
-        k, nsub = shapes[a % 3]
-        base = len(privs)
-        amino = []
-        for j in range(nsub):
-            priv = T.privkey_from_secret(b"gv-c4-" + struct.pack("<QQ", a, j))
-            privs.append(priv)
-            amino.append(T.amino_secp(T.secp_pubkey(priv)))
-        mk = T.amino_multisig(k, amino)
-        accts.append((k, nsub, base, mk, T.address(mk)))
-    sink = T.address(T.amino_secp(T.secp_pubkey(T.privkey_from_secret(b"gv-c4-sink"))))
-    fee = T.fee_json([(0, "stake")], 1000000)
-    msgs, kidx, digs = [], [], []
-    for i in range(ntx):
-        a = i % naccounts
-        k, nsub, base, mk, addr = accts[a]
-        msg = T.msg_send_json(addr, sink, [(1, "foocoin")])
-        sb = T.std_sign_bytes("gv-bench", a, i // naccounts, fee, [msg], "")
-        msgs.append(msg)
-        d = hashlib.sha256(sb).digest()
-        for j in range(k):
-            kidx.append(base + j)
-            digs.append(d)
-    L = len(kidx)
-    priv_arr = np.frombuffer(b"".join(privs), np.uint8).reshape(-1, 32).copy()
-    pub_arr = np.zeros((len(privs), 33), np.uint8)          # unused by gvw_sign's signing
-    kid = np.array(kidx, np.uint32)
-    dig = np.frombuffer(b"".join(digs), np.uint8).reshape(L, 32).copy()
-    o_pub = np.zeros((L, 33), np.uint8)
-    o_sig = np.zeros((L, 64), np.uint8)
-    o_dig = np.zeros((L, 32), np.uint8)
-    exp = np.zeros(L, np.uint8)
-    wl.gvw_sign(L, 0xC4, len(privs), priv_arr.ctypes.data, pub_arr.ctypes.data, kid.ctypes.data, dig.ctypes.data,
-                0.0, o_pub.ctypes.data, o_sig.ctypes.data, o_dig.ctypes.data, exp.ctypes.data, threads)
-    txs, pos = [], 0
-    for i in range(ntx):
-        k, nsub, base, mk, addr = accts[i % naccounts]
-        sigs = [o_sig[pos + j].tobytes() for j in range(k)]
-        pos += k
-        bits = [j < k for j in range(nsub)]
-        txs.append(T.flat_tx([msgs[i]], fee, "", [addr], [(mk, T.multisignature(bits, sigs))]))
+    nsub = sum(shapes[a % 3][1] for a in range(n_accounts))
+    priv = np.zeros((nsub, 32), np.uint8)
+    pub = np.zeros((nsub, 33), np.uint8)
+    wl.gvw_keys(nsub, 0xC4, priv.ctypes.data, pub.ctypes.data, threads)
+    sink = hashlib.sha256(b"gv-c4-sink").digest()[:20]
+    fee = T.Fee([(0, "stake")], 1000000)
+    sb_parts, head_parts, kk, kidx, tx_len, accts = [], [], [], np.zeros(n_accounts * 8, np.uint32), [], []
+    base = 0
+    for a in range(n_accounts):
+        k, n = shapes[a % 3]
+        mk = T.amino_multisig(k, [T.amino_secp(pub[base + j].tobytes()) for j in range(n)])
+        addr = hashlib.sha256(mk).digest()[:20]              # multisig Address(): SHA256(amino)[:20]
+        msgs = [T.MsgSend(addr, sink, [(1, "foocoin")])]
+        sb = T.std_sign_bytes(chain, a, 0, fee, msgs, "")
+        assert sb.endswith(b'"sequence":"0"}')
+        sb_parts.append(sb[:-3])
+        full = T.std_tx(msgs, fee, "", [(mk, T.multisignature([j < k for j in range(n)], [b"\0" * 64] * k))])
+        head_parts.append(full[:-66 * k])
+        tx_len.append(len(full))
+        kk.append(k)
+        kidx[a * 8:a * 8 + k] = np.arange(base, base + k, dtype=np.uint32)
+        accts.append((addr, a))
+        base += n
+
+    def pack(parts):
+        lens = np.array([len(x) for x in parts], np.uint32)
+        offs = np.zeros(len(parts), np.uint64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        return np.frombuffer(b"".join(parts), np.uint8).copy(), offs, lens
+
+    sbb, sbo, sbl = pack(sb_parts)
+    hb, ho, hl = pack(head_parts)
+    kk = np.array(kk, np.uint8)
+    ntx = n_accounts * txs_per_account
+    lens = np.tile(np.array(tx_len, np.uint64), txs_per_account)
+    offs = np.zeros(ntx, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    blob = np.zeros(int(offs[-1] + lens[-1]), np.uint8)
+    wl.gvw_c4_txs.argtypes = [ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t] + [ctypes.c_void_p] * 11 + [ctypes.c_int]
+    wl.gvw_c4_txs(ntx, n_accounts, nsub, priv.ctypes.data, sbb.ctypes.data, sbo.ctypes.data, sbl.ctypes.data,
+                  hb.ctypes.data, ho.ctypes.data, hl.ctypes.data, kk.ctypes.data, kidx.ctypes.data,
+                  offs.ctypes.data, blob.ctypes.data, threads)
+    leaves = int(kk.astype(np.int64).sum()) * txs_per_account
+    return blob, offs, lens, accts, leaves
+
+
+def c4_multisig(ver, wl, block: int = 10000, threads: int = 16, n_accounts: int = 30000, txs_per_account: int = 89):
+    """BASELINE.json configs[3] on one GPU: 8.01M multisig leaves (2.67M txs)
+    replayed in blocks of `block` txs through DeliverBlock (PreVerifyTxs: every
+    secp256k1 leaf of the block in one GPU batch with predicted sequences; then
+    the DeliverTx ante loop).  Every tx must pass (all signatures valid by
+    construction).  The 8-GPU config shards blocks across nodes' GPUs; on one
+    GPU this is the per-GPU share of the same replay."""
+    import gvhost
+    t = time.perf_counter()
+    blob, offs, lens, accts, leaves = c4_workload(wl, n_accounts, txs_per_account, threads)
+    t_gen = time.perf_counter() - t
     app = gvhost.HostApp(ver, chain_id="gv-bench", height=1)
-    for a, acct in enumerate(accts):
-        app.set_account(acct[4], a, 0)
-    ok = 0
-    t_pre = 0.0
+    app.set_threads(threads)
+    for addr, num in accts:
+        app.set_account(addr, num, 0)
+    ntx = len(offs)
+    # warm-up on a copy of the first block's accounts (separate app: state untouched)
+    wapp = gvhost.HostApp(ver, chain_id="gv-bench", height=1)
+    for addr, num in accts[:block]:
+        wapp.set_account(addr, num, 0)
+    wapp.deliver_block_blob(blob, offs[:block], lens[:block])
+    wapp.close()
+    bad = 0
     t = time.perf_counter()
     for b0 in range(0, ntx, block):
-        blk = txs[b0:b0 + block]
-        tp = time.perf_counter()
-        app.preverify(blk)
-        t_pre += time.perf_counter() - tp
-        for tx in blk:
-            rc_a, r = app.ante(tx)
-            ok += rc_a == 0 and r["code"] == 0
+        rc, codes = app.deliver_block_blob(blob, offs[b0:b0 + block], lens[b0:b0 + block])
+        assert rc == 0
+        bad += int(np.count_nonzero(codes))
     el = time.perf_counter() - t
+    st = app.stats()
     app.close()
-    return {"txs": ntx, "leaves": L, "block_txs": block, "accepted": ok,
-            "leaves_per_s": round(L / el, 1), "txs_per_s": round(ntx / el, 1),
-            "preverify_ms_per_block": round(t_pre * 1e3 / ((ntx + block - 1) // block), 2),
-            "note": "2-of-3 / 3-of-5 / 4-of-7 threshold accounts, all k bits set; host mirror path with host buffers"}
+    return {"txs": ntx, "leaves": leaves, "block_txs": block, "blocks": (ntx + block - 1) // block,
+            "rejected": bad, "mismatches": bad, "leaves_per_s": round(leaves / el, 1), "txs_per_s": round(ntx / el, 1),
+            "seconds": round(el, 3), "preverify_s": round(st["preverify_ns"] / 1e9, 3),
+            "gpu_s": round(st["gpu_ns"] / 1e9, 3), "ante_loop_s": round(st["deliver_loop_ns"] / 1e9, 3),
+            "gpu_calls": st["gpu_calls"], "gpu_leaves": st["gpu_leaves"], "memo_hits": st["memo_hits"],
+            "workload_gen_s": round(t_gen, 1), "host_threads": threads,
+            "note": "2-of-3 / 3-of-5 / 4-of-7 threshold accounts (30k), first k bits set, every tx valid by "
+                    "construction; amino StdTx bytes through the host mirror, host buffers"}

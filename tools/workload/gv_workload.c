@@ -331,3 +331,119 @@ int gvw_sign_digest(const uint8_t priv32[32], const uint8_t dig32[32], uint8_t s
   BN_free(d); BN_free(n); BN_free(half); BN_free(s2); EC_KEY_free(key);
   return rc;
 }
+
+/* ----------------------------------------------------------- C4 blocks */
+/* C4 workload: ntx k-of-n multisig MsgSend txs as amino
+ * StdTx bytes.  Tx t belongs to account a = t % nacct with sequence
+ * t / nacct.  Per account the caller gives the constant pieces:
+ *   sb_pre  StdSignBytes up to the sequence value ('..."sequence":"'),
+ *   head    the tx bytes up to its first multisignature entry (StdTx prefix,
+ *           msg, fee, StdSignature header, multisig pubkey, bit array),
+ *   k, kidx[a*8 + j]  the keys (indices into priv32) of the k set bits.
+ * This signs SHA256(sb_pre || seq || '"}') with each of the k keys and writes
+ * head || k x (0x12 0x40 r || s) at out + off[t].
+ * Signing speed: 8M OpenSSL ECDSA_do_sign calls take minutes, so each key
+ * signs with ONE nonce k (R = k*G and k^-1 precomputed per key): every
+ * signature is still a distinct valid low-S (r, s) over a distinct digest,
+ * s = k^-1 (e + r d) mod n; verification work does not depend on the nonce.
+ * (Nonce reuse would leak the key -- irrelevant for synthetic keys.) */
+typedef struct { size_t lo, hi; const uint8_t* priv; uint8_t *r, *kinv, *rd; } c4key;
+static void* c4_key_worker(void* arg) {
+  c4key* j = (c4key*)arg;
+  EC_GROUP* grp = EC_GROUP_new_by_curve_name(NID_secp256k1);
+  BN_CTX* ctx = BN_CTX_new();
+  EC_GROUP_precompute_mult(grp, ctx);
+  BIGNUM *n = NULL, *k = BN_new(), *d = BN_new(), *r = BN_new(), *t = BN_new(), *x = BN_new();
+  BN_hex2bn(&n, N_HEX);
+  EC_POINT* R = EC_POINT_new(grp);
+  for (size_t i = j->lo; i < j->hi; ++i) {
+    uint8_t m[40], h[32];
+    memcpy(m, j->priv + 32 * i, 32); memcpy(m + 32, "c4-nonce", 8);
+    SHA256(m, sizeof m, h);
+    BN_bin2bn(h, 32, k); BN_mod(k, k, n, ctx); if (BN_is_zero(k)) BN_one(k);
+    EC_POINT_mul(grp, R, k, NULL, NULL, ctx);
+    EC_POINT_get_affine_coordinates(grp, R, x, NULL, ctx);
+    BN_nnmod(r, x, n, ctx);
+    BN_bin2bn(j->priv + 32 * i, 32, d);
+    BN_mod_mul(t, r, d, n, ctx);
+    BN_bn2binpad(r, j->r + 32 * i, 32);
+    BN_bn2binpad(t, j->rd + 32 * i, 32);
+    BN_mod_inverse(t, k, n, ctx);
+    BN_bn2binpad(t, j->kinv + 32 * i, 32);
+  }
+  EC_POINT_free(R); BN_free(n); BN_free(k); BN_free(d); BN_free(r); BN_free(t); BN_free(x);
+  BN_CTX_free(ctx); EC_GROUP_free(grp);
+  return NULL;
+}
+
+typedef struct {
+  size_t lo, hi, nacct;
+  const uint8_t *r, *kinv, *rd;
+  const uint8_t* sbb; const uint64_t* sbo; const uint32_t* sbl;
+  const uint8_t* hb; const uint64_t* ho; const uint32_t* hl;
+  const uint8_t* k; const uint32_t* kidx;
+  const uint64_t* off; uint8_t* out;
+} c4job;
+
+static void* c4_worker(void* arg) {
+  c4job* j = (c4job*)arg;
+  BN_CTX* ctx = BN_CTX_new();
+  BIGNUM *n = NULL, *half = BN_new(), *e = BN_new(), *a = BN_new(), *ki = BN_new(), *s = BN_new();
+  BN_hex2bn(&n, N_HEX); BN_rshift1(half, n);
+  char seq[32];
+  for (size_t t = j->lo; t < j->hi; ++t) {
+    size_t ac = t % j->nacct;
+    int ns = snprintf(seq, sizeof seq, "%llu\"}", (unsigned long long)(t / j->nacct));
+    SHA256_CTX c; uint8_t dig[32];
+    SHA256_Init(&c); SHA256_Update(&c, j->sbb + j->sbo[ac], j->sbl[ac]); SHA256_Update(&c, seq, (size_t)ns);
+    SHA256_Final(dig, &c);
+    uint8_t* o = j->out + j->off[t];
+    memcpy(o, j->hb + j->ho[ac], j->hl[ac]);
+    o += j->hl[ac];
+    BN_bin2bn(dig, 32, e);                         /* hashToInt: 32-byte digest, no truncation */
+    for (int q = 0; q < j->k[ac]; ++q) {
+      const size_t key = j->kidx[ac * 8 + q];
+      BN_bin2bn(j->rd + 32 * key, 32, a);
+      BN_mod_add(a, a, e, n, ctx);                 /* e + r d */
+      BN_bin2bn(j->kinv + 32 * key, 32, ki);
+      BN_mod_mul(s, ki, a, n, ctx);                /* k^-1 (e + r d) */
+      if (BN_cmp(s, half) > 0) BN_sub(s, n, s);    /* low-S (tendermint Sign) */
+      o[0] = 0x12; o[1] = 0x40;
+      memcpy(o + 2, j->r + 32 * key, 32);
+      BN_bn2binpad(s, o + 34, 32);
+      o += 66;
+    }
+  }
+  BN_free(n); BN_free(half); BN_free(e); BN_free(a); BN_free(ki); BN_free(s); BN_CTX_free(ctx);
+  return NULL;
+}
+
+int gvw_c4_txs(size_t ntx, size_t nacct, size_t nkeys, const uint8_t* priv32,
+               const uint8_t* sb_blob, const uint64_t* sb_off, const uint32_t* sb_len,
+               const uint8_t* head_blob, const uint64_t* head_off, const uint32_t* head_len,
+               const uint8_t* k, const uint32_t* kidx, const uint64_t* tx_off, uint8_t* out, int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  uint8_t* r = malloc(32 * nkeys);
+  uint8_t* kinv = malloc(32 * nkeys);
+  uint8_t* rd = malloc(32 * nkeys);
+  if (!r || !kinv || !rd) { free(r); free(kinv); free(rd); return -1; }
+  pthread_t th[256];
+  c4key ks[256];
+  for (int t = 0; t < threads; ++t) {
+    c4key kk = {nkeys * t / threads, nkeys * (t + 1) / threads, priv32, r, kinv, rd};
+    ks[t] = kk;
+    pthread_create(&th[t], NULL, c4_key_worker, &ks[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  c4job js[256];
+  for (int t = 0; t < threads; ++t) {
+    c4job jj = {ntx * t / threads, ntx * (t + 1) / threads, nacct, r, kinv, rd, sb_blob, sb_off, sb_len,
+                head_blob, head_off, head_len, k, kidx, tx_off, out};
+    js[t] = jj;
+    pthread_create(&th[t], NULL, c4_worker, &js[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  free(r); free(kinv); free(rd);
+  return 0;
+}
