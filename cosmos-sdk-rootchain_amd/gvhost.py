@@ -71,6 +71,7 @@ def lib():
         L.gvh_bech32_address.restype = sz
         cpp = ctypes.POINTER(ctypes.c_char_p)
         L.gvh_deliver_block.argtypes = [vp, sz, cpp, ctypes.POINTER(sz), ctypes.POINTER(Result)]
+        L.gvh_deliver_block_codes.argtypes = [vp, sz, cpp, ctypes.POINTER(sz), ctypes.POINTER(ctypes.c_uint32)]
         L.gvh_deliver_gentxs.argtypes = [vp, sz, cpp, ctypes.POINTER(sz), ctypes.POINTER(Result), ctypes.POINTER(sz)]
         L.gvh_checktx.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(Result)]
         L.gvh_set_window.argtypes = [vp, sz, ctypes.c_int64]
@@ -178,25 +179,23 @@ class HostApp:
         """Same, returning only (rc, numpy array of codes) -- cheap for large blocks."""
         import numpy as np
         arr, lens = _arrays(txs)
-        res = (Result * max(1, len(txs)))()
-        rc = self._L.gvh_deliver_block(self._app, len(txs), arr, lens, res)
-        codes = np.frombuffer(res, dtype=np.dtype([("code", "<u4"), ("rest", "V%d" % (ctypes.sizeof(Result) - 4))]),
-                              count=len(txs))["code"].copy()
-        return rc, codes
+        codes = np.zeros(max(1, len(txs)), np.uint32)
+        rc = self._L.gvh_deliver_block_codes(self._app, len(txs), arr, lens,
+                                             codes.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+        return rc, codes[:len(txs)]
 
     def deliver_block_blob(self, blob, offs, lens):
         """A block held in one contiguous buffer (numpy u8 blob, u64 offsets, u64
         lengths): no per-tx Python objects.  Returns (rc, codes u32 array)."""
         import numpy as np
         n = len(offs)
-        ptrs = (np.uint64(blob.ctypes.data) + offs.astype(np.uint64)).astype(np.uint64)
+        ptrs = np.uint64(blob.ctypes.data) + offs.astype(np.uint64)
         lens = np.ascontiguousarray(lens, dtype=np.uint64)
-        res = (Result * max(1, n))()
-        rc = self._L.gvh_deliver_block(self._app, n, ptrs.ctypes.data_as(ctypes.POINTER(ctypes.c_char_p)),
-                                       lens.ctypes.data_as(ctypes.POINTER(ctypes.c_size_t)), res)
-        codes = np.frombuffer(res, dtype=np.dtype([("code", "<u4"), ("rest", "V%d" % (ctypes.sizeof(Result) - 4))]),
-                              count=n)["code"].copy()
-        return rc, codes
+        codes = np.zeros(max(1, n), np.uint32)
+        rc = self._L.gvh_deliver_block_codes(self._app, n, ptrs.ctypes.data_as(ctypes.POINTER(ctypes.c_char_p)),
+                                             lens.ctypes.data_as(ctypes.POINTER(ctypes.c_size_t)),
+                                             codes.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+        return rc, codes[:n]
 
     def deliver_gentxs(self, txs):
         arr, lens = _arrays(txs)

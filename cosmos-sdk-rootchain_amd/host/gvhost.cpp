@@ -24,6 +24,7 @@
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <random>
@@ -38,6 +39,11 @@ namespace {
 using Bytes = std::vector<uint8_t>;
 using Addr = std::array<uint8_t, 20>;
 using H32 = std::array<uint8_t, 32>;
+
+struct Span {
+  const uint8_t* p = nullptr;
+  size_t n = 0;
+};
 
 // ------------------------------------------------------------------ errors
 // sdkerrors codes (types/errors/errors.go)
@@ -101,6 +107,7 @@ H32 sha256(const uint8_t* p, size_t n) {
 }
 
 // ------------------------------------------------------------------ bech32
+std::string bech32(const std::string& hrp, const uint8_t* data, size_t n);
 uint32_t bech32_polymod(const std::vector<uint8_t>& v) {
   static const uint32_t G[5] = {0x3b6a57b2, 0x26508e6d, 0x1ea119fa, 0x3d4233dd, 0x2a1462b3};
   uint32_t chk = 1;
@@ -111,6 +118,73 @@ uint32_t bech32_polymod(const std::vector<uint8_t>& v) {
       if ((b >> i) & 1) chk ^= G[i];
   }
   return chk;
+}
+// bech32 of data appended to o (stack buffers, table-driven checksum).
+struct Bech32Gen {
+  uint32_t t[32];
+  Bech32Gen() {
+    static const uint32_t G[5] = {0x3b6a57b2, 0x26508e6d, 0x1ea119fa, 0x3d4233dd, 0x2a1462b3};
+    for (int b = 0; b < 32; ++b) {
+      t[b] = 0;
+      for (int k = 0; k < 5; ++k)
+        if ((b >> k) & 1) t[b] ^= G[k];
+    }
+  }
+};
+const Bech32Gen kBech32Gen;
+void bech32_encode_append(std::string& o, const char* hrp, const uint8_t* data, size_t n) {
+  static const char* CS = "qpzry9x8gf2tvdw0s3jn54khce6mua7l";
+  const size_t hl = strlen(hrp);
+  uint8_t v[2 * 16 + 1 + 420 + 6];
+  size_t nv = 0;
+  for (size_t i = 0; i < hl; ++i) v[nv++] = (uint8_t)hrp[i] >> 5;
+  v[nv++] = 0;
+  for (size_t i = 0; i < hl; ++i) v[nv++] = (uint8_t)hrp[i] & 31;
+  const size_t d0 = nv;
+  uint32_t acc = 0;
+  int bits = 0;
+  for (size_t i = 0; i < n; ++i) {
+    acc = (acc << 8) | data[i];
+    bits += 8;
+    while (bits >= 5) { bits -= 5; v[nv++] = (acc >> bits) & 31; }
+  }
+  if (bits) v[nv++] = (acc << (5 - bits)) & 31;
+  const size_t d1 = nv;
+  for (int i = 0; i < 6; ++i) v[nv++] = 0;
+  uint32_t chk = 1;
+  for (size_t i = 0; i < nv; ++i) chk = ((chk & 0x1ffffff) << 5) ^ v[i] ^ kBech32Gen.t[chk >> 25];
+  chk ^= 1;
+  o += hrp;
+  o += '1';
+  for (size_t i = d0; i < d1; ++i) o += CS[v[i]];
+  for (int i = 0; i < 6; ++i) o += CS[(chk >> (5 * (5 - i))) & 31];
+}
+// "cosmos" addresses repeat (a signer's every tx, a common recipient): a small
+// per-thread direct-mapped cache of recent 20-byte encodings.
+void bech32_append(std::string& o, const char* hrp, const uint8_t* data, size_t n) {
+  if (n != 20 || n > 256 || strcmp(hrp, "cosmos")) {
+    if (n > 256) o += bech32(hrp, data, n);
+    else bech32_encode_append(o, hrp, data, n);
+    return;
+  }
+  struct Ent {
+    uint8_t key[20];
+    uint8_t len;
+    char s[47];
+  };
+  static thread_local Ent cache[256];
+  uint32_t h;
+  memcpy(&h, data + 16, 4);
+  Ent& e = cache[(h ^ (h >> 8) ^ data[0]) & 255];
+  if (e.len && !memcmp(e.key, data, 20)) { o.append(e.s, e.len); return; }
+  const size_t o0 = o.size();
+  bech32_encode_append(o, hrp, data, n);
+  const size_t len = o.size() - o0;
+  if (len <= sizeof e.s) {
+    memcpy(e.key, data, 20);
+    memcpy(e.s, o.data() + o0, len);
+    e.len = (uint8_t)len;
+  }
 }
 std::string bech32(const std::string& hrp, const uint8_t* data, size_t n) {
   static const char* CS = "qpzry9x8gf2tvdw0s3jn54khce6mua7l";
@@ -137,7 +211,7 @@ std::string bech32(const std::string& hrp, const uint8_t* data, size_t n) {
 }
 // sdk.AccAddress.String(): "" for an empty address (types/address.go:222-234)
 std::string acc_string(const uint8_t* a, size_t n) { return n ? bech32("cosmos", a, n) : std::string(); }
-std::string acc_string(const Bytes& a) { return acc_string(a.data(), a.size()); }
+std::string acc_string(Span a) { return acc_string(a.p, a.n); }
 
 // --------------------------------------------------- Go encoding/json strings
 // json.Marshal(string): escapes '"', '\\', control chars, HTML <>&, U+2028/9;
@@ -193,10 +267,6 @@ std::string go_json_string(const std::string& s) {
 // fields as consecutive entries, unknown fields only after the known ones,
 // registered concrete types behind a 4-byte prefix (optionally preceded by
 // 0x00 + 3 disambiguation bytes).
-struct Span {
-  const uint8_t* p = nullptr;
-  size_t n = 0;
-};
 
 struct Reader {
   const uint8_t* p;
@@ -322,6 +392,11 @@ int interface_type(Span s, Span* body, std::initializer_list<const Disfix*> type
 // (marshalJSON, types/int.go:332-339).  nil (no bytes) prints "0".
 std::string int_text_canonical(Span s) {
   if (s.n == 0) return "0";
+  if (s.n <= 76 && s.p[0] >= '1' && s.p[0] <= '9') {   // plain decimal < 10^76 < 2^255: already canonical
+    bool plain = true;
+    for (size_t i = 1; i < s.n && plain; ++i) plain = s.p[i] >= '0' && s.p[i] <= '9';
+    if (plain) return std::string((const char*)s.p, s.n);
+  }
   const uint8_t* p = s.p;
   size_t i = 0, n = s.n;
   bool neg = false;
@@ -396,104 +471,110 @@ std::string int_text_canonical(Span s) {
 // sdk.Coin amino (types/types.pb.go:33-36: Denom field 1, Amount field 2);
 // JSON {"amount":"N","denom":"d"} with denom omitempty.
 void coin_json(std::string& o, Span s) {
-  std::string denom, amount = "0";
-  bool has_denom = false;
+  Span denom;
+  std::string amount = "0";
   static const FSpec spec[] = {{1, 2, false}, {2, 2, false}};
   for_fields(s, spec, [&](uint32_t f, Reader& r) {
     Span b = r.bytes();
-    if (f == 1) { denom.assign((const char*)b.p, b.n); has_denom = b.n > 0; }
+    if (f == 1) denom = b;
     else amount = int_text_canonical(b);
   });
   o += "{\"amount\":\"";
   o += amount;
   o += '"';
-  if (has_denom) { o += ",\"denom\":"; go_json_string(o, denom); }
+  if (denom.n) { o += ",\"denom\":"; go_json_string(o, denom.p, denom.n); }
   o += '}';
 }
-// sdk.Coins (repeated Coin) as JSON: null when absent (amino encodes a nil slice as null)
+// sdk.Coins (repeated Coin) as JSON into o: null when absent (amino encodes a
+// nil slice as null).  Call add() per element, then done().
 struct CoinsJson {
-  std::string s;
+  std::string& o;
   bool any = false;
+  explicit CoinsJson(std::string& out) : o(out) {}
   void add(Span c) {
-    s += any ? "," : "[";
+    o += any ? ',' : '[';
     any = true;
-    coin_json(s, c);
+    coin_json(o, c);
   }
-  std::string done() const { return any ? s + "]" : "null"; }
+  void done() { o += any ? "]" : "null"; }
 };
 
-struct Msg {
-  std::string json;                 // Msg.GetSignBytes(): MustSortJSON(amino JSON)
-  std::vector<Bytes> signers;       // Msg.GetSigners()
-};
+void add_signer(std::vector<Span>& signers, Span a) {   // StdTx.GetSigners(): dedupe, first occurrence
+  for (const Span& s : signers)
+    if (s.n == a.n && !memcmp(s.p, a.p, a.n)) return;
+  signers.push_back(a);
+}
 
 // x/bank MsgSend (types.pb.go:30-34): from field 1, to field 2, amount field 3;
-// GetSignBytes / GetSigners at x/bank/types/msgs.go:43-50.
-Msg decode_msg_send(Span body) {
-  Msg m;
-  Bytes from, to;
-  CoinsJson coins;
+// GetSignBytes (MustSortJSON of the amino JSON) / GetSigners at x/bank/types/msgs.go:43-50.
+// Appends the JSON to o, the signer to signers.
+void decode_msg_send(Span body, std::string& o, std::vector<Span>& signers) {
+  Span from, to;
+  std::string coins;
+  CoinsJson cj(coins);
   static const FSpec spec[] = {{1, 2, false}, {2, 2, false}, {3, 2, true}};
   for_fields(body, spec, [&](uint32_t f, Reader& r) {
     Span b = r.bytes();
-    if (f == 1) from.assign(b.p, b.p + b.n);
-    else if (f == 2) to.assign(b.p, b.p + b.n);
-    else coins.add(b);
+    if (f == 1) from = b;
+    else if (f == 2) to = b;
+    else cj.add(b);
   });
-  std::string& o = m.json;
-  o = "{\"type\":\"cosmos-sdk/MsgSend\",\"value\":{\"amount\":" + coins.done();
-  if (!from.empty()) { o += ",\"from_address\":\"" + acc_string(from) + "\""; }
-  if (!to.empty()) { o += ",\"to_address\":\"" + acc_string(to) + "\""; }
+  cj.done();
+  o += "{\"type\":\"cosmos-sdk/MsgSend\",\"value\":{\"amount\":";
+  o += coins;
+  if (from.n) { o += ",\"from_address\":\""; bech32_append(o, "cosmos", from.p, from.n); o += '"'; }
+  if (to.n) { o += ",\"to_address\":\""; bech32_append(o, "cosmos", to.p, to.n); o += '"'; }
   o += "}}";
-  m.signers.push_back(std::move(from));
-  return m;
+  add_signer(signers, from);
 }
 // x/bank MsgMultiSend: inputs field 1, outputs field 2; Input/Output {address 1, coins 2}
 // (types.pb.go:91-94,144-147); GetSigners = input addresses (msgs.go:86-90).
-Msg decode_msg_multisend(Span body) {
-  Msg m;
+void decode_msg_multisend(Span body, std::string& o, std::vector<Span>& signers) {
   std::string ins, outs;
   bool any_in = false, any_out = false;
   static const FSpec spec[] = {{1, 2, true}, {2, 2, true}};
   for_fields(body, spec, [&](uint32_t f, Reader& r) {
     Span io = r.bytes();
-    Bytes addr;
-    CoinsJson coins;
+    Span addr;
+    std::string coins;
+    CoinsJson cj(coins);
     static const FSpec ispec[] = {{1, 2, false}, {2, 2, true}};
     for_fields(io, ispec, [&](uint32_t g, Reader& r2) {
       Span b = r2.bytes();
-      if (g == 1) addr.assign(b.p, b.p + b.n);
-      else coins.add(b);
+      if (g == 1) addr = b;
+      else cj.add(b);
     });
-    std::string& o = f == 1 ? ins : outs;
+    cj.done();
+    std::string& s = f == 1 ? ins : outs;
     bool& any = f == 1 ? any_in : any_out;
-    o += any ? "," : "[";
+    s += any ? "," : "[";
     any = true;
-    o += "{";
-    if (!addr.empty()) o += "\"address\":\"" + acc_string(addr) + "\",";
-    o += "\"coins\":" + coins.done() + "}";
-    if (f == 1) m.signers.push_back(std::move(addr));
+    s += "{";
+    if (addr.n) { s += "\"address\":\""; bech32_append(s, "cosmos", addr.p, addr.n); s += "\","; }
+    s += "\"coins\":" + coins + "}";
+    if (f == 1) add_signer(signers, addr);
   });
-  m.json = "{\"type\":\"cosmos-sdk/MsgMultiSend\",\"value\":{\"inputs\":" + (any_in ? ins + "]" : std::string("null")) +
-           ",\"outputs\":" + (any_out ? outs + "]" : std::string("null")) + "}}";
-  return m;
+  o += "{\"type\":\"cosmos-sdk/MsgMultiSend\",\"value\":{\"inputs\":";
+  o += any_in ? ins + "]" : std::string("null");
+  o += ",\"outputs\":";
+  o += any_out ? outs + "]" : std::string("null");
+  o += "}}";
 }
 
 // auth.StdTx (x/auth/types/stdtx.go:147-152): Msgs field 1 (interface list),
 // Fee field 2 {Amount 1, Gas 2}, Signatures field 3 {PubKey 1, Signature 2},
-// Memo field 4.  Owns its bytes; spans point into them.
+// Memo field 4.  Spans point into `raw`: the caller's bytes (alive for the
+// call that decoded it) or `own`, a copy kept for the memo table.
 struct Tx {
-  Bytes raw;
-  std::vector<Msg> msgs;
+  Bytes own;
+  Span raw;
   bool nil_msg = false;
-  std::string fee_json;
   uint64_t gas = 0;
-  std::string memo;
   struct Sig {
     Span pub, sig;
   };
   std::vector<Sig> sigs;
-  std::vector<Bytes> signers;       // StdTx.GetSigners(): msg signers, deduplicated in order
+  std::vector<Span> signers;        // StdTx.GetSigners(): msg signers, deduplicated in order
   std::string sb_tail;              // sign bytes after chain_id: ,"fee":..,"memo":..,"msgs":[..],"sequence":"
   Tx() = default;
   Tx(const Tx&) = delete;
@@ -501,27 +582,39 @@ struct Tx {
 };
 
 // DefaultTxDecoder (stdtx.go:321-338): cdc.UnmarshalBinaryBare(txBytes, &StdTx{}).
-std::shared_ptr<Tx> decode_tx(const uint8_t* p, size_t n) {
+// StdSignBytes (stdtx.go:292-312) pieces are built on the way: the StdSignDoc
+// keys are in sorted order and every embedded JSON is canonical, so composing
+// them equals MustSortJSON(amino.MarshalJSON(StdSignDoc{...})).
+std::shared_ptr<Tx> decode_tx(const uint8_t* p, size_t n, bool copy) {
   auto tx = std::make_shared<Tx>();
   if (n == 0) throw AminoErr("tx bytes are empty");
-  tx->raw.assign(p, p + n);
+  if (copy) {
+    tx->own.assign(p, p + n);
+    p = tx->own.data();
+  }
+  tx->raw = Span{p, n};
   if (n < 4 || memcmp(p, kStdTx.p, 4))
     throw AminoErr("UnmarshalBinaryBare expected to read prefix bytes (since it is registered concrete)");
-  CoinsJson fee;
-  bool has_fee = false;
+  std::string msgs, fee;
+  msgs.reserve(256);
+  CoinsJson fj(fee);
+  bool first_msg = true;
+  Span memo;
   static const FSpec spec[] = {{1, 2, true}, {2, 2, false}, {3, 2, true}, {4, 2, false}};
-  for_fields(Span{tx->raw.data() + 4, n - 4}, spec, [&](uint32_t f, Reader& r) {
+  for_fields(Span{p + 4, n - 4}, spec, [&](uint32_t f, Reader& r) {
     Span b = r.bytes();
     if (f == 1) {
-      if (b.n == 0) { tx->nil_msg = true; tx->msgs.emplace_back(); return; }
+      if (!first_msg) msgs += ',';
+      first_msg = false;
+      if (b.n == 0) { tx->nil_msg = true; return; }
       Span body;
       const int k = interface_type(b, &body, {&kMsgSend, &kMsgMultiSend});
-      tx->msgs.push_back(k == 0 ? decode_msg_send(body) : decode_msg_multisend(body));
+      if (k == 0) decode_msg_send(body, msgs, tx->signers);
+      else decode_msg_multisend(body, msgs, tx->signers);
     } else if (f == 2) {
-      has_fee = true;
       static const FSpec fspec[] = {{1, 2, true}, {2, 0, false}};
       for_fields(b, fspec, [&](uint32_t g, Reader& r2) {
-        if (g == 1) fee.add(r2.bytes());
+        if (g == 1) fj.add(r2.bytes());
         else tx->gas = r2.uvarint();
       });
     } else if (f == 3) {
@@ -533,32 +626,21 @@ std::shared_ptr<Tx> decode_tx(const uint8_t* p, size_t n) {
       });
       tx->sigs.push_back(sg);
     } else {
-      tx->memo.assign((const char*)b.p, b.n);
+      memo = b;
     }
   });
-  (void)has_fee;
+  if (tx->nil_msg) tx->signers.clear();
   // StdFee.Bytes() (stdtx.go:47-58): an empty amount is normalised to [] (not null)
-  tx->fee_json = "{\"amount\":" + (fee.any ? fee.s + "]" : std::string("[]")) + ",\"gas\":\"" +
-                 std::to_string(tx->gas) + "\"}";
-  if (!tx->nil_msg) {
-    for (const Msg& m : tx->msgs)
-      for (const Bytes& a : m.signers) {
-        bool seen = false;
-        for (const Bytes& s : tx->signers) seen = seen || s == a;
-        if (!seen) tx->signers.push_back(a);
-      }
-  }
-  // StdSignBytes (stdtx.go:292-312): the StdSignDoc keys are in sorted order and
-  // every embedded JSON is canonical, so composing the pieces equals
-  // MustSortJSON(amino.MarshalJSON(StdSignDoc{...})).
   std::string& t = tx->sb_tail;
-  t = ",\"fee\":" + tx->fee_json + ",\"memo\":";
-  go_json_string(t, tx->memo);
+  t.reserve(64 + fee.size() + msgs.size() + memo.n);
+  t = ",\"fee\":{\"amount\":";
+  t += fj.any ? fee + "]" : std::string("[]");
+  t += ",\"gas\":\"";
+  t += std::to_string(tx->gas);
+  t += "\"},\"memo\":";
+  go_json_string(t, memo.p, memo.n);
   t += ",\"msgs\":[";
-  for (size_t i = 0; i < tx->msgs.size(); ++i) {
-    if (i) t += ",";
-    t += tx->msgs[i].json;
-  }
+  t += msgs;
   t += "],\"sequence\":\"";
   return tx;
 }
@@ -903,6 +985,68 @@ bool eval(const Node& n, const std::vector<Leaf>& leaves) {
 // ----------------------------------------------------------------- the app
 namespace {
 
+// Persistent worker threads: run(parts, fn) calls fn(0..parts-1), part 0 on
+// the caller (PreVerifyTxs runs several parallel stages per block; spawning
+// threads for each would cost more than the stage).
+class Pool {
+ public:
+  explicit Pool(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this, i] { loop(i + 1); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      quit_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return (int)th_.size() + 1; }
+  void run(int parts, const std::function<void(int)>& fn) {
+    parts = std::max(1, std::min(parts, size()));
+    if (parts == 1) { fn(0); return; }
+    std::lock_guard<std::mutex> one(run_mu_);            // one parallel stage at a time
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      fn_ = &fn;
+      parts_ = parts;
+      pending_ = parts - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0);
+    std::unique_lock<std::mutex> lk(m_);
+    done_cv_.wait(lk, [this] { return pending_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* fn;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+        if (quit_) return;
+        seen = gen_;
+        if (id >= parts_) continue;
+        fn = fn_;
+      }
+      (*fn)(id);
+      std::lock_guard<std::mutex> lk(m_);
+      if (--pending_ == 0) done_cv_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_, run_mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int parts_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool quit_ = false;
+};
+
 // store/types/gas.go basicGasMeter (limit) / infiniteGasMeter
 struct GasMeter {
   bool infinite;
@@ -982,9 +1126,10 @@ struct Account {
   uint64_t number = 0, sequence = 0;
   Bytes pub;                                  // amino (canonical), empty = not set
   std::shared_ptr<const PubInfo> info;        // GetPubKey() of pub (decoded once)
+  uint64_t bump_epoch = 0, bump = 0;          // PreVerifyTxs' sequence prediction (earlier txs this call)
 };
 struct AddrHash {
-  size_t operator()(const Bytes& a) const { return (size_t)fast_hash(a.data(), a.size()); }
+  size_t operator()(const Addr& a) const { return (size_t)fast_hash(a.data(), a.size()); }
 };
 
 // One signer's prepared verification: the sign bytes were built for
@@ -1022,13 +1167,13 @@ class MemoTable {
       auto it = m->find(h);
       if (it != m->end())
         for (auto e = it->second.rbegin(); e != it->second.rend(); ++e)     // newest first
-          if ((*e)->tx->raw.size() == n && !memcmp((*e)->tx->raw.data(), p, n)) return *e;
+          if ((*e)->tx->raw.n == n && !memcmp((*e)->tx->raw.p, p, n)) return *e;
     }
     return nullptr;
   }
   void put(std::shared_ptr<Memo> m) {
     if (!m->tx) return;
-    const uint64_t h = fast_hash(m->tx->raw.data(), m->tx->raw.size());
+    const uint64_t h = fast_hash(m->tx->raw.p, m->tx->raw.n);
     std::lock_guard<std::mutex> g(mu_);
     if (count_ >= limit_) {
       old_.swap(cur_);
@@ -1037,7 +1182,7 @@ class MemoTable {
     }
     auto& v = cur_[h];
     for (auto& e : v)
-      if (e->tx->raw == m->tx->raw) { e = std::move(m); return; }
+      if (e->tx->raw.n == m->tx->raw.n && !memcmp(e->tx->raw.p, m->tx->raw.p, m->tx->raw.n)) { e = std::move(m); return; }
     v.push_back(std::move(m));
     ++count_;
   }
@@ -1081,7 +1226,7 @@ struct gvh_app {
   int64_t height = 1;
   bool recheck = false;
   uint64_t gas_limit = 0;
-  std::unordered_map<Bytes, Account, AddrHash> accounts;
+  std::unordered_map<Addr, Account, AddrHash> accounts;   // AccountKeeper (20-byte addresses)
   std::mutex mu;                               // accounts + context
   VerdictCache cache{size_t(1) << 20};
   MemoTable memo;
@@ -1089,11 +1234,53 @@ struct gvh_app {
   Window window;
   std::mutex gpu_mu;                           // one GPU batch at a time per app
   int threads = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+  std::unique_ptr<Pool> pool{new Pool(threads - 1)};
+  std::mutex pool_mu;                          // guards replacing the pool (gvh_set_threads)
+  uint64_t bump_epoch = 0;
   std::atomic<uint64_t> st_gpu_calls{0}, st_gpu_leaves{0}, st_hits{0}, st_misses{0}, st_memo{0}, st_windows{0},
       st_window_txs{0}, st_pre_ns{0}, st_gpu_ns{0}, st_loop_ns{0};
 };
 
 namespace {
+
+// Run fn(i) for i in [0, n) on the app's pool (dynamic chunks).  Nested calls
+// (from inside a pool task) run inline.
+thread_local bool t_in_pool = false;
+template <class F>
+void parallel_for(gvh_app* app, size_t n, F fn) {
+  const size_t chunk = 16;
+  if (app->threads <= 1 || n <= chunk || t_in_pool) {
+    for (size_t i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::function<void(int)> work = [&](int) {
+    const bool was = t_in_pool;
+    t_in_pool = true;
+    for (size_t lo; (lo = next.fetch_add(chunk)) < n;)
+      for (size_t i = lo; i < std::min(n, lo + chunk); ++i) fn(i);
+    t_in_pool = was;
+  };
+  std::lock_guard<std::mutex> g(app->pool_mu);
+  app->pool->run((int)std::min<size_t>(app->threads, (n + chunk - 1) / chunk), work);
+}
+// Run fn(part) for part in [0, parts) on the pool (static partition).
+template <class F>
+void parallel_parts(gvh_app* app, int parts, F fn) {
+  if (parts <= 1 || t_in_pool) {
+    for (int p = 0; p < parts; ++p) fn(p);
+    return;
+  }
+  std::atomic<int> next{0};
+  std::function<void(int)> work = [&](int) {
+    const bool was = t_in_pool;
+    t_in_pool = true;
+    for (int p; (p = next.fetch_add(1)) < parts;) fn(p);
+    t_in_pool = was;
+  };
+  std::lock_guard<std::mutex> g(app->pool_mu);
+  app->pool->run(std::min(parts, app->threads), work);
+}
 
 // DefaultSigVerificationGasConsumer (sigverify.go:299-322) incl. the multisig
 // recursion (ConsumeMultisignatureVerificationGas :325-338, whose nested errors
@@ -1145,6 +1332,14 @@ void copy_result(gvh_result* out, const SdkError* e, uint64_t gas, uint32_t gpu_
   out->gpu_leaves = gpu_leaves;
   out->cache_hits = hits;
   out->gas_wanted = wanted;
+}
+
+Account* find_account(gvh_app* app, Span a) {
+  if (a.n != 20) return nullptr;                    // accounts have 20-byte addresses
+  Addr k;
+  memcpy(k.data(), a.p, 20);
+  auto it = app->accounts.find(k);
+  return it == app->accounts.end() ? nullptr : &it->second;
 }
 
 std::shared_ptr<const PubInfo> account_info(gvh_app* app, Account& acc) {
@@ -1212,11 +1407,21 @@ void make_plan(SignerPlan& p, gvh_app* app, const Tx& tx, size_t signer, std::sh
 // Resolve leaves: cache first, the secp256k1 misses in ONE GPU batch.
 int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint32_t* hits) {
   std::vector<Leaf*> miss;
-  for (Leaf* L : leaves) {
-    if (L->verdict >= 0) { if (hits) ++*hits; continue; }   // ed25519 leaves were decided in make_plan
-    const int v = app->cache.get(L->key);
-    if (v >= 0) { L->verdict = v; if (hits) ++*hits; }
-    else miss.push_back(L);
+  if (leaves.size() >= 4096) {                        // big batches: lookups on the pool
+    parallel_for(app, leaves.size(), [&](size_t i) {
+      Leaf* L = leaves[i];
+      if (L->verdict < 0) L->verdict = app->cache.get(L->key);
+    });
+    for (Leaf* L : leaves)
+      if (L->verdict < 0) miss.push_back(L);
+    if (hits) *hits += (uint32_t)(leaves.size() - miss.size());
+  } else {
+    for (Leaf* L : leaves) {
+      if (L->verdict >= 0) { if (hits) ++*hits; continue; }   // ed25519 leaves were decided in make_plan
+      const int v = app->cache.get(L->key);
+      if (v >= 0) { L->verdict = v; if (hits) ++*hits; }
+      else miss.push_back(L);
+    }
   }
   app->st_hits += leaves.size() - miss.size();
   app->st_misses += miss.size();
@@ -1224,43 +1429,23 @@ int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint
   if (!app->gpu) return GVH_ENOVERIFIER;
   const size_t m = miss.size();
   std::vector<uint8_t> pub(m * 33), sig(m * 64), dig(m * 32), ok(m);
-  for (size_t k = 0; k < m; ++k) {
+  parallel_for(app, m, [&](size_t k) {
     memcpy(&pub[k * 33], miss[k]->pub.data(), 33);
     memcpy(&sig[k * 64], miss[k]->sig.data(), 64);
     memcpy(&dig[k * 32], miss[k]->dig.data(), 32);
-  }
+  });
   {
     std::lock_guard<std::mutex> g(app->gpu_mu);
     if (gv_verify_digests(app->gpu, m, pub.data(), sig.data(), dig.data(), ok.data()) != GV_OK) return GVH_EDEVICE;
   }
   app->st_gpu_calls += 1;
   app->st_gpu_leaves += m;
-  for (size_t k = 0; k < m; ++k) {
+  parallel_for(app, m, [&](size_t k) {
     miss[k]->verdict = ok[k];
     app->cache.put(miss[k]->key, ok[k] != 0);
-  }
+  });
   if (gpu_leaves) *gpu_leaves += (uint32_t)m;
   return GVH_OK;
-}
-
-// Run fn(i) for i in [0, n) on up to `threads` threads (dynamic chunks).
-template <class F>
-void parallel_for(size_t n, int threads, F fn) {
-  const size_t chunk = 32;
-  if (threads <= 1 || n <= chunk) {
-    for (size_t i = 0; i < n; ++i) fn(i);
-    return;
-  }
-  std::atomic<size_t> next{0};
-  auto work = [&]() {
-    for (size_t lo; (lo = next.fetch_add(chunk)) < n;)
-      for (size_t i = lo; i < std::min(n, lo + chunk); ++i) fn(i);
-  };
-  const int nt = (int)std::min<size_t>(threads, (n + chunk - 1) / chunk);
-  std::vector<std::thread> th;
-  for (int t = 1; t < nt; ++t) th.emplace_back(work);
-  work();
-  for (auto& t : th) t.join();
 }
 
 // The ante chain on one decoded tx (app->mu held by the caller).  memo: the
@@ -1304,10 +1489,7 @@ int run_ante(gvh_app* app, const Tx& tx, Memo* memo, bool simulate, gvh_result* 
     // signer accounts, looked up once
     std::vector<Account*> accs(signers.size(), nullptr);
     auto acc_of = [&](size_t i) -> Account* {
-      if (!accs[i]) {
-        auto it = app->accounts.find(signers[i]);
-        if (it != app->accounts.end()) accs[i] = &it->second;
-      }
+      if (!accs[i]) accs[i] = find_account(app, signers[i]);
       return accs[i];
     };
     static const std::shared_ptr<const PubInfo> kSim = [] {
@@ -1326,7 +1508,7 @@ int run_ante(gvh_app* app, const Tx& tx, Memo* memo, bool simulate, gvh_result* 
       if (i >= signers.size()) throw Panic("runtime error: index out of range");
       if (!simulate) {
         if (pk->pk.kind == PubKey::Nil) throw Panic("runtime error: invalid memory address or nil pointer dereference");
-        if (!(signers[i].size() == 20 && !memcmp(pk->addr.data(), signers[i].data(), 20)))
+        if (!(signers[i].n == 20 && !memcmp(pk->addr.data(), signers[i].p, 20)))
           return fail(wrap(kErrInvalidPubKey, "pubKey does not match signer address " + acc_string(signers[i]) +
                                                   " with signer index: " + std::to_string(i)));
       }
@@ -1467,7 +1649,7 @@ int ante_bytes(gvh_app* app, const uint8_t* p, size_t n, bool simulate, gvh_resu
   if (m) return ante_memo(app, m.get(), simulate, out);
   std::shared_ptr<const Tx> tx;
   try {
-    tx = decode_tx(p, n);
+    tx = decode_tx(p, n, false);
   } catch (const AminoErr& e) {
     SdkError err = wrap(kErrTxDecode, e.what());
     copy_result(out, &err, 0, 0, 0, 0);
@@ -1491,14 +1673,14 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
   // (1) parallel: decode (sharing an earlier decode of the same bytes) and
   // GetPubKeys' tx-supplied keys with their address checks
   std::vector<std::shared_ptr<Memo>> memos(ntx);
-  parallel_for(ntx, app->threads, [&](size_t t) {
+  parallel_for(app, ntx, [&](size_t t) {
     // a fresh Memo every time (an earlier one may be in use by an ante run)
     auto m = std::make_shared<Memo>();
     auto old = keep ? app->memo.find(txs[t], lens[t]) : nullptr;
     if (old) m->tx = old->tx;
     else {
       try {
-        m->tx = decode_tx(txs[t], lens[t]);
+        m->tx = decode_tx(txs[t], lens[t], keep);
       } catch (const AminoErr& e) {
         m->decode_err = e.what();
       }
@@ -1530,36 +1712,54 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
   std::vector<Job> jobs;
   std::string chain_json;
   {
+    // sequence prediction = a per-signer prefix count in block order; signers
+    // are hash-partitioned over the pool, each part scanning the block in
+    // order for its own signers (every account is touched by one part only)
     std::lock_guard<std::mutex> lk(app->mu);
     chain_json = app->chain_json;
-    std::unordered_map<Bytes, uint64_t, AddrHash> bump;
-    bump.reserve(ntx * 2);
-    jobs.reserve(ntx);
-    for (size_t t = 0; t < ntx; ++t) {
-      Memo& m = *memos[t];
-      if (!m.tx || m.tx->nil_msg || m.pk_panic >= 0) continue;
-      const Tx& tx = *m.tx;
-      for (size_t i = 0; i < tx.sigs.size() && i < tx.signers.size(); ++i) {
-        auto it = app->accounts.find(tx.signers[i]);
-        if (it == app->accounts.end()) continue;
-        Account& acc = it->second;
-        std::shared_ptr<const PubInfo> pub;
-        try {
-          pub = account_info(app, acc);
-        } catch (const Panic&) {
-          continue;
+    const uint64_t epoch = ++app->bump_epoch;
+    const int parts = ntx >= 2048 ? std::max(1, app->threads) : 1;
+    std::vector<std::vector<Job>> pj(parts);
+    auto part_of = [&](Span a) { return a.n == 20 ? (int)((a.p[0] ^ a.p[7] ^ a.p[19]) % (unsigned)parts) : 0; };
+    parallel_parts(app, parts, [&](int part) {
+      std::vector<Job>& out = pj[part];
+      out.reserve(ntx / parts + 16);
+      for (size_t t = 0; t < ntx; ++t) {
+        Memo& m = *memos[t];
+        if (!m.tx || m.tx->nil_msg || m.pk_panic >= 0) continue;
+        const Tx& tx = *m.tx;
+        for (size_t i = 0; i < tx.sigs.size() && i < tx.signers.size(); ++i) {
+          if (part_of(tx.signers[i]) != part) continue;
+          Account* acc = find_account(app, tx.signers[i]);
+          if (!acc) continue;
+          std::shared_ptr<const PubInfo> pub;
+          try {
+            pub = account_info(app, *acc);
+          } catch (const Panic&) {
+            continue;
+          }
+          if (!pub) pub = m.tx_pk[i];          // SetPubKey will store the tx-supplied key
+          if (!pub) continue;
+          if (acc->bump_epoch != epoch) { acc->bump_epoch = epoch; acc->bump = 0; }
+          out.push_back(Job{t, i, app->height == 0 ? 0 : acc->number, acc->sequence + acc->bump, std::move(pub)});
         }
-        if (!pub) pub = m.tx_pk[i];          // SetPubKey will store the tx-supplied key
-        if (!pub) continue;
-        uint64_t& b = bump[tx.signers[i]];
-        jobs.push_back(Job{t, i, app->height == 0 ? 0 : acc.number, acc.sequence + b, std::move(pub)});
+        for (const Span& a : tx.signers)               // every signer's sequence moves if the tx passes
+          if (part_of(a) == part)
+            if (Account* acc = find_account(app, a)) {
+              if (acc->bump_epoch != epoch) { acc->bump_epoch = epoch; acc->bump = 0; }
+              acc->bump += 1;
+            }
       }
-      for (auto& a : tx.signers) bump[a] += 1;
-    }
+    });
+    size_t tot = 0;
+    for (auto& v : pj) tot += v.size();
+    jobs.reserve(tot);
+    for (auto& v : pj)
+      for (auto& j : v) jobs.push_back(std::move(j));
   }
   lap("jobs");
   // (3) parallel: gas charge, sign bytes, leaves, cache keys
-  parallel_for(jobs.size(), app->threads, [&](size_t k) {
+  parallel_for(app, jobs.size(), [&](size_t k) {
     Job& j = jobs[k];
     Memo& m = *memos[j.t];
     try {
@@ -1619,7 +1819,8 @@ void gvh_set_context(gvh_app* app, const char* chain_id, int64_t height, int rec
 int gvh_set_account(gvh_app* app, const uint8_t addr20[20], uint64_t num, uint64_t seq, const uint8_t* pub,
                     size_t pub_len) {
   if (!app || !addr20) return GVH_EINVAL;
-  Bytes a(addr20, addr20 + 20);
+  Addr a;
+  memcpy(a.data(), addr20, 20);
   Account acc;
   acc.number = num;
   acc.sequence = seq;
@@ -1630,7 +1831,8 @@ int gvh_set_account(gvh_app* app, const uint8_t addr20[20], uint64_t num, uint64
 }
 int gvh_get_account(gvh_app* app, const uint8_t addr20[20], uint64_t* num, uint64_t* seq, uint8_t* pub_out,
                     size_t* pub_len) {
-  Bytes a(addr20, addr20 + 20);
+  Addr a;
+  memcpy(a.data(), addr20, 20);
   std::lock_guard<std::mutex> lk(app->mu);
   auto it = app->accounts.find(a);
   if (it == app->accounts.end()) return 0;
@@ -1651,20 +1853,92 @@ int gvh_preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const siz
   return preverify(app, ntx, txs, lens, n_leaves, nullptr, true);
 }
 
-int gvh_deliver_block(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, gvh_result* out) {
-  if (!app || (ntx && (!txs || !lens || !out))) return GVH_EINVAL;
+}  // extern "C"
+
+namespace {
+
+// The DeliverTx ante loop of a pre-verified block.  out and/or codes receive
+// the results.  A tx's ante chain reads and writes only its signers'
+// accounts (SetPubKey, IncrementSequence); when every tx has at most one
+// signer, txs of different accounts are independent, so the loop runs as
+// per-account chains in parallel (block order kept within each account) --
+// the same results and final state as the serial loop.  Otherwise serial.
+int deliver_memos(gvh_app* app, std::vector<std::shared_ptr<Memo>>& memos, gvh_result* out, uint32_t* codes) {
+  const size_t ntx = memos.size();
+  bool single = true;
+  for (auto& m : memos)
+    if (m->tx && m->tx->signers.size() > 1) { single = false; break; }
+  auto one = [&](size_t t, gvh_result* r) {
+    Memo* m = memos[t].get();
+    if (!m->tx) {
+      SdkError err = wrap(kErrTxDecode, m->decode_err);
+      copy_result(r, &err, 0, 0, 0, 0);
+      return GVH_OK;
+    }
+    return run_ante(app, *m->tx, m, false, r);
+  };
+  std::lock_guard<std::mutex> lk(app->mu);
+  if (!single || ntx < 1024 || app->threads <= 1) {
+    gvh_result tmp;
+    for (size_t t = 0; t < ntx; ++t) {
+      gvh_result* r = out ? &out[t] : &tmp;
+      const int rc = one(t, r);
+      if (rc != GVH_OK) return rc;
+      if (codes) codes[t] = r->code;
+    }
+    return GVH_OK;
+  }
+  const int parts = app->threads;
+  std::vector<std::vector<uint32_t>> idx(parts);
+  for (size_t t = 0; t < ntx; ++t) {
+    const Tx* tx = memos[t]->tx.get();
+    int p = 0;
+    if (tx && !tx->signers.empty() && tx->signers[0].n == 20) {
+      const uint8_t* a = tx->signers[0].p;
+      p = (int)((a[0] ^ a[7] ^ a[19]) % (unsigned)parts);
+    }
+    idx[p].push_back((uint32_t)t);
+  }
+  std::atomic<int> err{GVH_OK};
+  parallel_parts(app, parts, [&](int p) {
+    gvh_result tmp;
+    for (uint32_t t : idx[p]) {
+      if (err.load(std::memory_order_relaxed) != GVH_OK) return;
+      gvh_result* r = out ? &out[t] : &tmp;
+      const int rc = one(t, r);
+      if (rc != GVH_OK) { err = rc; return; }
+      if (codes) codes[t] = r->code;
+    }
+  });
+  return err.load();
+}
+
+int deliver_block(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, gvh_result* out,
+                  uint32_t* codes) {
   std::vector<std::shared_ptr<Memo>> memos;
   const auto t0 = std::chrono::steady_clock::now();
   int rc = preverify(app, ntx, txs, lens, nullptr, &memos, false);
   const auto t1 = std::chrono::steady_clock::now();
   app->st_pre_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
   if (rc != GVH_OK) return rc;
-  for (size_t t = 0; t < ntx; ++t) {                 // the DeliverTx loop, in block order
-    rc = ante_memo(app, memos[t].get(), false, &out[t]);
-    if (rc != GVH_OK) return rc;
-  }
+  rc = deliver_memos(app, memos, out, codes);
   app->st_loop_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
-  return GVH_OK;
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gvh_deliver_block(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, gvh_result* out) {
+  if (!app || (ntx && (!txs || !lens || !out))) return GVH_EINVAL;
+  return deliver_block(app, ntx, txs, lens, out, nullptr);
+}
+
+int gvh_deliver_block_codes(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens,
+                            uint32_t* codes) {
+  if (!app || (ntx && (!txs || !lens || !codes))) return GVH_EINVAL;
+  return deliver_block(app, ntx, txs, lens, nullptr, codes);
 }
 
 int gvh_deliver_gentxs(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, gvh_result* out,
@@ -1772,7 +2046,10 @@ size_t gvh_cache_size(gvh_app* app) { return app->cache.size(); }
 void gvh_set_cache_capacity(gvh_app* app, size_t entries) { app->cache.resize(std::max<size_t>(entries, 512)); }
 
 void gvh_set_threads(gvh_app* app, int threads) {
-  if (app) app->threads = std::max(1, std::min(256, threads));
+  if (!app) return;
+  std::lock_guard<std::mutex> g(app->pool_mu);
+  app->threads = std::max(1, std::min(256, threads));
+  app->pool.reset(new Pool(app->threads - 1));
 }
 
 void gvh_get_stats(gvh_app* app, gvh_stats* o) {
@@ -1808,7 +2085,7 @@ size_t gvh_std_sign_bytes(const char* chain_id, uint64_t accnum, uint64_t seq, c
 size_t gvh_tx_sign_bytes(const uint8_t* tx, size_t tx_len, const char* chain_id, uint64_t accnum, uint64_t seq,
                          uint8_t* out, size_t cap, char* err, size_t err_cap) {
   try {
-    auto t = decode_tx(tx, tx_len);
+    auto t = decode_tx(tx, tx_len, false);
     const std::string s = sign_bytes(*t, go_json_string(chain_id ? chain_id : ""), accnum, seq);
     if (out) memcpy(out, s.data(), std::min(cap, s.size()));
     if (err && err_cap) err[0] = 0;

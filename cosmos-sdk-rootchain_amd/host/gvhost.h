@@ -108,6 +108,9 @@ int gvh_preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const siz
 /* A block: PreVerifyTxs, then the ante chain of every tx in order (the
  * DeliverTx loop); out[i] is tx i's result. */
 int gvh_deliver_block(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, gvh_result* out);
+/* Same, returning only each tx's code (codes[i]; 0 = OK). */
+int gvh_deliver_block_codes(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens,
+                            uint32_t* codes);
 /* genutil.DeliverGenTxs: the block path at height 0 (account number 0,
  * infinite gas); *first_failed = index of the first tx whose result is not OK
  * (the reference panics on it), or ntx if all passed. */

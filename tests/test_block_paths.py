@@ -308,3 +308,46 @@ def test_bounded_verdict_cache(ver):
     st = app.stats()
     assert st["cache_capacity"] == 512 and st["cache_entries"] <= 512
     app.close()
+
+
+def test_parallel_deliver_loop_equals_serial_ante(ver):
+    """A single-signer block large enough for DeliverBlock's per-account
+    parallel ante loop (>= 1024 txs): every result and every final account
+    sequence equal the per-tx serial ante with no pre-verification."""
+    rng = random.Random(5)
+    keys = [SecpKey(b"par-%d" % i) for i in range(40)]
+    addrs = [T.address(k.amino) for k in keys]
+    sink = T.address(SecpKey(b"par-sink").amino)
+    seq = [0] * len(keys)
+    txs = []
+    for t in range(3000):
+        i = rng.randrange(len(keys))
+        msgs = [T.MsgSend(addrs[i], sink, [(1 + t % 5, "p")])]
+        claimed = seq[i] + (2 if rng.random() < 0.03 else 0)          # some wrong sequences
+        sb = T.std_sign_bytes(CHAIN, i, claimed, FEE, msgs, "")
+        sig = keys[i].sign(sb) if rng.random() > 0.03 else keys[(i + 1) % len(keys)].sign(sb)
+        pub = keys[i].amino if rng.random() < 0.5 else b""
+        txs.append(T.std_tx(msgs, FEE, "", [(pub, sig)]))
+        seq[i] += 1                                    # the signer's view (failures shift later txs)
+    def fresh():
+        app = gvhost.HostApp(ver, chain_id=CHAIN, height=4)
+        app.set_threads(8)
+        for i, a in enumerate(addrs):
+            app.set_account(a, i, 0, keys[i].amino if i % 3 == 0 else b"")
+        return app
+    app = fresh()
+    rc, codes = app.deliver_block_codes(txs)
+    assert rc == 0
+    par_state = [app.get_account(a) for a in addrs]
+    app.close()
+    app = fresh()
+    serial = []
+    for tx in txs:
+        rc, r = app.ante(tx)
+        assert rc == 0
+        serial.append(r["code"])
+    ser_state = [app.get_account(a) for a in addrs]
+    app.close()
+    assert list(codes) == serial
+    assert par_state == ser_state
+    assert 0 < serial.count(0) < len(serial)

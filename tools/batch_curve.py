@@ -1,0 +1,50 @@
+"""Device-resident verify time vs batch size for both schedules (the fused
+latency kernel, gv_lat.hip, and the 4-kernel throughput pipeline), to place
+the "lat_max" crossover.  Prints one JSON line.  usage: batch_curve.py [reps]"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "cosmos-sdk-rootchain_amd"))
+import bench  # noqa: E402
+import gpuverify as gvm  # noqa: E402
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    nmax = 262144
+    pub, sig, dig, exp = bench.make_digest_workload(nmax, 0xCC, 4096, 0.0, 16)
+    ver = gvm.Verifier([0])
+    d = [ver.dev_alloc(a.nbytes) for a in (pub, sig, dig)]
+    for p, a in zip(d, (pub, sig, dig)):
+        ver.dev_upload(p, a)
+    bits = ver.dev_alloc(nmax // 8 + 64)
+    out = {}
+    for n in (1024, 4096, 8192, 16384, 32768, 65536, 131072, 262144):
+        row = {}
+        for name, lat in (("latency_kernel", 1 << 30), ("throughput_pipeline", 0)):
+            ver.set_option("lat_max", lat)
+            ver.dev_verify_digests(0, n, d[0], d[1], d[2], bits)
+            ver.dev_sync()
+            t = time.perf_counter()
+            for _ in range(reps):
+                ver.dev_verify_digests(0, n, d[0], d[1], d[2], bits)
+            ver.dev_sync()
+            ms = (time.perf_counter() - t) / reps * 1e3
+            got = np.zeros((n + 63) // 64, np.uint64)
+            ver.dev_download(got, bits)
+            ok = int(np.unpackbits(got.view(np.uint8), bitorder="little")[:n].sum())
+            row[name] = {"ms": round(ms, 4), "verifies_per_s": round(n / ms * 1e3, 1), "accepted": ok}
+        out[str(n)] = row
+        print(n, row, file=sys.stderr, flush=True)
+    ver.set_option("lat_max", 4096)
+    print(json.dumps({"batch_curve_device_resident": out}))
+
+
+if __name__ == "__main__":
+    main()
