@@ -1154,6 +1154,7 @@ struct Memo {
   int pk_panic = -1;                                 // first tx-supplied key that does not decode
   std::string pk_panic_msg;
   std::vector<SignerPlan> plans;
+  std::vector<Account*> sacc;                        // PreVerifyTxs: each signer's account (null: none)
 };
 
 // Memo table (CheckTx window and separate PreVerifyTxs / ante calls): tx
@@ -1259,6 +1260,25 @@ void parallel_for(gvh_app* app, size_t n, F fn) {
     t_in_pool = true;
     for (size_t lo; (lo = next.fetch_add(chunk)) < n;)
       for (size_t i = lo; i < std::min(n, lo + chunk); ++i) fn(i);
+    t_in_pool = was;
+  };
+  std::lock_guard<std::mutex> g(app->pool_mu);
+  app->pool->run((int)std::min<size_t>(app->threads, (n + chunk - 1) / chunk), work);
+}
+// parallel_for with the worker's index w in [0, app->threads) as fn(i, w).
+template <class F>
+void parallel_for_w(gvh_app* app, size_t n, F fn) {
+  const size_t chunk = 16;
+  if (app->threads <= 1 || n <= chunk || t_in_pool) {
+    for (size_t i = 0; i < n; ++i) fn(i, 0);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::function<void(int)> work = [&](int w) {
+    const bool was = t_in_pool;
+    t_in_pool = true;
+    for (size_t lo; (lo = next.fetch_add(chunk)) < n;)
+      for (size_t i = lo; i < std::min(n, lo + chunk); ++i) fn(i, w);
     t_in_pool = was;
   };
   std::lock_guard<std::mutex> g(app->pool_mu);
@@ -1436,7 +1456,11 @@ int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint
   });
   {
     std::lock_guard<std::mutex> g(app->gpu_mu);
+    const auto t0 = std::chrono::steady_clock::now();
     if (gv_verify_digests(app->gpu, m, pub.data(), sig.data(), dig.data(), ok.data()) != GV_OK) return GVH_EDEVICE;
+    if (getenv("GVH_PROFILE"))
+      fprintf(stderr, "gv_verify_digests %zu leaves %.3f ms\n", m,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   }
   app->st_gpu_calls += 1;
   app->st_gpu_leaves += m;
@@ -1486,8 +1510,14 @@ int run_ante(gvh_app* app, const Tx& tx, Memo* memo, bool simulate, gvh_result* 
         if (tx.sigs[i].pub.n) local[i] = app->pubs.get(tx.sigs[i].pub.p, tx.sigs[i].pub.n);
       tx_pk = &local;
     }
-    // signer accounts, looked up once
-    std::vector<Account*> accs(signers.size(), nullptr);
+    // signer accounts, looked up once (PreVerifyTxs' lookups reused: account
+    // entries are never removed, so a found pointer stays valid)
+    Account* accs_small[8] = {};
+    std::vector<Account*> accs_big;
+    if (signers.size() > 8) accs_big.assign(signers.size(), nullptr);
+    Account** accs = signers.size() > 8 ? accs_big.data() : accs_small;
+    if (memo && memo->sacc.size() == signers.size())
+      for (size_t i = 0; i < signers.size(); ++i) accs[i] = memo->sacc[i];
     auto acc_of = [&](size_t i) -> Account* {
       if (!accs[i]) accs[i] = find_account(app, signers[i]);
       return accs[i];
@@ -1557,11 +1587,10 @@ int run_ante(gvh_app* app, const Tx& tx, Memo* memo, bool simulate, gvh_result* 
       if (ns != signers.size())
         return fail(wrap(kErrUnauthorized, "invalid number of signer;  expected: " + std::to_string(signers.size()) +
                                                ", got " + std::to_string(ns)));
-      std::vector<SignerPlan> fresh;
+      std::vector<SignerPlan> fresh;                 // plans rebuilt here (a prediction missed)
       SignerPlan* plans_small[8];
       std::vector<SignerPlan*> plans_big;
       size_t np = 0;
-      fresh.reserve(ns);
       SdkError first_err;
       bool have_err = false;
       for (size_t i = 0; i < ns; ++i) {
@@ -1588,6 +1617,7 @@ int run_ante(gvh_app* app, const Tx& tx, Memo* memo, bool simulate, gvh_result* 
           }
         }
         if (!p) {
+          if (fresh.capacity() == 0) fresh.reserve(ns);   // pointers into it must stay valid
           fresh.emplace_back();
           p = &fresh.back();
           make_plan(*p, app, tx, i, account_info(app, *acc), accnum, acc->sequence, app->chain_json);
@@ -1659,7 +1689,16 @@ int ante_bytes(gvh_app* app, const uint8_t* p, size_t n, bool simulate, gvh_resu
   return run_ante(app, *tx, nullptr, simulate, out);
 }
 
-// PreVerifyTxs.  Returns the memos (one per tx, in order).
+// Drop a block's memos on the pool (freeing ~10 heap objects per tx serially
+// would cost more than building them in parallel).
+void release_memos(gvh_app* app, std::vector<std::shared_ptr<Memo>>& memos) {
+  parallel_for(app, memos.size(), [&](size_t t) { memos[t].reset(); });
+  memos.clear();
+}
+
+// PreVerifyTxs.  Returns the memos (one per tx, in order).  The app lock is
+// held while the block's state is read (decode, sequence prediction, plans)
+// and released for the GPU batch.
 int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, size_t* n_leaves,
               std::vector<std::shared_ptr<Memo>>* memos_out, bool keep) {
   auto T0 = std::chrono::steady_clock::now();
@@ -1670,8 +1709,10 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
     fprintf(stderr, "preverify %s %.3f ms\n", what, std::chrono::duration<double, std::milli>(t - T0).count());
     T0 = t;
   };
-  // (1) parallel: decode (sharing an earlier decode of the same bytes) and
-  // GetPubKeys' tx-supplied keys with their address checks
+  std::unique_lock<std::mutex> lk(app->mu);
+  const std::string chain_json = app->chain_json;
+  // (1) parallel: decode (sharing an earlier decode of the same bytes),
+  // GetPubKeys' tx-supplied keys, the signers' accounts
   std::vector<std::shared_ptr<Memo>> memos(ntx);
   parallel_for(app, ntx, [&](size_t t) {
     // a fresh Memo every time (an earlier one may be in use by an ante run)
@@ -1699,28 +1740,27 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
         }
       }
       m->plans.resize(tx.sigs.size());
+      m->sacc.resize(tx.signers.size());
+      for (size_t i = 0; i < tx.signers.size(); ++i) m->sacc[i] = find_account(app, tx.signers[i]);
     }
     memos[t] = std::move(m);
   });
   lap("decode");
-  // (2) serial: the state the plans depend on, predicting sequences
+  // (2) sequence prediction = a per-signer prefix count in block order; signers
+  // are hash-partitioned over the pool, each part scanning the block in order
+  // for its own signers (every account is touched by one part only)
   struct Job {
-    size_t t, signer;
+    uint32_t t, signer;
     uint64_t accnum, seq;
+    SignerPlan* plan;
     std::shared_ptr<const PubInfo> pub;       // the account's key after SetPubKey
   };
   std::vector<Job> jobs;
-  std::string chain_json;
   {
-    // sequence prediction = a per-signer prefix count in block order; signers
-    // are hash-partitioned over the pool, each part scanning the block in
-    // order for its own signers (every account is touched by one part only)
-    std::lock_guard<std::mutex> lk(app->mu);
-    chain_json = app->chain_json;
     const uint64_t epoch = ++app->bump_epoch;
     const int parts = ntx >= 2048 ? std::max(1, app->threads) : 1;
     std::vector<std::vector<Job>> pj(parts);
-    auto part_of = [&](Span a) { return a.n == 20 ? (int)((a.p[0] ^ a.p[7] ^ a.p[19]) % (unsigned)parts) : 0; };
+    auto part_of = [&](const Account* a) { return (int)(((uintptr_t)a >> 4) % (uintptr_t)parts); };
     parallel_parts(app, parts, [&](int part) {
       std::vector<Job>& out = pj[part];
       out.reserve(ntx / parts + 16);
@@ -1729,9 +1769,8 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
         if (!m.tx || m.tx->nil_msg || m.pk_panic >= 0) continue;
         const Tx& tx = *m.tx;
         for (size_t i = 0; i < tx.sigs.size() && i < tx.signers.size(); ++i) {
-          if (part_of(tx.signers[i]) != part) continue;
-          Account* acc = find_account(app, tx.signers[i]);
-          if (!acc) continue;
+          Account* acc = m.sacc[i];
+          if (!acc || part_of(acc) != part) continue;
           std::shared_ptr<const PubInfo> pub;
           try {
             pub = account_info(app, *acc);
@@ -1741,14 +1780,14 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
           if (!pub) pub = m.tx_pk[i];          // SetPubKey will store the tx-supplied key
           if (!pub) continue;
           if (acc->bump_epoch != epoch) { acc->bump_epoch = epoch; acc->bump = 0; }
-          out.push_back(Job{t, i, app->height == 0 ? 0 : acc->number, acc->sequence + acc->bump, std::move(pub)});
+          out.push_back(Job{(uint32_t)t, (uint32_t)i, app->height == 0 ? 0 : acc->number, acc->sequence + acc->bump,
+                            &m.plans[i], std::move(pub)});
         }
-        for (const Span& a : tx.signers)               // every signer's sequence moves if the tx passes
-          if (part_of(a) == part)
-            if (Account* acc = find_account(app, a)) {
-              if (acc->bump_epoch != epoch) { acc->bump_epoch = epoch; acc->bump = 0; }
-              acc->bump += 1;
-            }
+        for (Account* acc : m.sacc)                    // every signer's sequence moves if the tx passes
+          if (acc && part_of(acc) == part) {
+            if (acc->bump_epoch != epoch) { acc->bump_epoch = epoch; acc->bump = 0; }
+            acc->bump += 1;
+          }
       }
     });
     size_t tot = 0;
@@ -1758,35 +1797,50 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
       for (auto& j : v) jobs.push_back(std::move(j));
   }
   lap("jobs");
-  // (3) parallel: gas charge, sign bytes, leaves, cache keys
-  parallel_for(app, jobs.size(), [&](size_t k) {
+  // (3) parallel: gas charge, sign bytes, leaves, cache keys + lookups; the
+  // misses collect per worker
+  std::vector<std::vector<Leaf*>> wmiss(std::max(1, app->threads));
+  size_t n_all = 0;
+  std::atomic<size_t> n_leaf{0};
+  parallel_for_w(app, jobs.size(), [&](size_t k, int w) {
     Job& j = jobs[k];
     Memo& m = *memos[j.t];
     try {
-      make_plan(m.plans[j.signer], app, *m.tx, j.signer, j.pub, j.accnum, j.seq, chain_json);
+      make_plan(*j.plan, app, *m.tx, j.signer, j.pub, j.accnum, j.seq, chain_json);
     } catch (const Panic&) {
-      m.plans[j.signer].ok = false;                    // malformed: the ante chain will report it
+      j.plan->ok = false;                               // malformed: the ante chain will report it
+      return;
     }
+    for (Leaf& L : j.plan->leaves) {
+      if (L.verdict < 0) L.verdict = app->cache.get(L.key);
+      if (L.verdict < 0) wmiss[w].push_back(&L);
+    }
+    n_leaf.fetch_add(j.plan->leaves.size(), std::memory_order_relaxed);
   });
+  n_all = n_leaf.load();
   lap("plans");
+  lk.unlock();
   // (4) one GPU batch for the misses, no app lock held
-  std::vector<Leaf*> leaves;
-  for (auto& m : memos)
-    for (auto& p : m->plans)
-      if (p.ok)
-        for (Leaf& L : p.leaves) leaves.push_back(&L);
+  std::vector<Leaf*> miss;
+  {
+    size_t nm = 0;
+    for (auto& v : wmiss) nm += v.size();
+    miss.reserve(nm);
+    for (auto& v : wmiss) miss.insert(miss.end(), v.begin(), v.end());
+  }
+  app->st_hits += n_all - miss.size();
   uint32_t gpu_leaves = 0;
   const auto tg = std::chrono::steady_clock::now();
-  const int rc = leaves.empty() ? GVH_OK : resolve(app, leaves, &gpu_leaves, nullptr);
+  const int rc = miss.empty() ? GVH_OK : resolve(app, miss, &gpu_leaves, nullptr);
   app->st_gpu_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tg).count();
   if (rc == GVH_OK)
-    for (auto& m : memos)
-      for (auto& p : m->plans) p.resolved = p.ok;
+    parallel_for(app, jobs.size(), [&](size_t k) { jobs[k].plan->resolved = jobs[k].plan->ok; });
   lap("resolve");
   if (keep)
     for (auto& m : memos) app->memo.put(m);
   if (n_leaves) *n_leaves = gpu_leaves;
   if (memos_out) *memos_out = std::move(memos);
+  else release_memos(app, memos);
   return rc;
 }
 
@@ -1923,6 +1977,7 @@ int deliver_block(gvh_app* app, size_t ntx, const uint8_t* const* txs, const siz
   if (rc != GVH_OK) return rc;
   rc = deliver_memos(app, memos, out, codes);
   app->st_loop_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
+  release_memos(app, memos);
   return rc;
 }
 
