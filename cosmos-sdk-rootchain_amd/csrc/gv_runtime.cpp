@@ -105,7 +105,7 @@ class Pool {
 
 // memcpy split over the pool (large copies only: one core streams ~10 GB/s)
 void par_copy(Pool* pool, void* dst, const void* src, size_t bytes) {
-  constexpr size_t kMin = size_t(4) << 20;
+  constexpr size_t kMin = size_t(1) << 20;
   if (!pool || bytes < kMin) { if (bytes) memcpy(dst, src, bytes); return; }
   const int parts = (int)std::min<size_t>(pool->size(), bytes / (kMin / 2));
   const size_t per = round_up((bytes + parts - 1) / parts, 4096);
@@ -306,7 +306,7 @@ int ensure_keys(Dev* d, size_t need, size_t used, hipStream_t st) {
 struct gv_ctx {
   std::vector<Dev*> devs;
   size_t max_batch = size_t(1) << 20;
-  size_t lat_max = 4096;        // batches up to this size take the fused latency kernel (gv_lat.hip)
+  size_t lat_max = 8192;        // batches up to this size take the fused latency kernel (gv_lat.hip): crossover of profiles/r02/batch_curve.json
   size_t pipe_chunk = 262144;   // host path: chunk size of the two-set copy/compute pipeline (0 = max_batch)
   int stage_threads = 4;        // host path: staging memcpy threads per device
   bool time_kernels = false;

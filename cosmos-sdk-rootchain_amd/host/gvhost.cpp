@@ -1425,9 +1425,11 @@ void make_plan(SignerPlan& p, gvh_app* app, const Tx& tx, size_t signer, std::sh
 }
 
 // Resolve leaves: cache first, the secp256k1 misses in ONE GPU batch.
-int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint32_t* hits) {
+int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint32_t* hits, bool all_miss = false) {
   std::vector<Leaf*> miss;
-  if (leaves.size() >= 4096) {                        // big batches: lookups on the pool
+  if (all_miss) {                                     // the caller already looked every leaf up
+    miss.swap(leaves);
+  } else if (leaves.size() >= 4096) {                        // big batches: lookups on the pool
     parallel_for(app, leaves.size(), [&](size_t i) {
       Leaf* L = leaves[i];
       if (L->verdict < 0) L->verdict = app->cache.get(L->key);
@@ -1443,7 +1445,7 @@ int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint
       else miss.push_back(L);
     }
   }
-  app->st_hits += leaves.size() - miss.size();
+  if (!all_miss) app->st_hits += leaves.size() - miss.size();
   app->st_misses += miss.size();
   if (miss.empty()) return GVH_OK;
   if (!app->gpu) return GVH_ENOVERIFIER;
@@ -1831,7 +1833,7 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
   app->st_hits += n_all - miss.size();
   uint32_t gpu_leaves = 0;
   const auto tg = std::chrono::steady_clock::now();
-  const int rc = miss.empty() ? GVH_OK : resolve(app, miss, &gpu_leaves, nullptr);
+  const int rc = miss.empty() ? GVH_OK : resolve(app, miss, &gpu_leaves, nullptr, true);
   app->st_gpu_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tg).count();
   if (rc == GVH_OK)
     parallel_for(app, jobs.size(), [&](size_t k) { jobs[k].plan->resolved = jobs[k].plan->ok; });

@@ -143,7 +143,7 @@ int gv_dev_verify_digests_keyed(gv_ctx* ctx, int dev_slot, size_t n, const void*
 /* Options: "max_batch" (lanes per device launch, default 1<<20, at most
  * 0xFFFFFF00),
  * "lat_max" (batches of at most this many items -- per device slice -- take
- * the fused small-batch latency kernel, default 4096; 0 = never),
+ * the fused small-batch latency kernel, default 8192; 0 = never),
  * "pipe_chunk" (host-buffer calls: chunk size of the two-stream copy/compute
  * pipeline per device, default 262144; 0 = one chunk per max_batch),
  * "time_kernels" (0/1: record HIP events around each kernel stage),

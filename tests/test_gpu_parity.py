@@ -197,7 +197,7 @@ PATHS = {"throughput": 0, "latency": 1 << 30}
 def path(request, ver):
     ver.set_option("lat_max", PATHS[request.param])
     yield request.param
-    ver.set_option("lat_max", 4096)
+    ver.set_option("lat_max", 8192)
 
 
 def test_golden_digest_vectors(ver, path):
