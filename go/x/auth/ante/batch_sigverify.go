@@ -1,0 +1,285 @@
+package ante
+
+// BatchSigVerificationDecorator: the drop-in for SigVerificationDecorator
+// (x/auth/ante/sigverify.go:160-216) that verifies all of a transaction's
+// signature leaves in one batch (verdict cache first, then the GPU through
+// crypto/gpuverify), and NewPreVerifier, the block / mempool hook that fills
+// the verdict cache ahead of the ante handler (SURVEY.md §8b, §8f-1).
+//
+// Same API, same error types and strings, same ReCheck / simulate bypass,
+// same first-failure reporting order; gas is untouched (SigGasConsumeDecorator
+// runs before this decorator, unchanged).  Wiring: replace
+// NewSigVerificationDecorator(ak) at x/auth/ante/ante.go:27 with
+// NewBatchSigVerificationDecorator(ak, verifier, cache).
+//
+// Source-level only in this repository (no Go toolchain in the build image);
+// the C++ mirror host/gvhost.cpp implements the same logic and is tested.
+
+import (
+	"runtime"
+	"sync"
+
+	"github.com/tendermint/tendermint/crypto"
+	"github.com/tendermint/tendermint/crypto/ed25519"
+	"github.com/tendermint/tendermint/crypto/multisig"
+	"github.com/tendermint/tendermint/crypto/secp256k1"
+
+	"github.com/cosmos/cosmos-sdk/codec"
+	gv "github.com/cosmos/cosmos-sdk/crypto/gpuverify"
+	sdk "github.com/cosmos/cosmos-sdk/types"
+	sdkerrors "github.com/cosmos/cosmos-sdk/types/errors"
+)
+
+// BatchSigVerificationDecorator verifies every signer's signature of a tx
+// with one batched call.
+type BatchSigVerificationDecorator struct {
+	ak    AccountKeeper
+	v     gv.Verifier
+	cache *gv.VerdictCache
+}
+
+// NewBatchSigVerificationDecorator: v verifies the cache misses (a *gv.GPU,
+// or gv.CPU{}); cache may be nil (no cache).
+func NewBatchSigVerificationDecorator(ak AccountKeeper, v gv.Verifier, cache *gv.VerdictCache) BatchSigVerificationDecorator {
+	return BatchSigVerificationDecorator{ak: ak, v: v, cache: cache}
+}
+
+// AnteHandle implements sdk.AnteDecorator.
+func (d BatchSigVerificationDecorator) AnteHandle(ctx sdk.Context, tx sdk.Tx, simulate bool, next sdk.AnteHandler) (sdk.Context, error) {
+	// no need to verify signatures on recheck tx (sigverify.go:172)
+	if ctx.IsReCheckTx() {
+		return next(ctx, tx, simulate)
+	}
+	sigTx, ok := tx.(SigVerifiableTx)
+	if !ok {
+		return ctx, sdkerrors.Wrap(sdkerrors.ErrTxDecode, "invalid transaction type")
+	}
+	sigs := sigTx.GetSignatures()
+	signerAddrs := sigTx.GetSigners()
+	if len(sigs) != len(signerAddrs) { // sigverify.go:190-192
+		return ctx, sdkerrors.Wrapf(sdkerrors.ErrUnauthorized, "invalid number of signer;  expected: %d, got %d", len(signerAddrs), len(sigs))
+	}
+	// Phase 1 -- the non-cryptographic part of the reference loop in signer
+	// order, stopping where the loop would have returned; every signer before
+	// that point becomes a verification expression.
+	var (
+		exprs    []*expr
+		b        batch
+		firstErr error
+	)
+	for i, sig := range sigs {
+		acc, err := GetSignerAcc(ctx, d.ak, signerAddrs[i])
+		if err != nil {
+			firstErr = err
+			break
+		}
+		signBytes := sigTx.GetSignBytes(ctx, acc)
+		pubKey := acc.GetPubKey()
+		if !simulate && pubKey == nil {
+			firstErr = sdkerrors.Wrap(sdkerrors.ErrInvalidPubKey, "pubkey on account is not set")
+			break
+		}
+		if simulate { // sigverify.go:210: no verification when simulating
+			continue
+		}
+		exprs = append(exprs, b.build(pubKey, signBytes, sig))
+	}
+	// Phase 2 -- all leaves at once: verdict cache, then one Verifier batch.
+	b.resolve(d.v, d.cache)
+	for _, e := range exprs { // the FIRST failing signer is the one reported
+		if !e.eval(&b) {
+			return ctx, sdkerrors.Wrap(sdkerrors.ErrUnauthorized, "signature verification failed; verify correct account sequence and chain-id")
+		}
+	}
+	if firstErr != nil {
+		return ctx, firstErr
+	}
+	return next(ctx, tx, simulate)
+}
+
+// ---------------------------------------------------------------- leaves
+
+// expr is pk.VerifyBytes(msg, sig) as an expression over leaves:
+// a constant, one secp256k1 leaf, or the AND of a multisig's set bits.
+type expr struct {
+	konst bool
+	leaf  int // >= 0: index into batch.secp
+	and   []*expr
+	isAnd bool
+}
+
+func (e *expr) eval(b *batch) bool {
+	switch {
+	case e.isAnd:
+		for _, k := range e.and { // every leaf is a pure function: the AND equals the short-circuit
+			if !k.eval(b) {
+				return false
+			}
+		}
+		return true
+	case e.leaf >= 0:
+		return b.ok[e.leaf]
+	default:
+		return e.konst
+	}
+}
+
+type batch struct {
+	pubs []secp256k1.PubKeySecp256k1
+	msgs [][]byte
+	sigs [][]byte
+	keys [][32]byte
+	ok   []bool
+}
+
+// build mirrors the key types the reference verifies (sigverify.go:303-321):
+// secp256k1 leaves are batched; multisig (tendermint
+// multisig.PubKeyMultisigThreshold.VerifyBytes) fans out in bit order with
+// the same structural checks; ed25519 and any other key verify on the CPU.
+func (b *batch) build(pk crypto.PubKey, msg, sig []byte) *expr {
+	switch p := pk.(type) {
+	case secp256k1.PubKeySecp256k1:
+		if len(sig) != 64 { // VerifyBytes' first check
+			return &expr{leaf: -1}
+		}
+		b.pubs = append(b.pubs, p)
+		b.msgs = append(b.msgs, msg)
+		b.sigs = append(b.sigs, sig)
+		return &expr{leaf: len(b.pubs) - 1}
+	case multisig.PubKeyMultisigThreshold:
+		var ms multisig.Multisignature
+		if err := codec.Cdc.UnmarshalBinaryBare(sig, &ms); err != nil {
+			return &expr{leaf: -1}
+		}
+		size := ms.BitArray.Size()
+		if len(p.PubKeys) != size || len(ms.Sigs) < int(p.K) || len(ms.Sigs) > size ||
+			ms.BitArray.NumTrueBitsBefore(size) < int(p.K) {
+			return &expr{leaf: -1}
+		}
+		e := &expr{leaf: -1, isAnd: true}
+		j := 0
+		for i := 0; i < size; i++ {
+			if ms.BitArray.GetIndex(i) {
+				e.and = append(e.and, b.build(p.PubKeys[i], msg, ms.Sigs[j]))
+				j++
+			}
+		}
+		return e
+	case ed25519.PubKeyEd25519:
+		return &expr{leaf: -1, konst: p.VerifyBytes(msg, sig)}
+	default: // includes a nil sub-key: the method call panics exactly as in the reference
+		return &expr{leaf: -1, konst: pk.VerifyBytes(msg, sig)}
+	}
+}
+
+// resolve answers every secp256k1 leaf: cache hits first, the misses in one
+// Verifier call, then the cache is filled.
+func (b *batch) resolve(v gv.Verifier, cache *gv.VerdictCache) {
+	n := len(b.pubs)
+	b.ok = make([]bool, n)
+	b.keys = make([][32]byte, n)
+	var miss []int
+	for i := 0; i < n; i++ {
+		b.keys[i] = gv.LeafKey(gv.KindSecp256k1, b.pubs[i][:], b.sigs[i], b.msgs[i])
+		if cache != nil {
+			if ok, hit := cache.Get(b.keys[i]); hit {
+				b.ok[i] = ok
+				continue
+			}
+		}
+		miss = append(miss, i)
+	}
+	if len(miss) == 0 {
+		return
+	}
+	pubs := make([]secp256k1.PubKeySecp256k1, len(miss))
+	msgs := make([][]byte, len(miss))
+	sigs := make([][]byte, len(miss))
+	for k, i := range miss {
+		pubs[k], msgs[k], sigs[k] = b.pubs[i], b.msgs[i], b.sigs[i]
+	}
+	res := v.VerifyBatch(pubs, msgs, sigs)
+	for k, i := range miss {
+		b.ok[i] = res[k]
+		if cache != nil {
+			cache.Put(b.keys[i], res[k])
+		}
+	}
+}
+
+// ---------------------------------------------------------- PreVerifyTxs
+
+// NewPreVerifier returns the function baseapp.PreVerifyTxs calls on a batch
+// of decoded txs (a block before its DeliverTx loop, a CheckTx window, the
+// genesis gentxs): every signer's sign bytes are predicted -- account number
+// from state (0 at height 0, stdtx.go:249-253), sequence = state sequence +
+// earlier txs of the same signer in the batch -- and all leaves are verified
+// in one batch into the cache.  A wrong prediction is only a cache miss: the
+// decorator rebuilds the sign bytes from the state it runs on.
+func NewPreVerifier(ak AccountKeeper, v gv.Verifier, cache *gv.VerdictCache) func(ctx sdk.Context, txs []sdk.Tx) {
+	return func(ctx sdk.Context, txs []sdk.Tx) {
+		type job struct {
+			sigTx  SigVerifiableTx
+			signer int
+			pk     crypto.PubKey
+			sig    []byte
+			seq    uint64
+		}
+		var jobs []job
+		bump := map[string]uint64{}
+		for _, tx := range txs {
+			sigTx, ok := tx.(SigVerifiableTx)
+			if !ok {
+				continue
+			}
+			sigs, signers, txPks := sigTx.GetSignatures(), sigTx.GetSigners(), sigTx.GetPubKeys()
+			for i := 0; i < len(sigs) && i < len(signers); i++ {
+				acc := ak.GetAccount(ctx, signers[i]) // a fresh decode: mutating it is local
+				if acc == nil {
+					continue
+				}
+				pk := acc.GetPubKey()
+				if pk == nil && i < len(txPks) {
+					pk = txPks[i] // SetPubKeyDecorator will store the tx-supplied key
+				}
+				if pk == nil {
+					continue
+				}
+				seq := acc.GetSequence() + bump[signers[i].String()]
+				jobs = append(jobs, job{sigTx, i, pk, sigs[i], seq})
+			}
+			for _, a := range signers {
+				bump[a.String()]++
+			}
+		}
+		// sign bytes (JSON) on every core, then one batch
+		parts := make([]batch, runtime.NumCPU())
+		var wg sync.WaitGroup
+		for w := range parts {
+			wg.Add(1)
+			go func(w int) {
+				defer wg.Done()
+				for k := w; k < len(jobs); k += len(parts) {
+					j := jobs[k]
+					acc := ak.GetAccount(ctx, j.sigTx.GetSigners()[j.signer])
+					if acc == nil {
+						continue
+					}
+					_ = acc.SetSequence(j.seq)
+					func() {
+						defer func() { _ = recover() }() // malformed multisig: the ante chain reports it
+						parts[w].build(j.pk, j.sigTx.GetSignBytes(ctx, acc), j.sig)
+					}()
+				}
+			}(w)
+		}
+		wg.Wait()
+		var all batch
+		for _, p := range parts {
+			all.pubs = append(all.pubs, p.pubs...)
+			all.msgs = append(all.msgs, p.msgs...)
+			all.sigs = append(all.sigs, p.sigs...)
+		}
+		all.resolve(v, cache)
+	}
+}

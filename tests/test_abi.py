@@ -24,6 +24,41 @@ def test_header_declares_the_python_binding_symbols():
     assert declared_symbols() == sorted(gvm.EXPORTED_SYMBOLS)
 
 
+def _prototype_arity():
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    txt = re.sub(r"//[^\n]*", "", txt)
+    arity = {}
+    for name, args in re.findall(r"\b(gv_[a-z_0-9]+)\s*\(([^)]*)\)\s*;", txt):
+        a = args.strip()
+        arity[name] = 0 if a in ("", "void") else a.count(",") + 1
+    return arity
+
+
+def _call_args(src, start):
+    depth, i, n = 1, start, 1
+    if src[start:].lstrip().startswith(")"):
+        return 0
+    while depth:
+        c = src[i]
+        depth += c == "("
+        depth -= c == ")"
+        n += c == "," and depth == 1
+        i += 1
+    return n
+
+
+def test_go_binding_calls_declared_symbols_with_declared_arity():
+    """go/crypto/gpuverify (source-only: no Go toolchain here) calls only
+    functions include/gpuverify.h declares, each with its declared arity."""
+    arity = _prototype_arity()
+    src = open(os.path.join(REPO, "go", "crypto", "gpuverify", "gpuverify.go")).read()
+    calls = [(m.group(1), _call_args(src, m.end())) for m in re.finditer(r"\bC\.(gv_\w+)\(", src)]
+    assert len(calls) >= 8
+    for name, n in calls:
+        assert name in arity, name
+        assert n == arity[name], (name, n, arity[name])
+
+
 def test_library_exports_every_declared_symbol():
     if not os.path.exists(gvm.LIB_PATH):
         gvm.build()
