@@ -461,6 +461,7 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
         import bench_extras as X
         ex = {}
         t = time.perf_counter()
+        ex["c2_hostpath"] = X.c2_hostpath(ver, pub, sig, dig, exp, device_value=value)
         ex["c2_key_cache"] = X.c2_key_cache(ver, pub, sig, dig, exp, min(args.keys, n))
         ex["c2_unique_keys"] = X.c2_unique_keys(ver, make_digest_workload, n, args.threads)
         ex["c3_adversarial"] = X.c3_adversarial(ver, make_digest_workload, n, args.threads)

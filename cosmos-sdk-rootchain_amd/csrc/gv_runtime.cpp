@@ -115,6 +115,30 @@ void par_copy(Pool* pool, void* dst, const void* src, size_t bytes) {
   });
 }
 
+// Several copies as one pool pass: the total is cut into equal byte ranges,
+// one per thread, each range spanning whichever segments it covers.
+struct CopySeg {
+  uint8_t* dst;
+  const uint8_t* src;
+  size_t bytes;
+};
+void par_copy_segs(Pool* pool, const CopySeg* seg, int ns) {
+  constexpr size_t kMin = size_t(1) << 20;
+  size_t total = 0;
+  for (int i = 0; i < ns; ++i) total += seg[i].bytes;
+  auto copy_range = [&](size_t lo, size_t hi) {       // [lo, hi) of the concatenation
+    size_t base = 0;
+    for (int i = 0; i < ns && lo < hi; base += seg[i].bytes, ++i) {
+      const size_t a = std::max(lo, base), b = std::min(hi, base + seg[i].bytes);
+      if (a < b) memcpy(seg[i].dst + (a - base), seg[i].src + (a - base), b - a);
+    }
+  };
+  if (!pool || total < kMin) { copy_range(0, total); return; }
+  const int parts = (int)std::min<size_t>(pool->size(), total / (kMin / 2));
+  const size_t per = round_up((total + parts - 1) / parts, 4096);
+  pool->run(parts, [&](int p) { copy_range(std::min(total, p * per), std::min(total, (p + 1) * per)); });
+}
+
 // One persistent thread per extra device: runs the device's slice of a host batch.
 class Worker {
  public:
@@ -307,8 +331,9 @@ struct gv_ctx {
   std::vector<Dev*> devs;
   size_t max_batch = size_t(1) << 20;
   size_t lat_max = 8192;        // batches up to this size take the fused latency kernel (gv_lat.hip): crossover of profiles/r02/batch_curve.json
-  size_t pipe_chunk = 262144;   // host path: chunk size of the two-set copy/compute pipeline (0 = max_batch)
-  int stage_threads = 4;        // host path: staging memcpy threads per device
+  size_t pipe_chunk = 131072;   // host path: first chunk of the two-set copy/compute pipeline (0 = max_batch)
+  int pipe_growth = 4;          // host path: each later chunk at most this times the one before
+  int stage_threads = 8;        // host path: staging memcpy threads per device
   bool time_kernels = false;
   bool fault_inject = false;
   size_t keys = 0;              // key-arena slots in use (same on every device)
@@ -428,13 +453,17 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
   size_t hb_bytes = 0;
   if ((rc = ensure_pinned((uint8_t**)&s->h_bits, &s->h_bits_cap, (C / 64) * 8))) return rc;
   uint8_t* h = s->h_in;
-  if (keyed) par_copy(d->pool, h, hb.slots + c0, cn * 4);
-  else par_copy(d->pool, h, hb.pub33 + c0 * 33, cn * 33);
-  par_copy(d->pool, h + L.sig, hb.sig64 + c0 * 64, cn * 64);
   uint64_t bmin = 0;
-  if (!msgs) {
-    par_copy(d->pool, h + L.third, hb.dig32 + c0 * 32, cn * 32);
+  if (!msgs) {                              // keys/slots, signatures, digests: one pool pass
+    const CopySeg segs[3] = {keyed ? CopySeg{h, (const uint8_t*)(hb.slots + c0), cn * 4}
+                                   : CopySeg{h, hb.pub33 + c0 * 33, cn * 33},
+                             CopySeg{h + L.sig, hb.sig64 + c0 * 64, cn * 64},
+                             CopySeg{h + L.third, hb.dig32 + c0 * 32, cn * 32}};
+    par_copy_segs(d->pool, segs, 3);
   } else {
+    if (keyed) par_copy(d->pool, h, hb.slots + c0, cn * 4);
+    else par_copy(d->pool, h, hb.pub33 + c0 * 33, cn * 33);
+    par_copy(d->pool, h + L.sig, hb.sig64 + c0 * 64, cn * 64);
     uint64_t lo = UINT64_MAX, hi = 0;
     for (size_t i = c0; i < c0 + cn; ++i) {
       lo = std::min<uint64_t>(lo, hb.off[i]);
@@ -474,15 +503,38 @@ int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const HostBatch& hb) {
   std::lock_guard<std::mutex> lk(d->mu);
   CK(hipSetDevice(d->id));
   const size_t n = hi - lo;
-  size_t nch = (n + ctx->max_batch - 1) / ctx->max_batch;
-  if (n > ctx->lat_max && ctx->pipe_chunk) nch = std::max(nch, (n + ctx->pipe_chunk - 1) / ctx->pipe_chunk);
-  const size_t chunk = std::min(ctx->max_batch, round_up((n + nch - 1) / nch, 256));
+  // Chunk sizes.  Pipelined (past lat_max): a ramp -- pipe_chunk first, each
+  // later chunk at most pipe_growth times the one before -- so the first
+  // kernels start after a short staging copy and every later chunk is staged
+  // (pageable -> pinned copy, H2D) while the one before it computes.  Else
+  // equal chunks of at most max_batch.  Every chunk but the last is a multiple
+  // of 256 (harvest copies bitmap words).
+  std::vector<size_t> sizes;
+  if (n > ctx->lat_max && ctx->pipe_chunk) {
+    size_t c = std::min(ctx->pipe_chunk, ctx->max_batch), left = n;
+    while (left) {
+      const size_t take = std::min(left, c);
+      sizes.push_back(take);
+      left -= take;
+      c = std::min(ctx->max_batch, c * (size_t)ctx->pipe_growth);
+    }
+    const size_t m = sizes.size();          // a runt tail joins the chunk before it
+    if (m >= 2 && 2 * sizes[m - 1] < sizes[m - 2] && sizes[m - 1] + sizes[m - 2] <= ctx->max_batch) {
+      sizes[m - 2] += sizes[m - 1];
+      sizes.pop_back();
+    }
+  } else {
+    const size_t nch = (n + ctx->max_batch - 1) / ctx->max_batch;
+    const size_t chunk = std::min(ctx->max_batch, round_up((n + nch - 1) / nch, 256));
+    for (size_t c0 = 0; c0 < n; c0 += chunk) sizes.push_back(std::min(chunk, n - c0));
+  }
   int rc = GV_OK;
   int k = 0;
-  for (size_t c0 = lo; c0 < hi && rc == GV_OK; c0 += chunk, k ^= 1) {
+  size_t c0 = lo;
+  for (size_t i = 0; i < sizes.size() && rc == GV_OK; c0 += sizes[i], ++i, k ^= 1) {
     Set* s = &d->set[k];
     if (s->busy && (rc = harvest(d, s, hb))) break;
-    rc = submit(ctx, d, s, c0, std::min(chunk, hi - c0), hb);
+    rc = submit(ctx, d, s, c0, sizes[i], hb);
   }
   for (Set& s : d->set)                          // drain (also after an error)
     if (s.busy) {
@@ -766,6 +818,17 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "pipe_chunk")) {
     if (val != 0 && (val < 256 || (unsigned long long)val > kMaxItems)) return GV_EINVAL;
     ctx->pipe_chunk = val ? round_up((size_t)val, 256) : 0;
+  } else if (!strcmp(key, "pipe_growth")) {
+    if (val < 1 || val > 64) return GV_EINVAL;
+    ctx->pipe_growth = (int)val;
+  } else if (!strcmp(key, "stage_threads")) {
+    if (val < 1 || val > 64) return GV_EINVAL;
+    ctx->stage_threads = (int)val;
+    for (Dev* d : ctx->devs) {                    // replace each device's staging pool
+      std::lock_guard<std::mutex> lk(d->mu);
+      delete d->pool;
+      d->pool = new Pool((int)val - 1);
+    }
   } else if (!strcmp(key, "time_kernels")) {
     ctx->time_kernels = val != 0;
   } else if (!strcmp(key, "fault_inject")) {

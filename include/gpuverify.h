@@ -144,8 +144,12 @@ int gv_dev_verify_digests_keyed(gv_ctx* ctx, int dev_slot, size_t n, const void*
  * 0xFFFFFF00),
  * "lat_max" (batches of at most this many items -- per device slice -- take
  * the fused small-batch latency kernel, default 8192; 0 = never),
- * "pipe_chunk" (host-buffer calls: chunk size of the two-stream copy/compute
- * pipeline per device, default 262144; 0 = one chunk per max_batch),
+ * "pipe_chunk" (host-buffer calls past lat_max: first chunk of the two-stream
+ * copy/compute pipeline per device, default 131072; 0 = one chunk per
+ * max_batch), "pipe_growth" (each later chunk at most this many times the one
+ * before, default 4: the staging of chunk i+1 hides under the kernels of
+ * chunk i), "stage_threads" (pageable -> pinned staging copy threads per
+ * device, default 8),
  * "time_kernels" (0/1: record HIP events around each kernel stage),
  * "fault_inject" (0/1: every verify call fails with GV_EFAULT; test hook). */
 int gv_set_option(gv_ctx* ctx, const char* key, long long val);

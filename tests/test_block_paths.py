@@ -302,6 +302,8 @@ def test_bounded_verdict_cache(ver):
                 seq = blk * 25 + r
                 sb = T.std_sign_bytes(CHAIN, i, seq, FEE, msgs, "")
                 txs.append(T.std_tx(msgs, FEE, "", [(k.amino if seq == 0 else b"", k.sign(sb))]))
+        rc, n = app.preverify(txs)                  # PreVerifyTxs fills the cache (a delivered block only reads it)
+        assert rc == 0 and app.cache_size() <= 512
         rc, codes = app.deliver_block_codes(txs)
         assert rc == 0 and (codes == 0).all()
         assert app.cache_size() <= 512

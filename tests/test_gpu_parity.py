@@ -393,13 +393,16 @@ def test_overlapping_device_calls_on_separate_streams(ver):
         ver.stream_destroy(s2)
 
 
-@pytest.mark.parametrize("chunk", [256, 4096, 0])
-def test_host_pipeline_chunking(ver, chunk):
+@pytest.mark.parametrize("chunk,growth,stage", [(256, 1, 8), (256, 3, 3), (4096, 4, 8), (0, 4, 1)])
+def test_host_pipeline_chunking(ver, chunk, growth, stage):
     """The two-stream host pipeline (pinned staging, chunks alternating between
-    two scratch sets) over ragged chunk boundaries, digests and messages."""
+    two scratch sets, ramped chunk sizes) over ragged chunk boundaries, digests
+    and messages, with several staging-thread counts."""
     pub, sig, dig = make_random_batch(10007, seed=chunk + 1, adversarial=0.25, nkeys=29)
     want = O.verify_digests(pub, sig, dig, threads=16)
     ver.set_option("pipe_chunk", chunk)
+    ver.set_option("pipe_growth", growth)
+    ver.set_option("stage_threads", stage)
     try:
         assert np.array_equal(ver.verify_batch_digests(pub, sig, dig), want)
         bits = ver.verify_batch_digests_bits(pub, sig, dig)
@@ -414,11 +417,13 @@ def test_host_pipeline_chunking(ver, chunk):
         mwant = np.array([i % 7 != 0 for i in range(5000)], np.uint8)
         assert np.array_equal(ver.verify_batch_msgs(mpub, msig, msgs), mwant)
     finally:
-        ver.set_option("pipe_chunk", 262144)
+        ver.set_option("pipe_chunk", 131072)
+        ver.set_option("pipe_growth", 4)
+        ver.set_option("stage_threads", 8)
 
 
 def test_option_bounds(ver):
     for key, val in (("max_batch", 1 << 32), ("max_batch", 255), ("lat_max", -1), ("lat_max", 1 << 33),
-                     ("pipe_chunk", 100), ("no_such_option", 1)):
+                     ("pipe_chunk", 100), ("pipe_growth", 0), ("stage_threads", 0), ("no_such_option", 1)):
         with pytest.raises(gvm.GpuVerifyError):
             ver.set_option(key, val)

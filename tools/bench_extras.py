@@ -55,6 +55,31 @@ def _timed_device_runs(ver, run, steps: int, warmup: int = 1):
     return el, {"unpack_or_sha_ms": round(unpack_ms, 3), "prep_ms": round(prep_ms, 3), "ecmult_ms": round(ecmult_ms, 3)}
 
 
+def c2_hostpath(ver, pub, sig, dig, exp, steps: int = 5, device_value: float | None = None):
+    """C2 through the host-buffer entry points (SURVEY.md §8d names
+    gv_verify_digests for C2): pageable numpy inputs, the library stages them
+    through its pinned ring and overlaps H2D / kernels / D2H over chunks on two
+    streams; PCIe included.  Reported beside `value` (device-resident)."""
+    n = len(pub)
+    out = {}
+    for name, fn in (("bytes", ver.verify_batch_digests), ("bits", ver.verify_batch_digests_bits)):
+        fn(pub, sig, dig)                                   # warm the staging ring
+        t = time.perf_counter()
+        for _ in range(steps):
+            r = fn(pub, sig, dig)
+        el = time.perf_counter() - t
+        got = (r == 1) if name == "bytes" else _unpack_bits(r, n).astype(bool)
+        out[name] = {"value": round(n * steps / el, 1), "ms_per_call": round(el / steps * 1e3, 3),
+                     "mismatches": int(np.count_nonzero(got != exp.astype(bool)))}
+    best = max(out["bytes"]["value"], out["bits"]["value"])
+    res = {"items": n, "unit": "verifies/s", "value": best, "entry_points": out,
+           "note": "gv_verify_digests (u8 verdict per item) and gv_verify_digests_bits (bitmap) from pageable host "
+                   "buffers; whole call timed (staging, H2D, kernels, D2H)"}
+    if device_value:
+        res["frac_of_device_resident"] = round(best / device_value, 4)
+    return res
+
+
 def c2_unique_keys(ver, make_workload, n: int, threads: int, steps: int = 3):
     """SURVEY.md §8d C2 variant: one distinct key per item (no key reuse at
     all), device-resident, bitmap checked against construction."""
