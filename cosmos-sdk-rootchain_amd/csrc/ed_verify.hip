@@ -1,0 +1,76 @@
+// ed_verify.hip -- ed25519 VerifyBytes on gfx950: the
+// multisig ed25519 sub-key leaves of x/auth/ante/sigverify.go:303-306 /
+// :325-338 (tendermint v0.33.4 PubKeyEd25519.VerifyBytes -> go1.14
+// crypto/ed25519 Verify), one signature per lane.
+//
+//   k_ed_btab    one-time: the resident comb table j * 256^w * B
+//                (32 windows x 129 entries x 27 words = 436 KB, L2-resident)
+//   k_ed_verify  per lane: SHA-512(R || A || M) mod L, the sig[63] & 224 and
+//                ScMinimal checks, FromBytes(A), the per-lane table j(-A)
+//                (global scratch, lane-strided rows: coalesced), 252
+//                doublings + 64 signed radix-16 table adds for [h](-A), 32
+//                comb adds for [s]B, one inversion to encode R', a byte
+//                compare with sig[:32]; the accept bitmap by wave ballot.
+// The arithmetic lives in ed_group.cuh and is the same source the CPU tests
+// compile (tests/test_ed_host.py).
+#include <hip/hip_runtime.h>
+
+#include "ed_group.cuh"
+#include "gv_kernels.h"
+
+#if defined(__HIP_DEVICE_COMPILE__) && defined(__AMDGCN_WAVEFRONT_SIZE) && __AMDGCN_WAVEFRONT_SIZE != 64
+#error "ed_verify.hip writes one 64-bit ballot word per wave64"
+#endif
+
+namespace gv {
+namespace ed {
+
+static_assert(ED_ATAB_WORDS == GV_ED_ATAB_WORDS, "per-lane table size");
+static_assert(ED_BTAB_WORDS == GV_ED_BTAB_WORDS, "comb table size");
+
+__global__ __launch_bounds__(256) void k_ed_btab(u32* btab) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= ED_BTAB_WINDOWS * ED_BTAB_ENTRIES) return;
+  u32 out[ED_PRE_WORDS];
+  ed_btab_entry(out, t / ED_BTAB_ENTRIES, t % ED_BTAB_ENTRIES);
+#pragma unroll
+  for (int k = 0; k < ED_PRE_WORDS; ++k) btab[(size_t)t * ED_PRE_WORDS + k] = out[k];
+}
+
+__global__ __launch_bounds__(256) void k_ed_verify(gvk_ed b) {
+  const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+  bool ok = false;
+  if (g < b.n) {
+    u32 pw[8], sw[16];
+    const uint4* pp = (const uint4*)(b.pub32 + (size_t)g * 32);
+    const uint4* sp = (const uint4*)(b.sig64 + (size_t)g * 64);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint4 v = pp[k];
+      pw[4 * k] = v.x; pw[4 * k + 1] = v.y; pw[4 * k + 2] = v.z; pw[4 * k + 3] = v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = sp[k];
+      sw[4 * k] = v.x; sw[4 * k + 1] = v.y; sw[4 * k + 2] = v.z; sw[4 * k + 3] = v.w;
+    }
+    const uint8_t* m = b.msg_blob + b.msg_off[g];
+    ok = ed_verify_item(pw, sw, [=](u32 i) { return (u32)m[i]; }, b.msg_len[g], b.atab + g, b.C, b.btab);
+  }
+  const uint64_t mask = __ballot(ok);
+  if ((threadIdx.x & 63) == 0 && g < b.n) b.bits[g >> 6] = mask;   // words up to ceil(n / 64) only
+}
+
+}  // namespace ed
+}  // namespace gv
+
+extern "C" hipError_t gvk_ed_btab(uint32_t* btab, hipStream_t st) {
+  const int n = ED_BTAB_WINDOWS * ED_BTAB_ENTRIES;
+  hipLaunchKernelGGL(gv::ed::k_ed_btab, dim3((n + 255) / 256), dim3(256), 0, st, btab);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t gvk_ed_verify(const gvk_ed* b, hipStream_t st) {
+  hipLaunchKernelGGL(gv::ed::k_ed_verify, dim3(b->C / 256), dim3(256), 0, st, *b);
+  return hipGetLastError();
+}

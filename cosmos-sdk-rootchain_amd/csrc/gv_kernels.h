@@ -78,6 +78,23 @@ typedef struct gvk_lat {
   uint32_t kC, kcount;
 } gvk_lat;
 
+// ed25519 (ed_verify.hip): one signature per lane over C lanes (C % 256 == 0).
+#define GV_ED_ATAB_WORDS 288            // per-lane table j(-A), j = 1..8: 8 x 36 words, rows of stride C
+#define GV_ED_BTAB_WORDS (32 * 129 * 27)  // resident comb table j * 256^w * B
+typedef struct gvk_ed {
+  uint32_t n, C;
+  const uint8_t* pub32;         // n x 32
+  const uint8_t* sig64;         // n x 64
+  const uint8_t* msg_blob;
+  const uint64_t* msg_off;
+  const uint32_t* msg_len;
+  uint32_t* atab;               // GV_ED_ATAB_WORDS rows of C words (scratch)
+  const uint32_t* btab;         // GV_ED_BTAB_WORDS
+  uint64_t* bits;               // C/64 words
+} gvk_ed;
+hipError_t gvk_ed_btab(uint32_t* btab, hipStream_t st);
+hipError_t gvk_ed_verify(const gvk_ed* b, hipStream_t st);
+
 hipError_t gvk_gen_gtable(uint32_t* gtab, hipStream_t st);
 hipError_t gvk_verify_lat(const gvk_lat* b, hipStream_t st);
 hipError_t gvk_sha256(const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint32_t n, uint32_t C,

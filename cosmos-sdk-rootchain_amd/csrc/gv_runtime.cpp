@@ -244,6 +244,24 @@ struct Dev {
   static constexpr int kRing = 256;
   hipEvent_t ring[kRing][5] = {};
   int ring_next = 0, ring_count = 0, last = -1;
+  // ed25519: the resident comb table and one scratch set
+  uint32_t* edtab = nullptr;
+  struct Ed {
+    size_t cap = 0;                               // lanes
+    uint8_t* d_in = nullptr;                      // pub32 | sig64 | off u64 | len u32 (ed_layout)
+    uint32_t* atab = nullptr;                     // GV_ED_ATAB_WORDS rows of cap words
+    uint64_t* bits = nullptr;
+    uint8_t* d_blob = nullptr;
+    size_t blob_cap = 0;
+    uint8_t* h_in = nullptr;
+    size_t h_in_cap = 0;
+    uint8_t* h_blob = nullptr;
+    size_t h_blob_cap = 0;
+    uint8_t* h_bits = nullptr;
+    size_t h_bits_cap = 0;
+    hipEvent_t last = nullptr;                    // end of the last work using the scratch
+    hipStream_t last_st = nullptr;
+  } ed;
   std::mutex mu;
   Pool* pool = nullptr;                           // staging memcpy threads
   Worker* worker = nullptr;                       // slice runner (devices 1..n-1 of a context)
@@ -322,6 +340,75 @@ int ensure_keys(Dev* d, size_t need, size_t used, hipStream_t st) {
   if (d->kzq) (void)hipFree(d->kzq);
   if (d->kok) (void)hipFree(d->kok);
   d->kqt = qt; d->kzq = zq; d->kok = ok; d->kcap = cap;
+  return GV_OK;
+}
+
+// ---- ed25519 scratch
+struct EdLayout {
+  size_t sig, off, len, total;
+};
+EdLayout ed_layout(size_t C) {                    // C % 256 == 0: every part 256-aligned
+  EdLayout L;
+  L.sig = C * 32;
+  L.off = L.sig + C * 64;
+  L.len = L.off + C * 8;
+  L.total = L.len + C * 4;
+  return L;
+}
+
+int ed_ensure(Dev* d, size_t C, hipStream_t st) {
+  if (!d->edtab) {                                // one-time: the comb table, built on the device
+    if (hipMalloc(&d->edtab, (size_t)GV_ED_BTAB_WORDS * 4) != hipSuccess) { d->edtab = nullptr; return GV_ENOMEM; }
+    CK(gvk_ed_btab(d->edtab, st));
+    CK(hipStreamSynchronize(st));
+  }
+  if (!d->ed.last) CK(hipEventCreateWithFlags(&d->ed.last, hipEventDisableTiming));
+  if (C <= d->ed.cap) return GV_OK;
+  if (d->ed.last_st) CK(hipEventSynchronize(d->ed.last));
+  if (d->ed.d_in) (void)hipFree(d->ed.d_in);
+  if (d->ed.atab) (void)hipFree(d->ed.atab);
+  if (d->ed.bits) (void)hipFree(d->ed.bits);
+  d->ed.d_in = nullptr; d->ed.atab = nullptr; d->ed.bits = nullptr; d->ed.cap = 0;
+  if (hipMalloc(&d->ed.d_in, ed_layout(C).total) != hipSuccess ||
+      hipMalloc(&d->ed.atab, C * (size_t)GV_ED_ATAB_WORDS * 4) != hipSuccess ||
+      hipMalloc(&d->ed.bits, C / 8) != hipSuccess)
+    return GV_ENOMEM;
+  d->ed.cap = C;
+  return GV_OK;
+}
+
+// One k_ed_verify launch over n items (device pointers) on stream st.
+int ed_launch(bool timed, Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig, const uint8_t* blob,
+              const uint64_t* off, const uint32_t* len, uint64_t* bits, hipStream_t st) {
+  const size_t C = round_up(n, 256);
+  int rc = ed_ensure(d, C, st);
+  if (rc) return rc;
+  if (d->ed.last_st && d->ed.last_st != st) CK(hipStreamWaitEvent(st, d->ed.last, 0));
+  gvk_ed b;
+  memset(&b, 0, sizeof b);
+  b.n = (uint32_t)n;
+  b.C = (uint32_t)C;
+  b.pub32 = pub; b.sig64 = sig;
+  b.msg_blob = blob; b.msg_off = off; b.msg_len = len;
+  b.atab = d->ed.atab;
+  b.btab = d->edtab;
+  b.bits = bits;
+  hipEvent_t* rs = nullptr;
+  if (timed) {                                    // stages: (none) x 3 | the ed25519 kernel
+    rs = d->ring[d->ring_next];
+    for (int i = 0; i < 5; ++i)
+      if (!rs[i]) CK(hipEventCreate(&rs[i]));
+    for (int i = 0; i < 4; ++i) CK(hipEventRecord(rs[i], st));
+  }
+  CK(gvk_ed_verify(&b, st));
+  if (rs) {
+    CK(hipEventRecord(rs[4], st));
+    d->last = d->ring_next;
+    d->ring_next = (d->ring_next + 1) % Dev::kRing;
+    d->ring_count = std::min(d->ring_count + 1, Dev::kRing);
+  }
+  CK(hipEventRecord(d->ed.last, st));
+  d->ed.last_st = st;
   return GV_OK;
 }
 
@@ -545,6 +632,93 @@ int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const HostBatch& hb) {
   return rc;
 }
 
+// ---- ed25519 host-buffer batches: chunks of at most ed_chunk items, staged
+// through pinned memory on the device's first stream.
+struct EdHost {
+  const uint8_t* pub32;
+  const uint8_t* sig64;
+  const uint8_t* blob;
+  const uint64_t* off;
+  const uint32_t* len;
+  uint8_t* out_ok;
+};
+
+int ed_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const EdHost& hb) {
+  std::lock_guard<std::mutex> lk(d->mu);
+  CK(hipSetDevice(d->id));
+  hipStream_t st = d->set[0].st;
+  const size_t chunk = std::min<size_t>(ctx->max_batch, 262144);
+  for (size_t c0 = lo; c0 < hi; c0 += chunk) {
+    const size_t cn = std::min(chunk, hi - c0), C = round_up(cn, 256);
+    int rc = ed_ensure(d, C, st);
+    if (rc) return rc;
+    const EdLayout L = ed_layout(C);
+    if ((rc = ensure_pinned(&d->ed.h_in, &d->ed.h_in_cap, L.total))) return rc;
+    if ((rc = ensure_pinned(&d->ed.h_bits, &d->ed.h_bits_cap, C / 8))) return rc;
+    if (d->ed.last_st) CK(hipEventSynchronize(d->ed.last));      // the staging buffers are free
+    uint8_t* h = d->ed.h_in;
+    uint64_t lo_b = UINT64_MAX, hi_b = 0;
+    for (size_t i = c0; i < c0 + cn; ++i) {
+      lo_b = std::min<uint64_t>(lo_b, hb.off[i]);
+      hi_b = std::max<uint64_t>(hi_b, hb.off[i] + hb.len[i]);
+    }
+    if (lo_b > hi_b) lo_b = hi_b = 0;
+    const size_t nb = hi_b - lo_b;
+    if ((rc = ensure_pinned(&d->ed.h_blob, &d->ed.h_blob_cap, nb))) return rc;
+    if (nb > d->ed.blob_cap) {
+      if (d->ed.d_blob) (void)hipFree(d->ed.d_blob);
+      d->ed.blob_cap = round_up(nb, 1 << 20);
+      if (hipMalloc(&d->ed.d_blob, d->ed.blob_cap) != hipSuccess) { d->ed.d_blob = nullptr; d->ed.blob_cap = 0; return GV_ENOMEM; }
+    }
+    if (!d->ed.d_blob) {
+      d->ed.blob_cap = 1 << 20;
+      if (hipMalloc(&d->ed.d_blob, d->ed.blob_cap) != hipSuccess) { d->ed.d_blob = nullptr; d->ed.blob_cap = 0; return GV_ENOMEM; }
+    }
+    const CopySeg segs[2] = {CopySeg{h, hb.pub32 + c0 * 32, cn * 32}, CopySeg{h + L.sig, hb.sig64 + c0 * 64, cn * 64}};
+    par_copy_segs(d->pool, segs, 2);
+    uint64_t* ro = (uint64_t*)(h + L.off);
+    for (size_t i = 0; i < cn; ++i) ro[i] = hb.off[c0 + i] - lo_b;
+    memcpy(h + L.len, hb.len + c0, cn * 4);
+    if (nb) par_copy(d->pool, d->ed.h_blob, hb.blob + lo_b, nb);
+    CK(hipMemcpyAsync(d->ed.d_in, h, L.total, hipMemcpyHostToDevice, st));
+    if (nb) CK(hipMemcpyAsync(d->ed.d_blob, d->ed.h_blob, nb, hipMemcpyHostToDevice, st));
+    const uint8_t* din = d->ed.d_in;
+    rc = ed_launch(ctx->time_kernels, d, cn, din, din + L.sig, d->ed.d_blob, (const uint64_t*)(din + L.off),
+                   (const uint32_t*)(din + L.len), d->ed.bits, st);
+    if (rc) return rc;
+    CK(hipMemcpyAsync(d->ed.h_bits, d->ed.bits, ((cn + 63) / 64) * 8, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    const uint64_t* w = (const uint64_t*)d->ed.h_bits;
+    for (size_t i = 0; i < cn; ++i) hb.out_ok[c0 + i] = (uint8_t)((w[i >> 6] >> (i & 63)) & 1u);
+  }
+  return GV_OK;
+}
+
+int run_ed_host(gv_ctx* ctx, size_t n, const EdHost& hb) {
+  if (!ctx) return GV_EINVAL;
+  if (ctx->fault_inject) return GV_EFAULT;
+  if (n == 0) return GV_OK;
+  if (!hb.pub32 || !hb.sig64 || !hb.off || !hb.len || !hb.out_ok) return GV_EINVAL;
+  for (size_t i = 0; i < n; ++i)
+    if (hb.len[i] && !hb.blob) return GV_EINVAL;
+  const size_t nd = ctx->devs.size();
+  const size_t per = round_up((n + nd - 1) / nd, 256);
+  std::vector<int> rcs(nd, GV_OK);
+  std::vector<bool> posted(nd, false);
+  for (size_t k = 1; k < nd; ++k) {
+    const size_t lo = std::min(n, k * per), hi = std::min(n, (k + 1) * per);
+    if (lo >= hi) continue;
+    Dev* d = ctx->devs[k];
+    d->worker->post([=, &hb]() { return ed_slice(ctx, d, lo, hi, hb); });
+    posted[k] = true;
+  }
+  rcs[0] = ed_slice(ctx, ctx->devs[0], 0, std::min(n, per), hb);
+  for (size_t k = 1; k < nd; ++k)
+    if (posted[k]) rcs[k] = ctx->devs[k]->worker->wait();
+  for (int rc : rcs) if (rc) return rc;
+  return GV_OK;
+}
+
 int run_host(gv_ctx* ctx, size_t n, const HostBatch& hb) {
   if (!ctx) return GV_EINVAL;
   if (ctx->fault_inject) return GV_EFAULT;
@@ -640,6 +814,15 @@ void gv_close(gv_ctx* ctx) {
     if (d->kqt) (void)hipFree(d->kqt);
     if (d->kzq) (void)hipFree(d->kzq);
     if (d->kok) (void)hipFree(d->kok);
+    if (d->edtab) (void)hipFree(d->edtab);
+    if (d->ed.d_in) (void)hipFree(d->ed.d_in);
+    if (d->ed.atab) (void)hipFree(d->ed.atab);
+    if (d->ed.bits) (void)hipFree(d->ed.bits);
+    if (d->ed.d_blob) (void)hipFree(d->ed.d_blob);
+    if (d->ed.h_in) (void)hipHostFree(d->ed.h_in);
+    if (d->ed.h_blob) (void)hipHostFree(d->ed.h_blob);
+    if (d->ed.h_bits) (void)hipHostFree(d->ed.h_bits);
+    if (d->ed.last) (void)hipEventDestroy(d->ed.last);
     for (auto& rs : d->ring)
       for (auto e : rs) if (e) (void)hipEventDestroy(e);
     delete d->pool;
@@ -713,6 +896,27 @@ int gv_dev_verify_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub33,
   return launch(ctx, d, &d->set[0], n, (const uint8_t*)d_pub33, (const uint8_t*)d_sig64, nullptr,
                 (const uint8_t*)d_msg_blob, (const uint64_t*)d_msg_off, (const uint32_t*)d_msg_len,
                 (uint64_t*)d_bits, st);
+}
+
+// ---- ed25519
+int gv_verify_ed25519_msgs(gv_ctx* ctx, size_t n, const uint8_t* pub32, const uint8_t* sig64,
+                           const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len,
+                           uint8_t* out_ok) {
+  return run_ed_host(ctx, n, EdHost{pub32, sig64, msg_blob, msg_off, msg_len, out_ok});
+}
+
+int gv_dev_verify_ed25519_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub32, const void* d_sig64,
+                               const void* d_msg_blob, const void* d_msg_off, const void* d_msg_len, void* d_bits,
+                               void* stream) {
+  Dev* d = nullptr;
+  int rc = dev_common(ctx, dev_slot, n, d_pub32, d_sig64, d_bits, &d);
+  if (rc || n == 0) return rc;
+  if (!d_msg_off || !d_msg_len || ((uintptr_t)d_pub32 & 15) || ((uintptr_t)d_sig64 & 15)) return GV_EINVAL;
+  std::lock_guard<std::mutex> lk(d->mu);
+  CK(hipSetDevice(d->id));
+  hipStream_t st = stream ? (hipStream_t)stream : d->set[0].st;
+  return ed_launch(ctx->time_kernels, d, n, (const uint8_t*)d_pub32, (const uint8_t*)d_sig64, (const uint8_t*)d_msg_blob,
+                   (const uint64_t*)d_msg_off, (const uint32_t*)d_msg_len, (uint64_t*)d_bits, st);
 }
 
 // ---- key arena

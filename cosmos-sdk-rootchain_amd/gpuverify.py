@@ -35,6 +35,7 @@ EXPORTED_SYMBOLS = (
     "gv_dev_copy", "gv_dev_sync", "gv_stage_stats", "gv_keys_load", "gv_keys_reset", "gv_keys_count",
     "gv_verify_digests_keyed", "gv_verify_msgs_keyed", "gv_dev_verify_digests_keyed", "gv_stage_stats4",
     "gv_keys_point", "gv_dev_stream_create", "gv_dev_stream_sync", "gv_dev_stream_destroy",
+    "gv_verify_ed25519_msgs", "gv_dev_verify_ed25519_msgs",
 )
 
 
@@ -80,6 +81,10 @@ def load(path: str = LIB_PATH):
     L.gv_dev_verify_digests.restype = i32
     L.gv_dev_verify_msgs.argtypes = [vp, i32, sz, vp, vp, vp, vp, vp, vp, vp]
     L.gv_dev_verify_msgs.restype = i32
+    L.gv_verify_ed25519_msgs.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp]
+    L.gv_verify_ed25519_msgs.restype = i32
+    L.gv_dev_verify_ed25519_msgs.argtypes = [vp, i32, sz, vp, vp, vp, vp, vp, vp, vp]
+    L.gv_dev_verify_ed25519_msgs.restype = i32
     L.gv_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_longlong]
     L.gv_set_option.restype = i32
     L.gv_last_stage_ms.argtypes = [vp, i32] + [ctypes.POINTER(ctypes.c_float)] * 3
@@ -285,6 +290,29 @@ class Verifier:
                                           ctypes.c_void_p(d_blob), ctypes.c_void_p(d_off), ctypes.c_void_p(d_len),
                                           ctypes.c_void_p(d_bits), ctypes.c_void_p(stream or 0)),
                "gv_dev_verify_msgs")
+
+    # ---- ed25519
+    def verify_batch_ed25519(self, pub32: np.ndarray, sig64: np.ndarray, msgs) -> np.ndarray:
+        """out[i] = PubKeyEd25519(pub32[i]).VerifyBytes(msg_i, sig64[i]); msgs: list[bytes] or
+        a (blob, off, len) triple."""
+        pub32, sig64 = (np.ascontiguousarray(a, dtype=np.uint8) for a in (pub32, sig64))
+        blob, off, ln = pack_msgs(msgs) if isinstance(msgs, (list, tuple)) and (
+            len(msgs) == 0 or isinstance(msgs[0], (bytes, bytearray))) else msgs
+        n = pub32.shape[0]
+        assert pub32.shape == (n, 32) and sig64.shape == (n, 64) and len(off) == n and len(ln) == n
+        out = np.zeros(n, dtype=np.uint8)
+        if n:
+            _check(self._L.gv_verify_ed25519_msgs(self._ctx, n, _ptr(pub32), _ptr(sig64), _ptr(blob),
+                                                  _ptr(np.ascontiguousarray(off, dtype=np.uint64)),
+                                                  _ptr(np.ascontiguousarray(ln, dtype=np.uint32)), _ptr(out)),
+                   "gv_verify_ed25519_msgs")
+        return out
+
+    def dev_verify_ed25519(self, slot: int, n: int, d_pub, d_sig, d_blob, d_off, d_len, d_bits, stream=None):
+        _check(self._L.gv_dev_verify_ed25519_msgs(self._ctx, slot, n, ctypes.c_void_p(d_pub), ctypes.c_void_p(d_sig),
+                                                  ctypes.c_void_p(d_blob), ctypes.c_void_p(d_off),
+                                                  ctypes.c_void_p(d_len), ctypes.c_void_p(d_bits),
+                                                  ctypes.c_void_p(stream or 0)), "gv_dev_verify_ed25519_msgs")
 
     def last_stage_ms(self, slot: int = 0):
         a, b, c = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()

@@ -140,6 +140,26 @@ int gv_verify_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint
 int gv_dev_verify_digests_keyed(gv_ctx* ctx, int dev_slot, size_t n, const void* d_slot, const void* d_sig64,
                                 const void* d_dig32, void* d_bits, void* stream);
 
+/* ---- ed25519 ------------------------------------------
+ * out_ok[i] = tendermint v0.33.4 PubKeyEd25519(pub32[i]).VerifyBytes(msg_i,
+ * sig64[i]) for a 64-byte signature, i.e. go1.14 crypto/ed25519 Verify:
+ * sig[63] & 224 == 0, S < L (ScMinimal), A = FromBytes(pub) (non-canonical y
+ * accepted, no small-order check), encode([S]B - [SHA-512(R||A||M) mod L]A)
+ * == R as bytes.  Replaces, for a batch, the per-leaf call reached through
+ * multisig.PubKeyMultisigThreshold.VerifyBytes for ed25519 sub-keys
+ * (x/auth/ante/sigverify.go:210 via :303-306 / :325-338).  Signatures of any
+ * other length are false without a call (VerifyBytes' first check), as for
+ * secp256k1.  msg_blob may be NULL when every length is 0. */
+int gv_verify_ed25519_msgs(gv_ctx* ctx, size_t n, const uint8_t* pub32, const uint8_t* sig64,
+                           const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len,
+                           uint8_t* out_ok);
+/* Device-resident: d_pub32 (n x 32) and d_sig64 (n x 64) 16-byte aligned,
+ * d_msg_off u64 / d_msg_len u32 per item; accept bitmap into d_bits
+ * (ceil(n/64) u64 words).  Asynchronous on `stream` (NULL: the library's). */
+int gv_dev_verify_ed25519_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub32, const void* d_sig64,
+                               const void* d_msg_blob, const void* d_msg_off, const void* d_msg_len, void* d_bits,
+                               void* stream);
+
 /* Options: "max_batch" (lanes per device launch, default 1<<20, at most
  * 0xFFFFFF00),
  * "lat_max" (batches of at most this many items -- per device slice -- take

@@ -1,0 +1,139 @@
+"""ed25519 VerifyBytes on the GPU (csrc/ed_verify.hip through the C ABI
+gv_verify_ed25519_msgs / gv_dev_verify_ed25519_msgs) against the committed
+golden vectors (verdicts of oracle/ed25519_ref.py, go1.14 crypto/ed25519
+semantics: non-canonical and small-order keys, S >= L, sig[63] & 224,
+non-canonical R), the RFC 8032 vectors, and OpenSSL on random batches."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import ed_openssl as OSSL
+import gpuverify as gvm
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def ver():
+    v = gvm.Verifier([0])
+    yield v
+    v.close()
+
+
+def arrays(items):
+    pub = np.array([np.frombuffer(p, np.uint8) for p, _, _ in items]).reshape(-1, 32)
+    sig = np.array([np.frombuffer(s, np.uint8) for _, _, s in items]).reshape(-1, 64)
+    return pub, sig, [m for _, m, _ in items]
+
+
+def golden():
+    g = json.load(open(os.path.join(GOLD, "ed25519_vectors.json")))
+    out = []
+    for cat, vs in g["categories"].items():
+        for v in vs:
+            out.append((cat, bytes.fromhex(v["pub"]), bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"]), v["ok"]))
+    return out
+
+
+def test_golden_vectors(ver):
+    gv = golden()
+    pub, sig, msgs = arrays([(p, m, s) for _, p, m, s, _ in gv])
+    got = ver.verify_batch_ed25519(pub, sig, msgs)
+    bad = [(c, ok) for (c, _, _, _, ok), g in zip(gv, got) if bool(g) != ok]
+    assert not bad, bad[:10]
+    assert int(got.sum()) == sum(ok for *_, ok in gv)
+
+
+def test_rfc8032(ver):
+    vs = json.load(open(os.path.join(GOLD, "ed25519_rfc8032.json")))["vectors"]
+    items = [(bytes.fromhex(v["pub"]), bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"])) for v in vs]
+    pub, sig, msgs = arrays(items)
+    assert ver.verify_batch_ed25519(pub, sig, msgs).all()
+    assert not ver.verify_batch_ed25519(pub, sig, [m + b"." for m in msgs]).any()
+
+
+def test_random_batch_vs_openssl(ver):
+    rng = random.Random(11)
+    seeds = [rng.randbytes(32) for _ in range(64)]
+    pubs = [OSSL.public_key(s) for s in seeds]
+    items, want = [], []
+    for i in range(6000):
+        k = i % 64
+        msg = rng.randbytes(rng.randrange(0, 420))
+        sig = OSSL.sign(seeds[k], msg)
+        r = rng.random()
+        if r < 0.1:
+            sig = bytearray(sig)
+            sig[rng.randrange(64)] ^= 1 << rng.randrange(8)
+            sig = bytes(sig)
+        elif r < 0.2:
+            msg = msg + b"\x01"
+        elif r < 0.25:                                       # S + L: malleated, rejected by ScMinimal
+            s = int.from_bytes(sig[32:], "little") + 2**252 + 27742317777372353535851937790883648493
+            if s < 2**253:
+                sig = sig[:32] + s.to_bytes(32, "little")
+        items.append((pubs[k], msg, sig))
+        want.append(OSSL.verify(pubs[k], msg, sig))
+    pub, sig, msgs = arrays(items)
+    got = ver.verify_batch_ed25519(pub, sig, msgs)
+    assert np.array_equal(got.astype(bool), np.array(want)), np.nonzero(got.astype(bool) != np.array(want))[0][:10]
+    assert 0.6 < got.mean() < 0.9
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 257])
+def test_ragged_sizes_and_empty_messages(ver, n):
+    rng = random.Random(n)
+    seed = rng.randbytes(32)
+    pub = OSSL.public_key(seed)
+    items = [(pub, b"", OSSL.sign(seed, b"")) for _ in range(n)]
+    p, s, _ = arrays(items)
+    z = np.zeros(n, np.uint64)
+    got = ver.verify_batch_ed25519(p, s, (np.zeros(1, np.uint8), z, z.astype(np.uint32)))
+    assert got.all()
+    assert ver.verify_batch_ed25519(p[:0], s[:0], []).shape == (0,)
+
+
+def test_chunked_batch_and_device_resident(ver):
+    """> 262,144 items: several chunks of the host path; the same batch
+    device-resident (gv_dev_verify_ed25519_msgs) gives the same bitmap."""
+    base = 2048
+    rng = random.Random(5)
+    seeds = [rng.randbytes(32) for _ in range(16)]
+    pubs = [OSSL.public_key(s) for s in seeds]
+    items, want = [], []
+    for i in range(base):
+        msg = rng.randbytes(rng.randrange(0, 200))
+        sig = OSSL.sign(seeds[i % 16], msg)
+        if i % 5 == 0:
+            msg += b"!"
+        items.append((pubs[i % 16], msg, sig))
+        want.append(i % 5 != 0)
+    reps = 150                                               # 307,200 items
+    pub, sig, msgs = arrays(items)
+    blob, off, ln = gvm.pack_msgs(msgs)
+    total = base * reps
+    P = np.tile(pub, (reps, 1))
+    S = np.tile(sig, (reps, 1))
+    O = (np.tile(off, reps) + np.repeat(np.arange(reps, dtype=np.uint64) * np.uint64(len(blob)), base)).astype(np.uint64)
+    Lh = np.tile(ln, reps)
+    Bl = np.tile(blob, reps)
+    W = np.tile(np.array(want), reps)
+    got = ver.verify_batch_ed25519(P, S, (Bl, O, Lh))
+    assert np.array_equal(got.astype(bool), W)
+    d = [ver.dev_alloc(a.nbytes) for a in (P, S, Bl, O, Lh)]
+    for ptr, a in zip(d, (P, S, Bl, O, Lh)):
+        ver.dev_upload(ptr, np.ascontiguousarray(a))
+    nw = (total + 63) // 64
+    d_bits = ver.dev_alloc(nw * 8)
+    ver.dev_verify_ed25519(0, total, d[0], d[1], d[2], d[3], d[4], d_bits)
+    ver.dev_sync()
+    bits = np.zeros(nw, np.uint64)
+    ver.dev_download(bits, d_bits)
+    dev = np.unpackbits(bits.view(np.uint8), bitorder="little")[:total].astype(bool)
+    assert np.array_equal(dev, W)
+    for ptr in d + [d_bits]:
+        ver.dev_free(ptr)
