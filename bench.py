@@ -468,6 +468,7 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
         ex["msg_path"] = X.msg_path(ver, workload_lib(), min(n, 500_000), args.threads)
         ex["c1_ante"] = X.c1_ante(ver)
         ex["c4_multisig"] = X.c4_multisig(ver, workload_lib(), threads=min(args.threads, 16))
+        ex["ed25519"] = X.ed25519(ver, workload_lib(), n=n, threads=args.threads, peak=P_MUL)
         log(f"extras in {time.perf_counter() - t:.1f}s")
         result["extras"] = ex
     ver.close()

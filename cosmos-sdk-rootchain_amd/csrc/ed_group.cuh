@@ -29,7 +29,7 @@ struct ge_pre { fe29 ypx, ymx, xy2d; };           // (y+x, y-x, 2dxy), affine, m
 
 #define ED_CACHED_WORDS 36                        // 4 fe x 9 limbs
 #define ED_PRE_WORDS 27                           // 3 fe x 9 limbs
-#define ED_ATAB_ENTRIES 8                         // j(-A), j = 1..8 (entry 0 = identity, not stored)
+#define ED_ATAB_ENTRIES 9                         // j(-A), j = 0..8 (entry 0 = the identity)
 #define ED_ATAB_WORDS (ED_ATAB_ENTRIES * ED_CACHED_WORDS)
 #define ED_BTAB_WINDOWS 32
 #define ED_BTAB_ENTRIES 129                       // j = 0..128
@@ -74,8 +74,10 @@ GV_DEV void ge_identity(ge_ext& r) {
 }
 
 // r = 2p (ref10 ge_p2_dbl + p1p1 -> p3).  p: X, Y magnitude 1, Z <= 2.
-// Every output magnitude 1.  T of p is not read.
-GV_DEV void ge_dbl(ge_ext& r, const ge_ext& p) {
+// Every output magnitude 1.  T of p is not read; T of r is computed only
+// when T_OUT (the next operation is an addition).
+template <bool T_OUT>
+GV_DEV void ge_dbl_t(ge_ext& r, const ge_ext& p) {
   fe29 xx, yy, b, a, aa, y1, z1, x1, t1;
   e29_sqr(xx, p.X);
   e29_sqr(yy, p.Y);
@@ -90,8 +92,9 @@ GV_DEV void ge_dbl(ge_ext& r, const ge_ext& p) {
   e29_mul(r.X, x1, t1);
   e29_mul(r.Y, y1, z1);
   e29_mul(r.Z, z1, t1);
-  e29_mul(r.T, x1, y1);
+  if (T_OUT) e29_mul(r.T, x1, y1);
 }
+GV_DEV void ge_dbl(ge_ext& r, const ge_ext& p) { ge_dbl_t<true>(r, p); }
 
 // r = p + (neg ? -q : q) with q in cached form (ref10 ge_add / ge_sub).
 // p magnitude 1; outputs magnitude 1.  r may alias p.
@@ -252,21 +255,84 @@ GV_DEV void pre_load(ge_pre& q, const u32* btab, int w, int j) {
   }
 }
 
-// Build the table of j(-A) (j = 1..8) for one lane.
+// Build the table of j(-A) (j = 0..8; entry 0 = the identity) for one lane.
 GV_DEV void atab_build(u32* tab, size_t stride, const ge_ext& negA) {
   ge_cached c1, c;
+  cached_identity(c);
+  atab_store(tab, stride, 0, c);
   ge_to_cached(c1, negA);
-  atab_store(tab, stride, 0, c1);
+  atab_store(tab, stride, 1, c1);
   ge_ext p2, acc;
   ge_dbl(p2, negA);
   ge_to_cached(c, p2);
-  atab_store(tab, stride, 1, c);
+  atab_store(tab, stride, 2, c);
   acc = p2;
   for (int j = 3; j <= 8; ++j) {
     ge_add_cached(acc, acc, c1, false);
     ge_to_cached(c, acc);
-    atab_store(tab, stride, j - 1, c);
+    atab_store(tab, stride, j, c);
   }
+}
+
+// Load one field element of 9 limbs, limb k at f[k * stride].
+GV_DEV void fe_load(fe29& r, const u32* f, size_t stride) {
+#pragma unroll
+  for (int k = 0; k < 9; ++k) r.n[k] = f[(size_t)k * stride];
+}
+
+// r = p + (neg ? -q : q), q = entry e of this lane's table, its field
+// elements loaded from memory right before use (the negation picks
+// addresses, not values).  r may alias p.  T of r only when T_OUT.
+template <bool T_OUT>
+GV_DEV void ge_add_tab(ge_ext& r, const ge_ext& p, const u32* tab, size_t stride, int e, bool neg) {
+  const u32* ent = tab + (size_t)(e * ED_CACHED_WORDS) * stride;
+  const u32* qa = ent + (size_t)(neg ? 9 : 0) * stride;          // Y+X  (neg: Y-X)
+  const u32* qb = ent + (size_t)(neg ? 0 : 9) * stride;
+  fe29 t, q, a, b, x1, y1, dpc, dmc, z1, t1;
+  f29_add(t, p.Y, p.X);
+  fe_load(q, qa, stride);
+  e29_mul(a, t, q);
+  e29_sub<1>(t, p.Y, p.X);
+  fe_load(q, qb, stride);
+  e29_mul(b, t, q);
+  e29_sub_norm<1>(x1, a, b);
+  f29_add(y1, a, b);
+  fe_load(q, ent + (size_t)27 * stride, stride);                  // 2dT
+  e29_mul(a, q, p.T);
+  fe_load(q, ent + (size_t)18 * stride, stride);                  // 2Z
+  e29_mul(b, p.Z, q);
+  f29_add(dpc, b, a);
+  e29_sub_norm<1>(dmc, b, a);
+  fe_select(z1, neg, dmc, dpc);
+  fe_select(t1, neg, dpc, dmc);
+  e29_mul(r.X, x1, t1);
+  e29_mul(r.Y, y1, z1);
+  e29_mul(r.Z, z1, t1);
+  if (T_OUT) e29_mul(r.T, x1, y1);
+}
+
+// r = p + (neg ? -q : q), q = a comb-table entry (27 contiguous words).
+GV_DEV void ge_add_pretab(ge_ext& r, const ge_ext& p, const u32* ent, bool neg) {
+  fe29 t, q, a, b, x1, y1, dpc, dmc, z1, t1;
+  f29_add(t, p.Y, p.X);
+  fe_load(q, ent + (neg ? 9 : 0), 1);
+  e29_mul(a, t, q);
+  e29_sub<1>(t, p.Y, p.X);
+  fe_load(q, ent + (neg ? 0 : 9), 1);
+  e29_mul(b, t, q);
+  e29_sub_norm<1>(x1, a, b);
+  f29_add(y1, a, b);
+  fe_load(q, ent + 18, 1);                                        // 2dxy
+  e29_mul(a, q, p.T);
+  f29_add(b, p.Z, p.Z);                                           // 2Z (mag 2)
+  f29_add(dpc, b, a);                                             // mag 3
+  e29_sub_norm<1>(dmc, b, a);
+  fe_select(z1, neg, dmc, dpc);
+  fe_select(t1, neg, dpc, dmc);
+  e29_mul(r.X, x1, t1);
+  e29_mul(r.Y, y1, z1);
+  e29_mul(r.Z, z1, t1);
+  e29_mul(r.T, x1, y1);
 }
 
 // Signed radix-16 recoding carries of h (< 2^253): bit i of the result = the
@@ -295,13 +361,12 @@ GV_DEV bool ed_ladder_check(const u32 h[8], const u32 s[8], const u32* tab, size
   for (int i = 0; i < 8; ++i) hs[i] = h[i];
   ge_ext acc;
   ge_identity(acc);
-  ge_cached q;
   for (int i = 63; i >= 0; --i) {
     if (i != 63) {
-      ge_dbl(acc, acc);
-      ge_dbl(acc, acc);
-      ge_dbl(acc, acc);
-      ge_dbl(acc, acc);
+      ge_dbl_t<false>(acc, acc);
+      ge_dbl_t<false>(acc, acc);
+      ge_dbl_t<false>(acc, acc);
+      ge_dbl_t<true>(acc, acc);
     }
     const int nib = (int)(hs[7] >> 28);
     const int cin = i > 0 ? (int)((carries >> (i - 1)) & 1u) : 0;
@@ -312,16 +377,14 @@ GV_DEV bool ed_ladder_check(const u32 h[8], const u32 s[8], const u32* tab, size
     for (int k = 7; k > 0; --k) hs[k] = (hs[k] << 4) | (hs[k - 1] >> 28);
     hs[0] <<= 4;
     const int mag = dgt < 0 ? -dgt : dgt;
-    if (mag == 0) cached_identity(q);
-    else atab_load(q, tab, stride, mag - 1);
-    ge_add_cached(acc, acc, q, dgt < 0);
+    if (i) ge_add_tab<false>(acc, acc, tab, stride, mag, dgt < 0);   // a doubling follows
+    else ge_add_tab<true>(acc, acc, tab, stride, mag, dgt < 0);      // the comb adds follow
   }
   // + [s]B: signed radix-256 digits, LSB-first, one precomputed add each
   u32 ss[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) ss[i] = s[i];
   int carry = 0;
-  ge_pre pq;
   for (int w = 0; w < ED_BTAB_WINDOWS; ++w) {
     int dgt = (int)(ss[0] & 0xFFu) + carry;
 #pragma unroll
@@ -330,8 +393,7 @@ GV_DEV bool ed_ladder_check(const u32 h[8], const u32 s[8], const u32* tab, size
     carry = dgt > 128 ? 1 : 0;
     dgt -= 256 * carry;
     const int mag = dgt < 0 ? -dgt : dgt;
-    pre_load(pq, btab, w, mag);
-    ge_add_pre(acc, acc, pq, dgt < 0);
+    ge_add_pretab(acc, acc, btab + (size_t)(w * ED_BTAB_ENTRIES + mag) * ED_PRE_WORDS, dgt < 0);
   }
   u32 ew[8];
   ge_tobytes(ew, acc);
@@ -373,30 +435,40 @@ GV_DEV void ed_btab_entry(u32 out[ED_PRE_WORDS], int w, int j) {
   }
 }
 
-// One item of go1.14 crypto/ed25519 Verify (64-byte signature): pw = the 32
-// key bytes as 8 little-endian words, sw = the signature as 16 words, msg(i)
-// = message byte i.  tab/stride: this item's j(-A) scratch; btab: the comb
-// table.
+// The per-item work before the ladder: h = SHA-512(R || A || M) mod L, the
+// S checks (sig[63] & 224 == 0, ScMinimal), FromBytes(A) and the table
+// j(-A).  Returns whether the item can still verify.
 template <class Msg>
-GV_DEV bool ed_verify_item(const u32 pw[8], const u32 sw[16], Msg msg, u32 len, u32* tab, size_t stride,
-                           const u32* btab) {
+GV_DEV bool ed_prep_item(const u32 pw[8], const u32 sw[16], Msg msg, u32 len, u32* tab, size_t stride,
+                         u32 h[8]) {
   u32 pre[16];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     pre[i] = sw[i];                     // R
     pre[8 + i] = pw[i];                 // A
   }
-  u32 dig[16], h[8];
+  u32 dig[16];
   sha512_pre64(dig, pre, msg, len);
   sc_reduce512(h, dig);                 // ScReduce
-  const u32* s = sw + 8;
-  const bool s_ok = (sw[15] >> 29) == 0 && sc_minimal(s);   // sig[63] & 224 == 0, ScMinimal
+  const bool s_ok = (sw[15] >> 29) == 0 && sc_minimal(sw + 8);   // sig[63] & 224 == 0, ScMinimal
   ge_ext a, na;
   const bool a_ok = ge_frombytes(a, pw);
   ge_neg(na, a);
   atab_build(tab, stride, na);
-  const bool r_ok = ed_ladder_check(h, s, tab, stride, btab, sw);
-  return s_ok && a_ok && r_ok;
+  return s_ok && a_ok;
+}
+
+// One item of go1.14 crypto/ed25519 Verify (64-byte signature): pw = the 32
+// key bytes as 8 little-endian words, sw = the signature as 16 words, msg(i)
+// = message byte i.  tab/stride: this item's j(-A) scratch; btab: the comb
+// table.  (The kernels run the two halves as two launches.)
+template <class Msg>
+GV_DEV bool ed_verify_item(const u32 pw[8], const u32 sw[16], Msg msg, u32 len, u32* tab, size_t stride,
+                           const u32* btab) {
+  u32 h[8];
+  const bool pre_ok = ed_prep_item(pw, sw, msg, len, tab, stride, h);
+  const bool r_ok = ed_ladder_check(h, sw + 8, tab, stride, btab, sw);
+  return pre_ok && r_ok;
 }
 
 }  // namespace ed

@@ -249,7 +249,7 @@ struct Dev {
   struct Ed {
     size_t cap = 0;                               // lanes
     uint8_t* d_in = nullptr;                      // pub32 | sig64 | off u64 | len u32 (ed_layout)
-    uint32_t* atab = nullptr;                     // GV_ED_ATAB_WORDS rows of cap words
+    uint32_t* atab = nullptr;                     // GV_ED_ROWS rows of cap words
     uint64_t* bits = nullptr;
     uint8_t* d_blob = nullptr;
     size_t blob_cap = 0;
@@ -370,7 +370,7 @@ int ed_ensure(Dev* d, size_t C, hipStream_t st) {
   if (d->ed.bits) (void)hipFree(d->ed.bits);
   d->ed.d_in = nullptr; d->ed.atab = nullptr; d->ed.bits = nullptr; d->ed.cap = 0;
   if (hipMalloc(&d->ed.d_in, ed_layout(C).total) != hipSuccess ||
-      hipMalloc(&d->ed.atab, C * (size_t)GV_ED_ATAB_WORDS * 4) != hipSuccess ||
+      hipMalloc(&d->ed.atab, C * (size_t)GV_ED_ROWS * 4) != hipSuccess ||
       hipMalloc(&d->ed.bits, C / 8) != hipSuccess)
     return GV_ENOMEM;
   d->ed.cap = C;

@@ -751,17 +751,6 @@ Addr pubkey_address(const PubKey& pk) {
   return a;
 }
 
-bool ed25519_verify(const std::array<uint8_t, 32>& pub, const uint8_t* msg, size_t msg_len, Span sig) {
-  if (sig.n != 64) return false;
-  EVP_PKEY* k = EVP_PKEY_new_raw_public_key(EVP_PKEY_ED25519, nullptr, pub.data(), 32);
-  if (!k) return false;
-  EVP_MD_CTX* c = EVP_MD_CTX_new();
-  bool ok = c && EVP_DigestVerifyInit(c, nullptr, nullptr, nullptr, k) == 1 &&
-            EVP_DigestVerify(c, sig.p, sig.n, msg, msg_len) == 1;
-  EVP_MD_CTX_free(c);
-  EVP_PKEY_free(k);
-  return ok;
-}
 
 // tendermint libs/bits CompactBitArray + crypto/multisig Multisignature
 struct CompactBitArray {
@@ -897,6 +886,7 @@ struct Leaf {
   H32 dig{};                              // SHA256(signBytes)
   H32 key{};                              // verdict-cache key
   int verdict = -1;
+  std::shared_ptr<const std::string> msg; // ed25519: the sign bytes (SHA-512 runs over them)
 };
 void leaf_key(Leaf& L) {
   Sha256 h;
@@ -1410,8 +1400,8 @@ std::string sign_bytes(const Tx& tx, const std::string& chain_json, uint64_t acc
 }
 
 // Build a signer's plan: gas charge, sign bytes digest, leaves + keys.
-// ed25519 leaves need the sign bytes themselves (SHA-512 over them): verified
-// here on the CPU (OpenSSL), their verdict cached like the secp256k1 ones.
+// ed25519 leaves keep the sign bytes themselves (the GPU's SHA-512 runs over
+// them); every leaf is then decided by the cache or a GPU batch in resolve().
 void make_plan(SignerPlan& p, gvh_app* app, const Tx& tx, size_t signer, std::shared_ptr<const PubInfo> pub,
                uint64_t accnum, uint64_t seq, const std::string& chain_json) {
   p.accnum = accnum;
@@ -1432,16 +1422,9 @@ void make_plan(SignerPlan& p, gvh_app* app, const Tx& tx, size_t signer, std::sh
   bool has_ed = false;
   for (const Leaf& L : p.leaves) has_ed = has_ed || L.kind;
   if (has_ed) {
-    const std::string sb = sign_bytes(tx, chain_json, accnum, seq);
-    for (Leaf& L : p.leaves) {
-      if (!L.kind) continue;
-      const int v = app->cache.get(L.key);
-      if (v >= 0) { L.verdict = v; continue; }
-      std::array<uint8_t, 32> ed;
-      memcpy(ed.data(), L.pub.data(), 32);
-      L.verdict = ed25519_verify(ed, (const uint8_t*)sb.data(), sb.size(), Span{L.sig.data(), 64}) ? 1 : 0;
-      app->cache.put(L.key, L.verdict == 1);
-    }
+    auto sb = std::make_shared<const std::string>(sign_bytes(tx, chain_json, accnum, seq));
+    for (Leaf& L : p.leaves)
+      if (L.kind) L.msg = sb;
   }
   p.ok = true;
 }
@@ -1462,7 +1445,7 @@ int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint
     if (hits) *hits += (uint32_t)(leaves.size() - miss.size());
   } else {
     for (Leaf* L : leaves) {
-      if (L->verdict >= 0) { if (hits) ++*hits; continue; }   // ed25519 leaves were decided in make_plan
+      if (L->verdict >= 0) { if (hits) ++*hits; continue; }
       const int v = app->cache.get(L->key);
       if (v >= 0) { L->verdict = v; if (hits) ++*hits; }
       else miss.push_back(L);
@@ -1472,7 +1455,6 @@ int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint
   app->st_misses += miss.size();
   if (miss.empty()) return GVH_OK;
   if (!app->gpu) return GVH_ENOVERIFIER;
-  const size_t m = miss.size();
   const bool prof = getenv("GVH_PROFILE") != nullptr;
   auto tr = std::chrono::steady_clock::now();
   auto rlap = [&](const char* what) {
@@ -1481,29 +1463,58 @@ int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint
     fprintf(stderr, "resolve %s %.3f ms\n", what, std::chrono::duration<double, std::milli>(t - tr).count());
     tr = t;
   };
+  // secp256k1 misses -> gv_verify_digests, ed25519 misses -> gv_verify_ed25519_msgs
+  std::vector<Leaf*> ed;
+  {
+    size_t k = 0;
+    for (Leaf* L : miss) {
+      if (L->kind) ed.push_back(L);
+      else miss[k++] = L;
+    }
+    miss.resize(k);
+  }
+  const size_t m = miss.size();
   std::vector<uint8_t> pub(m * 33), sig(m * 64), dig(m * 32), ok(m);
   parallel_for(app, m, [&](size_t k) {
     memcpy(&pub[k * 33], miss[k]->pub.data(), 33);
     memcpy(&sig[k * 64], miss[k]->sig.data(), 64);
     memcpy(&dig[k * 32], miss[k]->dig.data(), 32);
   });
+  const size_t me = ed.size();
+  std::vector<uint8_t> epub(me * 32), esig(me * 64), eok(me), eblob;
+  std::vector<uint64_t> eoff(me);
+  std::vector<uint32_t> elen(me);
+  for (size_t k = 0; k < me; ++k) {
+    memcpy(&epub[k * 32], ed[k]->pub.data(), 32);
+    memcpy(&esig[k * 64], ed[k]->sig.data(), 64);
+    eoff[k] = eblob.size();
+    elen[k] = (uint32_t)ed[k]->msg->size();
+    eblob.insert(eblob.end(), ed[k]->msg->begin(), ed[k]->msg->end());
+  }
   {
     std::lock_guard<std::mutex> g(app->gpu_mu);
     rlap("pack");
-    if (gv_verify_digests(app->gpu, m, pub.data(), sig.data(), dig.data(), ok.data()) != GV_OK) return GVH_EDEVICE;
-    rlap("gv_verify_digests");
+    if (m && gv_verify_digests(app->gpu, m, pub.data(), sig.data(), dig.data(), ok.data()) != GV_OK)
+      return GVH_EDEVICE;
+    if (me && gv_verify_ed25519_msgs(app->gpu, me, epub.data(), esig.data(), eblob.empty() ? nullptr : eblob.data(),
+                                     eoff.data(), elen.data(), eok.data()) != GV_OK)
+      return GVH_EDEVICE;
+    rlap("gv_verify");
   }
-  app->st_gpu_calls += 1;
-  app->st_gpu_leaves += m;
+  app->st_gpu_calls += (m ? 1 : 0) + (me ? 1 : 0);
+  app->st_gpu_leaves += m + me;
+  for (size_t k = 0; k < me; ++k) miss.push_back(ed[k]);
+  ok.insert(ok.end(), eok.begin(), eok.end());
+  const size_t mt = miss.size();
   if (fill)
-    parallel_for(app, m, [&](size_t k) {
+    parallel_for(app, mt, [&](size_t k) {
       miss[k]->verdict = ok[k];
       app->cache.put(miss[k]->key, ok[k] != 0);
     });
   else
-    for (size_t k = 0; k < m; ++k) miss[k]->verdict = ok[k];
+    for (size_t k = 0; k < mt; ++k) miss[k]->verdict = ok[k];
   rlap("put");
-  if (gpu_leaves) *gpu_leaves += (uint32_t)m;
+  if (gpu_leaves) *gpu_leaves += (uint32_t)mt;
   return GVH_OK;
 }
 

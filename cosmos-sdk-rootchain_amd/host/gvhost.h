@@ -30,10 +30,11 @@
  * Transactions are the amino binary StdTx bytes a node receives (DeliverTx /
  * CheckTx req.Tx).  A tx that does not decode gets code 2 (ErrTxDecode).
  *
- * No CPU fallback for secp256k1: if the GPU batch fails the decorator
- * returns GVH_EDEVICE and the caller (the Go shim) re-verifies with the
- * reference VerifyBytes (fail closed).  ed25519 multisig leaves are verified
- * on the CPU, as in the reference.
+ * No CPU fallback: every secp256k1 leaf goes to gv_verify_digests and every
+ * ed25519 multisig sub-key leaf to gv_verify_ed25519_msgs (one batch each per
+ * resolve); if a GPU batch fails the decorator returns GVH_EDEVICE and the
+ * caller (the Go shim) re-verifies with the reference VerifyBytes (fail
+ * closed).
  */
 #ifndef GVHOST_H
 #define GVHOST_H

@@ -17,6 +17,9 @@
                   call per tx), host buffers / PCIe included.
   c4_multisig     BASELINE.json configs[3] shape on one GPU: k-of-n multisig
                   MsgSend txs replayed in blocks through PreVerifyTxs + ante.
+  c2_hostpath     C2 through the host-buffer entry points (PCIe included).
+  ed25519         SURVEY.md §8f-4: ed25519 VerifyBytes, device-resident, with
+                  its own roofline line and OpenSSL all-core beside it.
 
 Nothing here touches oracle/: verdicts come from construction (the workload
 signs valid items with OpenSSL and mutates the invalid ones).
@@ -383,3 +386,77 @@ def c4_multisig(ver, wl, block: int = 10000, threads: int = 16, n_accounts: int 
             "workload_gen_s": round(t_gen, 1), "host_threads": threads,
             "note": "2-of-3 / 3-of-5 / 4-of-7 threshold accounts (30k), first k bits set, every tx valid by "
                     "construction; amino StdTx bytes through the host mirror, host buffers"}
+
+
+# ed25519 work per verify, same basis as bench.py's W (field mul 72, square 44
+# 32x32 products): FromBytes 254S + 20M, table j(-A) 4S + 60M, 252 doublings
+# (4S + 4M) + 64 cached adds (8M), 32 comb adds (7M), encode 254S + 13M.
+ED_FS, ED_FM = 1520, 1837
+W_ED25519 = ED_FS * 44 + ED_FM * 72          # 199,144
+
+
+def ed25519(ver, wl, n: int = 1_000_000, threads: int = 16, steps: int = 3, nkeys: int = 4096,
+            cpu_sample: int = 100_000, peak: float = 3.7469e13):
+    """ed25519 VerifyBytes (multisig ed25519 sub-keys) on n
+    ~350-byte messages, 1/8 with a corrupted R byte, device-resident through
+    gv_dev_verify_ed25519_msgs; the bitmap checked against construction;
+    OpenSSL all-core on a sample beside it."""
+    import ctypes as C
+    rng = np.random.default_rng(0xED)
+    lens = rng.integers(300, 400, size=n, dtype=np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    blob = rng.integers(0, 256, size=int(lens.sum()), dtype=np.uint8)
+    seeds = rng.integers(0, 256, size=(nkeys, 32), dtype=np.uint8)
+    pub = np.zeros((n, 32), np.uint8)
+    sig = np.zeros((n, 64), np.uint8)
+    vp = C.c_void_p
+    wl.gvw_ed25519_sign.argtypes = [C.c_size_t, C.c_size_t, vp, vp, vp, vp, vp, vp, C.c_int]
+    wl.gvw_ed25519_verify.argtypes = [C.c_size_t, vp, vp, vp, vp, vp, vp, C.c_int]
+    t = time.perf_counter()
+    rc = wl.gvw_ed25519_sign(n, nkeys, seeds.ctypes.data, blob.ctypes.data, off.ctypes.data, lens.ctypes.data,
+                             pub.ctypes.data, sig.ctypes.data, threads)
+    assert rc == 0
+    t_gen = time.perf_counter() - t
+    bad = rng.random(n) < 0.125
+    sig[bad, 5] ^= 0x40                           # R no longer the encoding of [S]B - [h]A
+    exp = ~bad
+    d = [ver.dev_alloc(a.nbytes) for a in (pub, sig, blob, off, lens)]
+    for p, a in zip(d, (pub, sig, blob, off, lens)):
+        ver.dev_upload(p, a)
+    nw = (n + 63) // 64
+    d_bits = ver.dev_alloc(nw * 8)
+    run = lambda: ver.dev_verify_ed25519(0, n, d[0], d[1], d[2], d[3], d[4], d_bits)  # noqa: E731
+    run()
+    ver.dev_sync()
+    ver.set_option("time_kernels", 1)
+    ver.stage_stats4()
+    t = time.perf_counter()
+    for _ in range(steps):
+        run()
+    ver.dev_sync()
+    el = time.perf_counter() - t
+    cnt, ms = ver.stage_stats4()
+    ver.set_option("time_kernels", 0)
+    bits = np.zeros(nw, np.uint64)
+    ver.dev_download(bits, d_bits)
+    got = _unpack_bits(bits, n).astype(bool)
+    for p in d + [d_bits]:
+        ver.dev_free(p)
+    kms = ms[3]
+    achieved = n * W_ED25519 / (kms * 1e-3) if kms > 0 else 0.0
+    m = min(cpu_sample, n)
+    out = np.zeros(m, np.uint8)
+    t = time.perf_counter()
+    wl.gvw_ed25519_verify(m, pub.ctypes.data, sig.ctypes.data, blob.ctypes.data, off.ctypes.data, lens.ctypes.data,
+                          out.ctypes.data, threads)
+    cpu_rate = m / (time.perf_counter() - t)
+    cpu_mism = int(np.count_nonzero(out.astype(bool) != exp[:m]))
+    return {"items": n, "mean_msg_bytes": round(float(lens.mean()), 1), "value": round(n * steps / el, 1),
+            "unit": "ed25519 verifies/s", "mismatches": int(np.count_nonzero(got != exp)),
+            "rejects_expected": int(bad.sum()), "kernel_ms": round(kms, 4), "launches_averaged": cnt,
+            "roofline": {"kernel": "k_ed_verify", "work_per_verify": W_ED25519, "achieved_T": round(achieved / 1e12, 3),
+                         "peak_T": round(peak / 1e12, 3), "frac": round(achieved / peak, 4) if achieved else None},
+            "cpu_openssl": {"value": round(cpu_rate, 1), "threads": threads, "sample": m, "mismatches": cpu_mism},
+            "workload_gen_s": round(t_gen, 2),
+            "note": "device-resident (inputs in HBM); keys = 4,096 RFC 8032 seeds round-robin; OpenSSL Ed25519 signs"}
