@@ -234,7 +234,8 @@ def test_multi_signer_and_first_failure_order(ver):
 
 @pytest.mark.gpu
 def test_multisig_k_of_n(ver):
-    """tendermint multisig threshold verification, fanned out into GPU leaves."""
+    """tendermint multisig threshold verification, fanned out into GPU leaves
+    (secp256k1 and ed25519 sub-keys)."""
     app = new_app(ver)
     subs = [KEYS[0], KEYS[1], KEYS[2], KEYS[3], KEYS[4]]
     ed_seed, ed_pub = T.ed25519_keypair(b"\x11" * 32)
@@ -248,7 +249,8 @@ def test_multisig_k_of_n(ver):
     sigs = [subs[0].sign(sb), subs[2].sign(sb), subs[4].sign(sb), T.ed25519_sign(ed_seed, sb)]
     tx = T.std_tx(msgs, FEE, "", [(mk, T.multisignature(bits, sigs))])
     rc, r = app.ante(tx)
-    assert rc == 0 and r["code"] == 0 and r["gpu_leaves"] == 3 and r["gas_used"] == 3 * 1000 + 590
+    # 3 secp256k1 leaves + 1 ed25519 leaf, all on the GPU (gv_verify_ed25519_msgs for the ed25519 one)
+    assert rc == 0 and r["code"] == 0 and r["gpu_leaves"] == 4 and r["gas_used"] == 3 * 1000 + 590
     # one bad secp256k1 leaf -> whole multisig false
     sb1 = T.std_sign_bytes("gv-test", 40, 1, FEE, msgs, "")
     bad = [subs[0].sign(sb1), subs[1].sign(sb1), subs[4].sign(sb1), T.ed25519_sign(ed_seed, sb1)]

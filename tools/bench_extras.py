@@ -389,10 +389,12 @@ def c4_multisig(ver, wl, block: int = 10000, threads: int = 16, n_accounts: int 
 
 
 # ed25519 work per verify, same basis as bench.py's W (field mul 72, square 44
-# 32x32 products): FromBytes 254S + 20M, table j(-A) 4S + 60M, 252 doublings
-# (4S + 4M) + 64 cached adds (8M), 32 comb adds (7M), encode 254S + 13M.
-ED_FS, ED_FM = 1520, 1837
-W_ED25519 = ED_FS * 44 + ED_FM * 72          # 199,144
+# 32x32 products), as k_ed_prep + k_ed_ladder compute it: FromBytes 254S +
+# 20M, table j(-A) 4S + 60M, 252 doublings (4S + 3M; 4M for the 63 that feed
+# an add), 64 table adds (7M; 8M for the last), 32 comb adds (8M), encode
+# 254S + 13M.
+ED_FS, ED_FM = 1520, 1585
+W_ED25519 = ED_FS * 44 + ED_FM * 72          # 181,000
 
 
 def ed25519(ver, wl, n: int = 1_000_000, threads: int = 16, steps: int = 3, nkeys: int = 4096,
