@@ -29,6 +29,7 @@ import (
 	"sync"
 	"unsafe"
 
+	"github.com/tendermint/tendermint/crypto/ed25519"
 	"github.com/tendermint/tendermint/crypto/secp256k1"
 )
 
@@ -42,9 +43,25 @@ type Verifier interface {
 	VerifyBatch(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]byte) []bool
 }
 
+// EdVerifier verifies a batch of ed25519 leaves (multisig sub-keys):
+// ok[i] == pubs[i].VerifyBytes(msgs[i], sigs[i]).
+type EdVerifier interface {
+	VerifyBatchEd25519(pubs []ed25519.PubKeyEd25519, msgs, sigs [][]byte) []bool
+}
+
 // CPU is the reference path, one VerifyBytes per leaf (tendermint
-// secp256k1_nocgo.go).  It is the fallback of GPU and a Verifier of its own.
+// secp256k1_nocgo.go, ed25519.go).  It is the fallback of GPU and a Verifier
+// of its own.
 type CPU struct{}
+
+// VerifyBatchEd25519 implements EdVerifier.
+func (CPU) VerifyBatchEd25519(pubs []ed25519.PubKeyEd25519, msgs, sigs [][]byte) []bool {
+	ok := make([]bool, len(pubs))
+	for i := range pubs {
+		ok[i] = pubs[i].VerifyBytes(msgs[i], sigs[i])
+	}
+	return ok
+}
 
 // VerifyBatch implements Verifier.
 func (CPU) VerifyBatch(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]byte) []bool {
@@ -70,7 +87,11 @@ type GPU struct {
 	slots map[secp256k1.PubKeySecp256k1]uint32 // key -> key-arena slot (gv_keys_load)
 }
 
-var _ Verifier = (*GPU)(nil)
+var (
+	_ Verifier   = (*GPU)(nil)
+	_ EdVerifier = (*GPU)(nil)
+	_ EdVerifier = CPU{}
+)
 
 // Open binds the listed HIP devices (nil or empty = every visible device).
 func Open(devices []int) (*GPU, error) {
@@ -156,6 +177,52 @@ func (g *GPU) VerifyBatch(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]byte)
 		pos += copy(blob.b[pos:], msgs[i])
 	}
 	rc := C.gv_verify_msgs(g.ctx, C.size_t(m), (*C.uint8_t)(pub.p), (*C.uint8_t)(sig.p), (*C.uint8_t)(blob.p),
+		(*C.uint64_t)(off.p), (*C.uint32_t)(ln.p), (*C.uint8_t)(out.p))
+	for k, i := range idx {
+		if rc == 0 {
+			ok[i] = out.b[k] == 1
+		} else {
+			ok[i] = pubs[i].VerifyBytes(msgs[i], sigs[i]) // fail closed to the reference path
+		}
+	}
+	return ok
+}
+
+// VerifyBatchEd25519 implements EdVerifier with gv_verify_ed25519_msgs (go1.14
+// crypto/ed25519 semantics on the GPU).  Same fail-closed rule as VerifyBatch.
+func (g *GPU) VerifyBatchEd25519(pubs []ed25519.PubKeyEd25519, msgs, sigs [][]byte) []bool {
+	n := len(pubs)
+	ok := make([]bool, n)
+	idx := make([]int, 0, n)
+	total := 0
+	for i := range pubs {
+		if len(sigs[i]) == 64 { // VerifyBytes: len(sig) != SignatureSize -> false
+			idx = append(idx, i)
+			total += len(msgs[i])
+		}
+	}
+	if len(idx) == 0 {
+		return ok
+	}
+	if total+108*len(idx) > maxBatchBytes {
+		h := len(pubs) / 2
+		copy(ok, g.VerifyBatchEd25519(pubs[:h], msgs[:h], sigs[:h]))
+		copy(ok[h:], g.VerifyBatchEd25519(pubs[h:], msgs[h:], sigs[h:]))
+		return ok
+	}
+	m := len(idx)
+	pub, sig, blob, off, ln, out := newCBuf(32*m), newCBuf(64*m), newCBuf(total), newCBuf(8*m), newCBuf(4*m), newCBuf(m)
+	defer func() { pub.free(); sig.free(); blob.free(); off.free(); ln.free(); out.free() }()
+	o := (*[maxBatchBytes / 8]uint64)(off.p)[:m:m]
+	l := (*[maxBatchBytes / 4]uint32)(ln.p)[:m:m]
+	pos := 0
+	for k, i := range idx {
+		copy(pub.b[32*k:], pubs[i][:])
+		copy(sig.b[64*k:], sigs[i])
+		o[k], l[k] = uint64(pos), uint32(len(msgs[i]))
+		pos += copy(blob.b[pos:], msgs[i])
+	}
+	rc := C.gv_verify_ed25519_msgs(g.ctx, C.size_t(m), (*C.uint8_t)(pub.p), (*C.uint8_t)(sig.p), (*C.uint8_t)(blob.p),
 		(*C.uint64_t)(off.p), (*C.uint32_t)(ln.p), (*C.uint8_t)(out.p))
 	for k, i := range idx {
 		if rc == 0 {

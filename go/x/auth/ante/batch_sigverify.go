@@ -99,13 +99,14 @@ func (d BatchSigVerificationDecorator) AnteHandle(ctx sdk.Context, tx sdk.Tx, si
 
 // ---------------------------------------------------------------- leaves
 
-// expr is pk.VerifyBytes(msg, sig) as an expression over leaves:
-// a constant, one secp256k1 leaf, or the AND of a multisig's set bits.
+// expr is pk.VerifyBytes(msg, sig) as an expression over leaves: a
+// constant, one secp256k1 or ed25519 leaf, or the AND of a multisig's set bits.
 type expr struct {
-	konst bool
-	leaf  int // >= 0: index into batch.secp
-	and   []*expr
-	isAnd bool
+	konst  bool
+	leaf   int // >= 0: index into batch.pubs (secp256k1)
+	edLeaf int // >= 0: index into batch.ed (ed25519)
+	and    []*expr
+	isAnd  bool
 }
 
 func (e *expr) eval(b *batch) bool {
@@ -119,6 +120,8 @@ func (e *expr) eval(b *batch) bool {
 		return true
 	case e.leaf >= 0:
 		return b.ok[e.leaf]
+	case e.edLeaf >= 0:
+		return b.ed.ok[e.edLeaf]
 	default:
 		return e.konst
 	}
@@ -130,33 +133,41 @@ type batch struct {
 	sigs [][]byte
 	keys [][32]byte
 	ok   []bool
+	ed   edBatch
+}
+
+type edBatch struct {
+	pubs []ed25519.PubKeyEd25519
+	msgs [][]byte
+	sigs [][]byte
+	ok   []bool
 }
 
 // build mirrors the key types the reference verifies (sigverify.go:303-321):
-// secp256k1 leaves are batched; multisig (tendermint
+// secp256k1 and ed25519 leaves are batched; multisig (tendermint
 // multisig.PubKeyMultisigThreshold.VerifyBytes) fans out in bit order with
-// the same structural checks; ed25519 and any other key verify on the CPU.
+// the same structural checks; any other key type verifies on the CPU.
 func (b *batch) build(pk crypto.PubKey, msg, sig []byte) *expr {
 	switch p := pk.(type) {
 	case secp256k1.PubKeySecp256k1:
 		if len(sig) != 64 { // VerifyBytes' first check
-			return &expr{leaf: -1}
+			return &expr{leaf: -1, edLeaf: -1}
 		}
 		b.pubs = append(b.pubs, p)
 		b.msgs = append(b.msgs, msg)
 		b.sigs = append(b.sigs, sig)
-		return &expr{leaf: len(b.pubs) - 1}
+		return &expr{leaf: len(b.pubs) - 1, edLeaf: -1}
 	case multisig.PubKeyMultisigThreshold:
 		var ms multisig.Multisignature
 		if err := codec.Cdc.UnmarshalBinaryBare(sig, &ms); err != nil {
-			return &expr{leaf: -1}
+			return &expr{leaf: -1, edLeaf: -1}
 		}
 		size := ms.BitArray.Size()
 		if len(p.PubKeys) != size || len(ms.Sigs) < int(p.K) || len(ms.Sigs) > size ||
 			ms.BitArray.NumTrueBitsBefore(size) < int(p.K) {
-			return &expr{leaf: -1}
+			return &expr{leaf: -1, edLeaf: -1}
 		}
-		e := &expr{leaf: -1, isAnd: true}
+		e := &expr{leaf: -1, edLeaf: -1, isAnd: true}
 		j := 0
 		for i := 0; i < size; i++ {
 			if ms.BitArray.GetIndex(i) {
@@ -166,15 +177,23 @@ func (b *batch) build(pk crypto.PubKey, msg, sig []byte) *expr {
 		}
 		return e
 	case ed25519.PubKeyEd25519:
-		return &expr{leaf: -1, konst: p.VerifyBytes(msg, sig)}
+		if len(sig) != 64 { // VerifyBytes' first check
+			return &expr{leaf: -1, edLeaf: -1}
+		}
+		b.ed.pubs = append(b.ed.pubs, p)
+		b.ed.msgs = append(b.ed.msgs, msg)
+		b.ed.sigs = append(b.ed.sigs, sig)
+		return &expr{leaf: -1, edLeaf: len(b.ed.pubs) - 1}
 	default: // includes a nil sub-key: the method call panics exactly as in the reference
-		return &expr{leaf: -1, konst: pk.VerifyBytes(msg, sig)}
+		return &expr{leaf: -1, edLeaf: -1, konst: pk.VerifyBytes(msg, sig)}
 	}
 }
 
-// resolve answers every secp256k1 leaf: cache hits first, the misses in one
-// Verifier call, then the cache is filled.
+// resolve answers every leaf: cache hits first, the misses in one Verifier
+// call per key type (ed25519 through v's EdVerifier side when it has one),
+// then the cache is filled.
 func (b *batch) resolve(v gv.Verifier, cache *gv.VerdictCache) {
+	b.resolveEd(v, cache)
 	n := len(b.pubs)
 	b.ok = make([]bool, n)
 	b.keys = make([][32]byte, n)
@@ -203,6 +222,44 @@ func (b *batch) resolve(v gv.Verifier, cache *gv.VerdictCache) {
 		b.ok[i] = res[k]
 		if cache != nil {
 			cache.Put(b.keys[i], res[k])
+		}
+	}
+}
+
+func (b *batch) resolveEd(v gv.Verifier, cache *gv.VerdictCache) {
+	e := &b.ed
+	n := len(e.pubs)
+	e.ok = make([]bool, n)
+	keys := make([][32]byte, n)
+	var miss []int
+	for i := 0; i < n; i++ {
+		keys[i] = gv.LeafKey(gv.KindEd25519, e.pubs[i][:], e.sigs[i], e.msgs[i])
+		if cache != nil {
+			if ok, hit := cache.Get(keys[i]); hit {
+				e.ok[i] = ok
+				continue
+			}
+		}
+		miss = append(miss, i)
+	}
+	if len(miss) == 0 {
+		return
+	}
+	ev, isEd := v.(gv.EdVerifier)
+	if !isEd {
+		ev = gv.CPU{}
+	}
+	pubs := make([]ed25519.PubKeyEd25519, len(miss))
+	msgs := make([][]byte, len(miss))
+	sigs := make([][]byte, len(miss))
+	for k, i := range miss {
+		pubs[k], msgs[k], sigs[k] = e.pubs[i], e.msgs[i], e.sigs[i]
+	}
+	res := ev.VerifyBatchEd25519(pubs, msgs, sigs)
+	for k, i := range miss {
+		e.ok[i] = res[k]
+		if cache != nil {
+			cache.Put(keys[i], res[k])
 		}
 	}
 }
@@ -279,6 +336,9 @@ func NewPreVerifier(ak AccountKeeper, v gv.Verifier, cache *gv.VerdictCache) fun
 			all.pubs = append(all.pubs, p.pubs...)
 			all.msgs = append(all.msgs, p.msgs...)
 			all.sigs = append(all.sigs, p.sigs...)
+			all.ed.pubs = append(all.ed.pubs, p.ed.pubs...)
+			all.ed.msgs = append(all.ed.msgs, p.ed.msgs...)
+			all.ed.sigs = append(all.ed.sigs, p.ed.sigs...)
 		}
 		all.resolve(v, cache)
 	}
