@@ -466,7 +466,7 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
         ex["c2_unique_keys"] = X.c2_unique_keys(ver, make_digest_workload, n, args.threads)
         ex["c3_adversarial"] = X.c3_adversarial(ver, make_digest_workload, n, args.threads)
         ex["msg_path"] = X.msg_path(ver, workload_lib(), min(n, 500_000), args.threads)
-        ex["c1_ante"] = X.c1_ante(ver)
+        ex["c1_ante"] = X.c1_ante(ver, wl=workload_lib(), threads=min(args.threads, 16))
         ex["c4_multisig"] = X.c4_multisig(ver, workload_lib(), threads=min(args.threads, 16))
         ex["ed25519"] = X.ed25519(ver, workload_lib(), n=n, threads=args.threads, peak=P_MUL)
         log(f"extras in {time.perf_counter() - t:.1f}s")

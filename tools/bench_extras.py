@@ -206,27 +206,56 @@ def msg_path(ver, wl, n: int, threads: int, nkeys: int = 10000, steps: int = 3):
     return out
 
 
-def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: int = 64):
+def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: int = 64, steady_blocks: int = 4,
+            wl=None, threads: int = 16):
     """BASELINE.json configs[0] shape: 10k single-signer bank MsgSend txs (amino
     StdTx) through the host mirror: the block path (DeliverBlock = PreVerifyTxs,
-    one GPU batch, then the DeliverTx ante loop), the per-tx path with no
-    batching (one GPU call per tx) and the CheckTx accumulation window (txs
-    submitted from concurrent threads)."""
+    one GPU batch, then the DeliverTx ante loop) -- the first block (every
+    account's pubkey arrives in its tx: SetPubKey, cold caches) and
+    `steady_blocks` further blocks (sequences 1.., keys on the accounts) --
+    the per-tx path with no batching (one GPU call per tx) and the CheckTx
+    accumulation window (txs submitted from concurrent threads).  Sign bytes
+    and signatures come from tools/workload (C, OpenSSL); the amino tx bytes
+    from txkit."""
     import threading
     import gvhost
     import txkit as T
-    keys = []
-    for i in range(ntx + 1):
-        priv = T.privkey_from_secret(b"gv-c1-" + struct.pack("<Q", i))
-        amino = T.amino_secp(T.secp_pubkey(priv))
-        keys.append((priv, amino, T.address(amino)))
+    if wl is None:
+        import bench
+        wl = bench.workload_lib()
+    nk = ntx + 1
+    priv = np.zeros((nk, 32), np.uint8)
+    pubk = np.zeros((nk, 33), np.uint8)
+    wl.gvw_keys(nk, 0xC1, priv.ctypes.data, pubk.ctypes.data, threads)
+    amino = [T.amino_secp(pubk[i].tobytes()) for i in range(nk)]
+    addrs = [T.address(a) for a in amino]
+    keys = [(None, amino[i], addrs[i]) for i in range(nk)]
     fee = T.Fee([(0, "stake")], 1000000)
-    txs = []
-    for i in range(ntx):
-        priv, amino, addr = keys[i]
-        msgs = [T.MsgSend(addr, keys[i + 1][2], [(10, "foocoin")])]
-        sb = T.std_sign_bytes("gv-bench", i, 0, fee, msgs, "")
-        txs.append(T.std_tx(msgs, fee, "", [(amino, T.secp_sign(priv, sb))]))
+    wl.gvw_msgsend_signbytes.restype = ctypes.c_longlong
+    wl.gvw_msgsend_signbytes.argtypes = [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
+                                         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+    wl.gvw_sha256_msgs.argtypes = [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_void_p]
+
+    def block(seq):
+        cap = ntx * 512
+        blob = np.zeros(cap, np.uint8)
+        off = np.zeros(ntx, np.uint64)
+        ln = np.zeros(ntx, np.uint32)
+        assert wl.gvw_msgsend_signbytes(ntx, pubk.ctypes.data, nk, seq, blob.ctypes.data, cap, off.ctypes.data,
+                                        ln.ctypes.data) > 0
+        mdig = np.zeros((ntx, 32), np.uint8)
+        wl.gvw_sha256_msgs(ntx, blob.ctypes.data, off.ctypes.data, ln.ctypes.data, mdig.ctypes.data)
+        pub = np.zeros((ntx, 33), np.uint8)
+        sig = np.zeros((ntx, 64), np.uint8)
+        dig = np.zeros((ntx, 32), np.uint8)
+        exp = np.zeros(ntx, np.uint8)
+        wl.gvw_sign(ntx, 0xC1 + seq, nk, priv.ctypes.data, pubk.ctypes.data, None, mdig.ctypes.data, 0.0,
+                    pub.ctypes.data, sig.ctypes.data, dig.ctypes.data, exp.ctypes.data, threads)
+        return [T.std_tx([T.MsgSend(addrs[i], addrs[i + 1], [(10, "foocoin")])], fee, "",
+                         [(amino[i] if seq == 0 else b"", sig[i].tobytes())]) for i in range(ntx)]
+    txs = block(0)
+    later = [block(seq) for seq in range(1, steady_blocks + 1)]
 
     def fresh_app():
         app = gvhost.HostApp(ver, chain_id="gv-bench", height=1)
@@ -242,8 +271,21 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: in
     rc, codes = app.deliver_block_codes(txs)
     t_block = time.perf_counter() - t
     st = app.stats()
-    app.close()
     assert rc == 0
+    t = time.perf_counter()
+    acc_steady = 0
+    for b in later:
+        rc, c2 = app.deliver_block_codes(b)
+        assert rc == 0
+        acc_steady += int((c2 == 0).sum())
+    t_steady = time.perf_counter() - t
+    st2 = app.stats()
+    app.close()
+    steady = {"blocks": len(later), "txs_per_s": round(ntx * len(later) / t_steady, 1),
+              "ms_per_block": round(t_steady / len(later) * 1e3, 2), "accepted": acc_steady,
+              "preverify_ms_per_block": round((st2["preverify_ns"] - st["preverify_ns"]) / 1e6 / len(later), 2),
+              "gpu_ms_per_block": round((st2["gpu_ns"] - st["gpu_ns"]) / 1e6 / len(later), 2),
+              "ante_loop_ms_per_block": round((st2["deliver_loop_ns"] - st["deliver_loop_ns"]) / 1e6 / len(later), 2)}
     # per-tx path (CheckTx without batching): one GPU call per tx
     app = fresh_app()
     m = min(per_tx_sample, ntx)
@@ -281,6 +323,7 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: in
     app.close()
     okw = sum(1 for rc_a, r in res if rc_a == 0 and r["code"] == 0)
     return {"txs": ntx,
+            "block_path_steady": steady,
             "block_path": {"txs_per_s": round(ntx / t_block, 1), "total_ms": round(t_block * 1e3, 2),
                            "preverify_ms": round(st["preverify_ns"] / 1e6, 2), "gpu_ms": round(st["gpu_ns"] / 1e6, 2),
                            "ante_loop_ms": round(st["deliver_loop_ns"] / 1e6, 2),
