@@ -53,6 +53,17 @@ typedef struct gvk_batch {
 // build lives in the batch scratch).
 #define GV_KEY_WORDS (GV_QTAB_N * GV_QENT_WORDS)
 
+// Keyed latency schedule (gv_lat.hip k_verify_lat16): the 26 five-bit windows
+// of each 128-bit GLV half split into GV_LGRP groups starting at windows
+// 0, 7, 14, 20 (bit offsets 0, 35, 70, 100).  The key arena holds, besides
+// Q's table, the tables of 2^35 Q, 2^70 Q and 2^100 Q (rows of kqt2, Z in
+// kzq2); glat holds the 16 multiples of 2^(5 w0) G and 2^(5 w0) lambda G
+// per group (affine, 8 x 32 words x, y per entry).
+#define GV_LGRP 4
+#define GV_LAT16_SIGS 8                                   // signatures per 128-thread block: 16 lanes each
+#define GV_KEY2_TABLES (GV_LGRP - 1)
+#define GV_GLAT_WORDS (GV_LGRP * 2 * GV_QTAB_N * 16)
+
 // Small-batch latency path (gv_lat.hip): GV_LAT_SIGS signatures per block of
 // 128 threads, one fused kernel (after k_sha256 on the message path).  bits
 // receives ceil(n / GV_LAT_SIGS) 16-bit words (the caller zeroes the tail of
@@ -76,6 +87,10 @@ typedef struct gvk_lat {
   const uint32_t* kzq;
   const uint32_t* kok;
   uint32_t kC, kcount;
+  // keyed batches take k_verify_lat16: the group tables below
+  const uint32_t* kqt2;         // GV_KEY2_TABLES rows per slot (row slot * 3 + group - 1)
+  const uint32_t* kzq2;         // GV_KEY2_TABLES x 8 rows of stride kC
+  const uint32_t* glat;         // GV_GLAT_WORDS
 } gvk_lat;
 
 // ed25519 (ed_verify.hip): one signature per lane over C lanes (C % 256 == 0).
@@ -97,7 +112,9 @@ hipError_t gvk_ed_btab(uint32_t* btab, hipStream_t st);
 hipError_t gvk_ed_verify(const gvk_ed* b, hipStream_t st);
 
 hipError_t gvk_gen_gtable(uint32_t* gtab, hipStream_t st);
+hipError_t gvk_gen_glat(uint32_t* glat, hipStream_t st);
 hipError_t gvk_verify_lat(const gvk_lat* b, hipStream_t st);
+hipError_t gvk_verify_lat16(const gvk_lat* b, hipStream_t st);
 hipError_t gvk_sha256(const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint32_t n, uint32_t C,
                       uint32_t* e, hipStream_t st);
 hipError_t gvk_verify(const gvk_batch* b, hipStream_t st);
@@ -106,7 +123,8 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st);
 // qr (GV_QTAB_N - 1) * 9 rows of stride C.
 hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
                           uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t base,
-                          uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, hipStream_t st);
+                          uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2,
+                          hipStream_t st);
 hipError_t gvk_keys_point(uint32_t n, const uint32_t* slots, const uint32_t* kqt, const uint32_t* kzq, uint32_t kC,
                           const uint32_t* kok, uint32_t kcount, uint8_t* out_xy, uint8_t* out_ok, hipStream_t st);
 hipError_t gvk_debug(int op, uint32_t n, const uint32_t* in, uint32_t* out, hipStream_t st);

@@ -572,8 +572,24 @@ __global__ __launch_bounds__(256) void k_prep(u32 C, u32 n, const u32* in_x, con
 // stride kC) and the ParsePubKey verdict to kok.  A rejected key gets G's
 // table (never used: every item against it is false).  qr: Z-ratio scratch
 // rows of stride C.
+// Window-group start bits of the keyed latency schedule (GV_LGRP groups).
+__constant__ const int kLGrpBit[GV_LGRP] = {0, 35, 70, 100};
+
+// Affine x, y (8 x 32 words) of a finite Jacobian point.
+GV_DEV void gej29_to_affine_words(fe& x8, fe& y8, const gej29& p) {
+  fe29 zi, z2, z3, x, y;
+  f29_inv(zi, p.z);
+  f29_sqr(z2, zi);
+  f29_mul(z3, z2, zi);
+  f29_mul(x, p.x, z2);
+  f29_mul(y, p.y, z3);
+  f29_to_words(x8.v, x);
+  f29_to_words(y8.v, y);
+}
+
 __global__ __launch_bounds__(256) void k_keys_build(u32 n, u32 C, const u32* in_x, const u32* in_pfx, u32 base,
-                                                     u32* kqt, u32* kzq, u32 kC, u32* kok, u32* qr) {
+                                                     u32* kqt, u32* kzq, u32 kC, u32* kok, u32* qr, u32* kqt2,
+                                                     u32* kzq2) {
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n) return;                       // no cross-lane work below
   fe x, y, zq;
@@ -586,6 +602,52 @@ __global__ __launch_bounds__(256) void k_keys_build(u32 n, u32 C, const u32* in_
   build_q_table(kqt, base + g, qr, C, g, x, y, zq);
   store_fe(kzq, kC, base + g, zq);
   kok[base + g] = ok ? 1u : 0u;
+  // the keyed latency schedule's group tables: 2^35 Q, 2^70 Q, 2^100 Q
+  gej29 q;
+  f29_from_words(q.x, x.v);
+  f29_from_words(q.y, y.v);
+  f29_set_u32(q.z, 1);
+#pragma unroll 1
+  for (int grp = 1; grp < GV_LGRP; ++grp) {
+#pragma unroll 1
+    for (int k = kLGrpBit[grp - 1]; k < kLGrpBit[grp]; ++k) gej29_double(q, q);   // never infinite: odd order
+    fe qx, qy;
+    gej29_to_affine_words(qx, qy, q);
+    build_q_table(kqt2, (base + g) * GV_KEY2_TABLES + (grp - 1), qr, C, g, qx, qy, zq);
+    store_fe(kzq2 + (size_t)(grp - 1) * 8 * kC, kC, base + g, zq);
+  }
+}
+
+// glat: per group, the multiples m = 1..16 of 2^(bit) G and 2^(bit) lambda G,
+// affine; thread t = (group, part, m - 1).  Once per context.
+__global__ void k_gen_glat(u32* glat) {
+  const int t = threadIdx.x;
+  if (t >= GV_LGRP * 2 * GV_QTAB_N) return;
+  const int grp = t >> 5, part = (t >> 4) & 1, m = (t & 15) + 1;
+  fe gx, gy;
+  fe_from_const(gx, kGx);
+  fe_from_const(gy, kGy);
+  gej29 p;
+  f29_from_words(p.x, gx.v);
+  f29_from_words(p.y, gy.v);
+  f29_set_u32(p.z, 1);
+  if (part) {
+    fe b8;
+    fe29 beta;
+    fe_from_const(b8, kBeta);
+    f29_from_words(beta, b8.v);
+    f29_mul(p.x, p.x, beta);                // lambda G = (beta x, y)
+  }
+  for (int k = 0; k < kLGrpBit[grp]; ++k) gej29_double(p, p);
+  gej29 acc;
+  bool inf = true;
+  for (int b = 4; b >= 0; --b) {
+    if (!inf) gej29_double(acc, acc);
+    if ((m >> b) & 1) gej29_add_gej(acc, inf, acc, inf, p, false);
+  }
+  fe x8, y8;
+  gej29_to_affine_words(x8, y8, acc);
+  store_qent(glat, grp * 2 + part, m - 1, x8, y8);
 }
 
 // ------------------------------------------------------------ k_keys_point
@@ -901,14 +963,20 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   return hipGetLastError();
 }
 
+hipError_t gvk_gen_glat(uint32_t* glat, hipStream_t st) {
+  hipLaunchKernelGGL(gv::k_gen_glat, dim3(1), dim3(GV_LGRP * 2 * GV_QTAB_N), 0, st, glat);
+  return hipGetLastError();
+}
+
 hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
                           uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t base,
-                          uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, hipStream_t st) {
+                          uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2,
+                          hipStream_t st) {
   const dim3 blk(256), grd(C / 256);
   hipLaunchKernelGGL(gv::k_unpack, grd, blk, 0, st, pub33, (const uint8_t*)nullptr, (const uint8_t*)nullptr, n, C,
                      in_x, in_pfx, in_r, in_s, in_e);
   hipLaunchKernelGGL(gv::k_keys_build, grd, blk, 0, st, n, C, (const uint32_t*)in_x, (const uint32_t*)in_pfx, base,
-                     kqt, kzq, kC, kok, qr);
+                     kqt, kzq, kC, kok, qr, kqt2, kzq2);
   return hipGetLastError();
 }
 

@@ -68,6 +68,7 @@ static __constant__ const u32 kLP[8] = {0xFFFFFC2Fu, 0xFFFFFFFEu, 0xFFFFFFFFu, 0
                                         0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
 
 struct LatShared {
+  static constexpr bool kG5 = false;         // G digits: 20-bit windows (dg)
   u32 qtab[GV_LAT_SIGS][2][GV_QTAB_N][18];  // Q, lambda*Q entries: x, y raw 29-bit limbs (effective affine)
   u32 ratio[64][GV_QTAB_N - 1][9];          // per-lane Z-ratio scratch of the table build (raw limbs)
   u32 dq[GV_LAT_SIGS][GV_QWIN];             // packed int16 Q / lambda*Q digits per window
@@ -323,8 +324,20 @@ GV_DEV void lat_keyed_tables(LatShared& sh, int sig, int slot, bool live, u32 ks
   }
 }
 
-// Wave 1: the scalar chain of one signature (lane sig < GV_LAT_SIGS).
-GV_DEV void lat_scalars(LatShared& sh, int sig, bool live, const uint8_t* sig64, const uint8_t* dig32,
+// The keyed 16-lane schedule's shared state (k_verify_lat16).
+struct Lat16Shared {
+  static constexpr bool kG5 = true;          // G digits: 5-bit windows like Q (dg5)
+  u32 dq[GV_LAT16_SIGS][GV_QWIN];            // packed int16 Q / lambda*Q digits per window
+  u32 dg5[GV_LAT16_SIGS][GV_QWIN];           // packed int16 G / lambda*G digits per window
+  u32 r[GV_LAT16_SIGS][8];
+  u32 oks[GV_LAT16_SIGS];
+  u32 res[GV_LAT16_SIGS];
+};
+
+// The scalar chain of one signature (one lane): range / low-S checks, s^-1,
+// u1, u2, GLV split, Booth digits -> sh.
+template <class SH>
+GV_DEV void lat_scalars(SH& sh, int sig, bool live, const uint8_t* sig64, const uint8_t* dig32,
                         const u32* e_soa, u32 C, u32 gi) {
   u32 r[8], s[8], e[8];
 #pragma unroll
@@ -379,13 +392,23 @@ GV_DEV void lat_scalars(LatShared& sh, int sig, bool live, const uint8_t* sig64,
     if (n2q) d1 = -d1;
     sh.dq[sig][win] = ((u32)d0 & 0xFFFFu) | ((u32)d1 << 16);
   }
+  if constexpr (SH::kG5) {
 #pragma unroll
-  for (int j = 0; j < GV_GWIN; ++j) {
-    int d2 = booth_digit<GV_GW>(k1g, j), d3 = booth_digit<GV_GW>(k2g, j);
-    if (n1g) d2 = -d2;
-    if (n2g) d3 = -d3;
-    sh.dg[sig][j][0] = d2;
-    sh.dg[sig][j][1] = d3;
+    for (int win = 0; win < GV_QWIN; ++win) {
+      int d2 = booth_digit<GV_QW>(k1g, win), d3 = booth_digit<GV_QW>(k2g, win);
+      if (n1g) d2 = -d2;
+      if (n2g) d3 = -d3;
+      sh.dg5[sig][win] = ((u32)d2 & 0xFFFFu) | ((u32)d3 << 16);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < GV_GWIN; ++j) {
+      int d2 = booth_digit<GV_GW>(k1g, j), d3 = booth_digit<GV_GW>(k2g, j);
+      if (n1g) d2 = -d2;
+      if (n2g) d3 = -d3;
+      sh.dg[sig][j][0] = d2;
+      sh.dg[sig][j][1] = d3;
+    }
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) sh.r[sig][i] = r[i];
@@ -545,7 +568,165 @@ __global__ __launch_bounds__(128) void k_verify_lat(const u32* gtab, const uint8
   }
 }
 
+// ---------------------------------------------------------------------------
+// Keyed small batches (C5 with the account's key resident, gv_keys_load):
+// 16 lanes per signature, GV_LAT16_SIGS = 8 signatures per 128-thread block.
+// Lane (s, j): part = j & 3 picks k1q*Q, k2q*(lambda Q), k1g*G or k2g*(lambda
+// G); group = j >> 2 picks the windows [0,7), [7,14), [14,20) or [20,26) of
+// that 128-bit half, against the table of 2^(5 w0) times the base (the key
+// arena's group tables for Q, glat for G).  So each lane runs at most 30
+// doublings and 7 table additions instead of 125 and 26; four cross-lane
+// rounds of complete Jacobian additions combine the 16 partial sums and lane
+// j == 0 runs the same inversion-free final check.  The scalar chain runs
+// first, on lane j == 0 of each signature (the tables need no preparation).
+static __constant__ const int kL16Win[GV_LGRP + 1] = {0, 7, 14, 20, GV_QWIN};
+
+__global__ __launch_bounds__(128) void k_verify_lat16(const gvk_lat b) {
+  __shared__ Lat16Shared sh;
+  const u32 tid = threadIdx.x, sig = tid >> 4, j = tid & 15u;
+  const u32 gi = blockIdx.x * GV_LAT16_SIGS + sig;
+  const bool live = gi < b.n;
+  const u32 gs = live ? gi : 0u;
+  u32 sl = live ? b.kslot[gs] : 0xFFFFFFFFu;
+  bool kok = sl < b.kcount;
+  if (!kok) sl = 0;                                     // the arena always holds slot 0's memory
+  kok = kok && b.kok[sl] != 0u;
+  if (j == 0)
+    lat_scalars(sh, (int)sig, live, b.sig64 + (size_t)gs * 64u, b.dig32 ? b.dig32 + (size_t)gs * 32u : nullptr,
+                b.msg_blob ? (const u32*)b.e_soa : nullptr, b.C, gs);
+  __syncthreads();
+
+  const int part = (int)(j & 3u), grp = (int)(j >> 2);
+  const int w_lo = kL16Win[grp], w_hi = kL16Win[grp + 1] - 1;
+  fe29 beta;
+  {
+    u32 w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = kLBeta[i];
+    f29_from_words(beta, w);
+  }
+  const u32* qrow = grp == 0 ? b.kqt + (size_t)sl * GV_QTAB_N * GV_QENT_WORDS
+                             : b.kqt2 + ((size_t)sl * GV_KEY2_TABLES + (grp - 1)) * GV_QTAB_N * GV_QENT_WORDS;
+  const u32* grow = b.glat + (size_t)(grp * 2 + (part & 1)) * GV_QTAB_N * 16;
+  gej29 acc;
+  f29_set_zero(acc.x); f29_set_zero(acc.y); f29_set_zero(acc.z);
+  bool inf = true;
+#pragma unroll 1
+  for (int win = w_hi; win >= w_lo; --win) {
+    if (win != w_hi) {
+#pragma unroll 1
+      for (int d = 0; d < GV_QW; ++d) gej29_double(acc, acc);
+    }
+    const u32 dw = part < 2 ? sh.dq[sig][win] : sh.dg5[sig][win];
+    const int d = (part & 1) == 0 ? ((int)(dw << 16) >> 16) : ((int)dw >> 16);
+    if (d != 0) {
+      const u32 e = (u32)((d < 0 ? -d : d) - 1);
+      fe29 x, y;
+      if (part < 2) {                                   // Q / lambda Q: arena row, 29-bit limbs
+        const uint4* p = (const uint4*)(qrow + (size_t)e * GV_QENT_WORDS);
+        const uint4 a = p[0], bb = p[1], c = p[2], dd = p[3], ee = p[4];
+        x.n[0] = a.x; x.n[1] = a.y; x.n[2] = a.z; x.n[3] = a.w;
+        x.n[4] = bb.x; x.n[5] = bb.y; x.n[6] = bb.z; x.n[7] = bb.w;
+        x.n[8] = c.x; y.n[0] = c.y; y.n[1] = c.z; y.n[2] = c.w;
+        y.n[3] = dd.x; y.n[4] = dd.y; y.n[5] = dd.z; y.n[6] = dd.w;
+        y.n[7] = ee.x; y.n[8] = ee.y;
+        if (part == 1) f29_mul(x, x, beta);             // lambda Q = (beta x, y), same Z
+      } else {                                          // G / lambda G: affine words
+        const uint4* p = (const uint4*)(grow + (size_t)e * 16);
+        const uint4 a = p[0], bb = p[1], c = p[2], dd = p[3];
+        u32 wx[8] = {a.x, a.y, a.z, a.w, bb.x, bb.y, bb.z, bb.w};
+        u32 wy[8] = {c.x, c.y, c.z, c.w, dd.x, dd.y, dd.z, dd.w};
+        f29_from_words(x, wx);
+        f29_from_words(y, wy);
+      }
+      if (d < 0) f29_neg<1>(y, y);
+      fe29 az, z2, u2, s2;
+      if (inf) f29_set_u32(az, 1);
+      else az = acc.z;
+      f29_sqr(z2, az);
+      {
+        fe29 o[2];
+        const fe29 xa[2] = {x, z2}, ya[2] = {z2, az};
+        f29_multi<false, false>(o, xa, ya);
+        u2 = o[0]; z2 = o[1];
+      }
+      f29_mul(s2, y, z2);
+      if (inf) {
+        acc.x = u2; acc.y = s2; f29_set_u32(acc.z, 1); inf = false;
+      } else {
+        gej29_add_tail(acc, inf, u2, s2);
+      }
+    }
+  }
+  // Q parts live on the isomorphic curve of their table's Z: back to the real curve
+  if (part < 2) {
+    const u32* zrow = grp == 0 ? b.kzq : b.kzq2 + (size_t)(grp - 1) * 8 * b.kC;
+    u32 w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = zrow[(size_t)i * b.kC + sl];
+    fe29 zq;
+    f29_from_words(zq, w);
+    f29_mul(acc.z, acc.z, zq);
+  }
+  gej29 other;
+  bool oinf;
+#pragma unroll 1
+  for (int m = 1; m < 16; m <<= 1) {                    // 16 partial sums -> lane j == 0
+    shfl_xor_gej(other, oinf, acc, inf, m);
+    gej29_add_gej(acc, inf, acc, inf, other, oinf);
+  }
+  if (j == 0) {
+    const u32 fl = sh.oks[sig];
+    bool ok = (fl & 1u) && kok && !inf;
+    fe29 zz, rf, t;
+    f29_sqr(zz, acc.z);
+    u32 rw[8], X[8], tw[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rw[i] = sh.r[sig][i];
+    f29_from_words(rf, rw);
+    f29_mul(t, rf, zz);
+    f29_to_words(X, acc.x);
+    f29_to_words(tw, t);
+    bool eq = true;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) eq &= (X[i] == tw[i]);
+    if (!eq && (fl & 2u)) {
+      u32 rn[8], c = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) rn[i] = __builtin_addc(rw[i], kN[i], c, &c);
+      f29_from_words(rf, rn);
+      f29_mul(t, rf, zz);
+      f29_to_words(tw, t);
+      eq = true;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) eq &= (X[i] == tw[i]);
+    }
+    sh.res[sig] = (ok && eq) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    u32 b8 = 0;
+#pragma unroll
+    for (int q = 0; q < GV_LAT16_SIGS; ++q) b8 |= sh.res[q] << q;
+    uint8_t* bits8 = (uint8_t*)b.bits;
+    bits8[blockIdx.x] = (uint8_t)b8;
+    if (blockIdx.x == gridDim.x - 1)                    // zero the rest of the last 64-bit word
+      for (u32 k = blockIdx.x + 1; (k & 7u) != 0u; ++k) bits8[k] = 0;
+  }
+}
+
 }  // namespace gv
+
+extern "C" hipError_t gvk_verify_lat16(const gvk_lat* b, hipStream_t st) {
+  const uint32_t blocks = (b->n + GV_LAT16_SIGS - 1) / GV_LAT16_SIGS;
+  if (b->msg_blob) {
+    hipError_t e = gvk_sha256(b->msg_blob, b->msg_off, b->msg_len, b->n, b->C, b->e_soa, st);
+    if (e != hipSuccess) return e;
+  }
+  if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
+  hipLaunchKernelGGL(gv::k_verify_lat16, dim3(blocks), dim3(128), 0, st, *b);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t gvk_verify_lat(const gvk_lat* b, hipStream_t st) {
   const uint32_t blocks = (b->n + GV_LAT_SIGS - 1) / GV_LAT_SIGS;

@@ -239,6 +239,8 @@ struct Dev {
   Set set[2];
   // key arena (gv_keys_load): Q table rows, table Z (8 rows of stride kcap), verdicts
   uint32_t *kqt = nullptr, *kzq = nullptr, *kok = nullptr;
+  uint32_t *kqt2 = nullptr, *kzq2 = nullptr;      // the keyed latency schedule's group tables (2^35 Q, ...)
+  uint32_t* glat = nullptr;                       // group tables of G / lambda G (k_gen_glat)
   size_t kcap = 0;
   // ring of per-launch stage events for gv_stage_stats: start + 4 stage ends
   static constexpr int kRing = 256;
@@ -325,21 +327,28 @@ int set_release(Set* s, hipStream_t st) {
 int ensure_keys(Dev* d, size_t need, size_t used, hipStream_t st) {
   if (need <= d->kcap) return GV_OK;
   const size_t cap = round_up(std::max<size_t>({need, 2 * d->kcap, 4096}), 256);
-  uint32_t *qt = nullptr, *zq = nullptr, *ok = nullptr;
-  if (hipMalloc(&qt, cap * GV_KEY_WORDS * 4) != hipSuccess) return GV_ENOMEM;
-  if (hipMalloc(&zq, cap * 8 * 4) != hipSuccess) { (void)hipFree(qt); return GV_ENOMEM; }
-  if (hipMalloc(&ok, cap * 4) != hipSuccess) { (void)hipFree(qt); (void)hipFree(zq); return GV_ENOMEM; }
+  uint32_t *qt = nullptr, *zq = nullptr, *ok = nullptr, *qt2 = nullptr, *zq2 = nullptr;
+  auto fail = [&]() {
+    for (uint32_t* p : {qt, zq, ok, qt2, zq2}) if (p) (void)hipFree(p);
+    return GV_ENOMEM;
+  };
+  if (hipMalloc(&qt, cap * GV_KEY_WORDS * 4) != hipSuccess) return fail();
+  if (hipMalloc(&zq, cap * 8 * 4) != hipSuccess) return fail();
+  if (hipMalloc(&ok, cap * 4) != hipSuccess) return fail();
+  if (hipMalloc(&qt2, cap * GV_KEY2_TABLES * GV_KEY_WORDS * 4) != hipSuccess) return fail();
+  if (hipMalloc(&zq2, cap * GV_KEY2_TABLES * 8 * 4) != hipSuccess) return fail();
   if (used) {
     CK(hipMemcpyAsync(qt, d->kqt, used * GV_KEY_WORDS * 4, hipMemcpyDeviceToDevice, st));
+    CK(hipMemcpyAsync(qt2, d->kqt2, used * GV_KEY2_TABLES * GV_KEY_WORDS * 4, hipMemcpyDeviceToDevice, st));
     for (int r = 0; r < 8; ++r)
       CK(hipMemcpyAsync(zq + r * cap, d->kzq + r * d->kcap, used * 4, hipMemcpyDeviceToDevice, st));
+    for (int r = 0; r < GV_KEY2_TABLES * 8; ++r)
+      CK(hipMemcpyAsync(zq2 + r * cap, d->kzq2 + r * d->kcap, used * 4, hipMemcpyDeviceToDevice, st));
     CK(hipMemcpyAsync(ok, d->kok, used * 4, hipMemcpyDeviceToDevice, st));
     CK(hipStreamSynchronize(st));
   }
-  if (d->kqt) (void)hipFree(d->kqt);
-  if (d->kzq) (void)hipFree(d->kzq);
-  if (d->kok) (void)hipFree(d->kok);
-  d->kqt = qt; d->kzq = zq; d->kok = ok; d->kcap = cap;
+  for (uint32_t* p : {d->kqt, d->kzq, d->kok, d->kqt2, d->kzq2}) if (p) (void)hipFree(p);
+  d->kqt = qt; d->kzq = zq; d->kok = ok; d->kqt2 = qt2; d->kzq2 = zq2; d->kcap = cap;
   return GV_OK;
 }
 
@@ -479,7 +488,12 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
       lb.pub33 = nullptr;
       lb.kslot = kslot; lb.kqt = b.kqt; lb.kzq = b.kzq; lb.kok = b.kok; lb.kC = b.kC; lb.kcount = b.kcount;
     }
-    CK(gvk_verify_lat(&lb, st));
+    if (kslot) {                                // keyed: 16 lanes per signature (group tables)
+      lb.kqt2 = d->kqt2; lb.kzq2 = d->kzq2; lb.glat = d->glat;
+      CK(gvk_verify_lat16(&lb, st));
+    } else {
+      CK(gvk_verify_lat(&lb, st));
+    }
     if (rs) {                                   // stages: SHA | (none) | (none) | fused kernel
       CK(hipEventRecord(rs[2], st));
       CK(hipEventRecord(rs[3], st));
@@ -798,6 +812,8 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
     ok = ok && hipMalloc(&d->gtab, (size_t)2 * GV_GTAB_N * 16 * 4) == hipSuccess &&
          gvk_gen_gtable(d->gtab, d->set[0].st) == hipSuccess && hipStreamSynchronize(d->set[0].st) == hipSuccess;
+    ok = ok && hipMalloc(&d->glat, (size_t)GV_GLAT_WORDS * 4) == hipSuccess &&
+         gvk_gen_glat(d->glat, d->set[0].st) == hipSuccess && hipStreamSynchronize(d->set[0].st) == hipSuccess;
     if (!ok) { gv_close(ctx); return GV_EHIP; }
   }
   *out = ctx;
@@ -811,6 +827,9 @@ void gv_close(gv_ctx* ctx) {
     (void)hipSetDevice(d->id);
     for (Set& s : d->set) free_set(s);
     if (d->gtab) (void)hipFree(d->gtab);
+    if (d->glat) (void)hipFree(d->glat);
+    if (d->kqt2) (void)hipFree(d->kqt2);
+    if (d->kzq2) (void)hipFree(d->kzq2);
     if (d->kqt) (void)hipFree(d->kqt);
     if (d->kzq) (void)hipFree(d->kzq);
     if (d->kok) (void)hipFree(d->kok);
@@ -942,7 +961,7 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
       CK(hipMemcpyAsync(s->d_in, pub33 + c0 * 33, cn * 33, hipMemcpyHostToDevice, st));
       CK(gvk_keys_build(s->d_in, (uint32_t)cn, (uint32_t)C, s->in_x, s->in_pfx, s->in_r, s->in_s, s->in_e,
                         s->qtab + C * GV_QTAB_N * GV_QENT_WORDS, (uint32_t)(base + c0), d->kqt, d->kzq,
-                        (uint32_t)d->kcap, d->kok, st));
+                        (uint32_t)d->kcap, d->kok, d->kqt2, d->kzq2, st));
       if ((rc = set_release(s, st))) return rc;
       CK(hipStreamSynchronize(st));            // the caller's pub33 chunk is read by then
     }
