@@ -137,3 +137,25 @@ def test_chunked_batch_and_device_resident(ver):
     assert np.array_equal(dev, W)
     for ptr in d + [d_bits]:
         ver.dev_free(ptr)
+
+
+def test_two_device_slots_split_ed25519():
+    """gv_open with device slots [0, 0]: the ed25519 host path splits a batch
+    across the two slots (persistent worker for slot 1) and concatenates."""
+    v = gvm.Verifier([0, 0])
+    try:
+        rng = random.Random(21)
+        seeds = [rng.randbytes(32) for _ in range(8)]
+        pubs = [OSSL.public_key(s) for s in seeds]
+        items, want = [], []
+        for i in range(1500):
+            msg = rng.randbytes(rng.randrange(0, 120))
+            sig = OSSL.sign(seeds[i % 8], msg)
+            if i % 3 == 0:
+                msg += b"?"
+            items.append((pubs[i % 8], msg, sig))
+            want.append(i % 3 != 0)
+        pub, sig, msgs = arrays(items)
+        assert np.array_equal(v.verify_batch_ed25519(pub, sig, msgs).astype(bool), np.array(want))
+    finally:
+        v.close()
