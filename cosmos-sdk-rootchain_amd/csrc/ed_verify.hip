@@ -7,7 +7,10 @@
 //                (32 windows x 129 entries x 27 words = 436 KB, L2-resident)
 //   k_ed_prep    per lane: SHA-512(R || A || M) mod L, the sig[63] & 224 and
 //                ScMinimal checks, FromBytes(A), the per-lane table j(-A)
-//                (global scratch, lane-strided rows: coalesced)
+//                (global scratch, lane-major: each lane's entry is 144
+//                contiguous bytes, so a data-dependent lookup touches only
+//                its own lines -- the SoA layout made every lookup pull a
+//                line per lane per limb: 84 KB of HBM fetch per verify)
 //   k_ed_ladder  per lane: 252 doublings + 64 signed radix-16 table adds for
 //                [h](-A), 32 comb adds for [s]B, one inversion to encode R',
 //                a byte compare with sig[:32]; the accept bitmap by ballot.
@@ -59,11 +62,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
   const uint8_t* m = b.msg_blob + b.msg_off[g];
   u32 h[8];
-  u32* row = b.atab + g;
-  const bool ok = ed_prep_item(pw, sw, [=](u32 i) { return (u32)m[i]; }, b.msg_len[g], row, b.C, h);
+  u32* tab = b.atab + (size_t)g * ED_ATAB_WORDS;      // lane-major: this lane's 9 entries, 1,296 B
+  const bool ok = ed_prep_item(pw, sw, [=](u32 i) { return (u32)m[i]; }, b.msg_len[g], tab, 1, h);
+  u32* hrow = b.atab + (size_t)b.C * ED_ATAB_WORDS + g;  // h and the prep verdict: SoA rows
 #pragma unroll
-  for (int i = 0; i < 8; ++i) row[(size_t)(ED_ATAB_WORDS + i) * b.C] = h[i];
-  row[(size_t)(ED_ATAB_WORDS + 8) * b.C] = ok ? 1u : 0u;
+  for (int i = 0; i < 8; ++i) hrow[(size_t)i * b.C] = h[i];
+  hrow[(size_t)8 * b.C] = ok ? 1u : 0u;
 }
 
 // Stage 2: [h](-A) + [s]B, encode, compare; 3 waves per SIMD.
@@ -71,18 +75,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const uint32_t g = blockIdx.x * 256 + threadIdx.x;
   bool ok = false;
   if (g < b.n) {
-    const u32* row = b.atab + g;
+    const u32* tab = b.atab + (size_t)g * ED_ATAB_WORDS;
+    const u32* hrow = b.atab + (size_t)b.C * ED_ATAB_WORDS + g;
     u32 h[8], sw[16];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) h[i] = row[(size_t)(ED_ATAB_WORDS + i) * b.C];
+    for (int i = 0; i < 8; ++i) h[i] = hrow[(size_t)i * b.C];
     const uint4* sp = (const uint4*)(b.sig64 + (size_t)g * 64);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint4 v = sp[k];
       sw[4 * k] = v.x; sw[4 * k + 1] = v.y; sw[4 * k + 2] = v.z; sw[4 * k + 3] = v.w;
     }
-    const bool pre_ok = row[(size_t)(ED_ATAB_WORDS + 8) * b.C] != 0;
-    ok = ed_ladder_check(h, sw + 8, row, b.C, b.btab, sw) && pre_ok;
+    const bool pre_ok = hrow[(size_t)8 * b.C] != 0;
+    ok = ed_ladder_check(h, sw + 8, tab, 1, b.btab, sw) && pre_ok;
   }
   const uint64_t mask = __ballot(ok);
   if ((threadIdx.x & 63) == 0 && g < b.n) b.bits[g >> 6] = mask;   // words up to ceil(n / 64) only

@@ -94,7 +94,7 @@ typedef struct gvk_lat {
 } gvk_lat;
 
 // ed25519 (ed_verify.hip): one signature per lane over C lanes (C % 256 == 0).
-#define GV_ED_ATAB_WORDS 324            // per-lane table j(-A), j = 0..8: 9 x 36 words, rows of stride C
+#define GV_ED_ATAB_WORDS 324            // per-lane table j(-A), j = 0..8: 9 x 36 words, lane-major
 #define GV_ED_ROWS (GV_ED_ATAB_WORDS + 9)  // + h (8 rows) + the prep verdict (1 row)
 #define GV_ED_BTAB_WORDS (32 * 129 * 27)  // resident comb table j * 256^w * B
 typedef struct gvk_ed {
@@ -104,7 +104,7 @@ typedef struct gvk_ed {
   const uint8_t* msg_blob;
   const uint64_t* msg_off;
   const uint32_t* msg_len;
-  uint32_t* atab;               // GV_ED_ROWS rows of C words (scratch: table, h, prep verdict)
+  uint32_t* atab;               // scratch: C x GV_ED_ATAB_WORDS lane-major table, then h (8) + verdict SoA rows
   const uint32_t* btab;         // GV_ED_BTAB_WORDS
   uint64_t* bits;               // C/64 words
 } gvk_ed;
