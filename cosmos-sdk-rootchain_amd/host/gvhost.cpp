@@ -13,6 +13,7 @@
 // verdict: the ante run rebuilds the sign bytes from the actual state.
 #include "gvhost.h"
 
+#include <deque>
 #include <openssl/evp.h>
 #include <openssl/ripemd.h>
 #include <openssl/sha.h>
@@ -135,29 +136,38 @@ const Bech32Gen kBech32Gen;
 void bech32_encode_append(std::string& o, const char* hrp, const uint8_t* data, size_t n) {
   static const char* CS = "qpzry9x8gf2tvdw0s3jn54khce6mua7l";
   const size_t hl = strlen(hrp);
-  uint8_t v[2 * 16 + 1 + 420 + 6];
-  size_t nv = 0;
-  for (size_t i = 0; i < hl; ++i) v[nv++] = (uint8_t)hrp[i] >> 5;
-  v[nv++] = 0;
-  for (size_t i = 0; i < hl; ++i) v[nv++] = (uint8_t)hrp[i] & 31;
-  const size_t d0 = nv;
+  // checksum state after the expanded hrp (hi bits, 0, lo bits)
+  uint32_t chk = 1;
+  auto step = [&](uint32_t v) { chk = ((chk & 0x1ffffff) << 5) ^ v ^ kBech32Gen.t[chk >> 25]; };
+  for (size_t i = 0; i < hl; ++i) step((uint8_t)hrp[i] >> 5);
+  step(0);
+  for (size_t i = 0; i < hl; ++i) step((uint8_t)hrp[i] & 31);
+  char out[16 + 1 + 420 + 6];
+  size_t k = 0;
+  memcpy(out, hrp, hl);
+  k = hl;
+  out[k++] = '1';
   uint32_t acc = 0;
   int bits = 0;
   for (size_t i = 0; i < n; ++i) {
     acc = (acc << 8) | data[i];
     bits += 8;
-    while (bits >= 5) { bits -= 5; v[nv++] = (acc >> bits) & 31; }
+    while (bits >= 5) {
+      bits -= 5;
+      const uint32_t v = (acc >> bits) & 31;
+      step(v);
+      out[k++] = CS[v];
+    }
   }
-  if (bits) v[nv++] = (acc << (5 - bits)) & 31;
-  const size_t d1 = nv;
-  for (int i = 0; i < 6; ++i) v[nv++] = 0;
-  uint32_t chk = 1;
-  for (size_t i = 0; i < nv; ++i) chk = ((chk & 0x1ffffff) << 5) ^ v[i] ^ kBech32Gen.t[chk >> 25];
+  if (bits) {
+    const uint32_t v = (acc << (5 - bits)) & 31;
+    step(v);
+    out[k++] = CS[v];
+  }
+  for (int i = 0; i < 6; ++i) step(0);
   chk ^= 1;
-  o += hrp;
-  o += '1';
-  for (size_t i = d0; i < d1; ++i) o += CS[v[i]];
-  for (int i = 0; i < 6; ++i) o += CS[(chk >> (5 * (5 - i))) & 31];
+  for (int i = 0; i < 6; ++i) out[k++] = CS[(chk >> (5 * (5 - i))) & 31];
+  o.append(out, k);
 }
 // "cosmos" addresses repeat (a signer's every tx, a common recipient): a small
 // per-thread direct-mapped cache of recent 20-byte encodings.
@@ -1119,8 +1129,49 @@ struct Account {
   std::shared_ptr<const PubInfo> info;        // GetPubKey() of pub (decoded once)
   uint64_t bump_epoch = 0, bump = 0;          // PreVerifyTxs' sequence prediction (earlier txs this call)
 };
-struct AddrHash {
-  size_t operator()(const Addr& a) const { return (size_t)fast_hash(a.data(), a.size()); }
+// AccountKeeper store: 20-byte address -> Account.  Open addressing (linear
+// probing) over an index into a deque, so an Account never moves (PreVerifyTxs
+// and the ante loop keep Account pointers) and a lookup is one hash + one or
+// two cache lines instead of a node-based map's bucket chain.
+class AccountTable {
+ public:
+  Account* find(const uint8_t* a) {
+    if (!n_) return nullptr;
+    for (size_t i = fast_hash(a, 20) & mask_;; i = (i + 1) & mask_) {
+      const uint32_t s = slots_[i];
+      if (!s) return nullptr;
+      Entry& e = store_[s - 1];
+      if (!memcmp(e.addr.data(), a, 20)) return &e.acc;
+    }
+  }
+  Account& get_or_insert(const Addr& a) {
+    if (Account* p = find(a.data())) return *p;
+    if ((n_ + 1) * 2 > slots_.size()) grow();
+    store_.push_back(Entry{a, Account{}});
+    ++n_;
+    place(a.data(), (uint32_t)n_);
+    return store_.back().acc;
+  }
+
+ private:
+  struct Entry {
+    Addr addr;
+    Account acc;
+  };
+  void place(const uint8_t* a, uint32_t idx) {
+    size_t i = fast_hash(a, 20) & mask_;
+    while (slots_[i]) i = (i + 1) & mask_;
+    slots_[i] = idx;
+  }
+  void grow() {
+    const size_t cap = std::max<size_t>(1024, slots_.size() * 2);
+    slots_.assign(cap, 0);
+    mask_ = cap - 1;
+    for (size_t k = 0; k < n_; ++k) place(store_[k].addr.data(), (uint32_t)(k + 1));
+  }
+  std::deque<Entry> store_;
+  std::vector<uint32_t> slots_;
+  size_t mask_ = 0, n_ = 0;
 };
 
 // One signer's prepared verification: the sign bytes were built for
@@ -1220,7 +1271,7 @@ struct gvh_app {
   int64_t height = 1;
   bool recheck = false;
   uint64_t gas_limit = 0;
-  std::unordered_map<Addr, Account, AddrHash> accounts;   // AccountKeeper (20-byte addresses)
+  AccountTable accounts;                       // AccountKeeper (20-byte addresses)
   std::mutex mu;                               // accounts + context
   VerdictCache cache{size_t(1) << 20};
   MemoTable memo;
@@ -1367,10 +1418,7 @@ void copy_result(gvh_result* out, const SdkError* e, uint64_t gas, uint32_t gpu_
 
 Account* find_account(gvh_app* app, Span a) {
   if (a.n != 20) return nullptr;                    // accounts have 20-byte addresses
-  Addr k;
-  memcpy(k.data(), a.p, 20);
-  auto it = app->accounts.find(k);
-  return it == app->accounts.end() ? nullptr : &it->second;
+  return app->accounts.find(a.p);
 }
 
 std::shared_ptr<const PubInfo> account_info(gvh_app* app, Account& acc) {
@@ -1955,7 +2003,7 @@ int gvh_set_account(gvh_app* app, const uint8_t addr20[20], uint64_t num, uint64
   acc.sequence = seq;
   if (pub && pub_len) acc.pub.assign(pub, pub + pub_len);      // info decoded on first use
   std::lock_guard<std::mutex> lk(app->mu);
-  app->accounts[a] = acc;
+  app->accounts.get_or_insert(a) = acc;
   return GVH_OK;
 }
 int gvh_get_account(gvh_app* app, const uint8_t addr20[20], uint64_t* num, uint64_t* seq, uint8_t* pub_out,
@@ -1963,12 +2011,12 @@ int gvh_get_account(gvh_app* app, const uint8_t addr20[20], uint64_t* num, uint6
   Addr a;
   memcpy(a.data(), addr20, 20);
   std::lock_guard<std::mutex> lk(app->mu);
-  auto it = app->accounts.find(a);
-  if (it == app->accounts.end()) return 0;
-  if (num) *num = it->second.number;
-  if (seq) *seq = it->second.sequence;
-  if (pub_len) *pub_len = it->second.pub.size();
-  if (pub_out && !it->second.pub.empty()) memcpy(pub_out, it->second.pub.data(), std::min<size_t>(512, it->second.pub.size()));
+  Account* found = app->accounts.find(a.data());
+  if (!found) return 0;
+  if (num) *num = found->number;
+  if (seq) *seq = found->sequence;
+  if (pub_len) *pub_len = found->pub.size();
+  if (pub_out && !found->pub.empty()) memcpy(pub_out, found->pub.data(), std::min<size_t>(512, found->pub.size()));
   return 1;
 }
 
