@@ -28,6 +28,7 @@
 #include "secp_scalar.cuh"
 #include "secp_group.cuh"
 #include "secp_group29.cuh"
+#include "secp_group29x.cuh"
 #include "secp_sc29.cuh"
 #include "secp_modinv.cuh"
 #include "secp_sha256.cuh"
@@ -690,7 +691,34 @@ __global__ __launch_bounds__(256) void k_keys_point(u32 n, const u32* slots, con
 // (zinv == nullptr: Q-table entry) or an affine point of the real curve to be
 // lifted by zinv (G-table entry).  An infinite accumulator takes the point.
 // x magnitude 1, y magnitude <= 2 (a negated entry), zinv magnitude 1.
+// GV_FUSED: the ladder on the fused product engine (secp_group29x.cuh):
+// subtractions and small multiples folded into the product chains (same
+// results, fewer instructions per verify).  0 = the secp_group29.cuh formulas.
+#ifndef GV_FUSED
+#define GV_FUSED 1
+#endif
 GV_DEV void add_entry(gej29& acc, bool& inf, const fe29& x, const fe29& y, const fe29* zinv) {
+#if GV_FUSED
+  if (inf) {                                    // acc takes the entry, Z = 1
+    if (zinv) {                                 // wave-uniform
+      fe29 z2, z3;
+      f29x_sqr(z2, *zinv);
+      f29x_mul(acc.x, x, z2);
+      f29x_mul(z3, z2, *zinv);
+      f29x_mul(acc.y, y, z3);
+    } else {
+      acc.x = x;
+      f29_norm(acc.y, y);                       // a negated entry has magnitude 2
+    }
+    f29_set_u32(acc.z, 1);
+    inf = false;
+    return;
+  }
+  fe29 az;
+  if (zinv) f29x_mul(az, acc.z, *zinv);         // 1
+  else az = acc.z;                              // <= 2
+  gej29x_add_scaled(acc, inf, x, y, az);
+#else
   fe29 az;
   if (zinv) {                                   // wave-uniform
     if (inf) az = *zinv;
@@ -721,6 +749,7 @@ GV_DEV void add_entry(gej29& acc, bool& inf, const fe29& x, const fe29& y, const
     return;
   }
   gej29_add_tail(acc, inf, u2, s2);
+#endif
 }
 
 // GV_ECMULT_WAVES: minimum waves per SIMD the register allocator must allow
@@ -755,7 +784,11 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult(const u32* gtab, 
   for (int win = GV_QWIN - 1; win >= 0; --win) {
     if (win != GV_QWIN - 1) {
 #pragma unroll 1
+#if GV_FUSED
+      for (int d = 0; d < GV_QW; ++d) gej29x_double(acc, acc);
+#else
       for (int d = 0; d < GV_QW; ++d) gej29_double(acc, acc);
+#endif
     }
     const bool gwin = (win % GV_GSTEP) == 0;
     const u32 dq = digits[(size_t)win * C + g];
