@@ -47,6 +47,9 @@ typedef struct gvk_batch {
   const uint32_t* kzq;          // arena table Z: 8 rows of stride kC
   const uint32_t* kok;          // arena ParsePubKey verdicts
   uint32_t kC, kcount;          // arena capacity (row stride) and slots in use
+  // keyed batches with gtab4 set take k_ecmult_k4 (30-doubling 4-group ladder)
+  const uint32_t* kqt2;         // arena group tables (2^35 Q, 2^70 Q, 2^100 Q), on the slot's kzq
+  const uint32_t* gtab4;        // GV_KEY2_TABLES x (G-type, lambda) tables of 2^35 G, 2^70 G, 2^100 G
 } gvk_batch;
 
 // Key arena row of one slot: Q table entries only (the Z-ratio scratch of the
@@ -112,6 +115,8 @@ hipError_t gvk_ed_btab(uint32_t* btab, hipStream_t st);
 hipError_t gvk_ed_verify(const gvk_ed* b, hipStream_t st);
 
 hipError_t gvk_gen_gtable(uint32_t* gtab, hipStream_t st);
+// the keyed ladder's G tables (GV_KEY2_TABLES x 2 x GV_GTAB_N x 16 words); base_scratch: 48 words
+hipError_t gvk_gen_gtable4(uint32_t* gtab4, uint32_t* base_scratch, hipStream_t st);
 hipError_t gvk_gen_glat(uint32_t* glat, hipStream_t st);
 hipError_t gvk_verify_lat(const gvk_lat* b, hipStream_t st);
 hipError_t gvk_verify_lat16(const gvk_lat* b, hipStream_t st);

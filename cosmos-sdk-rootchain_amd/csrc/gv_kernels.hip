@@ -84,13 +84,20 @@ GV_DEV void fe_from_const(fe& r, const u32* c) {
 // gtab[e*16 + c]: e = 0..GV_GTAB_N-1 holds (e+1)*G affine, canonical; c = 0..7 x
 // limbs, 8..15 y limbs; gtab[(GV_GTAB_N + e)*16 + c] holds (e+1)*lambda*G =
 // (beta*x, y).  Run once per context.
-__global__ void k_gen_gtable(u32* gtab) {
+// base: affine x || y (16 words) of the point whose multiples are tabulated,
+// or null for G itself (the keyed ladder's tables of 2^35 G, 2^70 G, 2^100 G).
+__global__ void k_gen_gtable(u32* gtab, const u32* base) {
   const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= GV_GTAB_N) return;
   const u32 m = e + 1;
   fe gx, gy;
-  fe_from_const(gx, kGx);
-  fe_from_const(gy, kGy);
+  if (base) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { gx.v[i] = base[i]; gy.v[i] = base[8 + i]; }
+  } else {
+    fe_from_const(gx, kGx);
+    fe_from_const(gy, kGy);
+  }
   gej acc;
   acc.x = gx; acc.y = gy; fe_set_u32(acc.z, 1);
   bool inf = false;
@@ -603,6 +610,8 @@ __global__ __launch_bounds__(256) void k_keys_build(u32 n, u32 C, const u32* in_
   build_q_table(kqt, base + g, qr, C, g, x, y, zq);
   store_fe(kzq, kC, base + g, zq);
   kok[base + g] = ok ? 1u : 0u;
+  fe29 z0;                                  // every group table is rescaled to this Z
+  f29_from_words(z0, zq.v);
   // the keyed latency schedule's group tables: 2^35 Q, 2^70 Q, 2^100 Q
   gej29 q;
   f29_from_words(q.x, x.v);
@@ -614,9 +623,46 @@ __global__ __launch_bounds__(256) void k_keys_build(u32 n, u32 C, const u32* in_
     for (int k = kLGrpBit[grp - 1]; k < kLGrpBit[grp]; ++k) gej29_double(q, q);   // never infinite: odd order
     fe qx, qy;
     gej29_to_affine_words(qx, qy, q);
-    build_q_table(kqt2, (base + g) * GV_KEY2_TABLES + (grp - 1), qr, C, g, qx, qy, zq);
-    store_fe(kzq2 + (size_t)(grp - 1) * 8 * kC, kC, base + g, zq);
+    const u32 row = (base + g) * GV_KEY2_TABLES + (grp - 1);
+    build_q_table(kqt2, row, qr, C, g, qx, qy, zq);
+    // entries (x, y) on Z_g -> (x rho^2, y rho^3) on Z_0, rho = Z_0 / Z_g: one
+    // shared Z for all four tables of the key, so a single accumulator can
+    // take entries of every group (k_ecmult_k4)
+    fe29 zg, rho, r2, r3;
+    f29_from_words(zg, zq.v);
+    f29_inv(rho, zg);
+    f29_mul(rho, rho, z0);
+    f29_sqr(r2, rho);
+    f29_mul(r3, r2, rho);
+#pragma unroll 1
+    for (int m = 0; m < GV_QTAB_N; ++m) {
+      fe29 ex, ey;
+      load_qent29(ex, ey, kqt2, row, m);
+      f29_mul(ex, ex, r2);
+      f29_mul(ey, ey, r3);
+      store_qent29(kqt2, row, m, ex, ey);
+    }
+    store_f29(kzq2 + (size_t)(grp - 1) * 8 * kC, kC, base + g, z0);
   }
+}
+
+// Affine 2^35 G, 2^70 G, 2^100 G (16 words each) for the keyed ladder's G
+// tables; thread t = group - 1.  Once per device.
+__global__ void k_gen_gbase(u32* out) {
+  const int t = threadIdx.x;
+  if (t >= GV_KEY2_TABLES) return;
+  fe gx, gy;
+  fe_from_const(gx, kGx);
+  fe_from_const(gy, kGy);
+  gej29 p;
+  f29_from_words(p.x, gx.v);
+  f29_from_words(p.y, gy.v);
+  f29_set_u32(p.z, 1);
+  for (int k = 0; k < kLGrpBit[t + 1]; ++k) gej29_double(p, p);
+  fe x8, y8;
+  gej29_to_affine_words(x8, y8, p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { out[t * 16 + i] = x8.v[i]; out[t * 16 + 8 + i] = y8.v[i]; }
 }
 
 // glat: per group, the multiples m = 1..16 of 2^(bit) G and 2^(bit) lambda G,
@@ -752,6 +798,43 @@ GV_DEV void add_entry(gej29& acc, bool& inf, const fe29& x, const fe29& y, const
 #endif
 }
 
+// Final check of a ladder: R = (X, Y, Z*zq) on the real curve; x(R) mod n ==
+// r, inversion-free (X == r Z^2, or (r + n) Z^2 when r < p - n); accept
+// bitmap by ballot.
+GV_DEV void ecmult_finish(const gej29& acc, bool inf, const fe29& zq, const u32* flags, const u32* in_r,
+                          uint64_t* bits, u32 n, u32 C, u32 g) {
+  const u32 fl = flags[g];
+  bool ok = (fl & 1u) && !inf;
+  fe29 zr, zz, rf, t;
+  f29_mul(zr, acc.z, zq);
+  f29_sqr(zz, zr);
+  u32 rw[8], X[8], tw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rw[i] = in_r[(size_t)i * C + g];
+  f29_from_words(rf, rw);
+  f29_mul(t, rf, zz);
+  f29_to_words(X, acc.x);
+  f29_to_words(tw, t);
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) eq &= (X[i] == tw[i]);
+  if (!eq && (fl & 2u)) {                   // R.x in [n, p): x mod n == r  <=>  x == r + n
+    u32 rn[8];
+    u32 c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rn[i] = __builtin_addc(rw[i], kN[i], c, &c);
+    f29_from_words(rf, rn);
+    f29_mul(t, rf, zz);
+    f29_to_words(tw, t);
+    eq = true;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) eq &= (X[i] == tw[i]);
+  }
+  ok &= eq;
+  const uint64_t mask = __ballot(ok);
+  if ((threadIdx.x & 63u) == 0 && (g >> 6) < ((n + 63u) >> 6)) bits[g >> 6] = mask;
+}
+
 // GV_ECMULT_WAVES: minimum waves per SIMD the register allocator must allow
 // (0 = compiler's choice).
 #ifndef GV_ECMULT_WAVES
@@ -817,37 +900,83 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult(const u32* gtab, 
     }
   }
 
-  // ---- final check: R = (X, Y, Z*zq) on the real curve; x(R) mod n == r
-  const u32 fl = flags[g];
-  bool ok = (fl & 1u) && !inf;
-  fe29 zr, zz, rf, t;
-  f29_mul(zr, acc.z, zq);
-  f29_sqr(zz, zr);
-  u32 rw[8], X[8], tw[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) rw[i] = in_r[(size_t)i * C + g];
-  f29_from_words(rf, rw);
-  f29_mul(t, rf, zz);
-  f29_to_words(X, acc.x);
-  f29_to_words(tw, t);
-  bool eq = true;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) eq &= (X[i] == tw[i]);
-  if (!eq && (fl & 2u)) {                   // R.x in [n, p): x mod n == r  <=>  x == r + n
-    u32 rn[8];
-    u32 c = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) rn[i] = __builtin_addc(rw[i], kN[i], c, &c);
-    f29_from_words(rf, rn);
-    f29_mul(t, rf, zz);
-    f29_to_words(tw, t);
-    eq = true;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) eq &= (X[i] == tw[i]);
+  ecmult_finish(acc, inf, zq, flags, in_r, bits, n, C, g);
+}
+
+
+// ------------------------------------------------------------- k_ecmult_k4
+// Keyed batches: the key arena holds, per key, the tables of
+// Q, 2^35 Q, 2^70 Q and 2^100 Q on ONE shared Z (k_keys_build), and the
+// device holds the 20-bit-window tables of G, 2^35 G, 2^70 G, 2^100 G (and
+// lambda multiples).  Each 128-bit GLV half's 26 five-bit windows split into
+// the groups [0,7), [7,14), [14,20), [20,26); window w of group k sits at
+// local position w - w0(k) of a 35-bit ladder, so one accumulator takes every
+// group's entry at that position: 6 x 5 = 30 doublings instead of 125, the
+// same 52 Q + 14 G additions.  G window j (bit 20 j) is taken from the G
+// table of the largest group offset <= 20 j at local position (20 j - b)/5.
+static_assert(GV_GW == 20 && GV_QWIN == 26 && GV_LGRP == 4, "k_ecmult_k4 layout");
+__constant__ const int kK4WStart[4] = {0, 7, 14, 20};
+__constant__ const int kK4NWin[4] = {7, 7, 6, 6};
+__constant__ const int kK4GWin[7][2] = {{0, 5}, {2, -1}, {4, -1}, {-1, -1}, {1, 6}, {3, -1}, {-1, -1}};
+__constant__ const int kK4GGrp[7] = {0, 0, 1, 1, 2, 3, 3};
+
+__global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gtab, const u32* gtab4, u32 n, u32 C,
+                                                        const u32* digits, const u32* kqt, const u32* kqt2,
+                                                        const u32* kzq, const u32* flags, const u32* in_r,
+                                                        uint64_t* bits, const u32* qidx, u32 kC) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 qi = qidx[g];
+  fe29 zq;
+  load_f29(zq, kzq, kC, qi);
+  gej29 acc;
+  f29_set_zero(acc.x); f29_set_zero(acc.y); f29_set_zero(acc.z);
+  bool inf = true;
+#pragma unroll 1
+  for (int pos = 6; pos >= 0; --pos) {
+    if (pos != 6) {
+#pragma unroll 1
+      for (int d = 0; d < GV_QW; ++d) gej29x_double(acc, acc);
+    }
+    // slots 0..7: (group, Q / lambda Q); 8..11: up to two G windows x (G, lambda G)
+#pragma unroll 1
+    for (int slot = 0; slot < 12; ++slot) {
+      int d;
+      const u32* tab;
+      u32 row = 0;
+      const bool isg = slot >= 8;
+      if (!isg) {
+        const int grp = slot >> 1;
+        if (pos >= kK4NWin[grp]) continue;                 // wave-uniform
+        const u32 dq = digits[(size_t)(kK4WStart[grp] + pos) * C + g];
+        d = (slot & 1) ? ((int)dq >> 16) : ((int)(dq << 16) >> 16);
+        tab = grp == 0 ? kqt : kqt2;
+        row = grp == 0 ? qi : qi * GV_KEY2_TABLES + (grp - 1);
+      } else {
+        const int j = kK4GWin[pos][(slot - 8) >> 1];
+        if (j < 0) continue;                               // wave-uniform
+        d = (int)digits[(size_t)(GV_QWIN + 2 * j + (slot & 1)) * C + g];
+        const int gg = kK4GGrp[j];
+        tab = (gg == 0 ? gtab : gtab4 + (size_t)(gg - 1) * 2 * GV_GTAB_N * 16) +
+              ((slot & 1) ? (size_t)GV_GTAB_N * 16 : 0);
+      }
+      if (d == 0) continue;
+      const u32 e = (u32)((d < 0 ? -d : d) - 1);
+      fe29 x, y;
+      if (!isg) {
+        load_qent29(x, y, tab, row, e);
+        if (slot & 1) {                                    // lambda * P = (beta * x, y)
+          fe29 beta;
+          f29_from_const(beta, kBeta);
+          f29x_mul(x, x, beta);
+        }
+      } else {
+        load_gent29(x, y, tab, e);
+      }
+      if (d < 0) f29_neg<1>(y, y);                         // 2
+      add_entry(acc, inf, x, y, isg ? &zq : nullptr);
+    }
   }
-  ok &= eq;
-  const uint64_t mask = __ballot(ok);
-  if ((threadIdx.x & 63u) == 0 && (g >> 6) < ((n + 63u) >> 6)) bits[g >> 6] = mask;
+  ecmult_finish(acc, inf, zq, flags, in_r, bits, n, C, g);
 }
 
 // ------------------------------------------------------------------- k_debug
@@ -954,7 +1083,16 @@ __global__ void k_debug(int op, u32 n, const u32* in, u32* out) {
 extern "C" {
 
 hipError_t gvk_gen_gtable(uint32_t* gtab, hipStream_t st) {
-  hipLaunchKernelGGL(gv::k_gen_gtable, dim3((GV_GTAB_N + 63) / 64), dim3(64), 0, st, gtab);
+  hipLaunchKernelGGL(gv::k_gen_gtable, dim3((GV_GTAB_N + 63) / 64), dim3(64), 0, st, gtab,
+                     (const uint32_t*)nullptr);
+  return hipGetLastError();
+}
+
+hipError_t gvk_gen_gtable4(uint32_t* gtab4, uint32_t* base_scratch, hipStream_t st) {
+  hipLaunchKernelGGL(gv::k_gen_gbase, dim3(1), dim3(64), 0, st, base_scratch);
+  for (int k = 0; k < GV_KEY2_TABLES; ++k)
+    hipLaunchKernelGGL(gv::k_gen_gtable, dim3((GV_GTAB_N + 63) / 64), dim3(64), 0, st,
+                       gtab4 + (size_t)k * 2 * GV_GTAB_N * 16, (const uint32_t*)(base_scratch + 16 * k));
   return hipGetLastError();
 }
 
@@ -985,7 +1123,10 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
                          (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr);
   }
   if (b->ev[2]) (void)hipEventRecord(b->ev[2], st);
-  if (b->kslot)
+  if (b->kslot && b->gtab4)
+    hipLaunchKernelGGL(gv::k_ecmult_k4, grd, blk, 0, st, b->gtab, b->gtab4, b->n, C, b->digits, b->kqt, b->kqt2,
+                       b->kzq, b->flags, b->in_r, b->bits, (const uint32_t*)b->in_pfx, b->kC);
+  else if (b->kslot)
     hipLaunchKernelGGL(gv::k_ecmult<true>, grd, blk, 0, st, b->gtab, b->n, C, b->digits, b->kqt, b->kzq,
                        b->flags, b->in_r, b->bits, (const uint32_t*)b->in_pfx, b->kC);
   else

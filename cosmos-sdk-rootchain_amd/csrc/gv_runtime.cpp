@@ -241,6 +241,7 @@ struct Dev {
   uint32_t *kqt = nullptr, *kzq = nullptr, *kok = nullptr;
   uint32_t *kqt2 = nullptr, *kzq2 = nullptr;      // the keyed latency schedule's group tables (2^35 Q, ...)
   uint32_t* glat = nullptr;                       // group tables of G / lambda G (k_gen_glat)
+  uint32_t* gtab4 = nullptr;                      // k_ecmult_k4's tables of 2^35 G, 2^70 G, 2^100 G (+ lambda)
   size_t kcap = 0;
   // ring of per-launch stage events for gv_stage_stats: start + 4 stage ends
   static constexpr int kRing = 256;
@@ -432,6 +433,7 @@ struct gv_ctx {
   int stage_threads = 8;        // host path: staging memcpy threads per device
   bool time_kernels = false;
   bool fault_inject = false;
+  bool keyed_k4 = true;         // keyed batches on k_ecmult_k4 (GV_KEYED_K4=0: the 125-doubling ladder, A/B)
   size_t keys = 0;              // key-arena slots in use (same on every device)
   std::mutex keys_mu;
 };
@@ -466,6 +468,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     b.pub33 = nullptr;
     b.kslot = kslot; b.kqt = d->kqt; b.kzq = d->kzq; b.kok = d->kok;
     b.kC = (uint32_t)d->kcap; b.kcount = (uint32_t)ctx->keys;
+    b.kqt2 = d->kqt2; b.gtab4 = d->gtab4;       // null: the 125-doubling keyed ladder
   }
   hipEvent_t* rs = nullptr;
   if (ctx->time_kernels) {
@@ -799,6 +802,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   }
   gv_ctx* ctx = new gv_ctx();
   parse_size_env("GV_MAX_BATCH", &ctx->max_batch);
+  if (const char* k4 = getenv("GV_KEYED_K4")) ctx->keyed_k4 = strcmp(k4, "0") != 0;
   for (size_t k = 0; k < ids.size(); ++k) {
     Dev* d = new Dev();
     d->id = ids[k];
@@ -828,6 +832,7 @@ void gv_close(gv_ctx* ctx) {
     for (Set& s : d->set) free_set(s);
     if (d->gtab) (void)hipFree(d->gtab);
     if (d->glat) (void)hipFree(d->glat);
+    if (d->gtab4) (void)hipFree(d->gtab4);
     if (d->kqt2) (void)hipFree(d->kqt2);
     if (d->kzq2) (void)hipFree(d->kzq2);
     if (d->kqt) (void)hipFree(d->kqt);
@@ -953,6 +958,17 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
     hipStream_t st = s->st;
     int rc = ensure_keys(d, base + n, base, st);
     if (rc) return rc;
+    if (!d->gtab4 && ctx->keyed_k4) {          // first keys on this device: the k4 ladder's G tables
+      uint32_t* t4 = nullptr;
+      if (hipMalloc(&t4, (size_t)GV_KEY2_TABLES * 2 * GV_GTAB_N * 16 * 4) == hipSuccess) {
+        if ((rc = ensure_cap(s, 256))) { (void)hipFree(t4); return rc; }
+        if ((rc = set_acquire(s, st))) { (void)hipFree(t4); return rc; }
+        CK(gvk_gen_gtable4(t4, s->flags, st));   // 48 scratch words for the base points
+        if ((rc = set_release(s, st))) { (void)hipFree(t4); return rc; }
+        CK(hipStreamSynchronize(st));
+        d->gtab4 = t4;
+      }                                         // no memory: keyed batches keep k_ecmult<true>
+    }
     for (size_t c0 = 0; c0 < n; c0 += ctx->max_batch) {
       const size_t cn = std::min(ctx->max_batch, n - c0);
       const size_t C = round_up(cn, 256);

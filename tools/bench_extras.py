@@ -130,6 +130,8 @@ def c2_key_cache(ver, pub, sig, dig, exp, nkeys: int, steps: int = 5):
     `value`, never as it (key parsing is hoisted out of the timed region)."""
     n = len(pub)
     ver.keys_reset()
+    ver.keys_load(pub[:1])                        # one-time device tables (k_ecmult_k4's G tables) outside the timing
+    ver.keys_reset()
     t = time.perf_counter()
     slots_k = ver.keys_load(pub[:nkeys])          # item i uses key i % nkeys (bench workload)
     t_load = time.perf_counter() - t
@@ -149,7 +151,8 @@ def c2_key_cache(ver, pub, sig, dig, exp, nkeys: int, steps: int = 5):
     return {"items": n, "keys": nkeys, "value": round(n * steps / el, 1), "unit": "verifies/s",
             "keys_load_ms": round(t_load * 1e3, 2), "mismatches": int(np.count_nonzero(got != exp)),
             "stages": stages,
-            "note": "keys parsed once into the HBM key arena (1,280 B per key); items verified by slot"}
+            "note": "keys parsed once into the HBM key arena (Q, 2^35 Q, 2^70 Q, 2^100 Q tables on one Z: 5.4 KB "
+                    "per key); items verified by slot on the 4-group ladder (k_ecmult_k4: 30 doublings)"}
 
 
 def c1_items(wl, n: int, threads: int, nkeys: int = 10000):
