@@ -116,6 +116,57 @@ GV_DEV void f29x_core(fe29& r, const u32* a, const u32* dg, const u32* cr, const
   r = o;
 }
 
+// r = a * b + c * d (+ extras): both products summed in the same column
+// chains, one reduction.  mag(a) mag(b) + mag(c) mag(d) <= 6.
+template <class EX = f29x_none>
+GV_DEV void f29x_mul2(fe29& r, const fe29& a, const fe29& b, const fe29& c, const fe29& d, const EX& ex = EX()) {
+  u32 kr0 = F29_R0, kr1 = F29_R1;
+  f29x_k kk{1u, 8u};
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(kr0), "+v"(kr1));
+  asm("" : "+v"(kk.one), "+v"(kk.eight));
+#endif
+  u32 t[9];
+  u32 hi = 0;
+#pragma unroll
+  for (int k = 9; k <= 16; ++k) {
+    u64 acc = 0;
+#pragma unroll
+    for (int i = k - 8; i <= 8; ++i) acc = f29_mad(a.n[i], b.n[k - i], acc);
+#pragma unroll
+    for (int i = k - 8; i <= 8; ++i) acc = f29_mad(c.n[i], d.n[k - i], acc);
+    if (k > 9) acc = f29_mad(hi, kk.eight, acc);
+    t[k - 9] = (u32)acc;
+    hi = (u32)(acc >> 32);
+  }
+  F29_TRAP(hi >= (1u << 29), "x2 t17");
+  t[8] = hi << 3;
+  fe29 o;
+  u64 acc = 0;
+#pragma unroll
+  for (int j = 0; j <= 8; ++j) {
+#pragma unroll
+    for (int i = 0; i <= j; ++i) acc = f29_mad(a.n[i], b.n[j - i], acc);
+#pragma unroll
+    for (int i = 0; i <= j; ++i) acc = f29_mad(c.n[i], d.n[j - i], acc);
+    acc = f29_mad(t[j], kr0, acc);
+    if (j >= 1) acc = f29_mad(t[j - 1], kr1, acc);
+    acc = ex(j, acc, kk);
+    o.n[j] = (u32)acc & F29_M;
+    acc >>= 29;
+  }
+  acc = f29_mad(t[8], kr1, acc);
+  const u32 clo = (u32)acc, chi = (u32)(acc >> 32);
+  u64 x = f29_mad(clo, kr0, (u64)o.n[0]);
+  o.n[0] = (u32)x & F29_M;
+  x = (x >> 29) + o.n[1];
+  x = f29_mad(clo, kr1, x);
+  x = f29_mad(chi, F29_RH1, x);
+  o.n[1] = (u32)x & F29_M;
+  o.n[2] = f29_add32(o.n[2], f29_add32((u32)(x >> 29), chi * F29_RH2));
+  r = o;
+}
+
 // r = a * b (+ extras).  mag(a) * mag(b) <= 6.
 template <class EX = f29x_none>
 GV_DEV void f29x_mul(fe29& r, const fe29& a, const fe29& b, const EX& ex = EX()) {

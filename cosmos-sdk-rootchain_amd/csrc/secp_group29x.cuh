@@ -60,7 +60,6 @@ GV_DEV void gej29x_add_scaled(gej29& a, bool& inf, const fe29& x, const fe29& y,
     f29x_mul(h3, h2, h);                       // H^3: 1
     f29x_mul(v, a.x, h2);                      // V = X1 H^2: 1
     f29x_mul(a.z, a.z, h);                     // Z3 = Z1 H: 1   (2 x 1)
-    f29x_mul(yh, a.y, h3);                     // Y1 H^3: 1
 #pragma unroll
     for (int i = 0; i < 9; ++i)                // -(2V + H^3): K_3 - 3 -> 4
       w.n[i] = f29_kneg(3, i) - f29_add32(v.n[i] << 1, h3.n[i]);
@@ -68,8 +67,8 @@ GV_DEV void gej29x_add_scaled(gej29& a, bool& inf, const fe29& x, const fe29& y,
     f29x_sqr_d(a.x, rr, d, f29x_plus<1>{w.n}); // X3 = R^2 - H^3 - 2V: 1
     fe29 t;
     f29_sub<1>(t, v, a.x);                     // V - X3: 3
-    f29_neg<1>(yh, yh);                        // -Y1 H^3: 2
-    f29x_mul(a.y, rr, t, f29x_plus<1>{yh.n});  // Y3 = R(V - X3) - Y1 H^3: 1  (1 x 3)
+    f29_neg<1>(yh, a.y);                       // -Y1: 2
+    f29x_mul2(a.y, rr, t, yh, h3);             // Y3 = R(V - X3) + (-Y1) H^3: 1  (1 x 3 + 2 x 1)
   }
   if (dbl) gej29x_double(a, a);                // a == b: 2a (a untouched above)
 }

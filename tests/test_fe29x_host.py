@@ -46,6 +46,21 @@ def test_mul_with_extras(lib, ma, mb):
             assert is_mag(r, 1), [hex(x) for x in r]
 
 
+@pytest.mark.parametrize("ma,mb,mc,md", [(1, 3, 2, 1), (1, 1, 1, 1), (2, 1, 1, 4), (1, 5, 1, 1), (3, 1, 1, 3)])
+def test_mul2_sum_of_products(lib, ma, mb, mc, md):
+    rng = random.Random(ma * 1000 + mb * 100 + mc * 10 + md)
+    for it in range(500):
+        a, b, c, d = (rand_mag(rng, m, rng.choice(STYLES)) for m in (ma, mb, mc, md))
+        e = rand_mag(rng, 2, rng.choice(STYLES))
+        for mode in (0, 1):
+            r = (ctypes.c_uint32 * 9)()
+            lib.f29xh_mul2(arr(a), arr(b), arr(c), arr(d), arr(e), mode, r)
+            r = list(r)
+            want = val(a) * val(b) + val(c) * val(d) + (8 * val(e) if mode else 0)
+            assert val(r) % P == want % P, (mode, it)
+            assert is_mag(r, 1), [hex(x) for x in r]
+
+
 @pytest.mark.parametrize("m", [1, 2])
 def test_sqr_with_extras(lib, m):
     rng = random.Random(70 + m)

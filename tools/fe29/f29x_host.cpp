@@ -34,6 +34,14 @@ void f29xh_sqr(const u32* a, const u32* c, int mode, u32* r) {
   }
   st(r, z);
 }
+// a*b + c*d (+ 8*e when mode)
+void f29xh_mul2(const u32* a, const u32* b, const u32* c, const u32* d, const u32* e, int mode, u32* r) {
+  fe29 x, y, z, w, v, o;
+  ld(x, a); ld(y, b); ld(z, c); ld(w, d); ld(v, e);
+  if (mode) f29x_mul2(o, x, y, z, w, f29x_plus<8>{v.n});
+  else f29x_mul2(o, x, y, z, w);
+  st(r, o);
+}
 // in/out: X, Y, Z raw limbs (27 words)
 void g29xh_double(const u32* in, u32* out) {
   gej29 p;
