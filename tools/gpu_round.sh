@@ -24,9 +24,9 @@ if has bench; then
 fi
 if has prof; then
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof" -o run \
-      --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-latency --no-extras \
+      --output-format csv -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-latency --no-extras \
       > "$ROOT/$OUT/bench_prof.json" 2> "$ROOT/$OUT/bench_prof.err" ) || { echo "rocprof failed"; tail -30 "$OUT/bench_prof.err"; exit 1; }
-  find "$OUT/prof" -name "*kernel_stats*"
+  python3 tools/prof_timed.py "$OUT/prof/run_kernel_trace.csv" 5 "$OUT/prof/kernel_timed.csv"
 fi
 if has parity && [ "$M" -gt 0 ]; then
   GV_PARITY_MILLIONS=$M GV_PARITY_OUT="$OUT/parity.json" timeout -k 10 1000 python -u -m pytest tests/test_parity_large.py \
