@@ -520,7 +520,8 @@ void add_signer(std::vector<Span>& signers, Span a) {   // StdTx.GetSigners(): d
 // Appends the JSON to o, the signer to signers.
 void decode_msg_send(Span body, std::string& o, std::vector<Span>& signers) {
   Span from, to;
-  std::string coins;
+  thread_local std::string coins;                 // scratch: capacity reused across txs
+  coins.clear();
   CoinsJson cj(coins);
   static const FSpec spec[] = {{1, 2, false}, {2, 2, false}, {3, 2, true}};
   for_fields(body, spec, [&](uint32_t f, Reader& r) {
@@ -605,8 +606,9 @@ std::shared_ptr<Tx> decode_tx(const uint8_t* p, size_t n, bool copy) {
   tx->raw = Span{p, n};
   if (n < 4 || memcmp(p, kStdTx.p, 4))
     throw AminoErr("UnmarshalBinaryBare expected to read prefix bytes (since it is registered concrete)");
-  std::string msgs, fee;
-  msgs.reserve(256);
+  thread_local std::string msgs, fee;             // scratch: capacity reused across txs
+  msgs.clear();
+  fee.clear();
   CoinsJson fj(fee);
   bool first_msg = true;
   Span memo;
@@ -644,7 +646,8 @@ std::shared_ptr<Tx> decode_tx(const uint8_t* p, size_t n, bool copy) {
   std::string& t = tx->sb_tail;
   t.reserve(64 + fee.size() + msgs.size() + memo.n);
   t = ",\"fee\":{\"amount\":";
-  t += fj.any ? fee + "]" : std::string("[]");
+  if (fj.any) { t += fee; t += ']'; }
+  else t += "[]";
   t += ",\"gas\":\"";
   t += std::to_string(tx->gas);
   t += "\"},\"memo\":";
@@ -784,9 +787,24 @@ struct CompactBitArray {
     return c;
   }
 };
+// Inline storage for the first N elements (a multisig's signatures: no heap
+// allocation per decode for up to N sub-signatures).
+template <class T, size_t N>
+struct SmallVec {
+  T inl[N];
+  size_t n = 0;
+  std::vector<T> more;
+  void push_back(const T& v) {
+    if (n < N) inl[n] = v;
+    else more.push_back(v);
+    ++n;
+  }
+  size_t size() const { return n; }
+  const T& operator[](size_t i) const { return i < N ? inl[i] : more[i - N]; }
+};
 struct Multisignature {
   CompactBitArray bits;
-  std::vector<Span> sigs;
+  SmallVec<Span, 16> sigs;
 };
 Multisignature decode_multisig(Span s) {
   Multisignature m;
@@ -894,7 +912,8 @@ struct Leaf {
   std::array<uint8_t, 33> pub{};          // secp: 33 bytes; ed: first 32
   std::array<uint8_t, 64> sig{};
   H32 dig{};                              // SHA256(signBytes)
-  H32 key{};                              // verdict-cache key
+  H32 key{};                              // verdict-cache key (computed when first needed)
+  bool keyed = false;
   int verdict = -1;
   std::shared_ptr<const std::string> msg; // ed25519: the sign bytes (SHA-512 runs over them)
 };
@@ -905,6 +924,7 @@ void leaf_key(Leaf& L) {
   h.up(L.sig.data(), 64);
   h.up(L.dig.data(), 32);
   L.key = h.fin();
+  L.keyed = true;
 }
 
 // Verification expression for one signer: tendermint VerifyBytes semantics.
@@ -932,8 +952,7 @@ Node build_node(const PubKey& pk, const H32& dig, Span sig, std::vector<Leaf>& l
       if (L.kind) memcpy(L.pub.data(), pk.ed.data(), 32);
       else L.pub = pk.secp;
       memcpy(L.sig.data(), sig.p, 64);
-      L.dig = dig;
-      leaf_key(L);
+      L.dig = dig;                                    // key: leaf_key() on first cache use
       n.op = Node::LeafRef;
       n.leaf = (int)leaves.size();
       leaves.push_back(L);
@@ -1477,6 +1496,19 @@ void make_plan(SignerPlan& p, gvh_app* app, const Tx& tx, size_t signer, std::sh
   p.ok = true;
 }
 
+// Verdict-cache lookup / insert of one leaf.  The key (three SHA-256 blocks)
+// is computed only when the cache is used: a lookup in an empty cache is a
+// miss without hashing (block replay with no CheckTx history).
+int cache_lookup(gvh_app* app, Leaf& L) {
+  if (app->cache.size() == 0) return -1;
+  if (!L.keyed) leaf_key(L);
+  return app->cache.get(L.key);
+}
+void cache_insert(gvh_app* app, Leaf& L, bool v) {
+  if (!L.keyed) leaf_key(L);
+  app->cache.put(L.key, v);
+}
+
 // Resolve leaves: cache first, the secp256k1 misses in ONE GPU batch.
 int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint32_t* hits, bool all_miss = false,
             bool fill = true) {
@@ -1486,7 +1518,7 @@ int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint
   } else if (leaves.size() >= 4096) {                        // big batches: lookups on the pool
     parallel_for(app, leaves.size(), [&](size_t i) {
       Leaf* L = leaves[i];
-      if (L->verdict < 0) L->verdict = app->cache.get(L->key);
+      if (L->verdict < 0) L->verdict = cache_lookup(app, *L);
     });
     for (Leaf* L : leaves)
       if (L->verdict < 0) miss.push_back(L);
@@ -1494,7 +1526,7 @@ int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint
   } else {
     for (Leaf* L : leaves) {
       if (L->verdict >= 0) { if (hits) ++*hits; continue; }
-      const int v = app->cache.get(L->key);
+      const int v = cache_lookup(app, *L);
       if (v >= 0) { L->verdict = v; if (hits) ++*hits; }
       else miss.push_back(L);
     }
@@ -1557,7 +1589,7 @@ int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint
   if (fill)
     parallel_for(app, mt, [&](size_t k) {
       miss[k]->verdict = ok[k];
-      app->cache.put(miss[k]->key, ok[k] != 0);
+      cache_insert(app, *miss[k], ok[k] != 0);
     });
   else
     for (size_t k = 0; k < mt; ++k) miss[k]->verdict = ok[k];
@@ -1933,7 +1965,7 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
       return;
     }
     for (Leaf& L : j.plan->leaves) {
-      if (L.verdict < 0) L.verdict = app->cache.get(L.key);
+      if (L.verdict < 0) L.verdict = cache_lookup(app, L);
       if (L.verdict < 0) wmiss[w].push_back(&L);
     }
     n_leaf.fetch_add(j.plan->leaves.size(), std::memory_order_relaxed);
