@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -435,6 +436,7 @@ struct gv_ctx {
   bool fault_inject = false;
   bool keyed_k4 = true;         // keyed batches on k_ecmult_k4 (GV_KEYED_K4=0: the 125-doubling ladder, A/B)
   size_t keys = 0;              // key-arena slots in use (same on every device)
+  std::atomic<uint64_t> keys_gen{0};  // gv_keys_reset calls
   std::mutex keys_mu;
 };
 
@@ -991,10 +993,12 @@ int gv_keys_reset(gv_ctx* ctx) {
   if (!ctx) return GV_EINVAL;
   std::lock_guard<std::mutex> kl(ctx->keys_mu);
   ctx->keys = 0;
+  ctx->keys_gen.fetch_add(1);
   return GV_OK;
 }
 
 size_t gv_keys_count(const gv_ctx* ctx) { return ctx ? ctx->keys : 0; }
+uint64_t gv_keys_generation(const gv_ctx* ctx) { return ctx ? ctx->keys_gen.load() : 0; }
 
 int gv_keys_point(gv_ctx* ctx, size_t n, const uint32_t* slots, uint8_t* out_xy64, uint8_t* out_ok) {
   if (!ctx) return GV_EINVAL;

@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "gv_open", "gv_close", "gv_num_devices", "gv_verify_msgs", "gv_verify_digests",
     "gv_verify_digests_bits", "gv_verify_msgs_bits", "gv_dev_verify_digests", "gv_dev_verify_msgs",
     "gv_set_option", "gv_last_stage_ms", "gv_strerror", "gv_debug_op", "gv_dev_alloc", "gv_dev_free",
-    "gv_dev_copy", "gv_dev_sync", "gv_stage_stats", "gv_keys_load", "gv_keys_reset", "gv_keys_count",
+    "gv_dev_copy", "gv_dev_sync", "gv_stage_stats", "gv_keys_load", "gv_keys_reset", "gv_keys_count", "gv_keys_generation",
     "gv_verify_digests_keyed", "gv_verify_msgs_keyed", "gv_dev_verify_digests_keyed", "gv_stage_stats4",
     "gv_keys_point", "gv_dev_stream_create", "gv_dev_stream_sync", "gv_dev_stream_destroy",
     "gv_verify_ed25519_msgs", "gv_dev_verify_ed25519_msgs",
@@ -117,6 +117,8 @@ def load(path: str = LIB_PATH):
     L.gv_keys_reset.restype = i32
     L.gv_keys_count.argtypes = [vp]
     L.gv_keys_count.restype = sz
+    L.gv_keys_generation.argtypes = [vp]
+    L.gv_keys_generation.restype = ctypes.c_uint64
     L.gv_keys_point.argtypes = [vp, sz, vp, vp, vp]
     L.gv_keys_point.restype = i32
     L.gv_verify_digests_keyed.argtypes = [vp, sz, vp, vp, vp, vp]

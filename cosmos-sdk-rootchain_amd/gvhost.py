@@ -61,6 +61,7 @@ def lib():
         L.gvh_consume_sig_gas.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p, sz, u64, ctypes.POINTER(Result)]
         L.gvh_cache_clear.argtypes = [vp]
         L.gvh_set_threads.argtypes = [vp, ctypes.c_int]
+        L.gvh_set_keyed.argtypes = [vp, ctypes.c_int, ctypes.c_size_t]
         L.gvh_cache_size.argtypes = [vp]
         L.gvh_cache_size.restype = sz
         L.gvh_std_sign_bytes.argtypes = [ctypes.c_char_p, u64, u64, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p),
@@ -228,6 +229,11 @@ class HostApp:
 
     def set_threads(self, n: int):
         self._L.gvh_set_threads(self._app, n)
+
+    def set_keyed(self, keyed: bool, load_min: int = 4096):
+        """secp256k1 leaves through the GPU context's key arena (default; keys loaded by
+        batches of >= load_min leaves) or as pub33 batches."""
+        self._L.gvh_set_keyed(self._app, 1 if keyed else 0, load_min)
 
     def cache_size(self) -> int:
         return self._L.gvh_cache_size(self._app)

@@ -1297,6 +1297,21 @@ struct gvh_app {
   PubCache pubs;
   Window window;
   std::mutex gpu_mu;                           // one GPU batch at a time per app
+  // account key cache: pub33 -> key-arena slot of the GPU
+  // context (gv_keys_load); guarded by gpu_mu.  keyed = 0: pub33 batches.
+  struct Key33Hash {
+    size_t operator()(const std::array<uint8_t, 33>& k) const {
+      uint64_t h;
+      memcpy(&h, k.data() + 1, 8);                // x-coordinate bytes
+      return (size_t)h;
+    }
+  };
+  std::unordered_map<std::array<uint8_t, 33>, uint32_t, Key33Hash> key_slots;
+  uint64_t key_gen = 0;                        // gv_keys_generation the map belongs to
+  bool keyed = true;
+  size_t key_cap = size_t(1) << 22;            // arena reset past this many keys (5.4 KB of HBM each)
+  size_t key_load_min = 4096;                  // smaller batches never load keys (k_keys_build's ~ms latency):
+                                               // keyed only when all their keys are resident
   int threads = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
   std::unique_ptr<Pool> pool{new Pool(threads - 1)};
   std::mutex pool_mu;                          // guards replacing the pool (gvh_set_threads)
@@ -1509,6 +1524,71 @@ void cache_insert(gvh_app* app, Leaf& L, bool v) {
   app->cache.put(L.key, v);
 }
 
+// m secp256k1 digests -> verdicts (gpu_mu held).  Keyed: every key is looked
+// up in the app's slot map (parallel reads), the keys not seen before are
+// parsed into the context's key arena with ONE gv_keys_load (batches of at
+// least key_load_min leaves -- a block; a smaller batch with an unknown key
+// takes the pub33 path rather than wait on k_keys_build), and the batch
+// runs gv_verify_digests_keyed -- the same verdicts as the pub33 path (a key
+// ParsePubKey rejects keeps a false slot), without the per-item decompression
+// and Q-table build, on the 4-group ladder.  Any arena problem (cap reached,
+// load error) falls back to the pub33 batch for this call.
+int verify_secp(gvh_app* app, size_t m, const uint8_t* pub, const uint8_t* sig, const uint8_t* dig, uint8_t* ok) {
+  if (!app->keyed) return gv_verify_digests(app->gpu, m, pub, sig, dig, ok);
+  constexpr uint32_t kPending = 0x80000000u;      // map value of a key queued for this call's load
+  std::vector<uint32_t> slots(m);
+  auto& map = app->key_slots;
+  const uint64_t gen = gv_keys_generation(app->gpu);
+  if (gen != app->key_gen) {                      // the arena was reset (here or by another user)
+    map.clear();
+    app->key_gen = gen;
+  }
+  parallel_for(app, m, [&](size_t k) {
+    std::array<uint8_t, 33> key;
+    memcpy(key.data(), pub + 33 * k, 33);
+    auto it = map.find(key);
+    slots[k] = it == map.end() ? UINT32_MAX : it->second;
+  });
+  if (m < app->key_load_min) {                    // small batch (CheckTx window, per-tx ante)
+    bool all = true;
+    for (size_t k = 0; k < m && all; ++k) all = slots[k] != UINT32_MAX;
+    if (!all) return gv_verify_digests(app->gpu, m, pub, sig, dig, ok);
+  }
+  std::vector<uint8_t> fresh;
+  std::vector<std::array<uint8_t, 33>> fresh_keys;
+  for (size_t k = 0; k < m; ++k) {
+    if (slots[k] != UINT32_MAX) continue;
+    std::array<uint8_t, 33> key;
+    memcpy(key.data(), pub + 33 * k, 33);
+    auto ins = map.emplace(key, kPending + (uint32_t)fresh_keys.size());
+    if (ins.second) {
+      fresh.insert(fresh.end(), key.begin(), key.end());
+      fresh_keys.push_back(key);
+    }
+    slots[k] = ins.first->second;
+  }
+  if (!fresh_keys.empty()) {
+    const size_t nf = fresh_keys.size();
+    std::vector<uint32_t> got(nf);
+    const bool room = gv_keys_count(app->gpu) + nf <= app->key_cap;
+    if (!room || gv_keys_load(app->gpu, nf, fresh.data(), got.data()) != GV_OK) {
+      if (!room) {                                  // start the arena over; this call takes the pub33 path
+        gv_keys_reset(app->gpu);
+        map.clear();
+        app->key_gen = gv_keys_generation(app->gpu);
+      } else {
+        for (auto& key : fresh_keys) map.erase(key);
+      }
+      return gv_verify_digests(app->gpu, m, pub, sig, dig, ok);
+    }
+    for (size_t i = 0; i < nf; ++i) map[fresh_keys[i]] = got[i];
+    parallel_for(app, m, [&](size_t k) {
+      if (slots[k] >= kPending) slots[k] = got[slots[k] - kPending];
+    });
+  }
+  return gv_verify_digests_keyed(app->gpu, m, slots.data(), sig, dig, ok);
+}
+
 // Resolve leaves: cache first, the secp256k1 misses in ONE GPU batch.
 int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint32_t* hits, bool all_miss = false,
             bool fill = true) {
@@ -1574,7 +1654,7 @@ int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint
   {
     std::lock_guard<std::mutex> g(app->gpu_mu);
     rlap("pack");
-    if (m && gv_verify_digests(app->gpu, m, pub.data(), sig.data(), dig.data(), ok.data()) != GV_OK)
+    if (m && verify_secp(app, m, pub.data(), sig.data(), dig.data(), ok.data()) != GV_OK)
       return GVH_EDEVICE;
     if (me && gv_verify_ed25519_msgs(app->gpu, me, epub.data(), esig.data(), eblob.empty() ? nullptr : eblob.data(),
                                      eoff.data(), elen.data(), eok.data()) != GV_OK)
@@ -2260,6 +2340,12 @@ void gvh_cache_clear(gvh_app* app) {
 }
 size_t gvh_cache_size(gvh_app* app) { return app->cache.size(); }
 void gvh_set_cache_capacity(gvh_app* app, size_t entries) { app->cache.resize(std::max<size_t>(entries, 512)); }
+
+void gvh_set_keyed(gvh_app* app, int keyed, size_t load_min) {
+  std::lock_guard<std::mutex> g(app->gpu_mu);
+  app->keyed = keyed != 0;
+  app->key_load_min = load_min;
+}
 
 void gvh_set_threads(gvh_app* app, int threads) {
   if (!app) return;

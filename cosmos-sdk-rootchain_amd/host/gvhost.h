@@ -137,6 +137,14 @@ void gvh_set_cache_capacity(gvh_app* app, size_t entries);
 /* Host threads for PreVerifyTxs' decode / sign-bytes / SHA-256 stages
  * (default min(16, hardware threads)). */
 void gvh_set_threads(gvh_app* app, int threads);
+/* keyed = 1 (default): secp256k1 leaves verified through the GPU context's
+ * key arena (gv_verify_digests_keyed); keys not yet resident are loaded
+ * (gv_keys_load, once per distinct key) by batches of at least load_min
+ * leaves (default 4096: blocks), and a smaller batch with an unknown key
+ * takes the pub33 path.  keyed = 0: pub33 batches (gv_verify_digests).  Same
+ * verdicts either way.  While keyed, the app owns the context's key arena
+ * (a gv_keys_reset elsewhere is detected by gv_keys_generation). */
+void gvh_set_keyed(gvh_app* app, int keyed, size_t load_min);
 void gvh_get_stats(gvh_app* app, gvh_stats* out);
 
 /* StdSignBytes (x/auth/types/stdtx.go:292-312): canonical JSON.  Returns the

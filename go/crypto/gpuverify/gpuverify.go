@@ -83,8 +83,9 @@ type GPU struct {
 	// below the measured crossover a VerifyBytes loop answers first.
 	CPUBelow int
 
-	mu    sync.Mutex
-	slots map[secp256k1.PubKeySecp256k1]uint32 // key -> key-arena slot (gv_keys_load)
+	mu      sync.Mutex
+	slots   map[secp256k1.PubKeySecp256k1]uint32 // key -> key-arena slot (gv_keys_load)
+	slotGen uint64                               // gv_keys_generation the slot map belongs to
 }
 
 var (
@@ -252,6 +253,11 @@ func (g *GPU) VerifyBatchRouted(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][
 func (g *GPU) slotsFor(pubs []secp256k1.PubKeySecp256k1) (slots []uint32, loaded []bool) {
 	g.mu.Lock()
 	defer g.mu.Unlock()
+	if gen := uint64(C.gv_keys_generation(g.ctx)); gen != g.slotGen {
+		// the arena was reset elsewhere: every cached slot may name another key now
+		g.slots = map[secp256k1.PubKeySecp256k1]uint32{}
+		g.slotGen = gen
+	}
 	slots = make([]uint32, len(pubs))
 	loaded = make([]bool, len(pubs))
 	var fresh []secp256k1.PubKeySecp256k1
@@ -293,6 +299,7 @@ func (g *GPU) ResetKeys() {
 	defer g.mu.Unlock()
 	C.gv_keys_reset(g.ctx)
 	g.slots = map[secp256k1.PubKeySecp256k1]uint32{}
+	g.slotGen = uint64(C.gv_keys_generation(g.ctx))
 }
 
 // VerifyBatchKeyed is VerifyBatch with the keys kept parsed in HBM: every

@@ -112,13 +112,19 @@ int gv_dev_stream_destroy(gv_ctx* ctx, int dev_slot, void* stream);
  * node verifies the same accounts block after block.  gv_keys_load parses n
  * SEC1 keys once (prefix, x < p, square root) and keeps each key's table of
  * 16 multiples resident in HBM on every device of the context (1,280 B per
- * key: 1M accounts = 1.3 GB of the 288 GB); slot_out[i] receives key i's slot.
+ * key, plus the tables of 2^35 Q, 2^70 Q, 2^100 Q for the 30-doubling keyed
+ * ladder: 5.4 KB per key, 1M accounts = 5.4 GB of the 288 GB); slot_out[i]
+ * receives key i's slot.
  * A key that ParsePubKey rejects gets a slot too, and every verify against it
  * is false.  Slots are assigned in load order and stay valid until
  * gv_keys_reset.  Loading must not race keyed verifies of the same context. */
 int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out);
 int gv_keys_reset(gv_ctx* ctx);
 size_t gv_keys_count(const gv_ctx* ctx);
+/* Number of gv_keys_reset calls on ctx so far: a caller that keeps a
+ * pubkey -> slot map drops it when the generation moved (slots of an older
+ * generation may name other keys). */
+uint64_t gv_keys_generation(const gv_ctx* ctx);
 
 /* Key-arena readback (tests, tools): for each slot, the affine point the
  * arena holds for it, out_xy64 + 64*i = x || y (32 bytes each, big-endian),

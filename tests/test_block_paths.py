@@ -174,6 +174,45 @@ def test_c4_multisig_block_replay(ver):
     app.close()
 
 
+def test_keyed_and_pub33_block_paths_agree_across_arena_resets(ver):
+    """The host mirror's keyed resolve (gv_keys_load + gv_verify_digests_keyed,
+    the default) and the pub33 batches give the same result tx by tx, block
+    after block; an arena reset by another user of the context between blocks
+    (gv_keys_generation moves) makes the app drop its slot map instead of
+    verifying against stale slots."""
+    rng = random.Random(0xE7)
+    shapes = [(2, 3, False), (3, 5, False), (4, 7, True)]
+    accts = [MultiAcct(200 + i, *shapes[i % len(shapes)]) for i in range(9)]
+    sink_addr = T.address(SecpKey(b"sink-k").amino)
+    apps = {}
+    # keyed with every batch loading its new keys; keyed with the default
+    # threshold (these 200-tx blocks stay below it: pub33 for unknown keys);
+    # pub33 only
+    for name, keyed, load_min in (("load", True, 0), ("default", True, 4096), ("pub33", False, 0)):
+        app = gvhost.HostApp(ver, chain_id=CHAIN, height=6)
+        app.set_keyed(keyed, load_min=load_min)
+        for a in accts:
+            app.set_account(a.addr, a.number, 0)
+        apps[name] = app
+    seqs = {a.addr: 0 for a in accts}
+    strip = lambda r: (r["code"], r["log"], r["gas_used"], r["gas_wanted"])
+    for blk in range(4):
+        txs, parts = build_block(accts, seqs, rng, 200, sink_addr)
+        rc1, r1 = apps["load"].deliver_block(txs)
+        rc2, r2 = apps["default"].deliver_block(txs)
+        rc0, r0 = apps["pub33"].deliver_block(txs)
+        assert rc1 == 0 and rc2 == 0 and rc0 == 0
+        assert [strip(r) for r in r1] == [strip(r) for r in r0]
+        assert [strip(r) for r in r2] == [strip(r) for r in r0]
+        check_block(r1, parts, seqs)
+        if blk == 1:
+            ver.keys_reset()
+            ver.keys_load(np.frombuffer(bytes([2]) + bytes(range(1, 33)), np.uint8).reshape(1, 33))
+    assert sum(r["code"] == 0 for r in r1) > 100
+    for app in apps.values():
+        app.close()
+
+
 def test_deliver_block_equals_plain_ante(ver):
     """Same block through DeliverBlock (pre-verified, memoised) and through the
     per-tx ante with no pre-verification: identical results tx by tx."""
