@@ -31,6 +31,12 @@
 #pragma once
 #include "secp_fe29.cuh"
 
+// GV_F29X_HICARRY: high columns split as lo + 2^32 hi, hi re-entering the next
+// column by one mad (1), or the classic 29-bit extraction (0).
+#ifndef GV_F29X_HICARRY
+#define GV_F29X_HICARRY 1
+#endif
+
 // member functions: GV_DEV is "static inline" in host builds
 #if defined(__HIPCC__)
 #define GV_DEVM __device__ __forceinline__
@@ -79,6 +85,7 @@ GV_DEV void f29x_core(fe29& r, const u32* a, const u32* dg, const u32* cr, const
 #endif
 #define F29X_OP(i, j) (SQR ? ((i) == (j) ? dg[i] : cr[j]) : dg[j])
   u32 t[9];
+#if GV_F29X_HICARRY
   u32 hi = 0;
 #pragma unroll
   for (int k = 9; k <= 16; ++k) {
@@ -91,6 +98,20 @@ GV_DEV void f29x_core(fe29& r, const u32* a, const u32* dg, const u32* cr, const
   }
   F29_TRAP(hi >= (1u << 29), "x t17");
   t[8] = hi << 3;                             // limb 17
+#else
+  {
+    u64 acc = 0;                              // classic: 29-bit high limbs, carry chained
+#pragma unroll
+    for (int k = 9; k <= 16; ++k) {
+#pragma unroll
+      for (int i = k - 8; i <= (SQR ? (k >> 1) : 8); ++i) acc = f29_mad(a[i], F29X_OP(i, k - i), acc);
+      t[k - 9] = (u32)acc & F29_M;
+      acc >>= 29;
+    }
+    F29_TRAP((acc >> 32) != 0, "x t17");
+    t[8] = (u32)acc;                          // limb 17
+  }
+#endif
   fe29 o;
   u64 acc = 0;
 #pragma unroll
@@ -127,6 +148,7 @@ GV_DEV void f29x_mul2(fe29& r, const fe29& a, const fe29& b, const fe29& c, cons
   asm("" : "+v"(kk.one), "+v"(kk.eight));
 #endif
   u32 t[9];
+#if GV_F29X_HICARRY
   u32 hi = 0;
 #pragma unroll
   for (int k = 9; k <= 16; ++k) {
@@ -141,6 +163,22 @@ GV_DEV void f29x_mul2(fe29& r, const fe29& a, const fe29& b, const fe29& c, cons
   }
   F29_TRAP(hi >= (1u << 29), "x2 t17");
   t[8] = hi << 3;
+#else
+  {
+    u64 acc = 0;
+#pragma unroll
+    for (int k = 9; k <= 16; ++k) {
+#pragma unroll
+      for (int i = k - 8; i <= 8; ++i) acc = f29_mad(a.n[i], b.n[k - i], acc);
+#pragma unroll
+      for (int i = k - 8; i <= 8; ++i) acc = f29_mad(c.n[i], d.n[k - i], acc);
+      t[k - 9] = (u32)acc & F29_M;
+      acc >>= 29;
+    }
+    F29_TRAP((acc >> 32) != 0, "x2 t17");
+    t[8] = (u32)acc;
+  }
+#endif
   fe29 o;
   u64 acc = 0;
 #pragma unroll

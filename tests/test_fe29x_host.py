@@ -18,11 +18,11 @@ GX = 0x79BE667EF9DCBBAC55A06295CE870B07029BFCDB2DCE28D959F2815B16F81798
 GY = 0x483ADA7726A3C4655DA4FBFC0E1108A8FD17B448A68554199C47D08FFB10D4B8
 
 
-@pytest.fixture(scope="module")
-def lib():
+@pytest.fixture(scope="module", params=[1, 0], ids=["hicarry-mad", "hicarry-classic"])
+def lib(request):
     d = tempfile.mkdtemp()
-    so = os.path.join(d, "f29x.so")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", so, SRC], check=True)
+    so = os.path.join(d, f"f29x_{request.param}.so")
+    subprocess.run(["g++", "-O2", "-std=c++17", f"-DGV_F29X_HICARRY={request.param}", "-shared", "-fPIC", "-o", so, SRC], check=True)
     return ctypes.CDLL(so)
 
 
