@@ -148,9 +148,17 @@ def c2_key_cache(ver, pub, sig, dig, exp, nkeys: int, steps: int = 5):
     for p in d + [d_bits]:
         ver.dev_free(p)
     ver.keys_reset()
+    # k_ecmult_k4's work: the ladder's W with 95 of the 129 survey doublings gone (30 instead of 125)
+    import bench as B
+    w_k4 = B.W_LADDER - 95 * (2 * B.FM + 5 * B.FS)
+    ems = stages.get("ecmult_ms") or 0.0
+    ach = n * w_k4 / (ems * 1e-3) / 1e12 if ems else 0.0
     return {"items": n, "keys": nkeys, "value": round(n * steps / el, 1), "unit": "verifies/s",
             "keys_load_ms": round(t_load * 1e3, 2), "mismatches": int(np.count_nonzero(got != exp)),
             "stages": stages,
+            "roofline": {"kernel": "k_ecmult_k4", "work_per_verify": w_k4, "kernel_ms": ems,
+                         "achieved_T": round(ach, 3), "peak_T": round(B.P_MUL_COMMITTED / 1e12, 3),
+                         "frac": round(ach * 1e12 / B.P_MUL_COMMITTED, 4)},
             "note": "keys parsed once into the HBM key arena (Q, 2^35 Q, 2^70 Q, 2^100 Q tables on one Z: 5.4 KB "
                     "per key); items verified by slot on the 4-group ladder (k_ecmult_k4: 30 doublings)"}
 
