@@ -476,8 +476,17 @@ GV_DEV bool parse_pubkey(u32 pre, const fe& x, fe& y) {
 // KEYED = true: the item's key is slot kslot[g] of the key arena (gv_keys_load:
 // parsed once, table resident); an out-of-range slot or a rejected key makes
 // the item false.  qidx[g] receives the (clamped) slot for k_ecmult.
+// GV_PREP_WAVES: minimum waves per SIMD for k_prep (0 = compiler's choice; A/B)
+#ifndef GV_PREP_WAVES
+#define GV_PREP_WAVES 0
+#endif
+#if GV_PREP_WAVES
+#define GV_PREP_ATTR __attribute__((amdgpu_waves_per_eu(GV_PREP_WAVES)))
+#else
+#define GV_PREP_ATTR
+#endif
 template <bool KEYED>
-__global__ __launch_bounds__(256) void k_prep(u32 C, u32 n, const u32* in_x, const u32* in_pfx,
+__global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u32* in_x, const u32* in_pfx,
                                                const u32* in_r, const u32* in_s, const u32* in_e,
                                                const u32* in_w, u32* digits, u32* qt, u32* zq_out,
                                                u32* flags, const u32* kslot, const u32* kok, u32 kcount,
