@@ -28,6 +28,7 @@
 #include "secp_field.cuh"
 #include "secp_scalar.cuh"
 #include "secp_group29.cuh"
+#include "secp_group29x.cuh"
 #include "secp_sc29.cuh"
 #include "secp_modinv.cuh"
 #include "gv_kernels.h"
@@ -425,6 +426,52 @@ GV_DEV void shfl_xor_gej(gej29& o, bool& oinf, const gej29& a, bool ainf, int m)
   oinf = __shfl_xor((int)ainf, m, 64) != 0;
 }
 
+// GV_LAT_FUSED: the latency ladders on the fused formulas (secp_group29x.cuh,
+// two mad chains per column in this translation unit: F29X_NCH = 2); 0 = the
+// secp_group29.cuh formulas with lockstep product pairs.
+#ifndef GV_LAT_FUSED
+#define GV_LAT_FUSED 1
+#endif
+GV_DEV void lat_double(gej29& acc) {
+#if GV_LAT_FUSED
+  gej29x_double(acc, acc);
+#else
+  gej29_double(acc, acc);
+#endif
+}
+// acc += (x, y), an affine point of the lane's curve (y magnitude <= 2); an
+// infinite accumulator takes the point.
+GV_DEV void lat_add_affine(gej29& acc, bool& inf, const fe29& x, const fe29& y) {
+#if GV_LAT_FUSED
+  if (inf) {
+    acc.x = x;
+    f29_norm(acc.y, y);
+    f29_set_u32(acc.z, 1);
+    inf = false;
+  } else {
+    gej29x_add_scaled(acc, inf, x, y, acc.z);
+  }
+#else
+  fe29 az, z2, u2, s2;
+  if (inf) f29_set_u32(az, 1);
+  else az = acc.z;
+  f29_sqr(z2, az);
+  {
+    fe29 o[2];
+    const fe29 xa[2] = {x, z2}, ya[2] = {z2, az};
+    f29_multi<false, false>(o, xa, ya);
+    u2 = o[0]; z2 = o[1];
+  }
+  f29_mul(s2, y, z2);
+  if (inf) {
+    acc.x = u2; acc.y = s2; f29_set_u32(acc.z, 1); inf = false;
+  } else {
+    gej29_add_tail(acc, inf, u2, s2);
+  }
+#endif
+}
+
+
 // One block = GV_LAT_SIGS signatures, 128 threads.  Inputs: AoS bytes as in
 // gv_verify_digests; e from dig32 (digest path) or from the SoA rows e_soa
 // written by k_sha256 (message path, stride C).  Output: 16 verdict bits per
@@ -466,7 +513,7 @@ __global__ __launch_bounds__(128) void k_verify_lat(const u32* gtab, const uint8
   for (int win = GV_QWIN - 1; win >= 0; --win) {
     if (win != GV_QWIN - 1) {
 #pragma unroll 1
-      for (int d = 0; d < GV_QW; ++d) gej29_double(acc, acc);
+      for (int d = 0; d < GV_QW; ++d) lat_double(acc);
     }
     const bool gwin = (win % GV_GSTEP) == 0;          // block-uniform
     const u32 dq = sh.dq[sig][win];
@@ -489,22 +536,7 @@ __global__ __launch_bounds__(128) void k_verify_lat(const u32* gtab, const uint8
       if (d < 0) f29_neg<1>(y, y);
       // Q slots live on the isomorphic curve of the shared table Z, G slots on
       // the real curve: either way the entry is affine on the lane's curve.
-      fe29 az, z2, u2, s2;
-      if (inf) f29_set_u32(az, 1);
-      else az = acc.z;
-      f29_sqr(z2, az);
-      {
-        fe29 o[2];
-        const fe29 xa[2] = {x, z2}, ya[2] = {z2, az};
-        f29_multi<false, false>(o, xa, ya);
-        u2 = o[0]; z2 = o[1];
-      }
-      f29_mul(s2, y, z2);
-      if (inf) {
-        acc.x = u2; acc.y = s2; f29_set_u32(acc.z, 1); inf = false;
-      } else {
-        gej29_add_tail(acc, inf, u2, s2);
-      }
+      lat_add_affine(acc, inf, x, y);
     }
   }
 
@@ -615,7 +647,7 @@ __global__ __launch_bounds__(128) void k_verify_lat16(const gvk_lat b) {
   for (int win = w_hi; win >= w_lo; --win) {
     if (win != w_hi) {
 #pragma unroll 1
-      for (int d = 0; d < GV_QW; ++d) gej29_double(acc, acc);
+      for (int d = 0; d < GV_QW; ++d) lat_double(acc);
     }
     const u32 dw = part < 2 ? sh.dq[sig][win] : sh.dg5[sig][win];
     const int d = (part & 1) == 0 ? ((int)(dw << 16) >> 16) : ((int)dw >> 16);
@@ -640,22 +672,7 @@ __global__ __launch_bounds__(128) void k_verify_lat16(const gvk_lat b) {
         f29_from_words(y, wy);
       }
       if (d < 0) f29_neg<1>(y, y);
-      fe29 az, z2, u2, s2;
-      if (inf) f29_set_u32(az, 1);
-      else az = acc.z;
-      f29_sqr(z2, az);
-      {
-        fe29 o[2];
-        const fe29 xa[2] = {x, z2}, ya[2] = {z2, az};
-        f29_multi<false, false>(o, xa, ya);
-        u2 = o[0]; z2 = o[1];
-      }
-      f29_mul(s2, y, z2);
-      if (inf) {
-        acc.x = u2; acc.y = s2; f29_set_u32(acc.z, 1); inf = false;
-      } else {
-        gej29_add_tail(acc, inf, u2, s2);
-      }
+      lat_add_affine(acc, inf, x, y);
     }
   }
   // Q parts live on the isomorphic curve of their table's Z: back to the real curve

@@ -18,11 +18,16 @@ GX = 0x79BE667EF9DCBBAC55A06295CE870B07029BFCDB2DCE28D959F2815B16F81798
 GY = 0x483ADA7726A3C4655DA4FBFC0E1108A8FD17B448A68554199C47D08FFB10D4B8
 
 
-@pytest.fixture(scope="module", params=[1, 0], ids=["hicarry-mad", "hicarry-classic"])
+@pytest.fixture(scope="module", params=[(1, 1), (0, 1), (1, 2)],
+                ids=["hicarry-mad", "hicarry-classic", "two-chain"])
 def lib(request):
+    """Both high-column carry variants (throughput ladder) and the two-chain
+    accumulator of the latency kernels (F29X_NCH = 2)."""
+    hic, nch = request.param
     d = tempfile.mkdtemp()
-    so = os.path.join(d, f"f29x_{request.param}.so")
-    subprocess.run(["g++", "-O2", "-std=c++17", f"-DGV_F29X_HICARRY={request.param}", "-shared", "-fPIC", "-o", so, SRC], check=True)
+    so = os.path.join(d, f"f29x_{hic}_{nch}.so")
+    subprocess.run(["g++", "-O2", "-std=c++17", f"-DGV_F29X_HICARRY={hic}", f"-DF29X_NCH={nch}", "-shared",
+                    "-fPIC", "-o", so, SRC], check=True)
     return ctypes.CDLL(so)
 
 
