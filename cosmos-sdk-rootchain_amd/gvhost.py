@@ -17,7 +17,7 @@ import os
 import gpuverify as gvm
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libgvhost.so")
+LIB_PATH = os.environ.get("GVH_LIB") or os.path.join(HERE, "lib", "libgvhost.so")  # GVH_LIB: A/B builds
 
 GVH_OK, GVH_EINVAL, GVH_EDEVICE, GVH_ENOVERIFIER = 0, -1, -2, -3
 

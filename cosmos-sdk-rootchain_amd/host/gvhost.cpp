@@ -588,6 +588,15 @@ struct Tx {
   std::vector<Span> signers;        // StdTx.GetSigners(): msg signers, deduplicated in order
   std::string sb_tail;              // sign bytes after chain_id: ,"fee":..,"memo":..,"msgs":[..],"sequence":"
   Tx() = default;
+  void reset() {                    // for reuse (capacities kept)
+    own.clear();
+    raw = Span{};
+    nil_msg = false;
+    gas = 0;
+    sigs.clear();
+    signers.clear();
+    sb_tail.clear();
+  }
   Tx(const Tx&) = delete;
   Tx& operator=(const Tx&) = delete;
 };
@@ -596,8 +605,9 @@ struct Tx {
 // StdSignBytes (stdtx.go:292-312) pieces are built on the way: the StdSignDoc
 // keys are in sorted order and every embedded JSON is canonical, so composing
 // them equals MustSortJSON(amino.MarshalJSON(StdSignDoc{...})).
-std::shared_ptr<Tx> decode_tx(const uint8_t* p, size_t n, bool copy) {
-  auto tx = std::make_shared<Tx>();
+std::shared_ptr<Tx> decode_tx(const uint8_t* p, size_t n, bool copy, std::shared_ptr<Tx> tx = nullptr) {
+  if (tx) tx->reset();                              // a recycled Tx (PreVerifyTxs' per-worker pool)
+  else tx = std::make_shared<Tx>();
   if (n == 0) throw AminoErr("tx bytes are empty");
   if (copy) {
     tx->own.assign(p, p + n);
@@ -1218,6 +1228,26 @@ struct Memo {
   std::vector<SignerPlan> plans;
   std::vector<Account*> sacc;                        // PreVerifyTxs: each signer's account (null: none)
   int16_t owner = 0;                                 // pool worker that decoded it (release_memos)
+  void reset() {                                     // for reuse: every field as new, capacities kept
+    tx.reset();
+    decode_err.clear();
+    tx_pk.clear();
+    pk_panic = -1;
+    pk_panic_msg.clear();
+    for (SignerPlan& p : plans) {
+      p.ok = false;
+      p.accnum = p.seq = 0;
+      p.pub.reset();
+      p.gas = 0;
+      p.gas_status = 0;
+      p.resolved = false;
+      p.owner = 0;
+      p.node = Node{};
+      p.leaves.clear();
+    }
+    sacc.clear();
+    owner = 0;
+  }
 };
 
 // Memo table (CheckTx window and separate PreVerifyTxs / ante calls): tx
@@ -1315,12 +1345,50 @@ struct gvh_app {
   int threads = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
   std::unique_ptr<Pool> pool{new Pool(threads - 1)};
   std::mutex pool_mu;                          // guards replacing the pool (gvh_set_threads)
+  // Recycled Memo / Tx objects per pool worker (PreVerifyTxs allocates ~10
+  // objects per tx; reusing them keeps their vectors' capacity and takes
+  // malloc/free off the block path).  Index: worker id & 63.
+  struct ObjPool {
+    std::mutex mu;
+    std::vector<std::shared_ptr<Memo>> memos;
+    std::vector<std::shared_ptr<Tx>> txs;
+  };
+  std::array<ObjPool, 64> objs;
   uint64_t bump_epoch = 0;
   std::atomic<uint64_t> st_gpu_calls{0}, st_gpu_leaves{0}, st_hits{0}, st_misses{0}, st_memo{0}, st_windows{0},
       st_window_txs{0}, st_pre_ns{0}, st_gpu_ns{0}, st_loop_ns{0};
 };
 
 namespace {
+
+constexpr size_t kObjPoolCap = size_t(1) << 15;   // per worker
+std::shared_ptr<Memo> memo_get(gvh_app* app, int w) {
+  auto& p = app->objs[w & 63];
+  std::lock_guard<std::mutex> g(p.mu);
+  if (p.memos.empty()) return std::make_shared<Memo>();
+  auto m = std::move(p.memos.back());
+  p.memos.pop_back();
+  return m;
+}
+std::shared_ptr<Tx> tx_get(gvh_app* app, int w) {
+  auto& p = app->objs[w & 63];
+  std::lock_guard<std::mutex> g(p.mu);
+  if (p.txs.empty()) return nullptr;
+  auto t = std::move(p.txs.back());
+  p.txs.pop_back();
+  return t;
+}
+// m: a memo nobody else holds; back to worker w's pool (its Tx too when unshared)
+void memo_put(gvh_app* app, int w, std::shared_ptr<Memo>&& m) {
+  std::shared_ptr<Tx> t;
+  if (m->tx && m->tx.use_count() == 1) t = std::const_pointer_cast<Tx>(std::move(m->tx));
+  m->reset();
+  auto& p = app->objs[w & 63];
+  std::lock_guard<std::mutex> g(p.mu);
+  if (p.memos.size() < kObjPoolCap) p.memos.push_back(std::move(m));
+  if (t && p.txs.size() < kObjPoolCap) p.txs.push_back(std::move(t));
+  m.reset();
+}
 
 // Run fn(i) for i in [0, n) on the app's pool (dynamic chunks).  Nested calls
 // (from inside a pool task) run inline.
@@ -1901,20 +1969,19 @@ int ante_bytes(gvh_app* app, const uint8_t* p, size_t n, bool simulate, gvh_resu
 // random contend on the other arenas' locks (measured: 3.3 ms vs ~0.3 ms for a
 // 10k-tx multisig block on 16 threads).
 void release_memos(gvh_app* app, std::vector<std::shared_ptr<Memo>>& memos) {
+  // every unshared memo goes back to the pool of the worker that took it
+  // (shared ones -- the memo table's -- are just dropped here)
+  // (owners are read before any worker starts moving elements out: a worker
+  // must not read an element another worker is resetting)
+  std::vector<int16_t> own(memos.size());
+  for (size_t i = 0; i < memos.size(); ++i) own[i] = memos[i] ? memos[i]->owner : (int16_t)-1;
   parallel_workers(app, [&](int w, int nw) {
-    for (auto& m : memos) {
-      if (!m || m.use_count() != 1) continue;           // shared (memo table): not ours to empty
-      for (SignerPlan& p : m->plans)
-        if (p.owner % nw == w) {
-          std::vector<Leaf>().swap(p.leaves);
-          p.node = Node{};
-          p.pub.reset();
-        }
+    for (size_t i = 0; i < memos.size(); ++i) {
+      if (own[i] < 0 || own[i] % nw != w) continue;
+      std::shared_ptr<Memo>& m = memos[i];
+      if (m.use_count() == 1) memo_put(app, own[i], std::move(m));
+      else m.reset();
     }
-  });
-  parallel_workers(app, [&](int w, int nw) {
-    for (auto& m : memos)
-      if (m && m->owner % nw == w) m.reset();
   });
   memos.clear();
 }
@@ -1943,13 +2010,13 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
   std::vector<uint64_t> part_mask(ntx, 0);
   parallel_for_w(app, ntx, [&](size_t t, int w) {
     // a fresh Memo every time (an earlier one may be in use by an ante run)
-    auto m = std::make_shared<Memo>();
+    auto m = memo_get(app, w);
     m->owner = (int16_t)w;
     auto old = keep ? app->memo.find(txs[t], lens[t]) : nullptr;
     if (old) m->tx = old->tx;
     else {
       try {
-        m->tx = decode_tx(txs[t], lens[t], keep);
+        m->tx = decode_tx(txs[t], lens[t], keep, tx_get(app, w));
       } catch (const AminoErr& e) {
         m->decode_err = e.what();
       }
@@ -2209,7 +2276,10 @@ int deliver_block(gvh_app* app, size_t ntx, const uint8_t* const* txs, const siz
   int rc = preverify(app, ntx, txs, lens, nullptr, &memos, false);
   const auto t1 = std::chrono::steady_clock::now();
   app->st_pre_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
-  if (rc != GVH_OK) return rc;
+  if (rc != GVH_OK) {
+    release_memos(app, memos);
+    return rc;
+  }
   rc = deliver_memos(app, memos, out, codes);
   const auto t2 = std::chrono::steady_clock::now();
   app->st_loop_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
