@@ -31,6 +31,7 @@
 #include "secp_group29x.cuh"
 #include "secp_sc29.cuh"
 #include "secp_modinv.cuh"
+#include "secp_fsl.cuh"
 #include "gv_kernels.h"
 
 static_assert(F29_NCH == 2, "gv_lat.hip is built with -DF29_NCH=2");
@@ -732,6 +733,221 @@ __global__ __launch_bounds__(128) void k_verify_lat16(const gvk_lat b) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pub33 small batches on the limb-sliced field layer (secp_fsl.cuh): ONE
+// signature per 128-thread block.  Wave 0 does all the field work with one
+// element per 16-lane DPP row -- the four rows decompress the key (sqrt chain)
+// and build the Q table together, then row r accumulates the partial sum
+// r of {k1q Q, k2q lambda Q, k1g G, k2g lambda G} over the same 125-doubling
+// Booth ladder as k_verify_lat, and two cross-row rounds of complete
+// additions combine them.  Wave 1 lane 0 runs the scalar chain (lat_scalars)
+// concurrently, on its own SIMD.  A sliced product costs ~0.14 us on a lone
+// wave against ~0.37 us for the one-lane layer (profiles/r02/fsl), so the
+// sqrt chain, the table and the ladder all shorten ~2.5x.  Same checks, same
+// group law, same verdict as k_verify_lat.  Verdict bits: atomicOr into the
+// bitmap (zeroed by the launcher).
+struct LatSlShared {
+  static constexpr bool kG5 = false;         // G digits: 20-bit windows (dg)
+  u32 qtab[2][GV_QTAB_N][18];               // Q, lambda*Q entries: x, y sliced limbs (effective affine)
+  u32 ratio[GV_QTAB_N - 1][9];              // Z ratios, then their suffix products
+  u32 dq[1][GV_QWIN];
+  int dg[1][GV_GWIN][2];
+  u32 r[1][8];
+  u32 oks[1];
+};
+
+__global__ __launch_bounds__(128) void k_verify_lat_sl(const gvk_lat b) {
+  __shared__ LatSlShared sh;
+  const u32 gi = blockIdx.x;                            // grid = n: every block is live
+  if (threadIdx.x >= 64) {
+    if (threadIdx.x == 64)
+      lat_scalars(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.msg_blob ? nullptr : b.dig32 + (size_t)gi * 32u,
+                  b.msg_blob ? (const u32*)b.e_soa : nullptr, b.C, gi);
+    __syncthreads();
+    return;
+  }
+  const fslk k = fsl_consts();
+  const u32 row = threadIdx.x >> 4, L = k.L;
+  const bool lo = L < 9u;
+  // ---- pubkey: btcec ParsePubKey / decompressPoint
+  const uint8_t* p = b.pub33 + (size_t)gi * 33u;
+  const u32 pre = p[0];
+  fe x8, y8;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x8.v[i] = be32(p + 1 + 4 * (7 - i));
+  bool ok = (pre & 0xFEu) == 0x02u;
+  {
+    u32 br = 0, d;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d = __builtin_subc(x8.v[i], kLP[i], br, &br);
+    (void)d;
+    ok &= (br != 0);                                    // x < p
+  }
+  {
+    const u32 xs = fsl_from_words(x8.v, k);
+    const u32 c = fsl_mul(fsl_sqr(xs, k), xs, k) + (L == 0u ? 7u : 0u);   // x^3 + 7
+    const u32 y = fsl_sqrt_candidate(c, k);
+    u32 w1[8], w2[8];
+    fsl_to_words(w1, fsl_sqr(y, k));
+    fsl_to_words(w2, c);
+    u32 df = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) df |= w1[i] ^ w2[i];
+    ok &= df == 0u;                                     // "invalid square root"
+    fsl_to_words(y8.v, y);
+  }
+  if ((y8.v[0] & 1u) != (pre & 1u)) fe_neg(y8, y8);
+  fe_normalize(y8);
+  if (!ok) {                                            // harmless stand-in point: G
+    const u32 gx[8] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu,
+                       0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu};
+    const u32 gy[8] = {0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
+                       0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { x8.v[i] = gx[i]; y8.v[i] = gy[i]; }
+  }
+  const u32 qx = fsl_from_words(x8.v, k), qy = fsl_from_words(y8.v, k);
+  // ---- Q table: co-Z chain (as build_q_table / lat_pubkey_and_tables), row 0 stores
+  const bool st = row == 0u && lo;
+  u32 X1, Y1, X2, Y2;
+  {
+    const u32 E = fsl_sqr(qy, k);                       // y^2
+    X1 = fsl_mul(qx << 2, E, k);                        // S = 4 x y^2
+    const u32 M = fsl_norm(fsl_sqr(qx, k) * 3u, k);     // 3 x^2
+    X2 = fsl_mul_plus(M, M, k.big8 - ((u64)X1 << 1), k);               // 2Q.x = M^2 - 2S
+    Y1 = fsl_norm(fsl_mul(E << 1, E << 1, k) << 1, k);  // 8 y^4
+    Y2 = fsl_mul_plus(M, X1 + k.bias - X2, (u64)(k.bias - Y1), k);     // 2Q.y = M (S - X2) - 8y^4
+  }
+  if (st) {
+    sh.qtab[0][0][L] = X1; sh.qtab[0][0][9 + L] = Y1;
+    sh.qtab[0][1][L] = X2; sh.qtab[0][1][9 + L] = Y2;
+  }
+#pragma unroll 1
+  for (int m = 2; m < GV_QTAB_N; ++m) {
+    const u32 h = fsl_sub(X1, X2, k);
+    if (st) sh.ratio[m - 2][L] = h;                     // Z_m / Z_(m-1)
+    const u32 rr = fsl_sub(Y1, Y2, k);
+    const u32 cc = fsl_sqr(h, k);
+    const u32 w1 = fsl_mul(X1, cc, k), w2 = fsl_mul(X2, cc, k);
+    const u32 a1 = fsl_mul(Y1, w1 + k.bias - w2, k);
+    X2 = fsl_mul_plus(rr, rr, k.big8 - (u64)w1 - (u64)w2, k);
+    Y2 = fsl_mul_plus(rr, w1 + k.bias - X2, (u64)(k.bias - a1), k);
+    X1 = w1;
+    Y1 = a1;
+    if (st) { sh.qtab[0][m][L] = X2; sh.qtab[0][m][9 + L] = Y2; }
+  }
+  wave_lds_sync();
+  // back-propagation: suffix products acc_m = prod_{j=m..15} ratio_j (every
+  // row alike, row 0 overwrites the ratios with them), then row r scales
+  // entries r, r+4, r+8, r+12 to the last entry's Z and writes their
+  // lambda*Q entries (beta x, y)
+  u32 acc = 0;
+#pragma unroll 1
+  for (int m = GV_QTAB_N - 1; m >= 2; --m) {
+    const u32 ratio = lo ? sh.ratio[m - 2][L] : 0u;
+    acc = m == GV_QTAB_N - 1 ? ratio : fsl_mul(acc, ratio, k);
+    if (st) sh.ratio[m - 2][L] = acc;
+  }
+  wave_lds_sync();
+  u32 beta;
+  {
+    u32 w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = kLBeta[i];
+    beta = fsl_from_words(w, k);
+  }
+#pragma unroll 1
+  for (int j = 0; j < GV_QTAB_N / 4; ++j) {
+    const int e = 4 * j + (int)row;
+    u32 x = lo ? sh.qtab[0][e][L] : 0u, y = lo ? sh.qtab[0][e][9 + L] : 0u;
+    if (e != GV_QTAB_N - 1) {                           // the last entry is already on Z_15
+      const u32 a = e == 0 ? acc : (lo ? sh.ratio[e - 1][L] : 0u);     // acc_(e+1)
+      const u32 a2 = fsl_sqr(a, k);
+      const u32 a3 = fsl_mul(a2, a, k);
+      x = fsl_mul(x, a2, k);
+      y = fsl_mul(y, a3, k);
+    }
+    const u32 t = fsl_mul(x, beta, k);
+    if (lo) {
+      sh.qtab[0][e][L] = x; sh.qtab[0][e][9 + L] = y;
+      sh.qtab[1][e][L] = t; sh.qtab[1][e][9 + L] = y;
+    }
+  }
+  const u32 zq = fsl_mul(qy << 1, acc, k);              // Z_15 = 2y * prod(ratios)
+  __syncthreads();                                      // digits (wave 1) + tables
+
+  // ---- ladder: row r accumulates one of the four partial sums
+  gjsl A;
+  A.x = 0u; A.y = 0u; A.z = 0u;
+  bool inf = true;
+  const u32* gbase = b.gtab + (row == 3u ? (size_t)GV_GTAB_N * 16u : 0u);
+#pragma unroll 1
+  for (int win = GV_QWIN - 1; win >= 0; --win) {
+    if (win != GV_QWIN - 1) {
+#pragma unroll 1
+      for (int d = 0; d < GV_QW; ++d) gjsl_double(A, A, k);
+    }
+    const bool gwin = (win % GV_GSTEP) == 0;
+    const u32 dq = sh.dq[0][win];
+    int d;
+    if (row < 2u) d = row == 0u ? ((int)(dq << 16) >> 16) : ((int)dq >> 16);
+    else d = gwin ? sh.dg[0][win / GV_GSTEP][row - 2u] : 0;
+    if (d != 0) {
+      const u32 e = (u32)((d < 0 ? -d : d) - 1);
+      u32 x, y;
+      if (row < 2u) {
+        x = lo ? sh.qtab[row][e][L] : 0u;
+        y = lo ? sh.qtab[row][e][9 + L] : 0u;
+      } else {
+        const u32* pe = gbase + (size_t)e * 16u;
+        x = fsl_load_words(pe, k);
+        y = fsl_load_words(pe + 8, k);
+      }
+      if (d < 0) y = k.bias - y;
+      if (inf) {
+        A.x = x; A.y = fsl_norm(y, k); A.z = L == 0u ? 1u : 0u;
+        inf = false;
+      } else {
+        gjsl_add_scaled(A, inf, x, y, A.z, k);
+      }
+    }
+  }
+  // ---- combine: Q rows back to the real curve, two rounds across rows
+  if (row < 2u) A.z = fsl_mul(A.z, zq, k);
+#pragma unroll 1
+  for (int m = 16; m < 64; m <<= 1) {
+    gjsl O;
+    O.x = (u32)__shfl_xor((int)A.x, m, 64);
+    O.y = (u32)__shfl_xor((int)A.y, m, 64);
+    O.z = (u32)__shfl_xor((int)A.z, m, 64);
+    const bool oinf = __shfl_xor((int)inf, m, 64) != 0;
+    gjsl_add_gej(A, inf, A, inf, O, oinf, k);
+  }
+  // ---- final check (as k_ecmult): x(R) mod n == r, without inversion
+  const u32 fl = sh.oks[0];
+  bool okv = (fl & 1u) && ok && !inf;
+  u32 rw[8], X[8], T[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rw[i] = sh.r[0][i];
+  const u32 zz = fsl_sqr(A.z, k);
+  fsl_to_words(X, A.x);
+  fsl_to_words(T, fsl_mul(fsl_from_words(rw, k), zz, k));
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) eq &= (X[i] == T[i]);
+  if (!eq && (fl & 2u)) {
+    u32 rn[8], c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rn[i] = __builtin_addc(rw[i], kN[i], c, &c);
+    fsl_to_words(T, fsl_mul(fsl_from_words(rn, k), zz, k));
+    eq = true;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) eq &= (X[i] == T[i]);
+  }
+  okv &= eq;
+  if (threadIdx.x == 0 && okv) atomicOr((unsigned long long*)&b.bits[gi >> 6], 1ull << (gi & 63u));
+}
+
 }  // namespace gv
 
 extern "C" hipError_t gvk_verify_lat16(const gvk_lat* b, hipStream_t st) {
@@ -742,6 +958,18 @@ extern "C" hipError_t gvk_verify_lat16(const gvk_lat* b, hipStream_t st) {
   }
   if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
   hipLaunchKernelGGL(gv::k_verify_lat16, dim3(blocks), dim3(128), 0, st, *b);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t gvk_verify_lat_sl(const gvk_lat* b, hipStream_t st) {
+  if (b->msg_blob) {
+    hipError_t e = gvk_sha256(b->msg_blob, b->msg_off, b->msg_len, b->n, b->C, b->e_soa, st);
+    if (e != hipSuccess) return e;
+  }
+  hipError_t e = hipMemsetAsync(b->bits, 0, (size_t)((b->n + 63u) / 64u) * 8u, st);
+  if (e != hipSuccess) return e;
+  if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
+  hipLaunchKernelGGL(gv::k_verify_lat_sl, dim3(b->n), dim3(128), 0, st, *b);
   return hipGetLastError();
 }
 

@@ -434,6 +434,7 @@ struct gv_ctx {
   int stage_threads = 8;        // host path: staging memcpy threads per device
   bool time_kernels = false;
   bool fault_inject = false;
+  bool lat_sliced = true;       // pub33 small batches on k_verify_lat_sl (GV_LAT_SLICED=0: k_verify_lat, A/B)
   bool keyed_k4 = true;         // keyed batches on k_ecmult_k4 (GV_KEYED_K4=0: the 125-doubling ladder, A/B)
   size_t keys = 0;              // key-arena slots in use (same on every device)
   std::atomic<uint64_t> keys_gen{0};  // gv_keys_reset calls
@@ -496,6 +497,8 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     if (kslot) {                                // keyed: 16 lanes per signature (group tables)
       lb.kqt2 = d->kqt2; lb.kzq2 = d->kzq2; lb.glat = d->glat;
       CK(gvk_verify_lat16(&lb, st));
+    } else if (ctx->lat_sliced) {
+      CK(gvk_verify_lat_sl(&lb, st));
     } else {
       CK(gvk_verify_lat(&lb, st));
     }
@@ -805,6 +808,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   gv_ctx* ctx = new gv_ctx();
   parse_size_env("GV_MAX_BATCH", &ctx->max_batch);
   if (const char* k4 = getenv("GV_KEYED_K4")) ctx->keyed_k4 = strcmp(k4, "0") != 0;
+  if (const char* ls = getenv("GV_LAT_SLICED")) ctx->lat_sliced = strcmp(ls, "0") != 0;
   for (size_t k = 0; k < ids.size(); ++k) {
     Dev* d = new Dev();
     d->id = ids[k];

@@ -19,7 +19,7 @@
 //       K18 w18 (K_j = 2^(29 j) mod p, as per-lane limb constants), in 64 bits;
 //   R2  one carry pass, the carry out of limb 8 folded into limbs 0 and 1;
 //   R3  one more carry step over limbs 0..7 (limb 8 keeps its bit).
-// Bounds (N-form: every limb < 2^29 + 2^15, the output of every product and
+// Bounds (N-form: every limb < 2^29 + 2^17, the output of every product and
 // of fsl_norm):
 //   mul(a, b) needs max_limb(a) * max_limb(b) < 2^60.8 (column sums of nine
 //   products < 2^64): N x N, N x 4N, 2N x 2N, N x (4N + BIAS) all fit.
@@ -252,6 +252,73 @@ GV_DEV void gjsl_add_scaled(gjsl& a, bool& inf, u32 x, u32 y, u32 az, const fslk
     a.y = fsl_mul2(rr, t, ny, h3, k);                        // R (V - X3) - Y1 H^3
   }
   if (dbl) gjsl_double(a, a, k);
+}
+
+// r = a + b, two Jacobian points of the row's curve (gej29_add_gej's formula
+// and cases): either infinite -> the other; a == b -> 2a; a == -b -> infinity.
+GV_DEV void gjsl_add_gej(gjsl& r, bool& rinf, const gjsl& a, bool ainf, const gjsl& b, bool binf,
+                         const fslk& k) {
+  if (ainf || binf) {
+    r.x = ainf ? b.x : a.x;
+    r.y = ainf ? b.y : a.y;
+    r.z = ainf ? b.z : a.z;
+    rinf = ainf && binf;
+    return;
+  }
+  const u32 z1z1 = fsl_sqr(a.z, k), z2z2 = fsl_sqr(b.z, k);
+  const u32 u1 = fsl_mul(a.x, z2z2, k), u2 = fsl_mul(b.x, z1z1, k);
+  const u32 s1 = fsl_mul(a.y, fsl_mul(b.z, z2z2, k), k);
+  const u32 s2 = fsl_mul(b.y, fsl_mul(a.z, z1z1, k), k);
+  const u32 h = fsl_sub(u2, u1, k), rr = fsl_sub(s2, s1, k);
+  bool inf = false, dbl = false;
+  gjsl o = a;
+  if (fsl_is_zero(h)) {
+    dbl = fsl_is_zero(rr);
+    inf = !dbl;
+  } else {
+    const u32 h2 = fsl_sqr(h, k);
+    const u32 h3 = fsl_mul(h2, h, k);
+    const u32 v = fsl_mul(u1, h2, k);
+    o.z = fsl_mul(fsl_mul(a.z, b.z, k), h, k);
+    o.x = fsl_mul_plus(rr, rr, k.big8 - (u64)h3 - ((u64)v << 1), k);
+    const u32 t = v + k.bias - o.x;
+    o.y = fsl_mul2(rr, t, k.bias - s1, h3, k);             // R (V - X3) - S1 H^3
+  }
+  if (dbl) gjsl_double(o, a, k);
+  r = o;
+  rinf = inf;
+}
+
+// ------------------------------------------------------- exponentiation
+GV_DEV u32 fsl_sqr_n(u32 a, int n, const fslk& k) {
+#pragma unroll 1
+  for (int i = 0; i < n; ++i) a = fsl_sqr(a, k);
+  return a;
+}
+// a^((p+1)/4): btcec decompressPoint's square-root candidate, the addition
+// chain of f29_sqrt_candidate (secp_group29.cuh).
+GV_DEV u32 fsl_sqrt_candidate(u32 a, const fslk& k) {
+  const u32 x2 = fsl_mul(fsl_sqr(a, k), a, k);                 // 2^2 - 1
+  const u32 x3 = fsl_mul(fsl_sqr(x2, k), a, k);                // 2^3 - 1
+  const u32 x6 = fsl_mul(fsl_sqr_n(x3, 3, k), x3, k);
+  const u32 x9 = fsl_mul(fsl_sqr_n(x6, 3, k), x3, k);
+  const u32 x11 = fsl_mul(fsl_sqr_n(x9, 2, k), x2, k);
+  const u32 x22 = fsl_mul(fsl_sqr_n(x11, 11, k), x11, k);
+  const u32 x44 = fsl_mul(fsl_sqr_n(x22, 22, k), x22, k);
+  const u32 x88 = fsl_mul(fsl_sqr_n(x44, 44, k), x44, k);
+  const u32 x176 = fsl_mul(fsl_sqr_n(x88, 88, k), x88, k);
+  const u32 x220 = fsl_mul(fsl_sqr_n(x176, 44, k), x44, k);
+  const u32 x223 = fsl_mul(fsl_sqr_n(x220, 3, k), x3, k);
+  u32 t = fsl_mul(fsl_sqr_n(x223, 23, k), x22, k);
+  t = fsl_mul(fsl_sqr_n(t, 6, k), x2, k);
+  return fsl_sqr_n(t, 2, k);
+}
+
+// canonical 8 x 32 words of the row's element (every lane of the row)
+GV_DEV void fsl_to_words(u32 w[8], u32 a) {
+  fe29 t;
+  fsl_gather(t, a);
+  f29_to_words(w, t);
 }
 
 }  // namespace gv
