@@ -120,7 +120,8 @@ hipError_t gvk_gen_gtable4(uint32_t* gtab4, uint32_t* base_scratch, hipStream_t 
 hipError_t gvk_gen_glat(uint32_t* glat, hipStream_t st);
 hipError_t gvk_verify_lat(const gvk_lat* b, hipStream_t st);
 hipError_t gvk_verify_lat16(const gvk_lat* b, hipStream_t st);
-hipError_t gvk_verify_lat_sl(const gvk_lat* b, hipStream_t st);   // pub33, limb-sliced (one signature per block)
+hipError_t gvk_verify_lat_sl(const gvk_lat* b, hipStream_t st);
+hipError_t gvk_verify_lat16_sl(const gvk_lat* b, hipStream_t st); // keyed, limb-sliced (one signature per block)   // pub33, limb-sliced (one signature per block)
 hipError_t gvk_sha256(const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint32_t n, uint32_t C,
                       uint32_t* e, hipStream_t st);
 hipError_t gvk_verify(const gvk_batch* b, hipStream_t st);

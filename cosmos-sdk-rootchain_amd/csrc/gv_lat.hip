@@ -948,6 +948,141 @@ __global__ __launch_bounds__(128) void k_verify_lat_sl(const gvk_lat b) {
   if (threadIdx.x == 0 && okv) atomicOr((unsigned long long*)&b.bits[gi >> 6], 1ull << (gi & 63u));
 }
 
+// ---------------------------------------------------------------------------
+// Keyed small batches on the limb-sliced layer: ONE signature per 256-thread
+// block.  Lane 0 runs the scalar chain; then wave g (window group g of
+// k_verify_lat16) row r accumulates part r of {k1q Q, k2q lambda Q, k1g G,
+// k2g lambda G} over that group's <= 7 windows (<= 30 doublings) against the
+// arena group table (Q) or glat (G), one element per 16-lane row; two
+// cross-row rounds give each wave its group sum, two more (through LDS, in
+// wave 0) the whole sum, and wave 0 runs the final check.
+struct Lat16SlShared {
+  static constexpr bool kG5 = true;
+  u32 dq[1][GV_QWIN];
+  u32 dg5[1][GV_QWIN];
+  u32 r[1][8];
+  u32 oks[1];
+  u32 pt[GV_LGRP][3][16];                   // group sums, sliced (x, y, z rows)
+  u32 pinf[GV_LGRP];
+};
+
+__global__ __launch_bounds__(256) void k_verify_lat16_sl(const gvk_lat b) {
+  __shared__ Lat16SlShared sh;
+  const u32 gi = blockIdx.x;                            // grid = n: every block is live
+  u32 sl = b.kslot[gi];
+  bool kok = sl < b.kcount;
+  if (!kok) sl = 0;                                     // the arena always holds slot 0's memory
+  kok = kok && b.kok[sl] != 0u;
+  if (threadIdx.x == 0)
+    lat_scalars(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.msg_blob ? nullptr : b.dig32 + (size_t)gi * 32u,
+                b.msg_blob ? (const u32*)b.e_soa : nullptr, b.C, gi);
+  __syncthreads();
+  const fslk k = fsl_consts();
+  const u32 L = k.L, part = (threadIdx.x >> 4) & 3u, grp = threadIdx.x >> 6;
+  const bool lo = L < 9u;
+  const int w_lo = kL16Win[grp], w_hi = kL16Win[grp + 1] - 1;
+  u32 beta;
+  {
+    u32 w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = kLBeta[i];
+    beta = fsl_from_words(w, k);
+  }
+  const u32* qrow = grp == 0u ? b.kqt + (size_t)sl * GV_QTAB_N * GV_QENT_WORDS
+                              : b.kqt2 + ((size_t)sl * GV_KEY2_TABLES + (grp - 1u)) * GV_QTAB_N * GV_QENT_WORDS;
+  const u32* grow = b.glat + (size_t)(grp * 2u + (part & 1u)) * GV_QTAB_N * 16u;
+  gjsl A;
+  A.x = 0u; A.y = 0u; A.z = 0u;
+  bool inf = true;
+#pragma unroll 1
+  for (int win = w_hi; win >= w_lo; --win) {
+    if (win != w_hi) {
+#pragma unroll 1
+      for (int d = 0; d < GV_QW; ++d) gjsl_double(A, A, k);
+    }
+    const u32 dw = part < 2u ? sh.dq[0][win] : sh.dg5[0][win];
+    const int d = (part & 1u) == 0u ? ((int)(dw << 16) >> 16) : ((int)dw >> 16);
+    if (d != 0) {
+      const u32 e = (u32)((d < 0 ? -d : d) - 1);
+      u32 x, y;
+      if (part < 2u) {                                  // Q / lambda Q: arena row, 29-bit limbs
+        const u32* pe = qrow + (size_t)e * GV_QENT_WORDS;
+        x = lo ? pe[L] : 0u;
+        y = lo ? pe[9 + L] : 0u;
+        if (part == 1u) x = fsl_mul(x, beta, k);        // lambda Q = (beta x, y), same Z
+      } else {                                          // G / lambda G: affine words
+        const u32* pe = grow + (size_t)e * 16u;
+        x = fsl_load_words(pe, k);
+        y = fsl_load_words(pe + 8, k);
+      }
+      if (d < 0) y = k.bias - y;
+      if (inf) {
+        A.x = x; A.y = fsl_norm(y, k); A.z = L == 0u ? 1u : 0u;
+        inf = false;
+      } else {
+        gjsl_add_scaled(A, inf, x, y, A.z, k);
+      }
+    }
+  }
+  if (part < 2u) {                                      // Q parts: back to the real curve
+    const u32* zrow = grp == 0u ? b.kzq : b.kzq2 + (size_t)(grp - 1u) * 8u * b.kC;
+    u32 w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = zrow[(size_t)i * b.kC + sl];
+    A.z = fsl_mul(A.z, fsl_from_words(w, k), k);
+  }
+#pragma unroll 1
+  for (int m = 16; m < 64; m <<= 1) {                   // the group's four parts
+    gjsl O;
+    O.x = (u32)__shfl_xor((int)A.x, m, 64);
+    O.y = (u32)__shfl_xor((int)A.y, m, 64);
+    O.z = (u32)__shfl_xor((int)A.z, m, 64);
+    const bool oinf = __shfl_xor((int)inf, m, 64) != 0;
+    gjsl_add_gej(A, inf, A, inf, O, oinf, k);
+  }
+  if (part == 0u) {
+    if (lo) { sh.pt[grp][0][L] = A.x; sh.pt[grp][1][L] = A.y; sh.pt[grp][2][L] = A.z; }
+    if (L == 0u) sh.pinf[grp] = inf ? 1u : 0u;
+  }
+  __syncthreads();
+  if (grp != 0u) return;
+  A.x = lo ? sh.pt[part][0][L] : 0u;                    // wave 0, row r: group r's sum
+  A.y = lo ? sh.pt[part][1][L] : 0u;
+  A.z = lo ? sh.pt[part][2][L] : 0u;
+  inf = sh.pinf[part] != 0u;
+#pragma unroll 1
+  for (int m = 16; m < 64; m <<= 1) {
+    gjsl O;
+    O.x = (u32)__shfl_xor((int)A.x, m, 64);
+    O.y = (u32)__shfl_xor((int)A.y, m, 64);
+    O.z = (u32)__shfl_xor((int)A.z, m, 64);
+    const bool oinf = __shfl_xor((int)inf, m, 64) != 0;
+    gjsl_add_gej(A, inf, A, inf, O, oinf, k);
+  }
+  const u32 fl = sh.oks[0];
+  bool okv = (fl & 1u) && kok && !inf;
+  u32 rw[8], X[8], T[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rw[i] = sh.r[0][i];
+  const u32 zz = fsl_sqr(A.z, k);
+  fsl_to_words(X, A.x);
+  fsl_to_words(T, fsl_mul(fsl_from_words(rw, k), zz, k));
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) eq &= (X[i] == T[i]);
+  if (!eq && (fl & 2u)) {
+    u32 rn[8], c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rn[i] = __builtin_addc(rw[i], kN[i], c, &c);
+    fsl_to_words(T, fsl_mul(fsl_from_words(rn, k), zz, k));
+    eq = true;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) eq &= (X[i] == T[i]);
+  }
+  okv &= eq;
+  if (threadIdx.x == 0 && okv) atomicOr((unsigned long long*)&b.bits[gi >> 6], 1ull << (gi & 63u));
+}
+
 }  // namespace gv
 
 extern "C" hipError_t gvk_verify_lat16(const gvk_lat* b, hipStream_t st) {
@@ -970,6 +1105,18 @@ extern "C" hipError_t gvk_verify_lat_sl(const gvk_lat* b, hipStream_t st) {
   if (e != hipSuccess) return e;
   if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
   hipLaunchKernelGGL(gv::k_verify_lat_sl, dim3(b->n), dim3(128), 0, st, *b);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t gvk_verify_lat16_sl(const gvk_lat* b, hipStream_t st) {
+  if (b->msg_blob) {
+    hipError_t e = gvk_sha256(b->msg_blob, b->msg_off, b->msg_len, b->n, b->C, b->e_soa, st);
+    if (e != hipSuccess) return e;
+  }
+  hipError_t e = hipMemsetAsync(b->bits, 0, (size_t)((b->n + 63u) / 64u) * 8u, st);
+  if (e != hipSuccess) return e;
+  if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
+  hipLaunchKernelGGL(gv::k_verify_lat16_sl, dim3(b->n), dim3(256), 0, st, *b);
   return hipGetLastError();
 }
 

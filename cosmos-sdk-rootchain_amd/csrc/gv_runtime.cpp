@@ -428,13 +428,13 @@ int ed_launch(bool timed, Dev* d, size_t n, const uint8_t* pub, const uint8_t* s
 struct gv_ctx {
   std::vector<Dev*> devs;
   size_t max_batch = size_t(1) << 20;
-  size_t lat_max = 8192;        // batches up to this size take the fused latency kernel (gv_lat.hip): crossover of profiles/r02/batch_curve.json
+  size_t lat_max = 3072;        // batches up to this size take the fused latency kernel (gv_lat.hip): crossover of profiles/r02/lat_sliced/batch_curve.json
   size_t pipe_chunk = 131072;   // host path: first chunk of the two-set copy/compute pipeline (0 = max_batch)
   int pipe_growth = 4;          // host path: each later chunk at most this times the one before
   int stage_threads = 8;        // host path: staging memcpy threads per device
   bool time_kernels = false;
   bool fault_inject = false;
-  bool lat_sliced = true;       // pub33 small batches on k_verify_lat_sl (GV_LAT_SLICED=0: k_verify_lat, A/B)
+  bool lat_sliced = true;       // small batches on k_verify_lat_sl / k_verify_lat16_sl (GV_LAT_SLICED=0: the one-lane-field kernels, A/B)
   bool keyed_k4 = true;         // keyed batches on k_ecmult_k4 (GV_KEYED_K4=0: the 125-doubling ladder, A/B)
   size_t keys = 0;              // key-arena slots in use (same on every device)
   std::atomic<uint64_t> keys_gen{0};  // gv_keys_reset calls
@@ -496,7 +496,8 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     }
     if (kslot) {                                // keyed: 16 lanes per signature (group tables)
       lb.kqt2 = d->kqt2; lb.kzq2 = d->kzq2; lb.glat = d->glat;
-      CK(gvk_verify_lat16(&lb, st));
+      if (ctx->lat_sliced) CK(gvk_verify_lat16_sl(&lb, st));
+      else CK(gvk_verify_lat16(&lb, st));
     } else if (ctx->lat_sliced) {
       CK(gvk_verify_lat_sl(&lb, st));
     } else {
@@ -1059,6 +1060,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   if (!strcmp(key, "lat_max")) {
     if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
     ctx->lat_max = (size_t)val;
+  } else if (!strcmp(key, "lat_sliced")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->lat_sliced = val != 0;
   } else if (!strcmp(key, "max_batch")) {
     if (val < 256 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
     ctx->max_batch = round_up((size_t)val, 256);

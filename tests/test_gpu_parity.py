@@ -187,17 +187,23 @@ def test_point_double(ver):
 
 
 # ------------------------------------------------------------ full verification
-# Two schedules compute every verdict: the throughput pipeline (gv_kernels.hip,
-# one lane per signature) and the fused small-batch latency kernel
-# (gv_lat.hip, four lanes per signature); "lat_max" picks one per call.
-PATHS = {"throughput": 0, "latency": 1 << 30}
+# Three schedules compute every verdict: the throughput pipeline
+# (gv_kernels.hip, one lane per signature), the small-batch kernel on the
+# limb-sliced field layer (k_verify_lat_sl: one signature per block, one field
+# element per 16-lane row; the default) and the one-lane-field small-batch
+# kernel (k_verify_lat: four lanes per signature); "lat_max" and "lat_sliced"
+# pick one per call.
+PATHS = {"throughput": (0, 1), "latency": (1 << 30, 1), "latency_onelane": (1 << 30, 0)}
 
 
 @pytest.fixture(params=sorted(PATHS))
 def path(request, ver):
-    ver.set_option("lat_max", PATHS[request.param])
+    lat_max, sliced = PATHS[request.param]
+    ver.set_option("lat_max", lat_max)
+    ver.set_option("lat_sliced", sliced)
     yield request.param
-    ver.set_option("lat_max", 8192)
+    ver.set_option("lat_max", gvm.LAT_MAX_DEFAULT)
+    ver.set_option("lat_sliced", 1)
 
 
 def test_golden_digest_vectors(ver, path):

@@ -22,11 +22,15 @@ def ver():
 
 @pytest.fixture(params=sorted(PATHS))
 def path(request, ver):
-    """Keyed batches take the fused small-batch kernel up to lat_max, the
-    throughput pipeline above it: both schedules are checked."""
-    ver.set_option("lat_max", PATHS[request.param])
+    """Keyed batches take the fused small-batch kernel up to lat_max
+    (k_verify_lat16_sl, or k_verify_lat16 with lat_sliced 0), the throughput
+    pipeline above it: every schedule is checked."""
+    lat_max, sliced = PATHS[request.param]
+    ver.set_option("lat_max", lat_max)
+    ver.set_option("lat_sliced", sliced)
     yield request.param
-    ver.set_option("lat_max", 4096)
+    ver.set_option("lat_max", gvm.LAT_MAX_DEFAULT)
+    ver.set_option("lat_sliced", 1)
 
 
 def keyed_inputs(ver, pub):

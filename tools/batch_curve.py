@@ -1,6 +1,6 @@
 """Device-resident verify time vs batch size for both schedules (the fused
 latency kernel, gv_lat.hip, and the 4-kernel throughput pipeline), to place
-the "lat_max" crossover.  Prints one JSON line.  usage: batch_curve.py [reps]"""
+the "lat_max" crossover.  Prints one JSON line.  usage: batch_curve.py [reps] [n1,n2,...]"""
 import json
 import os
 import sys
@@ -17,7 +17,9 @@ import gpuverify as gvm  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-    nmax = 262144
+    sizes = ([int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else
+             [1024, 4096, 8192, 16384, 32768, 65536, 131072, 262144])
+    nmax = max(sizes)
     pub, sig, dig, exp = bench.make_digest_workload(nmax, 0xCC, 4096, 0.0, 16)
     ver = gvm.Verifier([0])
     d = [ver.dev_alloc(a.nbytes) for a in (pub, sig, dig)]
@@ -25,7 +27,7 @@ def main():
         ver.dev_upload(p, a)
     bits = ver.dev_alloc(nmax // 8 + 64)
     out = {}
-    for n in (1024, 4096, 8192, 16384, 32768, 65536, 131072, 262144):
+    for n in sizes:
         row = {}
         for name, lat in (("latency_kernel", 1 << 30), ("throughput_pipeline", 0)):
             ver.set_option("lat_max", lat)
@@ -40,7 +42,7 @@ def main():
             ver.dev_download(got, bits)
             ok = int(np.unpackbits(got.view(np.uint8), bitorder="little")[:n].sum())
             row[name] = {"ms": round(ms, 4), "verifies_per_s": round(n / ms * 1e3, 1), "accepted": ok}
-        ver.set_option("lat_max", 8192)
+        ver.set_option("lat_max", gvm.LAT_MAX_DEFAULT)
         hp, hs, hd = (np.ascontiguousarray(a[:n]) for a in (pub, sig, dig))
         ver.verify_batch_digests_bits(hp, hs, hd)
         t = time.perf_counter()
