@@ -337,8 +337,10 @@ struct Lat16Shared {
 };
 
 // The scalar chain of one signature (one lane): range / low-S checks, s^-1,
-// u1, u2, GLV split, Booth digits -> sh.
-template <class SH>
+// u1, u2, GLV split, Booth digits -> sh.  VAR: s^-1 by the variable-time
+// divsteps (s30_modinv_var) -- for a lone active lane (the sliced kernels);
+// the four-lanes-per-signature kernels keep the lockstep form.
+template <bool VAR = false, class SH>
 GV_DEV void lat_scalars(SH& sh, int sig, bool live, const uint8_t* sig64, const uint8_t* dig32,
                         const u32* e_soa, u32 C, u32 gi) {
   u32 r[8], s[8], e[8];
@@ -364,7 +366,8 @@ GV_DEV void lat_scalars(SH& sh, int sig, bool live, const uint8_t* sig64, const 
     sc29 s29, w, e29, r29, t;
 #if GV_LAT_DIVSTEPS
     u32 si[8];                              // s^-1 by divsteps: ~4x shorter chain than Fermat
-    s30_modinv(si, s, [](bool done) { return __all(done) != 0; });
+    if constexpr (VAR) s30_modinv_var(si, s, []() {});
+    else s30_modinv(si, s, [](bool done) { return __all(done) != 0; });
     sc29_from_words(s29, si);
     sc29_to_mont(w, s29);                   // s^-1 (Montgomery form)
 #else
@@ -761,7 +764,7 @@ __global__ __launch_bounds__(128) void k_verify_lat_sl(const gvk_lat b) {
   const u32 gi = blockIdx.x;                            // grid = n: every block is live
   if (threadIdx.x >= 64) {
     if (threadIdx.x == 64)
-      lat_scalars(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.msg_blob ? nullptr : b.dig32 + (size_t)gi * 32u,
+      lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.msg_blob ? nullptr : b.dig32 + (size_t)gi * 32u,
                   b.msg_blob ? (const u32*)b.e_soa : nullptr, b.C, gi);
     __syncthreads();
     return;
@@ -974,7 +977,7 @@ __global__ __launch_bounds__(256) void k_verify_lat16_sl(const gvk_lat b) {
   if (!kok) sl = 0;                                     // the arena always holds slot 0's memory
   kok = kok && b.kok[sl] != 0u;
   if (threadIdx.x == 0)
-    lat_scalars(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.msg_blob ? nullptr : b.dig32 + (size_t)gi * 32u,
+    lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.msg_blob ? nullptr : b.dig32 + (size_t)gi * 32u,
                 b.msg_blob ? (const u32*)b.e_soa : nullptr, b.C, gi);
   __syncthreads();
   const fslk k = fsl_consts();

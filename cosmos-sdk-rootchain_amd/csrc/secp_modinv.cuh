@@ -195,4 +195,90 @@ GV_DEV void s30_modinv(uint32_t w[8], const uint32_t x[8], AllDone all_done) {
   s30_to_words(w, d);
 }
 
+// ---------------------------------------------------------------------------
+// Variable-time divsteps (the signature data is public): the "eta = -delta"
+// form of Bernstein-Yang with the batching of libsecp256k1's var-time
+// modinv32 (Wuille's safegcd implementation notes, "divsteps_var"): a run of
+// zero low bits of g is ONE shift, and up to 8 low bits of g are cancelled at
+// once by g += w f with w = -g / f (mod 2^k), k <= eta + 1 so that no swap
+// falls inside the batch.  The same transition matrix as 30 single divsteps
+// of that form (|u| + |v| <= 2^30), in ~1/4 of the instructions on a lone
+// lane (the latency kernels' scalar chain).
+
+// f^-1 mod 2^8 for odd f (Newton from f*f == 1 mod 8)
+GV_DEV uint32_t s30_inv8(uint32_t f) {
+  uint32_t x = f;
+  x *= 2u - f * x;                              // mod 2^6
+  x *= 2u - f * x;                              // mod 2^12
+  return x;
+}
+
+GV_DEV int32_t s30_divsteps_var(int32_t eta, uint32_t f, uint32_t g, int32_t t[4]) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+  uint32_t nfi = 0u - s30_inv8(f);              // -f^-1 mod 2^8
+  int i = 30;
+#pragma unroll 1
+  for (;;) {
+    const int zeros = __builtin_ctz(g | (0xFFFFFFFFu << i));   // sentinel: at most i
+    g >>= zeros;
+    u <<= zeros;
+    v <<= zeros;
+    eta -= zeros;
+    i -= zeros;
+    if (i == 0) break;
+    if (eta < 0) {                              // (f, g) <- (g, -f)
+      uint32_t tmp;
+      eta = -eta;
+      tmp = f; f = g; g = 0u - tmp;
+      tmp = u; u = q; q = 0u - tmp;
+      tmp = v; v = r; r = 0u - tmp;
+      nfi = 0u - s30_inv8(f);
+    }
+    const int limit = (eta + 1) > i ? i : (eta + 1);
+    const uint32_t m = (0xFFFFFFFFu >> (32 - limit)) & 255u;
+    const uint32_t w = (g * nfi) & m;           // g + w f == 0 (mod 2^min(limit, 8))
+    g += f * w;
+    q += u * w;
+    r += v * w;
+  }
+  t[0] = (int32_t)u; t[1] = (int32_t)v; t[2] = (int32_t)q; t[3] = (int32_t)r;
+  return eta;
+}
+
+// w = x^-1 mod n (0 < x < n; x == 0 gives 0), one lane, variable time.
+// `done` counts rounds for the host tests.
+template <class Count>
+GV_DEV void s30_modinv_var(uint32_t w[8], const uint32_t x[8], Count count) {
+  s30 f, g, d, e;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) { f.v[i] = s30_n(i); d.v[i] = 0; e.v[i] = 0; }
+  e.v[0] = 1;
+  s30_from_words(g, x);
+  int32_t eta = -1;
+#pragma unroll 1
+  for (int round = 0; round < 25; ++round) {    // eta form from -1: g == 0 within 590 divsteps
+    int32_t gz = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) gz |= g.v[i];
+    if (gz == 0) break;
+    count();
+    int32_t t[4];
+    eta = s30_divsteps_var(eta, (uint32_t)f.v[0] | ((uint32_t)f.v[1] << 30),
+                           (uint32_t)g.v[0] | ((uint32_t)g.v[1] << 30), t);
+    s30_update_fg(f, g, t);
+    s30_update_de(d, e, t);
+  }
+  if (f.v[8] < 0) {                             // f = -1: the inverse is -d
+    int64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      c += (int64_t)s30_n(i) - d.v[i];
+      d.v[i] = i < 8 ? (int32_t)((uint32_t)c & S30_M) : (int32_t)c;
+      c >>= 30;
+    }
+    s30_normalize(d);
+  }
+  s30_to_words(w, d);
+}
+
 }  // namespace gv

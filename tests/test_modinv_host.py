@@ -64,3 +64,49 @@ def test_batch_matrix_bound(lib):
         u, v, q, r = t
         assert abs(u) + abs(v) <= 2**30 and abs(q) + abs(r) <= 2**30
         assert (u * f + v * g) % 2**30 == 0 and (q * f + r * g) % 2**30 == 0
+
+
+def inv_var(L, x):
+    w = (ctypes.c_uint32 * 8)()
+    rounds = L.mi_inv_var(words(x), w)
+    return sum(v << (32 * i) for i, v in enumerate(w)), rounds
+
+
+def test_var_time_inverses(lib):
+    """The variable-time divsteps (s30_modinv_var, gv_lat.hip's lat_scalars)
+    give the same inverse on random and edge scalars, within the round cap."""
+    rng = random.Random(11)
+    xs = [1, 2, 3, N - 1, N - 2, (N - 1) // 2, (N + 1) // 2, 2**255, 2**128 + 1, 0xFFFFFFFF, 1 << 30, (1 << 30) - 1]
+    xs += [rng.randrange(1, N) for _ in range(5000)]
+    xs += [rng.randrange(1, 2**k) for k in (8, 32, 64, 129, 200) for _ in range(40)]
+    worst = 0
+    for x in xs:
+        got, rounds = inv_var(lib, x)
+        assert got == pow(x, -1, N), hex(x)
+        worst = max(worst, rounds)
+    assert worst <= 20
+    assert inv_var(lib, 0)[0] == 0
+
+
+def test_var_batch_matches_single_steps(lib):
+    """One var-time batch is the same transition as 30 single divsteps of the
+    eta form (delta = -eta), hence the same matrix bound."""
+    lib.mi_divsteps_var.restype = ctypes.c_int32
+    rng = random.Random(13)
+    for _ in range(5000):
+        f = rng.getrandbits(32) | 1
+        g = rng.getrandbits(32)
+        eta = rng.randrange(-40, 41)
+        t = (ctypes.c_int32 * 4)()
+        eta2 = lib.mi_divsteps_var(eta, f, g, t)
+        # reference: 30 single eta-form divsteps on Python ints
+        uu, vv, qq, rr, ff, gg, e = 1, 0, 0, 1, f, g, eta
+        for _ in range(30):
+            if e < 0 and gg & 1:
+                e, ff, gg, uu, vv, qq, rr = -e, gg, -ff, qq, rr, -uu, -vv
+            if gg & 1:
+                gg, qq, rr = gg + ff, qq + uu, rr + vv
+            e, gg, uu, vv = e - 1, gg >> 1, uu << 1, vv << 1
+        assert eta2 == e
+        assert list(t) == [uu, vv, qq, rr], (f, g, eta)
+        assert abs(uu) + abs(vv) <= 2**30 and abs(qq) + abs(rr) <= 2**30

@@ -21,10 +21,10 @@
 using namespace gv;
 #define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
 
-enum { OP_MUL, OP_SQR, OP_MULX, OP_DBL, OP_ADD, OP_MODINV, OP_SCMUL, OP_GLV, OP_SQRT, OP_FERMAT, OP_N };
+enum { OP_MUL, OP_SQR, OP_MULX, OP_DBL, OP_ADD, OP_MODINV, OP_SCMUL, OP_GLV, OP_SQRT, OP_FERMAT, OP_MODINV_VAR, OP_N };
 static const char* kNames[OP_N] = {"f29_mul", "f29_sqr", "f29x_mul", "gej29x_double", "gej29x_add_scaled",
-                                   "s30_modinv", "sc29_mul", "glv_split", "f29_sqrt_candidate", "sc29_inv"};
-static const int kIters[OP_N] = {256, 256, 256, 64, 64, 8, 128, 32, 4, 4};
+                                   "s30_modinv", "sc29_mul", "glv_split", "f29_sqrt_candidate", "sc29_inv", "s30_modinv_var"};
+static const int kIters[OP_N] = {256, 256, 256, 64, 64, 8, 128, 32, 4, 4, 8};
 
 __device__ void seed(u32 w[8], u32 g, u32 s) {
   u32 x = g * 2654435761u + s;
@@ -88,6 +88,15 @@ __global__ __launch_bounds__(64) void k_lat(int op, int iters, uint64_t* t, u32*
     case OP_SQRT:
 #pragma unroll 1
       for (int i = 0; i < iters; ++i) f29_sqrt_candidate(a, a);
+      break;
+    case OP_MODINV_VAR:
+      if (g == 0) {                              // one lane, as in the sliced kernels
+#pragma unroll 1
+        for (int i = 0; i < iters; ++i) {
+          wa[0] |= 1u;
+          s30_modinv_var(wa, wa, []() {});
+        }
+      }
       break;
     case OP_FERMAT:
 #pragma unroll 1
