@@ -32,6 +32,7 @@
 #include "secp_sc29.cuh"
 #include "secp_modinv.cuh"
 #include "secp_fsl.cuh"
+#include "secp_modinv_sl.cuh"
 #include "gv_kernels.h"
 
 static_assert(F29_NCH == 2, "gv_lat.hip is built with -DF29_NCH=2");
@@ -337,9 +338,10 @@ struct Lat16Shared {
 };
 
 // The scalar chain of one signature (one lane): range / low-S checks, s^-1,
-// u1, u2, GLV split, Booth digits -> sh.  VAR: s^-1 by the variable-time
-// divsteps (s30_modinv_var) -- for a lone active lane (the sliced kernels);
-// the four-lanes-per-signature kernels keep the lockstep form.
+// u1, u2, GLV split, Booth digits -> sh.  VAR: called by a whole wave with
+// the same signature in every lane (the sliced kernels); s^-1 by the
+// variable-time divsteps with the state vectors sliced over the lanes
+// (s30_modinv_sl).  Otherwise one signature per lane, lockstep divsteps.
 template <bool VAR = false, class SH>
 GV_DEV void lat_scalars(SH& sh, int sig, bool live, const uint8_t* sig64, const uint8_t* dig32,
                         const u32* e_soa, u32 C, u32 gi) {
@@ -366,7 +368,7 @@ GV_DEV void lat_scalars(SH& sh, int sig, bool live, const uint8_t* sig64, const 
     sc29 s29, w, e29, r29, t;
 #if GV_LAT_DIVSTEPS
     u32 si[8];                              // s^-1 by divsteps: ~4x shorter chain than Fermat
-    if constexpr (VAR) s30_modinv_var(si, s, []() {});
+    if constexpr (VAR) s30_modinv_sl(si, s, fsl_consts());   // whole wave, limbs over lanes
     else s30_modinv(si, s, [](bool done) { return __all(done) != 0; });
     sc29_from_words(s29, si);
     sc29_to_mont(w, s29);                   // s^-1 (Montgomery form)
@@ -762,10 +764,9 @@ struct LatSlShared {
 __global__ __launch_bounds__(128) void k_verify_lat_sl(const gvk_lat b) {
   __shared__ LatSlShared sh;
   const u32 gi = blockIdx.x;                            // grid = n: every block is live
-  if (threadIdx.x >= 64) {
-    if (threadIdx.x == 64)
-      lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.msg_blob ? nullptr : b.dig32 + (size_t)gi * 32u,
-                  b.msg_blob ? (const u32*)b.e_soa : nullptr, b.C, gi);
+  if (threadIdx.x >= 64) {                              // wave 1: the scalar chain, whole wave
+    lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.msg_blob ? nullptr : b.dig32 + (size_t)gi * 32u,
+                      b.msg_blob ? (const u32*)b.e_soa : nullptr, b.C, gi);
     __syncthreads();
     return;
   }
@@ -976,7 +977,7 @@ __global__ __launch_bounds__(256) void k_verify_lat16_sl(const gvk_lat b) {
   bool kok = sl < b.kcount;
   if (!kok) sl = 0;                                     // the arena always holds slot 0's memory
   kok = kok && b.kok[sl] != 0u;
-  if (threadIdx.x == 0)
+  if (threadIdx.x < 64)                                 // wave 0: the scalar chain, whole wave
     lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.msg_blob ? nullptr : b.dig32 + (size_t)gi * 32u,
                 b.msg_blob ? (const u32*)b.e_soa : nullptr, b.C, gi);
   __syncthreads();
