@@ -428,7 +428,9 @@ int ed_launch(bool timed, Dev* d, size_t n, const uint8_t* pub, const uint8_t* s
 struct gv_ctx {
   std::vector<Dev*> devs;
   size_t max_batch = size_t(1) << 20;
-  size_t lat_max = 3072;        // batches up to this size take the fused latency kernel (gv_lat.hip): crossover of profiles/r02/lat_sliced/batch_curve.json
+  size_t lat_max = 8192;        // batches up to this size take a fused small-batch kernel (gv_lat.hip), larger ones the pipeline
+  size_t lat_sl_max = 2048;     // ... and up to this size the limb-sliced one (one signature per block); between the two the
+                                // four-lanes-per-signature kernel (0.50 ms flat to 8192): profiles/r02/lat_sliced/batch_curve*.json
   size_t pipe_chunk = 131072;   // host path: first chunk of the two-set copy/compute pipeline (0 = max_batch)
   int pipe_growth = 4;          // host path: each later chunk at most this times the one before
   int stage_threads = 8;        // host path: staging memcpy threads per device
@@ -494,11 +496,12 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
       lb.pub33 = nullptr;
       lb.kslot = kslot; lb.kqt = b.kqt; lb.kzq = b.kzq; lb.kok = b.kok; lb.kC = b.kC; lb.kcount = b.kcount;
     }
+    const bool sliced = ctx->lat_sliced && n <= ctx->lat_sl_max;
     if (kslot) {                                // keyed: 16 lanes per signature (group tables)
       lb.kqt2 = d->kqt2; lb.kzq2 = d->kzq2; lb.glat = d->glat;
-      if (ctx->lat_sliced) CK(gvk_verify_lat16_sl(&lb, st));
+      if (sliced) CK(gvk_verify_lat16_sl(&lb, st));
       else CK(gvk_verify_lat16(&lb, st));
-    } else if (ctx->lat_sliced) {
+    } else if (sliced) {
       CK(gvk_verify_lat_sl(&lb, st));
     } else {
       CK(gvk_verify_lat(&lb, st));
@@ -1060,6 +1063,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   if (!strcmp(key, "lat_max")) {
     if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
     ctx->lat_max = (size_t)val;
+  } else if (!strcmp(key, "lat_sl_max")) {
+    if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
+    ctx->lat_sl_max = (size_t)val;
   } else if (!strcmp(key, "lat_sliced")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->lat_sliced = val != 0;

@@ -23,8 +23,10 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 # GV_LIB overrides the library path (A/B runs of alternative builds); the default
 # is the in-tree build.
-# default of the "lat_max" option (gv_runtime.cpp): the small-batch / pipeline crossover
-LAT_MAX_DEFAULT = 3072
+# defaults of the "lat_max" / "lat_sl_max" options (gv_runtime.cpp): the small-batch / pipeline
+# crossover and the sliced / four-lanes-per-signature small-batch crossover
+LAT_MAX_DEFAULT = 8192
+LAT_SL_MAX_DEFAULT = 2048
 LIB_PATH = os.environ.get("GV_LIB") or os.path.join(HERE, "lib", "libgpuverify.so")
 
 GV_OK, GV_EINVAL, GV_ENODEV, GV_EHIP, GV_ENOMEM, GV_EFAULT = 0, -1, -2, -3, -4, -5

@@ -169,10 +169,12 @@ int gv_dev_verify_ed25519_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* 
 /* Options: "max_batch" (lanes per device launch, default 1<<20, at most
  * 0xFFFFFF00),
  * "lat_max" (batches of at most this many items -- per device slice -- take
- * the fused small-batch latency kernel, default 3072; 0 = never),
- * "lat_sliced" (1: the latency kernels on the limb-sliced field layer,
- * k_verify_lat_sl / k_verify_lat16_sl, default; 0: the one-lane-field
- * k_verify_lat / k_verify_lat16),
+ * a fused small-batch kernel, default 8192; 0 = never),
+ * "lat_sl_max" (batches of at most this many items take the limb-sliced
+ * small-batch kernels k_verify_lat_sl / k_verify_lat16_sl, one signature per
+ * block; larger ones up to lat_max the four-lanes-per-signature
+ * k_verify_lat / k_verify_lat16; default 2048),
+ * "lat_sliced" (0/1: 0 never takes the sliced kernels; default 1),
  * "pipe_chunk" (host-buffer calls past lat_max: first chunk of the two-stream
  * copy/compute pipeline per device, default 131072; 0 = one chunk per
  * max_batch), "pipe_growth" (each later chunk at most this many times the one

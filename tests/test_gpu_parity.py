@@ -193,7 +193,7 @@ def test_point_double(ver):
 # element per 16-lane row; the default) and the one-lane-field small-batch
 # kernel (k_verify_lat: four lanes per signature); "lat_max" and "lat_sliced"
 # pick one per call.
-PATHS = {"throughput": (0, 1), "latency": (1 << 30, 1), "latency_onelane": (1 << 30, 0)}
+PATHS = {"throughput": (0, 1), "latency": (1 << 30, 1), "latency_onelane": (1 << 30, 0)}  # (lat_max, sliced)
 
 
 @pytest.fixture(params=sorted(PATHS))
@@ -201,9 +201,11 @@ def path(request, ver):
     lat_max, sliced = PATHS[request.param]
     ver.set_option("lat_max", lat_max)
     ver.set_option("lat_sliced", sliced)
+    ver.set_option("lat_sl_max", 1 << 30)
     yield request.param
     ver.set_option("lat_max", gvm.LAT_MAX_DEFAULT)
     ver.set_option("lat_sliced", 1)
+    ver.set_option("lat_sl_max", gvm.LAT_SL_MAX_DEFAULT)
 
 
 def test_golden_digest_vectors(ver, path):
@@ -433,3 +435,31 @@ def test_option_bounds(ver):
                      ("pipe_chunk", 100), ("pipe_growth", 0), ("stage_threads", 0), ("no_such_option", 1)):
         with pytest.raises(gvm.GpuVerifyError):
             ver.set_option(key, val)
+
+
+def test_sliced_latency_kernels_at_scale(ver):
+    """k_verify_lat_sl (pub33) and k_verify_lat16_sl (keyed) far past their
+    production batch size: 262,144 mixed signatures (25 % invalid over the
+    generator's six classes, 4,096 keys) forced through the small-batch
+    schedule, against the verdicts the generator constructed, and a sample
+    against the C oracle."""
+    import bench
+    pub, sig, dig, exp = bench.make_digest_workload(262144, 0x5A, 4096, 0.25, 16)
+    assert 0.70 < exp.mean() < 0.80
+    want = O.verify_digests(pub[:4000], sig[:4000], dig[:4000], threads=16)
+    assert np.array_equal(want, exp[:4000])
+    uniq, inv = np.unique(pub, axis=0, return_inverse=True)
+    ver.set_option("lat_max", 1 << 30)
+    ver.set_option("lat_sl_max", 1 << 30)
+    try:
+        got = ver.verify_batch_digests(pub, sig, dig)
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, bad[:20]
+        slots = ver.keys_load(uniq)[inv.reshape(-1)]
+        got = ver.verify_batch_digests_keyed(slots, sig, dig)
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, bad[:20]
+    finally:
+        ver.set_option("lat_max", gvm.LAT_MAX_DEFAULT)
+        ver.set_option("lat_sl_max", gvm.LAT_SL_MAX_DEFAULT)
+        ver.keys_reset()

@@ -29,8 +29,10 @@ def main():
     out = {}
     for n in sizes:
         row = {}
-        for name, lat in (("latency_kernel", 1 << 30), ("throughput_pipeline", 0)):
+        for name, lat, slm in (("latency_sliced", 1 << 30, 1 << 30), ("latency_onelane", 1 << 30, 0),
+                               ("throughput_pipeline", 0, 0)):
             ver.set_option("lat_max", lat)
+            ver.set_option("lat_sl_max", slm)
             ver.dev_verify_digests(0, n, d[0], d[1], d[2], bits)
             ver.dev_sync()
             t = time.perf_counter()
@@ -43,6 +45,7 @@ def main():
             ok = int(np.unpackbits(got.view(np.uint8), bitorder="little")[:n].sum())
             row[name] = {"ms": round(ms, 4), "verifies_per_s": round(n / ms * 1e3, 1), "accepted": ok}
         ver.set_option("lat_max", gvm.LAT_MAX_DEFAULT)
+        ver.set_option("lat_sl_max", gvm.LAT_SL_MAX_DEFAULT)
         hp, hs, hd = (np.ascontiguousarray(a[:n]) for a in (pub, sig, dig))
         ver.verify_batch_digests_bits(hp, hs, hd)
         t = time.perf_counter()
