@@ -80,7 +80,9 @@ type GPU struct {
 	closeOnce sync.Once
 
 	// CPUBelow routes batches smaller than this to the CPU (VerifyBatchRouted):
-	// below the measured crossover a VerifyBytes loop answers first.
+	// below the measured crossover a VerifyBytes loop answers first (one core:
+	// ~0.21 ms per signature; the sliced small-batch kernels: ~0.26 ms for up
+	// to 1,024 signatures, DESIGN.md §6.3).
 	CPUBelow int
 
 	mu      sync.Mutex
@@ -111,7 +113,7 @@ func Open(devices []int) (*GPU, error) {
 	if rc := C.gv_open(ids, C.int(len(devices)), &ctx); rc != 0 {
 		return nil, errors.New("gpuverify: gv_open: " + C.GoString(C.gv_strerror(rc)))
 	}
-	return &GPU{ctx: ctx, CPUBelow: 16, slots: map[secp256k1.PubKeySecp256k1]uint32{}}, nil
+	return &GPU{ctx: ctx, CPUBelow: 4, slots: map[secp256k1.PubKeySecp256k1]uint32{}}, nil
 }
 
 // Close releases the context (idempotent).
