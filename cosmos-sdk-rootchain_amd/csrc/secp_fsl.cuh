@@ -72,9 +72,17 @@ GV_DEV fslk fsl_consts() {
   return k;
 }
 
+// FSL_BARRIER: an empty asm value barrier after every mad keeps the chains as
+// written (the compiler otherwise may split a mad into a product and a 64-bit
+// add); 0 lets the scheduler interleave independent products.
+#ifndef FSL_BARRIER
+#define FSL_BARRIER 0
+#endif
 GV_DEV u64 fsl_mad(u32 a, u32 b, u64 c) {
   u64 r = (u64)a * b + c;
-  asm("" : "+v"(r));              // value barrier: keep the chains as written
+#if FSL_BARRIER
+  asm("" : "+v"(r));
+#endif
   return r;
 }
 
@@ -215,13 +223,15 @@ struct gjsl { u32 x, y, z; };
 // r = 2a, 3M + 4S (gej29_double's formula):
 //   B = Y^2, Z3 = 2Y Z, E = 3X^2, D = X B, C = B^2,
 //   X3 = E^2 - 8D, Y3 = E (4D - X3) - 8C.
+// Operand order: products sharing a first operand share its nine row
+// broadcasts, products sharing a second operand its eight row shifts
+// (Y: B, Z3; X: E, D; B: D, C; E: X3, Y3).
 GV_DEV void gjsl_double(gjsl& r, const gjsl& a, const fslk& k) {
-  const u32 dy = a.y << 1;                                  // 2N
   const u32 B = fsl_sqr(a.y, k);
-  const u32 z3 = fsl_mul(dy, a.z, k);                       // 2N x N
+  const u32 z3 = fsl_mul(a.y, a.z << 1, k);                 // N x 2N
   const u32 E = fsl_mul(a.x, a.x * 3u, k);                  // N x 3N
   const u32 D = fsl_mul(a.x, B, k);
-  const u32 C = fsl_sqr(B, k);
+  const u32 C = fsl_mul(B, B, k);
   const u32 x3 = fsl_mul_plus(E, E, k.big8 - ((u64)D << 3), k);
   const u32 t = (D << 2) + k.bias - x3;                     // < 2^31.1
   r.y = fsl_mul_plus(E, t, k.big8 - ((u64)C << 3), k);     // N x (4N + BIAS)
