@@ -759,19 +759,16 @@ struct LatSlShared {
   int dg[1][GV_GWIN][2];
   u32 r[1][8];
   u32 oks[1];
+  u32 zq[16];                               // Z of the tables' curve, sliced
+  u32 okp;                                  // ParsePubKey verdict
+  u32 pt[3][16];                            // wave 2's sum (x, y, z sliced)
+  u32 pinf;
 };
 
-__global__ __launch_bounds__(128) void k_verify_lat_sl(const gvk_lat b) {
-  __shared__ LatSlShared sh;
-  const u32 gi = blockIdx.x;                            // grid = n: every block is live
-  if (threadIdx.x >= 64) {                              // wave 1: the scalar chain, whole wave
-    lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.msg_blob ? nullptr : b.dig32 + (size_t)gi * 32u,
-                      b.msg_blob ? (const u32*)b.e_soa : nullptr, b.C, gi);
-    __syncthreads();
-    return;
-  }
-  const fslk k = fsl_consts();
-  const u32 row = threadIdx.x >> 4, L = k.L;
+// Wave 0 of k_verify_lat_sl: key decompression, Q / lambda*Q tables into LDS,
+// zq (Z of the table's curve) and the ParsePubKey verdict into LDS.
+GV_DEV void lat_sl_prep(LatSlShared& sh, const gvk_lat& b, u32 gi, const fslk& k) {
+  const u32 row = (threadIdx.x >> 4) & 3u, L = k.L;
   const bool lo = L < 9u;
   // ---- pubkey: btcec ParsePubKey / decompressPoint
   const uint8_t* p = b.pub33 + (size_t)gi * 33u;
@@ -878,9 +875,40 @@ __global__ __launch_bounds__(128) void k_verify_lat_sl(const gvk_lat b) {
     }
   }
   const u32 zq = fsl_mul(qy << 1, acc, k);              // Z_15 = 2y * prod(ratios)
-  __syncthreads();                                      // digits (wave 1) + tables
+  if (row == 0u && lo) sh.zq[L] = zq;
+  if (threadIdx.x == 0) sh.okp = ok ? 1u : 0u;
+}
 
-  // ---- ladder: row r accumulates one of the four partial sums
+// GV_LAT_SL_SPLIT: batches of at most this many signatures split the pub33
+// ladder's windows over two waves (even windows + G on wave 0, odd windows on
+// wave 2; 192-thread blocks): each runs the 125 doublings but only half the
+// Q / lambda*Q additions, plus one complete addition through LDS.  Larger
+// batches keep one ladder wave (128-thread blocks): past ~1k signatures the
+// third wave per block costs more SIMD time than it saves.  0: never split.
+#ifndef GV_LAT_SL_SPLIT
+#define GV_LAT_SL_SPLIT 512
+#endif
+__global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
+  __shared__ LatSlShared sh;
+  const u32 gi = blockIdx.x;                            // grid = n: every block is live
+  const u32 wave = threadIdx.x >> 6;
+  if (wave == 1u) {                                     // the scalar chain, whole wave (own SIMD)
+    lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.msg_blob ? nullptr : b.dig32 + (size_t)gi * 32u,
+                      b.msg_blob ? (const u32*)b.e_soa : nullptr, b.C, gi);
+    __syncthreads();
+    __syncthreads();
+    return;
+  }
+  const fslk k = fsl_consts();
+  const u32 row = (threadIdx.x >> 4) & 3u, L = k.L;
+  const bool lo = L < 9u;
+  if (wave == 0u) lat_sl_prep(sh, b, gi, k);
+  __syncthreads();                                      // digits (wave 1) + tables, zq (wave 0)
+  const bool ok = sh.okp != 0u;
+  const u32 zq = lo ? sh.zq[L] : 0u;
+  // ---- ladder: row r accumulates one of the four partial sums (of its wave's windows)
+  const bool split = blockDim.x > 128u;
+  const int par = split ? (wave == 0u ? 0 : 1) : -1;
   gjsl A;
   A.x = 0u; A.y = 0u; A.z = 0u;
   bool inf = true;
@@ -891,10 +919,11 @@ __global__ __launch_bounds__(128) void k_verify_lat_sl(const gvk_lat b) {
 #pragma unroll 1
       for (int d = 0; d < GV_QW; ++d) gjsl_double(A, A, k);
     }
-    const bool gwin = (win % GV_GSTEP) == 0;
+    const bool gwin = (win % GV_GSTEP) == 0 && wave == 0u;
+    const bool mine = par < 0 || (win & 1) == par;
     const u32 dq = sh.dq[0][win];
     int d;
-    if (row < 2u) d = row == 0u ? ((int)(dq << 16) >> 16) : ((int)dq >> 16);
+    if (row < 2u) d = !mine ? 0 : row == 0u ? ((int)(dq << 16) >> 16) : ((int)dq >> 16);
     else d = gwin ? sh.dg[0][win / GV_GSTEP][row - 2u] : 0;
     if (d != 0) {
       const u32 e = (u32)((d < 0 ? -d : d) - 1);
@@ -916,7 +945,8 @@ __global__ __launch_bounds__(128) void k_verify_lat_sl(const gvk_lat b) {
       }
     }
   }
-  // ---- combine: Q rows back to the real curve, two rounds across rows
+  // ---- combine: Q rows back to the real curve, two rounds across rows,
+  // then wave 2's sum into wave 0 through LDS
   if (row < 2u) A.z = fsl_mul(A.z, zq, k);
 #pragma unroll 1
   for (int m = 16; m < 64; m <<= 1) {
@@ -926,6 +956,19 @@ __global__ __launch_bounds__(128) void k_verify_lat_sl(const gvk_lat b) {
     O.z = (u32)__shfl_xor((int)A.z, m, 64);
     const bool oinf = __shfl_xor((int)inf, m, 64) != 0;
     gjsl_add_gej(A, inf, A, inf, O, oinf, k);
+  }
+  if (wave == 2u && row == 0u) {
+    if (lo) { sh.pt[0][L] = A.x; sh.pt[1][L] = A.y; sh.pt[2][L] = A.z; }
+    if (L == 0u) sh.pinf = inf ? 1u : 0u;
+  }
+  __syncthreads();
+  if (wave == 2u) return;
+  if (split) {
+    gjsl O;
+    O.x = lo ? sh.pt[0][L] : 0u;
+    O.y = lo ? sh.pt[1][L] : 0u;
+    O.z = lo ? sh.pt[2][L] : 0u;
+    gjsl_add_gej(A, inf, A, inf, O, sh.pinf != 0u, k);
   }
   // ---- final check (as k_ecmult): x(R) mod n == r, without inversion
   const u32 fl = sh.oks[0];
@@ -1108,7 +1151,8 @@ extern "C" hipError_t gvk_verify_lat_sl(const gvk_lat* b, hipStream_t st) {
   hipError_t e = hipMemsetAsync(b->bits, 0, (size_t)((b->n + 63u) / 64u) * 8u, st);
   if (e != hipSuccess) return e;
   if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
-  hipLaunchKernelGGL(gv::k_verify_lat_sl, dim3(b->n), dim3(128), 0, st, *b);
+  const uint32_t threads = b->n <= GV_LAT_SL_SPLIT ? 192u : 128u;
+  hipLaunchKernelGGL(gv::k_verify_lat_sl, dim3(b->n), dim3(threads), 0, st, *b);
   return hipGetLastError();
 }
 
