@@ -61,10 +61,16 @@ struct fe29 { u32 n[9]; };
 // re-associates the column chains (each column summed from zero, then the
 // carries added with extra 64-bit adds) and strength-reduces the fold
 // constants into 64-bit shifts.
+// F29_BARRIER 0 drops it (A/B builds).
+#ifndef F29_BARRIER
+#define F29_BARRIER 1
+#endif
 GV_DEV u64 f29_mad(u32 a, u32 b, u64 c) {
 #if defined(__HIP_DEVICE_COMPILE__)
   u64 r = (u64)a * b + c;
+#if F29_BARRIER
   asm("" : "+v"(r));              // value barrier: keeps the chain order
+#endif
   return r;
 #else
 #if defined(GV_F29_CHECK)
