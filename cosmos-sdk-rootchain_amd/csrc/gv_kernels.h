@@ -83,6 +83,8 @@ typedef struct gvk_lat {
   const uint32_t* gtab;
   uint32_t* e_soa;              // message path: 8 rows of C words
   uint64_t* bits;
+  uint8_t* out8;                // sliced kernels: non-null -> one verdict byte per item here (e.g.
+                                // mapped pinned host memory), bits unused and not zeroed
   hipEvent_t ev[1];             // optional: after the SHA stage
   // keyed batch (kslot != NULL, pub33 unused): tables from the key arena
   const uint32_t* kslot;

@@ -992,7 +992,10 @@ __global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
     for (int i = 0; i < 8; ++i) eq &= (X[i] == T[i]);
   }
   okv &= eq;
-  if (threadIdx.x == 0 && okv) atomicOr((unsigned long long*)&b.bits[gi >> 6], 1ull << (gi & 63u));
+  if (threadIdx.x == 0) {
+    if (b.out8) b.out8[gi] = okv ? 1u : 0u;
+    else if (okv) atomicOr((unsigned long long*)&b.bits[gi >> 6], 1ull << (gi & 63u));
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1127,7 +1130,10 @@ __global__ __launch_bounds__(256) void k_verify_lat16_sl(const gvk_lat b) {
     for (int i = 0; i < 8; ++i) eq &= (X[i] == T[i]);
   }
   okv &= eq;
-  if (threadIdx.x == 0 && okv) atomicOr((unsigned long long*)&b.bits[gi >> 6], 1ull << (gi & 63u));
+  if (threadIdx.x == 0) {
+    if (b.out8) b.out8[gi] = okv ? 1u : 0u;
+    else if (okv) atomicOr((unsigned long long*)&b.bits[gi >> 6], 1ull << (gi & 63u));
+  }
 }
 
 }  // namespace gv
@@ -1148,8 +1154,10 @@ extern "C" hipError_t gvk_verify_lat_sl(const gvk_lat* b, hipStream_t st) {
     hipError_t e = gvk_sha256(b->msg_blob, b->msg_off, b->msg_len, b->n, b->C, b->e_soa, st);
     if (e != hipSuccess) return e;
   }
-  hipError_t e = hipMemsetAsync(b->bits, 0, (size_t)((b->n + 63u) / 64u) * 8u, st);
-  if (e != hipSuccess) return e;
+  if (!b->out8) {
+    hipError_t e = hipMemsetAsync(b->bits, 0, (size_t)((b->n + 63u) / 64u) * 8u, st);
+    if (e != hipSuccess) return e;
+  }
   if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
   const uint32_t threads = b->n <= GV_LAT_SL_SPLIT ? 192u : 128u;
   hipLaunchKernelGGL(gv::k_verify_lat_sl, dim3(b->n), dim3(threads), 0, st, *b);
@@ -1161,8 +1169,10 @@ extern "C" hipError_t gvk_verify_lat16_sl(const gvk_lat* b, hipStream_t st) {
     hipError_t e = gvk_sha256(b->msg_blob, b->msg_off, b->msg_len, b->n, b->C, b->e_soa, st);
     if (e != hipSuccess) return e;
   }
-  hipError_t e = hipMemsetAsync(b->bits, 0, (size_t)((b->n + 63u) / 64u) * 8u, st);
-  if (e != hipSuccess) return e;
+  if (!b->out8) {
+    hipError_t e = hipMemsetAsync(b->bits, 0, (size_t)((b->n + 63u) / 64u) * 8u, st);
+    if (e != hipSuccess) return e;
+  }
   if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
   hipLaunchKernelGGL(gv::k_verify_lat16_sl, dim3(b->n), dim3(256), 0, st, *b);
   return hipGetLastError();

@@ -215,8 +215,11 @@ struct Set {
   size_t h_blob_cap = 0;
   uint64_t* h_bits = nullptr;
   size_t h_bits_cap = 0;
+  uint8_t* h_out8 = nullptr;                      // zero-copy small batches: verdict bytes, written by the kernel
+  size_t h_out8_cap = 0;
   // chunk waiting to be harvested
   bool busy = false;
+  bool zc = false;                                // the chunk ran zero-copy (verdicts in h_out8)
   size_t c0 = 0, cn = 0;
 };
 
@@ -436,6 +439,8 @@ struct gv_ctx {
   int stage_threads = 8;        // host path: staging memcpy threads per device
   bool time_kernels = false;
   bool fault_inject = false;
+  bool lat_zero_copy = true;    // host-buffer batches on the sliced kernels read the pinned staging buffer and write
+                                // verdict bytes to pinned memory directly: no H2D, memset or D2H (GV_LAT_ZC=0: A/B)
   bool lat_sliced = true;       // small batches on k_verify_lat_sl / k_verify_lat16_sl (GV_LAT_SLICED=0: the one-lane-field kernels, A/B)
   bool keyed_k4 = true;         // keyed batches on k_ecmult_k4 (GV_KEYED_K4=0: the 125-doubling ladder, A/B)
   size_t keys = 0;              // key-arena slots in use (same on every device)
@@ -449,7 +454,7 @@ namespace {
 // set s's scratch, stream st.  The caller holds d->mu.
 int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint8_t* sig, const uint8_t* dig,
            const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint64_t* bits_out,
-           hipStream_t st, const uint32_t* kslot = nullptr) {
+           hipStream_t st, const uint32_t* kslot = nullptr, uint8_t* out8 = nullptr) {
   if (n == 0 || n > kMaxItems) return GV_EINVAL;
   const size_t C = round_up(n, 256);
   int rc = ensure_cap(s, C);
@@ -497,6 +502,8 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
       lb.kslot = kslot; lb.kqt = b.kqt; lb.kzq = b.kzq; lb.kok = b.kok; lb.kC = b.kC; lb.kcount = b.kcount;
     }
     const bool sliced = ctx->lat_sliced && n <= ctx->lat_sl_max;
+    if (out8 && !sliced) return GV_EINVAL;      // byte verdicts: the sliced kernels only
+    lb.out8 = out8;
     if (kslot) {                                // keyed: 16 lanes per signature (group tables)
       lb.kqt2 = d->kqt2; lb.kzq2 = d->kzq2; lb.glat = d->glat;
       if (sliced) CK(gvk_verify_lat16_sl(&lb, st));
@@ -535,6 +542,20 @@ struct HostBatch {
 int harvest(Dev* d, Set* s, const HostBatch& hb) {
   CK(hipEventSynchronize(s->done));
   const size_t c0 = s->c0, cn = s->cn, words = (cn + 63) / 64;
+  if (s->zc) {                                  // zero-copy small batch: verdict bytes in h_out8
+    if (hb.out_ok) {
+      memcpy(hb.out_ok + c0, s->h_out8, cn);
+    } else {                                    // c0 % 64 == 0
+      for (size_t w = 0; w < words; ++w) {
+        uint64_t v = 0;
+        const size_t lim = std::min<size_t>(64, cn - 64 * w);
+        for (size_t i = 0; i < lim; ++i) v |= (uint64_t)(s->h_out8[64 * w + i] & 1u) << i;
+        hb.out_bits[c0 / 64 + w] = v;
+      }
+    }
+    s->busy = false;
+    return GV_OK;
+  }
   if (hb.out_ok) {
     uint8_t* o = hb.out_ok + c0;
     const uint64_t* w = s->h_bits;
@@ -592,6 +613,20 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
     if ((rc = ensure_blob(s, hb_bytes))) return rc;
     par_copy(d->pool, s->h_blob, hb.blob + bmin, hb_bytes);
   }
+  if (!msgs && ctx->lat_zero_copy && ctx->lat_sliced && cn <= ctx->lat_sl_max && cn <= ctx->lat_max) {
+    // zero-copy small batch: the kernel reads the pinned staging buffer and
+    // writes one verdict byte per item to pinned memory (no H2D / memset / D2H)
+    if ((rc = ensure_pinned(&s->h_out8, &s->h_out8_cap, cn))) return rc;
+    rc = launch(ctx, d, s, cn, keyed ? nullptr : h, h + L.sig, h + L.third, nullptr, nullptr, nullptr, nullptr,
+                s->st, keyed ? (const uint32_t*)h : nullptr, s->h_out8);
+    if (rc) return rc;
+    CK(hipEventRecord(s->done, s->st));
+    s->busy = true;
+    s->zc = true;
+    s->c0 = c0;
+    s->cn = cn;
+    return GV_OK;
+  }
   if ((rc = set_acquire(s, s->st))) return rc;
   CK(hipMemcpyAsync(s->d_in, h, msgs ? L.total : L.third + cn * 32, hipMemcpyHostToDevice, s->st));
   if (msgs && hb_bytes) CK(hipMemcpyAsync(s->d_blob, s->h_blob, hb_bytes, hipMemcpyHostToDevice, s->st));
@@ -605,6 +640,7 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
   CK(hipEventRecord(s->done, s->st));
   if ((rc = set_release(s, s->st))) return rc;
   s->busy = true;
+  s->zc = false;
   s->c0 = c0;
   s->cn = cn;
   return GV_OK;
@@ -776,6 +812,7 @@ void free_set(Set& s) {
   if (s.h_in) (void)hipHostFree(s.h_in);
   if (s.h_blob) (void)hipHostFree(s.h_blob);
   if (s.h_bits) (void)hipHostFree(s.h_bits);
+  if (s.h_out8) (void)hipHostFree(s.h_out8);
   if (s.last) (void)hipEventDestroy(s.last);
   if (s.done) (void)hipEventDestroy(s.done);
   if (s.st) (void)hipStreamDestroy(s.st);
@@ -813,6 +850,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   parse_size_env("GV_MAX_BATCH", &ctx->max_batch);
   if (const char* k4 = getenv("GV_KEYED_K4")) ctx->keyed_k4 = strcmp(k4, "0") != 0;
   if (const char* ls = getenv("GV_LAT_SLICED")) ctx->lat_sliced = strcmp(ls, "0") != 0;
+  if (const char* zc = getenv("GV_LAT_ZC")) ctx->lat_zero_copy = strcmp(zc, "0") != 0;
   for (size_t k = 0; k < ids.size(); ++k) {
     Dev* d = new Dev();
     d->id = ids[k];
@@ -1066,6 +1104,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "lat_sl_max")) {
     if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
     ctx->lat_sl_max = (size_t)val;
+  } else if (!strcmp(key, "lat_zero_copy")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->lat_zero_copy = val != 0;
   } else if (!strcmp(key, "lat_sliced")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->lat_sliced = val != 0;

@@ -175,6 +175,9 @@ int gv_dev_verify_ed25519_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* 
  * block; larger ones up to lat_max the four-lanes-per-signature
  * k_verify_lat / k_verify_lat16; default 2048),
  * "lat_sliced" (0/1: 0 never takes the sliced kernels; default 1),
+ * "lat_zero_copy" (0/1: host-buffer digest batches on the sliced kernels
+ * are read by the kernel straight from the pinned staging buffer and answered
+ * as verdict bytes in pinned memory -- no H2D, memset or D2H; default 1),
  * "pipe_chunk" (host-buffer calls past lat_max: first chunk of the two-stream
  * copy/compute pipeline per device, default 131072; 0 = one chunk per
  * max_batch), "pipe_growth" (each later chunk at most this many times the one
