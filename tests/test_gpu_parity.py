@@ -463,3 +463,25 @@ def test_sliced_latency_kernels_at_scale(ver):
         ver.set_option("lat_max", gvm.LAT_MAX_DEFAULT)
         ver.set_option("lat_sl_max", gvm.LAT_SL_MAX_DEFAULT)
         ver.keys_reset()
+
+
+@pytest.mark.parametrize("zc", [0, 1])
+def test_small_batches_zero_copy_and_staged(ver, zc):
+    """Host-buffer small batches on the sliced kernels, zero-copy (the kernel
+    reads the pinned staging buffer, verdict bytes in pinned memory) and staged
+    (H2D + bitmap + D2H): same verdicts, byte and bitmap entry points, pub33
+    and keyed."""
+    pub, sig, dig = make_random_batch(700, seed=0x2C + zc, adversarial=0.3, nkeys=9)
+    want = O.verify_digests(pub, sig, dig, threads=8)
+    ver.set_option("lat_zero_copy", zc)
+    try:
+        assert np.array_equal(ver.verify_batch_digests(pub, sig, dig), want)
+        bits = ver.verify_batch_digests_bits(pub, sig, dig)
+        assert np.array_equal(np.unpackbits(bits.view(np.uint8), bitorder="little")[:700], want)
+        assert (int(bits[-1]) >> (700 % 64)) == 0
+        uniq, inv = np.unique(pub, axis=0, return_inverse=True)
+        slots = ver.keys_load(uniq)[inv.reshape(-1)]
+        assert np.array_equal(ver.verify_batch_digests_keyed(slots, sig, dig), want)
+    finally:
+        ver.set_option("lat_zero_copy", 1)
+        ver.keys_reset()
