@@ -915,19 +915,17 @@ __global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
   const u32* gbase = b.gtab + (row == 3u ? (size_t)GV_GTAB_N * 16u : 0u);
 #pragma unroll 1
   for (int win = GV_QWIN - 1; win >= 0; --win) {
-    if (win != GV_QWIN - 1) {
-#pragma unroll 1
-      for (int d = 0; d < GV_QW; ++d) gjsl_double(A, A, k);
-    }
+    // the window's entry is fetched before its doublings: the G rows' global
+    // loads (and the LDS reads) complete under the ~4 us of doubling work
     const bool gwin = (win % GV_GSTEP) == 0 && wave == 0u;
     const bool mine = par < 0 || (win & 1) == par;
     const u32 dq = sh.dq[0][win];
     int d;
     if (row < 2u) d = !mine ? 0 : row == 0u ? ((int)(dq << 16) >> 16) : ((int)dq >> 16);
     else d = gwin ? sh.dg[0][win / GV_GSTEP][row - 2u] : 0;
+    u32 x = 0u, y = 0u;
     if (d != 0) {
       const u32 e = (u32)((d < 0 ? -d : d) - 1);
-      u32 x, y;
       if (row < 2u) {
         x = lo ? sh.qtab[row][e][L] : 0u;
         y = lo ? sh.qtab[row][e][9 + L] : 0u;
@@ -936,6 +934,12 @@ __global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
         x = fsl_load_words(pe, k);
         y = fsl_load_words(pe + 8, k);
       }
+    }
+    if (win != GV_QWIN - 1) {
+#pragma unroll 1
+      for (int dd = 0; dd < GV_QW; ++dd) gjsl_double(A, A, k);
+    }
+    if (d != 0) {
       if (d < 0) y = k.bias - y;
       if (inf) {
         A.x = x; A.y = fsl_norm(y, k); A.z = L == 0u ? 1u : 0u;
@@ -1046,25 +1050,29 @@ __global__ __launch_bounds__(256) void k_verify_lat16_sl(const gvk_lat b) {
   bool inf = true;
 #pragma unroll 1
   for (int win = w_hi; win >= w_lo; --win) {
-    if (win != w_hi) {
-#pragma unroll 1
-      for (int d = 0; d < GV_QW; ++d) gjsl_double(A, A, k);
-    }
+    // the window's entry (HBM: key arena / glat) is fetched before its
+    // doublings, so the load latency hides under them
     const u32 dw = part < 2u ? sh.dq[0][win] : sh.dg5[0][win];
     const int d = (part & 1u) == 0u ? ((int)(dw << 16) >> 16) : ((int)dw >> 16);
+    u32 x = 0u, y = 0u;
     if (d != 0) {
       const u32 e = (u32)((d < 0 ? -d : d) - 1);
-      u32 x, y;
       if (part < 2u) {                                  // Q / lambda Q: arena row, 29-bit limbs
         const u32* pe = qrow + (size_t)e * GV_QENT_WORDS;
         x = lo ? pe[L] : 0u;
         y = lo ? pe[9 + L] : 0u;
-        if (part == 1u) x = fsl_mul(x, beta, k);        // lambda Q = (beta x, y), same Z
       } else {                                          // G / lambda G: affine words
         const u32* pe = grow + (size_t)e * 16u;
         x = fsl_load_words(pe, k);
         y = fsl_load_words(pe + 8, k);
       }
+    }
+    if (win != w_hi) {
+#pragma unroll 1
+      for (int dd = 0; dd < GV_QW; ++dd) gjsl_double(A, A, k);
+    }
+    if (d != 0) {
+      if (part == 1u) x = fsl_mul(x, beta, k);          // lambda Q = (beta x, y), same Z
       if (d < 0) y = k.bias - y;
       if (inf) {
         A.x = x; A.y = fsl_norm(y, k); A.z = L == 0u ? 1u : 0u;

@@ -13,6 +13,8 @@
 #include "../../cosmos-sdk-rootchain_amd/csrc/secp_group29.cuh"
 #include "../../cosmos-sdk-rootchain_amd/csrc/secp_group29x.cuh"
 #include "../../cosmos-sdk-rootchain_amd/csrc/secp_fsl.cuh"
+#include "../../cosmos-sdk-rootchain_amd/csrc/secp_modinv_sl.cuh"
+#include "../../cosmos-sdk-rootchain_amd/csrc/secp_scalar.cuh"
 
 using namespace gv;
 #define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
@@ -111,14 +113,14 @@ __global__ __launch_bounds__(64) void k_check(int test, int iters, u32* bad) {
   if ((threadIdx.x & 15u) == 0) atomicAdd(bad, nbad);
 }
 
-enum { L_MUL, L_SQRS, L_DBL, L_ADD, L_N };
-static const char* kL[L_N] = {"fsl_mul", "fsl_sqr", "gjsl_double", "gjsl_add_scaled"};
-static const int kLI[L_N] = {256, 256, 64, 64};
+enum { L_MUL, L_SQRS, L_DBL, L_ADD, L_INV, L_GLV, L_N };
+static const char* kL[L_N] = {"fsl_mul", "fsl_sqr", "gjsl_double", "gjsl_add_scaled", "s30_modinv_sl", "glv_split"};
+static const int kLI[L_N] = {256, 256, 64, 64, 8, 32};
 
 __global__ __launch_bounds__(64) void k_lat(int op, int iters, uint64_t* t, u32* sink) {
   const fslk k = fsl_consts();
   u32 w[8];
-  seed(w, threadIdx.x >> 4, 1, 0);
+  seed(w, 0, 1, 0);
   fe29 A; f29_from_words(A, w);
   u32 a = fsl_scatter(A, k), b = a ^ 0x1234u;
   b &= k.m29;
@@ -142,6 +144,24 @@ __global__ __launch_bounds__(64) void k_lat(int op, int iters, uint64_t* t, u32*
     case L_ADD:
 #pragma unroll 1
       for (int i = 0; i < iters; ++i) gjsl_add_scaled(Q, inf, a, b, Q.z, k);
+      break;
+    case L_INV:                                  // whole wave, the same scalar in every lane
+#pragma unroll 1
+      for (int i = 0; i < iters; ++i) {
+        w[0] |= 1u;
+        w[7] &= 0x7FFFFFFFu;
+        s30_modinv_sl(w, w, k);
+      }
+      a ^= w[0];
+      break;
+    case L_GLV:
+#pragma unroll 1
+      for (int i = 0; i < iters; ++i) {
+        u32 k1[4], k2[4], n1, n2;
+        glv_split(k1, n1, k2, n2, w);
+        w[0] ^= k1[0] ^ n1; w[1] ^= k2[1] ^ n2;
+      }
+      a ^= w[0];
       break;
   }
   const uint64_t c1 = clock64(), w1 = wall_clock64();
