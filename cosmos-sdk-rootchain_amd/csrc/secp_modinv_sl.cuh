@@ -95,8 +95,12 @@ GV_DEV void s30_modinv_sl(uint32_t w[8], const uint32_t x[8], const fslk& k) {
     if (__ballot(g != 0) == 0ull) break;
     const u32 f0 = fsl_bc<0>((u32)f), f1 = fsl_bc<1>((u32)f);
     const u32 g0 = fsl_bc<0>((u32)g), g1 = fsl_bc<1>((u32)g);
+    // the low words are the same in every lane: readfirstlane makes the
+    // divsteps wave-uniform, so they compile to scalar (SALU) code
+    const u32 flo = (u32)__builtin_amdgcn_readfirstlane((int)(f0 + (f1 << 30)));
+    const u32 glo = (u32)__builtin_amdgcn_readfirstlane((int)(g0 + (g1 << 30)));
     int32_t t[4];
-    eta = s30_divsteps_var(eta, f0 + (f1 << 30), g0 + (g1 << 30), t);
+    eta = s30_divsteps_var(eta, flo, glo, t);
     const int64_t cf = (int64_t)t[0] * f + (int64_t)t[1] * g;
     const int64_t cg = (int64_t)t[2] * f + (int64_t)t[3] * g;
     f = msl_div30(cf, L);
