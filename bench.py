@@ -208,11 +208,14 @@ def _pct(ts):
 
 
 def checktx_latency(ver, pub, sig, dig, threads, sizes=(1, 16, 32, 64, 128, 256, 1024, 4096), reps=1000):
-    """C5: host-path latency (pack -> H2D -> kernel(s) -> D2H -> verdicts) per
-    batch size.  p50/p99 are the default GPU path (the fused latency kernel,
-    gv_lat.hip, up to the "lat_max" option); next to it the throughput pipeline
-    forced for the same batches, the keyed path (account keys in the HBM key
-    arena, gv_verify_digests_keyed), and the CPU oracle (oracle/secp256k1_oracle.c,
+    """C5: host-path latency (host buffers in -> verdicts out) per batch size.
+    p50/p99 are the default GPU path: up to "lat_sl_max" (2048) the limb-sliced
+    small-batch kernels (gv_lat.hip k_verify_lat_sl / k_verify_lat16_sl, one
+    signature per block) reading the pinned staging buffer zero-copy, up to
+    "lat_max" (8192) the four-lanes-per-signature kernel, the pipeline above
+    ("schedule" per size); next to it the throughput pipeline forced for the
+    same batches, the keyed path (account keys in the HBM key arena,
+    gv_verify_digests_keyed), and the CPU oracle (oracle/secp256k1_oracle.c,
     the reference algorithm restated in C) serial and on `threads` cores."""
     from oracle import oracle as O
     O.lib()
@@ -252,7 +255,10 @@ def checktx_latency(ver, pub, sig, dig, threads, sizes=(1, 16, 32, 64, 128, 256,
                 if time.perf_counter() > budget and len(ts) >= 3:
                     break
             cpu[label] = _pct(ts)[0]
-        out[str(b)] = {"p50_ms": p50, "p99_ms": p99, "throughput_path_p50_ms": tp50, "keyed_p50_ms": keyed50, **cpu}
+        sched = ("k_verify_lat_sl (limb-sliced, zero-copy)" if b <= gvm.LAT_SL_MAX_DEFAULT else
+                 "k_verify_lat (4 lanes per signature)" if b <= gvm.LAT_MAX_DEFAULT else "pipeline")
+        out[str(b)] = {"p50_ms": p50, "p99_ms": p99, "throughput_path_p50_ms": tp50, "keyed_p50_ms": keyed50, **cpu,
+                       "schedule": sched}
     ver.keys_reset()
     return out
 
