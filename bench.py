@@ -214,12 +214,20 @@ def checktx_latency(ver, pub, sig, dig, threads, sizes=(1, 16, 32, 64, 128, 256,
     signature per block) reading the pinned staging buffer zero-copy, up to
     "lat_max" (8192) the four-lanes-per-signature kernel, the pipeline above
     ("schedule" per size); next to it the throughput pipeline forced for the
-    same batches, the keyed path (account keys in the HBM key arena,
+    same batches, the message path (gv_verify_msgs over ~355-byte StdSignBytes:
+    SHA-256 on the GPU, "msgs_p50_ms"), the keyed path (account keys in the HBM key arena,
     gv_verify_digests_keyed), and the CPU oracle (oracle/secp256k1_oracle.c,
     the reference algorithm restated in C) serial and on `threads` cores."""
     from oracle import oracle as O
+    if os.path.join(REPO, "tools") not in sys.path:
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+    import bench_extras as X
     O.lib()
     out = {}
+    # the message path (gv_verify_msgs: SHA-256 of the StdSignBytes on the GPU,
+    # what the Go drop-in's CheckTx calls): 4,096 C1 sign-bytes items
+    mn = 4096
+    mpub, msig, (mblob, moff, mln), _ = X.c1_items(workload_lib(), mn, threads, 1024)
     nkeys = 65536                                   # the C2 workload's keys, item i uses key i % nkeys
     ver.keys_reset()
     slots = ver.keys_load(pub[:nkeys])[np.arange(len(pub)) % nkeys]
@@ -240,6 +248,13 @@ def checktx_latency(ver, pub, sig, dig, threads, sizes=(1, 16, 32, 64, 128, 256,
             ver.verify_batch_digests_keyed(slots[o:o + b], sig[o:o + b], dig[o:o + b])
             ts.append(time.perf_counter() - t)
         keyed50, _ = _pct(ts[5:])
+        ts = []
+        for r in range(reps // 2 + 5):
+            o = (r * b) % (mn - b) if b < mn else 0
+            t = time.perf_counter()
+            ver.verify_batch_msgs(mpub[o:o + b], msig[o:o + b], (mblob, moff[o:o + b], mln[o:o + b]))
+            ts.append(time.perf_counter() - t)
+        msgs50, _ = _pct(ts[5:])
         ver.set_option("lat_max", 0)
         tp50, _ = _pct(run_gpu(max(20, reps // 4)))
         ver.set_option("lat_max", gvm.LAT_MAX_DEFAULT)
@@ -257,8 +272,8 @@ def checktx_latency(ver, pub, sig, dig, threads, sizes=(1, 16, 32, 64, 128, 256,
             cpu[label] = _pct(ts)[0]
         sched = ("k_verify_lat_sl (limb-sliced, zero-copy)" if b <= gvm.LAT_SL_MAX_DEFAULT else
                  "k_verify_lat (4 lanes per signature)" if b <= gvm.LAT_MAX_DEFAULT else "pipeline")
-        out[str(b)] = {"p50_ms": p50, "p99_ms": p99, "throughput_path_p50_ms": tp50, "keyed_p50_ms": keyed50, **cpu,
-                       "schedule": sched}
+        out[str(b)] = {"p50_ms": p50, "p99_ms": p99, "throughput_path_p50_ms": tp50, "keyed_p50_ms": keyed50,
+                       "msgs_p50_ms": msgs50, **cpu, "schedule": sched}
     ver.keys_reset()
     return out
 
