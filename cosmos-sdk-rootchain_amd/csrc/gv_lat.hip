@@ -33,6 +33,7 @@
 #include "secp_modinv.cuh"
 #include "secp_fsl.cuh"
 #include "secp_modinv_sl.cuh"
+#include "secp_sha256.cuh"
 #include "gv_kernels.h"
 
 static_assert(F29_NCH == 2, "gv_lat.hip is built with -DF29_NCH=2");
@@ -342,15 +343,13 @@ struct Lat16Shared {
 // the same signature in every lane (the sliced kernels); s^-1 by the
 // variable-time divsteps with the state vectors sliced over the lanes
 // (s30_modinv_sl).  Otherwise one signature per lane, lockstep divsteps.
-template <bool VAR = false, class SH>
-GV_DEV void lat_scalars(SH& sh, int sig, bool live, const uint8_t* sig64, const uint8_t* dig32,
-                        const u32* e_soa, u32 C, u32 gi) {
+template <bool VAR = false, class SH, class GetE>
+GV_DEV void lat_scalars_e(SH& sh, int sig, bool live, const uint8_t* sig64, GetE get_e) {
   u32 r[8], s[8], e[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     r[i] = live ? be32(sig64 + 4 * (7 - i)) : 0u;
     s[i] = live ? be32(sig64 + 32 + 4 * (7 - i)) : 0u;
-    e[i] = !live ? 0u : dig32 ? be32(dig32 + 4 * (7 - i)) : e_soa[(size_t)i * C + gi];
   }
   bool ok = live;
   ok &= !u256_is_zero(r);
@@ -358,10 +357,9 @@ GV_DEV void lat_scalars(SH& sh, int sig, bool live, const uint8_t* sig64, const 
   ok &= !u256_is_zero(s);
   ok &= u256_geq(kHalfN, s);                // tendermint low-S: s <= N/2
   const bool r_small = !u256_geq(r, kPminusN);
-  sc_reduce_once(e);                        // e mod n
   if (!ok) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { s[i] = (i == 0) ? 1u : 0u; e[i] = 0u; r[i] = 0u; }
+    for (int i = 0; i < 8; ++i) { s[i] = (i == 0) ? 1u : 0u; r[i] = 0u; }
   }
   u32 u1[8], u2[8];
   {
@@ -378,6 +376,18 @@ GV_DEV void lat_scalars(SH& sh, int sig, bool live, const uint8_t* sig64, const 
     sc29_to_mont(sm, s29);
     sc29_inv(w, sm);                        // s^-1 (Montgomery form), Fermat chain
 #endif
+    // e is needed only from here: a message digest computed by another wave
+    // meanwhile (get_e may wait for it)
+    get_e(e);
+    if (!live) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) e[i] = 0u;
+    }
+    sc_reduce_once(e);                      // e mod n
+    if (!ok) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) e[i] = 0u;
+    }
     sc29_from_words(e29, e);
     sc29_from_words(r29, r);
     sc29_mul(t, e29, w);
@@ -420,6 +430,18 @@ GV_DEV void lat_scalars(SH& sh, int sig, bool live, const uint8_t* sig64, const 
 #pragma unroll
   for (int i = 0; i < 8; ++i) sh.r[sig][i] = r[i];
   sh.oks[sig] = (ok ? 1u : 0u) | (r_small ? 2u : 0u);
+}
+
+// e from the digest bytes (dig32), the SHA state words (eh) or the SoA rows
+// written by k_sha256 (e_soa, stride C)
+template <bool VAR = false, class SH>
+GV_DEV void lat_scalars(SH& sh, int sig, bool live, const uint8_t* sig64, const uint8_t* dig32,
+                        const u32* e_soa, u32 C, u32 gi, const u32* eh = nullptr) {
+  lat_scalars_e<VAR>(sh, sig, live, sig64, [&](u32 e[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      e[i] = !live ? 0u : eh ? eh[7 - i] : dig32 ? be32(dig32 + 4 * (7 - i)) : e_soa[(size_t)i * C + gi];
+  });
 }
 
 GV_DEV void shfl_xor_gej(gej29& o, bool& oinf, const gej29& a, bool ainf, int m) {
@@ -893,8 +915,13 @@ __global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
   const u32 gi = blockIdx.x;                            // grid = n: every block is live
   const u32 wave = threadIdx.x >> 6;
   if (wave == 1u) {                                     // the scalar chain, whole wave (own SIMD)
-    lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.msg_blob ? nullptr : b.dig32 + (size_t)gi * 32u,
-                      b.msg_blob ? (const u32*)b.e_soa : nullptr, b.C, gi);
+    if (b.msg_len) {                                    // message path: SHA-256 of the sign bytes here
+      u32 eh[8];
+      sha256_msg_wave(eh, b.msg_blob + b.msg_off[gi], b.msg_len[gi]);
+      lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, nullptr, nullptr, b.C, gi, eh);
+    } else {
+      lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.dig32 + (size_t)gi * 32u, nullptr, b.C, gi);
+    }
     __syncthreads();
     __syncthreads();
     return;
@@ -1012,6 +1039,7 @@ __global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
 // wave 0) the whole sum, and wave 0 runs the final check.
 struct Lat16SlShared {
   static constexpr bool kG5 = true;
+  u32 eh[8];                                // message path: the SHA-256 state of the sign bytes (wave 1)
   u32 dq[1][GV_QWIN];
   u32 dg5[1][GV_QWIN];
   u32 r[1][8];
@@ -1027,9 +1055,29 @@ __global__ __launch_bounds__(256) void k_verify_lat16_sl(const gvk_lat b) {
   bool kok = sl < b.kcount;
   if (!kok) sl = 0;                                     // the arena always holds slot 0's memory
   kok = kok && b.kok[sl] != 0u;
-  if (threadIdx.x < 64)                                 // wave 0: the scalar chain, whole wave
-    lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.msg_blob ? nullptr : b.dig32 + (size_t)gi * 32u,
-                b.msg_blob ? (const u32*)b.e_soa : nullptr, b.C, gi);
+  if (b.msg_len) {
+    // message path: wave 1 hashes the sign bytes while wave 0 runs the
+    // scalar chain up to s^-1; one extra barrier hands the digest over
+    if (threadIdx.x < 64) {
+      lat_scalars_e<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, [&](u32 e[8]) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = sh.eh[7 - i];
+      });
+    } else {
+      if (threadIdx.x < 128) {
+        u32 eh[8];
+        sha256_msg_wave(eh, b.msg_blob + b.msg_off[gi], b.msg_len[gi]);
+        if (threadIdx.x == 64) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) sh.eh[i] = eh[i];
+        }
+      }
+      __syncthreads();
+    }
+  } else if (threadIdx.x < 64) {                        // wave 0: the scalar chain, whole wave
+    lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.dig32 + (size_t)gi * 32u, nullptr, b.C, gi);
+  }
   __syncthreads();
   const fslk k = fsl_consts();
   const u32 L = k.L, part = (threadIdx.x >> 4) & 3u, grp = threadIdx.x >> 6;
@@ -1158,10 +1206,7 @@ extern "C" hipError_t gvk_verify_lat16(const gvk_lat* b, hipStream_t st) {
 }
 
 extern "C" hipError_t gvk_verify_lat_sl(const gvk_lat* b, hipStream_t st) {
-  if (b->msg_blob) {
-    hipError_t e = gvk_sha256(b->msg_blob, b->msg_off, b->msg_len, b->n, b->C, b->e_soa, st);
-    if (e != hipSuccess) return e;
-  }
+  // message path: the kernel's scalar wave hashes the sign bytes itself
   if (!b->out8) {
     hipError_t e = hipMemsetAsync(b->bits, 0, (size_t)((b->n + 63u) / 64u) * 8u, st);
     if (e != hipSuccess) return e;
@@ -1173,10 +1218,7 @@ extern "C" hipError_t gvk_verify_lat_sl(const gvk_lat* b, hipStream_t st) {
 }
 
 extern "C" hipError_t gvk_verify_lat16_sl(const gvk_lat* b, hipStream_t st) {
-  if (b->msg_blob) {
-    hipError_t e = gvk_sha256(b->msg_blob, b->msg_off, b->msg_len, b->n, b->C, b->e_soa, st);
-    if (e != hipSuccess) return e;
-  }
+  // message path: the kernel's scalar wave hashes the sign bytes itself
   if (!b->out8) {
     hipError_t e = hipMemsetAsync(b->bits, 0, (size_t)((b->n + 63u) / 64u) * 8u, st);
     if (e != hipSuccess) return e;

@@ -609,16 +609,19 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
     uint64_t* ro = (uint64_t*)(h + L.third);
     for (size_t i = 0; i < cn; ++i) ro[i] = hb.off[c0 + i] - bmin;
     memcpy(h + L.len, hb.len + c0, cn * 4);
-    if ((rc = ensure_pinned(&s->h_blob, &s->h_blob_cap, hb_bytes))) return rc;
+    if ((rc = ensure_pinned(&s->h_blob, &s->h_blob_cap, std::max<size_t>(hb_bytes, 1)))) return rc;
     if ((rc = ensure_blob(s, hb_bytes))) return rc;
     par_copy(d->pool, s->h_blob, hb.blob + bmin, hb_bytes);
   }
-  if (!msgs && ctx->lat_zero_copy && ctx->lat_sliced && cn <= ctx->lat_sl_max && cn <= ctx->lat_max) {
-    // zero-copy small batch: the kernel reads the pinned staging buffer and
-    // writes one verdict byte per item to pinned memory (no H2D / memset / D2H)
+  if (ctx->lat_zero_copy && ctx->lat_sliced && cn <= ctx->lat_sl_max && cn <= ctx->lat_max) {
+    // zero-copy small batch: the kernel reads the pinned staging buffers
+    // (messages too: its scalar wave hashes them) and writes one verdict byte
+    // per item to pinned memory (no H2D / memset / D2H)
     if ((rc = ensure_pinned(&s->h_out8, &s->h_out8_cap, cn))) return rc;
-    rc = launch(ctx, d, s, cn, keyed ? nullptr : h, h + L.sig, h + L.third, nullptr, nullptr, nullptr, nullptr,
-                s->st, keyed ? (const uint32_t*)h : nullptr, s->h_out8);
+    rc = launch(ctx, d, s, cn, keyed ? nullptr : h, h + L.sig, msgs ? nullptr : h + L.third,
+                msgs ? s->h_blob : nullptr, msgs ? (const uint64_t*)(h + L.third) : nullptr,
+                msgs ? (const uint32_t*)(h + L.len) : nullptr, nullptr, s->st,
+                keyed ? (const uint32_t*)h : nullptr, s->h_out8);
     if (rc) return rc;
     CK(hipEventRecord(s->done, s->st));
     s->busy = true;

@@ -15,6 +15,7 @@
 #include "../../cosmos-sdk-rootchain_amd/csrc/secp_fsl.cuh"
 #include "../../cosmos-sdk-rootchain_amd/csrc/secp_modinv_sl.cuh"
 #include "../../cosmos-sdk-rootchain_amd/csrc/secp_scalar.cuh"
+#include "../../cosmos-sdk-rootchain_amd/csrc/secp_sha256.cuh"
 
 using namespace gv;
 #define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
@@ -113,11 +114,11 @@ __global__ __launch_bounds__(64) void k_check(int test, int iters, u32* bad) {
   if ((threadIdx.x & 15u) == 0) atomicAdd(bad, nbad);
 }
 
-enum { L_MUL, L_SQRS, L_DBL, L_ADD, L_INV, L_GLV, L_N };
-static const char* kL[L_N] = {"fsl_mul", "fsl_sqr", "gjsl_double", "gjsl_add_scaled", "s30_modinv_sl", "glv_split"};
-static const int kLI[L_N] = {256, 256, 64, 64, 8, 32};
+enum { L_MUL, L_SQRS, L_DBL, L_ADD, L_INV, L_GLV, L_SHAW, L_SHA1, L_N };
+static const char* kL[L_N] = {"fsl_mul", "fsl_sqr", "gjsl_double", "gjsl_add_scaled", "s30_modinv_sl", "glv_split", "sha256_msg_wave_355B", "sha256_msg_lane_355B"};
+static const int kLI[L_N] = {256, 256, 64, 64, 8, 32, 8, 8};
 
-__global__ __launch_bounds__(64) void k_lat(int op, int iters, uint64_t* t, u32* sink) {
+__global__ __launch_bounds__(64) void k_lat(int op, int iters, uint64_t* t, u32* sink, const uint8_t* msg) {
   const fslk k = fsl_consts();
   u32 w[8];
   seed(w, 0, 1, 0);
@@ -154,6 +155,24 @@ __global__ __launch_bounds__(64) void k_lat(int op, int iters, uint64_t* t, u32*
       }
       a ^= w[0];
       break;
+    case L_SHAW:
+#pragma unroll 1
+      for (int i = 0; i < iters; ++i) {
+        u32 h[8];
+        sha256_msg_wave(h, msg + (w[0] & 7u), 355);
+        w[0] ^= h[0]; w[1] ^= h[7];
+      }
+      a ^= w[0];
+      break;
+    case L_SHA1:
+#pragma unroll 1
+      for (int i = 0; i < iters; ++i) {
+        u32 h[8];
+        sha256_msg(h, msg + (w[0] & 7u), 355);
+        w[0] ^= h[0]; w[1] ^= h[7];
+      }
+      a ^= w[0];
+      break;
     case L_GLV:
 #pragma unroll 1
       for (int i = 0; i < iters; ++i) {
@@ -176,6 +195,9 @@ int main() {
   CHK(hipMalloc(&bad, 4));
   CHK(hipMalloc(&dt, 16));
   CHK(hipMalloc(&sink, 256));
+  uint8_t* msg;
+  CHK(hipMalloc(&msg, 1024));
+  CHK(hipMemset(msg, 0x5A, 1024));
   printf("{\"mismatches\": {");
   for (int t = 0; t < T_N; ++t) {
     CHK(hipMemset(bad, 0, 4));
@@ -189,7 +211,7 @@ int main() {
   for (int op = 0; op < L_N; ++op) {
     double best = 1e30, cyc = 0;
     for (int rep = 0; rep < 5; ++rep) {
-      hipLaunchKernelGGL(k_lat, dim3(1), dim3(64), 0, 0, op, kLI[op], dt, sink);
+      hipLaunchKernelGGL(k_lat, dim3(1), dim3(64), 0, 0, op, kLI[op], dt, sink, msg);
       CHK(hipDeviceSynchronize());
       uint64_t h[2];
       CHK(hipMemcpy(h, dt, 16, hipMemcpyDeviceToHost));
