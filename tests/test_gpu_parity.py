@@ -485,3 +485,38 @@ def test_small_batches_zero_copy_and_staged(ver, zc):
     finally:
         ver.set_option("lat_zero_copy", 1)
         ver.keys_reset()
+
+
+@pytest.mark.parametrize("zc", [0, 1])
+def test_message_lengths_at_block_and_chunk_edges(ver, zc):
+    """The sliced kernels hash the sign bytes themselves (sha256_msg_wave:
+    256-byte chunks, one word per lane, the next chunk prefetched): every
+    padding edge (55/56/63/64 mod 64) and chunk edge (multiples of 256, and
+    the 4-block boundary the padding can spill over), empty and long
+    messages, pub33 and keyed, zero-copy and staged, against the oracle."""
+    rng = random.Random(0x5A + zc)
+    lens = [0, 1, 55, 56, 57, 63, 64, 65, 119, 120, 127, 128, 183, 184, 191, 192, 247, 248, 255, 256, 257,
+            311, 312, 319, 320, 503, 504, 511, 512, 513, 1015, 1016, 1023, 1024, 1025, 2048, 4000]
+    msgs, pubs, sigs, want = [], [], [], []
+    for i, L in enumerate(lens * 2):
+        d = rng.randrange(1, N)
+        msg = rng.randbytes(L)
+        priv = d.to_bytes(32, "big")
+        sig = bytearray(O.sign(priv, O.sha256(msg)))
+        if i >= len(lens):                      # second copy: one flipped message bit
+            msg = bytes(msg[:-1]) + bytes([msg[-1] ^ 1]) if L else b"\x00"
+        pub = O.pubkey(priv)
+        msgs.append(msg)
+        pubs.append(np.frombuffer(pub, np.uint8))
+        sigs.append(np.frombuffer(bytes(sig), np.uint8))
+        want.append(O.verify_bytes(pub, msg, bytes(sig)))
+    pubs, sigs, want = np.array(pubs), np.array(sigs), np.array(want, dtype=np.uint8)
+    assert want[:len(lens)].all() and not want[len(lens):].any()
+    ver.set_option("lat_zero_copy", zc)
+    try:
+        assert np.array_equal(ver.verify_batch_msgs(pubs, sigs, msgs), want)
+        slots = ver.keys_load(pubs)
+        assert np.array_equal(ver.verify_batch_msgs_keyed(slots, sigs, msgs), want)
+    finally:
+        ver.set_option("lat_zero_copy", 1)
+        ver.keys_reset()
