@@ -821,6 +821,7 @@ GV_DEV void lat_sl_prep(LatSlShared& sh, const gvk_lat& b, u32 gi, const fslk& k
   }
   if ((y8.v[0] & 1u) != (pre & 1u)) fe_neg(y8, y8);
   fe_normalize(y8);
+  LAT_STAMP(1);                                         // trace builds: key decompressed
   if (!ok) {                                            // harmless stand-in point: G
     const u32 gx[8] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu,
                        0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu};
@@ -899,6 +900,7 @@ GV_DEV void lat_sl_prep(LatSlShared& sh, const gvk_lat& b, u32 gi, const fslk& k
   const u32 zq = fsl_mul(qy << 1, acc, k);              // Z_15 = 2y * prod(ratios)
   if (row == 0u && lo) sh.zq[L] = zq;
   if (threadIdx.x == 0) sh.okp = ok ? 1u : 0u;
+  LAT_STAMP(2);                                         // trace builds: tables done
 }
 
 // GV_LAT_SL_SPLIT: batches of at most this many signatures split the pub33
@@ -914,6 +916,7 @@ __global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
   __shared__ LatSlShared sh;
   const u32 gi = blockIdx.x;                            // grid = n: every block is live
   const u32 wave = threadIdx.x >> 6;
+  if (wave == 0u) LAT_STAMP(0);
   if (wave == 1u) {                                     // the scalar chain, whole wave (own SIMD)
     if (b.msg_len) {                                    // message path: SHA-256 of the sign bytes here
       u32 eh[8];
@@ -922,6 +925,7 @@ __global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
     } else {
       lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.dig32 + (size_t)gi * 32u, nullptr, b.C, gi);
     }
+    LAT_STAMP(3);                                       // trace builds: scalars done
     __syncthreads();
     __syncthreads();
     return;
@@ -931,6 +935,7 @@ __global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
   const bool lo = L < 9u;
   if (wave == 0u) lat_sl_prep(sh, b, gi, k);
   __syncthreads();                                      // digits (wave 1) + tables, zq (wave 0)
+  if (wave == 0u) LAT_STAMP(4);
   const bool ok = sh.okp != 0u;
   const u32 zq = lo ? sh.zq[L] : 0u;
   // ---- ladder: row r accumulates one of the four partial sums (of its wave's windows)
@@ -978,6 +983,7 @@ __global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
   }
   // ---- combine: Q rows back to the real curve, two rounds across rows,
   // then wave 2's sum into wave 0 through LDS
+  if (wave == 0u) LAT_STAMP(5);
   if (row < 2u) A.z = fsl_mul(A.z, zq, k);
 #pragma unroll 1
   for (int m = 16; m < 64; m <<= 1) {
@@ -1001,6 +1007,7 @@ __global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
     O.z = lo ? sh.pt[2][L] : 0u;
     gjsl_add_gej(A, inf, A, inf, O, sh.pinf != 0u, k);
   }
+  LAT_STAMP(6);
   // ---- final check (as k_ecmult): x(R) mod n == r, without inversion
   const u32 fl = sh.oks[0];
   bool okv = (fl & 1u) && ok && !inf;
@@ -1027,6 +1034,7 @@ __global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
     if (b.out8) b.out8[gi] = okv ? 1u : 0u;
     else if (okv) atomicOr((unsigned long long*)&b.bits[gi >> 6], 1ull << (gi & 63u));
   }
+  LAT_STAMP(7);
 }
 
 // ---------------------------------------------------------------------------
