@@ -1702,7 +1702,13 @@ int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint
     miss.resize(k);
   }
   const size_t m = miss.size();
-  std::vector<uint8_t> pub(m * 33), sig(m * 64), dig(m * 32), ok(m);
+  // one uninitialised buffer (no single-threaded zero fill of ~130 B per
+  // leaf before the parallel pack: its pages fault in on the pool)
+  std::unique_ptr<uint8_t[]> pack(new uint8_t[m * 129 + 1]);
+  uint8_t* const pub = pack.get();
+  uint8_t* const sig = pub + m * 33;
+  uint8_t* const dig = sig + m * 64;
+  std::vector<uint8_t> ok(m);
   parallel_for(app, m, [&](size_t k) {
     memcpy(&pub[k * 33], miss[k]->pub.data(), 33);
     memcpy(&sig[k * 64], miss[k]->sig.data(), 64);
@@ -1722,7 +1728,7 @@ int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint
   {
     std::lock_guard<std::mutex> g(app->gpu_mu);
     rlap("pack");
-    if (m && verify_secp(app, m, pub.data(), sig.data(), dig.data(), ok.data()) != GV_OK)
+    if (m && verify_secp(app, m, pub, sig, dig, ok.data()) != GV_OK)
       return GVH_EDEVICE;
     if (me && gv_verify_ed25519_msgs(app->gpu, me, epub.data(), esig.data(), eblob.empty() ? nullptr : eblob.data(),
                                      eoff.data(), elen.data(), eok.data()) != GV_OK)
