@@ -257,7 +257,7 @@ def checktx_latency(ver, pub, sig, dig, threads, sizes=(1, 16, 32, 64, 128, 256,
         msgs50, _ = _pct(ts[5:])
         ver.set_option("lat_max", 0)
         tp50, _ = _pct(run_gpu(max(20, reps // 4)))
-        ver.set_option("lat_max", gvm.LAT_MAX_DEFAULT)
+        ver.reset_schedule()
         cpu = {}
         for label, th in (("cpu_serial_p50_ms", 1), ("cpu_allcore_p50_ms", threads)):
             ts = []

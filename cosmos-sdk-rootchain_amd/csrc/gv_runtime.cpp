@@ -434,6 +434,12 @@ struct gv_ctx {
   size_t lat_max = 8192;        // batches up to this size take a fused small-batch kernel (gv_lat.hip), larger ones the pipeline
   size_t lat_sl_max = 2048;     // ... and up to this size the limb-sliced one (one signature per block); between the two the
                                 // four-lanes-per-signature kernel (0.50 ms flat to 8192): profiles/r02/lat_sliced/batch_curve*.json
+  // keyed batches (the key arena): the sliced keyed kernel takes 4 waves per
+  // signature and the 16-lanes-per-signature kernel beats the k4 pipeline to
+  // ~14k (profiles/r02/lat_sliced/keyed_curve.json).  Setting lat_max /
+  // lat_sl_max sets these too; lat_max_keyed / lat_sl_max_keyed only these.
+  size_t lat_max_keyed = 14336;
+  size_t lat_sl_max_keyed = 1536;
   size_t pipe_chunk = 131072;   // host path: first chunk of the two-set copy/compute pipeline (0 = max_batch)
   int pipe_growth = 4;          // host path: each later chunk at most this times the one before
   int stage_threads = 8;        // host path: staging memcpy threads per device
@@ -488,7 +494,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     CK(hipEventRecord(rs[0], st));
     for (int i = 0; i < 4; ++i) b.ev[i] = rs[i + 1];
   }
-  if (n <= ctx->lat_max) {
+  if (n <= (kslot ? ctx->lat_max_keyed : ctx->lat_max)) {
     // small batch: one fused kernel, several lanes per signature (gv_lat.hip)
     gvk_lat lb;
     memset(&lb, 0, sizeof lb);
@@ -501,7 +507,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
       lb.pub33 = nullptr;
       lb.kslot = kslot; lb.kqt = b.kqt; lb.kzq = b.kzq; lb.kok = b.kok; lb.kC = b.kC; lb.kcount = b.kcount;
     }
-    const bool sliced = ctx->lat_sliced && n <= ctx->lat_sl_max;
+    const bool sliced = ctx->lat_sliced && n <= (kslot ? ctx->lat_sl_max_keyed : ctx->lat_sl_max);
     if (out8 && !sliced) return GV_EINVAL;      // byte verdicts: the sliced kernels only
     lb.out8 = out8;
     if (kslot) {                                // keyed: 16 lanes per signature (group tables)
@@ -613,7 +619,9 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
     if ((rc = ensure_blob(s, hb_bytes))) return rc;
     par_copy(d->pool, s->h_blob, hb.blob + bmin, hb_bytes);
   }
-  if (ctx->lat_zero_copy && ctx->lat_sliced && cn <= ctx->lat_sl_max && cn <= ctx->lat_max) {
+  const size_t lmax = keyed ? ctx->lat_max_keyed : ctx->lat_max;
+  const size_t slmax = keyed ? ctx->lat_sl_max_keyed : ctx->lat_sl_max;
+  if (ctx->lat_zero_copy && ctx->lat_sliced && cn <= slmax && cn <= lmax) {
     // zero-copy small batch: the kernel reads the pinned staging buffers
     // (messages too: its scalar wave hashes them) and writes one verdict byte
     // per item to pinned memory (no H2D / memset / D2H)
@@ -662,7 +670,7 @@ int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const HostBatch& hb) {
   // equal chunks of at most max_batch.  Every chunk but the last is a multiple
   // of 256 (harvest copies bitmap words).
   std::vector<size_t> sizes;
-  if (n > ctx->lat_max && ctx->pipe_chunk) {
+  if (n > (hb.slots ? ctx->lat_max_keyed : ctx->lat_max) && ctx->pipe_chunk) {
     size_t c = std::min(ctx->pipe_chunk, ctx->max_batch), left = n;
     while (left) {
       const size_t take = std::min(left, c);
@@ -1101,12 +1109,14 @@ int gv_dev_verify_digests_keyed(gv_ctx* ctx, int dev_slot, size_t n, const void*
 
 int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   if (!ctx || !key) return GV_EINVAL;
-  if (!strcmp(key, "lat_max")) {
+  if (!strcmp(key, "lat_max") || !strcmp(key, "lat_max_keyed")) {
     if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
-    ctx->lat_max = (size_t)val;
-  } else if (!strcmp(key, "lat_sl_max")) {
+    if (!strcmp(key, "lat_max")) ctx->lat_max = (size_t)val;
+    ctx->lat_max_keyed = (size_t)val;
+  } else if (!strcmp(key, "lat_sl_max") || !strcmp(key, "lat_sl_max_keyed")) {
     if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
-    ctx->lat_sl_max = (size_t)val;
+    if (!strcmp(key, "lat_sl_max")) ctx->lat_sl_max = (size_t)val;
+    ctx->lat_sl_max_keyed = (size_t)val;
   } else if (!strcmp(key, "lat_zero_copy")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->lat_zero_copy = val != 0;

@@ -27,6 +27,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # crossover and the sliced / four-lanes-per-signature small-batch crossover
 LAT_MAX_DEFAULT = 8192
 LAT_SL_MAX_DEFAULT = 2048
+# keyed batches: their own defaults (setting "lat_max" / "lat_sl_max" sets the keyed ones too)
+LAT_MAX_KEYED_DEFAULT = 14336
+LAT_SL_MAX_KEYED_DEFAULT = 1536
 LIB_PATH = os.environ.get("GV_LIB") or os.path.join(HERE, "lib", "libgpuverify.so")
 
 GV_OK, GV_EINVAL, GV_ENODEV, GV_EHIP, GV_ENOMEM, GV_EFAULT = 0, -1, -2, -3, -4, -5
@@ -194,6 +197,13 @@ class Verifier:
     @property
     def num_devices(self) -> int:
         return self._L.gv_num_devices(self._ctx)
+
+    def reset_schedule(self):
+        """The small-batch schedule options back to their defaults."""
+        self.set_option("lat_max", LAT_MAX_DEFAULT)
+        self.set_option("lat_sl_max", LAT_SL_MAX_DEFAULT)
+        self.set_option("lat_max_keyed", LAT_MAX_KEYED_DEFAULT)
+        self.set_option("lat_sl_max_keyed", LAT_SL_MAX_KEYED_DEFAULT)
 
     def set_option(self, key: str, val: int):
         _check(self._L.gv_set_option(self._ctx, key.encode(), int(val)), f"gv_set_option({key})")

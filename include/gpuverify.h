@@ -174,6 +174,10 @@ int gv_dev_verify_ed25519_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* 
  * small-batch kernels k_verify_lat_sl / k_verify_lat16_sl, one signature per
  * block; larger ones up to lat_max the four-lanes-per-signature
  * k_verify_lat / k_verify_lat16; default 2048),
+ * "lat_max_keyed" / "lat_sl_max_keyed" (the same two bounds for keyed
+ * batches, defaults 14336 / 1536: the sliced keyed kernel takes four waves
+ * per signature, and the 16-lanes-per-signature keyed kernel beats the keyed
+ * pipeline to ~14k; setting "lat_max" / "lat_sl_max" sets these too),
  * "lat_sliced" (0/1: 0 never takes the sliced kernels; default 1),
  * "lat_zero_copy" (0/1: host-buffer digest batches on the sliced kernels
  * are read by the kernel straight from the pinned staging buffer and answered

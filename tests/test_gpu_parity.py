@@ -203,9 +203,8 @@ def path(request, ver):
     ver.set_option("lat_sliced", sliced)
     ver.set_option("lat_sl_max", 1 << 30)
     yield request.param
-    ver.set_option("lat_max", gvm.LAT_MAX_DEFAULT)
+    ver.reset_schedule()
     ver.set_option("lat_sliced", 1)
-    ver.set_option("lat_sl_max", gvm.LAT_SL_MAX_DEFAULT)
 
 
 def test_golden_digest_vectors(ver, path):
@@ -460,8 +459,7 @@ def test_sliced_latency_kernels_at_scale(ver):
         bad = np.nonzero(got != exp)[0]
         assert bad.size == 0, bad[:20]
     finally:
-        ver.set_option("lat_max", gvm.LAT_MAX_DEFAULT)
-        ver.set_option("lat_sl_max", gvm.LAT_SL_MAX_DEFAULT)
+        ver.reset_schedule()
         ver.keys_reset()
 
 

@@ -91,5 +91,5 @@ def test_kat_keys_sign_and_verify(ver, kat, lat_max):
         assert ver.verify_batch_msgs_keyed(slots, msig, msgs).all()
         assert not ver.verify_batch_msgs(pub, msig, [m + b" " for m in msgs]).any()
     finally:
-        ver.set_option("lat_max", gvm.LAT_MAX_DEFAULT)
+        ver.reset_schedule()
         ver.keys_reset()

@@ -30,9 +30,8 @@ def path(request, ver):
     ver.set_option("lat_sliced", sliced)
     ver.set_option("lat_sl_max", 1 << 30)
     yield request.param
-    ver.set_option("lat_max", gvm.LAT_MAX_DEFAULT)
+    ver.reset_schedule()
     ver.set_option("lat_sliced", 1)
-    ver.set_option("lat_sl_max", gvm.LAT_SL_MAX_DEFAULT)
 
 
 def keyed_inputs(ver, pub):

@@ -44,8 +44,7 @@ def main():
             ver.dev_download(got, bits)
             ok = int(np.unpackbits(got.view(np.uint8), bitorder="little")[:n].sum())
             row[name] = {"ms": round(ms, 4), "verifies_per_s": round(n / ms * 1e3, 1), "accepted": ok}
-        ver.set_option("lat_max", gvm.LAT_MAX_DEFAULT)
-        ver.set_option("lat_sl_max", gvm.LAT_SL_MAX_DEFAULT)
+        ver.reset_schedule()
         hp, hs, hd = (np.ascontiguousarray(a[:n]) for a in (pub, sig, dig))
         ver.verify_batch_digests_bits(hp, hs, hd)
         t = time.perf_counter()
