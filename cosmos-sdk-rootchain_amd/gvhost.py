@@ -52,6 +52,7 @@ def lib():
         L.gvh_app_new.argtypes = [vp]
         L.gvh_app_free.argtypes = [vp]
         L.gvh_set_params.argtypes = [vp, u64, u64, u64]
+        L.gvh_set_gas_model.argtypes = [vp, ctypes.c_int]
         L.gvh_set_context.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int, u64]
         L.gvh_set_account.argtypes = [vp, ctypes.c_char_p, u64, u64, ctypes.c_char_p, sz]
         L.gvh_get_account.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(u64), ctypes.POINTER(u64), vp,
@@ -62,6 +63,7 @@ def lib():
         L.gvh_cache_clear.argtypes = [vp]
         L.gvh_set_threads.argtypes = [vp, ctypes.c_int]
         L.gvh_set_keyed.argtypes = [vp, ctypes.c_int, ctypes.c_size_t]
+        L.gvh_get_keyed.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(sz), ctypes.POINTER(sz)]
         L.gvh_cache_size.argtypes = [vp]
         L.gvh_cache_size.restype = sz
         L.gvh_std_sign_bytes.argtypes = [ctypes.c_char_p, u64, u64, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p),
@@ -144,6 +146,10 @@ class HostApp:
 
     def set_params(self, tx_sig_limit=7, cost_secp=1000, cost_ed=590):
         self._L.gvh_set_params(self._app, tx_sig_limit, cost_secp, cost_ed)
+
+    def set_gas_model(self, kv_gas: bool):
+        """kv_gas: charge the ante chain's KV-store / params / tx-size gas (default) or signature gas only."""
+        self._L.gvh_set_gas_model(self._app, int(kv_gas))
 
     def set_context(self, chain_id: str, height: int = 1, recheck: bool = False, gas_limit: int = 0):
         self._L.gvh_set_context(self._app, chain_id.encode(), height, int(recheck), gas_limit)
@@ -234,6 +240,12 @@ class HostApp:
         """secp256k1 leaves through the GPU context's key arena (default; keys loaded by
         batches of >= load_min leaves) or as pub33 batches."""
         self._L.gvh_set_keyed(self._app, 1 if keyed else 0, load_min)
+
+    def keyed_policy(self):
+        """(keyed, load_min, key_cap) in force"""
+        k, lm, cap = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_size_t()
+        self._L.gvh_get_keyed(self._app, ctypes.byref(k), ctypes.byref(lm), ctypes.byref(cap))
+        return bool(k.value), lm.value, cap.value
 
     def cache_size(self) -> int:
         return self._L.gvh_cache_size(self._app)

@@ -49,7 +49,7 @@ struct Span {
 // ------------------------------------------------------------------ errors
 // sdkerrors codes (types/errors/errors.go)
 constexpr uint32_t kErrTxDecode = 2, kErrUnauthorized = 4, kErrInvalidPubKey = 8, kErrUnknownAddress = 9,
-                   kErrOutOfGas = 11, kErrTooManySignatures = 14, kErrPanic = 111222;
+                   kErrOutOfGas = 11, kErrMemoTooLarge = 12, kErrTooManySignatures = 14, kErrPanic = 111222;
 
 struct SdkError {
   uint32_t code = 0;
@@ -64,6 +64,7 @@ const char* err_desc(uint32_t code) {
     case kErrInvalidPubKey: return "invalid pubkey";
     case kErrUnknownAddress: return "unknown address";
     case kErrOutOfGas: return "out of gas";
+    case kErrMemoTooLarge: return "memo too large";
     case kErrTooManySignatures: return "maximum number of signatures exceeded";
     case kErrPanic: return "panic";
     default: return "internal";
@@ -581,6 +582,7 @@ struct Tx {
   Span raw;
   bool nil_msg = false;
   uint64_t gas = 0;
+  size_t memo_len = 0;              // len(GetMemo()) in bytes (ValidateMemoDecorator)
   struct Sig {
     Span pub, sig;
   };
@@ -593,6 +595,7 @@ struct Tx {
     raw = Span{};
     nil_msg = false;
     gas = 0;
+    memo_len = 0;
     sigs.clear();
     signers.clear();
     sb_tail.clear();
@@ -652,6 +655,7 @@ std::shared_ptr<Tx> decode_tx(const uint8_t* p, size_t n, bool copy, std::shared
     }
   });
   if (tx->nil_msg) tx->signers.clear();
+  tx->memo_len = memo.n;
   // StdFee.Bytes() (stdtx.go:47-58): an empty amount is normalised to [] (not null)
   std::string& t = tx->sb_tail;
   t.reserve(64 + fee.size() + msgs.size() + memo.n);
@@ -1089,6 +1093,44 @@ struct GasMeter {
   bool fits(uint64_t amount) const { return infinite || used + amount <= limit; }
 };
 
+// KV-store gas of the ante chain.  ctx.KVStore wraps every store in gaskv
+// (types/context.go:211-212), whose Get charges ReadCostFlat + ReadCostPerByte
+// x len(value) and Set WriteCostFlat + WriteCostPerByte x len(value)
+// (store/gaskv/store.go:36-52; KVGasConfig store/types/gas.go:165-173).
+constexpr uint64_t kReadCostFlat = 1000, kReadCostPerByte = 3, kWriteCostFlat = 2000, kWriteCostPerByte = 30;
+constexpr uint64_t kTxSizeCostPerByte = 10, kMaxMemoCharacters = 256;   // x/auth/types/params.go:16,18
+void kv_read(GasMeter& gm, size_t value_len) {
+  gm.consume(kReadCostFlat, "ReadFlat");
+  gm.consume(kReadCostPerByte * value_len, "ReadPerByte");
+}
+void kv_write(GasMeter& gm, size_t value_len) {
+  gm.consume(kWriteCostFlat, "WriteFlat");
+  gm.consume(kWriteCostPerByte * value_len, "WritePerByte");
+}
+size_t uvarint_len(uint64_t v) {
+  size_t n = 1;
+  while (v >= 0x80) { v >>= 7; ++n; }
+  return n;
+}
+// The value AccountKeeper.SetAccount stores (x/auth/keeper/account.go:51-61):
+// std.Codec.MarshalAccount (std/codec.go:41-48) = proto std.Account{base_account
+// = 1: BaseAccount{address = 1, pub_key = 2, account_number = 3, sequence = 4}}
+// (std/codec.proto:21-32, x/auth/types/types.proto:11-19); proto3 leaves out
+// empty and zero fields.  pub_key holds pubKey.Bytes() (amino, account.go:75-83).
+size_t account_value_len(size_t pub_len, uint64_t num, uint64_t seq) {
+  size_t inner = 2 + 20;
+  if (pub_len) inner += 1 + uvarint_len(pub_len) + pub_len;
+  if (num) inner += 1 + uvarint_len(num);
+  if (seq) inner += 1 + uvarint_len(seq);
+  return 1 + uvarint_len(inner) + inner;
+}
+// AccountKeeper.GetParams (x/auth/keeper/keeper.go GetParams -> params
+// Subspace.GetParamSet, x/params/types/subspace.go:100-109,218-222): one
+// gas-metered Get per ParamSetPair in x/auth/types/params.go:55-62 order; the
+// values are amino JSON (codec/hybrid_codec.go:51-53), uint64 as a quoted
+// decimal string.
+size_t amino_json_u64_len(uint64_t v) { return std::to_string(v).size() + 2; }
+
 // 64-bit hash of a byte string for in-process tables (entries are always
 // confirmed by a full comparison, so collisions cost time, never results).
 uint64_t fast_hash(const uint8_t* p, size_t n) {
@@ -1298,6 +1340,10 @@ struct Window {
   std::condition_variable cv;
   size_t max_txs = 64;
   int64_t max_wait_us = 200;
+  // Adaptive: a call waits for company only when calls are concurrent
+  // (another one in flight, or the last window held more than one).
+  std::atomic<int> inflight{0};
+  std::atomic<size_t> last_size{0};
   struct Batch {
     std::vector<std::pair<const uint8_t*, size_t>> items;
     std::chrono::steady_clock::time_point deadline;
@@ -1316,6 +1362,7 @@ const Bytes kSimPub = {0xEB, 0x5A, 0xE9, 0x87, 0x21, 0x03, 0x5A, 0xD6, 0x81, 0x0
 struct gvh_app {
   gv_ctx* gpu = nullptr;
   uint64_t sig_limit = 7, cost_secp = 1000, cost_ed = 590;
+  bool kv_gas = true;                          // charge the ante chain's KV-store and tx-size gas (gvh_set_gas_model)
   std::string chain_id = "", chain_json = "\"\"";
   int64_t height = 1;
   bool recheck = false;
@@ -1339,8 +1386,8 @@ struct gvh_app {
   std::unordered_map<std::array<uint8_t, 33>, uint32_t, Key33Hash> key_slots;
   uint64_t key_gen = 0;                        // gv_keys_generation the map belongs to
   bool keyed = true;
-  size_t key_cap = size_t(1) << 22;            // arena reset past this many keys (5.4 KB of HBM each)
-  size_t key_load_min = 4096;                  // smaller batches never load keys (k_keys_build's ~ms latency):
+  size_t key_cap = GV_KEY_CAP;                 // arena reset past this many keys (5.4 KB of HBM each)
+  size_t key_load_min = GV_KEY_LOAD_MIN;       // smaller batches never load keys (k_keys_build's ~ms latency):
                                                // keyed only when all their keys are resident
   int threads = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
   std::unique_ptr<Pool> pool{new Pool(threads - 1)};
@@ -1811,6 +1858,46 @@ int run_ante(gvh_app* app, const Tx& tx, Memo* memo, bool simulate, gvh_result* 
       return std::shared_ptr<const PubInfo>(p);
     }();
 
+    // KV-store gas (app->kv_gas): accounts and params are read through gaskv.
+    const bool kv = app->kv_gas;
+    auto acc_len = [](const Account& a) { return account_value_len(a.pub.size(), a.number, a.sequence); };
+    auto acc_read = [&](const Account* a) {          // AccountKeeper.GetAccount (keeper/account.go:30-38)
+      if (kv) kv_read(gm, a ? acc_len(*a) : 0);
+    };
+    auto acc_write = [&](const Account& a) {         // AccountKeeper.SetAccount (keeper/account.go:51-61)
+      if (kv) kv_write(gm, acc_len(a));
+    };
+    auto params_gas = [&]() {                        // AccountKeeper.GetParams: five metered Gets
+      if (!kv) return;
+      for (uint64_t v : {kMaxMemoCharacters, app->sig_limit, kTxSizeCostPerByte, app->cost_ed, app->cost_secp})
+        kv_read(gm, amino_json_u64_len(v));
+    };
+
+    // ---- ValidateMemoDecorator (x/auth/ante/basic.go:61-77)
+    params_gas();
+    if (tx.memo_len > kMaxMemoCharacters)
+      return fail(wrap(kErrMemoTooLarge, "maximum number of characters is " + std::to_string(kMaxMemoCharacters) +
+                                             " but received " + std::to_string(tx.memo_len) + " characters"));
+    // ---- ConsumeTxSizeGasDecorator (basic.go:98-148)
+    if (kv) {
+      params_gas();
+      gm.consume(kTxSizeCostPerByte * tx.raw.n, "txSize");
+      if (simulate) {                                // a signature left empty: the size of a full one
+        for (size_t i = 0; i < signers.size(); ++i) {
+          if (i >= ns) throw Panic("runtime error: index out of range");
+          if (tx.sigs[i].sig.n) continue;
+          Account* acc = acc_of(i);
+          acc_read(acc);
+          const std::shared_ptr<const PubInfo> info = acc ? account_info(app, *acc) : nullptr;
+          const PubInfo& pk = info ? *info : *kSim;
+          // amino StdSignature{PubKey: pk.Bytes(), Signature: simSecp256k1Sig[:]} + 6
+          uint64_t cost = 1 + uvarint_len(pk.canon.size()) + pk.canon.size() + 1 + 1 + 64 + 6;
+          if (pk.pk.kind == PubKey::Multisig) cost *= app->sig_limit;
+          gm.consume(kTxSizeCostPerByte * cost, "txSize");
+        }
+      }
+    }
+
     // ---- SetPubKeyDecorator (sigverify.go:60-99)
     for (size_t i = 0; i < ns; ++i) {
       const PubInfo* pk = (*tx_pk)[i].get();
@@ -1823,6 +1910,7 @@ int run_ante(gvh_app* app, const Tx& tx, Memo* memo, bool simulate, gvh_result* 
                                                   " with signer index: " + std::to_string(i)));
       }
       Account* acc = acc_of(i);
+      acc_read(acc);                                  // GetSignerAcc (:83)
       if (!acc) return fail(wrap(kErrUnknownAddress, "account " + acc_string(signers[i]) + " does not exist"));
       if (acc->pub.empty()) {
         const auto& info = pk ? (*tx_pk)[i] : kSim;
@@ -1830,9 +1918,11 @@ int run_ante(gvh_app* app, const Tx& tx, Memo* memo, bool simulate, gvh_result* 
         acc->info = info->canon == info->raw ? info : nullptr;
         if (n_set < 8) set_pub[n_set++] = acc;
         else set_pub_more.push_back(acc);
+        acc_write(*acc);                              // SetAccount (:95)
       }
     }
     // ---- ValidateSigCountDecorator (sigverify.go:275-294)
+    params_gas();
     {
       uint64_t count = 0;
       for (size_t i = 0; i < ns; ++i) {
@@ -1842,10 +1932,23 @@ int run_ante(gvh_app* app, const Tx& tx, Memo* memo, bool simulate, gvh_result* 
                            "signatures: " + std::to_string(count) + ", limit: " + std::to_string(app->sig_limit)));
       }
     }
+    // ---- DeductFeeDecorator (x/auth/ante/fee.go:84-108): the fee payer's
+    // account read.  (A nonzero fee's bank transfer is not modelled: the
+    // mirror keeps no balances.)
+    if (kv) {
+      Account* payer = signers.empty() ? nullptr : acc_of(0);     // StdTx.FeePayer() = GetSigners()[0]
+      acc_read(payer);
+      if (!payer)
+        return fail(wrap(kErrUnknownAddress, "fee payer address: " +
+                                                 (signers.empty() ? std::string() : acc_string(signers[0])) +
+                                                 " does not exist"));
+    }
     // ---- SigGasConsumeDecorator (sigverify.go:117-153)
+    params_gas();
     for (size_t i = 0; i < ns; ++i) {
       if (i >= signers.size()) throw Panic("runtime error: index out of range");
       Account* acc = acc_of(i);
+      acc_read(acc);                                  // GetSignerAcc (:131)
       if (!acc) return fail(wrap(kErrUnknownAddress, "account " + acc_string(signers[i]) + " does not exist"));
       std::shared_ptr<const PubInfo> pk = account_info(app, *acc);
       if (!pk) {
@@ -1863,6 +1966,11 @@ int run_ante(gvh_app* app, const Tx& tx, Memo* memo, bool simulate, gvh_result* 
       if (!consume_sig_gas(gm, tx.sigs[i].sig, pk->pk, app, &e)) return fail(e);
     }
     // ---- BatchSigVerificationDecorator (replaces sigverify.go:170-216)
+    // Gather every signer's leaves up to the first signer the reference loop
+    // would stop at (no gas: the look-ahead reads the state without a
+    // meter), answer all leaves at once, then walk the signers in the
+    // reference's order, charging each signer's account read only when the
+    // loop gets there: the same gas as verifying one signer at a time.
     if (!app->recheck) {
       if (ns != signers.size())
         return fail(wrap(kErrUnauthorized, "invalid number of signer;  expected: " + std::to_string(signers.size()) +
@@ -1871,22 +1979,10 @@ int run_ante(gvh_app* app, const Tx& tx, Memo* memo, bool simulate, gvh_result* 
       SignerPlan* plans_small[8];
       std::vector<SignerPlan*> plans_big;
       size_t np = 0;
-      SdkError first_err;
-      bool have_err = false;
-      for (size_t i = 0; i < ns; ++i) {
+      for (size_t i = 0; i < ns && !simulate; ++i) {
         Account* acc = acc_of(i);
-        if (!acc) {
-          first_err = wrap(kErrUnknownAddress, "account " + acc_string(signers[i]) + " does not exist");
-          have_err = true;
-          break;
-        }
+        if (!acc || acc->pub.empty()) break;          // the walk reports it at signer i
         const uint64_t accnum = app->height == 0 ? 0 : acc->number;
-        if (!simulate && acc->pub.empty()) {
-          first_err = wrap(kErrInvalidPubKey, "pubkey on account is not set");
-          have_err = true;
-          break;
-        }
-        if (simulate) continue;
         SignerPlan* p = nullptr;
         if (memo && i < memo->plans.size()) {
           SignerPlan& mp = memo->plans[i];
@@ -1920,17 +2016,24 @@ int run_ante(gvh_app* app, const Tx& tx, Memo* memo, bool simulate, gvh_result* 
           if (rc != GVH_OK) { rollback(); return rc; }
         }
       }
-      for (size_t k = 0; k < np; ++k)   // report the FIRST failing signer, as the reference loop does
-        if (!eval(plan_at(k)->node, plan_at(k)->leaves))
+      for (size_t i = 0; i < ns; ++i) {               // the reference loop (sigverify.go:194-213)
+        Account* acc = acc_of(i);
+        acc_read(acc);                                // GetSignerAcc (:195)
+        if (!acc) return fail(wrap(kErrUnknownAddress, "account " + acc_string(signers[i]) + " does not exist"));
+        if (!simulate && acc->pub.empty()) return fail(wrap(kErrInvalidPubKey, "pubkey on account is not set"));
+        if (simulate) continue;
+        if (!eval(plan_at(i)->node, plan_at(i)->leaves))
           return fail(wrap(kErrUnauthorized, "signature verification failed; verify correct account sequence and chain-id"));
-      if (have_err) return fail(first_err);
+      }
     }
     // ---- IncrementSequenceDecorator (sigverify.go:237-259)
     if (!app->recheck || simulate) {
       for (size_t i = 0; i < signers.size(); ++i) {
         Account* acc = acc_of(i);
+        acc_read(acc);
         if (!acc) throw Panic("account not found");
         acc->sequence += 1;
+        acc_write(*acc);
       }
     }
   } catch (const Panic& p) {
@@ -2169,6 +2272,10 @@ void gvh_set_params(gvh_app* app, uint64_t lim, uint64_t cs, uint64_t ce) {
   app->cost_secp = cs;
   app->cost_ed = ce;
 }
+void gvh_set_gas_model(gvh_app* app, int kv_gas) {
+  std::lock_guard<std::mutex> lk(app->mu);
+  app->kv_gas = kv_gas != 0;
+}
 void gvh_set_context(gvh_app* app, const char* chain_id, int64_t height, int recheck, uint64_t gas_limit) {
   std::lock_guard<std::mutex> lk(app->mu);
   app->chain_id = chain_id ? chain_id : "";
@@ -2350,8 +2457,25 @@ int gvh_checktx(gvh_app* app, const uint8_t* tx, size_t tx_len, gvh_result* out)
   if (!app || (!tx && tx_len) || !out) return GVH_EINVAL;
   Window& w = app->window;
   int rc = GVH_OK;
+  struct Inflight {
+    Window& w;
+    ~Inflight() { w.inflight.fetch_sub(1); }
+  };
   {
     std::unique_lock<std::mutex> lk(w.m);
+    const bool lone = !w.open && w.inflight.load() == 0 && w.last_size.load() <= 1;
+    w.inflight.fetch_add(1);
+    Inflight guard{w};
+    if (lone || w.max_wait_us == 0) {
+      // Nothing else can join (tendermint v0.33 delivers CheckTx one call at
+      // a time, baseapp/abci.go:165-196): no window, the ante chain verifies
+      // this tx's leaves in its own GPU batch right away.
+      w.last_size.store(1);
+      app->st_windows += 1;
+      app->st_window_txs += 1;
+      lk.unlock();
+      return ante_bytes(app, tx, tx_len, false, out);
+    }
     if (!w.open) {
       w.open = std::make_shared<Window::Batch>();
       w.open->deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(w.max_wait_us);
@@ -2361,6 +2485,7 @@ int gvh_checktx(gvh_app* app, const uint8_t* tx, size_t tx_len, gvh_result* out)
     auto flush = [&]() {                              // this caller verifies the window's batch
       w.open = nullptr;
       b->flushing = true;
+      w.last_size.store(b->items.size());
       lk.unlock();
       std::vector<const uint8_t*> ptrs;
       std::vector<size_t> ls;
@@ -2380,9 +2505,10 @@ int gvh_checktx(gvh_app* app, const uint8_t* tx, size_t tx_len, gvh_result* out)
         if (w.cv.wait_until(lk, b->deadline) == std::cv_status::timeout && !b->done && !b->flushing && w.open == b)
           rc = flush();
       }
+    lk.unlock();
+    if (rc == GVH_EDEVICE) return rc;                // the GPU failed: the caller falls back
+    return ante_bytes(app, tx, tx_len, false, out);
   }
-  if (rc == GVH_EDEVICE) return rc;                  // the GPU failed: the caller falls back
-  return ante_bytes(app, tx, tx_len, false, out);
 }
 
 int gvh_consume_sig_gas(gvh_app* app, const uint8_t* sig, size_t sig_len, const uint8_t* pub_amino, size_t pub_len,
@@ -2423,6 +2549,12 @@ void gvh_set_keyed(gvh_app* app, int keyed, size_t load_min) {
   app->key_load_min = load_min;
 }
 
+void gvh_get_keyed(gvh_app* app, int* keyed, size_t* load_min, size_t* key_cap) {
+  std::lock_guard<std::mutex> g(app->gpu_mu);
+  if (keyed) *keyed = app->keyed ? 1 : 0;
+  if (load_min) *load_min = app->key_load_min;
+  if (key_cap) *key_cap = app->key_cap;
+}
 void gvh_set_threads(gvh_app* app, int threads) {
   if (!app) return;
   std::lock_guard<std::mutex> g(app->pool_mu);

@@ -9,6 +9,8 @@
  *
  *   DefaultTxDecoder            x/auth/types/stdtx.go:321-338 (amino binary StdTx; bank MsgSend /
  *                               MsgMultiSend are the registered msgs, x/bank/types/codec.go:26-27)
+ *   ValidateMemoDecorator       x/auth/ante/basic.go:61-77 (memo length + params gas)
+ *   ConsumeTxSizeGasDecorator   x/auth/ante/basic.go:98-148
  *   SetPubKeyDecorator          x/auth/ante/sigverify.go:50-99
  *   ValidateSigCountDecorator   x/auth/ante/sigverify.go:265-294 (+ CountSubKeys stdtx.go:125-137)
  *   SigGasConsumeDecorator      x/auth/ante/sigverify.go:101-153, DefaultSigVerificationGasConsumer :299-322,
@@ -17,6 +19,7 @@
  *                               a tx (multisig fanned out, tendermint multisig.VerifyBytes semantics) are
  *                               answered from the verdict cache or verified in ONE libgpuverify batch;
  *                               failures are reported in signer order
+ *   DeductFeeDecorator          x/auth/ante/fee.go:84-108 (the fee payer's account read)
  *   IncrementSequenceDecorator  x/auth/ante/sigverify.go:218-259
  *   SetGasMeter                 x/auth/ante/setup.go:67-76 (limit = the tx's fee gas; infinite at height 0)
  *   PreVerifyTxs                baseapp batching hook: one GPU batch for a block of txs,
@@ -82,6 +85,15 @@ void gvh_app_free(gvh_app* app);
 
 /* x/auth params (params.go:16-20 defaults: 7, 1000, 590). */
 void gvh_set_params(gvh_app* app, uint64_t tx_sig_limit, uint64_t sig_cost_secp256k1, uint64_t sig_cost_ed25519);
+/* Gas model.  kv_gas = 1 (default): the chain charges what the reference's
+ * decorators charge besides signature gas -- every gas-metered account read
+ * and write (gaskv, store/gaskv/store.go:36-52: 1000 + 3/byte read, 2000 +
+ * 30/byte write of the proto account value), the five params reads of each
+ * AccountKeeper.GetParams, and ConsumeTxSizeGas (10 per tx byte); reads happen
+ * where the reference makes them, so a tx that fails at signer i is charged
+ * the reads of signers 0..i only.  A nonzero fee's bank transfer is not
+ * modelled (no balances).  kv_gas = 0: signature gas only. */
+void gvh_set_gas_model(gvh_app* app, int kv_gas);
 /* sdk.Context pieces the decorators read: chain id, block height (0 = genesis:
  * account number 0 in sign bytes, infinite gas), ReCheckTx flag.  gas_limit
  * 0 = SetGasMeter semantics (the tx's fee gas); nonzero overrides it. */
@@ -121,7 +133,12 @@ int gvh_deliver_gentxs(gvh_app* app, size_t ntx, const uint8_t* const* txs, cons
 /* CheckTx through the accumulation window: thread-safe and blocking; calls
  * arriving while a window is open share ONE PreVerifyTxs batch, flushed when
  * it holds max_txs txs or max_wait_us after its first tx; then each call runs
- * its own ante chain on the cached verdicts.  Defaults: 64 txs, 200 us. */
+ * its own ante chain on the cached verdicts.  Defaults: 64 txs, 200 us.
+ * Adaptive: a call opens a window only when calls are concurrent (another
+ * call in flight, or the previous window held more than one); a lone call --
+ * every call under tendermint's serial CheckTx delivery -- runs its ante
+ * chain at once (its leaves in their own GPU batch) and waits for nothing.
+ * max_wait_us = 0: never wait. */
 int gvh_checktx(gvh_app* app, const uint8_t* tx, size_t tx_len, gvh_result* out);
 void gvh_set_window(gvh_app* app, size_t max_txs, int64_t max_wait_us);
 
@@ -145,6 +162,8 @@ void gvh_set_threads(gvh_app* app, int threads);
  * verdicts either way.  While keyed, the app owns the context's key arena
  * (a gv_keys_reset elsewhere is detected by gv_keys_generation). */
 void gvh_set_keyed(gvh_app* app, int keyed, size_t load_min);
+/* The keyed-path policy in force (defaults: 1, GV_KEY_LOAD_MIN, GV_KEY_CAP of gpuverify.h). */
+void gvh_get_keyed(gvh_app* app, int* keyed, size_t* load_min, size_t* key_cap);
 void gvh_get_stats(gvh_app* app, gvh_stats* out);
 
 /* StdSignBytes (x/auth/types/stdtx.go:292-312): canonical JSON.  Returns the

@@ -72,20 +72,42 @@ func (CPU) VerifyBatch(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]byte) []
 	return ok
 }
 
+// Routing defaults, shared with the C++ mirror through gpuverify.h so the
+// two cannot drift apart (tests/test_go_policy.py checks both use them).
+var (
+	DefaultCPUBelow   = int(C.GV_CPU_CROSSOVER) // batches below: the reference VerifyBytes on the CPU
+	DefaultKeyLoadMin = int(C.GV_KEY_LOAD_MIN)  // batches from: keys not yet resident are loaded
+	DefaultKeyCap     = int(C.GV_KEY_CAP)       // key-arena size at which it is reset
+)
+
 // GPU is a libgpuverify context on one or more HIP devices.  Safe for
 // concurrent use: the library serialises calls per device, and the key-cache
 // maps below are guarded by mu.
+//
+// VerifyBatch (what BatchSigVerificationDecorator and NewPreVerifier call)
+// routes every batch by the policy below, the policy of the tested C++ mirror
+// (host/gvhost.cpp verify_secp): fewer than CPUBelow leaves -> the reference
+// VerifyBytes on the CPU; Keyed and every key resident -> the key-arena path;
+// Keyed and at least KeyLoadMin leaves -> the new keys are loaded once, then
+// the key-arena path; otherwise the pub33 path.  Same verdicts on every route.
 type GPU struct {
 	ctx       *C.gv_ctx
 	closeOnce sync.Once
 
-	// CPUBelow routes batches smaller than this to the CPU (VerifyBatchRouted):
-	// below the measured crossover a VerifyBytes loop answers first (one core:
-	// ~0.21 ms per signature; the sliced small-batch kernels: ~0.26 ms for up
-	// to 1,024 signatures, DESIGN.md §6.3).
+	// CPUBelow: below the measured crossover a VerifyBytes loop answers first
+	// (one core: ~0.20 ms per signature; the sliced small-batch kernels:
+	// ~0.21 ms for up to 256 signatures, DESIGN.md §6.3).
 	CPUBelow int
+	// Keyed: verify through the context's key arena (the account pubkey cache,
+	// SURVEY.md §8f-2: 197M/s vs 103M/s at 1M, 0.10 vs 0.21 ms at 64).
+	Keyed bool
+	// KeyLoadMin: the smallest batch that loads keys (k_keys_build costs about
+	// a millisecond; a CheckTx batch never waits on it).
+	KeyLoadMin int
+	// KeyCap: the arena is reset when a load would take it past this many keys.
+	KeyCap int
 
-	mu      sync.Mutex
+	mu      sync.Mutex                           // the slot map AND every keyed call (no reset in between)
 	slots   map[secp256k1.PubKeySecp256k1]uint32 // key -> key-arena slot (gv_keys_load)
 	slotGen uint64                               // gv_keys_generation the slot map belongs to
 }
@@ -113,7 +135,8 @@ func Open(devices []int) (*GPU, error) {
 	if rc := C.gv_open(ids, C.int(len(devices)), &ctx); rc != 0 {
 		return nil, errors.New("gpuverify: gv_open: " + C.GoString(C.gv_strerror(rc)))
 	}
-	return &GPU{ctx: ctx, CPUBelow: 4, slots: map[secp256k1.PubKeySecp256k1]uint32{}}, nil
+	return &GPU{ctx: ctx, CPUBelow: DefaultCPUBelow, Keyed: true, KeyLoadMin: DefaultKeyLoadMin, KeyCap: DefaultKeyCap,
+		slots: map[secp256k1.PubKeySecp256k1]uint32{}}, nil
 }
 
 // Close releases the context (idempotent).
@@ -144,10 +167,22 @@ func newCBuf(n int) cbuf {
 }
 func (c cbuf) free() { C.free(c.p) }
 
-// VerifyBatch implements Verifier.  Leaves whose signature is not 64 bytes
-// are false without reaching the GPU (VerifyBytes' first check).  On any
-// nonzero return the whole call is re-verified on the CPU.
+// VerifyBatch implements Verifier with the routing policy of the GPU type.
 func (g *GPU) VerifyBatch(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]byte) []bool {
+	if len(pubs) < g.CPUBelow {
+		return CPU{}.VerifyBatch(pubs, msgs, sigs)
+	}
+	if g.Keyed {
+		return g.VerifyBatchKeyed(pubs, msgs, sigs)
+	}
+	return g.VerifyBatchPub33(pubs, msgs, sigs)
+}
+
+// VerifyBatchPub33: every leaf with its compressed key (gv_verify_msgs).
+// Leaves whose signature is not 64 bytes are false without reaching the GPU
+// (VerifyBytes' first check).  On any nonzero return the whole call is
+// re-verified on the CPU.
+func (g *GPU) VerifyBatchPub33(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]byte) []bool {
 	n := len(pubs)
 	ok := make([]bool, n)
 	idx := make([]int, 0, n)
@@ -163,8 +198,8 @@ func (g *GPU) VerifyBatch(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]byte)
 	}
 	if total+97*len(idx) > maxBatchBytes { // split oversize batches
 		h := len(pubs) / 2
-		copy(ok, g.VerifyBatch(pubs[:h], msgs[:h], sigs[:h]))
-		copy(ok[h:], g.VerifyBatch(pubs[h:], msgs[h:], sigs[h:]))
+		copy(ok, g.VerifyBatchPub33(pubs[:h], msgs[:h], sigs[:h]))
+		copy(ok[h:], g.VerifyBatchPub33(pubs[h:], msgs[h:], sigs[h:]))
 		return ok
 	}
 	m := len(idx)
@@ -237,24 +272,15 @@ func (g *GPU) VerifyBatchEd25519(pubs []ed25519.PubKeyEd25519, msgs, sigs [][]by
 	return ok
 }
 
-// VerifyBatchRouted sends batches below CPUBelow to the CPU (where a
-// VerifyBytes loop answers before a GPU round trip) and the rest to the GPU.
-func (g *GPU) VerifyBatchRouted(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]byte) []bool {
-	if len(pubs) < g.CPUBelow {
-		return CPU{}.VerifyBatch(pubs, msgs, sigs)
-	}
-	return g.VerifyBatch(pubs, msgs, sigs)
-}
 
 // ---- account key cache (gv_keys_load, SURVEY.md §8f-2)
 
-// slotsFor returns each key's arena slot, loading the keys not yet cached
-// with ONE gv_keys_load call.  loaded[i] is false when key i could not be
-// cached (the load failed): the caller verifies that leaf on the CPU --
-// never a sentinel slot, whose keyed verify would read as a rejection.
-func (g *GPU) slotsFor(pubs []secp256k1.PubKeySecp256k1) (slots []uint32, loaded []bool) {
-	g.mu.Lock()
-	defer g.mu.Unlock()
+// slotsLocked returns each key's arena slot (g.mu held).  Keys not resident
+// are loaded with ONE gv_keys_load when load is true; loaded[i] is false for
+// a key that is not resident afterwards (not loaded, or the load failed):
+// the caller verifies that leaf by pub33 -- never a sentinel slot, whose
+// keyed verify would read as a rejection.
+func (g *GPU) slotsLocked(pubs []secp256k1.PubKeySecp256k1, load bool) (slots []uint32, loaded []bool, all bool) {
 	if gen := uint64(C.gv_keys_generation(g.ctx)); gen != g.slotGen {
 		// the arena was reset elsewhere: every cached slot may name another key now
 		g.slots = map[secp256k1.PubKeySecp256k1]uint32{}
@@ -272,26 +298,39 @@ func (g *GPU) slotsFor(pubs []secp256k1.PubKeySecp256k1) (slots []uint32, loaded
 			fresh = append(fresh, p)
 		}
 	}
-	if len(fresh) > 0 {
-		buf := newCBuf(33 * len(fresh))
-		out := newCBuf(4 * len(fresh))
-		defer func() { buf.free(); out.free() }()
+	if len(fresh) == 0 {
+		return slots, loaded, true
+	}
+	if !load {
+		return slots, loaded, false
+	}
+	if int(C.gv_keys_count(g.ctx))+len(fresh) > g.KeyCap { // start the arena over (the C++ mirror's rule)
+		C.gv_keys_reset(g.ctx)
+		g.slots = map[secp256k1.PubKeySecp256k1]uint32{}
+		g.slotGen = uint64(C.gv_keys_generation(g.ctx))
+		return g.slotsLocked(pubs, len(pubs) <= g.KeyCap)
+	}
+	buf := newCBuf(33 * len(fresh))
+	out := newCBuf(4 * len(fresh))
+	defer func() { buf.free(); out.free() }()
+	for k, p := range fresh {
+		copy(buf.b[33*k:], p[:])
+	}
+	if C.gv_keys_load(g.ctx, C.size_t(len(fresh)), (*C.uint8_t)(buf.p), (*C.uint32_t)(out.p)) == 0 {
+		s := (*[maxBatchBytes / 4]uint32)(out.p)[:len(fresh):len(fresh)]
 		for k, p := range fresh {
-			copy(buf.b[33*k:], p[:])
-		}
-		if C.gv_keys_load(g.ctx, C.size_t(len(fresh)), (*C.uint8_t)(buf.p), (*C.uint32_t)(out.p)) == 0 {
-			s := (*[maxBatchBytes / 4]uint32)(out.p)[:len(fresh):len(fresh)]
-			for k, p := range fresh {
-				g.slots[p] = s[k]
-			}
+			g.slots[p] = s[k]
 		}
 	}
+	all = true
 	for i, p := range pubs {
 		if s, ok := g.slots[p]; ok {
 			slots[i], loaded[i] = s, true
+		} else {
+			all = false
 		}
 	}
-	return slots, loaded
+	return slots, loaded, all
 }
 
 // ResetKeys empties the key arena and the slot map together (a slot number
@@ -304,52 +343,87 @@ func (g *GPU) ResetKeys() {
 	g.slotGen = uint64(C.gv_keys_generation(g.ctx))
 }
 
-// VerifyBatchKeyed is VerifyBatch with the keys kept parsed in HBM: every
-// key is parsed (decompressed, tabulated) once and verified by slot.  Same
-// verdicts; leaves whose key could not be cached go to the CPU.
+// VerifyBatchKeyed is VerifyBatchPub33 with the keys kept parsed in HBM:
+// every key is parsed (decompressed, tabulated) once and verified by slot.
+// Same verdicts.  Keys not resident are loaded only by batches of at least
+// KeyLoadMin leaves; the leaves of keys that are not resident go by pub33.
+// g.mu is held from the slot lookup through the keyed verify, so no
+// ResetKeys or reload can move a slot in between.
 func (g *GPU) VerifyBatchKeyed(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]byte) []bool {
 	n := len(pubs)
 	ok := make([]bool, n)
-	slots, loaded := g.slotsFor(pubs)
 	idx := make([]int, 0, n)
 	total := 0
 	for i := range pubs {
-		if len(sigs[i]) != 64 {
-			continue
+		if len(sigs[i]) == 64 { // VerifyBytes' first check
+			idx = append(idx, i)
+			total += len(msgs[i])
 		}
-		if !loaded[i] {
-			ok[i] = pubs[i].VerifyBytes(msgs[i], sigs[i])
-			continue
-		}
-		idx = append(idx, i)
-		total += len(msgs[i])
 	}
 	if len(idx) == 0 {
 		return ok
 	}
-	m := len(idx)
-	sl, sig, blob, off, ln, out := newCBuf(4*m), newCBuf(64*m), newCBuf(total), newCBuf(8*m), newCBuf(4*m), newCBuf(m)
-	defer func() { sl.free(); sig.free(); blob.free(); off.free(); ln.free(); out.free() }()
-	s := (*[maxBatchBytes / 4]uint32)(sl.p)[:m:m]
-	o := (*[maxBatchBytes / 8]uint64)(off.p)[:m:m]
-	l := (*[maxBatchBytes / 4]uint32)(ln.p)[:m:m]
-	pos := 0
-	for k, i := range idx {
-		s[k] = slots[i]
-		copy(sig.b[64*k:], sigs[i])
-		o[k], l[k] = uint64(pos), uint32(len(msgs[i]))
-		pos += copy(blob.b[pos:], msgs[i])
+	if total+76*len(idx) > maxBatchBytes { // split oversize batches
+		h := n / 2
+		copy(ok, g.VerifyBatchKeyed(pubs[:h], msgs[:h], sigs[:h]))
+		copy(ok[h:], g.VerifyBatchKeyed(pubs[h:], msgs[h:], sigs[h:]))
+		return ok
 	}
-	// the arena may not be reset while a keyed verify runs (gpuverify.h)
 	g.mu.Lock()
-	rc := C.gv_verify_msgs_keyed(g.ctx, C.size_t(m), (*C.uint32_t)(sl.p), (*C.uint8_t)(sig.p), (*C.uint8_t)(blob.p),
-		(*C.uint64_t)(off.p), (*C.uint32_t)(ln.p), (*C.uint8_t)(out.p))
+	slots, loaded, _ := g.slotsLocked(pubs, n >= g.KeyLoadMin)
+	var rest []int // leaves whose key is not resident: pub33
+	keyed := idx[:0:0]
+	for _, i := range idx {
+		if loaded[i] {
+			keyed = append(keyed, i)
+		} else {
+			rest = append(rest, i)
+		}
+	}
+	rc := C.int(0)
+	var out cbuf
+	if len(keyed) > 0 {
+		m := len(keyed)
+		sl, sig, blob, off, ln := newCBuf(4*m), newCBuf(64*m), newCBuf(total), newCBuf(8*m), newCBuf(4*m)
+		out = newCBuf(m)
+		s := (*[maxBatchBytes / 4]uint32)(sl.p)[:m:m]
+		o := (*[maxBatchBytes / 8]uint64)(off.p)[:m:m]
+		l := (*[maxBatchBytes / 4]uint32)(ln.p)[:m:m]
+		pos := 0
+		for k, i := range keyed {
+			s[k] = slots[i]
+			copy(sig.b[64*k:], sigs[i])
+			o[k], l[k] = uint64(pos), uint32(len(msgs[i]))
+			pos += copy(blob.b[pos:], msgs[i])
+		}
+		rc = C.gv_verify_msgs_keyed(g.ctx, C.size_t(m), (*C.uint32_t)(sl.p), (*C.uint8_t)(sig.p), (*C.uint8_t)(blob.p),
+			(*C.uint64_t)(off.p), (*C.uint32_t)(ln.p), (*C.uint8_t)(out.p))
+		sl.free()
+		sig.free()
+		blob.free()
+		off.free()
+		ln.free()
+	}
 	g.mu.Unlock()
-	for k, i := range idx {
+	for k, i := range keyed {
 		if rc == 0 {
 			ok[i] = out.b[k] == 1
 		} else {
-			ok[i] = pubs[i].VerifyBytes(msgs[i], sigs[i])
+			ok[i] = pubs[i].VerifyBytes(msgs[i], sigs[i]) // fail closed to the reference path
+		}
+	}
+	if len(keyed) > 0 {
+		out.free()
+	}
+	if len(rest) > 0 {
+		p := make([]secp256k1.PubKeySecp256k1, len(rest))
+		ms := make([][]byte, len(rest))
+		ss := make([][]byte, len(rest))
+		for k, i := range rest {
+			p[k], ms[k], ss[k] = pubs[i], msgs[i], sigs[i]
+		}
+		for k, v := range g.VerifyBatchPub33(p, ms, ss) {
+			ok[rest[k]] = v
 		}
 	}
 	return ok

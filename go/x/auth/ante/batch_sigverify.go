@@ -7,13 +7,21 @@ package ante
 // the verdict cache ahead of the ante handler (SURVEY.md §8b, §8f-1).
 //
 // Same API, same error types and strings, same ReCheck / simulate bypass,
-// same first-failure reporting order; gas is untouched (SigGasConsumeDecorator
-// runs before this decorator, unchanged).  Wiring: replace
+// same first-failure reporting order, and the same gas: the reference loop
+// reads signer i's account through the gas-metered store only after signers
+// 0..i-1 verified (sigverify.go:194-213; gaskv types/context.go:211-212,
+// store/gaskv/store.go:36-43).  This decorator gathers the leaves through a
+// look-ahead context whose gas meter is a fresh infinite one (nothing is
+// charged to the tx), verifies them in one batch, and then walks the signers
+// exactly as the reference loop does -- GetSignerAcc on the real context,
+// verdict, return at the first failure -- so every read the tx is charged
+// for is a read the reference makes, in the same order.  Wiring: replace
 // NewSigVerificationDecorator(ak) at x/auth/ante/ante.go:27 with
 // NewBatchSigVerificationDecorator(ak, verifier, cache).
 //
 // Source-level only in this repository (no Go toolchain in the build image);
-// the C++ mirror host/gvhost.cpp implements the same logic and is tested.
+// the C++ mirror host/gvhost.cpp implements the same logic and its gas is
+// tested against a reference-order restatement (tests/test_gas_order.py).
 
 import (
 	"runtime"
@@ -28,6 +36,7 @@ import (
 	gv "github.com/cosmos/cosmos-sdk/crypto/gpuverify"
 	sdk "github.com/cosmos/cosmos-sdk/types"
 	sdkerrors "github.com/cosmos/cosmos-sdk/types/errors"
+	"github.com/cosmos/cosmos-sdk/x/auth/exported"
 )
 
 // BatchSigVerificationDecorator verifies every signer's signature of a tx
@@ -59,58 +68,98 @@ func (d BatchSigVerificationDecorator) AnteHandle(ctx sdk.Context, tx sdk.Tx, si
 	if len(sigs) != len(signerAddrs) { // sigverify.go:190-192
 		return ctx, sdkerrors.Wrapf(sdkerrors.ErrUnauthorized, "invalid number of signer;  expected: %d, got %d", len(signerAddrs), len(sigs))
 	}
-	// Phase 1 -- the non-cryptographic part of the reference loop in signer
-	// order, stopping where the loop would have returned; every signer before
-	// that point becomes a verification expression.
-	var (
-		exprs    []*expr
-		b        batch
-		firstErr error
-	)
+	// Look-ahead: every signer's leaves up to the first signer the reference
+	// loop would stop at, read through a context whose gas meter is not the
+	// tx's, and all leaves answered at once.
+	var b batch
+	var exprs []*expr
+	if !simulate { // sigverify.go:210: no verification when simulating
+		exprs = d.gather(ctx.WithGasMeter(sdk.NewInfiniteGasMeter()), sigTx, sigs, signerAddrs, &b)
+		b.resolve(d.v, d.cache)
+	}
+	// The reference loop (sigverify.go:194-213) on the real context.
 	for i, sig := range sigs {
-		acc, err := GetSignerAcc(ctx, d.ak, signerAddrs[i])
+		acc, err := GetSignerAcc(ctx, d.ak, signerAddrs[i]) // gas-metered, as :195
 		if err != nil {
-			firstErr = err
-			break
+			return ctx, err
 		}
-		signBytes := sigTx.GetSignBytes(ctx, acc)
 		pubKey := acc.GetPubKey()
 		if !simulate && pubKey == nil {
-			firstErr = sdkerrors.Wrap(sdkerrors.ErrInvalidPubKey, "pubkey on account is not set")
-			break
+			return ctx, sdkerrors.Wrap(sdkerrors.ErrInvalidPubKey, "pubkey on account is not set")
 		}
-		if simulate { // sigverify.go:210: no verification when simulating
+		if simulate {
 			continue
 		}
-		exprs = append(exprs, b.build(pubKey, signBytes, sig))
-	}
-	// Phase 2 -- all leaves at once: verdict cache, then one Verifier batch.
-	b.resolve(d.v, d.cache)
-	for _, e := range exprs { // the FIRST failing signer is the one reported
-		if !e.eval(&b) {
+		var verified bool
+		if i < len(exprs) && exprs[i] != nil {
+			verified = exprs[i].eval(&b)
+		} else { // not gathered (its sign bytes panicked in the look-ahead): the reference call itself
+			verified = pubKey.VerifyBytes(sigTx.GetSignBytes(ctx, acc), sig)
+		}
+		if !verified {
 			return ctx, sdkerrors.Wrap(sdkerrors.ErrUnauthorized, "signature verification failed; verify correct account sequence and chain-id")
 		}
 	}
-	if firstErr != nil {
-		return ctx, firstErr
-	}
 	return next(ctx, tx, simulate)
+}
+
+// gather builds signer i's verification expression for i = 0.. until the
+// first signer whose account is missing or has no key (the loop reports it
+// when it gets there) or whose sign bytes panic (the loop recomputes them on
+// the real context and panics at the same point the reference does).
+func (d BatchSigVerificationDecorator) gather(look sdk.Context, sigTx SigVerifiableTx, sigs [][]byte,
+	signerAddrs []sdk.AccAddress, b *batch) []*expr {
+	exprs := make([]*expr, 0, len(sigs))
+	for i, sig := range sigs {
+		acc := d.ak.GetAccount(look, signerAddrs[i])
+		if acc == nil {
+			break
+		}
+		pubKey := acc.GetPubKey()
+		if pubKey == nil {
+			break
+		}
+		signBytes, ok := signBytesNoPanic(look, sigTx, acc)
+		if !ok {
+			break
+		}
+		exprs = append(exprs, b.build(pubKey, signBytes, sig))
+	}
+	return exprs
+}
+
+func signBytesNoPanic(ctx sdk.Context, sigTx SigVerifiableTx, acc exported.Account) (sb []byte, ok bool) {
+	defer func() {
+		if recover() != nil {
+			sb, ok = nil, false
+		}
+	}()
+	return sigTx.GetSignBytes(ctx, acc), true
 }
 
 // ---------------------------------------------------------------- leaves
 
 // expr is pk.VerifyBytes(msg, sig) as an expression over leaves: a
-// constant, one secp256k1 or ed25519 leaf, or the AND of a multisig's set bits.
+// constant, one secp256k1 or ed25519 leaf, the AND of a multisig's set bits,
+// or a deferred call for any other key (evaluated, on the CPU, only when the
+// evaluation reaches it -- a nil multisig sub-key panics there and only
+// there, after the sub-signatures before it passed, as in the reference).
 type expr struct {
 	konst  bool
 	leaf   int // >= 0: index into batch.pubs (secp256k1)
 	edLeaf int // >= 0: index into batch.ed (ed25519)
 	and    []*expr
 	isAnd  bool
+	cpu    bool // deferred pk.VerifyBytes(msg, sig)
+	pk     crypto.PubKey
+	msg    []byte
+	sig    []byte
 }
 
 func (e *expr) eval(b *batch) bool {
 	switch {
+	case e.cpu:
+		return e.pk.VerifyBytes(e.msg, e.sig)
 	case e.isAnd:
 		for _, k := range e.and { // every leaf is a pure function: the AND equals the short-circuit
 			if !k.eval(b) {
@@ -184,8 +233,8 @@ func (b *batch) build(pk crypto.PubKey, msg, sig []byte) *expr {
 		b.ed.msgs = append(b.ed.msgs, msg)
 		b.ed.sigs = append(b.ed.sigs, sig)
 		return &expr{leaf: -1, edLeaf: len(b.ed.pubs) - 1}
-	default: // includes a nil sub-key: the method call panics exactly as in the reference
-		return &expr{leaf: -1, edLeaf: -1, konst: pk.VerifyBytes(msg, sig)}
+	default: // includes a nil sub-key: deferred to eval, which panics exactly where the reference does
+		return &expr{leaf: -1, edLeaf: -1, cpu: true, pk: pk, msg: msg, sig: sig}
 	}
 }
 
@@ -267,20 +316,27 @@ func (b *batch) resolveEd(v gv.Verifier, cache *gv.VerdictCache) {
 // ---------------------------------------------------------- PreVerifyTxs
 
 // NewPreVerifier returns the function baseapp.PreVerifyTxs calls on a batch
-// of decoded txs (a block before its DeliverTx loop, a CheckTx window, the
-// genesis gentxs): every signer's sign bytes are predicted -- account number
-// from state (0 at height 0, stdtx.go:249-253), sequence = state sequence +
-// earlier txs of the same signer in the batch -- and all leaves are verified
-// in one batch into the cache.  A wrong prediction is only a cache miss: the
-// decorator rebuilds the sign bytes from the state it runs on.
-func NewPreVerifier(ak AccountKeeper, v gv.Verifier, cache *gv.VerdictCache) func(ctx sdk.Context, txs []sdk.Tx) {
-	return func(ctx sdk.Context, txs []sdk.Tx) {
+// of decoded txs (a block before its DeliverTx loop, a mempool ingress batch,
+// the genesis gentxs): every signer's sign bytes are predicted -- account
+// number from state (0 at height 0, stdtx.go:249-253), sequence = state
+// sequence + earlier txs of the same signer in the batch -- and all leaves
+// are verified in one batch into the cache.  A wrong prediction is only a
+// cache miss: the decorator rebuilds the sign bytes from the state it runs on.
+//
+// Two stages: the returned function reads the state (accounts, through a
+// context with its own infinite gas meter) and returns the second stage,
+// which touches no state -- sign bytes on every core, then the batch -- so a
+// caller can release its state lock before the GPU call (baseapp Ingress).
+func NewPreVerifier(ak AccountKeeper, v gv.Verifier, cache *gv.VerdictCache) func(ctx sdk.Context, txs []sdk.Tx) func() {
+	return func(ctx sdk.Context, txs []sdk.Tx) func() {
+		// Reads go through a context with its own infinite gas meter: the
+		// hook runs outside any tx and must not charge a block or tx meter.
+		look := ctx.WithGasMeter(sdk.NewInfiniteGasMeter())
 		type job struct {
-			sigTx  SigVerifiableTx
-			signer int
-			pk     crypto.PubKey
-			sig    []byte
-			seq    uint64
+			sigTx SigVerifiableTx
+			acc   exported.Account // this job's own decode, sequence set to the prediction
+			pk    crypto.PubKey
+			sig   []byte
 		}
 		var jobs []job
 		bump := map[string]uint64{}
@@ -291,7 +347,7 @@ func NewPreVerifier(ak AccountKeeper, v gv.Verifier, cache *gv.VerdictCache) fun
 			}
 			sigs, signers, txPks := sigTx.GetSignatures(), sigTx.GetSigners(), sigTx.GetPubKeys()
 			for i := 0; i < len(sigs) && i < len(signers); i++ {
-				acc := ak.GetAccount(ctx, signers[i]) // a fresh decode: mutating it is local
+				acc := ak.GetAccount(look, signers[i]) // a fresh decode: mutating it is local
 				if acc == nil {
 					continue
 				}
@@ -302,44 +358,43 @@ func NewPreVerifier(ak AccountKeeper, v gv.Verifier, cache *gv.VerdictCache) fun
 				if pk == nil {
 					continue
 				}
-				seq := acc.GetSequence() + bump[signers[i].String()]
-				jobs = append(jobs, job{sigTx, i, pk, sigs[i], seq})
+				_ = acc.SetSequence(acc.GetSequence() + bump[signers[i].String()])
+				jobs = append(jobs, job{sigTx, acc, pk, sigs[i]})
 			}
 			for _, a := range signers {
 				bump[a.String()]++
 			}
 		}
-		// sign bytes (JSON) on every core, then one batch
-		parts := make([]batch, runtime.NumCPU())
-		var wg sync.WaitGroup
-		for w := range parts {
-			wg.Add(1)
-			go func(w int) {
-				defer wg.Done()
-				for k := w; k < len(jobs); k += len(parts) {
-					j := jobs[k]
-					acc := ak.GetAccount(ctx, j.sigTx.GetSigners()[j.signer])
-					if acc == nil {
-						continue
+		// Sign bytes (JSON) on every core, then one batch.  The workers touch
+		// no store and no gas meter: GetSignBytes reads only the chain id and
+		// height of the context and the job's own account copy.
+		return func() {
+			parts := make([]batch, runtime.NumCPU())
+			var wg sync.WaitGroup
+			for w := range parts {
+				wg.Add(1)
+				go func(w int) {
+					defer wg.Done()
+					for k := w; k < len(jobs); k += len(parts) {
+						j := jobs[k]
+						func() {
+							defer func() { _ = recover() }() // malformed tx: the ante chain reports it
+							parts[w].build(j.pk, j.sigTx.GetSignBytes(look, j.acc), j.sig)
+						}()
 					}
-					_ = acc.SetSequence(j.seq)
-					func() {
-						defer func() { _ = recover() }() // malformed multisig: the ante chain reports it
-						parts[w].build(j.pk, j.sigTx.GetSignBytes(ctx, acc), j.sig)
-					}()
-				}
-			}(w)
+				}(w)
+			}
+			wg.Wait()
+			var all batch
+			for _, p := range parts {
+				all.pubs = append(all.pubs, p.pubs...)
+				all.msgs = append(all.msgs, p.msgs...)
+				all.sigs = append(all.sigs, p.sigs...)
+				all.ed.pubs = append(all.ed.pubs, p.ed.pubs...)
+				all.ed.msgs = append(all.ed.msgs, p.ed.msgs...)
+				all.ed.sigs = append(all.ed.sigs, p.ed.sigs...)
+			}
+			all.resolve(v, cache)
 		}
-		wg.Wait()
-		var all batch
-		for _, p := range parts {
-			all.pubs = append(all.pubs, p.pubs...)
-			all.msgs = append(all.msgs, p.msgs...)
-			all.sigs = append(all.sigs, p.sigs...)
-			all.ed.pubs = append(all.ed.pubs, p.ed.pubs...)
-			all.ed.msgs = append(all.ed.msgs, p.ed.msgs...)
-			all.ed.sigs = append(all.ed.sigs, p.ed.sigs...)
-		}
-		all.resolve(v, cache)
 	}
 }

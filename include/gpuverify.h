@@ -126,6 +126,24 @@ size_t gv_keys_count(const gv_ctx* ctx);
  * generation may name other keys). */
 uint64_t gv_keys_generation(const gv_ctx* ctx);
 
+/* Routing policy shared by the callers above this ABI (the Go shim
+ * go/crypto/gpuverify reads these through cgo; the C++ mirror host/gvhost.cpp
+ * uses them as its defaults), so the two cannot drift apart:
+ *   GV_CPU_CROSSOVER  batches smaller than this go to the reference CPU
+ *                     VerifyBytes (one host core answers a
+ *                     single signature in ~0.20 ms, the sliced small-batch
+ *                     kernels ~0.21 ms at any size up to 256);
+ *   GV_KEY_LOAD_MIN   only batches of at least this many leaves (a block)
+ *                     load keys that are not resident yet; a smaller batch
+ *                     (CheckTx) goes keyed only when all its keys are
+ *                     resident, else pub33 (loading per
+ *                     CheckTx window cost 35.8k -> 5.1k tx/s);
+ *   GV_KEY_CAP        arena size at which the caller resets the arena
+ *                     (5.4 KB of HBM per key). */
+#define GV_CPU_CROSSOVER 4
+#define GV_KEY_LOAD_MIN 4096
+#define GV_KEY_CAP (1u << 22)
+
 /* Key-arena readback (tests, tools): for each slot, the affine point the
  * arena holds for it, out_xy64 + 64*i = x || y (32 bytes each, big-endian),
  * and out_ok[i] = its ParsePubKey verdict (a slot >= gv_keys_count(): zeros

@@ -20,6 +20,7 @@ import pytest
 import gvhost
 import gpuverify as gvm
 import txkit as T
+from ante_ref import AnteRef
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FEE = T.Fee([(150, "atom")], 200000)
@@ -40,15 +41,20 @@ class Key:
 KEYS = [Key(i) for i in range(10)]
 
 
-def make_tx(app_chain, signers, accnums, seqs, msgs=None, fee=FEE, memo="", with_pub=True, sign_keys=None):
-    """An amino StdTx of MsgSends signed by `signers` (Key objects) over their sign bytes."""
+def make_parts(app_chain, signers, accnums, seqs, msgs=None, fee=FEE, memo="", with_pub=True, sign_keys=None):
+    """(msgs, fee, memo, sigs) of a StdTx of MsgSends signed by `signers` (Key objects) over their sign bytes."""
     msgs = msgs or [T.MsgSend(s.addr, KEYS[9].addr, [(10, "atom")]) for s in signers]
     sign_keys = sign_keys or signers
     sigs = []
     for k, s, an, sq in zip(sign_keys, signers, accnums, seqs):
         sb = T.std_sign_bytes(app_chain, an, sq, fee, msgs, memo)
         sigs.append((s.pub if with_pub else b"", k.sign(sb)))
-    return T.std_tx(msgs, fee, memo, sigs)
+    return msgs, fee, memo, sigs
+
+
+def make_tx(*a, **kw):
+    """The amino StdTx bytes of make_parts(...)."""
+    return T.std_tx(*make_parts(*a, **kw))
 
 
 def new_app(verifier=None, chain="gv-test", height=1):
@@ -56,6 +62,14 @@ def new_app(verifier=None, chain="gv-test", height=1):
     for i, k in enumerate(KEYS):
         app.set_account(k.addr, i, 0)
     return app
+
+
+def new_ref(chain="gv-test", height=1, recheck=False):
+    """tests/ante_ref.py over new_app's accounts: the reference chain's (code, log, gas)."""
+    ref = AnteRef(chain, height=height, recheck=recheck)
+    for i, k in enumerate(KEYS):
+        ref.set_account(k.addr, i, 0)
+    return ref
 
 
 # ---------------------------------------------------------------- CPU tests
@@ -137,15 +151,19 @@ def test_pubkey_mismatch_and_unknown_account():
 
 def test_recheck_and_simulate_skip_verification():
     app = new_app()
-    tx = make_tx("gv-test", [KEYS[0]], [0], [0])
+    parts = make_parts("gv-test", [KEYS[0]], [0], [0])
+    tx = T.std_tx(*parts)
     app.set_context("gv-test", 1, recheck=True)
     rc, r = app.ante(tx)                        # TestAnteHandlerReCheck: verification skipped
-    assert rc == 0 and r["code"] == 0 and r["gpu_leaves"] == 0 and r["gas_used"] == 1000
+    want = new_ref(recheck=True).ante(*parts, len(tx))
+    assert rc == 0 and r["code"] == 0 and r["gpu_leaves"] == 0 and r["gas_used"] == want[2]
     assert app.get_account(KEYS[0].addr)["sequence"] == 0          # no increment on ReCheck
     app.set_context("gv-test", 1)
     sim = T.std_tx([T.MsgSend(KEYS[1].addr, KEYS[9].addr, [(1, "atom")])], FEE, "", [(b"", b"")])
+    app.set_gas_model(False)                    # signature gas alone: the sim pubkey's charge
     rc, r = app.ante(sim, simulate=True)        # Simulate: sim pubkey for gas, no verification
     assert rc == 0 and r["code"] == 0 and r["gas_used"] == 1000
+    app.set_gas_model(True)
     assert app.get_account(KEYS[1].addr)["sequence"] == 1
 
 
@@ -190,9 +208,11 @@ def ver():
 def test_sig_verification_cases(ver):
     """TestSigVerification / TestAnteHandlerSigErrors / BadSignBytes."""
     app = new_app(ver)
-    ok_tx = make_tx("gv-test", [KEYS[0]], [0], [0])
+    parts = make_parts("gv-test", [KEYS[0]], [0], [0])
+    ok_tx = T.std_tx(*parts)
     rc, r = app.ante(ok_tx)
-    assert rc == 0 and r["code"] == 0 and r["gpu_leaves"] == 1 and r["gas_used"] == 1000
+    assert rc == 0 and r["code"] == 0 and r["gpu_leaves"] == 1
+    assert (r["code"], r["log"], r["gas_used"]) == new_ref().ante(*parts, len(ok_tx))
     assert app.get_account(KEYS[0].addr)["sequence"] == 1
     # replay (sequence now 1) -> bad sign bytes
     rc, r = app.ante(ok_tx)
@@ -212,9 +232,11 @@ def test_sig_verification_cases(ver):
 def test_multi_signer_and_first_failure_order(ver):
     """TestAnteHandlerMultiSigner + the reference's first-failure reporting."""
     app = new_app(ver)
-    tx = make_tx("gv-test", [KEYS[0], KEYS[1], KEYS[2]], [0, 1, 2], [0, 0, 0])
+    parts = make_parts("gv-test", [KEYS[0], KEYS[1], KEYS[2]], [0, 1, 2], [0, 0, 0])
+    tx = T.std_tx(*parts)
     rc, r = app.ante(tx)
-    assert r["code"] == 0 and r["gpu_leaves"] == 3 and r["gas_used"] == 3000
+    assert r["code"] == 0 and r["gpu_leaves"] == 3
+    assert (r["code"], r["log"], r["gas_used"]) == new_ref().ante(*parts, len(tx))
     # signer 1 signs with the wrong key; signer 2 has no pubkey anywhere
     app2 = new_app(ver)
     msgs = [T.MsgSend(k.addr, KEYS[9].addr, [(10, "atom")]) for k in KEYS[:3]]
@@ -243,14 +265,19 @@ def test_multisig_k_of_n(ver):
     mk = T.amino_multisig(3, pubs)
     maddr = T.address(mk)
     app.set_account(maddr, 40, 0)
+    ref = new_ref()
+    ref.set_account(maddr, 40, 0)
     msgs = [T.MsgSend(maddr, KEYS[9].addr, [(5, "atom")])]
     sb = T.std_sign_bytes("gv-test", 40, 0, FEE, msgs, "")
     bits = [True, False, True, False, True, True]
     sigs = [subs[0].sign(sb), subs[2].sign(sb), subs[4].sign(sb), T.ed25519_sign(ed_seed, sb)]
-    tx = T.std_tx(msgs, FEE, "", [(mk, T.multisignature(bits, sigs))])
+    tx_sigs = [(mk, T.multisignature(bits, sigs))]
+    tx = T.std_tx(msgs, FEE, "", tx_sigs)
     rc, r = app.ante(tx)
-    # 3 secp256k1 leaves + 1 ed25519 leaf, all on the GPU (gv_verify_ed25519_msgs for the ed25519 one)
-    assert rc == 0 and r["code"] == 0 and r["gpu_leaves"] == 4 and r["gas_used"] == 3 * 1000 + 590
+    # 3 secp256k1 leaves + 1 ed25519 leaf, all on the GPU (gv_verify_ed25519_msgs for the ed25519 one);
+    # gas: 3 x 1000 + 590 of signature gas besides the KV reads / writes
+    assert rc == 0 and r["code"] == 0 and r["gpu_leaves"] == 4
+    assert (r["code"], r["log"], r["gas_used"]) == ref.ante(msgs, FEE, "", tx_sigs, len(tx))
     # one bad secp256k1 leaf -> whole multisig false
     sb1 = T.std_sign_bytes("gv-test", 40, 1, FEE, msgs, "")
     bad = [subs[0].sign(sb1), subs[1].sign(sb1), subs[4].sign(sb1), T.ed25519_sign(ed_seed, sb1)]

@@ -25,7 +25,7 @@ import pytest
 import gpuverify as gvm
 import gvhost
 import txkit as T
-from oracle import oracle as O
+from ante_ref import AnteRef, _fields
 
 pytestmark = pytest.mark.gpu
 
@@ -73,37 +73,6 @@ class MultiAcct:
         self.number = 100 + idx
 
 
-def leaf_ok(key, msg, sig):
-    if len(sig) != 64:
-        return False
-    if key.ed:
-        return sig == key.sign(msg)                    # ed25519 signatures are deterministic
-    return O.verify_bytes(key.pub33, msg, sig)
-
-
-def expect(acct, seq_state, tx_parts):
-    """(code, log, gas) of the ante chain for one multisig tx, restating
-    DefaultSigVerificationGasConsumer + multisig.VerifyBytes; leaves by the oracle."""
-    msgs, bits, sigs, claimed = tx_parts
-    gas = 0
-    si = 0
-    for i, b in enumerate(bits):                       # gas consumer: per set bit (sigverify.go:325-338)
-        if b:
-            gas += 590 if acct.subs[i].ed else 1000
-            si += 1
-    msg = T.std_sign_bytes(CHAIN, acct.number, seq_state, FEE, msgs, "")
-    ok = len(bits) == acct.n and acct.k <= len(sigs) <= len(bits) and sum(bits) >= acct.k
-    if ok:
-        j = 0
-        for i, b in enumerate(bits):
-            if b:
-                ok = ok and leaf_ok(acct.subs[i], msg, sigs[j])
-                j += 1
-                if not ok:
-                    break
-    return (0, "", gas) if ok else (4, UNAUTH, gas)
-
-
 def build_block(accts, seqs, rng, ntx, sink):
     """Txs with their parts.  Each tx is signed for the sequence its signer
     expects (the state plus the earlier well-formed txs of the block); some
@@ -141,13 +110,29 @@ def build_block(accts, seqs, rng, ntx, sink):
     return txs, parts
 
 
-def check_block(results, parts, state_seq):
-    for r, (a, p) in zip(results, parts):
-        code, log, gas = expect(a, state_seq[a.addr], p)
-        assert (r["code"], r["log"]) == (code, log), (p[1], p[3], state_seq[a.addr])
-        assert r["gas_used"] == gas
-        if code == 0:
-            state_seq[a.addr] += 1
+def decode_sig(tx: bytes) -> bytes:
+    """the first StdSignature's signature bytes of an amino StdTx"""
+    for f, _, v in _fields(tx[4:]):
+        if f == 3:
+            return dict((g, w) for g, _, w in _fields(v))[2]
+    raise ValueError("no signature")
+
+
+def new_ref(accts, height):
+    """tests/ante_ref.py over the accounts of a test app: the reference chain's
+    (code, log, gas) per tx, state moved on success."""
+    ref = AnteRef(CHAIN, height=height)
+    for a in accts:
+        ref.set_account(a.addr, a.number, 0)
+    return ref
+
+
+def check_block(results, txs, parts, ref, state_seq):
+    for r, tx, (a, p) in zip(results, txs, parts):
+        msgs, bits, sigs, claimed = p
+        want = ref.ante(msgs, FEE, "", [(a.amino, T.multisignature(bits, sigs))], len(tx))
+        assert (r["code"], r["log"], r["gas_used"]) == want, (p[1], p[3], state_seq[a.addr])
+        state_seq[a.addr] = ref.accounts[a.addr].sequence
 
 
 def test_c4_multisig_block_replay(ver):
@@ -159,13 +144,14 @@ def test_c4_multisig_block_replay(ver):
     app = gvhost.HostApp(ver, chain_id=CHAIN, height=5)
     for a in accts:
         app.set_account(a.addr, a.number, 0)
+    ref = new_ref(accts, 5)
     seqs = {a.addr: 0 for a in accts}
     total_gpu = 0
     for blk in range(3):
         txs, parts = build_block(accts, seqs, rng, 300, sink_addr)
         rc, res = app.deliver_block(txs)
         assert rc == 0
-        check_block(res, parts, seqs)
+        check_block(res, txs, parts, ref, seqs)
         total_gpu += sum(r["gpu_leaves"] for r in res)
     codes = [r["code"] for r in res]
     assert set(codes) == {0, 4} and codes.count(0) > 200
@@ -195,6 +181,7 @@ def test_keyed_and_pub33_block_paths_agree_across_arena_resets(ver):
             app.set_account(a.addr, a.number, 0)
         apps[name] = app
     seqs = {a.addr: 0 for a in accts}
+    ref = new_ref(accts, 6)
     strip = lambda r: (r["code"], r["log"], r["gas_used"], r["gas_wanted"])
     for blk in range(4):
         txs, parts = build_block(accts, seqs, rng, 200, sink_addr)
@@ -204,7 +191,7 @@ def test_keyed_and_pub33_block_paths_agree_across_arena_resets(ver):
         assert rc1 == 0 and rc2 == 0 and rc0 == 0
         assert [strip(r) for r in r1] == [strip(r) for r in r0]
         assert [strip(r) for r in r2] == [strip(r) for r in r0]
-        check_block(r1, parts, seqs)
+        check_block(r1, txs, parts, ref, seqs)
         if blk == 1:
             ver.keys_reset()
             ver.keys_load(np.frombuffer(bytes([2]) + bytes(range(1, 33)), np.uint8).reshape(1, 33))
@@ -296,10 +283,51 @@ def test_checktx_window_batches_concurrent_calls(ver):
         t.join()
     st = app.stats()
     assert st["window_txs"] == len(txs) and st["windows"] <= len(txs) // 8
+    lone = 0
     for i, (rc, r) in enumerate(out):
         assert rc == 0 and r["code"] == (4 if i % 9 == 0 else 0), (i, r)
-        assert r["cache_hits"] == 1 and r["gpu_leaves"] == 0
+        if r["cache_hits"] == 0:                 # a call that found nothing else in flight: no window
+            assert r["gpu_leaves"] == 1
+            lone += 1
+        else:
+            assert r["cache_hits"] == 1 and r["gpu_leaves"] == 0
+    assert lone <= 2
     app.close()
+
+
+def test_checktx_serial_calls_do_not_wait(ver):
+    """Tendermint v0.33 delivers CheckTx one call at a time (local client
+    mutex, server/start.go:173; baseapp/abci.go:165-196).  A lone call finds
+    nothing in flight and runs its ante chain at once: with a 20 ms window,
+    30 sequential calls take far less than 30 x 20 ms, each verifying its own
+    leaf, with the serial ante path's results."""
+    import time
+    keys = [SecpKey(b"cs-%d" % i) for i in range(30)]
+    sink = T.address(SecpKey(b"cs-sink").amino)
+    txs = []
+    for i, k in enumerate(keys):
+        addr = T.address(k.amino)
+        msgs = [T.MsgSend(addr, sink, [(3, "z")])]
+        sb = T.std_sign_bytes(CHAIN, i, 0, FEE, msgs, "")
+        txs.append(T.std_tx(msgs, FEE, "", [(k.amino, k.sign(sb) if i % 7 else b"\x01" * 64)]))
+    app = gvhost.HostApp(ver, chain_id=CHAIN, height=3)
+    plain = gvhost.HostApp(ver, chain_id=CHAIN, height=3)
+    for i, k in enumerate(keys):
+        app.set_account(T.address(k.amino), i, 0)
+        plain.set_account(T.address(k.amino), i, 0)
+    app.set_window(32, 20000)
+    t = time.perf_counter()
+    out = [app.checktx(tx) for tx in txs]
+    elapsed = time.perf_counter() - t
+    assert elapsed < 0.3, elapsed
+    strip = lambda r: (r["code"], r["log"], r["gas_used"])
+    for tx, (rc, r) in zip(txs, out):
+        rc2, r2 = plain.ante(tx)
+        assert rc == 0 and rc2 == 0 and strip(r) == strip(r2)
+        assert r["gpu_leaves"] == 1 and r["cache_hits"] == 0
+    assert app.stats()["windows"] == len(txs)
+    app.close()
+    plain.close()
 
 
 def test_deliver_gentxs_height_zero(ver):
@@ -321,7 +349,14 @@ def test_deliver_gentxs_height_zero(ver):
     rc, res, first = app.deliver_gentxs(txs)
     assert rc == 0 and first == 3
     assert [r["code"] for r in res] == [0, 0, 0, 4, 0]
-    assert all(r["gas_used"] == 1000 for r in res)
+    ref = AnteRef(CHAIN, height=0)                          # infinite meter, account number 0
+    for i, k in enumerate(keys):
+        ref.set_account(T.address(k.amino), 40 + i, 0)
+    for r, tx, k in zip(res, txs, keys):
+        addr = T.address(k.amino)
+        msgs = [T.MsgSend(addr, addr, [(1, "stake")])]
+        want = ref.ante(msgs, T.Fee([], 0), "", [(k.amino, decode_sig(tx))], len(tx))
+        assert (r["code"], r["gas_used"]) == (want[0], want[2]), (r, want)
     app.close()
 
 

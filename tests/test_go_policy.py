@@ -1,0 +1,89 @@
+"""The Go drop-in (go/, source-only: no Go toolchain in this image) against
+the tested C++ mirror: the routing policy comes from one place (gpuverify.h
+macros read by both), and the decorator's structure keeps the reference's
+gas order (the C++ mirror's gas is checked numerically in test_gas_order.py).
+"""
+import os
+import re
+
+import gvhost
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def read(*p):
+    return open(os.path.join(REPO, *p)).read()
+
+
+def header_macros():
+    h = read("include", "gpuverify.h")
+    out = {}
+    for name in ("GV_CPU_CROSSOVER", "GV_KEY_LOAD_MIN", "GV_KEY_CAP"):
+        m = re.search(r"#define %s \(?(\d+)u?(?: << (\d+))?\)?" % name, h)
+        assert m, name
+        out[name] = int(m.group(1)) << int(m.group(2) or 0)
+    return out
+
+
+def strip_comments(go: str) -> str:
+    return re.sub(r"//[^\n]*", "", go)
+
+
+def test_policy_constants_shared_by_go_and_cpp():
+    mac = header_macros()
+    assert mac == {"GV_CPU_CROSSOVER": 4, "GV_KEY_LOAD_MIN": 4096, "GV_KEY_CAP": 1 << 22}
+    app = gvhost.HostApp(None)
+    assert app.keyed_policy() == (True, mac["GV_KEY_LOAD_MIN"], mac["GV_KEY_CAP"])
+    app.close()
+    go = strip_comments(read("go", "crypto", "gpuverify", "gpuverify.go"))
+    assert re.search(r"DefaultCPUBelow\s*=\s*int\(C\.GV_CPU_CROSSOVER\)", go)
+    assert re.search(r"DefaultKeyLoadMin\s*=\s*int\(C\.GV_KEY_LOAD_MIN\)", go)
+    assert re.search(r"DefaultKeyCap\s*=\s*int\(C\.GV_KEY_CAP\)", go)
+    opener = go[go.index("func Open("):go.index("func (g *GPU) Close()")]
+    for field in ("CPUBelow: DefaultCPUBelow", "Keyed: true", "KeyLoadMin: DefaultKeyLoadMin",
+                  "KeyCap: DefaultKeyCap"):
+        assert field in opener, field
+
+
+def test_go_verify_batch_routes_like_the_mirror():
+    go = strip_comments(read("go", "crypto", "gpuverify", "gpuverify.go"))
+    vb = go[go.index("func (g *GPU) VerifyBatch("):go.index("func (g *GPU) VerifyBatchPub33(")]
+    # CPU below the crossover, then keyed, else pub33 -- in that order
+    assert vb.index("g.CPUBelow") < vb.index("g.Keyed") < vb.index("VerifyBatchPub33")
+    keyed = go[go.index("func (g *GPU) VerifyBatchKeyed("):]
+    # loads only from KeyLoadMin leaves; the lock spans lookup and keyed verify
+    assert "g.slotsLocked(pubs, n >= g.KeyLoadMin)" in keyed
+    lock, unlock = keyed.index("g.mu.Lock()"), keyed.index("g.mu.Unlock()")
+    assert lock < keyed.index("slotsLocked") < keyed.index("gv_verify_msgs_keyed") < unlock
+    assert "maxBatchBytes" in keyed                      # oversize split
+
+
+def test_go_decorator_charges_reads_in_reference_order():
+    go = strip_comments(read("go", "x", "auth", "ante", "batch_sigverify.go"))
+    ah = go[go.index("func (d BatchSigVerificationDecorator) AnteHandle("):go.index("func (d BatchSigVerificationDecorator) gather(")]
+    # look-ahead on a context with its own meter, then the reference loop on ctx
+    assert "d.gather(ctx.WithGasMeter(sdk.NewInfiniteGasMeter())" in ah
+    loop = ah[ah.index("for i, sig := range sigs"):]
+    assert loop.index("GetSignerAcc(ctx, d.ak, signerAddrs[i])") < loop.index("exprs[i].eval(&b)")
+    assert "return ctx, sdkerrors.Wrap(sdkerrors.ErrUnauthorized" in loop
+    gather = go[go.index("func (d BatchSigVerificationDecorator) gather("):go.index("func signBytesNoPanic(")]
+    assert "d.ak.GetAccount(look," in gather and "GetSignerAcc(ctx" not in gather
+    # unknown / nil sub-keys are deferred to eval (no panic while gathering)
+    build = go[go.index("func (b *batch) build("):go.index("func (b *batch) resolve(")]
+    assert "cpu: true" in build and "VerifyBytes" not in build.split("default:")[1]
+    # the pre-verifier's workers never read the store or a gas meter
+    pv = go[go.index("func NewPreVerifier("):]
+    assert "ctx.WithGasMeter(sdk.NewInfiniteGasMeter())" in pv
+    workers = pv[pv.index("return func() {"):]
+    assert "GetAccount" not in workers and "GasMeter" not in workers
+
+
+def test_go_checktx_window_is_adaptive_and_ingress_releases_lock():
+    go = strip_comments(read("go", "baseapp", "preverify.go"))
+    join = go[go.index("func (w *CheckTxWindow) join("):go.index("func (w *CheckTxWindow) flush(")]
+    assert "lone := w.cur == nil && w.inflight == 0 && w.lastSize <= 1" in join
+    assert "full := lone ||" in join
+    loop = go[go.index("func (in *Ingress) loop()"):go.index("func (in *Ingress) CheckTx(")]
+    # state stage under the lock, GPU stage after it is released
+    assert loop.index("in.stateMu.Lock()") < loop.index("prepareCheckTxs(batch)") < \
+        loop.index("in.stateMu.Unlock()") < loop.index("verify()")

@@ -1,12 +1,21 @@
-"""Large-scale accept/reject parity (north star: bit-exact on 10M mixed
-valid/invalid signatures).  Opt-in: set GV_PARITY_MILLIONS=10 (it signs 10M
-items with OpenSSL, ~15 s per million on 16 threads).
+"""North-star parity (BASELINE.json: bit-exact accept/reject on 10M mixed
+valid/invalid signatures), run by default under -m gpu.
 
-Each million: C3 adversarial mix (25 % invalid: high-S, r >= n, s = 0 or
-2^256-1, random x, malformed prefix, wrong message), seed 0x5EED00 + chunk.
-The full GPU bitmap is compared with the verdicts known by construction, and a
-random 50k sample per chunk with the CPU oracle as well.  With GV_PARITY_OUT set,
-a JSON summary is written there.
+GV_PARITY_MILLIONS (default 10) chunks of 1M items, seed 0x5EED00 + chunk:
+the C3 adversarial mix of tools/workload (25 % invalid: high-S, r >= n,
+s = 0 or 2^256-1, random x, malformed prefix, wrong message) with fresh
+special cases written over random positions (tests/special_cases.py: point
+at infinity, R.x in [n, p) with r = R.x - n (accept) and r = R.x (reject),
+s = (n-1)/2 and (n+1)/2, small / lambda-related keys, forced (u1, u2)
+exceptional additions and Booth-extreme windows, e in {0, n, n+1, 2^256-1}),
+so the million-scale mix covers every acceptance and rejection rule.
+
+Every chunk runs the throughput schedule (the headline path); one more 1M
+chunk runs through the limb-sliced small-batch kernels (k_verify_lat_sl by
+pub33, k_verify_lat16_sl keyed) with the small-batch bounds lifted.  The GPU
+bitmaps are compared in full with the verdicts known by construction, and
+all special cases plus a random 20k sample per chunk with the C oracle.  A
+JSON summary goes to GV_PARITY_OUT when set.  GV_PARITY_MILLIONS=0 skips.
 """
 import json
 import os
@@ -19,42 +28,78 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-MILLIONS = int(os.environ.get("GV_PARITY_MILLIONS", "0"))
+MILLIONS = int(os.environ.get("GV_PARITY_MILLIONS", "10"))
+SPECIAL_PER_KIND = 100
+
+
+def sprinkle(rng, pub, sig, dig, exp, chunk):
+    import special_cases as S
+    sp, ss, sd, se, kinds = S.make(np.random.default_rng(0xC0FFEE + chunk), SPECIAL_PER_KIND)
+    pos = rng.choice(len(pub), len(kinds), replace=False)
+    pub[pos], sig[pos], dig[pos], exp[pos] = sp, ss, sd, se
+    return pos, kinds
+
+
+def check_chunk(ver, O, rng, pub, sig, dig, exp, pos, threads, got):
+    mism = int(np.count_nonzero(got != exp))
+    idx = np.union1d(rng.choice(len(pub), 20_000, replace=False), pos)
+    ref = O.verify_digests(pub[idx], sig[idx], dig[idx], threads=threads)
+    mo = int(np.count_nonzero(ref != got[idx])) + int(np.count_nonzero(ref != exp[idx]))
+    return mism, mo, len(idx)
 
 
 @pytest.mark.gpu
-@pytest.mark.skipif(MILLIONS <= 0, reason="set GV_PARITY_MILLIONS to run")
+@pytest.mark.skipif(MILLIONS <= 0, reason="GV_PARITY_MILLIONS=0")
 def test_parity_millions():
     import bench
     import gpuverify as gvm
     from oracle import oracle as O
     threads = min(16, os.cpu_count() or 1)
     n = 1_000_000
-    ver = gvm.Verifier([0])
     rng = np.random.default_rng(7)
-    summary = {"chunks": [], "items": 0, "mismatch_vs_construction": 0, "oracle_sampled": 0,
-               "mismatch_vs_oracle": 0, "invalid": 0}
+    summary = {"chunks": [], "items": 0, "mismatch_vs_construction": 0, "oracle_checked": 0,
+               "mismatch_vs_oracle": 0, "invalid": 0, "special": {}}
     t0 = time.time()
-    for c in range(MILLIONS):
-        pub, sig, dig, exp = bench.make_digest_workload(n, 0x5EED00 + c, 65536, 0.25, threads)
-        got = ver.verify_batch_digests(pub, sig, dig)
-        mism = int(np.count_nonzero(got != exp))
-        idx = rng.choice(n, 50_000, replace=False)
-        ref = O.verify_digests(pub[idx], sig[idx], dig[idx], threads=threads)
-        mo = int(np.count_nonzero(ref != got[idx]))
-        summary["chunks"].append({"seed": 0x5EED00 + c, "mismatch": mism, "oracle_mismatch": mo,
-                                  "invalid": int(n - exp.sum())})
-        summary["items"] += n
-        summary["mismatch_vs_construction"] += mism
-        summary["oracle_sampled"] += len(idx)
-        summary["mismatch_vs_oracle"] += mo
-        summary["invalid"] += int(n - exp.sum())
-        print(f"chunk {c}: mismatches {mism}, oracle sample mismatches {mo}, {time.time() - t0:.0f}s", flush=True)
-    ver.close()
+    with gvm.Verifier([0]) as ver:
+        for c in range(MILLIONS + 1):
+            sliced = c == MILLIONS                       # the extra chunk: small-batch kernels
+            pub, sig, dig, exp = bench.make_digest_workload(n, 0x5EED00 + c, 65536, 0.25, threads)
+            pos, kinds = sprinkle(rng, pub, sig, dig, exp, c)
+            for k in kinds:
+                summary["special"][k] = summary["special"].get(k, 0) + 1
+            rec = {"seed": 0x5EED00 + c, "schedule": "throughput", "invalid": int(n - exp.sum()),
+                   "special": len(kinds)}
+            if not sliced:
+                got = ver.verify_batch_digests(pub, sig, dig)
+                rec["mismatch"], rec["oracle_mismatch"], checked = check_chunk(ver, O, rng, pub, sig, dig, exp, pos,
+                                                                               threads, got)
+            else:
+                ver.set_option("lat_max", 1 << 30)       # every batch size through the sliced kernels
+                ver.set_option("lat_sl_max", 1 << 30)
+                got = ver.verify_batch_digests(pub, sig, dig)
+                uniq, inv = np.unique(pub, axis=0, return_inverse=True)
+                slots = ver.keys_load(np.ascontiguousarray(uniq))[inv.reshape(-1)]
+                gk = ver.verify_batch_digests_keyed(np.ascontiguousarray(slots, np.uint32), sig, dig)
+                ver.keys_reset()
+                m1, o1, checked = check_chunk(ver, O, rng, pub, sig, dig, exp, pos, threads, got)
+                m2, o2, _ = check_chunk(ver, O, rng, pub, sig, dig, exp, pos, threads, gk)
+                rec.update({"schedule": "sliced pub33 + sliced keyed", "mismatch": m1 + m2, "oracle_mismatch": o1 + o2,
+                            "mismatch_pub33": m1, "mismatch_keyed": m2})
+                n_items = 2 * n
+            summary["chunks"].append(rec)
+            summary["items"] += n if not sliced else n_items
+            summary["mismatch_vs_construction"] += rec["mismatch"]
+            summary["oracle_checked"] += checked
+            summary["mismatch_vs_oracle"] += rec["oracle_mismatch"]
+            summary["invalid"] += rec["invalid"]
+            print(f"chunk {c} ({rec['schedule']}): mismatches {rec['mismatch']}, oracle mismatches "
+                  f"{rec['oracle_mismatch']}, {time.time() - t0:.0f}s", flush=True)
     summary["seconds"] = round(time.time() - t0, 1)
     out = os.environ.get("GV_PARITY_OUT")
     if out:
         with open(out, "w") as f:
             json.dump(summary, f, indent=1)
+    print(json.dumps({k: v for k, v in summary.items() if k != "chunks"}))
     assert summary["mismatch_vs_construction"] == 0
     assert summary["mismatch_vs_oracle"] == 0
+    assert summary["items"] >= MILLIONS * n

@@ -263,8 +263,10 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: in
         exp = np.zeros(ntx, np.uint8)
         wl.gvw_sign(ntx, 0xC1 + seq, nk, priv.ctypes.data, pubk.ctypes.data, None, mdig.ctypes.data, 0.0,
                     pub.ctypes.data, sig.ctypes.data, dig.ctypes.data, exp.ctypes.data, threads)
+        raw[seq] = (blob, off, ln, sig)
         return [T.std_tx([T.MsgSend(addrs[i], addrs[i + 1], [(10, "foocoin")])], fee, "",
                          [(amino[i] if seq == 0 else b"", sig[i].tobytes())]) for i in range(ntx)]
+    raw = {}
     txs = block(0)
     later = [block(seq) for seq in range(1, steady_blocks + 1)]
 
@@ -341,7 +343,39 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: in
     wst = app.stats()
     app.close()
     okw = sum(1 for rc_a, r in res if rc_a == 0 and r["code"] == 0)
+    # CheckTx under tendermint's serial delivery (one caller, one tx at a time,
+    # baseapp/abci.go:165-196 behind the local client's mutex): p50 through
+    # gvh_checktx (adaptive window: a lone call does not wait) against the
+    # direct gv_verify_msgs of the same (pub, sign bytes, sig), one item.
+    app = fresh_app()
+    ns = min(ntx, 1000)
+    for i in range(ns, ns + 50):                       # warm-up (the lone path)
+        app.checktx(txs[i])
+    lat_ck, ok_ck = [], 0
+    for i in range(ns):
+        t = time.perf_counter()
+        rc_a, r = app.checktx(txs[i])
+        lat_ck.append(time.perf_counter() - t)
+        ok_ck += rc_a == 0 and r["code"] == 0
+    cst = app.stats()
+    app.close()
+    blob0, off0, ln0, sig0 = raw[0]
+    lat_dir = []
+    for i in range(ns):
+        m1 = blob0[int(off0[i]):int(off0[i]) + int(ln0[i])].tobytes()
+        t = time.perf_counter()
+        ver.verify_batch_msgs(pubk[i:i + 1], sig0[i:i + 1], [m1])
+        lat_dir.append(time.perf_counter() - t)
+    p50 = lambda a: round(float(np.percentile(np.array(a) * 1e3, 50)), 4)
+    p99 = lambda a: round(float(np.percentile(np.array(a) * 1e3, 99)), 4)
+    serial = {"txs": ns, "accepted": ok_ck, "p50_ms": p50(lat_ck), "p99_ms": p99(lat_ck),
+              "direct_gv_verify_msgs_p50_ms": p50(lat_dir), "direct_p99_ms": p99(lat_dir),
+              "overhead_p50_us": round((p50(lat_ck) - p50(lat_dir)) * 1e3, 1),
+              "windows": cst["windows"], "window_txs": cst["window_txs"],
+              "note": "one caller, sequential CheckTx of 1-signer MsgSends (new accounts: SetPubKey, pub33 path), "
+                      "Python ctypes call included on both sides"}
     return {"txs": ntx,
+            "checktx_serial": serial,
             "block_path_steady": steady,
             "block_path": {"txs_per_s": round(ntx / t_block, 1), "total_ms": round(t_block * 1e3, 2),
                            "preverify_ms": round(st["preverify_ns"] / 1e6, 2), "gpu_ms": round(st["gpu_ns"] / 1e6, 2),
