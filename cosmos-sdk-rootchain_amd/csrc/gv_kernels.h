@@ -137,6 +137,9 @@ hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t
 hipError_t gvk_keys_point(uint32_t n, const uint32_t* slots, const uint32_t* kqt, const uint32_t* kzq, uint32_t kC,
                           const uint32_t* kok, uint32_t kcount, uint8_t* out_xy, uint8_t* out_ok, hipStream_t st);
 hipError_t gvk_debug(int op, uint32_t n, const uint32_t* in, uint32_t* out, hipStream_t st);
+#if GV_STAMP
+hipError_t gvk_stamps_read(uint64_t* host, size_t n_u64);   // diagnostic builds (gv_kernels.hip GV_STAMP)
+#endif
 
 #ifdef __cplusplus
 }

@@ -844,6 +844,42 @@ GV_DEV void ecmult_finish(const gej29& acc, bool inf, const fe29& zq, const u32*
   if ((threadIdx.x & 63u) == 0 && (g >> 6) < ((n + 63u) >> 6)) bits[g >> 6] = mask;
 }
 
+// GV_STAMP (diagnostic builds only, `make ab NAME=stamp DEFS=-DGV_STAMP=1`):
+// every wave of k_ecmult records its start and end shader clock
+// (s_memtime) and 100 MHz real time (s_memrealtime) and where it ran (HW_ID,
+// XCC_ID) into a buffer of its own that nothing else reads (gv_diag_stamps,
+// tools/ecmult_stamps.py).  The product build has no stamp instruction.
+#ifndef GV_STAMP
+#define GV_STAMP 0
+#endif
+#if GV_STAMP
+#define GV_STAMP_WAVES 65536
+__device__ uint64_t g_stamps[2][GV_STAMP_WAVES * 6];
+struct wave_stamp {
+  uint64_t t0, r0;
+  GV_DEV void begin() {
+    t0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  GV_DEV void end(int which) {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    u32 hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const u32 w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if ((threadIdx.x & 63u) == 0 && w < GV_STAMP_WAVES) {
+      uint64_t* o = &g_stamps[which][(size_t)w * 6];
+      o[0] = t0; o[1] = t1; o[2] = r0; o[3] = r1; o[4] = hw | ((uint64_t)xcc << 32); o[5] = blockIdx.x;
+    }
+  }
+};
+#define GV_STAMP_BEGIN wave_stamp stamp_; stamp_.begin();
+#define GV_STAMP_END(k) stamp_.end(k);
+#else
+#define GV_STAMP_BEGIN
+#define GV_STAMP_END(k)
+#endif
+
 // GV_ECMULT_WAVES: minimum waves per SIMD the register allocator must allow
 // (0 = compiler's choice).
 #ifndef GV_ECMULT_WAVES
@@ -860,6 +896,7 @@ template <bool KEYED>
 __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult(const u32* gtab, u32 n, u32 C, const u32* digits,
                                                  const u32* qt, const u32* zq_in, const u32* flags,
                                                  const u32* in_r, uint64_t* bits, const u32* qidx, u32 zC) {
+  GV_STAMP_BEGIN
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   const u32 qi = KEYED ? qidx[g] : g;
   fe29 zq;
@@ -910,6 +947,7 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult(const u32* gtab, 
   }
 
   ecmult_finish(acc, inf, zq, flags, in_r, bits, n, C, g);
+  GV_STAMP_END(1)
 }
 
 
@@ -1175,6 +1213,13 @@ hipError_t gvk_sha256(const uint8_t* blob, const uint64_t* off, const uint32_t* 
   hipLaunchKernelGGL(gv::k_sha256, dim3(C / 256), dim3(256), 0, st, blob, off, len, n, C, e);
   return hipGetLastError();
 }
+
+#if GV_STAMP
+hipError_t gvk_stamps_read(uint64_t* host, size_t n_u64) {
+  const size_t cap = (size_t)2 * GV_STAMP_WAVES * 6;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gv::g_stamps), std::min(n_u64, cap) * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 hipError_t gvk_debug(int op, uint32_t n, const uint32_t* in, uint32_t* out, hipStream_t st) {
   hipLaunchKernelGGL(gv::k_debug, dim3((n + 255) / 256), dim3(256), 0, st, op, n, in, out);

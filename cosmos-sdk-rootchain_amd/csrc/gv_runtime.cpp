@@ -1279,6 +1279,20 @@ const char* gv_strerror(int code) {
   }
 }
 
+#if GV_STAMP
+// Diagnostic builds only (not in gpuverify.h): the k_ecmult wave stamps of
+// the last launches on dev_slot (tools/ecmult_stamps.py).
+int gv_diag_stamps(gv_ctx* ctx, int dev_slot, uint64_t* out, size_t n_u64) {
+  if (!ctx || dev_slot < 0 || dev_slot >= (int)ctx->devs.size() || !out) return GV_EINVAL;
+  Dev* d = ctx->devs[dev_slot];
+  std::lock_guard<std::mutex> lk(d->mu);
+  CK(hipSetDevice(d->id));
+  CK(hipDeviceSynchronize());
+  CK(gvk_stamps_read(out, n_u64));
+  return GV_OK;
+}
+#endif
+
 int gv_debug_op(gv_ctx* ctx, int dev_slot, int op, size_t n, const uint32_t* in, uint32_t* out) {
   if (!ctx || dev_slot < 0 || dev_slot >= (int)ctx->devs.size() || !in || !out) return GV_EINVAL;
   if (n == 0) return GV_OK;
