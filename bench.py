@@ -310,7 +310,12 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the C3 / message-path / C1 / C4 lines")
+    ap.add_argument("--inproc", action="store_true",
+                    help="the node's shape: ONE process, one gv_open over --gpus devices (0 = every visible one), "
+                         "gv_verify_digests_bits from host buffers of items x devices signatures; per-device rates")
     args = ap.parse_args(argv)
+    if args.inproc:
+        return run_inproc(args, verifier_factory, workload_fn)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -497,6 +502,53 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def run_inproc(args, verifier_factory=None, workload_fn=None):
+    """SURVEY.md §8e as the Go node runs it: one context over every device
+    (gv_open(n_dev=0) in crypto/gpuverify.Open), host buffers in, the library
+    splitting the batch into contiguous per-device slices (persistent
+    per-device workers, one shared staging pool) and gathering the bitmaps.
+    PCIe included (host buffers): this is the node-level rate, not `value` of
+    the device-resident line."""
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("--inproc runs as ONE process over all devices (do not launch it with torch.distributed.run)")
+    devs = list(range(args.gpus)) if args.gpus > 0 else None
+    ver = verifier_factory(devs) if verifier_factory else gvm.Verifier(devs)
+    nd = ver.num_devices
+    n = args.n * nd
+    t0 = time.perf_counter()
+    pub, sig, dig, exp = (workload_fn or make_digest_workload)(n, 0xC2, args.keys, args.adversarial, args.threads)
+    log(f"[inproc] workload {n} items over {nd} devices in {time.perf_counter() - t0:.1f}s")
+    for _ in range(args.warmup):
+        bits = ver.verify_batch_digests_bits(pub, sig, dig)
+    mismatches = int(np.count_nonzero(unpack_bits(bits, n) != exp))
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        ver.verify_batch_digests_bits(pub, sig, dig)
+    elapsed = time.perf_counter() - t
+    slices = ver.last_slices()
+    ver.close()
+    value = n * args.steps / elapsed
+    result = {
+        "metric": "secp256k1 verifies/sec at 1/2/4/8 MI355X; p50 latency @64-tx CheckTx batch",
+        "mode": "inproc",
+        "value": round(value, 1), "unit": "verifies/s", "n_gpus": nd, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic: OpenSSL-signed low-S ECDSA over random SHA-256 digests, 65,536 keys round-robin",
+        "config": {"workload": f"C2 x {nd}: {args.n} signatures per device in ONE host batch (pageable host "
+                               f"buffers, PCIe included)", "items_per_gpu": args.n, "global_batch": n,
+                   "parallelism": f"inproc{nd} (one gv_ctx over {nd} devices: contiguous slices, "
+                                  f"no collective, bitmaps gathered to the host)"},
+        "per_device": [{"slot": k, "items": int(c), "slice_ms": round(ms, 3),
+                        "verifies_per_s": round(c / (ms * 1e-3), 1) if ms > 0 else None}
+                       for k, (ms, c) in enumerate(slices)],
+        "parity": {"checked": n, "mismatches": mismatches, "reference": "verdicts known by construction"},
+        "host": host_cores(),
+    }
+    print(json.dumps(result), flush=True)
+    return result
 
 
 if __name__ == "__main__":

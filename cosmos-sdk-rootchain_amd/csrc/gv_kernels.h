@@ -41,6 +41,12 @@ typedef struct gvk_batch {
   uint32_t *zq, *flags, *qtab;  // shared Z of the Q table (8 rows), flags, Q table (192 rows)
   uint64_t* bits;               // C/64 words, bit (i%64) of word i/64
   hipEvent_t ev[4];             // optional: after unpack/sha, after scalar_inv, after prep, after ecmult
+  hipEvent_t ev_ecm_start;      // optional: the ladder kernel's start (after any wait on st_ecm)
+  // Pipelined calls (st_ecm set): the front kernels (unpack, s^-1, prep) run on
+  // the launch stream, the ladder on st_ecm after ecm_ready -- consecutive
+  // batches' front kernels then fill the previous ladder's tail.
+  hipStream_t st_ecm;
+  hipEvent_t ecm_ready;
   // keyed batch (kslot != NULL, pub33 unused): item i's key is arena slot kslot[i]
   const uint32_t* kslot;        // n slots (device)
   const uint32_t* kqt;          // arena Q tables, row per slot (GV_QTAB_N x GV_QENT_WORDS words)

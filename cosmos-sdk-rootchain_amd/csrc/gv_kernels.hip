@@ -1170,17 +1170,24 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
                          (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr);
   }
   if (b->ev[2]) (void)hipEventRecord(b->ev[2], st);
+  hipStream_t se = st;
+  if (b->st_ecm) {                             // the ladder on its own (high-priority) stream
+    (void)hipEventRecord(b->ecm_ready, st);
+    (void)hipStreamWaitEvent(b->st_ecm, b->ecm_ready, 0);
+    se = b->st_ecm;
+  }
+  if (b->ev_ecm_start) (void)hipEventRecord(b->ev_ecm_start, se);
   if (b->kslot && b->gtab4)
-    hipLaunchKernelGGL(gv::k_ecmult_k4, grd, blk, 0, st, b->gtab, b->gtab4, b->n, C, b->digits, b->kqt, b->kqt2,
+    hipLaunchKernelGGL(gv::k_ecmult_k4, grd, blk, 0, se, b->gtab, b->gtab4, b->n, C, b->digits, b->kqt, b->kqt2,
                        b->kzq, b->flags, b->in_r, b->bits, (const uint32_t*)b->in_pfx, b->kC);
   else if (b->kslot)
-    hipLaunchKernelGGL(gv::k_ecmult<true>, grd, blk, 0, st, b->gtab, b->n, C, b->digits, b->kqt, b->kzq,
+    hipLaunchKernelGGL(gv::k_ecmult<true>, grd, blk, 0, se, b->gtab, b->n, C, b->digits, b->kqt, b->kzq,
                        b->flags, b->in_r, b->bits, (const uint32_t*)b->in_pfx, b->kC);
   else
-    hipLaunchKernelGGL(gv::k_ecmult<false>, grd, blk, 0, st, b->gtab, b->n, C, b->digits,
+    hipLaunchKernelGGL(gv::k_ecmult<false>, grd, blk, 0, se, b->gtab, b->n, C, b->digits,
                        (const uint32_t*)b->qtab, (const uint32_t*)b->zq, b->flags, b->in_r, b->bits,
                        (const uint32_t*)nullptr, 0u);
-  if (b->ev[3]) (void)hipEventRecord(b->ev[3], st);
+  if (b->ev[3]) (void)hipEventRecord(b->ev[3], se);
   return hipGetLastError();
 }
 

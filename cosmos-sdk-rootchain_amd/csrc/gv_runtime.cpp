@@ -19,11 +19,14 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <mutex>
+#include <memory>
+#include <sched.h>
 #include <thread>
 #include <vector>
 
@@ -44,12 +47,16 @@ constexpr size_t kLaneWords = 8 + 1 + 8 + 8 + 8 + GV_DIGIT_ROWS + 8 + 1 + GV_QTA
 size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 
 // ------------------------------------------------------------ thread helpers
-// Runs fn(part) for part in [0, parts): part 0 on the caller, the rest on the
-// pool's persistent threads.
+// Runs fn(part) for part in [0, parts) on the caller plus the pool's
+// persistent threads.  ONE pool per context, shared by every device's staging
+// (a context over 8 devices stages 8 slices at once): run() may be called
+// from several threads concurrently -- each call is a job whose parts any
+// idle thread (or its own caller) claims, so the host cores are shared
+// instead of 8 devices x 8 threads oversubscribing them.
 class Pool {
  public:
   explicit Pool(int n) {
-    for (int i = 0; i < n; ++i) th_.emplace_back([this, i] { loop(i + 1); });
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
   }
   ~Pool() {
     {
@@ -63,46 +70,83 @@ class Pool {
   void run(int parts, const std::function<void(int)>& fn) {
     parts = std::max(1, std::min(parts, size()));
     if (parts == 1) { fn(0); return; }
+    auto job = std::make_shared<Job>();
+    job->fn = &fn;
+    job->parts = parts;
     {
       std::lock_guard<std::mutex> lk(m_);
-      fn_ = &fn;
-      parts_ = parts;
-      pending_ = parts - 1;
-      ++gen_;
+      jobs_.push_back(job);
     }
     cv_.notify_all();
-    fn(0);
+    for (int p; (p = job->next.fetch_add(1)) < parts;) {   // the caller works too
+      fn(p);
+      finish(*job);
+    }
     std::unique_lock<std::mutex> lk(m_);
-    done_cv_.wait(lk, [this] { return pending_ == 0; });
-    fn_ = nullptr;
+    done_cv_.wait(lk, [&] { return job->done == parts; });
+    drop(job.get());
   }
 
  private:
-  void loop(int id) {
-    uint64_t seen = 0;
+  struct Job {
+    const std::function<void(int)>* fn = nullptr;
+    int parts = 0;
+    std::atomic<int> next{0};
+    int done = 0;                                  // guarded by m_
+  };
+  void finish(Job& j) {
+    std::lock_guard<std::mutex> lk(m_);
+    if (++j.done == j.parts) done_cv_.notify_all();
+  }
+  void drop(Job* j) {                              // m_ held
+    for (size_t i = 0; i < jobs_.size(); ++i)
+      if (jobs_[i].get() == j) { jobs_.erase(jobs_.begin() + i); return; }
+  }
+  void loop() {
     for (;;) {
-      const std::function<void(int)>* fn;
+      std::shared_ptr<Job> job;
+      int p = 0;
       {
         std::unique_lock<std::mutex> lk(m_);
-        cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
-        if (quit_) return;
-        seen = gen_;
-        if (id >= parts_) continue;
-        fn = fn_;
+        for (;;) {
+          if (quit_) return;
+          while (!jobs_.empty()) {                 // a job with parts left to claim
+            p = jobs_.front()->next.fetch_add(1);
+            if (p < jobs_.front()->parts) { job = jobs_.front(); break; }
+            jobs_.erase(jobs_.begin());            // fully claimed: its caller finishes it
+          }
+          if (job) break;
+          cv_.wait(lk);
+        }
       }
-      (*fn)(id);
-      std::lock_guard<std::mutex> lk(m_);
-      if (--pending_ == 0) done_cv_.notify_all();
+      (*job->fn)(p);
+      finish(*job);
     }
   }
   std::vector<std::thread> th_;
   std::mutex m_;
   std::condition_variable cv_, done_cv_;
-  const std::function<void(int)>* fn_ = nullptr;
-  int parts_ = 0, pending_ = 0;
-  uint64_t gen_ = 0;
+  std::vector<std::shared_ptr<Job>> jobs_;
   bool quit_ = false;
 };
+
+// CPUs this process may run on: the affinity mask, capped by the cgroup v2
+// CPU quota when one is set (a GPU box shows 256 CPUs under a 16-CPU quota).
+int host_cpus() {
+  int n = (int)std::thread::hardware_concurrency();
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char quota[32] = {0};
+    long long period = 0;
+    if (fscanf(f, "%31s %lld", quota, &period) == 2 && strcmp(quota, "max") != 0 && period > 0) {
+      const long long q = atoll(quota);
+      if (q > 0) n = std::min<long long>(n, std::max<long long>(1, (q + period - 1) / period));
+    }
+    fclose(f);
+  }
+  return std::max(1, n);
+}
 
 // memcpy split over the pool (large copies only: one core streams ~10 GB/s)
 void par_copy(Pool* pool, void* dst, const void* src, size_t bytes) {
@@ -208,6 +252,7 @@ struct Set {
   hipEvent_t last = nullptr;                      // end of the last work using this set
   hipStream_t last_st = nullptr;
   hipEvent_t done = nullptr;                      // host path: chunk finished (bits on host)
+  hipEvent_t ecm_ready = nullptr;                 // pipelined device calls: front kernels done
   // pinned host staging
   uint8_t* h_in = nullptr;
   size_t h_in_cap = 0;
@@ -247,9 +292,9 @@ struct Dev {
   uint32_t* glat = nullptr;                       // group tables of G / lambda G (k_gen_glat)
   uint32_t* gtab4 = nullptr;                      // k_ecmult_k4's tables of 2^35 G, 2^70 G, 2^100 G (+ lambda)
   size_t kcap = 0;
-  // ring of per-launch stage events for gv_stage_stats: start + 4 stage ends
+  // ring of per-launch stage events for gv_stage_stats
   static constexpr int kRing = 256;
-  hipEvent_t ring[kRing][5] = {};
+  hipEvent_t ring[kRing][6] = {};                // start, after unpack / s^-1 / prep, ladder start, ladder end
   int ring_next = 0, ring_count = 0, last = -1;
   // ed25519: the resident comb table and one scratch set
   uint32_t* edtab = nullptr;
@@ -270,8 +315,18 @@ struct Dev {
     hipStream_t last_st = nullptr;
   } ed;
   std::mutex mu;
-  Pool* pool = nullptr;                           // staging memcpy threads
+  Pool* pool = nullptr;                           // staging memcpy threads: the context's shared pool
   Worker* worker = nullptr;                       // slice runner (devices 1..n-1 of a context)
+  // pipelined device-resident calls on the context stream (gv_dev_verify_*,
+  // stream NULL): the front kernels of call k+1 run under call k's ladder
+  hipStream_t lo_st[2] = {nullptr, nullptr};
+  hipStream_t hi_st = nullptr;
+  hipEvent_t hi_done = nullptr;                   // the last ladder enqueued on hi_st
+  hipEvent_t plain_done = nullptr;                // the last non-pipelined call on the context stream
+  bool hi_used = false, plain_used = false;
+  int flip = 0;
+  double last_slice_ms = 0;                       // host-buffer calls: this device's slice, wall time
+  size_t last_slice_n = 0;
 };
 
 int ensure_cap(Set* s, size_t C) {
@@ -410,13 +465,13 @@ int ed_launch(bool timed, Dev* d, size_t n, const uint8_t* pub, const uint8_t* s
   hipEvent_t* rs = nullptr;
   if (timed) {                                    // stages: (none) x 3 | the ed25519 kernel
     rs = d->ring[d->ring_next];
-    for (int i = 0; i < 5; ++i)
+    for (int i = 0; i < 6; ++i)
       if (!rs[i]) CK(hipEventCreate(&rs[i]));
-    for (int i = 0; i < 4; ++i) CK(hipEventRecord(rs[i], st));
+    for (int i = 0; i < 5; ++i) CK(hipEventRecord(rs[i], st));
   }
   CK(gvk_ed_verify(&b, st));
   if (rs) {
-    CK(hipEventRecord(rs[4], st));
+    CK(hipEventRecord(rs[5], st));
     d->last = d->ring_next;
     d->ring_next = (d->ring_next + 1) % Dev::kRing;
     d->ring_count = std::min(d->ring_count + 1, Dev::kRing);
@@ -442,13 +497,16 @@ struct gv_ctx {
   size_t lat_sl_max_keyed = 1536;
   size_t pipe_chunk = 131072;   // host path: first chunk of the two-set copy/compute pipeline (0 = max_batch)
   int pipe_growth = 4;          // host path: each later chunk at most this times the one before
-  int stage_threads = 8;        // host path: staging memcpy threads per device
+  int stage_threads = 8;        // host path: staging threads of the context's shared pool (gv_open: half
+                                // the process's CPUs -- affinity capped by the cgroup quota -- at most 8)
+  Pool* pool = nullptr;
   bool time_kernels = false;
   bool fault_inject = false;
   bool lat_zero_copy = true;    // host-buffer batches on the sliced kernels read the pinned staging buffer and write
                                 // verdict bytes to pinned memory directly: no H2D, memset or D2H (GV_LAT_ZC=0: A/B)
   bool lat_sliced = true;       // small batches on k_verify_lat_sl / k_verify_lat16_sl (GV_LAT_SLICED=0: the one-lane-field kernels, A/B)
   bool keyed_k4 = true;         // keyed batches on k_ecmult_k4 (GV_KEYED_K4=0: the 125-doubling ladder, A/B)
+  bool pipeline_dev = true;     // pipelined device-resident calls on the context stream (dev_run; GV_PIPELINE=0: A/B)
   size_t keys = 0;              // key-arena slots in use (same on every device)
   std::atomic<uint64_t> keys_gen{0};  // gv_keys_reset calls
   std::mutex keys_mu;
@@ -458,9 +516,11 @@ namespace {
 
 // Launch the pipeline for n items whose inputs already sit on the device, on
 // set s's scratch, stream st.  The caller holds d->mu.
+// st_ecm (pipelined device-resident calls): the ladder runs there, after the
+// front kernels on st; the set's scratch is released on st_ecm.
 int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint8_t* sig, const uint8_t* dig,
            const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint64_t* bits_out,
-           hipStream_t st, const uint32_t* kslot = nullptr, uint8_t* out8 = nullptr) {
+           hipStream_t st, const uint32_t* kslot = nullptr, uint8_t* out8 = nullptr, hipStream_t st_ecm = nullptr) {
   if (n == 0 || n > kMaxItems) return GV_EINVAL;
   const size_t C = round_up(n, 256);
   int rc = ensure_cap(s, C);
@@ -489,10 +549,17 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
   hipEvent_t* rs = nullptr;
   if (ctx->time_kernels) {
     rs = d->ring[d->ring_next];
-    for (int i = 0; i < 5; ++i)
+    for (int i = 0; i < 6; ++i)
       if (!rs[i]) CK(hipEventCreate(&rs[i]));
     CK(hipEventRecord(rs[0], st));
-    for (int i = 0; i < 4; ++i) b.ev[i] = rs[i + 1];
+    for (int i = 0; i < 3; ++i) b.ev[i] = rs[i + 1];
+    b.ev_ecm_start = rs[4];
+    b.ev[3] = rs[5];
+  }
+  const bool pipelined = st_ecm != nullptr && n > (kslot ? ctx->lat_max_keyed : ctx->lat_max);
+  if (pipelined) {
+    b.st_ecm = st_ecm;
+    b.ecm_ready = s->ecm_ready;
   }
   if (n <= (kslot ? ctx->lat_max_keyed : ctx->lat_max)) {
     // small batch: one fused kernel, several lanes per signature (gv_lat.hip)
@@ -519,10 +586,11 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     } else {
       CK(gvk_verify_lat(&lb, st));
     }
-    if (rs) {                                   // stages: SHA | (none) | (none) | fused kernel
+    if (rs) {                                   // stages: SHA | fused kernel | (none) | (none)
       CK(hipEventRecord(rs[2], st));
       CK(hipEventRecord(rs[3], st));
       CK(hipEventRecord(rs[4], st));
+      CK(hipEventRecord(rs[5], st));
     }
   } else {
     CK(gvk_verify(&b, st));
@@ -532,7 +600,44 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     d->ring_next = (d->ring_next + 1) % Dev::kRing;
     d->ring_count = std::min(d->ring_count + 1, Dev::kRing);
   }
-  return set_release(s, st);
+  return set_release(s, pipelined ? st_ecm : st);
+}
+
+// Device-resident calls.  A caller stream: everything on it, in order.  The
+// context stream (stream NULL): batches past the small-batch bound are
+// PIPELINED -- consecutive calls alternate the two scratch sets, their front
+// kernels (unpack, s^-1, prep) go to the set's low-priority stream and every
+// ladder to ONE high-priority stream, so call k+1's front kernels fill call
+// k's ladder tail (the last ~1 ms of a 7 ms ladder runs below full occupancy)
+// while the ladders stay in call order (their d_bits writes too).  Small
+// batches and the other calls on the context stream are ordered after every
+// pipelined ladder (hi_done) and the next ladder after them (plain_done).
+void order_after_pipeline(Dev* d, hipStream_t st) {
+  if (d->hi_used) (void)hipStreamWaitEvent(st, d->hi_done, 0);
+}
+template <class F>
+int dev_run(gv_ctx* ctx, Dev* d, void* stream, size_t n, bool keyed, F&& fn) {
+  if (stream) {
+    order_after_pipeline(d, (hipStream_t)stream);
+    return fn(&d->set[0], (hipStream_t)stream, (hipStream_t) nullptr);
+  }
+  if (!ctx->pipeline_dev || n <= (keyed ? ctx->lat_max_keyed : ctx->lat_max)) {
+    hipStream_t st = d->set[0].st;
+    order_after_pipeline(d, st);
+    const int rc = fn(&d->set[0], st, (hipStream_t) nullptr);
+    if (rc) return rc;
+    CK(hipEventRecord(d->plain_done, st));
+    d->plain_used = true;
+    return GV_OK;
+  }
+  if (d->plain_used) CK(hipStreamWaitEvent(d->hi_st, d->plain_done, 0));
+  const int j = d->flip;
+  d->flip ^= 1;
+  const int rc = fn(&d->set[j], d->lo_st[j], d->hi_st);
+  if (rc) return rc;
+  CK(hipEventRecord(d->hi_done, d->hi_st));
+  d->hi_used = true;
+  return GV_OK;
 }
 
 struct HostBatch {
@@ -663,6 +768,16 @@ int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const HostBatch& hb) {
   std::lock_guard<std::mutex> lk(d->mu);
   CK(hipSetDevice(d->id));
   const size_t n = hi - lo;
+  const auto t_begin = std::chrono::steady_clock::now();
+  struct SliceTimer {
+    Dev* d;
+    size_t n;
+    std::chrono::steady_clock::time_point t0;
+    ~SliceTimer() {
+      d->last_slice_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      d->last_slice_n = n;
+    }
+  } timer{d, n, t_begin};
   // Chunk sizes.  Pipelined (past lat_max): a ramp -- pipe_chunk first, each
   // later chunk at most pipe_growth times the one before -- so the first
   // kernels start after a short staging copy and every later chunk is staged
@@ -826,6 +941,7 @@ void free_set(Set& s) {
   if (s.h_out8) (void)hipHostFree(s.h_out8);
   if (s.last) (void)hipEventDestroy(s.last);
   if (s.done) (void)hipEventDestroy(s.done);
+  if (s.ecm_ready) (void)hipEventDestroy(s.ecm_ready);
   if (s.st) (void)hipStreamDestroy(s.st);
 }
 
@@ -862,17 +978,31 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* k4 = getenv("GV_KEYED_K4")) ctx->keyed_k4 = strcmp(k4, "0") != 0;
   if (const char* ls = getenv("GV_LAT_SLICED")) ctx->lat_sliced = strcmp(ls, "0") != 0;
   if (const char* zc = getenv("GV_LAT_ZC")) ctx->lat_zero_copy = strcmp(zc, "0") != 0;
+  if (const char* pl = getenv("GV_PIPELINE")) ctx->pipeline_dev = strcmp(pl, "0") != 0;
+  ctx->stage_threads = std::max(1, std::min(8, host_cpus() / 2));   // half the quota: the callers, HIP's
+                                                                    // own threads and the pool share it
+  ctx->pool = new Pool(ctx->stage_threads - 1);
   for (size_t k = 0; k < ids.size(); ++k) {
     Dev* d = new Dev();
     d->id = ids[k];
     ctx->devs.push_back(d);
-    d->pool = new Pool(ctx->stage_threads - 1);
+    d->pool = ctx->pool;
     if (k > 0) d->worker = new Worker();
     bool ok = hipSetDevice(d->id) == hipSuccess;
     for (Set& s : d->set)
       ok = ok && hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) == hipSuccess &&
            hipEventCreateWithFlags(&s.last, hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
+           hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&s.ecm_ready, hipEventDisableTiming) == hipSuccess;
+    // pipelined device-resident calls: front kernels on two low-priority
+    // streams (alternating sets), every ladder on one high-priority stream
+    int lo_prio = 0, hi_prio = 0;
+    ok = ok && hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) == hipSuccess;
+    for (int j = 0; j < 2; ++j)
+      ok = ok && hipStreamCreateWithPriority(&d->lo_st[j], hipStreamNonBlocking, lo_prio) == hipSuccess;
+    ok = ok && hipStreamCreateWithPriority(&d->hi_st, hipStreamNonBlocking, hi_prio) == hipSuccess &&
+         hipEventCreateWithFlags(&d->hi_done, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&d->plain_done, hipEventDisableTiming) == hipSuccess;
     ok = ok && hipMalloc(&d->gtab, (size_t)2 * GV_GTAB_N * 16 * 4) == hipSuccess &&
          gvk_gen_gtable(d->gtab, d->set[0].st) == hipSuccess && hipStreamSynchronize(d->set[0].st) == hipSuccess;
     ok = ok && hipMalloc(&d->glat, (size_t)GV_GLAT_WORDS * 4) == hipSuccess &&
@@ -908,9 +1038,13 @@ void gv_close(gv_ctx* ctx) {
     if (d->ed.last) (void)hipEventDestroy(d->ed.last);
     for (auto& rs : d->ring)
       for (auto e : rs) if (e) (void)hipEventDestroy(e);
-    delete d->pool;
+    for (hipStream_t t : {d->lo_st[0], d->lo_st[1], d->hi_st})
+      if (t) { (void)hipStreamSynchronize(t); (void)hipStreamDestroy(t); }
+    if (d->hi_done) (void)hipEventDestroy(d->hi_done);
+    if (d->plain_done) (void)hipEventDestroy(d->plain_done);
     delete d;
   }
+  delete ctx->pool;
   delete ctx;
 }
 
@@ -961,9 +1095,10 @@ int gv_dev_verify_digests(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub
   if (!d_dig32 || ((uintptr_t)d_dig32 & 3)) return GV_EINVAL;
   std::lock_guard<std::mutex> lk(d->mu);
   CK(hipSetDevice(d->id));
-  hipStream_t st = stream ? (hipStream_t)stream : d->set[0].st;
-  return launch(ctx, d, &d->set[0], n, (const uint8_t*)d_pub33, (const uint8_t*)d_sig64, (const uint8_t*)d_dig32,
-                nullptr, nullptr, nullptr, (uint64_t*)d_bits, st);
+  return dev_run(ctx, d, stream, n, false, [&](Set* s, hipStream_t st, hipStream_t se) {
+    return launch(ctx, d, s, n, (const uint8_t*)d_pub33, (const uint8_t*)d_sig64, (const uint8_t*)d_dig32, nullptr,
+                  nullptr, nullptr, (uint64_t*)d_bits, st, nullptr, nullptr, se);
+  });
 }
 
 int gv_dev_verify_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub33, const void* d_sig64,
@@ -975,10 +1110,11 @@ int gv_dev_verify_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub33,
   if (!d_msg_blob || !d_msg_off || !d_msg_len) return GV_EINVAL;
   std::lock_guard<std::mutex> lk(d->mu);
   CK(hipSetDevice(d->id));
-  hipStream_t st = stream ? (hipStream_t)stream : d->set[0].st;
-  return launch(ctx, d, &d->set[0], n, (const uint8_t*)d_pub33, (const uint8_t*)d_sig64, nullptr,
-                (const uint8_t*)d_msg_blob, (const uint64_t*)d_msg_off, (const uint32_t*)d_msg_len,
-                (uint64_t*)d_bits, st);
+  return dev_run(ctx, d, stream, n, false, [&](Set* s, hipStream_t st, hipStream_t se) {
+    return launch(ctx, d, s, n, (const uint8_t*)d_pub33, (const uint8_t*)d_sig64, nullptr,
+                  (const uint8_t*)d_msg_blob, (const uint64_t*)d_msg_off, (const uint32_t*)d_msg_len,
+                  (uint64_t*)d_bits, st, nullptr, nullptr, se);
+  });
 }
 
 // ---- ed25519
@@ -998,6 +1134,7 @@ int gv_dev_verify_ed25519_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* 
   std::lock_guard<std::mutex> lk(d->mu);
   CK(hipSetDevice(d->id));
   hipStream_t st = stream ? (hipStream_t)stream : d->set[0].st;
+  order_after_pipeline(d, st);
   return ed_launch(ctx->time_kernels, d, n, (const uint8_t*)d_pub32, (const uint8_t*)d_sig64, (const uint8_t*)d_msg_blob,
                    (const uint64_t*)d_msg_off, (const uint32_t*)d_msg_len, (uint64_t*)d_bits, st);
 }
@@ -1015,6 +1152,7 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
     CK(hipSetDevice(d->id));
     Set* s = &d->set[0];
     hipStream_t st = s->st;
+    CK(hipStreamSynchronize(d->hi_st));         // no pipelined ladder reads an arena being grown
     int rc = ensure_keys(d, base + n, base, st);
     if (rc) return rc;
     if (!d->gtab4 && ctx->keyed_k4) {          // first keys on this device: the k4 ladder's G tables
@@ -1055,6 +1193,18 @@ int gv_keys_reset(gv_ctx* ctx) {
 }
 
 size_t gv_keys_count(const gv_ctx* ctx) { return ctx ? ctx->keys : 0; }
+
+int gv_last_slices(gv_ctx* ctx, double* ms_out, size_t* n_out, int cap) {
+  if (!ctx || cap < 0 || (cap > 0 && (!ms_out || !n_out))) return GV_EINVAL;
+  const int m = std::min<int>(cap, (int)ctx->devs.size());
+  for (int k = 0; k < m; ++k) {
+    Dev* d = ctx->devs[k];
+    std::lock_guard<std::mutex> lk(d->mu);
+    ms_out[k] = d->last_slice_ms;
+    n_out[k] = d->last_slice_n;
+  }
+  return m;
+}
 uint64_t gv_keys_generation(const gv_ctx* ctx) { return ctx ? ctx->keys_gen.load() : 0; }
 
 int gv_keys_point(gv_ctx* ctx, size_t n, const uint32_t* slots, uint8_t* out_xy64, uint8_t* out_ok) {
@@ -1102,9 +1252,10 @@ int gv_dev_verify_digests_keyed(gv_ctx* ctx, int dev_slot, size_t n, const void*
   if (!d_dig32 || ((uintptr_t)d_dig32 & 3)) return GV_EINVAL;
   std::lock_guard<std::mutex> lk(d->mu);
   CK(hipSetDevice(d->id));
-  hipStream_t st = stream ? (hipStream_t)stream : d->set[0].st;
-  return launch(ctx, d, &d->set[0], n, nullptr, (const uint8_t*)d_sig64, (const uint8_t*)d_dig32, nullptr, nullptr,
-                nullptr, (uint64_t*)d_bits, st, (const uint32_t*)d_slot);
+  return dev_run(ctx, d, stream, n, true, [&](Set* s, hipStream_t st, hipStream_t se) {
+    return launch(ctx, d, s, n, nullptr, (const uint8_t*)d_sig64, (const uint8_t*)d_dig32, nullptr, nullptr, nullptr,
+                  (uint64_t*)d_bits, st, (const uint32_t*)d_slot, nullptr, se);
+  });
 }
 
 int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
@@ -1134,12 +1285,12 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
     ctx->pipe_growth = (int)val;
   } else if (!strcmp(key, "stage_threads")) {
     if (val < 1 || val > 64) return GV_EINVAL;
+    std::vector<std::unique_lock<std::mutex>> held;   // no device stages while the pool is replaced
+    for (Dev* d : ctx->devs) held.emplace_back(d->mu);
     ctx->stage_threads = (int)val;
-    for (Dev* d : ctx->devs) {                    // replace each device's staging pool
-      std::lock_guard<std::mutex> lk(d->mu);
-      delete d->pool;
-      d->pool = new Pool((int)val - 1);
-    }
+    delete ctx->pool;
+    ctx->pool = new Pool((int)val - 1);
+    for (Dev* d : ctx->devs) d->pool = ctx->pool;
   } else if (!strcmp(key, "time_kernels")) {
     ctx->time_kernels = val != 0;
   } else if (!strcmp(key, "fault_inject")) {
@@ -1150,9 +1301,11 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   return GV_OK;
 }
 
+// [unpack/sha, s^-1, prep, ladder] ms of one launch (ladder: its own start to end)
 static int stage_ms(hipEvent_t* e, float ms[4]) {
-  CK(hipEventSynchronize(e[4]));
-  for (int i = 0; i < 4; ++i) CK(hipEventElapsedTime(&ms[i], e[i], e[i + 1]));
+  CK(hipEventSynchronize(e[5]));
+  for (int i = 0; i < 3; ++i) CK(hipEventElapsedTime(&ms[i], e[i], e[i + 1]));
+  CK(hipEventElapsedTime(&ms[3], e[4], e[5]));
   return GV_OK;
 }
 
@@ -1229,6 +1382,8 @@ int gv_dev_copy(gv_ctx* ctx, int dev_slot, void* dst, const void* src, size_t by
   }
   Dev* d = ctx->devs[dev_slot];
   CK(hipSetDevice(d->id));
+  for (hipStream_t t : {d->lo_st[0], d->lo_st[1], d->hi_st})   // after every pipelined call (synchronous copy)
+    CK(hipStreamSynchronize(t));
   hipStream_t st = d->set[0].st;
   CK(hipMemcpyAsync(dst, src, bytes, k, st));
   CK(hipStreamSynchronize(st));
@@ -1264,6 +1419,7 @@ int gv_dev_sync(gv_ctx* ctx, int dev_slot) {
   Dev* d = ctx->devs[dev_slot];
   CK(hipSetDevice(d->id));
   for (Set& s : d->set) CK(hipStreamSynchronize(s.st));
+  for (hipStream_t t : {d->lo_st[0], d->lo_st[1], d->hi_st}) CK(hipStreamSynchronize(t));
   return GV_OK;
 }
 

@@ -42,7 +42,7 @@ EXPORTED_SYMBOLS = (
     "gv_dev_copy", "gv_dev_sync", "gv_stage_stats", "gv_keys_load", "gv_keys_reset", "gv_keys_count", "gv_keys_generation",
     "gv_verify_digests_keyed", "gv_verify_msgs_keyed", "gv_dev_verify_digests_keyed", "gv_stage_stats4",
     "gv_keys_point", "gv_dev_stream_create", "gv_dev_stream_sync", "gv_dev_stream_destroy",
-    "gv_verify_ed25519_msgs", "gv_dev_verify_ed25519_msgs",
+    "gv_verify_ed25519_msgs", "gv_dev_verify_ed25519_msgs", "gv_last_slices",
 )
 
 
@@ -118,6 +118,8 @@ def load(path: str = LIB_PATH):
     L.gv_stage_stats.restype = i32
     L.gv_stage_stats4.argtypes = [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double)]
     L.gv_stage_stats4.restype = i32
+    L.gv_last_slices.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_size_t), i32]
+    L.gv_last_slices.restype = i32
     L.gv_keys_load.argtypes = [vp, sz, vp, vp]
     L.gv_keys_load.restype = i32
     L.gv_keys_reset.argtypes = [vp]
@@ -380,6 +382,16 @@ class Verifier:
         ms = (ctypes.c_double * 4)()
         _check(self._L.gv_stage_stats4(self._ctx, slot, ctypes.byref(c), ms), "gv_stage_stats4")
         return c.value, list(ms)
+
+    def last_slices(self):
+        """[(ms, items)] per device slot: each device's slice of the last host-buffer call."""
+        nd = self.num_devices
+        ms = (ctypes.c_double * max(1, nd))()
+        nn = (ctypes.c_size_t * max(1, nd))()
+        m = self._L.gv_last_slices(self._ctx, ms, nn, nd)
+        if m < 0:
+            raise GpuVerifyError(m, "gv_last_slices")
+        return [(ms[k], nn[k]) for k in range(m)]
 
     def debug_op(self, op: int, words: np.ndarray, slot: int = 0) -> np.ndarray:
         words = np.ascontiguousarray(words, dtype=np.uint32)

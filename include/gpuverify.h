@@ -223,6 +223,10 @@ int gv_stage_stats(gv_ctx* ctx, int dev_slot, int* count, double* unpack_ms, dou
 /* Same, per stage: ms[0] unpack (+ SHA-256 on the message path), ms[1]
  * k_scalar_inv, ms[2] k_prep, ms[3] k_ecmult (fused latency kernel: ms[3]). */
 int gv_stage_stats4(gv_ctx* ctx, int dev_slot, int* count, double ms[4]);
+/* Host-buffer calls on a multi-device context: per device slot, the wall time
+ * (ms) and item count of that device's slice in the last gv_verify_* call
+ * (bench.py --inproc: per-device rates).  Returns the number of slots written. */
+int gv_last_slices(gv_ctx* ctx, double* ms_out, size_t* n_out, int cap);
 
 const char* gv_strerror(int code);
 

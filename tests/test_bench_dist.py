@@ -8,6 +8,8 @@ import socket
 import subprocess
 import sys
 
+import numpy as np
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -42,3 +44,45 @@ def test_two_rank_bench_aggregation():
     assert par["adversarial_checked"] == 2 * n and par["adversarial_mismatches"] == 0
     assert 0.2 * 2 * n < par["adversarial_rejects_expected"] < 0.5 * 2 * n
     assert set(out["roofline"]["kernels"]) == {"k_scalar_inv", "k_prep", "k_ecmult"}
+
+
+class _FakeMultiDevice:
+    """gpuverify.Verifier's host-buffer calls over `nd` fake devices: the batch
+    is cut into contiguous slices like gv_runtime's run_host."""
+
+    def __init__(self, devs):
+        self.nd = len(devs) if devs else 3
+        self._slices = []
+
+    @property
+    def num_devices(self):
+        return self.nd
+
+    def verify_batch_digests_bits(self, pub, sig, dig):
+        n = len(pub)
+        ok = ((pub[:, 0] == 2) & ((dig[:, 31] & 1) == 0)).astype(np.uint8)
+        per = -(-n // self.nd)
+        self._slices = [(0.5, min(n, (k + 1) * per) - min(n, k * per)) for k in range(self.nd)]
+        packed = np.packbits(ok, bitorder="little").tobytes().ljust(((n + 63) // 64) * 8, b"\0")
+        return np.frombuffer(packed, np.uint64)
+
+    def last_slices(self):
+        return self._slices
+
+    def close(self):
+        pass
+
+
+def test_inproc_mode_is_one_process_over_all_devices():
+    """bench.py --inproc: one context over every device (the Go node's shape),
+    host buffers in, per-device slice rates out; refuses a torchrun launch."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import bench
+    import dist_bench_worker as W
+    n = 2048
+    res = bench.main(["--inproc", "--gpus", "0", "--items", str(n), "--steps", "2", "--warmup", "1"],
+                     verifier_factory=_FakeMultiDevice, workload_fn=W.workload)
+    assert res["mode"] == "inproc" and res["n_gpus"] == 3 and res["config"]["global_batch"] == 3 * n
+    assert res["parity"]["mismatches"] == 0
+    assert [d["items"] for d in res["per_device"]] == [n, n, n]
+    assert all(d["verifies_per_s"] == n / 0.5e-3 for d in res["per_device"])
