@@ -181,6 +181,66 @@ __global__ __launch_bounds__(256) void k_unpack(const uint8_t* pub33, const uint
   }
 }
 
+// ------------------------------------------------------------ in-batch keys
+// A batch that repeats keys (a block with repeat signers; C2's 65,536 keys
+// round-robin over 1M signatures) parses each distinct key once: the keys are
+// grouped by an open-addressing hash table over the unpacked (prefix, x) rows,
+// each distinct key gets an id, its tables are built once (k_keys_build into a
+// per-batch arena) and the items run the keyed pipeline (k_prep<true>,
+// k_ecmult_k4) with the id as their slot.  ParsePubKey is a pure function of
+// the 33 bytes, so the verdicts are the per-item ones (SURVEY.md §8f-2 within
+// one batch).
+GV_DEV u32 key_hash(const u32 w[8], u32 pre) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ pre;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    h ^= w[i];
+    h *= 0xFF51AFD7ED558CCDull;
+    h ^= h >> 29;
+  }
+  return (u32)(h ^ (h >> 32));
+}
+GV_DEV bool key_equal(const u32* x, const u32* pfx, u32 C, u32 a, u32 b) {
+  bool eq = pfx[a] == pfx[b];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) eq &= x[(size_t)i * C + a] == x[(size_t)i * C + b];
+  return eq;
+}
+// rep[g] = the first-inserted item with g's key (table: tmask + 1 slots of
+// 0xFFFFFFFF, at least twice the items).
+__global__ __launch_bounds__(256) void k_dedupe(u32 n, u32 C, const u32* x, const u32* pfx, u32* table, u32 tmask,
+                                                 u32* rep) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  u32 w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = x[(size_t)i * C + g];
+  for (u32 sl = key_hash(w, pfx[g]) & tmask;; sl = (sl + 1) & tmask) {
+    const u32 cur = atomicCAS(&table[sl], 0xFFFFFFFFu, g);
+    if (cur == 0xFFFFFFFFu) { rep[g] = g; return; }
+    if (key_equal(x, pfx, C, cur, g)) { rep[g] = cur; return; }
+  }
+}
+// Each representative takes the next key id; its (prefix, x) goes to key row
+// id (stride CU) when id < capU (a batch with more distinct keys takes the
+// pub33 pipeline and never reads these rows).
+__global__ __launch_bounds__(256) void k_dedupe_assign(u32 n, u32 C, const u32* x, const u32* pfx, const u32* rep,
+                                                        u32* uid, u32* count, u32 capU, u32 CU, u32* kx, u32* kpfx) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n || rep[g] != g) return;
+  const u32 u = atomicAdd(count, 1u);
+  uid[g] = u;
+  if (u < capU) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kx[(size_t)i * CU + u] = x[(size_t)i * C + g];
+    kpfx[u] = pfx[g];
+  }
+}
+__global__ __launch_bounds__(256) void k_dedupe_map(u32 n, const u32* rep, const u32* uid, u32* kslot) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n) kslot[g] = uid[rep[g]];
+}
+
 // ------------------------------------------------------------------ k_sha256
 __global__ __launch_bounds__(256) void k_sha256(const uint8_t* blob, const uint64_t* off,
                                                  const u32* len, u32 n, u32 C, u32* e) {
@@ -1146,8 +1206,9 @@ hipError_t gvk_gen_gtable4(uint32_t* gtab4, uint32_t* base_scratch, hipStream_t 
 hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   const uint32_t C = b->C;
   const dim3 blk(256), grd(C / 256);
-  hipLaunchKernelGGL(gv::k_unpack, grd, blk, 0, st, b->pub33, b->sig64, b->dig32, b->n, C,
-                     b->in_x, b->in_pfx, b->in_r, b->in_s, b->in_e);
+  if (!b->unpacked)
+    hipLaunchKernelGGL(gv::k_unpack, grd, blk, 0, st, b->pub33, b->sig64, b->dig32, b->n, C,
+                       b->in_x, b->in_pfx, b->in_r, b->in_s, b->in_e);
   if (b->msg_blob)
     hipLaunchKernelGGL(gv::k_sha256, grd, blk, 0, st, b->msg_blob, b->msg_off, b->msg_len, b->n, C,
                        b->in_e);
@@ -1218,6 +1279,34 @@ hipError_t gvk_keys_point(uint32_t n, const uint32_t* slots, const uint32_t* kqt
 hipError_t gvk_sha256(const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint32_t n, uint32_t C,
                       uint32_t* e, hipStream_t st) {
   hipLaunchKernelGGL(gv::k_sha256, dim3(C / 256), dim3(256), 0, st, blob, off, len, n, C, e);
+  return hipGetLastError();
+}
+
+hipError_t gvk_unpack(const uint8_t* pub33, const uint8_t* sig64, const uint8_t* dig32, uint32_t n, uint32_t C,
+                      uint32_t* x, uint32_t* pfx, uint32_t* r, uint32_t* s, uint32_t* e, hipStream_t st) {
+  hipLaunchKernelGGL(gv::k_unpack, dim3(C / 256), dim3(256), 0, st, pub33, sig64, dig32, n, C, x, pfx, r, s, e);
+  return hipGetLastError();
+}
+
+hipError_t gvk_dedupe(uint32_t n, uint32_t C, const uint32_t* x, const uint32_t* pfx, uint32_t* table, uint32_t tslots,
+                      uint32_t* rep, uint32_t* uid, uint32_t* count, uint32_t* kslot, uint32_t capU, uint32_t CU,
+                      uint32_t* kx, uint32_t* kpfx, hipStream_t st) {
+  const dim3 blk(256), grd((n + 255) / 256);
+  if (hipMemsetAsync(table, 0xFF, (size_t)tslots * 4, st) != hipSuccess ||
+      hipMemsetAsync(count, 0, 4, st) != hipSuccess)
+    return hipErrorUnknown;
+  hipLaunchKernelGGL(gv::k_dedupe, grd, blk, 0, st, n, C, x, pfx, table, tslots - 1, rep);
+  hipLaunchKernelGGL(gv::k_dedupe_assign, grd, blk, 0, st, n, C, x, pfx, (const uint32_t*)rep, uid, count, capU, CU,
+                     kx, kpfx);
+  hipLaunchKernelGGL(gv::k_dedupe_map, grd, blk, 0, st, n, (const uint32_t*)rep, (const uint32_t*)uid, kslot);
+  return hipGetLastError();
+}
+
+hipError_t gvk_keys_build_rows(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx, uint32_t* qr,
+                               uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2,
+                               uint32_t* kzq2, hipStream_t st) {
+  hipLaunchKernelGGL(gv::k_keys_build, dim3(C / 256), dim3(256), 0, st, n, C, in_x, in_pfx, 0u, kqt, kzq, kC, kok, qr,
+                     kqt2, kzq2);
   return hipGetLastError();
 }
 

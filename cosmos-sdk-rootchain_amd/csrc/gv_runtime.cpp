@@ -253,6 +253,11 @@ struct Set {
   hipStream_t last_st = nullptr;
   hipEvent_t done = nullptr;                      // host path: chunk finished (bits on host)
   hipEvent_t ecm_ready = nullptr;                 // pipelined device calls: front kernels done
+  // in-batch key grouping: the per-batch key arena (tables of the batch's
+  // distinct keys, k_keys_build layout) for up to gcap keys, and the count
+  uint32_t *g_kqt = nullptr, *g_kzq = nullptr, *g_kok = nullptr, *g_kqt2 = nullptr, *g_kzq2 = nullptr;
+  size_t gcap = 0;
+  uint32_t* h_count = nullptr;                    // pinned: the distinct-key count read back
   // pinned host staging
   uint8_t* h_in = nullptr;
   size_t h_in_cap = 0;
@@ -324,6 +329,7 @@ struct Dev {
   hipEvent_t hi_done = nullptr;                   // the last ladder enqueued on hi_st
   hipEvent_t plain_done = nullptr;                // the last non-pipelined call on the context stream
   bool hi_used = false, plain_used = false;
+  uint64_t grouped_batches = 0, grouped_keys = 0;  // in-batch key grouping taken (gv_group_stats)
   int flip = 0;
   double last_slice_ms = 0;                       // host-buffer calls: this device's slice, wall time
   size_t last_slice_n = 0;
@@ -507,12 +513,93 @@ struct gv_ctx {
   bool lat_sliced = true;       // small batches on k_verify_lat_sl / k_verify_lat16_sl (GV_LAT_SLICED=0: the one-lane-field kernels, A/B)
   bool keyed_k4 = true;         // keyed batches on k_ecmult_k4 (GV_KEYED_K4=0: the 125-doubling ladder, A/B)
   bool pipeline_dev = true;     // pipelined device-resident calls on the context stream (dev_run; GV_PIPELINE=0: A/B)
+  bool group_keys = true;       // pub33 throughput batches parse each distinct key once (group_keys; GV_GROUP_KEYS=0: A/B)
+  size_t group_min = 16384;     // ... batches of at least this many items
+  int group_div = 5;            // ... taking the keyed pipeline when distinct keys <= items / group_div (break-even ~4:
+                                // a key build ~18 ns vs ~4 ns saved per item, profiles/r03/group_ab)
   size_t keys = 0;              // key-arena slots in use (same on every device)
   std::atomic<uint64_t> keys_gen{0};  // gv_keys_reset calls
   std::mutex keys_mu;
 };
 
 namespace {
+
+// The 20-bit-window tables of 2^35 G, 2^70 G, 2^100 G (and lambda images)
+// the 4-group keyed ladder reads (k_ecmult_k4): built on first use, 192 MiB.
+// set s is a scratch set with capacity >= 256 (its flags rows hold the base points).
+int ensure_gtab4(gv_ctx* ctx, Dev* d, Set* s, hipStream_t st) {
+  if (d->gtab4 || !ctx->keyed_k4) return GV_OK;
+  uint32_t* t4 = nullptr;
+  if (hipMalloc(&t4, (size_t)GV_KEY2_TABLES * 2 * GV_GTAB_N * 16 * 4) != hipSuccess) return GV_OK;   // keep k_ecmult<true>
+  int rc;
+  if ((rc = ensure_cap(s, 256))) { (void)hipFree(t4); return rc; }
+  if ((rc = set_acquire(s, st))) { (void)hipFree(t4); return rc; }
+  if (gvk_gen_gtable4(t4, s->flags, st) != hipSuccess) { (void)hipFree(t4); return GV_EHIP; }
+  if ((rc = set_release(s, st))) { (void)hipFree(t4); return rc; }
+  if (hipStreamSynchronize(st) != hipSuccess) { (void)hipFree(t4); return GV_EHIP; }
+  d->gtab4 = t4;
+  return GV_OK;
+}
+
+int ensure_group_arena(Set* s, size_t cap) {
+  if (cap <= s->gcap) return GV_OK;
+  for (uint32_t** p : {&s->g_kqt, &s->g_kzq, &s->g_kok, &s->g_kqt2, &s->g_kzq2})
+    if (*p) { (void)hipFree(*p); *p = nullptr; }
+  s->gcap = 0;
+  const size_t ent = (size_t)GV_KEY_WORDS * 4;
+  if (hipMalloc(&s->g_kqt, cap * ent) != hipSuccess || hipMalloc(&s->g_kzq, cap * 8 * 4) != hipSuccess ||
+      hipMalloc(&s->g_kok, cap * 4) != hipSuccess ||
+      hipMalloc(&s->g_kqt2, cap * GV_KEY2_TABLES * ent) != hipSuccess ||
+      hipMalloc(&s->g_kzq2, cap * GV_KEY2_TABLES * 8 * 4) != hipSuccess)
+    return GV_ENOMEM;
+  s->gcap = cap;
+  return GV_OK;
+}
+
+// In-batch key grouping for a pub33 throughput batch of n items (b prepared
+// for the pub33 pipeline, inputs on the device): the SoA rows are unpacked,
+// the items grouped by key (k_dedupe*), and when the batch has at most
+// n / group_div distinct keys their tables are built once into the set's
+// batch arena and b is switched to the keyed pipeline with the key id as
+// slot.  Scratch: the set's per-lane Q-table region (unused by the keyed
+// pipeline; the pub33 pipeline rewrites it).  One 4-byte read-back (the
+// distinct-key count) decides the route.
+int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t st) {
+  const size_t C = b.C;
+  size_t T = 512;
+  while (T < 2 * n) T <<= 1;
+  const size_t capU = round_up(std::max<size_t>(C / ctx->group_div, 256), 256);
+  uint32_t* q = s->qtab;
+  uint32_t *rep = q, *uid = q + C, *kslot = q + 2 * C, *count = q + 3 * C, *table = q + 3 * C + 256;
+  uint32_t* kx = table + T;
+  uint32_t* kpfx = kx + 8 * capU;
+  uint32_t* qr = kpfx + capU;
+  if ((size_t)(qr + (GV_QTAB_N - 1) * 9 * capU - q) > (size_t)GV_QTAB_WORDS * C) return GV_OK;   // no room: pub33
+  if (!s->h_count && hipHostMalloc((void**)&s->h_count, 64, hipHostMallocDefault) != hipSuccess) {
+    s->h_count = nullptr;
+    return GV_ENOMEM;
+  }
+  int rc = GV_OK;
+  CK(gvk_unpack(b.pub33, b.sig64, b.dig32, (uint32_t)n, (uint32_t)C, b.in_x, b.in_pfx, b.in_r, b.in_s, b.in_e, st));
+  b.unpacked = 1;
+  CK(gvk_dedupe((uint32_t)n, (uint32_t)C, b.in_x, b.in_pfx, table, (uint32_t)T, rep, uid, count, kslot,
+                (uint32_t)capU, (uint32_t)capU, kx, kpfx, st));
+  CK(hipMemcpyAsync(s->h_count, count, 4, hipMemcpyDeviceToHost, st));
+  CK(hipStreamSynchronize(st));
+  const size_t U = *s->h_count;
+  if (U == 0 || U * ctx->group_div > n || U > capU) return GV_OK;   // many distinct keys: the pub33 pipeline
+  if ((rc = ensure_gtab4(ctx, d, s, st))) return rc;
+  if ((rc = ensure_group_arena(s, capU))) return rc == GV_ENOMEM ? GV_OK : rc;
+  CK(gvk_keys_build_rows((uint32_t)U, (uint32_t)capU, kx, kpfx, qr, s->g_kqt, s->g_kzq, (uint32_t)capU,
+                         s->g_kok, s->g_kqt2, s->g_kzq2, st));
+  b.pub33 = nullptr;
+  b.kslot = kslot; b.kqt = s->g_kqt; b.kzq = s->g_kzq; b.kok = s->g_kok;
+  b.kC = (uint32_t)capU; b.kcount = (uint32_t)U;
+  b.kqt2 = s->g_kqt2; b.gtab4 = d->gtab4;       // null gtab4: the 125-doubling keyed ladder
+  d->grouped_batches++;
+  d->grouped_keys += U;
+  return GV_OK;
+}
 
 // Launch the pipeline for n items whose inputs already sit on the device, on
 // set s's scratch, stream st.  The caller holds d->mu.
@@ -593,6 +680,10 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
       CK(hipEventRecord(rs[5], st));
     }
   } else {
+    if (!kslot && pub && ctx->group_keys && n >= ctx->group_min) {
+      rc = group_keys(ctx, d, s, b, n, st);
+      if (rc) return rc;
+    }
     CK(gvk_verify(&b, st));
   }
   if (rs) {
@@ -942,6 +1033,9 @@ void free_set(Set& s) {
   if (s.last) (void)hipEventDestroy(s.last);
   if (s.done) (void)hipEventDestroy(s.done);
   if (s.ecm_ready) (void)hipEventDestroy(s.ecm_ready);
+  for (uint32_t* p : {s.g_kqt, s.g_kzq, s.g_kok, s.g_kqt2, s.g_kzq2})
+    if (p) (void)hipFree(p);
+  if (s.h_count) (void)hipHostFree(s.h_count);
   if (s.st) (void)hipStreamDestroy(s.st);
 }
 
@@ -979,6 +1073,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* ls = getenv("GV_LAT_SLICED")) ctx->lat_sliced = strcmp(ls, "0") != 0;
   if (const char* zc = getenv("GV_LAT_ZC")) ctx->lat_zero_copy = strcmp(zc, "0") != 0;
   if (const char* pl = getenv("GV_PIPELINE")) ctx->pipeline_dev = strcmp(pl, "0") != 0;
+  if (const char* gk = getenv("GV_GROUP_KEYS")) ctx->group_keys = strcmp(gk, "0") != 0;
   ctx->stage_threads = std::max(1, std::min(8, host_cpus() / 2));   // half the quota: the callers, HIP's
                                                                     // own threads and the pool share it
   ctx->pool = new Pool(ctx->stage_threads - 1);
@@ -1194,6 +1289,15 @@ int gv_keys_reset(gv_ctx* ctx) {
 
 size_t gv_keys_count(const gv_ctx* ctx) { return ctx ? ctx->keys : 0; }
 
+int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys) {
+  if (!ctx || dev_slot < 0 || dev_slot >= (int)ctx->devs.size()) return GV_EINVAL;
+  Dev* d = ctx->devs[dev_slot];
+  std::lock_guard<std::mutex> lk(d->mu);
+  if (batches) *batches = d->grouped_batches;
+  if (keys) *keys = d->grouped_keys;
+  return GV_OK;
+}
+
 int gv_last_slices(gv_ctx* ctx, double* ms_out, size_t* n_out, int cap) {
   if (!ctx || cap < 0 || (cap > 0 && (!ms_out || !n_out))) return GV_EINVAL;
   const int m = std::min<int>(cap, (int)ctx->devs.size());
@@ -1291,6 +1395,18 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
     delete ctx->pool;
     ctx->pool = new Pool((int)val - 1);
     for (Dev* d : ctx->devs) d->pool = ctx->pool;
+  } else if (!strcmp(key, "group_keys")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->group_keys = val != 0;
+  } else if (!strcmp(key, "group_min")) {
+    if (val < 256 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
+    ctx->group_min = (size_t)val;
+  } else if (!strcmp(key, "group_div")) {
+    if (val < 2 || val > 1024) return GV_EINVAL;
+    ctx->group_div = (int)val;
+  } else if (!strcmp(key, "pipeline_dev")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->pipeline_dev = val != 0;
   } else if (!strcmp(key, "time_kernels")) {
     ctx->time_kernels = val != 0;
   } else if (!strcmp(key, "fault_inject")) {

@@ -42,7 +42,7 @@ EXPORTED_SYMBOLS = (
     "gv_dev_copy", "gv_dev_sync", "gv_stage_stats", "gv_keys_load", "gv_keys_reset", "gv_keys_count", "gv_keys_generation",
     "gv_verify_digests_keyed", "gv_verify_msgs_keyed", "gv_dev_verify_digests_keyed", "gv_stage_stats4",
     "gv_keys_point", "gv_dev_stream_create", "gv_dev_stream_sync", "gv_dev_stream_destroy",
-    "gv_verify_ed25519_msgs", "gv_dev_verify_ed25519_msgs", "gv_last_slices",
+    "gv_verify_ed25519_msgs", "gv_dev_verify_ed25519_msgs", "gv_last_slices", "gv_group_stats",
 )
 
 
@@ -120,6 +120,8 @@ def load(path: str = LIB_PATH):
     L.gv_stage_stats4.restype = i32
     L.gv_last_slices.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_size_t), i32]
     L.gv_last_slices.restype = i32
+    L.gv_group_stats.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    L.gv_group_stats.restype = i32
     L.gv_keys_load.argtypes = [vp, sz, vp, vp]
     L.gv_keys_load.restype = i32
     L.gv_keys_reset.argtypes = [vp]
@@ -382,6 +384,12 @@ class Verifier:
         ms = (ctypes.c_double * 4)()
         _check(self._L.gv_stage_stats4(self._ctx, slot, ctypes.byref(c), ms), "gv_stage_stats4")
         return c.value, list(ms)
+
+    def group_stats(self, slot: int = 0):
+        """(batches that took the in-batch key grouping, distinct keys built) on device slot."""
+        b, k = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self._L.gv_group_stats(self._ctx, slot, ctypes.byref(b), ctypes.byref(k)), "gv_group_stats")
+        return b.value, k.value
 
     def last_slices(self):
         """[(ms, items)] per device slot: each device's slice of the last host-buffer call."""

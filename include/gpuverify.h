@@ -204,9 +204,21 @@ int gv_dev_verify_ed25519_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* 
  * copy/compute pipeline per device, default 131072; 0 = one chunk per
  * max_batch), "pipe_growth" (each later chunk at most this many times the one
  * before, default 4: the staging of chunk i+1 hides under the kernels of
- * chunk i), "stage_threads" (pageable -> pinned staging copy threads per
- * device, default 8),
- * "time_kernels" (0/1: record HIP events around each kernel stage),
+ * chunk i), "stage_threads" (pageable -> pinned staging copy threads of
+ * the context's ONE pool shared by its devices, default half the process's
+ * CPUs -- affinity capped by the cgroup quota -- at most 8),
+ * "group_keys" (0/1: a pub33 batch past the small-batch bound with at least
+ * "group_min" items (default 16384) whose distinct keys number at most
+ * items / "group_div" (default 5) parses each distinct key once -- grouped
+ * on the device, tables built into a per-batch arena, the items verified by
+ * the keyed pipeline; same verdicts; default 1, env GV_GROUP_KEYS),
+ * "pipeline_dev" (0/1: device-resident calls on the context stream past the
+ * small-batch bound are pipelined -- consecutive calls alternate scratch sets,
+ * their unpack / s^-1 / prep kernels run on a low-priority stream under the
+ * previous call's ladder, every ladder on one high-priority stream in call
+ * order; a caller stream is never pipelined; default 1, env GV_PIPELINE),
+ * "time_kernels" (0/1: record HIP events around each kernel stage; the
+ * ladder's time is its own start to end),
  * "fault_inject" (0/1: every verify call fails with GV_EFAULT; test hook). */
 int gv_set_option(gv_ctx* ctx, const char* key, long long val);
 
@@ -227,6 +239,10 @@ int gv_stage_stats4(gv_ctx* ctx, int dev_slot, int* count, double ms[4]);
  * (ms) and item count of that device's slice in the last gv_verify_* call
  * (bench.py --inproc: per-device rates).  Returns the number of slots written. */
 int gv_last_slices(gv_ctx* ctx, double* ms_out, size_t* n_out, int cap);
+/* In-batch key grouping (option "group_keys"): on dev_slot, the number of
+ * batches that took the grouped (keyed) pipeline and the distinct keys whose
+ * tables they built. */
+int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys);
 
 const char* gv_strerror(int code);
 

@@ -1,0 +1,90 @@
+"""In-batch key grouping (gv_set_option "group_keys"): a pub33 batch whose
+items repeat keys parses each distinct key once (k_dedupe*, k_keys_build into a
+per-batch arena) and runs the keyed pipeline.  The verdicts must be exactly the
+per-item pub33 pipeline's -- including keys that ParsePubKey rejects (repeated
+bad prefixes, x >= p, non-residue x), which get a slot too and make every item
+on them false -- and the route is taken only below the distinct-key bound."""
+import numpy as np
+import pytest
+
+import bench
+import gpuverify as gvm
+from golden_io import load_digest_vectors
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ver():
+    v = gvm.Verifier([0])
+    yield v
+    v.close()
+
+
+def grouped_vs_plain(ver, pub, sig, dig, msgs=None):
+    b0, _ = ver.group_stats()
+    ver.set_option("group_keys", 1)
+    got = ver.verify_batch_digests(pub, sig, dig) if msgs is None else ver.verify_batch_msgs(pub, sig, msgs)
+    b1, k1 = ver.group_stats()
+    ver.set_option("group_keys", 0)
+    ref = ver.verify_batch_digests(pub, sig, dig) if msgs is None else ver.verify_batch_msgs(pub, sig, msgs)
+    ver.set_option("group_keys", 1)
+    return got, ref, b1 - b0
+
+
+def test_repeated_keys_take_the_grouped_route_with_identical_verdicts(ver):
+    pub, sig, dig, exp = bench.make_digest_workload(200_000, 0x6A, 2048, 0.25, 16)
+    got, ref, grouped = grouped_vs_plain(ver, pub, sig, dig)
+    assert grouped >= 1
+    assert np.array_equal(got, exp) and np.array_equal(ref, exp)
+    idx = np.random.default_rng(3).choice(len(exp), 4000, replace=False)
+    assert np.array_equal(O.verify_digests(pub[idx], sig[idx], dig[idx], threads=16), got[idx])
+
+
+def test_rejected_keys_repeated_across_the_batch(ver):
+    """Goldens (every rejection class, infinity, x in [n, p), exceptional adds)
+    tiled 300 times: 549 distinct keys over ~165k items."""
+    gp, gs, gd, gok, _ = load_digest_vectors()
+    reps = 300
+    pub, sig, dig = (np.tile(a, (reps, 1)) for a in (gp, gs, gd))
+    perm = np.random.default_rng(5).permutation(len(pub))
+    pub, sig, dig = pub[perm], sig[perm], dig[perm]
+    exp = np.tile(gok, reps)[perm]
+    got, ref, grouped = grouped_vs_plain(ver, pub, sig, dig)
+    assert grouped >= 1
+    assert np.array_equal(got, exp) and np.array_equal(ref, exp)
+
+
+def test_unique_keys_keep_the_pub33_route(ver):
+    pub, sig, dig, exp = bench.make_digest_workload(100_000, 0x6B, 100_000, 0.0, 16)
+    got, ref, grouped = grouped_vs_plain(ver, pub, sig, dig)
+    assert grouped == 0
+    assert np.array_equal(got, exp)
+
+
+def test_grouped_device_resident_and_message_path(ver):
+    n = 131_072
+    pub, sig, dig, exp = bench.make_digest_workload(n, 0x6C, 1024, 0.25, 16)
+    d = [ver.dev_alloc(a.nbytes) for a in (pub, sig, dig)]
+    d_bits = ver.dev_alloc(((n + 63) // 64) * 8)
+    for p, a in zip(d, (pub, sig, dig)):
+        ver.dev_upload(p, a)
+    b0, _ = ver.group_stats()
+    for _ in range(3):                           # pipelined consecutive calls on the context stream
+        ver.dev_verify_digests(0, n, d[0], d[1], d[2], d_bits)
+    ver.dev_sync()
+    bits = np.zeros((n + 63) // 64, np.uint64)
+    ver.dev_download(bits, d_bits)
+    assert np.array_equal(bench.unpack_bits(bits, n), exp)
+    assert ver.group_stats()[0] - b0 == 3
+    for p in d + [d_bits]:
+        ver.dev_free(p)
+    # message path: sign bytes hashed on the GPU, keys grouped
+    from golden_io import load_msg_vectors
+    mp, ms, mm, mok, _ = load_msg_vectors()
+    reps = 400
+    pub, sig = np.tile(mp, (reps, 1)), np.tile(ms, (reps, 1))
+    msgs = mm * reps
+    got, ref, grouped = grouped_vs_plain(ver, pub, sig, None, msgs=msgs)
+    assert grouped >= 1 and np.array_equal(got, np.tile(mok, reps)) and np.array_equal(ref, got)

@@ -83,6 +83,31 @@ def c2_hostpath(ver, pub, sig, dig, exp, steps: int = 5, device_value: float | N
     return res
 
 
+def c2_per_item_parse(ver, pub, sig, dig, exp, steps: int = 10):
+    """The headline C2 batch with in-batch key grouping OFF (gv_set_option
+    "group_keys" 0): every item decompresses its own key and builds its own
+    Q table (the pub33 pipeline), device-resident, pipelined calls."""
+    n = len(pub)
+    d = [ver.dev_alloc(a.nbytes) for a in (pub, sig, dig)]
+    for p, a in zip(d, (pub, sig, dig)):
+        ver.dev_upload(p, a)
+    nw = (n + 63) // 64
+    d_bits = ver.dev_alloc(nw * 8)
+    ver.set_option("group_keys", 0)
+    try:
+        el, stages = _timed_device_runs(ver, lambda: ver.dev_verify_digests(0, n, d[0], d[1], d[2], d_bits), steps)
+    finally:
+        ver.set_option("group_keys", 1)
+    bits = np.zeros(nw, np.uint64)
+    ver.dev_download(bits, d_bits)
+    got = _unpack_bits(bits, n)
+    for p in d + [d_bits]:
+        ver.dev_free(p)
+    return {"items": n, "value": round(n * steps / el, 1), "unit": "verifies/s",
+            "mismatches": int(np.count_nonzero(got != exp)), "stages": stages,
+            "note": "group_keys off: the per-item pub33 pipeline on the same batch"}
+
+
 def c2_unique_keys(ver, make_workload, n: int, threads: int, steps: int = 3):
     """SURVEY.md §8d C2 variant: one distinct key per item (no key reuse at
     all), device-resident, bitmap checked against construction."""
