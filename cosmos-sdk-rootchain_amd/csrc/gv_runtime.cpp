@@ -23,7 +23,9 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <functional>
+#include <future>
 #include <mutex>
 #include <memory>
 #include <sched.h>
@@ -184,7 +186,10 @@ void par_copy_segs(Pool* pool, const CopySeg* seg, int ns) {
   pool->run(parts, [&](int p) { copy_range(std::min(total, p * per), std::min(total, (p + 1) * per)); });
 }
 
-// One persistent thread per extra device: runs the device's slice of a host batch.
+// One persistent thread per extra device: runs the device's slices of host
+// batches, in the order they were posted.  Every post gets its own future, so
+// concurrent callers of one context (gv_ctx is thread-safe) each wait for
+// THEIR slice, never for another caller's.
 class Worker {
  public:
   Worker() : th_([this] { loop(); }) {}
@@ -196,42 +201,35 @@ class Worker {
     cv_.notify_all();
     th_.join();
   }
-  void post(std::function<int()> job) {
-    std::lock_guard<std::mutex> lk(m_);
-    job_ = std::move(job);
-    has_ = true;
-    done_ = false;
+  std::future<int> post(std::function<int()> job) {
+    auto task = std::make_shared<std::packaged_task<int()>>(std::move(job));
+    std::future<int> f = task->get_future();
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      q_.push_back([task] { (*task)(); });
+    }
     cv_.notify_all();
-  }
-  int wait() {
-    std::unique_lock<std::mutex> lk(m_);
-    cv_.wait(lk, [this] { return done_; });
-    return rc_;
+    return f;
   }
 
  private:
   void loop() {
     for (;;) {
-      std::function<int()> job;
+      std::function<void()> job;
       {
         std::unique_lock<std::mutex> lk(m_);
-        cv_.wait(lk, [this] { return quit_ || has_; });
-        if (quit_) return;
-        job = std::move(job_);
-        has_ = false;
+        cv_.wait(lk, [this] { return quit_ || !q_.empty(); });
+        if (q_.empty()) return;                  // quit with nothing left
+        job = std::move(q_.front());
+        q_.pop_front();
       }
-      const int rc = job();
-      std::lock_guard<std::mutex> lk(m_);
-      rc_ = rc;
-      done_ = true;
-      cv_.notify_all();
+      job();
     }
   }
   std::mutex m_;
   std::condition_variable cv_;
-  std::function<int()> job_;
-  bool has_ = false, done_ = true, quit_ = false;
-  int rc_ = GV_OK;
+  std::deque<std::function<void()>> q_;
+  bool quit_ = false;
   std::thread th_;
 };
 
@@ -738,7 +736,20 @@ struct HostBatch {
   const uint32_t* slots;
   uint8_t* out_ok;
   uint64_t* out_bits;
+  bool pinned = false;          // digest inputs in pinned host memory (gv_host_alloc): no staging copy
 };
+
+// Host memory the device can read directly (hipHostMalloc / gv_host_alloc /
+// hipHostRegister), as opposed to pageable memory that must be staged.
+bool is_pinned(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
 
 // Harvest a finished chunk of set s into the caller's outputs.
 int harvest(Dev* d, Set* s, const HostBatch& hb) {
@@ -790,6 +801,41 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
   if ((rc = ensure_pinned((uint8_t**)&s->h_bits, &s->h_bits_cap, (C / 64) * 8))) return rc;
   uint8_t* h = s->h_in;
   uint64_t bmin = 0;
+  if (hb.pinned && !msgs) {                 // the caller's pinned buffers: read in place, no staging
+    const uint8_t* kp = keyed ? (const uint8_t*)(hb.slots + c0) : hb.pub33 + c0 * 33;
+    const uint8_t* sp = hb.sig64 + c0 * 64;
+    const uint8_t* dp = hb.dig32 + c0 * 32;
+    const size_t lmax = keyed ? ctx->lat_max_keyed : ctx->lat_max;
+    const size_t slmax = keyed ? ctx->lat_sl_max_keyed : ctx->lat_sl_max;
+    if (ctx->lat_zero_copy && ctx->lat_sliced && cn <= slmax && cn <= lmax) {
+      if ((rc = ensure_pinned(&s->h_out8, &s->h_out8_cap, cn))) return rc;
+      rc = launch(ctx, d, s, cn, keyed ? nullptr : kp, sp, dp, nullptr, nullptr, nullptr, nullptr, s->st,
+                  keyed ? (const uint32_t*)kp : nullptr, s->h_out8);
+      if (rc) return rc;
+      CK(hipEventRecord(s->done, s->st));
+      s->busy = true;
+      s->zc = true;
+      s->c0 = c0;
+      s->cn = cn;
+      return GV_OK;
+    }
+    if ((rc = set_acquire(s, s->st))) return rc;
+    CK(hipMemcpyAsync(s->d_in, kp, cn * (keyed ? 4 : 33), hipMemcpyHostToDevice, s->st));
+    CK(hipMemcpyAsync(s->d_in + L.sig, sp, cn * 64, hipMemcpyHostToDevice, s->st));
+    CK(hipMemcpyAsync(s->d_in + L.third, dp, cn * 32, hipMemcpyHostToDevice, s->st));
+    const uint8_t* din = s->d_in;
+    rc = launch(ctx, d, s, cn, keyed ? nullptr : din, din + L.sig, din + L.third, nullptr, nullptr, nullptr, s->bits,
+                s->st, keyed ? (const uint32_t*)din : nullptr);
+    if (rc) return rc;
+    CK(hipMemcpyAsync(s->h_bits, s->bits, ((cn + 63) / 64) * 8, hipMemcpyDeviceToHost, s->st));
+    CK(hipEventRecord(s->done, s->st));
+    if ((rc = set_release(s, s->st))) return rc;
+    s->busy = true;
+    s->zc = false;
+    s->c0 = c0;
+    s->cn = cn;
+    return GV_OK;
+  }
   if (!msgs) {                              // keys/slots, signatures, digests: one pool pass
     const CopySeg segs[3] = {keyed ? CopySeg{h, (const uint8_t*)(hb.slots + c0), cn * 4}
                                    : CopySeg{h, hb.pub33 + c0 * 33, cn * 33},
@@ -983,41 +1029,42 @@ int run_ed_host(gv_ctx* ctx, size_t n, const EdHost& hb) {
   const size_t nd = ctx->devs.size();
   const size_t per = round_up((n + nd - 1) / nd, 256);
   std::vector<int> rcs(nd, GV_OK);
-  std::vector<bool> posted(nd, false);
+  std::vector<std::future<int>> futs(nd);
   for (size_t k = 1; k < nd; ++k) {
     const size_t lo = std::min(n, k * per), hi = std::min(n, (k + 1) * per);
     if (lo >= hi) continue;
     Dev* d = ctx->devs[k];
-    d->worker->post([=, &hb]() { return ed_slice(ctx, d, lo, hi, hb); });
-    posted[k] = true;
+    futs[k] = d->worker->post([=, &hb]() { return ed_slice(ctx, d, lo, hi, hb); });
   }
   rcs[0] = ed_slice(ctx, ctx->devs[0], 0, std::min(n, per), hb);
   for (size_t k = 1; k < nd; ++k)
-    if (posted[k]) rcs[k] = ctx->devs[k]->worker->wait();
+    if (futs[k].valid()) rcs[k] = futs[k].get();
   for (int rc : rcs) if (rc) return rc;
   return GV_OK;
 }
 
-int run_host(gv_ctx* ctx, size_t n, const HostBatch& hb) {
+int run_host(gv_ctx* ctx, size_t n, const HostBatch& hb_in) {
   if (!ctx) return GV_EINVAL;
   if (ctx->fault_inject) return GV_EFAULT;
   if (n == 0) return GV_OK;
-  if ((!hb.pub33 && !hb.slots) || !hb.sig64 || (!hb.out_ok && !hb.out_bits)) return GV_EINVAL;
-  if (!hb.dig32 && (!hb.blob || !hb.off || !hb.len)) return GV_EINVAL;
+  if ((!hb_in.pub33 && !hb_in.slots) || !hb_in.sig64 || (!hb_in.out_ok && !hb_in.out_bits)) return GV_EINVAL;
+  if (!hb_in.dig32 && (!hb_in.blob || !hb_in.off || !hb_in.len)) return GV_EINVAL;
+  HostBatch hb = hb_in;
+  hb.pinned = hb.dig32 && is_pinned(hb.slots ? (const void*)hb.slots : hb.pub33) && is_pinned(hb.sig64) &&
+              is_pinned(hb.dig32);
   const size_t nd = ctx->devs.size();
   const size_t per = round_up((n + nd - 1) / nd, 256);
   std::vector<int> rcs(nd, GV_OK);
-  std::vector<bool> posted(nd, false);
+  std::vector<std::future<int>> futs(nd);
   for (size_t k = 1; k < nd; ++k) {             // devices 1.. on their persistent workers
     const size_t lo = std::min(n, k * per), hi = std::min(n, (k + 1) * per);
     if (lo >= hi) continue;
     Dev* d = ctx->devs[k];
-    d->worker->post([=, &hb]() { return run_slice(ctx, d, lo, hi, hb); });
-    posted[k] = true;
+    futs[k] = d->worker->post([=, &hb]() { return run_slice(ctx, d, lo, hi, hb); });
   }
   rcs[0] = run_slice(ctx, ctx->devs[0], 0, std::min(n, per), hb);   // device 0 on the caller
   for (size_t k = 1; k < nd; ++k)
-    if (posted[k]) rcs[k] = ctx->devs[k]->worker->wait();
+    if (futs[k].valid()) rcs[k] = futs[k].get();
   for (int rc : rcs) if (rc) return rc;
   return GV_OK;
 }
@@ -1288,6 +1335,18 @@ int gv_keys_reset(gv_ctx* ctx) {
 }
 
 size_t gv_keys_count(const gv_ctx* ctx) { return ctx ? ctx->keys : 0; }
+
+int gv_host_alloc(gv_ctx* ctx, size_t bytes, void** out) {
+  if (!ctx || !out || bytes == 0) return GV_EINVAL;
+  *out = nullptr;
+  if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) { *out = nullptr; return GV_ENOMEM; }
+  return GV_OK;
+}
+int gv_host_free(gv_ctx* ctx, void* p) {
+  if (!ctx) return GV_EINVAL;
+  if (p && hipHostFree(p) != hipSuccess) return GV_EHIP;
+  return GV_OK;
+}
 
 int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys) {
   if (!ctx || dev_slot < 0 || dev_slot >= (int)ctx->devs.size()) return GV_EINVAL;

@@ -42,7 +42,7 @@ EXPORTED_SYMBOLS = (
     "gv_dev_copy", "gv_dev_sync", "gv_stage_stats", "gv_keys_load", "gv_keys_reset", "gv_keys_count", "gv_keys_generation",
     "gv_verify_digests_keyed", "gv_verify_msgs_keyed", "gv_dev_verify_digests_keyed", "gv_stage_stats4",
     "gv_keys_point", "gv_dev_stream_create", "gv_dev_stream_sync", "gv_dev_stream_destroy",
-    "gv_verify_ed25519_msgs", "gv_dev_verify_ed25519_msgs", "gv_last_slices", "gv_group_stats",
+    "gv_verify_ed25519_msgs", "gv_dev_verify_ed25519_msgs", "gv_last_slices", "gv_group_stats", "gv_host_alloc", "gv_host_free",
 )
 
 
@@ -122,6 +122,10 @@ def load(path: str = LIB_PATH):
     L.gv_last_slices.restype = i32
     L.gv_group_stats.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     L.gv_group_stats.restype = i32
+    L.gv_host_alloc.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(vp)]
+    L.gv_host_alloc.restype = i32
+    L.gv_host_free.argtypes = [vp, vp]
+    L.gv_host_free.restype = i32
     L.gv_keys_load.argtypes = [vp, sz, vp, vp]
     L.gv_keys_load.restype = i32
     L.gv_keys_reset.argtypes = [vp]
@@ -384,6 +388,22 @@ class Verifier:
         ms = (ctypes.c_double * 4)()
         _check(self._L.gv_stage_stats4(self._ctx, slot, ctypes.byref(c), ms), "gv_stage_stats4")
         return c.value, list(ms)
+
+    def host_array(self, shape, dtype=np.uint8):
+        """A numpy array in pinned host memory (gv_host_alloc): host-buffer digest
+        calls on such arrays skip the staging copy.  Freed with host_free(arr)."""
+        nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        p = ctypes.c_void_p()
+        _check(self._L.gv_host_alloc(self._ctx, max(1, nbytes), ctypes.byref(p)), "gv_host_alloc")
+        buf = (ctypes.c_uint8 * max(1, nbytes)).from_address(p.value)
+        arr = np.frombuffer(buf, dtype=np.uint8, count=nbytes).view(dtype).reshape(shape)
+        self._pinned = getattr(self, "_pinned", {})
+        self._pinned[arr.ctypes.data] = p.value
+        return arr
+
+    def host_free(self, arr):
+        p = self._pinned.pop(arr.ctypes.data)
+        _check(self._L.gv_host_free(self._ctx, p), "gv_host_free")
 
     def group_stats(self, slot: int = 0):
         """(batches that took the in-batch key grouping, distinct keys built) on device slot."""

@@ -239,6 +239,13 @@ int gv_stage_stats4(gv_ctx* ctx, int dev_slot, int* count, double ms[4]);
  * (ms) and item count of that device's slice in the last gv_verify_* call
  * (bench.py --inproc: per-device rates).  Returns the number of slots written. */
 int gv_last_slices(gv_ctx* ctx, double* ms_out, size_t* n_out, int cap);
+/* Pinned host memory for a caller's input buffers: a host-buffer digest call
+ * (gv_verify_digests[_bits|_keyed]) whose pub33 / slot, sig64 and dig32
+ * arrays lie in such memory skips the library's pageable -> pinned staging
+ * copy (the device reads them in place: DMA, or zero-copy for small batches).
+ * The Go shim packs its batches into these buffers. */
+int gv_host_alloc(gv_ctx* ctx, size_t bytes, void** out);
+int gv_host_free(gv_ctx* ctx, void* p);
 /* In-batch key grouping (option "group_keys"): on dev_slot, the number of
  * batches that took the grouped (keyed) pipeline and the distinct keys whose
  * tables they built. */

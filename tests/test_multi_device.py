@@ -64,3 +64,20 @@ def test_shared_staging_pool_under_concurrent_callers():
         for got in out[i]:
             assert np.array_equal(got, batches[i][3])
     assert len(sl) == 2 and all(c > 0 for _, c in sl)
+
+
+@pytest.mark.parametrize("n", [1, 700, 5000, 300_000])
+def test_pinned_caller_buffers(n):
+    """Caller arrays in pinned memory (gv_host_alloc) skip the staging copy:
+    small batches read them in place (sliced kernels), large ones copy them
+    straight to the device.  Same verdicts as pageable arrays."""
+    pub, sig, dig, exp = bench.make_digest_workload(n, 0xD7 + n, 4096, 0.25, 16)
+    with gvm.Verifier([0]) as v:
+        hp = [v.host_array(a.shape, a.dtype) for a in (pub, sig, dig)]
+        for h, a in zip(hp, (pub, sig, dig)):
+            h[...] = a
+        got = v.verify_batch_digests(*hp)
+        again = v.verify_batch_digests(pub, sig, dig)
+        for h in hp:
+            v.host_free(h)
+    assert np.array_equal(got, exp) and np.array_equal(again, exp)
