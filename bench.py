@@ -51,12 +51,14 @@ W_KERNEL = {"k_scalar_inv": W_INV,
 W_MUL = sum(W_KERNEL.values())             # 121,032 ~ the survey's 1.2e5
 # In-batch key grouping (gv_set_option "group_keys", the default for pub33
 # batches with few distinct keys): each distinct key's tables are built once
-# (k_keys_build: decompress, Q table, 100 doublings to 2^35 Q / 2^70 Q /
-# 2^100 Q, three affine conversions + tables rescaled to one Z) and the items
-# run the keyed pipeline (u1/u2 in k_prep<true>, the 30-doubling k_ecmult_k4).
-W_INVF = 255 * FS + 15 * FM                # a field inversion (Fermat)              12,300
-W_KEYBUILD = (W_DECOMP + W_QTAB + 100 * (2 * FM + 5 * FS) +
-              3 * (2 * W_INVF + 6 * FM + W_QTAB + 32 * FM))                     # per distinct key 169,196
+# (k_keys_chain + k_keys_tables: decompress, 100 doublings to 2^35 Q /
+# 2^70 Q / 2^100 Q, four tables built straight from Jacobian coordinates, each
+# back-propagated onto the product of the four table Zs -- the running Z
+# product, rho and the last entry cost 20 products per table, no inversion)
+# and the items run the keyed pipeline (u1/u2 in k_prep<true>, the
+# 30-doubling k_ecmult_k4).
+W_KEYBUILD = (W_DECOMP + 4 * W_QTAB + 100 * (2 * FM + 5 * FS) + 3 * FM +
+              4 * (20 * FM + FS))                                              # per distinct key
 W_LADDER_K4 = W_LADDER - 95 * (2 * FM + 5 * FS)                                # 30 doublings: 61,524
 # Peak: the highest v_mad_u64_u32 issue rate measured on MI355X
 # (tools/microbench/alu_rate.hip; profiles/r01/alu_rate_v3.jsonl, dependent
@@ -439,7 +441,9 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
     grouped = gb - grp0[0] >= calib
     u_keys = (gk - grp0[1]) / max(1, gb - grp0[0]) if grouped else 0.0
     if grouped:
-        w = {"k_unpack+k_dedupe+k_keys_build": W_KEYBUILD * u_keys / n, "k_scalar_inv": W_INV,
+        # the key tables (k_keys_chain, k_keys_tables) run on a side stream
+        # beside k_scalar_inv: that stage's time covers both
+        w = {"k_unpack+k_dedupe": 0.0, "k_scalar_inv|k_keys_chain+k_keys_tables": W_INV + W_KEYBUILD * u_keys / n,
              "k_prep<keyed>": W_SCALAR, "k_ecmult_k4": W_LADDER_K4}
         kms = dict(zip(w, (unpack_ms, inv_ms, prep_ms, ecmult_ms)))
         ladder, w_route = "k_ecmult_k4", sum(w.values())
@@ -473,7 +477,7 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
                    "items_per_gpu": n, "keys": args.keys, "adversarial_fraction": args.adversarial,
                    "global_batch": n * world, "parallelism": f"shard{world} (independent per-GPU shards, no collective)",
                    "route": ("in-batch key grouping: each distinct key parsed and tabulated once (k_dedupe, "
-                             "k_keys_build), items on the keyed 30-doubling ladder" if grouped else
+                             "k_keys_chain + k_keys_tables), items on the keyed 30-doubling ladder" if grouped else
                              "per-item pub33 pipeline (every item decompresses its key)"),
                    "distinct_keys_per_batch": round(u_keys) if grouped else None},
         "roofline": {

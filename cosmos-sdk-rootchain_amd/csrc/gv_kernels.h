@@ -48,6 +48,7 @@ typedef struct gvk_batch {
   hipStream_t st_ecm;
   hipEvent_t ecm_ready;
   int unpacked;                 // the SoA rows are already written (in-batch key grouping ran k_unpack)
+  hipEvent_t keys_ready;        // optional: the batch's key tables are built on another stream; k_prep waits
   // keyed batch (kslot != NULL, pub33 unused): item i's key is arena slot kslot[i]
   const uint32_t* kslot;        // n slots (device)
   const uint32_t* kqt;          // arena Q tables, row per slot (GV_QTAB_N x GV_QENT_WORDS words)
@@ -143,13 +144,15 @@ hipError_t gvk_unpack(const uint8_t* pub33, const uint8_t* sig64, const uint8_t*
 hipError_t gvk_dedupe(uint32_t n, uint32_t C, const uint32_t* x, const uint32_t* pfx, uint32_t* table, uint32_t tslots,
                       uint32_t* rep, uint32_t* uid, uint32_t* count, uint32_t* kslot, uint32_t capU, uint32_t CU,
                       uint32_t* kx, uint32_t* kpfx, hipStream_t st);
-// k_keys_build over n keys already unpacked into rows in_x / in_pfx (stride C), slots 0..n-1.
+// The key tables (k_keys_chain, k_keys_tables) of n keys already unpacked into
+// rows in_x / in_pfx (stride C), slots 0..n-1; qr: (GV_QTAB_N - 1) * 9 ratio
+// rows of stride round_up(4 n, 256).
 hipError_t gvk_keys_build_rows(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx, uint32_t* qr,
                                uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2,
                                uint32_t* kzq2, hipStream_t st);
 // Parse n keys (device pub33) into arena slots base..base+n-1.  Scratch: the
 // batch rows in_x, in_pfx (and r, s, e as k_unpack targets) of stride C and
-// qr (GV_QTAB_N - 1) * 9 rows of stride C.
+// qr (GV_QTAB_N - 1) * 9 rows of stride round_up(4 n, 256).
 hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
                           uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t base,
                           uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2,

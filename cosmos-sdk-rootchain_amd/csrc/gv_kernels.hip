@@ -185,7 +185,7 @@ __global__ __launch_bounds__(256) void k_unpack(const uint8_t* pub33, const uint
 // A batch that repeats keys (a block with repeat signers; C2's 65,536 keys
 // round-robin over 1M signatures) parses each distinct key once: the keys are
 // grouped by an open-addressing hash table over the unpacked (prefix, x) rows,
-// each distinct key gets an id, its tables are built once (k_keys_build into a
+// each distinct key gets an id, its tables are built once (k_keys_chain + k_keys_tables into a
 // per-batch arena) and the items run the keyed pipeline (k_prep<true>,
 // k_ecmult_k4) with the id as their slot.  ParsePubKey is a pure function of
 // the 33 bytes, so the verdicts are the per-item ones (SURVEY.md §8f-2 within
@@ -643,7 +643,7 @@ __global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u
   }
 }
 
-// ------------------------------------------------------------ k_keys_build
+// ------------------------------------------------------------ key tables
 // Key arena (gv_keys_load): lane g parses key g of the load batch once and
 // writes its Q table to arena row base + g, the table's Z to kzq (8 rows of
 // stride kC) and the ParsePubKey verdict to kok.  A rejected key gets G's
@@ -664,24 +664,32 @@ GV_DEV void gej29_to_affine_words(fe& x8, fe& y8, const gej29& p) {
   f29_to_words(y8.v, y);
 }
 
-__global__ __launch_bounds__(256) void k_keys_build(u32 n, u32 C, const u32* in_x, const u32* in_pfx, u32 base,
-                                                     u32* kqt, u32* kzq, u32 kC, u32* kok, u32* qr, u32* kqt2,
-                                                     u32* kzq2) {
+// The key arena's tables are built in two launches so that the long serial
+// part runs one lane per key and the rest four lanes per key:
+//
+// k_keys_chain (lane = key): ParsePubKey (a rejected key gets G's tables,
+// never used: every item against it is false), then 100 doublings to
+// 2^35 Q, 2^70 Q, 2^100 Q.  Each group's base point is parked, as canonical
+// words x[8] y[8], in entry 0 of its own table row; the Jacobian Z of groups
+// 1..3 in their Z rows (kzq2), group 0 is affine.
+__global__ __launch_bounds__(256) void k_keys_chain(u32 n, u32 C, const u32* in_x, const u32* in_pfx, u32 base,
+                                                     u32* kqt, u32 kC, u32* kok, u32* kqt2, u32* kzq2) {
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n) return;                       // no cross-lane work below
-  fe x, y, zq;
+  if (g >= n) return;                       // no cross-lane work
+  fe x, y;
   load_fe(x, in_x, C, g);
   const bool ok = parse_pubkey(in_pfx[g], x, y);
   if (!ok) {
     fe_from_const(x, kGx);
     fe_from_const(y, kGy);
   }
-  build_q_table(kqt, base + g, qr, C, g, x, y, zq);
-  store_fe(kzq, kC, base + g, zq);
   kok[base + g] = ok ? 1u : 0u;
-  fe29 z0;                                  // every group table is rescaled to this Z
-  f29_from_words(z0, zq.v);
-  // the keyed latency schedule's group tables: 2^35 Q, 2^70 Q, 2^100 Q
+  auto park = [](u32* tab, u32 row, const u32* xw, const u32* yw) {
+    u32* p = tab + (size_t)row * GV_QTAB_N * GV_QENT_WORDS;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { p[i] = xw[i]; p[8 + i] = yw[i]; }
+  };
+  park(kqt, base + g, x.v, y.v);
   gej29 q;
   f29_from_words(q.x, x.v);
   f29_from_words(q.y, y.v);
@@ -690,29 +698,133 @@ __global__ __launch_bounds__(256) void k_keys_build(u32 n, u32 C, const u32* in_
   for (int grp = 1; grp < GV_LGRP; ++grp) {
 #pragma unroll 1
     for (int k = kLGrpBit[grp - 1]; k < kLGrpBit[grp]; ++k) gej29_double(q, q);   // never infinite: odd order
-    fe qx, qy;
-    gej29_to_affine_words(qx, qy, q);
-    const u32 row = (base + g) * GV_KEY2_TABLES + (grp - 1);
-    build_q_table(kqt2, row, qr, C, g, qx, qy, zq);
-    // entries (x, y) on Z_g -> (x rho^2, y rho^3) on Z_0, rho = Z_0 / Z_g: one
-    // shared Z for all four tables of the key, so a single accumulator can
-    // take entries of every group (k_ecmult_k4)
-    fe29 zg, rho, r2, r3;
-    f29_from_words(zg, zq.v);
-    f29_inv(rho, zg);
-    f29_mul(rho, rho, z0);
-    f29_sqr(r2, rho);
-    f29_mul(r3, r2, rho);
-#pragma unroll 1
-    for (int m = 0; m < GV_QTAB_N; ++m) {
-      fe29 ex, ey;
-      load_qent29(ex, ey, kqt2, row, m);
-      f29_mul(ex, ex, r2);
-      f29_mul(ey, ey, r3);
-      store_qent29(kqt2, row, m, ex, ey);
-    }
-    store_f29(kzq2 + (size_t)(grp - 1) * 8 * kC, kC, base + g, z0);
+    u32 xw[8], yw[8];
+    f29_to_words(xw, q.x);
+    f29_to_words(yw, q.y);
+    park(kqt2, (base + g) * GV_KEY2_TABLES + (grp - 1), xw, yw);
+    store_f29(kzq2 + (size_t)(grp - 1) * 8 * kC, kC, base + g, q.z);
   }
+}
+
+// k_keys_tables (lane L = 4 key + group, the four groups of a key in adjacent
+// lanes of one wave): the group's table from its parked base point (X, Y)
+// taken as affine -- the co-Z formulas never read the curve constant, so this
+// is the table of the point on the isomorphic curve y^2 = x^3 + 7 Z^6, i.e.
+// of the true point on table Z  E = Z_15 * Z.  The four lanes trade their E
+// (lane shuffles) right after the forward pass, and the back-propagation that
+// puts every entry on Z_15 also applies rho = the product of the other three
+// E's: all four tables end on the common Z = E_0 E_1 E_2 E_3, so ONE
+// accumulator can take entries of every group (k_ecmult_k4) -- no inversion
+// and no extra pass over the tables.  Same co-Z steps as build_q_table.
+// qr: Z-ratio scratch rows of stride C4 >= 4 n.
+__global__ __launch_bounds__(256) void k_keys_tables(u32 n, u32 C4, u32 base, u32* kqt, u32* kzq, u32 kC, u32* kqt2,
+                                                      u32* kzq2, u32* qr) {
+  const u32 L = blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 key = L >> 2, grp = L & 3u;
+  if (key >= n) return;                     // whole quads only: shuffles stay inside live quads
+  u32* tab = grp == 0u ? kqt : kqt2;
+  const u32 row = grp == 0u ? base + key : (base + key) * GV_KEY2_TABLES + (grp - 1u);
+  u32* zrow = grp == 0u ? kzq : kzq2 + (size_t)(grp - 1u) * 8 * kC;
+  fe29 qx, qy, X1, Y1, X2, Y2, t, u, prod;
+  {
+    const u32* p = tab + (size_t)row * GV_QTAB_N * GV_QENT_WORDS;
+    u32 w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = p[i];
+    f29_from_words(qx, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = p[8 + i];
+    f29_from_words(qy, w);
+  }
+  {
+    // co-Z doubling of (qx, qy): Z1 = 2y, 2Q = (M^2 - 2S, M(S - X) - 8y^4),
+    // Q' = (S, 8y^4) with S = 4xy^2, M = 3x^2.
+    fe29 B, E, Lq, M;
+    f29_sqr(B, qx);
+    f29_sqr(E, qy);
+    f29_sqr(Lq, E);
+    f29_add(t, qx, E);
+    f29_sqr(t, t);
+    f29_sub<1>(t, t, B);
+    f29_sub_norm<1>(t, t, Lq);
+    f29_shl_norm<1>(X1, t);
+    f29_mul3_norm(M, B);
+    f29_sqr(t, M);
+    f29_add(u, X1, X1);
+    f29_sub_norm<2>(X2, t, u);
+    f29_shl_norm<3>(Y1, Lq);
+    f29_sub<1>(t, X1, X2);
+    f29_mul(t, M, t);
+    f29_sub_norm<1>(Y2, t, Y1);
+  }
+  store_qent29(tab, row, 0, X1, Y1);        // 1*Q on Z1
+  store_qent29(tab, row, 1, X2, Y2);        // 2*Q on Z1
+  f29_add(prod, qy, qy);                    // Z1 = 2y; times every ratio below -> Z_15
+#pragma unroll 1
+  for (int m = 2; m < GV_QTAB_N; ++m) {     // (Q', mQ) -> ((m+1)Q, Q'')
+    fe29 h, rr, c, w1, w2, d, a1;
+    f29_sub_norm<1>(h, X1, X2);
+    store_ratio29(qr, C4, L, m - 2, h);     // Z_m / Z_{m-1}
+    f29_mul(prod, prod, h);
+    f29_sub_norm<1>(rr, Y1, Y2);
+    f29_sqr(c, h);
+    f29_mul(w1, X1, c);
+    f29_mul(w2, X2, c);
+    f29_sqr(d, rr);
+    f29_sub<1>(t, w1, w2);
+    f29_mul(a1, Y1, t);
+    f29_add(u, w1, w2);
+    f29_sub_norm<2>(X2, d, u);
+    f29_sub<1>(t, w1, X2);
+    f29_mul(t, rr, t);
+    f29_sub_norm<1>(Y2, t, a1);
+    X1 = w1;
+    Y1 = a1;
+    if (m + 1 < GV_QTAB_N) store_qent29(tab, row, m, X2, Y2);   // the last entry waits for rho
+  }
+  // E = Z_15 (times the parked Jacobian Z for groups 1..3); the quad's others
+  if (grp) {
+    fe29 z;
+    load_f29(z, zrow, kC, base + key);
+    f29_mul(prod, prod, z);
+  }
+  fe29 e1, e2, e3;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    e1.n[i] = (u32)__shfl_xor((int)prod.n[i], 1);
+    e2.n[i] = (u32)__shfl_xor((int)prod.n[i], 2);
+    e3.n[i] = (u32)__shfl_xor((int)prod.n[i], 3);
+  }
+  fe29 acc, zc;
+  f29_mul(acc, e1, e2);
+  f29_mul(acc, acc, e3);                    // rho
+  f29_mul(zc, acc, prod);                   // the common Z
+  {
+    fe29 a2, a3;                            // entry 16 (on Z_15): times rho^2, rho^3
+    f29_sqr(a2, acc);
+    f29_mul(a3, a2, acc);
+    f29_mul(X2, X2, a2);
+    f29_mul(Y2, Y2, a3);
+    store_qent29(tab, row, GV_QTAB_N - 1, X2, Y2);
+  }
+  // entry m (index m-1) on Z_{m-1} (m >= 2; entries 1, 2 on Z_1): times
+  // rho * Z_15 / Z_{m-1}
+#pragma unroll 1
+  for (int m = GV_QTAB_N - 1; m >= 1; --m) {
+    if (m >= 2) {
+      fe29 ratio;
+      load_ratio29(ratio, qr, C4, L, m - 2);
+      f29_mul(acc, acc, ratio);
+    }
+    fe29 x, y, a2, a3;
+    f29_sqr(a2, acc);
+    f29_mul(a3, a2, acc);
+    load_qent29(x, y, tab, row, m - 1);
+    f29_mul(x, x, a2);
+    f29_mul(y, y, a3);
+    store_qent29(tab, row, m - 1, x, y);
+  }
+  store_f29(zrow, kC, base + key, zc);
 }
 
 // Affine 2^35 G, 2^70 G, 2^100 G (16 words each) for the keyed ladder's G
@@ -1013,7 +1125,7 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult(const u32* gtab, 
 
 // ------------------------------------------------------------- k_ecmult_k4
 // Keyed batches: the key arena holds, per key, the tables of
-// Q, 2^35 Q, 2^70 Q and 2^100 Q on ONE shared Z (k_keys_build), and the
+// Q, 2^35 Q, 2^70 Q and 2^100 Q on ONE shared Z (k_keys_tables), and the
 // device holds the 20-bit-window tables of G, 2^35 G, 2^70 G, 2^100 G (and
 // lambda multiples).  Each 128-bit GLV half's 26 five-bit windows split into
 // the groups [0,7), [7,14), [14,20), [20,26); window w of group k sits at
@@ -1220,6 +1332,7 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
     uint32_t* w = b->digits;                   // rows 0..8
     uint32_t* pre = b->digits + (size_t)9 * C; // rows 9..17
     hipLaunchKernelGGL(gv::k_scalar_inv, dim3((waves + 3) / 4), blk, 0, st, C, b->in_s, w, pre);
+    if (b->keys_ready) (void)hipStreamWaitEvent(st, b->keys_ready, 0);   // grouped keys built beside s^-1
     if (b->ev[1]) (void)hipEventRecord(b->ev[1], st);
     if (b->kslot)   // keyed: in_pfx doubles as the clamped-slot row for k_ecmult
       hipLaunchKernelGGL(gv::k_prep<true>, grd, blk, 0, st, C, b->n, (const uint32_t*)nullptr,
@@ -1257,6 +1370,19 @@ hipError_t gvk_gen_glat(uint32_t* glat, hipStream_t st) {
   return hipGetLastError();
 }
 
+// The two key-table launches over n keys whose rows in_x / in_pfx (stride C)
+// are unpacked; qr: 14 x 9 ratio rows of stride round_up(4 n, 256).
+static hipError_t keys_tables_launch(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx,
+                                     uint32_t* qr, uint32_t base, uint32_t* kqt, uint32_t* kzq, uint32_t kC,
+                                     uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const uint32_t C4 = (4u * n + 255u) / 256u * 256u;
+  hipLaunchKernelGGL(gv::k_keys_chain, dim3((n + 255) / 256), dim3(256), 0, st, n, C, in_x, in_pfx, base, kqt, kC,
+                     kok, kqt2, kzq2);
+  hipLaunchKernelGGL(gv::k_keys_tables, dim3(C4 / 256), dim3(256), 0, st, n, C4, base, kqt, kzq, kC, kqt2, kzq2, qr);
+  return hipGetLastError();
+}
+
 hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
                           uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t base,
                           uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2,
@@ -1264,9 +1390,7 @@ hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t
   const dim3 blk(256), grd(C / 256);
   hipLaunchKernelGGL(gv::k_unpack, grd, blk, 0, st, pub33, (const uint8_t*)nullptr, (const uint8_t*)nullptr, n, C,
                      in_x, in_pfx, in_r, in_s, in_e);
-  hipLaunchKernelGGL(gv::k_keys_build, grd, blk, 0, st, n, C, (const uint32_t*)in_x, (const uint32_t*)in_pfx, base,
-                     kqt, kzq, kC, kok, qr, kqt2, kzq2);
-  return hipGetLastError();
+  return keys_tables_launch(n, C, in_x, in_pfx, qr, base, kqt, kzq, kC, kok, kqt2, kzq2, st);
 }
 
 hipError_t gvk_keys_point(uint32_t n, const uint32_t* slots, const uint32_t* kqt, const uint32_t* kzq, uint32_t kC,
@@ -1305,9 +1429,7 @@ hipError_t gvk_dedupe(uint32_t n, uint32_t C, const uint32_t* x, const uint32_t*
 hipError_t gvk_keys_build_rows(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx, uint32_t* qr,
                                uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2,
                                uint32_t* kzq2, hipStream_t st) {
-  hipLaunchKernelGGL(gv::k_keys_build, dim3(C / 256), dim3(256), 0, st, n, C, in_x, in_pfx, 0u, kqt, kzq, kC, kok, qr,
-                     kqt2, kzq2);
-  return hipGetLastError();
+  return keys_tables_launch(n, C, in_x, in_pfx, qr, 0u, kqt, kzq, kC, kok, kqt2, kzq2, st);
 }
 
 #if GV_STAMP

@@ -291,7 +291,7 @@ GV_DEV void lat_pubkey_and_tables(LatShared& sh, int sig, int slot, bool live, c
 
 
 // Wave 0 prep for a keyed signature (gv_keys_load): the Q table comes from the
-// key arena row (built once per key by k_keys_build, same effective-affine
+// key arena row (built once per key by k_keys_chain + k_keys_tables, same effective-affine
 // form and Z), so no square root and no table build.  Lane 4s + k copies
 // entries k, k+4, k+8, k+12 and forms their lambda*Q entries (beta*x, y).
 GV_DEV void lat_keyed_tables(LatShared& sh, int sig, int slot, bool live, u32 kslot, const u32* kqt,

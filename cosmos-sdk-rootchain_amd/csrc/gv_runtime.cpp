@@ -251,8 +251,10 @@ struct Set {
   hipStream_t last_st = nullptr;
   hipEvent_t done = nullptr;                      // host path: chunk finished (bits on host)
   hipEvent_t ecm_ready = nullptr;                 // pipelined device calls: front kernels done
+  hipStream_t side = nullptr;                     // grouped keys: table builds beside k_scalar_inv
+  hipEvent_t fork = nullptr, keys_done = nullptr;
   // in-batch key grouping: the per-batch key arena (tables of the batch's
-  // distinct keys, k_keys_build layout) for up to gcap keys, and the count
+  // distinct keys, key-arena layout) for up to gcap keys, and the count
   uint32_t *g_kqt = nullptr, *g_kzq = nullptr, *g_kok = nullptr, *g_kqt2 = nullptr, *g_kzq2 = nullptr;
   size_t gcap = 0;
   uint32_t* h_count = nullptr;                    // pinned: the distinct-key count read back
@@ -571,8 +573,8 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   uint32_t *rep = q, *uid = q + C, *kslot = q + 2 * C, *count = q + 3 * C, *table = q + 3 * C + 256;
   uint32_t* kx = table + T;
   uint32_t* kpfx = kx + 8 * capU;
-  uint32_t* qr = kpfx + capU;
-  if ((size_t)(qr + (GV_QTAB_N - 1) * 9 * capU - q) > (size_t)GV_QTAB_WORDS * C) return GV_OK;   // no room: pub33
+  uint32_t* qr = kpfx + capU;                   // ratio rows of the 4-lanes-per-key table build
+  if ((size_t)(qr + (GV_QTAB_N - 1) * 9 * 4 * capU - q) > (size_t)GV_QTAB_WORDS * C) return GV_OK;   // no room: pub33
   if (!s->h_count && hipHostMalloc((void**)&s->h_count, 64, hipHostMallocDefault) != hipSuccess) {
     s->h_count = nullptr;
     return GV_ENOMEM;
@@ -588,8 +590,14 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   if (U == 0 || U * ctx->group_div > n || U > capU) return GV_OK;   // many distinct keys: the pub33 pipeline
   if ((rc = ensure_gtab4(ctx, d, s, st))) return rc;
   if ((rc = ensure_group_arena(s, capU))) return rc == GV_ENOMEM ? GV_OK : rc;
+  // the tables are built on the set's side stream while k_scalar_inv (which
+  // does not read keys) runs on st: both are one wave per SIMD or so
+  CK(hipEventRecord(s->fork, st));
+  CK(hipStreamWaitEvent(s->side, s->fork, 0));
   CK(gvk_keys_build_rows((uint32_t)U, (uint32_t)capU, kx, kpfx, qr, s->g_kqt, s->g_kzq, (uint32_t)capU,
-                         s->g_kok, s->g_kqt2, s->g_kzq2, st));
+                         s->g_kok, s->g_kqt2, s->g_kzq2, s->side));
+  CK(hipEventRecord(s->keys_done, s->side));
+  b.keys_ready = s->keys_done;
   b.pub33 = nullptr;
   b.kslot = kslot; b.kqt = s->g_kqt; b.kzq = s->g_kzq; b.kok = s->g_kok;
   b.kC = (uint32_t)capU; b.kcount = (uint32_t)U;
@@ -1080,6 +1088,9 @@ void free_set(Set& s) {
   if (s.last) (void)hipEventDestroy(s.last);
   if (s.done) (void)hipEventDestroy(s.done);
   if (s.ecm_ready) (void)hipEventDestroy(s.ecm_ready);
+  if (s.fork) (void)hipEventDestroy(s.fork);
+  if (s.keys_done) (void)hipEventDestroy(s.keys_done);
+  if (s.side) { (void)hipStreamSynchronize(s.side); (void)hipStreamDestroy(s.side); }
   for (uint32_t* p : {s.g_kqt, s.g_kzq, s.g_kok, s.g_kqt2, s.g_kzq2})
     if (p) (void)hipFree(p);
   if (s.h_count) (void)hipHostFree(s.h_count);
@@ -1135,7 +1146,10 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
       ok = ok && hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) == hipSuccess &&
            hipEventCreateWithFlags(&s.last, hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&s.ecm_ready, hipEventDisableTiming) == hipSuccess;
+           hipEventCreateWithFlags(&s.ecm_ready, hipEventDisableTiming) == hipSuccess &&
+           hipStreamCreateWithFlags(&s.side, hipStreamNonBlocking) == hipSuccess &&
+           hipEventCreateWithFlags(&s.fork, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&s.keys_done, hipEventDisableTiming) == hipSuccess;
     // pipelined device-resident calls: front kernels on two low-priority
     // streams (alternating sets), every ladder on one high-priority stream
     int lo_prio = 0, hi_prio = 0;
@@ -1311,11 +1325,14 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
     for (size_t c0 = 0; c0 < n; c0 += ctx->max_batch) {
       const size_t cn = std::min(ctx->max_batch, n - c0);
       const size_t C = round_up(cn, 256);
-      if ((rc = ensure_cap(s, C))) return rc;
+      // scratch: the ratio rows of the 4-lanes-per-key table build (stride 4C)
+      // start the set's Q-table region, which must then hold 4 x 135 rows
+      const size_t Cs = std::max(C, round_up((size_t)4 * (GV_QTAB_N - 1) * 9 * C / GV_QTAB_WORDS + 1, 256));
+      if ((rc = ensure_cap(s, Cs))) return rc;
       if ((rc = set_acquire(s, st))) return rc;
       CK(hipMemcpyAsync(s->d_in, pub33 + c0 * 33, cn * 33, hipMemcpyHostToDevice, st));
       CK(gvk_keys_build(s->d_in, (uint32_t)cn, (uint32_t)C, s->in_x, s->in_pfx, s->in_r, s->in_s, s->in_e,
-                        s->qtab + C * GV_QTAB_N * GV_QENT_WORDS, (uint32_t)(base + c0), d->kqt, d->kzq,
+                        s->qtab, (uint32_t)(base + c0), d->kqt, d->kzq,
                         (uint32_t)d->kcap, d->kok, d->kqt2, d->kzq2, st));
       if ((rc = set_release(s, st))) return rc;
       CK(hipStreamSynchronize(st));            // the caller's pub33 chunk is read by then

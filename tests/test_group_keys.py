@@ -1,5 +1,5 @@
 """In-batch key grouping (gv_set_option "group_keys"): a pub33 batch whose
-items repeat keys parses each distinct key once (k_dedupe*, k_keys_build into a
+items repeat keys parses each distinct key once (k_dedupe*, k_keys_chain + k_keys_tables into a
 per-batch arena) and runs the keyed pipeline.  The verdicts must be exactly the
 per-item pub33 pipeline's -- including keys that ParsePubKey rejects (repeated
 bad prefixes, x >= p, non-residue x), which get a slot too and make every item
