@@ -291,6 +291,8 @@ struct Dev {
   int id = 0;
   uint32_t* gtab = nullptr;
   Set set[2];
+  Set gset;                                       // host slices: whole-slice key grouping (slice_group)
+  hipEvent_t grp_ready = nullptr;
   // key arena (gv_keys_load): Q table rows, table Z (8 rows of stride kcap), verdicts
   uint32_t *kqt = nullptr, *kzq = nullptr, *kok = nullptr;
   uint32_t *kqt2 = nullptr, *kzq2 = nullptr;      // the keyed latency schedule's group tables (2^35 Q, ...)
@@ -607,18 +609,28 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   return GV_OK;
 }
 
+// A key arena other than the device's gv_keys_load arena: a host slice's
+// grouped keys (slice_group).  The launch stream waits on `ready` first.
+struct KeyArena {
+  const uint32_t *kqt, *kzq, *kok, *kqt2, *kzq2;
+  uint32_t kC, kcount;
+  const uint32_t* gtab4;
+  hipEvent_t ready;
+};
+
 // Launch the pipeline for n items whose inputs already sit on the device, on
 // set s's scratch, stream st.  The caller holds d->mu.
 // st_ecm (pipelined device-resident calls): the ladder runs there, after the
 // front kernels on st; the set's scratch is released on st_ecm.
 int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint8_t* sig, const uint8_t* dig,
            const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint64_t* bits_out,
-           hipStream_t st, const uint32_t* kslot = nullptr, uint8_t* out8 = nullptr, hipStream_t st_ecm = nullptr) {
+           hipStream_t st, const uint32_t* kslot = nullptr, uint8_t* out8 = nullptr, hipStream_t st_ecm = nullptr,
+           const KeyArena* ka = nullptr) {
   if (n == 0 || n > kMaxItems) return GV_EINVAL;
   const size_t C = round_up(n, 256);
   int rc = ensure_cap(s, C);
   if (rc) return rc;
-  if (kslot) {                                  // the arena always exists for a keyed batch
+  if (kslot && !ka) {                           // the arena always exists for a keyed batch
     rc = ensure_keys(d, 1, ctx->keys, st);
     if (rc) return rc;
   }
@@ -633,7 +645,15 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
   b.in_x = s->in_x; b.in_pfx = s->in_pfx; b.in_r = s->in_r; b.in_s = s->in_s; b.in_e = s->in_e;
   b.digits = s->digits; b.zq = s->zq; b.flags = s->flags; b.qtab = s->qtab;
   b.bits = bits_out;
-  if (kslot) {
+  const uint32_t* kzq2 = d->kzq2;
+  if (kslot && ka) {                            // a host slice's grouped keys
+    b.pub33 = nullptr;
+    b.kslot = kslot; b.kqt = ka->kqt; b.kzq = ka->kzq; b.kok = ka->kok;
+    b.kC = ka->kC; b.kcount = ka->kcount;
+    b.kqt2 = ka->kqt2; b.gtab4 = ka->gtab4;
+    kzq2 = ka->kzq2;
+    if (ka->ready) CK(hipStreamWaitEvent(st, ka->ready, 0));
+  } else if (kslot) {
     b.pub33 = nullptr;
     b.kslot = kslot; b.kqt = d->kqt; b.kzq = d->kzq; b.kok = d->kok;
     b.kC = (uint32_t)d->kcap; b.kcount = (uint32_t)ctx->keys;
@@ -671,7 +691,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     if (out8 && !sliced) return GV_EINVAL;      // byte verdicts: the sliced kernels only
     lb.out8 = out8;
     if (kslot) {                                // keyed: 16 lanes per signature (group tables)
-      lb.kqt2 = d->kqt2; lb.kzq2 = d->kzq2; lb.glat = d->glat;
+      lb.kqt2 = b.kqt2; lb.kzq2 = kzq2; lb.glat = d->glat;
       if (sliced) CK(gvk_verify_lat16_sl(&lb, st));
       else CK(gvk_verify_lat16(&lb, st));
     } else if (sliced) {
@@ -745,6 +765,9 @@ struct HostBatch {
   uint8_t* out_ok;
   uint64_t* out_bits;
   bool pinned = false;          // digest inputs in pinned host memory (gv_host_alloc): no staging copy
+  const uint32_t* d_slots = nullptr;   // slice grouping: per-item key ids on the device (offset lo)
+  const KeyArena* ka = nullptr;        // ... and the arena they index
+  size_t d_slots_lo = 0;
 };
 
 // Host memory the device can read directly (hipHostMalloc / gv_host_alloc /
@@ -800,7 +823,9 @@ int harvest(Dev* d, Set* s, const HostBatch& hb) {
 // kernels -> D2H of the bitmap on the set's stream.
 int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& hb) {
   const size_t C = round_up(cn, 256);
-  const bool keyed = hb.slots != nullptr, msgs = hb.dig32 == nullptr;
+  const bool dslots = hb.d_slots != nullptr;    // slice grouping: slots already on the device
+  const bool keyed = hb.slots != nullptr || dslots, msgs = hb.dig32 == nullptr;
+  const uint32_t* dsl = dslots ? hb.d_slots + (c0 - hb.d_slots_lo) : nullptr;
   int rc = ensure_cap(s, C);
   if (rc) return rc;
   const InLayout L = in_layout(C, keyed, msgs);
@@ -815,7 +840,7 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
     const uint8_t* dp = hb.dig32 + c0 * 32;
     const size_t lmax = keyed ? ctx->lat_max_keyed : ctx->lat_max;
     const size_t slmax = keyed ? ctx->lat_sl_max_keyed : ctx->lat_sl_max;
-    if (ctx->lat_zero_copy && ctx->lat_sliced && cn <= slmax && cn <= lmax) {
+    if (ctx->lat_zero_copy && ctx->lat_sliced && cn <= slmax && cn <= lmax && !dslots) {
       if ((rc = ensure_pinned(&s->h_out8, &s->h_out8_cap, cn))) return rc;
       rc = launch(ctx, d, s, cn, keyed ? nullptr : kp, sp, dp, nullptr, nullptr, nullptr, nullptr, s->st,
                   keyed ? (const uint32_t*)kp : nullptr, s->h_out8);
@@ -828,12 +853,12 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
       return GV_OK;
     }
     if ((rc = set_acquire(s, s->st))) return rc;
-    CK(hipMemcpyAsync(s->d_in, kp, cn * (keyed ? 4 : 33), hipMemcpyHostToDevice, s->st));
+    if (!dslots) CK(hipMemcpyAsync(s->d_in, kp, cn * (keyed ? 4 : 33), hipMemcpyHostToDevice, s->st));
     CK(hipMemcpyAsync(s->d_in + L.sig, sp, cn * 64, hipMemcpyHostToDevice, s->st));
     CK(hipMemcpyAsync(s->d_in + L.third, dp, cn * 32, hipMemcpyHostToDevice, s->st));
     const uint8_t* din = s->d_in;
     rc = launch(ctx, d, s, cn, keyed ? nullptr : din, din + L.sig, din + L.third, nullptr, nullptr, nullptr, s->bits,
-                s->st, keyed ? (const uint32_t*)din : nullptr);
+                s->st, dslots ? dsl : keyed ? (const uint32_t*)din : nullptr, nullptr, nullptr, hb.ka);
     if (rc) return rc;
     CK(hipMemcpyAsync(s->h_bits, s->bits, ((cn + 63) / 64) * 8, hipMemcpyDeviceToHost, s->st));
     CK(hipEventRecord(s->done, s->st));
@@ -845,13 +870,14 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
     return GV_OK;
   }
   if (!msgs) {                              // keys/slots, signatures, digests: one pool pass
-    const CopySeg segs[3] = {keyed ? CopySeg{h, (const uint8_t*)(hb.slots + c0), cn * 4}
-                                   : CopySeg{h, hb.pub33 + c0 * 33, cn * 33},
-                             CopySeg{h + L.sig, hb.sig64 + c0 * 64, cn * 64},
-                             CopySeg{h + L.third, hb.dig32 + c0 * 32, cn * 32}};
-    par_copy_segs(d->pool, segs, 3);
+    const CopySeg segs[3] = {CopySeg{h + L.sig, hb.sig64 + c0 * 64, cn * 64},
+                             CopySeg{h + L.third, hb.dig32 + c0 * 32, cn * 32},
+                             keyed ? CopySeg{h, (const uint8_t*)(hb.slots + c0), cn * 4}
+                                   : CopySeg{h, hb.pub33 + c0 * 33, cn * 33}};
+    par_copy_segs(d->pool, segs, dslots ? 2 : 3);
   } else {
-    if (keyed) par_copy(d->pool, h, hb.slots + c0, cn * 4);
+    if (dslots) {
+    } else if (keyed) par_copy(d->pool, h, hb.slots + c0, cn * 4);
     else par_copy(d->pool, h, hb.pub33 + c0 * 33, cn * 33);
     par_copy(d->pool, h + L.sig, hb.sig64 + c0 * 64, cn * 64);
     uint64_t lo = UINT64_MAX, hi = 0;
@@ -871,7 +897,7 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
   }
   const size_t lmax = keyed ? ctx->lat_max_keyed : ctx->lat_max;
   const size_t slmax = keyed ? ctx->lat_sl_max_keyed : ctx->lat_sl_max;
-  if (ctx->lat_zero_copy && ctx->lat_sliced && cn <= slmax && cn <= lmax) {
+  if (ctx->lat_zero_copy && ctx->lat_sliced && cn <= slmax && cn <= lmax && !dslots) {
     // zero-copy small batch: the kernel reads the pinned staging buffers
     // (messages too: its scalar wave hashes them) and writes one verdict byte
     // per item to pinned memory (no H2D / memset / D2H)
@@ -889,13 +915,17 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
     return GV_OK;
   }
   if ((rc = set_acquire(s, s->st))) return rc;
-  CK(hipMemcpyAsync(s->d_in, h, msgs ? L.total : L.third + cn * 32, hipMemcpyHostToDevice, s->st));
+  {
+    const size_t from = dslots ? L.sig : 0;   // device slots: no key region to send
+    CK(hipMemcpyAsync(s->d_in + from, h + from, (msgs ? L.total : L.third + cn * 32) - from, hipMemcpyHostToDevice,
+                      s->st));
+  }
   if (msgs && hb_bytes) CK(hipMemcpyAsync(s->d_blob, s->h_blob, hb_bytes, hipMemcpyHostToDevice, s->st));
   const uint8_t* din = s->d_in;
   rc = launch(ctx, d, s, cn, keyed ? nullptr : din, din + L.sig, msgs ? nullptr : din + L.third,
               msgs ? s->d_blob : nullptr, msgs ? (const uint64_t*)(din + L.third) : nullptr,
               msgs ? (const uint32_t*)(din + L.len) : nullptr, s->bits, s->st,
-              keyed ? (const uint32_t*)din : nullptr);
+              dslots ? dsl : keyed ? (const uint32_t*)din : nullptr, nullptr, nullptr, hb.ka);
   if (rc) return rc;
   CK(hipMemcpyAsync(s->h_bits, s->bits, ((cn + 63) / 64) * 8, hipMemcpyDeviceToHost, s->st));
   CK(hipEventRecord(s->done, s->st));
@@ -905,6 +935,74 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
   s->c0 = c0;
   s->cn = cn;
   return GV_OK;
+}
+
+// Does a host slice repeat its keys enough for grouping?  Birthday count on a
+// pseudo-random sample of m keys: at average multiplicity k the sample holds
+// about m^2 (k - 1) / 2n repeated keys; take the route when a quarter of the
+// count expected at k = group_div is there (a strided sample would miss
+// round-robin key orders).
+bool worth_grouping(const uint8_t* pub33, size_t n, int div) {
+  const size_t m = std::min<size_t>(n, 4096);
+  std::vector<uint64_t> h(m);
+  uint64_t r = 0x9E3779B97F4A7C15ull;
+  for (size_t i = 0; i < m; ++i) {
+    r ^= r << 13; r ^= r >> 7; r ^= r << 17;
+    const uint8_t* p = pub33 + (r % n) * 33;
+    uint64_t v;
+    memcpy(&v, p + 1, 8);
+    h[i] = v ^ ((uint64_t)p[0] * 0xFF51AFD7ED558CCDull) ^ ((uint64_t)p[25] << 32 | p[32]);
+  }
+  std::sort(h.begin(), h.end());
+  size_t dups = 0;
+  for (size_t i = 1; i < m; ++i) dups += h[i] == h[i - 1];
+  const double expect = (double)m * (double)m * (double)(div - 1) / (2.0 * (double)n);
+  return (double)dups >= std::max(1.0, expect / 4);
+}
+
+// Whole-slice key grouping for a pub33 host slice [lo, lo + n): the slice's
+// keys are sent once (pageable input staged in pieces, each piece's H2D right
+// behind its copy), unpacked and grouped over the WHOLE slice -- so the key
+// tables are built once per slice, not once per pipeline chunk -- and when
+// the slice has few enough distinct keys the chunks then run keyed: only
+// signatures and digests (or messages) travel per chunk, the slots stay on
+// the device.  *ka is filled and *d_slots set when the route is taken.
+int slice_group(gv_ctx* ctx, Dev* d, size_t lo, size_t n, const HostBatch& hb, KeyArena* ka,
+                const uint32_t** d_slots) {
+  *d_slots = nullptr;
+  if (!worth_grouping(hb.pub33 + lo * 33, n, ctx->group_div)) return GV_OK;
+  Set* g = &d->gset;
+  const size_t C = round_up(n, 256);
+  int rc = ensure_cap(g, C);
+  if (rc) return rc;
+  if ((rc = set_acquire(g, g->st))) return rc;
+  const uint8_t* src = hb.pub33 + lo * 33;
+  if (hb.pinned) {
+    CK(hipMemcpyAsync(g->d_in, src, n * 33, hipMemcpyHostToDevice, g->st));
+  } else {
+    if ((rc = ensure_pinned(&g->h_in, &g->h_in_cap, n * 33))) return rc;
+    const size_t piece = round_up((n + 3) / 4, 256) * 33;
+    for (size_t o = 0; o < n * 33; o += piece) {
+      const size_t b = std::min(piece, n * 33 - o);
+      par_copy(d->pool, g->h_in + o, src + o, b);
+      CK(hipMemcpyAsync(g->d_in + o, g->h_in + o, b, hipMemcpyHostToDevice, g->st));
+    }
+  }
+  gvk_batch b;
+  memset(&b, 0, sizeof b);
+  b.n = (uint32_t)n; b.C = (uint32_t)C;
+  b.pub33 = g->d_in;
+  b.in_x = g->in_x; b.in_pfx = g->in_pfx; b.in_r = g->in_r; b.in_s = g->in_s; b.in_e = g->in_e;
+  if ((rc = group_keys(ctx, d, g, b, n, g->st))) return rc;
+  if (!b.kslot) return set_release(g, g->st);   // many distinct keys after all: per-chunk pipeline
+  if (!d->grp_ready) CK(hipEventCreateWithFlags(&d->grp_ready, hipEventDisableTiming));
+  CK(hipStreamWaitEvent(g->st, b.keys_ready, 0));
+  CK(hipEventRecord(d->grp_ready, g->st));
+  ka->kqt = b.kqt; ka->kzq = b.kzq; ka->kok = b.kok; ka->kqt2 = b.kqt2; ka->kzq2 = g->g_kzq2;
+  ka->kC = b.kC; ka->kcount = b.kcount; ka->gtab4 = b.gtab4;
+  ka->ready = d->grp_ready;
+  *d_slots = b.kslot;
+  return GV_OK;   // the set stays acquired until run_slice releases it after the last chunk
 }
 
 // Verify items [lo, hi) of a host batch on one device: chunks alternate
@@ -949,19 +1047,38 @@ int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const HostBatch& hb) {
     for (size_t c0 = 0; c0 < n; c0 += chunk) sizes.push_back(std::min(chunk, n - c0));
   }
   int rc = GV_OK;
+  // a pub33 slice big enough for the pipeline: group its keys once for all chunks
+  HostBatch hg = hb;
+  KeyArena ka;
+  bool grouped = false;
+  if (hb.pub33 && !hb.slots && ctx->group_keys && n >= ctx->group_min && sizes.size() > 1) {
+    const uint32_t* dsl = nullptr;
+    if ((rc = slice_group(ctx, d, lo, n, hb, &ka, &dsl))) return rc;
+    if (dsl) {
+      grouped = true;
+      hg.d_slots = dsl;
+      hg.d_slots_lo = lo;
+      hg.ka = &ka;
+    }
+  }
+  const HostBatch& hr = grouped ? hg : hb;
   int k = 0;
   size_t c0 = lo;
   for (size_t i = 0; i < sizes.size() && rc == GV_OK; c0 += sizes[i], ++i, k ^= 1) {
     Set* s = &d->set[k];
-    if (s->busy && (rc = harvest(d, s, hb))) break;
-    rc = submit(ctx, d, s, c0, sizes[i], hb);
+    if (s->busy && (rc = harvest(d, s, hr))) break;
+    rc = submit(ctx, d, s, c0, sizes[i], hr);
   }
   for (Set& s : d->set)                          // drain (also after an error)
     if (s.busy) {
-      const int r2 = harvest(d, &s, hb);
+      const int r2 = harvest(d, &s, hr);
       if (rc == GV_OK) rc = r2;
       s.busy = false;
     }
+  if (grouped) {                                  // every chunk done: the slice's arena is free
+    const int r2 = set_release(&d->gset, d->gset.st);
+    if (rc == GV_OK) rc = r2;
+  }
   return rc;
 }
 
@@ -1142,14 +1259,14 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
     d->pool = ctx->pool;
     if (k > 0) d->worker = new Worker();
     bool ok = hipSetDevice(d->id) == hipSuccess;
-    for (Set& s : d->set)
-      ok = ok && hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) == hipSuccess &&
-           hipEventCreateWithFlags(&s.last, hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&s.ecm_ready, hipEventDisableTiming) == hipSuccess &&
-           hipStreamCreateWithFlags(&s.side, hipStreamNonBlocking) == hipSuccess &&
-           hipEventCreateWithFlags(&s.fork, hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&s.keys_done, hipEventDisableTiming) == hipSuccess;
+    for (Set* sp : {&d->set[0], &d->set[1], &d->gset})
+      ok = ok && hipStreamCreateWithFlags(&sp->st, hipStreamNonBlocking) == hipSuccess &&
+           hipEventCreateWithFlags(&sp->last, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&sp->done, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&sp->ecm_ready, hipEventDisableTiming) == hipSuccess &&
+           hipStreamCreateWithFlags(&sp->side, hipStreamNonBlocking) == hipSuccess &&
+           hipEventCreateWithFlags(&sp->fork, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&sp->keys_done, hipEventDisableTiming) == hipSuccess;
     // pipelined device-resident calls: front kernels on two low-priority
     // streams (alternating sets), every ladder on one high-priority stream
     int lo_prio = 0, hi_prio = 0;
@@ -1175,6 +1292,8 @@ void gv_close(gv_ctx* ctx) {
     delete d->worker;
     (void)hipSetDevice(d->id);
     for (Set& s : d->set) free_set(s);
+    free_set(d->gset);
+    if (d->grp_ready) (void)hipEventDestroy(d->grp_ready);
     if (d->gtab) (void)hipFree(d->gtab);
     if (d->glat) (void)hipFree(d->glat);
     if (d->gtab4) (void)hipFree(d->gtab4);

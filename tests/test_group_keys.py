@@ -88,3 +88,42 @@ def test_grouped_device_resident_and_message_path(ver):
     msgs = mm * reps
     got, ref, grouped = grouped_vs_plain(ver, pub, sig, None, msgs=msgs)
     assert grouped >= 1 and np.array_equal(got, np.tile(mok, reps)) and np.array_equal(ref, got)
+
+
+def test_host_slice_grouped_once_for_all_chunks(ver):
+    """Host-buffer batches past the pipeline bound: the slice's keys are sent
+    and grouped ONCE (slice_group), every chunk then runs keyed with the slots
+    on the device -- pageable and pinned inputs, digests and messages, and a
+    unique-key slice that must keep the per-chunk pub33 route."""
+    pub, sig, dig, exp = bench.make_digest_workload(600_000, 0x6D, 4096, 0.25, 16)
+    b0, _ = ver.group_stats()
+    got = ver.verify_batch_digests(pub, sig, dig)
+    b1, k1 = ver.group_stats()
+    assert b1 - b0 == 1                          # one grouping for the whole slice, not one per chunk
+    assert np.array_equal(got, exp)
+    hp = [ver.host_array(a.shape, a.dtype) for a in (pub, sig, dig)]
+    for h, a in zip(hp, (pub, sig, dig)):
+        h[...] = a
+    bits = ver.verify_batch_digests_bits(*hp)
+    for h in hp:
+        ver.host_free(h)
+    assert ver.group_stats()[0] - b1 == 1
+    assert np.array_equal(bench.unpack_bits(bits, len(exp)), exp)
+    idx = np.random.default_rng(7).choice(len(exp), 3000, replace=False)
+    assert np.array_equal(O.verify_digests(pub[idx], sig[idx], dig[idx], threads=16), got[idx])
+    # message path: goldens tiled (every rejection class), shuffled
+    from golden_io import load_msg_vectors
+    mp, ms, mm, mok, _ = load_msg_vectors()
+    reps = max(1, 200_000 // len(mp))
+    perm = np.random.default_rng(8).permutation(reps * len(mp))
+    pub2, sig2 = np.tile(mp, (reps, 1))[perm], np.tile(ms, (reps, 1))[perm]
+    msgs = [(mm * reps)[i] for i in perm]
+    b2, _ = ver.group_stats()
+    got2 = ver.verify_batch_msgs(pub2, sig2, msgs)
+    assert ver.group_stats()[0] - b2 == 1
+    assert np.array_equal(got2, np.tile(mok, reps)[perm])
+    # unique keys: no slice grouping
+    pub3, sig3, dig3, exp3 = bench.make_digest_workload(300_000, 0x6E, 300_000, 0.1, 16)
+    b3, _ = ver.group_stats()
+    assert np.array_equal(ver.verify_batch_digests(pub3, sig3, dig3), exp3)
+    assert ver.group_stats()[0] == b3
