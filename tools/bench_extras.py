@@ -263,23 +263,11 @@ def msg_path(ver, wl, n: int, threads: int, nkeys: int = 10000, steps: int = 3):
     return out
 
 
-def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: int = 64, steady_blocks: int = 4,
-            wl=None, threads: int = 16):
-    """BASELINE.json configs[0] shape: 10k single-signer bank MsgSend txs (amino
-    StdTx) through the host mirror: the block path (DeliverBlock = PreVerifyTxs,
-    one GPU batch, then the DeliverTx ante loop) -- the first block (every
-    account's pubkey arrives in its tx: SetPubKey, cold caches) and
-    `steady_blocks` further blocks (sequences 1.., keys on the accounts) --
-    the per-tx path with no batching (one GPU call per tx) and the CheckTx
-    accumulation window (txs submitted from concurrent threads).  Sign bytes
-    and signatures come from tools/workload (C, OpenSSL); the amino tx bytes
-    from txkit."""
-    import threading
-    import gvhost
+def c1_blocks(wl, ntx: int = 10000, steady_blocks: int = 4, threads: int = 16):
+    """The C1 workload: ntx single-signer MsgSend txs per block, block 0 with
+    every account's pubkey in its tx (SetPubKey), blocks 1..steady_blocks at
+    sequences 1.. (amino StdTx bytes, one contiguous buffer per block)."""
     import txkit as T
-    if wl is None:
-        import bench
-        wl = bench.workload_lib()
     nk = ntx + 1
     priv = np.zeros((nk, 32), np.uint8)
     pubk = np.zeros((nk, 33), np.uint8)
@@ -293,6 +281,7 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: in
                                          ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
     wl.gvw_sha256_msgs.argtypes = [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                    ctypes.c_void_p]
+    raw = {}
 
     def block(seq):
         cap = ntx * 512
@@ -312,7 +301,6 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: in
         raw[seq] = (blob, off, ln, sig)
         return [T.std_tx([T.MsgSend(addrs[i], addrs[i + 1], [(10, "foocoin")])], fee, "",
                          [(amino[i] if seq == 0 else b"", sig[i].tobytes())]) for i in range(ntx)]
-    raw = {}
     txs = block(0)
     later = [block(seq) for seq in range(1, steady_blocks + 1)]
 
@@ -321,8 +309,29 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: in
         offs = np.zeros(len(ts), np.uint64)
         offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
         return np.frombuffer(b"".join(ts), np.uint8).copy(), offs, lens
-    first_blob = packed(txs)
-    later_blobs = [packed(b) for b in later]
+    return {"txs": txs, "first_blob": packed(txs), "later_blobs": [packed(b) for b in later], "keys": keys,
+            "raw": raw, "pubk": pubk}
+
+
+def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: int = 64, steady_blocks: int = 4,
+            wl=None, threads: int = 16):
+    """BASELINE.json configs[0] shape: 10k single-signer bank MsgSend txs (amino
+    StdTx) through the host mirror: the block path (DeliverBlock = PreVerifyTxs,
+    one GPU batch, then the DeliverTx ante loop) -- the first block (every
+    account's pubkey arrives in its tx: SetPubKey, cold caches) and
+    `steady_blocks` further blocks (sequences 1.., keys on the accounts) --
+    the per-tx path with no batching (one GPU call per tx) and the CheckTx
+    accumulation window (txs submitted from concurrent threads).  Sign bytes
+    and signatures come from tools/workload (C, OpenSSL); the amino tx bytes
+    from txkit."""
+    import threading
+    import gvhost
+    if wl is None:
+        import bench
+        wl = bench.workload_lib()
+    W = c1_blocks(wl, ntx, steady_blocks, threads)
+    txs, first_blob, later_blobs, keys, raw, pubk = (W[k] for k in ("txs", "first_blob", "later_blobs", "keys",
+                                                                    "raw", "pubk"))
 
     def fresh_app():
         app = gvhost.HostApp(ver, chain_id="gv-bench", height=1)
@@ -348,11 +357,11 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: in
     t_steady = time.perf_counter() - t
     st2 = app.stats()
     app.close()
-    steady = {"blocks": len(later), "txs_per_s": round(ntx * len(later) / t_steady, 1),
-              "ms_per_block": round(t_steady / len(later) * 1e3, 2), "accepted": acc_steady,
-              "preverify_ms_per_block": round((st2["preverify_ns"] - st["preverify_ns"]) / 1e6 / len(later), 2),
-              "gpu_ms_per_block": round((st2["gpu_ns"] - st["gpu_ns"]) / 1e6 / len(later), 2),
-              "ante_loop_ms_per_block": round((st2["deliver_loop_ns"] - st["deliver_loop_ns"]) / 1e6 / len(later), 2)}
+    steady = {"blocks": len(later_blobs), "txs_per_s": round(ntx * len(later_blobs) / t_steady, 1),
+              "ms_per_block": round(t_steady / len(later_blobs) * 1e3, 2), "accepted": acc_steady,
+              "preverify_ms_per_block": round((st2["preverify_ns"] - st["preverify_ns"]) / 1e6 / len(later_blobs), 2),
+              "gpu_ms_per_block": round((st2["gpu_ns"] - st["gpu_ns"]) / 1e6 / len(later_blobs), 2),
+              "ante_loop_ms_per_block": round((st2["deliver_loop_ns"] - st["deliver_loop_ns"]) / 1e6 / len(later_blobs), 2)}
     # per-tx path (CheckTx without batching): one GPU call per tx
     app = fresh_app()
     m = min(per_tx_sample, ntx)
