@@ -39,6 +39,23 @@ class Stats(ctypes.Structure):
                                                "preverify_ns", "gpu_ns", "deliver_loop_ns")]
 
 
+class Commit(ctypes.Structure):
+    """gvh_commit (gvhost.h): one VerifyCommit / VerifyCommitTrusting check."""
+    _fields_ = [("trusting", ctypes.c_int), ("trust_num", ctypes.c_int64), ("trust_den", ctypes.c_int64),
+                ("basic_ok", ctypes.c_int), ("n_vals", ctypes.c_size_t), ("val_pub32", ctypes.c_void_p),
+                ("val_addr20", ctypes.c_void_p), ("val_power", ctypes.c_void_p), ("n_sigs", ctypes.c_size_t),
+                ("flag", ctypes.c_void_p), ("sig_addr20", ctypes.c_void_p), ("sig64", ctypes.c_void_p),
+                ("sig_len", ctypes.c_void_p), ("msg_blob", ctypes.c_void_p), ("msg_off", ctypes.c_void_p),
+                ("msg_len", ctypes.c_void_p)]
+
+
+class CommitResult(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_int32), ("idx", ctypes.c_int32), ("idx2", ctypes.c_int32),
+                ("got", ctypes.c_int64), ("needed", ctypes.c_int64)]
+
+
+COMMIT_CODES = {0: "ok", 1: "basic", 2: "size", 3: "wrong_sig", 4: "not_enough", 5: "double_vote", 6: "bad_trust"}
+
 _L = None
 
 
@@ -81,6 +98,7 @@ def lib():
         L.gvh_set_cache_capacity.argtypes = [vp, sz]
         L.gvh_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
         L.gvh_tx_sign_bytes.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, u64, u64, vp, sz, vp, sz]
+        L.gvh_verify_commits.argtypes = [vp, sz, ctypes.POINTER(Commit), ctypes.POINTER(CommitResult)]
         L.gvh_tx_sign_bytes.restype = sz
         _L = L
     return _L
@@ -221,6 +239,44 @@ class HostApp:
 
     def set_cache_capacity(self, entries: int):
         self._L.gvh_set_cache_capacity(self._app, entries)
+
+    def verify_commits(self, commits):
+        """gvh_verify_commits over a list of dicts: vals = [(pub32, addr20, power)],
+        sigs = [(flag, addr20, sig_bytes, sign_bytes)], trusting (bool),
+        trust = (num, den), basic_ok (bool).  Returns [(code name, idx, idx2, got, needed)]."""
+        import numpy as np
+        keep = []
+        arr = (Commit * max(1, len(commits)))()
+        for c, d in enumerate(commits):
+            vals, sigs = d["vals"], d["sigs"]
+            vp32 = np.frombuffer(b"".join(v[0] for v in vals) or b"\0", np.uint8).copy()
+            va20 = np.frombuffer(b"".join(v[1] for v in vals) or b"\0", np.uint8).copy()
+            vpow = np.array([v[2] for v in vals] or [0], np.int64)
+            flags = np.array([x[0] for x in sigs] or [0], np.uint8)
+            sa20 = np.frombuffer(b"".join(x[1] for x in sigs) or b"\0", np.uint8).copy()
+            s64 = np.zeros((max(1, len(sigs)), 64), np.uint8)
+            slen = np.zeros(max(1, len(sigs)), np.uint32)
+            for i, x in enumerate(sigs):
+                b = x[2][:64]
+                s64[i, :len(b)] = np.frombuffer(b, np.uint8) if b else 0
+                slen[i] = len(x[2])
+            msgs = [x[3] for x in sigs]
+            blob = np.frombuffer(b"".join(msgs) or b"\0", np.uint8).copy()
+            off = np.zeros(max(1, len(msgs)), np.uint64)
+            ln = np.array([len(m) for m in msgs] or [0], np.uint32)
+            if len(msgs) > 1:
+                off[1:len(msgs)] = np.cumsum(ln[:len(msgs) - 1], dtype=np.uint64)
+            keep += [vp32, va20, vpow, flags, sa20, s64, slen, blob, off, ln]
+            num, den = d.get("trust", (1, 3))
+            arr[c] = Commit(1 if d.get("trusting") else 0, num, den, 1 if d.get("basic_ok", True) else 0, len(vals),
+                            vp32.ctypes.data, va20.ctypes.data, vpow.ctypes.data, len(sigs), flags.ctypes.data,
+                            sa20.ctypes.data, s64.ctypes.data, slen.ctypes.data, blob.ctypes.data, off.ctypes.data,
+                            ln.ctypes.data)
+        res = (CommitResult * max(1, len(commits)))()
+        rc = self._L.gvh_verify_commits(self._app, len(commits), arr, res)
+        if rc != 0:
+            raise RuntimeError(f"gvh_verify_commits rc {rc}")
+        return [(COMMIT_CODES[r.code], r.idx, r.idx2, r.got, r.needed) for r in res[:len(commits)]]
 
     def stats(self):
         st = Stats()

@@ -2624,3 +2624,133 @@ size_t gvh_bech32_address(const uint8_t addr20[20], char* out, size_t cap) {
 }
 
 }  // extern "C"
+
+// ---- IBC 07-tendermint light-client commit checks.
+//
+// x/ibc/07-tendermint/update.go:88 (lite.Verify -> VerifyAdjacent /
+// VerifyNonAdjacent) and misbehaviour.go:88-97 check validator commits with
+// tendermint v0.33.4 types/validator_set.go VerifyCommit (signature i <->
+// validator i, +2/3 of the total power, every present signature checked) and
+// VerifyCommitTrusting (validators found by address, trust level of the
+// total power, double votes rejected, returns as soon as the tally passes).
+// Each commit's loop stops at its first wrong signature.  Here every
+// signature any commit's loop could read -- present, validator known, 64
+// bytes long (tendermint's ed25519 VerifyBytes rejects other lengths without
+// verifying) -- of every commit in the call is verified in ONE
+// gv_verify_ed25519_msgs batch, then each loop is walked in reference order
+// over the verdicts.  A signature verified beyond the point where the
+// reference would have stopped is never read, so results (code, index,
+// tallies) are the sequential loop's.
+extern "C" int gvh_verify_commits(gvh_app* app, size_t n, const gvh_commit* commits, gvh_commit_result* out) {
+  if (!app || (n && (!commits || !out))) return GVH_EINVAL;
+  using AddrKey = std::array<uint8_t, 20>;
+  struct AddrHash {
+    size_t operator()(const AddrKey& a) const {
+      uint64_t v;
+      memcpy(&v, a.data(), 8);
+      return (size_t)(v * 0x9E3779B97F4A7C15ull);
+    }
+  };
+  std::vector<std::vector<int32_t>> vidx(n);        // per signature: the validator its loop would read (-1: none)
+  std::vector<std::vector<int32_t>> item(n);        // per signature: its batch item (-1: false without verifying)
+  std::vector<uint8_t> pub, sig, blob;
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> len;
+  size_t m = 0;
+  for (size_t c = 0; c < n; ++c) {
+    const gvh_commit& k = commits[c];
+    gvh_commit_result& r = out[c];
+    r = gvh_commit_result{GVH_COMMIT_OK, -1, -1, 0, 0};
+    if ((k.n_vals && (!k.val_pub32 || !k.val_power || (k.trusting && !k.val_addr20))) ||
+        (k.n_sigs && (!k.flag || !k.sig64 || !k.sig_len || !k.msg_off || !k.msg_len || (k.trusting && !k.sig_addr20))))
+      return GVH_EINVAL;
+    if (k.trusting) {
+      // "trustLevel must be within [1/3, 1]": the reference panics
+      if (k.trust_den <= 0 || k.trust_num * 3 < k.trust_den || k.trust_num > k.trust_den) {
+        r.code = GVH_COMMIT_BAD_TRUST;
+        continue;
+      }
+      if (!k.basic_ok) { r.code = GVH_COMMIT_BASIC; continue; }
+    } else {
+      if (k.n_vals != k.n_sigs) { r.code = GVH_COMMIT_SIZE; continue; }   // checked before verifyCommitBasic
+      if (!k.basic_ok) { r.code = GVH_COMMIT_BASIC; continue; }
+    }
+    std::unordered_map<AddrKey, int32_t, AddrHash> by_addr;
+    if (k.trusting) {
+      by_addr.reserve(k.n_vals * 2);
+      for (size_t v = 0; v < k.n_vals; ++v) {
+        AddrKey a;
+        memcpy(a.data(), k.val_addr20 + 20 * v, 20);
+        by_addr.emplace(a, (int32_t)v);               // addresses are unique in a validator set
+      }
+    }
+    vidx[c].assign(k.n_sigs, -1);
+    item[c].assign(k.n_sigs, -1);
+    for (size_t i = 0; i < k.n_sigs; ++i) {
+      if (k.flag[i] == GVH_COMMIT_FLAG_ABSENT) continue;
+      int32_t v = (int32_t)i;
+      if (k.trusting) {
+        AddrKey a;
+        memcpy(a.data(), k.sig_addr20 + 20 * i, 20);
+        auto it = by_addr.find(a);
+        v = it == by_addr.end() ? -1 : it->second;
+      }
+      vidx[c][i] = v;
+      if (v < 0 || k.sig_len[i] != 64) continue;
+      item[c][i] = (int32_t)m++;
+      pub.insert(pub.end(), k.val_pub32 + 32 * (size_t)v, k.val_pub32 + 32 * (size_t)v + 32);
+      sig.insert(sig.end(), k.sig64 + 64 * i, k.sig64 + 64 * i + 64);
+      off.push_back(blob.size());
+      len.push_back(k.msg_len[i]);
+      if (k.msg_len[i]) blob.insert(blob.end(), k.msg_blob + k.msg_off[i], k.msg_blob + k.msg_off[i] + k.msg_len[i]);
+    }
+  }
+  std::vector<uint8_t> ok(m);
+  if (m) {
+    if (!app->gpu) return GVH_ENOVERIFIER;
+    std::lock_guard<std::mutex> g(app->gpu_mu);
+    if (gv_verify_ed25519_msgs(app->gpu, m, pub.data(), sig.data(), blob.empty() ? nullptr : blob.data(), off.data(),
+                               len.data(), ok.data()) != GV_OK)
+      return GVH_EDEVICE;
+    app->st_gpu_calls += 1;
+    app->st_gpu_leaves += m;
+  }
+  for (size_t c = 0; c < n; ++c) {
+    const gvh_commit& k = commits[c];
+    gvh_commit_result& r = out[c];
+    if (r.code != GVH_COMMIT_OK) continue;
+    int64_t total = 0;
+    for (size_t v = 0; v < k.n_vals; ++v) total += k.val_power[v];
+    const int64_t needed = k.trusting ? total * k.trust_num / k.trust_den : total * 2 / 3;
+    int64_t tallied = 0;
+    std::unordered_map<int32_t, int32_t> seen;        // trusting: validator -> first commit index
+    bool passed = false;
+    for (size_t i = 0; i < k.n_sigs && r.code == GVH_COMMIT_OK && !passed; ++i) {
+      if (k.flag[i] == GVH_COMMIT_FLAG_ABSENT) continue;
+      const int32_t v = vidx[c][i];
+      if (k.trusting) {
+        if (v < 0) continue;                          // unknown validator: skipped
+        auto it = seen.find(v);
+        if (it != seen.end()) {
+          r.code = GVH_COMMIT_DOUBLE_VOTE;
+          r.idx = it->second;
+          r.idx2 = (int32_t)i;
+          break;
+        }
+        seen.emplace(v, (int32_t)i);
+      }
+      const bool good = item[c][i] >= 0 && ok[(size_t)item[c][i]] != 0;
+      if (!good) {
+        r.code = GVH_COMMIT_WRONG_SIG;
+        r.idx = (int32_t)i;
+        break;
+      }
+      if (k.flag[i] == GVH_COMMIT_FLAG_COMMIT) tallied += k.val_power[v];   // blockID.Equals(commitSig.BlockID(...))
+      if (k.trusting && tallied > needed) passed = true;
+    }
+    r.got = tallied;
+    r.needed = needed;
+    if (r.code == GVH_COMMIT_OK && !passed && tallied <= needed) r.code = GVH_COMMIT_NOT_ENOUGH;
+  }
+  return GVH_OK;
+}

@@ -179,6 +179,49 @@ size_t gvh_tx_sign_bytes(const uint8_t* tx, size_t tx_len, const char* chain_id,
                          uint64_t sequence, uint8_t* out, size_t cap, char* err, size_t err_cap);
 /* crypto.PubKey.Address() of an amino pubkey: secp256k1 RIPEMD160(SHA256(pub33)),
  * multisig SHA256(amino bytes)[:20], ed25519 SHA256(pub32)[:20]. 0 = ok. */
+
+/* ---- IBC 07-tendermint light-client commit checks ----
+ * tendermint v0.33.4 types/validator_set.go VerifyCommit (lite2 Verify ->
+ * VerifyAdjacent / VerifyNonAdjacent from x/ibc/07-tendermint/update.go:88)
+ * and VerifyCommitTrusting (VerifyNonAdjacent, misbehaviour.go:88-97) for n
+ * commits: every signature their loops could read is verified in ONE
+ * gv_verify_ed25519_msgs batch, each loop then walked in reference order over
+ * the verdicts -- same code, index and tallies as the sequential loop.  The
+ * caller supplies what needs the tendermint types: verifyCommitBasic's
+ * verdict and each signature's VoteSignBytes(chainID, i). */
+#define GVH_COMMIT_FLAG_ABSENT 1   /* types.BlockIDFlagAbsent */
+#define GVH_COMMIT_FLAG_COMMIT 2   /* types.BlockIDFlagCommit (counts toward the tally) */
+#define GVH_COMMIT_FLAG_NIL 3      /* types.BlockIDFlagNil (verified, not tallied) */
+typedef struct gvh_commit {
+  int trusting;                  /* 0: VerifyCommit (signature i <-> validator i); 1: VerifyCommitTrusting */
+  int64_t trust_num, trust_den;  /* trusting: tmmath.Fraction (lite.DefaultTrustLevel = 1/3) */
+  int basic_ok;                  /* verifyCommitBasic(commit, height, blockID) == nil */
+  size_t n_vals;
+  const uint8_t* val_pub32;      /* validator ed25519 keys (32 bytes each) */
+  const uint8_t* val_addr20;     /* validator addresses (trusting) */
+  const int64_t* val_power;      /* voting powers */
+  size_t n_sigs;
+  const uint8_t* flag;           /* BlockIDFlag per signature */
+  const uint8_t* sig_addr20;     /* CommitSig.ValidatorAddress (trusting) */
+  const uint8_t* sig64;          /* signatures, 64-byte stride */
+  const uint32_t* sig_len;       /* their lengths (!= 64: VerifyBytes is false) */
+  const uint8_t* msg_blob;       /* VoteSignBytes(chainID, i) at msg_off[i], msg_len[i] */
+  const uint64_t* msg_off;
+  const uint32_t* msg_len;
+} gvh_commit;
+#define GVH_COMMIT_OK 0
+#define GVH_COMMIT_BASIC 1         /* verifyCommitBasic's error (the caller's) */
+#define GVH_COMMIT_SIZE 2          /* NewErrInvalidCommitSignatures(vals.Size(), len(commit.Signatures)) */
+#define GVH_COMMIT_WRONG_SIG 3     /* "wrong signature (#idx): %X" */
+#define GVH_COMMIT_NOT_ENOUGH 4    /* ErrNotEnoughVotingPowerSigned{Got: got, Needed: needed} */
+#define GVH_COMMIT_DOUBLE_VOTE 5   /* "double vote from %v (idx and idx2)" */
+#define GVH_COMMIT_BAD_TRUST 6     /* trust level outside [1/3, 1]: the reference panics */
+typedef struct gvh_commit_result {
+  int32_t code, idx, idx2;
+  int64_t got, needed;           /* the tally when the loop ended and the power needed */
+} gvh_commit_result;
+int gvh_verify_commits(gvh_app* app, size_t n, const gvh_commit* commits, gvh_commit_result* out);
+
 int gvh_pubkey_address(const uint8_t* pub_amino, size_t len, uint8_t out20[20]);
 /* sdk.AccAddress.String(): bech32 "cosmos1..." (types/address.go:222-234). */
 size_t gvh_bech32_address(const uint8_t addr20[20], char* out, size_t cap);

@@ -92,3 +92,16 @@ def test_open_fails_loudly_without_gpu():
         pytest.skip("GPU present")
     with pytest.raises(gvm.GpuVerifyError):
         gvm.Verifier()
+
+
+def test_libgvhost_exports_every_function_its_header_declares():
+    """libgvhost.so (the host mirror) exports every gvh_* function
+    cosmos-sdk-rootchain_amd/host/gvhost.h declares (incl. the IBC commit hook)."""
+    import gvhost
+    hdr = os.path.join(REPO, "cosmos-sdk-rootchain_amd", "host", "gvhost.h")
+    txt = re.sub(r"/\*.*?\*/", "", open(hdr).read(), flags=re.S)
+    names = sorted(set(re.findall(r"\b(gvh_[a-z_0-9]+)\s*\(", txt)))
+    assert "gvh_verify_commits" in names and len(names) >= 25
+    L = gvhost.lib()
+    for n in names:
+        assert hasattr(L, n), n
