@@ -92,6 +92,8 @@ def lib():
         cpp = ctypes.POINTER(ctypes.c_char_p)
         L.gvh_deliver_block.argtypes = [vp, sz, cpp, ctypes.POINTER(sz), ctypes.POINTER(Result)]
         L.gvh_deliver_block_codes.argtypes = [vp, sz, cpp, ctypes.POINTER(sz), ctypes.POINTER(ctypes.c_uint32)]
+        L.gvh_deliver_blocks.argtypes = [vp, sz, ctypes.POINTER(sz), cpp, ctypes.POINTER(sz),
+                                         ctypes.POINTER(ctypes.c_uint32)]
         L.gvh_deliver_gentxs.argtypes = [vp, sz, cpp, ctypes.POINTER(sz), ctypes.POINTER(Result), ctypes.POINTER(sz)]
         L.gvh_checktx.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(Result)]
         L.gvh_set_window.argtypes = [vp, sz, ctypes.c_int64]
@@ -221,6 +223,40 @@ class HostApp:
                                              lens.ctypes.data_as(ctypes.POINTER(ctypes.c_size_t)),
                                              codes.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
         return rc, codes[:n]
+
+    def deliver_blocks_blob(self, blob, offs, lens, block_ntx):
+        """Consecutive blocks in one buffer (block b = the next block_ntx[b]
+        txs of offs / lens), delivered through the pipelined replay
+        (gvh_deliver_blocks): same codes and final state as deliver_block_blob
+        per block.  Returns (rc, codes u32 array over every tx)."""
+        import numpy as np
+        n = len(offs)
+        bn = np.ascontiguousarray(block_ntx, dtype=np.uint64)
+        assert int(bn.sum()) == n
+        ptrs = np.uint64(blob.ctypes.data) + np.asarray(offs).astype(np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        codes = np.zeros(max(1, n), np.uint32)
+        rc = self._L.gvh_deliver_blocks(self._app, len(bn), bn.ctypes.data_as(ctypes.POINTER(ctypes.c_size_t)),
+                                        ptrs.ctypes.data_as(ctypes.POINTER(ctypes.c_char_p)),
+                                        lens.ctypes.data_as(ctypes.POINTER(ctypes.c_size_t)),
+                                        codes.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+        return rc, codes[:n]
+
+    def deliver_blocks(self, blocks):
+        """blocks: list of lists of tx bytes.  Returns (rc, [codes per block])."""
+        import numpy as np
+        flat = [tx for blk in blocks for tx in blk]
+        lens = np.array([len(x) for x in flat], np.uint64)
+        offs = np.zeros(len(flat), np.uint64)
+        if len(flat):
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        blob = np.frombuffer(b"".join(flat) or b"\0", np.uint8).copy()
+        rc, codes = self.deliver_blocks_blob(blob, offs, lens, [len(b) for b in blocks])
+        out, k = [], 0
+        for b in blocks:
+            out.append(codes[k:k + len(b)])
+            k += len(b)
+        return rc, out
 
     def deliver_gentxs(self, txs):
         arr, lens = _arrays(txs)

@@ -26,9 +26,11 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <future>
 #include <memory>
 #include <mutex>
 #include <random>
+#include <shared_mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -1199,6 +1201,12 @@ struct Account {
   Bytes pub;                                  // amino (canonical), empty = not set
   std::shared_ptr<const PubInfo> info;        // GetPubKey() of pub (decoded once)
   uint64_t bump_epoch = 0, bump = 0;          // PreVerifyTxs' sequence prediction (earlier txs this call)
+  // Prediction carried across a pipelined replay (deliver_blocks): block E+1
+  // is pre-verified before block E is delivered, so its prediction adds
+  // block E's effects -- own = txs of block own_epoch signed by this account,
+  // own_info = the key its SetPubKey would store -- to the state.
+  uint64_t own_epoch = 0, own = 0;
+  std::shared_ptr<const PubInfo> own_info, pred_info;   // pred_info: predicted key for bump_epoch
 };
 // AccountKeeper store: 20-byte address -> Account.  Open addressing (linear
 // probing) over an index into a deque, so an Account never moves (PreVerifyTxs
@@ -1402,6 +1410,24 @@ struct gvh_app {
   };
   std::array<ObjPool, 64> objs;
   uint64_t bump_epoch = 0;
+  uint64_t carry_epoch = 0;                    // a pre-verified block not yet delivered (deliver_blocks), 0: none
+  // key_slots readers (slot lookups on the pool, before the GPU lock) share
+  // key_mu; verify_secp's updates take it exclusively (under gpu_mu)
+  std::shared_mutex key_mu;
+  // pinned pack buffers (gv_host_alloc): the GPU batch reads them in place, no staging copy
+  struct PinBuf {
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+    bool pinned = false;
+  };
+  std::mutex pin_mu;
+  std::vector<PinBuf> pin_free;
+  ~gvh_app() {
+    for (PinBuf& b : pin_free) {
+      if (b.pinned) gv_host_free(gpu, b.p);
+      else free(b.p);
+    }
+  }
   std::atomic<uint64_t> st_gpu_calls{0}, st_gpu_leaves{0}, st_hits{0}, st_misses{0}, st_memo{0}, st_windows{0},
       st_window_txs{0}, st_pre_ns{0}, st_gpu_ns{0}, st_loop_ns{0};
 };
@@ -1639,48 +1665,168 @@ void cache_insert(gvh_app* app, Leaf& L, bool v) {
   app->cache.put(L.key, v);
 }
 
-// m secp256k1 digests -> verdicts (gpu_mu held).  Keyed: every key is looked
-// up in the app's slot map (parallel reads), the keys not seen before are
-// parsed into the context's key arena with ONE gv_keys_load (batches of at
-// least key_load_min leaves -- a block; a smaller batch with an unknown key
-// takes the pub33 path rather than wait on k_keys_build), and the batch
-// runs gv_verify_digests_keyed -- the same verdicts as the pub33 path (a key
-// ParsePubKey rejects keeps a false slot), without the per-item decompression
-// and Q-table build, on the 4-group ladder.  Any arena problem (cap reached,
-// load error) falls back to the pub33 batch for this call.
-int verify_secp(gvh_app* app, size_t m, const uint8_t* pub, const uint8_t* sig, const uint8_t* dig, uint8_t* ok) {
-  if (!app->keyed) return gv_verify_digests(app->gpu, m, pub, sig, dig, ok);
+// Pack buffers for GPU batches: pinned (gv_host_alloc), so the library reads
+// them in place (direct H2D, or zero-copy for small batches) instead of
+// staging pageable memory; recycled, so a block's pack neither page-faults a
+// fresh allocation nor pays hipHostMalloc again.
+gvh_app::PinBuf pin_get(gvh_app* app, size_t bytes) {
+  {
+    std::lock_guard<std::mutex> g(app->pin_mu);
+    auto& v = app->pin_free;
+    size_t best = v.size();
+    for (size_t i = 0; i < v.size(); ++i)
+      if (v[i].cap >= bytes && (best == v.size() || v[i].cap < v[best].cap)) best = i;
+    if (best < v.size()) {
+      gvh_app::PinBuf b = v[best];
+      v.erase(v.begin() + (long)best);
+      return b;
+    }
+  }
+  gvh_app::PinBuf b;
+  b.cap = std::max<size_t>(bytes, size_t(1) << 20);
+  void* p = nullptr;
+  if (app->gpu && gv_host_alloc(app->gpu, b.cap, &p) == GV_OK && p) {
+    b.p = (uint8_t*)p;
+    b.pinned = true;
+  } else {
+    b.p = (uint8_t*)malloc(b.cap);
+    if (!b.p) throw std::bad_alloc();
+  }
+  return b;
+}
+void pin_put(gvh_app* app, gvh_app::PinBuf b) {
+  if (!b.p) return;
+  std::lock_guard<std::mutex> g(app->pin_mu);
+  auto& v = app->pin_free;
+  v.push_back(b);
+  if (v.size() > 4) {                                 // keep the four largest
+    size_t s = 0;
+    for (size_t i = 1; i < v.size(); ++i)
+      if (v[i].cap < v[s].cap) s = i;
+    if (v[s].pinned) gv_host_free(app->gpu, v[s].p);
+    else free(v[s].p);
+    v.erase(v.begin() + (long)s);
+  }
+}
+
+// One GPU batch of leaves: packed on the pool (batch_pack), verified under
+// the GPU lock with no pool use (batch_run: safe on another thread while the
+// pool runs a block's ante loop), verdicts written back (batch_finish).
+struct GpuBatch {
+  std::vector<Leaf*> miss;                     // secp256k1 leaves (the ed25519 ones appended by batch_finish)
+  std::vector<Leaf*> ed;
+  gvh_app::PinBuf buf;
+  size_t m = 0;
+  uint8_t *pub = nullptr, *sig = nullptr, *dig = nullptr, *ok = nullptr;
+  uint32_t* slots = nullptr;                   // keyed: key-arena slot per leaf, UINT32_MAX = not resident
+  bool looked_up = false;                      // slots filled against arena generation `gen`
+  uint64_t gen = 0;
+  std::vector<uint8_t> epub, esig, eok, eblob;
+  std::vector<uint64_t> eoff;
+  std::vector<uint32_t> elen;
+};
+
+// Layout of the pinned buffer: pub33 | sig64 | dig32 | slots (u32) | ok.
+// Keyed: every key is looked up in the app's slot map here, on the pool,
+// under the shared key lock (the map only gains entries while the arena
+// generation stays the same, so a slot found here is still valid when the
+// batch runs unless the generation moved -- batch_run checks).
+void batch_pack(gvh_app* app, GpuBatch& b) {
+  {
+    size_t k = 0;
+    for (Leaf* L : b.miss) {
+      if (L->kind) b.ed.push_back(L);
+      else b.miss[k++] = L;
+    }
+    b.miss.resize(k);
+  }
+  const size_t m = b.m = b.miss.size();
+  if (m) {
+    const size_t slot_off = (m * 129 + 15) & ~size_t(15);
+    b.buf = pin_get(app, slot_off + m * 4 + m + 16);
+    b.pub = b.buf.p;
+    b.sig = b.pub + m * 33;
+    b.dig = b.sig + m * 64;
+    b.slots = (uint32_t*)(b.buf.p + slot_off);
+    b.ok = b.buf.p + slot_off + m * 4;
+    std::shared_lock<std::shared_mutex> rk(app->key_mu);
+    const bool look = app->keyed && app->gpu && gv_keys_generation(app->gpu) == app->key_gen;
+    b.gen = app->key_gen;
+    b.looked_up = look;
+    auto& map = app->key_slots;
+    parallel_for(app, m, [&](size_t k) {
+      const Leaf& L = *b.miss[k];
+      memcpy(&b.pub[k * 33], L.pub.data(), 33);
+      memcpy(&b.sig[k * 64], L.sig.data(), 64);
+      memcpy(&b.dig[k * 32], L.dig.data(), 32);
+      if (look) {
+        std::array<uint8_t, 33> key;
+        memcpy(key.data(), L.pub.data(), 33);
+        auto it = map.find(key);
+        b.slots[k] = it == map.end() ? UINT32_MAX : it->second;
+      }
+    });
+  }
+  const size_t me = b.ed.size();
+  if (me) {
+    b.epub.resize(me * 32);
+    b.esig.resize(me * 64);
+    b.eok.resize(me);
+    b.eoff.resize(me);
+    b.elen.resize(me);
+    for (size_t k = 0; k < me; ++k) {
+      memcpy(&b.epub[k * 32], b.ed[k]->pub.data(), 32);
+      memcpy(&b.esig[k * 64], b.ed[k]->sig.data(), 64);
+      b.eoff[k] = b.eblob.size();
+      b.elen[k] = (uint32_t)b.ed[k]->msg->size();
+      b.eblob.insert(b.eblob.end(), b.ed[k]->msg->begin(), b.ed[k]->msg->end());
+    }
+  }
+}
+
+// The secp256k1 part of a batch (gpu_mu held).  Keyed: keys not yet in the
+// context's key arena are parsed into it with ONE gv_keys_load (batches of
+// at least key_load_min leaves -- a block; a smaller batch with an unknown
+// key takes the pub33 path rather than wait on the key-table build), and the
+// batch runs gv_verify_digests_keyed -- the same verdicts as the pub33 path
+// (a key ParsePubKey rejects keeps a false slot), without the per-item
+// decompression and Q-table build, on the 4-group ladder.  Any arena problem
+// (cap reached, load error) falls back to the pub33 batch for this call.
+int verify_secp(gvh_app* app, GpuBatch& b) {
+  const size_t m = b.m;
+  if (!app->keyed) return gv_verify_digests(app->gpu, m, b.pub, b.sig, b.dig, b.ok);
   constexpr uint32_t kPending = 0x80000000u;      // map value of a key queued for this call's load
-  std::vector<uint32_t> slots(m);
+  std::unique_lock<std::shared_mutex> wk(app->key_mu);
   auto& map = app->key_slots;
   const uint64_t gen = gv_keys_generation(app->gpu);
   if (gen != app->key_gen) {                      // the arena was reset (here or by another user)
     map.clear();
     app->key_gen = gen;
   }
-  parallel_for(app, m, [&](size_t k) {
-    std::array<uint8_t, 33> key;
-    memcpy(key.data(), pub + 33 * k, 33);
-    auto it = map.find(key);
-    slots[k] = it == map.end() ? UINT32_MAX : it->second;
-  });
+  if (!b.looked_up || b.gen != gen)               // packed against another arena: look up again
+    for (size_t k = 0; k < m; ++k) {
+      std::array<uint8_t, 33> key;
+      memcpy(key.data(), b.pub + 33 * k, 33);
+      auto it = map.find(key);
+      b.slots[k] = it == map.end() ? UINT32_MAX : it->second;
+    }
   if (m < app->key_load_min) {                    // small batch (CheckTx window, per-tx ante)
     bool all = true;
-    for (size_t k = 0; k < m && all; ++k) all = slots[k] != UINT32_MAX;
-    if (!all) return gv_verify_digests(app->gpu, m, pub, sig, dig, ok);
+    for (size_t k = 0; k < m && all; ++k) all = b.slots[k] != UINT32_MAX;
+    if (!all) return gv_verify_digests(app->gpu, m, b.pub, b.sig, b.dig, b.ok);
   }
   std::vector<uint8_t> fresh;
   std::vector<std::array<uint8_t, 33>> fresh_keys;
   for (size_t k = 0; k < m; ++k) {
-    if (slots[k] != UINT32_MAX) continue;
+    if (b.slots[k] != UINT32_MAX) continue;
     std::array<uint8_t, 33> key;
-    memcpy(key.data(), pub + 33 * k, 33);
+    memcpy(key.data(), b.pub + 33 * k, 33);
     auto ins = map.emplace(key, kPending + (uint32_t)fresh_keys.size());
     if (ins.second) {
       fresh.insert(fresh.end(), key.begin(), key.end());
       fresh_keys.push_back(key);
     }
-    slots[k] = ins.first->second;
+    b.slots[k] = ins.first->second;
   }
   if (!fresh_keys.empty()) {
     const size_t nf = fresh_keys.size();
@@ -1694,17 +1840,46 @@ int verify_secp(gvh_app* app, size_t m, const uint8_t* pub, const uint8_t* sig, 
       } else {
         for (auto& key : fresh_keys) map.erase(key);
       }
-      return gv_verify_digests(app->gpu, m, pub, sig, dig, ok);
+      return gv_verify_digests(app->gpu, m, b.pub, b.sig, b.dig, b.ok);
     }
     for (size_t i = 0; i < nf; ++i) map[fresh_keys[i]] = got[i];
-    parallel_for(app, m, [&](size_t k) {
-      if (slots[k] >= kPending) slots[k] = got[slots[k] - kPending];
-    });
+    for (size_t k = 0; k < m; ++k)
+      if (b.slots[k] >= kPending) b.slots[k] = got[b.slots[k] - kPending];
   }
-  return gv_verify_digests_keyed(app->gpu, m, slots.data(), sig, dig, ok);
+  return gv_verify_digests_keyed(app->gpu, m, b.slots, b.sig, b.dig, b.ok);
 }
 
-// Resolve leaves: cache first, the secp256k1 misses in ONE GPU batch.
+int batch_run(gvh_app* app, GpuBatch& b) {
+  if (!app->gpu) return GVH_ENOVERIFIER;
+  std::lock_guard<std::mutex> g(app->gpu_mu);
+  if (b.m && verify_secp(app, b) != GV_OK) return GVH_EDEVICE;
+  const size_t me = b.ed.size();
+  if (me && gv_verify_ed25519_msgs(app->gpu, me, b.epub.data(), b.esig.data(), b.eblob.empty() ? nullptr : b.eblob.data(),
+                                   b.eoff.data(), b.elen.data(), b.eok.data()) != GV_OK)
+    return GVH_EDEVICE;
+  return GVH_OK;
+}
+
+void batch_finish(gvh_app* app, GpuBatch& b, bool fill, uint32_t* gpu_leaves) {
+  const size_t m = b.m, me = b.ed.size();
+  app->st_gpu_calls += (m ? 1 : 0) + (me ? 1 : 0);
+  app->st_gpu_leaves += m + me;
+  parallel_for(app, m + me, [&](size_t k) {
+    Leaf* L = k < m ? b.miss[k] : b.ed[k - m];
+    const uint8_t v = k < m ? b.ok[k] : b.eok[k - m];
+    L->verdict = v;
+    if (fill) cache_insert(app, *L, v != 0);
+  });
+  if (gpu_leaves) *gpu_leaves += (uint32_t)(m + me);
+  pin_put(app, b.buf);
+  b.buf = gvh_app::PinBuf{};
+}
+void batch_drop(gvh_app* app, GpuBatch& b) {
+  pin_put(app, b.buf);
+  b.buf = gvh_app::PinBuf{};
+}
+
+// Resolve leaves: cache first, the misses in ONE GPU batch per key type.
 int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint32_t* hits, bool all_miss = false,
             bool fill = true) {
   std::vector<Leaf*> miss;
@@ -1738,64 +1913,17 @@ int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint
     fprintf(stderr, "resolve %s %.3f ms\n", what, std::chrono::duration<double, std::milli>(t - tr).count());
     tr = t;
   };
-  // secp256k1 misses -> gv_verify_digests, ed25519 misses -> gv_verify_ed25519_msgs
-  std::vector<Leaf*> ed;
-  {
-    size_t k = 0;
-    for (Leaf* L : miss) {
-      if (L->kind) ed.push_back(L);
-      else miss[k++] = L;
-    }
-    miss.resize(k);
+  GpuBatch b;
+  b.miss.swap(miss);
+  batch_pack(app, b);
+  rlap("pack");
+  if (batch_run(app, b) != GVH_OK) {
+    batch_drop(app, b);
+    return GVH_EDEVICE;
   }
-  const size_t m = miss.size();
-  // one uninitialised buffer (no single-threaded zero fill of ~130 B per
-  // leaf before the parallel pack: its pages fault in on the pool)
-  std::unique_ptr<uint8_t[]> pack(new uint8_t[m * 129 + 1]);
-  uint8_t* const pub = pack.get();
-  uint8_t* const sig = pub + m * 33;
-  uint8_t* const dig = sig + m * 64;
-  std::vector<uint8_t> ok(m);
-  parallel_for(app, m, [&](size_t k) {
-    memcpy(&pub[k * 33], miss[k]->pub.data(), 33);
-    memcpy(&sig[k * 64], miss[k]->sig.data(), 64);
-    memcpy(&dig[k * 32], miss[k]->dig.data(), 32);
-  });
-  const size_t me = ed.size();
-  std::vector<uint8_t> epub(me * 32), esig(me * 64), eok(me), eblob;
-  std::vector<uint64_t> eoff(me);
-  std::vector<uint32_t> elen(me);
-  for (size_t k = 0; k < me; ++k) {
-    memcpy(&epub[k * 32], ed[k]->pub.data(), 32);
-    memcpy(&esig[k * 64], ed[k]->sig.data(), 64);
-    eoff[k] = eblob.size();
-    elen[k] = (uint32_t)ed[k]->msg->size();
-    eblob.insert(eblob.end(), ed[k]->msg->begin(), ed[k]->msg->end());
-  }
-  {
-    std::lock_guard<std::mutex> g(app->gpu_mu);
-    rlap("pack");
-    if (m && verify_secp(app, m, pub, sig, dig, ok.data()) != GV_OK)
-      return GVH_EDEVICE;
-    if (me && gv_verify_ed25519_msgs(app->gpu, me, epub.data(), esig.data(), eblob.empty() ? nullptr : eblob.data(),
-                                     eoff.data(), elen.data(), eok.data()) != GV_OK)
-      return GVH_EDEVICE;
-    rlap("gv_verify");
-  }
-  app->st_gpu_calls += (m ? 1 : 0) + (me ? 1 : 0);
-  app->st_gpu_leaves += m + me;
-  for (size_t k = 0; k < me; ++k) miss.push_back(ed[k]);
-  ok.insert(ok.end(), eok.begin(), eok.end());
-  const size_t mt = miss.size();
-  if (fill)
-    parallel_for(app, mt, [&](size_t k) {
-      miss[k]->verdict = ok[k];
-      cache_insert(app, *miss[k], ok[k] != 0);
-    });
-  else
-    for (size_t k = 0; k < mt; ++k) miss[k]->verdict = ok[k];
+  rlap("gv_verify");
+  batch_finish(app, b, fill, gpu_leaves);
   rlap("put");
-  if (gpu_leaves) *gpu_leaves += (uint32_t)mt;
   return GVH_OK;
 }
 
@@ -2095,11 +2223,27 @@ void release_memos(gvh_app* app, std::vector<std::shared_ptr<Memo>>& memos) {
   memos.clear();
 }
 
-// PreVerifyTxs.  Returns the memos (one per tx, in order).  The app lock is
-// held while the block's state is read (decode, sequence prediction, plans)
-// and released for the GPU batch.
-int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, size_t* n_leaves,
-              std::vector<std::shared_ptr<Memo>>* memos_out, bool keep) {
+// PreVerifyTxs in three parts, so a pipelined replay (deliver_blocks) can run
+// one block's GPU batch on another thread while the pool delivers the block
+// before it:
+//   pre_front  decode, sequence prediction and plans (app lock held while the
+//              state is read), then the misses packed into one batch
+//   batch_run  the GPU batch (no pool, no app lock)
+//   pre_back   verdicts written back, plans marked resolved, memos kept or released
+// carry_from: the epoch of a block pre-verified but not yet delivered, whose
+// effects (sequence increments, SetPubKey) the prediction adds to the state
+// (0: none -- every block delivered).
+struct PreState {
+  std::vector<std::shared_ptr<Memo>> memos;
+  std::vector<SignerPlan*> plans;
+  GpuBatch batch;
+  bool has_batch = false, keep = false;
+  uint64_t epoch = 0;
+  size_t n_all = 0;
+};
+
+void pre_front(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, bool keep,
+               uint64_t carry_from, PreState& ps) {
   auto T0 = std::chrono::steady_clock::now();
   const bool prof = getenv("GVH_PROFILE") != nullptr;
   auto lap = [&](const char* what) {
@@ -2108,11 +2252,13 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
     fprintf(stderr, "preverify %s %.3f ms\n", what, std::chrono::duration<double, std::milli>(t - T0).count());
     T0 = t;
   };
+  ps.keep = keep;
   std::unique_lock<std::mutex> lk(app->mu);
   const std::string chain_json = app->chain_json;
   // (1) parallel: decode (sharing an earlier decode of the same bytes),
   // GetPubKeys' tx-supplied keys, the signers' accounts
-  std::vector<std::shared_ptr<Memo>> memos(ntx);
+  std::vector<std::shared_ptr<Memo>>& memos = ps.memos;
+  memos.assign(ntx, nullptr);
   // stage (2)'s signer partition, decided here: part_mask[t] = the parts tx t touches
   const int parts = ntx >= 2048 ? std::max(1, std::min(64, app->threads)) : 1;
   auto part_of = [&](const Account* a) { return (int)(((uintptr_t)a >> 4) % (uintptr_t)parts); };
@@ -2155,9 +2301,12 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
     memos[t] = std::move(m);
   });
   lap("decode");
-  // (2) sequence prediction = a per-signer prefix count in block order; signers
-  // are hash-partitioned over the pool, each part scanning the block in order
-  // for its own signers (every account is touched by one part only)
+  // (2) sequence prediction = a per-signer prefix count in block order (plus
+  // the carried block's count); signers are hash-partitioned over the pool,
+  // each part scanning the block in order for its own signers (every account
+  // is touched by one part only).  The predicted key is the account's, else
+  // the one an earlier SetPubKey (this block or the carried one) stores, else
+  // the tx-supplied one.
   struct Job {
     uint32_t t, signer;
     uint64_t accnum, seq;
@@ -2166,7 +2315,18 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
   };
   std::vector<Job> jobs;
   {
-    const uint64_t epoch = ++app->bump_epoch;
+    const uint64_t epoch = ps.epoch = ++app->bump_epoch;
+    const uint64_t prev = carry_from;
+    auto touch = [&](Account* acc) {
+      if (acc->bump_epoch == epoch) return;
+      const bool carry = prev && acc->own_epoch == prev;
+      acc->bump_epoch = epoch;
+      acc->bump = carry ? acc->own : 0;
+      acc->pred_info = carry ? acc->own_info : nullptr;
+      acc->own_epoch = epoch;
+      acc->own = 0;
+      acc->own_info = nullptr;
+    };
     std::vector<std::vector<Job>> pj(parts);
     parallel_parts(app, parts, [&](int part) {
       std::vector<Job>& out = pj[part];
@@ -2179,22 +2339,29 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
         for (size_t i = 0; i < tx.sigs.size() && i < tx.signers.size(); ++i) {
           Account* acc = m.sacc[i];
           if (!acc || part_of(acc) != part) continue;
+          touch(acc);
           std::shared_ptr<const PubInfo> pub;
           try {
             pub = account_info(app, *acc);
           } catch (const Panic&) {
             continue;
           }
-          if (!pub) pub = m.tx_pk[i];          // SetPubKey will store the tx-supplied key
+          if (!pub) {
+            pub = acc->pred_info;
+            if (!pub && m.tx_pk[i]) {               // SetPubKey will store the tx-supplied key
+              pub = m.tx_pk[i];
+              acc->pred_info = acc->own_info = pub;
+            }
+          }
           if (!pub) continue;
-          if (acc->bump_epoch != epoch) { acc->bump_epoch = epoch; acc->bump = 0; }
           out.push_back(Job{(uint32_t)t, (uint32_t)i, app->height == 0 ? 0 : acc->number, acc->sequence + acc->bump,
                             &m.plans[i], std::move(pub)});
         }
         for (Account* acc : m.sacc)                    // every signer's sequence moves if the tx passes
           if (acc && part_of(acc) == part) {
-            if (acc->bump_epoch != epoch) { acc->bump_epoch = epoch; acc->bump = 0; }
+            touch(acc);
             acc->bump += 1;
+            acc->own += 1;
           }
       }
     });
@@ -2208,7 +2375,6 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
   // (3) parallel: gas charge, sign bytes, leaves, cache keys + lookups; the
   // misses collect per worker
   std::vector<std::vector<Leaf*>> wmiss(std::max(1, app->threads));
-  size_t n_all = 0;
   std::atomic<size_t> n_leaf{0};
   parallel_for_w(app, jobs.size(), [&](size_t k, int w) {
     Job& j = jobs[k];
@@ -2226,32 +2392,64 @@ int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t*
     }
     n_leaf.fetch_add(j.plan->leaves.size(), std::memory_order_relaxed);
   });
-  n_all = n_leaf.load();
+  ps.n_all = n_leaf.load();
   lap("plans");
   lk.unlock();
-  // (4) one GPU batch for the misses, no app lock held
-  std::vector<Leaf*> miss;
+  ps.plans.resize(jobs.size());
+  for (size_t k = 0; k < jobs.size(); ++k) ps.plans[k] = jobs[k].plan;
+  std::vector<Leaf*>& miss = ps.batch.miss;
   {
     size_t nm = 0;
     for (auto& v : wmiss) nm += v.size();
     miss.reserve(nm);
     for (auto& v : wmiss) miss.insert(miss.end(), v.begin(), v.end());
   }
-  app->st_hits += n_all - miss.size();
-  uint32_t gpu_leaves = 0;
+  app->st_hits += ps.n_all - miss.size();
+  app->st_misses += miss.size();
+  // (4) the misses packed for one GPU batch (pinned buffer, key slots looked up)
+  if (!miss.empty()) {
+    ps.has_batch = true;
+    if (app->gpu) batch_pack(app, ps.batch);
+  }
+  lap("pack");
+}
+
+// The batch of a pre_front, timed into st_gpu_ns.
+int pre_gpu(gvh_app* app, PreState& ps) {
+  if (!ps.has_batch) return GVH_OK;
   const auto tg = std::chrono::steady_clock::now();
-  // a block being delivered (keep == false) reads the cache (txs seen by
-  // CheckTx) but does not fill it: its verdicts are used once, from the memos
-  const int rc = miss.empty() ? GVH_OK : resolve(app, miss, &gpu_leaves, nullptr, true, keep);
+  const int rc = batch_run(app, ps.batch);
   app->st_gpu_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tg).count();
+  return rc;
+}
+
+// rc: the batch's result.  A block being delivered (keep == false) reads the
+// cache (txs seen by CheckTx) but does not fill it: its verdicts are used
+// once, from the memos.
+void pre_back(gvh_app* app, PreState& ps, int rc, size_t* n_leaves, std::vector<std::shared_ptr<Memo>>* memos_out) {
+  uint32_t gpu_leaves = 0;
+  if (ps.has_batch) {
+    if (rc == GVH_OK) batch_finish(app, ps.batch, ps.keep, &gpu_leaves);
+    else batch_drop(app, ps.batch);
+  }
   if (rc == GVH_OK)
-    parallel_for(app, jobs.size(), [&](size_t k) { jobs[k].plan->resolved = jobs[k].plan->ok; });
-  lap("resolve");
-  if (keep)
-    for (auto& m : memos) app->memo.put(m);
+    parallel_for(app, ps.plans.size(), [&](size_t k) { ps.plans[k]->resolved = ps.plans[k]->ok; });
+  if (ps.keep)
+    for (auto& m : ps.memos) app->memo.put(m);
   if (n_leaves) *n_leaves = gpu_leaves;
-  if (memos_out) *memos_out = std::move(memos);
-  else release_memos(app, memos);
+  if (memos_out) *memos_out = std::move(ps.memos);
+  else release_memos(app, ps.memos);
+}
+
+// PreVerifyTxs.  Returns the memos (one per tx, in order).  The app lock is
+// held while the block's state is read (decode, sequence prediction, plans)
+// and released for the GPU batch.
+int preverify(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, size_t* n_leaves,
+              std::vector<std::shared_ptr<Memo>>* memos_out, bool keep) {
+  PreState ps;
+  pre_front(app, ntx, txs, lens, keep, 0, ps);
+  const int rc = ps.has_batch && !app->gpu ? GVH_ENOVERIFIER : pre_gpu(app, ps);
+  pre_back(app, ps, rc, n_leaves, memos_out);
   return rc;
 }
 
@@ -2405,6 +2603,67 @@ int deliver_block(gvh_app* app, size_t ntx, const uint8_t* const* txs, const siz
   return rc;
 }
 
+// A run of consecutive blocks (block sync / replay: the blocks are known
+// ahead of their delivery), pipelined: block b+1 is pre-verified -- its
+// prediction carrying block b's sequence increments and SetPubKeys -- and its
+// GPU batch runs on a helper thread while the pool delivers block b.  Results
+// and final state are those of delivering the blocks one by one (a carried
+// prediction that turns out wrong is a memo miss: the ante run rebuilds the
+// plan from the state and verifies it, never a different verdict).
+int deliver_blocks(gvh_app* app, size_t nb, const size_t* bn, const uint8_t* const* txs, const size_t* lens,
+                   uint32_t* codes) {
+  if (nb == 0) return GVH_OK;
+  auto ns_since = [](std::chrono::steady_clock::time_point t) {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t).count();
+  };
+  const bool prof = getenv("GVH_PROFILE") != nullptr;
+  PreState cur, nxt;
+  auto t0 = std::chrono::steady_clock::now();
+  pre_front(app, bn[0], txs, lens, false, 0, cur);
+  int rc = cur.has_batch && !app->gpu ? GVH_ENOVERIFIER : pre_gpu(app, cur);
+  std::vector<std::shared_ptr<Memo>> memos;
+  pre_back(app, cur, rc, nullptr, &memos);
+  app->st_pre_ns += ns_since(t0);
+  if (rc != GVH_OK) {
+    release_memos(app, memos);
+    return rc;
+  }
+  size_t off = 0;
+  for (size_t b = 0; b < nb; ++b) {
+    const bool more = b + 1 < nb;
+    std::future<int> gpu;
+    if (more) {
+      const auto tp = std::chrono::steady_clock::now();
+      nxt = PreState{};
+      pre_front(app, bn[b + 1], txs + off + bn[b], lens + off + bn[b], false, cur.epoch, nxt);
+      if (nxt.has_batch) {
+        if (!app->gpu) gpu = std::async(std::launch::deferred, [] { return (int)GVH_ENOVERIFIER; });
+        else gpu = std::async(std::launch::async, [app, &nxt] { return pre_gpu(app, nxt); });
+      }
+      app->st_pre_ns += ns_since(tp);
+      if (prof) fprintf(stderr, "blocks %zu: front %.3f ms\n", b + 1, ns_since(tp) / 1e6);
+    }
+    const auto tl = std::chrono::steady_clock::now();
+    rc = deliver_memos(app, memos, nullptr, codes + off);
+    app->st_loop_ns += ns_since(tl);
+    release_memos(app, memos);
+    if (prof) fprintf(stderr, "blocks %zu: loop+release %.3f ms\n", b, ns_since(tl) / 1e6);
+    if (!more) break;
+    const auto tw = std::chrono::steady_clock::now();
+    const int rg = gpu.valid() ? gpu.get() : GVH_OK;  // always joined before nxt goes away
+    pre_back(app, nxt, rg, nullptr, &memos);
+    if (prof) fprintf(stderr, "blocks %zu: gpu wait + back %.3f ms\n", b + 1, ns_since(tw) / 1e6);
+    if (rc == GVH_OK) rc = rg;
+    if (rc != GVH_OK) {
+      release_memos(app, memos);
+      return rc;
+    }
+    off += bn[b];
+    cur.epoch = nxt.epoch;
+  }
+  return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2418,6 +2677,15 @@ int gvh_deliver_block_codes(gvh_app* app, size_t ntx, const uint8_t* const* txs,
                             uint32_t* codes) {
   if (!app || (ntx && (!txs || !lens || !codes))) return GVH_EINVAL;
   return deliver_block(app, ntx, txs, lens, nullptr, codes);
+}
+
+int gvh_deliver_blocks(gvh_app* app, size_t n_blocks, const size_t* block_ntx, const uint8_t* const* txs,
+                       const size_t* lens, uint32_t* codes) {
+  if (!app || (n_blocks && !block_ntx)) return GVH_EINVAL;
+  size_t ntx = 0;
+  for (size_t b = 0; b < n_blocks; ++b) ntx += block_ntx[b];
+  if (ntx && (!txs || !lens || !codes)) return GVH_EINVAL;
+  return deliver_blocks(app, n_blocks, block_ntx, txs, lens, codes);
 }
 
 int gvh_deliver_gentxs(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, gvh_result* out,
@@ -2545,6 +2813,7 @@ void gvh_set_cache_capacity(gvh_app* app, size_t entries) { app->cache.resize(st
 
 void gvh_set_keyed(gvh_app* app, int keyed, size_t load_min) {
   std::lock_guard<std::mutex> g(app->gpu_mu);
+  std::unique_lock<std::shared_mutex> wk(app->key_mu);
   app->keyed = keyed != 0;
   app->key_load_min = load_min;
 }

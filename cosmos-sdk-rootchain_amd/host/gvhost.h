@@ -124,6 +124,14 @@ int gvh_deliver_block(gvh_app* app, size_t ntx, const uint8_t* const* txs, const
 /* Same, returning only each tx's code (codes[i]; 0 = OK). */
 int gvh_deliver_block_codes(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens,
                             uint32_t* codes);
+/* n_blocks consecutive blocks (block_ntx[b] txs each, concatenated in txs /
+ * lens / codes) delivered in order -- the results and final state of calling
+ * gvh_deliver_block_codes once per block -- pipelined for block sync /
+ * replay: block b+1 is pre-verified (its sequence prediction carrying block
+ * b's increments and SetPubKeys) and its GPU batch runs while block b's
+ * DeliverTx loop runs. */
+int gvh_deliver_blocks(gvh_app* app, size_t n_blocks, const size_t* block_ntx, const uint8_t* const* txs,
+                       const size_t* lens, uint32_t* codes);
 /* genutil.DeliverGenTxs: the block path at height 0 (account number 0,
  * infinite gas); *first_failed = index of the first tx whose result is not OK
  * (the reference panics on it), or ntx if all passed. */

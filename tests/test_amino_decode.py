@@ -114,3 +114,23 @@ def test_undecodable_tx_gets_err_tx_decode():
     for tx in (b"", b"\x01\x02", T.PREFIX_STDTX + b"\xff"):
         rc, r = app.ante(tx)
         assert rc == 0 and r["code"] == 2 and r["codespace"] == "sdk" and r["log"].endswith(": tx parse error")
+
+
+def test_pipelined_replay_without_gpu_work():
+    """gvh_deliver_blocks on blocks that never reach a signature (undecodable
+    txs, unknown signers) runs on the CPU alone and returns the codes of
+    delivering the blocks one by one; a block that does need the GPU reports
+    GVH_ENOVERIFIER instead of a verdict."""
+    app = gvhost.HostApp(None)
+    m = T.MsgSend(A, B, [(1, "x")])
+    unknown = T.std_tx([m], FEE, "", [(b"", b"\x00" * 64)])
+    blocks = [[b"", unknown, b"\x01\x02"], [unknown], [], [T.PREFIX_STDTX + b"\xff", unknown]]
+    rc, codes = app.deliver_blocks(blocks)
+    assert rc == 0
+    one = [list(app.deliver_block_codes(b)[1]) for b in blocks]
+    assert [list(c) for c in codes] == one
+    assert one[0] == [2, 9, 2] and one[3] == [2, 9]
+    app.set_account(A, 1, 0, T.amino_secp(bytes([2]) + bytes(range(1, 33))))
+    rc, _ = app.deliver_blocks([[unknown], [unknown]])
+    assert rc == gvhost.GVH_ENOVERIFIER
+    app.close()

@@ -313,7 +313,7 @@ def c1_blocks(wl, ntx: int = 10000, steady_blocks: int = 4, threads: int = 16):
             "raw": raw, "pubk": pubk}
 
 
-def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: int = 64, steady_blocks: int = 4,
+def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: int = 64, steady_blocks: int = 8,
             wl=None, threads: int = 16):
     """BASELINE.json configs[0] shape: 10k single-signer bank MsgSend txs (amino
     StdTx) through the host mirror: the block path (DeliverBlock = PreVerifyTxs,
@@ -361,7 +361,31 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: in
               "ms_per_block": round(t_steady / len(later_blobs) * 1e3, 2), "accepted": acc_steady,
               "preverify_ms_per_block": round((st2["preverify_ns"] - st["preverify_ns"]) / 1e6 / len(later_blobs), 2),
               "gpu_ms_per_block": round((st2["gpu_ns"] - st["gpu_ns"]) / 1e6 / len(later_blobs), 2),
-              "ante_loop_ms_per_block": round((st2["deliver_loop_ns"] - st["deliver_loop_ns"]) / 1e6 / len(later_blobs), 2)}
+              "ante_loop_ms_per_block": round((st2["deliver_loop_ns"] - st["deliver_loop_ns"]) / 1e6 / len(later_blobs), 2),
+              "note": "one block at a time (gvh_deliver_block_codes): PreVerifyTxs, GPU batch, DeliverTx loop"}
+    # the same steady blocks as one pipelined replay (gvh_deliver_blocks: block
+    # b+1 pre-verified and its GPU batch run while block b delivers)
+    app = fresh_app()
+    rc, _ = app.deliver_block_blob(*first_blob)
+    assert rc == 0
+    cat = np.concatenate([b[0] for b in later_blobs])
+    base = np.cumsum([0] + [len(b[0]) for b in later_blobs[:-1]]).astype(np.uint64)
+    offs = np.concatenate([b[1] + base[k] for k, b in enumerate(later_blobs)])
+    lens_ = np.concatenate([b[2] for b in later_blobs])
+    st = app.stats()
+    t = time.perf_counter()
+    rc, cp = app.deliver_blocks_blob(cat, offs, lens_, [len(b[1]) for b in later_blobs])
+    t_pipe = time.perf_counter() - t
+    st2 = app.stats()
+    app.close()
+    assert rc == 0
+    piped = {"blocks": len(later_blobs), "txs_per_s": round(ntx * len(later_blobs) / t_pipe, 1),
+             "ms_per_block": round(t_pipe / len(later_blobs) * 1e3, 2), "accepted": int((cp == 0).sum()),
+             "gpu_ms_per_block": round((st2["gpu_ns"] - st["gpu_ns"]) / 1e6 / len(later_blobs), 2),
+             "memo_hits": st2["memo_hits"] - st["memo_hits"],
+             "note": "the same steady blocks as ONE gvh_deliver_blocks call (block sync / replay): block b+1's "
+                     "PreVerifyTxs (prediction carrying block b's increments) before block b's DeliverTx loop, "
+                     "its GPU batch on a helper thread under that loop"}
     # per-tx path (CheckTx without batching): one GPU call per tx
     app = fresh_app()
     m = min(per_tx_sample, ntx)
@@ -432,6 +456,7 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: in
     return {"txs": ntx,
             "checktx_serial": serial,
             "block_path_steady": steady,
+            "replay_pipelined_steady": piped,
             "block_path": {"txs_per_s": round(ntx / t_block, 1), "total_ms": round(t_block * 1e3, 2),
                            "preverify_ms": round(st["preverify_ns"] / 1e6, 2), "gpu_ms": round(st["gpu_ns"] / 1e6, 2),
                            "ante_loop_ms": round(st["deliver_loop_ns"] / 1e6, 2),
@@ -529,14 +554,36 @@ def c4_multisig(ver, wl, block: int = 10000, threads: int = 16, n_accounts: int 
     el = time.perf_counter() - t
     st = app.stats()
     app.close()
-    return {"txs": ntx, "leaves": leaves, "block_txs": block, "blocks": (ntx + block - 1) // block,
-            "rejected": bad, "mismatches": bad, "leaves_per_s": round(leaves / el, 1), "txs_per_s": round(ntx / el, 1),
-            "seconds": round(el, 3), "preverify_s": round(st["preverify_ns"] / 1e9, 3),
+    one = {"leaves_per_s": round(leaves / el, 1), "txs_per_s": round(ntx / el, 1), "seconds": round(el, 3),
+           "rejected": bad, "preverify_s": round(st["preverify_ns"] / 1e9, 3), "gpu_s": round(st["gpu_ns"] / 1e9, 3),
+           "ante_loop_s": round(st["deliver_loop_ns"] / 1e9, 3), "gpu_calls": st["gpu_calls"],
+           "memo_hits": st["memo_hits"],
+           "note": "one block at a time (gvh_deliver_block_codes per block)"}
+    # the replay as it is run: one pipelined gvh_deliver_blocks call over every block
+    app = gvhost.HostApp(ver, chain_id="gv-bench", height=1)
+    app.set_threads(threads)
+    for addr, num in accts:
+        app.set_account(addr, num, 0)
+    nb = (ntx + block - 1) // block
+    t = time.perf_counter()
+    rc, codes = app.deliver_blocks_blob(blob, offs, lens, [min(block, ntx - b * block) for b in range(nb)])
+    el = time.perf_counter() - t
+    st = app.stats()
+    app.close()
+    assert rc == 0
+    bad_p = int(np.count_nonzero(codes))
+    return {"txs": ntx, "leaves": leaves, "block_txs": block, "blocks": nb,
+            "rejected": bad_p, "mismatches": bad_p, "leaves_per_s": round(leaves / el, 1),
+            "txs_per_s": round(ntx / el, 1), "seconds": round(el, 3), "preverify_front_s": round(st["preverify_ns"] / 1e9, 3),
             "gpu_s": round(st["gpu_ns"] / 1e9, 3), "ante_loop_s": round(st["deliver_loop_ns"] / 1e9, 3),
             "gpu_calls": st["gpu_calls"], "gpu_leaves": st["gpu_leaves"], "memo_hits": st["memo_hits"],
+            "one_block_at_a_time": one,
             "workload_gen_s": round(t_gen, 1), "host_threads": threads,
             "note": "2-of-3 / 3-of-5 / 4-of-7 threshold accounts (30k), first k bits set, every tx valid by "
-                    "construction; amino StdTx bytes through the host mirror, host buffers"}
+                    "construction; amino StdTx bytes through the host mirror, host buffers; leaves_per_s = the "
+                    "pipelined replay (gvh_deliver_blocks over all blocks: block b+1's PreVerifyTxs and GPU batch "
+                    "under block b's DeliverTx loop); one_block_at_a_time = the same blocks through "
+                    "gvh_deliver_block_codes one by one"}
 
 
 # ed25519 work per verify, same basis as bench.py's W (field mul 72, square 44
