@@ -1,0 +1,233 @@
+// ed_lat.hip -- small ed25519 batches against cached keys:
+// the IBC 07-tendermint commit checks (a validator set's keys sign every
+// block) and multisig ed25519 sub-keys of accounts, on the limb-sliced field
+// layer (ed_fsl.cuh).  Same verdict as go1.14 crypto/ed25519 Verify (via
+// tendermint v0.33.4 PubKeyEd25519.VerifyBytes) and as the throughput
+// kernels (ed_verify.hip); only the schedule differs.
+//
+//   k_ed_keys    one lane per key: FromBytes(A) (the reference's lenient
+//                decode), then the comb table of -A: j * 16^w * (-A) for
+//                w < 64, j = 1..8, cached form (Y+X, Y-X, 2Z, 2dT), no
+//                inversion: 73,728 B per key; the raw key bytes (hashed by
+//                Verify) and the decode verdict beside it.
+//   k_ed_lat_sl  one signature per 256-thread block.  Phase 1, concurrently:
+//                wave 0 stages the message in LDS and computes
+//                h = SHA-512(R || A || M) mod L and its 64 signed radix-16
+//                digits; wave 1 decodes R strictly (efsl_decode_strict: the
+//                point R' must equal, so no inversion of Z' is needed) and
+//                checks S (sig[63] & 224, ScMinimal); waves 2-3 add the 32
+//                [s]B comb entries (4 per row).  Phase 2: the 16 rows add the
+//                64 [h](-A) entries of the key's table (4 per row) -- no
+//                doublings at all --, two shuffle rounds per wave and two more
+//                in wave 0 sum the rows, and R' == (x_R, y_R) is checked
+//                projectively.
+#include <hip/hip_runtime.h>
+
+#include "ed_fsl.cuh"
+#include "gv_kernels.h"
+
+#if defined(__HIP_DEVICE_COMPILE__) && defined(__AMDGCN_WAVEFRONT_SIZE) && __AMDGCN_WAVEFRONT_SIZE != 64
+#error "ed_lat.hip places four 16-lane rows in a wave64"
+#endif
+
+namespace gv {
+namespace ed {
+
+static_assert(GV_EDK_WORDS == 64 * 8 * ED_CACHED_WORDS, "key table size");
+
+__global__ __launch_bounds__(64) void k_ed_keys(const uint8_t* pub32, uint32_t n, uint32_t base, uint32_t* ktab,
+                                                uint32_t* kpub, uint32_t* kok) {
+  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+  if (g >= n) return;
+  u32 pw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint8_t* p = pub32 + (size_t)g * 32 + 4 * i;
+    pw[i] = (u32)p[0] | ((u32)p[1] << 8) | ((u32)p[2] << 16) | ((u32)p[3] << 24);
+    kpub[(size_t)(base + g) * 8 + i] = pw[i];
+  }
+  ge_ext a, P;
+  const bool ok = ge_frombytes(a, pw);
+  kok[base + g] = ok ? 1u : 0u;
+  ge_neg(P, a);
+  u32* tab = ktab + (size_t)(base + g) * GV_EDK_WORDS;
+#pragma unroll 1
+  for (int w = 0; w < 64; ++w) {
+    if (w) {
+      ge_dbl_t<false>(P, P);
+      ge_dbl_t<false>(P, P);
+      ge_dbl_t<false>(P, P);
+      ge_dbl_t<true>(P, P);
+    }
+    ge_cached c1, c;
+    ge_to_cached(c1, P);
+    atab_store(tab + (size_t)(w * 8) * ED_CACHED_WORDS, 1, 0, c1);
+    ge_ext acc = P;
+#pragma unroll 1
+    for (int j = 2; j <= 8; ++j) {
+      ge_add_cached(acc, acc, c1, false);
+      ge_to_cached(c, acc);
+      atab_store(tab + (size_t)(w * 8 + j - 1) * ED_CACHED_WORDS, 1, 0, c);
+    }
+  }
+}
+
+#define EDL_MSG_LDS 2048
+
+// Message bytes for sha512_pre64: the staged prefix from LDS (an LDS
+// pointer, not a generic one), the rest from global memory.
+typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+struct LdsMsg {
+  lds_u8* s;
+  const uint8_t* g;
+  GV_DEV u32 operator()(u32 i) const { return i < EDL_MSG_LDS ? (u32)s[i] : (u32)g[i]; }
+};
+
+struct EdlShared {
+  uint8_t msg[EDL_MSG_LDS];                 // the message's first bytes (wave 0)
+  int hd[64];                               // signed radix-16 digits of h
+  u32 xr[16], yr[16];                       // the decoded R, sliced
+  u32 flags;                                // bit 0: R decodes, bit 1: S checks
+  u32 pt[4][4][16];                         // wave sums X, Y, Z, T
+};
+
+__global__ __launch_bounds__(256) void k_ed_lat_sl(const gvk_edl b) {
+  __shared__ EdlShared sh;
+  const u32 gi = blockIdx.x;                // grid = n: every block is live
+  const u32 lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  u32 sl = b.slot[gi];
+  bool kok = sl < b.kcount;
+  if (!kok) sl = 0;                         // the arena always holds slot 0's memory
+  kok = kok && b.kok[sl] != 0u;
+  u32 sw[16];
+  {
+    const uint4* sp = (const uint4*)(b.sig64 + (size_t)gi * 64);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4 v = sp[q];
+      sw[4 * q] = v.x; sw[4 * q + 1] = v.y; sw[4 * q + 2] = v.z; sw[4 * q + 3] = v.w;
+    }
+  }
+  const fslk k = efsl_consts();
+  const u32 L = k.L, row = threadIdx.x >> 4;            // row 0..15
+  const bool lo = L < 9u;
+  gesl A;
+  gesl_identity(A, k);
+  if (wave == 0u) {
+    // h = SHA-512(R || A || M) mod L; the message staged in LDS first (one
+    // load per lane per 64 bytes instead of a serial byte stream)
+    const uint8_t* m = b.msg_blob ? b.msg_blob + b.msg_off[gi] : nullptr;
+    const u32 len = b.msg_len[gi];
+    const u32 staged = len < EDL_MSG_LDS ? len : EDL_MSG_LDS;
+    for (u32 i = lane; i < staged; i += 64u) sh.msg[i] = m[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    u32 pre[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      pre[i] = sw[i];
+      pre[8 + i] = b.kpub[(size_t)sl * 8 + i];
+    }
+    u32 dig[16], h[8];
+    sha512_pre64(dig, pre, LdsMsg{(const lds_u8*)sh.msg, m}, len);
+    sc_reduce512(h, dig);
+    const uint64_t car = sc_radix16_carries(h);
+    const u32 nib = (h[lane >> 3] >> (4u * (lane & 7u))) & 15u;
+    const int cin = lane > 0u ? (int)((car >> (lane - 1u)) & 1u) : 0;
+    const int cout = lane < 63u ? (int)((car >> lane) & 1u) : 0;
+    sh.hd[lane] = (int)nib + cin - 16 * cout;
+  } else if (wave == 1u) {
+    u32 x, y;
+    const bool rok = efsl_decode_strict(x, y, sw, k);
+    const bool sok = (sw[15] >> 29) == 0u && sc_minimal(sw + 8);   // sig[63] & 224 == 0, ScMinimal
+    if (lane < 16u) {
+      sh.xr[L] = x;
+      sh.yr[L] = y;
+    }
+    if (lane == 0u) sh.flags = (rok ? 1u : 0u) | (sok ? 2u : 0u);
+  } else {
+    // [s]B: signed radix-256 digits of s (LSB-first carries, ed_ladder_check's
+    // recoding), windows r, r+8, r+16, r+24 of this row of waves 2-3
+    u32 cmask = 0, c = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const u32 byte = (sw[8 + (i >> 2)] >> (8 * (i & 3))) & 0xFFu;
+      c = (byte + c) > 128u ? 1u : 0u;
+      cmask |= c << i;
+    }
+    const u32 r8 = row - 8u;
+#pragma unroll 1
+    for (u32 w = r8; w < 32u; w += 8u) {
+      const int byte = (int)((sw[8 + (w >> 2)] >> (8 * (w & 3))) & 0xFFu);
+      const int cin = w > 0u ? (int)((cmask >> (w - 1u)) & 1u) : 0;
+      const int dg = byte + cin - 256 * (int)((cmask >> w) & 1u);
+      if (dg != 0) {
+        const u32 mag = (u32)(dg < 0 ? -dg : dg);
+        const u32* e = b.btab + (size_t)(w * ED_BTAB_ENTRIES + mag) * ED_PRE_WORDS;
+        gesl_add_pre(A, A, lo ? e[L] : 0u, lo ? e[9 + L] : 0u, lo ? e[18 + L] : 0u, dg < 0, k);
+      }
+    }
+  }
+  __syncthreads();
+  // [h](-A): windows row, row + 16, row + 32, row + 48 from the key's table
+  const u32* kt = b.ktab + (size_t)sl * GV_EDK_WORDS;
+#pragma unroll 1
+  for (u32 w = row; w < 64u; w += 16u) {
+    const int dg = sh.hd[w];
+    if (dg != 0) {
+      const u32 mag = (u32)(dg < 0 ? -dg : dg);
+      const u32* e = kt + (size_t)(w * 8u + mag - 1u) * ED_CACHED_WORDS;
+      gesl_add_cached(A, A, lo ? e[L] : 0u, lo ? e[9 + L] : 0u, lo ? e[18 + L] : 0u, lo ? e[27 + L] : 0u, dg < 0, k);
+    }
+  }
+  const u32 d2 = efsl_const(kEd2D, k);
+#pragma unroll 1
+  for (int msk = 16; msk < 64; msk <<= 1) {
+    const gesl O = gesl_shfl_xor(A, msk);
+    gesl_add(A, A, O, d2, k);
+  }
+  if (lane < 16u && lo) {
+    sh.pt[wave][0][L] = A.X; sh.pt[wave][1][L] = A.Y; sh.pt[wave][2][L] = A.Z; sh.pt[wave][3][L] = A.T;
+  }
+  __syncthreads();
+  if (wave != 0u) return;
+  const u32 part = lane >> 4;                           // wave 0, row r: wave r's sum
+  A.X = lo ? sh.pt[part][0][L] : 0u;
+  A.Y = lo ? sh.pt[part][1][L] : 0u;
+  A.Z = lo ? sh.pt[part][2][L] : 0u;
+  A.T = lo ? sh.pt[part][3][L] : 0u;
+#pragma unroll 1
+  for (int msk = 16; msk < 64; msk <<= 1) {
+    const gesl O = gesl_shfl_xor(A, msk);
+    gesl_add(A, A, O, d2, k);
+  }
+  // R' == (x_R, y_R): X' == x_R Z', Y' == y_R Z'
+  const u32 xr = lo ? sh.xr[L] : 0u, yr = lo ? sh.yr[L] : 0u;
+  u32 w1[8], w2[8], w3[8], w4[8];
+  efsl_to_words(w1, A.X);
+  efsl_to_words(w2, fsl_mul(xr, A.Z, k));
+  efsl_to_words(w3, A.Y);
+  efsl_to_words(w4, fsl_mul(yr, A.Z, k));
+  u32 diff = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) diff |= (w1[i] ^ w2[i]) | (w3[i] ^ w4[i]);
+  const bool ok = kok && (sh.flags & 3u) == 3u && diff == 0u;
+  if (threadIdx.x == 0) b.out8[gi] = ok ? 1u : 0u;
+}
+
+}  // namespace ed
+}  // namespace gv
+
+extern "C" hipError_t gvk_ed_keys(const uint8_t* pub32, uint32_t n, uint32_t base, uint32_t* ktab, uint32_t* kpub,
+                                  uint32_t* kok, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(gv::ed::k_ed_keys, dim3((n + 63) / 64), dim3(64), 0, st, pub32, n, base, ktab, kpub, kok);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t gvk_ed_lat(const gvk_edl* b, hipStream_t st) {
+  if (b->n == 0) return hipSuccess;
+  hipLaunchKernelGGL(gv::ed::k_ed_lat_sl, dim3(b->n), dim3(256), 0, st, *b);
+  return hipGetLastError();
+}

@@ -123,6 +123,27 @@ typedef struct gvk_ed {
 } gvk_ed;
 hipError_t gvk_ed_btab(uint32_t* btab, hipStream_t st);
 hipError_t gvk_ed_verify(const gvk_ed* b, hipStream_t st);
+// ed25519 key arena (gv_ed_keys_load): per slot the comb table of -A,
+// j * 16^w * (-A), w < 64, j = 1..8, cached form (36 words each), the raw key
+// words (8) and the FromBytes verdict.
+#define GV_EDK_WORDS (64 * 8 * 36)
+typedef struct gvk_edl {
+  uint32_t n;
+  const uint32_t* slot;         // n key slots
+  const uint8_t* sig64;         // n x 64
+  const uint8_t* msg_blob;
+  const uint64_t* msg_off;
+  const uint32_t* msg_len;
+  const uint32_t* ktab;         // kcap x GV_EDK_WORDS
+  const uint32_t* kpub;         // kcap x 8
+  const uint32_t* kok;          // kcap
+  uint32_t kcount;
+  const uint32_t* btab;         // GV_ED_BTAB_WORDS
+  uint8_t* out8;                // n verdict bytes
+} gvk_edl;
+hipError_t gvk_ed_keys(const uint8_t* pub32, uint32_t n, uint32_t base, uint32_t* ktab, uint32_t* kpub, uint32_t* kok,
+                       hipStream_t st);
+hipError_t gvk_ed_lat(const gvk_edl* b, hipStream_t st);
 
 hipError_t gvk_gen_gtable(uint32_t* gtab, hipStream_t st);
 // the keyed ladder's G tables (GV_KEY2_TABLES x 2 x GV_GTAB_N x 16 words); base_scratch: 48 words

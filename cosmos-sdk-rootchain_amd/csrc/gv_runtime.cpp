@@ -321,6 +321,12 @@ struct Dev {
     hipEvent_t last = nullptr;                    // end of the last work using the scratch
     hipStream_t last_st = nullptr;
   } ed;
+  // ed25519 key arena (gv_ed_keys_load): per slot the comb table of -A
+  // (GV_EDK_WORDS), the raw key words (8), the FromBytes verdict
+  uint32_t *ektab = nullptr, *ekpub = nullptr, *ekok = nullptr;
+  size_t ekcap = 0;
+  uint8_t* edl_h = nullptr;                       // small keyed ed25519 batches: pinned inputs + verdicts (zero-copy)
+  size_t edl_h_cap = 0;
   std::mutex mu;
   Pool* pool = nullptr;                           // staging memcpy threads: the context's shared pool
   Worker* worker = nullptr;                       // slice runner (devices 1..n-1 of a context)
@@ -522,6 +528,12 @@ struct gv_ctx {
   size_t keys = 0;              // key-arena slots in use (same on every device)
   std::atomic<uint64_t> keys_gen{0};  // gv_keys_reset calls
   std::mutex keys_mu;
+  // ed25519 key arena (gv_ed_keys_load), same on every device
+  size_t ed_keys = 0;
+  std::atomic<uint64_t> ed_keys_gen{0};
+  std::mutex ed_keys_mu;
+  std::vector<uint8_t> ed_kpub;  // the raw keys per slot (large keyed batches run the throughput kernels on them)
+  size_t ed_lat_max = 2048;      // keyed ed25519 batches up to this size take k_ed_lat_sl (one signature per block)
 };
 
 namespace {
@@ -1311,6 +1323,8 @@ void gv_close(gv_ctx* ctx) {
     if (d->ed.h_blob) (void)hipHostFree(d->ed.h_blob);
     if (d->ed.h_bits) (void)hipHostFree(d->ed.h_bits);
     if (d->ed.last) (void)hipEventDestroy(d->ed.last);
+    for (uint32_t* p : {d->ektab, d->ekpub, d->ekok}) if (p) (void)hipFree(p);
+    if (d->edl_h) (void)hipHostFree(d->edl_h);
     for (auto& rs : d->ring)
       for (auto e : rs) if (e) (void)hipEventDestroy(e);
     for (hipStream_t t : {d->lo_st[0], d->lo_st[1], d->hi_st})
@@ -1472,6 +1486,139 @@ int gv_keys_reset(gv_ctx* ctx) {
 
 size_t gv_keys_count(const gv_ctx* ctx) { return ctx ? ctx->keys : 0; }
 
+// ---- ed25519 key arena + small keyed batches (k_ed_keys, k_ed_lat_sl)
+namespace {
+int ensure_ed_keys(Dev* d, size_t need, size_t used, hipStream_t st) {
+  if (need <= d->ekcap) return GV_OK;
+  const size_t cap = round_up(std::max<size_t>({need, 2 * d->ekcap, 256}), 256);
+  uint32_t *t = nullptr, *p = nullptr, *o = nullptr;
+  auto fail = [&]() {
+    for (uint32_t* q : {t, p, o}) if (q) (void)hipFree(q);
+    return GV_ENOMEM;
+  };
+  if (hipMalloc(&t, cap * (size_t)GV_EDK_WORDS * 4) != hipSuccess) return fail();
+  if (hipMalloc(&p, cap * 8 * 4) != hipSuccess) return fail();
+  if (hipMalloc(&o, cap * 4) != hipSuccess) return fail();
+  if (used) {
+    CK(hipMemcpyAsync(t, d->ektab, used * (size_t)GV_EDK_WORDS * 4, hipMemcpyDeviceToDevice, st));
+    CK(hipMemcpyAsync(p, d->ekpub, used * 8 * 4, hipMemcpyDeviceToDevice, st));
+    CK(hipMemcpyAsync(o, d->ekok, used * 4, hipMemcpyDeviceToDevice, st));
+    CK(hipStreamSynchronize(st));
+  }
+  for (uint32_t* q : {d->ektab, d->ekpub, d->ekok}) if (q) (void)hipFree(q);
+  d->ektab = t; d->ekpub = p; d->ekok = o; d->ekcap = cap;
+  return GV_OK;
+}
+}  // namespace
+
+int gv_ed_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub32, uint32_t* slot_out) {
+  if (!ctx) return GV_EINVAL;
+  if (n == 0) return GV_OK;
+  if (!pub32 || !slot_out) return GV_EINVAL;
+  std::lock_guard<std::mutex> kl(ctx->ed_keys_mu);
+  const size_t base = ctx->ed_keys;
+  if (base + n > kMaxItems) return GV_EINVAL;
+  for (Dev* d : ctx->devs) {                    // every device holds every key
+    std::lock_guard<std::mutex> lk(d->mu);
+    CK(hipSetDevice(d->id));
+    hipStream_t st = d->set[0].st;
+    int rc = ensure_ed_keys(d, base + n, base, st);
+    if (rc) return rc;
+    uint8_t* dp = nullptr;
+    if (hipMalloc(&dp, n * 32) != hipSuccess) return GV_ENOMEM;
+    if (hipMemcpyAsync(dp, pub32, n * 32, hipMemcpyHostToDevice, st) != hipSuccess ||
+        gvk_ed_keys(dp, (uint32_t)n, (uint32_t)base, d->ektab, d->ekpub, d->ekok, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+      (void)hipFree(dp);
+      return GV_EHIP;
+    }
+    (void)hipFree(dp);
+  }
+  ctx->ed_kpub.insert(ctx->ed_kpub.end(), pub32, pub32 + n * 32);
+  ctx->ed_keys = base + n;
+  for (size_t i = 0; i < n; ++i) slot_out[i] = (uint32_t)(base + i);
+  return GV_OK;
+}
+
+int gv_ed_keys_reset(gv_ctx* ctx) {
+  if (!ctx) return GV_EINVAL;
+  std::lock_guard<std::mutex> kl(ctx->ed_keys_mu);
+  ctx->ed_keys = 0;
+  ctx->ed_kpub.clear();
+  ctx->ed_keys_gen.fetch_add(1);
+  return GV_OK;
+}
+size_t gv_ed_keys_count(const gv_ctx* ctx) { return ctx ? ctx->ed_keys : 0; }
+uint64_t gv_ed_keys_generation(const gv_ctx* ctx) { return ctx ? ctx->ed_keys_gen.load() : 0; }
+
+int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64,
+                                 const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len,
+                                 uint8_t* out_ok) {
+  if (!ctx) return GV_EINVAL;
+  if (ctx->fault_inject) return GV_EFAULT;
+  if (n == 0) return GV_OK;
+  if (!slot || !sig64 || !msg_off || !msg_len || !out_ok) return GV_EINVAL;
+  for (size_t i = 0; i < n; ++i)
+    if (msg_len[i] && !msg_blob) return GV_EINVAL;
+  size_t kcount;
+  {
+    std::lock_guard<std::mutex> kl(ctx->ed_keys_mu);
+    kcount = ctx->ed_keys;
+    if (n > ctx->ed_lat_max || kcount == 0) {
+      // large batches: the throughput kernels over the slots' raw keys
+      std::vector<uint8_t> pub(n * 32, 0);
+      for (size_t i = 0; i < n; ++i)
+        if (slot[i] < kcount) memcpy(&pub[i * 32], &ctx->ed_kpub[(size_t)slot[i] * 32], 32);
+      int rc = kcount ? run_ed_host(ctx, n, EdHost{pub.data(), sig64, msg_blob, msg_off, msg_len, out_ok}) : GV_OK;
+      if (rc) return rc;
+      for (size_t i = 0; i < n; ++i)
+        if (slot[i] >= kcount) out_ok[i] = 0;              // no key in that slot: never a valid signature
+      return GV_OK;
+    }
+  }
+  Dev* d = ctx->devs[0];
+  std::lock_guard<std::mutex> lk(d->mu);
+  CK(hipSetDevice(d->id));
+  hipStream_t st = d->set[0].st;
+  int rc = ed_ensure(d, 256, st);                 // the resident comb table of B
+  if (rc) return rc;
+  uint64_t lo = UINT64_MAX, hi = 0;
+  for (size_t i = 0; i < n; ++i) {
+    lo = std::min<uint64_t>(lo, msg_off[i]);
+    hi = std::max<uint64_t>(hi, msg_off[i] + msg_len[i]);
+  }
+  if (lo > hi) lo = hi = 0;
+  // zero-copy: the kernel reads the pinned inputs and writes verdict bytes
+  const size_t o_sig = round_up(n * 4, 64), o_off = o_sig + n * 64, o_len = o_off + n * 8, o_out = o_len + n * 4,
+               o_blob = round_up(o_out + n, 64), total = o_blob + (hi - lo);
+  if ((rc = ensure_pinned(&d->edl_h, &d->edl_h_cap, total))) return rc;
+  uint8_t* h = d->edl_h;
+  memcpy(h, slot, n * 4);
+  memcpy(h + o_sig, sig64, n * 64);
+  uint64_t* ro = (uint64_t*)(h + o_off);
+  for (size_t i = 0; i < n; ++i) ro[i] = msg_off[i] - lo;
+  memcpy(h + o_len, msg_len, n * 4);
+  if (hi > lo) memcpy(h + o_blob, msg_blob + lo, hi - lo);
+  gvk_edl b;
+  memset(&b, 0, sizeof b);
+  b.n = (uint32_t)n;
+  b.slot = (const uint32_t*)h;
+  b.sig64 = h + o_sig;
+  b.msg_blob = h + o_blob;
+  b.msg_off = (const uint64_t*)(h + o_off);
+  b.msg_len = (const uint32_t*)(h + o_len);
+  b.ktab = d->ektab;
+  b.kpub = d->ekpub;
+  b.kok = d->ekok;
+  b.kcount = (uint32_t)kcount;
+  b.btab = d->edtab;
+  b.out8 = h + o_out;
+  CK(gvk_ed_lat(&b, st));
+  CK(hipStreamSynchronize(st));
+  memcpy(out_ok, h + o_out, n);
+  return GV_OK;
+}
+
 int gv_host_alloc(gv_ctx* ctx, size_t bytes, void** out) {
   if (!ctx || !out || bytes == 0) return GV_EINVAL;
   *out = nullptr;
@@ -1567,6 +1714,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
     if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
     if (!strcmp(key, "lat_sl_max")) ctx->lat_sl_max = (size_t)val;
     ctx->lat_sl_max_keyed = (size_t)val;
+  } else if (!strcmp(key, "ed_lat_max")) {
+    if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
+    ctx->ed_lat_max = (size_t)val;
   } else if (!strcmp(key, "lat_zero_copy")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->lat_zero_copy = val != 0;

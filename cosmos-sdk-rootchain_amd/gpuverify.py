@@ -43,6 +43,7 @@ EXPORTED_SYMBOLS = (
     "gv_verify_digests_keyed", "gv_verify_msgs_keyed", "gv_dev_verify_digests_keyed", "gv_stage_stats4",
     "gv_keys_point", "gv_dev_stream_create", "gv_dev_stream_sync", "gv_dev_stream_destroy",
     "gv_verify_ed25519_msgs", "gv_dev_verify_ed25519_msgs", "gv_last_slices", "gv_group_stats", "gv_host_alloc", "gv_host_free",
+    "gv_ed_keys_load", "gv_ed_keys_reset", "gv_ed_keys_count", "gv_ed_keys_generation", "gv_verify_ed25519_msgs_keyed",
 )
 
 
@@ -92,6 +93,16 @@ def load(path: str = LIB_PATH):
     L.gv_verify_ed25519_msgs.restype = i32
     L.gv_dev_verify_ed25519_msgs.argtypes = [vp, i32, sz, vp, vp, vp, vp, vp, vp, vp]
     L.gv_dev_verify_ed25519_msgs.restype = i32
+    L.gv_ed_keys_load.argtypes = [vp, sz, vp, vp]
+    L.gv_ed_keys_load.restype = i32
+    L.gv_ed_keys_reset.argtypes = [vp]
+    L.gv_ed_keys_reset.restype = i32
+    L.gv_ed_keys_count.argtypes = [vp]
+    L.gv_ed_keys_count.restype = sz
+    L.gv_ed_keys_generation.argtypes = [vp]
+    L.gv_ed_keys_generation.restype = ctypes.c_uint64
+    L.gv_verify_ed25519_msgs_keyed.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp]
+    L.gv_verify_ed25519_msgs_keyed.restype = i32
     L.gv_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_longlong]
     L.gv_set_option.restype = i32
     L.gv_last_stage_ms.argtypes = [vp, i32] + [ctypes.POINTER(ctypes.c_float)] * 3
@@ -330,6 +341,43 @@ class Verifier:
                                                   _ptr(np.ascontiguousarray(off, dtype=np.uint64)),
                                                   _ptr(np.ascontiguousarray(ln, dtype=np.uint32)), _ptr(out)),
                    "gv_verify_ed25519_msgs")
+        return out
+
+    def ed_keys_load(self, pub32: np.ndarray) -> np.ndarray:
+        """FromBytes + the comb table of -A, kept resident per key; returns the slots (u32)."""
+        pub32 = np.ascontiguousarray(pub32, dtype=np.uint8)
+        n = pub32.shape[0]
+        assert pub32.shape == (n, 32)
+        slots = np.zeros(n, dtype=np.uint32)
+        if n:
+            _check(self._L.gv_ed_keys_load(self._ctx, n, _ptr(pub32), _ptr(slots)), "gv_ed_keys_load")
+        return slots
+
+    def ed_keys_reset(self):
+        _check(self._L.gv_ed_keys_reset(self._ctx), "gv_ed_keys_reset")
+
+    @property
+    def ed_keys_count(self) -> int:
+        return self._L.gv_ed_keys_count(self._ctx)
+
+    @property
+    def ed_keys_generation(self) -> int:
+        return self._L.gv_ed_keys_generation(self._ctx)
+
+    def verify_batch_ed25519_keyed(self, slots: np.ndarray, sig64: np.ndarray, msgs) -> np.ndarray:
+        """verify_batch_ed25519 with the key of each item given by its ed25519 key-arena slot."""
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        sig64 = np.ascontiguousarray(sig64, dtype=np.uint8)
+        blob, off, ln = pack_msgs(msgs) if isinstance(msgs, (list, tuple)) and (
+            len(msgs) == 0 or isinstance(msgs[0], (bytes, bytearray))) else msgs
+        n = slots.shape[0]
+        assert sig64.shape == (n, 64) and len(off) == n and len(ln) == n
+        out = np.zeros(n, dtype=np.uint8)
+        if n:
+            _check(self._L.gv_verify_ed25519_msgs_keyed(self._ctx, n, _ptr(slots), _ptr(sig64), _ptr(blob),
+                                                        _ptr(np.ascontiguousarray(off, dtype=np.uint64)),
+                                                        _ptr(np.ascontiguousarray(ln, dtype=np.uint32)), _ptr(out)),
+                   "gv_verify_ed25519_msgs_keyed")
         return out
 
     def dev_verify_ed25519(self, slot: int, n: int, d_pub, d_sig, d_blob, d_off, d_len, d_bits, stream=None):

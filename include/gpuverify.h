@@ -183,6 +183,27 @@ int gv_verify_ed25519_msgs(gv_ctx* ctx, size_t n, const uint8_t* pub32, const ui
 int gv_dev_verify_ed25519_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub32, const void* d_sig64,
                                const void* d_msg_blob, const void* d_msg_off, const void* d_msg_len, void* d_bits,
                                void* stream);
+/* Cached ed25519 keys: the IBC 07-tendermint light client verifies a
+ * validator set's commit signatures block after block
+ * (x/ibc/07-tendermint/update.go:88 lite.Verify, misbehaviour.go:88-97
+ * VerifyCommitTrusting), and multisig accounts keep their ed25519 sub-keys.
+ * gv_ed_keys_load runs FromBytes once per key and keeps the comb table of -A
+ * (j * 16^w * (-A), w < 64, j <= 8: 72 KB per key) and the raw key bytes
+ * resident on every device; slot_out[i] receives key i's slot (a key
+ * FromBytes rejects gets one too, and every verify against it is false).
+ * gv_verify_ed25519_msgs_keyed gives exactly gv_verify_ed25519_msgs's verdict
+ * with pub32 = the key loaded into slot[i] (a slot >= gv_ed_keys_count()
+ * gives false).  Batches up to "ed_lat_max" (default 2048) take k_ed_lat_sl
+ * (one signature per block, no doublings: ~0.1 ms end to end), larger ones the
+ * throughput kernels.  Loading must not race keyed verifies of the same
+ * context; gv_ed_keys_generation counts gv_ed_keys_reset calls. */
+int gv_ed_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub32, uint32_t* slot_out);
+int gv_ed_keys_reset(gv_ctx* ctx);
+size_t gv_ed_keys_count(const gv_ctx* ctx);
+uint64_t gv_ed_keys_generation(const gv_ctx* ctx);
+int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64,
+                                 const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len,
+                                 uint8_t* out_ok);
 
 /* Options: "max_batch" (lanes per device launch, default 1<<20, at most
  * 0xFFFFFF00),
