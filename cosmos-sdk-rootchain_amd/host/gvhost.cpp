@@ -1392,6 +1392,17 @@ struct gvh_app {
     }
   };
   std::unordered_map<std::array<uint8_t, 33>, uint32_t, Key33Hash> key_slots;
+  // ed25519 keys (IBC validator sets, multisig ed25519 sub-keys): pub32 ->
+  // slot of the context's ed25519 key arena (gv_ed_keys_load); gpu_mu
+  struct Key32Hash {
+    size_t operator()(const std::array<uint8_t, 32>& k) const {
+      uint64_t h;
+      memcpy(&h, k.data(), 8);
+      return (size_t)(h * 0x9E3779B97F4A7C15ull);
+    }
+  };
+  std::unordered_map<std::array<uint8_t, 32>, uint32_t, Key32Hash> ed_slots;
+  uint64_t ed_key_gen = 0;
   uint64_t key_gen = 0;                        // gv_keys_generation the map belongs to
   bool keyed = true;
   size_t key_cap = GV_KEY_CAP;                 // arena reset past this many keys (5.4 KB of HBM each)
@@ -1849,13 +1860,65 @@ int verify_secp(gvh_app* app, GpuBatch& b) {
   return gv_verify_digests_keyed(app->gpu, m, b.slots, b.sig, b.dig, b.ok);
 }
 
+// m ed25519 leaves (gpu_mu held): keyed against the context's ed25519 key
+// arena when every key is resident, or when `load` (a commit's validator set,
+// a block-sized batch) -- the missing keys are then loaded with one
+// gv_ed_keys_load; otherwise, or on any arena problem, the unkeyed batch.
+// Same verdicts either way (gv_verify_ed25519_msgs_keyed's contract).
+int verify_ed(gvh_app* app, size_t m, const uint8_t* pub, const uint8_t* sig, const uint8_t* blob, const uint64_t* off,
+              const uint32_t* len, uint8_t* ok, bool load) {
+  if (!app->keyed) return gv_verify_ed25519_msgs(app->gpu, m, pub, sig, blob, off, len, ok);
+  auto& map = app->ed_slots;
+  const uint64_t gen = gv_ed_keys_generation(app->gpu);
+  if (gen != app->ed_key_gen) {                   // the arena was reset (here or by another user)
+    map.clear();
+    app->ed_key_gen = gen;
+  }
+  std::vector<uint32_t> slots(m);
+  std::vector<uint8_t> fresh;
+  std::vector<std::array<uint8_t, 32>> fresh_keys;
+  constexpr uint32_t kPending = 0x80000000u;
+  for (size_t k = 0; k < m; ++k) {
+    std::array<uint8_t, 32> key;
+    memcpy(key.data(), pub + 32 * k, 32);
+    auto it = map.find(key);
+    if (it != map.end()) { slots[k] = it->second; continue; }
+    if (!load) return gv_verify_ed25519_msgs(app->gpu, m, pub, sig, blob, off, len, ok);
+    auto ins = map.emplace(key, kPending + (uint32_t)fresh_keys.size());
+    if (ins.second) {
+      fresh.insert(fresh.end(), key.begin(), key.end());
+      fresh_keys.push_back(key);
+    }
+    slots[k] = ins.first->second;
+  }
+  if (!fresh_keys.empty()) {
+    const size_t nf = fresh_keys.size();
+    std::vector<uint32_t> got(nf);
+    const bool room = gv_ed_keys_count(app->gpu) + nf <= GV_ED_KEY_CAP;
+    if (!room || gv_ed_keys_load(app->gpu, nf, fresh.data(), got.data()) != GV_OK) {
+      if (!room) {
+        gv_ed_keys_reset(app->gpu);
+        map.clear();
+        app->ed_key_gen = gv_ed_keys_generation(app->gpu);
+      } else {
+        for (auto& key : fresh_keys) map.erase(key);
+      }
+      return gv_verify_ed25519_msgs(app->gpu, m, pub, sig, blob, off, len, ok);
+    }
+    for (size_t i = 0; i < nf; ++i) map[fresh_keys[i]] = got[i];
+    for (size_t k = 0; k < m; ++k)
+      if (slots[k] >= kPending) slots[k] = got[slots[k] - kPending];
+  }
+  return gv_verify_ed25519_msgs_keyed(app->gpu, m, slots.data(), sig, blob, off, len, ok);
+}
+
 int batch_run(gvh_app* app, GpuBatch& b) {
   if (!app->gpu) return GVH_ENOVERIFIER;
   std::lock_guard<std::mutex> g(app->gpu_mu);
   if (b.m && verify_secp(app, b) != GV_OK) return GVH_EDEVICE;
   const size_t me = b.ed.size();
-  if (me && gv_verify_ed25519_msgs(app->gpu, me, b.epub.data(), b.esig.data(), b.eblob.empty() ? nullptr : b.eblob.data(),
-                                   b.eoff.data(), b.elen.data(), b.eok.data()) != GV_OK)
+  if (me && verify_ed(app, me, b.epub.data(), b.esig.data(), b.eblob.empty() ? nullptr : b.eblob.data(), b.eoff.data(),
+                      b.elen.data(), b.eok.data(), me >= app->key_load_min) != GV_OK)
     return GVH_EDEVICE;
   return GVH_OK;
 }
@@ -2978,8 +3041,9 @@ extern "C" int gvh_verify_commits(gvh_app* app, size_t n, const gvh_commit* comm
   if (m) {
     if (!app->gpu) return GVH_ENOVERIFIER;
     std::lock_guard<std::mutex> g(app->gpu_mu);
-    if (gv_verify_ed25519_msgs(app->gpu, m, pub.data(), sig.data(), blob.empty() ? nullptr : blob.data(), off.data(),
-                               len.data(), ok.data()) != GV_OK)
+    // a validator set signs block after block: its keys are loaded once
+    if (verify_ed(app, m, pub.data(), sig.data(), blob.empty() ? nullptr : blob.data(), off.data(), len.data(),
+                  ok.data(), true) != GV_OK)
       return GVH_EDEVICE;
     app->st_gpu_calls += 1;
     app->st_gpu_leaves += m;

@@ -115,7 +115,11 @@ func VerifyCommits(ev gv.EdVerifier, checks []CommitCheck) []error {
 	}
 	var ok []bool
 	if len(pubs) > 0 {
-		ok = ev.VerifyBatchEd25519(pubs, msgs, sigs)
+		if kc, cached := ev.(gv.EdKeyCache); cached {
+			ok = kc.VerifyBatchEd25519Cached(pubs, msgs, sigs) // validator sets repeat: their keys stay resident
+		} else {
+			ok = ev.VerifyBatchEd25519(pubs, msgs, sigs)
+		}
 	}
 	verdict := func(k CommitCheck, lf leaf, idx int) bool {
 		if lf.item >= 0 {

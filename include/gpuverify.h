@@ -143,6 +143,8 @@ uint64_t gv_keys_generation(const gv_ctx* ctx);
 #define GV_CPU_CROSSOVER 4
 #define GV_KEY_LOAD_MIN 4096
 #define GV_KEY_CAP (1u << 22)
+/* ... and the ed25519 key arena's (gv_ed_keys_load: 72 KB of HBM per key). */
+#define GV_ED_KEY_CAP (1u << 16)
 
 /* Key-arena readback (tests, tools): for each slot, the affine point the
  * arena holds for it, out_xy64 + 64*i = x || y (32 bytes each, big-endian),

@@ -18,7 +18,7 @@ def read(*p):
 def header_macros():
     h = read("include", "gpuverify.h")
     out = {}
-    for name in ("GV_CPU_CROSSOVER", "GV_KEY_LOAD_MIN", "GV_KEY_CAP"):
+    for name in ("GV_CPU_CROSSOVER", "GV_KEY_LOAD_MIN", "GV_KEY_CAP", "GV_ED_KEY_CAP"):
         m = re.search(r"#define %s \(?(\d+)u?(?: << (\d+))?\)?" % name, h)
         assert m, name
         out[name] = int(m.group(1)) << int(m.group(2) or 0)
@@ -31,7 +31,7 @@ def strip_comments(go: str) -> str:
 
 def test_policy_constants_shared_by_go_and_cpp():
     mac = header_macros()
-    assert mac == {"GV_CPU_CROSSOVER": 4, "GV_KEY_LOAD_MIN": 4096, "GV_KEY_CAP": 1 << 22}
+    assert mac == {"GV_CPU_CROSSOVER": 4, "GV_KEY_LOAD_MIN": 4096, "GV_KEY_CAP": 1 << 22, "GV_ED_KEY_CAP": 1 << 16}
     app = gvhost.HostApp(None)
     assert app.keyed_policy() == (True, mac["GV_KEY_LOAD_MIN"], mac["GV_KEY_CAP"])
     app.close()
@@ -39,6 +39,7 @@ def test_policy_constants_shared_by_go_and_cpp():
     assert re.search(r"DefaultCPUBelow\s*=\s*int\(C\.GV_CPU_CROSSOVER\)", go)
     assert re.search(r"DefaultKeyLoadMin\s*=\s*int\(C\.GV_KEY_LOAD_MIN\)", go)
     assert re.search(r"DefaultKeyCap\s*=\s*int\(C\.GV_KEY_CAP\)", go)
+    assert re.search(r"DefaultEdKeyCap\s*=\s*int\(C\.GV_ED_KEY_CAP\)", go)
     opener = go[go.index("func Open("):go.index("func (g *GPU) Close()")]
     for field in ("CPUBelow: DefaultCPUBelow", "Keyed: true", "KeyLoadMin: DefaultKeyLoadMin",
                   "KeyCap: DefaultKeyCap"):
@@ -87,3 +88,26 @@ def test_go_checktx_window_is_adaptive_and_ingress_releases_lock():
     # state stage under the lock, GPU stage after it is released
     assert loop.index("in.stateMu.Lock()") < loop.index("prepareCheckTxs(batch)") < \
         loop.index("in.stateMu.Unlock()") < loop.index("verify()")
+
+
+def test_go_ed25519_routes_like_the_mirror():
+    """ed25519 leaves: the Go shim and the C++ mirror (verify_ed) both go keyed
+    when every key is resident or the batch has KeyLoadMin leaves, and the
+    light-client commit path (Go EdKeyCache, C++ gvh_verify_commits) always
+    loads its validator set's keys; the arena is reset at GV_ED_KEY_CAP."""
+    go = strip_comments(read("go", "crypto", "gpuverify", "gpuverify.go"))
+    vb = go[go.index("func (g *GPU) VerifyBatchEd25519("):go.index("func (g *GPU) VerifyBatchEd25519Cached(")]
+    assert "g.verifyEdKeyed(pubs, msgs, sigs, len(pubs) >= g.KeyLoadMin)" in vb
+    cached = go[go.index("func (g *GPU) VerifyBatchEd25519Cached("):go.index("func (g *GPU) VerifyBatchEd25519Pub(")]
+    assert "g.verifyEdKeyed(pubs, msgs, sigs, true)" in cached
+    ek = go[go.index("func (g *GPU) verifyEdKeyed("):]
+    lock, unlock = ek.index("g.mu.Lock()"), ek.rindex("g.mu.Unlock()")
+    assert lock < ek.index("edSlotsLocked") < ek.index("gv_verify_ed25519_msgs_keyed") < unlock
+    assert "DefaultEdKeyCap" in go[go.index("func (g *GPU) edSlotsLocked("):]
+    ibc = strip_comments(read("go", "x", "ibc", "07-tendermint", "batch_verify.go"))
+    assert "ev.(gv.EdKeyCache)" in ibc and "VerifyBatchEd25519Cached(pubs, msgs, sigs)" in ibc
+    cpp = read("cosmos-sdk-rootchain_amd", "host", "gvhost.cpp")
+    assert "GV_ED_KEY_CAP" in cpp[cpp.index("int verify_ed("):]
+    assert "me >= app->key_load_min" in cpp
+    commits = cpp[cpp.index('extern "C" int gvh_verify_commits('):]
+    assert re.search(r"verify_ed\(app, m,[^;]*true\)", commits)

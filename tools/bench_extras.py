@@ -652,7 +652,9 @@ def ed25519(ver, wl, n: int = 1_000_000, threads: int = 16, steps: int = 3, nkey
                           out.ctypes.data, threads)
     cpu_rate = m / (time.perf_counter() - t)
     cpu_mism = int(np.count_nonzero(out.astype(bool) != exp[:m]))
+    small = ed25519_small_batches(ver, wl, pub, sig, blob, off, lens, exp, threads)
     return {"items": n, "mean_msg_bytes": round(float(lens.mean()), 1), "value": round(n * steps / el, 1),
+            "small_batches": small,
             "unit": "ed25519 verifies/s", "mismatches": int(np.count_nonzero(got != exp)),
             "rejects_expected": int(bad.sum()), "kernel_ms": round(kms, 4), "launches_averaged": cnt,
             "roofline": {"kernel": "k_ed_verify", "work_per_verify": W_ED25519, "achieved_T": round(achieved / 1e12, 3),
@@ -660,3 +662,51 @@ def ed25519(ver, wl, n: int = 1_000_000, threads: int = 16, steps: int = 3, nkey
             "cpu_openssl": {"value": round(cpu_rate, 1), "threads": threads, "sample": m, "mismatches": cpu_mism},
             "workload_gen_s": round(t_gen, 2),
             "note": "device-resident (inputs in HBM); keys = 4,096 RFC 8032 seeds round-robin; OpenSSL Ed25519 signs"}
+
+
+def ed25519_small_batches(ver, wl, pub, sig, blob, off, lens, exp, threads, sizes=(1, 16, 64, 150, 256, 1024)):
+    """Latency of small ed25519 batches (IBC commits: a ~100-150 validator
+    set signs every block; CheckTx multisig ed25519 sub-keys), host buffers,
+    p50 end to end: the cached-key sliced kernel (gv_verify_ed25519_msgs_keyed,
+    the batch's keys loaded once beforehand), the throughput kernels
+    (gv_verify_ed25519_msgs) and OpenSSL on 1 and `threads` host cores."""
+    import ctypes as C
+    top = max(sizes)
+    uk, inv = np.unique(pub[:top], axis=0, return_inverse=True)
+    ver.ed_keys_reset()
+    t = time.perf_counter()
+    kslots = ver.ed_keys_load(uk)
+    t_load = time.perf_counter() - t
+    slots = kslots[inv.reshape(-1)]
+    out, mism = {}, 0
+    for b in sizes:
+        reps = 200 if b <= 256 else 50
+        bo = off[:b] - off[0]
+        bb = blob[int(off[0]):int(off[b - 1] + lens[b - 1])]
+        msgs = (bb, bo, lens[:b])
+        tk, tu, tc1, tcn = [], [], [], []
+        for r in range(reps + 5):
+            t = time.perf_counter()
+            gk = ver.verify_batch_ed25519_keyed(slots[:b], sig[:b], msgs)
+            t1 = time.perf_counter()
+            gu = ver.verify_batch_ed25519(pub[:b], sig[:b], msgs)
+            t2 = time.perf_counter()
+            if r >= 5:
+                tk.append(t1 - t)
+                tu.append(t2 - t1)
+        mism += int(np.count_nonzero(gk.astype(bool) != exp[:b])) + int(np.count_nonzero(gu.astype(bool) != exp[:b]))
+        o = np.zeros(b, np.uint8)
+        for r in range(7 if b <= 256 else 3):
+            for th, acc in ((1, tc1), (threads, tcn)):
+                t = time.perf_counter()
+                wl.gvw_ed25519_verify(b, pub.ctypes.data, sig.ctypes.data, blob.ctypes.data, off.ctypes.data,
+                                      lens.ctypes.data, o.ctypes.data, th)
+                acc.append(time.perf_counter() - t)
+        p50 = lambda a: round(float(np.median(a)) * 1e3, 4)  # noqa: E731
+        out[str(b)] = {"keyed_sliced_p50_ms": p50(tk), "keyed_sliced_p99_ms": round(float(np.percentile(tk, 99)) * 1e3, 4),
+                       "throughput_p50_ms": p50(tu), "cpu_openssl_serial_p50_ms": p50(tc1),
+                       "cpu_openssl_allcore_p50_ms": p50(tcn)}
+    return {"batches": out, "mismatches": mism, "keys_loaded": int(len(uk)), "key_load_ms": round(t_load * 1e3, 2),
+            "note": "host buffers (~350 B messages), end to end; keyed = gv_verify_ed25519_msgs_keyed after one "
+                    "gv_ed_keys_load of the batch's keys (k_ed_lat_sl up to ed_lat_max = 2048), throughput = "
+                    "gv_verify_ed25519_msgs (k_ed_prep + k_ed_ladder)"}
