@@ -72,19 +72,14 @@ __global__ __launch_bounds__(64) void k_ed_keys(const uint8_t* pub32, uint32_t n
   }
 }
 
-#define EDL_MSG_LDS 2048
-
-// Message bytes for sha512_pre64: the staged prefix from LDS (an LDS
-// pointer, not a generic one), the rest from global memory.
-typedef __attribute__((address_space(3))) const uint8_t lds_u8;
-struct LdsMsg {
-  lds_u8* s;
-  const uint8_t* g;
-  GV_DEV u32 operator()(u32 i) const { return i < EDL_MSG_LDS ? (u32)s[i] : (u32)g[i]; }
-};
+#define EDL_MSG_LDS 2048                    // padded SHA-512 inputs up to 16 blocks take the LDS path
 
 struct EdlShared {
-  uint8_t msg[EDL_MSG_LDS];                 // the message's first bytes (wave 0)
+  union {                                   // the padded SHA-512 input (wave 0): R || A || M || padding
+    u32 pre[16];
+    uint8_t msg[EDL_MSG_LDS];
+    uint64_t words[EDL_MSG_LDS / 8];
+  };
   int hd[64];                               // signed radix-16 digits of h
   u32 xr[16], yr[16];                       // the decoded R, sliced
   u32 flags;                                // bit 0: R decodes, bit 1: S checks
@@ -118,19 +113,49 @@ __global__ __launch_bounds__(256) void k_ed_lat_sl(const gvk_edl b) {
     // load per lane per 64 bytes instead of a serial byte stream)
     const uint8_t* m = b.msg_blob ? b.msg_blob + b.msg_off[gi] : nullptr;
     const u32 len = b.msg_len[gi];
-    const u32 staged = len < EDL_MSG_LDS ? len : EDL_MSG_LDS;
-    for (u32 i = lane; i < staged; i += 64u) sh.msg[i] = m[i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    u32 pre[16];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      pre[i] = sw[i];
-      pre[8 + i] = b.kpub[(size_t)sl * 8 + i];
-    }
+    const u32 total = 64u + len, nblocks = (total + 17u + 127u) >> 7, padded = nblocks << 7;
     u32 dig[16], h[8];
-    sha512_pre64(dig, pre, LdsMsg{(const lds_u8*)sh.msg, m}, len);
+    if (padded <= EDL_MSG_LDS) {
+      // the whole SHA-512 input -- R || A || M, 0x80, zeros, the 128-bit
+      // big-endian bit length -- laid out in LDS by the wave (one load per
+      // lane per 64 message bytes); the compression then reads each block's
+      // sixteen 64-bit words with uniform addresses and runs on the scalar unit
+      if (lane < 8u) sh.pre[lane] = sw[lane];
+      else if (lane < 16u) sh.pre[lane] = b.kpub[(size_t)sl * 8 + (lane - 8u)];
+      const uint64_t bits = (uint64_t)total * 8u;
+      for (u32 i = 64u + lane; i < padded; i += 64u) {
+        u32 byte = 0;
+        if (i < total) byte = m[i - 64u];
+        else if (i == total) byte = 0x80u;
+        else if (i >= padded - 8u) byte = (u32)(bits >> (8u * (padded - 1u - i))) & 0xFFu;
+        sh.msg[i] = (uint8_t)byte;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      uint64_t hs[8] = {0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull, 0x3c6ef372fe94f82bull, 0xa54ff53a5f1d36f1ull,
+                        0x510e527fade682d1ull, 0x9b05688c2b3e6c1full, 0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull};
+#pragma unroll 1
+      for (u32 blk = 0; blk < nblocks; ++blk) {
+        uint64_t w[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = __builtin_bswap64(sh.words[blk * 16u + (u32)j]);
+        sha512_compress(hs, w);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        dig[2 * i] = __builtin_bswap32((u32)(hs[i] >> 32));
+        dig[2 * i + 1] = __builtin_bswap32((u32)hs[i]);
+      }
+    } else {                                            // long messages: byte stream from memory
+      u32 pre[16];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        pre[i] = sw[i];
+        pre[8 + i] = b.kpub[(size_t)sl * 8 + i];
+      }
+      sha512_pre64(dig, pre, [=](u32 i) { return (u32)m[i]; }, len);
+    }
     sc_reduce512(h, dig);
     const uint64_t car = sc_radix16_carries(h);
     const u32 nib = (h[lane >> 3] >> (4u * (lane & 7u))) & 15u;

@@ -509,7 +509,8 @@ struct gv_ctx {
   // lat_sl_max sets these too; lat_max_keyed / lat_sl_max_keyed only these.
   size_t lat_max_keyed = 14336;
   size_t lat_sl_max_keyed = 1536;
-  size_t pipe_chunk = 131072;   // host path: first chunk of the two-set copy/compute pipeline (0 = max_batch)
+  size_t pipe_chunk = 262144;   // host path: first chunk of the two-set copy/compute pipeline (0 = max_batch;
+                                // profiles/r03/hostpath_sweep.jsonl: 262144 x 4 steadiest on pageable input)
   int pipe_growth = 4;          // host path: each later chunk at most this times the one before
   int stage_threads = 8;        // host path: staging threads of the context's shared pool (gv_open: half
                                 // the process's CPUs -- affinity capped by the cgroup quota -- at most 8)

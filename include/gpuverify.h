@@ -224,7 +224,7 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * are read by the kernel straight from the pinned staging buffer and answered
  * as verdict bytes in pinned memory -- no H2D, memset or D2H; default 1),
  * "pipe_chunk" (host-buffer calls past lat_max: first chunk of the two-stream
- * copy/compute pipeline per device, default 131072; 0 = one chunk per
+ * copy/compute pipeline per device, default 262144; 0 = one chunk per
  * max_batch), "pipe_growth" (each later chunk at most this many times the one
  * before, default 4: the staging of chunk i+1 hides under the kernels of
  * chunk i), "stage_threads" (pageable -> pinned staging copy threads of
