@@ -2341,18 +2341,6 @@ void pre_front(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t
     }
     if (m->tx) {
       const Tx& tx = *m->tx;
-      m->tx_pk.resize(tx.sigs.size());
-      for (size_t i = 0; i < tx.sigs.size(); ++i) {
-        if (!tx.sigs[i].pub.n) continue;
-        try {
-          m->tx_pk[i] = app->pubs.get(tx.sigs[i].pub.p, tx.sigs[i].pub.n);
-        } catch (const Panic& e) {
-          m->pk_panic = (int)i;
-          m->pk_panic_msg = e.what();
-          break;
-        }
-      }
-      m->plans.resize(tx.sigs.size());
       m->sacc.resize(tx.signers.size());
       uint64_t mask = 0;
       for (size_t i = 0; i < tx.signers.size(); ++i) {
@@ -2360,6 +2348,26 @@ void pre_front(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t
         if (m->sacc[i]) mask |= uint64_t(1) << part_of(m->sacc[i]);
       }
       part_mask[t] = mask;
+      m->tx_pk.resize(tx.sigs.size());
+      for (size_t i = 0; i < tx.sigs.size(); ++i) {
+        const Span pb = tx.sigs[i].pub;
+        if (!pb.n) continue;
+        // the signer's account already holds these exact (canonical) bytes:
+        // its decoded key is the one GetPubKeys would decode (no table lookup)
+        const Account* a = i < m->sacc.size() ? m->sacc[i] : nullptr;
+        if (a && a->info && a->pub.size() == pb.n && !memcmp(a->pub.data(), pb.p, pb.n)) {
+          m->tx_pk[i] = a->info;
+          continue;
+        }
+        try {
+          m->tx_pk[i] = app->pubs.get(pb.p, pb.n);
+        } catch (const Panic& e) {
+          m->pk_panic = (int)i;
+          m->pk_panic_msg = e.what();
+          break;
+        }
+      }
+      m->plans.resize(tx.sigs.size());
     }
     memos[t] = std::move(m);
   });
