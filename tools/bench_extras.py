@@ -364,28 +364,35 @@ def c1_ante(ver, ntx: int = 10000, per_tx_sample: int = 500, checktx_threads: in
               "ante_loop_ms_per_block": round((st2["deliver_loop_ns"] - st["deliver_loop_ns"]) / 1e6 / len(later_blobs), 2),
               "note": "one block at a time (gvh_deliver_block_codes): PreVerifyTxs, GPU batch, DeliverTx loop"}
     # the same steady blocks as one pipelined replay (gvh_deliver_blocks: block
-    # b+1 pre-verified and its GPU batch run while block b delivers)
-    app = fresh_app()
-    rc, _ = app.deliver_block_blob(*first_blob)
-    assert rc == 0
+    # b+1 pre-verified and its GPU batch run while block b delivers); the
+    # shared GPU box's host cores are noisy (+-25 % run to run), so the replay
+    # is repeated on fresh apps and the median reported
     cat = np.concatenate([b[0] for b in later_blobs])
     base = np.cumsum([0] + [len(b[0]) for b in later_blobs[:-1]]).astype(np.uint64)
     offs = np.concatenate([b[1] + base[k] for k, b in enumerate(later_blobs)])
     lens_ = np.concatenate([b[2] for b in later_blobs])
-    st = app.stats()
-    t = time.perf_counter()
-    rc, cp = app.deliver_blocks_blob(cat, offs, lens_, [len(b[1]) for b in later_blobs])
-    t_pipe = time.perf_counter() - t
-    st2 = app.stats()
-    app.close()
-    assert rc == 0
+    runs = []
+    for _ in range(5):
+        app = fresh_app()
+        rc, _ = app.deliver_block_blob(*first_blob)
+        assert rc == 0
+        st = app.stats()
+        t = time.perf_counter()
+        rc, cp = app.deliver_blocks_blob(cat, offs, lens_, [len(b[1]) for b in later_blobs])
+        t_pipe = time.perf_counter() - t
+        st2 = app.stats()
+        app.close()
+        assert rc == 0 and int((cp == 0).sum()) == ntx * len(later_blobs)
+        runs.append((t_pipe, st2["gpu_ns"] - st["gpu_ns"], st2["memo_hits"] - st["memo_hits"]))
+    runs.sort()
+    t_pipe, gns, hits = runs[len(runs) // 2]
     piped = {"blocks": len(later_blobs), "txs_per_s": round(ntx * len(later_blobs) / t_pipe, 1),
-             "ms_per_block": round(t_pipe / len(later_blobs) * 1e3, 2), "accepted": int((cp == 0).sum()),
-             "gpu_ms_per_block": round((st2["gpu_ns"] - st["gpu_ns"]) / 1e6 / len(later_blobs), 2),
-             "memo_hits": st2["memo_hits"] - st["memo_hits"],
-             "note": "the same steady blocks as ONE gvh_deliver_blocks call (block sync / replay): block b+1's "
-                     "PreVerifyTxs (prediction carrying block b's increments) before block b's DeliverTx loop, "
-                     "its GPU batch on a helper thread under that loop"}
+             "ms_per_block": round(t_pipe / len(later_blobs) * 1e3, 2), "accepted": ntx * len(later_blobs),
+             "gpu_ms_per_block": round(gns / 1e6 / len(later_blobs), 2), "memo_hits": hits,
+             "runs_txs_per_s": [round(ntx * len(later_blobs) / r[0], 1) for r in runs],
+             "note": "median of 5 replays on fresh apps: the same steady blocks as ONE gvh_deliver_blocks call "
+                     "(block sync / replay): block b+1's PreVerifyTxs (prediction carrying block b's increments) "
+                     "before block b's DeliverTx loop, its GPU batch on a helper thread under that loop"}
     # per-tx path (CheckTx without batching): one GPU call per tx
     app = fresh_app()
     m = min(per_tx_sample, ntx)
@@ -559,19 +566,26 @@ def c4_multisig(ver, wl, block: int = 10000, threads: int = 16, n_accounts: int 
            "ante_loop_s": round(st["deliver_loop_ns"] / 1e9, 3), "gpu_calls": st["gpu_calls"],
            "memo_hits": st["memo_hits"],
            "note": "one block at a time (gvh_deliver_block_codes per block)"}
-    # the replay as it is run: one pipelined gvh_deliver_blocks call over every block
-    app = gvhost.HostApp(ver, chain_id="gv-bench", height=1)
-    app.set_threads(threads)
-    for addr, num in accts:
-        app.set_account(addr, num, 0)
+    # the replay as it is run: one pipelined gvh_deliver_blocks call over every
+    # block, three times on fresh apps (the median: the shared box's host cores
+    # vary +-25 % run to run)
     nb = (ntx + block - 1) // block
-    t = time.perf_counter()
-    rc, codes = app.deliver_blocks_blob(blob, offs, lens, [min(block, ntx - b * block) for b in range(nb)])
-    el = time.perf_counter() - t
-    st = app.stats()
-    app.close()
-    assert rc == 0
-    bad_p = int(np.count_nonzero(codes))
+    runs = []
+    for _ in range(3):
+        app = gvhost.HostApp(ver, chain_id="gv-bench", height=1)
+        app.set_threads(threads)
+        for addr, num in accts:
+            app.set_account(addr, num, 0)
+        t = time.perf_counter()
+        rc, codes = app.deliver_blocks_blob(blob, offs, lens, [min(block, ntx - b * block) for b in range(nb)])
+        el_r = time.perf_counter() - t
+        st_r = app.stats()
+        app.close()
+        assert rc == 0
+        bad_p = int(np.count_nonzero(codes))
+        runs.append((el_r, st_r, bad_p))
+    runs.sort(key=lambda r: r[0])
+    el, st, bad_p = runs[1]
     return {"txs": ntx, "leaves": leaves, "block_txs": block, "blocks": nb,
             "rejected": bad_p, "mismatches": bad_p, "leaves_per_s": round(leaves / el, 1),
             "txs_per_s": round(ntx / el, 1), "seconds": round(el, 3), "preverify_front_s": round(st["preverify_ns"] / 1e9, 3),
@@ -579,9 +593,10 @@ def c4_multisig(ver, wl, block: int = 10000, threads: int = 16, n_accounts: int 
             "gpu_calls": st["gpu_calls"], "gpu_leaves": st["gpu_leaves"], "memo_hits": st["memo_hits"],
             "one_block_at_a_time": one,
             "workload_gen_s": round(t_gen, 1), "host_threads": threads,
+            "runs_leaves_per_s": [round(leaves / r[0], 1) for r in runs],
             "note": "2-of-3 / 3-of-5 / 4-of-7 threshold accounts (30k), first k bits set, every tx valid by "
                     "construction; amino StdTx bytes through the host mirror, host buffers; leaves_per_s = the "
-                    "pipelined replay (gvh_deliver_blocks over all blocks: block b+1's PreVerifyTxs and GPU batch "
+                    "median of three pipelined replays (gvh_deliver_blocks over all blocks: block b+1's PreVerifyTxs and GPU batch "
                     "under block b's DeliverTx loop); one_block_at_a_time = the same blocks through "
                     "gvh_deliver_block_codes one by one"}
 
