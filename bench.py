@@ -310,8 +310,8 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
     injection points for tests/test_bench_dist.py (gloo, CPU, fake verifier)."""
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--items", "--n", dest="n", type=int, default=1_000_000, help="signatures per rank")
     ap.add_argument("--adversarial", type=float, default=0.0, help="C3: fraction of invalid signatures")
     ap.add_argument("--keys", type=int, default=65536)

@@ -169,7 +169,7 @@ hipError_t gvk_dedupe(uint32_t n, uint32_t C, const uint32_t* x, const uint32_t*
 // rows in_x / in_pfx (stride C), slots 0..n-1; qr: (GV_QTAB_N - 1) * 9 ratio
 // rows of stride round_up(4 n, 256).
 hipError_t gvk_keys_build_rows(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx, uint32_t* qr,
-                               uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2,
+                               uint32_t* qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2,
                                uint32_t* kzq2, hipStream_t st);
 // Parse n keys (device pub33) into arena slots base..base+n-1.  Scratch: the
 // batch rows in_x, in_pfx (and r, s, e as k_unpack targets) of stride C and

@@ -716,14 +716,40 @@ __global__ __launch_bounds__(256) void k_keys_chain(u32 n, u32 C, const u32* in_
 // E's: all four tables end on the common Z = E_0 E_1 E_2 E_3, so ONE
 // accumulator can take entries of every group (k_ecmult_k4) -- no inversion
 // and no extra pass over the tables.  Same co-Z steps as build_q_table.
-// qr: Z-ratio scratch rows of stride C4 >= 4 n.
+// qr: Z-ratio scratch rows of stride C4 >= 4 n.  qe (may be null): rows of
+// stride C4 for the forward pass's entries -- written and read back
+// coalesced, so each table entry is written once, by the back-propagation
+// (null: the entries go through the table itself: lanes 1,280 B apart write
+// 80 B each, twice, and read them back in between).
 __global__ __launch_bounds__(256) void k_keys_tables(u32 n, u32 C4, u32 base, u32* kqt, u32* kzq, u32 kC, u32* kqt2,
-                                                      u32* kzq2, u32* qr) {
+                                                      u32* kzq2, u32* qr, u32* qe) {
   const u32 L = blockIdx.x * blockDim.x + threadIdx.x;
   const u32 key = L >> 2, grp = L & 3u;
   if (key >= n) return;                     // whole quads only: shuffles stay inside live quads
   u32* tab = grp == 0u ? kqt : kqt2;
   const u32 row = grp == 0u ? base + key : (base + key) * GV_KEY2_TABLES + (grp - 1u);
+  auto put = [&](int e, const fe29& x, const fe29& y) {
+    if (qe) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        qe[((size_t)e * 18 + i) * C4 + L] = x.n[i];
+        qe[((size_t)e * 18 + 9 + i) * C4 + L] = y.n[i];
+      }
+    } else {
+      store_qent29(tab, row, e, x, y);
+    }
+  };
+  auto get = [&](int e, fe29& x, fe29& y) {
+    if (qe) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        x.n[i] = qe[((size_t)e * 18 + i) * C4 + L];
+        y.n[i] = qe[((size_t)e * 18 + 9 + i) * C4 + L];
+      }
+    } else {
+      load_qent29(x, y, tab, row, (u32)e);
+    }
+  };
   u32* zrow = grp == 0u ? kzq : kzq2 + (size_t)(grp - 1u) * 8 * kC;
   fe29 qx, qy, X1, Y1, X2, Y2, t, u, prod;
   {
@@ -757,8 +783,8 @@ __global__ __launch_bounds__(256) void k_keys_tables(u32 n, u32 C4, u32 base, u3
     f29_mul(t, M, t);
     f29_sub_norm<1>(Y2, t, Y1);
   }
-  store_qent29(tab, row, 0, X1, Y1);        // 1*Q on Z1
-  store_qent29(tab, row, 1, X2, Y2);        // 2*Q on Z1
+  put(0, X1, Y1);                           // 1*Q on Z1
+  put(1, X2, Y2);                           // 2*Q on Z1
   f29_add(prod, qy, qy);                    // Z1 = 2y; times every ratio below -> Z_15
 #pragma unroll 1
   for (int m = 2; m < GV_QTAB_N; ++m) {     // (Q', mQ) -> ((m+1)Q, Q'')
@@ -780,7 +806,7 @@ __global__ __launch_bounds__(256) void k_keys_tables(u32 n, u32 C4, u32 base, u3
     f29_sub_norm<1>(Y2, t, a1);
     X1 = w1;
     Y1 = a1;
-    if (m + 1 < GV_QTAB_N) store_qent29(tab, row, m, X2, Y2);   // the last entry waits for rho
+    if (m + 1 < GV_QTAB_N) put(m, X2, Y2);  // the last entry waits for rho
   }
   // E = Z_15 (times the parked Jacobian Z for groups 1..3); the quad's others
   if (grp) {
@@ -819,7 +845,7 @@ __global__ __launch_bounds__(256) void k_keys_tables(u32 n, u32 C4, u32 base, u3
     fe29 x, y, a2, a3;
     f29_sqr(a2, acc);
     f29_mul(a3, a2, acc);
-    load_qent29(x, y, tab, row, m - 1);
+    get(m - 1, x, y);
     f29_mul(x, x, a2);
     f29_mul(y, y, a3);
     store_qent29(tab, row, m - 1, x, y);
@@ -1373,13 +1399,14 @@ hipError_t gvk_gen_glat(uint32_t* glat, hipStream_t st) {
 // The two key-table launches over n keys whose rows in_x / in_pfx (stride C)
 // are unpacked; qr: 14 x 9 ratio rows of stride round_up(4 n, 256).
 static hipError_t keys_tables_launch(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx,
-                                     uint32_t* qr, uint32_t base, uint32_t* kqt, uint32_t* kzq, uint32_t kC,
+                                     uint32_t* qr, uint32_t* qe, uint32_t base, uint32_t* kqt, uint32_t* kzq, uint32_t kC,
                                      uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const uint32_t C4 = (4u * n + 255u) / 256u * 256u;
   hipLaunchKernelGGL(gv::k_keys_chain, dim3((n + 255) / 256), dim3(256), 0, st, n, C, in_x, in_pfx, base, kqt, kC,
                      kok, kqt2, kzq2);
-  hipLaunchKernelGGL(gv::k_keys_tables, dim3(C4 / 256), dim3(256), 0, st, n, C4, base, kqt, kzq, kC, kqt2, kzq2, qr);
+  hipLaunchKernelGGL(gv::k_keys_tables, dim3(C4 / 256), dim3(256), 0, st, n, C4, base, kqt, kzq, kC, kqt2, kzq2, qr,
+                     qe);
   return hipGetLastError();
 }
 
@@ -1390,7 +1417,7 @@ hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t
   const dim3 blk(256), grd(C / 256);
   hipLaunchKernelGGL(gv::k_unpack, grd, blk, 0, st, pub33, (const uint8_t*)nullptr, (const uint8_t*)nullptr, n, C,
                      in_x, in_pfx, in_r, in_s, in_e);
-  return keys_tables_launch(n, C, in_x, in_pfx, qr, base, kqt, kzq, kC, kok, kqt2, kzq2, st);
+  return keys_tables_launch(n, C, in_x, in_pfx, qr, nullptr, base, kqt, kzq, kC, kok, kqt2, kzq2, st);
 }
 
 hipError_t gvk_keys_point(uint32_t n, const uint32_t* slots, const uint32_t* kqt, const uint32_t* kzq, uint32_t kC,
@@ -1427,9 +1454,9 @@ hipError_t gvk_dedupe(uint32_t n, uint32_t C, const uint32_t* x, const uint32_t*
 }
 
 hipError_t gvk_keys_build_rows(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx, uint32_t* qr,
-                               uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2,
+                               uint32_t* qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2,
                                uint32_t* kzq2, hipStream_t st) {
-  return keys_tables_launch(n, C, in_x, in_pfx, qr, 0u, kqt, kzq, kC, kok, kqt2, kzq2, st);
+  return keys_tables_launch(n, C, in_x, in_pfx, qr, qe, 0u, kqt, kzq, kC, kok, kqt2, kzq2, st);
 }
 
 #if GV_STAMP

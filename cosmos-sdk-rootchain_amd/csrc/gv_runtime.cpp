@@ -523,6 +523,7 @@ struct gv_ctx {
   bool keyed_k4 = true;         // keyed batches on k_ecmult_k4 (GV_KEYED_K4=0: the 125-doubling ladder, A/B)
   bool pipeline_dev = true;     // pipelined device-resident calls on the context stream (dev_run; GV_PIPELINE=0: A/B)
   bool group_keys = true;       // pub33 throughput batches parse each distinct key once (group_keys; GV_GROUP_KEYS=0: A/B)
+  bool keys_scratch = true;     // key tables: forward entries through coalesced scratch rows (GV_KEYS_SCRATCH=0: A/B)
   size_t group_min = 16384;     // ... batches of at least this many items
   int group_div = 5;            // ... taking the keyed pipeline when distinct keys <= items / group_div (break-even ~4:
                                 // a key build ~18 ns vs ~4 ns saved per item, profiles/r03/group_ab)
@@ -609,7 +610,12 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   // does not read keys) runs on st: both are one wave per SIMD or so
   CK(hipEventRecord(s->fork, st));
   CK(hipStreamWaitEvent(s->side, s->fork, 0));
-  CK(gvk_keys_build_rows((uint32_t)U, (uint32_t)capU, kx, kpfx, qr, s->g_kqt, s->g_kzq, (uint32_t)capU,
+  // the forward pass's entries in coalesced scratch rows after the ratio rows, when they fit
+  const size_t C4 = round_up(4 * U, 256);
+  uint32_t* qe = qr + (size_t)(GV_QTAB_N - 1) * 9 * C4;
+  if (!ctx->keys_scratch || (size_t)(qe + (size_t)(GV_QTAB_N - 1) * 18 * C4 - q) > (size_t)GV_QTAB_WORDS * C)
+    qe = nullptr;
+  CK(gvk_keys_build_rows((uint32_t)U, (uint32_t)capU, kx, kpfx, qr, qe, s->g_kqt, s->g_kzq, (uint32_t)capU,
                          s->g_kok, s->g_kqt2, s->g_kzq2, s->side));
   CK(hipEventRecord(s->keys_done, s->side));
   b.keys_ready = s->keys_done;
@@ -1258,6 +1264,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   gv_ctx* ctx = new gv_ctx();
   parse_size_env("GV_MAX_BATCH", &ctx->max_batch);
   if (const char* k4 = getenv("GV_KEYED_K4")) ctx->keyed_k4 = strcmp(k4, "0") != 0;
+  if (const char* ks = getenv("GV_KEYS_SCRATCH")) ctx->keys_scratch = strcmp(ks, "0") != 0;
   if (const char* ls = getenv("GV_LAT_SLICED")) ctx->lat_sliced = strcmp(ls, "0") != 0;
   if (const char* zc = getenv("GV_LAT_ZC")) ctx->lat_zero_copy = strcmp(zc, "0") != 0;
   if (const char* pl = getenv("GV_PIPELINE")) ctx->pipeline_dev = strcmp(pl, "0") != 0;
