@@ -175,7 +175,7 @@ hipError_t gvk_keys_build_rows(uint32_t n, uint32_t C, const uint32_t* in_x, con
 // batch rows in_x, in_pfx (and r, s, e as k_unpack targets) of stride C and
 // qr (GV_QTAB_N - 1) * 9 rows of stride round_up(4 n, 256).
 hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
-                          uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t base,
+                          uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t* qe, uint32_t base,
                           uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2,
                           hipStream_t st);
 hipError_t gvk_keys_point(uint32_t n, const uint32_t* slots, const uint32_t* kqt, const uint32_t* kzq, uint32_t kC,

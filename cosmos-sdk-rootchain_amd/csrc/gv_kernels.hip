@@ -1411,13 +1411,13 @@ static hipError_t keys_tables_launch(uint32_t n, uint32_t C, const uint32_t* in_
 }
 
 hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
-                          uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t base,
+                          uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t* qe, uint32_t base,
                           uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2,
                           hipStream_t st) {
   const dim3 blk(256), grd(C / 256);
   hipLaunchKernelGGL(gv::k_unpack, grd, blk, 0, st, pub33, (const uint8_t*)nullptr, (const uint8_t*)nullptr, n, C,
                      in_x, in_pfx, in_r, in_s, in_e);
-  return keys_tables_launch(n, C, in_x, in_pfx, qr, nullptr, base, kqt, kzq, kC, kok, kqt2, kzq2, st);
+  return keys_tables_launch(n, C, in_x, in_pfx, qr, qe, base, kqt, kzq, kC, kok, kqt2, kzq2, st);
 }
 
 hipError_t gvk_keys_point(uint32_t n, const uint32_t* slots, const uint32_t* kqt, const uint32_t* kzq, uint32_t kC,

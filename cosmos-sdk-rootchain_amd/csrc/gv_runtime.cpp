@@ -1472,8 +1472,12 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
       if ((rc = ensure_cap(s, Cs))) return rc;
       if ((rc = set_acquire(s, st))) return rc;
       CK(hipMemcpyAsync(s->d_in, pub33 + c0 * 33, cn * 33, hipMemcpyHostToDevice, st));
+      // the forward-pass entries in coalesced scratch rows after the ratio rows when they fit
+      const size_t C4 = round_up(4 * cn, 256);
+      uint32_t* qe = s->qtab + (size_t)(GV_QTAB_N - 1) * 9 * C4;
+      if (!ctx->keys_scratch || (size_t)(GV_QTAB_N - 1) * 27 * C4 > (size_t)GV_QTAB_WORDS * s->cap) qe = nullptr;
       CK(gvk_keys_build(s->d_in, (uint32_t)cn, (uint32_t)C, s->in_x, s->in_pfx, s->in_r, s->in_s, s->in_e,
-                        s->qtab, (uint32_t)(base + c0), d->kqt, d->kzq,
+                        s->qtab, qe, (uint32_t)(base + c0), d->kqt, d->kzq,
                         (uint32_t)d->kcap, d->kok, d->kqt2, d->kzq2, st));
       if ((rc = set_release(s, st))) return rc;
       CK(hipStreamSynchronize(st));            // the caller's pub33 chunk is read by then
