@@ -25,6 +25,16 @@ static_assert(GV_GW * GV_GWIN >= 130 && GV_GW * (GV_GWIN - 1) <= GV_QW * (GV_QWI
 extern "C" {
 #endif
 
+// Key-ordered lanes scratch (gv_sort.hip), all device memory.
+typedef struct gvk_sort {
+  uint32_t *cnt, *off;          // kcount + 1 bucket counts / exclusive offsets
+  uint32_t *pos, *perm;         // item -> lane, lane -> item (C words each)
+  uint32_t* kslot;              // slot per lane (C words)
+  uint64_t* bits;               // slot-ordered accept bits (C / 64 words)
+  void* temp;                   // scan scratch (gvk_sort_temp_bytes)
+  size_t temp_bytes;
+} gvk_sort;
+
 // One device batch of C lanes (C % 256 == 0, n <= C live items).  All pointers
 // are device pointers.  Either dig32 (digest path) or msg_* (message path).
 typedef struct gvk_batch {
@@ -58,7 +68,17 @@ typedef struct gvk_batch {
   // keyed batches with gtab4 set take k_ecmult_k4 (30-doubling 4-group ladder)
   const uint32_t* kqt2;         // arena group tables (2^35 Q, 2^70 Q, 2^100 Q), on the slot's kzq
   const uint32_t* gtab4;        // GV_KEY2_TABLES x (G-type, lambda) tables of 2^35 G, 2^70 G, 2^100 G
+  // key-ordered lanes (gv_sort.hip; keyed k4 batches with srt.perm set): the
+  // lanes run in slot order, the bits are gathered back to item order
+  gvk_sort srt;
 } gvk_batch;
+// scan scratch bytes for nbuckets = kcount + 1 buckets
+size_t gvk_sort_temp_bytes(uint32_t nbuckets);
+// counting sort of n items by slot (clamped to kcount): pos / perm / kslot of so
+hipError_t gvk_sort_slots(const gvk_sort* so, uint32_t n, const uint32_t* kslot, uint32_t kcount, hipStream_t st);
+hipError_t gvk_unpack_perm(const uint8_t* sig64, const uint8_t* dig32, const uint32_t* perm, uint32_t n, uint32_t C,
+                           uint32_t* r, uint32_t* s, uint32_t* e, hipStream_t st);
+hipError_t gvk_unsort_bits(uint32_t n, const uint32_t* pos, const uint64_t* sbits, uint64_t* bits, hipStream_t st);
 
 // Key arena row of one slot: Q table entries only (the Z-ratio scratch of the
 // build lives in the batch scratch).

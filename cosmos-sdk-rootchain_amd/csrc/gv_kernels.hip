@@ -242,13 +242,15 @@ __global__ __launch_bounds__(256) void k_dedupe_map(u32 n, const u32* rep, const
 }
 
 // ------------------------------------------------------------------ k_sha256
+// perm (nullable): lane g hashes item perm[g] (key-ordered lanes, gv_sort.hip)
 __global__ __launch_bounds__(256) void k_sha256(const uint8_t* blob, const uint64_t* off,
-                                                 const u32* len, u32 n, u32 C, u32* e) {
+                                                 const u32* len, u32 n, u32 C, u32* e, const u32* perm) {
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= C) return;
   u32 h[8];
   if (g < n) {
-    sha256_msg(h, blob + off[g], len[g]);
+    const u32 i = perm ? perm[g] : g;
+    sha256_msg(h, blob + off[i], len[i]);
   } else {
 #pragma unroll
     for (int i = 0; i < 8; ++i) h[i] = 0;
@@ -1344,12 +1346,21 @@ hipError_t gvk_gen_gtable4(uint32_t* gtab4, uint32_t* base_scratch, hipStream_t 
 hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   const uint32_t C = b->C;
   const dim3 blk(256), grd(C / 256);
-  if (!b->unpacked)
-    hipLaunchKernelGGL(gv::k_unpack, grd, blk, 0, st, b->pub33, b->sig64, b->dig32, b->n, C,
-                       b->in_x, b->in_pfx, b->in_r, b->in_s, b->in_e);
+  // key-ordered lanes (gv_sort.hip): keyed k4 batches with sort scratch
+  const bool sorted = b->kslot && b->gtab4 && b->srt.perm;
+  const uint32_t* perm = sorted ? b->srt.perm : nullptr;
+  if (sorted) {
+    hipError_t e = gvk_sort_slots(&b->srt, b->n, b->kslot, b->kcount, st);
+    if (e != hipSuccess) return e;
+    e = gvk_unpack_perm(b->sig64, b->dig32, perm, b->n, C, b->in_r, b->in_s, b->in_e, st);
+    if (e != hipSuccess) return e;
+  } else if (b->unpacked != 1) {                 // 2: the key rows only (in-batch grouping)
+    hipLaunchKernelGGL(gv::k_unpack, grd, blk, 0, st, b->unpacked ? (const uint8_t*)nullptr : b->pub33, b->sig64,
+                       b->dig32, b->n, C, b->in_x, b->in_pfx, b->in_r, b->in_s, b->in_e);
+  }
   if (b->msg_blob)
     hipLaunchKernelGGL(gv::k_sha256, grd, blk, 0, st, b->msg_blob, b->msg_off, b->msg_len, b->n, C,
-                       b->in_e);
+                       b->in_e, perm);
   if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
   {
     const uint32_t waves = (C / 64 + GV_INV_M - 1) / GV_INV_M;
@@ -1363,7 +1374,8 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
     if (b->kslot)   // keyed: in_pfx doubles as the clamped-slot row for k_ecmult
       hipLaunchKernelGGL(gv::k_prep<true>, grd, blk, 0, st, C, b->n, (const uint32_t*)nullptr,
                          (const uint32_t*)nullptr, b->in_r, b->in_s, b->in_e, (const uint32_t*)w, b->digits,
-                         (uint32_t*)nullptr, (uint32_t*)nullptr, b->flags, b->kslot, b->kok, b->kcount, b->in_pfx);
+                         (uint32_t*)nullptr, (uint32_t*)nullptr, b->flags, sorted ? b->srt.kslot : b->kslot,
+                         b->kok, b->kcount, b->in_pfx);
     else
       hipLaunchKernelGGL(gv::k_prep<false>, grd, blk, 0, st, C, b->n, b->in_x, b->in_pfx, b->in_r, b->in_s,
                          b->in_e, (const uint32_t*)w, b->digits, b->qtab, b->zq, b->flags,
@@ -1379,7 +1391,8 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   if (b->ev_ecm_start) (void)hipEventRecord(b->ev_ecm_start, se);
   if (b->kslot && b->gtab4)
     hipLaunchKernelGGL(gv::k_ecmult_k4, grd, blk, 0, se, b->gtab, b->gtab4, b->n, C, b->digits, b->kqt, b->kqt2,
-                       b->kzq, b->flags, b->in_r, b->bits, (const uint32_t*)b->in_pfx, b->kC);
+                       b->kzq, b->flags, b->in_r, sorted ? b->srt.bits : b->bits, (const uint32_t*)b->in_pfx,
+                       b->kC);
   else if (b->kslot)
     hipLaunchKernelGGL(gv::k_ecmult<true>, grd, blk, 0, se, b->gtab, b->n, C, b->digits, b->kqt, b->kzq,
                        b->flags, b->in_r, b->bits, (const uint32_t*)b->in_pfx, b->kC);
@@ -1388,6 +1401,7 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
                        (const uint32_t*)b->qtab, (const uint32_t*)b->zq, b->flags, b->in_r, b->bits,
                        (const uint32_t*)nullptr, 0u);
   if (b->ev[3]) (void)hipEventRecord(b->ev[3], se);
+  if (sorted) return gvk_unsort_bits(b->n, b->srt.pos, b->srt.bits, b->bits, se);
   return hipGetLastError();
 }
 
@@ -1429,7 +1443,7 @@ hipError_t gvk_keys_point(uint32_t n, const uint32_t* slots, const uint32_t* kqt
 
 hipError_t gvk_sha256(const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint32_t n, uint32_t C,
                       uint32_t* e, hipStream_t st) {
-  hipLaunchKernelGGL(gv::k_sha256, dim3(C / 256), dim3(256), 0, st, blob, off, len, n, C, e);
+  hipLaunchKernelGGL(gv::k_sha256, dim3(C / 256), dim3(256), 0, st, blob, off, len, n, C, e, (const uint32_t*)nullptr);
   return hipGetLastError();
 }
 

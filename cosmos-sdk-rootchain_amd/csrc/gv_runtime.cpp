@@ -524,6 +524,7 @@ struct gv_ctx {
   bool pipeline_dev = true;     // pipelined device-resident calls on the context stream (dev_run; GV_PIPELINE=0: A/B)
   bool group_keys = true;       // pub33 throughput batches parse each distinct key once (group_keys; GV_GROUP_KEYS=0: A/B)
   bool keys_scratch = true;     // key tables: forward entries through coalesced scratch rows (GV_KEYS_SCRATCH=0: A/B)
+  bool sort_keys = true;        // keyed k4 batches run their lanes in slot order (gv_sort.hip; GV_SORT_KEYS=0: A/B)
   size_t group_min = 16384;     // ... batches of at least this many items
   int group_div = 5;            // ... taking the keyed pipeline when distinct keys <= items / group_div (break-even ~4:
                                 // a key build ~18 ns vs ~4 ns saved per item, profiles/r03/group_ab)
@@ -580,7 +581,7 @@ int ensure_group_arena(Set* s, size_t cap) {
 // slot.  Scratch: the set's per-lane Q-table region (unused by the keyed
 // pipeline; the pub33 pipeline rewrites it).  One 4-byte read-back (the
 // distinct-key count) decides the route.
-int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t st) {
+int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t st, uint32_t** used_end = nullptr) {
   const size_t C = b.C;
   size_t T = 512;
   while (T < 2 * n) T <<= 1;
@@ -596,8 +597,10 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
     return GV_ENOMEM;
   }
   int rc = GV_OK;
-  CK(gvk_unpack(b.pub33, b.sig64, b.dig32, (uint32_t)n, (uint32_t)C, b.in_x, b.in_pfx, b.in_r, b.in_s, b.in_e, st));
-  b.unpacked = 1;
+  // the key rows only: the signature / digest rows follow in gvk_verify, in
+  // item order or (keyed, key-ordered lanes) in slot order
+  CK(gvk_unpack(b.pub33, nullptr, nullptr, (uint32_t)n, (uint32_t)C, b.in_x, b.in_pfx, b.in_r, b.in_s, b.in_e, st));
+  b.unpacked = 2;
   CK(gvk_dedupe((uint32_t)n, (uint32_t)C, b.in_x, b.in_pfx, table, (uint32_t)T, rep, uid, count, kslot,
                 (uint32_t)capU, (uint32_t)capU, kx, kpfx, st));
   CK(hipMemcpyAsync(s->h_count, count, 4, hipMemcpyDeviceToHost, st));
@@ -617,6 +620,7 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
     qe = nullptr;
   CK(gvk_keys_build_rows((uint32_t)U, (uint32_t)capU, kx, kpfx, qr, qe, s->g_kqt, s->g_kzq, (uint32_t)capU,
                          s->g_kok, s->g_kqt2, s->g_kzq2, s->side));
+  if (used_end) *used_end = qe ? qe + (size_t)(GV_QTAB_N - 1) * 18 * C4 : qr + (size_t)(GV_QTAB_N - 1) * 9 * C4;
   CK(hipEventRecord(s->keys_done, s->side));
   b.keys_ready = s->keys_done;
   b.pub33 = nullptr;
@@ -626,6 +630,27 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   d->grouped_batches++;
   d->grouped_keys += U;
   return GV_OK;
+}
+
+// Key-ordered lanes (gv_sort.hip) for a keyed k4 batch: scratch from word
+// `base` of the set's Q-table region (unused by the keyed pipeline past the
+// grouping rows); no room or the option off: item order.
+void plan_sort(gv_ctx* ctx, Set* s, gvk_batch& b, uint32_t* base) {
+  if (!ctx->sort_keys || !b.kslot || !b.gtab4) return;
+  const size_t C = b.C, nb = (size_t)b.kcount + 1;
+  const size_t tb = gvk_sort_temp_bytes((uint32_t)nb);
+  uint32_t* p = s->qtab + round_up((size_t)(base - s->qtab), 64);
+  gvk_sort so;
+  so.pos = p; p += C;
+  so.perm = p; p += C;
+  so.kslot = p; p += C;
+  so.bits = (uint64_t*)p; p += C / 32;
+  so.cnt = p; p += round_up(nb, 64);
+  so.off = p; p += round_up(nb, 64);
+  so.temp = p; p += round_up(tb / 4 + 1, 64);
+  so.temp_bytes = tb;
+  if ((size_t)(p - s->qtab) > (size_t)GV_QTAB_WORDS * C) return;
+  b.srt = so;
 }
 
 // A key arena other than the device's gv_keys_load arena: a host slice's
@@ -725,10 +750,12 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
       CK(hipEventRecord(rs[5], st));
     }
   } else {
+    uint32_t* sort_base = s->qtab;                // keyed: the Q-table region is free
     if (!kslot && pub && ctx->group_keys && n >= ctx->group_min) {
-      rc = group_keys(ctx, d, s, b, n, st);
+      rc = group_keys(ctx, d, s, b, n, st, &sort_base);
       if (rc) return rc;
     }
+    plan_sort(ctx, s, b, sort_base);
     CK(gvk_verify(&b, st));
   }
   if (rs) {
@@ -1265,6 +1292,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   parse_size_env("GV_MAX_BATCH", &ctx->max_batch);
   if (const char* k4 = getenv("GV_KEYED_K4")) ctx->keyed_k4 = strcmp(k4, "0") != 0;
   if (const char* ks = getenv("GV_KEYS_SCRATCH")) ctx->keys_scratch = strcmp(ks, "0") != 0;
+  if (const char* sk = getenv("GV_SORT_KEYS")) ctx->sort_keys = strcmp(sk, "0") != 0;
   if (const char* ls = getenv("GV_LAT_SLICED")) ctx->lat_sliced = strcmp(ls, "0") != 0;
   if (const char* zc = getenv("GV_LAT_ZC")) ctx->lat_zero_copy = strcmp(zc, "0") != 0;
   if (const char* pl = getenv("GV_PIPELINE")) ctx->pipeline_dev = strcmp(pl, "0") != 0;
@@ -1761,6 +1789,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "group_div")) {
     if (val < 2 || val > 1024) return GV_EINVAL;
     ctx->group_div = (int)val;
+  } else if (!strcmp(key, "sort_keys")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->sort_keys = val != 0;
   } else if (!strcmp(key, "pipeline_dev")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->pipeline_dev = val != 0;

@@ -235,6 +235,10 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * items / "group_div" (default 5) parses each distinct key once -- grouped
  * on the device, tables built into a per-batch arena, the items verified by
  * the keyed pipeline; same verdicts; default 1, env GV_GROUP_KEYS),
+ * "sort_keys" (0/1: keyed throughput batches on the 4-group ladder -- cached
+ * slots, grouped keys -- run their lanes in slot order: a counting sort by
+ * slot, the signature rows read in that order, the accept bits gathered back
+ * to item order; same verdicts; default 1, env GV_SORT_KEYS),
  * "pipeline_dev" (0/1: device-resident calls on the context stream past the
  * small-batch bound are pipelined -- consecutive calls alternate scratch sets,
  * their unpack / s^-1 / prep kernels run on a low-priority stream under the
