@@ -16,7 +16,9 @@
 #define GV_QWIN 26              // Q windows over a 128-bit GLV half: positions 0,5,..,125
 #define GV_GWIN ((GV_QWIN - 1) / GV_GSTEP + 1)   // G windows at positions 0, GV_GW, ..
 #define GV_DIGIT_ROWS (GV_QWIN + 2 * GV_GWIN)    // Q: packed int16 pair per window; G: int32 per digit
+#ifndef GV_INV_M
 #define GV_INV_M 16             // signatures folded per lane by k_scalar_inv
+#endif
 
 static_assert(GV_GW % GV_QW == 0, "G windows must sit on Q window positions");
 static_assert(GV_GW * GV_GWIN >= 130 && GV_GW * (GV_GWIN - 1) <= GV_QW * (GV_QWIN - 1), "G window count");
