@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -696,7 +697,10 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     b.kC = ka->kC; b.kcount = ka->kcount;
     b.kqt2 = ka->kqt2; b.gtab4 = ka->gtab4;
     kzq2 = ka->kzq2;
-    if (ka->ready) CK(hipStreamWaitEvent(st, ka->ready, 0));
+    // the slots are on the device already (slice_group read the key count
+    // back after k_dedupe_map); only k_prep on reads the tables, so the
+    // chunk's unpack / sort / s^-1 overlap the slice's table build
+    b.keys_ready = ka->ready;
   } else if (kslot) {
     b.pub33 = nullptr;
     b.kslot = kslot; b.kqt = d->kqt; b.kzq = d->kzq; b.kok = d->kok;
@@ -720,6 +724,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
   }
   if (n <= (kslot ? ctx->lat_max_keyed : ctx->lat_max)) {
     // small batch: one fused kernel, several lanes per signature (gv_lat.hip)
+    if (b.keys_ready) CK(hipStreamWaitEvent(st, b.keys_ready, 0));   // a host slice's tables
     gvk_lat lb;
     memset(&lb, 0, sizeof lb);
     lb.n = (uint32_t)n; lb.C = (uint32_t)C;
@@ -849,8 +854,21 @@ int harvest(Dev* d, Set* s, const HostBatch& hb) {
   if (hb.out_ok) {
     uint8_t* o = hb.out_ok + c0;
     const uint64_t* w = s->h_bits;
+    // 8 verdict bytes per bitmap byte through a 256-entry table (lo % 64 == 0)
+    static const std::array<uint64_t, 256> spread = [] {
+      std::array<uint64_t, 256> t{};
+      for (int v = 0; v < 256; ++v)
+        for (int b = 0; b < 8; ++b) t[v] |= (uint64_t)((v >> b) & 1) << (8 * b);
+      return t;
+    }();
     auto unpack = [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; ++i) o[i] = (uint8_t)((w[i >> 6] >> (i & 63)) & 1u);
+      const uint8_t* wb = (const uint8_t*)w;
+      size_t i = lo;
+      for (; i + 8 <= hi; i += 8) {
+        const uint64_t v = spread[wb[i >> 3]];
+        memcpy(o + i, &v, 8);
+      }
+      for (; i < hi; ++i) o[i] = (uint8_t)((w[i >> 6] >> (i & 63)) & 1u);
     };
     if (cn < (size_t(1) << 18)) unpack(0, cn);
     else {
