@@ -241,8 +241,86 @@ __global__ __launch_bounds__(256) void k_ed_lat_sl(const gvk_edl b) {
   if (threadIdx.x == 0) b.out8[gi] = ok ? 1u : 0u;
 }
 
+// Large batches against cached keys (k_ed_keyed, one signature per lane):
+// the key's comb table of -A replaces FromBytes(A), the per-lane table and
+// the 252 doublings of the throughput ladder -- [h](-A) is 64 table adds, no
+// doubling --, then the 32 [s]B comb adds and the encode / compare of
+// ed_ladder_check.  Lanes run in slot order (perm from gv_sort.hip's counting
+// sort): a validator set's commits name their keys in the same order every
+// block, so item order would put 64 different 73 KB tables under one wave.
+__global__ __launch_bounds__(256) void k_ed_keyed(const gvk_edk b) {
+  const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= b.n) return;
+  const uint32_t it = b.perm ? b.perm[g] : g;
+  u32 sl = b.slot[it];
+  bool ok = sl < b.kcount;
+  if (!ok) sl = 0;                          // the arena always holds slot 0's memory
+  ok = ok && b.kok[sl] != 0u;
+  u32 sw[16], pre[16];
+  const uint4* sp = (const uint4*)(b.sig64 + (size_t)it * 64);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint4 v = sp[q];
+    sw[4 * q] = v.x; sw[4 * q + 1] = v.y; sw[4 * q + 2] = v.z; sw[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    pre[i] = sw[i];                         // R
+    pre[8 + i] = b.kpub[(size_t)sl * 8 + i];   // A (the bytes Verify hashes)
+  }
+  const uint8_t* m = b.msg_blob ? b.msg_blob + b.msg_off[it] : nullptr;
+  u32 dig[16], h[8];
+  sha512_pre64(dig, pre, [=](u32 i) { return (u32)m[i]; }, b.msg_len[it]);
+  sc_reduce512(h, dig);                     // ScReduce
+  ok = ok && (sw[15] >> 29) == 0 && sc_minimal(sw + 8);   // sig[63] & 224 == 0, ScMinimal
+  // [h](-A) = sum_w digit_w * 16^w (-A): one cached-table add per nonzero digit
+  const uint64_t car = sc_radix16_carries(h);
+  const u32* kt = b.ktab + (size_t)sl * GV_EDK_WORDS;
+  ge_ext acc;
+  ge_identity(acc);
+#pragma unroll 1
+  for (int w = 0; w < 64; ++w) {
+    const int nib = (int)((h[w >> 3] >> (4 * (w & 7))) & 15u);
+    const int cin = w > 0 ? (int)((car >> (w - 1)) & 1u) : 0;
+    const int cout = w < 63 ? (int)((car >> w) & 1u) : 0;
+    const int dg = nib + cin - 16 * cout;
+    if (dg != 0) {
+      const int mag = dg < 0 ? -dg : dg;
+      ge_add_tab<true>(acc, acc, kt + (size_t)(w * 8 + mag - 1) * ED_CACHED_WORDS, 1, 0, dg < 0);
+    }
+  }
+  // + [s]B: signed radix-256 digits, LSB-first (ed_ladder_check's recoding)
+  u32 ss[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ss[i] = sw[8 + i];
+  int carry = 0;
+#pragma unroll 1
+  for (int w = 0; w < ED_BTAB_WINDOWS; ++w) {
+    int dgt = (int)(ss[0] & 0xFFu) + carry;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) ss[k] = (ss[k] >> 8) | (ss[k + 1] << 24);
+    ss[7] >>= 8;
+    carry = dgt > 128 ? 1 : 0;
+    dgt -= 256 * carry;
+    const int mag = dgt < 0 ? -dgt : dgt;
+    ge_add_pretab(acc, acc, b.btab + (size_t)(w * ED_BTAB_ENTRIES + mag) * ED_PRE_WORDS, dgt < 0);
+  }
+  u32 ew[8];
+  ge_tobytes(ew, acc);
+  u32 diff = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) diff |= ew[i] ^ sw[i];
+  b.out8[it] = (ok && diff == 0u) ? 1u : 0u;
+}
+
 }  // namespace ed
 }  // namespace gv
+
+extern "C" hipError_t gvk_ed_keyed(const gvk_edk* b, hipStream_t st) {
+  if (b->n == 0) return hipSuccess;
+  hipLaunchKernelGGL(gv::ed::k_ed_keyed, dim3((b->n + 255) / 256), dim3(256), 0, st, *b);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t gvk_ed_keys(const uint8_t* pub32, uint32_t n, uint32_t base, uint32_t* ktab, uint32_t* kpub,
                                   uint32_t* kok, hipStream_t st) {

@@ -166,6 +166,24 @@ typedef struct gvk_edl {
 hipError_t gvk_ed_keys(const uint8_t* pub32, uint32_t n, uint32_t base, uint32_t* ktab, uint32_t* kpub, uint32_t* kok,
                        hipStream_t st);
 hipError_t gvk_ed_lat(const gvk_edl* b, hipStream_t st);
+// Large ed25519 batches against cached keys (k_ed_keyed): one signature per
+// lane, lane g takes item perm[g] (null: g), verdict byte out8[item].
+typedef struct gvk_edk {
+  uint32_t n;
+  const uint32_t* perm;         // n lanes -> items (gv_sort.hip), or null
+  const uint32_t* slot;         // n key slots (item order)
+  const uint8_t* sig64;         // n x 64
+  const uint8_t* msg_blob;
+  const uint64_t* msg_off;
+  const uint32_t* msg_len;
+  const uint32_t* ktab;
+  const uint32_t* kpub;
+  const uint32_t* kok;
+  uint32_t kcount;
+  const uint32_t* btab;
+  uint8_t* out8;                // n verdict bytes (device)
+} gvk_edk;
+hipError_t gvk_ed_keyed(const gvk_edk* b, hipStream_t st);
 
 hipError_t gvk_gen_gtable(uint32_t* gtab, hipStream_t st);
 // the keyed ladder's G tables (GV_KEY2_TABLES x 2 x GV_GTAB_N x 16 words); base_scratch: 48 words

@@ -328,6 +328,10 @@ struct Dev {
   size_t ekcap = 0;
   uint8_t* edl_h = nullptr;                       // small keyed ed25519 batches: pinned inputs + verdicts (zero-copy)
   size_t edl_h_cap = 0;
+  uint8_t *edk_h = nullptr, *edk_d = nullptr;     // large keyed ed25519 batches: pinned staging / device copy
+  size_t edk_h_cap = 0, edk_d_cap = 0;
+  uint32_t* edk_s = nullptr;                      // ... and their slot-order sort scratch (words)
+  size_t edk_s_cap = 0;
   std::mutex mu;
   Pool* pool = nullptr;                           // staging memcpy threads: the context's shared pool
   Worker* worker = nullptr;                       // slice runner (devices 1..n-1 of a context)
@@ -537,6 +541,7 @@ struct gv_ctx {
   std::atomic<uint64_t> ed_keys_gen{0};
   std::mutex ed_keys_mu;
   std::vector<uint8_t> ed_kpub;  // the raw keys per slot (large keyed batches run the throughput kernels on them)
+  bool ed_keyed = true;          // keyed ed25519 batches past ed_lat_max on k_ed_keyed (GV_ED_KEYED=0: the throughput kernels)
   size_t ed_lat_max = 2048;      // keyed ed25519 batches up to this size take k_ed_lat_sl (one signature per block)
 };
 
@@ -1311,6 +1316,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* k4 = getenv("GV_KEYED_K4")) ctx->keyed_k4 = strcmp(k4, "0") != 0;
   if (const char* ks = getenv("GV_KEYS_SCRATCH")) ctx->keys_scratch = strcmp(ks, "0") != 0;
   if (const char* sk = getenv("GV_SORT_KEYS")) ctx->sort_keys = strcmp(sk, "0") != 0;
+  if (const char* ek = getenv("GV_ED_KEYED")) ctx->ed_keyed = strcmp(ek, "0") != 0;
   if (const char* ls = getenv("GV_LAT_SLICED")) ctx->lat_sliced = strcmp(ls, "0") != 0;
   if (const char* zc = getenv("GV_LAT_ZC")) ctx->lat_zero_copy = strcmp(zc, "0") != 0;
   if (const char* pl = getenv("GV_PIPELINE")) ctx->pipeline_dev = strcmp(pl, "0") != 0;
@@ -1379,6 +1385,9 @@ void gv_close(gv_ctx* ctx) {
     if (d->ed.last) (void)hipEventDestroy(d->ed.last);
     for (uint32_t* p : {d->ektab, d->ekpub, d->ekok}) if (p) (void)hipFree(p);
     if (d->edl_h) (void)hipHostFree(d->edl_h);
+    if (d->edk_h) (void)hipHostFree(d->edk_h);
+    if (d->edk_d) (void)hipFree(d->edk_d);
+    if (d->edk_s) (void)hipFree(d->edk_s);
     for (auto& rs : d->ring)
       for (auto e : rs) if (e) (void)hipEventDestroy(e);
     for (hipStream_t t : {d->lo_st[0], d->lo_st[1], d->hi_st})
@@ -1609,6 +1618,94 @@ int gv_ed_keys_reset(gv_ctx* ctx) {
 size_t gv_ed_keys_count(const gv_ctx* ctx) { return ctx ? ctx->ed_keys : 0; }
 uint64_t gv_ed_keys_generation(const gv_ctx* ctx) { return ctx ? ctx->ed_keys_gen.load() : 0; }
 
+namespace {
+struct EdKeyedHost {
+  const uint32_t* slot;
+  const uint8_t* sig64;
+  const uint8_t* blob;
+  const uint64_t* off;
+  const uint32_t* len;
+  uint8_t* out_ok;
+};
+
+int ensure_dev(uint8_t** p, size_t* cap, size_t bytes) {
+  if (bytes <= *cap) return GV_OK;
+  if (*p) (void)hipFree(*p);
+  *cap = 0;
+  const size_t c = round_up(bytes, (size_t)1 << 20);
+  if (hipMalloc((void**)p, c) != hipSuccess) { *p = nullptr; return GV_ENOMEM; }
+  *cap = c;
+  return GV_OK;
+}
+
+// Items [lo, hi) of a large keyed ed25519 batch on one device (k_ed_keyed):
+// chunks staged through pinned memory, lanes sorted by slot on the device.
+int ed_keyed_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const EdKeyedHost& hb, size_t kcount) {
+  std::lock_guard<std::mutex> lk(d->mu);
+  CK(hipSetDevice(d->id));
+  hipStream_t st = d->set[0].st;
+  int rc = ed_ensure(d, 256, st);                 // the resident comb table of B
+  if (rc) return rc;
+  const size_t chunk = std::min<size_t>(ctx->max_batch, 262144);
+  const size_t nb = kcount + 1, tb = gvk_sort_temp_bytes((uint32_t)nb);
+  for (size_t c0 = lo; c0 < hi; c0 += chunk) {
+    const size_t cn = std::min(chunk, hi - c0);
+    uint64_t lo_b = UINT64_MAX, hi_b = 0;
+    for (size_t i = c0; i < c0 + cn; ++i) {
+      lo_b = std::min<uint64_t>(lo_b, hb.off[i]);
+      hi_b = std::max<uint64_t>(hi_b, hb.off[i] + hb.len[i]);
+    }
+    if (lo_b > hi_b) lo_b = hi_b = 0;
+    const size_t o_sig = round_up(cn * 4, 256), o_off = o_sig + cn * 64, o_len = o_off + cn * 8,
+                 o_out = o_len + cn * 4, o_blob = round_up(o_out + cn, 256), total = o_blob + (hi_b - lo_b);
+    const size_t C = round_up(cn, 256), sw = 3 * C + 2 * round_up(nb, 64) + round_up(tb / 4 + 1, 64);
+    if ((rc = ensure_pinned(&d->edk_h, &d->edk_h_cap, total))) return rc;
+    if ((rc = ensure_dev(&d->edk_d, &d->edk_d_cap, total))) return rc;
+    if ((rc = ensure_dev((uint8_t**)&d->edk_s, &d->edk_s_cap, sw * 4))) return rc;
+    uint8_t* h = d->edk_h;
+    const CopySeg segs[2] = {CopySeg{h, (const uint8_t*)(hb.slot + c0), cn * 4}, CopySeg{h + o_sig, hb.sig64 + c0 * 64, cn * 64}};
+    par_copy_segs(d->pool, segs, 2);
+    uint64_t* ro = (uint64_t*)(h + o_off);
+    for (size_t i = 0; i < cn; ++i) ro[i] = hb.off[c0 + i] - lo_b;
+    memcpy(h + o_len, hb.len + c0, cn * 4);
+    if (hi_b > lo_b) par_copy(d->pool, h + o_blob, hb.blob + lo_b, hi_b - lo_b);
+    uint8_t* dd = d->edk_d;
+    CK(hipMemcpyAsync(dd, h, total, hipMemcpyHostToDevice, st));
+    uint32_t* p = d->edk_s;
+    gvk_sort so;
+    so.pos = p; p += C;
+    so.perm = p; p += C;
+    so.kslot = p; p += C;
+    so.bits = nullptr;
+    so.cnt = p; p += round_up(nb, 64);
+    so.off = p; p += round_up(nb, 64);
+    so.temp = p;
+    so.temp_bytes = tb;
+    CK(gvk_sort_slots(&so, (uint32_t)cn, (const uint32_t*)dd, (uint32_t)kcount, st));
+    gvk_edk b;
+    memset(&b, 0, sizeof b);
+    b.n = (uint32_t)cn;
+    b.perm = ctx->sort_keys ? so.perm : nullptr;
+    b.slot = (const uint32_t*)dd;
+    b.sig64 = dd + o_sig;
+    b.msg_blob = dd + o_blob;
+    b.msg_off = (const uint64_t*)(dd + o_off);
+    b.msg_len = (const uint32_t*)(dd + o_len);
+    b.ktab = d->ektab;
+    b.kpub = d->ekpub;
+    b.kok = d->ekok;
+    b.kcount = (uint32_t)kcount;
+    b.btab = d->edtab;
+    b.out8 = dd + o_out;
+    CK(gvk_ed_keyed(&b, st));
+    CK(hipMemcpyAsync(h + o_out, dd + o_out, cn, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    memcpy(hb.out_ok + c0, h + o_out, cn);
+  }
+  return GV_OK;
+}
+}  // namespace
+
 int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64,
                                  const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len,
                                  uint8_t* out_ok) {
@@ -1622,8 +1719,27 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
   {
     std::lock_guard<std::mutex> kl(ctx->ed_keys_mu);
     kcount = ctx->ed_keys;
+    if (n > ctx->ed_lat_max && kcount && ctx->ed_keyed) {
+      // large batches: one signature per lane against the key tables
+      // (k_ed_keyed), split over the devices like run_ed_host
+      const EdKeyedHost hb{slot, sig64, msg_blob, msg_off, msg_len, out_ok};
+      const size_t nd = ctx->devs.size(), per = round_up((n + nd - 1) / nd, 256);
+      std::vector<int> rcs(nd, GV_OK);
+      std::vector<std::future<int>> futs(nd);
+      for (size_t k = 1; k < nd; ++k) {
+        const size_t lo = std::min(n, k * per), hi = std::min(n, (k + 1) * per);
+        if (lo >= hi) continue;
+        Dev* dk = ctx->devs[k];
+        futs[k] = dk->worker->post([=, &hb]() { return ed_keyed_slice(ctx, dk, lo, hi, hb, kcount); });
+      }
+      rcs[0] = ed_keyed_slice(ctx, ctx->devs[0], 0, std::min(n, per), hb, kcount);
+      for (size_t k = 1; k < nd; ++k)
+        if (futs[k].valid()) rcs[k] = futs[k].get();
+      for (int rc : rcs) if (rc) return rc;
+      return GV_OK;
+    }
     if (n > ctx->ed_lat_max || kcount == 0) {
-      // large batches: the throughput kernels over the slots' raw keys
+      // large batches (ed_keyed 0): the throughput kernels over the slots' raw keys
       std::vector<uint8_t> pub(n * 32, 0);
       for (size_t i = 0; i < n; ++i)
         if (slot[i] < kcount) memcpy(&pub[i * 32], &ctx->ed_kpub[(size_t)slot[i] * 32], 32);
@@ -1807,6 +1923,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "group_div")) {
     if (val < 2 || val > 1024) return GV_EINVAL;
     ctx->group_div = (int)val;
+  } else if (!strcmp(key, "ed_keyed")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->ed_keyed = val != 0;
   } else if (!strcmp(key, "sort_keys")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->sort_keys = val != 0;

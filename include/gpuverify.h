@@ -235,6 +235,11 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * items / "group_div" (default 5) parses each distinct key once -- grouped
  * on the device, tables built into a per-batch arena, the items verified by
  * the keyed pipeline; same verdicts; default 1, env GV_GROUP_KEYS),
+ * "ed_keyed" (0/1: gv_verify_ed25519_msgs_keyed batches past "ed_lat_max"
+ * run one signature per lane against the cached comb tables of -A -- 64
+ * table adds for [h](-A), no doublings, lanes in slot order; 0 = the
+ * throughput kernels over the slots' raw keys; same verdicts; default 1, env
+ * GV_ED_KEYED),
  * "sort_keys" (0/1: keyed throughput batches on the 4-group ladder -- cached
  * slots, grouped keys -- run their lanes in slot order: a counting sort by
  * slot, the signature rows read in that order, the accept bits gathered back

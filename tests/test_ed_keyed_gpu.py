@@ -162,3 +162,31 @@ def test_small_batch_latency(ver):
     pk, pu = float(np.median(tk)) * 1e3, float(np.median(tu)) * 1e3
     print(f"ed25519 @64: keyed sliced p50 {pk:.3f} ms, throughput kernels p50 {pu:.3f} ms")
     assert pk < pu
+
+
+def test_large_keyed_batches_schedules_agree(ver):
+    """Past ed_lat_max the cached-key throughput kernel (k_ed_keyed, lanes in
+    slot order) must give the throughput kernels' verdicts: goldens tiled and
+    shuffled (every rejection class, keys that FromBytes rejects included),
+    never-loaded slots interleaved, both lane orders."""
+    gv = golden()
+    reps = max(1, 6000 // len(gv))
+    order = np.random.default_rng(21).permutation(reps * len(gv))
+    items = [gv[i % len(gv)] for i in order]
+    slots = load_keys(ver, [p for _, p, _, _, _ in items])
+    slots[::7] = ver.ed_keys_count + np.arange(len(slots[::7]), dtype=np.uint32)   # no key: false
+    exp = np.array([ok for *_, ok in items])
+    exp[::7] = False
+    sg, msgs = sigs([s for *_, s, _ in items]), [m for _, _, m, _, _ in items]
+    runs = {}
+    try:
+        for keyed, srt in ((1, 1), (1, 0), (0, 1)):
+            ver.set_option("ed_keyed", keyed)
+            ver.set_option("sort_keys", srt)
+            runs[(keyed, srt)] = ver.verify_batch_ed25519_keyed(slots, sg, msgs)
+    finally:
+        ver.set_option("ed_keyed", 1)
+        ver.set_option("sort_keys", 1)
+    for k, got in runs.items():
+        bad = np.nonzero(got.astype(bool) != exp)[0]
+        assert bad.size == 0, (k, [(items[i][0], bool(exp[i])) for i in bad[:10]])

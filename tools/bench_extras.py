@@ -668,8 +668,9 @@ def ed25519(ver, wl, n: int = 1_000_000, threads: int = 16, steps: int = 3, nkey
     cpu_rate = m / (time.perf_counter() - t)
     cpu_mism = int(np.count_nonzero(out.astype(bool) != exp[:m]))
     small = ed25519_small_batches(ver, wl, pub, sig, blob, off, lens, exp, threads)
+    keyed = ed25519_keyed_throughput(ver, pub, sig, blob, off, lens, exp)
     return {"items": n, "mean_msg_bytes": round(float(lens.mean()), 1), "value": round(n * steps / el, 1),
-            "small_batches": small,
+            "small_batches": small, "keyed_throughput": keyed,
             "unit": "ed25519 verifies/s", "mismatches": int(np.count_nonzero(got != exp)),
             "rejects_expected": int(bad.sum()), "kernel_ms": round(kms, 4), "launches_averaged": cnt,
             "roofline": {"kernel": "k_ed_verify", "work_per_verify": W_ED25519, "achieved_T": round(achieved / 1e12, 3),
@@ -677,6 +678,33 @@ def ed25519(ver, wl, n: int = 1_000_000, threads: int = 16, steps: int = 3, nkey
             "cpu_openssl": {"value": round(cpu_rate, 1), "threads": threads, "sample": m, "mismatches": cpu_mism},
             "workload_gen_s": round(t_gen, 2),
             "note": "device-resident (inputs in HBM); keys = 4,096 RFC 8032 seeds round-robin; OpenSSL Ed25519 signs"}
+
+
+def ed25519_keyed_throughput(ver, pub, sig, blob, off, lens, exp, m: int = 262_144, steps: int = 3):
+    """Large ed25519 batches against cached keys (IBC commit catch-up: a
+    validator set's keys sign every block), host buffers end to end:
+    gv_verify_ed25519_msgs_keyed past ed_lat_max (k_ed_keyed: 64 table adds
+    for [h](-A), no doublings, lanes in slot order) beside the throughput
+    kernels (gv_verify_ed25519_msgs) on the same items."""
+    m = min(m, len(pub))
+    uk, inv = np.unique(pub[:m], axis=0, return_inverse=True)
+    ver.ed_keys_reset()
+    slots = ver.ed_keys_load(uk)[inv.reshape(-1)].astype(np.uint32)
+    msgs = (blob[:int(off[m - 1] + lens[m - 1])], off[:m], lens[:m])
+    out = {}
+    for name, fn in (("keyed", lambda: ver.verify_batch_ed25519_keyed(slots, sig[:m], msgs)),
+                     ("unkeyed", lambda: ver.verify_batch_ed25519(pub[:m], sig[:m], msgs))):
+        g = fn()
+        t = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        el = time.perf_counter() - t
+        out[name] = {"value": round(m * steps / el, 1), "ms_per_call": round(el / steps * 1e3, 3),
+                     "mismatches": int(np.count_nonzero(g.astype(bool) != exp[:m]))}
+    ver.ed_keys_reset()
+    return {"items": m, "keys": int(len(uk)), "unit": "ed25519 verifies/s", **out,
+            "note": "host buffers (~350 B messages, PCIe incl.), keys loaded once beforehand; keyed = "
+                    "gv_verify_ed25519_msgs_keyed (k_ed_keyed), unkeyed = gv_verify_ed25519_msgs"}
 
 
 def ed25519_small_batches(ver, wl, pub, sig, blob, off, lens, exp, threads, sizes=(1, 16, 64, 150, 256, 1024)):
