@@ -227,8 +227,16 @@ __global__ __launch_bounds__(256) void k_dedupe(u32 n, u32 C, const u32* x, cons
 __global__ __launch_bounds__(256) void k_dedupe_assign(u32 n, u32 C, const u32* x, const u32* pfx, const u32* rep,
                                                         u32* uid, u32* count, u32 capU, u32 CU, u32* kx, u32* kpfx) {
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n || rep[g] != g) return;
-  const u32 u = atomicAdd(count, 1u);
+  const bool first = g < n && rep[g] == g;
+  // one atomic per wave: the wave's representatives take consecutive ids
+  const uint64_t m = __ballot(first);
+  if (m == 0) return;                                  // wave-uniform
+  const u32 lane = threadIdx.x & 63u, leader = (u32)__builtin_ctzll(m);
+  u32 b0 = 0;
+  if (lane == leader) b0 = atomicAdd(count, (u32)__builtin_popcountll(m));
+  b0 = (u32)__shfl((int)b0, (int)leader);
+  if (!first) return;
+  const u32 u = b0 + (u32)__builtin_popcountll(m & ((1ull << lane) - 1ull));
   uid[g] = u;
   if (u < capU) {
 #pragma unroll
