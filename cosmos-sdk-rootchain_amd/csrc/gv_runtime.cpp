@@ -328,10 +328,12 @@ struct Dev {
   size_t ekcap = 0;
   uint8_t* edl_h = nullptr;                       // small keyed ed25519 batches: pinned inputs + verdicts (zero-copy)
   size_t edl_h_cap = 0;
-  uint8_t *edk_h = nullptr, *edk_d = nullptr;     // large keyed ed25519 batches: pinned staging / device copy
-  size_t edk_h_cap = 0, edk_d_cap = 0;
-  uint32_t* edk_s = nullptr;                      // ... and their slot-order sort scratch (words)
-  size_t edk_s_cap = 0;
+  // large keyed ed25519 batches, two buffers (chunk i on set[i % 2]'s stream):
+  // pinned staging, device copy, slot-order sort scratch (words)
+  uint8_t *edk_h[2] = {nullptr, nullptr}, *edk_d[2] = {nullptr, nullptr};
+  size_t edk_h_cap[2] = {0, 0}, edk_d_cap[2] = {0, 0};
+  uint32_t* edk_s[2] = {nullptr, nullptr};
+  size_t edk_s_cap[2] = {0, 0};
   std::mutex mu;
   Pool* pool = nullptr;                           // staging memcpy threads: the context's shared pool
   Worker* worker = nullptr;                       // slice runner (devices 1..n-1 of a context)
@@ -1385,9 +1387,11 @@ void gv_close(gv_ctx* ctx) {
     if (d->ed.last) (void)hipEventDestroy(d->ed.last);
     for (uint32_t* p : {d->ektab, d->ekpub, d->ekok}) if (p) (void)hipFree(p);
     if (d->edl_h) (void)hipHostFree(d->edl_h);
-    if (d->edk_h) (void)hipHostFree(d->edk_h);
-    if (d->edk_d) (void)hipFree(d->edk_d);
-    if (d->edk_s) (void)hipFree(d->edk_s);
+    for (int k = 0; k < 2; ++k) {
+      if (d->edk_h[k]) (void)hipHostFree(d->edk_h[k]);
+      if (d->edk_d[k]) (void)hipFree(d->edk_d[k]);
+      if (d->edk_s[k]) (void)hipFree(d->edk_s[k]);
+    }
     for (auto& rs : d->ring)
       for (auto e : rs) if (e) (void)hipEventDestroy(e);
     for (hipStream_t t : {d->lo_st[0], d->lo_st[1], d->hi_st})
@@ -1639,16 +1643,29 @@ int ensure_dev(uint8_t** p, size_t* cap, size_t bytes) {
 }
 
 // Items [lo, hi) of a large keyed ed25519 batch on one device (k_ed_keyed):
-// chunks staged through pinned memory, lanes sorted by slot on the device.
+// chunks alternate between two buffers / streams, so the host staging of
+// chunk i + 1 (slots, signatures, offsets, messages into pinned memory) runs
+// while chunk i copies and computes; lanes sorted by slot on the device.
 int ed_keyed_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const EdKeyedHost& hb, size_t kcount) {
   std::lock_guard<std::mutex> lk(d->mu);
   CK(hipSetDevice(d->id));
-  hipStream_t st = d->set[0].st;
-  int rc = ed_ensure(d, 256, st);                 // the resident comb table of B
+  int rc = ed_ensure(d, 256, d->set[0].st);       // the resident comb table of B
   if (rc) return rc;
-  const size_t chunk = std::min<size_t>(ctx->max_batch, 262144);
+  const size_t n = hi - lo;
+  const size_t chunk = std::min<size_t>(ctx->max_batch, n > 131072 ? round_up((n + 3) / 4, 256) : n);
   const size_t nb = kcount + 1, tb = gvk_sort_temp_bytes((uint32_t)nb);
-  for (size_t c0 = lo; c0 < hi; c0 += chunk) {
+  struct Pending { size_t c0 = 0, cn = 0, o_out = 0; bool busy = false; } pend[2];
+  auto finish = [&](int k) -> int {                // chunk on buffer k: wait, copy the verdicts out
+    if (!pend[k].busy) return GV_OK;
+    pend[k].busy = false;
+    CK(hipStreamSynchronize(d->set[k].st));
+    memcpy(hb.out_ok + pend[k].c0, d->edk_h[k] + pend[k].o_out, pend[k].cn);
+    return GV_OK;
+  };
+  auto submit = [&](int k, size_t c0) -> int {
+    int rc = finish(k);
+    if (rc) return rc;
+    hipStream_t st = d->set[k].st;
     const size_t cn = std::min(chunk, hi - c0);
     uint64_t lo_b = UINT64_MAX, hi_b = 0;
     for (size_t i = c0; i < c0 + cn; ++i) {
@@ -1659,19 +1676,20 @@ int ed_keyed_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const EdKeyedHost&
     const size_t o_sig = round_up(cn * 4, 256), o_off = o_sig + cn * 64, o_len = o_off + cn * 8,
                  o_out = o_len + cn * 4, o_blob = round_up(o_out + cn, 256), total = o_blob + (hi_b - lo_b);
     const size_t C = round_up(cn, 256), sw = 3 * C + 2 * round_up(nb, 64) + round_up(tb / 4 + 1, 64);
-    if ((rc = ensure_pinned(&d->edk_h, &d->edk_h_cap, total))) return rc;
-    if ((rc = ensure_dev(&d->edk_d, &d->edk_d_cap, total))) return rc;
-    if ((rc = ensure_dev((uint8_t**)&d->edk_s, &d->edk_s_cap, sw * 4))) return rc;
-    uint8_t* h = d->edk_h;
-    const CopySeg segs[2] = {CopySeg{h, (const uint8_t*)(hb.slot + c0), cn * 4}, CopySeg{h + o_sig, hb.sig64 + c0 * 64, cn * 64}};
+    if ((rc = ensure_pinned(&d->edk_h[k], &d->edk_h_cap[k], total))) return rc;
+    if ((rc = ensure_dev(&d->edk_d[k], &d->edk_d_cap[k], total))) return rc;
+    if ((rc = ensure_dev((uint8_t**)&d->edk_s[k], &d->edk_s_cap[k], sw * 4))) return rc;
+    uint8_t* h = d->edk_h[k];
+    const CopySeg segs[2] = {CopySeg{h, (const uint8_t*)(hb.slot + c0), cn * 4},
+                             CopySeg{h + o_sig, hb.sig64 + c0 * 64, cn * 64}};
     par_copy_segs(d->pool, segs, 2);
     uint64_t* ro = (uint64_t*)(h + o_off);
     for (size_t i = 0; i < cn; ++i) ro[i] = hb.off[c0 + i] - lo_b;
     memcpy(h + o_len, hb.len + c0, cn * 4);
     if (hi_b > lo_b) par_copy(d->pool, h + o_blob, hb.blob + lo_b, hi_b - lo_b);
-    uint8_t* dd = d->edk_d;
+    uint8_t* dd = d->edk_d[k];
     CK(hipMemcpyAsync(dd, h, total, hipMemcpyHostToDevice, st));
-    uint32_t* p = d->edk_s;
+    uint32_t* p = d->edk_s[k];
     gvk_sort so;
     so.pos = p; p += C;
     so.perm = p; p += C;
@@ -1681,7 +1699,7 @@ int ed_keyed_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const EdKeyedHost&
     so.off = p; p += round_up(nb, 64);
     so.temp = p;
     so.temp_bytes = tb;
-    CK(gvk_sort_slots(&so, (uint32_t)cn, (const uint32_t*)dd, (uint32_t)kcount, st));
+    if (ctx->sort_keys) CK(gvk_sort_slots(&so, (uint32_t)cn, (const uint32_t*)dd, (uint32_t)kcount, st));
     gvk_edk b;
     memset(&b, 0, sizeof b);
     b.n = (uint32_t)cn;
@@ -1699,10 +1717,20 @@ int ed_keyed_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const EdKeyedHost&
     b.out8 = dd + o_out;
     CK(gvk_ed_keyed(&b, st));
     CK(hipMemcpyAsync(h + o_out, dd + o_out, cn, hipMemcpyDeviceToHost, st));
-    CK(hipStreamSynchronize(st));
-    memcpy(hb.out_ok + c0, h + o_out, cn);
+    pend[k] = Pending{c0, cn, o_out, true};
+    return GV_OK;
+  };
+  int k = 0;
+  for (size_t c0 = lo; c0 < hi && rc == GV_OK; c0 += chunk, k ^= 1) rc = submit(k, c0);
+  for (int j = 0; j < 2; ++j) {                   // drain, the older chunk first (also after an error)
+    const int r2 = finish(k ^ j);
+    if (rc == GV_OK) rc = r2;
   }
-  return GV_OK;
+  if (rc) {
+    (void)hipStreamSynchronize(d->set[0].st);
+    (void)hipStreamSynchronize(d->set[1].st);
+  }
+  return rc;
 }
 }  // namespace
 
