@@ -313,8 +313,92 @@ __global__ __launch_bounds__(256) void k_ed_keyed(const gvk_edk b) {
   b.out8[it] = (ok && diff == 0u) ? 1u : 0u;
 }
 
+// In-batch key grouping for the throughput entry points (a relayer's batch
+// of commits repeats a validator set's keys): the 32 key bytes of every item
+// go into an open-addressing table (2n+ slots, atomicCAS; the first item of a
+// key is its representative), representatives take dense ids (one atomic per
+// wave) and copy their bytes to the compact key rows k_ed_keys reads, every
+// item gets its key's id.  The verdicts are the per-item ones: the key table
+// is a pure function of the 32 bytes.
+GV_DEV void ed_key_words(u32 w[8], const uint8_t* pub32, u32 i) {
+  const uint4* p = (const uint4*)(pub32 + (size_t)i * 32);
+  const uint4 a = p[0], c = p[1];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = c.x; w[5] = c.y; w[6] = c.z; w[7] = c.w;
+}
+__global__ __launch_bounds__(256) void k_ed_dedupe(u32 n, const uint8_t* pub32, u32* table, u32 tmask, u32* rep) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  u32 w[8];
+  ed_key_words(w, pub32, g);
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    h ^= w[i];
+    h *= 0xFF51AFD7ED558CCDull;
+    h ^= h >> 29;
+  }
+  for (u32 sl = (u32)(h ^ (h >> 32)) & tmask;; sl = (sl + 1) & tmask) {
+    const u32 cur = atomicCAS(&table[sl], 0xFFFFFFFFu, g);
+    if (cur == 0xFFFFFFFFu) { rep[g] = g; return; }
+    u32 o[8];
+    ed_key_words(o, pub32, cur);
+    bool eq = true;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) eq &= o[i] == w[i];
+    if (eq) { rep[g] = cur; return; }
+  }
+}
+__global__ __launch_bounds__(256) void k_ed_dedupe_assign(u32 n, const uint8_t* pub32, const u32* rep, u32* uid,
+                                                          u32* count, u32 capU, uint8_t* kpub32) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool first = g < n && rep[g] == g;
+  const uint64_t m = __ballot(first);
+  if (m == 0) return;                                  // wave-uniform
+  const u32 lane = threadIdx.x & 63u, leader = (u32)__builtin_ctzll(m);
+  u32 b0 = 0;
+  if (lane == leader) b0 = atomicAdd(count, (u32)__builtin_popcountll(m));
+  b0 = (u32)__shfl((int)b0, (int)leader);
+  if (!first) return;
+  const u32 u = b0 + (u32)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+  uid[g] = u;
+  if (u < capU) {
+    const uint4* p = (const uint4*)(pub32 + (size_t)g * 32);
+    uint4* q = (uint4*)(kpub32 + (size_t)u * 32);
+    q[0] = p[0];
+    q[1] = p[1];
+  }
+}
+__global__ __launch_bounds__(256) void k_ed_dedupe_map(u32 n, const u32* rep, const u32* uid, u32* slot) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n) slot[g] = uid[rep[g]];
+}
+// item-order verdict bytes -> accept bitmap (words up to ceil(n / 64))
+__global__ __launch_bounds__(256) void k_ed_pack_bits(u32 n, const uint8_t* out8, uint64_t* bits) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t m = __ballot(g < n && out8[g] != 0);
+  if ((threadIdx.x & 63u) == 0 && g < n) bits[g >> 6] = m;
+}
+
 }  // namespace ed
 }  // namespace gv
+
+extern "C" hipError_t gvk_ed_group(uint32_t n, const uint8_t* pub32, uint32_t* table, uint32_t tslots, uint32_t* rep,
+                                   uint32_t* uid, uint32_t* count, uint32_t capU, uint8_t* kpub32, uint32_t* slot,
+                                   hipStream_t st) {
+  const dim3 blk(256), grd((n + 255) / 256);
+  if (hipMemsetAsync(table, 0xFF, (size_t)tslots * 4, st) != hipSuccess || hipMemsetAsync(count, 0, 4, st) != hipSuccess)
+    return hipErrorUnknown;
+  hipLaunchKernelGGL(gv::ed::k_ed_dedupe, grd, blk, 0, st, n, pub32, table, tslots - 1, rep);
+  hipLaunchKernelGGL(gv::ed::k_ed_dedupe_assign, grd, blk, 0, st, n, pub32, (const uint32_t*)rep, uid, count, capU,
+                     kpub32);
+  hipLaunchKernelGGL(gv::ed::k_ed_dedupe_map, grd, blk, 0, st, n, (const uint32_t*)rep, (const uint32_t*)uid, slot);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t gvk_ed_pack_bits(uint32_t n, const uint8_t* out8, uint64_t* bits, hipStream_t st) {
+  hipLaunchKernelGGL(gv::ed::k_ed_pack_bits, dim3((n + 255) / 256), dim3(256), 0, st, n, out8, bits);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t gvk_ed_keyed(const gvk_edk* b, hipStream_t st) {
   if (b->n == 0) return hipSuccess;

@@ -184,6 +184,13 @@ typedef struct gvk_edk {
   uint8_t* out8;                // n verdict bytes (device)
 } gvk_edk;
 hipError_t gvk_ed_keyed(const gvk_edk* b, hipStream_t st);
+// ed25519 in-batch key grouping over n items' pub32 (device AoS): table
+// (tslots = power of two >= 2n words), rep / uid / slot (n words each),
+// count (1 word); the first capU distinct keys' bytes go to kpub32 (32 B each).
+hipError_t gvk_ed_group(uint32_t n, const uint8_t* pub32, uint32_t* table, uint32_t tslots, uint32_t* rep,
+                        uint32_t* uid, uint32_t* count, uint32_t capU, uint8_t* kpub32, uint32_t* slot,
+                        hipStream_t st);
+hipError_t gvk_ed_pack_bits(uint32_t n, const uint8_t* out8, uint64_t* bits, hipStream_t st);
 
 hipError_t gvk_gen_gtable(uint32_t* gtab, hipStream_t st);
 // the keyed ladder's G tables (GV_KEY2_TABLES x 2 x GV_GTAB_N x 16 words); base_scratch: 48 words

@@ -328,6 +328,11 @@ struct Dev {
   size_t ekcap = 0;
   uint8_t* edl_h = nullptr;                       // small keyed ed25519 batches: pinned inputs + verdicts (zero-copy)
   size_t edl_h_cap = 0;
+  // ed25519 in-batch key grouping: per-batch key arena (comb tables of -A), pinned count, stats
+  uint32_t *edg_ktab = nullptr, *edg_kpub = nullptr, *edg_kok = nullptr;
+  size_t edg_cap = 0;
+  uint32_t* ed_h_count = nullptr;
+  uint64_t ed_grouped_batches = 0, ed_grouped_keys = 0;
   // large keyed ed25519 batches, two buffers (chunk i on set[i % 2]'s stream):
   // pinned staging, device copy, slot-order sort scratch (words)
   uint8_t *edk_h[2] = {nullptr, nullptr}, *edk_d[2] = {nullptr, nullptr};
@@ -468,8 +473,95 @@ int ed_ensure(Dev* d, size_t C, hipStream_t st) {
 }
 
 // One k_ed_verify launch over n items (device pointers) on stream st.
+// ed25519 in-batch key grouping (option "ed_group"): batches of at least
+// `min` items with at most items / `div` (and `cap`) distinct keys build each
+// key's comb table once (k_ed_keys into a per-batch arena) and verify on
+// k_ed_keyed; else the throughput kernels.
+struct EdGroupCfg {
+  bool on;
+  size_t min;
+  int div;
+  size_t cap;
+  bool sorted;
+};
+
+int ensure_edg(Dev* d, size_t need) {
+  if (need <= d->edg_cap) return GV_OK;
+  for (uint32_t** q : {&d->edg_ktab, &d->edg_kpub, &d->edg_kok})
+    if (*q) { (void)hipFree(*q); *q = nullptr; }
+  d->edg_cap = 0;
+  const size_t cap = round_up(std::max<size_t>(need, 1024), 1024);
+  if (hipMalloc(&d->edg_ktab, cap * (size_t)GV_EDK_WORDS * 4) != hipSuccess ||
+      hipMalloc(&d->edg_kpub, cap * 8 * 4) != hipSuccess || hipMalloc(&d->edg_kok, cap * 4) != hipSuccess)
+    return GV_ENOMEM;
+  d->edg_cap = cap;
+  return GV_OK;
+}
+
+// The grouped route on the device (scratch: the per-lane table region, which
+// the keyed kernel does not use).  *taken = false: the batch has too many
+// distinct keys (or no room) and the caller runs the throughput kernels.
+int ed_grouped(Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig, const uint8_t* blob, const uint64_t* off,
+               const uint32_t* len, uint64_t* bits, hipStream_t st, const EdGroupCfg& gc, bool* taken) {
+  *taken = false;
+  const size_t C = round_up(n, 256);
+  size_t T = 512;
+  while (T < 2 * n) T <<= 1;
+  const size_t capU = std::min(gc.cap, std::max<size_t>(n / (size_t)gc.div, 1));
+  const size_t nb = capU + 1, tb = gvk_sort_temp_bytes((uint32_t)nb);
+  uint32_t* q = d->ed.atab;
+  uint32_t *table = q, *rep = table + T, *uid = rep + C, *slot = uid + C, *count = slot + C;
+  uint8_t* kpub32 = (uint8_t*)(count + 64);
+  uint32_t* sp = count + 64 + round_up(capU * 8, 64);
+  gvk_sort so;
+  so.pos = sp;
+  so.perm = sp + C;
+  so.kslot = sp + 2 * C;
+  so.bits = nullptr;
+  so.cnt = sp + 3 * C;
+  so.off = so.cnt + round_up(nb, 64);
+  so.temp = so.off + round_up(nb, 64);
+  so.temp_bytes = tb;
+  uint32_t* o8 = (uint32_t*)so.temp + round_up(tb / 4 + 1, 64);
+  if ((size_t)(o8 + C / 4 - q) > C * (size_t)GV_ED_ROWS) return GV_OK;
+  if (!d->ed_h_count && hipHostMalloc((void**)&d->ed_h_count, 64, hipHostMallocDefault) != hipSuccess) {
+    d->ed_h_count = nullptr;
+    return GV_ENOMEM;
+  }
+  CK(gvk_ed_group((uint32_t)n, pub, table, (uint32_t)T, rep, uid, count, (uint32_t)capU, kpub32, slot, st));
+  CK(hipMemcpyAsync(d->ed_h_count, count, 4, hipMemcpyDeviceToHost, st));
+  CK(hipStreamSynchronize(st));
+  const size_t U = *d->ed_h_count;
+  if (U == 0 || U > capU || U * (size_t)gc.div > n) return GV_OK;
+  int rc = ensure_edg(d, U);
+  if (rc) return rc == GV_ENOMEM ? GV_OK : rc;
+  CK(gvk_ed_keys(kpub32, (uint32_t)U, 0u, d->edg_ktab, d->edg_kpub, d->edg_kok, st));
+  if (gc.sorted) CK(gvk_sort_slots(&so, (uint32_t)n, slot, (uint32_t)U, st));
+  gvk_edk b;
+  memset(&b, 0, sizeof b);
+  b.n = (uint32_t)n;
+  b.perm = gc.sorted ? so.perm : nullptr;
+  b.slot = slot;
+  b.sig64 = sig;
+  b.msg_blob = blob;
+  b.msg_off = off;
+  b.msg_len = len;
+  b.ktab = d->edg_ktab;
+  b.kpub = d->edg_kpub;
+  b.kok = d->edg_kok;
+  b.kcount = (uint32_t)U;
+  b.btab = d->edtab;
+  b.out8 = (uint8_t*)o8;
+  CK(gvk_ed_keyed(&b, st));
+  CK(gvk_ed_pack_bits((uint32_t)n, (const uint8_t*)o8, bits, st));
+  d->ed_grouped_batches++;
+  d->ed_grouped_keys += U;
+  *taken = true;
+  return GV_OK;
+}
+
 int ed_launch(bool timed, Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig, const uint8_t* blob,
-              const uint64_t* off, const uint32_t* len, uint64_t* bits, hipStream_t st) {
+              const uint64_t* off, const uint32_t* len, uint64_t* bits, hipStream_t st, const EdGroupCfg& gc) {
   const size_t C = round_up(n, 256);
   int rc = ed_ensure(d, C, st);
   if (rc) return rc;
@@ -490,7 +582,9 @@ int ed_launch(bool timed, Dev* d, size_t n, const uint8_t* pub, const uint8_t* s
       if (!rs[i]) CK(hipEventCreate(&rs[i]));
     for (int i = 0; i < 5; ++i) CK(hipEventRecord(rs[i], st));
   }
-  CK(gvk_ed_verify(&b, st));
+  bool grouped = false;
+  if (gc.on && n >= gc.min && (rc = ed_grouped(d, n, pub, sig, blob, off, len, bits, st, gc, &grouped))) return rc;
+  if (!grouped) CK(gvk_ed_verify(&b, st));
   if (rs) {
     CK(hipEventRecord(rs[5], st));
     d->last = d->ring_next;
@@ -543,11 +637,20 @@ struct gv_ctx {
   std::atomic<uint64_t> ed_keys_gen{0};
   std::mutex ed_keys_mu;
   std::vector<uint8_t> ed_kpub;  // the raw keys per slot (large keyed batches run the throughput kernels on them)
+  bool ed_group = true;          // ed25519 throughput batches: in-batch key grouping + k_ed_keyed (GV_ED_GROUP=0: A/B)
+  size_t ed_group_min = 393216;  // ... from this many items (k_ed_keys is ~2 ms of one-lane chains whatever the key
+                                 // count up to ~65k keys; the keyed kernel saves ~6.4 ns per item)
+  int ed_group_div = 16;         // ... with at most items / ed_group_div distinct keys
+  size_t ed_group_cap = 16384;   // ... and at most this many (72 KB of comb table per key)
   bool ed_keyed = true;          // keyed ed25519 batches past ed_lat_max on k_ed_keyed (GV_ED_KEYED=0: the throughput kernels)
   size_t ed_lat_max = 2048;      // keyed ed25519 batches up to this size take k_ed_lat_sl (one signature per block)
 };
 
 namespace {
+
+EdGroupCfg ed_group_cfg(const gv_ctx* ctx) {
+  return EdGroupCfg{ctx->ed_group, ctx->ed_group_min, ctx->ed_group_div, ctx->ed_group_cap, ctx->sort_keys};
+}
 
 // The 20-bit-window tables of 2^35 G, 2^70 G, 2^100 G (and lambda images)
 // the 4-group keyed ladder reads (k_ecmult_k4): built on first use, 192 MiB.
@@ -1205,7 +1308,7 @@ int ed_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const EdHost& hb) {
     if (nb) CK(hipMemcpyAsync(d->ed.d_blob, d->ed.h_blob, nb, hipMemcpyHostToDevice, st));
     const uint8_t* din = d->ed.d_in;
     rc = ed_launch(ctx->time_kernels, d, cn, din, din + L.sig, d->ed.d_blob, (const uint64_t*)(din + L.off),
-                   (const uint32_t*)(din + L.len), d->ed.bits, st);
+                   (const uint32_t*)(din + L.len), d->ed.bits, st, ed_group_cfg(ctx));
     if (rc) return rc;
     CK(hipMemcpyAsync(d->ed.h_bits, d->ed.bits, ((cn + 63) / 64) * 8, hipMemcpyDeviceToHost, st));
     CK(hipStreamSynchronize(st));
@@ -1319,6 +1422,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* ks = getenv("GV_KEYS_SCRATCH")) ctx->keys_scratch = strcmp(ks, "0") != 0;
   if (const char* sk = getenv("GV_SORT_KEYS")) ctx->sort_keys = strcmp(sk, "0") != 0;
   if (const char* ek = getenv("GV_ED_KEYED")) ctx->ed_keyed = strcmp(ek, "0") != 0;
+  if (const char* eg = getenv("GV_ED_GROUP")) ctx->ed_group = strcmp(eg, "0") != 0;
   if (const char* ls = getenv("GV_LAT_SLICED")) ctx->lat_sliced = strcmp(ls, "0") != 0;
   if (const char* zc = getenv("GV_LAT_ZC")) ctx->lat_zero_copy = strcmp(zc, "0") != 0;
   if (const char* pl = getenv("GV_PIPELINE")) ctx->pipeline_dev = strcmp(pl, "0") != 0;
@@ -1387,6 +1491,8 @@ void gv_close(gv_ctx* ctx) {
     if (d->ed.last) (void)hipEventDestroy(d->ed.last);
     for (uint32_t* p : {d->ektab, d->ekpub, d->ekok}) if (p) (void)hipFree(p);
     if (d->edl_h) (void)hipHostFree(d->edl_h);
+    for (uint32_t* q : {d->edg_ktab, d->edg_kpub, d->edg_kok}) if (q) (void)hipFree(q);
+    if (d->ed_h_count) (void)hipHostFree(d->ed_h_count);
     for (int k = 0; k < 2; ++k) {
       if (d->edk_h[k]) (void)hipHostFree(d->edk_h[k]);
       if (d->edk_d[k]) (void)hipFree(d->edk_d[k]);
@@ -1492,7 +1598,7 @@ int gv_dev_verify_ed25519_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* 
   hipStream_t st = stream ? (hipStream_t)stream : d->set[0].st;
   order_after_pipeline(d, st);
   return ed_launch(ctx->time_kernels, d, n, (const uint8_t*)d_pub32, (const uint8_t*)d_sig64, (const uint8_t*)d_msg_blob,
-                   (const uint64_t*)d_msg_off, (const uint32_t*)d_msg_len, (uint64_t*)d_bits, st);
+                   (const uint64_t*)d_msg_off, (const uint32_t*)d_msg_len, (uint64_t*)d_bits, st, ed_group_cfg(ctx));
 }
 
 // ---- key arena
@@ -1837,8 +1943,8 @@ int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys)
   if (!ctx || dev_slot < 0 || dev_slot >= (int)ctx->devs.size()) return GV_EINVAL;
   Dev* d = ctx->devs[dev_slot];
   std::lock_guard<std::mutex> lk(d->mu);
-  if (batches) *batches = d->grouped_batches;
-  if (keys) *keys = d->grouped_keys;
+  if (batches) *batches = d->grouped_batches + d->ed_grouped_batches;
+  if (keys) *keys = d->grouped_keys + d->ed_grouped_keys;
   return GV_OK;
 }
 
@@ -1951,6 +2057,12 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "group_div")) {
     if (val < 2 || val > 1024) return GV_EINVAL;
     ctx->group_div = (int)val;
+  } else if (!strcmp(key, "ed_group")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->ed_group = val != 0;
+  } else if (!strcmp(key, "ed_group_min")) {
+    if (val < 256 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
+    ctx->ed_group_min = (size_t)val;
   } else if (!strcmp(key, "ed_keyed")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->ed_keyed = val != 0;

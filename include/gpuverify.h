@@ -235,6 +235,11 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * items / "group_div" (default 5) parses each distinct key once -- grouped
  * on the device, tables built into a per-batch arena, the items verified by
  * the keyed pipeline; same verdicts; default 1, env GV_GROUP_KEYS),
+ * "ed_group" (0/1: ed25519 throughput batches -- gv_verify_ed25519_msgs and
+ * the device-resident variant -- of at least "ed_group_min" items (default
+ * 393216) with at most items / 16 (and 16384) distinct keys build each key's
+ * comb table once (k_ed_keys into a per-batch arena) and verify on k_ed_keyed,
+ * lanes in slot order; same verdicts; default 1, env GV_ED_GROUP),
  * "ed_keyed" (0/1: gv_verify_ed25519_msgs_keyed batches past "ed_lat_max"
  * run one signature per lane against the cached comb tables of -A -- 64
  * table adds for [h](-A), no doublings, lanes in slot order; 0 = the
@@ -278,9 +283,9 @@ int gv_last_slices(gv_ctx* ctx, double* ms_out, size_t* n_out, int cap);
  * The Go shim packs its batches into these buffers. */
 int gv_host_alloc(gv_ctx* ctx, size_t bytes, void** out);
 int gv_host_free(gv_ctx* ctx, void* p);
-/* In-batch key grouping (option "group_keys"): on dev_slot, the number of
- * batches that took the grouped (keyed) pipeline and the distinct keys whose
- * tables they built. */
+/* In-batch key grouping (options "group_keys", "ed_group"): on dev_slot, the
+ * number of batches -- secp256k1 and ed25519 -- that took the grouped (keyed)
+ * pipeline and the distinct keys whose tables they built. */
 int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys);
 
 const char* gv_strerror(int code);

@@ -159,3 +159,60 @@ def test_two_device_slots_split_ed25519():
         assert np.array_equal(v.verify_batch_ed25519(pub, sig, msgs).astype(bool), np.array(want))
     finally:
         v.close()
+
+
+def test_in_batch_key_grouping_matches_throughput_kernels(ver):
+    """ed_group: a batch repeating few keys builds each key's comb table once
+    (k_ed_keys) and verifies on k_ed_keyed; every golden vector (keys that
+    FromBytes rejects, small-order keys, S >= L, non-canonical R ...) tiled
+    and shuffled with random OpenSSL items must give the throughput kernels'
+    verdicts, host and device-resident, both lane orders."""
+    gv = golden()
+    rng = random.Random(0x6E)
+    seeds = [rng.randbytes(32) for _ in range(24)]
+    pubs = [OSSL.public_key(s) for s in seeds]
+    items, want = [], []
+    for i in range(1200):
+        msg = rng.randbytes(rng.randrange(0, 300))
+        sig = OSSL.sign(seeds[i % 24], msg)
+        if i % 7 == 0:
+            sig = sig[:5] + bytes([sig[5] ^ 4]) + sig[6:]
+        items.append((pubs[i % 24], msg, sig))
+        want.append(i % 7 != 0)
+    items += [(p, m, s) for _, p, m, s, _ in gv]
+    want += [ok for *_, ok in gv]
+    reps = 20
+    order = np.random.default_rng(9).permutation(reps * len(items))
+    items = [items[i % len(items)] for i in order]
+    want = np.array([want[i % len(want)] for i in order])
+    pub, sig, msgs = arrays(items)
+    blob, off, ln = gvm.pack_msgs(msgs)
+    n = len(items)
+    ver.set_option("ed_group_min", 4096)
+    try:
+        runs = {}
+        for grp, srt in ((1, 1), (1, 0), (0, 1)):
+            ver.set_option("ed_group", grp)
+            ver.set_option("sort_keys", srt)
+            b0, _ = ver.group_stats()
+            host = ver.verify_batch_ed25519(pub, sig, (blob, off, ln))
+            d = [ver.dev_alloc(a.nbytes) for a in (pub, sig, blob, off, ln)]
+            for ptr, a in zip(d, (pub, sig, blob, off, ln)):
+                ver.dev_upload(ptr, np.ascontiguousarray(a))
+            d_bits = ver.dev_alloc(((n + 63) // 64) * 8)
+            ver.dev_verify_ed25519(0, n, d[0], d[1], d[2], d[3], d[4], d_bits)
+            ver.dev_sync()
+            bits = np.zeros((n + 63) // 64, np.uint64)
+            ver.dev_download(bits, d_bits)
+            for ptr in d + [d_bits]:
+                ver.dev_free(ptr)
+            dev = np.unpackbits(bits.view(np.uint8), bitorder="little")[:n].astype(bool)
+            runs[(grp, srt)] = (host.astype(bool), dev, ver.group_stats()[0] - b0)
+    finally:
+        ver.set_option("ed_group", 1)
+        ver.set_option("sort_keys", 1)
+        ver.set_option("ed_group_min", 393216)
+    for k, (host, dev, grouped) in runs.items():
+        assert grouped == (2 if k[0] else 0), (k, grouped)
+        assert np.array_equal(host, want), (k, np.nonzero(host != want)[0][:10])
+        assert np.array_equal(dev, want), (k, np.nonzero(dev != want)[0][:10])

@@ -608,6 +608,12 @@ def c4_multisig(ver, wl, block: int = 10000, threads: int = 16, n_accounts: int 
 # 254S + 13M.
 ED_FS, ED_FM = 1520, 1585
 W_ED25519 = ED_FS * 44 + ED_FM * 72          # 181,000
+# The grouped route (ed_group: k_ed_keys once per distinct key, then
+# k_ed_keyed): per item 64 cached table adds (8M), 32 comb adds (8M), encode
+# 254S + 13M; per key FromBytes 254S + 20M, 252 doublings (4S + 3.25M avg),
+# 512 entries to cached form (1M), 448 cached adds (8M).
+W_ED_KEYED = 254 * 44 + 781 * 72             # 67,408 per item
+W_ED_KEY = 1262 * 44 + 4935 * 72             # 410,848 per distinct key
 
 
 def ed25519(ver, wl, n: int = 1_000_000, threads: int = 16, steps: int = 3, nkeys: int = 4096,
@@ -642,24 +648,37 @@ def ed25519(ver, wl, n: int = 1_000_000, threads: int = 16, steps: int = 3, nkey
     nw = (n + 63) // 64
     d_bits = ver.dev_alloc(nw * 8)
     run = lambda: ver.dev_verify_ed25519(0, n, d[0], d[1], d[2], d[3], d[4], d_bits)  # noqa: E731
-    run()
-    ver.dev_sync()
-    ver.set_option("time_kernels", 1)
-    ver.stage_stats4()
-    t = time.perf_counter()
-    for _ in range(steps):
+
+    def timed():
         run()
-    ver.dev_sync()
-    el = time.perf_counter() - t
-    cnt, ms = ver.stage_stats4()
-    ver.set_option("time_kernels", 0)
-    bits = np.zeros(nw, np.uint64)
-    ver.dev_download(bits, d_bits)
-    got = _unpack_bits(bits, n).astype(bool)
+        ver.dev_sync()
+        ver.set_option("time_kernels", 1)
+        ver.stage_stats4()
+        g0 = ver.group_stats()
+        t = time.perf_counter()
+        for _ in range(steps):
+            run()
+        ver.dev_sync()
+        el = time.perf_counter() - t
+        g1 = ver.group_stats()
+        cnt, ms = ver.stage_stats4()
+        ver.set_option("time_kernels", 0)
+        bits = np.zeros(nw, np.uint64)
+        ver.dev_download(bits, d_bits)
+        keys = (g1[1] - g0[1]) // steps if g1[0] > g0[0] else 0
+        return el, cnt, ms[3], _unpack_bits(bits, n).astype(bool), keys
+
+    el, cnt, kms, got, gkeys = timed()               # default options: the grouped route when it applies
+    ver.set_option("ed_group", 0)                    # A/B: the throughput kernels on the same batch
+    try:
+        el0, _, kms0, got0, _ = timed()
+    finally:
+        ver.set_option("ed_group", 1)
     for p in d + [d_bits]:
         ver.dev_free(p)
-    kms = ms[3]
-    achieved = n * W_ED25519 / (kms * 1e-3) if kms > 0 else 0.0
+    w_item = (W_ED_KEYED + W_ED_KEY * gkeys / n) if gkeys else W_ED25519
+    achieved = n * w_item / (kms * 1e-3) if kms > 0 else 0.0
+    achieved0 = n * W_ED25519 / (kms0 * 1e-3) if kms0 > 0 else 0.0
     m = min(cpu_sample, n)
     out = np.zeros(m, np.uint8)
     t = time.perf_counter()
@@ -671,10 +690,18 @@ def ed25519(ver, wl, n: int = 1_000_000, threads: int = 16, steps: int = 3, nkey
     keyed = ed25519_keyed_throughput(ver, pub, sig, blob, off, lens, exp)
     return {"items": n, "mean_msg_bytes": round(float(lens.mean()), 1), "value": round(n * steps / el, 1),
             "small_batches": small, "keyed_throughput": keyed,
+            "route": ("in-batch key grouping (%d keys: k_ed_keys once per key, k_ed_keyed, lanes in slot order)" % gkeys
+                      if gkeys else "throughput kernels (k_ed_prep + k_ed_ladder)"),
             "unit": "ed25519 verifies/s", "mismatches": int(np.count_nonzero(got != exp)),
             "rejects_expected": int(bad.sum()), "kernel_ms": round(kms, 4), "launches_averaged": cnt,
-            "roofline": {"kernel": "k_ed_verify", "work_per_verify": W_ED25519, "achieved_T": round(achieved / 1e12, 3),
+            "roofline": {"kernel": "k_ed_keys+k_ed_keyed" if gkeys else "k_ed_verify",
+                         "work_per_verify": round(w_item), "achieved_T": round(achieved / 1e12, 3),
                          "peak_T": round(peak / 1e12, 3), "frac": round(achieved / peak, 4) if achieved else None},
+            "throughput_kernels": {"value": round(n * steps / el0, 1), "kernel_ms": round(kms0, 4),
+                                   "mismatches": int(np.count_nonzero(got0 != exp)),
+                                   "roofline": {"kernel": "k_ed_verify", "work_per_verify": W_ED25519,
+                                                "achieved_T": round(achieved0 / 1e12, 3),
+                                                "frac": round(achieved0 / peak, 4) if achieved0 else None}},
             "cpu_openssl": {"value": round(cpu_rate, 1), "threads": threads, "sample": m, "mismatches": cpu_mism},
             "workload_gen_s": round(t_gen, 2),
             "note": "device-resident (inputs in HBM); keys = 4,096 RFC 8032 seeds round-robin; OpenSSL Ed25519 signs"}
