@@ -17,7 +17,7 @@
 #define GV_GWIN ((GV_QWIN - 1) / GV_GSTEP + 1)   // G windows at positions 0, GV_GW, ..
 #define GV_DIGIT_ROWS (GV_QWIN + 2 * GV_GWIN)    // Q: packed int16 pair per window; G: int32 per digit
 #ifndef GV_INV_M
-#define GV_INV_M 16             // signatures folded per lane by k_scalar_inv
+#define GV_INV_M 32             // signatures folded per lane by k_scalar_inv (A/B: profiles/r03/invm_ab)
 #endif
 
 static_assert(GV_GW % GV_QW == 0, "G windows must sit on Q window positions");
