@@ -72,6 +72,66 @@ __global__ __launch_bounds__(64) void k_ed_keys(const uint8_t* pub32, uint32_t n
   }
 }
 
+// The same tables in two launches, so the 448 table additions per key leave
+// the serial chain: k_ed_keys_chain (lane = key) runs FromBytes and the 252
+// doublings and parks the 64 window bases 16^w (-A) (extended coordinates,
+// 36 words each, in scratch); k_ed_keys_tab (lane = key x window) adds each
+// base to itself seven times into the table -- the same operations on the
+// same values as k_ed_keys, so the same table words.
+GV_DEV void ext_store(u32* p, const ge_ext& a) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) { p[i] = a.X.n[i]; p[9 + i] = a.Y.n[i]; p[18 + i] = a.Z.n[i]; p[27 + i] = a.T.n[i]; }
+}
+GV_DEV void ext_load(ge_ext& a, const u32* p) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) { a.X.n[i] = p[i]; a.Y.n[i] = p[9 + i]; a.Z.n[i] = p[18 + i]; a.T.n[i] = p[27 + i]; }
+}
+__global__ __launch_bounds__(64) void k_ed_keys_chain(const uint8_t* pub32, uint32_t n, uint32_t base, uint32_t* kpub,
+                                                      uint32_t* kok, uint32_t* wbase) {
+  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+  if (g >= n) return;
+  u32 pw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint8_t* p = pub32 + (size_t)g * 32 + 4 * i;
+    pw[i] = (u32)p[0] | ((u32)p[1] << 8) | ((u32)p[2] << 16) | ((u32)p[3] << 24);
+    kpub[(size_t)(base + g) * 8 + i] = pw[i];
+  }
+  ge_ext a, P;
+  const bool ok = ge_frombytes(a, pw);
+  kok[base + g] = ok ? 1u : 0u;
+  ge_neg(P, a);
+  u32* wb = wbase + (size_t)g * 64 * ED_CACHED_WORDS;
+#pragma unroll 1
+  for (int w = 0; w < 64; ++w) {
+    if (w) {
+      ge_dbl_t<false>(P, P);
+      ge_dbl_t<false>(P, P);
+      ge_dbl_t<false>(P, P);
+      ge_dbl_t<true>(P, P);
+    }
+    ext_store(wb + (size_t)w * ED_CACHED_WORDS, P);
+  }
+}
+__global__ __launch_bounds__(256) void k_ed_keys_tab(uint32_t n, uint32_t base, uint32_t* ktab, const uint32_t* wbase) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= n * 64u) return;
+  const uint32_t g = t >> 6, w = t & 63u;
+  ge_ext P;
+  ext_load(P, wbase + (size_t)t * ED_CACHED_WORDS);
+  u32* tab = ktab + (size_t)(base + g) * GV_EDK_WORDS;
+  ge_cached c1, c;
+  ge_to_cached(c1, P);
+  atab_store(tab + (size_t)(w * 8) * ED_CACHED_WORDS, 1, 0, c1);
+  ge_ext acc = P;
+#pragma unroll 1
+  for (int j = 2; j <= 8; ++j) {
+    ge_add_cached(acc, acc, c1, false);
+    ge_to_cached(c, acc);
+    atab_store(tab + (size_t)(w * 8 + j - 1) * ED_CACHED_WORDS, 1, 0, c);
+  }
+}
+
 #define EDL_MSG_LDS 2048                    // padded SHA-512 inputs up to 16 blocks take the LDS path
 
 struct EdlShared {
@@ -407,9 +467,15 @@ extern "C" hipError_t gvk_ed_keyed(const gvk_edk* b, hipStream_t st) {
 }
 
 extern "C" hipError_t gvk_ed_keys(const uint8_t* pub32, uint32_t n, uint32_t base, uint32_t* ktab, uint32_t* kpub,
-                                  uint32_t* kok, hipStream_t st) {
+                                  uint32_t* kok, uint32_t* wbase, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(gv::ed::k_ed_keys, dim3((n + 63) / 64), dim3(64), 0, st, pub32, n, base, ktab, kpub, kok);
+  if (wbase) {                              // chain + table launches (scratch: n * 64 * 36 words)
+    hipLaunchKernelGGL(gv::ed::k_ed_keys_chain, dim3((n + 63) / 64), dim3(64), 0, st, pub32, n, base, kpub, kok, wbase);
+    hipLaunchKernelGGL(gv::ed::k_ed_keys_tab, dim3((n * 64 + 255) / 256), dim3(256), 0, st, n, base, ktab,
+                       (const uint32_t*)wbase);
+  } else {
+    hipLaunchKernelGGL(gv::ed::k_ed_keys, dim3((n + 63) / 64), dim3(64), 0, st, pub32, n, base, ktab, kpub, kok);
+  }
   return hipGetLastError();
 }
 

@@ -163,8 +163,11 @@ typedef struct gvk_edl {
   const uint32_t* btab;         // GV_ED_BTAB_WORDS
   uint8_t* out8;                // n verdict bytes
 } gvk_edl;
+// wbase (may be null: one lane per key does everything): n * 64 * 36 words of
+// scratch for the window bases -- the chain and the table adds then run as
+// two launches (k_ed_keys_chain, k_ed_keys_tab), same table words.
 hipError_t gvk_ed_keys(const uint8_t* pub32, uint32_t n, uint32_t base, uint32_t* ktab, uint32_t* kpub, uint32_t* kok,
-                       hipStream_t st);
+                       uint32_t* wbase, hipStream_t st);
 hipError_t gvk_ed_lat(const gvk_edl* b, hipStream_t st);
 // Large ed25519 batches against cached keys (k_ed_keyed): one signature per
 // lane, lane g takes item perm[g] (null: g), verdict byte out8[item].

@@ -483,6 +483,7 @@ struct EdGroupCfg {
   int div;
   size_t cap;
   bool sorted;
+  bool split_keys;   // k_ed_keys_chain + k_ed_keys_tab (the table adds off the serial chain)
 };
 
 int ensure_edg(Dev* d, size_t need) {
@@ -535,7 +536,9 @@ int ed_grouped(Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig, const u
   if (U == 0 || U > capU || U * (size_t)gc.div > n) return GV_OK;
   int rc = ensure_edg(d, U);
   if (rc) return rc == GV_ENOMEM ? GV_OK : rc;
-  CK(gvk_ed_keys(kpub32, (uint32_t)U, 0u, d->edg_ktab, d->edg_kpub, d->edg_kok, st));
+  uint32_t* wb = o8 + round_up(C / 4, 64);        // window-base scratch of the split key build
+  if (!gc.split_keys || (size_t)(wb + U * 64 * 36 - q) > C * (size_t)GV_ED_ROWS) wb = nullptr;
+  CK(gvk_ed_keys(kpub32, (uint32_t)U, 0u, d->edg_ktab, d->edg_kpub, d->edg_kok, wb, st));
   if (gc.sorted) CK(gvk_sort_slots(&so, (uint32_t)n, slot, (uint32_t)U, st));
   gvk_edk b;
   memset(&b, 0, sizeof b);
@@ -642,6 +645,7 @@ struct gv_ctx {
                                  // count up to ~65k keys; the keyed kernel saves ~6.4 ns per item)
   int ed_group_div = 16;         // ... with at most items / ed_group_div distinct keys
   size_t ed_group_cap = 16384;   // ... and at most this many (72 KB of comb table per key)
+  bool ed_keys_split = true;     // ed25519 key tables: serial chain and table adds in two launches (GV_ED_KEYS_SPLIT=0: A/B)
   bool ed_keyed = true;          // keyed ed25519 batches past ed_lat_max on k_ed_keyed (GV_ED_KEYED=0: the throughput kernels)
   size_t ed_lat_max = 2048;      // keyed ed25519 batches up to this size take k_ed_lat_sl (one signature per block)
 };
@@ -649,7 +653,8 @@ struct gv_ctx {
 namespace {
 
 EdGroupCfg ed_group_cfg(const gv_ctx* ctx) {
-  return EdGroupCfg{ctx->ed_group, ctx->ed_group_min, ctx->ed_group_div, ctx->ed_group_cap, ctx->sort_keys};
+  return EdGroupCfg{ctx->ed_group, ctx->ed_group_min, ctx->ed_group_div, ctx->ed_group_cap, ctx->sort_keys,
+                    ctx->ed_keys_split};
 }
 
 // The 20-bit-window tables of 2^35 G, 2^70 G, 2^100 G (and lambda images)
@@ -1423,6 +1428,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* sk = getenv("GV_SORT_KEYS")) ctx->sort_keys = strcmp(sk, "0") != 0;
   if (const char* ek = getenv("GV_ED_KEYED")) ctx->ed_keyed = strcmp(ek, "0") != 0;
   if (const char* eg = getenv("GV_ED_GROUP")) ctx->ed_group = strcmp(eg, "0") != 0;
+  if (const char* es = getenv("GV_ED_KEYS_SPLIT")) ctx->ed_keys_split = strcmp(es, "0") != 0;
   if (const char* ls = getenv("GV_LAT_SLICED")) ctx->lat_sliced = strcmp(ls, "0") != 0;
   if (const char* zc = getenv("GV_LAT_ZC")) ctx->lat_zero_copy = strcmp(zc, "0") != 0;
   if (const char* pl = getenv("GV_PIPELINE")) ctx->pipeline_dev = strcmp(pl, "0") != 0;
@@ -1702,9 +1708,12 @@ int gv_ed_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub32, uint32_t* slot_
     int rc = ensure_ed_keys(d, base + n, base, st);
     if (rc) return rc;
     uint8_t* dp = nullptr;
-    if (hipMalloc(&dp, n * 32) != hipSuccess) return GV_ENOMEM;
+    const size_t o_wb = round_up(n * 32, 256), wb_bytes = n * 64 * 36 * 4;
+    const bool split = ctx->ed_keys_split && wb_bytes <= ((size_t)1 << 30);
+    if (hipMalloc(&dp, o_wb + (split ? wb_bytes : 0)) != hipSuccess) return GV_ENOMEM;
     if (hipMemcpyAsync(dp, pub32, n * 32, hipMemcpyHostToDevice, st) != hipSuccess ||
-        gvk_ed_keys(dp, (uint32_t)n, (uint32_t)base, d->ektab, d->ekpub, d->ekok, st) != hipSuccess ||
+        gvk_ed_keys(dp, (uint32_t)n, (uint32_t)base, d->ektab, d->ekpub, d->ekok,
+                    split ? (uint32_t*)(dp + o_wb) : nullptr, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess) {
       (void)hipFree(dp);
       return GV_EHIP;
@@ -2057,6 +2066,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "group_div")) {
     if (val < 2 || val > 1024) return GV_EINVAL;
     ctx->group_div = (int)val;
+  } else if (!strcmp(key, "ed_keys_split")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->ed_keys_split = val != 0;
   } else if (!strcmp(key, "ed_group")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->ed_group = val != 0;

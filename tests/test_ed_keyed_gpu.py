@@ -190,3 +190,32 @@ def test_large_keyed_batches_schedules_agree(ver):
     for k, got in runs.items():
         bad = np.nonzero(got.astype(bool) != exp)[0]
         assert bad.size == 0, (k, [(items[i][0], bool(exp[i])) for i in bad[:10]])
+
+
+def test_split_key_build_same_verdicts(ver):
+    """gv_ed_keys_load with the key chain and the table additions in two
+    launches (ed_keys_split, default) and in one serial lane per key: the
+    golden vectors (keys FromBytes rejects included) and random validator-set
+    items verify identically, on the sliced and the per-lane keyed kernels."""
+    gv = golden()
+    rng = random.Random(0x5B)
+    seeds = [rng.randbytes(32) for _ in range(40)]
+    pubs = [OSSL.public_key(s) for s in seeds]
+    items, want = random_items(rng, seeds, pubs, 3000)
+    res = {}
+    try:
+        for split in (1, 0):
+            ver.set_option("ed_keys_split", split)
+            ver.ed_keys_reset()
+            slots = load_keys(ver, [p for _, p, _, _, _ in gv] + pubs)
+            gs, rs = slots[:len(gv)], slots[len(gv):]
+            g = ver.verify_batch_ed25519_keyed(gs, sigs([s for *_, s, _ in gv]), [m for _, _, m, _, _ in gv])
+            r = ver.verify_batch_ed25519_keyed(rs[[k for k, _, _ in items]], sigs([s for *_, s in items]),
+                                               [m for _, m, _ in items])
+            res[split] = (g.astype(bool), r.astype(bool))
+    finally:
+        ver.set_option("ed_keys_split", 1)
+    exp = np.array([ok for *_, ok in gv])
+    for split, (g, r) in res.items():
+        assert np.array_equal(g, exp), (split, np.nonzero(g != exp)[0][:10])
+        assert np.array_equal(r, want), (split, np.nonzero(r != want)[0][:10])
