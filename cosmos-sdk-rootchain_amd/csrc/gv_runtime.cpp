@@ -641,8 +641,9 @@ struct gv_ctx {
   std::mutex ed_keys_mu;
   std::vector<uint8_t> ed_kpub;  // the raw keys per slot (large keyed batches run the throughput kernels on them)
   bool ed_group = true;          // ed25519 throughput batches: in-batch key grouping + k_ed_keyed (GV_ED_GROUP=0: A/B)
-  size_t ed_group_min = 393216;  // ... from this many items (k_ed_keys is ~2 ms of one-lane chains whatever the key
-                                 // count up to ~65k keys; the keyed kernel saves ~6.4 ns per item)
+  size_t ed_group_min = 196608;  // ... from this many items (the key build's chain is ~1 ms of one-lane chains whatever
+                                 // the key count up to ~65k keys; the keyed kernel saves ~6.4 ns per item; host
+                                 // chunks of 262,144 qualify)
   int ed_group_div = 16;         // ... with at most items / ed_group_div distinct keys
   size_t ed_group_cap = 16384;   // ... and at most this many (72 KB of comb table per key)
   bool ed_keys_split = true;     // ed25519 key tables: serial chain and table adds in two launches (GV_ED_KEYS_SPLIT=0: A/B)

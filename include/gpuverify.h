@@ -237,7 +237,7 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * the keyed pipeline; same verdicts; default 1, env GV_GROUP_KEYS),
  * "ed_group" (0/1: ed25519 throughput batches -- gv_verify_ed25519_msgs and
  * the device-resident variant -- of at least "ed_group_min" items (default
- * 393216) with at most items / 16 (and 16384) distinct keys build each key's
+ * 196608; host chunks of 262,144 qualify) with at most items / 16 (and 16384) distinct keys build each key's
  * comb table once (k_ed_keys into a per-batch arena) and verify on k_ed_keyed,
  * lanes in slot order; same verdicts; default 1, env GV_ED_GROUP),
  * "ed_keyed" (0/1: gv_verify_ed25519_msgs_keyed batches past "ed_lat_max"

@@ -211,7 +211,7 @@ def test_in_batch_key_grouping_matches_throughput_kernels(ver):
     finally:
         ver.set_option("ed_group", 1)
         ver.set_option("sort_keys", 1)
-        ver.set_option("ed_group_min", 393216)
+        ver.set_option("ed_group_min", 196608)
     for k, (host, dev, grouped) in runs.items():
         assert grouped == (2 if k[0] else 0), (k, grouped)
         assert np.array_equal(host, want), (k, np.nonzero(host != want)[0][:10])
