@@ -36,30 +36,64 @@ sys.path.insert(0, REPO)
 
 import gpuverify as gvm  # noqa: E402
 
-# Algorithmic work per verify, in 32x32->64-bit multiply
-# products (field mul = 64 + 8 = 72, field square = 36 + 8 = 44, mod-n
-# Montgomery product = 136), attributed to the kernel that does it:
+# Work per verify W, in 32x32->64-bit multiply products of
+# the 8 x 32 layout (field mul = 64 + 8 = 72, field square = 36 + 8 = 44,
+# mod-n Montgomery product = 136), counted from each kernel's own operations
+# and attributed to the kernel that does them:
 FM, FS, NM = 72, 44, 136
-W_DECOMP = 255 * FS + 14 * FM              # sqrt chain (btcec decompressPoint)      12,228
-W_QTAB = 107 * FM + 44 * FS                # Q table: 1 dbl + 7 adds + affine conv.   9,640
-W_LADDER = 129 * (2 * FM + 5 * FS) + 72 * (7 * FM + 4 * FS) + (2 * FM + FS)   # dbl + adds + final 96,104
-W_INV = 4 * NM                             # s^-1 by batch inversion (~3 products/item + the shared chain)
-W_SCALAR = 6 * NM + 1700                   # u1, u2, Montgomery conversions, GLV split
+# field operations of the kernels' group law (csrc/secp_group29x.cuh,
+# secp_group29.cuh): Jacobian doubling 3M + 4S; mixed addition of a table
+# entry scaled by az (gej29x_add_scaled) 8M + 3S; a G entry's lift az = Z zq
+# 1M; a lambda-Q entry's beta x 1M; final check (ecmult_finish) Z zq, its
+# square and r Z^2: 2M + 1S.  The first addition of a ladder takes the entry
+# (no products); a zero digit skips its addition.
+DBL, MADD, LIFT, BETA, FINISH = 3 * FM + 4 * FS, 8 * FM + 3 * FS, FM, FM, 2 * FM + FS
+
+
+def w_ladder(ndbl: int, nq: int, ng: int, qw: int) -> float:
+    """Expected products of one ladder: ndbl doublings, nq Q-type additions (half
+    of them lambda-Q, each with a beta multiply; a qw-bit Booth digit is zero
+    with probability 2 / 2^(qw+1)), ng lifted G additions, the final check."""
+    q = nq * (1 - 2.0 / 2 ** (qw + 1))
+    return ndbl * DBL + (q - 1) * MADD + (q / 2) * BETA + ng * (MADD + LIFT) + FINISH
+
+
+W_DECOMP = 255 * FS + 15 * FM              # ParsePubKey: x^3 + 7, the (p+1)/4 chain, y^2 check   12,300
+# per-item Q table (build_q_table): co-Z doubling 1M + 5S, 14 co-Z additions
+# 5M + 2S, back-propagation 15 x (3M + 1S) + 13 ratio products, Z 1M
+W_QTAB = (1 + 14 * 5 + 15 * 3 + 13 + 1) * FM + (5 + 14 * 2 + 15) * FS
+W_LADDER = w_ladder(125, 52, 14, 5)        # per-item k_ecmult: 125 doublings, 5-bit Q, 20-bit G windows
+# k_scalar_inv: per item to_mont + the running product (forward), 2 products
+# (backward); per lane (32 items) the wave scans (12 + 2 products) and the
+# shared inversion (sc29_inv: ~256 squarings + ~84 products), which every
+# lane executes
+W_INV = (4 + (14 + 340) / 32) * NM
+# k_prep's scalar work: u1 = e w, u2 = r w (2 Montgomery products) and two
+# GLV splits (2 x 256x256 rounding products + 68 for c1 B1, c2 A1, c1 A1, c2 A2)
+W_SCALAR = 2 * NM + 2 * (2 * 64 + 68)
 W_KERNEL = {"k_scalar_inv": W_INV,
             "k_prep": W_DECOMP + W_QTAB + W_SCALAR,
             "k_ecmult": W_LADDER}
-W_MUL = sum(W_KERNEL.values())             # 121,032 ~ the survey's 1.2e5
+W_MUL = sum(W_KERNEL.values())
 # In-batch key grouping (gv_set_option "group_keys", the default for pub33
 # batches with few distinct keys): each distinct key's tables are built once
-# (k_keys_chain + k_keys_tables: decompress, 100 doublings to 2^35 Q /
-# 2^70 Q / 2^100 Q, four tables built straight from Jacobian coordinates, each
-# back-propagated onto the product of the four table Zs -- the running Z
-# product, rho and the last entry cost 20 products per table, no inversion)
-# and the items run the keyed pipeline (u1/u2 in k_prep<true>, the
-# 30-doubling k_ecmult_k4).
-W_KEYBUILD = (W_DECOMP + 4 * W_QTAB + 100 * (2 * FM + 5 * FS) + 3 * FM +
-              4 * (20 * FM + FS))                                              # per distinct key
-W_LADDER_K4 = W_LADDER - 95 * (2 * FM + 5 * FS)                                # 30 doublings: 61,524
+# (k_keys_chain: ParsePubKey + the doublings to the last group offset;
+# k_keys_tables, per group of NT entries: co-Z doubling 1M + 5S, NT - 2 co-Z
+# additions with the running Z product 6M + 2S, rho and the last entry
+# 6M + 1S, back-propagation (NT - 1)(3M + 1S) + (NT - 2) ratio products; the
+# three parked group Zs 1M each) and the items run the keyed pipeline.
+
+
+def w_keybuild(nt: int, last_offset: int) -> float:
+    grp = (1 + (nt - 2) * 6 + 6 + (nt - 1) * 3 + (nt - 2)) * FM + (5 + (nt - 2) * 2 + 1 + (nt - 1)) * FS
+    return W_DECOMP + last_offset * DBL + 4 * grp + 3 * FM
+
+
+W_KEYBUILD_K4 = w_keybuild(16, 100)        # 4 groups of 16 entries, offsets 0/35/70/100
+W_KEYBUILD_K6 = w_keybuild(32, 102)        # 4 groups of 32 entries, offsets 0/36/72/102
+W_PREP_KEYED = W_SCALAR
+W_LADDER_K4 = w_ladder(30, 52, 14, 5)      # k_ecmult_k4: 30 doublings, 52 Q (26 lambda), 14 G additions
+W_LADDER_K6 = w_ladder(30, 44, 12, 6)      # k_ecmult_k6: 30 doublings, 44 Q (22 lambda), 12 G additions
 # Peak: the highest v_mad_u64_u32 issue rate measured on MI355X
 # (tools/microbench/alu_rate.hip; profiles/r01/alu_rate_v3.jsonl, dependent
 # chains at 8 waves/SIMD), lane-products per second, whole chip.  bench.py
@@ -412,6 +446,7 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
     elapsed = time.perf_counter() - t_start
     cnt_p, pipe_stages = ver.stage_stats4()
     grp0 = ver.group_stats() if hasattr(ver, "group_stats") else (0, 0)
+    routes0 = ver.route_stats() if hasattr(ver, "route_stats") else {}
     # The timed loop is pipelined (gv_set_option "pipeline_dev": call k+1's
     # front kernels run under call k's ladder), so its kernels overlap and
     # their event durations include each other.  Each kernel's own speed --
@@ -440,13 +475,17 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
     gb, gk = (ver.group_stats() if hasattr(ver, "group_stats") else (0, 0))
     grouped = gb - grp0[0] >= calib
     u_keys = (gk - grp0[1]) / max(1, gb - grp0[0]) if grouped else 0.0
+    routes1 = ver.route_stats() if hasattr(ver, "route_stats") else {}
+    k6 = grouped and routes1.get("k6", 0) - routes0.get("k6", 0) >= calib
     if grouped:
         # the key tables (k_keys_chain, k_keys_tables) run on a side stream
         # beside k_scalar_inv: that stage's time covers both
-        w = {"k_unpack+k_dedupe": 0.0, "k_scalar_inv|k_keys_chain+k_keys_tables": W_INV + W_KEYBUILD * u_keys / n,
-             "k_prep<keyed>": W_SCALAR, "k_ecmult_k4": W_LADDER_K4}
+        lad = "k_ecmult_k6" if k6 else "k_ecmult_k4"
+        wkb = W_KEYBUILD_K6 if k6 else W_KEYBUILD_K4
+        w = {"k_unpack+k_dedupe": 0.0, "k_scalar_inv|k_keys_chain+k_keys_tables": W_INV + wkb * u_keys / n,
+             "k_prep<keyed>": W_PREP_KEYED, lad: W_LADDER_K6 if k6 else W_LADDER_K4}
         kms = dict(zip(w, (unpack_ms, inv_ms, prep_ms, ecmult_ms)))
-        ladder, w_route = "k_ecmult_k4", sum(w.values())
+        ladder, w_route = lad, sum(w.values())
     else:
         w = dict(W_KERNEL)
         kms = {"k_scalar_inv": inv_ms, "k_prep": prep_ms, "k_ecmult": ecmult_ms}
@@ -477,8 +516,9 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
                    "items_per_gpu": n, "keys": args.keys, "adversarial_fraction": args.adversarial,
                    "global_batch": n * world, "parallelism": f"shard{world} (independent per-GPU shards, no collective)",
                    "route": ("in-batch key grouping: each distinct key parsed and tabulated once (k_dedupe, "
-                             "k_keys_chain + k_keys_tables), items on the keyed 30-doubling ladder" if grouped else
-                             "per-item pub33 pipeline (every item decompresses its key)"),
+                             "k_keys_chain + k_keys_tables), items on the keyed 30-doubling ladder "
+                             + ("k_ecmult_k6 (6-bit Q / 24-bit G windows)" if k6 else "k_ecmult_k4")
+                             if grouped else "per-item pub33 pipeline (every item decompresses its key)"),
                    "distinct_keys_per_batch": round(u_keys) if grouped else None},
         "roofline": {
             "bound": "valu",
@@ -524,10 +564,9 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
                                 "adversarial copy (1/8 malformed prefix, 1/8 flipped digest bit -> rejected)"},
     }
 
+    lat = None
     if rank == 0 and world == 1 and not args.no_latency:
         lat = checktx_latency(ver, pub, sig, dig, args.threads)
-        result["checktx_latency_ms"] = lat
-        result["checktx_p50_ms_64"] = lat["64"]["p50_ms"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(pub, sig, dig, args.threads, ver)
         result["cpu_baseline"] = cb
@@ -552,6 +591,11 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
         ex["ed25519"] = X.ed25519(ver, workload_lib(), n=n, threads=args.threads, peak=P_MUL)
         log(f"extras in {time.perf_counter() - t:.1f}s")
         result["extras"] = ex
+    if lat is not None:
+        # BASELINE's second number, last in the line so that a truncated tail
+        # of stdout still shows it: the full curve, then p50 @ 64
+        result["checktx_latency_ms"] = lat
+        result["checktx_p50_ms_64"] = lat["64"]["p50_ms"]
     ver.close()
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -70,6 +70,10 @@ typedef struct gvk_batch {
   // keyed batches with gtab4 set take k_ecmult_k4 (30-doubling 4-group ladder)
   const uint32_t* kqt2;         // arena group tables (2^35 Q, 2^70 Q, 2^100 Q), on the slot's kzq
   const uint32_t* gtab4;        // GV_KEY2_TABLES x (G-type, lambda) tables of 2^35 G, 2^70 G, 2^100 G
+  // k6 set: kqt / kqt2 hold 32-entry group tables (k_keys_build_rows6) and the
+  // ladder is k_ecmult_k6 over gtab6 (GV_K6_GTAB_WORDS); gtab4 unused
+  const uint32_t* gtab6;
+  int k6;
   // key-ordered lanes (gv_sort.hip; keyed k4 batches with srt.perm set): the
   // lanes run in slot order, the bits are gathered back to item order
   gvk_sort srt;
@@ -96,6 +100,23 @@ hipError_t gvk_unsort_bits(uint32_t n, const uint32_t* pos, const uint64_t* sbit
 #define GV_LAT16_SIGS 8                                   // signatures per 128-thread block: 16 lanes each
 #define GV_KEY2_TABLES (GV_LGRP - 1)
 #define GV_GLAT_WORDS (GV_LGRP * 2 * GV_QTAB_N * 16)
+
+// The grouped route's ladder (k_ecmult_k6, in-batch key grouping): the
+// per-batch key tables hold 32 multiples per group (6-bit signed windows: 22
+// per 128-bit GLV half, groups starting at windows 0, 6, 12, 17 = bit offsets
+// 0, 36, 72, 102; 6 positions, 30 doublings, 44 Q additions) and G takes
+// 24-bit windows (6 per half: 12 additions) from 2^23-entry tables of
+// 2^b G and 2^b lambda G for the four group offsets b (4 GiB per device).
+#define GV_K6_QW 6
+#define GV_K6_NT 32                                       // table entries per group
+#define GV_K6_QWIN 22
+#define GV_K6_GW 24
+#define GV_K6_GWIN 6
+#define GV_K6_GTAB_N (1 << (GV_K6_GW - 1))
+#define GV_K6_KEY_WORDS (GV_K6_NT * GV_QENT_WORDS)       // one group table (2,560 B)
+#define GV_K6_GTAB_WORDS ((size_t)GV_LGRP * 2 * GV_K6_GTAB_N * 16)
+static_assert(GV_K6_QWIN + 2 * GV_K6_GWIN <= GV_DIGIT_ROWS, "k6 digits fit the digit rows");
+static_assert(GV_K6_QW * GV_K6_QWIN >= 130 && GV_K6_GW * GV_K6_GWIN >= 130, "k6 windows cover 129-bit halves");
 
 // Small-batch latency path (gv_lat.hip): GV_LAT_SIGS signatures per block of
 // 128 threads, one fused kernel (after k_sha256 on the message path).  bits
@@ -199,6 +220,15 @@ hipError_t gvk_gen_gtable(uint32_t* gtab, hipStream_t st);
 // the keyed ladder's G tables (GV_KEY2_TABLES x 2 x GV_GTAB_N x 16 words); base_scratch: 48 words
 hipError_t gvk_gen_gtable4(uint32_t* gtab4, uint32_t* base_scratch, hipStream_t st);
 hipError_t gvk_gen_glat(uint32_t* glat, hipStream_t st);
+// the k6 ladder's G tables (GV_K6_GTAB_WORDS words); base_scratch: 64 words
+hipError_t gvk_gen_gtable6(uint32_t* gtab6, uint32_t* base_scratch, hipStream_t st);
+// k6 key tables (32 entries per group) of n keys already unpacked into rows
+// in_x / in_pfx (stride C), slots 0..n-1; qr: (GV_K6_NT - 1) * 9 ratio rows of
+// stride round_up(4 n, 256), qe (may be null): (GV_K6_NT - 1) * 18 rows of the
+// same stride.  kqt: n x GV_K6_KEY_WORDS, kqt2: 3 n x GV_K6_KEY_WORDS.
+hipError_t gvk_keys_build_rows6(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx, uint32_t* qr,
+                                uint32_t* qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok,
+                                uint32_t* kqt2, uint32_t* kzq2, hipStream_t st);
 hipError_t gvk_verify_lat(const gvk_lat* b, hipStream_t st);
 hipError_t gvk_verify_lat16(const gvk_lat* b, hipStream_t st);
 hipError_t gvk_verify_lat_sl(const gvk_lat* b, hipStream_t st);

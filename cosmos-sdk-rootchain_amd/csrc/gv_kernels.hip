@@ -86,9 +86,11 @@ GV_DEV void fe_from_const(fe& r, const u32* c) {
 // (beta*x, y).  Run once per context.
 // base: affine x || y (16 words) of the point whose multiples are tabulated,
 // or null for G itself (the keyed ladder's tables of 2^35 G, 2^70 G, 2^100 G).
+// GTN: entries per table (GV_GTAB_N; GV_K6_GTAB_N for the k6 tables).
+template <u32 GTN = GV_GTAB_N>
 __global__ void k_gen_gtable(u32* gtab, const u32* base) {
   const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= GV_GTAB_N) return;
+  if (e >= GTN) return;
   const u32 m = e + 1;
   fe gx, gy;
   if (base) {
@@ -119,7 +121,7 @@ __global__ void k_gen_gtable(u32* gtab, const u32* base) {
   fe_mul(lx, x, beta);
   fe_normalize(lx);
   u32* t0 = gtab + (size_t)e * 16;
-  u32* t1 = gtab + ((size_t)GV_GTAB_N + e) * 16;
+  u32* t1 = gtab + ((size_t)GTN + e) * 16;
 #pragma unroll
   for (int i = 0; i < 8; ++i) { t0[i] = x.v[i]; t0[8 + i] = y.v[i]; t1[i] = lx.v[i]; t1[8 + i] = y.v[i]; }
 }
@@ -302,16 +304,19 @@ GV_DEV void load_qent(fe& x, fe& y, const u32* qt, u32 g, u32 j) {
 // Q-table entries (built and read on the 9 x 29 layer) are stored as raw
 // limbs: x[9], y[9], 2 pad words = 80 bytes, five 16-byte accesses per lane;
 // no word conversion on either side.  G-table entries stay 8 x 32 words.
+// NT: entries per table row (GV_QTAB_N; GV_K6_NT for the k6 group tables).
+template <int NT = GV_QTAB_N>
 GV_DEV void store_qent29(u32* qt, u32 g, int j, const fe29& x, const fe29& y) {
-  uint4* p = (uint4*)(qt + ((size_t)g * GV_QTAB_N + j) * GV_QENT_WORDS);
+  uint4* p = (uint4*)(qt + ((size_t)g * NT + j) * GV_QENT_WORDS);
   p[0] = make_uint4(x.n[0], x.n[1], x.n[2], x.n[3]);
   p[1] = make_uint4(x.n[4], x.n[5], x.n[6], x.n[7]);
   p[2] = make_uint4(x.n[8], y.n[0], y.n[1], y.n[2]);
   p[3] = make_uint4(y.n[3], y.n[4], y.n[5], y.n[6]);
   p[4] = make_uint4(y.n[7], y.n[8], 0u, 0u);
 }
+template <int NT = GV_QTAB_N>
 GV_DEV void load_qent29(fe29& x, fe29& y, const u32* qt, u32 g, u32 j) {
-  const uint4* p = (const uint4*)(qt + ((size_t)g * GV_QTAB_N + j) * GV_QENT_WORDS);
+  const uint4* p = (const uint4*)(qt + ((size_t)g * NT + j) * GV_QENT_WORDS);
   const uint4 a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
   x.n[0] = a.x; x.n[1] = a.y; x.n[2] = a.z; x.n[3] = a.w;
   x.n[4] = b.x; x.n[5] = b.y; x.n[6] = b.z; x.n[7] = b.w;
@@ -555,7 +560,9 @@ GV_DEV bool parse_pubkey(u32 pre, const fe& x, fe& y) {
 #else
 #define GV_PREP_ATTR
 #endif
-template <bool KEYED>
+// K6 (keyed only): the digits of the k6 ladder (GV_K6_QW-bit Q windows,
+// GV_K6_GW-bit G windows) instead of GV_QW / GV_GW.
+template <bool KEYED, bool K6 = false>
 __global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u32* in_x, const u32* in_pfx,
                                                const u32* in_r, const u32* in_s, const u32* in_e,
                                                const u32* in_w, u32* digits, u32* qt, u32* zq_out,
@@ -628,20 +635,22 @@ __global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u
   // (int16 halves), win = 0..GV_QWIN-1.  G digits (GV_GW-bit windows,
   // [-2^(GV_GW-1), 2^(GV_GW-1)]) as int32: digits[(GV_QWIN + 2j)*C + g] = dG1,
   // digits[(GV_QWIN + 2j + 1)*C + g] = dG2, j = 0..GV_GWIN-1.
+  constexpr int QW = K6 ? GV_K6_QW : GV_QW, QWIN = K6 ? GV_K6_QWIN : GV_QWIN;
+  constexpr int GW = K6 ? GV_K6_GW : GV_GW, GWIN = K6 ? GV_K6_GWIN : GV_GWIN;
 #pragma unroll
-  for (int win = 0; win < GV_QWIN; ++win) {
-    int d0 = booth_digit<GV_QW>(k1q, win), d1 = booth_digit<GV_QW>(k2q, win);
+  for (int win = 0; win < QWIN; ++win) {
+    int d0 = booth_digit<QW>(k1q, win), d1 = booth_digit<QW>(k2q, win);
     if (n1q) d0 = -d0;
     if (n2q) d1 = -d1;
     digits[(size_t)win * C + g] = ((u32)d0 & 0xFFFFu) | ((u32)d1 << 16);
   }
 #pragma unroll
-  for (int j = 0; j < GV_GWIN; ++j) {
-    int d2 = booth_digit<GV_GW>(k1g, j), d3 = booth_digit<GV_GW>(k2g, j);
+  for (int j = 0; j < GWIN; ++j) {
+    int d2 = booth_digit<GW>(k1g, j), d3 = booth_digit<GW>(k2g, j);
     if (n1g) d2 = -d2;
     if (n2g) d3 = -d3;
-    digits[(size_t)(GV_QWIN + 2 * j) * C + g] = (u32)d2;
-    digits[(size_t)(GV_QWIN + 2 * j + 1) * C + g] = (u32)d3;
+    digits[(size_t)(QWIN + 2 * j) * C + g] = (u32)d2;
+    digits[(size_t)(QWIN + 2 * j + 1) * C + g] = (u32)d3;
   }
   flags[g] = (ok ? 1u : 0u) | (r_small ? 2u : 0u);
 
@@ -661,6 +670,7 @@ __global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u
 // rows of stride C.
 // Window-group start bits of the keyed latency schedule (GV_LGRP groups).
 __constant__ const int kLGrpBit[GV_LGRP] = {0, 35, 70, 100};
+__constant__ const int kK6GrpBit[GV_LGRP] = {0, 6 * GV_K6_QW, 12 * GV_K6_QW, 17 * GV_K6_QW};   // 0, 36, 72, 102
 
 // Affine x, y (8 x 32 words) of a finite Jacobian point.
 GV_DEV void gej29_to_affine_words(fe& x8, fe& y8, const gej29& p) {
@@ -682,8 +692,12 @@ GV_DEV void gej29_to_affine_words(fe& x8, fe& y8, const gej29& p) {
 // 2^35 Q, 2^70 Q, 2^100 Q.  Each group's base point is parked, as canonical
 // words x[8] y[8], in entry 0 of its own table row; the Jacobian Z of groups
 // 1..3 in their Z rows (kzq2), group 0 is affine.
+// K6: the k6 group offsets (kK6GrpBit) and 32-entry table rows.
+template <bool K6 = false>
 __global__ __launch_bounds__(256) void k_keys_chain(u32 n, u32 C, const u32* in_x, const u32* in_pfx, u32 base,
                                                      u32* kqt, u32 kC, u32* kok, u32* kqt2, u32* kzq2) {
+  constexpr int NT = K6 ? GV_K6_NT : GV_QTAB_N;
+  const int* grp_bit = K6 ? kK6GrpBit : kLGrpBit;
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n) return;                       // no cross-lane work
   fe x, y;
@@ -695,7 +709,7 @@ __global__ __launch_bounds__(256) void k_keys_chain(u32 n, u32 C, const u32* in_
   }
   kok[base + g] = ok ? 1u : 0u;
   auto park = [](u32* tab, u32 row, const u32* xw, const u32* yw) {
-    u32* p = tab + (size_t)row * GV_QTAB_N * GV_QENT_WORDS;
+    u32* p = tab + (size_t)row * NT * GV_QENT_WORDS;
 #pragma unroll
     for (int i = 0; i < 8; ++i) { p[i] = xw[i]; p[8 + i] = yw[i]; }
   };
@@ -707,7 +721,7 @@ __global__ __launch_bounds__(256) void k_keys_chain(u32 n, u32 C, const u32* in_
 #pragma unroll 1
   for (int grp = 1; grp < GV_LGRP; ++grp) {
 #pragma unroll 1
-    for (int k = kLGrpBit[grp - 1]; k < kLGrpBit[grp]; ++k) gej29_double(q, q);   // never infinite: odd order
+    for (int k = grp_bit[grp - 1]; k < grp_bit[grp]; ++k) gej29_double(q, q);   // never infinite: odd order
     u32 xw[8], yw[8];
     f29_to_words(xw, q.x);
     f29_to_words(yw, q.y);
@@ -731,6 +745,8 @@ __global__ __launch_bounds__(256) void k_keys_chain(u32 n, u32 C, const u32* in_
 // coalesced, so each table entry is written once, by the back-propagation
 // (null: the entries go through the table itself: lanes 1,280 B apart write
 // 80 B each, twice, and read them back in between).
+// NT: entries per group table (16; GV_K6_NT for the k6 tables).
+template <int NT = GV_QTAB_N>
 __global__ __launch_bounds__(256) void k_keys_tables(u32 n, u32 C4, u32 base, u32* kqt, u32* kzq, u32 kC, u32* kqt2,
                                                       u32* kzq2, u32* qr, u32* qe) {
   const u32 L = blockIdx.x * blockDim.x + threadIdx.x;
@@ -746,7 +762,7 @@ __global__ __launch_bounds__(256) void k_keys_tables(u32 n, u32 C4, u32 base, u3
         qe[((size_t)e * 18 + 9 + i) * C4 + L] = y.n[i];
       }
     } else {
-      store_qent29(tab, row, e, x, y);
+      store_qent29<NT>(tab, row, e, x, y);
     }
   };
   auto get = [&](int e, fe29& x, fe29& y) {
@@ -757,13 +773,13 @@ __global__ __launch_bounds__(256) void k_keys_tables(u32 n, u32 C4, u32 base, u3
         y.n[i] = qe[((size_t)e * 18 + 9 + i) * C4 + L];
       }
     } else {
-      load_qent29(x, y, tab, row, (u32)e);
+      load_qent29<NT>(x, y, tab, row, (u32)e);
     }
   };
   u32* zrow = grp == 0u ? kzq : kzq2 + (size_t)(grp - 1u) * 8 * kC;
   fe29 qx, qy, X1, Y1, X2, Y2, t, u, prod;
   {
-    const u32* p = tab + (size_t)row * GV_QTAB_N * GV_QENT_WORDS;
+    const u32* p = tab + (size_t)row * NT * GV_QENT_WORDS;
     u32 w[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = p[i];
@@ -797,7 +813,7 @@ __global__ __launch_bounds__(256) void k_keys_tables(u32 n, u32 C4, u32 base, u3
   put(1, X2, Y2);                           // 2*Q on Z1
   f29_add(prod, qy, qy);                    // Z1 = 2y; times every ratio below -> Z_15
 #pragma unroll 1
-  for (int m = 2; m < GV_QTAB_N; ++m) {     // (Q', mQ) -> ((m+1)Q, Q'')
+  for (int m = 2; m < NT; ++m) {            // (Q', mQ) -> ((m+1)Q, Q'')
     fe29 h, rr, c, w1, w2, d, a1;
     f29_sub_norm<1>(h, X1, X2);
     store_ratio29(qr, C4, L, m - 2, h);     // Z_m / Z_{m-1}
@@ -816,7 +832,7 @@ __global__ __launch_bounds__(256) void k_keys_tables(u32 n, u32 C4, u32 base, u3
     f29_sub_norm<1>(Y2, t, a1);
     X1 = w1;
     Y1 = a1;
-    if (m + 1 < GV_QTAB_N) put(m, X2, Y2);  // the last entry waits for rho
+    if (m + 1 < NT) put(m, X2, Y2);         // the last entry waits for rho
   }
   // E = Z_15 (times the parked Jacobian Z for groups 1..3); the quad's others
   if (grp) {
@@ -841,12 +857,12 @@ __global__ __launch_bounds__(256) void k_keys_tables(u32 n, u32 C4, u32 base, u3
     f29_mul(a3, a2, acc);
     f29_mul(X2, X2, a2);
     f29_mul(Y2, Y2, a3);
-    store_qent29(tab, row, GV_QTAB_N - 1, X2, Y2);
+    store_qent29<NT>(tab, row, NT - 1, X2, Y2);
   }
   // entry m (index m-1) on Z_{m-1} (m >= 2; entries 1, 2 on Z_1): times
   // rho * Z_15 / Z_{m-1}
 #pragma unroll 1
-  for (int m = GV_QTAB_N - 1; m >= 1; --m) {
+  for (int m = NT - 1; m >= 1; --m) {
     if (m >= 2) {
       fe29 ratio;
       load_ratio29(ratio, qr, C4, L, m - 2);
@@ -858,16 +874,19 @@ __global__ __launch_bounds__(256) void k_keys_tables(u32 n, u32 C4, u32 base, u3
     get(m - 1, x, y);
     f29_mul(x, x, a2);
     f29_mul(y, y, a3);
-    store_qent29(tab, row, m - 1, x, y);
+    store_qent29<NT>(tab, row, m - 1, x, y);
   }
   store_f29(zrow, kC, base + key, zc);
 }
 
 // Affine 2^35 G, 2^70 G, 2^100 G (16 words each) for the keyed ladder's G
 // tables; thread t = group - 1.  Once per device.
+// K6: 2^36 G, 2^72 G, 2^102 G (the k6 group offsets).
+template <bool K6 = false>
 __global__ void k_gen_gbase(u32* out) {
   const int t = threadIdx.x;
   if (t >= GV_KEY2_TABLES) return;
+  const int* grp_bit = K6 ? kK6GrpBit : kLGrpBit;
   fe gx, gy;
   fe_from_const(gx, kGx);
   fe_from_const(gy, kGy);
@@ -875,7 +894,7 @@ __global__ void k_gen_gbase(u32* out) {
   f29_from_words(p.x, gx.v);
   f29_from_words(p.y, gy.v);
   f29_set_u32(p.z, 1);
-  for (int k = 0; k < kLGrpBit[t + 1]; ++k) gej29_double(p, p);
+  for (int k = 0; k < grp_bit[t + 1]; ++k) gej29_double(p, p);
   fe x8, y8;
   gej29_to_affine_words(x8, y8, p);
 #pragma unroll
@@ -1234,6 +1253,80 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gta
   ecmult_finish(acc, inf, zq, flags, in_r, bits, n, C, g);
 }
 
+// ------------------------------------------------------------- k_ecmult_k6
+// The grouped route's ladder (gv_kernels.h GV_K6_*): the per-batch key
+// tables hold 32 multiples per group, so each 128-bit GLV half takes 22
+// six-bit windows, split into the groups [0,6), [6,12), [12,17), [17,22)
+// (bit offsets 0, 36, 72, 102); window w of group k is added at local
+// position w - w0(k) of a 36-bit ladder: 5 x 6 = 30 doublings and 44 Q
+// additions (52 with 5-bit windows).  G takes 24-bit windows (6 per half, 12
+// additions instead of 14) from the 2^23-entry tables of 2^b G and
+// 2^b lambda G, b the group offsets: G window j (bit 24 j) sits in the group
+// of the largest offset b <= 24 j at position (24 j - b) / 6.  Same
+// additions, final check and semantics as k_ecmult_k4 otherwise.
+__constant__ const int kK6WStart[4] = {0, 6, 12, 17};
+__constant__ const int kK6NWin[4] = {6, 6, 5, 5};
+// G windows at each position (up to two), their group
+__constant__ const int kK6GWin[6][2] = {{0, 3}, {-1, -1}, {2, -1}, {5, -1}, {1, 4}, {-1, -1}};
+__constant__ const int kK6GGrp[GV_K6_GWIN] = {0, 0, 1, 2, 2, 3};
+
+__global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k6(const u32* gtab6, u32 n, u32 C, const u32* digits,
+                                                        const u32* kqt, const u32* kqt2, const u32* kzq,
+                                                        const u32* flags, const u32* in_r, uint64_t* bits,
+                                                        const u32* qidx, u32 kC) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 qi = qidx[g];
+  fe29 zq;
+  load_f29(zq, kzq, kC, qi);
+  gej29 acc;
+  f29_set_zero(acc.x); f29_set_zero(acc.y); f29_set_zero(acc.z);
+  bool inf = true;
+#pragma unroll 1
+  for (int pos = 5; pos >= 0; --pos) {
+    if (pos != 5) {
+#pragma unroll 1
+      for (int d = 0; d < GV_K6_QW; ++d) gej29x_double(acc, acc);
+    }
+    // slots 0..7: (group, Q / lambda Q); 8..11: up to two G windows x (G, lambda G)
+#pragma unroll 1
+    for (int slot = 0; slot < 12; ++slot) {
+      int d;
+      const u32* tab;
+      u32 row = 0;
+      const bool isg = slot >= 8;
+      if (!isg) {
+        const int grp = slot >> 1;
+        if (pos >= kK6NWin[grp]) continue;                 // wave-uniform
+        const u32 dq = digits[(size_t)(kK6WStart[grp] + pos) * C + g];
+        d = (slot & 1) ? ((int)dq >> 16) : ((int)(dq << 16) >> 16);
+        tab = grp == 0 ? kqt : kqt2;
+        row = grp == 0 ? qi : qi * GV_KEY2_TABLES + (grp - 1);
+      } else {
+        const int j = kK6GWin[pos][(slot - 8) >> 1];
+        if (j < 0) continue;                               // wave-uniform
+        d = (int)digits[(size_t)(GV_K6_QWIN + 2 * j + (slot & 1)) * C + g];
+        tab = gtab6 + ((size_t)kK6GGrp[j] * 2 + (slot & 1)) * GV_K6_GTAB_N * 16;
+      }
+      if (d == 0) continue;
+      const u32 e = (u32)((d < 0 ? -d : d) - 1);
+      fe29 x, y;
+      if (!isg) {
+        load_qent29<GV_K6_NT>(x, y, tab, row, e);
+        if (slot & 1) {                                    // lambda * P = (beta * x, y)
+          fe29 beta;
+          f29_from_const(beta, kBeta);
+          f29x_mul(x, x, beta);
+        }
+      } else {
+        load_gent29(x, y, tab, e);
+      }
+      if (d < 0) f29_neg<1>(y, y);                         // 2
+      add_entry(acc, inf, x, y, isg ? &zq : nullptr);
+    }
+  }
+  ecmult_finish(acc, inf, zq, flags, in_r, bits, n, C, g);
+}
+
 // ------------------------------------------------------------------- k_debug
 // Test hook (gv_debug_op in the C-ABI): exercises one building block per lane
 // so the GPU tests can pin field/scalar/GLV arithmetic against the oracle.
@@ -1338,16 +1431,25 @@ __global__ void k_debug(int op, u32 n, const u32* in, u32* out) {
 extern "C" {
 
 hipError_t gvk_gen_gtable(uint32_t* gtab, hipStream_t st) {
-  hipLaunchKernelGGL(gv::k_gen_gtable, dim3((GV_GTAB_N + 63) / 64), dim3(64), 0, st, gtab,
+  hipLaunchKernelGGL(gv::k_gen_gtable<GV_GTAB_N>, dim3((GV_GTAB_N + 63) / 64), dim3(64), 0, st, gtab,
                      (const uint32_t*)nullptr);
   return hipGetLastError();
 }
 
 hipError_t gvk_gen_gtable4(uint32_t* gtab4, uint32_t* base_scratch, hipStream_t st) {
-  hipLaunchKernelGGL(gv::k_gen_gbase, dim3(1), dim3(64), 0, st, base_scratch);
+  hipLaunchKernelGGL(gv::k_gen_gbase<false>, dim3(1), dim3(64), 0, st, base_scratch);
   for (int k = 0; k < GV_KEY2_TABLES; ++k)
-    hipLaunchKernelGGL(gv::k_gen_gtable, dim3((GV_GTAB_N + 63) / 64), dim3(64), 0, st,
+    hipLaunchKernelGGL(gv::k_gen_gtable<GV_GTAB_N>, dim3((GV_GTAB_N + 63) / 64), dim3(64), 0, st,
                        gtab4 + (size_t)k * 2 * GV_GTAB_N * 16, (const uint32_t*)(base_scratch + 16 * k));
+  return hipGetLastError();
+}
+
+hipError_t gvk_gen_gtable6(uint32_t* gtab6, uint32_t* base_scratch, hipStream_t st) {
+  hipLaunchKernelGGL(gv::k_gen_gbase<true>, dim3(1), dim3(64), 0, st, base_scratch);
+  const dim3 grd((GV_K6_GTAB_N + 255) / 256), blk(256);
+  for (int k = 0; k < GV_LGRP; ++k)
+    hipLaunchKernelGGL(gv::k_gen_gtable<GV_K6_GTAB_N>, grd, blk, 0, st, gtab6 + (size_t)k * 2 * GV_K6_GTAB_N * 16,
+                       k == 0 ? (const uint32_t*)nullptr : (const uint32_t*)(base_scratch + 16 * (k - 1)));
   return hipGetLastError();
 }
 
@@ -1355,7 +1457,8 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   const uint32_t C = b->C;
   const dim3 blk(256), grd(C / 256);
   // key-ordered lanes (gv_sort.hip): keyed k4 batches with sort scratch
-  const bool sorted = b->kslot && b->gtab4 && b->srt.perm;
+  const bool k6 = b->kslot && b->k6 && b->gtab6;
+  const bool sorted = b->kslot && (b->gtab4 || k6) && b->srt.perm;
   const uint32_t* perm = sorted ? b->srt.perm : nullptr;
   if (sorted) {
     hipError_t e = gvk_sort_slots(&b->srt, b->n, b->kslot, b->kcount, st);
@@ -1379,7 +1482,12 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
     hipLaunchKernelGGL(gv::k_scalar_inv, dim3((waves + 3) / 4), blk, 0, st, C, b->in_s, w, pre);
     if (b->keys_ready) (void)hipStreamWaitEvent(st, b->keys_ready, 0);   // grouped keys built beside s^-1
     if (b->ev[1]) (void)hipEventRecord(b->ev[1], st);
-    if (b->kslot)   // keyed: in_pfx doubles as the clamped-slot row for k_ecmult
+    if (k6)
+      hipLaunchKernelGGL((gv::k_prep<true, true>), grd, blk, 0, st, C, b->n, (const uint32_t*)nullptr,
+                         (const uint32_t*)nullptr, b->in_r, b->in_s, b->in_e, (const uint32_t*)w, b->digits,
+                         (uint32_t*)nullptr, (uint32_t*)nullptr, b->flags, sorted ? b->srt.kslot : b->kslot,
+                         b->kok, b->kcount, b->in_pfx);
+    else if (b->kslot)   // keyed: in_pfx doubles as the clamped-slot row for k_ecmult
       hipLaunchKernelGGL(gv::k_prep<true>, grd, blk, 0, st, C, b->n, (const uint32_t*)nullptr,
                          (const uint32_t*)nullptr, b->in_r, b->in_s, b->in_e, (const uint32_t*)w, b->digits,
                          (uint32_t*)nullptr, (uint32_t*)nullptr, b->flags, sorted ? b->srt.kslot : b->kslot,
@@ -1397,7 +1505,10 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
     se = b->st_ecm;
   }
   if (b->ev_ecm_start) (void)hipEventRecord(b->ev_ecm_start, se);
-  if (b->kslot && b->gtab4)
+  if (k6)
+    hipLaunchKernelGGL(gv::k_ecmult_k6, grd, blk, 0, se, b->gtab6, b->n, C, b->digits, b->kqt, b->kqt2, b->kzq,
+                       b->flags, b->in_r, sorted ? b->srt.bits : b->bits, (const uint32_t*)b->in_pfx, b->kC);
+  else if (b->kslot && b->gtab4)
     hipLaunchKernelGGL(gv::k_ecmult_k4, grd, blk, 0, se, b->gtab, b->gtab4, b->n, C, b->digits, b->kqt, b->kqt2,
                        b->kzq, b->flags, b->in_r, sorted ? b->srt.bits : b->bits, (const uint32_t*)b->in_pfx,
                        b->kC);
@@ -1425,10 +1536,22 @@ static hipError_t keys_tables_launch(uint32_t n, uint32_t C, const uint32_t* in_
                                      uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const uint32_t C4 = (4u * n + 255u) / 256u * 256u;
-  hipLaunchKernelGGL(gv::k_keys_chain, dim3((n + 255) / 256), dim3(256), 0, st, n, C, in_x, in_pfx, base, kqt, kC,
-                     kok, kqt2, kzq2);
-  hipLaunchKernelGGL(gv::k_keys_tables, dim3(C4 / 256), dim3(256), 0, st, n, C4, base, kqt, kzq, kC, kqt2, kzq2, qr,
-                     qe);
+  hipLaunchKernelGGL(gv::k_keys_chain<false>, dim3((n + 255) / 256), dim3(256), 0, st, n, C, in_x, in_pfx, base, kqt,
+                     kC, kok, kqt2, kzq2);
+  hipLaunchKernelGGL(gv::k_keys_tables<GV_QTAB_N>, dim3(C4 / 256), dim3(256), 0, st, n, C4, base, kqt, kzq, kC, kqt2,
+                     kzq2, qr, qe);
+  return hipGetLastError();
+}
+
+hipError_t gvk_keys_build_rows6(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx, uint32_t* qr,
+                                uint32_t* qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok,
+                                uint32_t* kqt2, uint32_t* kzq2, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const uint32_t C4 = (4u * n + 255u) / 256u * 256u;
+  hipLaunchKernelGGL(gv::k_keys_chain<true>, dim3((n + 255) / 256), dim3(256), 0, st, n, C, in_x, in_pfx, 0u, kqt,
+                     kC, kok, kqt2, kzq2);
+  hipLaunchKernelGGL(gv::k_keys_tables<GV_K6_NT>, dim3(C4 / 256), dim3(256), 0, st, n, C4, 0u, kqt, kzq, kC, kqt2,
+                     kzq2, qr, qe);
   return hipGetLastError();
 }
 

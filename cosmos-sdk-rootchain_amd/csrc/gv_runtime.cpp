@@ -258,6 +258,7 @@ struct Set {
   // distinct keys, key-arena layout) for up to gcap keys, and the count
   uint32_t *g_kqt = nullptr, *g_kzq = nullptr, *g_kok = nullptr, *g_kqt2 = nullptr, *g_kzq2 = nullptr;
   size_t gcap = 0;
+  bool gk6 = false;                               // the arena's group tables are k6 (32 entries)
   uint32_t* h_count = nullptr;                    // pinned: the distinct-key count read back
   // pinned host staging
   uint8_t* h_in = nullptr;
@@ -299,6 +300,8 @@ struct Dev {
   uint32_t *kqt2 = nullptr, *kzq2 = nullptr;      // the keyed latency schedule's group tables (2^35 Q, ...)
   uint32_t* glat = nullptr;                       // group tables of G / lambda G (k_gen_glat)
   uint32_t* gtab4 = nullptr;                      // k_ecmult_k4's tables of 2^35 G, 2^70 G, 2^100 G (+ lambda)
+  uint32_t* gtab6 = nullptr;                      // k_ecmult_k6's 24-bit-window tables of 2^b G, 2^b lambda G (4 GiB)
+  bool gtab6_failed = false;                      // its allocation failed once: the grouped route stays on k4
   size_t kcap = 0;
   // ring of per-launch stage events for gv_stage_stats
   static constexpr int kRing = 256;
@@ -350,6 +353,7 @@ struct Dev {
   hipEvent_t plain_done = nullptr;                // the last non-pipelined call on the context stream
   bool hi_used = false, plain_used = false;
   uint64_t grouped_batches = 0, grouped_keys = 0;  // in-batch key grouping taken (gv_group_stats)
+  uint64_t routes[GV_ROUTES] = {};                // batches per schedule (gv_route_stats)
   int flip = 0;
   double last_slice_ms = 0;                       // host-buffer calls: this device's slice, wall time
   size_t last_slice_n = 0;
@@ -625,6 +629,7 @@ struct gv_ctx {
                                 // verdict bytes to pinned memory directly: no H2D, memset or D2H (GV_LAT_ZC=0: A/B)
   bool lat_sliced = true;       // small batches on k_verify_lat_sl / k_verify_lat16_sl (GV_LAT_SLICED=0: the one-lane-field kernels, A/B)
   bool keyed_k4 = true;         // keyed batches on k_ecmult_k4 (GV_KEYED_K4=0: the 125-doubling ladder, A/B)
+  bool k6 = true;               // grouped batches on k_ecmult_k6: 6-bit Q / 24-bit G windows (GV_K6=0: k4, A/B)
   bool pipeline_dev = true;     // pipelined device-resident calls on the context stream (dev_run; GV_PIPELINE=0: A/B)
   bool group_keys = true;       // pub33 throughput batches parse each distinct key once (group_keys; GV_GROUP_KEYS=0: A/B)
   bool keys_scratch = true;     // key tables: forward entries through coalesced scratch rows (GV_KEYS_SCRATCH=0: A/B)
@@ -675,12 +680,33 @@ int ensure_gtab4(gv_ctx* ctx, Dev* d, Set* s, hipStream_t st) {
   return GV_OK;
 }
 
-int ensure_group_arena(Set* s, size_t cap) {
-  if (cap <= s->gcap) return GV_OK;
+// k_ecmult_k6's G tables (GV_K6_GTAB_WORDS, 4 GiB): built on first use, ~0.1 s.
+// An allocation failure is remembered and the grouped route stays on k4.
+int ensure_gtab6(gv_ctx* ctx, Dev* d, Set* s, hipStream_t st) {
+  if (d->gtab6 || !ctx->k6 || d->gtab6_failed) return GV_OK;
+  uint32_t* t6 = nullptr;
+  if (hipMalloc(&t6, GV_K6_GTAB_WORDS * 4) != hipSuccess) {
+    (void)hipGetLastError();
+    d->gtab6_failed = true;
+    return GV_OK;
+  }
+  int rc;
+  if ((rc = ensure_cap(s, 256))) { (void)hipFree(t6); return rc; }
+  if ((rc = set_acquire(s, st))) { (void)hipFree(t6); return rc; }
+  if (gvk_gen_gtable6(t6, s->flags, st) != hipSuccess) { (void)hipFree(t6); return GV_EHIP; }
+  if ((rc = set_release(s, st))) { (void)hipFree(t6); return rc; }
+  if (hipStreamSynchronize(st) != hipSuccess) { (void)hipFree(t6); return GV_EHIP; }
+  d->gtab6 = t6;
+  return GV_OK;
+}
+
+int ensure_group_arena(Set* s, size_t cap, bool k6) {
+  if (cap <= s->gcap && k6 == s->gk6) return GV_OK;
   for (uint32_t** p : {&s->g_kqt, &s->g_kzq, &s->g_kok, &s->g_kqt2, &s->g_kzq2})
     if (*p) { (void)hipFree(*p); *p = nullptr; }
   s->gcap = 0;
-  const size_t ent = (size_t)GV_KEY_WORDS * 4;
+  s->gk6 = k6;
+  const size_t ent = (size_t)(k6 ? GV_K6_KEY_WORDS : GV_KEY_WORDS) * 4;
   if (hipMalloc(&s->g_kqt, cap * ent) != hipSuccess || hipMalloc(&s->g_kzq, cap * 8 * 4) != hipSuccess ||
       hipMalloc(&s->g_kok, cap * 4) != hipSuccess ||
       hipMalloc(&s->g_kqt2, cap * GV_KEY2_TABLES * ent) != hipSuccess ||
@@ -709,6 +735,7 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   uint32_t* kpfx = kx + 8 * capU;
   uint32_t* qr = kpfx + capU;                   // ratio rows of the 4-lanes-per-key table build
   if ((size_t)(qr + (GV_QTAB_N - 1) * 9 * 4 * capU - q) > (size_t)GV_QTAB_WORDS * C) return GV_OK;   // no room: pub33
+  const bool k6_room = (size_t)(qr + (size_t)(GV_K6_NT - 1) * 9 * 4 * capU - q) <= (size_t)GV_QTAB_WORDS * C;
   if (!s->h_count && hipHostMalloc((void**)&s->h_count, 64, hipHostMallocDefault) != hipSuccess) {
     s->h_count = nullptr;
     return GV_ENOMEM;
@@ -724,26 +751,33 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   CK(hipStreamSynchronize(st));
   const size_t U = *s->h_count;
   if (U == 0 || U * ctx->group_div > n || U > capU) return GV_OK;   // many distinct keys: the pub33 pipeline
-  if ((rc = ensure_gtab4(ctx, d, s, st))) return rc;
-  if ((rc = ensure_group_arena(s, capU))) return rc == GV_ENOMEM ? GV_OK : rc;
+  if (ctx->k6 && k6_room && (rc = ensure_gtab6(ctx, d, s, st))) return rc;
+  const bool k6 = ctx->k6 && k6_room && d->gtab6;
+  if (!k6 && (rc = ensure_gtab4(ctx, d, s, st))) return rc;
+  if ((rc = ensure_group_arena(s, capU, k6))) return rc == GV_ENOMEM ? GV_OK : rc;
   // the tables are built on the set's side stream while k_scalar_inv (which
   // does not read keys) runs on st: both are one wave per SIMD or so
   CK(hipEventRecord(s->fork, st));
   CK(hipStreamWaitEvent(s->side, s->fork, 0));
   // the forward pass's entries in coalesced scratch rows after the ratio rows, when they fit
   const size_t C4 = round_up(4 * U, 256);
-  uint32_t* qe = qr + (size_t)(GV_QTAB_N - 1) * 9 * C4;
-  if (!ctx->keys_scratch || (size_t)(qe + (size_t)(GV_QTAB_N - 1) * 18 * C4 - q) > (size_t)GV_QTAB_WORDS * C)
-    qe = nullptr;
-  CK(gvk_keys_build_rows((uint32_t)U, (uint32_t)capU, kx, kpfx, qr, qe, s->g_kqt, s->g_kzq, (uint32_t)capU,
-                         s->g_kok, s->g_kqt2, s->g_kzq2, s->side));
-  if (used_end) *used_end = qe ? qe + (size_t)(GV_QTAB_N - 1) * 18 * C4 : qr + (size_t)(GV_QTAB_N - 1) * 9 * C4;
+  const size_t nr = (size_t)(k6 ? GV_K6_NT : GV_QTAB_N) - 1;   // ratio / forward-entry rows per lane
+  uint32_t* qe = qr + nr * 9 * C4;
+  if (!ctx->keys_scratch || (size_t)(qe + nr * 18 * C4 - q) > (size_t)GV_QTAB_WORDS * C) qe = nullptr;
+  if (k6)
+    CK(gvk_keys_build_rows6((uint32_t)U, (uint32_t)capU, kx, kpfx, qr, qe, s->g_kqt, s->g_kzq, (uint32_t)capU,
+                            s->g_kok, s->g_kqt2, s->g_kzq2, s->side));
+  else
+    CK(gvk_keys_build_rows((uint32_t)U, (uint32_t)capU, kx, kpfx, qr, qe, s->g_kqt, s->g_kzq, (uint32_t)capU,
+                           s->g_kok, s->g_kqt2, s->g_kzq2, s->side));
+  if (used_end) *used_end = qe ? qe + nr * 18 * C4 : qr + nr * 9 * C4;
   CK(hipEventRecord(s->keys_done, s->side));
   b.keys_ready = s->keys_done;
   b.pub33 = nullptr;
   b.kslot = kslot; b.kqt = s->g_kqt; b.kzq = s->g_kzq; b.kok = s->g_kok;
   b.kC = (uint32_t)capU; b.kcount = (uint32_t)U;
   b.kqt2 = s->g_kqt2; b.gtab4 = d->gtab4;       // null gtab4: the 125-doubling keyed ladder
+  b.k6 = k6 ? 1 : 0; b.gtab6 = d->gtab6;
   d->grouped_batches++;
   d->grouped_keys += U;
   return GV_OK;
@@ -753,7 +787,7 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
 // `base` of the set's Q-table region (unused by the keyed pipeline past the
 // grouping rows); no room or the option off: item order.
 void plan_sort(gv_ctx* ctx, Set* s, gvk_batch& b, uint32_t* base) {
-  if (!ctx->sort_keys || !b.kslot || !b.gtab4) return;
+  if (!ctx->sort_keys || !b.kslot || !(b.gtab4 || (b.k6 && b.gtab6))) return;
   const size_t C = b.C, nb = (size_t)b.kcount + 1;
   const size_t tb = gvk_sort_temp_bytes((uint32_t)nb);
   uint32_t* p = s->qtab + round_up((size_t)(base - s->qtab), 64);
@@ -776,6 +810,8 @@ struct KeyArena {
   const uint32_t *kqt, *kzq, *kok, *kqt2, *kzq2;
   uint32_t kC, kcount;
   const uint32_t* gtab4;
+  const uint32_t* gtab6;
+  int k6;                                       // k6 group tables: the throughput pipeline only
   hipEvent_t ready;
 };
 
@@ -812,6 +848,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     b.kslot = kslot; b.kqt = ka->kqt; b.kzq = ka->kzq; b.kok = ka->kok;
     b.kC = ka->kC; b.kcount = ka->kcount;
     b.kqt2 = ka->kqt2; b.gtab4 = ka->gtab4;
+    b.k6 = ka->k6; b.gtab6 = ka->gtab6;
     kzq2 = ka->kzq2;
     // the slots are on the device already (slice_group read the key count
     // back after k_dedupe_map); only k_prep on reads the tables, so the
@@ -833,12 +870,15 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     b.ev_ecm_start = rs[4];
     b.ev[3] = rs[5];
   }
-  const bool pipelined = st_ecm != nullptr && n > (kslot ? ctx->lat_max_keyed : ctx->lat_max);
+  // k6 group tables (a grouped slice's chunks) are read by k_ecmult_k6 only:
+  // such a chunk takes the pipeline whatever its size
+  const bool small = n <= (kslot ? ctx->lat_max_keyed : ctx->lat_max) && !b.k6;
+  const bool pipelined = st_ecm != nullptr && !small;
   if (pipelined) {
     b.st_ecm = st_ecm;
     b.ecm_ready = s->ecm_ready;
   }
-  if (n <= (kslot ? ctx->lat_max_keyed : ctx->lat_max)) {
+  if (small) {
     // small batch: one fused kernel, several lanes per signature (gv_lat.hip)
     if (b.keys_ready) CK(hipStreamWaitEvent(st, b.keys_ready, 0));   // a host slice's tables
     gvk_lat lb;
@@ -855,6 +895,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     const bool sliced = ctx->lat_sliced && n <= (kslot ? ctx->lat_sl_max_keyed : ctx->lat_sl_max);
     if (out8 && !sliced) return GV_EINVAL;      // byte verdicts: the sliced kernels only
     lb.out8 = out8;
+    d->routes[kslot ? GV_ROUTE_LAT_KEYED : GV_ROUTE_LAT]++;
     if (kslot) {                                // keyed: 16 lanes per signature (group tables)
       lb.kqt2 = b.kqt2; lb.kzq2 = kzq2; lb.glat = d->glat;
       if (sliced) CK(gvk_verify_lat16_sl(&lb, st));
@@ -877,6 +918,8 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
       if (rc) return rc;
     }
     plan_sort(ctx, s, b, sort_base);
+    d->routes[b.k6 && b.gtab6 ? GV_ROUTE_K6 : b.kslot && b.gtab4 ? GV_ROUTE_K4 : b.kslot ? GV_ROUTE_KEYED125
+                                                                                       : GV_ROUTE_PUB33]++;
     CK(gvk_verify(&b, st));
   }
   if (rs) {
@@ -1180,6 +1223,7 @@ int slice_group(gv_ctx* ctx, Dev* d, size_t lo, size_t n, const HostBatch& hb, K
   CK(hipEventRecord(d->grp_ready, g->st));
   ka->kqt = b.kqt; ka->kzq = b.kzq; ka->kok = b.kok; ka->kqt2 = b.kqt2; ka->kzq2 = g->g_kzq2;
   ka->kC = b.kC; ka->kcount = b.kcount; ka->gtab4 = b.gtab4;
+  ka->gtab6 = b.gtab6; ka->k6 = b.k6;
   ka->ready = d->grp_ready;
   *d_slots = b.kslot;
   return GV_OK;   // the set stays acquired until run_slice releases it after the last chunk
@@ -1425,6 +1469,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   gv_ctx* ctx = new gv_ctx();
   parse_size_env("GV_MAX_BATCH", &ctx->max_batch);
   if (const char* k4 = getenv("GV_KEYED_K4")) ctx->keyed_k4 = strcmp(k4, "0") != 0;
+  if (const char* k6 = getenv("GV_K6")) ctx->k6 = strcmp(k6, "0") != 0;
   if (const char* ks = getenv("GV_KEYS_SCRATCH")) ctx->keys_scratch = strcmp(ks, "0") != 0;
   if (const char* sk = getenv("GV_SORT_KEYS")) ctx->sort_keys = strcmp(sk, "0") != 0;
   if (const char* ek = getenv("GV_ED_KEYED")) ctx->ed_keyed = strcmp(ek, "0") != 0;
@@ -1482,6 +1527,7 @@ void gv_close(gv_ctx* ctx) {
     if (d->gtab) (void)hipFree(d->gtab);
     if (d->glat) (void)hipFree(d->glat);
     if (d->gtab4) (void)hipFree(d->gtab4);
+    if (d->gtab6) (void)hipFree(d->gtab6);
     if (d->kqt2) (void)hipFree(d->kqt2);
     if (d->kzq2) (void)hipFree(d->kzq2);
     if (d->kqt) (void)hipFree(d->kqt);
@@ -1949,6 +1995,14 @@ int gv_host_free(gv_ctx* ctx, void* p) {
   return GV_OK;
 }
 
+int gv_route_stats(gv_ctx* ctx, int dev_slot, uint64_t out[GV_ROUTES]) {
+  if (!ctx || !out || dev_slot < 0 || dev_slot >= (int)ctx->devs.size()) return GV_EINVAL;
+  Dev* d = ctx->devs[dev_slot];
+  std::lock_guard<std::mutex> lk(d->mu);
+  for (int i = 0; i < GV_ROUTES; ++i) out[i] = d->routes[i];
+  return GV_OK;
+}
+
 int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys) {
   if (!ctx || dev_slot < 0 || dev_slot >= (int)ctx->devs.size()) return GV_EINVAL;
   Dev* d = ctx->devs[dev_slot];
@@ -2079,6 +2133,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "ed_keyed")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->ed_keyed = val != 0;
+  } else if (!strcmp(key, "k6")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->k6 = val != 0;
   } else if (!strcmp(key, "sort_keys")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->sort_keys = val != 0;

@@ -48,7 +48,11 @@ GV_DEV void gej29x_add_scaled(gej29& a, bool& inf, const fe29& x, const fe29& y,
   f29x_mul(z3, z2, az);                        // 1
   f29_neg<1>(n, a.y);                          // -Y1: 2
   f29x_mul(rr, y, z3, f29x_plus<1>{n.n});      // R = y az^3 - Y1: 1  (2 x 1)
+#if defined(GV_ISA_NOEXC)
+  const bool exc = false;                      // tools/isa_ops.hip: main path only
+#else
   const bool exc = f29_is_zero_fast(h);
+#endif
   bool dbl = false;
   if (exc) {
     dbl = f29_is_zero(rr);

@@ -42,7 +42,7 @@ EXPORTED_SYMBOLS = (
     "gv_dev_copy", "gv_dev_sync", "gv_stage_stats", "gv_keys_load", "gv_keys_reset", "gv_keys_count", "gv_keys_generation",
     "gv_verify_digests_keyed", "gv_verify_msgs_keyed", "gv_dev_verify_digests_keyed", "gv_stage_stats4",
     "gv_keys_point", "gv_dev_stream_create", "gv_dev_stream_sync", "gv_dev_stream_destroy",
-    "gv_verify_ed25519_msgs", "gv_dev_verify_ed25519_msgs", "gv_last_slices", "gv_group_stats", "gv_host_alloc", "gv_host_free",
+    "gv_verify_ed25519_msgs", "gv_dev_verify_ed25519_msgs", "gv_last_slices", "gv_group_stats", "gv_route_stats", "gv_host_alloc", "gv_host_free",
     "gv_ed_keys_load", "gv_ed_keys_reset", "gv_ed_keys_count", "gv_ed_keys_generation", "gv_verify_ed25519_msgs_keyed",
 )
 
@@ -133,6 +133,8 @@ def load(path: str = LIB_PATH):
     L.gv_last_slices.restype = i32
     L.gv_group_stats.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     L.gv_group_stats.restype = i32
+    L.gv_route_stats.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_uint64)]
+    L.gv_route_stats.restype = i32
     L.gv_host_alloc.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(vp)]
     L.gv_host_alloc.restype = i32
     L.gv_host_free.argtypes = [vp, vp]
@@ -458,6 +460,14 @@ class Verifier:
         b, k = ctypes.c_uint64(), ctypes.c_uint64()
         _check(self._L.gv_group_stats(self._ctx, slot, ctypes.byref(b), ctypes.byref(k)), "gv_group_stats")
         return b.value, k.value
+
+    ROUTES = ("pub33", "keyed125", "k4", "k6", "lat", "lat_keyed")
+
+    def route_stats(self, slot: int = 0) -> dict:
+        """Batches per secp256k1 schedule on device slot since open (gv_route_stats)."""
+        out = (ctypes.c_uint64 * len(self.ROUTES))()
+        _check(self._L.gv_route_stats(self._ctx, slot, out), "gv_route_stats")
+        return dict(zip(self.ROUTES, (int(v) for v in out)))
 
     def last_slices(self):
         """[(ms, items)] per device slot: each device's slice of the last host-buffer call."""

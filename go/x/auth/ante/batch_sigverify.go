@@ -83,6 +83,19 @@ func (d BatchSigVerificationDecorator) AnteHandle(ctx sdk.Context, tx sdk.Tx, si
 		if err != nil {
 			return ctx, err
 		}
+		// Sign bytes where the reference computes them (:201): after the
+		// account read, before the nil-key check, and when simulating too.  A
+		// gathered signer's bytes were computed by the look-ahead from the same
+		// account and chain id (GetSignBytes reads nothing else), so only a
+		// signer the look-ahead did not reach -- a nil key, a missing account
+		// before it, or sign bytes that panicked -- recomputes them here, and
+		// a Msg whose GetSignBytes panics panics at this point, as in the
+		// reference (runTx turns it into ErrPanic).
+		gathered := i < len(exprs) && exprs[i] != nil
+		var signBytes []byte
+		if !gathered {
+			signBytes = sigTx.GetSignBytes(ctx, acc)
+		}
 		pubKey := acc.GetPubKey()
 		if !simulate && pubKey == nil {
 			return ctx, sdkerrors.Wrap(sdkerrors.ErrInvalidPubKey, "pubkey on account is not set")
@@ -91,10 +104,10 @@ func (d BatchSigVerificationDecorator) AnteHandle(ctx sdk.Context, tx sdk.Tx, si
 			continue
 		}
 		var verified bool
-		if i < len(exprs) && exprs[i] != nil {
+		if gathered {
 			verified = exprs[i].eval(&b)
-		} else { // not gathered (its sign bytes panicked in the look-ahead): the reference call itself
-			verified = pubKey.VerifyBytes(sigTx.GetSignBytes(ctx, acc), sig)
+		} else {
+			verified = pubKey.VerifyBytes(signBytes, sig)
 		}
 		if !verified {
 			return ctx, sdkerrors.Wrap(sdkerrors.ErrUnauthorized, "signature verification failed; verify correct account sequence and chain-id")
@@ -106,7 +119,8 @@ func (d BatchSigVerificationDecorator) AnteHandle(ctx sdk.Context, tx sdk.Tx, si
 // gather builds signer i's verification expression for i = 0.. until the
 // first signer whose account is missing or has no key (the loop reports it
 // when it gets there) or whose sign bytes panic (the loop recomputes them on
-// the real context and panics at the same point the reference does).
+// the real context and panics at the same point the reference does: before
+// the nil-key check, sigverify.go:201-207).
 func (d BatchSigVerificationDecorator) gather(look sdk.Context, sigTx SigVerifiableTx, sigs [][]byte,
 	signerAddrs []sdk.AccAddress, b *batch) []*expr {
 	exprs := make([]*expr, 0, len(sigs))

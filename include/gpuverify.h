@@ -287,6 +287,21 @@ int gv_host_free(gv_ctx* ctx, void* p);
  * number of batches -- secp256k1 and ed25519 -- that took the grouped (keyed)
  * pipeline and the distinct keys whose tables they built. */
 int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys);
+/* Batches per secp256k1 schedule on dev_slot since gv_open, out[GV_ROUTES]:
+ * GV_ROUTE_PUB33 (per-item pipeline: k_prep + k_ecmult), GV_ROUTE_KEYED125
+ * (keyed, 125-doubling ladder), GV_ROUTE_K4 (keyed 4-group ladder over the
+ * key arena), GV_ROUTE_K6 (in-batch key grouping on the 6-bit-window ladder),
+ * GV_ROUTE_LAT (small pub33 batches: gv_lat.hip kernels), GV_ROUTE_LAT_KEYED
+ * (small keyed batches).  Instrumentation only (bench route attribution, node
+ * metrics). */
+#define GV_ROUTE_PUB33 0
+#define GV_ROUTE_KEYED125 1
+#define GV_ROUTE_K4 2
+#define GV_ROUTE_K6 3
+#define GV_ROUTE_LAT 4
+#define GV_ROUTE_LAT_KEYED 5
+#define GV_ROUTES 6
+int gv_route_stats(gv_ctx* ctx, int dev_slot, uint64_t out[GV_ROUTES]);
 
 const char* gv_strerror(int code);
 

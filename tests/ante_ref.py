@@ -55,6 +55,11 @@ class Fail(Exception):
         self.code, self.msg = code, msg
 
 
+class Panic(Exception):
+    """A reference panic inside the ante chain; runTx recovers it into
+    ErrPanic (baseapp/baseapp.go:490-512): code 111222, codespace undefined."""
+
+
 class Meter:
     def __init__(self, limit):
         self.limit, self.used = limit, 0              # limit None: infinite
@@ -185,6 +190,9 @@ class AnteRef:
         self.chain_id, self.height, self.recheck, self.gas_limit = chain_id, height, recheck, gas_limit
         self.sig_limit, self.cost_secp, self.cost_ed = sig_limit, cost_secp, cost_ed
         self.accounts = {}
+        # StdSignBytes (x/auth/types/stdtx.go:292-312); a test may substitute a
+        # function that raises Panic (a Msg whose GetSignBytes panics)
+        self.sign_bytes = T.std_sign_bytes
 
     def set_account(self, addr, number, sequence=0, pub=b""):
         self.accounts[addr] = Account(number, sequence, pub)
@@ -272,10 +280,11 @@ class AnteRef:
                     acc = self._read(m, signers[i])
                     if acc is None:
                         raise Fail(9, f"account {T.bech32('cosmos', signers[i])} does not exist")
+                    # sign bytes before the nil-key check (sigverify.go:201-207)
+                    accnum = 0 if self.height == 0 else acc.number
+                    sb = self.sign_bytes(self.chain_id, accnum, acc.sequence, fee, msgs, memo)
                     if not acc.pub:
                         raise Fail(8, "pubkey on account is not set")
-                    accnum = 0 if self.height == 0 else acc.number
-                    sb = T.std_sign_bytes(self.chain_id, accnum, acc.sequence, fee, msgs, memo)
                     if not verify_bytes(decode_pubkey(acc.pub), sb, sig):
                         raise Fail(4, UNAUTH_MSG)
                 for a in signers:                                              # IncrementSequence
@@ -285,6 +294,9 @@ class AnteRef:
         except Fail as f:
             self._restore(saved)
             return f.code, f"{f.msg}: {ERR_DESC[f.code]}", m.used
+        except Panic as p:
+            self._restore(saved)
+            return 111222, f"{p}: panic", m.used
         except OutOfGas as o:
             self._restore(saved)
             return 11, (f"out of gas in location: {o}; gasWanted: {wanted}, gasUsed: {m.used}: out of gas"), m.used

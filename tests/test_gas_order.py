@@ -94,6 +94,47 @@ def test_failures_before_verification_cpu():
     assert code == 9
 
 
+def test_sign_bytes_panic_precedes_key_checks_in_restatement():
+    """sigverify.go:194-207 computes signer i's sign bytes right after its
+    (metered) account read and before the nil-key check: a Msg whose
+    GetSignBytes panics ends the tx in ErrPanic at the first signer, charged
+    for the chain's reads up to that account read.  The Go decorator keeps that
+    order (batch_sigverify.go: sign bytes before the nil-key check, also under
+    simulate); the restatement does too.  The mirror decodes only MsgSend /
+    MsgMultiSend, whose sign bytes cannot panic, so this is a restatement-level
+    check of the ordering the Go drop-in follows."""
+    from ante_ref import Panic
+    app, ref = setup(None, with_pub=True)
+    parts = multisend(KEYS[:2], 200000, ref=ref)
+    msgs, fee, memo, sigs = parts
+    ok_code, _, ok_gas = ref.ante(msgs, fee, memo, sigs, 400)
+    assert ok_code == 0
+
+    calls = []
+
+    def panicking(*a):
+        calls.append(a)
+        raise Panic("json: unsupported value")
+
+    app, ref = setup(None, with_pub=True)
+    ref.sign_bytes = panicking
+    code, log, gas = ref.ante(msgs, fee, memo, sigs, 400)
+    assert (code, log) == (111222, "json: unsupported value: panic")
+    assert len(calls) == 1                      # the first signer's, right after its account read
+    assert gas < ok_gas
+    # nothing applied: sequences unchanged
+    assert all(ref.accounts[k.addr].sequence == 4 + i for i, k in enumerate(KEYS))
+    # the first signer's key missing from its account: the decorator chain
+    # stops in SigGasConsume before any sign bytes are built
+    calls.clear()
+    app, ref = setup(None, with_pub=True)
+    ref.sign_bytes = panicking
+    ref.accounts[KEYS[0].addr].pub = b""
+    # (in the full chain SigGasConsume rejects the nil key first: sigverify.go:342)
+    code, _, _ = ref.ante(msgs, fee, memo, sigs, 400)
+    assert code == 8 and not calls[1:]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [2, 3])
 def test_multi_signer_gas_follows_reference_order(n):

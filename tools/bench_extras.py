@@ -194,9 +194,9 @@ def c2_key_cache(ver, pub, sig, dig, exp, nkeys: int, steps: int = 5):
     for p in d + [d_bits]:
         ver.dev_free(p)
     ver.keys_reset()
-    # k_ecmult_k4's work: the ladder's W with 95 of the 129 survey doublings gone (30 instead of 125)
+    # k_ecmult_k4's work, counted from the kernel's operations (bench.w_ladder)
     import bench as B
-    w_k4 = B.W_LADDER - 95 * (2 * B.FM + 5 * B.FS)
+    w_k4 = round(B.W_LADDER_K4)
     ems = stages.get("ecmult_ms") or 0.0
     ach = n * w_k4 / (ems * 1e-3) / 1e12 if ems else 0.0
     return {"items": n, "keys": nkeys, "value": round(n * steps / el, 1), "unit": "verifies/s",
