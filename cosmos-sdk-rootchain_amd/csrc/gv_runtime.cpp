@@ -416,7 +416,9 @@ int set_release(Set* s, hipStream_t st) {
 // stride of kzq changes with the capacity).
 int ensure_keys(Dev* d, size_t need, size_t used, hipStream_t st) {
   if (need <= d->kcap) return GV_OK;
-  const size_t cap = round_up(std::max<size_t>({need, 2 * d->kcap, 4096}), 256);
+  // doubling, but not past GV_KEY_CAP (the callers' reset point) unless asked
+  const size_t grow = std::min<size_t>(2 * d->kcap, std::max<size_t>(need, GV_KEY_CAP));
+  const size_t cap = round_up(std::max<size_t>({need, grow, 4096}), 256);
   uint32_t *qt = nullptr, *zq = nullptr, *ok = nullptr, *qt2 = nullptr, *zq2 = nullptr;
   auto fail = [&]() {
     for (uint32_t* p : {qt, zq, ok, qt2, zq2}) if (p) (void)hipFree(p);
@@ -1718,9 +1720,13 @@ size_t gv_keys_count(const gv_ctx* ctx) { return ctx ? ctx->keys : 0; }
 
 // ---- ed25519 key arena + small keyed batches (k_ed_keys, k_ed_lat_sl)
 namespace {
+// Growth doubles the arena but stops at GV_ED_KEY_CAP (the callers' reset
+// point): the transient peak of a growth -- old and new arena both allocated,
+// 72 KB per key each -- stays within cap + the old arena.
 int ensure_ed_keys(Dev* d, size_t need, size_t used, hipStream_t st) {
   if (need <= d->ekcap) return GV_OK;
-  const size_t cap = round_up(std::max<size_t>({need, 2 * d->ekcap, 256}), 256);
+  const size_t grow = std::min<size_t>(2 * d->ekcap, std::max<size_t>(need, GV_ED_KEY_CAP));
+  const size_t cap = round_up(std::max<size_t>({need, grow, 256}), 256);
   uint32_t *t = nullptr, *p = nullptr, *o = nullptr;
   auto fail = [&]() {
     for (uint32_t* q : {t, p, o}) if (q) (void)hipFree(q);
@@ -1905,10 +1911,13 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
   if (!slot || !sig64 || !msg_off || !msg_len || !out_ok) return GV_EINVAL;
   for (size_t i = 0; i < n; ++i)
     if (msg_len[i] && !msg_blob) return GV_EINVAL;
-  size_t kcount;
+  // ed_keys_mu is held for the whole call, small batches included: a
+  // concurrent gv_ed_keys_reset + load cannot move a slot between the lookup
+  // of kcount and the kernel (the large-batch path always held it; lock order
+  // ed_keys_mu -> d->mu, as in gv_ed_keys_load)
+  std::lock_guard<std::mutex> kl(ctx->ed_keys_mu);
+  const size_t kcount = ctx->ed_keys;
   {
-    std::lock_guard<std::mutex> kl(ctx->ed_keys_mu);
-    kcount = ctx->ed_keys;
     if (n > ctx->ed_lat_max && kcount && ctx->ed_keyed) {
       // large batches: one signature per lane against the key tables
       // (k_ed_keyed), split over the devices like run_ed_host

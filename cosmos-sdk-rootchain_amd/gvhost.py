@@ -46,7 +46,7 @@ class Commit(ctypes.Structure):
                 ("val_addr20", ctypes.c_void_p), ("val_power", ctypes.c_void_p), ("n_sigs", ctypes.c_size_t),
                 ("flag", ctypes.c_void_p), ("sig_addr20", ctypes.c_void_p), ("sig64", ctypes.c_void_p),
                 ("sig_len", ctypes.c_void_p), ("msg_blob", ctypes.c_void_p), ("msg_off", ctypes.c_void_p),
-                ("msg_len", ctypes.c_void_p)]
+                ("msg_len", ctypes.c_void_p), ("keys_trusted", ctypes.c_int)]
 
 
 class CommitResult(ctypes.Structure):
@@ -279,7 +279,9 @@ class HostApp:
     def verify_commits(self, commits):
         """gvh_verify_commits over a list of dicts: vals = [(pub32, addr20, power)],
         sigs = [(flag, addr20, sig_bytes, sign_bytes)], trusting (bool),
-        trust = (num, den), basic_ok (bool).  Returns [(code name, idx, idx2, got, needed)]."""
+        trust = (num, den), basic_ok (bool), keys_trusted (bool, default: trusting -- the
+        trusted set of VerifyCommitTrusting; an adjacent VerifyCommit's set passes True).
+        Returns [(code name, idx, idx2, got, needed)]."""
         import numpy as np
         keep = []
         arr = (Commit * max(1, len(commits)))()
@@ -307,7 +309,7 @@ class HostApp:
             arr[c] = Commit(1 if d.get("trusting") else 0, num, den, 1 if d.get("basic_ok", True) else 0, len(vals),
                             vp32.ctypes.data, va20.ctypes.data, vpow.ctypes.data, len(sigs), flags.ctypes.data,
                             sa20.ctypes.data, s64.ctypes.data, slen.ctypes.data, blob.ctypes.data, off.ctypes.data,
-                            ln.ctypes.data)
+                            ln.ctypes.data, 1 if d.get("keys_trusted", d.get("trusting")) else 0)
         res = (CommitResult * max(1, len(commits)))()
         rc = self._L.gvh_verify_commits(self._app, len(commits), arr, res)
         if rc != 0:

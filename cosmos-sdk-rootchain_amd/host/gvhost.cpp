@@ -2993,10 +2993,15 @@ extern "C" int gvh_verify_commits(gvh_app* app, size_t n, const gvh_commit* comm
   };
   std::vector<std::vector<int32_t>> vidx(n);        // per signature: the validator its loop would read (-1: none)
   std::vector<std::vector<int32_t>> item(n);        // per signature: its batch item (-1: false without verifying)
-  std::vector<uint8_t> pub, sig, blob;
-  std::vector<uint64_t> off;
-  std::vector<uint32_t> len;
-  size_t m = 0;
+  // two batches: trusted sets (keys loaded into the arena: a validator set
+  // signs block after block) and relayer-supplied sets (keys not loaded)
+  struct EdB {
+    std::vector<uint8_t> pub, sig, blob, ok;
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> len;
+    size_t m = 0;
+  } bt[2];
+  std::vector<uint8_t> plain(n, 0);                 // per commit: its items are in bt[1]
   for (size_t c = 0; c < n; ++c) {
     const gvh_commit& k = commits[c];
     gvh_commit_result& r = out[c];
@@ -3037,24 +3042,30 @@ extern "C" int gvh_verify_commits(gvh_app* app, size_t n, const gvh_commit* comm
       }
       vidx[c][i] = v;
       if (v < 0 || k.sig_len[i] != 64) continue;
-      item[c][i] = (int32_t)m++;
-      pub.insert(pub.end(), k.val_pub32 + 32 * (size_t)v, k.val_pub32 + 32 * (size_t)v + 32);
-      sig.insert(sig.end(), k.sig64 + 64 * i, k.sig64 + 64 * i + 64);
-      off.push_back(blob.size());
-      len.push_back(k.msg_len[i]);
-      if (k.msg_len[i]) blob.insert(blob.end(), k.msg_blob + k.msg_off[i], k.msg_blob + k.msg_off[i] + k.msg_len[i]);
+      plain[c] = k.keys_trusted ? 0 : 1;
+      EdB& e = bt[plain[c]];
+      item[c][i] = (int32_t)e.m++;
+      e.pub.insert(e.pub.end(), k.val_pub32 + 32 * (size_t)v, k.val_pub32 + 32 * (size_t)v + 32);
+      e.sig.insert(e.sig.end(), k.sig64 + 64 * i, k.sig64 + 64 * i + 64);
+      e.off.push_back(e.blob.size());
+      e.len.push_back(k.msg_len[i]);
+      if (k.msg_len[i])
+        e.blob.insert(e.blob.end(), k.msg_blob + k.msg_off[i], k.msg_blob + k.msg_off[i] + k.msg_len[i]);
     }
   }
-  std::vector<uint8_t> ok(m);
-  if (m) {
+  for (int t = 0; t < 2; ++t) {
+    EdB& e = bt[t];
+    e.ok.assign(e.m, 0);
+    if (!e.m) continue;
     if (!app->gpu) return GVH_ENOVERIFIER;
     std::lock_guard<std::mutex> g(app->gpu_mu);
-    // a validator set signs block after block: its keys are loaded once
-    if (verify_ed(app, m, pub.data(), sig.data(), blob.empty() ? nullptr : blob.data(), off.data(), len.data(),
-                  ok.data(), true) != GV_OK)
+    // a trusted validator set signs block after block: its keys are loaded
+    // once; a relayer-supplied set is verified without touching the arena
+    if (verify_ed(app, e.m, e.pub.data(), e.sig.data(), e.blob.empty() ? nullptr : e.blob.data(), e.off.data(),
+                  e.len.data(), e.ok.data(), t == 0) != GV_OK)
       return GVH_EDEVICE;
     app->st_gpu_calls += 1;
-    app->st_gpu_leaves += m;
+    app->st_gpu_leaves += e.m;
   }
   for (size_t c = 0; c < n; ++c) {
     const gvh_commit& k = commits[c];
@@ -3080,7 +3091,7 @@ extern "C" int gvh_verify_commits(gvh_app* app, size_t n, const gvh_commit* comm
         }
         seen.emplace(v, (int32_t)i);
       }
-      const bool good = item[c][i] >= 0 && ok[(size_t)item[c][i]] != 0;
+      const bool good = item[c][i] >= 0 && bt[plain[c]].ok[(size_t)item[c][i]] != 0;
       if (!good) {
         r.code = GVH_COMMIT_WRONG_SIG;
         r.idx = (int32_t)i;

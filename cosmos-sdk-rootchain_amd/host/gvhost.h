@@ -216,6 +216,11 @@ typedef struct gvh_commit {
   const uint8_t* msg_blob;       /* VoteSignBytes(chainID, i) at msg_off[i], msg_len[i] */
   const uint64_t* msg_off;
   const uint32_t* msg_len;
+  int keys_trusted;              /* the set is already trusted (the trusted next validators of
+                                    VerifyCommitTrusting, or an adjacent header's set matching the
+                                    trusted NextValidatorsHash): its keys may be loaded into the
+                                    ed25519 key arena.  0: a relayer-supplied set -- verified without
+                                    loading its keys, so fresh sets cannot churn the arena */
 } gvh_commit;
 #define GVH_COMMIT_OK 0
 #define GVH_COMMIT_BASIC 1         /* verifyCommitBasic's error (the caller's) */

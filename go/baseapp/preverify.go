@@ -43,8 +43,17 @@ import (
 // PreVerifier pre-verifies a batch of decoded txs against the state of ctx
 // (x/auth/ante.NewPreVerifier).  It reads the state and returns the second,
 // state-free stage (sign bytes + the verification batch + cache fill), so a
-// caller may release its state lock before running it.
+// caller may release its state lock before running it.  A nil second stage
+// means nothing to do.
 type PreVerifier func(ctx sdk.Context, txs []sdk.Tx) func()
+
+// PreVerifierAhead is a PreVerifier whose sequence / key prediction also
+// carries the effects of txs that precede the batch but are not in the state
+// yet (x/auth/ante.NewPreVerifierAhead): every signer of a carry tx advances
+// its sequence by one, and a key a carry tx supplies for an account that has
+// none is the key its SetPubKeyDecorator stores.  The carry's own leaves are
+// not verified.
+type PreVerifierAhead func(ctx sdk.Context, carry, txs []sdk.Tx) func()
 
 // SetPreVerifier registers the pre-verification hook (app construction,
 // simapp/app.go:335-339, next to SetAnteHandler).
@@ -53,6 +62,15 @@ func (app *BaseApp) SetPreVerifier(pv PreVerifier) {
 		panic("SetPreVerifier() on sealed BaseApp")
 	}
 	app.preVerifier = pv
+}
+
+// SetPreVerifierAhead registers the block-replay hook (PreVerifyAhead).  One
+// more BaseApp field: preVerifierAhead PreVerifierAhead.
+func (app *BaseApp) SetPreVerifierAhead(pa PreVerifierAhead) {
+	if app.sealed {
+		panic("SetPreVerifierAhead() on sealed BaseApp")
+	}
+	app.preVerifierAhead = pa
 }
 
 func (app *BaseApp) decodeAll(txs [][]byte) []sdk.Tx {
@@ -79,7 +97,54 @@ func (app *BaseApp) PreVerifyTxs(txs [][]byte) {
 	if st == nil {
 		return
 	}
-	app.preVerifier(st.ctx, app.decodeAll(txs))()
+	if verify := app.preVerifier(st.ctx, app.decodeAll(txs)); verify != nil {
+		verify()
+	}
+}
+
+// PreVerifyAhead pipelines block replay (fast sync, catching up, the replay
+// command -- wherever block h+1 is known while block h is delivered).  Call it
+// after BeginBlock of block h and before h's first DeliverTx, with h's txs
+// (cur) and h+1's (next): the state stage runs now, against the deliver state
+// with cur's effects carried (they are not written yet), and the state-free
+// stage -- sign bytes, the GPU batch, the cache fill -- runs on a goroutine
+// beside h's DeliverTx loop.  Call the returned wait before BeginBlock of
+// h+1.  A misprediction (a tx of block h that fails, so its signers'
+// sequences do not advance) is only a cache miss.  The C++ mirror's
+// gvh_deliver_blocks runs this schedule (C1 steady blocks 1.54 -> 2.50M tx/s,
+// tests/test_block_paths.py::test_pipelined_replay_equals_block_by_block).
+//
+//	for h := range blocks {
+//		app.BeginBlock(...)
+//		if h == 0 {
+//			app.PreVerifyTxs(blocks[0])
+//		}
+//		wait := func() {}
+//		if h+1 < len(blocks) {
+//			wait = app.PreVerifyAhead(blocks[h], blocks[h+1])
+//		}
+//		for _, tx := range blocks[h] {
+//			app.DeliverTx(abci.RequestDeliverTx{Tx: tx})
+//		}
+//		app.EndBlock(...)
+//		app.Commit()
+//		wait()
+//	}
+func (app *BaseApp) PreVerifyAhead(cur, next [][]byte) (wait func()) {
+	nop := func() {}
+	if app.preVerifierAhead == nil || len(next) == 0 || app.deliverState == nil {
+		return nop
+	}
+	verify := app.preVerifierAhead(app.deliverState.ctx, app.decodeAll(cur), app.decodeAll(next))
+	if verify == nil {
+		return nop
+	}
+	done := make(chan struct{})
+	go func() {
+		defer close(done)
+		verify() // touches no state: the job's own account copies, the cache, the GPU
+	}()
+	return func() { <-done }
 }
 
 // prepareCheckTxs runs the state stage against the check state (the caller

@@ -26,7 +26,12 @@ import "C"
 
 import (
 	"errors"
+	"math/bits"
+	"os"
+	"strconv"
 	"sync"
+	"sync/atomic"
+	"time"
 	"unsafe"
 
 	"github.com/tendermint/tendermint/crypto/ed25519"
@@ -91,6 +96,88 @@ var (
 	DefaultEdKeyCap   = int(C.GV_ED_KEY_CAP)    // ed25519 key-arena size at which it is reset
 )
 
+// envInt: a positive integer from the environment, else def.
+func envInt(name string, def int) int {
+	if v, err := strconv.Atoi(os.Getenv(name)); err == nil && v > 0 {
+		return v
+	}
+	return def
+}
+
+// Logger is the subset of tendermint's libs/log.Logger the shim reports
+// through (baseapp.go:44 keeps one per app): a device failure is logged once
+// per fallback call, with the batch size and the library's error string.
+type Logger interface {
+	Error(msg string, keyvals ...interface{})
+}
+
+// Stats counts what the shim did since Open (SURVEY.md §5: GPU vs CPU
+// fallback, batch sizes, latency).  Histograms are log2 buckets: bucket k
+// holds values in [2^k, 2^(k+1)) (batch leaves; call latency in us).
+type Stats struct {
+	GPUCalls, GPULeaves             uint64 // library calls that answered, and their leaves
+	CPURouted, CPURoutedLeaves      uint64 // batches below CPUBelow: the reference VerifyBytes by policy
+	FallbackCalls, FallbackLeaves   uint64 // library errors: leaves re-verified on the CPU (fail closed)
+	KeyedCalls, Pub33Calls, EdCalls uint64
+	KeyLoads, KeyResets             uint64
+	BatchLog2                       [24]uint64
+	LatencyUsLog2                   [24]uint64
+}
+
+type counters struct {
+	gpuCalls, gpuLeaves, cpuRouted, cpuRoutedLeaves, fbCalls, fbLeaves uint64
+	keyed, pub33, ed, keyLoads, keyResets                             uint64
+	batch, lat                                                        [24]uint64
+}
+
+func log2b(v uint64) int {
+	if v == 0 {
+		return 0
+	}
+	k := bits.Len64(v) - 1
+	if k > 23 {
+		k = 23
+	}
+	return k
+}
+
+// done records one library call of n leaves that took d; rc != 0 is a
+// fallback (the leaves were re-verified on the CPU).
+func (g *GPU) done(what string, n int, d time.Duration, rc C.int) {
+	c := &g.cnt
+	atomic.AddUint64(&c.batch[log2b(uint64(n))], 1)
+	if rc == 0 {
+		atomic.AddUint64(&c.gpuCalls, 1)
+		atomic.AddUint64(&c.gpuLeaves, uint64(n))
+		atomic.AddUint64(&c.lat[log2b(uint64(d.Microseconds()))], 1)
+		return
+	}
+	atomic.AddUint64(&c.fbCalls, 1)
+	atomic.AddUint64(&c.fbLeaves, uint64(n))
+	if g.Logger != nil {
+		g.Logger.Error("gpuverify: device call failed, leaves re-verified on the CPU", "call", what, "leaves", n,
+			"err", C.GoString(C.gv_strerror(rc)))
+	}
+}
+
+// Stats returns a snapshot of the counters.
+func (g *GPU) Stats() Stats {
+	c := &g.cnt
+	s := Stats{
+		GPUCalls: atomic.LoadUint64(&c.gpuCalls), GPULeaves: atomic.LoadUint64(&c.gpuLeaves),
+		CPURouted: atomic.LoadUint64(&c.cpuRouted), CPURoutedLeaves: atomic.LoadUint64(&c.cpuRoutedLeaves),
+		FallbackCalls: atomic.LoadUint64(&c.fbCalls), FallbackLeaves: atomic.LoadUint64(&c.fbLeaves),
+		KeyedCalls: atomic.LoadUint64(&c.keyed), Pub33Calls: atomic.LoadUint64(&c.pub33),
+		EdCalls: atomic.LoadUint64(&c.ed), KeyLoads: atomic.LoadUint64(&c.keyLoads),
+		KeyResets: atomic.LoadUint64(&c.keyResets),
+	}
+	for k := range s.BatchLog2 {
+		s.BatchLog2[k] = atomic.LoadUint64(&c.batch[k])
+		s.LatencyUsLog2[k] = atomic.LoadUint64(&c.lat[k])
+	}
+	return s
+}
+
 // GPU is a libgpuverify context on one or more HIP devices.  Safe for
 // concurrent use: the library serialises calls per device, and the key-cache
 // maps below are guarded by mu.
@@ -117,6 +204,14 @@ type GPU struct {
 	KeyLoadMin int
 	// KeyCap: the arena is reset when a load would take it past this many keys.
 	KeyCap int
+	// EdKeyCap: the same for the ed25519 key arena (72 KB of HBM per key;
+	// default GV_ED_KEY_CAP, env GV_ED_KEY_CAP).
+	EdKeyCap int
+	// Logger, when set, reports every call that fell back to the CPU.
+	Logger Logger
+
+	cnt  counters
+	pool pinnedPool
 
 	mu      sync.Mutex                           // the slot maps AND every keyed call (no reset in between)
 	slots   map[secp256k1.PubKeySecp256k1]uint32 // key -> key-arena slot (gv_keys_load)
@@ -149,12 +244,20 @@ func Open(devices []int) (*GPU, error) {
 	if rc := C.gv_open(ids, C.int(len(devices)), &ctx); rc != 0 {
 		return nil, errors.New("gpuverify: gv_open: " + C.GoString(C.gv_strerror(rc)))
 	}
-	return &GPU{ctx: ctx, CPUBelow: DefaultCPUBelow, Keyed: true, KeyLoadMin: DefaultKeyLoadMin, KeyCap: DefaultKeyCap,
-		slots: map[secp256k1.PubKeySecp256k1]uint32{}, edSlots: map[ed25519.PubKeyEd25519]uint32{}}, nil
+	g := &GPU{ctx: ctx, CPUBelow: DefaultCPUBelow, Keyed: true, KeyLoadMin: DefaultKeyLoadMin,
+		KeyCap: envInt("GV_KEY_CAP", DefaultKeyCap), EdKeyCap: envInt("GV_ED_KEY_CAP", DefaultEdKeyCap),
+		slots: map[secp256k1.PubKeySecp256k1]uint32{}, edSlots: map[ed25519.PubKeyEd25519]uint32{}}
+	g.pool.ctx = ctx
+	return g, nil
 }
 
-// Close releases the context (idempotent).
-func (g *GPU) Close() { g.closeOnce.Do(func() { C.gv_close(g.ctx) }) }
+// Close releases the pinned buffers and the context (idempotent).
+func (g *GPU) Close() {
+	g.closeOnce.Do(func() {
+		g.pool.drain()
+		C.gv_close(g.ctx)
+	})
+}
 
 // SetOption forwards to gv_set_option ("max_batch", "lat_max", "pipe_chunk", ...).
 func (g *GPU) SetOption(key string, val int64) error {
@@ -166,24 +269,99 @@ func (g *GPU) SetOption(key string, val int64) error {
 	return nil
 }
 
-// cbuf is a C allocation viewed as a Go byte slice (freed by free()).
+// cbuf is a C allocation viewed as a Go byte slice (returned by free()).
+// Batch buffers come from the context's pinned host memory (gv_host_alloc):
+// the library reads such inputs in place (DMA, or zero-copy for small
+// batches) instead of staging pageable memory through its copy pool, which
+// cost ~47 % of the device rate on one GPU (DESIGN.md §6.4).  They are
+// recycled by power-of-two size class; a failed pinned allocation falls back
+// to C.malloc (the library then stages it, same verdicts).
 type cbuf struct {
-	p unsafe.Pointer
-	b []byte
+	p     unsafe.Pointer
+	b     []byte
+	class int // size class (pinned), -1: C.malloc
+	pool  *pinnedPool
 }
 
-func newCBuf(n int) cbuf {
+// pinnedPool: free lists of gv_host_alloc buffers per size class 2^k bytes,
+// at most pinnedKeep bytes parked in all.
+type pinnedPool struct {
+	ctx    *C.gv_ctx
+	mu     sync.Mutex
+	free   [32][]unsafe.Pointer
+	parked int
+}
+
+const pinnedKeep = 1 << 30
+
+func (p *pinnedPool) get(n int) cbuf {
+	k := bits.Len(uint(n - 1))
+	if k < 12 {
+		k = 12 // 4 KiB minimum class
+	}
+	if k < 32 {
+		p.mu.Lock()
+		if l := len(p.free[k]); l > 0 {
+			ptr := p.free[k][l-1]
+			p.free[k] = p.free[k][:l-1]
+			p.parked -= 1 << k
+			p.mu.Unlock()
+			return cbuf{ptr, (*[maxBatchBytes]byte)(ptr)[:n:n], k, p}
+		}
+		p.mu.Unlock()
+		var ptr unsafe.Pointer
+		if p.ctx != nil && C.gv_host_alloc(p.ctx, C.size_t(1)<<uint(k), &ptr) == 0 {
+			return cbuf{ptr, (*[maxBatchBytes]byte)(ptr)[:n:n], k, p}
+		}
+	}
+	ptr := C.malloc(C.size_t(n))
+	return cbuf{ptr, (*[maxBatchBytes]byte)(ptr)[:n:n], -1, nil}
+}
+
+func (p *pinnedPool) put(c cbuf) {
+	p.mu.Lock()
+	if p.parked+(1<<c.class) <= pinnedKeep {
+		p.free[c.class] = append(p.free[c.class], c.p)
+		p.parked += 1 << c.class
+		p.mu.Unlock()
+		return
+	}
+	p.mu.Unlock()
+	C.gv_host_free(p.ctx, c.p)
+}
+
+func (p *pinnedPool) drain() {
+	p.mu.Lock()
+	defer p.mu.Unlock()
+	for k := range p.free {
+		for _, ptr := range p.free[k] {
+			C.gv_host_free(p.ctx, ptr)
+		}
+		p.free[k] = nil
+	}
+	p.parked = 0
+}
+
+func (g *GPU) newCBuf(n int) cbuf {
 	if n < 1 {
 		n = 1
 	}
-	p := C.malloc(C.size_t(n))
-	return cbuf{p, (*[maxBatchBytes]byte)(p)[:n:n]}
+	return g.pool.get(n)
 }
-func (c cbuf) free() { C.free(c.p) }
+
+func (c cbuf) free() {
+	if c.class < 0 {
+		C.free(c.p)
+		return
+	}
+	c.pool.put(c)
+}
 
 // VerifyBatch implements Verifier with the routing policy of the GPU type.
 func (g *GPU) VerifyBatch(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]byte) []bool {
 	if len(pubs) < g.CPUBelow {
+		atomic.AddUint64(&g.cnt.cpuRouted, 1)
+		atomic.AddUint64(&g.cnt.cpuRoutedLeaves, uint64(len(pubs)))
 		return CPU{}.VerifyBatch(pubs, msgs, sigs)
 	}
 	if g.Keyed {
@@ -217,7 +395,7 @@ func (g *GPU) VerifyBatchPub33(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]
 		return ok
 	}
 	m := len(idx)
-	pub, sig, blob, off, ln, out := newCBuf(33*m), newCBuf(64*m), newCBuf(total), newCBuf(8*m), newCBuf(4*m), newCBuf(m)
+	pub, sig, blob, off, ln, out := g.newCBuf(33*m), g.newCBuf(64*m), g.newCBuf(total), g.newCBuf(8*m), g.newCBuf(4*m), g.newCBuf(m)
 	defer func() { pub.free(); sig.free(); blob.free(); off.free(); ln.free(); out.free() }()
 	o := (*[maxBatchBytes / 8]uint64)(off.p)[:m:m]
 	l := (*[maxBatchBytes / 4]uint32)(ln.p)[:m:m]
@@ -228,8 +406,11 @@ func (g *GPU) VerifyBatchPub33(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]
 		o[k], l[k] = uint64(pos), uint32(len(msgs[i]))
 		pos += copy(blob.b[pos:], msgs[i])
 	}
+	t0 := time.Now()
 	rc := C.gv_verify_msgs(g.ctx, C.size_t(m), (*C.uint8_t)(pub.p), (*C.uint8_t)(sig.p), (*C.uint8_t)(blob.p),
 		(*C.uint64_t)(off.p), (*C.uint32_t)(ln.p), (*C.uint8_t)(out.p))
+	atomic.AddUint64(&g.cnt.pub33, 1)
+	g.done("gv_verify_msgs", m, time.Since(t0), rc)
 	for k, i := range idx {
 		if rc == 0 {
 			ok[i] = out.b[k] == 1
@@ -280,7 +461,7 @@ func (g *GPU) VerifyBatchEd25519Pub(pubs []ed25519.PubKeyEd25519, msgs, sigs [][
 		return ok
 	}
 	m := len(idx)
-	pub, sig, blob, off, ln, out := newCBuf(32*m), newCBuf(64*m), newCBuf(total), newCBuf(8*m), newCBuf(4*m), newCBuf(m)
+	pub, sig, blob, off, ln, out := g.newCBuf(32*m), g.newCBuf(64*m), g.newCBuf(total), g.newCBuf(8*m), g.newCBuf(4*m), g.newCBuf(m)
 	defer func() { pub.free(); sig.free(); blob.free(); off.free(); ln.free(); out.free() }()
 	o := (*[maxBatchBytes / 8]uint64)(off.p)[:m:m]
 	l := (*[maxBatchBytes / 4]uint32)(ln.p)[:m:m]
@@ -291,8 +472,11 @@ func (g *GPU) VerifyBatchEd25519Pub(pubs []ed25519.PubKeyEd25519, msgs, sigs [][
 		o[k], l[k] = uint64(pos), uint32(len(msgs[i]))
 		pos += copy(blob.b[pos:], msgs[i])
 	}
+	t0 := time.Now()
 	rc := C.gv_verify_ed25519_msgs(g.ctx, C.size_t(m), (*C.uint8_t)(pub.p), (*C.uint8_t)(sig.p), (*C.uint8_t)(blob.p),
 		(*C.uint64_t)(off.p), (*C.uint32_t)(ln.p), (*C.uint8_t)(out.p))
+	atomic.AddUint64(&g.cnt.ed, 1)
+	g.done("gv_verify_ed25519_msgs", m, time.Since(t0), rc)
 	for k, i := range idx {
 		if rc == 0 {
 			ok[i] = out.b[k] == 1
@@ -336,17 +520,19 @@ func (g *GPU) slotsLocked(pubs []secp256k1.PubKeySecp256k1, load bool) (slots []
 		return slots, loaded, false
 	}
 	if int(C.gv_keys_count(g.ctx))+len(fresh) > g.KeyCap { // start the arena over (the C++ mirror's rule)
+		atomic.AddUint64(&g.cnt.keyResets, 1)
 		C.gv_keys_reset(g.ctx)
 		g.slots = map[secp256k1.PubKeySecp256k1]uint32{}
 		g.slotGen = uint64(C.gv_keys_generation(g.ctx))
 		return g.slotsLocked(pubs, len(pubs) <= g.KeyCap)
 	}
-	buf := newCBuf(33 * len(fresh))
-	out := newCBuf(4 * len(fresh))
+	buf := g.newCBuf(33 * len(fresh))
+	out := g.newCBuf(4 * len(fresh))
 	defer func() { buf.free(); out.free() }()
 	for k, p := range fresh {
 		copy(buf.b[33*k:], p[:])
 	}
+	atomic.AddUint64(&g.cnt.keyLoads, 1)
 	if C.gv_keys_load(g.ctx, C.size_t(len(fresh)), (*C.uint8_t)(buf.p), (*C.uint32_t)(out.p)) == 0 {
 		s := (*[maxBatchBytes / 4]uint32)(out.p)[:len(fresh):len(fresh)]
 		for k, p := range fresh {
@@ -415,8 +601,8 @@ func (g *GPU) VerifyBatchKeyed(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]
 	var out cbuf
 	if len(keyed) > 0 {
 		m := len(keyed)
-		sl, sig, blob, off, ln := newCBuf(4*m), newCBuf(64*m), newCBuf(total), newCBuf(8*m), newCBuf(4*m)
-		out = newCBuf(m)
+		sl, sig, blob, off, ln := g.newCBuf(4*m), g.newCBuf(64*m), g.newCBuf(total), g.newCBuf(8*m), g.newCBuf(4*m)
+		out = g.newCBuf(m)
 		s := (*[maxBatchBytes / 4]uint32)(sl.p)[:m:m]
 		o := (*[maxBatchBytes / 8]uint64)(off.p)[:m:m]
 		l := (*[maxBatchBytes / 4]uint32)(ln.p)[:m:m]
@@ -427,8 +613,11 @@ func (g *GPU) VerifyBatchKeyed(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]
 			o[k], l[k] = uint64(pos), uint32(len(msgs[i]))
 			pos += copy(blob.b[pos:], msgs[i])
 		}
+		t0 := time.Now()
 		rc = C.gv_verify_msgs_keyed(g.ctx, C.size_t(m), (*C.uint32_t)(sl.p), (*C.uint8_t)(sig.p), (*C.uint8_t)(blob.p),
 			(*C.uint64_t)(off.p), (*C.uint32_t)(ln.p), (*C.uint8_t)(out.p))
+		atomic.AddUint64(&g.cnt.keyed, 1)
+		g.done("gv_verify_msgs_keyed", m, time.Since(t0), rc)
 		sl.free()
 		sig.free()
 		blob.free()
@@ -484,21 +673,23 @@ func (g *GPU) edSlotsLocked(pubs []ed25519.PubKeyEd25519, load bool) (slots []ui
 	if len(fresh) == 0 {
 		return slots, true
 	}
-	if !load || len(fresh) > DefaultEdKeyCap {
+	if !load || len(fresh) > g.EdKeyCap {
 		return slots, false
 	}
-	if int(C.gv_ed_keys_count(g.ctx))+len(fresh) > DefaultEdKeyCap { // start the arena over (the C++ mirror's rule)
+	if int(C.gv_ed_keys_count(g.ctx))+len(fresh) > g.EdKeyCap { // start the arena over (the C++ mirror's rule)
+		atomic.AddUint64(&g.cnt.keyResets, 1)
 		C.gv_ed_keys_reset(g.ctx)
 		g.edSlots = map[ed25519.PubKeyEd25519]uint32{}
 		g.edGen = uint64(C.gv_ed_keys_generation(g.ctx))
 		return g.edSlotsLocked(pubs, true)
 	}
-	buf := newCBuf(32 * len(fresh))
-	out := newCBuf(4 * len(fresh))
+	buf := g.newCBuf(32 * len(fresh))
+	out := g.newCBuf(4 * len(fresh))
 	defer func() { buf.free(); out.free() }()
 	for k, p := range fresh {
 		copy(buf.b[32*k:], p[:])
 	}
+	atomic.AddUint64(&g.cnt.keyLoads, 1)
 	if C.gv_ed_keys_load(g.ctx, C.size_t(len(fresh)), (*C.uint8_t)(buf.p), (*C.uint32_t)(out.p)) != 0 {
 		return slots, false
 	}
@@ -546,7 +737,7 @@ func (g *GPU) verifyEdKeyed(pubs []ed25519.PubKeyEd25519, msgs, sigs [][]byte, l
 		return g.VerifyBatchEd25519Pub(pubs, msgs, sigs)
 	}
 	m := len(idx)
-	sl, sig, blob, off, ln, out := newCBuf(4*m), newCBuf(64*m), newCBuf(total), newCBuf(8*m), newCBuf(4*m), newCBuf(m)
+	sl, sig, blob, off, ln, out := g.newCBuf(4*m), g.newCBuf(64*m), g.newCBuf(total), g.newCBuf(8*m), g.newCBuf(4*m), g.newCBuf(m)
 	defer func() { sl.free(); sig.free(); blob.free(); off.free(); ln.free(); out.free() }()
 	sv := (*[maxBatchBytes / 4]uint32)(sl.p)[:m:m]
 	o := (*[maxBatchBytes / 8]uint64)(off.p)[:m:m]
@@ -558,9 +749,12 @@ func (g *GPU) verifyEdKeyed(pubs []ed25519.PubKeyEd25519, msgs, sigs [][]byte, l
 		o[k], l[k] = uint64(pos), uint32(len(msgs[i]))
 		pos += copy(blob.b[pos:], msgs[i])
 	}
+	t0 := time.Now()
 	rc := C.gv_verify_ed25519_msgs_keyed(g.ctx, C.size_t(m), (*C.uint32_t)(sl.p), (*C.uint8_t)(sig.p),
 		(*C.uint8_t)(blob.p), (*C.uint64_t)(off.p), (*C.uint32_t)(ln.p), (*C.uint8_t)(out.p))
 	g.mu.Unlock()
+	atomic.AddUint64(&g.cnt.ed, 1)
+	g.done("gv_verify_ed25519_msgs_keyed", m, time.Since(t0), rc)
 	for k, i := range idx {
 		if rc == 0 {
 			ok[i] = out.b[k] == 1

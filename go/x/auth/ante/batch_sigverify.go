@@ -342,7 +342,19 @@ func (b *batch) resolveEd(v gv.Verifier, cache *gv.VerdictCache) {
 // which touches no state -- sign bytes on every core, then the batch -- so a
 // caller can release its state lock before the GPU call (baseapp Ingress).
 func NewPreVerifier(ak AccountKeeper, v gv.Verifier, cache *gv.VerdictCache) func(ctx sdk.Context, txs []sdk.Tx) func() {
-	return func(ctx sdk.Context, txs []sdk.Tx) func() {
+	ahead := NewPreVerifierAhead(ak, v, cache)
+	return func(ctx sdk.Context, txs []sdk.Tx) func() { return ahead(ctx, nil, txs) }
+}
+
+// NewPreVerifierAhead is NewPreVerifier with a carry: txs that run before the
+// batch but whose effects are not in ctx's state yet (block h while block h+1
+// is pre-verified, baseapp.PreVerifyAhead).  Each carry tx advances every
+// signer's predicted sequence by one (IncrementSequenceDecorator), and a key
+// it supplies for an account without one is the key SetPubKeyDecorator will
+// have stored -- the C++ mirror's carry (gvhost.cpp gvh_deliver_blocks: own,
+// own_info).  The carry's leaves are not verified.
+func NewPreVerifierAhead(ak AccountKeeper, v gv.Verifier, cache *gv.VerdictCache) func(ctx sdk.Context, carry, txs []sdk.Tx) func() {
+	return func(ctx sdk.Context, carry, txs []sdk.Tx) func() {
 		// Reads go through a context with its own infinite gas meter: the
 		// hook runs outside any tx and must not charge a block or tx meter.
 		look := ctx.WithGasMeter(sdk.NewInfiniteGasMeter())
@@ -354,6 +366,28 @@ func NewPreVerifier(ak AccountKeeper, v gv.Verifier, cache *gv.VerdictCache) fun
 		}
 		var jobs []job
 		bump := map[string]uint64{}
+		stored := map[string]crypto.PubKey{} // keys the carry's SetPubKey stores
+		for _, tx := range carry {
+			sigTx, ok := tx.(SigVerifiableTx)
+			if !ok {
+				continue
+			}
+			signers, txPks := sigTx.GetSigners(), sigTx.GetPubKeys()
+			for i, a := range signers {
+				if i >= len(txPks) || txPks[i] == nil {
+					continue
+				}
+				if _, have := stored[a.String()]; have {
+					continue
+				}
+				if acc := ak.GetAccount(look, a); acc != nil && acc.GetPubKey() == nil {
+					stored[a.String()] = txPks[i]
+				}
+			}
+			for _, a := range signers {
+				bump[a.String()]++
+			}
+		}
 		for _, tx := range txs {
 			sigTx, ok := tx.(SigVerifiableTx)
 			if !ok {
@@ -366,6 +400,9 @@ func NewPreVerifier(ak AccountKeeper, v gv.Verifier, cache *gv.VerdictCache) fun
 					continue
 				}
 				pk := acc.GetPubKey()
+				if pk == nil {
+					pk = stored[signers[i].String()] // stored by a carry tx's SetPubKey
+				}
 				if pk == nil && i < len(txPks) {
 					pk = txPks[i] // SetPubKeyDecorator will store the tx-supplied key
 				}
@@ -382,6 +419,9 @@ func NewPreVerifier(ak AccountKeeper, v gv.Verifier, cache *gv.VerdictCache) fun
 		// Sign bytes (JSON) on every core, then one batch.  The workers touch
 		// no store and no gas meter: GetSignBytes reads only the chain id and
 		// height of the context and the job's own account copy.
+		if len(jobs) == 0 {
+			return nil
+		}
 		return func() {
 			parts := make([]batch, runtime.NumCPU())
 			var wg sync.WaitGroup

@@ -57,12 +57,35 @@ type CommitCheck struct {
 	Commit     *tmtypes.Commit
 	Trusting   bool
 	TrustLevel tmmath.Fraction
+	// KeysTrusted: Vals is a set the client already trusts (the trusted
+	// next-validator set of VerifyCommitTrusting, or an adjacent header's set
+	// whose hash equals the trusted header's NextValidatorsHash).  Only such
+	// sets' keys go through the resident-key path (gv.EdKeyCache): a set
+	// supplied by an arbitrary relayer is verified without loading its keys,
+	// so fresh keys in every MsgUpdateClient cannot churn the key arena and
+	// evict the honest sets it keeps.
+	KeysTrusted bool
 }
 
 // leaf: one signature a check's loop could read, and its batch position.
 type leaf struct {
-	val  int // validator index in the check's set
-	item int // batch item, -1: VerifyBytes is false without verifying (len(sig) != 64)
+	val   int // validator index in the check's set
+	item  int // batch item, -1: VerifyBytes is false without verifying (len(sig) != 64)
+	plain bool // item indexes the plain (untrusted keys) batch
+}
+
+// edBatch gathers one verification batch.
+type edBatch struct {
+	pubs       []ed25519.PubKeyEd25519
+	msgs, sigs [][]byte
+	ok         []bool
+}
+
+func (b *edBatch) add(pk ed25519.PubKeyEd25519, msg, sig []byte) int {
+	b.pubs = append(b.pubs, pk)
+	b.msgs = append(b.msgs, msg)
+	b.sigs = append(b.sigs, sig)
+	return len(b.pubs) - 1
 }
 
 // VerifyCommits returns, for each check, exactly the error the reference
@@ -72,8 +95,7 @@ type leaf struct {
 func VerifyCommits(ev gv.EdVerifier, checks []CommitCheck) []error {
 	errs := make([]error, len(checks))
 	leaves := make([][]leaf, len(checks))
-	var pubs []ed25519.PubKeyEd25519
-	var msgs, sigs [][]byte
+	var cached, plain edBatch // trusted sets' keys may stay resident; untrusted sets' are not loaded
 	for c, k := range checks {
 		if k.Trusting {
 			if k.TrustLevel.Numerator*3 < k.TrustLevel.Denominator || // < 1/3
@@ -106,24 +128,31 @@ func VerifyCommits(ev gv.EdVerifier, checks []CommitCheck) []error {
 			if !ok || len(cs.Signature) != ed25519.SignatureSize {
 				continue // resolved one at a time below (non-ed25519 key) or false (length)
 			}
-			lv[idx].item = len(pubs)
-			pubs = append(pubs, pk)
-			msgs = append(msgs, k.Commit.VoteSignBytes(k.ChainID, idx))
-			sigs = append(sigs, cs.Signature)
+			msg := k.Commit.VoteSignBytes(k.ChainID, idx)
+			if k.KeysTrusted {
+				lv[idx].item = cached.add(pk, msg, cs.Signature)
+			} else {
+				lv[idx].item, lv[idx].plain = plain.add(pk, msg, cs.Signature), true
+			}
 		}
 		leaves[c] = lv
 	}
-	var ok []bool
-	if len(pubs) > 0 {
-		if kc, cached := ev.(gv.EdKeyCache); cached {
-			ok = kc.VerifyBatchEd25519Cached(pubs, msgs, sigs) // validator sets repeat: their keys stay resident
+	if len(cached.pubs) > 0 {
+		if kc, isCache := ev.(gv.EdKeyCache); isCache {
+			cached.ok = kc.VerifyBatchEd25519Cached(cached.pubs, cached.msgs, cached.sigs) // trusted sets repeat
 		} else {
-			ok = ev.VerifyBatchEd25519(pubs, msgs, sigs)
+			cached.ok = ev.VerifyBatchEd25519(cached.pubs, cached.msgs, cached.sigs)
 		}
+	}
+	if len(plain.pubs) > 0 {
+		plain.ok = ev.VerifyBatchEd25519(plain.pubs, plain.msgs, plain.sigs)
 	}
 	verdict := func(k CommitCheck, lf leaf, idx int) bool {
 		if lf.item >= 0 {
-			return ok[lf.item]
+			if lf.plain {
+				return plain.ok[lf.item]
+			}
+			return cached.ok[lf.item]
 		}
 		cs := k.Commit.Signatures[idx]
 		if _, isEd := k.Vals.Validators[lf.val].PubKey.(ed25519.PubKeyEd25519); isEd {
@@ -236,13 +265,17 @@ func BatchVerify(ev gv.EdVerifier, chainID string, trustedHeader *tmtypes.Signed
 			return errors.Errorf("expected old header next validators (%X) to match those from new header (%X)",
 				trustedHeader.NextValidatorsHash, untrustedHeader.ValidatorsHash)
 		}
+		// untrustedVals hashes to the trusted header's next validators (checked
+		// just above and in verifyNewHeaderAndVals): a trusted set
+		full.KeysTrusted = true
 		if err := VerifyCommits(ev, []CommitCheck{full})[0]; err != nil {
 			return lite.ErrInvalidHeader{Reason: err}
 		}
 		return nil
 	}
 	trusted := CommitCheck{Vals: trustedNextVals, ChainID: chainID, BlockID: untrustedHeader.Commit.BlockID,
-		Height: untrustedHeader.Height, Commit: untrustedHeader.Commit, Trusting: true, TrustLevel: trustLevel}
+		Height: untrustedHeader.Height, Commit: untrustedHeader.Commit, Trusting: true, TrustLevel: trustLevel,
+		KeysTrusted: true}
 	errs := VerifyCommits(ev, []CommitCheck{trusted, full})
 	if err := errs[0]; err != nil {
 		switch e := err.(type) {
@@ -291,9 +324,9 @@ func CheckMisbehaviourCommits(ev gv.EdVerifier, trusted *tmtypes.ValidatorSet, c
 	h1, h2 *tmtypes.SignedHeader) error {
 	errs := VerifyCommits(ev, []CommitCheck{
 		{Vals: trusted, ChainID: chainID, BlockID: h1.Commit.BlockID, Height: h1.Height, Commit: h1.Commit,
-			Trusting: true, TrustLevel: lite.DefaultTrustLevel},
+			Trusting: true, TrustLevel: lite.DefaultTrustLevel, KeysTrusted: true},
 		{Vals: trusted, ChainID: chainID, BlockID: h2.Commit.BlockID, Height: h2.Height, Commit: h2.Commit,
-			Trusting: true, TrustLevel: lite.DefaultTrustLevel},
+			Trusting: true, TrustLevel: lite.DefaultTrustLevel, KeysTrusted: true},
 	})
 	if errs[0] != nil {
 		return fmt.Errorf("validator set in header 1 has too much change from last known validator set: %v", errs[0])

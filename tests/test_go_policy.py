@@ -42,7 +42,7 @@ def test_policy_constants_shared_by_go_and_cpp():
     assert re.search(r"DefaultEdKeyCap\s*=\s*int\(C\.GV_ED_KEY_CAP\)", go)
     opener = go[go.index("func Open("):go.index("func (g *GPU) Close()")]
     for field in ("CPUBelow: DefaultCPUBelow", "Keyed: true", "KeyLoadMin: DefaultKeyLoadMin",
-                  "KeyCap: DefaultKeyCap"):
+                  'KeyCap: envInt("GV_KEY_CAP", DefaultKeyCap)', 'EdKeyCap: envInt("GV_ED_KEY_CAP", DefaultEdKeyCap)'):
         assert field in opener, field
 
 
@@ -66,6 +66,10 @@ def test_go_decorator_charges_reads_in_reference_order():
     assert "d.gather(ctx.WithGasMeter(sdk.NewInfiniteGasMeter())" in ah
     loop = ah[ah.index("for i, sig := range sigs"):]
     assert loop.index("GetSignerAcc(ctx, d.ak, signerAddrs[i])") < loop.index("exprs[i].eval(&b)")
+    # sign bytes right after the account read, before the nil-key check and the
+    # simulate bypass (sigverify.go:201-207)
+    assert loop.index("GetSignerAcc(ctx") < loop.index("sigTx.GetSignBytes(ctx, acc)") < \
+        loop.index("pubKey == nil") < loop.index("if simulate {")
     assert "return ctx, sdkerrors.Wrap(sdkerrors.ErrUnauthorized" in loop
     gather = go[go.index("func (d BatchSigVerificationDecorator) gather("):go.index("func signBytesNoPanic(")]
     assert "d.ak.GetAccount(look," in gather and "GetSignerAcc(ctx" not in gather
@@ -103,11 +107,14 @@ def test_go_ed25519_routes_like_the_mirror():
     ek = go[go.index("func (g *GPU) verifyEdKeyed("):]
     lock, unlock = ek.index("g.mu.Lock()"), ek.rindex("g.mu.Unlock()")
     assert lock < ek.index("edSlotsLocked") < ek.index("gv_verify_ed25519_msgs_keyed") < unlock
-    assert "DefaultEdKeyCap" in go[go.index("func (g *GPU) edSlotsLocked("):]
+    assert "g.EdKeyCap" in go[go.index("func (g *GPU) edSlotsLocked("):]
     ibc = strip_comments(read("go", "x", "ibc", "07-tendermint", "batch_verify.go"))
-    assert "ev.(gv.EdKeyCache)" in ibc and "VerifyBatchEd25519Cached(pubs, msgs, sigs)" in ibc
+    # only trusted validator sets go through the resident-key path
+    assert "ev.(gv.EdKeyCache)" in ibc and "VerifyBatchEd25519Cached(cached.pubs, cached.msgs, cached.sigs)" in ibc
+    assert "plain.ok = ev.VerifyBatchEd25519(plain.pubs, plain.msgs, plain.sigs)" in ibc
+    assert "if k.KeysTrusted {" in ibc and ibc.count("KeysTrusted: true") == 3 and "full.KeysTrusted = true" in ibc
     cpp = read("cosmos-sdk-rootchain_amd", "host", "gvhost.cpp")
     assert "GV_ED_KEY_CAP" in cpp[cpp.index("int verify_ed("):]
     assert "me >= app->key_load_min" in cpp
     commits = cpp[cpp.index('extern "C" int gvh_verify_commits('):]
-    assert re.search(r"verify_ed\(app, m,[^;]*true\)", commits)
+    assert re.search(r"verify_ed\(app, e\.m,[^;]*t == 0\)", commits) and "k.keys_trusted ? 0 : 1" in commits

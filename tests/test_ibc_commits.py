@@ -186,7 +186,7 @@ def test_one_gpu_batch_for_many_commits(app):
         s = ch.commit(100 + h, [COMMIT] * 100)
         if h % 5 == 0:
             s = flip(s, int(rng.integers(100)))
-        cs.append({"vals": ch.vals, "sigs": s})
+        cs.append({"vals": ch.vals, "sigs": s, "keys_trusted": True})   # adjacent: the trusted next set
     c0 = app.stats()["gpu_calls"]
     got = app.verify_commits(cs)
     assert app.stats()["gpu_calls"] - c0 == 1
@@ -198,3 +198,27 @@ def test_one_gpu_batch_for_many_commits(app):
     # spot-check against the restatement (pure-Python ed25519 is slow)
     for h in (0, 1, 5, 63):
         assert got[h] == ref(cs[h])
+
+
+@pytest.mark.gpu
+def test_untrusted_sets_do_not_load_keys(app):
+    """a relayer-supplied validator set (VerifyNonAdjacent's new set)
+    is verified without loading its keys into the ed25519 key arena, so fresh
+    keys in every update cannot churn the arena; the trusted set's keys are
+    loaded (they sign block after block).  Same verdicts either way."""
+    wl = _signer()
+    rng = np.random.default_rng(11)
+    v = app._v
+    v.ed_keys_reset()
+    fresh = Chain(wl, rng, 30)
+    s = fresh.commit(500, [COMMIT] * 30)
+    s = flip(s, 7)
+    untrusted = {"vals": fresh.vals, "sigs": s}                  # keys_trusted defaults to trusting (False)
+    got = app.verify_commits([untrusted])
+    assert got == [ref(untrusted)] and got[0][0] == "wrong_sig"
+    assert v.ed_keys_count() == 0
+    trusted = {"vals": fresh.vals, "sigs": fresh.commit(501, [COMMIT] * 30), "keys_trusted": True}
+    got = app.verify_commits([trusted])
+    assert got == [ref(trusted)] and got[0][0] == "ok"
+    assert v.ed_keys_count() == 30
+    v.ed_keys_reset()
