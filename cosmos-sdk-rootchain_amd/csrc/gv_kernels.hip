@@ -450,6 +450,11 @@ GV_DEV sc29 sc29_shfl(const sc29& a, int mode, int d) {
   return r;
 }
 
+// GV_SINV_DIVSTEPS (default 1): the shared inversion by var-time divsteps
+// instead of the Fermat chain s^(n-2) (0: A/B).
+#ifndef GV_SINV_DIVSTEPS
+#define GV_SINV_DIVSTEPS 1
+#endif
 // Batch inversion across the wavefront: every lane holds a nonzero x
 // (Montgomery form); returns x^-1 (Montgomery form).  All 64 lanes active.
 // Prefix/suffix products by Hillis-Steele scans (6 steps each) + one Fermat
@@ -469,7 +474,25 @@ GV_DEV void sc29_batch_inv_wave(sc29& inv, const sc29& x) {
     for (int i = 0; i < 9; ++i) suf.n[i] = (lane + (u32)d < 64u) ? m.n[i] : suf.n[i];
   }
   sc29 tot = sc29_shfl(pre, 2, 63), tinv, one;
+#if GV_SINV_DIVSTEPS
+  {
+    // every lane inverts the same total, so the variable-time divsteps
+    // (secp_modinv.cuh, ~1/10 of the Fermat chain's instructions) never
+    // diverge: Montgomery -> plain, x^-1, plain -> Montgomery
+    sc29 p1, xp;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) p1.n[i] = i == 0 ? 1u : 0u;
+    sc29_mul(xp, tot, p1);                     // tot * 1 / R = x
+    u32 xw[8], iw[8];
+    sc29_to_words(xw, xp);
+    s30_modinv_var(iw, xw, []() {});
+    sc29 ip;
+    sc29_from_words(ip, iw);
+    sc29_to_mont(tinv, ip);
+  }
+#else
   sc29_inv(tinv, tot);
+#endif
   sc29_mont_one(one);
   sc29 pe = sc29_shfl(pre, 0, 1), se = sc29_shfl(suf, 1, 1), m;
   if (lane == 0) pe = one;
@@ -721,7 +744,7 @@ __global__ __launch_bounds__(256) void k_keys_chain(u32 n, u32 C, const u32* in_
 #pragma unroll 1
   for (int grp = 1; grp < GV_LGRP; ++grp) {
 #pragma unroll 1
-    for (int k = grp_bit[grp - 1]; k < grp_bit[grp]; ++k) gej29_double(q, q);   // never infinite: odd order
+    for (int k = grp_bit[grp - 1]; k < grp_bit[grp]; ++k) gej29x_double(q, q);  // never infinite: odd order
     u32 xw[8], yw[8];
     f29_to_words(xw, q.x);
     f29_to_words(yw, q.y);

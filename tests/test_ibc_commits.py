@@ -216,9 +216,9 @@ def test_untrusted_sets_do_not_load_keys(app):
     untrusted = {"vals": fresh.vals, "sigs": s}                  # keys_trusted defaults to trusting (False)
     got = app.verify_commits([untrusted])
     assert got == [ref(untrusted)] and got[0][0] == "wrong_sig"
-    assert v.ed_keys_count() == 0
+    assert v.ed_keys_count == 0
     trusted = {"vals": fresh.vals, "sigs": fresh.commit(501, [COMMIT] * 30), "keys_trusted": True}
     got = app.verify_commits([trusted])
     assert got == [ref(trusted)] and got[0][0] == "ok"
-    assert v.ed_keys_count() == 30
+    assert v.ed_keys_count == 30
     v.ed_keys_reset()
