@@ -59,6 +59,11 @@ typedef struct gvk_batch {
   // batches' front kernels then fill the previous ladder's tail.
   hipStream_t st_ecm;
   hipEvent_t ecm_ready;
+  // Consecutive pipelined calls may run their ladders on two streams (the
+  // next ladder fills the current one's tail): the call's final bitmap write
+  // (k_unsort_bits, or the ladder itself when unsorted) waits on bits_wait
+  // (the previous call's) and records bits_done, so results land in call order.
+  hipEvent_t bits_wait, bits_done;
   int unpacked;                 // the SoA rows are already written (in-batch key grouping ran k_unpack)
   hipEvent_t keys_ready;        // optional: the batch's key tables are built on another stream; k_prep waits
   // keyed batch (kslot != NULL, pub33 unused): item i's key is arena slot kslot[i]

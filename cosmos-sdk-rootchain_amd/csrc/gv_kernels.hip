@@ -414,6 +414,18 @@ GV_DEV void build_q_table(u32* qt, u32 qi, u32* qr, u32 C, u32 g, const fe& qx8,
   f29_to_words(zq8.v, t);
 }
 
+// GV_FRONT_VGPR: VGPR cap of the front kernels (k_keys_chain, k_keys_tables,
+// k_scalar_inv), so that a front wave fits beside three ladder waves
+// (k_ecmult_k4 / k6: 134 VGPRs) and the next call's front runs under the
+// current ladder instead of after it (0: compiler's choice).
+#ifndef GV_FRONT_VGPR
+#define GV_FRONT_VGPR 0
+#endif
+#if GV_FRONT_VGPR
+#define GV_FRONT_ATTR __attribute__((amdgpu_waves_per_eu(512 / GV_FRONT_VGPR)))
+#else
+#define GV_FRONT_ATTR
+#endif
 // ------------------------------------------------------------- k_scalar_inv
 // w = s^-1 mod n for every lane, Montgomery form (radix 2^29, R = 2^261,
 // secp_sc29.cuh), by Montgomery's trick: each lane folds GV_INV_M signatures
@@ -501,7 +513,7 @@ GV_DEV void sc29_batch_inv_wave(sc29& inv, const sc29& x) {
   sc29_mul(inv, m, tinv);
 }
 
-__global__ __launch_bounds__(256) void k_scalar_inv(u32 C, const u32* in_s, u32* w, u32* pre) {
+__global__ __launch_bounds__(256) GV_FRONT_ATTR void k_scalar_inv(u32 C, const u32* in_s, u32* w, u32* pre) {
   const u32 lane = threadIdx.x & 63u;
   const u32 wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   sc29 acc;
@@ -717,7 +729,7 @@ GV_DEV void gej29_to_affine_words(fe& x8, fe& y8, const gej29& p) {
 // 1..3 in their Z rows (kzq2), group 0 is affine.
 // K6: the k6 group offsets (kK6GrpBit) and 32-entry table rows.
 template <bool K6 = false>
-__global__ __launch_bounds__(256) void k_keys_chain(u32 n, u32 C, const u32* in_x, const u32* in_pfx, u32 base,
+__global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_chain(u32 n, u32 C, const u32* in_x, const u32* in_pfx, u32 base,
                                                      u32* kqt, u32 kC, u32* kok, u32* kqt2, u32* kzq2) {
   constexpr int NT = K6 ? GV_K6_NT : GV_QTAB_N;
   const int* grp_bit = K6 ? kK6GrpBit : kLGrpBit;
@@ -770,7 +782,7 @@ __global__ __launch_bounds__(256) void k_keys_chain(u32 n, u32 C, const u32* in_
 // 80 B each, twice, and read them back in between).
 // NT: entries per group table (16; GV_K6_NT for the k6 tables).
 template <int NT = GV_QTAB_N>
-__global__ __launch_bounds__(256) void k_keys_tables(u32 n, u32 C4, u32 base, u32* kqt, u32* kzq, u32 kC, u32* kqt2,
+__global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_tables(u32 n, u32 C4, u32 base, u32* kqt, u32* kzq, u32 kC, u32* kqt2,
                                                       u32* kzq2, u32* qr, u32* qe) {
   const u32 L = blockIdx.x * blockDim.x + threadIdx.x;
   const u32 key = L >> 2, grp = L & 3u;
@@ -1528,6 +1540,7 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
     se = b->st_ecm;
   }
   if (b->ev_ecm_start) (void)hipEventRecord(b->ev_ecm_start, se);
+  if (b->bits_wait && !sorted) (void)hipStreamWaitEvent(se, b->bits_wait, 0);   // the ladder writes the bits
   if (k6)
     hipLaunchKernelGGL(gv::k_ecmult_k6, grd, blk, 0, se, b->gtab6, b->n, C, b->digits, b->kqt, b->kqt2, b->kzq,
                        b->flags, b->in_r, sorted ? b->srt.bits : b->bits, (const uint32_t*)b->in_pfx, b->kC);
@@ -1543,7 +1556,13 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
                        (const uint32_t*)b->qtab, (const uint32_t*)b->zq, b->flags, b->in_r, b->bits,
                        (const uint32_t*)nullptr, 0u);
   if (b->ev[3]) (void)hipEventRecord(b->ev[3], se);
-  if (sorted) return gvk_unsort_bits(b->n, b->srt.pos, b->srt.bits, b->bits, se);
+  if (sorted) {
+    if (b->bits_wait) (void)hipStreamWaitEvent(se, b->bits_wait, 0);
+    const hipError_t e = gvk_unsort_bits(b->n, b->srt.pos, b->srt.bits, b->bits, se);
+    if (b->bits_done) (void)hipEventRecord(b->bits_done, se);
+    return e;
+  }
+  if (b->bits_done) (void)hipEventRecord(b->bits_done, se);
   return hipGetLastError();
 }
 

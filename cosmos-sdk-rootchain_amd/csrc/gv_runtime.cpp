@@ -348,10 +348,12 @@ struct Dev {
   // pipelined device-resident calls on the context stream (gv_dev_verify_*,
   // stream NULL): the front kernels of call k+1 run under call k's ladder
   hipStream_t lo_st[2] = {nullptr, nullptr};
-  hipStream_t hi_st = nullptr;
-  hipEvent_t hi_done = nullptr;                   // the last ladder enqueued on hi_st
+  hipStream_t hi_st[2] = {nullptr, nullptr};      // the ladders of set 0 / set 1 (two_ladders), else hi_st[0]
+  hipEvent_t hi_done[2] = {nullptr, nullptr};     // the last ladder enqueued on hi_st[j]
+  hipEvent_t bits_ev[2] = {nullptr, nullptr};     // the bitmap write of the last pipelined call of set j
+  hipEvent_t bits_wait = nullptr, bits_rec = nullptr;   // the pipelined call being launched (dev_run -> launch)
   hipEvent_t plain_done = nullptr;                // the last non-pipelined call on the context stream
-  bool hi_used = false, plain_used = false;
+  bool hi_used[2] = {false, false}, plain_used = false, bits_used = false;
   uint64_t grouped_batches = 0, grouped_keys = 0;  // in-batch key grouping taken (gv_group_stats)
   uint64_t routes[GV_ROUTES] = {};                // batches per schedule (gv_route_stats)
   int flip = 0;
@@ -631,8 +633,12 @@ struct gv_ctx {
                                 // verdict bytes to pinned memory directly: no H2D, memset or D2H (GV_LAT_ZC=0: A/B)
   bool lat_sliced = true;       // small batches on k_verify_lat_sl / k_verify_lat16_sl (GV_LAT_SLICED=0: the one-lane-field kernels, A/B)
   bool keyed_k4 = true;         // keyed batches on k_ecmult_k4 (GV_KEYED_K4=0: the 125-doubling ladder, A/B)
-  bool k6 = true;               // grouped batches on k_ecmult_k6: 6-bit Q / 24-bit G windows (GV_K6=0: k4, A/B)
+  bool k6 = false;              // grouped batches on k_ecmult_k6: 6-bit Q / 24-bit G windows, 32-entry key tables
+                                // (GV_K6=1).  Its ladder is 10 % faster than k4's but the doubled key tables cost
+                                // more than that under C2's 16 items per key: 218-220 vs 222M/s (profiles/r04/prio_ab)
   bool pipeline_dev = true;     // pipelined device-resident calls on the context stream (dev_run; GV_PIPELINE=0: A/B)
+  bool two_ladders = true;      // ... whose ladders alternate two high-priority streams, so the next ladder starts in
+                                // the current one's tail (bitmap writes kept in call order; GV_TWO_LADDERS=0: A/B)
   bool group_keys = true;       // pub33 throughput batches parse each distinct key once (group_keys; GV_GROUP_KEYS=0: A/B)
   bool keys_scratch = true;     // key tables: forward entries through coalesced scratch rows (GV_KEYS_SCRATCH=0: A/B)
   bool sort_keys = true;        // keyed k4 batches run their lanes in slot order (gv_sort.hip; GV_SORT_KEYS=0: A/B)
@@ -879,6 +885,8 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
   if (pipelined) {
     b.st_ecm = st_ecm;
     b.ecm_ready = s->ecm_ready;
+    b.bits_wait = d->bits_wait;
+    b.bits_done = d->bits_rec;
   }
   if (small) {
     // small batch: one fused kernel, several lanes per signature (gv_lat.hip)
@@ -942,7 +950,8 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
 // batches and the other calls on the context stream are ordered after every
 // pipelined ladder (hi_done) and the next ladder after them (plain_done).
 void order_after_pipeline(Dev* d, hipStream_t st) {
-  if (d->hi_used) (void)hipStreamWaitEvent(st, d->hi_done, 0);
+  for (int j = 0; j < 2; ++j)
+    if (d->hi_used[j]) (void)hipStreamWaitEvent(st, d->hi_done[j], 0);
 }
 template <class F>
 int dev_run(gv_ctx* ctx, Dev* d, void* stream, size_t n, bool keyed, F&& fn) {
@@ -959,13 +968,22 @@ int dev_run(gv_ctx* ctx, Dev* d, void* stream, size_t n, bool keyed, F&& fn) {
     d->plain_used = true;
     return GV_OK;
   }
-  if (d->plain_used) CK(hipStreamWaitEvent(d->hi_st, d->plain_done, 0));
   const int j = d->flip;
   d->flip ^= 1;
-  const int rc = fn(&d->set[j], d->lo_st[j], d->hi_st);
+  // two_ladders: set j's ladder on hi_st[j], so call k+1's ladder starts in
+  // call k's tail (its front ran under call k's ladder); the bitmap writes
+  // stay in call order through bits_ev.  Else one ladder stream.
+  hipStream_t hs = d->hi_st[ctx->two_ladders ? j : 0];
+  hipEvent_t& hd = d->hi_done[ctx->two_ladders ? j : 0];
+  if (d->plain_used) CK(hipStreamWaitEvent(hs, d->plain_done, 0));
+  d->bits_wait = (ctx->two_ladders && d->bits_used) ? d->bits_ev[j ^ 1] : nullptr;
+  d->bits_rec = ctx->two_ladders ? d->bits_ev[j] : nullptr;
+  const int rc = fn(&d->set[j], d->lo_st[j], hs);
+  d->bits_wait = d->bits_rec = nullptr;
   if (rc) return rc;
-  CK(hipEventRecord(d->hi_done, d->hi_st));
-  d->hi_used = true;
+  CK(hipEventRecord(hd, hs));
+  d->hi_used[ctx->two_ladders ? j : 0] = true;
+  d->bits_used = ctx->two_ladders;
   return GV_OK;
 }
 
@@ -1472,6 +1490,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   parse_size_env("GV_MAX_BATCH", &ctx->max_batch);
   if (const char* k4 = getenv("GV_KEYED_K4")) ctx->keyed_k4 = strcmp(k4, "0") != 0;
   if (const char* k6 = getenv("GV_K6")) ctx->k6 = strcmp(k6, "0") != 0;
+  if (const char* tl = getenv("GV_TWO_LADDERS")) ctx->two_ladders = strcmp(tl, "0") != 0;
   if (const char* ks = getenv("GV_KEYS_SCRATCH")) ctx->keys_scratch = strcmp(ks, "0") != 0;
   if (const char* sk = getenv("GV_SORT_KEYS")) ctx->sort_keys = strcmp(sk, "0") != 0;
   if (const char* ek = getenv("GV_ED_KEYED")) ctx->ed_keyed = strcmp(ek, "0") != 0;
@@ -1491,23 +1510,37 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
     d->pool = ctx->pool;
     if (k > 0) d->worker = new Worker();
     bool ok = hipSetDevice(d->id) == hipSuccess;
+    // Stream priorities of the pipelined device-resident calls (env
+    // GV_LADDER_PRIO): "front" (default) -- the front kernels (unpack, key
+    // grouping, the key-table build on the side stream, s^-1, prep) above the
+    // ladders, so a slot a ladder workgroup frees goes to the next call's
+    // front first and it is done before the current ladder drains; "ladder" --
+    // the ladders above (the round-3 order: the front then runs in the ladder's
+    // tail); "equal".
+    int lo_prio = 0, hi_prio = 0;
+    ok = ok && hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) == hipSuccess;
+    int front_prio = hi_prio, ladder_prio = lo_prio;
+    if (const char* lp = getenv("GV_LADDER_PRIO")) {
+      if (!strcmp(lp, "ladder")) { front_prio = lo_prio; ladder_prio = hi_prio; }
+      else if (!strcmp(lp, "equal")) front_prio = ladder_prio = lo_prio;
+    }
     for (Set* sp : {&d->set[0], &d->set[1], &d->gset})
       ok = ok && hipStreamCreateWithFlags(&sp->st, hipStreamNonBlocking) == hipSuccess &&
            hipEventCreateWithFlags(&sp->last, hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&sp->done, hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&sp->ecm_ready, hipEventDisableTiming) == hipSuccess &&
-           hipStreamCreateWithFlags(&sp->side, hipStreamNonBlocking) == hipSuccess &&
+           hipStreamCreateWithPriority(&sp->side, hipStreamNonBlocking, front_prio) == hipSuccess &&
            hipEventCreateWithFlags(&sp->fork, hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&sp->keys_done, hipEventDisableTiming) == hipSuccess;
-    // pipelined device-resident calls: front kernels on two low-priority
-    // streams (alternating sets), every ladder on one high-priority stream
-    int lo_prio = 0, hi_prio = 0;
-    ok = ok && hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) == hipSuccess;
+    // pipelined device-resident calls: front kernels on two streams
+    // (alternating sets), the ladders on two more (two_ladders)
     for (int j = 0; j < 2; ++j)
-      ok = ok && hipStreamCreateWithPriority(&d->lo_st[j], hipStreamNonBlocking, lo_prio) == hipSuccess;
-    ok = ok && hipStreamCreateWithPriority(&d->hi_st, hipStreamNonBlocking, hi_prio) == hipSuccess &&
-         hipEventCreateWithFlags(&d->hi_done, hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&d->plain_done, hipEventDisableTiming) == hipSuccess;
+      ok = ok && hipStreamCreateWithPriority(&d->lo_st[j], hipStreamNonBlocking, front_prio) == hipSuccess;
+    for (int j = 0; j < 2; ++j)
+      ok = ok && hipStreamCreateWithPriority(&d->hi_st[j], hipStreamNonBlocking, ladder_prio) == hipSuccess &&
+           hipEventCreateWithFlags(&d->hi_done[j], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&d->bits_ev[j], hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&d->plain_done, hipEventDisableTiming) == hipSuccess;
     ok = ok && hipMalloc(&d->gtab, (size_t)2 * GV_GTAB_N * 16 * 4) == hipSuccess &&
          gvk_gen_gtable(d->gtab, d->set[0].st) == hipSuccess && hipStreamSynchronize(d->set[0].st) == hipSuccess;
     ok = ok && hipMalloc(&d->glat, (size_t)GV_GLAT_WORDS * 4) == hipSuccess &&
@@ -1555,9 +1588,10 @@ void gv_close(gv_ctx* ctx) {
     }
     for (auto& rs : d->ring)
       for (auto e : rs) if (e) (void)hipEventDestroy(e);
-    for (hipStream_t t : {d->lo_st[0], d->lo_st[1], d->hi_st})
+    for (hipStream_t t : {d->lo_st[0], d->lo_st[1], d->hi_st[0], d->hi_st[1]})
       if (t) { (void)hipStreamSynchronize(t); (void)hipStreamDestroy(t); }
-    if (d->hi_done) (void)hipEventDestroy(d->hi_done);
+    for (hipEvent_t e : {d->hi_done[0], d->hi_done[1], d->bits_ev[0], d->bits_ev[1]})
+      if (e) (void)hipEventDestroy(e);
     if (d->plain_done) (void)hipEventDestroy(d->plain_done);
     delete d;
   }
@@ -1669,7 +1703,7 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
     CK(hipSetDevice(d->id));
     Set* s = &d->set[0];
     hipStream_t st = s->st;
-    CK(hipStreamSynchronize(d->hi_st));         // no pipelined ladder reads an arena being grown
+    for (hipStream_t t : d->hi_st) CK(hipStreamSynchronize(t));   // no pipelined ladder reads an arena being grown
     int rc = ensure_keys(d, base + n, base, st);
     if (rc) return rc;
     if (!d->gtab4 && ctx->keyed_k4) {          // first keys on this device: the k4 ladder's G tables
@@ -2142,6 +2176,14 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "ed_keyed")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->ed_keyed = val != 0;
+  } else if (!strcmp(key, "two_ladders")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    for (Dev* d : ctx->devs) {                  // no pipelined call in flight across the switch
+      std::lock_guard<std::mutex> lk(d->mu);
+      for (hipStream_t t : d->hi_st) CK(hipStreamSynchronize(t));
+      d->bits_used = false;
+    }
+    ctx->two_ladders = val != 0;
   } else if (!strcmp(key, "k6")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->k6 = val != 0;
@@ -2242,7 +2284,7 @@ int gv_dev_copy(gv_ctx* ctx, int dev_slot, void* dst, const void* src, size_t by
   }
   Dev* d = ctx->devs[dev_slot];
   CK(hipSetDevice(d->id));
-  for (hipStream_t t : {d->lo_st[0], d->lo_st[1], d->hi_st})   // after every pipelined call (synchronous copy)
+  for (hipStream_t t : {d->lo_st[0], d->lo_st[1], d->hi_st[0], d->hi_st[1]})   // after every pipelined call (synchronous copy)
     CK(hipStreamSynchronize(t));
   hipStream_t st = d->set[0].st;
   CK(hipMemcpyAsync(dst, src, bytes, k, st));
@@ -2279,7 +2321,7 @@ int gv_dev_sync(gv_ctx* ctx, int dev_slot) {
   Dev* d = ctx->devs[dev_slot];
   CK(hipSetDevice(d->id));
   for (Set& s : d->set) CK(hipStreamSynchronize(s.st));
-  for (hipStream_t t : {d->lo_st[0], d->lo_st[1], d->hi_st}) CK(hipStreamSynchronize(t));
+  for (hipStream_t t : {d->lo_st[0], d->lo_st[1], d->hi_st[0], d->hi_st[1]}) CK(hipStreamSynchronize(t));
   return GV_OK;
 }
 

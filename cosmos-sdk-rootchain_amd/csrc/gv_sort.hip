@@ -11,10 +11,10 @@
 // unpacked straight from the AoS input of item perm[g] into lane g, and after
 // the ladder the accept bits are gathered back to item order.  A wave then
 // covers ~4 keys (C2), whose tables stay in L1 / L2 for its 16 lanes each.
+// Every kernel here is hand-written (the slot-count scan included).
 // Verdicts are a pure function of the item, so the order within a slot
 // (atomic arrival order) does not matter.
 #include <hip/hip_runtime.h>
-#include <hipcub/device/device_scan.hpp>
 #include "gv_kernels.h"
 
 namespace gv {
@@ -38,6 +38,86 @@ __global__ __launch_bounds__(256) void k_slot_place(u32 n, const u32* kslot, u32
   rank[g] = pos;
   perm[pos] = g;
   kslot_s[pos] = sl;
+}
+
+// ---- exclusive scan of the slot counts (hand-written, three launches): each
+// 256-thread block scans 2,048 counts (8 per thread: a sequential prefix, a
+// wave scan of the thread totals by lane shuffles, the four wave totals
+// through LDS) and writes its total; one block scans the block totals
+// (sequential carry over chunks of 2,048); every block adds its offset.
+#define GV_SCAN_PER 8
+#define GV_SCAN_BLK (256 * GV_SCAN_PER)
+
+// exclusive scan of the 256 threads' values v in a block; returns the block total
+__device__ __forceinline__ u32 block_excl_scan(u32 v, u32& excl) {
+  __shared__ u32 wsum[4];
+  const u32 lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  u32 inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const u32 t = (u32)__shfl_up((int)inc, d, 64);
+    if (lane >= (u32)d) inc += t;
+  }
+  if (lane == 63u) wsum[w] = inc;
+  __syncthreads();
+  u32 woff = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    woff += (u32)k < w ? wsum[k] : 0u;
+    tot += wsum[k];
+  }
+  __syncthreads();                          // wsum reusable by a later call
+  excl = woff + inc - v;
+  return tot;
+}
+
+__global__ __launch_bounds__(256) void k_scan_local(u32 n, const u32* in, u32* out, u32* sums) {
+  const u32 base = blockIdx.x * GV_SCAN_BLK + threadIdx.x * GV_SCAN_PER;
+  u32 v[GV_SCAN_PER], t = 0;
+#pragma unroll
+  for (int k = 0; k < GV_SCAN_PER; ++k) {
+    v[k] = base + k < n ? in[base + k] : 0u;
+    t += v[k];
+  }
+  u32 excl;
+  const u32 tot = block_excl_scan(t, excl);
+#pragma unroll
+  for (int k = 0; k < GV_SCAN_PER; ++k) {
+    if (base + k < n) out[base + k] = excl;
+    excl += v[k];
+  }
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// one block: sums[0..m) -> exclusive prefix sums, in place
+__global__ __launch_bounds__(256) void k_scan_top(u32 m, u32* sums) {
+  u32 carry = 0;
+  for (u32 c0 = 0; c0 < m; c0 += GV_SCAN_BLK) {   // uniform loop: every thread reaches each barrier
+    const u32 base = c0 + threadIdx.x * GV_SCAN_PER;
+    u32 v[GV_SCAN_PER], t = 0;
+#pragma unroll
+    for (int k = 0; k < GV_SCAN_PER; ++k) {
+      v[k] = base + k < m ? sums[base + k] : 0u;
+      t += v[k];
+    }
+    u32 excl;
+    const u32 tot = block_excl_scan(t, excl);
+    excl += carry;
+#pragma unroll
+    for (int k = 0; k < GV_SCAN_PER; ++k) {
+      if (base + k < m) sums[base + k] = excl;
+      excl += v[k];
+    }
+    carry += tot;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_scan_add(u32 n, u32* out, const u32* sums) {
+  const u32 off = sums[blockIdx.x];
+  const u32 base = blockIdx.x * GV_SCAN_BLK + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < GV_SCAN_PER; ++k)
+    if (base + k * 256u < n) out[base + k * 256u] += off;
 }
 
 // big-endian 32-bit word k (0 = most significant) of a 16-byte vector pair
@@ -95,10 +175,19 @@ __global__ __launch_bounds__(256) void k_unsort_bits(u32 n, const u32* pos, cons
 extern "C" {
 
 size_t gvk_sort_temp_bytes(uint32_t nbuckets) {
-  size_t bytes = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                         (int)nbuckets);
-  return bytes;
+  return ((size_t)(nbuckets + GV_SCAN_BLK - 1) / GV_SCAN_BLK) * 4;   // one total per scan block
+}
+
+// exclusive prefix sums of n counts (temp: gvk_sort_temp_bytes(n))
+static hipError_t excl_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* temp, hipStream_t st) {
+  const uint32_t nblk = (n + GV_SCAN_BLK - 1) / GV_SCAN_BLK;
+  if (nblk == 0) return hipSuccess;
+  hipLaunchKernelGGL(gv::k_scan_local, dim3(nblk), dim3(256), 0, st, n, in, out, temp);
+  if (nblk > 1) {
+    hipLaunchKernelGGL(gv::k_scan_top, dim3(1), dim3(256), 0, st, nblk, temp);
+    hipLaunchKernelGGL(gv::k_scan_add, dim3(nblk), dim3(256), 0, st, n, out, (const uint32_t*)temp);
+  }
+  return hipGetLastError();
 }
 
 hipError_t gvk_sort_slots(const gvk_sort* so, uint32_t n, const uint32_t* kslot, uint32_t kcount, hipStream_t st) {
@@ -107,8 +196,8 @@ hipError_t gvk_sort_slots(const gvk_sort* so, uint32_t n, const uint32_t* kslot,
   hipError_t e = hipMemsetAsync(so->cnt, 0, (size_t)nb * 4, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(gv::k_slot_rank, grd, blk, 0, st, n, kslot, kcount, so->cnt, so->pos);
-  size_t bytes = so->temp_bytes;
-  e = hipcub::DeviceScan::ExclusiveSum(so->temp, bytes, (const uint32_t*)so->cnt, so->off, (int)nb, st);
+  if (so->temp_bytes < gvk_sort_temp_bytes(nb)) return hipErrorInvalidValue;
+  e = excl_scan((const uint32_t*)so->cnt, so->off, nb, (uint32_t*)so->temp, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(gv::k_slot_place, grd, blk, 0, st, n, kslot, kcount, (const uint32_t*)so->off, so->pos,
                      so->perm, so->kslot);
