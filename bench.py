@@ -92,8 +92,10 @@ def w_keybuild(nt: int, last_offset: int) -> float:
 W_KEYBUILD_K4 = w_keybuild(16, 100)        # 4 groups of 16 entries, offsets 0/35/70/100
 W_KEYBUILD_K6 = w_keybuild(32, 102)        # 4 groups of 32 entries, offsets 0/36/72/102
 W_PREP_KEYED = W_SCALAR
+W_PREP_KEYED_F = 2 * NM + (2 * 64 + 68)   # k4f: u2's GLV split only (u1 is recoded unsplit)
 W_LADDER_K4 = w_ladder(30, 52, 14, 5)      # k_ecmult_k4: 30 doublings, 52 Q (26 lambda), 14 G additions
 W_LADDER_K6 = w_ladder(30, 44, 12, 6)      # k_ecmult_k6: 30 doublings, 44 Q (22 lambda), 12 G additions
+W_LADDER_K4F = w_ladder(30, 52, 11, 5)     # k_ecmult_k4<true>: G on the unsplit u1, 11 25-bit windows
 # Peak: the highest v_mad_u64_u32 issue rate measured on MI355X
 # (tools/microbench/alu_rate.hip; profiles/r01/alu_rate_v3.jsonl, dependent
 # chains at 8 waves/SIMD), lane-products per second, whole chip.  bench.py
@@ -477,13 +479,14 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
     u_keys = (gk - grp0[1]) / max(1, gb - grp0[0]) if grouped else 0.0
     routes1 = ver.route_stats() if hasattr(ver, "route_stats") else {}
     k6 = grouped and routes1.get("k6", 0) - routes0.get("k6", 0) >= calib
+    k4f = grouped and routes1.get("k4f", 0) - routes0.get("k4f", 0) >= calib
     if grouped:
         # the key tables (k_keys_chain, k_keys_tables) run on a side stream
         # beside k_scalar_inv: that stage's time covers both
         lad = "k_ecmult_k6" if k6 else "k_ecmult_k4"
         wkb = W_KEYBUILD_K6 if k6 else W_KEYBUILD_K4
         w = {"k_unpack+k_dedupe": 0.0, "k_scalar_inv|k_keys_chain+k_keys_tables": W_INV + wkb * u_keys / n,
-             "k_prep<keyed>": W_PREP_KEYED, lad: W_LADDER_K6 if k6 else W_LADDER_K4}
+             "k_prep<keyed>": W_PREP_KEYED_F if k4f else W_PREP_KEYED, lad: W_LADDER_K6 if k6 else W_LADDER_K4F if k4f else W_LADDER_K4}
         kms = dict(zip(w, (unpack_ms, inv_ms, prep_ms, ecmult_ms)))
         ladder, w_route = lad, sum(w.values())
     else:
@@ -517,7 +520,9 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
                    "global_batch": n * world, "parallelism": f"shard{world} (independent per-GPU shards, no collective)",
                    "route": ("in-batch key grouping: each distinct key parsed and tabulated once (k_dedupe, "
                              "k_keys_chain + k_keys_tables), items on the keyed 30-doubling ladder "
-                             + ("k_ecmult_k6 (6-bit Q / 24-bit G windows)" if k6 else "k_ecmult_k4")
+                             + ("k_ecmult_k6 (6-bit Q / 24-bit G windows)" if k6
+                                else "k_ecmult_k4 (G on the unsplit scalar: 11 25-bit windows)" if k4f
+                                else "k_ecmult_k4 (GLV G: 14 20-bit windows)")
                              if grouped else "per-item pub33 pipeline (every item decompresses its key)"),
                    "distinct_keys_per_batch": round(u_keys) if grouped else None},
         "roofline": {

@@ -79,6 +79,9 @@ typedef struct gvk_batch {
   // ladder is k_ecmult_k6 over gtab6 (GV_K6_GTAB_WORDS); gtab4 unused
   const uint32_t* gtab6;
   int k6;
+  // k4 batches with gtabf set: the G half on the unsplit scalar (GV_GF_*),
+  // k_prep<.., GF> digits and k_ecmult_k4<true> over gtabf (GV_GF_WORDS)
+  const uint32_t* gtabf;
   // key-ordered lanes (gv_sort.hip; keyed k4 batches with srt.perm set): the
   // lanes run in slot order, the bits are gathered back to item order
   gvk_sort srt;
@@ -122,6 +125,20 @@ hipError_t gvk_unsort_bits(uint32_t n, const uint32_t* pos, const uint64_t* sbit
 #define GV_K6_GTAB_WORDS ((size_t)GV_LGRP * 2 * GV_K6_GTAB_N * 16)
 static_assert(GV_K6_QWIN + 2 * GV_K6_GWIN <= GV_DIGIT_ROWS, "k6 digits fit the digit rows");
 static_assert(GV_K6_QW * GV_K6_QWIN >= 130 && GV_K6_GW * GV_K6_GWIN >= 130, "k6 windows cover 129-bit halves");
+
+// The k4 ladder's G half on the unsplit scalar (k_ecmult_k4<true>): u1 = e/s
+// is not GLV-split; its 11 signed 25-bit windows (window j at bit 25 j) are
+// added from 2^24-entry tables of 2^o G for six offsets o (gv_kernels.hip
+// kGFOff), window j at ladder position p reading the table of offset
+// 25 j - 5 p.  11 G additions per verify instead of 14 and no lambda tables:
+// 6 GiB per device.
+#define GV_GF_W 25
+#define GV_GF_WIN 11
+#define GV_GF_NTAB 6
+#define GV_GF_TAB_N (1u << (GV_GF_W - 1))
+#define GV_GF_WORDS ((size_t)GV_GF_NTAB * GV_GF_TAB_N * 16)
+static_assert(GV_QWIN + GV_GF_WIN <= GV_DIGIT_ROWS, "full-scalar G digits fit the digit rows");
+static_assert(GV_GF_W * GV_GF_WIN >= 257, "the windows cover a 256-bit scalar plus the Booth carry");
 
 // Small-batch latency path (gv_lat.hip): GV_LAT_SIGS signatures per block of
 // 128 threads, one fused kernel (after k_sha256 on the message path).  bits
@@ -227,6 +244,8 @@ hipError_t gvk_gen_gtable4(uint32_t* gtab4, uint32_t* base_scratch, hipStream_t 
 hipError_t gvk_gen_glat(uint32_t* glat, hipStream_t st);
 // the k6 ladder's G tables (GV_K6_GTAB_WORDS words); base_scratch: 64 words
 hipError_t gvk_gen_gtable6(uint32_t* gtab6, uint32_t* base_scratch, hipStream_t st);
+// the full-scalar G tables (GV_GF_WORDS words); base_scratch: 96 words
+hipError_t gvk_gen_gtablef(uint32_t* gtabf, uint32_t* base_scratch, hipStream_t st);
 // k6 key tables (32 entries per group) of n keys already unpacked into rows
 // in_x / in_pfx (stride C), slots 0..n-1; qr: (GV_K6_NT - 1) * 9 ratio rows of
 // stride round_up(4 n, 256), qe (may be null): (GV_K6_NT - 1) * 18 rows of the

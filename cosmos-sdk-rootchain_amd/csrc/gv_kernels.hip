@@ -87,7 +87,8 @@ GV_DEV void fe_from_const(fe& r, const u32* c) {
 // base: affine x || y (16 words) of the point whose multiples are tabulated,
 // or null for G itself (the keyed ladder's tables of 2^35 G, 2^70 G, 2^100 G).
 // GTN: entries per table (GV_GTAB_N; GV_K6_GTAB_N for the k6 tables).
-template <u32 GTN = GV_GTAB_N>
+// LAM false: the first table only (the full-scalar G tables).
+template <u32 GTN = GV_GTAB_N, bool LAM = true>
 __global__ void k_gen_gtable(u32* gtab, const u32* base) {
   const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= GTN) return;
@@ -116,14 +117,17 @@ __global__ void k_gen_gtable(u32* gtab, const u32* base) {
   fe_mul(y, acc.y, zi3);
   fe_normalize(x);
   fe_normalize(y);
+  u32* t0 = gtab + (size_t)e * 16;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { t0[i] = x.v[i]; t0[8 + i] = y.v[i]; }
+  if (!LAM) return;
   fe beta, lx;
   fe_from_const(beta, kBeta);
   fe_mul(lx, x, beta);
   fe_normalize(lx);
-  u32* t0 = gtab + (size_t)e * 16;
   u32* t1 = gtab + ((size_t)GTN + e) * 16;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { t0[i] = x.v[i]; t0[8 + i] = y.v[i]; t1[i] = lx.v[i]; t1[8 + i] = y.v[i]; }
+  for (int i = 0; i < 8; ++i) { t1[i] = lx.v[i]; t1[8 + i] = y.v[i]; }
 }
 
 // ------------------------------------------------------------------ k_unpack
@@ -597,7 +601,9 @@ GV_DEV bool parse_pubkey(u32 pre, const fe& x, fe& y) {
 #endif
 // K6 (keyed only): the digits of the k6 ladder (GV_K6_QW-bit Q windows,
 // GV_K6_GW-bit G windows) instead of GV_QW / GV_GW.
-template <bool KEYED, bool K6 = false>
+// GF (keyed k4 only): G digits of the unsplit u1 (GV_GF_WIN signed
+// GV_GF_W-bit windows, one int32 row each: digits[(GV_QWIN + j)*C + g]).
+template <bool KEYED, bool K6 = false, bool GF = false>
 __global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u32* in_x, const u32* in_pfx,
                                                const u32* in_r, const u32* in_s, const u32* in_e,
                                                const u32* in_w, u32* digits, u32* qt, u32* zq_out,
@@ -657,12 +663,14 @@ __global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u
   }
 
   // ---- GLV split
-  u32 k1g[4], k2g[4], k1q[4], k2q[4], n1g, n2g, n1q, n2q;
-  glv_split(k1g, n1g, k2g, n2g, u1);
+  u32 k1g[4] = {}, k2g[4] = {}, k1q[4], k2q[4], n1g = 0, n2g = 0, n1q, n2q;
+  if (!GF) glv_split(k1g, n1g, k2g, n2g, u1);
   glv_split(k1q, n1q, k2q, n2q, u2);
   if (!ok) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) { k1g[i] = k2g[i] = k1q[i] = k2q[i] = 0u; }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) u1[i] = 0u;
   }
 
   // ---- signed fixed-window (Booth) recoding, scalar signs folded in.
@@ -679,13 +687,18 @@ __global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u
     if (n2q) d1 = -d1;
     digits[(size_t)win * C + g] = ((u32)d0 & 0xFFFFu) | ((u32)d1 << 16);
   }
+  if (GF) {
 #pragma unroll
-  for (int j = 0; j < GWIN; ++j) {
-    int d2 = booth_digit<GW>(k1g, j), d3 = booth_digit<GW>(k2g, j);
-    if (n1g) d2 = -d2;
-    if (n2g) d3 = -d3;
-    digits[(size_t)(QWIN + 2 * j) * C + g] = (u32)d2;
-    digits[(size_t)(QWIN + 2 * j + 1) * C + g] = (u32)d3;
+    for (int j = 0; j < GV_GF_WIN; ++j) digits[(size_t)(QWIN + j) * C + g] = (u32)booth_digit8<GV_GF_W>(u1, j);
+  } else {
+#pragma unroll
+    for (int j = 0; j < GWIN; ++j) {
+      int d2 = booth_digit<GW>(k1g, j), d3 = booth_digit<GW>(k2g, j);
+      if (n1g) d2 = -d2;
+      if (n2g) d3 = -d3;
+      digits[(size_t)(QWIN + 2 * j) * C + g] = (u32)d2;
+      digits[(size_t)(QWIN + 2 * j + 1) * C + g] = (u32)d3;
+    }
   }
   flags[g] = (ok ? 1u : 0u) | (r_small ? 2u : 0u);
 
@@ -930,6 +943,25 @@ __global__ void k_gen_gbase(u32* out) {
   f29_from_words(p.y, gy.v);
   f29_set_u32(p.z, 1);
   for (int k = 0; k < grp_bit[t + 1]; ++k) gej29_double(p, p);
+  fe x8, y8;
+  gej29_to_affine_words(x8, y8, p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { out[t * 16 + i] = x8.v[i]; out[t * 16 + 8 + i] = y8.v[i]; }
+}
+
+// Affine 2^o G (16 words each) for the full-scalar G tables' offsets o = kGFOff[t].
+__constant__ const int kGFOff[GV_GF_NTAB] = {0, 45, 100, 145, 195, 220};
+__global__ void k_gen_gbasef(u32* out) {
+  const int t = threadIdx.x;
+  if (t >= GV_GF_NTAB) return;
+  fe gx, gy;
+  fe_from_const(gx, kGx);
+  fe_from_const(gy, kGy);
+  gej29 p;
+  f29_from_words(p.x, gx.v);
+  f29_from_words(p.y, gy.v);
+  f29_set_u32(p.z, 1);
+  for (int k = 0; k < kGFOff[t]; ++k) gej29_double(p, p);
   fe x8, y8;
   gej29_to_affine_words(x8, y8, p);
 #pragma unroll
@@ -1228,7 +1260,14 @@ __constant__ const int kK4WStart[4] = {0, 7, 14, 20};
 __constant__ const int kK4NWin[4] = {7, 7, 6, 6};
 __constant__ const int kK4GWin[7][2] = {{0, 5}, {2, -1}, {4, -1}, {-1, -1}, {1, 6}, {3, -1}, {-1, -1}};
 __constant__ const int kK4GGrp[7] = {0, 0, 1, 1, 2, 3, 3};
+// GF (gv_kernels.h GV_GF_*): the G windows j at each position (up to four)
+// and the table each reads (offset kGFOff[kGFTab[j]] = 25 j - 5 p)
+__constant__ const int kGFWin[7][4] = {{0, 4, -1, -1}, {2, 6, 8, -1}, {-1, -1, -1, -1}, {-1, -1, -1, -1},
+                                       {-1, -1, -1, -1}, {1, 5, -1, -1}, {3, 7, 9, 10}};
+__constant__ const int kGFTab[GV_GF_WIN] = {0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5};
 
+// GF: gtab is the full-scalar G tables (gtabf), gtab4 unused.
+template <bool GF>
 __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gtab, const u32* gtab4, u32 n, u32 C,
                                                         const u32* digits, const u32* kqt, const u32* kqt2,
                                                         const u32* kzq, const u32* flags, const u32* in_r,
@@ -1260,6 +1299,11 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gta
         d = (slot & 1) ? ((int)dq >> 16) : ((int)(dq << 16) >> 16);
         tab = grp == 0 ? kqt : kqt2;
         row = grp == 0 ? qi : qi * GV_KEY2_TABLES + (grp - 1);
+      } else if (GF) {
+        const int j = kGFWin[pos][slot - 8];
+        if (j < 0) continue;                               // wave-uniform
+        d = (int)digits[(size_t)(GV_QWIN + j) * C + g];
+        tab = gtab + (size_t)kGFTab[j] * GV_GF_TAB_N * 16;
       } else {
         const int j = kK4GWin[pos][(slot - 8) >> 1];
         if (j < 0) continue;                               // wave-uniform
@@ -1488,11 +1532,21 @@ hipError_t gvk_gen_gtable6(uint32_t* gtab6, uint32_t* base_scratch, hipStream_t 
   return hipGetLastError();
 }
 
+hipError_t gvk_gen_gtablef(uint32_t* gtabf, uint32_t* base_scratch, hipStream_t st) {
+  hipLaunchKernelGGL(gv::k_gen_gbasef, dim3(1), dim3(64), 0, st, base_scratch);
+  const dim3 grd((GV_GF_TAB_N + 255) / 256), blk(256);
+  for (int k = 0; k < GV_GF_NTAB; ++k)
+    hipLaunchKernelGGL((gv::k_gen_gtable<GV_GF_TAB_N, false>), grd, blk, 0, st, gtabf + (size_t)k * GV_GF_TAB_N * 16,
+                       (const uint32_t*)(base_scratch + 16 * k));
+  return hipGetLastError();
+}
+
 hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   const uint32_t C = b->C;
   const dim3 blk(256), grd(C / 256);
   // key-ordered lanes (gv_sort.hip): keyed k4 batches with sort scratch
   const bool k6 = b->kslot && b->k6 && b->gtab6;
+  const bool gf = b->kslot && b->gtab4 && b->gtabf && !k6;   // k_ecmult_k4<true>
   const bool sorted = b->kslot && (b->gtab4 || k6) && b->srt.perm;
   const uint32_t* perm = sorted ? b->srt.perm : nullptr;
   if (sorted) {
@@ -1522,6 +1576,11 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
                          (const uint32_t*)nullptr, b->in_r, b->in_s, b->in_e, (const uint32_t*)w, b->digits,
                          (uint32_t*)nullptr, (uint32_t*)nullptr, b->flags, sorted ? b->srt.kslot : b->kslot,
                          b->kok, b->kcount, b->in_pfx);
+    else if (gf)
+      hipLaunchKernelGGL((gv::k_prep<true, false, true>), grd, blk, 0, st, C, b->n, (const uint32_t*)nullptr,
+                         (const uint32_t*)nullptr, b->in_r, b->in_s, b->in_e, (const uint32_t*)w, b->digits,
+                         (uint32_t*)nullptr, (uint32_t*)nullptr, b->flags, sorted ? b->srt.kslot : b->kslot,
+                         b->kok, b->kcount, b->in_pfx);
     else if (b->kslot)   // keyed: in_pfx doubles as the clamped-slot row for k_ecmult
       hipLaunchKernelGGL(gv::k_prep<true>, grd, blk, 0, st, C, b->n, (const uint32_t*)nullptr,
                          (const uint32_t*)nullptr, b->in_r, b->in_s, b->in_e, (const uint32_t*)w, b->digits,
@@ -1544,8 +1603,12 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   if (k6)
     hipLaunchKernelGGL(gv::k_ecmult_k6, grd, blk, 0, se, b->gtab6, b->n, C, b->digits, b->kqt, b->kqt2, b->kzq,
                        b->flags, b->in_r, sorted ? b->srt.bits : b->bits, (const uint32_t*)b->in_pfx, b->kC);
+  else if (gf)
+    hipLaunchKernelGGL(gv::k_ecmult_k4<true>, grd, blk, 0, se, b->gtabf, b->gtab4, b->n, C, b->digits, b->kqt,
+                       b->kqt2, b->kzq, b->flags, b->in_r, sorted ? b->srt.bits : b->bits,
+                       (const uint32_t*)b->in_pfx, b->kC);
   else if (b->kslot && b->gtab4)
-    hipLaunchKernelGGL(gv::k_ecmult_k4, grd, blk, 0, se, b->gtab, b->gtab4, b->n, C, b->digits, b->kqt, b->kqt2,
+    hipLaunchKernelGGL(gv::k_ecmult_k4<false>, grd, blk, 0, se, b->gtab, b->gtab4, b->n, C, b->digits, b->kqt, b->kqt2,
                        b->kzq, b->flags, b->in_r, sorted ? b->srt.bits : b->bits, (const uint32_t*)b->in_pfx,
                        b->kC);
   else if (b->kslot)

@@ -302,6 +302,8 @@ struct Dev {
   uint32_t* gtab4 = nullptr;                      // k_ecmult_k4's tables of 2^35 G, 2^70 G, 2^100 G (+ lambda)
   uint32_t* gtab6 = nullptr;                      // k_ecmult_k6's 24-bit-window tables of 2^b G, 2^b lambda G (4 GiB)
   bool gtab6_failed = false;                      // its allocation failed once: the grouped route stays on k4
+  uint32_t* gtabf = nullptr;                      // k_ecmult_k4<true>'s full-scalar G tables (GV_GF_WORDS, 6 GiB)
+  bool gtabf_failed = false;                      // its allocation failed once: k4 keeps the GLV G tables
   size_t kcap = 0;
   // ring of per-launch stage events for gv_stage_stats
   static constexpr int kRing = 256;
@@ -633,6 +635,8 @@ struct gv_ctx {
                                 // verdict bytes to pinned memory directly: no H2D, memset or D2H (GV_LAT_ZC=0: A/B)
   bool lat_sliced = true;       // small batches on k_verify_lat_sl / k_verify_lat16_sl (GV_LAT_SLICED=0: the one-lane-field kernels, A/B)
   bool keyed_k4 = true;         // keyed batches on k_ecmult_k4 (GV_KEYED_K4=0: the 125-doubling ladder, A/B)
+  bool gfull = true;            // k4 batches take G on the unsplit scalar: 11 25-bit windows instead of 14 20-bit
+                                // GLV windows (k_ecmult_k4<true>, 6 GiB of tables; GV_GFULL=0: A/B)
   bool k6 = false;              // grouped batches on k_ecmult_k6: 6-bit Q / 24-bit G windows, 32-entry key tables
                                 // (GV_K6=1).  Its ladder is 10 % faster than k4's but the doubled key tables cost
                                 // more than that under C2's 16 items per key: 218-220 vs 222M/s (profiles/r04/prio_ab)
@@ -674,8 +678,29 @@ EdGroupCfg ed_group_cfg(const gv_ctx* ctx) {
 // The 20-bit-window tables of 2^35 G, 2^70 G, 2^100 G (and lambda images)
 // the 4-group keyed ladder reads (k_ecmult_k4): built on first use, 192 MiB.
 // set s is a scratch set with capacity >= 256 (its flags rows hold the base points).
+// The full-scalar G tables (GV_GF_WORDS, 6 GiB): built beside gtab4, ~0.2 s.
+// An allocation failure is remembered and k4 batches keep the GLV G tables.
+int ensure_gtabf(gv_ctx* ctx, Dev* d, Set* s, hipStream_t st) {
+  if (d->gtabf || !ctx->gfull || d->gtabf_failed) return GV_OK;
+  uint32_t* tf = nullptr;
+  if (hipMalloc(&tf, GV_GF_WORDS * 4) != hipSuccess) {
+    (void)hipGetLastError();
+    d->gtabf_failed = true;
+    return GV_OK;
+  }
+  int rc;
+  if ((rc = ensure_cap(s, 256))) { (void)hipFree(tf); return rc; }
+  if ((rc = set_acquire(s, st))) { (void)hipFree(tf); return rc; }
+  if (gvk_gen_gtablef(tf, s->flags, st) != hipSuccess) { (void)hipFree(tf); return GV_EHIP; }
+  if ((rc = set_release(s, st))) { (void)hipFree(tf); return rc; }
+  if (hipStreamSynchronize(st) != hipSuccess) { (void)hipFree(tf); return GV_EHIP; }
+  d->gtabf = tf;
+  return GV_OK;
+}
+
 int ensure_gtab4(gv_ctx* ctx, Dev* d, Set* s, hipStream_t st) {
-  if (d->gtab4 || !ctx->keyed_k4) return GV_OK;
+  if (!ctx->keyed_k4) return GV_OK;
+  if (d->gtab4) return ensure_gtabf(ctx, d, s, st);
   uint32_t* t4 = nullptr;
   if (hipMalloc(&t4, (size_t)GV_KEY2_TABLES * 2 * GV_GTAB_N * 16 * 4) != hipSuccess) return GV_OK;   // keep k_ecmult<true>
   int rc;
@@ -685,7 +710,7 @@ int ensure_gtab4(gv_ctx* ctx, Dev* d, Set* s, hipStream_t st) {
   if ((rc = set_release(s, st))) { (void)hipFree(t4); return rc; }
   if (hipStreamSynchronize(st) != hipSuccess) { (void)hipFree(t4); return GV_EHIP; }
   d->gtab4 = t4;
-  return GV_OK;
+  return ensure_gtabf(ctx, d, s, st);
 }
 
 // k_ecmult_k6's G tables (GV_K6_GTAB_WORDS, 4 GiB): built on first use, ~0.1 s.
@@ -785,6 +810,7 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   b.kslot = kslot; b.kqt = s->g_kqt; b.kzq = s->g_kzq; b.kok = s->g_kok;
   b.kC = (uint32_t)capU; b.kcount = (uint32_t)U;
   b.kqt2 = s->g_kqt2; b.gtab4 = d->gtab4;       // null gtab4: the 125-doubling keyed ladder
+  b.gtabf = ctx->gfull ? d->gtabf : nullptr;    // built by ensure_gtab4 above on first use
   b.k6 = k6 ? 1 : 0; b.gtab6 = d->gtab6;
   d->grouped_batches++;
   d->grouped_keys += U;
@@ -847,6 +873,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
   b.pub33 = pub; b.sig64 = sig; b.dig32 = dig;
   b.msg_blob = blob; b.msg_off = off; b.msg_len = len;
   b.gtab = d->gtab;
+  b.gtabf = ctx->gfull ? d->gtabf : nullptr;
   b.in_x = s->in_x; b.in_pfx = s->in_pfx; b.in_r = s->in_r; b.in_s = s->in_s; b.in_e = s->in_e;
   b.digits = s->digits; b.zq = s->zq; b.flags = s->flags; b.qtab = s->qtab;
   b.bits = bits_out;
@@ -928,8 +955,11 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
       if (rc) return rc;
     }
     plan_sort(ctx, s, b, sort_base);
-    d->routes[b.k6 && b.gtab6 ? GV_ROUTE_K6 : b.kslot && b.gtab4 ? GV_ROUTE_K4 : b.kslot ? GV_ROUTE_KEYED125
-                                                                                       : GV_ROUTE_PUB33]++;
+    d->routes[b.k6 && b.gtab6                  ? GV_ROUTE_K6
+              : b.kslot && b.gtab4 && b.gtabf ? GV_ROUTE_K4F
+              : b.kslot && b.gtab4            ? GV_ROUTE_K4
+              : b.kslot                       ? GV_ROUTE_KEYED125
+                                              : GV_ROUTE_PUB33]++;
     CK(gvk_verify(&b, st));
   }
   if (rs) {
@@ -1490,6 +1520,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   parse_size_env("GV_MAX_BATCH", &ctx->max_batch);
   if (const char* k4 = getenv("GV_KEYED_K4")) ctx->keyed_k4 = strcmp(k4, "0") != 0;
   if (const char* k6 = getenv("GV_K6")) ctx->k6 = strcmp(k6, "0") != 0;
+  if (const char* gf = getenv("GV_GFULL")) ctx->gfull = strcmp(gf, "0") != 0;
   if (const char* tl = getenv("GV_TWO_LADDERS")) ctx->two_ladders = strcmp(tl, "0") != 0;
   if (const char* ks = getenv("GV_KEYS_SCRATCH")) ctx->keys_scratch = strcmp(ks, "0") != 0;
   if (const char* sk = getenv("GV_SORT_KEYS")) ctx->sort_keys = strcmp(sk, "0") != 0;
@@ -1563,6 +1594,7 @@ void gv_close(gv_ctx* ctx) {
     if (d->glat) (void)hipFree(d->glat);
     if (d->gtab4) (void)hipFree(d->gtab4);
     if (d->gtab6) (void)hipFree(d->gtab6);
+    if (d->gtabf) (void)hipFree(d->gtabf);
     if (d->kqt2) (void)hipFree(d->kqt2);
     if (d->kzq2) (void)hipFree(d->kzq2);
     if (d->kqt) (void)hipFree(d->kqt);
@@ -1706,17 +1738,9 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
     for (hipStream_t t : d->hi_st) CK(hipStreamSynchronize(t));   // no pipelined ladder reads an arena being grown
     int rc = ensure_keys(d, base + n, base, st);
     if (rc) return rc;
-    if (!d->gtab4 && ctx->keyed_k4) {          // first keys on this device: the k4 ladder's G tables
-      uint32_t* t4 = nullptr;
-      if (hipMalloc(&t4, (size_t)GV_KEY2_TABLES * 2 * GV_GTAB_N * 16 * 4) == hipSuccess) {
-        if ((rc = ensure_cap(s, 256))) { (void)hipFree(t4); return rc; }
-        if ((rc = set_acquire(s, st))) { (void)hipFree(t4); return rc; }
-        CK(gvk_gen_gtable4(t4, s->flags, st));   // 48 scratch words for the base points
-        if ((rc = set_release(s, st))) { (void)hipFree(t4); return rc; }
-        CK(hipStreamSynchronize(st));
-        d->gtab4 = t4;
-      }                                         // no memory: keyed batches keep k_ecmult<true>
-    }
+    // first keys on this device: the k4 ladder's G tables (no memory: keyed
+    // batches keep k_ecmult<true>)
+    if ((rc = ensure_gtab4(ctx, d, s, st))) return rc;
     for (size_t c0 = 0; c0 < n; c0 += ctx->max_batch) {
       const size_t cn = std::min(ctx->max_batch, n - c0);
       const size_t C = round_up(cn, 256);
@@ -2184,6 +2208,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
       d->bits_used = false;
     }
     ctx->two_ladders = val != 0;
+  } else if (!strcmp(key, "gfull")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->gfull = val != 0;
   } else if (!strcmp(key, "k6")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->k6 = val != 0;

@@ -254,4 +254,22 @@ GV_DEV int booth_digit(const u32 k[4], int win) {
   return mag - (int)((v >> W) << (W - 1));
 }
 
+// The same recoding of a 256-bit k (8 words; win a compile-time constant
+// after unrolling, so the limb selects fold away).  W <= 31.
+template <int W>
+GV_DEV int booth_digit8(const u32 k[8], int win) {
+  const int p = W * win - 1;
+  u32 v;
+  if (p < 0) {
+    v = (k[0] << 1) & ((1u << (W + 1)) - 1u);
+  } else {
+    const int limb = p >> 5, sh = p & 31;
+    const u32 lo = limb < 8 ? k[limb] : 0u;
+    const u32 hi = limb + 1 < 8 ? k[limb + 1] : 0u;
+    v = (u32)((((u64)hi << 32) | lo) >> sh) & ((1u << (W + 1)) - 1u);
+  }
+  const int mag = (int)((v >> 1) & ((1u << (W - 1)) - 1u)) + (int)(v & 1u);
+  return mag - (int)((v >> W) << (W - 1));
+}
+
 }  // namespace gv

@@ -292,7 +292,8 @@ int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys)
  * (keyed, 125-doubling ladder), GV_ROUTE_K4 (keyed 4-group ladder over the
  * key arena), GV_ROUTE_K6 (in-batch key grouping on the 6-bit-window ladder),
  * GV_ROUTE_LAT (small pub33 batches: gv_lat.hip kernels), GV_ROUTE_LAT_KEYED
- * (small keyed batches).  Instrumentation only (bench route attribution, node
+ * (small keyed batches), GV_ROUTE_K4F (the 4-group ladder with the G half on
+ * the unsplit scalar, 25-bit windows).  Instrumentation only (bench route attribution, node
  * metrics). */
 #define GV_ROUTE_PUB33 0
 #define GV_ROUTE_KEYED125 1
@@ -300,7 +301,8 @@ int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys)
 #define GV_ROUTE_K6 3
 #define GV_ROUTE_LAT 4
 #define GV_ROUTE_LAT_KEYED 5
-#define GV_ROUTES 6
+#define GV_ROUTE_K4F 6
+#define GV_ROUTES 7
 int gv_route_stats(gv_ctx* ctx, int dev_slot, uint64_t out[GV_ROUTES]);
 
 const char* gv_strerror(int code);

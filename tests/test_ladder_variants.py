@@ -1,0 +1,150 @@
+"""The keyed ladder's schedules must agree bit for bit: k_ecmult_k4 with the G
+half on the unsplit scalar (gv_set_option "gfull" 1, the default: 11 signed
+25-bit windows of u1 from the 2^o G tables), k_ecmult_k4 on the GLV-split G
+half (gfull 0: 14 20-bit windows) and k_ecmult_k6 (k6 1: 6-bit Q, 24-bit G
+windows, 32-entry key tables).  Each is run on the grouped route (pub33 batches
+with repeated keys), the cached-key route (gv_keys_load slots) and the message
+path, against the oracle's expected verdicts, and the route counters must show
+the schedule that ran."""
+import numpy as np
+import pytest
+
+import bench
+import gpuverify as gvm
+from golden_io import load_digest_vectors, load_msg_vectors
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SCHEDULES = {"k4f": {"gfull": 1, "k6": 0}, "k4": {"gfull": 0, "k6": 0}, "k6": {"gfull": 1, "k6": 1}}
+
+
+@pytest.fixture(scope="module")
+def ver():
+    v = gvm.Verifier([0])
+    yield v
+    v.set_option("gfull", 1)
+    v.set_option("k6", 0)
+    v.close()
+
+
+def run(ver, sched, fn):
+    for k, val in SCHEDULES[sched].items():
+        ver.set_option(k, val)
+    r0 = ver.route_stats()
+    try:
+        out = fn()
+    finally:
+        ver.set_option("gfull", 1)
+        ver.set_option("k6", 0)
+    r1 = ver.route_stats()
+    return out, {k: r1[k] - r0[k] for k in r1}
+
+
+@pytest.mark.parametrize("sched", list(SCHEDULES))
+def test_grouped_random_with_adversarial(ver, sched):
+    pub, sig, dig, exp = bench.make_digest_workload(70_001, 0x91, 1500, 0.25, 16)
+    got, routes = run(ver, sched, lambda: ver.verify_batch_digests(pub, sig, dig))
+    assert routes[sched] >= 1, routes
+    assert np.array_equal(got, exp)
+    idx = np.random.default_rng(21).choice(len(exp), 2000, replace=False)
+    assert np.array_equal(O.verify_digests(pub[idx], sig[idx], dig[idx], threads=16), got[idx])
+
+
+@pytest.mark.parametrize("sched", list(SCHEDULES))
+def test_grouped_goldens_tiled(ver, sched):
+    """every rejection class and the exceptional-add vectors, tiled and shuffled"""
+    gp, gs, gd, gok, _ = load_digest_vectors()
+    reps = 100
+    perm = np.random.default_rng(22).permutation(reps * len(gp))
+    pub, sig, dig = (np.tile(x, (reps, 1))[perm] for x in (gp, gs, gd))
+    exp = np.tile(gok, reps)[perm]
+    got, routes = run(ver, sched, lambda: ver.verify_batch_digests(pub, sig, dig))
+    assert routes[sched] >= 1, routes
+    assert np.array_equal(got, exp)
+
+
+P = 2**256 - 2**32 - 977
+N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+
+
+def ec_add(a, b):
+    if a is None:
+        return b
+    if b is None:
+        return a
+    if a[0] == b[0]:
+        if (a[1] + b[1]) % P == 0:
+            return None
+        lam = 3 * a[0] * a[0] * pow(2 * a[1], -1, P) % P
+    else:
+        lam = (b[1] - a[1]) * pow(b[0] - a[0], -1, P) % P
+    x = (lam * lam - a[0] - b[0]) % P
+    return x, (lam * (a[0] - x) - a[1]) % P
+
+
+def forge(pub, u1, rng):
+    """(sig, digest) that verifies under pub with e/s = u1 exactly: R = u1 G +
+    u2 Q for a random u2, r = R.x mod n, s = r/u2 (retried until low-S), e = u1 s"""
+    while True:
+        u2 = int(rng.integers(1, 1 << 62)) * int(rng.integers(1, 1 << 62)) % N or 1
+        R = ec_add(O.point_mul(u1) if u1 else None, O.point_mul(u2, pub))
+        if R is None or R[0] % N == 0:
+            continue
+        r = R[0] % N
+        s = r * pow(u2, -1, N) % N
+        if s > N // 2:
+            continue
+        e = u1 * s % N
+        return r.to_bytes(32, "big") + s.to_bytes(32, "big"), e.to_bytes(32, "big")
+
+
+def test_scalar_edges_on_the_full_scalar_windows(ver):
+    """u1 = e/s on the edges of the 25-bit G windows (0, 1, n - 1, every
+    digit at +-2^24, the top window's carry, all-ones patterns), forged so
+    they verify, plus the same signatures under the wrong key"""
+    rng = np.random.default_rng(24)
+    keys = [O.pubkey(O.privkey_from_secret(b"ladder-variants-%d" % i)) for i in range(8)]
+    top = sum(1 << (25 * j + 24) for j in range(10))           # every window's top bit: digits -2^24 (+carry)
+    low = sum(((1 << 24) - 1) << (25 * j) for j in range(10))  # low 24 bits ones, no borrow
+    u1s = [0, 1, 2, N - 1, N - 2, (1 << 24), (1 << 24) - 1, (1 << 24) + 1, top % N, (top | low) % N,
+           low % N, ((1 << 256) - 1) % N, (1 << 255) % N, ((1 << 250) - 1) % N, (N - 1) >> 1]
+    pubs, sigs, digs = [], [], []
+    for u1 in u1s:
+        for qi, q in enumerate(keys):
+            sg, dg = forge(q, u1, rng)
+            pubs += [q, keys[(qi + 1) % len(keys)]]
+            sigs += [sg, sg]
+            digs += [dg, dg]
+    m = len(pubs)
+    pub = np.frombuffer(b"".join(pubs), np.uint8).reshape(m, 33)
+    sig = np.frombuffer(b"".join(sigs), np.uint8).reshape(m, 64)
+    dig = np.frombuffer(b"".join(digs), np.uint8).reshape(m, 32)
+    want = O.verify_digests(pub, sig, dig, threads=16)
+    assert want[0::2].all() and not want[1::2].any()
+    reps = 80                                                   # 19,200 items on 8 keys: the grouped route
+    pub, sig, dig = (np.tile(x, (reps, 1)) for x in (pub, sig, dig))
+    exp = np.tile(want, reps)
+    for sched in SCHEDULES:
+        got, routes = run(ver, sched, lambda: ver.verify_batch_digests(pub, sig, dig))
+        assert routes[sched] >= 1, (sched, routes)
+        assert np.array_equal(got, exp), sched
+
+
+@pytest.mark.parametrize("sched", ["k4f", "k4"])
+def test_cached_keys_and_messages(ver, sched):
+    ver.keys_reset()
+    pub, sig, dig, exp = bench.make_digest_workload(40_000, 0x92, 300, 0.25, 16)
+    uniq, inv = np.unique(pub, axis=0, return_inverse=True)
+    slots = ver.keys_load(uniq)[inv.reshape(-1)].astype(np.uint32)
+    got, routes = run(ver, sched, lambda: ver.verify_batch_digests_keyed(slots, sig, dig))
+    assert routes[sched] >= 1, routes
+    assert np.array_equal(got, exp)
+    mp, ms, mm, mok, _ = load_msg_vectors()
+    reps = max(1, 40_000 // len(mp))
+    perm = np.random.default_rng(23).permutation(reps * len(mp))
+    pub2, sig2 = np.tile(mp, (reps, 1))[perm], np.tile(ms, (reps, 1))[perm]
+    msgs = [(mm * reps)[i] for i in perm]
+    got2, routes = run(ver, sched, lambda: ver.verify_batch_msgs(pub2, sig2, msgs))
+    assert routes[sched] >= 1, routes
+    assert np.array_equal(got2, np.tile(mok, reps)[perm])

@@ -187,7 +187,9 @@ def c2_key_cache(ver, pub, sig, dig, exp, nkeys: int, steps: int = 5):
         ver.dev_upload(p, a)
     nw = (n + 63) // 64
     d_bits = ver.dev_alloc(nw * 8)
+    r0 = ver.route_stats()
     el, stages = _timed_device_runs(ver, lambda: ver.dev_verify_digests_keyed(0, n, d[0], d[1], d[2], d_bits), steps)
+    k4f = ver.route_stats()["k4f"] > r0["k4f"]
     bits = np.zeros(nw, np.uint64)
     ver.dev_download(bits, d_bits)
     got = _unpack_bits(bits, n)
@@ -196,7 +198,7 @@ def c2_key_cache(ver, pub, sig, dig, exp, nkeys: int, steps: int = 5):
     ver.keys_reset()
     # k_ecmult_k4's work, counted from the kernel's operations (bench.w_ladder)
     import bench as B
-    w_k4 = round(B.W_LADDER_K4)
+    w_k4 = round(B.W_LADDER_K4F if k4f else B.W_LADDER_K4)
     ems = stages.get("ecmult_ms") or 0.0
     ach = n * w_k4 / (ems * 1e-3) / 1e12 if ems else 0.0
     return {"items": n, "keys": nkeys, "value": round(n * steps / el, 1), "unit": "verifies/s",
