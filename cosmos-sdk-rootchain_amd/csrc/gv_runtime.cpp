@@ -35,6 +35,7 @@
 
 #include "../../include/gpuverify.h"
 #include "gv_kernels.h"
+#include "gv_stage.h"
 
 namespace {
 
@@ -50,189 +51,14 @@ constexpr size_t kLaneWords = 8 + 1 + 8 + 8 + 8 + GV_DIGIT_ROWS + 8 + 1 + GV_QTA
 size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 
 // ------------------------------------------------------------ thread helpers
-// Runs fn(part) for part in [0, parts) on the caller plus the pool's
-// persistent threads.  ONE pool per context, shared by every device's staging
-// (a context over 8 devices stages 8 slices at once): run() may be called
-// from several threads concurrently -- each call is a job whose parts any
-// idle thread (or its own caller) claims, so the host cores are shared
-// instead of 8 devices x 8 threads oversubscribing them.
-class Pool {
- public:
-  explicit Pool(int n) {
-    for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
-  }
-  ~Pool() {
-    {
-      std::lock_guard<std::mutex> lk(m_);
-      quit_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
-  int size() const { return (int)th_.size() + 1; }
-  void run(int parts, const std::function<void(int)>& fn) {
-    parts = std::max(1, std::min(parts, size()));
-    if (parts == 1) { fn(0); return; }
-    auto job = std::make_shared<Job>();
-    job->fn = &fn;
-    job->parts = parts;
-    {
-      std::lock_guard<std::mutex> lk(m_);
-      jobs_.push_back(job);
-    }
-    cv_.notify_all();
-    for (int p; (p = job->next.fetch_add(1)) < parts;) {   // the caller works too
-      fn(p);
-      finish(*job);
-    }
-    std::unique_lock<std::mutex> lk(m_);
-    done_cv_.wait(lk, [&] { return job->done == parts; });
-    drop(job.get());
-  }
-
- private:
-  struct Job {
-    const std::function<void(int)>* fn = nullptr;
-    int parts = 0;
-    std::atomic<int> next{0};
-    int done = 0;                                  // guarded by m_
-  };
-  void finish(Job& j) {
-    std::lock_guard<std::mutex> lk(m_);
-    if (++j.done == j.parts) done_cv_.notify_all();
-  }
-  void drop(Job* j) {                              // m_ held
-    for (size_t i = 0; i < jobs_.size(); ++i)
-      if (jobs_[i].get() == j) { jobs_.erase(jobs_.begin() + i); return; }
-  }
-  void loop() {
-    for (;;) {
-      std::shared_ptr<Job> job;
-      int p = 0;
-      {
-        std::unique_lock<std::mutex> lk(m_);
-        for (;;) {
-          if (quit_) return;
-          while (!jobs_.empty()) {                 // a job with parts left to claim
-            p = jobs_.front()->next.fetch_add(1);
-            if (p < jobs_.front()->parts) { job = jobs_.front(); break; }
-            jobs_.erase(jobs_.begin());            // fully claimed: its caller finishes it
-          }
-          if (job) break;
-          cv_.wait(lk);
-        }
-      }
-      (*job->fn)(p);
-      finish(*job);
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex m_;
-  std::condition_variable cv_, done_cv_;
-  std::vector<std::shared_ptr<Job>> jobs_;
-  bool quit_ = false;
-};
-
-// CPUs this process may run on: the affinity mask, capped by the cgroup v2
-// CPU quota when one is set (a GPU box shows 256 CPUs under a 16-CPU quota).
-int host_cpus() {
-  int n = (int)std::thread::hardware_concurrency();
-  cpu_set_t set;
-  if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
-  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
-    char quota[32] = {0};
-    long long period = 0;
-    if (fscanf(f, "%31s %lld", quota, &period) == 2 && strcmp(quota, "max") != 0 && period > 0) {
-      const long long q = atoll(quota);
-      if (q > 0) n = std::min<long long>(n, std::max<long long>(1, (q + period - 1) / period));
-    }
-    fclose(f);
-  }
-  return std::max(1, n);
-}
-
-// memcpy split over the pool (large copies only: one core streams ~10 GB/s)
-void par_copy(Pool* pool, void* dst, const void* src, size_t bytes) {
-  constexpr size_t kMin = size_t(1) << 20;
-  if (!pool || bytes < kMin) { if (bytes) memcpy(dst, src, bytes); return; }
-  const int parts = (int)std::min<size_t>(pool->size(), bytes / (kMin / 2));
-  const size_t per = round_up((bytes + parts - 1) / parts, 4096);
-  pool->run(parts, [&](int p) {
-    const size_t lo = std::min(bytes, p * per), hi = std::min(bytes, lo + per);
-    if (hi > lo) memcpy((uint8_t*)dst + lo, (const uint8_t*)src + lo, hi - lo);
-  });
-}
-
-// Several copies as one pool pass: the total is cut into equal byte ranges,
-// one per thread, each range spanning whichever segments it covers.
-struct CopySeg {
-  uint8_t* dst;
-  const uint8_t* src;
-  size_t bytes;
-};
-void par_copy_segs(Pool* pool, const CopySeg* seg, int ns) {
-  constexpr size_t kMin = size_t(1) << 20;
-  size_t total = 0;
-  for (int i = 0; i < ns; ++i) total += seg[i].bytes;
-  auto copy_range = [&](size_t lo, size_t hi) {       // [lo, hi) of the concatenation
-    size_t base = 0;
-    for (int i = 0; i < ns && lo < hi; base += seg[i].bytes, ++i) {
-      const size_t a = std::max(lo, base), b = std::min(hi, base + seg[i].bytes);
-      if (a < b) memcpy(seg[i].dst + (a - base), seg[i].src + (a - base), b - a);
-    }
-  };
-  if (!pool || total < kMin) { copy_range(0, total); return; }
-  const int parts = (int)std::min<size_t>(pool->size(), total / (kMin / 2));
-  const size_t per = round_up((total + parts - 1) / parts, 4096);
-  pool->run(parts, [&](int p) { copy_range(std::min(total, p * per), std::min(total, (p + 1) * per)); });
-}
-
-// One persistent thread per extra device: runs the device's slices of host
-// batches, in the order they were posted.  Every post gets its own future, so
-// concurrent callers of one context (gv_ctx is thread-safe) each wait for
-// THEIR slice, never for another caller's.
-class Worker {
- public:
-  Worker() : th_([this] { loop(); }) {}
-  ~Worker() {
-    {
-      std::lock_guard<std::mutex> lk(m_);
-      quit_ = true;
-    }
-    cv_.notify_all();
-    th_.join();
-  }
-  std::future<int> post(std::function<int()> job) {
-    auto task = std::make_shared<std::packaged_task<int()>>(std::move(job));
-    std::future<int> f = task->get_future();
-    {
-      std::lock_guard<std::mutex> lk(m_);
-      q_.push_back([task] { (*task)(); });
-    }
-    cv_.notify_all();
-    return f;
-  }
-
- private:
-  void loop() {
-    for (;;) {
-      std::function<void()> job;
-      {
-        std::unique_lock<std::mutex> lk(m_);
-        cv_.wait(lk, [this] { return quit_ || !q_.empty(); });
-        if (q_.empty()) return;                  // quit with nothing left
-        job = std::move(q_.front());
-        q_.pop_front();
-      }
-      job();
-    }
-  }
-  std::mutex m_;
-  std::condition_variable cv_;
-  std::deque<std::function<void()>> q_;
-  bool quit_ = false;
-  std::thread th_;
-};
+// Pool, Worker, par_copy*, host_cpus, run_sliced: gv_stage.h
+using gvstage::CopySeg;
+using gvstage::Pool;
+using gvstage::Worker;
+using gvstage::host_cpus;
+using gvstage::par_copy;
+using gvstage::par_copy_segs;
+using gvstage::run_sliced;
 
 // ------------------------------------------------------------ device state
 // Device scratch of one batch chunk of C lanes (C % 256 == 0): the staged
@@ -345,7 +171,7 @@ struct Dev {
   uint32_t* edk_s[2] = {nullptr, nullptr};
   size_t edk_s_cap[2] = {0, 0};
   std::mutex mu;
-  Pool* pool = nullptr;                           // staging memcpy threads: the context's shared pool
+  Pool* pool = nullptr;                           // staging memcpy threads of this device (owned)
   Worker* worker = nullptr;                       // slice runner (devices 1..n-1 of a context)
   // pipelined device-resident calls on the context stream (gv_dev_verify_*,
   // stream NULL): the front kernels of call k+1 run under call k's ladder
@@ -626,9 +452,9 @@ struct gv_ctx {
   size_t pipe_chunk = 262144;   // host path: first chunk of the two-set copy/compute pipeline (0 = max_batch;
                                 // profiles/r03/hostpath_sweep.jsonl: 262144 x 4 steadiest on pageable input)
   int pipe_growth = 4;          // host path: each later chunk at most this times the one before
-  int stage_threads = 8;        // host path: staging threads of the context's shared pool (gv_open: half
-                                // the process's CPUs -- affinity capped by the cgroup quota -- at most 8)
-  Pool* pool = nullptr;
+  int stage_threads = 8;        // host path: staging threads per device, its slice's thread included (gv_open:
+                                // gvstage::stage_pool_threads -- half the process's CPUs, affinity capped by
+                                // the cgroup quota, split over the devices, 1..8 each)
   bool time_kernels = false;
   bool fault_inject = false;
   bool lat_zero_copy = true;    // host-buffer batches on the sliced kernels read the pinned staging buffer and write
@@ -1279,6 +1105,12 @@ int slice_group(gv_ctx* ctx, Dev* d, size_t lo, size_t n, const HostBatch& hb, K
   return GV_OK;   // the set stays acquired until run_slice releases it after the last chunk
 }
 
+std::vector<Worker*> workers(const gv_ctx* ctx) {
+  std::vector<Worker*> w;
+  for (Dev* d : ctx->devs) w.push_back(d->worker);
+  return w;
+}
+
 // Verify items [lo, hi) of a host batch on one device: chunks alternate
 // between the two sets so staging + H2D of one overlaps the kernels of the other.
 int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const HostBatch& hb) {
@@ -1425,21 +1257,8 @@ int run_ed_host(gv_ctx* ctx, size_t n, const EdHost& hb) {
   if (!hb.pub32 || !hb.sig64 || !hb.off || !hb.len || !hb.out_ok) return GV_EINVAL;
   for (size_t i = 0; i < n; ++i)
     if (hb.len[i] && !hb.blob) return GV_EINVAL;
-  const size_t nd = ctx->devs.size();
-  const size_t per = round_up((n + nd - 1) / nd, 256);
-  std::vector<int> rcs(nd, GV_OK);
-  std::vector<std::future<int>> futs(nd);
-  for (size_t k = 1; k < nd; ++k) {
-    const size_t lo = std::min(n, k * per), hi = std::min(n, (k + 1) * per);
-    if (lo >= hi) continue;
-    Dev* d = ctx->devs[k];
-    futs[k] = d->worker->post([=, &hb]() { return ed_slice(ctx, d, lo, hi, hb); });
-  }
-  rcs[0] = ed_slice(ctx, ctx->devs[0], 0, std::min(n, per), hb);
-  for (size_t k = 1; k < nd; ++k)
-    if (futs[k].valid()) rcs[k] = futs[k].get();
-  for (int rc : rcs) if (rc) return rc;
-  return GV_OK;
+  return run_sliced(workers(ctx), n, 256,
+                    [&](size_t k, size_t lo, size_t hi) { return ed_slice(ctx, ctx->devs[k], lo, hi, hb); });
 }
 
 int run_host(gv_ctx* ctx, size_t n, const HostBatch& hb_in) {
@@ -1451,21 +1270,9 @@ int run_host(gv_ctx* ctx, size_t n, const HostBatch& hb_in) {
   HostBatch hb = hb_in;
   hb.pinned = hb.dig32 && is_pinned(hb.slots ? (const void*)hb.slots : hb.pub33) && is_pinned(hb.sig64) &&
               is_pinned(hb.dig32);
-  const size_t nd = ctx->devs.size();
-  const size_t per = round_up((n + nd - 1) / nd, 256);
-  std::vector<int> rcs(nd, GV_OK);
-  std::vector<std::future<int>> futs(nd);
-  for (size_t k = 1; k < nd; ++k) {             // devices 1.. on their persistent workers
-    const size_t lo = std::min(n, k * per), hi = std::min(n, (k + 1) * per);
-    if (lo >= hi) continue;
-    Dev* d = ctx->devs[k];
-    futs[k] = d->worker->post([=, &hb]() { return run_slice(ctx, d, lo, hi, hb); });
-  }
-  rcs[0] = run_slice(ctx, ctx->devs[0], 0, std::min(n, per), hb);   // device 0 on the caller
-  for (size_t k = 1; k < nd; ++k)
-    if (futs[k].valid()) rcs[k] = futs[k].get();
-  for (int rc : rcs) if (rc) return rc;
-  return GV_OK;
+  // device 0's slice on the caller, devices 1.. on their persistent workers
+  return run_sliced(workers(ctx), n, 256,
+                    [&](size_t k, size_t lo, size_t hi) { return run_slice(ctx, ctx->devs[k], lo, hi, hb); });
 }
 
 void free_set(Set& s) {
@@ -1531,14 +1338,12 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* zc = getenv("GV_LAT_ZC")) ctx->lat_zero_copy = strcmp(zc, "0") != 0;
   if (const char* pl = getenv("GV_PIPELINE")) ctx->pipeline_dev = strcmp(pl, "0") != 0;
   if (const char* gk = getenv("GV_GROUP_KEYS")) ctx->group_keys = strcmp(gk, "0") != 0;
-  ctx->stage_threads = std::max(1, std::min(8, host_cpus() / 2));   // half the quota: the callers, HIP's
-                                                                    // own threads and the pool share it
-  ctx->pool = new Pool(ctx->stage_threads - 1);
+  ctx->stage_threads = gvstage::stage_pool_threads(host_cpus(), (int)ids.size());
   for (size_t k = 0; k < ids.size(); ++k) {
     Dev* d = new Dev();
     d->id = ids[k];
     ctx->devs.push_back(d);
-    d->pool = ctx->pool;
+    d->pool = new Pool(ctx->stage_threads - 1);
     if (k > 0) d->worker = new Worker();
     bool ok = hipSetDevice(d->id) == hipSuccess;
     // Stream priorities of the pipelined device-resident calls (env
@@ -1625,9 +1430,9 @@ void gv_close(gv_ctx* ctx) {
     for (hipEvent_t e : {d->hi_done[0], d->hi_done[1], d->bits_ev[0], d->bits_ev[1]})
       if (e) (void)hipEventDestroy(e);
     if (d->plain_done) (void)hipEventDestroy(d->plain_done);
+    delete d->pool;
     delete d;
   }
-  delete ctx->pool;
   delete ctx;
 }
 
@@ -1980,20 +1785,9 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
       // large batches: one signature per lane against the key tables
       // (k_ed_keyed), split over the devices like run_ed_host
       const EdKeyedHost hb{slot, sig64, msg_blob, msg_off, msg_len, out_ok};
-      const size_t nd = ctx->devs.size(), per = round_up((n + nd - 1) / nd, 256);
-      std::vector<int> rcs(nd, GV_OK);
-      std::vector<std::future<int>> futs(nd);
-      for (size_t k = 1; k < nd; ++k) {
-        const size_t lo = std::min(n, k * per), hi = std::min(n, (k + 1) * per);
-        if (lo >= hi) continue;
-        Dev* dk = ctx->devs[k];
-        futs[k] = dk->worker->post([=, &hb]() { return ed_keyed_slice(ctx, dk, lo, hi, hb, kcount); });
-      }
-      rcs[0] = ed_keyed_slice(ctx, ctx->devs[0], 0, std::min(n, per), hb, kcount);
-      for (size_t k = 1; k < nd; ++k)
-        if (futs[k].valid()) rcs[k] = futs[k].get();
-      for (int rc : rcs) if (rc) return rc;
-      return GV_OK;
+      return run_sliced(workers(ctx), n, 256, [&](size_t k, size_t lo, size_t hi) {
+        return ed_keyed_slice(ctx, ctx->devs[k], lo, hi, hb, kcount);
+      });
     }
     if (n > ctx->ed_lat_max || kcount == 0) {
       // large batches (ed_keyed 0): the throughput kernels over the slots' raw keys
@@ -2173,12 +1967,13 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
     ctx->pipe_growth = (int)val;
   } else if (!strcmp(key, "stage_threads")) {
     if (val < 1 || val > 64) return GV_EINVAL;
-    std::vector<std::unique_lock<std::mutex>> held;   // no device stages while the pool is replaced
+    std::vector<std::unique_lock<std::mutex>> held;   // no device stages while its pool is replaced
     for (Dev* d : ctx->devs) held.emplace_back(d->mu);
     ctx->stage_threads = (int)val;
-    delete ctx->pool;
-    ctx->pool = new Pool((int)val - 1);
-    for (Dev* d : ctx->devs) d->pool = ctx->pool;
+    for (Dev* d : ctx->devs) {
+      delete d->pool;
+      d->pool = new Pool((int)val - 1);
+    }
   } else if (!strcmp(key, "group_keys")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->group_keys = val != 0;
