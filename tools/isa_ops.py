@@ -5,7 +5,8 @@ built from the product sources with the exceptional branches compiled out) to
 device assembly and counts each kernel's instructions by class, minus the
 load/store frame.  Then weights the counts by the ladder's operation counts
 per verify (derived from the ladder's schedule in gv_kernels.hip k_ecmult_k4:
-6 x 5 doublings, 52 Q adds of which 26 lambda-Q, 14 G adds, one final check)
+6 x 5 doublings, 52 Q adds of which 26 lambda-Q, 11 G adds, one final check;
+--glv: the 14 G adds of the GLV G schedule)
 and prints the predicted VALU instructions per verify next to the PMC figure.
 
 Usage: python tools/isa_ops.py [--json out.json] [--defs "-DFOO=1"]
@@ -21,10 +22,13 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "tools", "isa_ops.hip")
 
-# operations per verify of k_ecmult_k4 (schedule: positions 6..0, 5 doublings
-# between positions; Q windows per group 7, 7, 6, 6 -> 26 per GLV half, each
-# with a Q and a lambda-Q digit; G windows j = 0..6 per half, G and lambda-G)
-LADDER_OPS = {"isa_dbl": 30, "isa_addq": 26, "isa_addlq": 26, "isa_addg": 14, "isa_finish": 1}
+# operations per verify of k_ecmult_k4<true> (schedule: positions 6..0, 5
+# doublings between positions; Q windows per group 7, 7, 6, 6 -> 26 per GLV
+# half, each with a Q and a lambda-Q digit; G: 11 25-bit windows of the
+# unsplit u1)
+LADDER_OPS = {"isa_dbl": 30, "isa_addq": 26, "isa_addlq": 26, "isa_addg": 11, "isa_finish": 1}
+# the GLV G schedule (gv_set_option "gfull" 0): 7 20-bit windows per GLV half
+LADDER_OPS_GLV = dict(LADDER_OPS, isa_addg=14)
 
 
 def classify(op):
@@ -70,6 +74,7 @@ def main():
     ap.add_argument("--json")
     ap.add_argument("--defs", default="")
     ap.add_argument("--asm", default="/tmp/isa_ops.s")
+    ap.add_argument("--glv", action="store_true", help="the GLV G schedule (14 G additions)")
     a = ap.parse_args()
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
            SRC, "-o", a.asm] + a.defs.split()
@@ -89,15 +94,16 @@ def main():
         valu = net.get("mad64", 0) + net.get("mul32", 0) + net.get("valu", 0)
         print(f"{name:11s} mad64 {net.get('mad64', 0):5d}  other VALU {net.get('mul32', 0) + net.get('valu', 0):5d}"
               f"  VALU {valu:5d}  s_nop {net.get('s_nop', 0):4d}  vmem {net.get('vmem', 0):3d}")
+    ops = LADDER_OPS_GLV if a.glv else LADDER_OPS
     pred = collections.Counter()
-    for name, cnt in LADDER_OPS.items():
+    for name, cnt in ops.items():
         for c, n in rows[name]["net"].items():
             pred[c] += cnt * n
     valu = pred["mad64"] + pred["mul32"] + pred["valu"]
-    print(f"per verify (ops {LADDER_OPS}): mad64 {pred['mad64']}, other VALU {pred['mul32'] + pred['valu']}, "
+    print(f"per verify (ops {ops}): mad64 {pred['mad64']}, other VALU {pred['mul32'] + pred['valu']}, "
           f"VALU {valu}, s_nop {pred['s_nop']}")
     if a.json:
-        json.dump({"ladder_ops_per_verify": LADDER_OPS, "per_op": rows, "per_verify": dict(pred),
+        json.dump({"ladder_ops_per_verify": ops, "per_op": rows, "per_verify": dict(pred),
                    "valu_per_verify": valu, "defs": a.defs}, open(a.json, "w"), indent=1)
 
 
