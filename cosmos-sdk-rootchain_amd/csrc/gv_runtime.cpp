@@ -452,6 +452,8 @@ struct gv_ctx {
   size_t pipe_chunk = 262144;   // host path: first chunk of the two-set copy/compute pipeline (0 = max_batch;
                                 // profiles/r03/hostpath_sweep.jsonl: 262144 x 4 steadiest on pageable input)
   int pipe_growth = 4;          // host path: each later chunk at most this times the one before
+  size_t slice_plain_first = 0; // host path, grouped slices: this many items first on the per-item pipeline while
+                                // the slice's key tables build (0 = off; GV_SLICE_PLAIN_FIRST)
   int stage_threads = 8;        // host path: staging threads per device, its slice's thread included (gv_open:
                                 // gvstage::stage_pool_threads -- half the process's CPUs, affinity capped by
                                 // the cgroup quota, split over the devices, 1..8 each)
@@ -682,7 +684,7 @@ struct KeyArena {
 int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint8_t* sig, const uint8_t* dig,
            const uint8_t* blob, const uint64_t* off, const uint32_t* len, uint64_t* bits_out,
            hipStream_t st, const uint32_t* kslot = nullptr, uint8_t* out8 = nullptr, hipStream_t st_ecm = nullptr,
-           const KeyArena* ka = nullptr) {
+           const KeyArena* ka = nullptr, bool no_group = false) {
   if (n == 0 || n > kMaxItems) return GV_EINVAL;
   const size_t C = round_up(n, 256);
   int rc = ensure_cap(s, C);
@@ -776,7 +778,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     }
   } else {
     uint32_t* sort_base = s->qtab;                // keyed: the Q-table region is free
-    if (!kslot && pub && ctx->group_keys && n >= ctx->group_min) {
+    if (!kslot && pub && ctx->group_keys && !no_group && n >= ctx->group_min) {
       rc = group_keys(ctx, d, s, b, n, st, &sort_base);
       if (rc) return rc;
     }
@@ -854,6 +856,8 @@ struct HostBatch {
   const uint32_t* d_slots = nullptr;   // slice grouping: per-item key ids on the device (offset lo)
   const KeyArena* ka = nullptr;        // ... and the arena they index
   size_t d_slots_lo = 0;
+  bool plain = false;                  // the per-item pub33 pipeline, no in-batch grouping (a grouped
+                                       // slice's first chunk, run while the slice's key tables build)
 };
 
 // Host memory the device can read directly (hipHostMalloc / gv_host_alloc /
@@ -957,7 +961,7 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
     CK(hipMemcpyAsync(s->d_in + L.third, dp, cn * 32, hipMemcpyHostToDevice, s->st));
     const uint8_t* din = s->d_in;
     rc = launch(ctx, d, s, cn, keyed ? nullptr : din, din + L.sig, din + L.third, nullptr, nullptr, nullptr, s->bits,
-                s->st, dslots ? dsl : keyed ? (const uint32_t*)din : nullptr, nullptr, nullptr, hb.ka);
+                s->st, dslots ? dsl : keyed ? (const uint32_t*)din : nullptr, nullptr, nullptr, hb.ka, hb.plain);
     if (rc) return rc;
     CK(hipMemcpyAsync(s->h_bits, s->bits, ((cn + 63) / 64) * 8, hipMemcpyDeviceToHost, s->st));
     CK(hipEventRecord(s->done, s->st));
@@ -1024,7 +1028,7 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
   rc = launch(ctx, d, s, cn, keyed ? nullptr : din, din + L.sig, msgs ? nullptr : din + L.third,
               msgs ? s->d_blob : nullptr, msgs ? (const uint64_t*)(din + L.third) : nullptr,
               msgs ? (const uint32_t*)(din + L.len) : nullptr, s->bits, s->st,
-              dslots ? dsl : keyed ? (const uint32_t*)din : nullptr, nullptr, nullptr, hb.ka);
+              dslots ? dsl : keyed ? (const uint32_t*)din : nullptr, nullptr, nullptr, hb.ka, hb.plain);
   if (rc) return rc;
   CK(hipMemcpyAsync(s->h_bits, s->bits, ((cn + 63) / 64) * 8, hipMemcpyDeviceToHost, s->st));
   CK(hipEventRecord(s->done, s->st));
@@ -1168,12 +1172,36 @@ int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const HostBatch& hb) {
     }
   }
   const HostBatch& hr = grouped ? hg : hb;
+  // a grouped slice's first `slice_plain_first` items run the per-item pub33
+  // pipeline (their own key parse and Q tables) while the slice's key tables
+  // build on the grouping set's side stream: the GPU has ladder work from the
+  // start instead of waiting for the tables; the other chunks follow the ramp
+  HostBatch hp = hb;
+  hp.plain = true;
+  const size_t np = grouped && ctx->slice_plain_first
+                        ? std::min(round_up(ctx->slice_plain_first, 256), round_up(n / 4, 256)) : 0;
+  if (np) {
+    std::vector<size_t> rest{np};
+    size_t c = std::min(ctx->pipe_chunk ? ctx->pipe_chunk : ctx->max_batch, ctx->max_batch), left = n - np;
+    while (left) {
+      const size_t take = std::min(left, c);
+      rest.push_back(take);
+      left -= take;
+      c = std::min(ctx->max_batch, c * (size_t)ctx->pipe_growth);
+    }
+    const size_t m = rest.size();
+    if (m >= 3 && 2 * rest[m - 1] < rest[m - 2] && rest[m - 1] + rest[m - 2] <= ctx->max_batch) {
+      rest[m - 2] += rest[m - 1];
+      rest.pop_back();
+    }
+    sizes.swap(rest);
+  }
   int k = 0;
   size_t c0 = lo;
   for (size_t i = 0; i < sizes.size() && rc == GV_OK; c0 += sizes[i], ++i, k ^= 1) {
     Set* s = &d->set[k];
     if (s->busy && (rc = harvest(d, s, hr))) break;
-    rc = submit(ctx, d, s, c0, sizes[i], hr);
+    rc = submit(ctx, d, s, c0, sizes[i], (np && i == 0) ? hp : hr);
   }
   for (Set& s : d->set)                          // drain (also after an error)
     if (s.busy) {
@@ -1338,6 +1366,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* zc = getenv("GV_LAT_ZC")) ctx->lat_zero_copy = strcmp(zc, "0") != 0;
   if (const char* pl = getenv("GV_PIPELINE")) ctx->pipeline_dev = strcmp(pl, "0") != 0;
   if (const char* gk = getenv("GV_GROUP_KEYS")) ctx->group_keys = strcmp(gk, "0") != 0;
+  if (const char* pf = getenv("GV_SLICE_PLAIN_FIRST")) ctx->slice_plain_first = strtoull(pf, nullptr, 10);
   ctx->stage_threads = gvstage::stage_pool_threads(host_cpus(), (int)ids.size());
   for (size_t k = 0; k < ids.size(); ++k) {
     Dev* d = new Dev();
@@ -1974,6 +2003,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
       delete d->pool;
       d->pool = new Pool((int)val - 1);
     }
+  } else if (!strcmp(key, "slice_plain_first")) {
+    if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
+    ctx->slice_plain_first = (size_t)val;
   } else if (!strcmp(key, "group_keys")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->group_keys = val != 0;

@@ -127,3 +127,29 @@ def test_host_slice_grouped_once_for_all_chunks(ver):
     b3, _ = ver.group_stats()
     assert np.array_equal(ver.verify_batch_digests(pub3, sig3, dig3), exp3)
     assert ver.group_stats()[0] == b3
+
+
+def test_host_slice_plain_first_chunk(ver):
+    """gv_set_option("slice_plain_first"): a grouped host slice's first chunk
+    runs the per-item pipeline while the slice's key tables build; the
+    verdicts are the same, the slice is still grouped once, and exactly one
+    chunk takes the per-item route."""
+    pub, sig, dig, exp = bench.make_digest_workload(600_000, 0x6F, 4096, 0.25, 16)
+    ver.set_option("slice_plain_first", 65536)
+    try:
+        b0, _ = ver.group_stats()
+        r0 = ver.route_stats()
+        got = ver.verify_batch_digests(pub, sig, dig)
+        r1 = ver.route_stats()
+        assert ver.group_stats()[0] - b0 == 1
+        assert r1["pub33"] - r0["pub33"] == 1
+        assert np.array_equal(got, exp)
+        hp = [ver.host_array(a.shape, a.dtype) for a in (pub, sig, dig)]
+        for h, a in zip(hp, (pub, sig, dig)):
+            h[...] = a
+        bits = ver.verify_batch_digests_bits(*hp)
+        for h in hp:
+            ver.host_free(h)
+        assert np.array_equal(bench.unpack_bits(bits, len(exp)), exp)
+    finally:
+        ver.set_option("slice_plain_first", 0)
