@@ -227,9 +227,13 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * copy/compute pipeline per device, default 262144; 0 = one chunk per
  * max_batch), "pipe_growth" (each later chunk at most this many times the one
  * before, default 4: the staging of chunk i+1 hides under the kernels of
- * chunk i), "stage_threads" (pageable -> pinned staging copy threads of
- * the context's ONE pool shared by its devices, default half the process's
- * CPUs -- affinity capped by the cgroup quota -- at most 8),
+ * chunk i), "stage_threads" (pageable -> pinned staging copy threads PER
+ * DEVICE, the slice's own thread included: each device stages through its own
+ * pool; default half the process's CPUs -- affinity capped by the cgroup
+ * quota -- split over the devices, 1..8 each),
+ * "slice_plain_first" (host-buffer pub33 slices grouped by key: this many
+ * items first on the per-item pipeline while the slice's key tables build;
+ * 0 = off, the default; env GV_SLICE_PLAIN_FIRST),
  * "group_keys" (0/1: a pub33 batch past the small-batch bound with at least
  * "group_min" items (default 16384) whose distinct keys number at most
  * items / "group_div" (default 5) parses each distinct key once -- grouped
@@ -251,9 +255,20 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * to item order; same verdicts; default 1, env GV_SORT_KEYS),
  * "pipeline_dev" (0/1: device-resident calls on the context stream past the
  * small-batch bound are pipelined -- consecutive calls alternate scratch sets,
- * their unpack / s^-1 / prep kernels run on a low-priority stream under the
- * previous call's ladder, every ladder on one high-priority stream in call
- * order; a caller stream is never pipelined; default 1, env GV_PIPELINE),
+ * their unpack / s^-1 / prep kernels run under the previous call's ladder on
+ * a stream above the ladders' priority (env GV_LADDER_PRIO "front", the
+ * default; "ladder" / "equal" for A/B); a caller stream is never pipelined;
+ * default 1, env GV_PIPELINE),
+ * "two_ladders" (0/1: pipelined calls' ladders alternate two streams, so the
+ * next ladder fills the current one's tail; bitmap writes stay in call order;
+ * default 1, env GV_TWO_LADDERS),
+ * "gfull" (0/1: keyed batches on the 4-group ladder add G from the unsplit
+ * u1 = e/s -- 11 signed 25-bit windows from tables of 2^o G (6 GiB per device,
+ * built on first keyed use) -- instead of 14 GLV windows; same verdicts;
+ * default 1, env GV_GFULL; route counter GV_ROUTE_K4F),
+ * "k6" (0/1: in-batch grouped keys on the 6-bit-window ladder k_ecmult_k6 --
+ * 32-entry key tables, 24-bit G windows (4 GiB); same verdicts; default 0,
+ * env GV_K6),
  * "time_kernels" (0/1: record HIP events around each kernel stage; the
  * ladder's time is its own start to end),
  * "fault_inject" (0/1: every verify call fails with GV_EFAULT; test hook). */
