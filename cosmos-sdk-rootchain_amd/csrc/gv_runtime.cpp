@@ -452,8 +452,9 @@ struct gv_ctx {
   size_t pipe_chunk = 262144;   // host path: first chunk of the two-set copy/compute pipeline (0 = max_batch;
                                 // profiles/r03/hostpath_sweep.jsonl: 262144 x 4 steadiest on pageable input)
   int pipe_growth = 4;          // host path: each later chunk at most this times the one before
-  size_t slice_plain_first = 0; // host path, grouped slices: this many items first on the per-item pipeline while
-                                // the slice's key tables build (0 = off; GV_SLICE_PLAIN_FIRST)
+  size_t slice_plain_first = 0; // host path, slices to be grouped: this many items first on the per-item pipeline,
+                                // submitted before the rest's keys are sent, grouped and tabulated (0 = off;
+                                // GV_SLICE_PLAIN_FIRST)
   int stage_threads = 8;        // host path: staging threads per device, its slice's thread included (gv_open:
                                 // gvstage::stage_pool_threads -- half the process's CPUs, affinity capped by
                                 // the cgroup quota, split over the devices, 1..8 each)
@@ -1137,71 +1138,67 @@ int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const HostBatch& hb) {
   // (pageable -> pinned copy, H2D) while the one before it computes.  Else
   // equal chunks of at most max_batch.  Every chunk but the last is a multiple
   // of 256 (harvest copies bitmap words).
-  std::vector<size_t> sizes;
-  if (n > (hb.slots ? ctx->lat_max_keyed : ctx->lat_max) && ctx->pipe_chunk) {
-    size_t c = std::min(ctx->pipe_chunk, ctx->max_batch), left = n;
-    while (left) {
-      const size_t take = std::min(left, c);
-      sizes.push_back(take);
-      left -= take;
-      c = std::min(ctx->max_batch, c * (size_t)ctx->pipe_growth);
+  const bool pipelined = n > (hb.slots ? ctx->lat_max_keyed : ctx->lat_max) && ctx->pipe_chunk;
+  auto chunk_sizes = [&](size_t count) {
+    std::vector<size_t> sz;
+    if (pipelined) {
+      size_t c = std::min(ctx->pipe_chunk, ctx->max_batch), left = count;
+      while (left) {
+        const size_t take = std::min(left, c);
+        sz.push_back(take);
+        left -= take;
+        c = std::min(ctx->max_batch, c * (size_t)ctx->pipe_growth);
+      }
+      const size_t m = sz.size();             // a runt tail joins the chunk before it
+      if (m >= 2 && 2 * sz[m - 1] < sz[m - 2] && sz[m - 1] + sz[m - 2] <= ctx->max_batch) {
+        sz[m - 2] += sz[m - 1];
+        sz.pop_back();
+      }
+    } else {
+      const size_t nch = (count + ctx->max_batch - 1) / ctx->max_batch;
+      const size_t chunk = std::min(ctx->max_batch, round_up((count + nch - 1) / nch, 256));
+      for (size_t c0 = 0; c0 < count; c0 += chunk) sz.push_back(std::min(chunk, count - c0));
     }
-    const size_t m = sizes.size();          // a runt tail joins the chunk before it
-    if (m >= 2 && 2 * sizes[m - 1] < sizes[m - 2] && sizes[m - 1] + sizes[m - 2] <= ctx->max_batch) {
-      sizes[m - 2] += sizes[m - 1];
-      sizes.pop_back();
-    }
-  } else {
-    const size_t nch = (n + ctx->max_batch - 1) / ctx->max_batch;
-    const size_t chunk = std::min(ctx->max_batch, round_up((n + nch - 1) / nch, 256));
-    for (size_t c0 = 0; c0 < n; c0 += chunk) sizes.push_back(std::min(chunk, n - c0));
-  }
+    return sz;
+  };
+  std::vector<size_t> sizes = chunk_sizes(n);
   int rc = GV_OK;
   // a pub33 slice big enough for the pipeline: group its keys once for all chunks
+  const bool try_group = hb.pub33 && !hb.slots && ctx->group_keys && n >= ctx->group_min && sizes.size() > 1;
+  // ... and with slice_plain_first, its first items run the per-item pub33
+  // pipeline (their own key parse and Q tables), submitted BEFORE the
+  // grouping: their H2D and kernels run while the rest of the slice's keys
+  // are sent, grouped and tabulated, so the GPU has ladder work from the
+  // start instead of waiting for the key tables
+  HostBatch hp = hb;
+  hp.plain = true;
+  const size_t np = try_group && pipelined && ctx->slice_plain_first
+                        ? std::min(round_up(ctx->slice_plain_first, 256), round_up(n / 4, 256)) : 0;
+  int k = 0;
+  if (np) {
+    if ((rc = submit(ctx, d, &d->set[0], lo, np, hp))) return rc;
+    k = 1;
+  }
   HostBatch hg = hb;
   KeyArena ka;
   bool grouped = false;
-  if (hb.pub33 && !hb.slots && ctx->group_keys && n >= ctx->group_min && sizes.size() > 1) {
+  if (try_group) {
     const uint32_t* dsl = nullptr;
-    if ((rc = slice_group(ctx, d, lo, n, hb, &ka, &dsl))) return rc;
-    if (dsl) {
+    rc = slice_group(ctx, d, lo + np, n - np, hb, &ka, &dsl);
+    if (rc == GV_OK && dsl) {
       grouped = true;
       hg.d_slots = dsl;
-      hg.d_slots_lo = lo;
+      hg.d_slots_lo = lo + np;
       hg.ka = &ka;
     }
   }
   const HostBatch& hr = grouped ? hg : hb;
-  // a grouped slice's first `slice_plain_first` items run the per-item pub33
-  // pipeline (their own key parse and Q tables) while the slice's key tables
-  // build on the grouping set's side stream: the GPU has ladder work from the
-  // start instead of waiting for the tables; the other chunks follow the ramp
-  HostBatch hp = hb;
-  hp.plain = true;
-  const size_t np = grouped && ctx->slice_plain_first
-                        ? std::min(round_up(ctx->slice_plain_first, 256), round_up(n / 4, 256)) : 0;
-  if (np) {
-    std::vector<size_t> rest{np};
-    size_t c = std::min(ctx->pipe_chunk ? ctx->pipe_chunk : ctx->max_batch, ctx->max_batch), left = n - np;
-    while (left) {
-      const size_t take = std::min(left, c);
-      rest.push_back(take);
-      left -= take;
-      c = std::min(ctx->max_batch, c * (size_t)ctx->pipe_growth);
-    }
-    const size_t m = rest.size();
-    if (m >= 3 && 2 * rest[m - 1] < rest[m - 2] && rest[m - 1] + rest[m - 2] <= ctx->max_batch) {
-      rest[m - 2] += rest[m - 1];
-      rest.pop_back();
-    }
-    sizes.swap(rest);
-  }
-  int k = 0;
-  size_t c0 = lo;
+  if (np) sizes = chunk_sizes(n - np);
+  size_t c0 = lo + np;
   for (size_t i = 0; i < sizes.size() && rc == GV_OK; c0 += sizes[i], ++i, k ^= 1) {
     Set* s = &d->set[k];
     if (s->busy && (rc = harvest(d, s, hr))) break;
-    rc = submit(ctx, d, s, c0, sizes[i], (np && i == 0) ? hp : hr);
+    rc = submit(ctx, d, s, c0, sizes[i], hr);
   }
   for (Set& s : d->set)                          // drain (also after an error)
     if (s.busy) {
