@@ -430,6 +430,16 @@ GV_DEV void build_q_table(u32* qt, u32 qi, u32* qr, u32 C, u32 g, const fe& qx8,
 #else
 #define GV_FRONT_ATTR
 #endif
+// GV_SINV_VGPR: the same cap for k_scalar_inv alone (96: it then fits beside
+// three ladder waves of 136 allocated VGPRs; A/B)
+#ifndef GV_SINV_VGPR
+#define GV_SINV_VGPR 0
+#endif
+#if GV_SINV_VGPR
+#define GV_SINV_ATTR __attribute__((amdgpu_waves_per_eu(512 / GV_SINV_VGPR)))
+#else
+#define GV_SINV_ATTR GV_FRONT_ATTR
+#endif
 // ------------------------------------------------------------- k_scalar_inv
 // w = s^-1 mod n for every lane, Montgomery form (radix 2^29, R = 2^261,
 // secp_sc29.cuh), by Montgomery's trick: each lane folds GV_INV_M signatures
@@ -517,7 +527,7 @@ GV_DEV void sc29_batch_inv_wave(sc29& inv, const sc29& x) {
   sc29_mul(inv, m, tinv);
 }
 
-__global__ __launch_bounds__(256) GV_FRONT_ATTR void k_scalar_inv(u32 C, const u32* in_s, u32* w, u32* pre) {
+__global__ __launch_bounds__(256) GV_SINV_ATTR void k_scalar_inv(u32 C, const u32* in_s, u32* w, u32* pre) {
   const u32 lane = threadIdx.x & 63u;
   const u32 wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   sc29 acc;
