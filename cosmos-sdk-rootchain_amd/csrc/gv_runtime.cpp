@@ -452,6 +452,9 @@ struct gv_ctx {
   size_t pipe_chunk = 262144;   // host path: first chunk of the two-set copy/compute pipeline (0 = max_batch;
                                 // profiles/r03/hostpath_sweep.jsonl: 262144 x 4 steadiest on pageable input)
   int pipe_growth = 4;          // host path: each later chunk at most this times the one before
+  int stage_pieces = 2;         // host path, pageable chunks of >= 65,536 items: staged in this many pieces, each
+                                // piece's H2D behind its copy (1 = one copy then one H2D; GV_STAGE_PIECES):
+                                // 121.4 / 129.4 / 126.2 / 126.8M/s at 1 / 2 / 4 / 8 (profiles/r04/hostpath/stage_pieces_ab.jsonl)
   size_t slice_plain_first = 0; // host path, slices to be grouped: this many items first on the per-item pipeline,
                                 // submitted before the rest's keys are sent, grouped and tabulated (0 = off;
                                 // GV_SLICE_PLAIN_FIRST)
@@ -973,7 +976,29 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
     s->cn = cn;
     return GV_OK;
   }
-  if (!msgs) {                              // keys/slots, signatures, digests: one pool pass
+  const size_t lmax0 = keyed ? ctx->lat_max_keyed : ctx->lat_max;
+  const size_t slmax0 = keyed ? ctx->lat_sl_max_keyed : ctx->lat_sl_max;
+  const bool zc_path = ctx->lat_zero_copy && ctx->lat_sliced && cn <= slmax0 && cn <= lmax0 && !dslots;
+  bool sent = false;
+  if (!msgs && !zc_path && ctx->stage_pieces > 1 && cn >= 65536) {
+    // large pageable chunk: staged in pieces, each piece's H2D right behind
+    // its copy, so the transfer of piece i overlaps the staging of piece i+1
+    if ((rc = set_acquire(s, s->st))) return rc;
+    const size_t per = round_up((cn + ctx->stage_pieces - 1) / ctx->stage_pieces, 256);
+    const size_t kb = keyed ? 4 : 33;
+    for (size_t a = 0; a < cn; a += per) {
+      const size_t m = std::min(per, cn - a);
+      const CopySeg segs[3] = {CopySeg{h + L.sig + a * 64, hb.sig64 + (c0 + a) * 64, m * 64},
+                               CopySeg{h + L.third + a * 32, hb.dig32 + (c0 + a) * 32, m * 32},
+                               keyed ? CopySeg{h + a * 4, (const uint8_t*)(hb.slots + c0 + a), m * 4}
+                                     : CopySeg{h + a * 33, hb.pub33 + (c0 + a) * 33, m * 33}};
+      par_copy_segs(d->pool, segs, dslots ? 2 : 3);
+      if (!dslots) CK(hipMemcpyAsync(s->d_in + a * kb, h + a * kb, m * kb, hipMemcpyHostToDevice, s->st));
+      CK(hipMemcpyAsync(s->d_in + L.sig + a * 64, h + L.sig + a * 64, m * 64, hipMemcpyHostToDevice, s->st));
+      CK(hipMemcpyAsync(s->d_in + L.third + a * 32, h + L.third + a * 32, m * 32, hipMemcpyHostToDevice, s->st));
+    }
+    sent = true;
+  } else if (!msgs) {                       // keys/slots, signatures, digests: one pool pass
     const CopySeg segs[3] = {CopySeg{h + L.sig, hb.sig64 + c0 * 64, cn * 64},
                              CopySeg{h + L.third, hb.dig32 + c0 * 32, cn * 32},
                              keyed ? CopySeg{h, (const uint8_t*)(hb.slots + c0), cn * 4}
@@ -1018,8 +1043,8 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
     s->cn = cn;
     return GV_OK;
   }
-  if ((rc = set_acquire(s, s->st))) return rc;
-  {
+  if (!sent) {
+    if ((rc = set_acquire(s, s->st))) return rc;
     const size_t from = dslots ? L.sig : 0;   // device slots: no key region to send
     CK(hipMemcpyAsync(s->d_in + from, h + from, (msgs ? L.total : L.third + cn * 32) - from, hipMemcpyHostToDevice,
                       s->st));
@@ -1363,6 +1388,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* zc = getenv("GV_LAT_ZC")) ctx->lat_zero_copy = strcmp(zc, "0") != 0;
   if (const char* pl = getenv("GV_PIPELINE")) ctx->pipeline_dev = strcmp(pl, "0") != 0;
   if (const char* gk = getenv("GV_GROUP_KEYS")) ctx->group_keys = strcmp(gk, "0") != 0;
+  if (const char* sp = getenv("GV_STAGE_PIECES")) ctx->stage_pieces = std::max(1, atoi(sp));
   if (const char* pf = getenv("GV_SLICE_PLAIN_FIRST")) ctx->slice_plain_first = strtoull(pf, nullptr, 10);
   ctx->stage_threads = gvstage::stage_pool_threads(host_cpus(), (int)ids.size());
   for (size_t k = 0; k < ids.size(); ++k) {
@@ -2000,6 +2026,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
       delete d->pool;
       d->pool = new Pool((int)val - 1);
     }
+  } else if (!strcmp(key, "stage_pieces")) {
+    if (val < 1 || val > 64) return GV_EINVAL;
+    ctx->stage_pieces = (int)val;
   } else if (!strcmp(key, "slice_plain_first")) {
     if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
     ctx->slice_plain_first = (size_t)val;

@@ -231,6 +231,9 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * DEVICE, the slice's own thread included: each device stages through its own
  * pool; default half the process's CPUs -- affinity capped by the cgroup
  * quota -- split over the devices, 1..8 each),
+ * "stage_pieces" (pageable host chunks of at least 65,536 items are staged
+ * into pinned memory in this many pieces, each piece's H2D right behind its
+ * copy; default 2, env GV_STAGE_PIECES),
  * "slice_plain_first" (host-buffer pub33 slices grouped by key: this many
  * items first on the per-item pipeline while the slice's key tables build;
  * 0 = off, the default; env GV_SLICE_PLAIN_FIRST),

@@ -153,3 +153,18 @@ def test_host_slice_plain_first_chunk(ver):
         assert np.array_equal(bench.unpack_bits(bits, len(exp)), exp)
     finally:
         ver.set_option("slice_plain_first", 0)
+
+
+@pytest.mark.parametrize("pieces", [1, 3, 8])
+def test_pageable_chunks_staged_in_pieces(ver, pieces):
+    """gv_set_option("stage_pieces"): large pageable chunks are staged in
+    pieces, each piece's H2D behind its copy; same verdicts for grouped and
+    unique-key slices, digest bytes and bitmaps."""
+    pub, sig, dig, exp = bench.make_digest_workload(500_000, 0x73, 4096, 0.25, 16)
+    pu, su, du, eu = bench.make_digest_workload(200_000, 0x74, 200_000, 0.1, 16)
+    ver.set_option("stage_pieces", pieces)
+    try:
+        assert np.array_equal(ver.verify_batch_digests(pub, sig, dig), exp)
+        assert np.array_equal(bench.unpack_bits(ver.verify_batch_digests_bits(pu, su, du), len(eu)), eu)
+    finally:
+        ver.set_option("stage_pieces", 2)
