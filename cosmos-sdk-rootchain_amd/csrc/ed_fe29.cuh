@@ -19,6 +19,11 @@ namespace ed {
 
 #define E29_R 1216u        // 2^261 mod p
 #define E29_RH 9728u       // 2^293 mod p = 1216 * 2^32 = 9728 * 2^29: limb 1
+// E29_HICARRY: high columns of the products split as lo + 2^32 hi (1), or
+// the classic 29-bit extraction (0; A/B)
+#ifndef E29_HICARRY
+#define E29_HICARRY 1
+#endif
 
 template <bool SQR>
 GV_DEV void e29_mulsqr(fe29& r, const fe29& a, const fe29& b) {
@@ -33,6 +38,28 @@ GV_DEV void e29_mulsqr(fe29& r, const fe29& a, const fe29& b) {
 #define E29_Y(i, j) (SQR ? a.n[j] : b.n[j])
   u32 t[9];
   u64 acc = 0;
+#if E29_HICARRY
+  // high columns split as lo + 2^32 hi (secp_fe29x.cuh's GV_F29X_HICARRY):
+  // t_k keeps all 32 bits (the fold multiplies it by 1216: < 2^43) and 8 hi
+  // re-enters column k+1 by one mad instead of a mask and a 64-bit shift
+  {
+    u32 hi = 0, k8 = 8u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm("" : "+v"(k8));                       // keep "mad by 8" a mad
+#endif
+#pragma unroll
+    for (int k = 9; k <= 16; ++k) {
+      u64 col = 0;
+#pragma unroll
+      for (int i = k - 8; i <= f29_col_hi<SQR>(k); ++i) col = f29_mad(E29_X(i, k - i), E29_Y(i, k - i), col);
+      if (k > 9) col = f29_mad(hi, k8, col);  // carry of column k-1 (weight 2^32 there)
+      t[k - 9] = (u32)col;
+      hi = (u32)(col >> 32);
+    }
+    F29_TRAP(hi >= (1u << 29), "e29 mul t17");
+    t[8] = hi << 3;                           // limb 17
+  }
+#else
 #pragma unroll
   for (int k = 9; k <= 16; ++k) {             // high columns 9..16, carry chained
 #pragma unroll
@@ -42,6 +69,7 @@ GV_DEV void e29_mulsqr(fe29& r, const fe29& a, const fe29& b) {
   }
   F29_TRAP((acc >> 32) != 0, "e29 mul t17");
   t[8] = (u32)acc;                            // limb 17
+#endif
   fe29 o;
   acc = 0;
 #pragma unroll
