@@ -80,6 +80,8 @@ def lib():
         L.gvh_cache_clear.argtypes = [vp]
         L.gvh_set_threads.argtypes = [vp, ctypes.c_int]
         L.gvh_set_keyed.argtypes = [vp, ctypes.c_int, ctypes.c_size_t]
+        L.gvh_set_gpu_hash.argtypes = [vp, ctypes.c_int]
+        L.gvh_get_gpu_hash.argtypes = [vp]
         L.gvh_get_keyed.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(sz), ctypes.POINTER(sz)]
         L.gvh_cache_size.argtypes = [vp]
         L.gvh_cache_size.restype = sz
@@ -334,6 +336,14 @@ class HostApp:
         """secp256k1 leaves through the GPU context's key arena (default; keys loaded by
         batches of >= load_min leaves) or as pub33 batches."""
         self._L.gvh_set_keyed(self._app, 1 if keyed else 0, load_min)
+
+    def set_gpu_hash(self, on: bool):
+        """delivered blocks with an empty verdict cache: secp256k1 sign bytes hashed
+        in the GPU batch or on the host (default: measured faster)"""
+        self._L.gvh_set_gpu_hash(self._app, 1 if on else 0)
+
+    def gpu_hash(self) -> bool:
+        return bool(self._L.gvh_get_gpu_hash(self._app))
 
     def keyed_policy(self):
         """(keyed, load_min, key_cap) in force"""

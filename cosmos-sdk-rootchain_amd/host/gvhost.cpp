@@ -927,13 +927,22 @@ struct Leaf {
   uint8_t kind = 0;                       // 0 secp256k1, 1 ed25519
   std::array<uint8_t, 33> pub{};          // secp: 33 bytes; ed: first 32
   std::array<uint8_t, 64> sig{};
-  H32 dig{};                              // SHA256(signBytes)
+  H32 dig{};                              // SHA256(signBytes), valid when has_dig
   H32 key{};                              // verdict-cache key (computed when first needed)
   bool keyed = false;
+  bool has_dig = true;                    // false: secp leaf of a gpu_hash plan, dig computed on first need
   int verdict = -1;
-  std::shared_ptr<const std::string> msg; // ed25519: the sign bytes (SHA-512 runs over them)
+  std::shared_ptr<const std::string> msg; // the sign bytes: ed25519 (SHA-512 runs over them) and gpu_hash secp
 };
+void ensure_dig(Leaf& L) {
+  if (L.has_dig) return;
+  Sha256 h;
+  h.up(*L.msg);
+  L.dig = h.fin();
+  L.has_dig = true;
+}
 void leaf_key(Leaf& L) {
+  ensure_dig(L);
   Sha256 h;
   h.up(&L.kind, 1);
   h.up(L.pub.data(), L.kind ? 32 : 33);
@@ -1405,6 +1414,12 @@ struct gvh_app {
   uint64_t ed_key_gen = 0;
   uint64_t key_gen = 0;                        // gv_keys_generation the map belongs to
   bool keyed = true;
+  // PreVerifyTxs of a delivered block (keep == false) with an empty verdict
+  // cache: secp256k1 sign bytes hashed by the GPU batch (gv_verify_msgs*)
+  // rather than on the host (the digest would serve no cache key).  Off by
+  // default: measured slower (DESIGN.md §6.5 -- OpenSSL's SHA-256 costs less
+  // per tx than building the sign-bytes string and shipping it to the GPU)
+  bool gpu_hash = getenv("GVH_GPU_HASH") ? atoi(getenv("GVH_GPU_HASH")) != 0 : false;
   size_t key_cap = GV_KEY_CAP;                 // arena reset past this many keys (5.4 KB of HBM each)
   size_t key_load_min = GV_KEY_LOAD_MIN;       // smaller batches never load keys (k_keys_build's ~ms latency):
                                                // keyed only when all their keys are resident
@@ -1636,8 +1651,11 @@ std::string sign_bytes(const Tx& tx, const std::string& chain_json, uint64_t acc
 // Build a signer's plan: gas charge, sign bytes digest, leaves + keys.
 // ed25519 leaves keep the sign bytes themselves (the GPU's SHA-512 runs over
 // them); every leaf is then decided by the cache or a GPU batch in resolve().
+// gpu_hash: the secp256k1 leaves keep the sign bytes too and no digest (the
+// GPU batch hashes them, gv_verify_msgs*); ensure_dig() computes it if the
+// leaf meets the cache after all.
 void make_plan(SignerPlan& p, gvh_app* app, const Tx& tx, size_t signer, std::shared_ptr<const PubInfo> pub,
-               uint64_t accnum, uint64_t seq, const std::string& chain_json) {
+               uint64_t accnum, uint64_t seq, const std::string& chain_json, bool gpu_hash = false) {
   p.accnum = accnum;
   p.seq = seq;
   p.pub = std::move(pub);
@@ -1650,15 +1668,17 @@ void make_plan(SignerPlan& p, gvh_app* app, const Tx& tx, size_t signer, std::sh
   } catch (const Panic&) {
     p.gas_status = 2;
   }
-  const H32 dig = sign_digest(tx, chain_json, accnum, seq);
+  const H32 dig = gpu_hash ? H32{} : sign_digest(tx, chain_json, accnum, seq);
   p.leaves.reserve((size_t)std::max(1, p.pub->subkeys));
   p.node = build_node(p.pub->pk, dig, tx.sigs[signer].sig, p.leaves);
-  bool has_ed = false;
-  for (const Leaf& L : p.leaves) has_ed = has_ed || L.kind;
-  if (has_ed) {
+  bool need_msg = false;
+  for (const Leaf& L : p.leaves) need_msg = need_msg || L.kind || gpu_hash;
+  if (need_msg) {
     auto sb = std::make_shared<const std::string>(sign_bytes(tx, chain_json, accnum, seq));
-    for (Leaf& L : p.leaves)
-      if (L.kind) L.msg = sb;
+    for (Leaf& L : p.leaves) {
+      if (L.kind || gpu_hash) L.msg = sb;
+      if (gpu_hash) L.has_dig = false;            // either kind: the cache key hashes the digest
+    }
   }
   p.ok = true;
 }
@@ -1730,6 +1750,10 @@ struct GpuBatch {
   size_t m = 0;
   uint8_t *pub = nullptr, *sig = nullptr, *dig = nullptr, *ok = nullptr;
   uint32_t* slots = nullptr;                   // keyed: key-arena slot per leaf, UINT32_MAX = not resident
+  bool msgs = false;                           // gpu_hash: sign bytes in blob/moff/mlen instead of dig
+  uint8_t* blob = nullptr;
+  uint64_t* moff = nullptr;
+  uint32_t* mlen = nullptr;
   bool looked_up = false;                      // slots filled against arena generation `gen`
   uint64_t gen = 0;
   std::vector<uint8_t> epub, esig, eok, eblob;
@@ -1737,7 +1761,11 @@ struct GpuBatch {
   std::vector<uint32_t> elen;
 };
 
-// Layout of the pinned buffer: pub33 | sig64 | dig32 | slots (u32) | ok.
+// Layout of the pinned buffer: pub33 | sig64 | dig32 | slots (u32) | ok, or
+// when no leaf has its digest (gpu_hash plans): pub33 | sig64 | sign bytes
+// (each distinct message once: a multisig's leaves share one) | off (u64) |
+// len (u32) | slots | ok, for gv_verify_msgs*.  A batch mixing both kinds
+// hashes the missing digests here.
 // Keyed: every key is looked up in the app's slot map here, on the pool,
 // under the shared key lock (the map only gains entries while the arena
 // generation stays the same, so a slot found here is still valid when the
@@ -1753,11 +1781,40 @@ void batch_pack(gvh_app* app, GpuBatch& b) {
   }
   const size_t m = b.m = b.miss.size();
   if (m) {
-    const size_t slot_off = (m * 129 + 15) & ~size_t(15);
+    size_t undig = 0;
+    for (const Leaf* L : b.miss) undig += L->has_dig ? 0 : 1;
+    b.msgs = undig == m;
+    std::vector<uint64_t> src;                 // msgs: leaf k's message starts at moff[k]; src[k] = 1 if k copies it
+    size_t blob_n = 0;
+    if (b.msgs) {
+      src.resize(m);
+      const std::string* prev = nullptr;
+      for (size_t k = 0; k < m; ++k) {
+        const std::string* s = b.miss[k]->msg.get();
+        src[k] = s != prev;
+        if (s != prev) blob_n += s->size();
+        prev = s;
+      }
+    }
+    const size_t off_at = (m * 97 + blob_n + 7) & ~size_t(7);   // msgs: the u64 offsets
+    const size_t body = b.msgs ? off_at + m * 12 : m * 129;
+    const size_t slot_off = (body + 15) & ~size_t(15);
     b.buf = pin_get(app, slot_off + m * 4 + m + 16);
     b.pub = b.buf.p;
     b.sig = b.pub + m * 33;
-    b.dig = b.sig + m * 64;
+    if (b.msgs) {
+      b.blob = b.sig + m * 64;
+      b.moff = (uint64_t*)(b.buf.p + off_at);
+      b.mlen = (uint32_t*)(b.moff + m);
+      uint64_t at = 0;
+      for (size_t k = 0; k < m; ++k) {         // offsets in order; copies below, on the pool
+        if (src[k] && k) at += b.mlen[k - 1];
+        b.moff[k] = at;
+        b.mlen[k] = (uint32_t)b.miss[k]->msg->size();
+      }
+    } else {
+      b.dig = b.sig + m * 64;
+    }
     b.slots = (uint32_t*)(b.buf.p + slot_off);
     b.ok = b.buf.p + slot_off + m * 4;
     std::shared_lock<std::shared_mutex> rk(app->key_mu);
@@ -1766,10 +1823,15 @@ void batch_pack(gvh_app* app, GpuBatch& b) {
     b.looked_up = look;
     auto& map = app->key_slots;
     parallel_for(app, m, [&](size_t k) {
-      const Leaf& L = *b.miss[k];
+      Leaf& L = *b.miss[k];
       memcpy(&b.pub[k * 33], L.pub.data(), 33);
       memcpy(&b.sig[k * 64], L.sig.data(), 64);
-      memcpy(&b.dig[k * 32], L.dig.data(), 32);
+      if (b.msgs) {
+        if (src[k]) memcpy(b.blob + b.moff[k], L.msg->data(), L.msg->size());
+      } else {
+        ensure_dig(L);
+        memcpy(&b.dig[k * 32], L.dig.data(), 32);
+      }
       if (look) {
         std::array<uint8_t, 33> key;
         memcpy(key.data(), L.pub.data(), 33);
@@ -1805,7 +1867,11 @@ void batch_pack(gvh_app* app, GpuBatch& b) {
 // (cap reached, load error) falls back to the pub33 batch for this call.
 int verify_secp(gvh_app* app, GpuBatch& b) {
   const size_t m = b.m;
-  if (!app->keyed) return gv_verify_digests(app->gpu, m, b.pub, b.sig, b.dig, b.ok);
+  auto plain = [&] {
+    return b.msgs ? gv_verify_msgs(app->gpu, m, b.pub, b.sig, b.blob, b.moff, b.mlen, b.ok)
+                  : gv_verify_digests(app->gpu, m, b.pub, b.sig, b.dig, b.ok);
+  };
+  if (!app->keyed) return plain();
   constexpr uint32_t kPending = 0x80000000u;      // map value of a key queued for this call's load
   std::unique_lock<std::shared_mutex> wk(app->key_mu);
   auto& map = app->key_slots;
@@ -1824,7 +1890,7 @@ int verify_secp(gvh_app* app, GpuBatch& b) {
   if (m < app->key_load_min) {                    // small batch (CheckTx window, per-tx ante)
     bool all = true;
     for (size_t k = 0; k < m && all; ++k) all = b.slots[k] != UINT32_MAX;
-    if (!all) return gv_verify_digests(app->gpu, m, b.pub, b.sig, b.dig, b.ok);
+    if (!all) return plain();
   }
   std::vector<uint8_t> fresh;
   std::vector<std::array<uint8_t, 33>> fresh_keys;
@@ -1851,13 +1917,14 @@ int verify_secp(gvh_app* app, GpuBatch& b) {
       } else {
         for (auto& key : fresh_keys) map.erase(key);
       }
-      return gv_verify_digests(app->gpu, m, b.pub, b.sig, b.dig, b.ok);
+      return plain();
     }
     for (size_t i = 0; i < nf; ++i) map[fresh_keys[i]] = got[i];
     for (size_t k = 0; k < m; ++k)
       if (b.slots[k] >= kPending) b.slots[k] = got[b.slots[k] - kPending];
   }
-  return gv_verify_digests_keyed(app->gpu, m, b.slots, b.sig, b.dig, b.ok);
+  return b.msgs ? gv_verify_msgs_keyed(app->gpu, m, b.slots, b.sig, b.blob, b.moff, b.mlen, b.ok)
+                : gv_verify_digests_keyed(app->gpu, m, b.slots, b.sig, b.dig, b.ok);
 }
 
 // m ed25519 leaves (gpu_mu held): keyed against the context's ed25519 key
@@ -2318,6 +2385,7 @@ void pre_front(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t
   ps.keep = keep;
   std::unique_lock<std::mutex> lk(app->mu);
   const std::string chain_json = app->chain_json;
+  const bool gpu_hash = !keep && app->gpu_hash && app->gpu && app->cache.size() == 0;
   // (1) parallel: decode (sharing an earlier decode of the same bytes),
   // GetPubKeys' tx-supplied keys, the signers' accounts
   std::vector<std::shared_ptr<Memo>>& memos = ps.memos;
@@ -2452,7 +2520,7 @@ void pre_front(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t
     Memo& m = *memos[j.t];
     j.plan->owner = (int16_t)w;
     try {
-      make_plan(*j.plan, app, *m.tx, j.signer, j.pub, j.accnum, j.seq, chain_json);
+      make_plan(*j.plan, app, *m.tx, j.signer, j.pub, j.accnum, j.seq, chain_json, gpu_hash);
     } catch (const Panic&) {
       j.plan->ok = false;                               // malformed: the ante chain will report it
       return;
@@ -2887,6 +2955,15 @@ void gvh_set_keyed(gvh_app* app, int keyed, size_t load_min) {
   std::unique_lock<std::shared_mutex> wk(app->key_mu);
   app->keyed = keyed != 0;
   app->key_load_min = load_min;
+}
+
+void gvh_set_gpu_hash(gvh_app* app, int on) {
+  std::lock_guard<std::mutex> g(app->mu);
+  app->gpu_hash = on != 0;
+}
+int gvh_get_gpu_hash(gvh_app* app) {
+  std::lock_guard<std::mutex> g(app->mu);
+  return app->gpu_hash ? 1 : 0;
 }
 
 void gvh_get_keyed(gvh_app* app, int* keyed, size_t* load_min, size_t* key_cap) {

@@ -170,6 +170,13 @@ void gvh_set_threads(gvh_app* app, int threads);
  * verdicts either way.  While keyed, the app owns the context's key arena
  * (a gv_keys_reset elsewhere is detected by gv_keys_generation). */
 void gvh_set_keyed(gvh_app* app, int keyed, size_t load_min);
+/* gpu_hash = 1: PreVerifyTxs of a block being delivered, with an empty
+ * verdict cache, hands the secp256k1 leaves' sign bytes to the GPU
+ * (gv_verify_msgs / gv_verify_msgs_keyed, SHA-256 in the batch) instead of
+ * hashing them on the host; 0 (default; env GVH_GPU_HASH): host SHA-256 +
+ * gv_verify_digests*, measured faster.  Same verdicts either way. */
+void gvh_set_gpu_hash(gvh_app* app, int on);
+int gvh_get_gpu_hash(gvh_app* app);
 /* The keyed-path policy in force (defaults: 1, GV_KEY_LOAD_MIN, GV_KEY_CAP of gpuverify.h). */
 void gvh_get_keyed(gvh_app* app, int* keyed, size_t* load_min, size_t* key_cap);
 void gvh_get_stats(gvh_app* app, gvh_stats* out);

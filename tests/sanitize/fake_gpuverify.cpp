@@ -75,6 +75,28 @@ int gv_verify_digests_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const u
   return GV_OK;
 }
 
+// the message entry points: SHA-256 of each message here, then the digest path
+static std::vector<uint8_t> hash_msgs(size_t n, const uint8_t* blob, const uint64_t* off, const uint32_t* len) {
+  std::vector<uint8_t> d(32 * n);
+  for (size_t i = 0; i < n; ++i) {
+    unsigned int dl = 32;
+    EVP_Digest(len[i] ? blob + off[i] : (const uint8_t*)"", len[i], &d[32 * i], &dl, EVP_sha256(), nullptr);
+  }
+  return d;
+}
+int gv_verify_msgs(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64, const uint8_t* msg_blob,
+                   const uint64_t* msg_off, const uint32_t* msg_len, uint8_t* out_ok) {
+  if (!ctx || (n && (!msg_off || !msg_len))) return GV_EINVAL;
+  const std::vector<uint8_t> d = hash_msgs(n, msg_blob, msg_off, msg_len);
+  return gv_verify_digests(ctx, n, pub33, sig64, d.data(), out_ok);
+}
+int gv_verify_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64, const uint8_t* msg_blob,
+                         const uint64_t* msg_off, const uint32_t* msg_len, uint8_t* out_ok) {
+  if (!ctx || (n && (!msg_off || !msg_len))) return GV_EINVAL;
+  const std::vector<uint8_t> d = hash_msgs(n, msg_blob, msg_off, msg_len);
+  return gv_verify_digests_keyed(ctx, n, slot, sig64, d.data(), out_ok);
+}
+
 static uint8_t ed_verify(const uint8_t* pub32, const uint8_t* sig64, const uint8_t* msg, size_t len) {
   EVP_PKEY* k = EVP_PKEY_new_raw_public_key(EVP_PKEY_ED25519, nullptr, pub32, 32);
   if (!k) return 0;

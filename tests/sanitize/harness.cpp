@@ -5,7 +5,8 @@
 // test with txkit): accounts, blocks, CheckTx txs grouped per thread.
 //   1. gvh_deliver_blocks (pipelined: block b+1's pre-verification and its
 //      batch on the helper thread while block b's DeliverTx loop runs on the
-//      8-thread pool) == gvh_deliver_block_codes block by block == gvh_ante
+//      8-thread pool; gpu_hash on: message batches) == gvh_deliver_block_codes
+//      block by block (host digests) == gvh_ante
 //      tx by tx: same codes, same final accounts;
 //   2. gvh_checktx from 8 threads at once (the accumulation window, shared
 //      batches; each thread signs for its own accounts) == gvh_ante in the
@@ -118,6 +119,7 @@ int main(int argc, char** argv) {
   }
   std::vector<uint32_t> piped(ptr.size());
   gvh_app* a1 = fresh(ctx);
+  gvh_set_gpu_hash(a1, 1);
   if (gvh_deliver_blocks(a1, blocks.size(), ntx.data(), ptr.data(), len.data(), piped.data()) != GVH_OK)
     return fail("gvh_deliver_blocks");
   // 1b. block by block

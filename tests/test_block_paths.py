@@ -521,3 +521,89 @@ def test_pipelined_replay_equals_block_by_block(ver):
         app.close()
     assert stats[1]["memo_hits"] == stats[0]["memo_hits"] == sum(len(b) for b in clean)
     assert stats[1]["gpu_calls"] == stats[0]["gpu_calls"] == len(clean)
+
+
+@pytest.mark.parametrize("keyed", [True, False])
+def test_gpu_hash_and_host_digest_paths_agree(ver, keyed):
+    """A delivered block with an empty verdict cache hands the secp256k1
+    leaves' sign bytes to the GPU batch (gv_verify_msgs*, gpu_hash on -- the
+    default) instead of host SHA-256 + gv_verify_digests*: multisig blocks
+    with ed25519 sub-keys, bad leaves and wrong sequences, single-key txs, a
+    block large enough for the keyed load, and a pipelined replay give the
+    same codes, logs, gas and final state either way, and match
+    tests/ante_ref.py.  After a CheckTx-style preverify fills the cache the
+    next delivered block takes the digest path (every leaf keyed on the
+    host) with the same results."""
+    rng = random.Random(0x6A5 + keyed)
+    shapes = [(2, 3, False), (3, 5, True), (4, 7, False)]
+    accts = [MultiAcct(700 + i, *shapes[i % len(shapes)]) for i in range(9)]
+    singles = [SecpKey(b"gh-%d" % i) for i in range(48)]
+    saddr = [T.address(k.amino) for k in singles]
+    sink = T.address(SecpKey(b"gh-sink").amino)
+    seqs = {a.addr: 0 for a in accts}
+    sseq = [0] * len(singles)
+    blocks, parts_all = [], []
+    for b in range(3):
+        txs, parts = build_block(accts, seqs, rng, 120, sink)
+        for t in range(1600 if b == 1 else 200):
+            i = t % len(singles)
+            msgs = [T.MsgSend(saddr[i], sink, [(1 + t % 4, "h")])]
+            sb = T.std_sign_bytes(CHAIN, 500 + i, sseq[i], FEE, msgs, "m%d" % (t % 3))
+            bad = rng.random() < 0.02
+            sig = singles[(i + 1) % len(singles)].sign(sb) if bad else singles[i].sign(sb)
+            pub = singles[i].amino if b == 0 and t < len(singles) else b""
+            txs.append(T.std_tx(msgs, FEE, "m%d" % (t % 3), [(pub, sig)]))
+            sseq[i] += 0 if bad else 1
+        blocks.append(txs)
+        parts_all.append(parts)
+
+    def fresh(gpu_hash):
+        app = gvhost.HostApp(ver, chain_id=CHAIN, height=10)
+        app.set_keyed(keyed, load_min=1024)
+        app.set_gpu_hash(gpu_hash)
+        assert app.gpu_hash() == gpu_hash
+        for a in accts:
+            app.set_account(a.addr, a.number, 0)
+        for i, a in enumerate(saddr):
+            app.set_account(a, 500 + i, 0)
+        return app
+
+    def state(app):
+        return [app.get_account(a.addr) for a in accts] + [app.get_account(a) for a in saddr]
+
+    strip = lambda r: (r["code"], r["log"], r["gas_used"], r["gas_wanted"])
+    runs = {}
+    for gh in (True, False):
+        app = fresh(gh)
+        res = []
+        for txs in blocks:
+            rc, r = app.deliver_block(txs)
+            assert rc == 0
+            res.append([strip(x) for x in r])
+        runs[gh] = (res, state(app), app.stats())
+        app.close()
+    assert runs[True][0] == runs[False][0]
+    assert runs[True][1] == runs[False][1]
+    assert runs[True][2]["gpu_leaves"] == runs[False][2]["gpu_leaves"] > 2000
+    ref = new_ref(accts, 10)
+    mseq = {a.addr: 0 for a in accts}
+    for b in range(3):                               # the multisig txs (first 120 of each block) vs the reference
+        n = len(parts_all[b])
+        res = [dict(zip(("code", "log", "gas_used"), x[:3])) for x in runs[True][0][b][:n]]
+        check_block(res, blocks[b][:n], parts_all[b], ref, mseq)
+    flat = [x[0] for blk in runs[True][0] for x in blk]
+    assert flat.count(0) > 0.8 * len(flat) and flat.count(4) > 20
+    # pipelined replay (block b+1's batch while b delivers) with gpu_hash
+    app = fresh(True)
+    rc, piped = app.deliver_blocks(blocks)
+    assert rc == 0
+    assert [[int(c) for c in blk] for blk in piped] == [[x[0] for x in blk] for blk in runs[True][0]]
+    assert state(app) == runs[True][1]
+    app.close()
+    # a filled cache: the delivered block's leaves are keyed on the host (digest path)
+    app = fresh(True)
+    rc, n = app.preverify(blocks[0])
+    assert rc == 0 and app.cache_size() > 0
+    rc, r = app.deliver_block(blocks[0])
+    assert rc == 0 and [strip(x) for x in r] == runs[True][0][0]
+    app.close()
