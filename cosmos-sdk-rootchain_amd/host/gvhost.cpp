@@ -1456,6 +1456,12 @@ struct gvh_app {
   }
   std::atomic<uint64_t> st_gpu_calls{0}, st_gpu_leaves{0}, st_hits{0}, st_misses{0}, st_memo{0}, st_windows{0},
       st_window_txs{0}, st_pre_ns{0}, st_gpu_ns{0}, st_loop_ns{0};
+  // the last delivered block's memos, released (back to the worker pools)
+  // while the next block's GPU batch runs instead of on the block's own
+  // critical path (deliver_block); declared last: dropped first
+  std::mutex deferred_mu;
+  std::vector<std::shared_ptr<Memo>> deferred;
+  bool defer_release = getenv("GVH_DEFER_RELEASE") ? atoi(getenv("GVH_DEFER_RELEASE")) != 0 : true;
 };
 
 namespace {
@@ -2335,21 +2341,26 @@ int ante_bytes(gvh_app* app, const uint8_t* p, size_t n, bool simulate, gvh_resu
 // to the freeing thread's own malloc arena: frees spread over the pool at
 // random contend on the other arenas' locks (measured: 3.3 ms vs ~0.3 ms for a
 // 10k-tx multisig block on 16 threads).
-void release_memos(gvh_app* app, std::vector<std::shared_ptr<Memo>>& memos) {
-  // every unshared memo goes back to the pool of the worker that took it
-  // (shared ones -- the memo table's -- are just dropped here)
-  // (owners are read before any worker starts moving elements out: a worker
-  // must not read an element another worker is resetting)
+// Owners are read before any worker starts moving elements out (a worker must
+// not read an element another worker is resetting); part p of np releases the
+// memos whose owner is p modulo np.
+std::vector<int16_t> memo_owners(const std::vector<std::shared_ptr<Memo>>& memos) {
   std::vector<int16_t> own(memos.size());
   for (size_t i = 0; i < memos.size(); ++i) own[i] = memos[i] ? memos[i]->owner : (int16_t)-1;
-  parallel_workers(app, [&](int w, int nw) {
-    for (size_t i = 0; i < memos.size(); ++i) {
-      if (own[i] < 0 || own[i] % nw != w) continue;
-      std::shared_ptr<Memo>& m = memos[i];
-      if (m.use_count() == 1) memo_put(app, own[i], std::move(m));
-      else m.reset();
-    }
-  });
+  return own;
+}
+void release_part(gvh_app* app, std::vector<std::shared_ptr<Memo>>& memos, const std::vector<int16_t>& own, int p,
+                  int np) {
+  for (size_t i = 0; i < memos.size(); ++i) {
+    if (own[i] < 0 || own[i] % np != p) continue;
+    std::shared_ptr<Memo>& m = memos[i];
+    if (m.use_count() == 1) memo_put(app, own[i], std::move(m));   // unshared: back to its worker's pool
+    else m.reset();                                                // the memo table's: just dropped
+  }
+}
+void release_memos(gvh_app* app, std::vector<std::shared_ptr<Memo>>& memos) {
+  const std::vector<int16_t> own = memo_owners(memos);
+  parallel_workers(app, [&](int w, int nw) { release_part(app, memos, own, w, nw); });
   memos.clear();
 }
 
@@ -2719,11 +2730,40 @@ int deliver_memos(gvh_app* app, std::vector<std::shared_ptr<Memo>>& memos, gvh_r
   return err.load();
 }
 
+// One block: PreVerifyTxs, then the DeliverTx loop.  The previous block's
+// memos (defer_release) go back to the worker pools while this block's GPU
+// batch runs (the pool is otherwise idle then), and this block's wait for the
+// next call.
 int deliver_block(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, gvh_result* out,
                   uint32_t* codes) {
-  std::vector<std::shared_ptr<Memo>> memos;
+  std::vector<std::shared_ptr<Memo>> memos, stale;
+  {
+    std::lock_guard<std::mutex> g(app->deferred_mu);
+    stale.swap(app->deferred);
+  }
   const auto t0 = std::chrono::steady_clock::now();
-  int rc = preverify(app, ntx, txs, lens, nullptr, &memos, false);
+  int rc;
+  {
+    PreState ps;
+    pre_front(app, ntx, txs, lens, false, 0, ps);
+    if (ps.has_batch && !app->gpu) {
+      rc = GVH_ENOVERIFIER;
+    } else if (ps.has_batch && !stale.empty() && app->threads > 1) {
+      // the caller (worker 0) runs the batch, workers 1.. release the memos
+      const std::vector<int16_t> own = memo_owners(stale);
+      int rg = GVH_OK;
+      parallel_workers(app, [&](int w, int nw) {
+        if (w == 0) rg = pre_gpu(app, ps);
+        else release_part(app, stale, own, w - 1, nw - 1);
+      });
+      stale.clear();
+      rc = rg;
+    } else {
+      rc = pre_gpu(app, ps);
+    }
+    release_memos(app, stale);
+    pre_back(app, ps, rc, nullptr, &memos);
+  }
   const auto t1 = std::chrono::steady_clock::now();
   app->st_pre_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
   if (rc != GVH_OK) {
@@ -2733,7 +2773,11 @@ int deliver_block(gvh_app* app, size_t ntx, const uint8_t* const* txs, const siz
   rc = deliver_memos(app, memos, out, codes);
   const auto t2 = std::chrono::steady_clock::now();
   app->st_loop_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
-  release_memos(app, memos);
+  if (app->defer_release) {
+    std::lock_guard<std::mutex> g(app->deferred_mu);
+    if (app->deferred.empty()) app->deferred.swap(memos);
+  }
+  release_memos(app, memos);                        // not deferred (option off, or another call's memos wait)
   if (getenv("GVH_PROFILE"))
     fprintf(stderr, "deliver preverify %.3f ms loop %.3f ms release %.3f ms\n",
             std::chrono::duration<double, std::milli>(t1 - t0).count(),
