@@ -65,6 +65,7 @@ typedef struct gvk_batch {
   // (the previous call's) and records bits_done, so results land in call order.
   hipEvent_t bits_wait, bits_done;
   int unpacked;                 // the SoA rows are already written (in-batch key grouping ran k_unpack)
+  uint32_t inv_m;               // k_scalar_inv signatures per lane (0: gvk_inv_m(C))
   hipEvent_t keys_ready;        // optional: the batch's key tables are built on another stream; k_prep waits
   // keyed batch (kslot != NULL, pub33 unused): item i's key is arena slot kslot[i]
   const uint32_t* kslot;        // n slots (device)
@@ -86,6 +87,16 @@ typedef struct gvk_batch {
   // lanes run in slot order, the bits are gathered back to item order
   gvk_sort srt;
 } gvk_batch;
+// k_scalar_inv's fold for a batch of C lanes: GV_INV_M from 2^19 lanes up
+// (the throughput pipeline: fewest instructions, the kernel runs beside a
+// ladder); below, C / 65,536 (at least 4) so it still launches ~1,024 waves
+// -- there it is latency-bound on the path to the first ladder (a host
+// slice's first chunk), and its duration follows the per-lane chain length.
+inline uint32_t gvk_inv_m(uint32_t C) {
+  if (C >= (1u << 19)) return GV_INV_M;
+  const uint32_t m = C / 65536u;
+  return m < 4u ? 4u : m > (uint32_t)GV_INV_M ? (uint32_t)GV_INV_M : m;
+}
 // scan scratch bytes for nbuckets = kcount + 1 buckets
 size_t gvk_sort_temp_bytes(uint32_t nbuckets);
 // counting sort of n items by slot (clamped to kcount): pos / perm / kslot of so

@@ -527,13 +527,15 @@ GV_DEV void sc29_batch_inv_wave(sc29& inv, const sc29& x) {
   sc29_mul(inv, m, tinv);
 }
 
-__global__ __launch_bounds__(256) GV_SINV_ATTR void k_scalar_inv(u32 C, const u32* in_s, u32* w, u32* pre) {
+// M: signatures per lane (GV_INV_M for large batches; fewer for a batch whose
+// s^-1 is on a latency path, gvk_inv_m).
+__global__ __launch_bounds__(256) GV_SINV_ATTR void k_scalar_inv(u32 C, const u32* in_s, u32* w, u32* pre, u32 M) {
   const u32 lane = threadIdx.x & 63u;
   const u32 wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   sc29 acc;
   sc29_mont_one(acc);
-  for (int j = 0; j < GV_INV_M; ++j) {
-    const u32 e = (wave * GV_INV_M + j) * 64u + lane;
+  for (u32 j = 0; j < M; ++j) {
+    const u32 e = (wave * M + j) * 64u + lane;
     if (e >= C) break;                       // wave-uniform (C % 64 == 0)
     u32 s[8];
     load_sc(s, in_s, C, e);
@@ -551,8 +553,8 @@ __global__ __launch_bounds__(256) GV_SINV_ATTR void k_scalar_inv(u32 C, const u3
   }
   sc29 inv_lane;
   sc29_batch_inv_wave(inv_lane, acc);        // (lane total)^-1, one Fermat chain per wave
-  for (int j = GV_INV_M - 1; j >= 0; --j) {
-    const u32 e = (wave * GV_INV_M + j) * 64u + lane;
+  for (int j = (int)M - 1; j >= 0; --j) {
+    const u32 e = (wave * M + (u32)j) * 64u + lane;
     if (e >= C) continue;
     sc29 p, sm, inv;
     load_sc29(p, pre, C, e);
@@ -1573,12 +1575,13 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
                        b->in_e, perm);
   if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
   {
-    const uint32_t waves = (C / 64 + GV_INV_M - 1) / GV_INV_M;
+    const uint32_t M = b->inv_m ? b->inv_m : gvk_inv_m(C);
+    const uint32_t waves = (C / 64 + M - 1) / M;
     // scratch for w and the prefix products: the digit rows.  k_prep reads
     // its lane's w before writing that lane's digits (same lane, same rows).
     uint32_t* w = b->digits;                   // rows 0..8
     uint32_t* pre = b->digits + (size_t)9 * C; // rows 9..17
-    hipLaunchKernelGGL(gv::k_scalar_inv, dim3((waves + 3) / 4), blk, 0, st, C, b->in_s, w, pre);
+    hipLaunchKernelGGL(gv::k_scalar_inv, dim3((waves + 3) / 4), blk, 0, st, C, b->in_s, w, pre, M);
     if (b->keys_ready) (void)hipStreamWaitEvent(st, b->keys_ready, 0);   // grouped keys built beside s^-1
     if (b->ev[1]) (void)hipEventRecord(b->ev[1], st);
     if (k6)

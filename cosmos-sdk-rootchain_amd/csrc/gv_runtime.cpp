@@ -455,6 +455,8 @@ struct gv_ctx {
   int stage_pieces = 2;         // host path, pageable chunks of >= 65,536 items: staged in this many pieces, each
                                 // piece's H2D behind its copy (1 = one copy then one H2D; GV_STAGE_PIECES):
                                 // 121.4 / 129.4 / 126.2 / 126.8M/s at 1 / 2 / 4 / 8 (profiles/r04/hostpath/stage_pieces_ab.jsonl)
+  bool inv_small = true;        // k_scalar_inv folds fewer signatures per lane below 2^19 items (gvk_inv_m);
+                                // 0: GV_INV_M always (GV_INV_SMALL)
   size_t slice_plain_first = 0; // host path, slices to be grouped: this many items first on the per-item pipeline,
                                 // submitted before the rest's keys are sent, grouped and tabulated (0 = off;
                                 // GV_SLICE_PLAIN_FIRST)
@@ -709,6 +711,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
   b.in_x = s->in_x; b.in_pfx = s->in_pfx; b.in_r = s->in_r; b.in_s = s->in_s; b.in_e = s->in_e;
   b.digits = s->digits; b.zq = s->zq; b.flags = s->flags; b.qtab = s->qtab;
   b.bits = bits_out;
+  b.inv_m = ctx->inv_small ? 0u : (uint32_t)GV_INV_M;
   const uint32_t* kzq2 = d->kzq2;
   if (kslot && ka) {                            // a host slice's grouped keys
     b.pub33 = nullptr;
@@ -1390,6 +1393,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* gk = getenv("GV_GROUP_KEYS")) ctx->group_keys = strcmp(gk, "0") != 0;
   if (const char* sp = getenv("GV_STAGE_PIECES")) ctx->stage_pieces = std::max(1, atoi(sp));
   if (const char* pf = getenv("GV_SLICE_PLAIN_FIRST")) ctx->slice_plain_first = strtoull(pf, nullptr, 10);
+  if (const char* is = getenv("GV_INV_SMALL")) ctx->inv_small = strcmp(is, "0") != 0;
   ctx->stage_threads = gvstage::stage_pool_threads(host_cpus(), (int)ids.size());
   for (size_t k = 0; k < ids.size(); ++k) {
     Dev* d = new Dev();
@@ -2029,6 +2033,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "stage_pieces")) {
     if (val < 1 || val > 64) return GV_EINVAL;
     ctx->stage_pieces = (int)val;
+  } else if (!strcmp(key, "inv_small")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->inv_small = val != 0;
   } else if (!strcmp(key, "slice_plain_first")) {
     if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
     ctx->slice_plain_first = (size_t)val;

@@ -234,6 +234,9 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * "stage_pieces" (pageable host chunks of at least 65,536 items are staged
  * into pinned memory in this many pieces, each piece's H2D right behind its
  * copy; default 2, env GV_STAGE_PIECES),
+ * "inv_small" (0/1: batches under 2^19 items fold fewer signatures per lane
+ * in the s^-1 batch inversion, so it stays short where it precedes the first
+ * ladder -- a host slice's first chunk; default 1, env GV_INV_SMALL),
  * "slice_plain_first" (host-buffer pub33 slices grouped by key: this many
  * items first on the per-item pipeline while the slice's key tables build;
  * 0 = off, the default; env GV_SLICE_PLAIN_FIRST),
