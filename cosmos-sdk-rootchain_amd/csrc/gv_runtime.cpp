@@ -77,6 +77,7 @@ struct Set {
   hipEvent_t last = nullptr;                      // end of the last work using this set
   hipStream_t last_st = nullptr;
   hipEvent_t done = nullptr;                      // host path: chunk finished (bits on host)
+  hipEvent_t h2d = nullptr;                       // host path: the chunk's H2D copies enqueued so far done
   hipEvent_t ecm_ready = nullptr;                 // pipelined device calls: front kernels done
   hipStream_t side = nullptr;                     // grouped keys: table builds beside k_scalar_inv
   hipEvent_t fork = nullptr, keys_done = nullptr;
@@ -121,6 +122,7 @@ struct Dev {
   Set set[2];
   Set gset;                                       // host slices: whole-slice key grouping (slice_group)
   hipEvent_t grp_ready = nullptr;
+  hipEvent_t last_h2d = nullptr;                  // host slice: the previous chunk's H2D (h2d_serial)
   // key arena (gv_keys_load): Q table rows, table Z (8 rows of stride kcap), verdicts
   uint32_t *kqt = nullptr, *kzq = nullptr, *kok = nullptr;
   uint32_t *kqt2 = nullptr, *kzq2 = nullptr;      // the keyed latency schedule's group tables (2^35 Q, ...)
@@ -455,6 +457,9 @@ struct gv_ctx {
   int stage_pieces = 2;         // host path, pageable chunks of >= 65,536 items: staged in this many pieces, each
                                 // piece's H2D behind its copy (1 = one copy then one H2D; GV_STAGE_PIECES):
                                 // 121.4 / 129.4 / 126.2 / 126.8M/s at 1 / 2 / 4 / 8 (profiles/r04/hostpath/stage_pieces_ab.jsonl)
+  bool h2d_serial = true;       // host slices: a chunk's H2D waits for the previous chunk's, so concurrent
+                                // transfers do not share the link and delay the chunk the GPU needs first
+                                // (GV_H2D_SERIAL)
   bool inv_small = true;        // k_scalar_inv folds fewer signatures per lane below 2^19 items (gvk_inv_m);
                                 // 0: GV_INV_M always (GV_INV_SMALL)
   size_t slice_plain_first = 0; // host path, slices to be grouped: this many items first on the per-item pipeline,
@@ -944,6 +949,16 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
   if ((rc = ensure_pinned((uint8_t**)&s->h_bits, &s->h_bits_cap, (C / 64) * 8))) return rc;
   uint8_t* h = s->h_in;
   uint64_t bmin = 0;
+  // h2d_serial: this chunk's copies start after the previous chunk's
+  auto h2d_begin = [&]() -> int {
+    if (ctx->h2d_serial && d->last_h2d) CK(hipStreamWaitEvent(s->st, d->last_h2d, 0));
+    return GV_OK;
+  };
+  auto h2d_end = [&]() -> int {
+    CK(hipEventRecord(s->h2d, s->st));
+    d->last_h2d = s->h2d;
+    return GV_OK;
+  };
   if (hb.pinned && !msgs) {                 // the caller's pinned buffers: read in place, no staging
     const uint8_t* kp = keyed ? (const uint8_t*)(hb.slots + c0) : hb.pub33 + c0 * 33;
     const uint8_t* sp = hb.sig64 + c0 * 64;
@@ -962,10 +977,11 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
       s->cn = cn;
       return GV_OK;
     }
-    if ((rc = set_acquire(s, s->st))) return rc;
+    if ((rc = set_acquire(s, s->st)) || (rc = h2d_begin())) return rc;
     if (!dslots) CK(hipMemcpyAsync(s->d_in, kp, cn * (keyed ? 4 : 33), hipMemcpyHostToDevice, s->st));
     CK(hipMemcpyAsync(s->d_in + L.sig, sp, cn * 64, hipMemcpyHostToDevice, s->st));
     CK(hipMemcpyAsync(s->d_in + L.third, dp, cn * 32, hipMemcpyHostToDevice, s->st));
+    if ((rc = h2d_end())) return rc;
     const uint8_t* din = s->d_in;
     rc = launch(ctx, d, s, cn, keyed ? nullptr : din, din + L.sig, din + L.third, nullptr, nullptr, nullptr, s->bits,
                 s->st, dslots ? dsl : keyed ? (const uint32_t*)din : nullptr, nullptr, nullptr, hb.ka, hb.plain);
@@ -986,7 +1002,7 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
   if (!msgs && !zc_path && ctx->stage_pieces > 1 && cn >= 65536) {
     // large pageable chunk: staged in pieces, each piece's H2D right behind
     // its copy, so the transfer of piece i overlaps the staging of piece i+1
-    if ((rc = set_acquire(s, s->st))) return rc;
+    if ((rc = set_acquire(s, s->st)) || (rc = h2d_begin())) return rc;
     const size_t per = round_up((cn + ctx->stage_pieces - 1) / ctx->stage_pieces, 256);
     const size_t kb = keyed ? 4 : 33;
     for (size_t a = 0; a < cn; a += per) {
@@ -1000,6 +1016,7 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
       CK(hipMemcpyAsync(s->d_in + L.sig + a * 64, h + L.sig + a * 64, m * 64, hipMemcpyHostToDevice, s->st));
       CK(hipMemcpyAsync(s->d_in + L.third + a * 32, h + L.third + a * 32, m * 32, hipMemcpyHostToDevice, s->st));
     }
+    if ((rc = h2d_end())) return rc;
     sent = true;
   } else if (!msgs) {                       // keys/slots, signatures, digests: one pool pass
     const CopySeg segs[3] = {CopySeg{h + L.sig, hb.sig64 + c0 * 64, cn * 64},
@@ -1047,12 +1064,15 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
     return GV_OK;
   }
   if (!sent) {
-    if ((rc = set_acquire(s, s->st))) return rc;
+    if ((rc = set_acquire(s, s->st)) || (rc = h2d_begin())) return rc;
     const size_t from = dslots ? L.sig : 0;   // device slots: no key region to send
     CK(hipMemcpyAsync(s->d_in + from, h + from, (msgs ? L.total : L.third + cn * 32) - from, hipMemcpyHostToDevice,
                       s->st));
+    if (msgs && hb_bytes) CK(hipMemcpyAsync(s->d_blob, s->h_blob, hb_bytes, hipMemcpyHostToDevice, s->st));
+    if ((rc = h2d_end())) return rc;
+  } else if (msgs && hb_bytes) {
+    CK(hipMemcpyAsync(s->d_blob, s->h_blob, hb_bytes, hipMemcpyHostToDevice, s->st));
   }
-  if (msgs && hb_bytes) CK(hipMemcpyAsync(s->d_blob, s->h_blob, hb_bytes, hipMemcpyHostToDevice, s->st));
   const uint8_t* din = s->d_in;
   rc = launch(ctx, d, s, cn, keyed ? nullptr : din, din + L.sig, msgs ? nullptr : din + L.third,
               msgs ? s->d_blob : nullptr, msgs ? (const uint64_t*)(din + L.third) : nullptr,
@@ -1160,6 +1180,7 @@ int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const HostBatch& hb) {
       d->last_slice_n = n;
     }
   } timer{d, n, t_begin};
+  d->last_h2d = nullptr;                          // no earlier chunk of this slice
   // Chunk sizes.  Pipelined (past lat_max): a ramp -- pipe_chunk first, each
   // later chunk at most pipe_growth times the one before -- so the first
   // kernels start after a short staging copy and every later chunk is staged
@@ -1394,6 +1415,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* sp = getenv("GV_STAGE_PIECES")) ctx->stage_pieces = std::max(1, atoi(sp));
   if (const char* pf = getenv("GV_SLICE_PLAIN_FIRST")) ctx->slice_plain_first = strtoull(pf, nullptr, 10);
   if (const char* is = getenv("GV_INV_SMALL")) ctx->inv_small = strcmp(is, "0") != 0;
+  if (const char* hs = getenv("GV_H2D_SERIAL")) ctx->h2d_serial = strcmp(hs, "0") != 0;
   ctx->stage_threads = gvstage::stage_pool_threads(host_cpus(), (int)ids.size());
   for (size_t k = 0; k < ids.size(); ++k) {
     Dev* d = new Dev();
@@ -1420,6 +1442,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
       ok = ok && hipStreamCreateWithFlags(&sp->st, hipStreamNonBlocking) == hipSuccess &&
            hipEventCreateWithFlags(&sp->last, hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&sp->done, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&sp->h2d, hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&sp->ecm_ready, hipEventDisableTiming) == hipSuccess &&
            hipStreamCreateWithPriority(&sp->side, hipStreamNonBlocking, front_prio) == hipSuccess &&
            hipEventCreateWithFlags(&sp->fork, hipEventDisableTiming) == hipSuccess &&
@@ -2033,6 +2056,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "stage_pieces")) {
     if (val < 1 || val > 64) return GV_EINVAL;
     ctx->stage_pieces = (int)val;
+  } else if (!strcmp(key, "h2d_serial")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->h2d_serial = val != 0;
   } else if (!strcmp(key, "inv_small")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->inv_small = val != 0;

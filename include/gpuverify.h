@@ -234,6 +234,10 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * "stage_pieces" (pageable host chunks of at least 65,536 items are staged
  * into pinned memory in this many pieces, each piece's H2D right behind its
  * copy; default 2, env GV_STAGE_PIECES),
+ * "h2d_serial" (0/1: a host slice's chunks send their inputs one after the
+ * other -- each chunk's H2D waits for the previous chunk's -- so the chunk
+ * the GPU needs first is not slowed by the next one's transfer; default 1,
+ * env GV_H2D_SERIAL),
  * "inv_small" (0/1: batches under 2^19 items fold fewer signatures per lane
  * in the s^-1 batch inversion, so it stays short where it precedes the first
  * ladder -- a host slice's first chunk; default 1, env GV_INV_SMALL),
