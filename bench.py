@@ -50,12 +50,15 @@ FM, FS, NM = 72, 44, 136
 DBL, MADD, LIFT, BETA, FINISH = 3 * FM + 4 * FS, 8 * FM + 3 * FS, FM, FM, 2 * FM + FS
 
 
-def w_ladder(ndbl: int, nq: int, ng: int, qw: int) -> float:
+def w_ladder(ndbl: int, nq: int, ng: int, qw: int, nbeta: float | None = None) -> float:
     """Expected products of one ladder: ndbl doublings, nq Q-type additions (half
-    of them lambda-Q, each with a beta multiply; a qw-bit Booth digit is zero
-    with probability 2 / 2^(qw+1)), ng lifted G additions, the final check."""
+    of them lambda-Q; a qw-bit Booth digit is zero with probability 2 /
+    2^(qw+1)), ng lifted G additions, the final check.  Beta products: one per
+    lambda-Q addition, or nbeta (the k4 ladders' lambda frame, GV_LAMFRAME:
+    two per ladder position)."""
     q = nq * (1 - 2.0 / 2 ** (qw + 1))
-    return ndbl * DBL + (q - 1) * MADD + (q / 2) * BETA + ng * (MADD + LIFT) + FINISH
+    nb = q / 2 if nbeta is None else nbeta
+    return ndbl * DBL + (q - 1) * MADD + nb * BETA + ng * (MADD + LIFT) + FINISH
 
 
 W_DECOMP = 255 * FS + 15 * FM              # ParsePubKey: x^3 + 7, the (p+1)/4 chain, y^2 check   12,300
@@ -93,9 +96,10 @@ W_KEYBUILD_K4 = w_keybuild(16, 100)        # 4 groups of 16 entries, offsets 0/3
 W_KEYBUILD_K6 = w_keybuild(32, 102)        # 4 groups of 32 entries, offsets 0/36/72/102
 W_PREP_KEYED = W_SCALAR
 W_PREP_KEYED_F = 2 * NM + (2 * 64 + 68)   # k4f: u2's GLV split only (u1 is recoded unsplit)
-W_LADDER_K4 = w_ladder(30, 52, 14, 5)      # k_ecmult_k4: 30 doublings, 52 Q (26 lambda), 14 G additions
+# k_ecmult_k4: 30 doublings, 52 Q (26 lambda, on the lambda frame: 2 beta products at each of 7 positions), 14 G additions
+W_LADDER_K4 = w_ladder(30, 52, 14, 5, nbeta=14)
 W_LADDER_K6 = w_ladder(30, 44, 12, 6)      # k_ecmult_k6: 30 doublings, 44 Q (22 lambda), 12 G additions
-W_LADDER_K4F = w_ladder(30, 52, 11, 5)     # k_ecmult_k4<true>: G on the unsplit u1, 11 25-bit windows
+W_LADDER_K4F = w_ladder(30, 52, 11, 5, nbeta=14)   # k_ecmult_k4<true>: G on the unsplit u1, 11 25-bit windows
 # Peak: the highest v_mad_u64_u32 issue rate measured on MI355X
 # (tools/microbench/alu_rate.hip; profiles/r01/alu_rate_v3.jsonl, dependent
 # chains at 8 waves/SIMD), lane-products per second, whole chip.  bench.py

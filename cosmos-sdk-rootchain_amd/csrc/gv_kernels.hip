@@ -42,6 +42,9 @@ __constant__ const u32 kGy[8] = {0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B4
                                  0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
 __constant__ const u32 kBeta[8] = {0x719501EEu, 0xC1396C28u, 0x12F58995u, 0x9CF04975u,
                                    0xAC3434E9u, 0x6E64479Eu, 0x657C0710u, 0x7AE96A2Bu};
+// beta^2 mod p (the other cube root of unity: lambda^2 (x, y) = (beta^2 x, y))
+__constant__ const u32 kBeta2[8] = {0x8E6AFA40u, 0x3EC693D6u, 0xED0A766Au, 0x630FB68Au,
+                                    0x53CBCB16u, 0x919BB861u, 0x9A83F8EFu, 0x851695D4u};
 __constant__ const u32 kP[8] = {0xFFFFFC2Fu, 0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu,
                                 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
 
@@ -1278,6 +1281,16 @@ __constant__ const int kGFWin[7][4] = {{0, 4, -1, -1}, {2, 6, 8, -1}, {-1, -1, -
                                        {-1, -1, -1, -1}, {1, 5, -1, -1}, {3, 7, 9, 10}};
 __constant__ const int kGFTab[GV_GF_WIN] = {0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5};
 
+// GV_LAMFRAME (default 1): at each position the four groups' Q entries are
+// added first, then the accumulator moves to lambda^2 (x -> beta^2 x), takes
+// the lambda-Q entries' plain (x, y) -- lambda^2 A + T = lambda^2 (A + lambda T),
+// lambda^3 = 1 -- and moves back (x -> beta x) before the G entries: two
+// beta products per position instead of one per lambda-Q entry.  The same
+// sum (lambda is a group automorphism, so the exceptional cases -- H == 0 --
+// meet the same points); 0: beta x per lambda-Q entry.
+#ifndef GV_LAMFRAME
+#define GV_LAMFRAME 1
+#endif
 // GF: gtab is the full-scalar G tables (gtabf), gtab4 unused.
 template <bool GF>
 __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gtab, const u32* gtab4, u32 n, u32 C,
@@ -1297,18 +1310,26 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gta
 #pragma unroll 1
       for (int d = 0; d < GV_QW; ++d) gej29x_double(acc, acc);
     }
-    // slots 0..7: (group, Q / lambda Q); 8..11: up to two G windows x (G, lambda G)
+    // slots 0..7: (group, Q / lambda Q) -- LAMFRAME: Q of groups 0..3, then
+    // lambda Q of groups 0..3 on lambda^2 (acc); 8..11: up to two G windows x
+    // (G, lambda G) or (GF) up to four G windows
 #pragma unroll 1
     for (int slot = 0; slot < 12; ++slot) {
+      if (GV_LAMFRAME && (slot == 4 || slot == 8) && !inf) {
+        fe29 c;                                            // into lambda^2 (acc) / back to acc
+        f29_from_const(c, slot == 4 ? kBeta2 : kBeta);
+        f29x_mul(acc.x, acc.x, c);
+      }
       int d;
       const u32* tab;
       u32 row = 0;
       const bool isg = slot >= 8;
+      const bool lam = GV_LAMFRAME ? slot >= 4 : (slot & 1) != 0;
       if (!isg) {
-        const int grp = slot >> 1;
+        const int grp = GV_LAMFRAME ? (slot & 3) : (slot >> 1);
         if (pos >= kK4NWin[grp]) continue;                 // wave-uniform
         const u32 dq = digits[(size_t)(kK4WStart[grp] + pos) * C + g];
-        d = (slot & 1) ? ((int)dq >> 16) : ((int)(dq << 16) >> 16);
+        d = lam ? ((int)dq >> 16) : ((int)(dq << 16) >> 16);
         tab = grp == 0 ? kqt : kqt2;
         row = grp == 0 ? qi : qi * GV_KEY2_TABLES + (grp - 1);
       } else if (GF) {
@@ -1329,7 +1350,7 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gta
       fe29 x, y;
       if (!isg) {
         load_qent29(x, y, tab, row, e);
-        if (slot & 1) {                                    // lambda * P = (beta * x, y)
+        if (lam && !GV_LAMFRAME) {                         // lambda * P = (beta * x, y)
           fe29 beta;
           f29_from_const(beta, kBeta);
           f29x_mul(x, x, beta);

@@ -24,9 +24,12 @@ SRC = os.path.join(ROOT, "tools", "isa_ops.hip")
 
 # operations per verify of k_ecmult_k4<true> (schedule: positions 6..0, 5
 # doublings between positions; Q windows per group 7, 7, 6, 6 -> 26 per GLV
-# half, each with a Q and a lambda-Q digit; G: 11 25-bit windows of the
-# unsplit u1)
-LADDER_OPS = {"isa_dbl": 30, "isa_addq": 26, "isa_addlq": 26, "isa_addg": 11, "isa_finish": 1}
+# half, each with a Q and a lambda-Q digit -- the lambda-Q entries added as
+# plain Q additions on lambda^2 (acc), entered and left by a beta product at
+# each of the 7 positions (GV_LAMFRAME); G: 11 25-bit windows of the unsplit u1)
+LADDER_OPS = {"isa_dbl": 30, "isa_addq": 52, "isa_mul": 14, "isa_addg": 11, "isa_finish": 1}
+# without the lambda frame (GV_LAMFRAME=0): a beta product inside each lambda-Q addition
+LADDER_OPS_NOFRAME = {"isa_dbl": 30, "isa_addq": 26, "isa_addlq": 26, "isa_addg": 11, "isa_finish": 1}
 # the GLV G schedule (gv_set_option "gfull" 0): 7 20-bit windows per GLV half
 LADDER_OPS_GLV = dict(LADDER_OPS, isa_addg=14)
 
