@@ -1756,6 +1756,8 @@ struct GpuBatch {
   size_t m = 0;
   uint8_t *pub = nullptr, *sig = nullptr, *dig = nullptr, *ok = nullptr;
   uint32_t* slots = nullptr;                   // keyed: key-arena slot per leaf, UINT32_MAX = not resident
+  bool split = false;                          // miss holds the secp256k1 leaves only, ed the ed25519 ones
+  bool all_dig = false;                        // (split) every secp256k1 leaf has its digest
   bool msgs = false;                           // gpu_hash: sign bytes in blob/moff/mlen instead of dig
   uint8_t* blob = nullptr;
   uint64_t* moff = nullptr;
@@ -1777,18 +1779,23 @@ struct GpuBatch {
 // generation stays the same, so a slot found here is still valid when the
 // batch runs unless the generation moved -- batch_run checks).
 void batch_pack(gvh_app* app, GpuBatch& b) {
-  {
+  size_t undig = 0;
+  if (!b.split) {                              // mixed misses (resolve): one pass splits them
     size_t k = 0;
     for (Leaf* L : b.miss) {
-      if (L->kind) b.ed.push_back(L);
-      else b.miss[k++] = L;
+      if (L->kind) {
+        b.ed.push_back(L);
+      } else {
+        undig += L->has_dig ? 0 : 1;
+        b.miss[k++] = L;
+      }
     }
     b.miss.resize(k);
+  } else if (!b.all_dig) {
+    undig = b.miss.size();                     // gpu_hash plans: no secp256k1 leaf has a digest
   }
   const size_t m = b.m = b.miss.size();
   if (m) {
-    size_t undig = 0;
-    for (const Leaf* L : b.miss) undig += L->has_dig ? 0 : 1;
     b.msgs = undig == m;
     std::vector<uint64_t> src;                 // msgs: leaf k's message starts at moff[k]; src[k] = 1 if k copies it
     size_t blob_n = 0;
@@ -2524,7 +2531,8 @@ void pre_front(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t
   lap("jobs");
   // (3) parallel: gas charge, sign bytes, leaves, cache keys + lookups; the
   // misses collect per worker
-  std::vector<std::vector<Leaf*>> wmiss(std::max(1, app->threads));
+  // (secp256k1 and ed25519 misses apart, so batch_pack need not walk the leaves)
+  std::vector<std::vector<Leaf*>> wmiss(std::max(1, app->threads)), wed(std::max(1, app->threads));
   std::atomic<size_t> n_leaf{0};
   parallel_for_w(app, jobs.size(), [&](size_t k, int w) {
     Job& j = jobs[k];
@@ -2538,7 +2546,7 @@ void pre_front(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t
     }
     for (Leaf& L : j.plan->leaves) {
       if (L.verdict < 0) L.verdict = cache_lookup(app, L);
-      if (L.verdict < 0) wmiss[w].push_back(&L);
+      if (L.verdict < 0) (L.kind ? wed[w] : wmiss[w]).push_back(&L);
     }
     n_leaf.fetch_add(j.plan->leaves.size(), std::memory_order_relaxed);
   });
@@ -2553,11 +2561,14 @@ void pre_front(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t
     for (auto& v : wmiss) nm += v.size();
     miss.reserve(nm);
     for (auto& v : wmiss) miss.insert(miss.end(), v.begin(), v.end());
+    for (auto& v : wed) ps.batch.ed.insert(ps.batch.ed.end(), v.begin(), v.end());
+    ps.batch.split = true;
+    ps.batch.all_dig = !gpu_hash;                    // fresh plans: digests exactly when not gpu_hash
   }
-  app->st_hits += ps.n_all - miss.size();
-  app->st_misses += miss.size();
+  app->st_hits += ps.n_all - miss.size() - ps.batch.ed.size();
+  app->st_misses += miss.size() + ps.batch.ed.size();
   // (4) the misses packed for one GPU batch (pinned buffer, key slots looked up)
-  if (!miss.empty()) {
+  if (!miss.empty() || !ps.batch.ed.empty()) {
     ps.has_batch = true;
     if (app->gpu) batch_pack(app, ps.batch);
   }
