@@ -1291,6 +1291,9 @@ __constant__ const int kGFTab[GV_GF_WIN] = {0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5};
 #ifndef GV_LAMFRAME
 #define GV_LAMFRAME 1
 #endif
+#ifndef GV_LAMREV
+#define GV_LAMREV 1
+#endif
 // GF: gtab is the full-scalar G tables (gtabf), gtab4 unused.
 template <bool GF>
 __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gtab, const u32* gtab4, u32 n, u32 C,
@@ -1326,7 +1329,8 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gta
       const bool isg = slot >= 8;
       const bool lam = GV_LAMFRAME ? slot >= 4 : (slot & 1) != 0;
       if (!isg) {
-        const int grp = GV_LAMFRAME ? (slot & 3) : (slot >> 1);
+        // (lambda entries in reverse group order: group 3's row was read last)
+        const int grp = GV_LAMFRAME ? (lam && GV_LAMREV ? 3 - (slot & 3) : (slot & 3)) : (slot >> 1);
         if (pos >= kK4NWin[grp]) continue;                 // wave-uniform
         const u32 dq = digits[(size_t)(kK4WStart[grp] + pos) * C + g];
         d = lam ? ((int)dq >> 16) : ((int)(dq << 16) >> 16);

@@ -14,4 +14,4 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /root/repo/$O/prof -o run -- \
   python3 /root/repo/bench.py --steps 10 --warmup 3 --no-extras --no-cpu-baseline --no-latency \
   > /root/repo/$O/bench_prof.json 2> /root/repo/$O/bench_prof.err || { tail -20 /root/repo/$O/bench_prof.err; exit 1; }
-python3 /root/repo/tools/prof_timed.py /root/repo/$O/prof/run_kernel_trace.csv 10 /root/repo/$O/kernel_timed.csv | head -12
+python3 /root/repo/tools/prof_timed.py /root/repo/$O/prof/run_kernel_trace.csv 10 /root/repo/$O/kernel_timed.csv > /root/repo/$O/timed.txt; head -12 /root/repo/$O/timed.txt
