@@ -1201,7 +1201,17 @@ struct wave_stamp {
 #endif
 // KEYED: the Q table and its Z come from key-arena row qidx[g] (zq rows of
 // stride zC) instead of the lane's own row g (stride C).
-template <bool KEYED>
+// GF: G on the unsplit u1 from the full-scalar tables (gtab = gtabf; k_prep
+// GF digits): window j (bit 25 j) is added at window position win from the
+// table of offset kGFOff[kPGTab[j]] = 25 j - 5 win -- 11 G additions instead
+// of the GLV schedule's 14 (the 26-window ladder spans bits 0..125, so the
+// windows past it come from the 2^45, 2^100 and 2^145 tables).
+__constant__ const int kPGWin[GV_QWIN][2] = {
+    {0, -1}, {-1, -1}, {-1, -1}, {-1, -1}, {-1, -1}, {1, -1}, {-1, -1}, {-1, -1}, {-1, -1}, {-1, -1},
+    {2, -1}, {-1, -1}, {-1, -1}, {-1, -1}, {-1, -1}, {3, 7},   {9, -1},  {-1, -1}, {-1, -1}, {-1, -1},
+    {4, 8},  {6, 10},  {-1, -1}, {-1, -1}, {-1, -1}, {5, -1}};
+__constant__ const int kPGTab[GV_GF_WIN] = {0, 0, 0, 0, 0, 0, 1, 2, 2, 3, 3};
+template <bool KEYED, bool GF = false>
 __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult(const u32* gtab, u32 n, u32 C, const u32* digits,
                                                  const u32* qt, const u32* zq_in, const u32* flags,
                                                  const u32* in_r, uint64_t* bits, const u32* qidx, u32 zC) {
@@ -1228,10 +1238,17 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult(const u32* gtab, 
       for (int d = 0; d < GV_QW; ++d) gej29_double(acc, acc);
 #endif
     }
-    const bool gwin = (win % GV_GSTEP) == 0;
+    const bool gwin = GF ? kPGWin[win][0] >= 0 : (win % GV_GSTEP) == 0;   // wave-uniform
     const u32 dq = digits[(size_t)win * C + g];
-    const u32* grow = digits + (size_t)(GV_QWIN + 2 * (win / GV_GSTEP)) * C + g;
-    const u32 dg0 = gwin ? grow[0] : 0u, dg1 = gwin ? grow[C] : 0u;
+    u32 dg0 = 0u, dg1 = 0u;
+    if (GF) {
+      if (kPGWin[win][0] >= 0) dg0 = digits[(size_t)(GV_QWIN + kPGWin[win][0]) * C + g];
+      if (kPGWin[win][1] >= 0) dg1 = digits[(size_t)(GV_QWIN + kPGWin[win][1]) * C + g];
+    } else if (gwin) {
+      const u32* grow = digits + (size_t)(GV_QWIN + 2 * (win / GV_GSTEP)) * C + g;
+      dg0 = grow[0];
+      dg1 = grow[C];
+    }
     const int nslots = gwin ? 4 : 2;
 #pragma unroll 1
     for (int slot = 0; slot < nslots; ++slot) {
@@ -1247,6 +1264,8 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult(const u32* gtab, 
           f29_from_const(beta, kBeta);
           f29_mul(x, x, beta);
         }
+      } else if (GF) {                             // a missing second window has d == 0 (skipped above)
+        load_gent29(x, y, gtab + (size_t)kPGTab[kPGWin[win][slot - 2]] * GV_GF_TAB_N * 16, e);
       } else {
         load_gent29(x, y, gtab + (slot == 3 ? (size_t)GV_GTAB_N * 16 : 0), e);
       }
@@ -1584,6 +1603,7 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   // key-ordered lanes (gv_sort.hip): keyed k4 batches with sort scratch
   const bool k6 = b->kslot && b->k6 && b->gtab6;
   const bool gf = b->kslot && b->gtab4 && b->gtabf && !k6;   // k_ecmult_k4<true>
+  const bool gfp = !b->kslot && b->gtabf;                     // per-item pub33: k_ecmult<false, true>
   const bool sorted = b->kslot && (b->gtab4 || k6) && b->srt.perm;
   const uint32_t* perm = sorted ? b->srt.perm : nullptr;
   if (sorted) {
@@ -1624,6 +1644,10 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
                          (const uint32_t*)nullptr, b->in_r, b->in_s, b->in_e, (const uint32_t*)w, b->digits,
                          (uint32_t*)nullptr, (uint32_t*)nullptr, b->flags, sorted ? b->srt.kslot : b->kslot,
                          b->kok, b->kcount, b->in_pfx);
+    else if (gfp)
+      hipLaunchKernelGGL((gv::k_prep<false, false, true>), grd, blk, 0, st, C, b->n, b->in_x, b->in_pfx, b->in_r,
+                         b->in_s, b->in_e, (const uint32_t*)w, b->digits, b->qtab, b->zq, b->flags,
+                         (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr);
     else
       hipLaunchKernelGGL(gv::k_prep<false>, grd, blk, 0, st, C, b->n, b->in_x, b->in_pfx, b->in_r, b->in_s,
                          b->in_e, (const uint32_t*)w, b->digits, b->qtab, b->zq, b->flags,
@@ -1652,6 +1676,10 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   else if (b->kslot)
     hipLaunchKernelGGL(gv::k_ecmult<true>, grd, blk, 0, se, b->gtab, b->n, C, b->digits, b->kqt, b->kzq,
                        b->flags, b->in_r, b->bits, (const uint32_t*)b->in_pfx, b->kC);
+  else if (gfp)
+    hipLaunchKernelGGL((gv::k_ecmult<false, true>), grd, blk, 0, se, b->gtabf, b->n, C, b->digits,
+                       (const uint32_t*)b->qtab, (const uint32_t*)b->zq, b->flags, b->in_r, b->bits,
+                       (const uint32_t*)nullptr, 0u);
   else
     hipLaunchKernelGGL(gv::k_ecmult<false>, grd, blk, 0, se, b->gtab, b->n, C, b->digits,
                        (const uint32_t*)b->qtab, (const uint32_t*)b->zq, b->flags, b->in_r, b->bits,

@@ -460,6 +460,8 @@ struct gv_ctx {
   bool h2d_serial = true;       // host slices: a chunk's H2D waits for the previous chunk's, so concurrent
                                 // transfers do not share the link and delay the chunk the GPU needs first
                                 // (GV_H2D_SERIAL)
+  bool gfull_item = true;       // the per-item (pub33, ungrouped) route takes G on the unsplit u1 too: 11 G
+                                // additions from the full-scalar tables instead of 14 (GV_GFULL_ITEM)
   bool inv_small = true;        // k_scalar_inv folds fewer signatures per lane below 2^19 items (gvk_inv_m);
                                 // 0: GV_INV_M always (GV_INV_SMALL)
   size_t slice_plain_first = 0; // host path, slices to be grouped: this many items first on the per-item pipeline,
@@ -794,11 +796,16 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
       rc = group_keys(ctx, d, s, b, n, st, &sort_base);
       if (rc) return rc;
     }
+    if (!b.kslot) {                               // the per-item route: G on the unsplit u1 (gfull_item)
+      if (ctx->gfull && ctx->gfull_item && (rc = ensure_gtabf(ctx, d, s, st))) return rc;
+      b.gtabf = ctx->gfull && ctx->gfull_item ? d->gtabf : nullptr;
+    }
     plan_sort(ctx, s, b, sort_base);
     d->routes[b.k6 && b.gtab6                  ? GV_ROUTE_K6
               : b.kslot && b.gtab4 && b.gtabf ? GV_ROUTE_K4F
               : b.kslot && b.gtab4            ? GV_ROUTE_K4
               : b.kslot                       ? GV_ROUTE_KEYED125
+              : b.gtabf                       ? GV_ROUTE_ITEMF
                                               : GV_ROUTE_PUB33]++;
     CK(gvk_verify(&b, st));
   }
@@ -1415,6 +1422,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* sp = getenv("GV_STAGE_PIECES")) ctx->stage_pieces = std::max(1, atoi(sp));
   if (const char* pf = getenv("GV_SLICE_PLAIN_FIRST")) ctx->slice_plain_first = strtoull(pf, nullptr, 10);
   if (const char* is = getenv("GV_INV_SMALL")) ctx->inv_small = strcmp(is, "0") != 0;
+  if (const char* gi = getenv("GV_GFULL_ITEM")) ctx->gfull_item = strcmp(gi, "0") != 0;
   if (const char* hs = getenv("GV_H2D_SERIAL")) ctx->h2d_serial = strcmp(hs, "0") != 0;
   ctx->stage_threads = gvstage::stage_pool_threads(host_cpus(), (int)ids.size());
   for (size_t k = 0; k < ids.size(); ++k) {
@@ -2059,6 +2067,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "h2d_serial")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->h2d_serial = val != 0;
+  } else if (!strcmp(key, "gfull_item")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->gfull_item = val != 0;
   } else if (!strcmp(key, "inv_small")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->inv_small = val != 0;

@@ -238,6 +238,9 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * other -- each chunk's H2D waits for the previous chunk's -- so the chunk
  * the GPU needs first is not slowed by the next one's transfer; default 1,
  * env GV_H2D_SERIAL),
+ * "gfull_item" (0/1: the per-item pub33 route -- batches not grouped by
+ * key -- also adds G on the unsplit u1 from the "gfull" tables: 11 G
+ * additions instead of 14; default 1, env GV_GFULL_ITEM),
  * "inv_small" (0/1: batches under 2^19 items fold fewer signatures per lane
  * in the s^-1 batch inversion, so it stays short where it precedes the first
  * ladder -- a host slice's first chunk; default 1, env GV_INV_SMALL),
@@ -318,8 +321,9 @@ int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys)
  * key arena), GV_ROUTE_K6 (in-batch key grouping on the 6-bit-window ladder),
  * GV_ROUTE_LAT (small pub33 batches: gv_lat.hip kernels), GV_ROUTE_LAT_KEYED
  * (small keyed batches), GV_ROUTE_K4F (the 4-group ladder with the G half on
- * the unsplit scalar, 25-bit windows).  Instrumentation only (bench route attribution, node
- * metrics). */
+ * the unsplit scalar, 25-bit windows), GV_ROUTE_ITEMF (the per-item pipeline
+ * with the G half on the unsplit scalar, "gfull_item").  Instrumentation only
+ * (bench route attribution, node metrics). */
 #define GV_ROUTE_PUB33 0
 #define GV_ROUTE_KEYED125 1
 #define GV_ROUTE_K4 2
@@ -327,7 +331,8 @@ int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys)
 #define GV_ROUTE_LAT 4
 #define GV_ROUTE_LAT_KEYED 5
 #define GV_ROUTE_K4F 6
-#define GV_ROUTES 7
+#define GV_ROUTE_ITEMF 7
+#define GV_ROUTES 8
 int gv_route_stats(gv_ctx* ctx, int dev_slot, uint64_t out[GV_ROUTES]);
 
 const char* gv_strerror(int code);

@@ -5,7 +5,11 @@ half (gfull 0: 14 20-bit windows) and k_ecmult_k6 (k6 1: 6-bit Q, 24-bit G
 windows, 32-entry key tables).  Each is run on the grouped route (pub33 batches
 with repeated keys), the cached-key route (gv_keys_load slots) and the message
 path, against the oracle's expected verdicts, and the route counters must show
-the schedule that ran."""
+the schedule that ran.  The per-item route (group_keys 0: each item parses its
+key, 26 five-bit windows over 125 doublings) runs both its G schedules too:
+"gfull_item" 1 (the default: u1's 11 25-bit windows from the same 2^o G
+tables, windows past bit 125 from the 2^45 / 2^100 / 2^145 ones) and 0 (14
+GLV windows)."""
 import numpy as np
 import pytest
 
@@ -16,15 +20,18 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-SCHEDULES = {"k4f": {"gfull": 1, "k6": 0}, "k4": {"gfull": 0, "k6": 0}, "k6": {"gfull": 1, "k6": 1}}
+SCHEDULES = {"k4f": {"gfull": 1, "k6": 0}, "k4": {"gfull": 0, "k6": 0}, "k6": {"gfull": 1, "k6": 1},
+             "item_gf": {"group_keys": 0, "gfull_item": 1}, "item_glv": {"group_keys": 0, "gfull_item": 0}}
+ROUTE = {"k4f": "k4f", "k4": "k4", "k6": "k6", "item_gf": "item_f", "item_glv": "pub33"}
+DEFAULTS = {"gfull": 1, "k6": 0, "group_keys": 1, "gfull_item": 1}
 
 
 @pytest.fixture(scope="module")
 def ver():
     v = gvm.Verifier([0])
     yield v
-    v.set_option("gfull", 1)
-    v.set_option("k6", 0)
+    for k, val in DEFAULTS.items():
+        v.set_option(k, val)
     v.close()
 
 
@@ -35,10 +42,11 @@ def run(ver, sched, fn):
     try:
         out = fn()
     finally:
-        ver.set_option("gfull", 1)
-        ver.set_option("k6", 0)
+        for k, val in DEFAULTS.items():
+            ver.set_option(k, val)
     r1 = ver.route_stats()
-    return out, {k: r1[k] - r0[k] for k in r1}
+    d = {k: r1[k] - r0[k] for k in r1}
+    return out, dict(d, **{sched: d[ROUTE[sched]]})
 
 
 @pytest.mark.parametrize("sched", list(SCHEDULES))
