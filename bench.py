@@ -66,6 +66,7 @@ W_DECOMP = 255 * FS + 15 * FM              # ParsePubKey: x^3 + 7, the (p+1)/4 c
 # 5M + 2S, back-propagation 15 x (3M + 1S) + 13 ratio products, Z 1M
 W_QTAB = (1 + 14 * 5 + 15 * 3 + 13 + 1) * FM + (5 + 14 * 2 + 15) * FS
 W_LADDER = w_ladder(125, 52, 14, 5)        # per-item k_ecmult: 125 doublings, 5-bit Q, 20-bit G windows
+W_LADDER_F = w_ladder(125, 52, 11, 5)      # per-item k_ecmult<false, true> ("gfull_item"): G on the unsplit u1
 # k_scalar_inv: per item to_mont + the running product (forward), 2 products
 # (backward); per lane (32 items) the wave scans (12 + 2 products) and the
 # shared inversion (sc29_inv: ~256 squarings + ~84 products), which every
@@ -484,6 +485,7 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
     routes1 = ver.route_stats() if hasattr(ver, "route_stats") else {}
     k6 = grouped and routes1.get("k6", 0) - routes0.get("k6", 0) >= calib
     k4f = grouped and routes1.get("k4f", 0) - routes0.get("k4f", 0) >= calib
+    itemf = not grouped and routes1.get("item_f", 0) - routes0.get("item_f", 0) >= calib
     if grouped:
         # the key tables (k_keys_chain, k_keys_tables) run on a side stream
         # beside k_scalar_inv: that stage's time covers both
@@ -495,8 +497,11 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
         ladder, w_route = lad, sum(w.values())
     else:
         w = dict(W_KERNEL)
+        if itemf:                                  # one GLV split fewer in k_prep, 11 G additions
+            w["k_prep"] = W_DECOMP + W_QTAB + 2 * NM + (2 * 64 + 68)
+            w["k_ecmult"] = W_LADDER_F
         kms = {"k_scalar_inv": inv_ms, "k_prep": prep_ms, "k_ecmult": ecmult_ms}
-        ladder, w_route = "k_ecmult", W_MUL
+        ladder, w_route = "k_ecmult", sum(w.values())
     kernels = {}
     for k, ms in kms.items():
         a = n * w[k] / (ms * 1e-3) if ms > 0 else 0.0
