@@ -584,12 +584,12 @@ GV_DEV bool parse_pubkey(u32 pre, const fe& x, fe& y) {
   {
     fe29 x29, c, y29, y2, seven;
     f29_from_words(x29, x.v);
-    f29_sqr(c, x29);
-    f29_mul(c, c, x29);
+    f29x_sqr(c, x29);
+    f29x_mul(c, c, x29);
     f29_set_u32(seven, 7);
     f29_add(c, c, seven);                   // c = x^3 + 7 (magnitude 2)
-    f29_sqrt_candidate(y29, c);             // y = c^((p+1)/4)
-    f29_sqr(y2, y29);
+    f29x_sqrt_candidate(y29, c);            // y = c^((p+1)/4)
+    f29x_sqr(y2, y29);
     ok &= f29_equal(y2, c);                 // "invalid square root"
     f29_to_words(y.v, y29);                 // canonical
   }
@@ -855,21 +855,21 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_tables(u32 n, u32 C4
     // co-Z doubling of (qx, qy): Z1 = 2y, 2Q = (M^2 - 2S, M(S - X) - 8y^4),
     // Q' = (S, 8y^4) with S = 4xy^2, M = 3x^2.
     fe29 B, E, Lq, M;
-    f29_sqr(B, qx);
-    f29_sqr(E, qy);
-    f29_sqr(Lq, E);
+    f29x_sqr(B, qx);
+    f29x_sqr(E, qy);
+    f29x_sqr(Lq, E);
     f29_add(t, qx, E);
-    f29_sqr(t, t);
+    f29x_sqr(t, t);
     f29_sub<1>(t, t, B);
     f29_sub_norm<1>(t, t, Lq);
     f29_shl_norm<1>(X1, t);
     f29_mul3_norm(M, B);
-    f29_sqr(t, M);
+    f29x_sqr(t, M);
     f29_add(u, X1, X1);
     f29_sub_norm<2>(X2, t, u);
     f29_shl_norm<3>(Y1, Lq);
     f29_sub<1>(t, X1, X2);
-    f29_mul(t, M, t);
+    f29x_mul(t, M, t);
     f29_sub_norm<1>(Y2, t, Y1);
   }
   put(0, X1, Y1);                           // 1*Q on Z1
@@ -880,18 +880,18 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_tables(u32 n, u32 C4
     fe29 h, rr, c, w1, w2, d, a1;
     f29_sub_norm<1>(h, X1, X2);
     store_ratio29(qr, C4, L, m - 2, h);     // Z_m / Z_{m-1}
-    f29_mul(prod, prod, h);
+    f29x_mul(prod, prod, h);
     f29_sub_norm<1>(rr, Y1, Y2);
-    f29_sqr(c, h);
-    f29_mul(w1, X1, c);
-    f29_mul(w2, X2, c);
-    f29_sqr(d, rr);
+    f29x_sqr(c, h);
+    f29x_mul(w1, X1, c);
+    f29x_mul(w2, X2, c);
+    f29x_sqr(d, rr);
     f29_sub<1>(t, w1, w2);
-    f29_mul(a1, Y1, t);
+    f29x_mul(a1, Y1, t);
     f29_add(u, w1, w2);
     f29_sub_norm<2>(X2, d, u);
     f29_sub<1>(t, w1, X2);
-    f29_mul(t, rr, t);
+    f29x_mul(t, rr, t);
     f29_sub_norm<1>(Y2, t, a1);
     X1 = w1;
     Y1 = a1;
@@ -901,7 +901,7 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_tables(u32 n, u32 C4
   if (grp) {
     fe29 z;
     load_f29(z, zrow, kC, base + key);
-    f29_mul(prod, prod, z);
+    f29x_mul(prod, prod, z);
   }
   fe29 e1, e2, e3;
 #pragma unroll
@@ -911,15 +911,15 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_tables(u32 n, u32 C4
     e3.n[i] = (u32)__shfl_xor((int)prod.n[i], 3);
   }
   fe29 acc, zc;
-  f29_mul(acc, e1, e2);
-  f29_mul(acc, acc, e3);                    // rho
-  f29_mul(zc, acc, prod);                   // the common Z
+  f29x_mul(acc, e1, e2);
+  f29x_mul(acc, acc, e3);                    // rho
+  f29x_mul(zc, acc, prod);                   // the common Z
   {
     fe29 a2, a3;                            // entry 16 (on Z_15): times rho^2, rho^3
-    f29_sqr(a2, acc);
-    f29_mul(a3, a2, acc);
-    f29_mul(X2, X2, a2);
-    f29_mul(Y2, Y2, a3);
+    f29x_sqr(a2, acc);
+    f29x_mul(a3, a2, acc);
+    f29x_mul(X2, X2, a2);
+    f29x_mul(Y2, Y2, a3);
     store_qent29<NT>(tab, row, NT - 1, X2, Y2);
   }
   // entry m (index m-1) on Z_{m-1} (m >= 2; entries 1, 2 on Z_1): times
@@ -929,14 +929,14 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_tables(u32 n, u32 C4
     if (m >= 2) {
       fe29 ratio;
       load_ratio29(ratio, qr, C4, L, m - 2);
-      f29_mul(acc, acc, ratio);
+      f29x_mul(acc, acc, ratio);
     }
     fe29 x, y, a2, a3;
-    f29_sqr(a2, acc);
-    f29_mul(a3, a2, acc);
+    f29x_sqr(a2, acc);
+    f29x_mul(a3, a2, acc);
     get(m - 1, x, y);
-    f29_mul(x, x, a2);
-    f29_mul(y, y, a3);
+    f29x_mul(x, x, a2);
+    f29x_mul(y, y, a3);
     store_qent29<NT>(tab, row, m - 1, x, y);
   }
   store_f29(zrow, kC, base + key, zc);

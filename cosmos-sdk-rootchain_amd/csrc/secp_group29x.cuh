@@ -77,4 +77,31 @@ GV_DEV void gej29x_add_scaled(gej29& a, bool& inf, const fe29& x, const fe29& y,
   if (dbl) gej29x_double(a, a);                // a == b: 2a (a untouched above)
 }
 
+// ---------------------------------------------------- exponentiation chains
+// The (p+1)/4 square-root chain of secp_group29.cuh (f29_pow_prefix /
+// f29_sqrt_candidate: the same addition chain, the same result) on the fused
+// products.  a magnitude <= 2.
+GV_DEV void f29x_sqr_n(fe29& r, const fe29& a, int k) {
+  r = a;
+#pragma unroll 1
+  for (int i = 0; i < k; ++i) f29x_sqr(r, r);
+}
+GV_DEV void f29x_sqrt_candidate(fe29& r, const fe29& a) {
+  fe29 x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223, t;
+  f29x_sqr(x2, a); f29x_mul(x2, x2, a);            // 2^2-1
+  f29x_sqr(x3, x2); f29x_mul(x3, x3, a);           // 2^3-1
+  f29x_sqr_n(t, x3, 3); f29x_mul(x6, t, x3);       // 2^6-1
+  f29x_sqr_n(t, x6, 3); f29x_mul(x9, t, x3);       // 2^9-1
+  f29x_sqr_n(t, x9, 2); f29x_mul(x11, t, x2);      // 2^11-1
+  f29x_sqr_n(t, x11, 11); f29x_mul(x22, t, x11);   // 2^22-1
+  f29x_sqr_n(t, x22, 22); f29x_mul(x44, t, x22);   // 2^44-1
+  f29x_sqr_n(t, x44, 44); f29x_mul(x88, t, x44);   // 2^88-1
+  f29x_sqr_n(t, x88, 88); f29x_mul(x176, t, x88);  // 2^176-1
+  f29x_sqr_n(t, x176, 44); f29x_mul(x220, t, x44); // 2^220-1
+  f29x_sqr_n(t, x220, 3); f29x_mul(x223, t, x3);   // 2^223-1
+  f29x_sqr_n(t, x223, 23); f29x_mul(t, t, x22);
+  f29x_sqr_n(t, t, 6); f29x_mul(t, t, x2);
+  f29x_sqr_n(r, t, 2);
+}
+
 }  // namespace gv
