@@ -68,10 +68,15 @@ W_QTAB = (1 + 14 * 5 + 15 * 3 + 13 + 1) * FM + (5 + 14 * 2 + 15) * FS
 W_LADDER = w_ladder(125, 52, 14, 5)        # per-item k_ecmult: 125 doublings, 5-bit Q, 20-bit G windows
 W_LADDER_F = w_ladder(125, 52, 11, 5)      # per-item k_ecmult<false, true> ("gfull_item"): G on the unsplit u1
 # k_scalar_inv: per item to_mont + the running product (forward), 2 products
-# (backward); per lane (32 items) the wave scans (12 + 2 products) and the
-# shared inversion (sc29_inv: ~256 squarings + ~84 products), which every
-# lane executes
-W_INV = (4 + (14 + 340) / 32) * NM
+# (backward); per lane (GV_INV_M = 32 items) the wave scans (12 + 2
+# products), the Montgomery <-> plain conversions of the wave total (3) and
+# the shared inversion by variable-time divsteps (secp_modinv.cuh
+# s30_modinv_var: ~13 rounds of 30 divsteps for a random 256-bit input, each
+# round's matrix applied to (f, g) and (d, e): 4 x 9 + 4 x 9 + 2 x 9
+# products), which every lane executes.  (Rounds 1-4 charged the Fermat
+# chain's ~340 products here; the kernel has run divsteps since round 3.)
+W_DIVSTEPS = 13 * (36 + 36 + 18)
+W_INV = 4 * NM + ((14 + 3) * NM + W_DIVSTEPS) / 32
 # k_prep's scalar work: u1 = e w, u2 = r w (2 Montgomery products) and two
 # GLV splits (2 x 256x256 rounding products + 68 for c1 B1, c2 A1, c1 A1, c2 A2)
 W_SCALAR = 2 * NM + 2 * (2 * 64 + 68)
@@ -99,7 +104,9 @@ W_PREP_KEYED = W_SCALAR
 W_PREP_KEYED_F = 2 * NM + (2 * 64 + 68)   # k4f: u2's GLV split only (u1 is recoded unsplit)
 # k_ecmult_k4: 30 doublings, 52 Q (26 lambda, on the lambda frame: 2 beta products at each of 7 positions), 14 G additions
 W_LADDER_K4 = w_ladder(30, 52, 14, 5, nbeta=14)
-W_LADDER_K6 = w_ladder(30, 44, 12, 6)      # k_ecmult_k6: 30 doublings, 44 Q (22 lambda), 12 G additions
+# k_ecmult_k6: 30 doublings, 44 Q (22 lambda, on the lambda frame: 2 beta products at each of 6 positions),
+# 11 G additions (G on the unsplit u1, 24-bit windows)
+W_LADDER_K6 = w_ladder(30, 44, 11, 6, nbeta=12)
 W_LADDER_K4F = w_ladder(30, 52, 11, 5, nbeta=14)   # k_ecmult_k4<true>: G on the unsplit u1, 11 25-bit windows
 # Peak: the highest v_mad_u64_u32 issue rate measured on MI355X
 # (tools/microbench/alu_rate.hip; profiles/r01/alu_rate_v3.jsonl, dependent
@@ -211,6 +218,9 @@ def cpu_baseline(pub, sig, dig, threads: int, ver=None):
         c1["gpu_hostpath"] = round(n1 / (time.perf_counter() - t), 1)
         c1["gpu_mismatches"] = int(np.count_nonzero(got != cexp))
     return {"value": c2["port_allcore"], "unit": "verifies/s", "cores": threads, "kind": "port",
+            "label": "no-GLV C restatement, not btcec (the reference's btcec uses GLV and would likely be faster; "
+                     "the Go toolchain is absent, so the reference itself cannot be timed): a reported baseline, "
+                     "never a target",
             "host": host_cores(),
             "sample": f"first {s2} items of the same C2 batch, {threads} threads = every CPU this process may run on "
                       f"(affinity mask, capped by the cgroup quota; see host) (oracle/secp256k1_oracle.c: a clarity-first 4x64-limb port of the reference "
@@ -492,7 +502,7 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
         lad = "k_ecmult_k6" if k6 else "k_ecmult_k4"
         wkb = W_KEYBUILD_K6 if k6 else W_KEYBUILD_K4
         w = {"k_unpack+k_dedupe": 0.0, "k_scalar_inv|k_keys_chain+k_keys_tables": W_INV + wkb * u_keys / n,
-             "k_prep<keyed>": W_PREP_KEYED_F if k4f else W_PREP_KEYED, lad: W_LADDER_K6 if k6 else W_LADDER_K4F if k4f else W_LADDER_K4}
+             "k_prep<keyed>": W_PREP_KEYED_F if (k4f or k6) else W_PREP_KEYED, lad: W_LADDER_K6 if k6 else W_LADDER_K4F if k4f else W_LADDER_K4}
         kms = dict(zip(w, (unpack_ms, inv_ms, prep_ms, ecmult_ms)))
         ladder, w_route = lad, sum(w.values())
     else:
@@ -529,7 +539,8 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
                    "global_batch": n * world, "parallelism": f"shard{world} (independent per-GPU shards, no collective)",
                    "route": ("in-batch key grouping: each distinct key parsed and tabulated once (k_dedupe, "
                              "k_keys_chain + k_keys_tables), items on the keyed 30-doubling ladder "
-                             + ("k_ecmult_k6 (6-bit Q / 24-bit G windows)" if k6
+                             + ("k_ecmult_k6 (6-bit Q windows on 32-entry key tables, G on the unsplit "
+                                "scalar: 11 24-bit windows)" if k6
                                 else "k_ecmult_k4 (G on the unsplit scalar: 11 25-bit windows)" if k4f
                                 else "k_ecmult_k4 (GLV G: 14 20-bit windows)")
                              if grouped else "per-item pub33 pipeline (every item decompresses its key)"),
@@ -594,6 +605,7 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
         import bench_extras as X
         ex = {}
         t = time.perf_counter()
+        ex["first_call"] = X.first_call(pub, sig, dig, exp)
         ex["c2_hostpath"] = X.c2_hostpath(ver, pub, sig, dig, exp, device_value=value)
         ex["c2_key_cache"] = X.c2_key_cache(ver, pub, sig, dig, exp, min(args.keys, n))
         ex["c2_unique_keys"] = X.c2_unique_keys(ver, make_digest_workload, n, args.threads)
@@ -605,6 +617,7 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
         ex["ed25519"] = X.ed25519(ver, workload_lib(), n=n, threads=args.threads, peak=P_MUL)
         log(f"extras in {time.perf_counter() - t:.1f}s")
         result["extras"] = ex
+        result["summary"] = summarize(result, ex)
     if lat is not None:
         # BASELINE's second number, last in the line so that a truncated tail
         # of stdout still shows it: the full curve, then p50 @ 64
@@ -615,6 +628,45 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def summarize(result, ex):
+    """One compact block of the side lines, placed right before the C5 curve
+    at the end of the JSON line so that a truncated tail of stdout still
+    carries them: the node paths (host buffers, C1, C4), the other C2 routes
+    and their rooflines from serialized passes, ed25519."""
+    def g(d, *path):
+        for k in path:
+            if not isinstance(d, dict) or k not in d:
+                return None
+            d = d[k]
+        return d
+    v = result["value"]
+    return {
+        "c2_device_resident": v,
+        "c2_hostpath": {"pageable": g(ex, "c2_hostpath", "value"), "pinned": g(ex, "c2_hostpath", "value_pinned"),
+                        "frac_pageable": g(ex, "c2_hostpath", "frac_of_device_resident"),
+                        "frac_pinned": g(ex, "c2_hostpath", "frac_of_device_resident_pinned")},
+        "c2_key_cache": {"value": g(ex, "c2_key_cache", "value"), "route": g(ex, "c2_key_cache", "route"),
+                         "frac": g(ex, "c2_key_cache", "roofline", "frac"),
+                         "ladder_ms": g(ex, "c2_key_cache", "roofline", "kernel_ms")},
+        "c2_unique_keys": {"value": g(ex, "c2_unique_keys", "value"),
+                           "ladder_frac": g(ex, "c2_unique_keys", "roofline", "k_ecmult", "frac"),
+                           "front_frac": g(ex, "c2_unique_keys", "roofline", "k_scalar_inv+k_prep", "frac")},
+        "c2_per_item_parse": g(ex, "c2_per_item_parse", "value"),
+        "c3_adversarial": g(ex, "c3_adversarial", "value"),
+        "msg_path": g(ex, "msg_path", "value"),
+        "c1_one_block_tx_s": g(ex, "c1_ante", "block_path_steady", "txs_per_s"),
+        "c1_replay_tx_s": g(ex, "c1_ante", "replay_pipelined_steady", "txs_per_s"),
+        "c4_replay_leaves_s": g(ex, "c4_multisig", "leaves_per_s"),
+        "c4_one_block_leaves_s": g(ex, "c4_multisig", "one_block_at_a_time", "leaves_per_s"),
+        "ed25519_grouped": g(ex, "ed25519", "value"),
+        "ed25519_64_cached_p50_ms": g(ex, "ed25519", "small_batches", "batches", "64", "keyed_sliced_p50_ms"),
+        "ed25519_64_uncached_p50_ms": g(ex, "ed25519", "small_batches", "batches", "64", "uncached_p50_ms"),
+        "first_call": g(ex, "first_call"),
+        "cpu_baseline_kind": "no-GLV C restatement of the reference algorithm (oracle/secp256k1_oracle.c), not btcec: "
+                             "the Go reference (btcec with GLV) cannot run here and would likely be faster",
+    }
 
 
 def run_inproc(args, verifier_factory=None, workload_fn=None):

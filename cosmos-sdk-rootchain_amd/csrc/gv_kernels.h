@@ -76,8 +76,9 @@ typedef struct gvk_batch {
   // keyed batches with gtab4 set take k_ecmult_k4 (30-doubling 4-group ladder)
   const uint32_t* kqt2;         // arena group tables (2^35 Q, 2^70 Q, 2^100 Q), on the slot's kzq
   const uint32_t* gtab4;        // GV_KEY2_TABLES x (G-type, lambda) tables of 2^35 G, 2^70 G, 2^100 G
-  // k6 set: kqt / kqt2 hold 32-entry group tables (k_keys_build_rows6) and the
-  // ladder is k_ecmult_k6 over gtab6 (GV_K6_GTAB_WORDS); gtab4 unused
+  // k6 set: kqt / kqt2 hold 32-entry group tables (k_keys_build_rows6 or the
+  // resident k6 arena) and the ladder is k_ecmult_k6 over gtab6
+  // (GV_K6_GTAB_WORDS: the full-scalar 24-bit-window G tables); gtab4 unused
   const uint32_t* gtab6;
   int k6;
   // k4 batches with gtabf set: the G half on the unsplit scalar (GV_GF_*),
@@ -120,22 +121,27 @@ hipError_t gvk_unsort_bits(uint32_t n, const uint32_t* pos, const uint64_t* sbit
 #define GV_KEY2_TABLES (GV_LGRP - 1)
 #define GV_GLAT_WORDS (GV_LGRP * 2 * GV_QTAB_N * 16)
 
-// The grouped route's ladder (k_ecmult_k6, in-batch key grouping): the
-// per-batch key tables hold 32 multiples per group (6-bit signed windows: 22
-// per 128-bit GLV half, groups starting at windows 0, 6, 12, 17 = bit offsets
-// 0, 36, 72, 102; 6 positions, 30 doublings, 44 Q additions) and G takes
-// 24-bit windows (6 per half: 12 additions) from 2^23-entry tables of
-// 2^b G and 2^b lambda G for the four group offsets b (4 GiB per device).
+// The 6-bit-window keyed ladder (k_ecmult_k6): the key tables hold 32
+// multiples per group (6-bit signed windows: 22 per 128-bit GLV half, groups
+// starting at windows 0, 6, 12, 17 = bit offsets 0, 36, 72, 102; 6 positions,
+// 30 doublings, 44 Q additions), the lambda frame of k_ecmult_k4 (two beta
+// products per position), and G on the unsplit u1 = e/s: 11 signed 24-bit
+// windows (window j at bit 24 j) added from 2^23-entry tables of 2^o G for
+// the seven offsets o = 36 t (3.5 GiB per device): window j at ladder
+// position p (bit 6 p of the 36-bit group ladder) reads the table of offset
+// 24 j - 6 p (gv_kernels.hip kK6GWin).  Key tables: the resident arena
+// (gv_keys_load, option "keys_k6") and the grouped route's per-batch arena.
 #define GV_K6_QW 6
 #define GV_K6_NT 32                                       // table entries per group
 #define GV_K6_QWIN 22
 #define GV_K6_GW 24
-#define GV_K6_GWIN 6
-#define GV_K6_GTAB_N (1 << (GV_K6_GW - 1))
+#define GV_K6_GWIN 11
+#define GV_K6_GNTAB 7
+#define GV_K6_GTAB_N (1u << (GV_K6_GW - 1))
 #define GV_K6_KEY_WORDS (GV_K6_NT * GV_QENT_WORDS)       // one group table (2,560 B)
-#define GV_K6_GTAB_WORDS ((size_t)GV_LGRP * 2 * GV_K6_GTAB_N * 16)
-static_assert(GV_K6_QWIN + 2 * GV_K6_GWIN <= GV_DIGIT_ROWS, "k6 digits fit the digit rows");
-static_assert(GV_K6_QW * GV_K6_QWIN >= 130 && GV_K6_GW * GV_K6_GWIN >= 130, "k6 windows cover 129-bit halves");
+#define GV_K6_GTAB_WORDS ((size_t)GV_K6_GNTAB * GV_K6_GTAB_N * 16)
+static_assert(GV_K6_QWIN + GV_K6_GWIN <= GV_DIGIT_ROWS, "k6 digits fit the digit rows");
+static_assert(GV_K6_QW * GV_K6_QWIN >= 130 && GV_K6_GW * GV_K6_GWIN >= 257, "k6 windows cover the scalars");
 
 // The k4 ladder's G half on the unsplit scalar (k_ecmult_k4<true>): u1 = e/s
 // is not GLV-split; its 11 signed 25-bit windows (window j at bit 25 j) are
@@ -253,8 +259,15 @@ hipError_t gvk_gen_gtable(uint32_t* gtab, hipStream_t st);
 // the keyed ladder's G tables (GV_KEY2_TABLES x 2 x GV_GTAB_N x 16 words); base_scratch: 48 words
 hipError_t gvk_gen_gtable4(uint32_t* gtab4, uint32_t* base_scratch, hipStream_t st);
 hipError_t gvk_gen_glat(uint32_t* glat, hipStream_t st);
-// the k6 ladder's G tables (GV_K6_GTAB_WORDS words); base_scratch: 64 words
+// the k6 ladder's G tables (GV_K6_GTAB_WORDS words); base_scratch: 112 words
 hipError_t gvk_gen_gtable6(uint32_t* gtab6, uint32_t* base_scratch, hipStream_t st);
+// k6 key tables of n keys (device pub33) into resident-arena slots
+// base..base+n-1 (rows of kqt6: GV_K6_KEY_WORDS, kqt62: 3 per slot); scratch
+// as gvk_keys_build with qr / qe rows of (GV_K6_NT - 1) * 9 / * 18.
+hipError_t gvk_keys_build6(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
+                           uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t* qe, uint32_t base,
+                           uint32_t* kqt6, uint32_t* kzq6, uint32_t kC, uint32_t* kok, uint32_t* kqt62,
+                           uint32_t* kzq62, hipStream_t st);
 // the full-scalar G tables (GV_GF_WORDS words); base_scratch: 96 words
 hipError_t gvk_gen_gtablef(uint32_t* gtabf, uint32_t* base_scratch, hipStream_t st);
 // k6 key tables (32 entries per group) of n keys already unpacked into rows

@@ -693,8 +693,10 @@ __global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u
   // (int16 halves), win = 0..GV_QWIN-1.  G digits (GV_GW-bit windows,
   // [-2^(GV_GW-1), 2^(GV_GW-1)]) as int32: digits[(GV_QWIN + 2j)*C + g] = dG1,
   // digits[(GV_QWIN + 2j + 1)*C + g] = dG2, j = 0..GV_GWIN-1.
+  static_assert(GF || !K6, "the k6 ladder takes G on the unsplit scalar");
   constexpr int QW = K6 ? GV_K6_QW : GV_QW, QWIN = K6 ? GV_K6_QWIN : GV_QWIN;
-  constexpr int GW = K6 ? GV_K6_GW : GV_GW, GWIN = K6 ? GV_K6_GWIN : GV_GWIN;
+  constexpr int GW = GV_GW, GWIN = GV_GWIN;
+  constexpr int GFW = K6 ? GV_K6_GW : GV_GF_W, GFWIN = K6 ? GV_K6_GWIN : GV_GF_WIN;
 #pragma unroll
   for (int win = 0; win < QWIN; ++win) {
     int d0 = booth_digit<QW>(k1q, win), d1 = booth_digit<QW>(k2q, win);
@@ -704,7 +706,7 @@ __global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u
   }
   if (GF) {
 #pragma unroll
-    for (int j = 0; j < GV_GF_WIN; ++j) digits[(size_t)(QWIN + j) * C + g] = (u32)booth_digit8<GV_GF_W>(u1, j);
+    for (int j = 0; j < GFWIN; ++j) digits[(size_t)(QWIN + j) * C + g] = (u32)booth_digit8<GFW>(u1, j);
   } else {
 #pragma unroll
     for (int j = 0; j < GWIN; ++j) {
@@ -944,12 +946,10 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_tables(u32 n, u32 C4
 
 // Affine 2^35 G, 2^70 G, 2^100 G (16 words each) for the keyed ladder's G
 // tables; thread t = group - 1.  Once per device.
-// K6: 2^36 G, 2^72 G, 2^102 G (the k6 group offsets).
-template <bool K6 = false>
 __global__ void k_gen_gbase(u32* out) {
   const int t = threadIdx.x;
   if (t >= GV_KEY2_TABLES) return;
-  const int* grp_bit = K6 ? kK6GrpBit : kLGrpBit;
+  const int* grp_bit = kLGrpBit;
   fe gx, gy;
   fe_from_const(gx, kGx);
   fe_from_const(gy, kGy);
@@ -964,11 +964,14 @@ __global__ void k_gen_gbase(u32* out) {
   for (int i = 0; i < 8; ++i) { out[t * 16 + i] = x8.v[i]; out[t * 16 + 8 + i] = y8.v[i]; }
 }
 
-// Affine 2^o G (16 words each) for the full-scalar G tables' offsets o = kGFOff[t].
+// Affine 2^o G (16 words each) for the full-scalar G tables' offsets o =
+// kGFOff[t] (K6: the k6 ladder's tables, o = 36 t).
 __constant__ const int kGFOff[GV_GF_NTAB] = {0, 45, 100, 145, 195, 220};
+template <bool K6 = false>
 __global__ void k_gen_gbasef(u32* out) {
   const int t = threadIdx.x;
-  if (t >= GV_GF_NTAB) return;
+  if (t >= (K6 ? GV_K6_GNTAB : GV_GF_NTAB)) return;
+  const int off = K6 ? 6 * GV_K6_QW * t : kGFOff[t];
   fe gx, gy;
   fe_from_const(gx, kGx);
   fe_from_const(gy, kGy);
@@ -976,7 +979,7 @@ __global__ void k_gen_gbasef(u32* out) {
   f29_from_words(p.x, gx.v);
   f29_from_words(p.y, gy.v);
   f29_set_u32(p.z, 1);
-  for (int k = 0; k < kGFOff[t]; ++k) gej29_double(p, p);
+  for (int k = 0; k < off; ++k) gej29_double(p, p);
   fe x8, y8;
   gej29_to_affine_words(x8, y8, p);
 #pragma unroll
@@ -1389,21 +1392,25 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gta
 }
 
 // ------------------------------------------------------------- k_ecmult_k6
-// The grouped route's ladder (gv_kernels.h GV_K6_*): the per-batch key
-// tables hold 32 multiples per group, so each 128-bit GLV half takes 22
-// six-bit windows, split into the groups [0,6), [6,12), [12,17), [17,22)
-// (bit offsets 0, 36, 72, 102); window w of group k is added at local
-// position w - w0(k) of a 36-bit ladder: 5 x 6 = 30 doublings and 44 Q
-// additions (52 with 5-bit windows).  G takes 24-bit windows (6 per half, 12
-// additions instead of 14) from the 2^23-entry tables of 2^b G and
-// 2^b lambda G, b the group offsets: G window j (bit 24 j) sits in the group
-// of the largest offset b <= 24 j at position (24 j - b) / 6.  Same
-// additions, final check and semantics as k_ecmult_k4 otherwise.
+// The 6-bit-window keyed ladder (gv_kernels.h GV_K6_*): the key tables hold
+// 32 multiples per group, so each 128-bit GLV half takes 22 six-bit windows,
+// split into the groups [0,6), [6,12), [12,17), [17,22) (bit offsets 0, 36,
+// 72, 102); window w of group k is added at local position w - w0(k) of a
+// 36-bit ladder: 5 x 6 = 30 doublings and 44 Q additions (52 with 5-bit
+// windows).  The lambda-Q entries go through the lambda frame of
+// k_ecmult_k4 (two beta products per position).  G on the unsplit u1: its 11
+// signed 24-bit windows (window j at bit 24 j) from the 2^23-entry tables of
+// 2^o G, o = 36 t: window j at position p reads the table of offset
+// 24 j - 6 p -- positions 0, 2, 4 take windows {0, 3, 6, 9}, {2, 5, 8},
+// {1, 4, 7, 10} from the tables of offsets {0, 72, 144, 216},
+// {36, 108, 180}, {0, 72, 144, 216}.  Same additions, final check and
+// semantics as k_ecmult_k4 otherwise.
 __constant__ const int kK6WStart[4] = {0, 6, 12, 17};
 __constant__ const int kK6NWin[4] = {6, 6, 5, 5};
-// G windows at each position (up to two), their group
-__constant__ const int kK6GWin[6][2] = {{0, 3}, {-1, -1}, {2, -1}, {5, -1}, {1, 4}, {-1, -1}};
-__constant__ const int kK6GGrp[GV_K6_GWIN] = {0, 0, 1, 2, 2, 3};
+// G windows at each position (up to four) and the table each reads (o / 36)
+__constant__ const int kK6GWin[6][4] = {{0, 3, 6, 9}, {-1, -1, -1, -1}, {2, 5, 8, -1},
+                                        {-1, -1, -1, -1}, {1, 4, 7, 10}, {-1, -1, -1, -1}};
+__constant__ const int kK6GTab[GV_K6_GWIN] = {0, 0, 1, 2, 2, 3, 4, 4, 5, 6, 6};
 
 __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k6(const u32* gtab6, u32 n, u32 C, const u32* digits,
                                                         const u32* kqt, const u32* kqt2, const u32* kzq,
@@ -1422,39 +1429,38 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k6(const u32* gta
 #pragma unroll 1
       for (int d = 0; d < GV_K6_QW; ++d) gej29x_double(acc, acc);
     }
-    // slots 0..7: (group, Q / lambda Q); 8..11: up to two G windows x (G, lambda G)
+    // slots 0..3: Q of groups 0..3; 4..7: lambda Q of groups 3..0 on the
+    // lambda^2 frame; 8..11: up to four G windows
 #pragma unroll 1
     for (int slot = 0; slot < 12; ++slot) {
+      if ((slot == 4 || slot == 8) && !inf) {
+        fe29 c;                                            // into lambda^2 (acc) / back to acc
+        f29_from_const(c, slot == 4 ? kBeta2 : kBeta);
+        f29x_mul(acc.x, acc.x, c);
+      }
       int d;
       const u32* tab;
       u32 row = 0;
       const bool isg = slot >= 8;
       if (!isg) {
-        const int grp = slot >> 1;
+        const bool lam = slot >= 4;
+        const int grp = lam ? 7 - slot : slot;
         if (pos >= kK6NWin[grp]) continue;                 // wave-uniform
         const u32 dq = digits[(size_t)(kK6WStart[grp] + pos) * C + g];
-        d = (slot & 1) ? ((int)dq >> 16) : ((int)(dq << 16) >> 16);
+        d = lam ? ((int)dq >> 16) : ((int)(dq << 16) >> 16);
         tab = grp == 0 ? kqt : kqt2;
         row = grp == 0 ? qi : qi * GV_KEY2_TABLES + (grp - 1);
       } else {
-        const int j = kK6GWin[pos][(slot - 8) >> 1];
+        const int j = kK6GWin[pos][slot - 8];
         if (j < 0) continue;                               // wave-uniform
-        d = (int)digits[(size_t)(GV_K6_QWIN + 2 * j + (slot & 1)) * C + g];
-        tab = gtab6 + ((size_t)kK6GGrp[j] * 2 + (slot & 1)) * GV_K6_GTAB_N * 16;
+        d = (int)digits[(size_t)(GV_K6_QWIN + j) * C + g];
+        tab = gtab6 + (size_t)kK6GTab[j] * GV_K6_GTAB_N * 16;
       }
       if (d == 0) continue;
       const u32 e = (u32)((d < 0 ? -d : d) - 1);
       fe29 x, y;
-      if (!isg) {
-        load_qent29<GV_K6_NT>(x, y, tab, row, e);
-        if (slot & 1) {                                    // lambda * P = (beta * x, y)
-          fe29 beta;
-          f29_from_const(beta, kBeta);
-          f29x_mul(x, x, beta);
-        }
-      } else {
-        load_gent29(x, y, tab, e);
-      }
+      if (!isg) load_qent29<GV_K6_NT>(x, y, tab, row, e);
+      else load_gent29(x, y, tab, e);
       if (d < 0) f29_neg<1>(y, y);                         // 2
       add_entry(acc, inf, x, y, isg ? &zq : nullptr);
     }
@@ -1572,7 +1578,7 @@ hipError_t gvk_gen_gtable(uint32_t* gtab, hipStream_t st) {
 }
 
 hipError_t gvk_gen_gtable4(uint32_t* gtab4, uint32_t* base_scratch, hipStream_t st) {
-  hipLaunchKernelGGL(gv::k_gen_gbase<false>, dim3(1), dim3(64), 0, st, base_scratch);
+  hipLaunchKernelGGL(gv::k_gen_gbase, dim3(1), dim3(64), 0, st, base_scratch);
   for (int k = 0; k < GV_KEY2_TABLES; ++k)
     hipLaunchKernelGGL(gv::k_gen_gtable<GV_GTAB_N>, dim3((GV_GTAB_N + 63) / 64), dim3(64), 0, st,
                        gtab4 + (size_t)k * 2 * GV_GTAB_N * 16, (const uint32_t*)(base_scratch + 16 * k));
@@ -1580,16 +1586,16 @@ hipError_t gvk_gen_gtable4(uint32_t* gtab4, uint32_t* base_scratch, hipStream_t 
 }
 
 hipError_t gvk_gen_gtable6(uint32_t* gtab6, uint32_t* base_scratch, hipStream_t st) {
-  hipLaunchKernelGGL(gv::k_gen_gbase<true>, dim3(1), dim3(64), 0, st, base_scratch);
+  hipLaunchKernelGGL(gv::k_gen_gbasef<true>, dim3(1), dim3(64), 0, st, base_scratch);
   const dim3 grd((GV_K6_GTAB_N + 255) / 256), blk(256);
-  for (int k = 0; k < GV_LGRP; ++k)
-    hipLaunchKernelGGL(gv::k_gen_gtable<GV_K6_GTAB_N>, grd, blk, 0, st, gtab6 + (size_t)k * 2 * GV_K6_GTAB_N * 16,
-                       k == 0 ? (const uint32_t*)nullptr : (const uint32_t*)(base_scratch + 16 * (k - 1)));
+  for (int k = 0; k < GV_K6_GNTAB; ++k)
+    hipLaunchKernelGGL((gv::k_gen_gtable<GV_K6_GTAB_N, false>), grd, blk, 0, st, gtab6 + (size_t)k * GV_K6_GTAB_N * 16,
+                       (const uint32_t*)(base_scratch + 16 * k));
   return hipGetLastError();
 }
 
 hipError_t gvk_gen_gtablef(uint32_t* gtabf, uint32_t* base_scratch, hipStream_t st) {
-  hipLaunchKernelGGL(gv::k_gen_gbasef, dim3(1), dim3(64), 0, st, base_scratch);
+  hipLaunchKernelGGL(gv::k_gen_gbasef<false>, dim3(1), dim3(64), 0, st, base_scratch);
   const dim3 grd((GV_GF_TAB_N + 255) / 256), blk(256);
   for (int k = 0; k < GV_GF_NTAB; ++k)
     hipLaunchKernelGGL((gv::k_gen_gtable<GV_GF_TAB_N, false>), grd, blk, 0, st, gtabf + (size_t)k * GV_GF_TAB_N * 16,
@@ -1630,7 +1636,7 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
     if (b->keys_ready) (void)hipStreamWaitEvent(st, b->keys_ready, 0);   // grouped keys built beside s^-1
     if (b->ev[1]) (void)hipEventRecord(b->ev[1], st);
     if (k6)
-      hipLaunchKernelGGL((gv::k_prep<true, true>), grd, blk, 0, st, C, b->n, (const uint32_t*)nullptr,
+      hipLaunchKernelGGL((gv::k_prep<true, true, true>), grd, blk, 0, st, C, b->n, (const uint32_t*)nullptr,
                          (const uint32_t*)nullptr, b->in_r, b->in_s, b->in_e, (const uint32_t*)w, b->digits,
                          (uint32_t*)nullptr, (uint32_t*)nullptr, b->flags, sorted ? b->srt.kslot : b->kslot,
                          b->kok, b->kcount, b->in_pfx);
@@ -1734,6 +1740,22 @@ hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t
   hipLaunchKernelGGL(gv::k_unpack, grd, blk, 0, st, pub33, (const uint8_t*)nullptr, (const uint8_t*)nullptr, n, C,
                      in_x, in_pfx, in_r, in_s, in_e);
   return keys_tables_launch(n, C, in_x, in_pfx, qr, qe, base, kqt, kzq, kC, kok, kqt2, kzq2, st);
+}
+
+hipError_t gvk_keys_build6(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
+                           uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t* qe, uint32_t base,
+                           uint32_t* kqt6, uint32_t* kzq6, uint32_t kC, uint32_t* kok, uint32_t* kqt62,
+                           uint32_t* kzq62, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const dim3 blk(256), grd(C / 256);
+  hipLaunchKernelGGL(gv::k_unpack, grd, blk, 0, st, pub33, (const uint8_t*)nullptr, (const uint8_t*)nullptr, n, C,
+                     in_x, in_pfx, in_r, in_s, in_e);
+  const uint32_t C4 = (4u * n + 255u) / 256u * 256u;
+  hipLaunchKernelGGL(gv::k_keys_chain<true>, dim3((n + 255) / 256), dim3(256), 0, st, n, C, in_x, in_pfx, base, kqt6,
+                     kC, kok, kqt62, kzq62);
+  hipLaunchKernelGGL(gv::k_keys_tables<GV_K6_NT>, dim3(C4 / 256), dim3(256), 0, st, n, C4, base, kqt6, kzq6, kC,
+                     kqt62, kzq62, qr, qe);
+  return hipGetLastError();
 }
 
 hipError_t gvk_keys_point(uint32_t n, const uint32_t* slots, const uint32_t* kqt, const uint32_t* kzq, uint32_t kC,

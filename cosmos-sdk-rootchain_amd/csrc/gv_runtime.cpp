@@ -128,11 +128,19 @@ struct Dev {
   uint32_t *kqt2 = nullptr, *kzq2 = nullptr;      // the keyed latency schedule's group tables (2^35 Q, ...)
   uint32_t* glat = nullptr;                       // group tables of G / lambda G (k_gen_glat)
   uint32_t* gtab4 = nullptr;                      // k_ecmult_k4's tables of 2^35 G, 2^70 G, 2^100 G (+ lambda)
-  uint32_t* gtab6 = nullptr;                      // k_ecmult_k6's 24-bit-window tables of 2^b G, 2^b lambda G (4 GiB)
-  bool gtab6_failed = false;                      // its allocation failed once: the grouped route stays on k4
+  uint32_t* gtab6 = nullptr;                      // k_ecmult_k6's full-scalar 24-bit-window tables of 2^(36 t) G (3.5 GiB)
+  bool gtab6_failed = false;                      // its allocation failed once: keyed / grouped batches stay on k4
   uint32_t* gtabf = nullptr;                      // k_ecmult_k4<true>'s full-scalar G tables (GV_GF_WORDS, 6 GiB)
   bool gtabf_failed = false;                      // its allocation failed once: k4 keeps the GLV G tables
+  bool gtab4_failed = false;                      // gtab4's allocation failed: keyed batches on the 125-doubling ladder
   size_t kcap = 0;
+  // the resident k6 arena (option "keys_k6"): per slot the four 32-entry group
+  // tables of Q, 2^36 Q, 2^72 Q, 2^102 Q on one Z (kzq6, 8 rows of stride
+  // kcap; kzq62 holds the chain's parked Zs), read by k_ecmult_k6
+  uint32_t *kqt6 = nullptr, *kzq6 = nullptr, *kqt62 = nullptr, *kzq62 = nullptr;
+  size_t keys6 = 0;                               // leading slots whose k6 tables are built
+  // HBM held by the optional tables (G tables, key arenas) against ctx->hbm_budget
+  size_t opt_bytes = 0;
   // ring of per-launch stage events for gv_stage_stats
   static constexpr int kRing = 256;
   hipEvent_t ring[kRing][6] = {};                // start, after unpack / s^-1 / prep, ladder start, ladder end
@@ -244,16 +252,47 @@ int set_release(Set* s, hipStream_t st) {
   return GV_OK;
 }
 
+// Bytes per slot of the resident key arena: the k4 tables (Q table, the three
+// group tables, their Zs, the verdict) and, with the k6 arena, its four
+// 32-entry group tables and Zs.
+size_t key_slot_bytes(bool k6) {
+  size_t b = ((size_t)GV_KEY_WORDS * (1 + GV_KEY2_TABLES) + 8 * (1 + GV_KEY2_TABLES) + 1) * 4;
+  if (k6) b += ((size_t)GV_K6_KEY_WORDS * (1 + GV_KEY2_TABLES) + 8 * (1 + GV_KEY2_TABLES)) * 4;
+  return b;
+}
+
 // Grow the key arena to hold `need` slots, keeping the first `used` (row
-// stride of kzq changes with the capacity).
-int ensure_keys(Dev* d, size_t need, size_t used, hipStream_t st) {
-  if (need <= d->kcap) return GV_OK;
-  // doubling, but not past GV_KEY_CAP (the callers' reset point) unless asked
-  const size_t grow = std::min<size_t>(2 * d->kcap, std::max<size_t>(need, GV_KEY_CAP));
-  const size_t cap = round_up(std::max<size_t>({need, grow, 4096}), 256);
+// stride of the Z rows changes with the capacity).  Doubling, but not past
+// key_cap (the callers' reset point: GV_KEY_CAP or the "key_cap" option) --
+// past it the arena grows to exactly what is needed (a caller that never
+// resets pays one copy per load, not a quadratic series of doublings).
+// k6: the arena also holds the k6 group tables (allocated on the first k6
+// load; *k6 is cleared when they do not fit the budget, the k4 tables stay).
+int ensure_keys(Dev* d, size_t need, size_t used, hipStream_t st, size_t key_cap, size_t budget, bool* k6) {
+  const bool want6 = k6 && *k6;
+  if (need <= d->kcap && (!want6 || d->kqt6)) return GV_OK;
+  size_t cap = d->kcap;
+  if (need > d->kcap) {
+    const size_t grow = d->kcap >= key_cap ? need : std::min<size_t>(2 * d->kcap, std::max<size_t>(need, key_cap));
+    cap = round_up(std::max<size_t>({need, grow, 4096}), 256);
+  }
+  const bool has6 = d->kqt6 != nullptr;
+  bool alloc6 = want6 || has6;
+  // budget: the new arena beside the old one during the copy, plus the other
+  // optional tables
+  const size_t old_b = d->kcap * key_slot_bytes(has6);
+  const size_t base_b = d->opt_bytes - std::min(d->opt_bytes, old_b);
+  if (base_b + old_b + cap * key_slot_bytes(alloc6) > budget) {
+    if (!alloc6 || has6 || base_b + old_b + cap * key_slot_bytes(false) > budget) return GV_ENOMEM;
+    alloc6 = false;                             // no room for the k6 tables: k4 only
+    *k6 = false;
+    if (need <= d->kcap) return GV_OK;
+  }
   uint32_t *qt = nullptr, *zq = nullptr, *ok = nullptr, *qt2 = nullptr, *zq2 = nullptr;
+  uint32_t *qt6 = nullptr, *zq6 = nullptr, *qt62 = nullptr, *zq62 = nullptr;
   auto fail = [&]() {
-    for (uint32_t* p : {qt, zq, ok, qt2, zq2}) if (p) (void)hipFree(p);
+    for (uint32_t* p : {qt, zq, ok, qt2, zq2, qt6, zq6, qt62, zq62}) if (p) (void)hipFree(p);
+    (void)hipGetLastError();
     return GV_ENOMEM;
   };
   if (hipMalloc(&qt, cap * GV_KEY_WORDS * 4) != hipSuccess) return fail();
@@ -261,6 +300,14 @@ int ensure_keys(Dev* d, size_t need, size_t used, hipStream_t st) {
   if (hipMalloc(&ok, cap * 4) != hipSuccess) return fail();
   if (hipMalloc(&qt2, cap * GV_KEY2_TABLES * GV_KEY_WORDS * 4) != hipSuccess) return fail();
   if (hipMalloc(&zq2, cap * GV_KEY2_TABLES * 8 * 4) != hipSuccess) return fail();
+  if (alloc6) {
+    if (hipMalloc(&qt6, cap * GV_K6_KEY_WORDS * 4) != hipSuccess) return fail();
+    if (hipMalloc(&zq6, cap * 8 * 4) != hipSuccess) return fail();
+    if (hipMalloc(&qt62, cap * GV_KEY2_TABLES * GV_K6_KEY_WORDS * 4) != hipSuccess) return fail();
+    if (hipMalloc(&zq62, cap * GV_KEY2_TABLES * 8 * 4) != hipSuccess) return fail();
+  }
+  // the k6 tables of the slots below `used` exist only if the old arena had them
+  const size_t used6 = d->kqt6 ? used : 0;
   if (used) {
     CK(hipMemcpyAsync(qt, d->kqt, used * GV_KEY_WORDS * 4, hipMemcpyDeviceToDevice, st));
     CK(hipMemcpyAsync(qt2, d->kqt2, used * GV_KEY2_TABLES * GV_KEY_WORDS * 4, hipMemcpyDeviceToDevice, st));
@@ -269,10 +316,22 @@ int ensure_keys(Dev* d, size_t need, size_t used, hipStream_t st) {
     for (int r = 0; r < GV_KEY2_TABLES * 8; ++r)
       CK(hipMemcpyAsync(zq2 + r * cap, d->kzq2 + r * d->kcap, used * 4, hipMemcpyDeviceToDevice, st));
     CK(hipMemcpyAsync(ok, d->kok, used * 4, hipMemcpyDeviceToDevice, st));
-    CK(hipStreamSynchronize(st));
   }
-  for (uint32_t* p : {d->kqt, d->kzq, d->kok, d->kqt2, d->kzq2}) if (p) (void)hipFree(p);
-  d->kqt = qt; d->kzq = zq; d->kok = ok; d->kqt2 = qt2; d->kzq2 = zq2; d->kcap = cap;
+  if (used6 && alloc6) {
+    CK(hipMemcpyAsync(qt6, d->kqt6, used6 * GV_K6_KEY_WORDS * 4, hipMemcpyDeviceToDevice, st));
+    CK(hipMemcpyAsync(qt62, d->kqt62, used6 * GV_KEY2_TABLES * GV_K6_KEY_WORDS * 4, hipMemcpyDeviceToDevice, st));
+    for (int r = 0; r < 8; ++r)
+      CK(hipMemcpyAsync(zq6 + r * cap, d->kzq6 + r * d->kcap, used6 * 4, hipMemcpyDeviceToDevice, st));
+    for (int r = 0; r < GV_KEY2_TABLES * 8; ++r)
+      CK(hipMemcpyAsync(zq62 + r * cap, d->kzq62 + r * d->kcap, used6 * 4, hipMemcpyDeviceToDevice, st));
+  }
+  if (used) CK(hipStreamSynchronize(st));
+  for (uint32_t* p : {d->kqt, d->kzq, d->kok, d->kqt2, d->kzq2, d->kqt6, d->kzq6, d->kqt62, d->kzq62})
+    if (p) (void)hipFree(p);
+  d->kqt = qt; d->kzq = zq; d->kok = ok; d->kqt2 = qt2; d->kzq2 = zq2;
+  d->kqt6 = qt6; d->kzq6 = zq6; d->kqt62 = qt62; d->kzq62 = zq62;
+  d->kcap = cap;
+  d->opt_bytes = base_b + cap * key_slot_bytes(alloc6);
   return GV_OK;
 }
 
@@ -478,9 +537,14 @@ struct gv_ctx {
   bool keyed_k4 = true;         // keyed batches on k_ecmult_k4 (GV_KEYED_K4=0: the 125-doubling ladder, A/B)
   bool gfull = true;            // k4 batches take G on the unsplit scalar: 11 25-bit windows instead of 14 20-bit
                                 // GLV windows (k_ecmult_k4<true>, 6 GiB of tables; GV_GFULL=0: A/B)
-  bool k6 = false;              // grouped batches on k_ecmult_k6: 6-bit Q / 24-bit G windows, 32-entry key tables
-                                // (GV_K6=1).  Its ladder is 10 % faster than k4's but the doubled key tables cost
-                                // more than that under C2's 16 items per key: 218-220 vs 222M/s (profiles/r04/prio_ab)
+  bool k6 = false;              // grouped batches on k_ecmult_k6: 6-bit Q windows on 32-entry key tables, the lambda
+                                // frame, G on the unsplit u1 in 24-bit windows (GV_K6=1)
+  bool keys_k6 = true;          // the resident arena (gv_keys_load) also holds k6 tables and its throughput batches
+                                // run k_ecmult_k6: the table build is paid once per key, not per batch (GV_KEYS_K6)
+  size_t key_cap = GV_KEY_CAP;  // the callers' key-arena reset point: growth doubles up to here ("key_cap", GV_KEY_CAP)
+  size_t hbm_budget = SIZE_MAX; // bytes of optional device tables per device (G tables, key arenas; "hbm_budget_mb",
+                                // GV_HBM_BUDGET_MB): a table past it is not built and batches take the schedule
+                                // that needs less, with the same verdicts
   bool pipeline_dev = true;     // pipelined device-resident calls on the context stream (dev_run; GV_PIPELINE=0: A/B)
   bool two_ladders = true;      // ... whose ladders alternate two high-priority streams, so the next ladder starts in
                                 // the current one's tail (bitmap writes kept in call order; GV_TWO_LADDERS=0: A/B)
@@ -516,77 +580,115 @@ EdGroupCfg ed_group_cfg(const gv_ctx* ctx) {
                     ctx->ed_keys_split};
 }
 
-// The 20-bit-window tables of 2^35 G, 2^70 G, 2^100 G (and lambda images)
-// the 4-group keyed ladder reads (k_ecmult_k4): built on first use, 192 MiB.
-// set s is a scratch set with capacity >= 256 (its flags rows hold the base points).
-// The full-scalar G tables (GV_GF_WORDS, 6 GiB): built beside gtab4, ~0.2 s.
-// An allocation failure is remembered and k4 batches keep the GLV G tables.
-int ensure_gtabf(gv_ctx* ctx, Dev* d, Set* s, hipStream_t st) {
-  if (d->gtabf || !ctx->gfull || d->gtabf_failed) return GV_OK;
-  uint32_t* tf = nullptr;
-  if (hipMalloc(&tf, GV_GF_WORDS * 4) != hipSuccess) {
+// Optional device tables (the G tables past the 64 MiB GLV pair, the key
+// arenas) are allocated against the context's HBM budget (gv_set_option
+// "hbm_budget_mb", env GV_HBM_BUDGET_MB; default: whatever hipMalloc grants).
+// A table that does not fit is remembered as failed and the batches take the
+// schedule that needs less (k6 -> k4 -> the 125-doubling keyed ladder; the
+// full-scalar G tables -> the GLV G windows) with the same verdicts.
+uint32_t* opt_alloc(gv_ctx* ctx, Dev* d, size_t bytes) {
+  if (d->opt_bytes + bytes > ctx->hbm_budget) return nullptr;
+  uint32_t* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) {
     (void)hipGetLastError();
-    d->gtabf_failed = true;
-    return GV_OK;
+    return nullptr;
   }
+  d->opt_bytes += bytes;
+  return p;
+}
+void opt_free(Dev* d, uint32_t*& p, size_t bytes) {
+  if (!p) return;
+  (void)hipFree(p);
+  p = nullptr;
+  d->opt_bytes -= std::min(d->opt_bytes, bytes);
+}
+constexpr size_t kGtab4Bytes = (size_t)GV_KEY2_TABLES * 2 * GV_GTAB_N * 16 * 4;
+
+// Build one G table set on stream st (set s is a scratch set with capacity >=
+// 256: its flags rows hold the base points).  Enqueued only; the caller syncs.
+template <class GEN>
+int gen_table(Set* s, hipStream_t st, GEN&& gen) {
   int rc;
-  if ((rc = ensure_cap(s, 256))) { (void)hipFree(tf); return rc; }
-  if ((rc = set_acquire(s, st))) { (void)hipFree(tf); return rc; }
-  if (gvk_gen_gtablef(tf, s->flags, st) != hipSuccess) { (void)hipFree(tf); return GV_EHIP; }
-  if ((rc = set_release(s, st))) { (void)hipFree(tf); return rc; }
-  if (hipStreamSynchronize(st) != hipSuccess) { (void)hipFree(tf); return GV_EHIP; }
+  if ((rc = ensure_cap(s, 256))) return rc;
+  if ((rc = set_acquire(s, st))) return rc;
+  if (gen(s->flags) != hipSuccess) return GV_EHIP;
+  return set_release(s, st);
+}
+
+// The full-scalar G tables (GV_GF_WORDS, 6 GiB: k_ecmult_k4<true> and the
+// per-item route's k_ecmult<false, true>), the 20-bit-window tables of 2^35 G,
+// 2^70 G, 2^100 G and their lambda images (k_ecmult_k4, 192 MiB) and the k6
+// ladder's full-scalar 24-bit-window tables (GV_K6_GTAB_WORDS, 3.5 GiB):
+// built at gv_open on every device at once (gv_open: enqueue on each device,
+// then one sync each; ~0.5 s), or on first use after an option switched a
+// schedule on.  sync = false: enqueue only.
+int ensure_gtabf(gv_ctx* ctx, Dev* d, Set* s, hipStream_t st, bool sync = true) {
+  if (d->gtabf || !ctx->gfull || d->gtabf_failed) return GV_OK;
+  uint32_t* tf = opt_alloc(ctx, d, GV_GF_WORDS * 4);
+  if (!tf) { d->gtabf_failed = true; return GV_OK; }
+  int rc = gen_table(s, st, [&](uint32_t* sc) { return gvk_gen_gtablef(tf, sc, st); });
+  if (!rc && sync && hipStreamSynchronize(st) != hipSuccess) rc = GV_EHIP;
+  if (rc) { opt_free(d, tf, GV_GF_WORDS * 4); return rc; }
   d->gtabf = tf;
   return GV_OK;
 }
 
-int ensure_gtab4(gv_ctx* ctx, Dev* d, Set* s, hipStream_t st) {
+int ensure_gtab4(gv_ctx* ctx, Dev* d, Set* s, hipStream_t st, bool sync = true) {
   if (!ctx->keyed_k4) return GV_OK;
-  if (d->gtab4) return ensure_gtabf(ctx, d, s, st);
-  uint32_t* t4 = nullptr;
-  if (hipMalloc(&t4, (size_t)GV_KEY2_TABLES * 2 * GV_GTAB_N * 16 * 4) != hipSuccess) return GV_OK;   // keep k_ecmult<true>
-  int rc;
-  if ((rc = ensure_cap(s, 256))) { (void)hipFree(t4); return rc; }
-  if ((rc = set_acquire(s, st))) { (void)hipFree(t4); return rc; }
-  if (gvk_gen_gtable4(t4, s->flags, st) != hipSuccess) { (void)hipFree(t4); return GV_EHIP; }
-  if ((rc = set_release(s, st))) { (void)hipFree(t4); return rc; }
-  if (hipStreamSynchronize(st) != hipSuccess) { (void)hipFree(t4); return GV_EHIP; }
-  d->gtab4 = t4;
-  return ensure_gtabf(ctx, d, s, st);
+  if (!d->gtab4 && !d->gtab4_failed) {
+    uint32_t* t4 = opt_alloc(ctx, d, kGtab4Bytes);
+    if (!t4) {
+      d->gtab4_failed = true;                   // keyed batches keep k_ecmult<true>
+      return GV_OK;
+    }
+    int rc = gen_table(s, st, [&](uint32_t* sc) { return gvk_gen_gtable4(t4, sc, st); });
+    if (!rc && sync && hipStreamSynchronize(st) != hipSuccess) rc = GV_EHIP;
+    if (rc) { opt_free(d, t4, kGtab4Bytes); return rc; }
+    d->gtab4 = t4;
+  }
+  return ensure_gtabf(ctx, d, s, st, sync);
 }
 
-// k_ecmult_k6's G tables (GV_K6_GTAB_WORDS, 4 GiB): built on first use, ~0.1 s.
-// An allocation failure is remembered and the grouped route stays on k4.
-int ensure_gtab6(gv_ctx* ctx, Dev* d, Set* s, hipStream_t st) {
-  if (d->gtab6 || !ctx->k6 || d->gtab6_failed) return GV_OK;
-  uint32_t* t6 = nullptr;
-  if (hipMalloc(&t6, GV_K6_GTAB_WORDS * 4) != hipSuccess) {
-    (void)hipGetLastError();
-    d->gtab6_failed = true;
-    return GV_OK;
-  }
-  int rc;
-  if ((rc = ensure_cap(s, 256))) { (void)hipFree(t6); return rc; }
-  if ((rc = set_acquire(s, st))) { (void)hipFree(t6); return rc; }
-  if (gvk_gen_gtable6(t6, s->flags, st) != hipSuccess) { (void)hipFree(t6); return GV_EHIP; }
-  if ((rc = set_release(s, st))) { (void)hipFree(t6); return rc; }
-  if (hipStreamSynchronize(st) != hipSuccess) { (void)hipFree(t6); return GV_EHIP; }
+// k_ecmult_k6's G tables.  A failure is remembered and keyed / grouped batches
+// stay on k4.  `want`: the schedule is on (ctx->k6 for the grouped route,
+// ctx->keys_k6 for the resident arena).
+int ensure_gtab6(gv_ctx* ctx, Dev* d, Set* s, hipStream_t st, bool want, bool sync = true) {
+  if (d->gtab6 || !want || d->gtab6_failed) return GV_OK;
+  uint32_t* t6 = opt_alloc(ctx, d, GV_K6_GTAB_WORDS * 4);
+  if (!t6) { d->gtab6_failed = true; return GV_OK; }
+  int rc = gen_table(s, st, [&](uint32_t* sc) { return gvk_gen_gtable6(t6, sc, st); });
+  if (!rc && sync && hipStreamSynchronize(st) != hipSuccess) rc = GV_EHIP;
+  if (rc) { opt_free(d, t6, GV_K6_GTAB_WORDS * 4); return rc; }
   d->gtab6 = t6;
   return GV_OK;
 }
 
-int ensure_group_arena(Set* s, size_t cap, bool k6) {
+// The set's per-batch key arena for in-batch grouping (cap keys; k6: 32-entry
+// group tables), charged to the HBM budget like the other optional tables.
+size_t group_arena_bytes(size_t cap, bool k6) {
+  const size_t ent = (size_t)(k6 ? GV_K6_KEY_WORDS : GV_KEY_WORDS) * 4;
+  return cap * (ent * (1 + GV_KEY2_TABLES) + 8 * 4 * (1 + GV_KEY2_TABLES) + 4);
+}
+int ensure_group_arena(gv_ctx* ctx, Dev* d, Set* s, size_t cap, bool k6) {
   if (cap <= s->gcap && k6 == s->gk6) return GV_OK;
   for (uint32_t** p : {&s->g_kqt, &s->g_kzq, &s->g_kok, &s->g_kqt2, &s->g_kzq2})
     if (*p) { (void)hipFree(*p); *p = nullptr; }
+  d->opt_bytes -= std::min(d->opt_bytes, group_arena_bytes(s->gcap, s->gk6));
   s->gcap = 0;
   s->gk6 = k6;
   const size_t ent = (size_t)(k6 ? GV_K6_KEY_WORDS : GV_KEY_WORDS) * 4;
+  if (d->opt_bytes + group_arena_bytes(cap, k6) > ctx->hbm_budget) return GV_ENOMEM;
   if (hipMalloc(&s->g_kqt, cap * ent) != hipSuccess || hipMalloc(&s->g_kzq, cap * 8 * 4) != hipSuccess ||
       hipMalloc(&s->g_kok, cap * 4) != hipSuccess ||
       hipMalloc(&s->g_kqt2, cap * GV_KEY2_TABLES * ent) != hipSuccess ||
-      hipMalloc(&s->g_kzq2, cap * GV_KEY2_TABLES * 8 * 4) != hipSuccess)
+      hipMalloc(&s->g_kzq2, cap * GV_KEY2_TABLES * 8 * 4) != hipSuccess) {
+    (void)hipGetLastError();
+    for (uint32_t** p : {&s->g_kqt, &s->g_kzq, &s->g_kok, &s->g_kqt2, &s->g_kzq2})
+      if (*p) { (void)hipFree(*p); *p = nullptr; }
     return GV_ENOMEM;
+  }
   s->gcap = cap;
+  d->opt_bytes += group_arena_bytes(cap, k6);
   return GV_OK;
 }
 
@@ -625,10 +727,14 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   CK(hipStreamSynchronize(st));
   const size_t U = *s->h_count;
   if (U == 0 || U * ctx->group_div > n || U > capU) return GV_OK;   // many distinct keys: the pub33 pipeline
-  if (ctx->k6 && k6_room && (rc = ensure_gtab6(ctx, d, s, st))) return rc;
-  const bool k6 = ctx->k6 && k6_room && d->gtab6;
+  if (ctx->k6 && k6_room && (rc = ensure_gtab6(ctx, d, s, st, true))) return rc;
+  bool k6 = ctx->k6 && k6_room && d->gtab6;
+  if (k6 && (rc = ensure_group_arena(ctx, d, s, capU, true))) {
+    if (rc != GV_ENOMEM) return rc;
+    k6 = false;                                 // no room for the 32-entry tables: k4
+  }
   if (!k6 && (rc = ensure_gtab4(ctx, d, s, st))) return rc;
-  if ((rc = ensure_group_arena(s, capU, k6))) return rc == GV_ENOMEM ? GV_OK : rc;
+  if (!k6 && (rc = ensure_group_arena(ctx, d, s, capU, false))) return rc == GV_ENOMEM ? GV_OK : rc;
   // the tables are built on the set's side stream while k_scalar_inv (which
   // does not read keys) runs on st: both are one wave per SIMD or so
   CK(hipEventRecord(s->fork, st));
@@ -703,7 +809,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
   int rc = ensure_cap(s, C);
   if (rc) return rc;
   if (kslot && !ka) {                           // the arena always exists for a keyed batch
-    rc = ensure_keys(d, 1, ctx->keys, st);
+    rc = ensure_keys(d, 1, ctx->keys, st, ctx->key_cap, ctx->hbm_budget, nullptr);
     if (rc) return rc;
   }
   rc = set_acquire(s, st);
@@ -751,6 +857,12 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
   // such a chunk takes the pipeline whatever its size
   const bool small = n <= (kslot ? ctx->lat_max_keyed : ctx->lat_max) && !b.k6;
   const bool pipelined = st_ecm != nullptr && !small;
+  // the resident arena's k6 tables (every slot in use has them): throughput
+  // batches on k_ecmult_k6; the small-batch kernels keep the k4 tables
+  if (kslot && !ka && !small && ctx->keys_k6 && d->kqt6 && d->gtab6 && d->keys6 >= ctx->keys) {
+    b.kqt = d->kqt6; b.kzq = d->kzq6; b.kqt2 = d->kqt62;
+    b.k6 = 1; b.gtab6 = d->gtab6;
+  }
   if (pipelined) {
     b.st_ecm = st_ecm;
     b.ecm_ready = s->ecm_ready;
@@ -1424,6 +1536,15 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* is = getenv("GV_INV_SMALL")) ctx->inv_small = strcmp(is, "0") != 0;
   if (const char* gi = getenv("GV_GFULL_ITEM")) ctx->gfull_item = strcmp(gi, "0") != 0;
   if (const char* hs = getenv("GV_H2D_SERIAL")) ctx->h2d_serial = strcmp(hs, "0") != 0;
+  if (const char* kk = getenv("GV_KEYS_K6")) ctx->keys_k6 = strcmp(kk, "0") != 0;
+  if (const char* kc = getenv("GV_KEY_CAP")) {
+    const long long v = atoll(kc);
+    if (v >= 256 && (unsigned long long)v <= kMaxItems) ctx->key_cap = (size_t)v;
+  }
+  if (const char* hb = getenv("GV_HBM_BUDGET_MB")) {
+    const long long v = atoll(hb);
+    if (v > 0) ctx->hbm_budget = (size_t)v << 20;
+  }
   ctx->stage_threads = gvstage::stage_pool_threads(host_cpus(), (int)ids.size());
   for (size_t k = 0; k < ids.size(); ++k) {
     Dev* d = new Dev();
@@ -1470,6 +1591,25 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
          gvk_gen_glat(d->glat, d->set[0].st) == hipSuccess && hipStreamSynchronize(d->set[0].st) == hipSuccess;
     if (!ok) { gv_close(ctx); return GV_EHIP; }
   }
+  // The large G tables of the default schedules (full-scalar k4 / per-item,
+  // k4's group tables, k6), enqueued on every device before waiting on any, so
+  // a node's first block does not build them (~0.5 s per device, concurrent
+  // across devices).  GV_EAGER_TABLES=0: built on first use instead.
+  const char* eager = getenv("GV_EAGER_TABLES");
+  if (!eager || strcmp(eager, "0") != 0) {
+    for (Dev* d : ctx->devs) {
+      if (hipSetDevice(d->id) != hipSuccess) { gv_close(ctx); return GV_EHIP; }
+      Set* s = &d->set[0];
+      int rc = ensure_gtab4(ctx, d, s, s->st, false);
+      if (!rc) rc = ensure_gtab6(ctx, d, s, s->st, ctx->k6 || ctx->keys_k6, false);
+      if (rc) { gv_close(ctx); return rc; }
+    }
+    for (Dev* d : ctx->devs)
+      if (hipSetDevice(d->id) != hipSuccess || hipStreamSynchronize(d->set[0].st) != hipSuccess) {
+        gv_close(ctx);
+        return GV_EHIP;
+      }
+  }
   *out = ctx;
   return GV_OK;
 }
@@ -1487,11 +1627,8 @@ void gv_close(gv_ctx* ctx) {
     if (d->gtab4) (void)hipFree(d->gtab4);
     if (d->gtab6) (void)hipFree(d->gtab6);
     if (d->gtabf) (void)hipFree(d->gtabf);
-    if (d->kqt2) (void)hipFree(d->kqt2);
-    if (d->kzq2) (void)hipFree(d->kzq2);
-    if (d->kqt) (void)hipFree(d->kqt);
-    if (d->kzq) (void)hipFree(d->kzq);
-    if (d->kok) (void)hipFree(d->kok);
+    for (uint32_t* p : {d->kqt, d->kzq, d->kok, d->kqt2, d->kzq2, d->kqt6, d->kzq6, d->kqt62, d->kzq62})
+      if (p) (void)hipFree(p);
     if (d->edtab) (void)hipFree(d->edtab);
     if (d->ed.d_in) (void)hipFree(d->ed.d_in);
     if (d->ed.atab) (void)hipFree(d->ed.atab);
@@ -1628,30 +1765,44 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
     Set* s = &d->set[0];
     hipStream_t st = s->st;
     for (hipStream_t t : d->hi_st) CK(hipStreamSynchronize(t));   // no pipelined ladder reads an arena being grown
-    int rc = ensure_keys(d, base + n, base, st);
+    if (base == 0) d->keys6 = 0;                // after gv_keys_reset the slots are rewritten from 0
+    // the k6 tables too when their G tables exist (or can be built) and the
+    // arena has room for them (else k4 only: the k4 route serves the slots)
+    int rc = ensure_gtab4(ctx, d, s, st);
+    if (!rc) rc = ensure_gtab6(ctx, d, s, st, ctx->keys_k6);
     if (rc) return rc;
-    // first keys on this device: the k4 ladder's G tables (no memory: keyed
-    // batches keep k_ecmult<true>)
-    if ((rc = ensure_gtab4(ctx, d, s, st))) return rc;
-    for (size_t c0 = 0; c0 < n; c0 += ctx->max_batch) {
-      const size_t cn = std::min(ctx->max_batch, n - c0);
+    bool k6 = ctx->keys_k6 && d->gtab6 && d->keys6 == base;
+    if ((rc = ensure_keys(d, base + n, base, st, ctx->key_cap, ctx->hbm_budget, &k6))) return rc;
+    // chunks: the k4 build takes max_batch keys at a time; the k6 build's
+    // scratch rows are twice as many per key, so its chunks are smaller
+    const size_t step = k6 ? std::min<size_t>(ctx->max_batch, 131072) : ctx->max_batch;
+    for (size_t c0 = 0; c0 < n; c0 += step) {
+      const size_t cn = std::min(step, n - c0);
       const size_t C = round_up(cn, 256);
-      // scratch: the ratio rows of the 4-lanes-per-key table build (stride 4C)
-      // start the set's Q-table region, which must then hold 4 x 135 rows
-      const size_t Cs = std::max(C, round_up((size_t)4 * (GV_QTAB_N - 1) * 9 * C / GV_QTAB_WORDS + 1, 256));
+      const size_t C4 = round_up(4 * cn, 256);
+      // scratch: the ratio rows of the 4-lanes-per-key table build (stride C4)
+      // start the set's Q-table region, then (when they fit) the forward-pass
+      // entries in coalesced rows; k6: 31 instead of 15 entries per group
+      const size_t nr4 = GV_QTAB_N - 1, nr6 = GV_K6_NT - 1, nr = k6 ? nr6 : nr4;
+      const size_t Cs = std::max(C, round_up(nr * 9 * C4 / GV_QTAB_WORDS + 1, 256));
       if ((rc = ensure_cap(s, Cs))) return rc;
       if ((rc = set_acquire(s, st))) return rc;
       CK(hipMemcpyAsync(s->d_in, pub33 + c0 * 33, cn * 33, hipMemcpyHostToDevice, st));
-      // the forward-pass entries in coalesced scratch rows after the ratio rows when they fit
-      const size_t C4 = round_up(4 * cn, 256);
-      uint32_t* qe = s->qtab + (size_t)(GV_QTAB_N - 1) * 9 * C4;
-      if (!ctx->keys_scratch || (size_t)(GV_QTAB_N - 1) * 27 * C4 > (size_t)GV_QTAB_WORDS * s->cap) qe = nullptr;
+      const size_t room = (size_t)GV_QTAB_WORDS * s->cap;
+      uint32_t* qe = ctx->keys_scratch && nr4 * 27 * C4 <= room ? s->qtab + nr4 * 9 * C4 : nullptr;
       CK(gvk_keys_build(s->d_in, (uint32_t)cn, (uint32_t)C, s->in_x, s->in_pfx, s->in_r, s->in_s, s->in_e,
                         s->qtab, qe, (uint32_t)(base + c0), d->kqt, d->kzq,
                         (uint32_t)d->kcap, d->kok, d->kqt2, d->kzq2, st));
+      if (k6) {
+        uint32_t* qe6 = ctx->keys_scratch && nr6 * 27 * C4 <= room ? s->qtab + nr6 * 9 * C4 : nullptr;
+        CK(gvk_keys_build6(s->d_in, (uint32_t)cn, (uint32_t)C, s->in_x, s->in_pfx, s->in_r, s->in_s, s->in_e,
+                           s->qtab, qe6, (uint32_t)(base + c0), d->kqt6, d->kzq6, (uint32_t)d->kcap, d->kok,
+                           d->kqt62, d->kzq62, st));
+      }
       if ((rc = set_release(s, st))) return rc;
       CK(hipStreamSynchronize(st));            // the caller's pub33 chunk is read by then
     }
+    if (k6) d->keys6 = base + n;
   }
   ctx->keys = base + n;
   for (size_t i = 0; i < n; ++i) slot_out[i] = (uint32_t)(base + i);
@@ -1981,7 +2132,7 @@ int gv_keys_point(gv_ctx* ctx, size_t n, const uint32_t* slots, uint8_t* out_xy6
   std::lock_guard<std::mutex> lk(d->mu);
   CK(hipSetDevice(d->id));
   hipStream_t st = d->set[0].st;
-  int rc = ensure_keys(d, 1, ctx->keys, st);
+  int rc = ensure_keys(d, 1, ctx->keys, st, ctx->key_cap, ctx->hbm_budget, nullptr);
   if (rc) return rc;
   uint8_t* buf = nullptr;
   const size_t sb = round_up(n * 4, 256), xb = round_up(n * 64, 256);
@@ -2097,20 +2248,27 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "ed_keyed")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->ed_keyed = val != 0;
-  } else if (!strcmp(key, "two_ladders")) {
+  } else if (!strcmp(key, "two_ladders") || !strcmp(key, "gfull") || !strcmp(key, "k6") ||
+             !strcmp(key, "keys_k6")) {
+    // schedule switches: every device lock held across the drain and the
+    // write, so no pipelined call launches on a mix of old and new state
     if (val != 0 && val != 1) return GV_EINVAL;
-    for (Dev* d : ctx->devs) {                  // no pipelined call in flight across the switch
-      std::lock_guard<std::mutex> lk(d->mu);
+    std::vector<std::unique_lock<std::mutex>> held;
+    for (Dev* d : ctx->devs) held.emplace_back(d->mu);
+    for (Dev* d : ctx->devs) {
+      CK(hipSetDevice(d->id));
       for (hipStream_t t : d->hi_st) CK(hipStreamSynchronize(t));
       d->bits_used = false;
     }
-    ctx->two_ladders = val != 0;
-  } else if (!strcmp(key, "gfull")) {
-    if (val != 0 && val != 1) return GV_EINVAL;
-    ctx->gfull = val != 0;
-  } else if (!strcmp(key, "k6")) {
-    if (val != 0 && val != 1) return GV_EINVAL;
-    ctx->k6 = val != 0;
+    bool& flag = !strcmp(key, "two_ladders") ? ctx->two_ladders : !strcmp(key, "gfull") ? ctx->gfull
+                 : !strcmp(key, "k6") ? ctx->k6 : ctx->keys_k6;
+    flag = val != 0;
+  } else if (!strcmp(key, "key_cap")) {
+    if (val < 256 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
+    ctx->key_cap = (size_t)val;
+  } else if (!strcmp(key, "hbm_budget_mb")) {
+    if (val < 0) return GV_EINVAL;
+    ctx->hbm_budget = val == 0 ? SIZE_MAX : (size_t)val << 20;
   } else if (!strcmp(key, "sort_keys")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->sort_keys = val != 0;

@@ -1,11 +1,13 @@
 """The keyed ladder's schedules must agree bit for bit: k_ecmult_k4 with the G
 half on the unsplit scalar (gv_set_option "gfull" 1, the default: 11 signed
 25-bit windows of u1 from the 2^o G tables), k_ecmult_k4 on the GLV-split G
-half (gfull 0: 14 20-bit windows) and k_ecmult_k6 (k6 1: 6-bit Q, 24-bit G
-windows, 32-entry key tables).  Each is run on the grouped route (pub33 batches
-with repeated keys), the cached-key route (gv_keys_load slots) and the message
-path, against the oracle's expected verdicts, and the route counters must show
-the schedule that ran.  The per-item route (group_keys 0: each item parses its
+half (gfull 0: 14 20-bit windows) and k_ecmult_k6 (6-bit Q windows on 32-entry
+key tables, the lambda frame, G on the unsplit u1 in 11 signed 24-bit windows
+from the 2^(36 t) G tables: "k6" 1 on the grouped route, "keys_k6" 1 -- the
+default -- on the resident key arena).  Each is run on the grouped route (pub33
+batches with repeated keys), the cached-key route (gv_keys_load slots) and the
+message path, against the oracle's expected verdicts, and the route counters
+must show the schedule that ran.  The per-item route (group_keys 0: each item parses its
 key, 26 five-bit windows over 125 doublings) runs both its G schedules too:
 "gfull_item" 1 (the default: u1's 11 25-bit windows from the same 2^o G
 tables, windows past bit 125 from the 2^45 / 2^100 / 2^145 ones) and 0 (14
@@ -23,7 +25,11 @@ pytestmark = pytest.mark.gpu
 SCHEDULES = {"k4f": {"gfull": 1, "k6": 0}, "k4": {"gfull": 0, "k6": 0}, "k6": {"gfull": 1, "k6": 1},
              "item_gf": {"group_keys": 0, "gfull_item": 1}, "item_glv": {"group_keys": 0, "gfull_item": 0}}
 ROUTE = {"k4f": "k4f", "k4": "k4", "k6": "k6", "item_gf": "item_f", "item_glv": "pub33"}
-DEFAULTS = {"gfull": 1, "k6": 0, "group_keys": 1, "gfull_item": 1}
+DEFAULTS = {"gfull": 1, "k6": 0, "group_keys": 1, "gfull_item": 1, "keys_k6": 1}
+# the cached-key route (gv_keys_load slots): k6 tables are built at load time
+# when "keys_k6" is on; the message part of the test runs the grouped route
+CACHED = {"k4f": {"gfull": 1, "keys_k6": 0, "k6": 0}, "k4": {"gfull": 0, "keys_k6": 0, "k6": 0},
+          "k6": {"gfull": 1, "keys_k6": 1, "k6": 1}}
 
 
 @pytest.fixture(scope="module")
@@ -35,8 +41,8 @@ def ver():
     v.close()
 
 
-def run(ver, sched, fn):
-    for k, val in SCHEDULES[sched].items():
+def run(ver, sched, fn, table=None):
+    for k, val in (table or SCHEDULES)[sched].items():
         ver.set_option(k, val)
     r0 = ver.route_stats()
     try:
@@ -115,8 +121,11 @@ def test_scalar_edges_on_the_full_scalar_windows(ver):
     keys = [O.pubkey(O.privkey_from_secret(b"ladder-variants-%d" % i)) for i in range(8)]
     top = sum(1 << (25 * j + 24) for j in range(10))           # every window's top bit: digits -2^24 (+carry)
     low = sum(((1 << 24) - 1) << (25 * j) for j in range(10))  # low 24 bits ones, no borrow
+    top6 = sum(1 << (24 * j + 23) for j in range(10))          # the same for k6's 24-bit windows
+    low6 = sum(((1 << 23) - 1) << (24 * j) for j in range(10))
     u1s = [0, 1, 2, N - 1, N - 2, (1 << 24), (1 << 24) - 1, (1 << 24) + 1, top % N, (top | low) % N,
-           low % N, ((1 << 256) - 1) % N, (1 << 255) % N, ((1 << 250) - 1) % N, (N - 1) >> 1]
+           low % N, ((1 << 256) - 1) % N, (1 << 255) % N, ((1 << 250) - 1) % N, (N - 1) >> 1,
+           (1 << 23), (1 << 23) - 1, (1 << 23) + 1, top6 % N, (top6 | low6) % N, low6 % N, (1 << 240) % N]
     pubs, sigs, digs = [], [], []
     for u1 in u1s:
         for qi, q in enumerate(keys):
@@ -130,7 +139,7 @@ def test_scalar_edges_on_the_full_scalar_windows(ver):
     dig = np.frombuffer(b"".join(digs), np.uint8).reshape(m, 32)
     want = O.verify_digests(pub, sig, dig, threads=16)
     assert want[0::2].all() and not want[1::2].any()
-    reps = 80                                                   # 19,200 items on 8 keys: the grouped route
+    reps = 60                                                   # 21,120 items on 8 keys: the grouped route
     pub, sig, dig = (np.tile(x, (reps, 1)) for x in (pub, sig, dig))
     exp = np.tile(want, reps)
     for sched in SCHEDULES:
@@ -139,13 +148,15 @@ def test_scalar_edges_on_the_full_scalar_windows(ver):
         assert np.array_equal(got, exp), sched
 
 
-@pytest.mark.parametrize("sched", ["k4f", "k4"])
+@pytest.mark.parametrize("sched", list(CACHED))
 def test_cached_keys_and_messages(ver, sched):
+    for k, val in CACHED[sched].items():                       # keys_k6 decides which tables the load builds
+        ver.set_option(k, val)
     ver.keys_reset()
     pub, sig, dig, exp = bench.make_digest_workload(40_000, 0x92, 300, 0.25, 16)
     uniq, inv = np.unique(pub, axis=0, return_inverse=True)
     slots = ver.keys_load(uniq)[inv.reshape(-1)].astype(np.uint32)
-    got, routes = run(ver, sched, lambda: ver.verify_batch_digests_keyed(slots, sig, dig))
+    got, routes = run(ver, sched, lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
     assert routes[sched] >= 1, routes
     assert np.array_equal(got, exp)
     mp, ms, mm, mok, _ = load_msg_vectors()
@@ -153,6 +164,38 @@ def test_cached_keys_and_messages(ver, sched):
     perm = np.random.default_rng(23).permutation(reps * len(mp))
     pub2, sig2 = np.tile(mp, (reps, 1))[perm], np.tile(ms, (reps, 1))[perm]
     msgs = [(mm * reps)[i] for i in perm]
-    got2, routes = run(ver, sched, lambda: ver.verify_batch_msgs(pub2, sig2, msgs))
+    got2, routes = run(ver, sched, lambda: ver.verify_batch_msgs(pub2, sig2, msgs), CACHED)
     assert routes[sched] >= 1, routes
     assert np.array_equal(got2, np.tile(mok, reps)[perm])
+
+
+def test_cached_keys_k6_goldens_and_slots(ver):
+    """k6 on the resident arena: the golden rejection classes loaded as keys
+    (ParsePubKey rejects get a slot too) tiled over a throughput batch,
+    out-of-range slots, a second load appended to the arena (the k6 tables of
+    both loads), all against the k4 route on the same slots"""
+    gp, gs, gd, gok, _ = load_digest_vectors()
+    ver.keys_reset()
+    half = len(gp) // 2
+    s1 = ver.keys_load(gp[:half])
+    s2 = ver.keys_load(gp[half:])                                 # appended: slots half..
+    slots_g = np.concatenate([s1, s2]).astype(np.uint32)
+    reps = 150
+    perm = np.random.default_rng(25).permutation(reps * len(gp))
+    slots = np.tile(slots_g, reps)[perm]
+    sig, dig = np.tile(gs, (reps, 1))[perm], np.tile(gd, (reps, 1))[perm]
+    exp = np.tile(gok, reps)[perm].copy()
+    bad = np.random.default_rng(26).random(len(slots)) < 0.01     # slots past the arena: never valid
+    slots[bad] = len(gp) + 7
+    exp[bad] = 0
+    got6, r6 = run(ver, "k6", lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
+    assert r6["k6"] >= 1, r6
+    assert np.array_equal(got6, exp)
+    ver.set_option("keys_k6", 0)                                  # the k4 tables of the same slots
+    try:
+        got4, r4 = run(ver, "k4f", lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
+    finally:
+        ver.set_option("keys_k6", 1)
+    assert r4["k4f"] >= 1, r4
+    assert np.array_equal(got4, got6)
+    ver.keys_reset()

@@ -54,8 +54,36 @@ def _timed_device_runs(ver, run, steps: int, warmup: int = 1):
     ver.dev_sync()
     el = time.perf_counter() - t
     cnt, unpack_ms, prep_ms, ecmult_ms = ver.stage_stats()
+    # the same launches serialized (one call at a time, no pipelining): each
+    # kernel's own duration, the denominator of a per-kernel roofline (the
+    # pipelined stage times above overlap the previous call's kernels)
+    ver.set_option("pipeline_dev", 0)
+    for _ in range(steps):
+        run()
+    ver.dev_sync()
+    _, s_unpack, s_prep, s_ecmult = ver.stage_stats()
+    ver.set_option("pipeline_dev", 1)
     ver.set_option("time_kernels", 0)
-    return el, {"unpack_or_sha_ms": round(unpack_ms, 3), "prep_ms": round(prep_ms, 3), "ecmult_ms": round(ecmult_ms, 3)}
+    return el, {"unpack_or_sha_ms": round(unpack_ms, 3), "prep_ms": round(prep_ms, 3), "ecmult_ms": round(ecmult_ms, 3),
+                "serialized": {"unpack_or_sha_ms": round(s_unpack, 3), "prep_ms": round(s_prep, 3),
+                               "ecmult_ms": round(s_ecmult, 3)},
+                "note": "stage ms of the pipelined (timed) calls overlap each other; 'serialized' is a pass of the "
+                        "same calls one at a time after the timed loop (per-kernel durations)"}
+
+
+def _item_roofline(n, stages):
+    """Per-kernel roofline of the per-item pub33 route (k_scalar_inv + k_prep,
+    k_ecmult<false, true>) from the serialized pass: W per verify counted from
+    the kernels' operations (bench.W_*), over each stage's own duration."""
+    import bench as B
+    ser = stages["serialized"]
+    w_front = B.W_INV + B.W_DECOMP + B.W_QTAB + 2 * B.NM + (2 * 64 + 68)
+    out = {}
+    for name, w, ms in (("k_scalar_inv+k_prep", w_front, ser["prep_ms"]), ("k_ecmult", B.W_LADDER_F, ser["ecmult_ms"])):
+        ach = n * w / (ms * 1e-3) if ms else 0.0
+        out[name] = {"work_per_verify": round(w), "kernel_ms": ms, "achieved_T": round(ach / 1e12, 3),
+                     "frac": round(ach / B.P_MUL_COMMITTED, 4) if ach else None}
+    return out
 
 
 def c2_hostpath(ver, pub, sig, dig, exp, steps: int = 5, device_value: float | None = None):
@@ -126,6 +154,7 @@ def c2_per_item_parse(ver, pub, sig, dig, exp, steps: int = 10):
         ver.dev_free(p)
     return {"items": n, "value": round(n * steps / el, 1), "unit": "verifies/s",
             "mismatches": int(np.count_nonzero(got != exp)), "stages": stages,
+            "roofline": _item_roofline(n, stages),
             "note": "group_keys off: the per-item pub33 pipeline on the same batch"}
 
 
@@ -145,7 +174,8 @@ def c2_unique_keys(ver, make_workload, n: int, threads: int, steps: int = 3):
     for p in d + [d_bits]:
         ver.dev_free(p)
     return {"items": n, "keys": n, "value": round(n * steps / el, 1), "unit": "verifies/s",
-            "mismatches": int(np.count_nonzero(got != exp)), "stages": stages}
+            "mismatches": int(np.count_nonzero(got != exp)), "stages": stages,
+            "roofline": _item_roofline(n, stages)}
 
 
 def c3_adversarial(ver, make_workload, n: int, threads: int, steps: int = 3):
@@ -189,26 +219,33 @@ def c2_key_cache(ver, pub, sig, dig, exp, nkeys: int, steps: int = 5):
     d_bits = ver.dev_alloc(nw * 8)
     r0 = ver.route_stats()
     el, stages = _timed_device_runs(ver, lambda: ver.dev_verify_digests_keyed(0, n, d[0], d[1], d[2], d_bits), steps)
-    k4f = ver.route_stats()["k4f"] > r0["k4f"]
+    r1 = ver.route_stats()
+    k4f = r1["k4f"] > r0["k4f"]
+    k6 = r1["k6"] > r0["k6"]
     bits = np.zeros(nw, np.uint64)
     ver.dev_download(bits, d_bits)
     got = _unpack_bits(bits, n)
     for p in d + [d_bits]:
         ver.dev_free(p)
     ver.keys_reset()
-    # k_ecmult_k4's work, counted from the kernel's operations (bench.w_ladder)
+    # the ladder's work, counted from the kernel's operations (bench.w_ladder),
+    # over its serialized launch duration
     import bench as B
-    w_k4 = round(B.W_LADDER_K4F if k4f else B.W_LADDER_K4)
-    ems = stages.get("ecmult_ms") or 0.0
-    ach = n * w_k4 / (ems * 1e-3) / 1e12 if ems else 0.0
+    w_l = round(B.W_LADDER_K6 if k6 else B.W_LADDER_K4F if k4f else B.W_LADDER_K4)
+    ems = stages["serialized"]["ecmult_ms"] or 0.0
+    ach = n * w_l / (ems * 1e-3) / 1e12 if ems else 0.0
     return {"items": n, "keys": nkeys, "value": round(n * steps / el, 1), "unit": "verifies/s",
             "keys_load_ms": round(t_load * 1e3, 2), "mismatches": int(np.count_nonzero(got != exp)),
+            "route": "k6" if k6 else "k4f" if k4f else "k4",
             "stages": stages,
-            "roofline": {"kernel": "k_ecmult_k4", "work_per_verify": w_k4, "kernel_ms": ems,
+            "roofline": {"kernel": "k_ecmult_k6" if k6 else "k_ecmult_k4", "work_per_verify": w_l, "kernel_ms": ems,
+                         "kernel_ms_source": "serialized pass (one call at a time)",
                          "achieved_T": round(ach, 3), "peak_T": round(B.P_MUL_COMMITTED / 1e12, 3),
                          "frac": round(ach * 1e12 / B.P_MUL_COMMITTED, 4)},
-            "note": "keys parsed once into the HBM key arena (Q, 2^35 Q, 2^70 Q, 2^100 Q tables on one Z: 5.4 KB "
-                    "per key); items verified by slot on the 4-group ladder (k_ecmult_k4: 30 doublings)"}
+            "note": "keys parsed once into the HBM key arena (k4: Q, 2^35 Q, 2^70 Q, 2^100 Q tables of 16 entries on "
+                    "one Z, 5.4 KB per key, read by the small-batch kernels; k6 (option keys_k6): Q, 2^36 Q, 2^72 Q, "
+                    "2^102 Q tables of 32 entries, 10.4 KB per key); items verified by slot on the 30-doubling "
+                    "ladder (k_ecmult_k6: 44 Q + 11 G additions; k_ecmult_k4: 52 + 11)"}
 
 
 def c1_items(wl, n: int, threads: int, nkeys: int = 10000):
@@ -782,3 +819,39 @@ def ed25519_small_batches(ver, wl, pub, sig, blob, off, lens, exp, threads, size
             "note": "host buffers (~350 B messages), end to end; keyed = gv_verify_ed25519_msgs_keyed after one "
                     "gv_ed_keys_load of the batch's keys (k_ed_lat_sl up to ed_lat_max = 2048), throughput = "
                     "gv_verify_ed25519_msgs (k_ed_prep + k_ed_ladder)"}
+
+
+def first_call(pub, sig, dig, exp, calls: int = 6):
+    """A node's first block on a fresh context: gv_open (which
+    builds the G tables of every default schedule on the device), then the
+    first device-resident C2 call against the next ones, each call timed alone
+    (dev_sync after it)."""
+    import gpuverify as gvm
+    t = time.perf_counter()
+    ver = gvm.Verifier([0])
+    open_ms = (time.perf_counter() - t) * 1e3
+    n = len(pub)
+    try:
+        d = [ver.dev_alloc(a.nbytes) for a in (pub, sig, dig)]
+        for p, a in zip(d, (pub, sig, dig)):
+            ver.dev_upload(p, a)
+        nw = (n + 63) // 64
+        d_bits = ver.dev_alloc(nw * 8)
+        ts = []
+        for _ in range(calls):
+            t = time.perf_counter()
+            ver.dev_verify_digests(0, n, d[0], d[1], d[2], d_bits)
+            ver.dev_sync()
+            ts.append((time.perf_counter() - t) * 1e3)
+        bits = np.zeros(nw, np.uint64)
+        ver.dev_download(bits, d_bits)
+        mm = int(np.count_nonzero(_unpack_bits(bits, n) != exp))
+        for p in d + [d_bits]:
+            ver.dev_free(p)
+    finally:
+        ver.close()
+    steady = float(np.median(ts[1:]))
+    return {"open_ms": round(open_ms, 1), "first_call_ms": round(ts[0], 3), "steady_call_ms": round(steady, 3),
+            "first_over_steady": round(ts[0] / steady, 3), "calls_ms": [round(x, 3) for x in ts], "mismatches": mm,
+            "note": "one synchronous device-resident C2 call at a time on a fresh context; the G tables are built "
+                    "by gv_open (open_ms), so the first call pays only its scratch allocation"}
