@@ -76,8 +76,9 @@ typedef struct gvk_batch {
   // keyed batches with gtab4 set take k_ecmult_k4 (30-doubling 4-group ladder)
   const uint32_t* kqt2;         // arena group tables (2^35 Q, 2^70 Q, 2^100 Q), on the slot's kzq
   const uint32_t* gtab4;        // GV_KEY2_TABLES x (G-type, lambda) tables of 2^35 G, 2^70 G, 2^100 G
-  // k6 set: kqt / kqt2 hold 32-entry group tables (k_keys_build_rows6 or the
-  // resident k6 arena) and the ladder is k_ecmult_k6 over gtab6
+  // k6 set: kqt / kqt2 hold 32-entry group tables of k6 groups (4: the grouped
+  // route, k_keys_build_rows6; GV_KN_ARENA_NG: the resident arena; kqt2 rows
+  // slot * (k6 - 1) + group - 1) and the ladder is k_ecmult_kn<k6> over gtab6
   // (GV_K6_GTAB_WORDS: the full-scalar 24-bit-window G tables); gtab4 unused
   const uint32_t* gtab6;
   int k6;
@@ -121,25 +122,31 @@ hipError_t gvk_unsort_bits(uint32_t n, const uint32_t* pos, const uint64_t* sbit
 #define GV_KEY2_TABLES (GV_LGRP - 1)
 #define GV_GLAT_WORDS (GV_LGRP * 2 * GV_QTAB_N * 16)
 
-// The 6-bit-window keyed ladder (k_ecmult_k6): the key tables hold 32
-// multiples per group (6-bit signed windows: 22 per 128-bit GLV half, groups
-// starting at windows 0, 6, 12, 17 = bit offsets 0, 36, 72, 102; 6 positions,
-// 30 doublings, 44 Q additions), the lambda frame of k_ecmult_k4 (two beta
-// products per position), and G on the unsplit u1 = e/s: 11 signed 24-bit
-// windows (window j at bit 24 j) added from 2^23-entry tables of 2^o G for
-// the seven offsets o = 36 t (3.5 GiB per device): window j at ladder
-// position p (bit 6 p of the 36-bit group ladder) reads the table of offset
-// 24 j - 6 p (gv_kernels.hip kK6GWin).  Key tables: the resident arena
-// (gv_keys_load, option "keys_k6") and the grouped route's per-batch arena.
+// The 6-bit-window keyed ladders (k_ecmult_kn<NG>): the key tables hold 32
+// multiples per group (6-bit signed windows: 22 per 128-bit GLV half), the
+// 22 windows split into NG groups -- the first R = 22 - (P - 1) NG groups of
+// P = ceil(22 / NG) windows, the rest of P - 1 -- each with its own table of
+// 2^(6 w0) Q on ONE shared Z, so the ladder runs P positions: 6 (P - 1)
+// doublings and 44 Q additions.  NG = 4 ("k6": groups at windows 0, 6, 12,
+// 17, 30 doublings; the grouped route's per-batch tables) and the resident
+// arena's NG = GV_KN_ARENA_NG (more groups: fewer doublings per verify, more
+// table memory per key, built once at gv_keys_load).  The lambda-Q entries go
+// through the lambda frame (two beta products per position), and G is taken
+// on the unsplit u1 = e/s: 11 signed 24-bit windows (window j at bit 24 j)
+// added after the last doubling from 2^23-entry tables of 2^(24 j) G
+// (5.5 GiB per device).  Group layout: gv_kernels.hip KLayout.
 #define GV_K6_QW 6
 #define GV_K6_NT 32                                       // table entries per group
 #define GV_K6_QWIN 22
 #define GV_K6_GW 24
 #define GV_K6_GWIN 11
-#define GV_K6_GNTAB 7
+#define GV_K6_GNTAB GV_K6_GWIN                            // one G table per window
 #define GV_K6_GTAB_N (1u << (GV_K6_GW - 1))
 #define GV_K6_KEY_WORDS (GV_K6_NT * GV_QENT_WORDS)       // one group table (2,560 B)
 #define GV_K6_GTAB_WORDS ((size_t)GV_K6_GNTAB * GV_K6_GTAB_N * 16)
+#ifndef GV_KN_ARENA_NG
+#define GV_KN_ARENA_NG 11                                 // resident arena: 11 groups of 2 windows, 6 doublings
+#endif
 static_assert(GV_K6_QWIN + GV_K6_GWIN <= GV_DIGIT_ROWS, "k6 digits fit the digit rows");
 static_assert(GV_K6_QW * GV_K6_QWIN >= 130 && GV_K6_GW * GV_K6_GWIN >= 257, "k6 windows cover the scalars");
 
@@ -261,22 +268,28 @@ hipError_t gvk_gen_gtable4(uint32_t* gtab4, uint32_t* base_scratch, hipStream_t 
 hipError_t gvk_gen_glat(uint32_t* glat, hipStream_t st);
 // the k6 ladder's G tables (GV_K6_GTAB_WORDS words); base_scratch: 112 words
 hipError_t gvk_gen_gtable6(uint32_t* gtab6, uint32_t* base_scratch, hipStream_t st);
-// k6 key tables of n keys (device pub33) into resident-arena slots
-// base..base+n-1 (rows of kqt6: GV_K6_KEY_WORDS, kqt62: 3 per slot); scratch
-// as gvk_keys_build with qr / qe rows of (GV_K6_NT - 1) * 9 / * 18.
+// The resident arena's k6 tables (GV_KN_ARENA_NG groups of 32 entries) of n
+// keys (device pub33) into slots base..base+n-1 (rows of kqt6:
+// GV_K6_KEY_WORDS, kqt62: GV_KN_ARENA_NG - 1 per slot, kzq62:
+// (GV_KN_ARENA_NG - 1) x 8 rows); scratch as gvk_keys_build.
 hipError_t gvk_keys_build6(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
-                           uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t* qe, uint32_t base,
-                           uint32_t* kqt6, uint32_t* kzq6, uint32_t kC, uint32_t* kok, uint32_t* kqt62,
+                           uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* scratch, int with_qe,
+                           uint32_t base, uint32_t* kqt6, uint32_t* kzq6, uint32_t kC, uint32_t* kok, uint32_t* kqt62,
                            uint32_t* kzq62, hipStream_t st);
 // the full-scalar G tables (GV_GF_WORDS words); base_scratch: 96 words
 hipError_t gvk_gen_gtablef(uint32_t* gtabf, uint32_t* base_scratch, hipStream_t st);
-// k6 key tables (32 entries per group) of n keys already unpacked into rows
-// in_x / in_pfx (stride C), slots 0..n-1; qr: (GV_K6_NT - 1) * 9 ratio rows of
-// stride round_up(4 n, 256), qe (may be null): (GV_K6_NT - 1) * 18 rows of the
-// same stride.  kqt: n x GV_K6_KEY_WORDS, kqt2: 3 n x GV_K6_KEY_WORDS.
-hipError_t gvk_keys_build_rows6(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx, uint32_t* qr,
-                                uint32_t* qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok,
-                                uint32_t* kqt2, uint32_t* kzq2, hipStream_t st);
+// Key-table builds (k_keys_chain + k_keys_fwd + k_keys_back): scratch of
+// gvk_keys_scratch_words(n, groups, entries, with_qe) words -- the ratio rows,
+// the E rows and (with_qe) the forward entries, all of stride
+// gvk_keys_lanes(n, groups) = round_up(groups * n, 256).
+uint32_t gvk_keys_lanes(uint32_t n, int ng);
+size_t gvk_keys_scratch_words(uint32_t n, int ng, int nt, int with_qe);
+// k6 key tables (4 groups of 32 entries) of n keys already unpacked into rows
+// in_x / in_pfx (stride C), slots 0..n-1.  kqt: n x GV_K6_KEY_WORDS, kqt2:
+// 3 n x GV_K6_KEY_WORDS.
+hipError_t gvk_keys_build_rows6(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx,
+                                uint32_t* scratch, int with_qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC,
+                                uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2, hipStream_t st);
 hipError_t gvk_verify_lat(const gvk_lat* b, hipStream_t st);
 hipError_t gvk_verify_lat16(const gvk_lat* b, hipStream_t st);
 hipError_t gvk_verify_lat_sl(const gvk_lat* b, hipStream_t st);
@@ -293,19 +306,18 @@ hipError_t gvk_unpack(const uint8_t* pub33, const uint8_t* sig64, const uint8_t*
 hipError_t gvk_dedupe(uint32_t n, uint32_t C, const uint32_t* x, const uint32_t* pfx, uint32_t* table, uint32_t tslots,
                       uint32_t* rep, uint32_t* uid, uint32_t* count, uint32_t* kslot, uint32_t capU, uint32_t CU,
                       uint32_t* kx, uint32_t* kpfx, hipStream_t st);
-// The key tables (k_keys_chain, k_keys_tables) of n keys already unpacked into
-// rows in_x / in_pfx (stride C), slots 0..n-1; qr: (GV_QTAB_N - 1) * 9 ratio
-// rows of stride round_up(4 n, 256).
-hipError_t gvk_keys_build_rows(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx, uint32_t* qr,
-                               uint32_t* qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2,
-                               uint32_t* kzq2, hipStream_t st);
-// Parse n keys (device pub33) into arena slots base..base+n-1.  Scratch: the
-// batch rows in_x, in_pfx (and r, s, e as k_unpack targets) of stride C and
-// qr (GV_QTAB_N - 1) * 9 rows of stride round_up(4 n, 256).
+// The k4 key tables (4 groups of 16 entries) of n keys already unpacked into
+// rows in_x / in_pfx (stride C), slots 0..n-1 (scratch: gvk_keys_scratch_words).
+hipError_t gvk_keys_build_rows(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx,
+                               uint32_t* scratch, int with_qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC,
+                               uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2, hipStream_t st);
+// Parse n keys (device pub33) into arena slots base..base+n-1 (k4 tables).
+// Scratch: the batch rows in_x, in_pfx (and r, s, e as k_unpack targets) of
+// stride C and gvk_keys_scratch_words(n, 4, GV_QTAB_N, with_qe) words.
 hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
-                          uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t* qe, uint32_t base,
-                          uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2,
-                          hipStream_t st);
+                          uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* scratch, int with_qe,
+                          uint32_t base, uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2,
+                          uint32_t* kzq2, hipStream_t st);
 hipError_t gvk_keys_point(uint32_t n, const uint32_t* slots, const uint32_t* kqt, const uint32_t* kzq, uint32_t kC,
                           const uint32_t* kok, uint32_t kcount, uint8_t* out_xy, uint8_t* out_ok, hipStream_t st);
 hipError_t gvk_debug(int op, uint32_t n, const uint32_t* in, uint32_t* out, hipStream_t st);

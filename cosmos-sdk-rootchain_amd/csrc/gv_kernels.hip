@@ -735,7 +735,30 @@ __global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u
 // rows of stride C.
 // Window-group start bits of the keyed latency schedule (GV_LGRP groups).
 __constant__ const int kLGrpBit[GV_LGRP] = {0, 35, 70, 100};
-__constant__ const int kK6GrpBit[GV_LGRP] = {0, 6 * GV_K6_QW, 12 * GV_K6_QW, 17 * GV_K6_QW};   // 0, 36, 72, 102
+
+// Group layout of the keyed throughput ladders (gv_kernels.h): QWIN signed
+// QW-bit windows per 128-bit GLV half split into NG groups -- the first R of
+// P = ceil(QWIN / NG) windows, the rest of P - 1 -- group k starting at window
+// w0(k), i.e. its table is that of 2^(QW w0(k)) Q; the ladder runs P
+// positions.  <5, 4>: k_ecmult_k4 (groups at bits 0, 35, 70, 100); <6, 4>:
+// the grouped route's k6 (0, 36, 72, 102); <6, GV_KN_ARENA_NG>: the resident
+// arena.
+template <int QW, int NG>
+struct KLayout {
+  static constexpr int QWIN = QW == GV_QW ? GV_QWIN : GV_K6_QWIN;
+  static constexpr int NT = 1 << (QW - 1);                  // table entries per group
+  static constexpr int P = (QWIN + NG - 1) / NG;            // ladder positions
+  static constexpr int R = QWIN - (P - 1) * NG;             // groups with P windows
+  static constexpr int nw(int k) { return k < R ? P : P - 1; }
+  static constexpr int w0(int k) { return k * P - (k > R ? k - R : 0); }
+  static constexpr int bit(int k) { return QW * w0(k); }
+};
+static_assert(KLayout<5, 4>::bit(1) == 35 && KLayout<5, 4>::bit(2) == 70 && KLayout<5, 4>::bit(3) == 100 &&
+              KLayout<5, 4>::P == 7, "k4 groups");
+static_assert(KLayout<6, 4>::bit(1) == 36 && KLayout<6, 4>::bit(2) == 72 && KLayout<6, 4>::bit(3) == 102 &&
+              KLayout<6, 4>::P == 6, "k6 groups");
+static_assert(KLayout<6, GV_KN_ARENA_NG>::w0(GV_KN_ARENA_NG - 1) + KLayout<6, GV_KN_ARENA_NG>::nw(GV_KN_ARENA_NG - 1) ==
+              GV_K6_QWIN, "arena groups cover the windows");
 
 // Affine x, y (8 x 32 words) of a finite Jacobian point.
 GV_DEV void gej29_to_affine_words(fe& x8, fe& y8, const gej29& p) {
@@ -749,20 +772,19 @@ GV_DEV void gej29_to_affine_words(fe& x8, fe& y8, const gej29& p) {
   f29_to_words(y8.v, y);
 }
 
-// The key arena's tables are built in two launches so that the long serial
-// part runs one lane per key and the rest four lanes per key:
+// The keyed ladders' tables are built in three launches so that the long
+// serial part runs one lane per key and the rest one lane per (key, group):
 //
 // k_keys_chain (lane = key): ParsePubKey (a rejected key gets G's tables,
-// never used: every item against it is false), then 100 doublings to
-// 2^35 Q, 2^70 Q, 2^100 Q.  Each group's base point is parked, as canonical
-// words x[8] y[8], in entry 0 of its own table row; the Jacobian Z of groups
-// 1..3 in their Z rows (kzq2), group 0 is affine.
-// K6: the k6 group offsets (kK6GrpBit) and 32-entry table rows.
-template <bool K6 = false>
+// never used: every item against it is false), then the doublings to each
+// group's base 2^bit(k) Q (100 for k4).  Each group's base point is parked, as
+// canonical words x[8] y[8], in entry 0 of its own table row (group 0 in kqt,
+// groups 1.. in kqt2 rows slot * (NG - 1) + k - 1); the Jacobian Z of groups
+// 1.. in their Z rows (kzq2, (NG - 1) x 8 rows of stride kC), group 0 is affine.
+template <int QW, int NG>
 __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_chain(u32 n, u32 C, const u32* in_x, const u32* in_pfx, u32 base,
                                                      u32* kqt, u32 kC, u32* kok, u32* kqt2, u32* kzq2) {
-  constexpr int NT = K6 ? GV_K6_NT : GV_QTAB_N;
-  const int* grp_bit = K6 ? kK6GrpBit : kLGrpBit;
+  using L = KLayout<QW, NG>;
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n) return;                       // no cross-lane work
   fe x, y;
@@ -774,7 +796,7 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_chain(u32 n, u32 C, 
   }
   kok[base + g] = ok ? 1u : 0u;
   auto park = [](u32* tab, u32 row, const u32* xw, const u32* yw) {
-    u32* p = tab + (size_t)row * NT * GV_QENT_WORDS;
+    u32* p = tab + (size_t)row * L::NT * GV_QENT_WORDS;
 #pragma unroll
     for (int i = 0; i < 8; ++i) { p[i] = xw[i]; p[8 + i] = yw[i]; }
   };
@@ -784,13 +806,13 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_chain(u32 n, u32 C, 
   f29_from_words(q.y, y.v);
   f29_set_u32(q.z, 1);
 #pragma unroll 1
-  for (int grp = 1; grp < GV_LGRP; ++grp) {
+  for (int grp = 1; grp < NG; ++grp) {
 #pragma unroll 1
-    for (int k = grp_bit[grp - 1]; k < grp_bit[grp]; ++k) gej29x_double(q, q);  // never infinite: odd order
+    for (int k = L::bit(grp - 1); k < L::bit(grp); ++k) gej29x_double(q, q);  // never infinite: odd order
     u32 xw[8], yw[8];
     f29_to_words(xw, q.x);
     f29_to_words(yw, q.y);
-    park(kqt2, (base + g) * GV_KEY2_TABLES + (grp - 1), xw, yw);
+    park(kqt2, (base + g) * (NG - 1) + (grp - 1), xw, yw);
     store_f29(kzq2 + (size_t)(grp - 1) * 8 * kC, kC, base + g, q.z);
   }
 }
@@ -810,10 +832,11 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_chain(u32 n, u32 C, 
 // coalesced, so each table entry is written once, by the back-propagation
 // (null: the entries go through the table itself: lanes 1,280 B apart write
 // 80 B each, twice, and read them back in between).
-// NT: entries per group table (16; GV_K6_NT for the k6 tables).
-template <int NT = GV_QTAB_N>
+// QW: 5 (k4, 16 entries per table) or 6 (the grouped route's k6, 32 entries).
+template <int QW>
 __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_tables(u32 n, u32 C4, u32 base, u32* kqt, u32* kzq, u32 kC, u32* kqt2,
                                                       u32* kzq2, u32* qr, u32* qe) {
+  constexpr int NT = KLayout<QW, 4>::NT;
   const u32 L = blockIdx.x * blockDim.x + threadIdx.x;
   const u32 key = L >> 2, grp = L & 3u;
   if (key >= n) return;                     // whole quads only: shuffles stay inside live quads
@@ -944,6 +967,165 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_tables(u32 n, u32 C4
   store_f29(zrow, kC, base + key, zc);
 }
 
+
+// k_keys_fwd (lane L = NG key + group): the group's table from its parked base
+// point (X, Y) taken as affine -- the co-Z formulas never read the curve
+// constant, so this is the table of the point on the isomorphic curve
+// y^2 = x^3 + 7 Z^6, i.e. of the true point on table Z  E = Z_last * Z.
+// Forward pass only (co-Z doubling, then NT - 2 co-Z additions, Meloni's
+// ZADDU: (Q', mQ) -> ((m+1) Q, Q'') for 4M + 2S, the new Z never formed --
+// only the ratio X1 - X2 is kept): entry m - 1 (= m Q) lands on Z_{m-1}; the
+// ratios go to the SoA rows qr (stride CL), the entries to the coalesced rows
+// qe (or, qe null, the table itself: lanes a row apart writing 80 B each), E
+// to the rows er.  No exceptional case: X(Q') == X(mQ) would need
+// mQ == +-Q, i.e. n | m -+ 1, for 2 <= m <= NT - 1.
+template <int QW, int NG>
+GV_DEV void keys_put(u32* qe, u32 CL, u32 L, u32* tab, u32 row, int e, const fe29& x, const fe29& y) {
+  if (qe) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      qe[((size_t)e * 18 + i) * CL + L] = x.n[i];
+      qe[((size_t)e * 18 + 9 + i) * CL + L] = y.n[i];
+    }
+  } else {
+    store_qent29<KLayout<QW, NG>::NT>(tab, row, e, x, y);
+  }
+}
+template <int QW, int NG>
+GV_DEV void keys_get(const u32* qe, u32 CL, u32 L, const u32* tab, u32 row, int e, fe29& x, fe29& y) {
+  if (qe) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      x.n[i] = qe[((size_t)e * 18 + i) * CL + L];
+      y.n[i] = qe[((size_t)e * 18 + 9 + i) * CL + L];
+    }
+  } else {
+    load_qent29<KLayout<QW, NG>::NT>(x, y, tab, row, (u32)e);
+  }
+}
+
+template <int QW, int NG>
+__global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_fwd(u32 n, u32 CL, u32 base, u32* kqt, u32 kC, u32* kqt2,
+                                                   const u32* kzq2, u32* qr, u32* qe, u32* er) {
+  constexpr int NT = KLayout<QW, NG>::NT;
+  const u32 L = blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 key = L / NG, grp = L % NG;
+  if (key >= n) return;
+  u32* tab = grp == 0u ? kqt : kqt2;
+  const u32 row = grp == 0u ? base + key : (base + key) * (NG - 1) + (grp - 1u);
+  fe29 qx, qy, X1, Y1, X2, Y2, t, u, prod;
+  {
+    const u32* p = tab + (size_t)row * NT * GV_QENT_WORDS;
+    u32 w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = p[i];
+    f29_from_words(qx, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = p[8 + i];
+    f29_from_words(qy, w);
+  }
+  {
+    // co-Z doubling of (qx, qy): Z1 = 2y, 2Q = (M^2 - 2S, M(S - X) - 8y^4),
+    // Q' = (S, 8y^4) with S = 4xy^2, M = 3x^2.
+    fe29 B, E, Lq, M;
+    f29x_sqr(B, qx);
+    f29x_sqr(E, qy);
+    f29x_sqr(Lq, E);
+    f29_add(t, qx, E);
+    f29x_sqr(t, t);
+    f29_sub<1>(t, t, B);
+    f29_sub_norm<1>(t, t, Lq);
+    f29_shl_norm<1>(X1, t);
+    f29_mul3_norm(M, B);
+    f29x_sqr(t, M);
+    f29_add(u, X1, X1);
+    f29_sub_norm<2>(X2, t, u);
+    f29_shl_norm<3>(Y1, Lq);
+    f29_sub<1>(t, X1, X2);
+    f29x_mul(t, M, t);
+    f29_sub_norm<1>(Y2, t, Y1);
+  }
+  keys_put<QW, NG>(qe, CL, L, tab, row, 0, X1, Y1);    // 1*Q on Z1
+  keys_put<QW, NG>(qe, CL, L, tab, row, 1, X2, Y2);    // 2*Q on Z1
+  f29_add(prod, qy, qy);                                 // Z1 = 2y; times every ratio below -> Z_last
+#pragma unroll 1
+  for (int m = 2; m < NT; ++m) {                         // (Q', mQ) -> ((m+1)Q, Q'')
+    fe29 h, rr, c, w1, w2, d, a1;
+    f29_sub_norm<1>(h, X1, X2);
+    store_ratio29(qr, CL, L, m - 2, h);                  // Z_m / Z_{m-1}
+    f29x_mul(prod, prod, h);
+    f29_sub_norm<1>(rr, Y1, Y2);
+    f29x_sqr(c, h);
+    f29x_mul(w1, X1, c);
+    f29x_mul(w2, X2, c);
+    f29x_sqr(d, rr);
+    f29_sub<1>(t, w1, w2);
+    f29x_mul(a1, Y1, t);
+    f29_add(u, w1, w2);
+    f29_sub_norm<2>(X2, d, u);
+    f29_sub<1>(t, w1, X2);
+    f29x_mul(t, rr, t);
+    f29_sub_norm<1>(Y2, t, a1);
+    X1 = w1;
+    Y1 = a1;
+    keys_put<QW, NG>(qe, CL, L, tab, row, m, X2, Y2);    // (m+1)*Q on Z_m
+  }
+  // E = Z_last (times the parked Jacobian Z for groups 1..)
+  if (grp) {
+    fe29 z;
+    load_f29(z, kzq2 + (size_t)(grp - 1u) * 8 * kC, kC, base + key);
+    f29x_mul(prod, prod, z);
+  }
+  store_ratio29(er, CL, L, 0, prod);
+}
+
+// k_keys_back (lane L = NG key + group): rho = the product of the OTHER
+// groups' E (read from er), so every table lands on the key's common Z =
+// E_0 ... E_{NG-1} -- ONE accumulator takes entries of every group, with no
+// inversion -- then the back-propagation: entry m - 1 (on Z_{m-1}) times
+// (rho Z_last / Z_{m-1})^2 and ^3, each table entry written once.
+template <int QW, int NG>
+__global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_back(u32 n, u32 CL, u32 base, u32* kqt, u32* kzq, u32 kC,
+                                                    u32* kqt2, u32* kzq2, const u32* qr, const u32* qe,
+                                                    const u32* er) {
+  constexpr int NT = KLayout<QW, NG>::NT;
+  const u32 L = blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 key = L / NG, grp = L % NG;
+  if (key >= n) return;
+  u32* tab = grp == 0u ? kqt : kqt2;
+  const u32 row = grp == 0u ? base + key : (base + key) * (NG - 1) + (grp - 1u);
+  u32* zrow = grp == 0u ? kzq : kzq2 + (size_t)(grp - 1u) * 8 * kC;
+  fe29 acc, zc, own;
+  bool first = true;
+#pragma unroll 1
+  for (u32 j = 0; j < (u32)NG; ++j) {
+    fe29 e;
+    load_ratio29(e, er, CL, key * NG + j, 0);
+    if (j == grp) { own = e; continue; }
+    if (first) acc = e;
+    else f29x_mul(acc, acc, e);
+    first = false;
+  }
+  f29x_mul(zc, acc, own);                                // the common Z
+  // entry m - 1 on Z_{m-1} (m >= 2; entries 1, 2 on Z_1): times rho Z_last / Z_{m-1}
+#pragma unroll 1
+  for (int m = NT; m >= 1; --m) {
+    if (m >= 2 && m < NT) {
+      fe29 ratio;
+      load_ratio29(ratio, qr, CL, L, m - 2);
+      f29x_mul(acc, acc, ratio);
+    }
+    fe29 x, y, a2, a3;
+    f29x_sqr(a2, acc);
+    f29x_mul(a3, a2, acc);
+    keys_get<QW, NG>(qe, CL, L, tab, row, m - 1, x, y);
+    f29x_mul(x, x, a2);
+    f29x_mul(y, y, a3);
+    store_qent29<NT>(tab, row, m - 1, x, y);
+  }
+  store_f29(zrow, kC, base + key, zc);
+}
+
 // Affine 2^35 G, 2^70 G, 2^100 G (16 words each) for the keyed ladder's G
 // tables; thread t = group - 1.  Once per device.
 __global__ void k_gen_gbase(u32* out) {
@@ -965,13 +1147,13 @@ __global__ void k_gen_gbase(u32* out) {
 }
 
 // Affine 2^o G (16 words each) for the full-scalar G tables' offsets o =
-// kGFOff[t] (K6: the k6 ladder's tables, o = 36 t).
+// kGFOff[t] (K6: the 6-bit-window ladders' tables, o = 24 t).
 __constant__ const int kGFOff[GV_GF_NTAB] = {0, 45, 100, 145, 195, 220};
 template <bool K6 = false>
 __global__ void k_gen_gbasef(u32* out) {
   const int t = threadIdx.x;
   if (t >= (K6 ? GV_K6_GNTAB : GV_GF_NTAB)) return;
-  const int off = K6 ? 6 * GV_K6_QW * t : kGFOff[t];
+  const int off = K6 ? GV_K6_GW * t : kGFOff[t];
   fe gx, gy;
   fe_from_const(gx, kGx);
   fe_from_const(gy, kGy);
@@ -1391,31 +1573,47 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gta
   ecmult_finish(acc, inf, zq, flags, in_r, bits, n, C, g);
 }
 
-// ------------------------------------------------------------- k_ecmult_k6
-// The 6-bit-window keyed ladder (gv_kernels.h GV_K6_*): the key tables hold
-// 32 multiples per group, so each 128-bit GLV half takes 22 six-bit windows,
-// split into the groups [0,6), [6,12), [12,17), [17,22) (bit offsets 0, 36,
-// 72, 102); window w of group k is added at local position w - w0(k) of a
-// 36-bit ladder: 5 x 6 = 30 doublings and 44 Q additions (52 with 5-bit
-// windows).  The lambda-Q entries go through the lambda frame of
-// k_ecmult_k4 (two beta products per position).  G on the unsplit u1: its 11
-// signed 24-bit windows (window j at bit 24 j) from the 2^23-entry tables of
-// 2^o G, o = 36 t: window j at position p reads the table of offset
-// 24 j - 6 p -- positions 0, 2, 4 take windows {0, 3, 6, 9}, {2, 5, 8},
-// {1, 4, 7, 10} from the tables of offsets {0, 72, 144, 216},
-// {36, 108, 180}, {0, 72, 144, 216}.  Same additions, final check and
-// semantics as k_ecmult_k4 otherwise.
-__constant__ const int kK6WStart[4] = {0, 6, 12, 17};
-__constant__ const int kK6NWin[4] = {6, 6, 5, 5};
-// G windows at each position (up to four) and the table each reads (o / 36)
-__constant__ const int kK6GWin[6][4] = {{0, 3, 6, 9}, {-1, -1, -1, -1}, {2, 5, 8, -1},
-                                        {-1, -1, -1, -1}, {1, 4, 7, 10}, {-1, -1, -1, -1}};
-__constant__ const int kK6GTab[GV_K6_GWIN] = {0, 0, 1, 2, 2, 3, 4, 4, 5, 6, 6};
+// ------------------------------------------------------------- k_ecmult_kn
+// The 6-bit-window keyed ladders (gv_kernels.h GV_K6_*, KLayout<6, NG>): the
+// key tables hold 32 multiples per group, so each 128-bit GLV half takes 22
+// six-bit windows, split into NG groups; window w of group k is added at
+// local position w - w0(k) of a P-position ladder: 6 (P - 1) doublings
+// (NG = 4: 30; the resident arena's NG = 11: 6) and 44 Q additions (52 with
+// 5-bit windows).  At each position the Q entries of groups 0.. go first,
+// then the accumulator moves to lambda^2 (x -> beta^2 x), takes the
+// lambda-Q entries of groups ..0 as plain (x, y) -- lambda^2 A + T =
+// lambda^2 (A + lambda T) since lambda^3 = 1 -- and moves back (x -> beta x):
+// two beta products per position.  G on the unsplit u1: its 11 signed 24-bit
+// windows (window j at bit 24 j) are added after the last doubling from the
+// 2^23-entry tables of 2^(24 j) G.  Same additions, final check and semantics
+// as k_ecmult_k4 otherwise (lambda is a group automorphism, so every
+// exceptional case -- H == 0 -- meets the same points).
+// The group layout as constant tables (row 0: NG = 4, row 1: the arena's NG)
+// -- indexing them keeps the ladder's register allocation at that of k4
+__constant__ const int kKnW0[2][16] = {
+    {KLayout<6, 4>::w0(0), KLayout<6, 4>::w0(1), KLayout<6, 4>::w0(2), KLayout<6, 4>::w0(3)},
+    {KLayout<6, GV_KN_ARENA_NG>::w0(0), KLayout<6, GV_KN_ARENA_NG>::w0(1), KLayout<6, GV_KN_ARENA_NG>::w0(2),
+     KLayout<6, GV_KN_ARENA_NG>::w0(3), KLayout<6, GV_KN_ARENA_NG>::w0(4), KLayout<6, GV_KN_ARENA_NG>::w0(5),
+     KLayout<6, GV_KN_ARENA_NG>::w0(6), KLayout<6, GV_KN_ARENA_NG>::w0(7), KLayout<6, GV_KN_ARENA_NG>::w0(8),
+     KLayout<6, GV_KN_ARENA_NG>::w0(9), KLayout<6, GV_KN_ARENA_NG>::w0(10), KLayout<6, GV_KN_ARENA_NG>::w0(11),
+     KLayout<6, GV_KN_ARENA_NG>::w0(12), KLayout<6, GV_KN_ARENA_NG>::w0(13), KLayout<6, GV_KN_ARENA_NG>::w0(14),
+     KLayout<6, GV_KN_ARENA_NG>::w0(15)}};
+__constant__ const int kKnNW[2][16] = {
+    {KLayout<6, 4>::nw(0), KLayout<6, 4>::nw(1), KLayout<6, 4>::nw(2), KLayout<6, 4>::nw(3)},
+    {KLayout<6, GV_KN_ARENA_NG>::nw(0), KLayout<6, GV_KN_ARENA_NG>::nw(1), KLayout<6, GV_KN_ARENA_NG>::nw(2),
+     KLayout<6, GV_KN_ARENA_NG>::nw(3), KLayout<6, GV_KN_ARENA_NG>::nw(4), KLayout<6, GV_KN_ARENA_NG>::nw(5),
+     KLayout<6, GV_KN_ARENA_NG>::nw(6), KLayout<6, GV_KN_ARENA_NG>::nw(7), KLayout<6, GV_KN_ARENA_NG>::nw(8),
+     KLayout<6, GV_KN_ARENA_NG>::nw(9), KLayout<6, GV_KN_ARENA_NG>::nw(10), KLayout<6, GV_KN_ARENA_NG>::nw(11),
+     KLayout<6, GV_KN_ARENA_NG>::nw(12), KLayout<6, GV_KN_ARENA_NG>::nw(13), KLayout<6, GV_KN_ARENA_NG>::nw(14),
+     KLayout<6, GV_KN_ARENA_NG>::nw(15)}};
+static_assert(GV_KN_ARENA_NG <= 16, "layout table rows");
 
-__global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k6(const u32* gtab6, u32 n, u32 C, const u32* digits,
+template <int NG>
+__global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_kn(const u32* gtab6, u32 n, u32 C, const u32* digits,
                                                         const u32* kqt, const u32* kqt2, const u32* kzq,
                                                         const u32* flags, const u32* in_r, uint64_t* bits,
                                                         const u32* qidx, u32 kC) {
+  using L = KLayout<GV_K6_QW, NG>;
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   const u32 qi = qidx[g];
   fe29 zq;
@@ -1424,37 +1622,38 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k6(const u32* gta
   f29_set_zero(acc.x); f29_set_zero(acc.y); f29_set_zero(acc.z);
   bool inf = true;
 #pragma unroll 1
-  for (int pos = 5; pos >= 0; --pos) {
-    if (pos != 5) {
+  for (int pos = L::P - 1; pos >= 0; --pos) {
+    if (pos != L::P - 1) {
 #pragma unroll 1
       for (int d = 0; d < GV_K6_QW; ++d) gej29x_double(acc, acc);
     }
-    // slots 0..3: Q of groups 0..3; 4..7: lambda Q of groups 3..0 on the
-    // lambda^2 frame; 8..11: up to four G windows
+    // slots 0..NG-1: Q of groups 0..NG-1; NG..2NG-1: lambda Q of groups
+    // NG-1..0 on the lambda^2 frame; then (position 0) the 11 G windows
 #pragma unroll 1
-    for (int slot = 0; slot < 12; ++slot) {
-      if ((slot == 4 || slot == 8) && !inf) {
+    for (int slot = 0; slot < 2 * NG + GV_K6_GWIN; ++slot) {
+      if ((slot == NG || slot == 2 * NG) && !inf) {
         fe29 c;                                            // into lambda^2 (acc) / back to acc
-        f29_from_const(c, slot == 4 ? kBeta2 : kBeta);
+        f29_from_const(c, slot == NG ? kBeta2 : kBeta);
         f29x_mul(acc.x, acc.x, c);
       }
+      if (slot >= 2 * NG && pos != 0) break;               // wave-uniform: G after the last doubling
       int d;
       const u32* tab;
       u32 row = 0;
-      const bool isg = slot >= 8;
+      const bool isg = slot >= 2 * NG;
       if (!isg) {
-        const bool lam = slot >= 4;
-        const int grp = lam ? 7 - slot : slot;
-        if (pos >= kK6NWin[grp]) continue;                 // wave-uniform
-        const u32 dq = digits[(size_t)(kK6WStart[grp] + pos) * C + g];
+        const bool lam = slot >= NG;
+        const int grp = lam ? 2 * NG - 1 - slot : slot;
+        constexpr int T = NG == 4 ? 0 : 1;
+        if (pos >= kKnNW[T][grp]) continue;                // wave-uniform
+        const u32 dq = digits[(size_t)(kKnW0[T][grp] + pos) * C + g];
         d = lam ? ((int)dq >> 16) : ((int)(dq << 16) >> 16);
         tab = grp == 0 ? kqt : kqt2;
-        row = grp == 0 ? qi : qi * GV_KEY2_TABLES + (grp - 1);
+        row = grp == 0 ? qi : qi * (NG - 1) + (grp - 1);
       } else {
-        const int j = kK6GWin[pos][slot - 8];
-        if (j < 0) continue;                               // wave-uniform
+        const int j = slot - 2 * NG;
         d = (int)digits[(size_t)(GV_K6_QWIN + j) * C + g];
-        tab = gtab6 + (size_t)kK6GTab[j] * GV_K6_GTAB_N * 16;
+        tab = gtab6 + (size_t)j * GV_K6_GTAB_N * 16;
       }
       if (d == 0) continue;
       const u32 e = (u32)((d < 0 ? -d : d) - 1);
@@ -1668,8 +1867,11 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   }
   if (b->ev_ecm_start) (void)hipEventRecord(b->ev_ecm_start, se);
   if (b->bits_wait && !sorted) (void)hipStreamWaitEvent(se, b->bits_wait, 0);   // the ladder writes the bits
-  if (k6)
-    hipLaunchKernelGGL(gv::k_ecmult_k6, grd, blk, 0, se, b->gtab6, b->n, C, b->digits, b->kqt, b->kqt2, b->kzq,
+  if (k6 && b->k6 == GV_KN_ARENA_NG)
+    hipLaunchKernelGGL(gv::k_ecmult_kn<GV_KN_ARENA_NG>, grd, blk, 0, se, b->gtab6, b->n, C, b->digits, b->kqt, b->kqt2,
+                       b->kzq, b->flags, b->in_r, sorted ? b->srt.bits : b->bits, (const uint32_t*)b->in_pfx, b->kC);
+  else if (k6)
+    hipLaunchKernelGGL(gv::k_ecmult_kn<4>, grd, blk, 0, se, b->gtab6, b->n, C, b->digits, b->kqt, b->kqt2, b->kzq,
                        b->flags, b->in_r, sorted ? b->srt.bits : b->bits, (const uint32_t*)b->in_pfx, b->kC);
   else if (gf)
     hipLaunchKernelGGL(gv::k_ecmult_k4<true>, grd, blk, 0, se, b->gtabf, b->gtab4, b->n, C, b->digits, b->kqt,
@@ -1706,56 +1908,69 @@ hipError_t gvk_gen_glat(uint32_t* glat, hipStream_t st) {
   return hipGetLastError();
 }
 
-// The two key-table launches over n keys whose rows in_x / in_pfx (stride C)
-// are unpacked; qr: 14 x 9 ratio rows of stride round_up(4 n, 256).
+// The key-table launches (k_keys_chain, k_keys_fwd, k_keys_back) over n keys
+// whose rows in_x / in_pfx (stride C) are unpacked.  Scratch (gv_kernels.h
+// gvk_keys_scratch_words): ratio rows, the E rows, the forward entries.
+}  // extern "C"
+template <int QW, int NG>
 static hipError_t keys_tables_launch(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx,
-                                     uint32_t* qr, uint32_t* qe, uint32_t base, uint32_t* kqt, uint32_t* kzq, uint32_t kC,
-                                     uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2, hipStream_t st) {
+                                     uint32_t* scratch, int with_qe, uint32_t base, uint32_t* kqt, uint32_t* kzq,
+                                     uint32_t kC, uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  const uint32_t C4 = (4u * n + 255u) / 256u * 256u;
-  hipLaunchKernelGGL(gv::k_keys_chain<false>, dim3((n + 255) / 256), dim3(256), 0, st, n, C, in_x, in_pfx, base, kqt,
-                     kC, kok, kqt2, kzq2);
-  hipLaunchKernelGGL(gv::k_keys_tables<GV_QTAB_N>, dim3(C4 / 256), dim3(256), 0, st, n, C4, base, kqt, kzq, kC, kqt2,
-                     kzq2, qr, qe);
+  constexpr int NT = gv::KLayout<QW, NG>::NT;
+  const uint32_t CL = gvk_keys_lanes(n, NG);
+  uint32_t* qr = scratch;
+  uint32_t* er = qr + (size_t)(NT - 2) * 9 * CL;
+  uint32_t* qe = with_qe ? er + (size_t)9 * CL : nullptr;
+  hipLaunchKernelGGL((gv::k_keys_chain<QW, NG>), dim3((n + 255) / 256), dim3(256), 0, st, n, C, in_x, in_pfx, base,
+                     kqt, kC, kok, kqt2, kzq2);
+  if (NG == 4) {
+    // four groups: one launch, the quad trades its Zs by lane shuffles (the
+    // last entry stays in registers; the E rows are unused)
+    hipLaunchKernelGGL((gv::k_keys_tables<QW>), dim3(CL / 256), dim3(256), 0, st, n, CL, base, kqt, kzq, kC, kqt2, kzq2,
+                       qr, qe);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL((gv::k_keys_fwd<QW, NG>), dim3(CL / 256), dim3(256), 0, st, n, CL, base, kqt, kC, kqt2,
+                     (const uint32_t*)kzq2, qr, qe, er);
+  hipLaunchKernelGGL((gv::k_keys_back<QW, NG>), dim3(CL / 256), dim3(256), 0, st, n, CL, base, kqt, kzq, kC, kqt2,
+                     kzq2, (const uint32_t*)qr, (const uint32_t*)qe, (const uint32_t*)er);
   return hipGetLastError();
 }
 
-hipError_t gvk_keys_build_rows6(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx, uint32_t* qr,
-                                uint32_t* qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok,
-                                uint32_t* kqt2, uint32_t* kzq2, hipStream_t st) {
-  if (n == 0) return hipSuccess;
-  const uint32_t C4 = (4u * n + 255u) / 256u * 256u;
-  hipLaunchKernelGGL(gv::k_keys_chain<true>, dim3((n + 255) / 256), dim3(256), 0, st, n, C, in_x, in_pfx, 0u, kqt,
-                     kC, kok, kqt2, kzq2);
-  hipLaunchKernelGGL(gv::k_keys_tables<GV_K6_NT>, dim3(C4 / 256), dim3(256), 0, st, n, C4, 0u, kqt, kzq, kC, kqt2,
-                     kzq2, qr, qe);
-  return hipGetLastError();
+extern "C" {
+uint32_t gvk_keys_lanes(uint32_t n, int ng) { return ((uint32_t)ng * n + 255u) / 256u * 256u; }
+size_t gvk_keys_scratch_words(uint32_t n, int ng, int nt, int with_qe) {
+  return (size_t)gvk_keys_lanes(n, ng) * ((size_t)(nt - 2) * 9 + 9 + (with_qe ? (size_t)nt * 18 : 0));
+}
+
+hipError_t gvk_keys_build_rows6(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx,
+                                uint32_t* scratch, int with_qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC,
+                                uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2, hipStream_t st) {
+  return keys_tables_launch<GV_K6_QW, 4>(n, C, in_x, in_pfx, scratch, with_qe, 0u, kqt, kzq, kC, kok, kqt2, kzq2, st);
 }
 
 hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
-                          uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t* qe, uint32_t base,
-                          uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2,
-                          hipStream_t st) {
+                          uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* scratch, int with_qe,
+                          uint32_t base, uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2,
+                          uint32_t* kzq2, hipStream_t st) {
   const dim3 blk(256), grd(C / 256);
   hipLaunchKernelGGL(gv::k_unpack, grd, blk, 0, st, pub33, (const uint8_t*)nullptr, (const uint8_t*)nullptr, n, C,
                      in_x, in_pfx, in_r, in_s, in_e);
-  return keys_tables_launch(n, C, in_x, in_pfx, qr, qe, base, kqt, kzq, kC, kok, kqt2, kzq2, st);
+  return keys_tables_launch<GV_QW, GV_LGRP>(n, C, in_x, in_pfx, scratch, with_qe, base, kqt, kzq, kC, kok, kqt2, kzq2,
+                                            st);
 }
 
 hipError_t gvk_keys_build6(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
-                           uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* qr, uint32_t* qe, uint32_t base,
-                           uint32_t* kqt6, uint32_t* kzq6, uint32_t kC, uint32_t* kok, uint32_t* kqt62,
+                           uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* scratch, int with_qe,
+                           uint32_t base, uint32_t* kqt6, uint32_t* kzq6, uint32_t kC, uint32_t* kok, uint32_t* kqt62,
                            uint32_t* kzq62, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const dim3 blk(256), grd(C / 256);
   hipLaunchKernelGGL(gv::k_unpack, grd, blk, 0, st, pub33, (const uint8_t*)nullptr, (const uint8_t*)nullptr, n, C,
                      in_x, in_pfx, in_r, in_s, in_e);
-  const uint32_t C4 = (4u * n + 255u) / 256u * 256u;
-  hipLaunchKernelGGL(gv::k_keys_chain<true>, dim3((n + 255) / 256), dim3(256), 0, st, n, C, in_x, in_pfx, base, kqt6,
-                     kC, kok, kqt62, kzq62);
-  hipLaunchKernelGGL(gv::k_keys_tables<GV_K6_NT>, dim3(C4 / 256), dim3(256), 0, st, n, C4, base, kqt6, kzq6, kC,
-                     kqt62, kzq62, qr, qe);
-  return hipGetLastError();
+  return keys_tables_launch<GV_K6_QW, GV_KN_ARENA_NG>(n, C, in_x, in_pfx, scratch, with_qe, base, kqt6, kzq6, kC, kok,
+                                                       kqt62, kzq62, st);
 }
 
 hipError_t gvk_keys_point(uint32_t n, const uint32_t* slots, const uint32_t* kqt, const uint32_t* kzq, uint32_t kC,
@@ -1791,10 +2006,11 @@ hipError_t gvk_dedupe(uint32_t n, uint32_t C, const uint32_t* x, const uint32_t*
   return hipGetLastError();
 }
 
-hipError_t gvk_keys_build_rows(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx, uint32_t* qr,
-                               uint32_t* qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC, uint32_t* kok, uint32_t* kqt2,
-                               uint32_t* kzq2, hipStream_t st) {
-  return keys_tables_launch(n, C, in_x, in_pfx, qr, qe, 0u, kqt, kzq, kC, kok, kqt2, kzq2, st);
+hipError_t gvk_keys_build_rows(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx,
+                               uint32_t* scratch, int with_qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC,
+                               uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2, hipStream_t st) {
+  return keys_tables_launch<GV_QW, GV_LGRP>(n, C, in_x, in_pfx, scratch, with_qe, 0u, kqt, kzq, kC, kok, kqt2, kzq2,
+                                            st);
 }
 
 #if GV_STAMP

@@ -257,7 +257,7 @@ int set_release(Set* s, hipStream_t st) {
 // 32-entry group tables and Zs.
 size_t key_slot_bytes(bool k6) {
   size_t b = ((size_t)GV_KEY_WORDS * (1 + GV_KEY2_TABLES) + 8 * (1 + GV_KEY2_TABLES) + 1) * 4;
-  if (k6) b += ((size_t)GV_K6_KEY_WORDS * (1 + GV_KEY2_TABLES) + 8 * (1 + GV_KEY2_TABLES)) * 4;
+  if (k6) b += ((size_t)GV_K6_KEY_WORDS * GV_KN_ARENA_NG + 8 * GV_KN_ARENA_NG) * 4;
   return b;
 }
 
@@ -303,8 +303,8 @@ int ensure_keys(Dev* d, size_t need, size_t used, hipStream_t st, size_t key_cap
   if (alloc6) {
     if (hipMalloc(&qt6, cap * GV_K6_KEY_WORDS * 4) != hipSuccess) return fail();
     if (hipMalloc(&zq6, cap * 8 * 4) != hipSuccess) return fail();
-    if (hipMalloc(&qt62, cap * GV_KEY2_TABLES * GV_K6_KEY_WORDS * 4) != hipSuccess) return fail();
-    if (hipMalloc(&zq62, cap * GV_KEY2_TABLES * 8 * 4) != hipSuccess) return fail();
+    if (hipMalloc(&qt62, cap * (GV_KN_ARENA_NG - 1) * GV_K6_KEY_WORDS * 4) != hipSuccess) return fail();
+    if (hipMalloc(&zq62, cap * (GV_KN_ARENA_NG - 1) * 8 * 4) != hipSuccess) return fail();
   }
   // the k6 tables of the slots below `used` exist only if the old arena had them
   const size_t used6 = d->kqt6 ? used : 0;
@@ -319,10 +319,11 @@ int ensure_keys(Dev* d, size_t need, size_t used, hipStream_t st, size_t key_cap
   }
   if (used6 && alloc6) {
     CK(hipMemcpyAsync(qt6, d->kqt6, used6 * GV_K6_KEY_WORDS * 4, hipMemcpyDeviceToDevice, st));
-    CK(hipMemcpyAsync(qt62, d->kqt62, used6 * GV_KEY2_TABLES * GV_K6_KEY_WORDS * 4, hipMemcpyDeviceToDevice, st));
+    CK(hipMemcpyAsync(qt62, d->kqt62, used6 * (GV_KN_ARENA_NG - 1) * GV_K6_KEY_WORDS * 4, hipMemcpyDeviceToDevice,
+                      st));
     for (int r = 0; r < 8; ++r)
       CK(hipMemcpyAsync(zq6 + r * cap, d->kzq6 + r * d->kcap, used6 * 4, hipMemcpyDeviceToDevice, st));
-    for (int r = 0; r < GV_KEY2_TABLES * 8; ++r)
+    for (int r = 0; r < (GV_KN_ARENA_NG - 1) * 8; ++r)
       CK(hipMemcpyAsync(zq62 + r * cap, d->kzq62 + r * d->kcap, used6 * 4, hipMemcpyDeviceToDevice, st));
   }
   if (used) CK(hipStreamSynchronize(st));
@@ -709,9 +710,11 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   uint32_t *rep = q, *uid = q + C, *kslot = q + 2 * C, *count = q + 3 * C, *table = q + 3 * C + 256;
   uint32_t* kx = table + T;
   uint32_t* kpfx = kx + 8 * capU;
-  uint32_t* qr = kpfx + capU;                   // ratio rows of the 4-lanes-per-key table build
-  if ((size_t)(qr + (GV_QTAB_N - 1) * 9 * 4 * capU - q) > (size_t)GV_QTAB_WORDS * C) return GV_OK;   // no room: pub33
-  const bool k6_room = (size_t)(qr + (size_t)(GV_K6_NT - 1) * 9 * 4 * capU - q) <= (size_t)GV_QTAB_WORDS * C;
+  uint32_t* sc = kpfx + capU;                   // the key-table build's scratch rows (gvk_keys_scratch_words)
+  const size_t used = (size_t)(sc - q), total = (size_t)GV_QTAB_WORDS * C;
+  const size_t room = used < total ? total - used : 0;
+  if (gvk_keys_scratch_words((uint32_t)capU, GV_LGRP, GV_QTAB_N, 0) > room) return GV_OK;   // no room: pub33
+  const bool k6_room = gvk_keys_scratch_words((uint32_t)capU, 4, GV_K6_NT, 0) <= room;
   if (!s->h_count && hipHostMalloc((void**)&s->h_count, 64, hipHostMallocDefault) != hipSuccess) {
     s->h_count = nullptr;
     return GV_ENOMEM;
@@ -739,18 +742,17 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   // does not read keys) runs on st: both are one wave per SIMD or so
   CK(hipEventRecord(s->fork, st));
   CK(hipStreamWaitEvent(s->side, s->fork, 0));
-  // the forward pass's entries in coalesced scratch rows after the ratio rows, when they fit
-  const size_t C4 = round_up(4 * U, 256);
-  const size_t nr = (size_t)(k6 ? GV_K6_NT : GV_QTAB_N) - 1;   // ratio / forward-entry rows per lane
-  uint32_t* qe = qr + nr * 9 * C4;
-  if (!ctx->keys_scratch || (size_t)(qe + nr * 18 * C4 - q) > (size_t)GV_QTAB_WORDS * C) qe = nullptr;
+  // the forward pass's entries in coalesced scratch rows after the ratio and
+  // E rows, when they fit (else through the tables themselves)
+  const int nt = k6 ? GV_K6_NT : GV_QTAB_N;
+  const int with_qe = ctx->keys_scratch && gvk_keys_scratch_words((uint32_t)U, 4, nt, 1) <= room ? 1 : 0;
   if (k6)
-    CK(gvk_keys_build_rows6((uint32_t)U, (uint32_t)capU, kx, kpfx, qr, qe, s->g_kqt, s->g_kzq, (uint32_t)capU,
+    CK(gvk_keys_build_rows6((uint32_t)U, (uint32_t)capU, kx, kpfx, sc, with_qe, s->g_kqt, s->g_kzq, (uint32_t)capU,
                             s->g_kok, s->g_kqt2, s->g_kzq2, s->side));
   else
-    CK(gvk_keys_build_rows((uint32_t)U, (uint32_t)capU, kx, kpfx, qr, qe, s->g_kqt, s->g_kzq, (uint32_t)capU,
+    CK(gvk_keys_build_rows((uint32_t)U, (uint32_t)capU, kx, kpfx, sc, with_qe, s->g_kqt, s->g_kzq, (uint32_t)capU,
                            s->g_kok, s->g_kqt2, s->g_kzq2, s->side));
-  if (used_end) *used_end = qe ? qe + nr * 18 * C4 : qr + nr * 9 * C4;
+  if (used_end) *used_end = sc + gvk_keys_scratch_words((uint32_t)U, 4, nt, with_qe);
   CK(hipEventRecord(s->keys_done, s->side));
   b.keys_ready = s->keys_done;
   b.pub33 = nullptr;
@@ -758,7 +760,7 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   b.kC = (uint32_t)capU; b.kcount = (uint32_t)U;
   b.kqt2 = s->g_kqt2; b.gtab4 = d->gtab4;       // null gtab4: the 125-doubling keyed ladder
   b.gtabf = ctx->gfull ? d->gtabf : nullptr;    // built by ensure_gtab4 above on first use
-  b.k6 = k6 ? 1 : 0; b.gtab6 = d->gtab6;
+  b.k6 = k6 ? 4 : 0; b.gtab6 = d->gtab6;
   d->grouped_batches++;
   d->grouped_keys += U;
   return GV_OK;
@@ -861,7 +863,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
   // batches on k_ecmult_k6; the small-batch kernels keep the k4 tables
   if (kslot && !ka && !small && ctx->keys_k6 && d->kqt6 && d->gtab6 && d->keys6 >= ctx->keys) {
     b.kqt = d->kqt6; b.kzq = d->kzq6; b.kqt2 = d->kqt62;
-    b.k6 = 1; b.gtab6 = d->gtab6;
+    b.k6 = GV_KN_ARENA_NG; b.gtab6 = d->gtab6;
   }
   if (pipelined) {
     b.st_ecm = st_ecm;
@@ -913,7 +915,8 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
       b.gtabf = ctx->gfull && ctx->gfull_item ? d->gtabf : nullptr;
     }
     plan_sort(ctx, s, b, sort_base);
-    d->routes[b.k6 && b.gtab6                  ? GV_ROUTE_K6
+    d->routes[b.k6 == GV_KN_ARENA_NG && b.gtab6 ? GV_ROUTE_KN
+              : b.k6 && b.gtab6                ? GV_ROUTE_K6
               : b.kslot && b.gtab4 && b.gtabf ? GV_ROUTE_K4F
               : b.kslot && b.gtab4            ? GV_ROUTE_K4
               : b.kslot                       ? GV_ROUTE_KEYED125
@@ -1773,32 +1776,30 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
     if (rc) return rc;
     bool k6 = ctx->keys_k6 && d->gtab6 && d->keys6 == base;
     if ((rc = ensure_keys(d, base + n, base, st, ctx->key_cap, ctx->hbm_budget, &k6))) return rc;
-    // chunks: the k4 build takes max_batch keys at a time; the k6 build's
-    // scratch rows are twice as many per key, so its chunks are smaller
-    const size_t step = k6 ? std::min<size_t>(ctx->max_batch, 131072) : ctx->max_batch;
+    // chunks: the k4 build takes max_batch keys at a time; the resident k6
+    // tables have GV_KN_ARENA_NG groups of 32 entries (scratch rows per key
+    // ~12x the k4 build's), so those chunks are smaller
+    const size_t step = k6 ? std::min<size_t>(ctx->max_batch, 32768) : ctx->max_batch;
     for (size_t c0 = 0; c0 < n; c0 += step) {
       const size_t cn = std::min(step, n - c0);
       const size_t C = round_up(cn, 256);
-      const size_t C4 = round_up(4 * cn, 256);
-      // scratch: the ratio rows of the 4-lanes-per-key table build (stride C4)
-      // start the set's Q-table region, then (when they fit) the forward-pass
-      // entries in coalesced rows; k6: 31 instead of 15 entries per group
-      const size_t nr4 = GV_QTAB_N - 1, nr6 = GV_K6_NT - 1, nr = k6 ? nr6 : nr4;
-      const size_t Cs = std::max(C, round_up(nr * 9 * C4 / GV_QTAB_WORDS + 1, 256));
+      // scratch: the key-table build's rows (ratios, E, and when they fit the
+      // forward-pass entries) from the start of the set's Q-table region
+      const size_t w4 = gvk_keys_scratch_words((uint32_t)cn, GV_LGRP, GV_QTAB_N, 0);
+      const size_t w6 = k6 ? gvk_keys_scratch_words((uint32_t)cn, GV_KN_ARENA_NG, GV_K6_NT, 1) : 0;
+      const size_t Cs = std::max(C, round_up(std::max(w4, w6) / GV_QTAB_WORDS + 1, 256));
       if ((rc = ensure_cap(s, Cs))) return rc;
       if ((rc = set_acquire(s, st))) return rc;
       CK(hipMemcpyAsync(s->d_in, pub33 + c0 * 33, cn * 33, hipMemcpyHostToDevice, st));
       const size_t room = (size_t)GV_QTAB_WORDS * s->cap;
-      uint32_t* qe = ctx->keys_scratch && nr4 * 27 * C4 <= room ? s->qtab + nr4 * 9 * C4 : nullptr;
+      const int qe4 = ctx->keys_scratch && gvk_keys_scratch_words((uint32_t)cn, GV_LGRP, GV_QTAB_N, 1) <= room;
       CK(gvk_keys_build(s->d_in, (uint32_t)cn, (uint32_t)C, s->in_x, s->in_pfx, s->in_r, s->in_s, s->in_e,
-                        s->qtab, qe, (uint32_t)(base + c0), d->kqt, d->kzq,
+                        s->qtab, qe4, (uint32_t)(base + c0), d->kqt, d->kzq,
                         (uint32_t)d->kcap, d->kok, d->kqt2, d->kzq2, st));
-      if (k6) {
-        uint32_t* qe6 = ctx->keys_scratch && nr6 * 27 * C4 <= room ? s->qtab + nr6 * 9 * C4 : nullptr;
+      if (k6)
         CK(gvk_keys_build6(s->d_in, (uint32_t)cn, (uint32_t)C, s->in_x, s->in_pfx, s->in_r, s->in_s, s->in_e,
-                           s->qtab, qe6, (uint32_t)(base + c0), d->kqt6, d->kzq6, (uint32_t)d->kcap, d->kok,
-                           d->kqt62, d->kzq62, st));
-      }
+                           s->qtab, ctx->keys_scratch ? 1 : 0, (uint32_t)(base + c0), d->kqt6, d->kzq6,
+                           (uint32_t)d->kcap, d->kok, d->kqt62, d->kzq62, st));
       if ((rc = set_release(s, st))) return rc;
       CK(hipStreamSynchronize(st));            // the caller's pub33 chunk is read by then
     }

@@ -277,11 +277,26 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * default 1, env GV_TWO_LADDERS),
  * "gfull" (0/1: keyed batches on the 4-group ladder add G from the unsplit
  * u1 = e/s -- 11 signed 25-bit windows from tables of 2^o G (6 GiB per device,
- * built on first keyed use) -- instead of 14 GLV windows; same verdicts;
+ * built by gv_open) -- instead of 14 GLV windows; same verdicts;
  * default 1, env GV_GFULL; route counter GV_ROUTE_K4F),
- * "k6" (0/1: in-batch grouped keys on the 6-bit-window ladder k_ecmult_k6 --
- * 32-entry key tables, 24-bit G windows (4 GiB); same verdicts; default 0,
- * env GV_K6),
+ * "k6" (0/1: in-batch grouped keys on the 6-bit-window ladder -- 4 groups of
+ * 32-entry key tables, 30 doublings, G from 11 24-bit windows of the unsplit
+ * u1 (5.5 GiB of tables, built by gv_open); same verdicts; default 0, env
+ * GV_K6; route counter GV_ROUTE_K6),
+ * "keys_k6" (0/1: gv_keys_load also builds each key's 6-bit-window tables --
+ * 11 groups of 32 entries on one Z, 28 KB per key beside the 5.4 KB of k4
+ * tables -- and keyed throughput batches whose slots all have them run the
+ * 6-doubling ladder; small keyed batches keep the k4 tables; same verdicts;
+ * default 1, env GV_KEYS_K6; route counter GV_ROUTE_KN),
+ * "key_cap" (the callers' key-arena reset point: the arena grows by doubling
+ * up to it and exactly past it; default GV_KEY_CAP, env GV_KEY_CAP),
+ * "hbm_budget_mb" (MiB of optional device tables per device -- the G tables
+ * past the GLV pair, the key arenas, the grouping arenas; a table past the
+ * budget is not built and batches take the schedule that needs less, with the
+ * same verdicts: k6 -> k4 -> the 125-doubling keyed ladder, full-scalar G ->
+ * GLV G; keys_load returns GV_ENOMEM when not even the k4 arena fits; 0 = no
+ * limit, the default; env GV_HBM_BUDGET_MB; the large G tables are built by
+ * gv_open unless env GV_EAGER_TABLES=0),
  * "time_kernels" (0/1: record HIP events around each kernel stage; the
  * ladder's time is its own start to end),
  * "fault_inject" (0/1: every verify call fails with GV_EFAULT; test hook). */
@@ -322,7 +337,9 @@ int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys)
  * GV_ROUTE_LAT (small pub33 batches: gv_lat.hip kernels), GV_ROUTE_LAT_KEYED
  * (small keyed batches), GV_ROUTE_K4F (the 4-group ladder with the G half on
  * the unsplit scalar, 25-bit windows), GV_ROUTE_ITEMF (the per-item pipeline
- * with the G half on the unsplit scalar, "gfull_item").  Instrumentation only
+ * with the G half on the unsplit scalar, "gfull_item"), GV_ROUTE_KN (keyed
+ * batches on the resident arena's k6 tables: 11 groups of 6-bit windows, 6
+ * doublings, option "keys_k6").  Instrumentation only
  * (bench route attribution, node metrics). */
 #define GV_ROUTE_PUB33 0
 #define GV_ROUTE_KEYED125 1
@@ -332,7 +349,8 @@ int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys)
 #define GV_ROUTE_LAT_KEYED 5
 #define GV_ROUTE_K4F 6
 #define GV_ROUTE_ITEMF 7
-#define GV_ROUTES 8
+#define GV_ROUTE_KN 8
+#define GV_ROUTES 9
 int gv_route_stats(gv_ctx* ctx, int dev_slot, uint64_t out[GV_ROUTES]);
 
 const char* gv_strerror(int code);

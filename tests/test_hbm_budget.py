@@ -13,7 +13,7 @@ the device:
   1 MiB      nothing optional                  per-item pub33       keys_load -> GV_ENOMEM
   1 GiB      k4 group G tables, small arenas   k4 (GLV G windows)   k4
   8 GiB      + full-scalar G tables            k4f                  k4f (no k6 tables)
-  default    everything                        k4f / k6             k6
+  default    everything                        k4f / k6             kn (the arena's k6 tables)
 """
 import os
 
@@ -94,7 +94,7 @@ def test_budget_degrades_with_the_same_verdicts(batch, mb, grouped_route, keyed_
         ver.close()
 
 
-def test_default_budget_takes_k6_on_cached_keys(batch):
+def test_default_budget_takes_the_arena_k6_tables(batch):
     pub, sig, dig, exp = batch
     ver = gvm.Verifier([0])
     try:
@@ -102,6 +102,6 @@ def test_default_budget_takes_k6_on_cached_keys(batch):
         slots = ver.keys_load(uniq)[inv.reshape(-1)].astype(np.uint32)
         got, routes = routes_of(ver, lambda: ver.verify_batch_digests_keyed(slots, sig, dig))
         assert np.array_equal(got, exp)
-        assert routes.get("k6", 0) >= 1, routes
+        assert routes.get("kn", 0) >= 1, routes
     finally:
         ver.close()

@@ -157,7 +157,7 @@ def test_cached_keys_and_messages(ver, sched):
     uniq, inv = np.unique(pub, axis=0, return_inverse=True)
     slots = ver.keys_load(uniq)[inv.reshape(-1)].astype(np.uint32)
     got, routes = run(ver, sched, lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
-    assert routes[sched] >= 1, routes
+    assert routes["kn" if sched == "k6" else sched] >= 1, routes       # the arena's k6 tables: 11 groups
     assert np.array_equal(got, exp)
     mp, ms, mm, mok, _ = load_msg_vectors()
     reps = max(1, 40_000 // len(mp))
@@ -189,7 +189,7 @@ def test_cached_keys_k6_goldens_and_slots(ver):
     slots[bad] = len(gp) + 7
     exp[bad] = 0
     got6, r6 = run(ver, "k6", lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
-    assert r6["k6"] >= 1, r6
+    assert r6["kn"] >= 1, r6
     assert np.array_equal(got6, exp)
     ver.set_option("keys_k6", 0)                                  # the k4 tables of the same slots
     try:
