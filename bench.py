@@ -649,7 +649,11 @@ def summarize(result, ex):
         "c2_device_resident": v,
         "c2_hostpath": {"pageable": g(ex, "c2_hostpath", "value"), "pinned": g(ex, "c2_hostpath", "value_pinned"),
                         "frac_pageable": g(ex, "c2_hostpath", "frac_of_device_resident"),
-                        "frac_pinned": g(ex, "c2_hostpath", "frac_of_device_resident_pinned")},
+                        "frac_pinned": g(ex, "c2_hostpath", "frac_of_device_resident_pinned"),
+                        "async": g(ex, "c2_hostpath", "value_async"),
+                        "async_pinned": g(ex, "c2_hostpath", "value_async_pinned"),
+                        "frac_async": g(ex, "c2_hostpath", "frac_of_device_resident_async"),
+                        "frac_async_pinned": g(ex, "c2_hostpath", "frac_of_device_resident_async_pinned")},
         "c2_key_cache": {"value": g(ex, "c2_key_cache", "value"), "route": g(ex, "c2_key_cache", "route"),
                          "frac": g(ex, "c2_key_cache", "roofline", "frac"),
                          "ladder_ms": g(ex, "c2_key_cache", "roofline", "kernel_ms")},

@@ -26,6 +26,8 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <list>
+#include <unordered_map>
 #include <future>
 #include <mutex>
 #include <memory>
@@ -73,7 +75,10 @@ struct Set {
   uint64_t* bits = nullptr;
   uint8_t* d_blob = nullptr;                      // message path blob
   size_t blob_cap = 0;
-  hipStream_t st = nullptr;                       // the set's own stream (host path)
+  hipStream_t st = nullptr;                       // the set's own stream (host path; front priority)
+  hipStream_t lad = nullptr;                      // host path: the chunk's ladder (ladder priority), so the
+                                                  // next chunk's / batch's front kernels take CU slots first
+  hipEvent_t lad_done = nullptr;
   hipEvent_t last = nullptr;                      // end of the last work using this set
   hipStream_t last_st = nullptr;
   hipEvent_t done = nullptr;                      // host path: chunk finished (bits on host)
@@ -81,6 +86,7 @@ struct Set {
   hipEvent_t ecm_ready = nullptr;                 // pipelined device calls: front kernels done
   hipStream_t side = nullptr;                     // grouped keys: table builds beside k_scalar_inv
   hipEvent_t fork = nullptr, keys_done = nullptr;
+  hipEvent_t grp_ready = nullptr;                 // slice grouping on this set: the keys' tables are built
   // in-batch key grouping: the per-batch key arena (tables of the batch's
   // distinct keys, key-arena layout) for up to gcap keys, and the count
   uint32_t *g_kqt = nullptr, *g_kzq = nullptr, *g_kok = nullptr, *g_kqt2 = nullptr, *g_kzq2 = nullptr;
@@ -120,8 +126,9 @@ struct Dev {
   int id = 0;
   uint32_t* gtab = nullptr;
   Set set[2];
-  Set gset;                                       // host slices: whole-slice key grouping (slice_group)
-  hipEvent_t grp_ready = nullptr;
+  Set gset[2];                                    // host slices: whole-slice key grouping (slice_group); the
+                                                  // async lane alternates the two (a slice's grouping under the
+                                                  // previous slice's chunks)
   hipEvent_t last_h2d = nullptr;                  // host slice: the previous chunk's H2D (h2d_serial)
   // key arena (gv_keys_load): Q table rows, table Z (8 rows of stride kcap), verdicts
   uint32_t *kqt = nullptr, *kzq = nullptr, *kok = nullptr;
@@ -499,8 +506,11 @@ int ed_launch(bool timed, Dev* d, size_t n, const uint8_t* pub, const uint8_t* s
 
 }  // namespace
 
+struct AsyncState;                               // gv_submit_* / gv_wait (below)
+
 struct gv_ctx {
   std::vector<Dev*> devs;
+  AsyncState* async = nullptr;                    // created by the first gv_submit_*
   size_t max_batch = size_t(1) << 20;
   size_t lat_max = 8192;        // batches up to this size take a fused small-batch kernel (gv_lat.hip), larger ones the pipeline
   size_t lat_sl_max = 2048;     // ... and up to this size the limb-sliced one (one signature per block); between the two the
@@ -517,6 +527,11 @@ struct gv_ctx {
   int stage_pieces = 2;         // host path, pageable chunks of >= 65,536 items: staged in this many pieces, each
                                 // piece's H2D behind its copy (1 = one copy then one H2D; GV_STAGE_PIECES):
                                 // 121.4 / 129.4 / 126.2 / 126.8M/s at 1 / 2 / 4 / 8 (profiles/r04/hostpath/stage_pieces_ab.jsonl)
+  size_t async_chunk = 262144;  // submitted batches: chunk size (the stream of chunks is steady, no ramp needed;
+  int async_growth = 1;         // GV_ASYNC_CHUNK, GV_ASYNC_GROWTH; "async_chunk" / "async_growth")
+  bool host_ladder_stream = false;  // host chunks' ladders on the set's low-priority ladder stream (chunk_ladder;
+                                    // GV_HOST_LADDER_STREAM=1).  Measured off: async pinned 185 vs 157-167M/s,
+                                    // sync pinned 158-160 vs 150-152M/s (profiles/r05/async_ab.jsonl)
   bool h2d_serial = true;       // host slices: a chunk's H2D waits for the previous chunk's, so concurrent
                                 // transfers do not share the link and delay the chunk the GPU needs first
                                 // (GV_H2D_SERIAL)
@@ -543,6 +558,7 @@ struct gv_ctx {
   bool keys_k6 = true;          // the resident arena (gv_keys_load) also holds k6 tables and its throughput batches
                                 // run k_ecmult_k6: the table build is paid once per key, not per batch (GV_KEYS_K6)
   size_t key_cap = GV_KEY_CAP;  // the callers' key-arena reset point: growth doubles up to here ("key_cap", GV_KEY_CAP)
+  size_t ed_key_cap = GV_ED_KEY_CAP;   // the same for the ed25519 arena ("ed_key_cap", GV_ED_KEY_CAP)
   size_t hbm_budget = SIZE_MAX; // bytes of optional device tables per device (G tables, key arenas; "hbm_budget_mb",
                                 // GV_HBM_BUDGET_MB): a table past it is not built and batches take the schedule
                                 // that needs less, with the same verdicts
@@ -1056,6 +1072,24 @@ int harvest(Dev* d, Set* s, const HostBatch& hb) {
   return GV_OK;
 }
 
+// A host chunk's ladder runs on the set's ladder stream (below the front
+// priority of the set streams), so the next chunk's front kernels -- and an
+// asynchronously submitted batch's grouping and key tables -- take CU slots
+// as this ladder's workgroups retire instead of queueing behind it (the
+// device-resident pipeline's stream priorities, dev_run).  Small batches run
+// one fused kernel on the set stream.
+hipStream_t chunk_ladder(const gv_ctx* ctx, Set* s, size_t cn, bool keyed) {
+  const size_t lmax = keyed ? ctx->lat_max_keyed : ctx->lat_max;
+  return ctx->host_ladder_stream && cn > lmax ? s->lad : nullptr;
+}
+// The set stream continues after the chunk's ladder (the bitmap's D2H).
+int ladder_join(Set* s) {
+  if (s->last_st != s->lad) return GV_OK;       // the ladder ran on the set stream
+  CK(hipEventRecord(s->lad_done, s->lad));
+  CK(hipStreamWaitEvent(s->st, s->lad_done, 0));
+  return GV_OK;
+}
+
 // Stage chunk [c0, c0 + cn) of a host batch into set s and enqueue H2D ->
 // kernels -> D2H of the bitmap on the set's stream.
 int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& hb) {
@@ -1106,8 +1140,9 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
     if ((rc = h2d_end())) return rc;
     const uint8_t* din = s->d_in;
     rc = launch(ctx, d, s, cn, keyed ? nullptr : din, din + L.sig, din + L.third, nullptr, nullptr, nullptr, s->bits,
-                s->st, dslots ? dsl : keyed ? (const uint32_t*)din : nullptr, nullptr, nullptr, hb.ka, hb.plain);
-    if (rc) return rc;
+                s->st, dslots ? dsl : keyed ? (const uint32_t*)din : nullptr, nullptr, chunk_ladder(ctx, s, cn, keyed),
+                hb.ka, hb.plain);
+    if (rc || (rc = ladder_join(s))) return rc;
     CK(hipMemcpyAsync(s->h_bits, s->bits, ((cn + 63) / 64) * 8, hipMemcpyDeviceToHost, s->st));
     CK(hipEventRecord(s->done, s->st));
     if ((rc = set_release(s, s->st))) return rc;
@@ -1199,8 +1234,9 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
   rc = launch(ctx, d, s, cn, keyed ? nullptr : din, din + L.sig, msgs ? nullptr : din + L.third,
               msgs ? s->d_blob : nullptr, msgs ? (const uint64_t*)(din + L.third) : nullptr,
               msgs ? (const uint32_t*)(din + L.len) : nullptr, s->bits, s->st,
-              dslots ? dsl : keyed ? (const uint32_t*)din : nullptr, nullptr, nullptr, hb.ka, hb.plain);
-  if (rc) return rc;
+              dslots ? dsl : keyed ? (const uint32_t*)din : nullptr, nullptr, chunk_ladder(ctx, s, cn, keyed), hb.ka,
+              hb.plain);
+  if (rc || (rc = ladder_join(s))) return rc;
   CK(hipMemcpyAsync(s->h_bits, s->bits, ((cn + 63) / 64) * 8, hipMemcpyDeviceToHost, s->st));
   CK(hipEventRecord(s->done, s->st));
   if ((rc = set_release(s, s->st))) return rc;
@@ -1242,10 +1278,9 @@ bool worth_grouping(const uint8_t* pub33, size_t n, int div) {
 // signatures and digests (or messages) travel per chunk, the slots stay on
 // the device.  *ka is filled and *d_slots set when the route is taken.
 int slice_group(gv_ctx* ctx, Dev* d, size_t lo, size_t n, const HostBatch& hb, KeyArena* ka,
-                const uint32_t** d_slots) {
+                const uint32_t** d_slots, Set* g) {
   *d_slots = nullptr;
   if (!worth_grouping(hb.pub33 + lo * 33, n, ctx->group_div)) return GV_OK;
-  Set* g = &d->gset;
   const size_t C = round_up(n, 256);
   int rc = ensure_cap(g, C);
   if (rc) return rc;
@@ -1269,13 +1304,12 @@ int slice_group(gv_ctx* ctx, Dev* d, size_t lo, size_t n, const HostBatch& hb, K
   b.in_x = g->in_x; b.in_pfx = g->in_pfx; b.in_r = g->in_r; b.in_s = g->in_s; b.in_e = g->in_e;
   if ((rc = group_keys(ctx, d, g, b, n, g->st))) return rc;
   if (!b.kslot) return set_release(g, g->st);   // many distinct keys after all: per-chunk pipeline
-  if (!d->grp_ready) CK(hipEventCreateWithFlags(&d->grp_ready, hipEventDisableTiming));
   CK(hipStreamWaitEvent(g->st, b.keys_ready, 0));
-  CK(hipEventRecord(d->grp_ready, g->st));
+  CK(hipEventRecord(g->grp_ready, g->st));
   ka->kqt = b.kqt; ka->kzq = b.kzq; ka->kok = b.kok; ka->kqt2 = b.kqt2; ka->kzq2 = g->g_kzq2;
   ka->kC = b.kC; ka->kcount = b.kcount; ka->gtab4 = b.gtab4;
   ka->gtab6 = b.gtab6; ka->k6 = b.k6;
-  ka->ready = d->grp_ready;
+  ka->ready = g->grp_ready;
   *d_slots = b.kslot;
   return GV_OK;   // the set stays acquired until run_slice releases it after the last chunk
 }
@@ -1284,6 +1318,37 @@ std::vector<Worker*> workers(const gv_ctx* ctx) {
   std::vector<Worker*> w;
   for (Dev* d : ctx->devs) w.push_back(d->worker);
   return w;
+}
+
+// Chunk sizes of a host slice of `count` items.  Pipelined (past lat_max): a
+// ramp -- pipe_chunk first, each later chunk at most pipe_growth times the one
+// before -- so the first kernels start after a short staging copy and every
+// later chunk is staged (pageable -> pinned copy, H2D) while the one before it
+// computes.  Else equal chunks of at most max_batch.  Every chunk but the last
+// is a multiple of 256 (harvest copies bitmap words).
+std::vector<size_t> chunk_ramp(const gv_ctx* ctx, size_t count, bool pipelined, bool async = false) {
+  std::vector<size_t> sz;
+  if (pipelined) {
+    const size_t first = async ? ctx->async_chunk : ctx->pipe_chunk;
+    const size_t growth = async ? (size_t)ctx->async_growth : (size_t)ctx->pipe_growth;
+    size_t c = std::min(first, ctx->max_batch), left = count;
+    while (left) {
+      const size_t take = std::min(left, c);
+      sz.push_back(take);
+      left -= take;
+      c = std::min(ctx->max_batch, c * growth);
+    }
+    const size_t m = sz.size();             // a runt tail joins the chunk before it
+    if (m >= 2 && 2 * sz[m - 1] < sz[m - 2] && sz[m - 1] + sz[m - 2] <= ctx->max_batch) {
+      sz[m - 2] += sz[m - 1];
+      sz.pop_back();
+    }
+  } else {
+    const size_t nch = (count + ctx->max_batch - 1) / ctx->max_batch;
+    const size_t chunk = std::min(ctx->max_batch, round_up((count + nch - 1) / nch, 256));
+    for (size_t c0 = 0; c0 < count; c0 += chunk) sz.push_back(std::min(chunk, count - c0));
+  }
+  return sz;
 }
 
 // Verify items [lo, hi) of a host batch on one device: chunks alternate
@@ -1303,35 +1368,8 @@ int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const HostBatch& hb) {
     }
   } timer{d, n, t_begin};
   d->last_h2d = nullptr;                          // no earlier chunk of this slice
-  // Chunk sizes.  Pipelined (past lat_max): a ramp -- pipe_chunk first, each
-  // later chunk at most pipe_growth times the one before -- so the first
-  // kernels start after a short staging copy and every later chunk is staged
-  // (pageable -> pinned copy, H2D) while the one before it computes.  Else
-  // equal chunks of at most max_batch.  Every chunk but the last is a multiple
-  // of 256 (harvest copies bitmap words).
   const bool pipelined = n > (hb.slots ? ctx->lat_max_keyed : ctx->lat_max) && ctx->pipe_chunk;
-  auto chunk_sizes = [&](size_t count) {
-    std::vector<size_t> sz;
-    if (pipelined) {
-      size_t c = std::min(ctx->pipe_chunk, ctx->max_batch), left = count;
-      while (left) {
-        const size_t take = std::min(left, c);
-        sz.push_back(take);
-        left -= take;
-        c = std::min(ctx->max_batch, c * (size_t)ctx->pipe_growth);
-      }
-      const size_t m = sz.size();             // a runt tail joins the chunk before it
-      if (m >= 2 && 2 * sz[m - 1] < sz[m - 2] && sz[m - 1] + sz[m - 2] <= ctx->max_batch) {
-        sz[m - 2] += sz[m - 1];
-        sz.pop_back();
-      }
-    } else {
-      const size_t nch = (count + ctx->max_batch - 1) / ctx->max_batch;
-      const size_t chunk = std::min(ctx->max_batch, round_up((count + nch - 1) / nch, 256));
-      for (size_t c0 = 0; c0 < count; c0 += chunk) sz.push_back(std::min(chunk, count - c0));
-    }
-    return sz;
-  };
+  auto chunk_sizes = [&](size_t count) { return chunk_ramp(ctx, count, pipelined); };
   std::vector<size_t> sizes = chunk_sizes(n);
   int rc = GV_OK;
   // a pub33 slice big enough for the pipeline: group its keys once for all chunks
@@ -1355,7 +1393,7 @@ int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const HostBatch& hb) {
   bool grouped = false;
   if (try_group) {
     const uint32_t* dsl = nullptr;
-    rc = slice_group(ctx, d, lo + np, n - np, hb, &ka, &dsl);
+    rc = slice_group(ctx, d, lo + np, n - np, hb, &ka, &dsl, &d->gset[0]);
     if (rc == GV_OK && dsl) {
       grouped = true;
       hg.d_slots = dsl;
@@ -1378,7 +1416,7 @@ int run_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const HostBatch& hb) {
       s.busy = false;
     }
   if (grouped) {                                  // every chunk done: the slice's arena is free
-    const int r2 = set_release(&d->gset, d->gset.st);
+    const int r2 = set_release(&d->gset[0], d->gset[0].st);
     if (rc == GV_OK) rc = r2;
   }
   return rc;
@@ -1471,6 +1509,218 @@ int run_host(gv_ctx* ctx, size_t n, const HostBatch& hb_in) {
                     [&](size_t k, size_t lo, size_t hi) { return run_slice(ctx, ctx->devs[k], lo, hi, hb); });
 }
 
+
+}  // namespace
+
+// ---- asynchronous host batches (gv_submit_* / gv_wait)
+//
+// One lane thread per device takes the device's slices of submitted batches
+// in submission order and runs them as ONE stream of chunks over the two
+// scratch sets: the next slice's staging, key grouping and key tables (on the
+// other grouping set) are enqueued while the previous slice's last chunks
+// still compute, so consecutive batches overlap the way pipelined
+// device-resident calls do -- the synchronous entry points drain every slice
+// before they return.  A batch is done when every device's slice has been
+// harvested; gv_wait returns its result.  The lane holds the device lock from
+// its first queued slice until its queue is empty and every chunk harvested.
+struct AsyncJob {
+  HostBatch hb;
+  int left = 0;                                   // device slices not finished (AsyncState::m)
+  int rc = GV_OK;
+  bool done = false;
+};
+struct AsyncSlice {
+  std::shared_ptr<AsyncJob> job;
+  size_t lo = 0, hi = 0;
+};
+struct AsyncState {
+  std::mutex m;
+  std::condition_variable cv;                     // lanes: work or quit; waiters: a job done
+  std::vector<std::deque<AsyncSlice>> q;          // per device
+  std::vector<std::thread> lanes;
+  std::unordered_map<uint64_t, std::shared_ptr<AsyncJob>> jobs;
+  uint64_t next_ticket = 1;
+  size_t pending = 0;                             // jobs submitted, not done
+  bool quit = false;
+};
+
+namespace {
+
+struct ActiveSlice {
+  AsyncSlice sl;
+  HostBatch hr;                                   // what the chunks run (a grouped slice: device slots)
+  KeyArena ka;
+  Set* g = nullptr;                               // its grouping set (released after its last chunk)
+  int inflight = 0;
+  bool submitted = false;
+  int rc = GV_OK;
+};
+
+void finish_slice(AsyncState* as, ActiveSlice& a) {
+  if (a.g) {
+    const int rc = set_release(a.g, a.g->st);
+    if (rc && !a.rc) a.rc = rc;
+  }
+  std::lock_guard<std::mutex> lk(as->m);
+  AsyncJob& j = *a.sl.job;
+  if (a.rc && !j.rc) j.rc = a.rc;
+  if (--j.left == 0) {
+    j.done = true;
+    --as->pending;
+  }
+  as->cv.notify_all();
+}
+
+// Runs device k's queued slices (d->mu held) until the queue is empty, then
+// drains.
+void lane_stream(gv_ctx* ctx, AsyncState* as, size_t k, Dev* d) {
+  std::list<ActiveSlice> act;
+  ActiveSlice* owner[2] = {nullptr, nullptr};
+  int sk = 0, gflip = 0;
+  d->last_h2d = nullptr;
+  auto retire = [&](ActiveSlice* a) {
+    finish_slice(as, *a);
+    for (auto it = act.begin(); it != act.end(); ++it)
+      if (&*it == a) { act.erase(it); break; }
+  };
+  auto harvest_set = [&](int j) {                 // the chunk in flight on set j
+    Set* s = &d->set[j];
+    if (!s->busy) return;
+    ActiveSlice* a = owner[j];
+    const int rc = harvest(d, s, a->hr);
+    if (rc && !a->rc) a->rc = rc;
+    owner[j] = nullptr;
+    if (--a->inflight == 0 && a->submitted) retire(a);
+  };
+  auto drain = [&]() {                            // the older chunk first
+    harvest_set(sk);
+    harvest_set(sk ^ 1);
+  };
+  for (;;) {
+    AsyncSlice sl;
+    {
+      std::lock_guard<std::mutex> lk(as->m);
+      if (as->q[k].empty()) break;
+      sl = as->q[k].front();
+      as->q[k].pop_front();
+    }
+    act.emplace_back();
+    ActiveSlice& a = act.back();
+    a.sl = sl;
+    a.hr = sl.job->hb;
+    const size_t lo = sl.lo, n = sl.hi - sl.lo;
+    const HostBatch& hb = sl.job->hb;
+    const bool pipelined = n > (hb.slots ? ctx->lat_max_keyed : ctx->lat_max) && ctx->pipe_chunk;
+    const std::vector<size_t> sizes = chunk_ramp(ctx, n, pipelined, true);
+    const bool try_group = hb.pub33 && !hb.slots && ctx->group_keys && n >= ctx->group_min && sizes.size() > 1;
+    if (try_group) {
+      Set* g = &d->gset[gflip];
+      gflip ^= 1;
+      for (const ActiveSlice& o : act)            // an older slice still on this grouping set: drain it
+        if (&o != &a && o.g == g) { drain(); break; }
+      const uint32_t* dsl = nullptr;
+      const int rc = slice_group(ctx, d, lo, n, hb, &a.ka, &dsl, g);
+      if (rc) a.rc = rc;
+      else if (dsl) {
+        a.g = g;
+        a.hr.d_slots = dsl;
+        a.hr.d_slots_lo = lo;
+        a.hr.ka = &a.ka;
+      }
+    }
+    size_t c0 = lo;
+    for (size_t i = 0; i < sizes.size() && a.rc == GV_OK; c0 += sizes[i], ++i) {
+      harvest_set(sk);
+      const int rc = submit(ctx, d, &d->set[sk], c0, sizes[i], a.hr);
+      if (rc) { a.rc = rc; break; }
+      owner[sk] = &a;
+      ++a.inflight;
+      sk ^= 1;
+    }
+    a.submitted = true;
+    if (a.inflight == 0) retire(&a);
+  }
+  drain();
+}
+
+void lane_main(gv_ctx* ctx, AsyncState* as, size_t k) {
+  Dev* d = ctx->devs[k];
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> lk(as->m);
+      as->cv.wait(lk, [&] { return as->quit || !as->q[k].empty(); });
+      if (as->q[k].empty()) return;               // quit, nothing left
+    }
+    std::lock_guard<std::mutex> dl(d->mu);
+    if (hipSetDevice(d->id) != hipSuccess) {      // fail every queued slice of this device
+      std::lock_guard<std::mutex> lk(as->m);
+      for (AsyncSlice& sl : as->q[k]) {
+        if (!sl.job->rc) sl.job->rc = GV_EHIP;
+        if (--sl.job->left == 0) { sl.job->done = true; --as->pending; }
+      }
+      as->q[k].clear();
+      as->cv.notify_all();
+      continue;
+    }
+    lane_stream(ctx, as, k, d);
+  }
+}
+
+AsyncState* async_state(gv_ctx* ctx) {
+  static std::mutex create_mu;
+  std::lock_guard<std::mutex> lk(create_mu);
+  if (!ctx->async) {
+    AsyncState* as = new AsyncState();
+    as->q.resize(ctx->devs.size());
+    for (size_t k = 0; k < ctx->devs.size(); ++k) as->lanes.emplace_back(lane_main, ctx, as, k);
+    ctx->async = as;
+  }
+  return ctx->async;
+}
+
+// Wait until no submitted batch is pending (the key arenas change meaning
+// under a keyed batch otherwise).
+void async_quiesce(gv_ctx* ctx) {
+  AsyncState* as = ctx->async;
+  if (!as) return;
+  std::unique_lock<std::mutex> lk(as->m);
+  as->cv.wait(lk, [&] { return as->pending == 0; });
+}
+
+int submit_host(gv_ctx* ctx, size_t n, const HostBatch& hb_in, uint64_t* ticket) {
+  if (!ctx || !ticket) return GV_EINVAL;
+  *ticket = 0;
+  if (ctx->fault_inject) return GV_EFAULT;
+  if (n > 0) {
+    if ((!hb_in.pub33 && !hb_in.slots) || !hb_in.sig64 || (!hb_in.out_ok && !hb_in.out_bits)) return GV_EINVAL;
+    if (!hb_in.dig32 && (!hb_in.blob || !hb_in.off || !hb_in.len)) return GV_EINVAL;
+  }
+  auto job = std::make_shared<AsyncJob>();
+  job->hb = hb_in;
+  job->hb.pinned = hb_in.dig32 && is_pinned(hb_in.slots ? (const void*)hb_in.slots : hb_in.pub33) &&
+                   is_pinned(hb_in.sig64) && is_pinned(hb_in.dig32);
+  AsyncState* as = async_state(ctx);
+  const size_t nd = ctx->devs.size(), per = round_up((n + nd - 1) / std::max<size_t>(nd, 1), 256);
+  std::lock_guard<std::mutex> lk(as->m);
+  for (size_t k = 0; k < nd; ++k) {
+    const size_t lo = std::min(n, k * per), hi = std::min(n, (k + 1) * per);
+    if (lo >= hi) continue;
+    as->q[k].push_back(AsyncSlice{job, lo, hi});
+    ++job->left;
+  }
+  if (job->left == 0) job->done = true;
+  else ++as->pending;
+  const uint64_t t = as->next_ticket++;
+  as->jobs.emplace(t, job);
+  *ticket = t;
+  as->cv.notify_all();
+  return GV_OK;
+}
+
+}  // namespace
+
+namespace {
+
 void free_set(Set& s) {
   if (s.st) (void)hipStreamSynchronize(s.st);
   if (s.scratch) (void)hipFree(s.scratch);
@@ -1484,10 +1734,13 @@ void free_set(Set& s) {
   if (s.ecm_ready) (void)hipEventDestroy(s.ecm_ready);
   if (s.fork) (void)hipEventDestroy(s.fork);
   if (s.keys_done) (void)hipEventDestroy(s.keys_done);
+  if (s.grp_ready) (void)hipEventDestroy(s.grp_ready);
   if (s.side) { (void)hipStreamSynchronize(s.side); (void)hipStreamDestroy(s.side); }
   for (uint32_t* p : {s.g_kqt, s.g_kzq, s.g_kok, s.g_kqt2, s.g_kzq2})
     if (p) (void)hipFree(p);
   if (s.h_count) (void)hipHostFree(s.h_count);
+  if (s.lad) { (void)hipStreamSynchronize(s.lad); (void)hipStreamDestroy(s.lad); }
+  if (s.lad_done) (void)hipEventDestroy(s.lad_done);
   if (s.st) (void)hipStreamDestroy(s.st);
 }
 
@@ -1540,9 +1793,16 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* gi = getenv("GV_GFULL_ITEM")) ctx->gfull_item = strcmp(gi, "0") != 0;
   if (const char* hs = getenv("GV_H2D_SERIAL")) ctx->h2d_serial = strcmp(hs, "0") != 0;
   if (const char* kk = getenv("GV_KEYS_K6")) ctx->keys_k6 = strcmp(kk, "0") != 0;
+  if (const char* hl = getenv("GV_HOST_LADDER_STREAM")) ctx->host_ladder_stream = strcmp(hl, "0") != 0;
+  parse_size_env("GV_ASYNC_CHUNK", &ctx->async_chunk);
+  if (const char* ag = getenv("GV_ASYNC_GROWTH")) ctx->async_growth = std::max(1, std::min(64, atoi(ag)));
   if (const char* kc = getenv("GV_KEY_CAP")) {
     const long long v = atoll(kc);
     if (v >= 256 && (unsigned long long)v <= kMaxItems) ctx->key_cap = (size_t)v;
+  }
+  if (const char* kc = getenv("GV_ED_KEY_CAP")) {
+    const long long v = atoll(kc);
+    if (v >= 256 && (unsigned long long)v <= kMaxItems) ctx->ed_key_cap = (size_t)v;
   }
   if (const char* hb = getenv("GV_HBM_BUDGET_MB")) {
     const long long v = atoll(hb);
@@ -1570,15 +1830,18 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
       if (!strcmp(lp, "ladder")) { front_prio = lo_prio; ladder_prio = hi_prio; }
       else if (!strcmp(lp, "equal")) front_prio = ladder_prio = lo_prio;
     }
-    for (Set* sp : {&d->set[0], &d->set[1], &d->gset})
-      ok = ok && hipStreamCreateWithFlags(&sp->st, hipStreamNonBlocking) == hipSuccess &&
+    for (Set* sp : {&d->set[0], &d->set[1], &d->gset[0], &d->gset[1]})
+      ok = ok && hipStreamCreateWithPriority(&sp->st, hipStreamNonBlocking, front_prio) == hipSuccess &&
+           hipStreamCreateWithPriority(&sp->lad, hipStreamNonBlocking, ladder_prio) == hipSuccess &&
+           hipEventCreateWithFlags(&sp->lad_done, hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&sp->last, hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&sp->done, hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&sp->h2d, hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&sp->ecm_ready, hipEventDisableTiming) == hipSuccess &&
            hipStreamCreateWithPriority(&sp->side, hipStreamNonBlocking, front_prio) == hipSuccess &&
            hipEventCreateWithFlags(&sp->fork, hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&sp->keys_done, hipEventDisableTiming) == hipSuccess;
+           hipEventCreateWithFlags(&sp->keys_done, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&sp->grp_ready, hipEventDisableTiming) == hipSuccess;
     // pipelined device-resident calls: front kernels on two streams
     // (alternating sets), the ladders on two more (two_ladders)
     for (int j = 0; j < 2; ++j)
@@ -1619,12 +1882,21 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
 
 void gv_close(gv_ctx* ctx) {
   if (!ctx) return;
+  if (AsyncState* as = ctx->async) {              // the lanes finish what is queued, then quit
+    {
+      std::lock_guard<std::mutex> lk(as->m);
+      as->quit = true;
+    }
+    as->cv.notify_all();
+    for (std::thread& t : as->lanes) t.join();
+    delete as;
+    ctx->async = nullptr;
+  }
   for (Dev* d : ctx->devs) {
     delete d->worker;
     (void)hipSetDevice(d->id);
     for (Set& s : d->set) free_set(s);
-    free_set(d->gset);
-    if (d->grp_ready) (void)hipEventDestroy(d->grp_ready);
+    for (Set& g : d->gset) free_set(g);
     if (d->gtab) (void)hipFree(d->gtab);
     if (d->glat) (void)hipFree(d->glat);
     if (d->gtab4) (void)hipFree(d->gtab4);
@@ -1702,6 +1974,45 @@ static int dev_common(gv_ctx* ctx, int slot, size_t n, const void* pub, const vo
   return GV_OK;
 }
 
+int gv_submit_digests(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64, const uint8_t* dig32,
+                      uint8_t* out_ok, uint64_t* ticket) {
+  if (n && !dig32) return GV_EINVAL;
+  return submit_host(ctx, n, HostBatch{pub33, sig64, dig32, nullptr, nullptr, nullptr, nullptr, out_ok, nullptr},
+                     ticket);
+}
+
+int gv_submit_digests_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64, const uint8_t* dig32,
+                            uint8_t* out_ok, uint64_t* ticket) {
+  if (n && (!slot || !dig32)) return GV_EINVAL;
+  return submit_host(ctx, n, HostBatch{nullptr, sig64, dig32, nullptr, nullptr, nullptr, slot, out_ok, nullptr},
+                     ticket);
+}
+
+int gv_submit_msgs(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64, const uint8_t* msg_blob,
+                   const uint64_t* msg_off, const uint32_t* msg_len, uint8_t* out_ok, uint64_t* ticket) {
+  return submit_host(ctx, n, HostBatch{pub33, sig64, nullptr, msg_blob, msg_off, msg_len, nullptr, out_ok, nullptr},
+                     ticket);
+}
+
+int gv_submit_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64, const uint8_t* msg_blob,
+                         const uint64_t* msg_off, const uint32_t* msg_len, uint8_t* out_ok, uint64_t* ticket) {
+  if (n && !slot) return GV_EINVAL;
+  return submit_host(ctx, n, HostBatch{nullptr, sig64, nullptr, msg_blob, msg_off, msg_len, slot, out_ok, nullptr},
+                     ticket);
+}
+
+int gv_wait(gv_ctx* ctx, uint64_t ticket) {
+  if (!ctx || !ctx->async) return GV_EINVAL;
+  AsyncState* as = ctx->async;
+  std::unique_lock<std::mutex> lk(as->m);
+  auto it = as->jobs.find(ticket);
+  if (it == as->jobs.end()) return GV_EINVAL;
+  std::shared_ptr<AsyncJob> j = it->second;
+  as->cv.wait(lk, [&] { return j->done; });
+  as->jobs.erase(ticket);
+  return j->rc;
+}
+
 int gv_dev_verify_digests(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub33,
                           const void* d_sig64, const void* d_dig32, void* d_bits, void* stream) {
   Dev* d = nullptr;
@@ -1759,6 +2070,7 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
   if (!ctx) return GV_EINVAL;
   if (n == 0) return GV_OK;
   if (!pub33 || !slot_out) return GV_EINVAL;
+  async_quiesce(ctx);                           // no submitted keyed batch reads slots that move
   std::lock_guard<std::mutex> kl(ctx->keys_mu);
   const size_t base = ctx->keys;
   if (base + n > kMaxItems) return GV_EINVAL;
@@ -1812,6 +2124,7 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
 
 int gv_keys_reset(gv_ctx* ctx) {
   if (!ctx) return GV_EINVAL;
+  async_quiesce(ctx);
   std::lock_guard<std::mutex> kl(ctx->keys_mu);
   ctx->keys = 0;
   ctx->keys_gen.fetch_add(1);
@@ -1822,12 +2135,14 @@ size_t gv_keys_count(const gv_ctx* ctx) { return ctx ? ctx->keys : 0; }
 
 // ---- ed25519 key arena + small keyed batches (k_ed_keys, k_ed_lat_sl)
 namespace {
-// Growth doubles the arena but stops at GV_ED_KEY_CAP (the callers' reset
-// point): the transient peak of a growth -- old and new arena both allocated,
-// 72 KB per key each -- stays within cap + the old arena.
-int ensure_ed_keys(Dev* d, size_t need, size_t used, hipStream_t st) {
+// Growth doubles the arena but stops at the callers' reset point (ed_key_cap:
+// GV_ED_KEY_CAP or the option) and past it grows to exactly what is needed:
+// the transient peak of a growth -- old and new arena both allocated, 72 KB
+// per key each -- stays within cap + the old arena.
+int ensure_ed_keys(Dev* d, size_t need, size_t used, hipStream_t st, size_t cap_limit) {
   if (need <= d->ekcap) return GV_OK;
-  const size_t grow = std::min<size_t>(2 * d->ekcap, std::max<size_t>(need, GV_ED_KEY_CAP));
+  const size_t grow = d->ekcap >= cap_limit ? need
+                                            : std::min<size_t>(2 * d->ekcap, std::max<size_t>(need, cap_limit));
   const size_t cap = round_up(std::max<size_t>({need, grow, 256}), 256);
   uint32_t *t = nullptr, *p = nullptr, *o = nullptr;
   auto fail = [&]() {
@@ -1860,7 +2175,7 @@ int gv_ed_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub32, uint32_t* slot_
     std::lock_guard<std::mutex> lk(d->mu);
     CK(hipSetDevice(d->id));
     hipStream_t st = d->set[0].st;
-    int rc = ensure_ed_keys(d, base + n, base, st);
+    int rc = ensure_ed_keys(d, base + n, base, st, ctx->ed_key_cap);
     if (rc) return rc;
     uint8_t* dp = nullptr;
     const size_t o_wb = round_up(n * 32, 256), wb_bytes = n * 64 * 36 * 4;
@@ -2264,9 +2579,18 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
     bool& flag = !strcmp(key, "two_ladders") ? ctx->two_ladders : !strcmp(key, "gfull") ? ctx->gfull
                  : !strcmp(key, "k6") ? ctx->k6 : ctx->keys_k6;
     flag = val != 0;
-  } else if (!strcmp(key, "key_cap")) {
+  } else if (!strcmp(key, "async_chunk")) {
     if (val < 256 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
-    ctx->key_cap = (size_t)val;
+    ctx->async_chunk = round_up((size_t)val, 256);
+  } else if (!strcmp(key, "async_growth")) {
+    if (val < 1 || val > 64) return GV_EINVAL;
+    ctx->async_growth = (int)val;
+  } else if (!strcmp(key, "host_ladder_stream")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->host_ladder_stream = val != 0;
+  } else if (!strcmp(key, "key_cap") || !strcmp(key, "ed_key_cap")) {
+    if (val < 256 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
+    (!strcmp(key, "key_cap") ? ctx->key_cap : ctx->ed_key_cap) = (size_t)val;
   } else if (!strcmp(key, "hbm_budget_mb")) {
     if (val < 0) return GV_EINVAL;
     ctx->hbm_budget = val == 0 ? SIZE_MAX : (size_t)val << 20;

@@ -44,6 +44,7 @@ EXPORTED_SYMBOLS = (
     "gv_keys_point", "gv_dev_stream_create", "gv_dev_stream_sync", "gv_dev_stream_destroy",
     "gv_verify_ed25519_msgs", "gv_dev_verify_ed25519_msgs", "gv_last_slices", "gv_group_stats", "gv_route_stats", "gv_host_alloc", "gv_host_free",
     "gv_ed_keys_load", "gv_ed_keys_reset", "gv_ed_keys_count", "gv_ed_keys_generation", "gv_verify_ed25519_msgs_keyed",
+    "gv_submit_digests", "gv_submit_digests_keyed", "gv_submit_msgs", "gv_submit_msgs_keyed", "gv_wait",
 )
 
 
@@ -155,6 +156,13 @@ def load(path: str = LIB_PATH):
     L.gv_verify_msgs_keyed.restype = i32
     L.gv_dev_verify_digests_keyed.argtypes = [vp, i32, sz, vp, vp, vp, vp, vp]
     L.gv_dev_verify_digests_keyed.restype = i32
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    for name, nargs in (("gv_submit_digests", 4), ("gv_submit_digests_keyed", 4), ("gv_submit_msgs", 6),
+                        ("gv_submit_msgs_keyed", 6)):
+        getattr(L, name).argtypes = [vp, sz] + [vp] * nargs + [u64p]
+        getattr(L, name).restype = i32
+    L.gv_wait.argtypes = [vp, ctypes.c_uint64]
+    L.gv_wait.restype = i32
     _lib = L
     return L
 
@@ -258,6 +266,45 @@ class Verifier:
             _check(self._L.gv_verify_msgs(self._ctx, n, _ptr(pub33), _ptr(sig64), _ptr(blob), _ptr(off),
                                           _ptr(ln), _ptr(out)), "gv_verify_msgs")
         return out
+
+    # ---- asynchronous host batches (gv_submit_* / gv_wait)
+    class Pending:
+        """A submitted batch: holds its input arrays (the library reads them
+        until gv_wait) and its verdict array."""
+        def __init__(self, ticket, out, keep):
+            self.ticket, self.out, self._keep = ticket, out, keep
+
+    def _submit(self, fn, name, n, args, keep):
+        out = np.zeros(n, dtype=np.uint8)
+        t = ctypes.c_uint64(0)
+        _check(fn(self._ctx, n, *[_ptr(a) for a in args], _ptr(out), ctypes.byref(t)), name)
+        return Verifier.Pending(t.value, out, keep)
+
+    def submit_digests(self, pub33, sig64, dig32) -> "Verifier.Pending":
+        a = [np.ascontiguousarray(x, dtype=np.uint8) for x in (pub33, sig64, dig32)]
+        return self._submit(self._L.gv_submit_digests, "gv_submit_digests", a[0].shape[0], a, a)
+
+    def submit_digests_keyed(self, slots, sig64, dig32) -> "Verifier.Pending":
+        a = [np.ascontiguousarray(slots, dtype=np.uint32)] + [np.ascontiguousarray(x, dtype=np.uint8)
+                                                             for x in (sig64, dig32)]
+        return self._submit(self._L.gv_submit_digests_keyed, "gv_submit_digests_keyed", a[0].shape[0], a, a)
+
+    def submit_msgs(self, pub33, sig64, msgs, slots=None) -> "Verifier.Pending":
+        blob, off, ln = pack_msgs(msgs) if isinstance(msgs, (list, tuple)) and (
+            len(msgs) == 0 or isinstance(msgs[0], (bytes, bytearray))) else msgs
+        sig64 = np.ascontiguousarray(sig64, dtype=np.uint8)
+        if slots is not None:
+            k = np.ascontiguousarray(slots, dtype=np.uint32)
+            a = [k, sig64, blob, off, ln]
+            return self._submit(self._L.gv_submit_msgs_keyed, "gv_submit_msgs_keyed", k.shape[0], a, a)
+        p = np.ascontiguousarray(pub33, dtype=np.uint8)
+        a = [p, sig64, blob, off, ln]
+        return self._submit(self._L.gv_submit_msgs, "gv_submit_msgs", p.shape[0], a, a)
+
+    def wait(self, pending: "Verifier.Pending") -> np.ndarray:
+        _check(self._L.gv_wait(self._ctx, pending.ticket), "gv_wait")
+        pending._keep = None
+        return pending.out
 
     # ---- account pubkey cache (gv_keys_*; SURVEY.md §8f-2)
     def keys_load(self, pub33: np.ndarray) -> np.ndarray:

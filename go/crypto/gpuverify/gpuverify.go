@@ -248,13 +248,26 @@ func Open(devices []int) (*GPU, error) {
 		KeyCap: envInt("GV_KEY_CAP", DefaultKeyCap), EdKeyCap: envInt("GV_ED_KEY_CAP", DefaultEdKeyCap),
 		slots: map[secp256k1.PubKeySecp256k1]uint32{}, edSlots: map[ed25519.PubKeyEd25519]uint32{}}
 	g.pool.ctx = ctx
+	// the library's arena growth doubles up to the reset points the shim uses
+	// (past them it grows to exactly what is needed, no quadratic copying)
+	if err := g.SetOption("key_cap", int64(g.KeyCap)); err != nil {
+		g.Close()
+		return nil, err
+	}
+	if err := g.SetOption("ed_key_cap", int64(g.EdKeyCap)); err != nil {
+		g.Close()
+		return nil, err
+	}
 	return g, nil
 }
 
-// Close releases the pinned buffers and the context (idempotent).
+// Close releases the pinned buffers and the context (idempotent).  It first
+// waits for the pinned buffers that in-flight calls still hold: they go back
+// to the pool while the context is valid (gv_host_free needs it), and no new
+// pinned buffer is handed out once closing has begun.
 func (g *GPU) Close() {
 	g.closeOnce.Do(func() {
-		g.pool.drain()
+		g.pool.close()
 		C.gv_close(g.ctx)
 	})
 }
@@ -286,10 +299,13 @@ type cbuf struct {
 // pinnedPool: free lists of gv_host_alloc buffers per size class 2^k bytes,
 // at most pinnedKeep bytes parked in all.
 type pinnedPool struct {
-	ctx    *C.gv_ctx
-	mu     sync.Mutex
-	free   [32][]unsafe.Pointer
-	parked int
+	ctx     *C.gv_ctx
+	mu      sync.Mutex
+	free    [32][]unsafe.Pointer
+	parked  int
+	out     int        // pinned buffers handed out and not yet returned
+	closing bool       // Close has begun: get() hands out C.malloc buffers only
+	idle    *sync.Cond // signalled when out drops to 0 while closing
 }
 
 const pinnedKeep = 1 << 30
@@ -301,38 +317,63 @@ func (p *pinnedPool) get(n int) cbuf {
 	}
 	if k < 32 {
 		p.mu.Lock()
-		if l := len(p.free[k]); l > 0 {
+		if p.closing {
+			p.mu.Unlock()
+		} else if l := len(p.free[k]); l > 0 {
 			ptr := p.free[k][l-1]
 			p.free[k] = p.free[k][:l-1]
 			p.parked -= 1 << k
+			p.out++
 			p.mu.Unlock()
 			return cbuf{ptr, (*[maxBatchBytes]byte)(ptr)[:n:n], k, p}
-		}
-		p.mu.Unlock()
-		var ptr unsafe.Pointer
-		if p.ctx != nil && C.gv_host_alloc(p.ctx, C.size_t(1)<<uint(k), &ptr) == 0 {
-			return cbuf{ptr, (*[maxBatchBytes]byte)(ptr)[:n:n], k, p}
+		} else {
+			p.out++ // reserved before the allocation, so Close waits for it
+			p.mu.Unlock()
+			var ptr unsafe.Pointer
+			if p.ctx != nil && C.gv_host_alloc(p.ctx, C.size_t(1)<<uint(k), &ptr) == 0 {
+				return cbuf{ptr, (*[maxBatchBytes]byte)(ptr)[:n:n], k, p}
+			}
+			p.mu.Lock()
+			p.release()
+			p.mu.Unlock()
 		}
 	}
 	ptr := C.malloc(C.size_t(n))
 	return cbuf{ptr, (*[maxBatchBytes]byte)(ptr)[:n:n], -1, nil}
 }
 
-func (p *pinnedPool) put(c cbuf) {
-	p.mu.Lock()
-	if p.parked+(1<<c.class) <= pinnedKeep {
-		p.free[c.class] = append(p.free[c.class], c.p)
-		p.parked += 1 << c.class
-		p.mu.Unlock()
-		return
+// release: one handed-out buffer is back (p.mu held).
+func (p *pinnedPool) release() {
+	p.out--
+	if p.out == 0 && p.closing && p.idle != nil {
+		p.idle.Broadcast()
 	}
-	p.mu.Unlock()
-	C.gv_host_free(p.ctx, c.p)
 }
 
-func (p *pinnedPool) drain() {
+func (p *pinnedPool) put(c cbuf) {
 	p.mu.Lock()
 	defer p.mu.Unlock()
+	if !p.closing && p.parked+(1<<c.class) <= pinnedKeep {
+		p.free[c.class] = append(p.free[c.class], c.p)
+		p.parked += 1 << c.class
+	} else {
+		C.gv_host_free(p.ctx, c.p) // Close is waiting for this buffer: the context is still open
+	}
+	p.release()
+}
+
+// close: no more pinned buffers out, wait for the outstanding ones, free
+// every parked buffer.  The context stays open until it returns.
+func (p *pinnedPool) close() {
+	p.mu.Lock()
+	defer p.mu.Unlock()
+	p.closing = true
+	if p.idle == nil {
+		p.idle = sync.NewCond(&p.mu)
+	}
+	for p.out > 0 {
+		p.idle.Wait()
+	}
 	for k := range p.free {
 		for _, ptr := range p.free[k] {
 			C.gv_host_free(p.ctx, ptr)

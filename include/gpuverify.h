@@ -17,7 +17,8 @@
  *
  * Plain pointers and sizes only (cgo / ctypes / JNI friendly).  The caller owns
  * every buffer; the library copies inputs into its own device memory and keeps
- * no caller pointer after a call returns.  Host-buffer calls are synchronous
+ * no caller pointer after a call returns (the gv_submit_* calls excepted: they
+ * keep theirs until gv_wait).  Host-buffer gv_verify_* calls are synchronous
  * and a gv_ctx may be shared by concurrent threads (calls on one device
  * serialise; every use of a device's scratch, on any stream, is ordered after
  * the previous one, so gv_dev_* calls on different caller streams never
@@ -112,9 +113,11 @@ int gv_dev_stream_destroy(gv_ctx* ctx, int dev_slot, void* stream);
  * node verifies the same accounts block after block.  gv_keys_load parses n
  * SEC1 keys once (prefix, x < p, square root) and keeps each key's table of
  * 16 multiples resident in HBM on every device of the context (1,280 B per
- * key, plus the tables of 2^35 Q, 2^70 Q, 2^100 Q for the 30-doubling keyed
- * ladder: 5.4 KB per key, 1M accounts = 5.4 GB of the 288 GB); slot_out[i]
- * receives key i's slot.
+ * key, plus the tables of 2^35 Q, 2^70 Q, 2^100 Q for the small-batch keyed
+ * kernels: 5.4 KB per key) and, with option "keys_k6" (default), the
+ * throughput ladder's 11 tables of 32 multiples of 2^(12 k) Q on one Z (28 KB
+ * per key: 1M accounts = 34 GB of the 288 GB); slot_out[i] receives key i's
+ * slot.
  * A key that ParsePubKey rejects gets a slot too, and every verify against it
  * is false.  Slots are assigned in load order and stay valid until
  * gv_keys_reset.  Loading must not race keyed verifies of the same context. */
@@ -288,8 +291,10 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * tables -- and keyed throughput batches whose slots all have them run the
  * 6-doubling ladder; small keyed batches keep the k4 tables; same verdicts;
  * default 1, env GV_KEYS_K6; route counter GV_ROUTE_KN),
- * "key_cap" (the callers' key-arena reset point: the arena grows by doubling
- * up to it and exactly past it; default GV_KEY_CAP, env GV_KEY_CAP),
+ * "key_cap" / "ed_key_cap" (the callers' reset points of the secp256k1 /
+ * ed25519 key arenas: an arena grows by doubling up to it and exactly past it;
+ * defaults GV_KEY_CAP / GV_ED_KEY_CAP, env of the same names; the Go shim sets
+ * both to its KeyCap / EdKeyCap at Open),
  * "hbm_budget_mb" (MiB of optional device tables per device -- the G tables
  * past the GLV pair, the key arenas, the grouping arenas; a table past the
  * budget is not built and batches take the schedule that needs less, with the
@@ -301,6 +306,32 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * ladder's time is its own start to end),
  * "fault_inject" (0/1: every verify call fails with GV_EFAULT; test hook). */
 int gv_set_option(gv_ctx* ctx, const char* key, long long val);
+
+/* Asynchronous host batches.  gv_submit_* queue a batch with the arguments
+ * of the matching gv_verify_* entry point and return at once with a ticket;
+ * gv_wait(ticket) blocks until that batch's verdicts are in out_ok and
+ * returns its result (the gv_verify_* codes; a ticket is waited for once).
+ * Batches run in submission order per context, each device's slices as one
+ * stream of chunks: the next batch's staging, key grouping and key tables run
+ * while the previous batch's last chunks compute, so a caller that keeps a
+ * batch queued ahead (the next block's PreVerifyTxs, a replay) gets the
+ * device-resident pipeline's overlap from host buffers.  Unlike gv_verify_*,
+ * the library keeps the caller's pointers until gv_wait returns: the buffers
+ * (ideally gv_host_alloc memory, read in place) must stay valid and unchanged
+ * until then.  gv_keys_load / gv_keys_reset wait for every submitted batch
+ * first; gv_close finishes the queued batches.  Replaces nothing in the
+ * reference (its ante handler verifies synchronously, x/auth/ante/
+ * sigverify.go:210); it is how baseapp's pre-verification hook keeps the
+ * GPU busy across blocks (baseapp/abci.go:203-221). */
+int gv_submit_digests(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64, const uint8_t* dig32,
+                      uint8_t* out_ok, uint64_t* ticket);
+int gv_submit_digests_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64, const uint8_t* dig32,
+                            uint8_t* out_ok, uint64_t* ticket);
+int gv_submit_msgs(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64, const uint8_t* msg_blob,
+                   const uint64_t* msg_off, const uint32_t* msg_len, uint8_t* out_ok, uint64_t* ticket);
+int gv_submit_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64, const uint8_t* msg_blob,
+                         const uint64_t* msg_off, const uint32_t* msg_len, uint8_t* out_ok, uint64_t* ticket);
+int gv_wait(gv_ctx* ctx, uint64_t ticket);
 
 /* With "time_kernels" on: milliseconds of the last launch's stages on dev_slot
  * (unpack+sha, prep, ecmult), measured with HIP events on the launch stream. */
