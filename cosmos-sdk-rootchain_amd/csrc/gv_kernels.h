@@ -193,6 +193,9 @@ typedef struct gvk_lat {
   const uint32_t* kqt2;         // GV_KEY2_TABLES rows per slot (row slot * 3 + group - 1)
   const uint32_t* kzq2;         // GV_KEY2_TABLES x 8 rows of stride kC
   const uint32_t* glat;         // GV_GLAT_WORDS
+  // pub33 sliced batches with gtab6 set (the runtime: n <= lat_rows_max)
+  // take k_verify_lat_sl4 (row-parallel ladders, G from the 24-bit tables)
+  const uint32_t* gtab6;
 } gvk_lat;
 
 // ed25519 (ed_verify.hip): one signature per lane over C lanes (C % 256 == 0).

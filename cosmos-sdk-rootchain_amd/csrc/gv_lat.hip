@@ -73,6 +73,7 @@ static __constant__ const u32 kLP[8] = {0xFFFFFC2Fu, 0xFFFFFFFEu, 0xFFFFFFFFu, 0
 
 struct LatShared {
   static constexpr bool kG5 = false;         // G digits: 20-bit windows (dg)
+  static constexpr bool kG24 = false;
   u32 qtab[GV_LAT_SIGS][2][GV_QTAB_N][18];  // Q, lambda*Q entries: x, y raw 29-bit limbs (effective affine)
   u32 ratio[64][GV_QTAB_N - 1][9];          // per-lane Z-ratio scratch of the table build (raw limbs)
   u32 dq[GV_LAT_SIGS][GV_QWIN];             // packed int16 Q / lambda*Q digits per window
@@ -331,6 +332,7 @@ GV_DEV void lat_keyed_tables(LatShared& sh, int sig, int slot, bool live, u32 ks
 // The keyed 16-lane schedule's shared state (k_verify_lat16).
 struct Lat16Shared {
   static constexpr bool kG5 = true;          // G digits: 5-bit windows like Q (dg5)
+  static constexpr bool kG24 = false;
   u32 dq[GV_LAT16_SIGS][GV_QWIN];            // packed int16 Q / lambda*Q digits per window
   u32 dg5[GV_LAT16_SIGS][GV_QWIN];           // packed int16 G / lambda*G digits per window
   u32 r[GV_LAT16_SIGS][8];
@@ -409,7 +411,15 @@ GV_DEV void lat_scalars_e(SH& sh, int sig, bool live, const uint8_t* sig64, GetE
     if (n2q) d1 = -d1;
     sh.dq[sig][win] = ((u32)d0 & 0xFFFFu) | ((u32)d1 << 16);
   }
-  if constexpr (SH::kG5) {
+  if constexpr (SH::kG24) {
+    // G on the unsplit u1: 11 signed 24-bit windows (the k6 tables' digits)
+    if (!ok) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) u1[i] = 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < GV_K6_GWIN; ++j) sh.dg24[sig][j] = booth_digit8<GV_K6_GW>(u1, j);
+  } else if constexpr (SH::kG5) {
 #pragma unroll
     for (int win = 0; win < GV_QWIN; ++win) {
       int d2 = booth_digit<GV_QW>(k1g, win), d3 = booth_digit<GV_QW>(k2g, win);
@@ -775,6 +785,7 @@ __global__ __launch_bounds__(128) void k_verify_lat16(const gvk_lat b) {
 // bitmap (zeroed by the launcher).
 struct LatSlShared {
   static constexpr bool kG5 = false;         // G digits: 20-bit windows (dg)
+  static constexpr bool kG24 = false;
   u32 qtab[2][GV_QTAB_N][18];               // Q, lambda*Q entries: x, y sliced limbs (effective affine)
   u32 ratio[GV_QTAB_N - 1][9];              // Z ratios, then their suffix products
   u32 dq[1][GV_QWIN];
@@ -789,7 +800,8 @@ struct LatSlShared {
 
 // Wave 0 of k_verify_lat_sl: key decompression, Q / lambda*Q tables into LDS,
 // zq (Z of the table's curve) and the ParsePubKey verdict into LDS.
-GV_DEV void lat_sl_prep(LatSlShared& sh, const gvk_lat& b, u32 gi, const fslk& k) {
+template <class SH>
+GV_DEV void lat_sl_prep(SH& sh, const gvk_lat& b, u32 gi, const fslk& k) {
   const u32 row = (threadIdx.x >> 4) & 3u, L = k.L;
   const bool lo = L < 9u;
   // ---- pubkey: btcec ParsePubKey / decompressPoint
@@ -1038,6 +1050,263 @@ __global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
 }
 
 // ---------------------------------------------------------------------------
+// Pub33 small batches, row-parallel (k_verify_lat_sl4): ONE signature per
+// 256-thread block, and each ladder wave's four 16-lane rows cooperate on ONE
+// accumulator -- the products of a doubling / addition that do not depend on
+// each other run in different rows at once and every row gets every row's
+// result from three lane swaps (v_permlane16_swap, v_permlane32_swap: VALU,
+// no LDS round trip), so a doubling is 3 product rounds instead of 7 serial
+// products and an addition 5 instead of 11.  Four ladder waves, one per SIMD:
+// Q and lambda*Q, even and odd windows (each 125 doublings, 13 windows'
+// additions).  G is added on its own, from the 2^23-entry tables of
+// 2^(24 j) G (gtab6: u1 unsplit, 11 signed 24-bit windows, no doublings), by
+// the scalar wave right after the scalar chain, inside the time the key
+// decompression and tables take on wave 0.  Same checks, group law results
+// (every exceptional case as gjsl_add_scaled / gjsl_add_gej) and verdict as
+// k_verify_lat_sl.
+struct LatSl4Shared {
+  static constexpr bool kG5 = false;
+  static constexpr bool kG24 = true;
+  u32 qtab[2][GV_QTAB_N][18];               // Q, lambda*Q entries (effective affine, sliced limbs)
+  u32 ratio[GV_QTAB_N - 1][9];
+  u32 dq[1][GV_QWIN];
+  int dg24[1][GV_K6_GWIN];                  // u1's 24-bit Booth digits
+  u32 r[1][8];
+  u32 oks[1];
+  u32 zq[16];
+  u32 okp;
+  u32 pt[4][3][16];                         // the partial sums of waves 1, 2, 3 and the G sum
+  u32 pinf[4];
+  u32 gent[GV_K6_GWIN][18];                 // the G entries (x, +-y), sliced
+};
+
+// The four rows' values of v, each in every row: r[i] = row i's v.
+struct rows4 { u32 r[4]; };
+GV_DEV rows4 rows_all(u32 v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);     // {v0 v0 v2 v2}, {v1 v1 v3 v3}
+  const auto e = __builtin_amdgcn_permlane32_swap(a[0], a[0], false, false);   // v0, v2
+  const auto o = __builtin_amdgcn_permlane32_swap(a[1], a[1], false, false);   // v1, v3
+  rows4 r;
+  r.r[0] = e[0]; r.r[1] = o[0]; r.r[2] = e[1]; r.r[3] = o[1];
+  return r;
+}
+
+// Every round below is ONE product per lane whose operands (and 64-bit extra)
+// the row selects -- never a branch on the row, which would run each row's
+// product in turn.
+//
+// A = 2A, the accumulator replicated in the wave's four rows:
+//   round 1: B = Y^2 (row 0), Z3 = Y 2Z (row 1), E = 3X^2 (rows 2, 3)
+//   round 2: D = X B (row 0), C = B^2 (row 1), E2 = E^2 (rows 2, 3)
+//   round 3: X3 = E^2 - 8D (row 0), Y3 = E (12D - E2) - 8C (rows 1..3)
+// (Y3 = E (4D - X3) - 8C with X3 = E^2 - 8D): gjsl_double's values mod p.
+GV_DEV void gj4_double(gjsl& A, u32 row, const fslk& k) {
+  const rows4 p1 = rows_all(fsl_mul(row >= 2u ? A.x : A.y, row == 0u ? A.y : row == 1u ? A.z << 1 : A.x * 3u, k));
+  const u32 B = p1.r[0], Z3 = p1.r[1], E = p1.r[2];
+  const rows4 p2 = rows_all(fsl_mul(row == 0u ? A.x : row == 1u ? B : E, row >= 2u ? E : B, k));
+  const u32 D = p2.r[0], C = p2.r[1], E2 = p2.r[2];
+  const u32 t = (fsl_norm(D * 3u, k) << 2) + k.bias - E2;          // 12D - E^2 < 2^31.6
+  const rows4 p3 = rows_all(fsl_mul_plus(E, row == 0u ? E : t, k.big8 - ((u64)(row == 0u ? D : C) << 3), k));
+  A.x = p3.r[0];
+  A.y = p3.r[1];
+  A.z = Z3;
+}
+
+// A += (x, y), affine on the curve scaled by A.z (gjsl_add_scaled's formula
+// and cases), row-parallel:
+//   round 1: z2 = Z1^2 (every row)
+//   round 2: H = x z2 - X1 (row 0), z3 = z2 Z1 (rows 1..3)
+//   round 3: R = y z3 - Y1 (row 0), H2 = H^2 (row 1), Z3 = Z1 H (row 2), Y1 H (row 3)
+//   round 4: H3 = H2 H (row 0), V = X1 H2 (row 1), R2 = R^2 (row 2), Y1 H3 (row 3)
+//   X3 = R2 - H3 - 2V (sums only)
+//   round 5: Y3 = R (V - X3) - Y1 H3 (every row: nothing to exchange)
+GV_DEV void gj4_add(gjsl& A, bool& inf, u32 x, u32 y, u32 row, const fslk& k) {
+  const u32 z2 = fsl_sqr(A.z, k);
+  const rows4 p2 = rows_all(fsl_mul_plus(row == 0u ? x : z2, row == 0u ? z2 : A.z,
+                                         row == 0u ? (u64)(k.bias - A.x) : 0ull, k));
+  const u32 h = p2.r[0], z3 = p2.r[1];
+  const rows4 p3 = rows_all(fsl_mul_plus(row == 0u ? y : row == 1u ? h : row == 2u ? A.z : A.y, row == 0u ? z3 : h,
+                                         row == 0u ? (u64)(k.bias - A.y) : 0ull, k));
+  const u32 rr = p3.r[0];
+  if (fsl_is_zero(h)) {                                  // the same answer in every row
+    if (fsl_is_zero(rr)) gj4_double(A, row, k);          // A == entry: 2A
+    else inf = true;                                     // A == -entry
+    return;
+  }
+  const u32 h2 = p3.r[1], zn = p3.r[2], y1h = p3.r[3];
+  const rows4 p4 = rows_all(fsl_mul(row == 0u ? h2 : row == 1u ? A.x : row == 2u ? rr : y1h,
+                                    row == 0u ? h : row == 2u ? rr : h2, k));
+  const u32 h3 = p4.r[0], v = p4.r[1], r2 = p4.r[2], y1h3 = p4.r[3];
+  const u32 x3 = fsl_norm(r2 + 3u * k.bias - h3 - (v << 1), k);   // < 2^31.9 before the carry pass
+  A.y = fsl_mul_plus(rr, v + k.bias - x3, (u64)(k.bias - y1h3), k);
+  A.x = x3;
+  A.z = zn;
+}
+
+// A += O, two Jacobian points of the real curve (gjsl_add_gej's formula and
+// cases: either infinite -> the other; A == O -> 2A; A == -O -> infinity):
+//   round 1: Z1^2 (row 0), Z2^2 (row 1), Z1 Z2 (rows 2, 3)
+//   round 2: U1 = X1 Z2^2 (row 0), U2 = X2 Z1^2 (row 1), Z2^3 (row 2), Z1^3 (row 3)
+//   round 3: S1 = Y1 Z2^3 (row 0), S2 = Y2 Z1^3 (row 1), Z3 = Z1 Z2 H (row 2), H2 = H^2 (row 3)
+//   round 4: R2 = R^2 (row 0), H3 = H2 H (row 1), V = U1 H2 (rows 2, 3)
+//   X3 = R2 - H3 - 2V (sums only)
+//   round 5: Y3 = R (V - X3) - S1 H3 (every row)
+GV_DEV void gj4_add_gej(gjsl& A, bool& inf, const gjsl& O, bool oinf, u32 row, const fslk& k) {
+  if (inf || oinf) {
+    if (inf) A = O;
+    inf = inf && oinf;
+    return;
+  }
+  const rows4 p1 = rows_all(fsl_mul(row == 1u ? O.z : A.z, row == 0u ? A.z : O.z, k));
+  const u32 z11 = p1.r[0], z22 = p1.r[1], z12 = p1.r[2];
+  const rows4 p2 = rows_all(fsl_mul(row == 0u ? A.x : row == 1u ? O.x : row == 2u ? O.z : A.z,
+                                    row == 0u || row == 2u ? z22 : z11, k));
+  const u32 u1 = p2.r[0], u2 = p2.r[1], z23 = p2.r[2], z13 = p2.r[3];
+  const u32 h = fsl_sub(u2, u1, k);
+  const rows4 p3 = rows_all(fsl_mul(row == 0u ? A.y : row == 1u ? O.y : row == 2u ? z12 : h,
+                                    row == 0u ? z23 : row == 1u ? z13 : h, k));
+  const u32 s1 = p3.r[0], s2 = p3.r[1];
+  const u32 rr = fsl_sub(s2, s1, k);
+  if (fsl_is_zero(h)) {
+    if (fsl_is_zero(rr)) gj4_double(A, row, k);
+    else inf = true;
+    return;
+  }
+  const u32 zn = p3.r[2], h2 = p3.r[3];
+  const rows4 p4 = rows_all(fsl_mul(row == 0u ? rr : row == 1u ? h2 : u1, row == 0u ? rr : row == 1u ? h : h2, k));
+  const u32 r2 = p4.r[0], h3 = p4.r[1], v = p4.r[2];
+  const u32 x3 = fsl_norm(r2 + 3u * k.bias - h3 - (v << 1), k);
+  A.y = fsl_mul2(rr, v + k.bias - x3, k.bias - s1, h3, k);
+  A.x = x3;
+  A.z = zn;
+}
+
+// A += the affine point (x, y) (sliced limbs, y < 2^30.1); A may be infinity
+GV_DEV void gj4_add_affine(gjsl& A, bool& inf, u32 x, u32 y, u32 row, const fslk& k) {
+  if (inf) {
+    A.x = x; A.y = fsl_norm(y, k); A.z = k.L == 0u ? 1u : 0u;
+    inf = false;
+  } else {
+    gj4_add(A, inf, x, y, row, k);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_verify_lat_sl4(const gvk_lat b) {
+  __shared__ LatSl4Shared sh;
+  const u32 gi = blockIdx.x;                            // grid = n: every block is live
+  const u32 wave = threadIdx.x >> 6;
+  const fslk k = fsl_consts();
+  const u32 row = (threadIdx.x >> 4) & 3u, L = k.L;
+  const bool lo = L < 9u;
+  gjsl A;
+  A.x = 0u; A.y = 0u; A.z = 0u;
+  bool inf = true;
+  if (wave == 0u) LAT_STAMP(0);
+  if (wave == 1u) {                                     // the scalar chain (and the hash), then G
+    if (b.msg_len) {
+      u32 eh[8];
+      sha256_msg_wave(eh, b.msg_blob + b.msg_off[gi], b.msg_len[gi]);
+      lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, nullptr, nullptr, b.C, gi, eh);
+    } else {
+      lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.dig32 + (size_t)gi * 32u, nullptr, b.C, gi);
+    }
+    LAT_STAMP(3);                                       // trace builds: scalars done
+    wave_lds_sync();
+    // G = sum of d_j (2^(24 j) G): every entry's loads in flight at once,
+    // parked in LDS (row j & 3 stores entry j)
+#pragma unroll
+    for (int j = 0; j < GV_K6_GWIN; ++j) {
+      const int d = sh.dg24[0][j];
+      const u32 e = d == 0 ? 0u : (u32)((d < 0 ? -d : d) - 1);
+      const u32* pe = b.gtab6 + ((size_t)j * GV_K6_GTAB_N + e) * 16u;
+      const u32 x = fsl_load_words(pe, k), y = fsl_load_words(pe + 8, k);
+      if (row == (u32)(j & 3) && lo) { sh.gent[j][L] = x; sh.gent[j][9 + L] = d < 0 ? k.bias - y : y; }
+    }
+    wave_lds_sync();
+#pragma unroll 1
+    for (int j = 0; j < GV_K6_GWIN; ++j) {
+      if (sh.dg24[0][j] == 0) continue;
+      gj4_add_affine(A, inf, lo ? sh.gent[j][L] : 0u, lo ? sh.gent[j][9 + L] : 0u, row, k);
+    }
+    if (row == 0u) {
+      if (lo) { sh.pt[3][0][L] = A.x; sh.pt[3][1][L] = A.y; sh.pt[3][2][L] = A.z; }
+      if (L == 0u) sh.pinf[3] = inf ? 1u : 0u;
+    }
+    LAT_STAMP(7);                                       // trace builds: G sum done
+    A.x = 0u; A.y = 0u; A.z = 0u;
+    inf = true;
+  } else if (wave == 0u) {
+    lat_sl_prep(sh, b, gi, k);                          // the key and its tables
+  }
+  __syncthreads();                                      // digits, G sum (wave 1), tables + zq (wave 0)
+  if (wave == 0u) LAT_STAMP(4);
+  {
+    // Q (waves 0, 2) or lambda*Q (waves 3, 1), even (waves 0, 3) or odd (2, 1) windows
+    const int par = (wave == 0u || wave == 3u) ? 0 : 1;
+    const int tab = (wave == 0u || wave == 2u) ? 0 : 1;
+#pragma unroll 1
+    for (int win = GV_QWIN - 1; win >= 0; --win) {
+      if (win != GV_QWIN - 1 && !inf) {
+#pragma unroll 1
+        for (int dd = 0; dd < GV_QW; ++dd) gj4_double(A, row, k);
+      }
+      if ((win & 1) != par) continue;
+      const u32 dq = sh.dq[0][win];
+      const int d = tab == 0 ? ((int)(dq << 16) >> 16) : ((int)dq >> 16);
+      if (d == 0) continue;
+      const u32 e = (u32)((d < 0 ? -d : d) - 1);
+      const u32 x = lo ? sh.qtab[tab][e][L] : 0u;
+      const u32 y = lo ? sh.qtab[tab][e][9 + L] : 0u;
+      gj4_add_affine(A, inf, x, d < 0 ? k.bias - y : y, row, k);
+    }
+    if (!inf) A.z = fsl_mul(A.z, lo ? sh.zq[L] : 0u, k);   // back to the real curve
+  }
+  if (wave == 0u) LAT_STAMP(5);
+  if (wave != 0u && row == 0u) {                        // partial sums into LDS, wave 0 adds them
+    if (lo) { sh.pt[wave - 1][0][L] = A.x; sh.pt[wave - 1][1][L] = A.y; sh.pt[wave - 1][2][L] = A.z; }
+    if (L == 0u) sh.pinf[wave - 1] = inf ? 1u : 0u;
+  }
+  __syncthreads();
+  if (wave != 0u) return;
+#pragma unroll 1
+  for (int j = 0; j < 4; ++j) {
+    gjsl O;
+    O.x = lo ? sh.pt[j][0][L] : 0u;
+    O.y = lo ? sh.pt[j][1][L] : 0u;
+    O.z = lo ? sh.pt[j][2][L] : 0u;
+    gj4_add_gej(A, inf, O, sh.pinf[j] != 0u, row, k);
+  }
+  LAT_STAMP(6);
+  // ---- final check (as k_verify_lat_sl): x(R) mod n == r, without inversion
+  const bool ok = sh.okp != 0u;
+  const u32 fl = sh.oks[0];
+  bool okv = (fl & 1u) && ok && !inf;
+  u32 rw[8], X[8], T[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rw[i] = sh.r[0][i];
+  const u32 zz = fsl_sqr(A.z, k);
+  fsl_to_words(X, A.x);
+  fsl_to_words(T, fsl_mul(fsl_from_words(rw, k), zz, k));
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) eq &= (X[i] == T[i]);
+  if (!eq && (fl & 2u)) {
+    u32 rn[8], c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rn[i] = __builtin_addc(rw[i], kN[i], c, &c);
+    fsl_to_words(T, fsl_mul(fsl_from_words(rn, k), zz, k));
+    eq = true;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) eq &= (X[i] == T[i]);
+  }
+  okv &= eq;
+  if (threadIdx.x == 0) {
+    if (b.out8) b.out8[gi] = okv ? 1u : 0u;
+    else if (okv) atomicOr((unsigned long long*)&b.bits[gi >> 6], 1ull << (gi & 63u));
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Keyed small batches on the limb-sliced layer: ONE signature per 256-thread
 // block.  Lane 0 runs the scalar chain; then wave g (window group g of
 // k_verify_lat16) row r accumulates part r of {k1q Q, k2q lambda Q, k1g G,
@@ -1047,6 +1316,7 @@ __global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
 // wave 0) the whole sum, and wave 0 runs the final check.
 struct Lat16SlShared {
   static constexpr bool kG5 = true;
+  static constexpr bool kG24 = false;
   u32 eh[8];                                // message path: the SHA-256 state of the sign bytes (wave 1)
   u32 dq[1][GV_QWIN];
   u32 dg5[1][GV_QWIN];
@@ -1220,6 +1490,10 @@ extern "C" hipError_t gvk_verify_lat_sl(const gvk_lat* b, hipStream_t st) {
     if (e != hipSuccess) return e;
   }
   if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
+  if (b->gtab6) {                                      // the caller's choice (lat_rows_max)
+    hipLaunchKernelGGL(gv::k_verify_lat_sl4, dim3(b->n), dim3(256), 0, st, *b);
+    return hipGetLastError();
+  }
   const uint32_t threads = b->n <= GV_LAT_SL_SPLIT ? 192u : 128u;
   hipLaunchKernelGGL(gv::k_verify_lat_sl, dim3(b->n), dim3(threads), 0, st, *b);
   return hipGetLastError();

@@ -550,6 +550,7 @@ struct gv_ctx {
   bool lat_zero_copy = true;    // host-buffer batches on the sliced kernels read the pinned staging buffer and write
                                 // verdict bytes to pinned memory directly: no H2D, memset or D2H (GV_LAT_ZC=0: A/B)
   bool lat_sliced = true;       // small batches on k_verify_lat_sl / k_verify_lat16_sl (GV_LAT_SLICED=0: the one-lane-field kernels, A/B)
+  size_t lat_rows_max = 512;     // pub33 small batches of at most this many: k_verify_lat_sl4 (rows of a wave on one accumulator, G from gtab6); 0: k_verify_lat_sl
   bool keyed_k4 = true;         // keyed batches on k_ecmult_k4 (GV_KEYED_K4=0: the 125-doubling ladder, A/B)
   bool gfull = true;            // k4 batches take G on the unsplit scalar: 11 25-bit windows instead of 14 20-bit
                                 // GLV windows (k_ecmult_k4<true>, 6 GiB of tables; GV_GFULL=0: A/B)
@@ -897,6 +898,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     lb.msg_blob = blob; lb.msg_off = off; lb.msg_len = len;
     lb.gtab = d->gtab; lb.e_soa = s->in_e; lb.bits = bits_out;
     lb.ev[0] = b.ev[0];
+    if (!kslot && n <= ctx->lat_rows_max) lb.gtab6 = d->gtab6;   // k_verify_lat_sl4 (null: not built)
     if (kslot) {
       lb.pub33 = nullptr;
       lb.kslot = kslot; lb.kqt = b.kqt; lb.kzq = b.kzq; lb.kok = b.kok; lb.kC = b.kC; lb.kcount = b.kcount;
@@ -1784,6 +1786,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* eg = getenv("GV_ED_GROUP")) ctx->ed_group = strcmp(eg, "0") != 0;
   if (const char* es = getenv("GV_ED_KEYS_SPLIT")) ctx->ed_keys_split = strcmp(es, "0") != 0;
   if (const char* ls = getenv("GV_LAT_SLICED")) ctx->lat_sliced = strcmp(ls, "0") != 0;
+  if (const char* lr = getenv("GV_LAT_ROWS_MAX")) ctx->lat_rows_max = (size_t)strtoull(lr, nullptr, 10);
   if (const char* zc = getenv("GV_LAT_ZC")) ctx->lat_zero_copy = strcmp(zc, "0") != 0;
   if (const char* pl = getenv("GV_PIPELINE")) ctx->pipeline_dev = strcmp(pl, "0") != 0;
   if (const char* gk = getenv("GV_GROUP_KEYS")) ctx->group_keys = strcmp(gk, "0") != 0;
@@ -2510,6 +2513,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "lat_sliced")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->lat_sliced = val != 0;
+  } else if (!strcmp(key, "lat_rows_max")) {
+    if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
+    ctx->lat_rows_max = (size_t)val;
   } else if (!strcmp(key, "max_batch")) {
     if (val < 256 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
     ctx->max_batch = round_up((size_t)val, 256);

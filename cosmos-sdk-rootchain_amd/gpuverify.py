@@ -27,6 +27,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # crossover and the sliced / four-lanes-per-signature small-batch crossover
 LAT_MAX_DEFAULT = 8192
 LAT_SL_MAX_DEFAULT = 2048
+LAT_ROWS_MAX_DEFAULT = 512        # pub33 batches up to this many: k_verify_lat_sl4 ("lat_rows_max")
 # keyed batches: their own defaults (setting "lat_max" / "lat_sl_max" sets the keyed ones too)
 LAT_MAX_KEYED_DEFAULT = 14336
 LAT_SL_MAX_KEYED_DEFAULT = 1536
@@ -233,6 +234,7 @@ class Verifier:
         self.set_option("lat_sl_max", LAT_SL_MAX_DEFAULT)
         self.set_option("lat_max_keyed", LAT_MAX_KEYED_DEFAULT)
         self.set_option("lat_sl_max_keyed", LAT_SL_MAX_KEYED_DEFAULT)
+        self.set_option("lat_rows_max", LAT_ROWS_MAX_DEFAULT)
 
     def set_option(self, key: str, val: int):
         _check(self._L.gv_set_option(self._ctx, key.encode(), int(val)), f"gv_set_option({key})")

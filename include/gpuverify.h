@@ -223,6 +223,10 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * per signature, and the 16-lanes-per-signature keyed kernel beats the keyed
  * pipeline to ~14k; setting "lat_max" / "lat_sl_max" sets these too),
  * "lat_sliced" (0/1: 0 never takes the sliced kernels; default 1),
+ * "lat_rows_max" (pub33 sliced batches of at most this many items take
+ * k_verify_lat_sl4: five waves per signature, each ladder wave's four rows on
+ * one accumulator, G from the k6 tables after the ladder; default 512, 0 =
+ * never, env GV_LAT_ROWS_MAX),
  * "lat_zero_copy" (0/1: host-buffer digest batches on the sliced kernels
  * are read by the kernel straight from the pinned staging buffer and answered
  * as verdict bytes in pinned memory -- no H2D, memset or D2H; default 1),

@@ -187,21 +187,25 @@ def test_point_double(ver):
 
 
 # ------------------------------------------------------------ full verification
-# Three schedules compute every verdict: the throughput pipeline
-# (gv_kernels.hip, one lane per signature), the small-batch kernel on the
-# limb-sliced field layer (k_verify_lat_sl: one signature per block, one field
-# element per 16-lane row; the default) and the one-lane-field small-batch
-# kernel (k_verify_lat: four lanes per signature); "lat_max" and "lat_sliced"
-# pick one per call.
-PATHS = {"throughput": (0, 1), "latency": (1 << 30, 1), "latency_onelane": (1 << 30, 0)}  # (lat_max, sliced)
+# Four schedules compute every verdict: the throughput pipeline
+# (gv_kernels.hip, one lane per signature), the small-batch kernels on the
+# limb-sliced field layer (one signature per block, one field element per
+# 16-lane row: k_verify_lat_sl, and k_verify_lat_sl4 whose ladder waves keep
+# one accumulator in four rows, G from the 24-bit tables -- the default up to
+# "lat_rows_max") and the one-lane-field small-batch kernel (k_verify_lat:
+# four lanes per signature); "lat_max", "lat_sliced" and "lat_rows_max" pick
+# one per call.
+PATHS = {"throughput": (0, 1, 0), "latency": (1 << 30, 1, 0), "latency_rows": (1 << 30, 1, 1 << 30),
+         "latency_onelane": (1 << 30, 0, 0)}  # (lat_max, sliced, rows)
 
 
 @pytest.fixture(params=sorted(PATHS))
 def path(request, ver):
-    lat_max, sliced = PATHS[request.param]
+    lat_max, sliced, rows = PATHS[request.param]
     ver.set_option("lat_max", lat_max)
     ver.set_option("lat_sliced", sliced)
     ver.set_option("lat_sl_max", 1 << 30)
+    ver.set_option("lat_rows_max", rows)
     yield request.param
     ver.reset_schedule()
     ver.set_option("lat_sliced", 1)
@@ -437,7 +441,7 @@ def test_option_bounds(ver):
 
 
 def test_sliced_latency_kernels_at_scale(ver):
-    """k_verify_lat_sl (pub33) and k_verify_lat16_sl (keyed) far past their
+    """k_verify_lat_sl and k_verify_lat_sl4 (pub33) and k_verify_lat16_sl (keyed) far past their
     production batch size: 262,144 mixed signatures (25 % invalid over the
     generator's six classes, 4,096 keys) forced through the small-batch
     schedule, against the verdicts the generator constructed, and a sample
@@ -451,9 +455,11 @@ def test_sliced_latency_kernels_at_scale(ver):
     ver.set_option("lat_max", 1 << 30)
     ver.set_option("lat_sl_max", 1 << 30)
     try:
-        got = ver.verify_batch_digests(pub, sig, dig)
-        bad = np.nonzero(got != exp)[0]
-        assert bad.size == 0, bad[:20]
+        for rows in (0, 1 << 30):                            # k_verify_lat_sl, k_verify_lat_sl4
+            ver.set_option("lat_rows_max", rows)
+            got = ver.verify_batch_digests(pub, sig, dig)
+            bad = np.nonzero(got != exp)[0]
+            assert bad.size == 0, (rows, bad[:20])
         slots = ver.keys_load(uniq)[inv.reshape(-1)]
         got = ver.verify_batch_digests_keyed(slots, sig, dig)
         bad = np.nonzero(got != exp)[0]

@@ -11,8 +11,8 @@ exceptional additions and Booth-extreme windows, e in {0, n, n+1, 2^256-1}),
 so the million-scale mix covers every acceptance and rejection rule.
 
 Every chunk runs the throughput schedule (the headline path); one more 1M
-chunk runs through the limb-sliced small-batch kernels (k_verify_lat_sl by
-pub33, k_verify_lat16_sl keyed) with the small-batch bounds lifted.  The GPU
+chunk runs through the limb-sliced small-batch kernels (k_verify_lat_sl and
+k_verify_lat_sl4 by pub33, k_verify_lat16_sl keyed) with the small-batch bounds lifted.  The GPU
 bitmaps are compared in full with the verdicts known by construction, and
 all special cases plus a random 20k sample per chunk with the C oracle.  A
 JSON summary goes to GV_PARITY_OUT when set.  GV_PARITY_MILLIONS=0 skips.
@@ -76,16 +76,22 @@ def test_parity_millions():
             else:
                 ver.set_option("lat_max", 1 << 30)       # every batch size through the sliced kernels
                 ver.set_option("lat_sl_max", 1 << 30)
+                ver.set_option("lat_rows_max", 0)        # k_verify_lat_sl
                 got = ver.verify_batch_digests(pub, sig, dig)
+                ver.set_option("lat_rows_max", 1 << 30)  # k_verify_lat_sl4
+                gr = ver.verify_batch_digests(pub, sig, dig)
+                ver.set_option("lat_rows_max", gvm.LAT_ROWS_MAX_DEFAULT)
                 uniq, inv = np.unique(pub, axis=0, return_inverse=True)
                 slots = ver.keys_load(np.ascontiguousarray(uniq))[inv.reshape(-1)]
                 gk = ver.verify_batch_digests_keyed(np.ascontiguousarray(slots, np.uint32), sig, dig)
                 ver.keys_reset()
                 m1, o1, checked = check_chunk(ver, O, rng, pub, sig, dig, exp, pos, threads, got)
                 m2, o2, _ = check_chunk(ver, O, rng, pub, sig, dig, exp, pos, threads, gk)
-                rec.update({"schedule": "sliced pub33 + sliced keyed", "mismatch": m1 + m2, "oracle_mismatch": o1 + o2,
-                            "mismatch_pub33": m1, "mismatch_keyed": m2})
-                n_items = 2 * n
+                m3, o3, _ = check_chunk(ver, O, rng, pub, sig, dig, exp, pos, threads, gr)
+                rec.update({"schedule": "sliced pub33 (lat_sl, lat_sl4) + sliced keyed", "mismatch": m1 + m2 + m3,
+                            "oracle_mismatch": o1 + o2 + o3, "mismatch_pub33": m1, "mismatch_keyed": m2,
+                            "mismatch_pub33_rows": m3})
+                n_items = 3 * n
             summary["chunks"].append(rec)
             summary["items"] += n if not sliced else n_items
             summary["mismatch_vs_construction"] += rec["mismatch"]

@@ -24,9 +24,11 @@ def main():
     n = 64
     pub, sig, dig, exp = bench.make_digest_workload(4096, 0xC5, 256, 0.0, 16)
     ver = gvm.Verifier([0])
+    rows = int(sys.argv[1]) if len(sys.argv) > 1 else 0     # 1: k_verify_lat_sl4 (mark 7: G sum done)
+    ver.set_option("lat_rows_max", 1 << 30 if rows else 0)
     L = gvm._lib
     L.gv_debug_lat_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    rows = []
+    acc = []
     for r in range(40):
         o = r * n
         got = ver.verify_batch_digests(pub[o:o + n], sig[o:o + n], dig[o:o + n])
@@ -34,11 +36,13 @@ def main():
         tr = np.zeros((n, 8), np.uint64)
         assert L.gv_debug_lat_trace(tr.ctypes.data, n) == 0
         t = tr.astype(np.int64)
-        rows.append((t - t[:, :1]) * 0.01)            # 100 MHz ticks -> us from the block's start
-    a = np.concatenate(rows[5:])
+        acc.append((t - t[:, :1]) * 0.01)            # 100 MHz ticks -> us from the block's start
+    a = np.concatenate(acc[5:])
     med = np.median(a, 0)
     ver.close()
-    print(json.dumps({k: round(float(v), 2) for k, v in zip(MARKS, med)}))
+    marks = MARKS[:7] + (["g_sum_done(wave1)"] if rows else MARKS[7:])
+    print(json.dumps({"kernel": "k_verify_lat_sl4" if rows else "k_verify_lat_sl",
+                      **{k: round(float(v), 2) for k, v in zip(marks, med)}}))
 
 
 if __name__ == "__main__":
