@@ -798,16 +798,13 @@ struct LatSlShared {
   u32 pinf;
 };
 
-// Wave 0 of k_verify_lat_sl: key decompression, Q / lambda*Q tables into LDS,
-// zq (Z of the table's curve) and the ParsePubKey verdict into LDS.
-template <class SH>
-GV_DEV void lat_sl_prep(SH& sh, const gvk_lat& b, u32 gi, const fslk& k) {
-  const u32 row = (threadIdx.x >> 4) & 3u, L = k.L;
-  const bool lo = L < 9u;
+// Key decompression (btcec ParsePubKey): the ParsePubKey verdict and (x, y),
+// with G standing in for an invalid key.
+GV_DEV bool lat_sl_decompress(fe& x8, fe& y8, const gvk_lat& b, u32 gi, const fslk& k) {
+  const u32 L = k.L;
   // ---- pubkey: btcec ParsePubKey / decompressPoint
   const uint8_t* p = b.pub33 + (size_t)gi * 33u;
   const u32 pre = p[0];
-  fe x8, y8;
 #pragma unroll
   for (int i = 0; i < 8; ++i) x8.v[i] = be32(p + 1 + 4 * (7 - i));
   bool ok = (pre & 0xFEu) == 0x02u;
@@ -842,7 +839,15 @@ GV_DEV void lat_sl_prep(SH& sh, const gvk_lat& b, u32 gi, const fslk& k) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) { x8.v[i] = gx[i]; y8.v[i] = gy[i]; }
   }
-  const u32 qx = fsl_from_words(x8.v, k), qy = fsl_from_words(y8.v, k);
+  return ok;
+}
+
+// Q / lambda*Q tables of the point (qx, qy) into LDS and zq (Z of the
+// tables' curve), for a whole wave.
+template <class SH>
+GV_DEV void lat_sl_tables(SH& sh, u32 qx, u32 qy, const fslk& k) {
+  const u32 row = (threadIdx.x >> 4) & 3u, L = k.L;
+  const bool lo = L < 9u;
   // ---- Q table: co-Z chain (as build_q_table / lat_pubkey_and_tables), row 0 stores
   const bool st = row == 0u && lo;
   u32 X1, Y1, X2, Y2;
@@ -911,6 +916,16 @@ GV_DEV void lat_sl_prep(SH& sh, const gvk_lat& b, u32 gi, const fslk& k) {
   }
   const u32 zq = fsl_mul(qy << 1, acc, k);              // Z_15 = 2y * prod(ratios)
   if (row == 0u && lo) sh.zq[L] = zq;
+}
+
+
+// Wave 0 of k_verify_lat_sl: key decompression, Q / lambda*Q tables into LDS,
+// zq (Z of the table's curve) and the ParsePubKey verdict into LDS.
+template <class SH>
+GV_DEV void lat_sl_prep(SH& sh, const gvk_lat& b, u32 gi, const fslk& k) {
+  fe x8, y8;
+  const bool ok = lat_sl_decompress(x8, y8, b, gi, k);
+  lat_sl_tables(sh, fsl_from_words(x8.v, k), fsl_from_words(y8.v, k), k);
   if (threadIdx.x == 0) sh.okp = ok ? 1u : 0u;
   LAT_STAMP(2);                                         // trace builds: tables done
 }
@@ -1056,29 +1071,52 @@ __global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
 // each other run in different rows at once and every row gets every row's
 // result from three lane swaps (v_permlane16_swap, v_permlane32_swap: VALU,
 // no LDS round trip), so a doubling is 3 product rounds instead of 7 serial
-// products and an addition 5 instead of 11.  Four ladder waves, one per SIMD:
-// Q and lambda*Q, even and odd windows (each 125 doublings, 13 windows'
-// additions).  G is added on its own, from the 2^23-entry tables of
-// 2^(24 j) G (gtab6: u1 unsplit, 11 signed 24-bit windows, no doublings), by
-// the scalar wave right after the scalar chain, inside the time the key
-// decompression and tables take on wave 0.  Same checks, group law results
-// (every exceptional case as gjsl_add_scaled / gjsl_add_gej) and verdict as
-// k_verify_lat_sl.
+// products and an addition 5 instead of 11.
+//
+// The key's square root is off the critical path: with c = x^3 + 7 the point
+// Q' = (c x, c^2) lies on E': Y^2 = X^3 + 7 c^3, the image of Q = (x, y) under
+// (x, y) -> (u^2 x, u^3 y) with u = y (u^2 = c), and doubling / addition
+// formulas of a = 0 curves never read b: the Q / lambda*Q tables and ladders
+// run on Q' as soon as c is known, and a Jacobian (X, Y, Z) of E' is the point
+// (X, Y, y Z) of E.  The square root (ParsePubKey's "invalid square root" and
+// y's parity) runs on its own wave meanwhile and only y joins at the end.
+//
+// Waves (one per SIMD), started by LDS flags instead of a block barrier:
+//   0: c, tables of Q' (LDS) -> Q ladder, even windows -> the combination
+//   1: scalar chain (digits, r) -> lambda*Q ladder, windows 13..25
+//   2: (message path: SHA-256 of the sign bytes, handed to wave 1's chain
+//      after s^-1) -> Q ladder, odd windows
+//   3: square root -> G sum (gtab6: u1 unsplit, 11 signed 24-bit windows, no
+//      doublings) -> lambda*Q ladder, windows 0..12 (60 doublings)
+// Same checks, group law results (every exceptional case as gjsl_add_scaled /
+// gjsl_add_gej, mapped through the isomorphism) and verdict as k_verify_lat_sl.
 struct LatSl4Shared {
   static constexpr bool kG5 = false;
   static constexpr bool kG24 = true;
-  u32 qtab[2][GV_QTAB_N][18];               // Q, lambda*Q entries (effective affine, sliced limbs)
+  u32 qtab[2][GV_QTAB_N][18];               // Q', lambda*Q' entries (effective affine, sliced limbs)
   u32 ratio[GV_QTAB_N - 1][9];
   u32 dq[1][GV_QWIN];
   int dg24[1][GV_K6_GWIN];                  // u1's 24-bit Booth digits
   u32 r[1][8];
   u32 oks[1];
   u32 zq[16];
-  u32 okp;
+  u32 okp;                                  // ParsePubKey verdict (wave 3)
+  u32 ysl[16];                              // y (wave 3)
   u32 pt[4][3][16];                         // the partial sums of waves 1, 2, 3 and the G sum
   u32 pinf[4];
   u32 gent[GV_K6_GWIN][18];                 // the G entries (x, +-y), sliced
+  u32 eh[8];                                // message path: SHA-256 of the sign bytes (wave 2)
+  u32 flag_tab, flag_sc, flag_e;            // tables / scalars / digest ready
 };
+
+GV_DEV void lds_flag_set(u32* f) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+GV_DEV void lds_flag_wait(u32* f) {
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(2);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 
 // The four rows' values of v, each in every row: r[i] = row i's v.
 struct rows4 { u32 r[4]; };
@@ -1198,20 +1236,51 @@ __global__ __launch_bounds__(256) void k_verify_lat_sl4(const gvk_lat b) {
   const fslk k = fsl_consts();
   const u32 row = (threadIdx.x >> 4) & 3u, L = k.L;
   const bool lo = L < 9u;
+  if (threadIdx.x == 0) { sh.flag_tab = 0u; sh.flag_sc = 0u; sh.flag_e = 0u; }
+  __syncthreads();
+  if (wave == 0u) LAT_STAMP(0);
   gjsl A;
   A.x = 0u; A.y = 0u; A.z = 0u;
   bool inf = true;
-  if (wave == 0u) LAT_STAMP(0);
-  if (wave == 1u) {                                     // the scalar chain (and the hash), then G
-    if (b.msg_len) {
-      u32 eh[8];
-      sha256_msg_wave(eh, b.msg_blob + b.msg_off[gi], b.msg_len[gi]);
-      lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, nullptr, nullptr, b.C, gi, eh);
+  if (wave == 0u) {                                     // tables of Q' = (c x, c^2)
+    const uint8_t* p = b.pub33 + (size_t)gi * 33u;
+    u32 xw[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xw[i] = be32(p + 1 + 4 * (7 - i));
+    const u32 xs = fsl_from_words(xw, k);
+    const u32 c = fsl_mul(fsl_sqr(xs, k), xs, k) + (L == 0u ? 7u : 0u);
+    lat_sl_tables(sh, fsl_mul(c, xs, k), fsl_sqr(c, k), k);
+    LAT_STAMP(2);                                       // trace builds: tables done
+    lds_flag_set(&sh.flag_tab);
+  } else if (wave == 1u) {                              // the scalar chain
+    if (b.msg_len) {                                    // e from wave 2's hash, first needed after s^-1
+      lat_scalars_e<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, [&](u32 e[8]) {
+        lds_flag_wait(&sh.flag_e);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = sh.eh[7 - i];
+      });
     } else {
       lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.dig32 + (size_t)gi * 32u, nullptr, b.C, gi);
     }
     LAT_STAMP(3);                                       // trace builds: scalars done
-    wave_lds_sync();
+    lds_flag_set(&sh.flag_sc);
+  } else if (wave == 2u) {                              // message path: the hash, beside s^-1
+    if (b.msg_len) {
+      u32 eh[8];
+      sha256_msg_wave(eh, b.msg_blob + b.msg_off[gi], b.msg_len[gi]);
+      if (threadIdx.x == 128u) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sh.eh[i] = eh[i];
+      }
+      lds_flag_set(&sh.flag_e);
+    }
+  } else if (wave == 3u) {                              // ParsePubKey's square root, then G
+    fe x8, y8;
+    const bool ok = lat_sl_decompress(x8, y8, b, gi, k);
+    const u32 y = fsl_from_words(y8.v, k);
+    if (row == 0u && lo) sh.ysl[L] = y;
+    if (threadIdx.x == 192u) sh.okp = ok ? 1u : 0u;
+    lds_flag_wait(&sh.flag_sc);
     // G = sum of d_j (2^(24 j) G): every entry's loads in flight at once,
     // parked in LDS (row j & 3 stores entry j)
 #pragma unroll
@@ -1219,8 +1288,8 @@ __global__ __launch_bounds__(256) void k_verify_lat_sl4(const gvk_lat b) {
       const int d = sh.dg24[0][j];
       const u32 e = d == 0 ? 0u : (u32)((d < 0 ? -d : d) - 1);
       const u32* pe = b.gtab6 + ((size_t)j * GV_K6_GTAB_N + e) * 16u;
-      const u32 x = fsl_load_words(pe, k), y = fsl_load_words(pe + 8, k);
-      if (row == (u32)(j & 3) && lo) { sh.gent[j][L] = x; sh.gent[j][9 + L] = d < 0 ? k.bias - y : y; }
+      const u32 x = fsl_load_words(pe, k), yv = fsl_load_words(pe + 8, k);
+      if (row == (u32)(j & 3) && lo) { sh.gent[j][L] = x; sh.gent[j][9 + L] = d < 0 ? k.bias - yv : yv; }
     }
     wave_lds_sync();
 #pragma unroll 1
@@ -1235,22 +1304,23 @@ __global__ __launch_bounds__(256) void k_verify_lat_sl4(const gvk_lat b) {
     LAT_STAMP(7);                                       // trace builds: G sum done
     A.x = 0u; A.y = 0u; A.z = 0u;
     inf = true;
-  } else if (wave == 0u) {
-    lat_sl_prep(sh, b, gi, k);                          // the key and its tables
   }
-  __syncthreads();                                      // digits, G sum (wave 1), tables + zq (wave 0)
+  lds_flag_wait(&sh.flag_tab);
+  lds_flag_wait(&sh.flag_sc);
   if (wave == 0u) LAT_STAMP(4);
   {
-    // Q (waves 0, 2) or lambda*Q (waves 3, 1), even (waves 0, 3) or odd (2, 1) windows
-    const int par = (wave == 0u || wave == 3u) ? 0 : 1;
+    // wave 0: Q even windows, 2: Q odd, 1: lambda*Q windows 13..25, 3: lambda*Q windows 0..12
     const int tab = (wave == 0u || wave == 2u) ? 0 : 1;
+    const int top = wave == 3u ? GV_QWIN / 2 - 1 : GV_QWIN - 1;
 #pragma unroll 1
-    for (int win = GV_QWIN - 1; win >= 0; --win) {
-      if (win != GV_QWIN - 1 && !inf) {
+    for (int win = top; win >= 0; --win) {
+      if (win != top && !inf) {
 #pragma unroll 1
         for (int dd = 0; dd < GV_QW; ++dd) gj4_double(A, row, k);
       }
-      if ((win & 1) != par) continue;
+      const bool mine = wave == 0u ? (win & 1) == 0 : wave == 2u ? (win & 1) == 1
+                      : wave == 1u ? win >= GV_QWIN / 2 : true;
+      if (!mine) continue;
       const u32 dq = sh.dq[0][win];
       const int d = tab == 0 ? ((int)(dq << 16) >> 16) : ((int)dq >> 16);
       if (d == 0) continue;
@@ -1259,7 +1329,6 @@ __global__ __launch_bounds__(256) void k_verify_lat_sl4(const gvk_lat b) {
       const u32 y = lo ? sh.qtab[tab][e][9 + L] : 0u;
       gj4_add_affine(A, inf, x, d < 0 ? k.bias - y : y, row, k);
     }
-    if (!inf) A.z = fsl_mul(A.z, lo ? sh.zq[L] : 0u, k);   // back to the real curve
   }
   if (wave == 0u) LAT_STAMP(5);
   if (wave != 0u && row == 0u) {                        // partial sums into LDS, wave 0 adds them
@@ -1268,8 +1337,10 @@ __global__ __launch_bounds__(256) void k_verify_lat_sl4(const gvk_lat b) {
   }
   __syncthreads();
   if (wave != 0u) return;
+  // the Q' partial sums (the tables' curve), then back to E: Z * zq * y
 #pragma unroll 1
   for (int j = 0; j < 4; ++j) {
+    if (j == 3 && !inf) A.z = fsl_mul(A.z, fsl_mul(lo ? sh.zq[L] : 0u, lo ? sh.ysl[L] : 0u, k), k);
     gjsl O;
     O.x = lo ? sh.pt[j][0][L] : 0u;
     O.y = lo ? sh.pt[j][1][L] : 0u;

@@ -25,8 +25,13 @@ def main():
     n_all = 4096
     pub, sig, (blob, off, ln), exp = X.c1_items(bench.workload_lib(), n_all, 16, 1024)
     ver = gvm.Verifier([0])
+    if len(sys.argv) > 1:                      # lat_rows_max (0: k_verify_lat_sl for pub33)
+        ver.set_option("lat_rows_max", int(sys.argv[1]))
+        out0 = {"lat_rows_max": int(sys.argv[1])}
+    else:
+        out0 = {}
     slots = ver.keys_load(pub[:1024])[np.arange(n_all) % 1024]
-    out = {"mean_msg_bytes": round(float(ln.mean()), 1)}
+    out = {**out0, "mean_msg_bytes": round(float(ln.mean()), 1)}
     for n in (1, 16, 64, 256, 1024):
         got = ver.verify_batch_msgs(pub[:n], sig[:n], (blob, off[:n], ln[:n]))
         assert np.array_equal(got, exp[:n])
