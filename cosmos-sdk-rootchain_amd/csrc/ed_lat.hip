@@ -21,6 +21,11 @@
 //                doublings at all --, two shuffle rounds per wave and two more
 //                in wave 0 sum the rows, and R' == (x_R, y_R) is checked
 //                projectively.
+//   k_ed_lat_unc small batches against UNCACHED keys (first-seen multisig
+//                sub-keys, gv_verify_ed25519_msgs up to "ed_unc_lat_max"):
+//                FromBytes(A) and j (-A) in the kernel, the 252-doubling
+//                ladder on four waves with one point per wave spread over its
+//                rows (see the kernel's comment).
 #include <hip/hip_runtime.h>
 
 #include "ed_fsl.cuh"
@@ -146,6 +151,63 @@ struct EdlShared {
   u32 pt[4][4][16];                         // wave sums X, Y, Z, T
 };
 
+// Wave-wide: h = SHA-512(R || A || M) mod L and its 64 signed radix-16 digits
+// into sh.hd; sw = the signature words, aw = A's words (the bytes Verify hashes).
+template <class SH>
+GV_DEV void edl_hash_digits(SH& sh, const u32 sw[16], const u32 aw[8], const uint8_t* m, u32 len, u32 lane) {
+  // the message staged in LDS first (one load per lane per 64 bytes instead
+  // of a serial byte stream)
+  const u32 total = 64u + len, nblocks = (total + 17u + 127u) >> 7, padded = nblocks << 7;
+  u32 dig[16], h[8];
+  if (padded <= EDL_MSG_LDS) {
+    // the whole SHA-512 input -- R || A || M, 0x80, zeros, the 128-bit
+    // big-endian bit length -- laid out in LDS by the wave (one load per
+    // lane per 64 message bytes); the compression then reads each block's
+    // sixteen 64-bit words with uniform addresses and runs on the scalar unit
+    if (lane < 8u) sh.pre[lane] = sw[lane];
+    else if (lane < 16u) sh.pre[lane] = aw[lane - 8u];
+    const uint64_t bits = (uint64_t)total * 8u;
+    for (u32 i = 64u + lane; i < padded; i += 64u) {
+      u32 byte = 0;
+      if (i < total) byte = m[i - 64u];
+      else if (i == total) byte = 0x80u;
+      else if (i >= padded - 8u) byte = (u32)(bits >> (8u * (padded - 1u - i))) & 0xFFu;
+      sh.msg[i] = (uint8_t)byte;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    uint64_t hs[8] = {0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull, 0x3c6ef372fe94f82bull, 0xa54ff53a5f1d36f1ull,
+                      0x510e527fade682d1ull, 0x9b05688c2b3e6c1full, 0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull};
+#pragma unroll 1
+    for (u32 blk = 0; blk < nblocks; ++blk) {
+      uint64_t w[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = __builtin_bswap64(sh.words[blk * 16u + (u32)j]);
+      sha512_compress(hs, w);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      dig[2 * i] = __builtin_bswap32((u32)(hs[i] >> 32));
+      dig[2 * i + 1] = __builtin_bswap32((u32)hs[i]);
+    }
+  } else {                                            // long messages: byte stream from memory
+    u32 pre[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      pre[i] = sw[i];
+      pre[8 + i] = aw[i];
+    }
+    sha512_pre64(dig, pre, [=](u32 i) { return (u32)m[i]; }, len);
+  }
+  sc_reduce512(h, dig);
+  const uint64_t car = sc_radix16_carries(h);
+  const u32 nib = (h[lane >> 3] >> (4u * (lane & 7u))) & 15u;
+  const int cin = lane > 0u ? (int)((car >> (lane - 1u)) & 1u) : 0;
+  const int cout = lane < 63u ? (int)((car >> lane) & 1u) : 0;
+  sh.hd[lane] = (int)nib + cin - 16 * cout;
+}
+
 __global__ __launch_bounds__(256) void k_ed_lat_sl(const gvk_edl b) {
   __shared__ EdlShared sh;
   const u32 gi = blockIdx.x;                // grid = n: every block is live
@@ -169,59 +231,10 @@ __global__ __launch_bounds__(256) void k_ed_lat_sl(const gvk_edl b) {
   gesl A;
   gesl_identity(A, k);
   if (wave == 0u) {
-    // h = SHA-512(R || A || M) mod L; the message staged in LDS first (one
-    // load per lane per 64 bytes instead of a serial byte stream)
-    const uint8_t* m = b.msg_blob ? b.msg_blob + b.msg_off[gi] : nullptr;
-    const u32 len = b.msg_len[gi];
-    const u32 total = 64u + len, nblocks = (total + 17u + 127u) >> 7, padded = nblocks << 7;
-    u32 dig[16], h[8];
-    if (padded <= EDL_MSG_LDS) {
-      // the whole SHA-512 input -- R || A || M, 0x80, zeros, the 128-bit
-      // big-endian bit length -- laid out in LDS by the wave (one load per
-      // lane per 64 message bytes); the compression then reads each block's
-      // sixteen 64-bit words with uniform addresses and runs on the scalar unit
-      if (lane < 8u) sh.pre[lane] = sw[lane];
-      else if (lane < 16u) sh.pre[lane] = b.kpub[(size_t)sl * 8 + (lane - 8u)];
-      const uint64_t bits = (uint64_t)total * 8u;
-      for (u32 i = 64u + lane; i < padded; i += 64u) {
-        u32 byte = 0;
-        if (i < total) byte = m[i - 64u];
-        else if (i == total) byte = 0x80u;
-        else if (i >= padded - 8u) byte = (u32)(bits >> (8u * (padded - 1u - i))) & 0xFFu;
-        sh.msg[i] = (uint8_t)byte;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      uint64_t hs[8] = {0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull, 0x3c6ef372fe94f82bull, 0xa54ff53a5f1d36f1ull,
-                        0x510e527fade682d1ull, 0x9b05688c2b3e6c1full, 0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull};
-#pragma unroll 1
-      for (u32 blk = 0; blk < nblocks; ++blk) {
-        uint64_t w[16];
+    u32 aw[8];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) w[j] = __builtin_bswap64(sh.words[blk * 16u + (u32)j]);
-        sha512_compress(hs, w);
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        dig[2 * i] = __builtin_bswap32((u32)(hs[i] >> 32));
-        dig[2 * i + 1] = __builtin_bswap32((u32)hs[i]);
-      }
-    } else {                                            // long messages: byte stream from memory
-      u32 pre[16];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        pre[i] = sw[i];
-        pre[8 + i] = b.kpub[(size_t)sl * 8 + i];
-      }
-      sha512_pre64(dig, pre, [=](u32 i) { return (u32)m[i]; }, len);
-    }
-    sc_reduce512(h, dig);
-    const uint64_t car = sc_radix16_carries(h);
-    const u32 nib = (h[lane >> 3] >> (4u * (lane & 7u))) & 15u;
-    const int cin = lane > 0u ? (int)((car >> (lane - 1u)) & 1u) : 0;
-    const int cout = lane < 63u ? (int)((car >> lane) & 1u) : 0;
-    sh.hd[lane] = (int)nib + cin - 16 * cout;
+    for (int i = 0; i < 8; ++i) aw[i] = b.kpub[(size_t)sl * 8 + i];
+    edl_hash_digits(sh, sw, aw, b.msg_blob ? b.msg_blob + b.msg_off[gi] : nullptr, b.msg_len[gi], lane);
   } else if (wave == 1u) {
     u32 x, y;
     const bool rok = efsl_decode_strict(x, y, sw, k);
@@ -299,6 +312,276 @@ __global__ __launch_bounds__(256) void k_ed_lat_sl(const gvk_edl b) {
   for (int i = 0; i < 8; ++i) diff |= (w1[i] ^ w2[i]) | (w3[i] ^ w4[i]);
   const bool ok = kok && (sh.flags & 3u) == 3u && diff == 0u;
   if (threadIdx.x == 0) b.out8[gi] = ok ? 1u : 0u;
+}
+
+// ---------------------------------------------------------------------------
+// Small batches against UNCACHED keys (k_ed_lat_unc): one signature per
+// 256-thread block, FromBytes(A) in the kernel, and every wave keeps ONE
+// point in its four 16-lane rows with each row computing a different product
+// of the same round (rows_all, secp_fsl.cuh): an a = -1 doubling is two
+// rounds of four products (X^2, Y^2, Z^2, (X+Y)^2, then E F, G H, E H, F G),
+// an addition of a cached point two rounds as well.
+//   wave 0: h = SHA-512(R || A || M) mod L, its radix-16 digits -> ladder
+//           windows 4j
+//   wave 1: FromBytes(A) (the reference's lenient decode) -> j (-A), j = 1..8,
+//           cached form, into LDS -> ladder windows 4j + 1
+//   wave 2: R decoded strictly, S checked -> ladder windows 4j + 2
+//   wave 3: [s]B (the 32 comb entries of the resident table, fetched at once)
+//           -> ladder windows 4j + 3
+// Each ladder wave runs the doublings of all 64 windows (from its first
+// non-zero digit) and adds only its own; wave 0 sums the four partial sums and
+// [s]B and compares R' with R projectively.  The same operations' results as
+// ed_verify_core's (the formulas are complete), so the same verdict.
+
+// P = 2P (dbl-2008-hwcd, a = -1): A = X^2, B = Y^2, C = 2 Z^2, E = (X+Y)^2 -
+// A - B, G = B - A, F = G - C, H = -A - B; X3 = E F, Y3 = G H, T3 = E H, Z3 = F G.
+GV_DEV void ge4_double(gesl& P, u32 row, const fslk& k) {
+  const u32 s = rsel(row, P.X, P.Y, P.Z, P.X + P.Y);
+  const rows4 p1 = rows_all(fsl_sqr(s, k));
+  const u32 a = p1.r[0], bb = p1.r[1], cz = p1.r[2], sq = p1.r[3];
+  // E, G < 2^31.1 / 2^30.6 stay raw; F, H are carried so every product of
+  // round 2 is (raw x N-form): max_limb products < 2^60.2
+  const u32 e = sq + 2u * k.bias - a - bb;
+  const u32 g = bb + k.bias - a;
+  const u32 h = fsl_norm(2u * k.bias - a - bb, k);
+  const u32 f = fsl_norm(bb + 3u * k.bias - a - (cz << 1), k);     // < 2^31.9 before the carry pass
+  const rows4 p2 = rows_all(fsl_mul(rsel(row, e, g, e, g), rsel(row, f, h, h, f), k));
+  P.X = p2.r[0]; P.Y = p2.r[1]; P.T = p2.r[2]; P.Z = p2.r[3];
+}
+
+// P = P + (neg ? -q : q), q cached (Y+X, Y-X, 2Z, 2dT): gesl_add_cached's
+// products in two rounds -- (Y1+X1) qa, (Y1-X1) qb, 2dT2 T1, Z1 2Z2, then
+// X = (A-B)(D-C), Y = (A+B)(D+C), Z = (D+C)(D-C), T = (A-B)(A+B) (C, D
+// swapped for -q).  d2z: 2 Z2, or null for an affine precomputed q
+// (y+x, y-x, 2dxy): D = 2 Z1.
+GV_DEV void ge4_add_cached(gesl& P, u32 ypx, u32 ymx, u32 z2, u32 t2d, bool pre, bool neg, u32 row, const fslk& k) {
+  const u32 qa = neg ? ymx : ypx, qb = neg ? ypx : ymx;
+  const rows4 p1 = rows_all(fsl_mul(rsel(row, P.Y + P.X, P.Y + k.bias - P.X, t2d, P.Z), rsel(row, qa, qb, P.T, z2), k));
+  const u32 a = p1.r[0], b = p1.r[1], c = p1.r[2], d = pre ? P.Z << 1 : p1.r[3];
+  const u32 x1 = fsl_norm(a + k.bias - b, k);
+  const u32 y1 = a + b;
+  const u32 dpc = d + c;
+  const u32 dmc = fsl_norm(d + k.bias - c, k);
+  const u32 z1 = neg ? dmc : dpc, t1 = neg ? dpc : dmc;
+  const rows4 p2 = rows_all(fsl_mul(rsel(row, x1, y1, z1, x1), rsel(row, t1, z1, t1, y1), k));
+  P.X = p2.r[0]; P.Y = p2.r[1]; P.Z = p2.r[2]; P.T = p2.r[3];
+}
+
+// P = P + Q, both extended
+GV_DEV void ge4_add(gesl& P, const gesl& Q, u32 d2, u32 row, const fslk& k) {
+  ge4_add_cached(P, Q.Y + Q.X, fsl_norm(Q.Y + k.bias - Q.X, k), Q.Z << 1, fsl_mul(Q.T, d2, k), false, false, row, k);
+}
+
+// ExtendedGroupElement.FromBytes (ge_frombytes: y = bytes mod 2^255, no
+// canonicality check, x from the (p-5)/8 power, sign fix-up), sliced.
+GV_DEV bool efsl_decode_lenient(u32& x, u32& y, const u32 w[8], const fslk& k) {
+  y = efsl_from_words(w, k);
+  const u32 one = efsl_small(1u, k);
+  const u32 yy = fsl_sqr(y, k);
+  const u32 u = fsl_norm(yy + k.bias - one, k);                 // y^2 - 1
+  const u32 v = fsl_norm(fsl_mul(yy, efsl_const(kEdD, k), k) + one, k);   // d y^2 + 1
+  const u32 v3 = fsl_mul(fsl_sqr(v, k), v, k);
+  u32 t = fsl_mul(fsl_sqr(v3, k), v, k);                        // v^7
+  t = efsl_pow22523(fsl_mul(t, u, k), k);                       // (u v^7)^((p-5)/8)
+  x = fsl_mul(fsl_mul(t, v3, k), u, k);                         // u v^3 (u v^7)^((p-5)/8)
+  const u32 vxx = fsl_mul(fsl_sqr(x, k), v, k);
+  const bool root = efsl_is_zero(vxx + k.bias - u);
+  const bool neg_root = efsl_is_zero(vxx + u);
+  if (!root) x = fsl_mul(x, efsl_const(kEdSqrtM1, k), k);
+  u32 xw[8];
+  efsl_to_words(xw, x);
+  if ((xw[0] & 1u) != (w[7] >> 31)) x = fsl_norm(k.bias - x, k);
+  return root || neg_root;
+}
+
+// GV_LAT_TRACE (A/B builds only): per block, wall-clock stamps (100 MHz) of
+// k_ed_lat_unc's phases, read back with gv_debug_edl_trace.  Off in the
+// product build.
+#ifndef GV_LAT_TRACE
+#define GV_LAT_TRACE 0
+#endif
+#if GV_LAT_TRACE
+__device__ uint64_t g_edl_trace[256][8];
+#define EDL_STAMP(k) do { if ((threadIdx.x & 63u) == 0 && blockIdx.x < 256) g_edl_trace[blockIdx.x][k] = wall_clock64(); } while (0)
+#else
+#define EDL_STAMP(k) do { } while (0)
+#endif
+
+GV_DEV void edl_wave_sync() {                 // one wave's LDS writes -> the wave's other lanes
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct EduShared {
+  union {                                   // the padded SHA-512 input (wave 0)
+    u32 pre[16];
+    uint8_t msg[EDL_MSG_LDS];
+    uint64_t words[EDL_MSG_LDS / 8];
+  };
+  int hd[64];                               // signed radix-16 digits of h
+  u32 xr[16], yr[16];                       // the decoded R, sliced
+  u32 flags;                                // bit 0: R decodes, bit 1: S checks
+  u32 aok;                                  // A decodes
+  u32 atab[8][4][9];                        // j (-A), j = 1..8: Y+X, Y-X, 2Z, 2dT
+  u32 pt[4][4][16];                         // ladder sums of waves 1..3, [s]B
+  u32 bent[32][3][9];                       // the [s]B comb entries (wave 3)
+  int sdg[32];                              // their signed radix-256 digits of s
+  u32 flag_h, flag_a;
+};
+
+__global__ __launch_bounds__(256) void k_ed_lat_unc(const gvk_edl b) {
+  __shared__ EduShared sh;
+  const u32 gi = blockIdx.x;                // grid = n: every block is live
+  const u32 lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const fslk k = efsl_consts();
+  const u32 L = k.L, row = (threadIdx.x >> 4) & 3u;
+  const bool lo = L < 9u;
+  if (threadIdx.x == 0) { sh.flag_h = 0u; sh.flag_a = 0u; }
+  __syncthreads();
+  if (wave == 0u) EDL_STAMP(0);
+  u32 sw[16], aw[8];
+  {
+    const uint4* sp = (const uint4*)(b.sig64 + (size_t)gi * 64);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4 v = sp[q];
+      sw[4 * q] = v.x; sw[4 * q + 1] = v.y; sw[4 * q + 2] = v.z; sw[4 * q + 3] = v.w;
+    }
+    const uint8_t* pa = b.pub32 + (size_t)gi * 32;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      aw[i] = (u32)pa[4 * i] | ((u32)pa[4 * i + 1] << 8) | ((u32)pa[4 * i + 2] << 16) | ((u32)pa[4 * i + 3] << 24);
+  }
+  const u32 d2 = efsl_const(kEd2D, k);
+  gesl P;
+  gesl_identity(P, k);
+  if (wave == 0u) {
+    edl_hash_digits(sh, sw, aw, b.msg_blob ? b.msg_blob + b.msg_off[gi] : nullptr, b.msg_len[gi], lane);
+    EDL_STAMP(1);
+    lds_flag_set(&sh.flag_h);
+  } else if (wave == 1u) {
+    u32 x, y;
+    const bool aok = efsl_decode_lenient(x, y, aw, k);
+    EDL_STAMP(2);
+    // -A = (-x, y, 1, -x y), then j (-A) in cached form
+    gesl A1;
+    A1.X = fsl_norm(k.bias - x, k);
+    A1.Y = y;
+    A1.Z = efsl_small(1u, k);
+    A1.T = fsl_mul(A1.X, y, k);
+    const u32 ypx1 = A1.Y + A1.X, ymx1 = fsl_norm(A1.Y + k.bias - A1.X, k), z21 = A1.Z << 1, t2d1 = fsl_mul(A1.T, d2, k);
+    gesl Q = A1;
+#pragma unroll 1
+    for (int j = 1; j <= 8; ++j) {
+      if (j == 2) ge4_double(Q, row, k);
+      else if (j > 2) ge4_add_cached(Q, ypx1, ymx1, z21, t2d1, false, false, row, k);
+      const u32 t2d = j == 1 ? t2d1 : fsl_mul(Q.T, d2, k);
+      const u32 ymx = fsl_norm(Q.Y + k.bias - Q.X, k);        // row-wide (DPP) before the store branch
+      if (row == 0u && lo) {
+        sh.atab[j - 1][0][L] = Q.Y + Q.X;
+        sh.atab[j - 1][1][L] = ymx;
+        sh.atab[j - 1][2][L] = Q.Z << 1;
+        sh.atab[j - 1][3][L] = t2d;
+      }
+    }
+    if (threadIdx.x == 64u) sh.aok = aok ? 1u : 0u;
+    EDL_STAMP(3);
+    lds_flag_set(&sh.flag_a);
+  } else if (wave == 2u) {
+    u32 x, y;
+    const bool rok = efsl_decode_strict(x, y, sw, k);
+    const bool sok = (sw[15] >> 29) == 0u && sc_minimal(sw + 8);   // sig[63] & 224 == 0, ScMinimal
+    if (lane < 16u) {
+      sh.xr[L] = x;
+      sh.yr[L] = y;
+    }
+    if (lane == 0u) sh.flags = (rok ? 1u : 0u) | (sok ? 2u : 0u);
+    EDL_STAMP(4);
+  } else {
+    // [s]B: signed radix-256 digits of s (ed_ladder_check's recoding), the
+    // comb entries of windows 0..31 -- no doublings; every entry's loads in
+    // flight at once (row r fetches windows r, r + 4, ...), parked in LDS
+    u32 cmask = 0, c = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const u32 byte = (sw[8 + (i >> 2)] >> (8 * (i & 3))) & 0xFFu;
+      c = (byte + c) > 128u ? 1u : 0u;
+      cmask |= c << i;
+    }
+#pragma unroll
+    for (int w = 0; w < 32; ++w) {
+      const int byte = (int)((sw[8 + (w >> 2)] >> (8 * (w & 3))) & 0xFFu);
+      const int cin = w > 0 ? (int)((cmask >> (w - 1)) & 1u) : 0;
+      if (lane == (u32)w) sh.sdg[w] = byte + cin - 256 * (int)((cmask >> w) & 1u);
+    }
+    edl_wave_sync();
+#pragma unroll
+    for (u32 i = 0; i < 8u; ++i) {
+      const u32 w = 4u * i + row;
+      const int dg = sh.sdg[w];
+      const u32 mag = (u32)(dg < 0 ? -dg : dg);
+      const u32* e = b.btab + (size_t)(w * ED_BTAB_ENTRIES + mag) * ED_PRE_WORDS;
+      if (lo) { sh.bent[w][0][L] = e[L]; sh.bent[w][1][L] = e[9 + L]; sh.bent[w][2][L] = e[18 + L]; }
+    }
+    edl_wave_sync();
+#pragma unroll 1
+    for (u32 w = 0; w < 32u; ++w) {
+      const int dg = sh.sdg[w];
+      if (dg != 0)
+        ge4_add_cached(P, lo ? sh.bent[w][0][L] : 0u, lo ? sh.bent[w][1][L] : 0u, 0u, lo ? sh.bent[w][2][L] : 0u,
+                       true, dg < 0, row, k);
+    }
+    if (row == 0u && lo) { sh.pt[3][0][L] = P.X; sh.pt[3][1][L] = P.Y; sh.pt[3][2][L] = P.Z; sh.pt[3][3][L] = P.T; }
+    gesl_identity(P, k);
+    EDL_STAMP(5);
+  }
+  lds_flag_wait(&sh.flag_h);
+  lds_flag_wait(&sh.flag_a);
+  // [h](-A): this wave's windows 4j + wave, MSB first
+  {
+    bool id = true;
+#pragma unroll 1
+    for (int w = 63; w >= 0; --w) {
+      if (!id) {
+#pragma unroll 1
+        for (int dd = 0; dd < 4; ++dd) ge4_double(P, row, k);
+      }
+      if ((u32)(w & 3) != wave) continue;
+      const int dg = sh.hd[w];
+      if (dg == 0) continue;
+      const u32 m = (u32)(dg < 0 ? -dg : dg) - 1u;
+      ge4_add_cached(P, lo ? sh.atab[m][0][L] : 0u, lo ? sh.atab[m][1][L] : 0u, lo ? sh.atab[m][2][L] : 0u,
+                     lo ? sh.atab[m][3][L] : 0u, false, dg < 0, row, k);
+      id = false;
+    }
+  }
+  if (wave == 0u) EDL_STAMP(6);
+  if (wave != 0u && row == 0u && lo) {
+    sh.pt[wave - 1][0][L] = P.X; sh.pt[wave - 1][1][L] = P.Y; sh.pt[wave - 1][2][L] = P.Z; sh.pt[wave - 1][3][L] = P.T;
+  }
+  __syncthreads();
+  if (wave != 0u) return;
+#pragma unroll 1
+  for (int j = 0; j < 4; ++j) {
+    gesl O;
+    O.X = lo ? sh.pt[j][0][L] : 0u; O.Y = lo ? sh.pt[j][1][L] : 0u;
+    O.Z = lo ? sh.pt[j][2][L] : 0u; O.T = lo ? sh.pt[j][3][L] : 0u;
+    ge4_add(P, O, d2, row, k);
+  }
+  // R' == (x_R, y_R): X' == x_R Z', Y' == y_R Z'
+  const u32 xr = lo ? sh.xr[L] : 0u, yr = lo ? sh.yr[L] : 0u;
+  u32 w1[8], w2[8], w3[8], w4[8];
+  efsl_to_words(w1, P.X);
+  efsl_to_words(w2, fsl_mul(xr, P.Z, k));
+  efsl_to_words(w3, P.Y);
+  efsl_to_words(w4, fsl_mul(yr, P.Z, k));
+  u32 diff = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) diff |= (w1[i] ^ w2[i]) | (w3[i] ^ w4[i]);
+  const bool ok = sh.aok != 0u && (sh.flags & 3u) == 3u && diff == 0u;
+  if (threadIdx.x == 0) b.out8[gi] = ok ? 1u : 0u;
+  EDL_STAMP(7);
 }
 
 // Large batches against cached keys (k_ed_keyed, one signature per lane):
@@ -482,5 +765,19 @@ extern "C" hipError_t gvk_ed_keys(const uint8_t* pub32, uint32_t n, uint32_t bas
 extern "C" hipError_t gvk_ed_lat(const gvk_edl* b, hipStream_t st) {
   if (b->n == 0) return hipSuccess;
   hipLaunchKernelGGL(gv::ed::k_ed_lat_sl, dim3(b->n), dim3(256), 0, st, *b);
+  return hipGetLastError();
+}
+
+#if GV_LAT_TRACE
+extern "C" int gv_debug_edl_trace(uint64_t* out, int blocks) {
+  if (blocks < 0 || blocks > 256) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gv::ed::g_edl_trace), (size_t)blocks * 8 * 8) == hipSuccess ? 0 : -3;
+}
+#endif
+
+extern "C" hipError_t gvk_ed_lat_unc(const gvk_edl* b, hipStream_t st) {
+  if (b->n == 0) return hipSuccess;
+  if (!b->pub32 || !b->btab || !b->out8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gv::ed::k_ed_lat_unc, dim3(b->n), dim3(256), 0, st, *b);
   return hipGetLastError();
 }

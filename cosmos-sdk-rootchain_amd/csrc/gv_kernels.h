@@ -232,6 +232,7 @@ typedef struct gvk_edl {
   uint32_t kcount;
   const uint32_t* btab;         // GV_ED_BTAB_WORDS
   uint8_t* out8;                // n verdict bytes
+  const uint8_t* pub32;         // gvk_ed_lat_unc: n x 32 key bytes (slot / ktab / kpub / kok unused)
 } gvk_edl;
 // wbase (may be null: one lane per key does everything): n * 64 * 36 words of
 // scratch for the window bases -- the chain and the table adds then run as
@@ -239,6 +240,8 @@ typedef struct gvk_edl {
 hipError_t gvk_ed_keys(const uint8_t* pub32, uint32_t n, uint32_t base, uint32_t* ktab, uint32_t* kpub, uint32_t* kok,
                        uint32_t* wbase, hipStream_t st);
 hipError_t gvk_ed_lat(const gvk_edl* b, hipStream_t st);
+// Small ed25519 batches against uncached keys (k_ed_lat_unc): b->pub32 per item.
+hipError_t gvk_ed_lat_unc(const gvk_edl* b, hipStream_t st);
 // Large ed25519 batches against cached keys (k_ed_keyed): one signature per
 // lane, lane g takes item perm[g] (null: g), verdict byte out8[item].
 typedef struct gvk_edk {

@@ -1109,25 +1109,6 @@ struct LatSl4Shared {
   u32 flag_tab, flag_sc, flag_e;            // tables / scalars / digest ready
 };
 
-GV_DEV void lds_flag_set(u32* f) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-GV_DEV void lds_flag_wait(u32* f) {
-  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(2);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-// The four rows' values of v, each in every row: r[i] = row i's v.
-struct rows4 { u32 r[4]; };
-GV_DEV rows4 rows_all(u32 v) {
-  const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);     // {v0 v0 v2 v2}, {v1 v1 v3 v3}
-  const auto e = __builtin_amdgcn_permlane32_swap(a[0], a[0], false, false);   // v0, v2
-  const auto o = __builtin_amdgcn_permlane32_swap(a[1], a[1], false, false);   // v1, v3
-  rows4 r;
-  r.r[0] = e[0]; r.r[1] = o[0]; r.r[2] = e[1]; r.r[3] = o[1];
-  return r;
-}
 
 // Every round below is ONE product per lane whose operands (and 64-bit extra)
 // the row selects -- never a branch on the row, which would run each row's

@@ -589,6 +589,7 @@ struct gv_ctx {
   bool ed_keys_split = true;     // ed25519 key tables: serial chain and table adds in two launches (GV_ED_KEYS_SPLIT=0: A/B)
   bool ed_keyed = true;          // keyed ed25519 batches past ed_lat_max on k_ed_keyed (GV_ED_KEYED=0: the throughput kernels)
   size_t ed_lat_max = 2048;      // keyed ed25519 batches up to this size take k_ed_lat_sl (one signature per block)
+  size_t ed_unc_lat_max = 2048;  // uncached ed25519 host batches up to this size take k_ed_lat_unc (one signature per block)
 };
 
 namespace {
@@ -2047,10 +2048,61 @@ int gv_dev_verify_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub33,
 }
 
 // ---- ed25519
+namespace {
+// Small uncached ed25519 batches on one device (k_ed_lat_unc, one signature
+// per block): the kernel reads keys, signatures and messages from the pinned
+// staging buffer and writes verdict bytes there (no H2D / D2H copies).
+int ed_unc_small(gv_ctx* ctx, size_t n, const EdHost& hb) {
+  Dev* d = ctx->devs[0];
+  std::lock_guard<std::mutex> lk(d->mu);
+  CK(hipSetDevice(d->id));
+  hipStream_t st = d->set[0].st;
+  int rc = ed_ensure(d, 256, st);                 // the resident comb table of B
+  if (rc) return rc;
+  uint64_t lo = UINT64_MAX, hi = 0;
+  for (size_t i = 0; i < n; ++i) {
+    lo = std::min<uint64_t>(lo, hb.off[i]);
+    hi = std::max<uint64_t>(hi, hb.off[i] + hb.len[i]);
+  }
+  if (lo > hi) lo = hi = 0;
+  const size_t o_sig = round_up(n * 32, 64), o_off = o_sig + n * 64, o_len = o_off + n * 8, o_out = o_len + n * 4,
+               o_blob = round_up(o_out + n, 64), total = o_blob + (hi - lo);
+  if ((rc = ensure_pinned(&d->edl_h, &d->edl_h_cap, total))) return rc;
+  uint8_t* h = d->edl_h;
+  memcpy(h, hb.pub32, n * 32);
+  memcpy(h + o_sig, hb.sig64, n * 64);
+  uint64_t* ro = (uint64_t*)(h + o_off);
+  for (size_t i = 0; i < n; ++i) ro[i] = hb.off[i] - lo;
+  memcpy(h + o_len, hb.len, n * 4);
+  if (hi > lo) memcpy(h + o_blob, hb.blob + lo, hi - lo);
+  gvk_edl b;
+  memset(&b, 0, sizeof b);
+  b.n = (uint32_t)n;
+  b.pub32 = h;
+  b.sig64 = h + o_sig;
+  b.msg_blob = h + o_blob;
+  b.msg_off = (const uint64_t*)(h + o_off);
+  b.msg_len = (const uint32_t*)(h + o_len);
+  b.btab = d->edtab;
+  b.out8 = h + o_out;
+  d->routes[GV_ROUTE_ED_LAT]++;
+  CK(gvk_ed_lat_unc(&b, st));
+  CK(hipStreamSynchronize(st));
+  memcpy(hb.out_ok, h + o_out, n);
+  return GV_OK;
+}
+}  // namespace
+
 int gv_verify_ed25519_msgs(gv_ctx* ctx, size_t n, const uint8_t* pub32, const uint8_t* sig64,
                            const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len,
                            uint8_t* out_ok) {
-  return run_ed_host(ctx, n, EdHost{pub32, sig64, msg_blob, msg_off, msg_len, out_ok});
+  const EdHost hb{pub32, sig64, msg_blob, msg_off, msg_len, out_ok};
+  if (ctx && !ctx->fault_inject && n && n <= ctx->ed_unc_lat_max && pub32 && sig64 && msg_off && msg_len && out_ok) {
+    for (size_t i = 0; i < n; ++i)
+      if (msg_len[i] && !msg_blob) return GV_EINVAL;
+    return ed_unc_small(ctx, n, hb);
+  }
+  return run_ed_host(ctx, n, hb);
 }
 
 int gv_dev_verify_ed25519_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub32, const void* d_sig64,
@@ -2504,6 +2556,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
     if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
     if (!strcmp(key, "lat_sl_max")) ctx->lat_sl_max = (size_t)val;
     ctx->lat_sl_max_keyed = (size_t)val;
+  } else if (!strcmp(key, "ed_unc_lat_max")) {
+    if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
+    ctx->ed_unc_lat_max = (size_t)val;
   } else if (!strcmp(key, "ed_lat_max")) {
     if (val < 0 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
     ctx->ed_lat_max = (size_t)val;

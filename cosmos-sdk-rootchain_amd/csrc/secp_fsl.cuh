@@ -216,6 +216,49 @@ GV_DEV bool fsl_is_zero(u32 a) {
   return res;
 }
 
+// ------------------------------------------------------------ rows of a wave
+// The row-parallel kernels (k_verify_lat_sl4, k_ed_lat_unc) keep ONE point
+// per wave, replicated in its four rows, and give each row a different
+// product of the same round; every row then needs every row's result.
+// The four rows' values of v, each in every row: r[i] = row i's v (three
+// lane swaps, VALU only).
+struct rows4 { u32 r[4]; };
+GV_DEV rows4 rows_all(u32 v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);     // {v0 v0 v2 v2}, {v1 v1 v3 v3}
+  const auto e = __builtin_amdgcn_permlane32_swap(a[0], a[0], false, false);   // v0, v2
+  const auto o = __builtin_amdgcn_permlane32_swap(a[1], a[1], false, false);   // v1, v3
+  rows4 r;
+  r.r[0] = e[0]; r.r[1] = o[0]; r.r[2] = e[1]; r.r[3] = o[1];
+  return r;
+}
+
+// Row r's operand of four: every candidate is materialised first (the empty
+// asm keeps the compiler from sinking a candidate's arithmetic into a branch
+// on the row), then one v_cndmask per step.
+GV_DEV u32 rsel(u32 row, u32 a, u32 b, u32 c, u32 d) {
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+  u32 r = row == 1u ? b : a;
+  r = row == 2u ? c : r;
+  return row == 3u ? d : r;
+}
+GV_DEV u64 rsel64(u32 row, u64 a, u64 b, u64 c, u64 d) {
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+  u64 r = row == 1u ? b : a;
+  r = row == 2u ? c : r;
+  return row == 3u ? d : r;
+}
+
+// One-shot LDS flags between the waves of a block (a wave waits only for the
+// producer it needs, instead of a block barrier).
+GV_DEV void lds_flag_set(u32* f) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+GV_DEV void lds_flag_wait(u32* f) {
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(2);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // ------------------------------------------------------------ group law
 // Jacobian point, one row: X, Y, Z sliced (N-form).
 struct gjsl { u32 x, y, z; };

@@ -223,6 +223,9 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * per signature, and the 16-lanes-per-signature keyed kernel beats the keyed
  * pipeline to ~14k; setting "lat_max" / "lat_sl_max" sets these too),
  * "lat_sliced" (0/1: 0 never takes the sliced kernels; default 1),
+ * "ed_unc_lat_max" (uncached ed25519 host batches of at most this many
+ * items take k_ed_lat_unc: one signature per block, FromBytes(A) in the
+ * kernel; default 2048, 0 = never),
  * "lat_rows_max" (pub33 sliced batches of at most this many items take
  * k_verify_lat_sl4: five waves per signature, each ladder wave's four rows on
  * one accumulator, G from the k6 tables after the ladder; default 512, 0 =
@@ -374,8 +377,9 @@ int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys)
  * the unsplit scalar, 25-bit windows), GV_ROUTE_ITEMF (the per-item pipeline
  * with the G half on the unsplit scalar, "gfull_item"), GV_ROUTE_KN (keyed
  * batches on the resident arena's k6 tables: 11 groups of 6-bit windows, 6
- * doublings, option "keys_k6").  Instrumentation only
- * (bench route attribution, node metrics). */
+ * doublings, option "keys_k6"), GV_ROUTE_ED_LAT (small uncached ed25519
+ * host batches on k_ed_lat_unc, option "ed_unc_lat_max").  Instrumentation
+ * only (bench route attribution, node metrics). */
 #define GV_ROUTE_PUB33 0
 #define GV_ROUTE_KEYED125 1
 #define GV_ROUTE_K4 2
@@ -385,7 +389,8 @@ int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys)
 #define GV_ROUTE_K4F 6
 #define GV_ROUTE_ITEMF 7
 #define GV_ROUTE_KN 8
-#define GV_ROUTES 9
+#define GV_ROUTE_ED_LAT 9
+#define GV_ROUTES 10
 int gv_route_stats(gv_ctx* ctx, int dev_slot, uint64_t out[GV_ROUTES]);
 
 const char* gv_strerror(int code);

@@ -2,7 +2,10 @@
 gv_verify_ed25519_msgs / gv_dev_verify_ed25519_msgs) against the committed
 golden vectors (verdicts of oracle/ed25519_ref.py, go1.14 crypto/ed25519
 semantics: non-canonical and small-order keys, S >= L, sig[63] & 224,
-non-canonical R), the RFC 8032 vectors, and OpenSSL on random batches."""
+non-canonical R), the RFC 8032 vectors, and OpenSSL on random batches --
+on both host-batch schedules: the throughput kernels and the small-batch
+kernel k_ed_lat_unc (csrc/ed_lat.hip, one signature per block, FromBytes(A)
+in the kernel; "ed_unc_lat_max" picks one per call)."""
 import json
 import os
 import random
@@ -24,6 +27,16 @@ def ver():
     v.close()
 
 
+SCHEDULES = {"throughput": 0, "small": 1 << 30}      # ed_unc_lat_max
+
+
+@pytest.fixture(params=sorted(SCHEDULES))
+def sched(request, ver):
+    ver.set_option("ed_unc_lat_max", SCHEDULES[request.param])
+    yield request.param
+    ver.set_option("ed_unc_lat_max", 2048)
+
+
 def arrays(items):
     pub = np.array([np.frombuffer(p, np.uint8) for p, _, _ in items]).reshape(-1, 32)
     sig = np.array([np.frombuffer(s, np.uint8) for _, _, s in items]).reshape(-1, 64)
@@ -39,7 +52,7 @@ def golden():
     return out
 
 
-def test_golden_vectors(ver):
+def test_golden_vectors(ver, sched):
     gv = golden()
     pub, sig, msgs = arrays([(p, m, s) for _, p, m, s, _ in gv])
     got = ver.verify_batch_ed25519(pub, sig, msgs)
@@ -48,7 +61,7 @@ def test_golden_vectors(ver):
     assert int(got.sum()) == sum(ok for *_, ok in gv)
 
 
-def test_rfc8032(ver):
+def test_rfc8032(ver, sched):
     vs = json.load(open(os.path.join(GOLD, "ed25519_rfc8032.json")))["vectors"]
     items = [(bytes.fromhex(v["pub"]), bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"])) for v in vs]
     pub, sig, msgs = arrays(items)
@@ -56,7 +69,7 @@ def test_rfc8032(ver):
     assert not ver.verify_batch_ed25519(pub, sig, [m + b"." for m in msgs]).any()
 
 
-def test_random_batch_vs_openssl(ver):
+def test_random_batch_vs_openssl(ver, sched):
     rng = random.Random(11)
     seeds = [rng.randbytes(32) for _ in range(64)]
     pubs = [OSSL.public_key(s) for s in seeds]
@@ -79,13 +92,15 @@ def test_random_batch_vs_openssl(ver):
         items.append((pubs[k], msg, sig))
         want.append(OSSL.verify(pubs[k], msg, sig))
     pub, sig, msgs = arrays(items)
+    r0 = ver.route_stats()["ed_lat"]
     got = ver.verify_batch_ed25519(pub, sig, msgs)
     assert np.array_equal(got.astype(bool), np.array(want)), np.nonzero(got.astype(bool) != np.array(want))[0][:10]
     assert 0.6 < got.mean() < 0.9
+    assert (ver.route_stats()["ed_lat"] > r0) == (sched == "small")
 
 
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 257])
-def test_ragged_sizes_and_empty_messages(ver, n):
+def test_ragged_sizes_and_empty_messages(ver, sched, n):
     rng = random.Random(n)
     seed = rng.randbytes(32)
     pub = OSSL.public_key(seed)

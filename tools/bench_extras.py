@@ -820,7 +820,7 @@ def ed25519_small_batches(ver, wl, pub, sig, blob, off, lens, exp, threads, size
         bo = off[:b] - off[0]
         bb = blob[int(off[0]):int(off[b - 1] + lens[b - 1])]
         msgs = (bb, bo, lens[:b])
-        tk, tu, tc1, tcn = [], [], [], []
+        tk, tu, tt, tc1, tcn = [], [], [], [], []
         for r in range(reps + 5):
             t = time.perf_counter()
             gk = ver.verify_batch_ed25519_keyed(slots[:b], sig[:b], msgs)
@@ -830,7 +830,14 @@ def ed25519_small_batches(ver, wl, pub, sig, blob, off, lens, exp, threads, size
             if r >= 5:
                 tk.append(t1 - t)
                 tu.append(t2 - t1)
-        mism += int(np.count_nonzero(gk.astype(bool) != exp[:b])) + int(np.count_nonzero(gu.astype(bool) != exp[:b]))
+        ver.set_option("ed_unc_lat_max", 0)                  # the throughput kernels, forced
+        for r in range(reps // 4 + 3):
+            t = time.perf_counter()
+            gt = ver.verify_batch_ed25519(pub[:b], sig[:b], msgs)
+            if r >= 3:
+                tt.append(time.perf_counter() - t)
+        ver.set_option("ed_unc_lat_max", 2048)
+        mism += sum(int(np.count_nonzero(g.astype(bool) != exp[:b])) for g in (gk, gu, gt))
         o = np.zeros(b, np.uint8)
         for r in range(7 if b <= 256 else 3):
             for th, acc in ((1, tc1), (threads, tcn)):
@@ -840,12 +847,14 @@ def ed25519_small_batches(ver, wl, pub, sig, blob, off, lens, exp, threads, size
                 acc.append(time.perf_counter() - t)
         p50 = lambda a: round(float(np.median(a)) * 1e3, 4)  # noqa: E731
         out[str(b)] = {"keyed_sliced_p50_ms": p50(tk), "keyed_sliced_p99_ms": round(float(np.percentile(tk, 99)) * 1e3, 4),
-                       "throughput_p50_ms": p50(tu), "cpu_openssl_serial_p50_ms": p50(tc1),
+                       "uncached_p50_ms": p50(tu), "uncached_p99_ms": round(float(np.percentile(tu, 99)) * 1e3, 4),
+                       "throughput_p50_ms": p50(tt), "cpu_openssl_serial_p50_ms": p50(tc1),
                        "cpu_openssl_allcore_p50_ms": p50(tcn)}
     return {"batches": out, "mismatches": mism, "keys_loaded": int(len(uk)), "key_load_ms": round(t_load * 1e3, 2),
             "note": "host buffers (~350 B messages), end to end; keyed = gv_verify_ed25519_msgs_keyed after one "
-                    "gv_ed_keys_load of the batch's keys (k_ed_lat_sl up to ed_lat_max = 2048), throughput = "
-                    "gv_verify_ed25519_msgs (k_ed_prep + k_ed_ladder)"}
+                    "gv_ed_keys_load of the batch's keys (k_ed_lat_sl up to ed_lat_max = 2048); uncached = "
+                    "gv_verify_ed25519_msgs, the default schedule (k_ed_lat_unc up to ed_unc_lat_max = 2048); "
+                    "throughput = the same call with ed_unc_lat_max 0 (k_ed_prep + k_ed_ladder)"}
 
 
 def first_call(pub, sig, dig, exp, calls: int = 6):
