@@ -275,8 +275,9 @@ def _pct(ts):
 def checktx_latency(ver, pub, sig, dig, threads, sizes=(1, 16, 32, 64, 128, 256, 1024, 4096), reps=1000):
     """C5: host-path latency (host buffers in -> verdicts out) per batch size.
     p50/p99 are the default GPU path: up to "lat_sl_max" (2048) the limb-sliced
-    small-batch kernels (gv_lat.hip k_verify_lat_sl / k_verify_lat16_sl, one
-    signature per block) reading the pinned staging buffer zero-copy, up to
+    small-batch kernels (gv_lat.hip k_verify_lat_sl4 up to "lat_rows_max" = 512,
+    k_verify_lat_sl above / k_verify_lat16_sl keyed, one signature per block)
+    reading the pinned staging buffer zero-copy, up to
     "lat_max" (8192) the four-lanes-per-signature kernel, the pipeline above
     ("schedule" per size); next to it the throughput pipeline forced for the
     same batches, the message path (gv_verify_msgs over ~355-byte StdSignBytes:
@@ -335,7 +336,8 @@ def checktx_latency(ver, pub, sig, dig, threads, sizes=(1, 16, 32, 64, 128, 256,
                 if time.perf_counter() > budget and len(ts) >= 3:
                     break
             cpu[label] = _pct(ts)[0]
-        sched = ("k_verify_lat_sl (limb-sliced, zero-copy)" if b <= gvm.LAT_SL_MAX_DEFAULT else
+        sched = ("k_verify_lat_sl4 (limb-sliced, row-parallel ladders, zero-copy)" if b <= gvm.LAT_ROWS_MAX_DEFAULT else
+                 "k_verify_lat_sl (limb-sliced, zero-copy)" if b <= gvm.LAT_SL_MAX_DEFAULT else
                  "k_verify_lat (4 lanes per signature)" if b <= gvm.LAT_MAX_DEFAULT else "pipeline")
         out[str(b)] = {"p50_ms": p50, "p99_ms": p99, "throughput_path_p50_ms": tp50, "keyed_p50_ms": keyed50,
                        "msgs_p50_ms": msgs50, **cpu, "schedule": sched}
