@@ -130,7 +130,9 @@ def c2_hostpath(ver, pub, sig, dig, exp, steps: int = 5, device_value: float | N
                 for h, a in zip(hpa, (pub, sig, dig)):
                     h[...] = a
             src = arrs or hpa
-            ver.wait(ver.submit_digests(*src))              # warm
+            for _ in range(2):                              # warm: two batches in flight (both grouping sets)
+                for p in [ver.submit_digests(*src) for _ in range(2)]:
+                    ver.wait(p)
             t = time.perf_counter()
             pend = [ver.submit_digests(*src) for _ in range(steps)]
             got = [ver.wait(p) for p in pend]
