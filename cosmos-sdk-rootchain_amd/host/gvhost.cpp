@@ -1462,6 +1462,10 @@ struct gvh_app {
   std::mutex deferred_mu;
   std::vector<std::shared_ptr<Memo>> deferred;
   bool defer_release = getenv("GVH_DEFER_RELEASE") ? atoi(getenv("GVH_DEFER_RELEASE")) != 0 : true;
+  // gvh_deliver_blocks queues block b+1's secp256k1 batch with gv_submit_* and
+  // waits for it after block b's loop (no helper thread); 0: a helper thread
+  // runs the synchronous call (also the path of batches with ed25519 leaves)
+  bool async_blocks = getenv("GVH_ASYNC_BLOCKS") ? atoi(getenv("GVH_ASYNC_BLOCKS")) != 0 : true;
 };
 
 namespace {
@@ -1878,9 +1882,16 @@ void batch_pack(gvh_app* app, GpuBatch& b) {
 // (a key ParsePubKey rejects keeps a false slot), without the per-item
 // decompression and Q-table build, on the 4-group ladder.  Any arena problem
 // (cap reached, load error) falls back to the pub33 batch for this call.
-int verify_secp(gvh_app* app, GpuBatch& b) {
+// ticket: queue the batch (gv_submit_*) instead of verifying it; the caller
+// waits for *ticket (gv_wait) before it reads b.ok.  A batch queued keyed
+// stays valid across a later gv_keys_load / gv_keys_reset: the library runs
+// the queued batches before it moves a slot.
+int verify_secp(gvh_app* app, GpuBatch& b, uint64_t* ticket = nullptr) {
   const size_t m = b.m;
   auto plain = [&] {
+    if (ticket)
+      return b.msgs ? gv_submit_msgs(app->gpu, m, b.pub, b.sig, b.blob, b.moff, b.mlen, b.ok, ticket)
+                    : gv_submit_digests(app->gpu, m, b.pub, b.sig, b.dig, b.ok, ticket);
     return b.msgs ? gv_verify_msgs(app->gpu, m, b.pub, b.sig, b.blob, b.moff, b.mlen, b.ok)
                   : gv_verify_digests(app->gpu, m, b.pub, b.sig, b.dig, b.ok);
   };
@@ -1936,6 +1947,9 @@ int verify_secp(gvh_app* app, GpuBatch& b) {
     for (size_t k = 0; k < m; ++k)
       if (b.slots[k] >= kPending) b.slots[k] = got[b.slots[k] - kPending];
   }
+  if (ticket)
+    return b.msgs ? gv_submit_msgs_keyed(app->gpu, m, b.slots, b.sig, b.blob, b.moff, b.mlen, b.ok, ticket)
+                  : gv_submit_digests_keyed(app->gpu, m, b.slots, b.sig, b.dig, b.ok, ticket);
   return b.msgs ? gv_verify_msgs_keyed(app->gpu, m, b.slots, b.sig, b.blob, b.moff, b.mlen, b.ok)
                 : gv_verify_digests_keyed(app->gpu, m, b.slots, b.sig, b.dig, b.ok);
 }
@@ -2001,6 +2015,20 @@ int batch_run(gvh_app* app, GpuBatch& b) {
                       b.elen.data(), b.eok.data(), me >= app->key_load_min) != GV_OK)
     return GVH_EDEVICE;
   return GVH_OK;
+}
+
+// A batch without ed25519 leaves queued on the library's asynchronous path:
+// *ticket = 0 when there is nothing to wait for.
+int batch_submit(gvh_app* app, GpuBatch& b, uint64_t* ticket) {
+  *ticket = 0;
+  if (!app->gpu) return GVH_ENOVERIFIER;
+  std::lock_guard<std::mutex> g(app->gpu_mu);
+  if (b.m && verify_secp(app, b, ticket) != GV_OK) return GVH_EDEVICE;
+  return GVH_OK;
+}
+int batch_wait(gvh_app* app, uint64_t ticket) {
+  if (!ticket) return GVH_OK;
+  return gv_wait(app->gpu, ticket) == GV_OK ? GVH_OK : GVH_EDEVICE;
 }
 
 void batch_finish(gvh_app* app, GpuBatch& b, bool fill, uint32_t* gpu_leaves) {
@@ -2826,13 +2854,24 @@ int deliver_blocks(gvh_app* app, size_t nb, const size_t* bn, const uint8_t* con
   for (size_t b = 0; b < nb; ++b) {
     const bool more = b + 1 < nb;
     std::future<int> gpu;
+    uint64_t ticket = 0;                              // block b+1's queued batch
     if (more) {
       const auto tp = std::chrono::steady_clock::now();
       nxt = PreState{};
       pre_front(app, bn[b + 1], txs + off + bn[b], lens + off + bn[b], false, cur.epoch, nxt);
       if (nxt.has_batch) {
-        if (!app->gpu) gpu = std::async(std::launch::deferred, [] { return (int)GVH_ENOVERIFIER; });
-        else gpu = std::async(std::launch::async, [app, &nxt] { return pre_gpu(app, nxt); });
+        if (!app->gpu) {
+          gpu = std::async(std::launch::deferred, [] { return (int)GVH_ENOVERIFIER; });
+        } else if (app->async_blocks && nxt.batch.ed.empty()) {
+          // queued on the library's asynchronous path: it runs while this
+          // thread and the pool deliver block b (gv_wait below)
+          const auto tg = std::chrono::steady_clock::now();
+          const int rs = batch_submit(app, nxt.batch, &ticket);
+          app->st_gpu_ns += ns_since(tg);
+          if (rs != GVH_OK) gpu = std::async(std::launch::deferred, [rs] { return rs; });
+        } else {
+          gpu = std::async(std::launch::async, [app, &nxt] { return pre_gpu(app, nxt); });
+        }
       }
       app->st_pre_ns += ns_since(tp);
       if (prof) fprintf(stderr, "blocks %zu: front %.3f ms\n", b + 1, ns_since(tp) / 1e6);
@@ -2844,7 +2883,12 @@ int deliver_blocks(gvh_app* app, size_t nb, const size_t* bn, const uint8_t* con
     if (prof) fprintf(stderr, "blocks %zu: loop+release %.3f ms\n", b, ns_since(tl) / 1e6);
     if (!more) break;
     const auto tw = std::chrono::steady_clock::now();
-    const int rg = gpu.valid() ? gpu.get() : GVH_OK;  // always joined before nxt goes away
+    int rg = gpu.valid() ? gpu.get() : GVH_OK;        // always joined before nxt goes away
+    if (ticket) {
+      const auto tg = std::chrono::steady_clock::now();
+      rg = batch_wait(app, ticket);
+      app->st_gpu_ns += ns_since(tg);
+    }
     pre_back(app, nxt, rg, nullptr, &memos);
     if (prof) fprintf(stderr, "blocks %zu: gpu wait + back %.3f ms\n", b + 1, ns_since(tw) / 1e6);
     if (rc == GVH_OK) rc = rg;

@@ -13,6 +13,8 @@
 #include <string.h>
 
 #include <atomic>
+#include <future>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -27,7 +29,17 @@ struct gv_ctx {
   std::vector<uint8_t> ed_keys;   // 32 B per slot
   std::atomic<uint64_t> gen{0}, ed_gen{0};
   std::atomic<uint64_t> calls{0};
+  std::mutex qmu;                 // the asynchronous entry points: ticket -> the batch's result
+  std::map<uint64_t, std::future<int>> queued;
+  uint64_t next_ticket = 1;
 };
+
+// gv_keys_load / gv_keys_reset wait for every queued batch first (the
+// library's contract: a queued keyed batch never sees a slot move)
+static void quiesce(gv_ctx* ctx) {
+  std::lock_guard<std::mutex> g(ctx->qmu);
+  for (auto& q : ctx->queued) q.second.wait();
+}
 
 extern "C" {
 
@@ -46,6 +58,7 @@ int gv_verify_digests(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t
 
 int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out) {
   if (!ctx || (n && (!pub33 || !slot_out))) return GV_EINVAL;
+  quiesce(ctx);
   std::lock_guard<std::mutex> g(ctx->mu);
   const size_t base = ctx->keys.size() / 33;
   ctx->keys.insert(ctx->keys.end(), pub33, pub33 + 33 * n);
@@ -53,6 +66,7 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
   return GV_OK;
 }
 int gv_keys_reset(gv_ctx* ctx) {
+  quiesce(ctx);
   std::lock_guard<std::mutex> g(ctx->mu);
   ctx->keys.clear();
   ctx->gen++;
@@ -98,6 +112,47 @@ int gv_verify_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint
   if (!ctx || (n && (!msg_off || !msg_len))) return GV_EINVAL;
   const std::vector<uint8_t> d = hash_msgs(n, msg_blob, msg_off, msg_len);
   return gv_verify_digests_keyed(ctx, n, slot, sig64, d.data(), out_ok);
+}
+
+}  // extern "C"
+// asynchronous batches: each runs on a thread of its own, gv_wait joins it
+template <class F>
+static int submit(gv_ctx* ctx, uint64_t* ticket, F f) {
+  if (!ctx || !ticket) return GV_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->qmu);
+  *ticket = ctx->next_ticket++;
+  ctx->queued.emplace(*ticket, std::async(std::launch::async, f));
+  return GV_OK;
+}
+extern "C" {
+int gv_submit_digests(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64, const uint8_t* dig32,
+                      uint8_t* out_ok, uint64_t* ticket) {
+  return submit(ctx, ticket, [=] { return gv_verify_digests(ctx, n, pub33, sig64, dig32, out_ok); });
+}
+int gv_submit_digests_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64, const uint8_t* dig32,
+                            uint8_t* out_ok, uint64_t* ticket) {
+  return submit(ctx, ticket, [=] { return gv_verify_digests_keyed(ctx, n, slot, sig64, dig32, out_ok); });
+}
+int gv_submit_msgs(gv_ctx* ctx, size_t n, const uint8_t* pub33, const uint8_t* sig64, const uint8_t* msg_blob,
+                   const uint64_t* msg_off, const uint32_t* msg_len, uint8_t* out_ok, uint64_t* ticket) {
+  return submit(ctx, ticket, [=] { return gv_verify_msgs(ctx, n, pub33, sig64, msg_blob, msg_off, msg_len, out_ok); });
+}
+int gv_submit_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint8_t* sig64, const uint8_t* msg_blob,
+                         const uint64_t* msg_off, const uint32_t* msg_len, uint8_t* out_ok, uint64_t* ticket) {
+  return submit(ctx, ticket,
+                [=] { return gv_verify_msgs_keyed(ctx, n, slot, sig64, msg_blob, msg_off, msg_len, out_ok); });
+}
+int gv_wait(gv_ctx* ctx, uint64_t ticket) {
+  if (!ctx) return GV_EINVAL;
+  std::future<int> f;
+  {
+    std::lock_guard<std::mutex> g(ctx->qmu);
+    auto it = ctx->queued.find(ticket);
+    if (it == ctx->queued.end()) return GV_EINVAL;
+    f = std::move(it->second);
+    ctx->queued.erase(it);
+  }
+  return f.get();
 }
 
 static uint8_t ed_verify(const uint8_t* pub32, const uint8_t* sig64, const uint8_t* msg, size_t len) {
