@@ -54,6 +54,15 @@ type EdVerifier interface {
 	VerifyBatchEd25519(pubs []ed25519.PubKeyEd25519, msgs, sigs [][]byte) []bool
 }
 
+// AsyncVerifier queues a batch and returns at once: wait returns the
+// verdicts (VerifyBatch's), called exactly once.  The GPU implements it with
+// gv_submit_msgs[_keyed] / gv_wait, so the batch runs while the caller does
+// other work -- the same block's ed25519 leaves, the next block's state stage
+// -- and consecutive batches run as one stream of chunks on the device.
+type AsyncVerifier interface {
+	SubmitBatch(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]byte) (wait func() []bool)
+}
+
 // EdKeyCache is an EdVerifier that can keep a key set resident whatever the
 // batch size: a light client's validator set signs block after block, so its
 // keys are parsed and tabulated once (gv_ed_keys_load) and every later commit
@@ -528,6 +537,123 @@ func (g *GPU) VerifyBatchEd25519Pub(pubs []ed25519.PubKeyEd25519, msgs, sigs [][
 	return ok
 }
 
+
+// SubmitBatch implements AsyncVerifier with VerifyBatch's routing (CPU below
+// CPUBelow, keyed leaves by arena slot, the rest by pub33) and fail-closed
+// rule.  g.mu is held from the slot lookup through the submission: once
+// queued, a batch needs no lock -- the library runs every queued batch
+// before a gv_keys_load / gv_keys_reset moves a slot.  The pinned buffers
+// stay referenced until wait returns (the library reads them until gv_wait).
+func (g *GPU) SubmitBatch(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]byte) func() []bool {
+	n := len(pubs)
+	idx := make([]int, 0, n)
+	total := 0
+	for i := range pubs {
+		if len(sigs[i]) == 64 { // VerifyBytes' first check
+			idx = append(idx, i)
+			total += len(msgs[i])
+		}
+	}
+	if n < g.CPUBelow || len(idx) == 0 || total+97*len(idx) > maxBatchBytes {
+		res := g.VerifyBatch(pubs, msgs, sigs) // nothing to overlap (CPU, empty) or split: synchronous
+		return func() []bool { return res }
+	}
+	type queued struct {
+		sel    []int
+		ticket C.uint64_t
+		rc     C.int
+		out    cbuf
+		bufs   []cbuf
+		what   string
+	}
+	submit := func(sel []int, slots []uint32) *queued {
+		m := len(sel)
+		q := &queued{sel: sel}
+		size := 0
+		for _, i := range sel {
+			size += len(msgs[i])
+		}
+		var key cbuf
+		if slots != nil {
+			key = g.newCBuf(4 * m)
+		} else {
+			key = g.newCBuf(33 * m)
+		}
+		sig, blob, off, ln := g.newCBuf(64*m), g.newCBuf(size), g.newCBuf(8*m), g.newCBuf(4*m)
+		q.out = g.newCBuf(m)
+		q.bufs = []cbuf{key, sig, blob, off, ln}
+		o := (*[maxBatchBytes / 8]uint64)(off.p)[:m:m]
+		l := (*[maxBatchBytes / 4]uint32)(ln.p)[:m:m]
+		pos := 0
+		for k, i := range sel {
+			if slots != nil {
+				(*[maxBatchBytes / 4]uint32)(key.p)[k] = slots[i]
+			} else {
+				copy(key.b[33*k:], pubs[i][:])
+			}
+			copy(sig.b[64*k:], sigs[i])
+			o[k], l[k] = uint64(pos), uint32(len(msgs[i]))
+			pos += copy(blob.b[pos:], msgs[i])
+		}
+		if slots != nil {
+			q.what = "gv_submit_msgs_keyed"
+			q.rc = C.gv_submit_msgs_keyed(g.ctx, C.size_t(m), (*C.uint32_t)(key.p), (*C.uint8_t)(sig.p),
+				(*C.uint8_t)(blob.p), (*C.uint64_t)(off.p), (*C.uint32_t)(ln.p), (*C.uint8_t)(q.out.p), &q.ticket)
+			atomic.AddUint64(&g.cnt.keyed, 1)
+		} else {
+			q.what = "gv_submit_msgs"
+			q.rc = C.gv_submit_msgs(g.ctx, C.size_t(m), (*C.uint8_t)(key.p), (*C.uint8_t)(sig.p),
+				(*C.uint8_t)(blob.p), (*C.uint64_t)(off.p), (*C.uint32_t)(ln.p), (*C.uint8_t)(q.out.p), &q.ticket)
+			atomic.AddUint64(&g.cnt.pub33, 1)
+		}
+		return q
+	}
+	var qs []*queued
+	if g.Keyed {
+		g.mu.Lock()
+		slots, loaded, _ := g.slotsLocked(pubs, n >= g.KeyLoadMin)
+		var keyed, rest []int
+		for _, i := range idx {
+			if loaded[i] {
+				keyed = append(keyed, i)
+			} else {
+				rest = append(rest, i)
+			}
+		}
+		if len(keyed) > 0 {
+			qs = append(qs, submit(keyed, slots))
+		}
+		g.mu.Unlock()
+		if len(rest) > 0 {
+			qs = append(qs, submit(rest, nil))
+		}
+	} else {
+		qs = append(qs, submit(idx, nil))
+	}
+	t0 := time.Now()
+	return func() []bool {
+		ok := make([]bool, n)
+		for _, q := range qs {
+			rc := q.rc
+			if rc == 0 {
+				rc = C.gv_wait(g.ctx, q.ticket)
+			}
+			g.done(q.what, len(q.sel), time.Since(t0), rc)
+			for k, i := range q.sel {
+				if rc == 0 {
+					ok[i] = q.out.b[k] == 1
+				} else {
+					ok[i] = pubs[i].VerifyBytes(msgs[i], sigs[i]) // fail closed to the reference path
+				}
+			}
+			for _, b := range q.bufs {
+				b.free()
+			}
+			q.out.free()
+		}
+		return ok
+	}
+}
 
 // ---- account key cache (gv_keys_load, SURVEY.md §8f-2)
 

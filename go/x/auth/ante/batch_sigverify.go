@@ -255,8 +255,14 @@ func (b *batch) build(pk crypto.PubKey, msg, sig []byte) *expr {
 // resolve answers every leaf: cache hits first, the misses in one Verifier
 // call per key type (ed25519 through v's EdVerifier side when it has one),
 // then the cache is filled.
+//
+// With an AsyncVerifier the secp256k1 misses are queued first and the ed25519
+// leaves resolved while the GPU runs them.
 func (b *batch) resolve(v gv.Verifier, cache *gv.VerdictCache) {
-	b.resolveEd(v, cache)
+	av, async := v.(gv.AsyncVerifier)
+	if !async {
+		b.resolveEd(v, cache)
+	}
 	n := len(b.pubs)
 	b.ok = make([]bool, n)
 	b.keys = make([][32]byte, n)
@@ -272,6 +278,9 @@ func (b *batch) resolve(v gv.Verifier, cache *gv.VerdictCache) {
 		miss = append(miss, i)
 	}
 	if len(miss) == 0 {
+		if async {
+			b.resolveEd(v, cache)
+		}
 		return
 	}
 	pubs := make([]secp256k1.PubKeySecp256k1, len(miss))
@@ -280,7 +289,14 @@ func (b *batch) resolve(v gv.Verifier, cache *gv.VerdictCache) {
 	for k, i := range miss {
 		pubs[k], msgs[k], sigs[k] = b.pubs[i], b.msgs[i], b.sigs[i]
 	}
-	res := v.VerifyBatch(pubs, msgs, sigs)
+	var res []bool
+	if async {
+		wait := av.SubmitBatch(pubs, msgs, sigs)
+		b.resolveEd(v, cache) // beside the queued secp256k1 batch
+		res = wait()
+	} else {
+		res = v.VerifyBatch(pubs, msgs, sigs)
+	}
 	for k, i := range miss {
 		b.ok[i] = res[k]
 		if cache != nil {

@@ -118,3 +118,56 @@ def test_go_ed25519_routes_like_the_mirror():
     assert "me >= app->key_load_min" in cpp
     commits = cpp[cpp.index('extern "C" int gvh_verify_commits('):]
     assert re.search(r"verify_ed\(app, e\.m,[^;]*t == 0\)", commits) and "k.keys_trusted ? 0 : 1" in commits
+
+
+def _split_args(text, start):
+    """The top-level arguments of the call whose '(' is at text[start]."""
+    depth, args, cur, i = 0, [], "", start
+    while i < len(text):
+        ch = text[i]
+        if ch in "([{":
+            depth += 1
+            if depth > 1:
+                cur += ch
+        elif ch in ")]}":
+            depth -= 1
+            if depth == 0:
+                if cur.strip():
+                    args.append(cur.strip())
+                return args
+            cur += ch
+        elif ch == "," and depth == 1:
+            args.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+        i += 1
+    raise AssertionError("unbalanced call")
+
+
+def test_go_cgo_calls_match_header_arity():
+    """No Go toolchain here: every C.gv_* call in the Go drop-in passes as many
+    arguments as include/gpuverify.h declares (the asynchronous gv_submit_* /
+    gv_wait calls of SubmitBatch included)."""
+    import re
+    hdr = open(os.path.join(REPO, "include", "gpuverify.h")).read()
+    protos = {}
+    for m in re.finditer(r"^[\w\s\*]*?\b(gv_\w+)\(([^;]*?)\);", hdr, re.M | re.S):
+        params = [p for p in m.group(2).replace("\n", " ").split(",") if p.strip()]
+        if params == ["void"]:
+            params = []
+        protos[m.group(1)] = len(params)
+    assert {"gv_submit_msgs", "gv_submit_msgs_keyed", "gv_wait"} <= set(protos)
+    seen = set()
+    for root, _, files in os.walk(os.path.join(REPO, "go")):
+        for f in files:
+            if not f.endswith(".go"):
+                continue
+            src = open(os.path.join(root, f)).read()
+            for m in re.finditer(r"C\.(gv_\w+)\(", src):
+                name = m.group(1)
+                assert name in protos, name
+                args = _split_args(src, m.end() - 1)
+                assert len(args) == protos[name], (f, name, len(args), protos[name])
+                seen.add(name)
+    assert {"gv_submit_msgs", "gv_submit_msgs_keyed", "gv_wait"} <= seen
