@@ -138,6 +138,11 @@ __global__ __launch_bounds__(256) void k_ed_keys_tab(uint32_t n, uint32_t base, 
 }
 
 #define EDL_MSG_LDS 2048                    // padded SHA-512 inputs up to 16 blocks take the LDS path
+// GV_EDL_SHA_VALU: the LDS-path SHA-512 on the VALU with the schedules of all
+// blocks expanded at once (sha512_wave); 0: the scalar-unit compression.
+#ifndef GV_EDL_SHA_VALU
+#define GV_EDL_SHA_VALU 1
+#endif
 
 struct EdlShared {
   union {                                   // the padded SHA-512 input (wave 0): R || A || M || padding
@@ -145,11 +150,83 @@ struct EdlShared {
     uint8_t msg[EDL_MSG_LDS];
     uint64_t words[EDL_MSG_LDS / 8];
   };
+  uint64_t wk[EDL_MSG_LDS / 128][80];       // each block's message schedule + round constants (sha512_wave)
   int hd[64];                               // signed radix-16 digits of h
   u32 xr[16], yr[16];                       // the decoded R, sliced
   u32 flags;                                // bit 0: R decodes, bit 1: S checks
   u32 pt[4][4][16];                         // wave sums X, Y, Z, T
 };
+
+// SHA-512 of the nblocks blocks staged in sh.words (one wave, every lane
+// alike), on the VALU.  Lane b < nblocks expands block b's message schedule
+// into sh.wk (W_t + K_t), all blocks at once; then the 80 rounds of each
+// block run with the state in VGPRs: a lane-varying zero added to the state
+// keeps the compiler from moving the (uniform) chain to the scalar unit,
+// where a 64-bit rotate is three dependent SALU operations -- on the VALU it
+// is two v_alignbit, and the xor / choose / majority terms fold into
+// three-input v_xor3 / v_bitop3.
+GV_DEV uint64_t sha_rotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit values as (lo, hi) 32-bit halves: a rotate is two v_alignbit, the
+// three-term xors one v_xor3 per half
+struct u64p { u32 lo, hi; };
+template <int N>
+GV_DEV u64p rotr_p(u64p x) {
+  if constexpr (N < 32) return {__builtin_amdgcn_alignbit(x.hi, x.lo, N), __builtin_amdgcn_alignbit(x.lo, x.hi, N)};
+  else return {__builtin_amdgcn_alignbit(x.lo, x.hi, N - 32), __builtin_amdgcn_alignbit(x.hi, x.lo, N - 32)};
+}
+// gfx950 v_bitop3_b32: any function of three inputs (truth table indexed by
+// a*4 + b*2 + c): 0x96 a ^ b ^ c, 0xCA choose (a ? b : c), 0xE8 majority
+template <int TT>
+GV_DEV u64p bop3_p(u64p a, u64p b, u64p c) {
+  return {(u32)__builtin_amdgcn_bitop3_b32(a.lo, b.lo, c.lo, TT), (u32)__builtin_amdgcn_bitop3_b32(a.hi, b.hi, c.hi, TT)};
+}
+GV_DEV u64p xor3_p(u64p a, u64p b, u64p c) { return bop3_p<0x96>(a, b, c); }
+GV_DEV u64p to_p(uint64_t v) { return {(u32)v, (u32)(v >> 32)}; }
+GV_DEV uint64_t from_p(u64p v) { return ((uint64_t)v.hi << 32) | v.lo; }
+template <class SH>
+GV_DEV void sha512_wave(uint64_t hs[8], SH& sh, u32 nblocks, u32 lane) {
+  if (lane < nblocks) {
+    uint64_t w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      w[j] = __builtin_bswap64(sh.words[lane * 16u + (u32)j]);
+      sh.wk[lane][j] = w[j] + kSha512K[j];
+    }
+#pragma unroll
+    for (int t = 16; t < 80; ++t) {
+      const u64p w15 = to_p(w[(t - 15) & 15]), w2 = to_p(w[(t - 2) & 15]);
+      const uint64_t s0 = from_p(xor3_p(rotr_p<1>(w15), rotr_p<8>(w15), to_p(w[(t - 15) & 15] >> 7)));
+      const uint64_t s1 = from_p(xor3_p(rotr_p<19>(w2), rotr_p<61>(w2), to_p(w[(t - 2) & 15] >> 6)));
+      w[t & 15] += s0 + w[(t - 7) & 15] + s1;
+      sh.wk[lane][t] = w[t & 15] + kSha512K[t];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  u32 vz;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+  uint64_t st[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) st[i] = hs[i] + vz;
+#pragma unroll 1
+  for (u32 blk = 0; blk < nblocks; ++blk) {
+    uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], hh = st[7];
+#pragma unroll
+    for (int t = 0; t < 80; ++t) {
+      const u64p ep = to_p(e), ap = to_p(a);
+      const uint64_t S1 = from_p(xor3_p(rotr_p<14>(ep), rotr_p<18>(ep), rotr_p<41>(ep)));
+      const uint64_t ch = from_p(bop3_p<0xCA>(ep, to_p(f), to_p(g)));      // (e & f) ^ (~e & g)
+      const uint64_t t1 = hh + S1 + ch + sh.wk[blk][t];
+      const uint64_t S0 = from_p(xor3_p(rotr_p<28>(ap), rotr_p<34>(ap), rotr_p<39>(ap)));
+      const uint64_t mj = from_p(bop3_p<0xE8>(ap, to_p(b), to_p(c)));     // majority
+      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += hh;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) hs[i] = st[i];
+}
 
 // Wave-wide: h = SHA-512(R || A || M) mod L and its 64 signed radix-16 digits
 // into sh.hd; sw = the signature words, aw = A's words (the bytes Verify hashes).
@@ -179,6 +256,9 @@ GV_DEV void edl_hash_digits(SH& sh, const u32 sw[16], const u32 aw[8], const uin
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     uint64_t hs[8] = {0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull, 0x3c6ef372fe94f82bull, 0xa54ff53a5f1d36f1ull,
                       0x510e527fade682d1ull, 0x9b05688c2b3e6c1full, 0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull};
+#if GV_EDL_SHA_VALU
+    sha512_wave(hs, sh, nblocks, lane);
+#else
 #pragma unroll 1
     for (u32 blk = 0; blk < nblocks; ++blk) {
       uint64_t w[16];
@@ -186,6 +266,7 @@ GV_DEV void edl_hash_digits(SH& sh, const u32 sw[16], const u32 aw[8], const uin
       for (int j = 0; j < 16; ++j) w[j] = __builtin_bswap64(sh.words[blk * 16u + (u32)j]);
       sha512_compress(hs, w);
     }
+#endif
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       dig[2 * i] = __builtin_bswap32((u32)(hs[i] >> 32));
@@ -419,6 +500,7 @@ struct EduShared {
     uint8_t msg[EDL_MSG_LDS];
     uint64_t words[EDL_MSG_LDS / 8];
   };
+  uint64_t wk[EDL_MSG_LDS / 128][80];       // each block's message schedule + round constants (sha512_wave)
   int hd[64];                               // signed radix-16 digits of h
   u32 xr[16], yr[16];                       // the decoded R, sliced
   u32 flags;                                // bit 0: R decodes, bit 1: S checks
