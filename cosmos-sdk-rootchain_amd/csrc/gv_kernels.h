@@ -196,6 +196,9 @@ typedef struct gvk_lat {
   // pub33 sliced batches with gtab6 set (the runtime: n <= lat_rows_max)
   // take k_verify_lat_sl4 (row-parallel ladders, G from the 24-bit tables)
   const uint32_t* gtab6;
+  // keyed sliced batches with kn != 0 (and gtab6): k_verify_lat16_kn over the
+  // resident arena's kn tables (kqt = kqt6, kqt2 = kqt62, kzq = kzq6)
+  int kn;
 } gvk_lat;
 
 // ed25519 (ed_verify.hip): one signature per lane over C lanes (C % 256 == 0).

@@ -74,6 +74,7 @@ static __constant__ const u32 kLP[8] = {0xFFFFFC2Fu, 0xFFFFFFFEu, 0xFFFFFFFFu, 0
 struct LatShared {
   static constexpr bool kG5 = false;         // G digits: 20-bit windows (dg)
   static constexpr bool kG24 = false;
+  static constexpr bool kQ6 = false;          // Q digits: 5-bit windows (6-bit: the kn arena)
   u32 qtab[GV_LAT_SIGS][2][GV_QTAB_N][18];  // Q, lambda*Q entries: x, y raw 29-bit limbs (effective affine)
   u32 ratio[64][GV_QTAB_N - 1][9];          // per-lane Z-ratio scratch of the table build (raw limbs)
   u32 dq[GV_LAT_SIGS][GV_QWIN];             // packed int16 Q / lambda*Q digits per window
@@ -333,6 +334,7 @@ GV_DEV void lat_keyed_tables(LatShared& sh, int sig, int slot, bool live, u32 ks
 struct Lat16Shared {
   static constexpr bool kG5 = true;          // G digits: 5-bit windows like Q (dg5)
   static constexpr bool kG24 = false;
+  static constexpr bool kQ6 = false;          // Q digits: 5-bit windows (6-bit: the kn arena)
   u32 dq[GV_LAT16_SIGS][GV_QWIN];            // packed int16 Q / lambda*Q digits per window
   u32 dg5[GV_LAT16_SIGS][GV_QWIN];           // packed int16 G / lambda*G digits per window
   u32 r[GV_LAT16_SIGS][8];
@@ -404,9 +406,10 @@ GV_DEV void lat_scalars_e(SH& sh, int sig, bool live, const uint8_t* sig64, GetE
 #pragma unroll
     for (int i = 0; i < 4; ++i) { k1g[i] = k2g[i] = k1q[i] = k2q[i] = 0u; }
   }
+  constexpr int QW = SH::kQ6 ? GV_K6_QW : GV_QW, QWIN = SH::kQ6 ? GV_K6_QWIN : GV_QWIN;
 #pragma unroll
-  for (int win = 0; win < GV_QWIN; ++win) {
-    int d0 = booth_digit<GV_QW>(k1q, win), d1 = booth_digit<GV_QW>(k2q, win);
+  for (int win = 0; win < QWIN; ++win) {
+    int d0 = booth_digit<QW>(k1q, win), d1 = booth_digit<QW>(k2q, win);
     if (n1q) d0 = -d0;
     if (n2q) d1 = -d1;
     sh.dq[sig][win] = ((u32)d0 & 0xFFFFu) | ((u32)d1 << 16);
@@ -786,6 +789,7 @@ __global__ __launch_bounds__(128) void k_verify_lat16(const gvk_lat b) {
 struct LatSlShared {
   static constexpr bool kG5 = false;         // G digits: 20-bit windows (dg)
   static constexpr bool kG24 = false;
+  static constexpr bool kQ6 = false;          // Q digits: 5-bit windows (6-bit: the kn arena)
   u32 qtab[2][GV_QTAB_N][18];               // Q, lambda*Q entries: x, y sliced limbs (effective affine)
   u32 ratio[GV_QTAB_N - 1][9];              // Z ratios, then their suffix products
   u32 dq[1][GV_QWIN];
@@ -1093,6 +1097,7 @@ __global__ __launch_bounds__(192) void k_verify_lat_sl(const gvk_lat b) {
 struct LatSl4Shared {
   static constexpr bool kG5 = false;
   static constexpr bool kG24 = true;
+  static constexpr bool kQ6 = false;          // Q digits: 5-bit windows (6-bit: the kn arena)
   u32 qtab[2][GV_QTAB_N][18];               // Q', lambda*Q' entries (effective affine, sliced limbs)
   u32 ratio[GV_QTAB_N - 1][9];
   u32 dq[1][GV_QWIN];
@@ -1369,6 +1374,7 @@ __global__ __launch_bounds__(256) void k_verify_lat_sl4(const gvk_lat b) {
 struct Lat16SlShared {
   static constexpr bool kG5 = true;
   static constexpr bool kG24 = false;
+  static constexpr bool kQ6 = false;          // Q digits: 5-bit windows (6-bit: the kn arena)
   u32 eh[8];                                // message path: the SHA-256 state of the sign bytes (wave 1)
   u32 dq[1][GV_QWIN];
   u32 dg5[1][GV_QWIN];
@@ -1522,6 +1528,180 @@ __global__ __launch_bounds__(256) void k_verify_lat16_sl(const gvk_lat b) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Keyed small batches on the resident arena's kn tables (k_verify_lat16_kn):
+// the slot's 11 group tables of 32 entries (2^(12 g) Q, g < 11, on one Z,
+// 6-bit Booth windows: window 2g + p at position p of group g) need only 6
+// doublings, and G comes from the 24-bit tables (u1 unsplit, 11 windows, no
+// doubling at all).  One signature per 256-thread block, 16 rows: row g < 11
+// adds group g's Q and lambda*Q entries of its two positions around the 6
+// doublings and lifts its sum by the tables' Z; rows 12..15 (wave 3) add the
+// G windows j == row - 12 (mod 4); row 11 has nothing to add.  The 16 sums
+// are joined four per wave with the row-parallel complete addition
+// (gj4_add_gej), then by wave 0.  Same verdicts as k_verify_lat16_sl.
+struct Lat16KnShared {
+  static constexpr bool kG5 = false;
+  static constexpr bool kG24 = true;
+  static constexpr bool kQ6 = true;
+  u32 eh[8];                                // message path: the SHA-256 state of the sign bytes (wave 1)
+  u32 dq[1][GV_QWIN];                       // GV_K6_QWIN used
+  int dg24[1][GV_K6_GWIN];
+  u32 r[1][8];
+  u32 oks[1];
+  u32 pt[16][3][16];                        // the rows' sums, sliced
+  u32 pinf[16];
+  u32 pw[4][3][16];                         // the waves' sums
+  u32 pwinf[4];
+};
+static_assert(GV_K6_QWIN == 2 * GV_KN_ARENA_NG && GV_KN_ARENA_NG <= 12 && GV_K6_GWIN <= 12, "kn rows");
+
+__global__ __launch_bounds__(256) void k_verify_lat16_kn(const gvk_lat b) {
+  __shared__ Lat16KnShared sh;
+  const u32 gi = blockIdx.x;                            // grid = n: every block is live
+  u32 sl = b.kslot[gi];
+  bool kok = sl < b.kcount;
+  if (!kok) sl = 0;                                     // the arena always holds slot 0's memory
+  kok = kok && b.kok[sl] != 0u;
+  if (b.msg_len) {
+    if (threadIdx.x < 64) {
+      lat_scalars_e<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, [&](u32 e[8]) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = sh.eh[7 - i];
+      });
+    } else {
+      if (threadIdx.x < 128) {
+        u32 eh[8];
+        sha256_msg_wave(eh, b.msg_blob + b.msg_off[gi], b.msg_len[gi]);
+        if (threadIdx.x == 64) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) sh.eh[i] = eh[i];
+        }
+      }
+      __syncthreads();
+    }
+  } else if (threadIdx.x < 64) {
+    lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.dig32 + (size_t)gi * 32u, nullptr, b.C, gi);
+  }
+  __syncthreads();
+  const fslk k = fsl_consts();
+  const u32 L = k.L, r16 = threadIdx.x >> 4, wave = threadIdx.x >> 6, row = r16 & 3u;
+  const bool lo = L < 9u;
+  gjsl A;
+  A.x = 0u; A.y = 0u; A.z = 0u;
+  bool inf = true;
+  if (wave < 3u) {                                      // rows 0..11: Q groups (row 11: none)
+    const u32 g = r16;
+    u32 beta;
+    {
+      u32 w[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) w[i] = kLBeta[i];
+      beta = fsl_from_words(w, k);
+    }
+    const u32* tab = g == 0u ? b.kqt + (size_t)sl * GV_K6_KEY_WORDS
+                             : b.kqt2 + ((size_t)sl * (GV_KN_ARENA_NG - 1) + (g - 1u)) * GV_K6_KEY_WORDS;
+#pragma unroll 1
+    for (int p = 1; p >= 0; --p) {
+      if (p == 0 && !inf) {
+#pragma unroll 1
+        for (int dd = 0; dd < GV_K6_QW; ++dd) gjsl_double(A, A, k);
+      }
+      const u32 dq = g < GV_KN_ARENA_NG ? sh.dq[0][2u * g + (u32)p] : 0u;
+#pragma unroll 1
+      for (int t = 0; t < 2; ++t) {
+        const int d = t == 0 ? ((int)(dq << 16) >> 16) : ((int)dq >> 16);
+        if (d == 0) continue;
+        const u32* pe = tab + (size_t)((d < 0 ? -d : d) - 1) * GV_QENT_WORDS;
+        u32 x = lo ? pe[L] : 0u;
+        u32 y = lo ? pe[9 + L] : 0u;
+        if (t == 1) x = fsl_mul(x, beta, k);            // lambda Q = (beta x, y), same Z
+        if (d < 0) y = k.bias - y;
+        if (inf) {
+          A.x = x; A.y = fsl_norm(y, k); A.z = L == 0u ? 1u : 0u;
+          inf = false;
+        } else {
+          gjsl_add_scaled(A, inf, x, y, A.z, k);
+        }
+      }
+    }
+    {                                                   // back to the real curve: Z * (the tables' Z)
+      u32 w[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) w[i] = b.kzq[(size_t)i * b.kC + sl];
+      A.z = fsl_mul(A.z, fsl_from_words(w, k), k);
+    }
+  } else {                                              // rows 12..15: G windows j = row (mod 4)
+#pragma unroll 1
+    for (u32 j = row; j < GV_K6_GWIN; j += 4u) {
+      const int d = sh.dg24[0][j];
+      if (d == 0) continue;
+      const u32* pe = b.gtab6 + ((size_t)j * GV_K6_GTAB_N + (u32)((d < 0 ? -d : d) - 1)) * 16u;
+      const u32 x = fsl_load_words(pe, k);
+      u32 y = fsl_load_words(pe + 8, k);
+      if (d < 0) y = k.bias - y;
+      if (inf) {
+        A.x = x; A.y = fsl_norm(y, k); A.z = L == 0u ? 1u : 0u;
+        inf = false;
+      } else {
+        gjsl_add_scaled(A, inf, x, y, A.z, k);
+      }
+    }
+  }
+  if (lo) { sh.pt[r16][0][L] = A.x; sh.pt[r16][1][L] = A.y; sh.pt[r16][2][L] = A.z; }
+  if (L == 0u) sh.pinf[r16] = inf ? 1u : 0u;
+  __syncthreads();
+  // each wave: its four rows' sums, replicated over its rows, row-parallel additions
+  {
+    const u32 r0 = wave * 4u;
+    A.x = lo ? sh.pt[r0][0][L] : 0u; A.y = lo ? sh.pt[r0][1][L] : 0u; A.z = lo ? sh.pt[r0][2][L] : 0u;
+    inf = sh.pinf[r0] != 0u;
+#pragma unroll 1
+    for (u32 j = 1; j < 4u; ++j) {
+      gjsl O;
+      O.x = lo ? sh.pt[r0 + j][0][L] : 0u; O.y = lo ? sh.pt[r0 + j][1][L] : 0u; O.z = lo ? sh.pt[r0 + j][2][L] : 0u;
+      gj4_add_gej(A, inf, O, sh.pinf[r0 + j] != 0u, row, k);
+    }
+    if (row == 0u) {
+      if (lo) { sh.pw[wave][0][L] = A.x; sh.pw[wave][1][L] = A.y; sh.pw[wave][2][L] = A.z; }
+      if (L == 0u) sh.pwinf[wave] = inf ? 1u : 0u;
+    }
+  }
+  __syncthreads();
+  if (wave != 0u) return;
+#pragma unroll 1
+  for (u32 j = 1; j < 4u; ++j) {
+    gjsl O;
+    O.x = lo ? sh.pw[j][0][L] : 0u; O.y = lo ? sh.pw[j][1][L] : 0u; O.z = lo ? sh.pw[j][2][L] : 0u;
+    gj4_add_gej(A, inf, O, sh.pwinf[j] != 0u, row, k);
+  }
+  const u32 fl = sh.oks[0];
+  bool okv = (fl & 1u) && kok && !inf;
+  u32 rw[8], X[8], T[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rw[i] = sh.r[0][i];
+  const u32 zz = fsl_sqr(A.z, k);
+  fsl_to_words(X, A.x);
+  fsl_to_words(T, fsl_mul(fsl_from_words(rw, k), zz, k));
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) eq &= (X[i] == T[i]);
+  if (!eq && (fl & 2u)) {
+    u32 rn[8], c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rn[i] = __builtin_addc(rw[i], kN[i], c, &c);
+    fsl_to_words(T, fsl_mul(fsl_from_words(rn, k), zz, k));
+    eq = true;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) eq &= (X[i] == T[i]);
+  }
+  okv &= eq;
+  if (threadIdx.x == 0) {
+    if (b.out8) b.out8[gi] = okv ? 1u : 0u;
+    else if (okv) atomicOr((unsigned long long*)&b.bits[gi >> 6], 1ull << (gi & 63u));
+  }
+}
+
 }  // namespace gv
 
 extern "C" hipError_t gvk_verify_lat16(const gvk_lat* b, hipStream_t st) {
@@ -1558,7 +1738,8 @@ extern "C" hipError_t gvk_verify_lat16_sl(const gvk_lat* b, hipStream_t st) {
     if (e != hipSuccess) return e;
   }
   if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
-  hipLaunchKernelGGL(gv::k_verify_lat16_sl, dim3(b->n), dim3(256), 0, st, *b);
+  if (b->kn && b->gtab6) hipLaunchKernelGGL(gv::k_verify_lat16_kn, dim3(b->n), dim3(256), 0, st, *b);
+  else hipLaunchKernelGGL(gv::k_verify_lat16_sl, dim3(b->n), dim3(256), 0, st, *b);
   return hipGetLastError();
 }
 

@@ -910,6 +910,11 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     d->routes[kslot ? GV_ROUTE_LAT_KEYED : GV_ROUTE_LAT]++;
     if (kslot) {                                // keyed: 16 lanes per signature (group tables)
       lb.kqt2 = b.kqt2; lb.kzq2 = kzq2; lb.glat = d->glat;
+      if (sliced && !ka && ctx->keys_k6 && d->kqt6 && d->gtab6 && d->keys6 >= ctx->keys) {
+        // every slot has its kn tables: k_verify_lat16_kn (6 doublings, G from the 24-bit tables)
+        lb.kqt = d->kqt6; lb.kzq = d->kzq6; lb.kqt2 = d->kqt62; lb.kzq2 = nullptr;
+        lb.gtab6 = d->gtab6; lb.kn = 1;
+      }
       if (sliced) CK(gvk_verify_lat16_sl(&lb, st));
       else CK(gvk_verify_lat16(&lb, st));
     } else if (sliced) {

@@ -20,18 +20,27 @@ def ver():
     v.close()
 
 
-@pytest.fixture(params=sorted(p for p in PATHS if p != "latency_rows"))   # rows: pub33 only
+# (lat_max, sliced, keys_k6): the PATHS schedules (rows: pub33 only) with the
+# resident arena's kn tables, plus the sliced kernel on the k4 tables
+KEYED_PATHS = {**{p: (v[0], v[1], 1) for p, v in PATHS.items() if p != "latency_rows"},
+               "latency_k4_arena": (1 << 30, 1, 0)}
+
+
+@pytest.fixture(params=sorted(KEYED_PATHS))
 def path(request, ver):
     """Keyed batches take the fused small-batch kernel up to lat_max
-    (k_verify_lat16_sl, or k_verify_lat16 with lat_sliced 0), the throughput
-    pipeline above it: every schedule is checked."""
-    lat_max, sliced, _ = PATHS[request.param]
+    (k_verify_lat16_kn on the arena's kn tables, k_verify_lat16_sl on its k4
+    tables with keys_k6 0, or k_verify_lat16 with lat_sliced 0), the
+    throughput pipeline above it: every schedule is checked."""
+    lat_max, sliced, keys_k6 = KEYED_PATHS[request.param]
     ver.set_option("lat_max", lat_max)
     ver.set_option("lat_sliced", sliced)
     ver.set_option("lat_sl_max", 1 << 30)
+    ver.set_option("keys_k6", keys_k6)
     yield request.param
     ver.reset_schedule()
     ver.set_option("lat_sliced", 1)
+    ver.set_option("keys_k6", 1)
 
 
 def keyed_inputs(ver, pub):
