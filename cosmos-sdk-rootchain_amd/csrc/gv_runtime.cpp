@@ -141,9 +141,10 @@ struct Dev {
   bool gtabf_failed = false;                      // its allocation failed once: k4 keeps the GLV G tables
   bool gtab4_failed = false;                      // gtab4's allocation failed: keyed batches on the 125-doubling ladder
   size_t kcap = 0;
-  // the resident k6 arena (option "keys_k6"): per slot the four 32-entry group
-  // tables of Q, 2^36 Q, 2^72 Q, 2^102 Q on one Z (kzq6, 8 rows of stride
-  // kcap; kzq62 holds the chain's parked Zs), read by k_ecmult_k6
+  // the resident kn arena (option "keys_k6"): per slot the GV_KN_ARENA_NG (11)
+  // 32-entry group tables of 2^(12 g) Q on one Z (kqt6: group 0, kqt62: groups
+  // 1.., kzq6: the Z, 8 rows of stride kcap; kzq62 holds the chain's parked
+  // Zs), read by k_ecmult_kn and k_verify_lat16_kn
   uint32_t *kqt6 = nullptr, *kzq6 = nullptr, *kqt62 = nullptr, *kzq62 = nullptr;
   size_t keys6 = 0;                               // leading slots whose k6 tables are built
   // HBM held by the optional tables (G tables, key arenas) against ctx->hbm_budget
