@@ -216,7 +216,11 @@ GV_DEV bool key_equal(const u32* x, const u32* pfx, u32 C, u32 a, u32 b) {
   return eq;
 }
 // rep[g] = the first-inserted item with g's key (table: tmask + 1 slots of
-// 0xFFFFFFFF, at least twice the items).
+// 0xFFFFFFFF, at least twice the items).  A key ParsePubKey rejects on its
+// bytes alone -- prefix not 02/03, x >= p -- gets no id and no tables:
+// rep[g] = 0xFFFFFFFF, and k_dedupe_map gives its items an out-of-range slot,
+// which the keyed pipeline answers false (the adversarial mix's malformed
+// keys are distinct per item: each would otherwise cost a table build).
 __global__ __launch_bounds__(256) void k_dedupe(u32 n, u32 C, const u32* x, const u32* pfx, u32* table, u32 tmask,
                                                  u32* rep) {
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -224,6 +228,13 @@ __global__ __launch_bounds__(256) void k_dedupe(u32 n, u32 C, const u32* x, cons
   u32 w[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) w[i] = x[(size_t)i * C + g];
+  {
+    u32 br = 0, d;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d = __builtin_subc(w[i], kP[i], br, &br);
+    (void)d;
+    if ((pfx[g] & 0xFEu) != 0x02u || br == 0u) { rep[g] = 0xFFFFFFFFu; return; }   // x >= p: no borrow
+  }
   for (u32 sl = key_hash(w, pfx[g]) & tmask;; sl = (sl + 1) & tmask) {
     const u32 cur = atomicCAS(&table[sl], 0xFFFFFFFFu, g);
     if (cur == 0xFFFFFFFFu) { rep[g] = g; return; }
@@ -255,7 +266,7 @@ __global__ __launch_bounds__(256) void k_dedupe_assign(u32 n, u32 C, const u32* 
 }
 __global__ __launch_bounds__(256) void k_dedupe_map(u32 n, const u32* rep, const u32* uid, u32* kslot) {
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n) kslot[g] = uid[rep[g]];
+  if (g < n) kslot[g] = rep[g] == 0xFFFFFFFFu ? 0xFFFFFFFFu : uid[rep[g]];
 }
 
 // ------------------------------------------------------------------ k_sha256
