@@ -41,6 +41,21 @@ def ver():
     v.close()
 
 
+@pytest.fixture(scope="module")
+def ver2():
+    """Two device slots on GPU 0: every host batch over 256 items is split
+    across two contexts' worth of streams and staging (run_sliced, one slice
+    on the caller and one on slot 1's persistent worker), the path an 8-GPU
+    node's batches take, exercised on a 1-GPU box."""
+    v = gvm.Verifier([0, 0])
+    yield v
+    v.close()
+
+
+def slot_ver(request, slots):
+    return request.getfixturevalue("ver" if slots == 1 else "ver2")
+
+
 class SecpKey:
     def __init__(self, tag: bytes):
         self.priv = T.privkey_from_secret(b"c4-" + tag)
@@ -135,7 +150,9 @@ def check_block(results, txs, parts, ref, state_seq):
         state_seq[a.addr] = ref.accounts[a.addr].sequence
 
 
-def test_c4_multisig_block_replay(ver):
+@pytest.mark.parametrize("slots", [1, 2])
+def test_c4_multisig_block_replay(request, slots):
+    ver = slot_ver(request, slots)
     rng = random.Random(0xC4)
     shapes = [(2, 3, False), (3, 5, False), (4, 7, False), (2, 3, True), (3, 5, True)]
     accts = [MultiAcct(i, *shapes[i % len(shapes)]) for i in range(15)]
@@ -157,6 +174,9 @@ def test_c4_multisig_block_replay(ver):
     assert set(codes) == {0, 4} and codes.count(0) > 200
     st = app.stats()
     assert st["gpu_calls"] >= 3 and st["memo_hits"] > 0
+    if slots == 2:                                      # the last batch was split over both slots
+        sl = ver.last_slices()
+        assert len(sl) == 2 and all(n > 0 for _, n in sl), sl
     app.close()
 
 
@@ -429,7 +449,8 @@ def test_parallel_deliver_loop_equals_serial_ante(ver):
     assert 0 < serial.count(0) < len(serial)
 
 
-def test_pipelined_replay_equals_block_by_block(ver):
+@pytest.mark.parametrize("slots", [1, 2])
+def test_pipelined_replay_equals_block_by_block(request, slots):
     """gvh_deliver_blocks (block b+1 pre-verified, its prediction carrying
     block b's sequence increments and SetPubKeys, and its GPU batch run while
     block b delivers) gives the codes and final state of delivering the blocks
@@ -439,7 +460,9 @@ def test_pipelined_replay_equals_block_by_block(ver):
     stored: later txs fail 'pubkey on account is not set'), and blocks large
     enough for the parallel ante loop.  The carried predictions must hit: the
     pipelined replay's memo hits stay within 1 % of the one-by-one
-    replay's."""
+    replay's.  slots = 2: the same over two device slots (every batch split,
+    the queued batches of the replay on both slots' lanes)."""
+    ver = slot_ver(request, slots)
     rng = random.Random(0xB10C)
     shapes = [(2, 3, False), (3, 5, False), (4, 7, True)]
     accts = [MultiAcct(300 + i, *shapes[i % len(shapes)]) for i in range(12)]
