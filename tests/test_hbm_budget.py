@@ -94,12 +94,16 @@ def test_budget_degrades_with_the_same_verdicts(batch, mb, grouped_route, keyed_
         ver.close()
 
 
-def test_default_budget_takes_the_arena_k6_tables(batch):
+def test_default_budget_takes_the_arena_k8_then_k6_tables(batch):
     pub, sig, dig, exp = batch
     ver = gvm.Verifier([0])
     try:
         uniq, inv = np.unique(pub, axis=0, return_inverse=True)
         slots = ver.keys_load(uniq)[inv.reshape(-1)].astype(np.uint32)
+        got, routes = routes_of(ver, lambda: ver.verify_batch_digests_keyed(slots, sig, dig))
+        assert np.array_equal(got, exp)
+        assert routes.get("kn8", 0) >= 1, routes
+        ver.set_option("keys_k8", 0)                  # the k6 tables of the same slots
         got, routes = routes_of(ver, lambda: ver.verify_batch_digests_keyed(slots, sig, dig))
         assert np.array_equal(got, exp)
         assert routes.get("kn", 0) >= 1, routes
