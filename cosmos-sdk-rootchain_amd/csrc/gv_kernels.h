@@ -82,10 +82,10 @@ typedef struct gvk_batch {
   // (GV_K6_GTAB_WORDS: the full-scalar 24-bit-window G tables); gtab4 unused
   const uint32_t* gtab6;
   int k6;
-  // kq8 set (with k6 == GV_K8_ARENA_NG): kqt / kqt2 / kzq are the resident
-  // arena's 8-bit-window tables (128 entries per group) and the ladder is
-  // k_ecmult_kn<8, GV_K8_ARENA_NG>
-  int kq8;
+  // kqw set (with k6 == GV_KW_ARENA_NG): kqt / kqt2 / kzq are the resident
+  // arena's wide-window tables (GV_KW_NT entries per group) and the ladder is
+  // k_ecmult_kn<GV_KW_QW, GV_KW_ARENA_NG>
+  int kqw;
   // k4 batches with gtabf set: the G half on the unsplit scalar (GV_GF_*),
   // k_prep<.., GF> digits and k_ecmult_k4<true> over gtabf (GV_GF_WORDS)
   const uint32_t* gtabf;
@@ -154,22 +154,26 @@ hipError_t gvk_unsort_bits(uint32_t n, const uint32_t* pos, const uint64_t* sbit
 static_assert(GV_K6_QWIN + GV_K6_GWIN <= GV_DIGIT_ROWS, "k6 digits fit the digit rows");
 static_assert(GV_K6_QW * GV_K6_QWIN >= 130 && GV_K6_GW * GV_K6_GWIN >= 257, "k6 windows cover the scalars");
 
-// The resident arena's 8-bit-window tables (option "keys_k8", k_ecmult_kn<8,
-// GV_K8_ARENA_NG>): 128 multiples per group, 17 signed 8-bit windows per
-// 128-bit GLV half in 9 groups (8 of two windows, one of one), so the ladder
-// runs 2 positions: 8 doublings and 34 Q additions (k6 arena: 6 and 44).  G
-// as on the k6 ladders (11 24-bit windows after the last doubling, gtab6).
-// 9 x 10 KiB of tables per key: built at gv_keys_load beside the k6 tables
-// while the key set fits the HBM budget (kn on the k6 tables otherwise).
-#define GV_K8_QW 8
-#define GV_K8_NT 128
-#define GV_K8_QWIN 17
-#define GV_K8_KEY_WORDS (GV_K8_NT * GV_QENT_WORDS)       // one group table (10,240 B)
-#ifndef GV_K8_ARENA_NG
-#define GV_K8_ARENA_NG 9
+// The resident arena's wide-window tables (option "keys_wide",
+// k_ecmult_kn<GV_KW_QW, GV_KW_ARENA_NG>): 2^(QW-1) multiples per group, the
+// signed QW-bit windows of each 128-bit GLV half two per group, so the ladder
+// runs 2 positions.  QW = 9 (default): 256 entries, 15 windows in 8 groups,
+// 9 doublings and 30 Q additions (k6 arena: 6 and 44; QW 8: 8 and 34; QW 7:
+// 7 and 38).  G as on the k6 ladders (11 24-bit windows after the last
+// doubling, gtab6).  8 x 20 KiB of tables per key, built at gv_keys_load
+// beside the k6 tables while the key set fits (kn on the k6 tables otherwise).
+// A/B on one box (profiles/r05/kw/): c2_key_cache QW 7 / 8 / 9 = 329-344 /
+// 366 / 380-381M/s, k6 arena 312-317M/s.
+#ifndef GV_KW_QW
+#define GV_KW_QW 9                                        // (an A/B build may set 7 or 8)
 #endif
-static_assert(GV_K8_QWIN + GV_K6_GWIN <= GV_DIGIT_ROWS, "k8 digits fit the digit rows");
-static_assert(GV_K8_QW * GV_K8_QWIN >= 130, "k8 windows cover the GLV halves");
+#define GV_KW_NT (1 << (GV_KW_QW - 1))                    // 256 table entries per group
+#define GV_KW_QWIN ((130 + GV_KW_QW - 1) / GV_KW_QW)      // 15 windows per GLV half
+#define GV_KW_KEY_WORDS (GV_KW_NT * GV_QENT_WORDS)       // one group table (20,480 B)
+#define GV_KW_ARENA_NG ((GV_KW_QWIN + 1) / 2)             // 8 groups: two windows each, the last one or two
+static_assert(GV_KW_QW >= 7 && GV_KW_QW <= 9, "wide arena window width");
+static_assert(GV_KW_QWIN + GV_K6_GWIN <= GV_DIGIT_ROWS, "wide-window digits fit the digit rows");
+static_assert(GV_KW_QW * GV_KW_QWIN >= 130, "wide windows cover the GLV halves");
 
 // The k4 ladder's G half on the unsplit scalar (k_ecmult_k4<true>): u1 = e/s
 // is not GLV-split; its 11 signed 25-bit windows (window j at bit 25 j) are
@@ -306,13 +310,13 @@ hipError_t gvk_keys_build6(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_
                            uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* scratch, int with_qe,
                            uint32_t base, uint32_t* kqt6, uint32_t* kzq6, uint32_t kC, uint32_t* kok, uint32_t* kqt62,
                            uint32_t* kzq62, hipStream_t st);
-// The resident arena's k8 tables (GV_K8_ARENA_NG groups of 128 entries),
-// same arguments as gvk_keys_build6 (kqt8: GV_K8_KEY_WORDS per slot, kqt82:
-// GV_K8_ARENA_NG - 1 rows per slot, kzq82: (GV_K8_ARENA_NG - 1) x 8 rows).
-hipError_t gvk_keys_build8(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
+// The resident arena's wide-window tables (GV_KW_ARENA_NG groups of GV_KW_NT entries),
+// same arguments as gvk_keys_build6 (kqtw: GV_KW_KEY_WORDS per slot, kqtw2:
+// GV_KW_ARENA_NG - 1 rows per slot, kzqw2: (GV_KW_ARENA_NG - 1) x 8 rows).
+hipError_t gvk_keys_build_wide(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
                            uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* scratch, int with_qe,
-                           uint32_t base, uint32_t* kqt8, uint32_t* kzq8, uint32_t kC, uint32_t* kok, uint32_t* kqt82,
-                           uint32_t* kzq82, hipStream_t st);
+                           uint32_t base, uint32_t* kqtw, uint32_t* kzqw, uint32_t kC, uint32_t* kok, uint32_t* kqtw2,
+                           uint32_t* kzqw2, hipStream_t st);
 // the full-scalar G tables (GV_GF_WORDS words); base_scratch: 96 words
 hipError_t gvk_gen_gtablef(uint32_t* gtabf, uint32_t* base_scratch, hipStream_t st);
 // Key-table builds (k_keys_chain + k_keys_fwd + k_keys_back): scratch of

@@ -629,8 +629,9 @@ GV_DEV bool parse_pubkey(u32 pre, const fe& x, fe& y) {
 // GV_K6_GW-bit G windows) instead of GV_QW / GV_GW.
 // GF (keyed k4 only): G digits of the unsplit u1 (GV_GF_WIN signed
 // GV_GF_W-bit windows, one int32 row each: digits[(GV_QWIN + j)*C + g]).
-// K8 (with K6, GF): 8-bit Q windows (the resident arena's k8 tables), G as K6.
-template <bool KEYED, bool K6 = false, bool GF = false, bool K8 = false>
+// KW (with K6, GF): GV_KW_QW-bit Q windows (the resident arena's wide-window
+// tables), G as K6.
+template <bool KEYED, bool K6 = false, bool GF = false, bool KW = false>
 __global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u32* in_x, const u32* in_pfx,
                                                const u32* in_r, const u32* in_s, const u32* in_e,
                                                const u32* in_w, u32* digits, u32* qt, u32* zq_out,
@@ -706,8 +707,8 @@ __global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u
   // [-2^(GV_GW-1), 2^(GV_GW-1)]) as int32: digits[(GV_QWIN + 2j)*C + g] = dG1,
   // digits[(GV_QWIN + 2j + 1)*C + g] = dG2, j = 0..GV_GWIN-1.
   static_assert(GF || !K6, "the k6 ladder takes G on the unsplit scalar");
-  static_assert(!K8 || K6, "k8 digits: the k6 ladder's G windows");
-  constexpr int QW = K8 ? GV_K8_QW : K6 ? GV_K6_QW : GV_QW, QWIN = K8 ? GV_K8_QWIN : K6 ? GV_K6_QWIN : GV_QWIN;
+  static_assert(!KW || K6, "wide-window digits: the k6 ladder's G windows");
+  constexpr int QW = KW ? GV_KW_QW : K6 ? GV_K6_QW : GV_QW, QWIN = KW ? GV_KW_QWIN : K6 ? GV_K6_QWIN : GV_QWIN;
   constexpr int GW = GV_GW, GWIN = GV_GWIN;
   constexpr int GFW = K6 ? GV_K6_GW : GV_GF_W, GFWIN = K6 ? GV_K6_GWIN : GV_GF_WIN;
 #pragma unroll
@@ -755,10 +756,10 @@ __constant__ const int kLGrpBit[GV_LGRP] = {0, 35, 70, 100};
 // w0(k), i.e. its table is that of 2^(QW w0(k)) Q; the ladder runs P
 // positions.  <5, 4>: k_ecmult_k4 (groups at bits 0, 35, 70, 100); <6, 4>:
 // the grouped route's k6 (0, 36, 72, 102); <6, GV_KN_ARENA_NG> and
-// <8, GV_K8_ARENA_NG>: the resident arena's two table sets.
+// <GV_KW_QW, GV_KW_ARENA_NG>: the resident arena's two table sets.
 template <int QW, int NG>
 struct KLayout {
-  static constexpr int QWIN = QW == GV_QW ? GV_QWIN : QW == GV_K8_QW ? GV_K8_QWIN : GV_K6_QWIN;
+  static constexpr int QWIN = QW == GV_QW ? GV_QWIN : QW == GV_KW_QW ? GV_KW_QWIN : GV_K6_QWIN;
   static constexpr int NT = 1 << (QW - 1);                  // table entries per group
   static constexpr int P = (QWIN + NG - 1) / NG;            // ladder positions
   static constexpr int R = QWIN - (P - 1) * NG;             // groups with P windows
@@ -772,8 +773,9 @@ static_assert(KLayout<6, 4>::bit(1) == 36 && KLayout<6, 4>::bit(2) == 72 && KLay
               KLayout<6, 4>::P == 6, "k6 groups");
 static_assert(KLayout<6, GV_KN_ARENA_NG>::w0(GV_KN_ARENA_NG - 1) + KLayout<6, GV_KN_ARENA_NG>::nw(GV_KN_ARENA_NG - 1) ==
               GV_K6_QWIN, "arena groups cover the windows");
-static_assert(KLayout<8, GV_K8_ARENA_NG>::w0(GV_K8_ARENA_NG - 1) + KLayout<8, GV_K8_ARENA_NG>::nw(GV_K8_ARENA_NG - 1) ==
-                  GV_K8_QWIN && KLayout<8, GV_K8_ARENA_NG>::P == 2, "k8 arena groups cover the windows");
+static_assert(KLayout<GV_KW_QW, GV_KW_ARENA_NG>::w0(GV_KW_ARENA_NG - 1) +
+                      KLayout<GV_KW_QW, GV_KW_ARENA_NG>::nw(GV_KW_ARENA_NG - 1) == GV_KW_QWIN &&
+                  KLayout<GV_KW_QW, GV_KW_ARENA_NG>::P == 2, "wide arena groups cover the windows");
 
 // Affine x, y (8 x 32 words) of a finite Jacobian point.
 GV_DEV void gej29_to_affine_words(fe& x8, fe& y8, const gej29& p) {
@@ -1603,14 +1605,15 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gta
 // 2^23-entry tables of 2^(24 j) G.  Same additions, final check and semantics
 // as k_ecmult_k4 otherwise (lambda is a group automorphism, so every
 // exceptional case -- H == 0 -- meets the same points).
-// QW = 8 (the arena's k8 tables, GV_K8_*): 17 eight-bit windows per half in
-// NG groups, 128-entry tables, 8 (P - 1) doublings and 34 Q additions.
+// QW = GV_KW_QW (the arena's wide-window tables, GV_KW_*: 9 by default): 15
+// nine-bit windows per half in 8 groups, 256-entry tables, 9 doublings and 30
+// Q additions.
 // The group layout as constant tables (row 0: NG = 4, row 1: the arena's NG,
-// row 2: the k8 arena's NG) -- indexing them keeps the ladder's register
+// row 2: the wide arena's NG) -- indexing them keeps the ladder's register
 // allocation at that of k4
 #define GV_KN_ROW(QW, NG, F) KLayout<QW, NG>::F(0), KLayout<QW, NG>::F(1), KLayout<QW, NG>::F(2), \
     KLayout<QW, NG>::F(3), KLayout<QW, NG>::F(4), KLayout<QW, NG>::F(5), KLayout<QW, NG>::F(6), \
-    KLayout<QW, NG>::F(7), KLayout<QW, NG>::F(8)
+    KLayout<QW, NG>::F(7), KLayout<QW, NG>::F(8), KLayout<QW, NG>::F(9), KLayout<QW, NG>::F(10)
 __constant__ const int kKnW0[3][16] = {
     {KLayout<6, 4>::w0(0), KLayout<6, 4>::w0(1), KLayout<6, 4>::w0(2), KLayout<6, 4>::w0(3)},
     {KLayout<6, GV_KN_ARENA_NG>::w0(0), KLayout<6, GV_KN_ARENA_NG>::w0(1), KLayout<6, GV_KN_ARENA_NG>::w0(2),
@@ -1619,7 +1622,7 @@ __constant__ const int kKnW0[3][16] = {
      KLayout<6, GV_KN_ARENA_NG>::w0(9), KLayout<6, GV_KN_ARENA_NG>::w0(10), KLayout<6, GV_KN_ARENA_NG>::w0(11),
      KLayout<6, GV_KN_ARENA_NG>::w0(12), KLayout<6, GV_KN_ARENA_NG>::w0(13), KLayout<6, GV_KN_ARENA_NG>::w0(14),
      KLayout<6, GV_KN_ARENA_NG>::w0(15)},
-    {GV_KN_ROW(8, GV_K8_ARENA_NG, w0)}};
+    {GV_KN_ROW(GV_KW_QW, GV_KW_ARENA_NG, w0)}};
 __constant__ const int kKnNW[3][16] = {
     {KLayout<6, 4>::nw(0), KLayout<6, 4>::nw(1), KLayout<6, 4>::nw(2), KLayout<6, 4>::nw(3)},
     {KLayout<6, GV_KN_ARENA_NG>::nw(0), KLayout<6, GV_KN_ARENA_NG>::nw(1), KLayout<6, GV_KN_ARENA_NG>::nw(2),
@@ -1628,9 +1631,9 @@ __constant__ const int kKnNW[3][16] = {
      KLayout<6, GV_KN_ARENA_NG>::nw(9), KLayout<6, GV_KN_ARENA_NG>::nw(10), KLayout<6, GV_KN_ARENA_NG>::nw(11),
      KLayout<6, GV_KN_ARENA_NG>::nw(12), KLayout<6, GV_KN_ARENA_NG>::nw(13), KLayout<6, GV_KN_ARENA_NG>::nw(14),
      KLayout<6, GV_KN_ARENA_NG>::nw(15)},
-    {GV_KN_ROW(8, GV_K8_ARENA_NG, nw)}};
+    {GV_KN_ROW(GV_KW_QW, GV_KW_ARENA_NG, nw)}};
 #undef GV_KN_ROW
-static_assert(GV_KN_ARENA_NG <= 16 && GV_K8_ARENA_NG == 9, "layout table rows");
+static_assert(GV_KN_ARENA_NG <= 16 && GV_KW_ARENA_NG <= 11, "layout table rows");
 
 template <int QW, int NG>
 __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_kn(const u32* gtab6, u32 n, u32 C, const u32* digits,
@@ -1638,7 +1641,7 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_kn(const u32* gta
                                                         const u32* flags, const u32* in_r, uint64_t* bits,
                                                         const u32* qidx, u32 kC) {
   using L = KLayout<QW, NG>;
-  static_assert(QW == GV_K8_QW ? NG == GV_K8_ARENA_NG : QW == GV_K6_QW && (NG == 4 || NG == GV_KN_ARENA_NG),
+  static_assert(QW == GV_KW_QW ? NG == GV_KW_ARENA_NG : QW == GV_K6_QW && (NG == 4 || NG == GV_KN_ARENA_NG),
                 "a layout row of kKnW0 / kKnNW");
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   const u32 qi = qidx[g];
@@ -1670,7 +1673,7 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_kn(const u32* gta
       if (!isg) {
         const bool lam = slot >= NG;
         const int grp = lam ? 2 * NG - 1 - slot : slot;
-        constexpr int T = QW == GV_K8_QW ? 2 : NG == 4 ? 0 : 1;
+        constexpr int T = QW == GV_KW_QW ? 2 : NG == 4 ? 0 : 1;
         if (pos >= kKnNW[T][grp]) continue;                // wave-uniform
         const u32 dq = digits[(size_t)(kKnW0[T][grp] + pos) * C + g];
         d = lam ? ((int)dq >> 16) : ((int)(dq << 16) >> 16);
@@ -1833,7 +1836,7 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   const dim3 blk(256), grd(C / 256);
   // key-ordered lanes (gv_sort.hip): keyed k4 batches with sort scratch
   const bool k6 = b->kslot && b->k6 && b->gtab6;
-  const bool k8 = k6 && b->kq8 && b->k6 == GV_K8_ARENA_NG;   // the resident arena's k8 tables
+  const bool kw = k6 && b->kqw && b->k6 == GV_KW_ARENA_NG;   // the resident arena's wide-window tables
   const bool gf = b->kslot && b->gtab4 && b->gtabf && !k6;   // k_ecmult_k4<true>
   const bool gfp = !b->kslot && b->gtabf;                     // per-item pub33: k_ecmult<false, true>
   const bool sorted = b->kslot && (b->gtab4 || k6) && b->srt.perm;
@@ -1861,7 +1864,7 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
     hipLaunchKernelGGL(gv::k_scalar_inv, dim3((waves + 3) / 4), blk, 0, st, C, b->in_s, w, pre, M);
     if (b->keys_ready) (void)hipStreamWaitEvent(st, b->keys_ready, 0);   // grouped keys built beside s^-1
     if (b->ev[1]) (void)hipEventRecord(b->ev[1], st);
-    if (k8)
+    if (kw)
       hipLaunchKernelGGL((gv::k_prep<true, true, true, true>), grd, blk, 0, st, C, b->n, (const uint32_t*)nullptr,
                          (const uint32_t*)nullptr, b->in_r, b->in_s, b->in_e, (const uint32_t*)w, b->digits,
                          (uint32_t*)nullptr, (uint32_t*)nullptr, b->flags, sorted ? b->srt.kslot : b->kslot,
@@ -1899,8 +1902,8 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   }
   if (b->ev_ecm_start) (void)hipEventRecord(b->ev_ecm_start, se);
   if (b->bits_wait && !sorted) (void)hipStreamWaitEvent(se, b->bits_wait, 0);   // the ladder writes the bits
-  if (k8)
-    hipLaunchKernelGGL((gv::k_ecmult_kn<GV_K8_QW, GV_K8_ARENA_NG>), grd, blk, 0, se, b->gtab6, b->n, C, b->digits,
+  if (kw)
+    hipLaunchKernelGGL((gv::k_ecmult_kn<GV_KW_QW, GV_KW_ARENA_NG>), grd, blk, 0, se, b->gtab6, b->n, C, b->digits,
                        b->kqt, b->kqt2, b->kzq, b->flags, b->in_r, sorted ? b->srt.bits : b->bits,
                        (const uint32_t*)b->in_pfx, b->kC);
   else if (k6 && b->k6 == GV_KN_ARENA_NG)
@@ -1986,16 +1989,16 @@ hipError_t gvk_keys_build_rows6(uint32_t n, uint32_t C, const uint32_t* in_x, co
   return keys_tables_launch<GV_K6_QW, 4>(n, C, in_x, in_pfx, scratch, with_qe, 0u, kqt, kzq, kC, kok, kqt2, kzq2, st);
 }
 
-hipError_t gvk_keys_build8(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
+hipError_t gvk_keys_build_wide(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
                            uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* scratch, int with_qe,
-                           uint32_t base, uint32_t* kqt8, uint32_t* kzq8, uint32_t kC, uint32_t* kok, uint32_t* kqt82,
-                           uint32_t* kzq82, hipStream_t st) {
+                           uint32_t base, uint32_t* kqtw, uint32_t* kzqw, uint32_t kC, uint32_t* kok, uint32_t* kqtw2,
+                           uint32_t* kzqw2, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const dim3 blk(256), grd(C / 256);
   hipLaunchKernelGGL(gv::k_unpack, grd, blk, 0, st, pub33, (const uint8_t*)nullptr, (const uint8_t*)nullptr, n, C,
                      in_x, in_pfx, in_r, in_s, in_e);
-  return keys_tables_launch<GV_K8_QW, GV_K8_ARENA_NG>(n, C, in_x, in_pfx, scratch, with_qe, base, kqt8, kzq8, kC, kok,
-                                                      kqt82, kzq82, st);
+  return keys_tables_launch<GV_KW_QW, GV_KW_ARENA_NG>(n, C, in_x, in_pfx, scratch, with_qe, base, kqtw, kzqw, kC, kok,
+                                                      kqtw2, kzqw2, st);
 }
 
 hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,

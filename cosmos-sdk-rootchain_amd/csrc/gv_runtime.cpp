@@ -147,15 +147,15 @@ struct Dev {
   // Zs), read by k_ecmult_kn and k_verify_lat16_kn
   uint32_t *kqt6 = nullptr, *kzq6 = nullptr, *kqt62 = nullptr, *kzq62 = nullptr;
   size_t keys6 = 0;                               // leading slots whose k6 tables are built
-  // the resident arena's k8 tables (option "keys_k8"): per slot GV_K8_ARENA_NG
-  // (9) 128-entry group tables of 2^(16 g) Q on one Z (kqt8: group 0, kqt82:
-  // groups 1.., kzq8: the Z, 8 rows of stride kcap8; kzq82: the chain's parked
-  // Zs), in an arena of their own (capacity kcap8) grown by doubling while the
-  // HBM budget holds it; keys8 leading slots built.  k8_full: the budget
-  // refused a growth (no more k8 builds until gv_keys_reset)
-  uint32_t *kqt8 = nullptr, *kzq8 = nullptr, *kqt82 = nullptr, *kzq82 = nullptr;
-  size_t kcap8 = 0, keys8 = 0;
-  bool k8_full = false;
+  // the resident arena's wide-window tables (option "keys_wide"): per slot
+  // GV_KW_ARENA_NG (8) 256-entry group tables of 2^(18 g) Q on one Z (kqtw: group 0, kqtw2:
+  // groups 1.., kzqw: the Z, 8 rows of stride kcapw; kzqw2: the chain's parked
+  // Zs), in an arena of their own (capacity kcapw) grown by doubling while the
+  // HBM budget holds it; keysw leading slots built.  kw_full: the budget
+  // refused a growth (no more wide-window builds until gv_keys_reset)
+  uint32_t *kqtw = nullptr, *kzqw = nullptr, *kqtw2 = nullptr, *kzqw2 = nullptr;
+  size_t kcapw = 0, keysw = 0;
+  bool kw_full = false;
   // HBM held by the optional tables (G tables, key arenas) against ctx->hbm_budget
   size_t opt_bytes = 0;
   // ring of per-launch stage events for gv_stage_stats
@@ -353,36 +353,43 @@ int ensure_keys(Dev* d, size_t need, size_t used, hipStream_t st, size_t key_cap
   return GV_OK;
 }
 
-// Bytes per slot of the k8 tables.
-constexpr size_t kKey8SlotBytes = ((size_t)GV_K8_KEY_WORDS * GV_K8_ARENA_NG + 8 * GV_K8_ARENA_NG) * 4;
+// Bytes per slot of the wide-window tables.
+constexpr size_t kKeyWSlotBytes = ((size_t)GV_KW_KEY_WORDS * GV_KW_ARENA_NG + 8 * GV_KW_ARENA_NG) * 4;
 
-// Grow the k8 arena to `need` slots keeping the first `used` (doubling, not
+// Grow the wide-window arena to `need` slots keeping the first `used` (doubling, not
 // past key_cap, then exact -- as ensure_keys).  Returns false when the budget
-// (the new arena beside the old one during the copy) does not hold it or an
-// allocation fails: the arena is left as it was and batches keep the k6 tables.
-bool ensure_keys8(Dev* d, size_t need, size_t used, hipStream_t st, size_t key_cap, size_t budget) {
-  if (need <= d->kcap8) return true;
-  const size_t grow = d->kcap8 >= key_cap ? need : std::min<size_t>(2 * d->kcap8, std::max<size_t>(need, key_cap));
+// (the new arena beside the old one during the copy) does not hold it, when
+// it would take device memory the k4 / k6 arena needs to grow to key_cap
+// (plus 8 GiB of batch scratch: these tables are an optimisation and never
+// make a later gv_keys_load or batch fail), or when an allocation fails: the
+// arena is left as it was and batches keep the k6 tables.
+bool ensure_keys_wide(Dev* d, size_t need, size_t used, hipStream_t st, size_t key_cap, size_t budget) {
+  if (need <= d->kcapw) return true;
+  const size_t grow = d->kcapw >= key_cap ? need : std::min<size_t>(2 * d->kcapw, std::max<size_t>(need, key_cap));
   const size_t cap = round_up(std::max<size_t>({need, grow, 4096}), 256);
-  if (d->opt_bytes + cap * kKey8SlotBytes > budget) return false;
-  const size_t ng1 = GV_K8_ARENA_NG - 1;
+  if (d->opt_bytes + cap * kKeyWSlotBytes > budget) return false;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return false;
+  const size_t reserve = (key_cap > d->kcap ? key_cap - d->kcap : 0) * key_slot_bytes(true) + (size_t(8) << 30);
+  if (free_b < cap * kKeyWSlotBytes + reserve) return false;
+  const size_t ng1 = GV_KW_ARENA_NG - 1;
   uint32_t *qt = nullptr, *zq = nullptr, *qt2 = nullptr, *zq2 = nullptr;
-  if (hipMalloc(&qt, cap * GV_K8_KEY_WORDS * 4) != hipSuccess || hipMalloc(&zq, cap * 8 * 4) != hipSuccess ||
-      hipMalloc(&qt2, cap * ng1 * GV_K8_KEY_WORDS * 4) != hipSuccess ||
+  if (hipMalloc(&qt, cap * GV_KW_KEY_WORDS * 4) != hipSuccess || hipMalloc(&zq, cap * 8 * 4) != hipSuccess ||
+      hipMalloc(&qt2, cap * ng1 * GV_KW_KEY_WORDS * 4) != hipSuccess ||
       hipMalloc(&zq2, cap * ng1 * 8 * 4) != hipSuccess) {
     for (uint32_t* p : {qt, zq, qt2, zq2}) if (p) (void)hipFree(p);
     (void)hipGetLastError();
     return false;
   }
-  used = std::min(used, d->keys8);                // the slots whose k8 tables exist
+  used = std::min(used, d->keysw);                // the slots whose wide-window tables exist
   if (used) {
-    bool ok = hipMemcpyAsync(qt, d->kqt8, used * GV_K8_KEY_WORDS * 4, hipMemcpyDeviceToDevice, st) == hipSuccess &&
-              hipMemcpyAsync(qt2, d->kqt82, used * ng1 * GV_K8_KEY_WORDS * 4, hipMemcpyDeviceToDevice, st) ==
+    bool ok = hipMemcpyAsync(qt, d->kqtw, used * GV_KW_KEY_WORDS * 4, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+              hipMemcpyAsync(qt2, d->kqtw2, used * ng1 * GV_KW_KEY_WORDS * 4, hipMemcpyDeviceToDevice, st) ==
                   hipSuccess;
     for (int r = 0; ok && r < 8; ++r)
-      ok = hipMemcpyAsync(zq + r * cap, d->kzq8 + r * d->kcap8, used * 4, hipMemcpyDeviceToDevice, st) == hipSuccess;
+      ok = hipMemcpyAsync(zq + r * cap, d->kzqw + r * d->kcapw, used * 4, hipMemcpyDeviceToDevice, st) == hipSuccess;
     for (size_t r = 0; ok && r < ng1 * 8; ++r)
-      ok = hipMemcpyAsync(zq2 + r * cap, d->kzq82 + r * d->kcap8, used * 4, hipMemcpyDeviceToDevice, st) ==
+      ok = hipMemcpyAsync(zq2 + r * cap, d->kzqw2 + r * d->kcapw, used * 4, hipMemcpyDeviceToDevice, st) ==
            hipSuccess;
     if (!ok || hipStreamSynchronize(st) != hipSuccess) {
       for (uint32_t* p : {qt, zq, qt2, zq2}) (void)hipFree(p);
@@ -390,11 +397,11 @@ bool ensure_keys8(Dev* d, size_t need, size_t used, hipStream_t st, size_t key_c
       return false;
     }
   }
-  for (uint32_t* p : {d->kqt8, d->kzq8, d->kqt82, d->kzq82})
+  for (uint32_t* p : {d->kqtw, d->kzqw, d->kqtw2, d->kzqw2})
     if (p) (void)hipFree(p);
-  d->opt_bytes = d->opt_bytes - std::min(d->opt_bytes, d->kcap8 * kKey8SlotBytes) + cap * kKey8SlotBytes;
-  d->kqt8 = qt; d->kzq8 = zq; d->kqt82 = qt2; d->kzq82 = zq2;
-  d->kcap8 = cap;
+  d->opt_bytes = d->opt_bytes - std::min(d->opt_bytes, d->kcapw * kKeyWSlotBytes) + cap * kKeyWSlotBytes;
+  d->kqtw = qt; d->kzqw = zq; d->kqtw2 = qt2; d->kzqw2 = zq2;
+  d->kcapw = cap;
   return true;
 }
 
@@ -611,8 +618,8 @@ struct gv_ctx {
                                 // GLV windows (k_ecmult_k4<true>, 6 GiB of tables; GV_GFULL=0: A/B)
   bool k6 = false;              // grouped batches on k_ecmult_k6: 6-bit Q windows on 32-entry key tables, the lambda
                                 // frame, G on the unsplit u1 in 24-bit windows (GV_K6=1)
-  bool keys_k8 = true;          // ... and k8 tables (9 groups of 128 entries: 8 doublings, 34 Q additions) while
-                                // the HBM budget holds them (GV_KEYS_K8)
+  bool keys_wide = true;        // ... and wide-window tables (8 groups of 256 entries: 9 doublings, 30 Q additions)
+                                // while device memory holds them (GV_KEYS_WIDE)
   bool keys_k6 = true;          // the resident arena (gv_keys_load) also holds k6 tables and its throughput batches
                                 // run k_ecmult_k6: the table build is paid once per key, not per batch (GV_KEYS_K6)
   size_t key_cap = GV_KEY_CAP;  // the callers' key-arena reset point: growth doubles up to here ("key_cap", GV_KEY_CAP)
@@ -936,10 +943,10 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
   const bool pipelined = st_ecm != nullptr && !small;
   // the resident arena's k6 tables (every slot in use has them): throughput
   // batches on k_ecmult_k6; the small-batch kernels keep the k4 tables
-  if (kslot && !ka && !small && ctx->keys_k8 && d->kqt8 && d->gtab6 && d->keys8 >= ctx->keys) {
-    // the k8 tables (their own arena: Z rows of stride kcap8)
-    b.kqt = d->kqt8; b.kzq = d->kzq8; b.kqt2 = d->kqt82; b.kC = (uint32_t)d->kcap8;
-    b.k6 = GV_K8_ARENA_NG; b.kq8 = 1; b.gtab6 = d->gtab6;
+  if (kslot && !ka && !small && ctx->keys_wide && d->kqtw && d->gtab6 && d->keysw >= ctx->keys) {
+    // the wide-window tables (their own arena: Z rows of stride kcapw)
+    b.kqt = d->kqtw; b.kzq = d->kzqw; b.kqt2 = d->kqtw2; b.kC = (uint32_t)d->kcapw;
+    b.k6 = GV_KW_ARENA_NG; b.kqw = 1; b.gtab6 = d->gtab6;
   } else if (kslot && !ka && !small && ctx->keys_k6 && d->kqt6 && d->gtab6 && d->keys6 >= ctx->keys) {
     b.kqt = d->kqt6; b.kzq = d->kzq6; b.kqt2 = d->kqt62;
     b.k6 = GV_KN_ARENA_NG; b.gtab6 = d->gtab6;
@@ -1000,7 +1007,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
       b.gtabf = ctx->gfull && ctx->gfull_item ? d->gtabf : nullptr;
     }
     plan_sort(ctx, s, b, sort_base);
-    d->routes[b.kq8 && b.gtab6                  ? GV_ROUTE_KN8
+    d->routes[b.kqw && b.gtab6                  ? GV_ROUTE_KW
               : b.k6 == GV_KN_ARENA_NG && b.gtab6 ? GV_ROUTE_KN
               : b.k6 && b.gtab6                ? GV_ROUTE_K6
               : b.kslot && b.gtab4 && b.gtabf ? GV_ROUTE_K4F
@@ -1864,7 +1871,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* gi = getenv("GV_GFULL_ITEM")) ctx->gfull_item = strcmp(gi, "0") != 0;
   if (const char* hs = getenv("GV_H2D_SERIAL")) ctx->h2d_serial = strcmp(hs, "0") != 0;
   if (const char* kk = getenv("GV_KEYS_K6")) ctx->keys_k6 = strcmp(kk, "0") != 0;
-  if (const char* kk = getenv("GV_KEYS_K8")) ctx->keys_k8 = strcmp(kk, "0") != 0;
+  if (const char* kk = getenv("GV_KEYS_WIDE")) ctx->keys_wide = strcmp(kk, "0") != 0;
   if (const char* hl = getenv("GV_HOST_LADDER_STREAM")) ctx->host_ladder_stream = strcmp(hl, "0") != 0;
   parse_size_env("GV_ASYNC_CHUNK", &ctx->async_chunk);
   if (const char* ag = getenv("GV_ASYNC_GROWTH")) ctx->async_growth = std::max(1, std::min(64, atoi(ag)));
@@ -1974,8 +1981,8 @@ void gv_close(gv_ctx* ctx) {
     if (d->gtab4) (void)hipFree(d->gtab4);
     if (d->gtab6) (void)hipFree(d->gtab6);
     if (d->gtabf) (void)hipFree(d->gtabf);
-    for (uint32_t* p : {d->kqt, d->kzq, d->kok, d->kqt2, d->kzq2, d->kqt6, d->kzq6, d->kqt62, d->kzq62, d->kqt8,
-                        d->kzq8, d->kqt82, d->kzq82})
+    for (uint32_t* p : {d->kqt, d->kzq, d->kok, d->kqt2, d->kzq2, d->kqt6, d->kzq6, d->kqt62, d->kzq62, d->kqtw,
+                        d->kzqw, d->kqtw2, d->kzqw2})
       if (p) (void)hipFree(p);
     if (d->edtab) (void)hipFree(d->edtab);
     if (d->ed.d_in) (void)hipFree(d->ed.d_in);
@@ -2205,13 +2212,13 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
     hipStream_t st = s->st;
     for (hipStream_t t : d->hi_st) CK(hipStreamSynchronize(t));   // no pipelined ladder reads an arena being grown
     if (base == 0) {                            // after gv_keys_reset the slots are rewritten from 0
-      d->keys6 = d->keys8 = 0;
-      d->k8_full = false;
+      d->keys6 = d->keysw = 0;
+      d->kw_full = false;
     }
     // the k6 tables too when their G tables exist (or can be built) and the
     // arena has room for them (else k4 only: the k4 route serves the slots)
     int rc = ensure_gtab4(ctx, d, s, st);
-    if (!rc) rc = ensure_gtab6(ctx, d, s, st, ctx->keys_k6 || ctx->keys_k8);
+    if (!rc) rc = ensure_gtab6(ctx, d, s, st, ctx->keys_k6 || ctx->keys_wide);
     if (rc) return rc;
     bool k6 = ctx->keys_k6 && d->gtab6 && d->keys6 == base;
     if ((rc = ensure_keys(d, base + n, base, st, ctx->key_cap, ctx->hbm_budget, &k6))) return rc;
@@ -2243,31 +2250,33 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
       CK(hipStreamSynchronize(st));            // the caller's pub33 chunk is read by then
     }
     if (k6) d->keys6 = base + n;
-    // the k8 tables: while every earlier slot has them and the budget holds
+    // the wide-window tables: while every earlier slot has them and memory holds
     // the grown arena (a refusal stops them until gv_keys_reset: batches
     // then take the k6 tables)
-    if (ctx->keys_k8 && d->gtab6 && d->keys8 == base && !d->k8_full) {
-      if (!ensure_keys8(d, base + n, base, st, ctx->key_cap, ctx->hbm_budget)) {
-        d->k8_full = true;
+    if (ctx->keys_wide && d->gtab6 && d->keysw == base && !d->kw_full) {
+      if (!ensure_keys_wide(d, base + n, base, st, ctx->key_cap, ctx->hbm_budget)) {
+        d->kw_full = true;
       } else {
-        // 9 groups x 128 entries: scratch rows per key ~4x the k6 build's
-        const size_t step8 = std::min<size_t>(ctx->max_batch, 8192);
-        for (size_t c0 = 0; c0 < n; c0 += step8) {
-          const size_t cn = std::min(step8, n - c0);
+        // GV_KW_ARENA_NG groups of GV_KW_NT entries: scratch rows per key ~6x
+        // the k6 build's (QW 9), so the chunks are smaller (scratch within
+        // what the k6 build's chunks take)
+        const size_t stepw = std::min<size_t>(ctx->max_batch, GV_KW_QW >= 9 ? 4096 : 8192);
+        for (size_t c0 = 0; c0 < n; c0 += stepw) {
+          const size_t cn = std::min(stepw, n - c0);
           const size_t C = round_up(cn, 256);
-          const int qe8 = ctx->keys_scratch ? 1 : 0;
-          const size_t w8 = gvk_keys_scratch_words((uint32_t)cn, GV_K8_ARENA_NG, GV_K8_NT, qe8);
-          const size_t Cs = std::max(C, round_up(w8 / GV_QTAB_WORDS + 1, 256));
+          const int qew = ctx->keys_scratch ? 1 : 0;
+          const size_t ww = gvk_keys_scratch_words((uint32_t)cn, GV_KW_ARENA_NG, GV_KW_NT, qew);
+          const size_t Cs = std::max(C, round_up(ww / GV_QTAB_WORDS + 1, 256));
           if ((rc = ensure_cap(s, Cs))) return rc;
           if ((rc = set_acquire(s, st))) return rc;
           CK(hipMemcpyAsync(s->d_in, pub33 + c0 * 33, cn * 33, hipMemcpyHostToDevice, st));
-          CK(gvk_keys_build8(s->d_in, (uint32_t)cn, (uint32_t)C, s->in_x, s->in_pfx, s->in_r, s->in_s, s->in_e,
-                             s->qtab, qe8, (uint32_t)(base + c0), d->kqt8, d->kzq8, (uint32_t)d->kcap8, d->kok,
-                             d->kqt82, d->kzq82, st));
+          CK(gvk_keys_build_wide(s->d_in, (uint32_t)cn, (uint32_t)C, s->in_x, s->in_pfx, s->in_r, s->in_s, s->in_e,
+                                 s->qtab, qew, (uint32_t)(base + c0), d->kqtw, d->kzqw, (uint32_t)d->kcapw, d->kok,
+                                 d->kqtw2, d->kzqw2, st));
           if ((rc = set_release(s, st))) return rc;
           CK(hipStreamSynchronize(st));
         }
-        d->keys8 = base + n;
+        d->keysw = base + n;
       }
     }
   }
@@ -2725,7 +2734,7 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->ed_keyed = val != 0;
   } else if (!strcmp(key, "two_ladders") || !strcmp(key, "gfull") || !strcmp(key, "k6") ||
-             !strcmp(key, "keys_k6") || !strcmp(key, "keys_k8")) {
+             !strcmp(key, "keys_k6") || !strcmp(key, "keys_wide")) {
     // schedule switches: every device lock held across the drain and the
     // write, so no pipelined call launches on a mix of old and new state
     if (val != 0 && val != 1) return GV_EINVAL;
@@ -2737,7 +2746,7 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
       d->bits_used = false;
     }
     bool& flag = !strcmp(key, "two_ladders") ? ctx->two_ladders : !strcmp(key, "gfull") ? ctx->gfull
-                 : !strcmp(key, "k6") ? ctx->k6 : !strcmp(key, "keys_k8") ? ctx->keys_k8 : ctx->keys_k6;
+                 : !strcmp(key, "k6") ? ctx->k6 : !strcmp(key, "keys_wide") ? ctx->keys_wide : ctx->keys_k6;
     flag = val != 0;
   } else if (!strcmp(key, "async_chunk")) {
     if (val < 256 || (unsigned long long)val > kMaxItems) return GV_EINVAL;

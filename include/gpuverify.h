@@ -298,12 +298,13 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * tables -- and keyed throughput batches whose slots all have them run the
  * 6-doubling ladder; small keyed batches keep the k4 tables; same verdicts;
  * default 1, env GV_KEYS_K6; route counter GV_ROUTE_KN),
- * "keys_k8" (0/1: with "keys_k6", gv_keys_load also builds each key's
- * 8-bit-window tables -- 9 groups of 128 entries on one Z, 90 KB per key, in
- * an arena of their own that grows by doubling while the HBM budget holds
- * it -- and keyed throughput batches whose slots all have them run the
- * 8-doubling, 34-addition ladder (else the k6 one); same verdicts; default
- * 1, env GV_KEYS_K8; route counter GV_ROUTE_KN8),
+ * "keys_wide" (0/1: gv_keys_load also builds each key's 9-bit-window
+ * tables -- 8 groups of 256 entries on one Z, 160 KB per key, in an arena of
+ * their own that grows by doubling while the HBM budget holds it and the
+ * device keeps room for the k4 / k6 arena to reach key_cap -- and keyed
+ * throughput batches whose slots all have them run the 9-doubling,
+ * 30-addition ladder (else the k6 one); same verdicts; default 1, env
+ * GV_KEYS_WIDE; route counter GV_ROUTE_KW),
  * "key_cap" / "ed_key_cap" (the callers' reset points of the secp256k1 /
  * ed25519 key arenas: an arena grows by doubling up to it and exactly past it;
  * defaults GV_KEY_CAP / GV_ED_KEY_CAP, env of the same names; the Go shim sets
@@ -384,9 +385,9 @@ int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys)
  * with the G half on the unsplit scalar, "gfull_item"), GV_ROUTE_KN (keyed
  * batches on the resident arena's k6 tables: 11 groups of 6-bit windows, 6
  * doublings, option "keys_k6"), GV_ROUTE_ED_LAT (small uncached ed25519
- * host batches on k_ed_lat_unc, option "ed_unc_lat_max"), GV_ROUTE_KN8 (keyed
- * batches on the resident arena's k8 tables: 9 groups of 8-bit windows, 8
- * doublings, option "keys_k8").  Instrumentation only (bench route
+ * host batches on k_ed_lat_unc, option "ed_unc_lat_max"), GV_ROUTE_KW (keyed
+ * batches on the resident arena's wide-window tables: 8 groups of 9-bit
+ * windows, 9 doublings, option "keys_wide").  Instrumentation only (bench route
  * attribution, node metrics). */
 #define GV_ROUTE_PUB33 0
 #define GV_ROUTE_KEYED125 1
@@ -398,7 +399,7 @@ int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys)
 #define GV_ROUTE_ITEMF 7
 #define GV_ROUTE_KN 8
 #define GV_ROUTE_ED_LAT 9
-#define GV_ROUTE_KN8 10
+#define GV_ROUTE_KW 10
 #define GV_ROUTES 11
 int gv_route_stats(gv_ctx* ctx, int dev_slot, uint64_t out[GV_ROUTES]);
 

@@ -94,7 +94,7 @@ def test_budget_degrades_with_the_same_verdicts(batch, mb, grouped_route, keyed_
         ver.close()
 
 
-def test_default_budget_takes_the_arena_k8_then_k6_tables(batch):
+def test_default_budget_takes_the_arena_wide_then_k6_tables(batch):
     pub, sig, dig, exp = batch
     ver = gvm.Verifier([0])
     try:
@@ -102,8 +102,8 @@ def test_default_budget_takes_the_arena_k8_then_k6_tables(batch):
         slots = ver.keys_load(uniq)[inv.reshape(-1)].astype(np.uint32)
         got, routes = routes_of(ver, lambda: ver.verify_batch_digests_keyed(slots, sig, dig))
         assert np.array_equal(got, exp)
-        assert routes.get("kn8", 0) >= 1, routes
-        ver.set_option("keys_k8", 0)                  # the k6 tables of the same slots
+        assert routes.get("kw", 0) >= 1, routes
+        ver.set_option("keys_wide", 0)                  # the k6 tables of the same slots
         got, routes = routes_of(ver, lambda: ver.verify_batch_digests_keyed(slots, sig, dig))
         assert np.array_equal(got, exp)
         assert routes.get("kn", 0) >= 1, routes

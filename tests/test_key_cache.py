@@ -20,8 +20,8 @@ def ver():
     v.close()
 
 
-# (lat_max, sliced, keys_k6, keys_k8): the PATHS schedules (rows: pub33 only)
-# with the resident arena's kn tables (throughput: the k8 tables), plus the
+# (lat_max, sliced, keys_k6, keys_wide): the PATHS schedules (rows: pub33 only)
+# with the resident arena's kn tables (throughput: the wide-window tables), plus the
 # sliced kernel on the k4 tables and the throughput ladder on the k6 tables
 KEYED_PATHS = {**{p: (v[0], v[1], 1, 1) for p, v in PATHS.items() if p != "latency_rows"},
                "latency_k4_arena": (1 << 30, 1, 0, 0), "throughput_k6_arena": (0, 1, 1, 0)}
@@ -33,17 +33,17 @@ def path(request, ver):
     (k_verify_lat16_kn on the arena's kn tables, k_verify_lat16_sl on its k4
     tables with keys_k6 0, or k_verify_lat16 with lat_sliced 0), the
     throughput pipeline above it: every schedule is checked."""
-    lat_max, sliced, keys_k6, keys_k8 = KEYED_PATHS[request.param]
+    lat_max, sliced, keys_k6, keys_wide = KEYED_PATHS[request.param]
     ver.set_option("lat_max", lat_max)
     ver.set_option("lat_sliced", sliced)
     ver.set_option("lat_sl_max", 1 << 30)
     ver.set_option("keys_k6", keys_k6)
-    ver.set_option("keys_k8", keys_k8)
+    ver.set_option("keys_wide", keys_wide)
     yield request.param
     ver.reset_schedule()
     ver.set_option("lat_sliced", 1)
     ver.set_option("keys_k6", 1)
-    ver.set_option("keys_k8", 1)
+    ver.set_option("keys_wide", 1)
 
 
 def keyed_inputs(ver, pub):

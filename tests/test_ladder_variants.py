@@ -4,8 +4,8 @@ half on the unsplit scalar (gv_set_option "gfull" 1, the default: 11 signed
 half (gfull 0: 14 20-bit windows) and k_ecmult_k6 (6-bit Q windows on 32-entry
 key tables, the lambda frame, G on the unsplit u1 in 11 signed 24-bit windows
 from the 2^(36 t) G tables: "k6" 1 on the grouped route, "keys_k6" 1 -- the
-default -- on the resident key arena), and the arena's k8 tables ("keys_k8",
-the default: 8-bit Q windows on 128-entry tables, 8 doublings).  Each is run on the grouped route (pub33
+default -- on the resident key arena), and the arena's wide-window tables
+("keys_wide", the default: 9-bit Q windows on 256-entry tables, 9 doublings).  Each is run on the grouped route (pub33
 batches with repeated keys), the cached-key route (gv_keys_load slots) and the
 message path, against the oracle's expected verdicts, and the route counters
 must show the schedule that ran.  The per-item route (group_keys 0: each item parses its
@@ -25,16 +25,16 @@ pytestmark = pytest.mark.gpu
 
 SCHEDULES = {"k4f": {"gfull": 1, "k6": 0}, "k4": {"gfull": 0, "k6": 0}, "k6": {"gfull": 1, "k6": 1},
              "item_gf": {"group_keys": 0, "gfull_item": 1}, "item_glv": {"group_keys": 0, "gfull_item": 0}}
-ROUTE = {"k4f": "k4f", "k4": "k4", "k6": "k6", "k8": "k6", "item_gf": "item_f", "item_glv": "pub33"}
-DEFAULTS = {"gfull": 1, "k6": 0, "group_keys": 1, "gfull_item": 1, "keys_k6": 1, "keys_k8": 1}
-# the cached-key route (gv_keys_load slots): k6 / k8 tables are built at load
-# time when "keys_k6" / "keys_k8" are on; the message part of the test runs
+ROUTE = {"k4f": "k4f", "k4": "k4", "k6": "k6", "wide": "k6", "item_gf": "item_f", "item_glv": "pub33"}
+DEFAULTS = {"gfull": 1, "k6": 0, "group_keys": 1, "gfull_item": 1, "keys_k6": 1, "keys_wide": 1}
+# the cached-key route (gv_keys_load slots): k6 / wide-window tables are built
+# at load time when "keys_k6" / "keys_wide" are on; the message part of the test runs
 # the grouped route
-CACHED = {"k4f": {"gfull": 1, "keys_k6": 0, "keys_k8": 0, "k6": 0},
-          "k4": {"gfull": 0, "keys_k6": 0, "keys_k8": 0, "k6": 0},
-          "k6": {"gfull": 1, "keys_k6": 1, "keys_k8": 0, "k6": 1},
-          "k8": {"gfull": 1, "keys_k6": 1, "keys_k8": 1, "k6": 1}}
-ARENA_ROUTE = {"k6": "kn", "k8": "kn8"}
+CACHED = {"k4f": {"gfull": 1, "keys_k6": 0, "keys_wide": 0, "k6": 0},
+          "k4": {"gfull": 0, "keys_k6": 0, "keys_wide": 0, "k6": 0},
+          "k6": {"gfull": 1, "keys_k6": 1, "keys_wide": 0, "k6": 1},
+          "wide": {"gfull": 1, "keys_k6": 1, "keys_wide": 1, "k6": 1}}
+ARENA_ROUTE = {"k6": "kn", "wide": "kw"}                          # schedule -> the arena's route counter
 
 
 @pytest.fixture(scope="module")
@@ -162,7 +162,7 @@ def test_cached_keys_and_messages(ver, sched):
     uniq, inv = np.unique(pub, axis=0, return_inverse=True)
     slots = ver.keys_load(uniq)[inv.reshape(-1)].astype(np.uint32)
     got, routes = run(ver, sched, lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
-    assert routes[ARENA_ROUTE.get(sched, sched)] >= 1, routes   # the arena's k6 (11 groups) / k8 (9 groups) tables
+    assert routes[ARENA_ROUTE.get(sched, sched)] >= 1, routes   # the arena's k6 (11 groups) / wide (8 groups) tables
     assert np.array_equal(got, exp)
     mp, ms, mm, mok, _ = load_msg_vectors()
     reps = max(1, 40_000 // len(mp))
@@ -196,9 +196,9 @@ def test_cached_keys_k6_goldens_and_slots(ver):
     got6, r6 = run(ver, "k6", lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
     assert r6["kn"] >= 1, r6
     assert np.array_equal(got6, exp)
-    got8, r8 = run(ver, "k8", lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
-    assert r8["kn8"] >= 1, r8
-    assert np.array_equal(got8, exp)
+    gotw, rw = run(ver, "wide", lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
+    assert rw["kw"] >= 1, rw
+    assert np.array_equal(gotw, exp)
     ver.set_option("keys_k6", 0)                                  # the k4 tables of the same slots
     try:
         got4, r4 = run(ver, "k4f", lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
@@ -209,11 +209,11 @@ def test_cached_keys_k6_goldens_and_slots(ver):
     ver.keys_reset()
 
 
-def test_k8_arena_growth_keeps_the_loaded_slots(ver):
-    """The k8 tables live in an arena of their own that grows by doubling from
+def test_wide_arena_growth_keeps_the_loaded_slots(ver):
+    """The wide-window tables live in an arena of their own that grows by doubling from
     4,096 slots: a second load past it copies the first load's tables into the
     grown arena (Z rows re-strided) and builds the rest; every slot then
-    verifies on the k8 ladder exactly as on the k6 one, and a load after
+    verifies on the wide-window ladder exactly as on the k6 one, and a load after
     gv_keys_reset rebuilds from slot 0."""
     pub, sig, dig, exp = bench.make_digest_workload(30_000, 0x98, 6000, 0.25, 16)
     want = O.verify_digests(pub, sig, dig, threads=16)
@@ -221,14 +221,14 @@ def test_k8_arena_growth_keeps_the_loaded_slots(ver):
     uniq, first, inv = np.unique(pub, axis=0, return_index=True, return_inverse=True)
     order = np.argsort(first)
     a = ver.keys_load(uniq[order][:3000])
-    b = ver.keys_load(uniq[order][3000:])                          # past 4,096 slots: the k8 arena grows
+    b = ver.keys_load(uniq[order][3000:])                          # past 4,096 slots: the wide arena grows
     slots_u = np.concatenate([a, b]).astype(np.uint32)
     rank = np.empty_like(order)
     rank[order] = np.arange(len(order))
     slots = slots_u[rank[inv.reshape(-1)]]
-    got8, r8 = run(ver, "k8", lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
-    assert r8["kn8"] >= 1, r8
-    assert np.array_equal(got8, want)
+    gotw, rw = run(ver, "wide", lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
+    assert rw["kw"] >= 1, rw
+    assert np.array_equal(gotw, want)
     got6, r6 = run(ver, "k6", lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
     assert r6["kn"] >= 1, r6
     assert np.array_equal(got6, want)
@@ -236,7 +236,7 @@ def test_k8_arena_growth_keeps_the_loaded_slots(ver):
     c = ver.keys_load(uniq[order][3000:]).astype(np.uint32)
     sub = rank[inv.reshape(-1)] >= 3000
     s2 = c[rank[inv.reshape(-1)][sub] - 3000]
-    got, r = run(ver, "k8", lambda: ver.verify_batch_digests_keyed(s2, sig[sub], dig[sub]), CACHED)
-    assert r["kn8"] >= 1, r
+    got, r = run(ver, "wide", lambda: ver.verify_batch_digests_keyed(s2, sig[sub], dig[sub]), CACHED)
+    assert r["kw"] >= 1, r
     assert np.array_equal(got, want[sub])
     ver.keys_reset()

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""c2_key_cache with the resident arena's k8 tables (keys_k8 1) against the
-k6 tables (keys_k8 0), alternated on one context: one JSON line per run."""
+"""c2_key_cache with the resident arena's wide-window tables (keys_wide 1) against the
+k6 tables (keys_wide 0), alternated on one context: one JSON line per run."""
 import json
 import os
 import sys
@@ -19,13 +19,13 @@ def main():
     pub, sig, dig, exp = B.make_digest_workload(n, 0xC2, 65536, 0.0, B.host_cores()["effective"])
     ver = gvm.Verifier([0])
     for _ in range(reps):
-        for k8 in (1, 0):
-            ver.set_option("keys_k8", k8)
+        for kw in (1, 0):
+            ver.set_option("keys_wide", kw)
             r = X.c2_key_cache(ver, pub, sig, dig, exp, 65536, steps=20)
-            print(json.dumps({"keys_k8": k8, "value": r["value"], "route": r["route"], "mismatches": r["mismatches"],
+            print(json.dumps({"keys_wide": kw, "value": r["value"], "route": r["route"], "mismatches": r["mismatches"],
                               "keys_load_ms": r["keys_load_ms"], "ladder_ms": r["roofline"]["kernel_ms"],
                               "frac": r["roofline"]["frac"], "stages": r["stages"]}), flush=True)
-    ver.set_option("keys_k8", 1)
+    ver.set_option("keys_wide", 1)
     ver.close()
 
 
