@@ -110,10 +110,12 @@ W_LADDER_K6 = w_ladder(30, 44, 11, 6, nbeta=12)
 # k_ecmult_kn<11> (the resident arena's k6 tables, option keys_k6): 11 groups of two 6-bit windows, 2 positions:
 # 6 doublings, 44 Q (22 lambda, 2 beta products per position), 11 G additions
 W_LADDER_KN = w_ladder(6, 44, 11, 6, nbeta=4)
-# k_ecmult_kn<9, 8> (the resident arena's wide-window tables, option keys_wide): 8 groups of 9-bit windows (15 per
-# half: 7 groups of two, one of one), 2 positions: 9 doublings, 30 Q (15 lambda, 2 beta products per position),
-# 11 G additions
-W_LADDER_KW = w_ladder(9, 30, 11, 9, nbeta=4)
+# k_ecmult_kn<9, 15> (the resident arena's wide-window tables, option keys_wide 2): 15 groups of one 9-bit window,
+# one position: no doublings, 30 Q (15 lambda, 2 beta products), 11 G additions
+W_LADDER_KW = w_ladder(0, 30, 11, 9, nbeta=2)
+# k_ecmult_kn<9, 8> (keys_wide 1, or an arena past the one-window layout's room): 8 groups of two 9-bit windows
+# (7 of two, one of one), 2 positions: 9 doublings, 30 Q (2 beta products per position), 11 G additions
+W_LADDER_KW2 = w_ladder(9, 30, 11, 9, nbeta=4)
 W_LADDER_K4F = w_ladder(30, 52, 11, 5, nbeta=14)   # k_ecmult_k4<true>: G on the unsplit u1, 11 25-bit windows
 # Peak: the highest v_mad_u64_u32 issue rate measured on MI355X
 # (tools/microbench/alu_rate.hip; profiles/r01/alu_rate_v3.jsonl, dependent

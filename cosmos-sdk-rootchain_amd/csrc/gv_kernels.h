@@ -82,9 +82,9 @@ typedef struct gvk_batch {
   // (GV_K6_GTAB_WORDS: the full-scalar 24-bit-window G tables); gtab4 unused
   const uint32_t* gtab6;
   int k6;
-  // kqw set (with k6 == GV_KW_ARENA_NG): kqt / kqt2 / kzq are the resident
-  // arena's wide-window tables (GV_KW_NT entries per group) and the ladder is
-  // k_ecmult_kn<GV_KW_QW, GV_KW_ARENA_NG>
+  // kqw set (with k6 == GV_KW_NG1 or GV_KW_NG2): kqt / kqt2 / kzq are the
+  // resident arena's wide-window tables (GV_KW_NT entries per group) and the
+  // ladder is k_ecmult_kn<GV_KW_QW, k6>
   int kqw;
   // k4 batches with gtabf set: the G half on the unsplit scalar (GV_GF_*),
   // k_prep<.., GF> digits and k_ecmult_k4<true> over gtabf (GV_GF_WORDS)
@@ -155,12 +155,13 @@ static_assert(GV_K6_QWIN + GV_K6_GWIN <= GV_DIGIT_ROWS, "k6 digits fit the digit
 static_assert(GV_K6_QW * GV_K6_QWIN >= 130 && GV_K6_GW * GV_K6_GWIN >= 257, "k6 windows cover the scalars");
 
 // The resident arena's wide-window tables (option "keys_wide",
-// k_ecmult_kn<GV_KW_QW, GV_KW_ARENA_NG>): 2^(QW-1) multiples per group, the
-// signed QW-bit windows of each 128-bit GLV half two per group, so the ladder
-// runs 2 positions.  QW = 9 (default): 256 entries, 15 windows in 8 groups,
-// 9 doublings and 30 Q additions (k6 arena: 6 and 44; QW 8: 8 and 34; QW 7:
-// 7 and 38).  G as on the k6 ladders (11 24-bit windows after the last
-// doubling, gtab6).  8 x 20 KiB of tables per key, built at gv_keys_load
+// k_ecmult_kn<GV_KW_QW, NG>): 2^(QW-1) multiples per group, the signed QW-bit
+// windows of each 128-bit GLV half one per group (NG = GV_KW_NG1: one ladder
+// position, no doublings) or two per group (GV_KW_NG2: 2 positions).  QW = 9
+// (default): 256 entries, 15 windows, 30 Q additions; 15 groups and no
+// doublings, or 8 groups and 9 doublings (k6 arena: 6 doublings and 44
+// additions; QW 8: 8 and 34; QW 7: 7 and 38 with two windows per group).  G as on the k6 ladders (11 24-bit windows after the last
+// doubling, gtab6).  15 (8) x 20 KiB of tables per key, built at gv_keys_load
 // beside the k6 tables while the key set fits (kn on the k6 tables otherwise).
 // A/B on one box (profiles/r05/kw/): c2_key_cache QW 7 / 8 / 9 = 329-344 /
 // 366 / 380-381M/s, k6 arena 312-317M/s.
@@ -170,8 +171,9 @@ static_assert(GV_K6_QW * GV_K6_QWIN >= 130 && GV_K6_GW * GV_K6_GWIN >= 257, "k6 
 #define GV_KW_NT (1 << (GV_KW_QW - 1))                    // 256 table entries per group
 #define GV_KW_QWIN ((130 + GV_KW_QW - 1) / GV_KW_QW)      // 15 windows per GLV half
 #define GV_KW_KEY_WORDS (GV_KW_NT * GV_QENT_WORDS)       // one group table (20,480 B)
-#define GV_KW_ARENA_NG ((GV_KW_QWIN + 1) / 2)             // 8 groups: two windows each, the last one or two
-static_assert(GV_KW_QW >= 7 && GV_KW_QW <= 9, "wide arena window width");
+#define GV_KW_NG1 GV_KW_QWIN                              // one window per group: 15 groups
+#define GV_KW_NG2 ((GV_KW_QWIN + 1) / 2)                  // two windows per group (the last one): 8 groups
+static_assert(GV_KW_QW >= 7 && GV_KW_QW <= 9 && GV_KW_NG1 <= 19, "wide arena layout");
 static_assert(GV_KW_QWIN + GV_K6_GWIN <= GV_DIGIT_ROWS, "wide-window digits fit the digit rows");
 static_assert(GV_KW_QW * GV_KW_QWIN >= 130, "wide windows cover the GLV halves");
 
@@ -310,13 +312,13 @@ hipError_t gvk_keys_build6(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_
                            uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* scratch, int with_qe,
                            uint32_t base, uint32_t* kqt6, uint32_t* kzq6, uint32_t kC, uint32_t* kok, uint32_t* kqt62,
                            uint32_t* kzq62, hipStream_t st);
-// The resident arena's wide-window tables (GV_KW_ARENA_NG groups of GV_KW_NT entries),
-// same arguments as gvk_keys_build6 (kqtw: GV_KW_KEY_WORDS per slot, kqtw2:
-// GV_KW_ARENA_NG - 1 rows per slot, kzqw2: (GV_KW_ARENA_NG - 1) x 8 rows).
+// The resident arena's wide-window tables (ng = GV_KW_NG1 or GV_KW_NG2 groups
+// of GV_KW_NT entries), same arguments as gvk_keys_build6 (kqtw:
+// GV_KW_KEY_WORDS per slot, kqtw2: ng - 1 rows per slot, kzqw2: (ng - 1) x 8 rows).
 hipError_t gvk_keys_build_wide(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
                            uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* scratch, int with_qe,
                            uint32_t base, uint32_t* kqtw, uint32_t* kzqw, uint32_t kC, uint32_t* kok, uint32_t* kqtw2,
-                           uint32_t* kzqw2, hipStream_t st);
+                           uint32_t* kzqw2, int ng, hipStream_t st);
 // the full-scalar G tables (GV_GF_WORDS words); base_scratch: 96 words
 hipError_t gvk_gen_gtablef(uint32_t* gtabf, uint32_t* base_scratch, hipStream_t st);
 // Key-table builds (k_keys_chain + k_keys_fwd + k_keys_back): scratch of

@@ -756,7 +756,7 @@ __constant__ const int kLGrpBit[GV_LGRP] = {0, 35, 70, 100};
 // w0(k), i.e. its table is that of 2^(QW w0(k)) Q; the ladder runs P
 // positions.  <5, 4>: k_ecmult_k4 (groups at bits 0, 35, 70, 100); <6, 4>:
 // the grouped route's k6 (0, 36, 72, 102); <6, GV_KN_ARENA_NG> and
-// <GV_KW_QW, GV_KW_ARENA_NG>: the resident arena's two table sets.
+// <GV_KW_QW, GV_KW_NG1 / GV_KW_NG2>: the resident arena's table sets.
 template <int QW, int NG>
 struct KLayout {
   static constexpr int QWIN = QW == GV_QW ? GV_QWIN : QW == GV_KW_QW ? GV_KW_QWIN : GV_K6_QWIN;
@@ -773,9 +773,9 @@ static_assert(KLayout<6, 4>::bit(1) == 36 && KLayout<6, 4>::bit(2) == 72 && KLay
               KLayout<6, 4>::P == 6, "k6 groups");
 static_assert(KLayout<6, GV_KN_ARENA_NG>::w0(GV_KN_ARENA_NG - 1) + KLayout<6, GV_KN_ARENA_NG>::nw(GV_KN_ARENA_NG - 1) ==
               GV_K6_QWIN, "arena groups cover the windows");
-static_assert(KLayout<GV_KW_QW, GV_KW_ARENA_NG>::w0(GV_KW_ARENA_NG - 1) +
-                      KLayout<GV_KW_QW, GV_KW_ARENA_NG>::nw(GV_KW_ARENA_NG - 1) == GV_KW_QWIN &&
-                  KLayout<GV_KW_QW, GV_KW_ARENA_NG>::P == 2, "wide arena groups cover the windows");
+static_assert(KLayout<GV_KW_QW, GV_KW_NG2>::w0(GV_KW_NG2 - 1) + KLayout<GV_KW_QW, GV_KW_NG2>::nw(GV_KW_NG2 - 1) ==
+                      GV_KW_QWIN && KLayout<GV_KW_QW, GV_KW_NG2>::P == 2 && KLayout<GV_KW_QW, GV_KW_NG1>::P == 1,
+              "wide arena groups cover the windows");
 
 // Affine x, y (8 x 32 words) of a finite Jacobian point.
 GV_DEV void gej29_to_affine_words(fe& x8, fe& y8, const gej29& p) {
@@ -1613,8 +1613,10 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gta
 // allocation at that of k4
 #define GV_KN_ROW(QW, NG, F) KLayout<QW, NG>::F(0), KLayout<QW, NG>::F(1), KLayout<QW, NG>::F(2), \
     KLayout<QW, NG>::F(3), KLayout<QW, NG>::F(4), KLayout<QW, NG>::F(5), KLayout<QW, NG>::F(6), \
-    KLayout<QW, NG>::F(7), KLayout<QW, NG>::F(8), KLayout<QW, NG>::F(9), KLayout<QW, NG>::F(10)
-__constant__ const int kKnW0[3][16] = {
+    KLayout<QW, NG>::F(7), KLayout<QW, NG>::F(8), KLayout<QW, NG>::F(9), KLayout<QW, NG>::F(10), \
+    KLayout<QW, NG>::F(11), KLayout<QW, NG>::F(12), KLayout<QW, NG>::F(13), KLayout<QW, NG>::F(14), \
+    KLayout<QW, NG>::F(15), KLayout<QW, NG>::F(16), KLayout<QW, NG>::F(17), KLayout<QW, NG>::F(18)
+__constant__ const int kKnW0[4][19] = {
     {KLayout<6, 4>::w0(0), KLayout<6, 4>::w0(1), KLayout<6, 4>::w0(2), KLayout<6, 4>::w0(3)},
     {KLayout<6, GV_KN_ARENA_NG>::w0(0), KLayout<6, GV_KN_ARENA_NG>::w0(1), KLayout<6, GV_KN_ARENA_NG>::w0(2),
      KLayout<6, GV_KN_ARENA_NG>::w0(3), KLayout<6, GV_KN_ARENA_NG>::w0(4), KLayout<6, GV_KN_ARENA_NG>::w0(5),
@@ -1622,8 +1624,9 @@ __constant__ const int kKnW0[3][16] = {
      KLayout<6, GV_KN_ARENA_NG>::w0(9), KLayout<6, GV_KN_ARENA_NG>::w0(10), KLayout<6, GV_KN_ARENA_NG>::w0(11),
      KLayout<6, GV_KN_ARENA_NG>::w0(12), KLayout<6, GV_KN_ARENA_NG>::w0(13), KLayout<6, GV_KN_ARENA_NG>::w0(14),
      KLayout<6, GV_KN_ARENA_NG>::w0(15)},
-    {GV_KN_ROW(GV_KW_QW, GV_KW_ARENA_NG, w0)}};
-__constant__ const int kKnNW[3][16] = {
+    {GV_KN_ROW(GV_KW_QW, GV_KW_NG2, w0)},
+    {GV_KN_ROW(GV_KW_QW, GV_KW_NG1, w0)}};
+__constant__ const int kKnNW[4][19] = {
     {KLayout<6, 4>::nw(0), KLayout<6, 4>::nw(1), KLayout<6, 4>::nw(2), KLayout<6, 4>::nw(3)},
     {KLayout<6, GV_KN_ARENA_NG>::nw(0), KLayout<6, GV_KN_ARENA_NG>::nw(1), KLayout<6, GV_KN_ARENA_NG>::nw(2),
      KLayout<6, GV_KN_ARENA_NG>::nw(3), KLayout<6, GV_KN_ARENA_NG>::nw(4), KLayout<6, GV_KN_ARENA_NG>::nw(5),
@@ -1631,9 +1634,10 @@ __constant__ const int kKnNW[3][16] = {
      KLayout<6, GV_KN_ARENA_NG>::nw(9), KLayout<6, GV_KN_ARENA_NG>::nw(10), KLayout<6, GV_KN_ARENA_NG>::nw(11),
      KLayout<6, GV_KN_ARENA_NG>::nw(12), KLayout<6, GV_KN_ARENA_NG>::nw(13), KLayout<6, GV_KN_ARENA_NG>::nw(14),
      KLayout<6, GV_KN_ARENA_NG>::nw(15)},
-    {GV_KN_ROW(GV_KW_QW, GV_KW_ARENA_NG, nw)}};
+    {GV_KN_ROW(GV_KW_QW, GV_KW_NG2, nw)},
+    {GV_KN_ROW(GV_KW_QW, GV_KW_NG1, nw)}};
 #undef GV_KN_ROW
-static_assert(GV_KN_ARENA_NG <= 16 && GV_KW_ARENA_NG <= 11, "layout table rows");
+static_assert(GV_KN_ARENA_NG <= 16 && GV_KW_NG1 <= 19, "layout table rows");
 
 template <int QW, int NG>
 __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_kn(const u32* gtab6, u32 n, u32 C, const u32* digits,
@@ -1641,7 +1645,7 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_kn(const u32* gta
                                                         const u32* flags, const u32* in_r, uint64_t* bits,
                                                         const u32* qidx, u32 kC) {
   using L = KLayout<QW, NG>;
-  static_assert(QW == GV_KW_QW ? NG == GV_KW_ARENA_NG : QW == GV_K6_QW && (NG == 4 || NG == GV_KN_ARENA_NG),
+  static_assert(QW == GV_KW_QW ? NG == GV_KW_NG1 || NG == GV_KW_NG2 : QW == GV_K6_QW && (NG == 4 || NG == GV_KN_ARENA_NG),
                 "a layout row of kKnW0 / kKnNW");
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   const u32 qi = qidx[g];
@@ -1673,7 +1677,7 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_kn(const u32* gta
       if (!isg) {
         const bool lam = slot >= NG;
         const int grp = lam ? 2 * NG - 1 - slot : slot;
-        constexpr int T = QW == GV_KW_QW ? 2 : NG == 4 ? 0 : 1;
+        constexpr int T = QW == GV_KW_QW ? (NG == GV_KW_NG1 ? 3 : 2) : NG == 4 ? 0 : 1;
         if (pos >= kKnNW[T][grp]) continue;                // wave-uniform
         const u32 dq = digits[(size_t)(kKnW0[T][grp] + pos) * C + g];
         d = lam ? ((int)dq >> 16) : ((int)(dq << 16) >> 16);
@@ -1836,7 +1840,7 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   const dim3 blk(256), grd(C / 256);
   // key-ordered lanes (gv_sort.hip): keyed k4 batches with sort scratch
   const bool k6 = b->kslot && b->k6 && b->gtab6;
-  const bool kw = k6 && b->kqw && b->k6 == GV_KW_ARENA_NG;   // the resident arena's wide-window tables
+  const bool kw = k6 && b->kqw && (b->k6 == GV_KW_NG1 || b->k6 == GV_KW_NG2);   // the arena's wide-window tables
   const bool gf = b->kslot && b->gtab4 && b->gtabf && !k6;   // k_ecmult_k4<true>
   const bool gfp = !b->kslot && b->gtabf;                     // per-item pub33: k_ecmult<false, true>
   const bool sorted = b->kslot && (b->gtab4 || k6) && b->srt.perm;
@@ -1902,8 +1906,12 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   }
   if (b->ev_ecm_start) (void)hipEventRecord(b->ev_ecm_start, se);
   if (b->bits_wait && !sorted) (void)hipStreamWaitEvent(se, b->bits_wait, 0);   // the ladder writes the bits
-  if (kw)
-    hipLaunchKernelGGL((gv::k_ecmult_kn<GV_KW_QW, GV_KW_ARENA_NG>), grd, blk, 0, se, b->gtab6, b->n, C, b->digits,
+  if (kw && b->k6 == GV_KW_NG1)
+    hipLaunchKernelGGL((gv::k_ecmult_kn<GV_KW_QW, GV_KW_NG1>), grd, blk, 0, se, b->gtab6, b->n, C, b->digits,
+                       b->kqt, b->kqt2, b->kzq, b->flags, b->in_r, sorted ? b->srt.bits : b->bits,
+                       (const uint32_t*)b->in_pfx, b->kC);
+  else if (kw)
+    hipLaunchKernelGGL((gv::k_ecmult_kn<GV_KW_QW, GV_KW_NG2>), grd, blk, 0, se, b->gtab6, b->n, C, b->digits,
                        b->kqt, b->kqt2, b->kzq, b->flags, b->in_r, sorted ? b->srt.bits : b->bits,
                        (const uint32_t*)b->in_pfx, b->kC);
   else if (k6 && b->k6 == GV_KN_ARENA_NG)
@@ -1990,15 +1998,19 @@ hipError_t gvk_keys_build_rows6(uint32_t n, uint32_t C, const uint32_t* in_x, co
 }
 
 hipError_t gvk_keys_build_wide(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,
-                           uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* scratch, int with_qe,
-                           uint32_t base, uint32_t* kqtw, uint32_t* kzqw, uint32_t kC, uint32_t* kok, uint32_t* kqtw2,
-                           uint32_t* kzqw2, hipStream_t st) {
+                               uint32_t* in_r, uint32_t* in_s, uint32_t* in_e, uint32_t* scratch, int with_qe,
+                               uint32_t base, uint32_t* kqtw, uint32_t* kzqw, uint32_t kC, uint32_t* kok,
+                               uint32_t* kqtw2, uint32_t* kzqw2, int ng, hipStream_t st) {
   if (n == 0) return hipSuccess;
+  if (ng != GV_KW_NG1 && ng != GV_KW_NG2) return hipErrorInvalidValue;
   const dim3 blk(256), grd(C / 256);
   hipLaunchKernelGGL(gv::k_unpack, grd, blk, 0, st, pub33, (const uint8_t*)nullptr, (const uint8_t*)nullptr, n, C,
                      in_x, in_pfx, in_r, in_s, in_e);
-  return keys_tables_launch<GV_KW_QW, GV_KW_ARENA_NG>(n, C, in_x, in_pfx, scratch, with_qe, base, kqtw, kzqw, kC, kok,
-                                                      kqtw2, kzqw2, st);
+  if (ng == GV_KW_NG1)
+    return keys_tables_launch<GV_KW_QW, GV_KW_NG1>(n, C, in_x, in_pfx, scratch, with_qe, base, kqtw, kzqw, kC, kok,
+                                                   kqtw2, kzqw2, st);
+  return keys_tables_launch<GV_KW_QW, GV_KW_NG2>(n, C, in_x, in_pfx, scratch, with_qe, base, kqtw, kzqw, kC, kok,
+                                                 kqtw2, kzqw2, st);
 }
 
 hipError_t gvk_keys_build(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,

@@ -148,13 +148,15 @@ struct Dev {
   uint32_t *kqt6 = nullptr, *kzq6 = nullptr, *kqt62 = nullptr, *kzq62 = nullptr;
   size_t keys6 = 0;                               // leading slots whose k6 tables are built
   // the resident arena's wide-window tables (option "keys_wide"): per slot
-  // GV_KW_ARENA_NG (8) 256-entry group tables of 2^(18 g) Q on one Z (kqtw: group 0, kqtw2:
+  // kw_ng (GV_KW_NG1 = 15: one 9-bit window per group, or GV_KW_NG2 = 8: two)
+  // 256-entry group tables on one Z (kqtw: group 0, kqtw2:
   // groups 1.., kzqw: the Z, 8 rows of stride kcapw; kzqw2: the chain's parked
   // Zs), in an arena of their own (capacity kcapw) grown by doubling while the
   // HBM budget holds it; keysw leading slots built.  kw_full: the budget
   // refused a growth (no more wide-window builds until gv_keys_reset)
   uint32_t *kqtw = nullptr, *kzqw = nullptr, *kqtw2 = nullptr, *kzqw2 = nullptr;
   size_t kcapw = 0, keysw = 0;
+  int kw_ng = 0;
   bool kw_full = false;
   // HBM held by the optional tables (G tables, key arenas) against ctx->hbm_budget
   size_t opt_bytes = 0;
@@ -353,8 +355,8 @@ int ensure_keys(Dev* d, size_t need, size_t used, hipStream_t st, size_t key_cap
   return GV_OK;
 }
 
-// Bytes per slot of the wide-window tables.
-constexpr size_t kKeyWSlotBytes = ((size_t)GV_KW_KEY_WORDS * GV_KW_ARENA_NG + 8 * GV_KW_ARENA_NG) * 4;
+// Bytes per slot of the wide-window tables of ng groups.
+constexpr size_t key_wide_slot_bytes(int ng) { return ((size_t)GV_KW_KEY_WORDS * ng + 8 * (size_t)ng) * 4; }
 
 // Grow the wide-window arena to `need` slots keeping the first `used` (doubling, not
 // past key_cap, then exact -- as ensure_keys).  Returns false when the budget
@@ -363,16 +365,21 @@ constexpr size_t kKeyWSlotBytes = ((size_t)GV_KW_KEY_WORDS * GV_KW_ARENA_NG + 8 
 // (plus 8 GiB of batch scratch: these tables are an optimisation and never
 // make a later gv_keys_load or batch fail), or when an allocation fails: the
 // arena is left as it was and batches keep the k6 tables.
-bool ensure_keys_wide(Dev* d, size_t need, size_t used, hipStream_t st, size_t key_cap, size_t budget) {
+// The layout is d->kw_ng's; cap1 bounds the one-window layout's capacity (a
+// test hook, option "keys_wide1_cap").
+bool ensure_keys_wide(Dev* d, size_t need, size_t used, hipStream_t st, size_t key_cap, size_t budget,
+                      size_t cap1 = SIZE_MAX) {
   if (need <= d->kcapw) return true;
   const size_t grow = d->kcapw >= key_cap ? need : std::min<size_t>(2 * d->kcapw, std::max<size_t>(need, key_cap));
   const size_t cap = round_up(std::max<size_t>({need, grow, 4096}), 256);
-  if (d->opt_bytes + cap * kKeyWSlotBytes > budget) return false;
+  const size_t slot_b = key_wide_slot_bytes(d->kw_ng);
+  if (d->kw_ng == GV_KW_NG1 && cap > cap1) return false;
+  if (d->opt_bytes + cap * slot_b > budget) return false;
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return false;
   const size_t reserve = (key_cap > d->kcap ? key_cap - d->kcap : 0) * key_slot_bytes(true) + (size_t(8) << 30);
-  if (free_b < cap * kKeyWSlotBytes + reserve) return false;
-  const size_t ng1 = GV_KW_ARENA_NG - 1;
+  if (free_b < cap * slot_b + reserve) return false;
+  const size_t ng1 = (size_t)d->kw_ng - 1;
   uint32_t *qt = nullptr, *zq = nullptr, *qt2 = nullptr, *zq2 = nullptr;
   if (hipMalloc(&qt, cap * GV_KW_KEY_WORDS * 4) != hipSuccess || hipMalloc(&zq, cap * 8 * 4) != hipSuccess ||
       hipMalloc(&qt2, cap * ng1 * GV_KW_KEY_WORDS * 4) != hipSuccess ||
@@ -399,10 +406,18 @@ bool ensure_keys_wide(Dev* d, size_t need, size_t used, hipStream_t st, size_t k
   }
   for (uint32_t* p : {d->kqtw, d->kzqw, d->kqtw2, d->kzqw2})
     if (p) (void)hipFree(p);
-  d->opt_bytes = d->opt_bytes - std::min(d->opt_bytes, d->kcapw * kKeyWSlotBytes) + cap * kKeyWSlotBytes;
+  d->opt_bytes = d->opt_bytes - std::min(d->opt_bytes, d->kcapw * slot_b) + cap * slot_b;
   d->kqtw = qt; d->kzqw = zq; d->kqtw2 = qt2; d->kzqw2 = zq2;
   d->kcapw = cap;
   return true;
+}
+
+// Drop the wide-window arena (its memory back to the device).
+void free_keys_wide(Dev* d) {
+  for (uint32_t** p : {&d->kqtw, &d->kzqw, &d->kqtw2, &d->kzqw2})
+    if (*p) { (void)hipFree(*p); *p = nullptr; }
+  d->opt_bytes -= std::min(d->opt_bytes, d->kcapw * key_wide_slot_bytes(d->kw_ng));
+  d->kcapw = d->keysw = 0;
 }
 
 // ---- ed25519 scratch
@@ -618,8 +633,11 @@ struct gv_ctx {
                                 // GLV windows (k_ecmult_k4<true>, 6 GiB of tables; GV_GFULL=0: A/B)
   bool k6 = false;              // grouped batches on k_ecmult_k6: 6-bit Q windows on 32-entry key tables, the lambda
                                 // frame, G on the unsplit u1 in 24-bit windows (GV_K6=1)
-  bool keys_wide = true;        // ... and wide-window tables (8 groups of 256 entries: 9 doublings, 30 Q additions)
-                                // while device memory holds them (GV_KEYS_WIDE)
+  int keys_wide = 2;            // ... and wide-window tables while device memory holds them (GV_KEYS_WIDE): 2 = one
+                                // 9-bit window per group (15 groups of 256 entries, no doublings, 30 Q additions),
+                                // moving to two per group (8 groups, 9 doublings) when that no longer fits;
+                                // 1 = two per group; 0 = none
+  size_t keys_wide1_cap = SIZE_MAX;   // test hook: the one-window layout's slot capacity ("keys_wide1_cap")
   bool keys_k6 = true;          // the resident arena (gv_keys_load) also holds k6 tables and its throughput batches
                                 // run k_ecmult_k6: the table build is paid once per key, not per batch (GV_KEYS_K6)
   size_t key_cap = GV_KEY_CAP;  // the callers' key-arena reset point: growth doubles up to here ("key_cap", GV_KEY_CAP)
@@ -943,10 +961,10 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
   const bool pipelined = st_ecm != nullptr && !small;
   // the resident arena's k6 tables (every slot in use has them): throughput
   // batches on k_ecmult_k6; the small-batch kernels keep the k4 tables
-  if (kslot && !ka && !small && ctx->keys_wide && d->kqtw && d->gtab6 && d->keysw >= ctx->keys) {
+  if (kslot && !ka && !small && ctx->keys_wide && d->kqtw && d->kw_ng && d->gtab6 && d->keysw >= ctx->keys) {
     // the wide-window tables (their own arena: Z rows of stride kcapw)
     b.kqt = d->kqtw; b.kzq = d->kzqw; b.kqt2 = d->kqtw2; b.kC = (uint32_t)d->kcapw;
-    b.k6 = GV_KW_ARENA_NG; b.kqw = 1; b.gtab6 = d->gtab6;
+    b.k6 = d->kw_ng; b.kqw = 1; b.gtab6 = d->gtab6;
   } else if (kslot && !ka && !small && ctx->keys_k6 && d->kqt6 && d->gtab6 && d->keys6 >= ctx->keys) {
     b.kqt = d->kqt6; b.kzq = d->kzq6; b.kqt2 = d->kqt62;
     b.k6 = GV_KN_ARENA_NG; b.gtab6 = d->gtab6;
@@ -1007,7 +1025,8 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
       b.gtabf = ctx->gfull && ctx->gfull_item ? d->gtabf : nullptr;
     }
     plan_sort(ctx, s, b, sort_base);
-    d->routes[b.kqw && b.gtab6                  ? GV_ROUTE_KW
+    d->routes[b.kqw && b.gtab6 && b.k6 == GV_KW_NG2 ? GV_ROUTE_KW2
+              : b.kqw && b.gtab6                ? GV_ROUTE_KW
               : b.k6 == GV_KN_ARENA_NG && b.gtab6 ? GV_ROUTE_KN
               : b.k6 && b.gtab6                ? GV_ROUTE_K6
               : b.kslot && b.gtab4 && b.gtabf ? GV_ROUTE_K4F
@@ -1871,7 +1890,10 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* gi = getenv("GV_GFULL_ITEM")) ctx->gfull_item = strcmp(gi, "0") != 0;
   if (const char* hs = getenv("GV_H2D_SERIAL")) ctx->h2d_serial = strcmp(hs, "0") != 0;
   if (const char* kk = getenv("GV_KEYS_K6")) ctx->keys_k6 = strcmp(kk, "0") != 0;
-  if (const char* kk = getenv("GV_KEYS_WIDE")) ctx->keys_wide = strcmp(kk, "0") != 0;
+  if (const char* kk = getenv("GV_KEYS_WIDE")) {
+    const int v = atoi(kk);
+    if (v >= 0 && v <= 2) ctx->keys_wide = v;
+  }
   if (const char* hl = getenv("GV_HOST_LADDER_STREAM")) ctx->host_ladder_stream = strcmp(hl, "0") != 0;
   parse_size_env("GV_ASYNC_CHUNK", &ctx->async_chunk);
   if (const char* ag = getenv("GV_ASYNC_GROWTH")) ctx->async_growth = std::max(1, std::min(64, atoi(ag)));
@@ -2197,6 +2219,61 @@ int gv_dev_verify_ed25519_msgs(gv_ctx* ctx, int dev_slot, size_t n, const void* 
 }
 
 // ---- key arena
+namespace {
+// The wide-window tables (layout d->kw_ng) of the n keys pub33 (host) into
+// slots base.. of the wide arena, in chunks whose build scratch stays within
+// what the k6 build's chunks take.  The caller holds d->mu.
+int build_wide(gv_ctx* ctx, Dev* d, Set* s, hipStream_t st, const uint8_t* pub33, size_t n, size_t base) {
+  const size_t stepw = std::min<size_t>(ctx->max_batch, std::max<size_t>(256, 32768 / (size_t)d->kw_ng / 256 * 256));
+  int rc;
+  for (size_t c0 = 0; c0 < n; c0 += stepw) {
+    const size_t cn = std::min(stepw, n - c0);
+    const size_t C = round_up(cn, 256);
+    const int qew = ctx->keys_scratch ? 1 : 0;
+    const size_t ww = gvk_keys_scratch_words((uint32_t)cn, d->kw_ng, GV_KW_NT, qew);
+    const size_t Cs = std::max(C, round_up(ww / GV_QTAB_WORDS + 1, 256));
+    if ((rc = ensure_cap(s, Cs))) return rc;
+    if ((rc = set_acquire(s, st))) return rc;
+    CK(hipMemcpyAsync(s->d_in, pub33 + c0 * 33, cn * 33, hipMemcpyHostToDevice, st));
+    CK(gvk_keys_build_wide(s->d_in, (uint32_t)cn, (uint32_t)C, s->in_x, s->in_pfx, s->in_r, s->in_s, s->in_e, s->qtab,
+                           qew, (uint32_t)(base + c0), d->kqtw, d->kzqw, (uint32_t)d->kcapw, d->kok, d->kqtw2,
+                           d->kzqw2, d->kw_ng, st));
+    if ((rc = set_release(s, st))) return rc;
+    CK(hipStreamSynchronize(st));
+  }
+  return GV_OK;
+}
+
+// The compressed keys of slots 0..n-1 read back from the k4 tables (affine
+// 1*Q of each slot); a slot whose key ParsePubKey rejected gets a prefix
+// byte it rejects again (0x00), so a rebuild keeps its verdict.
+int read_back_pub33(gv_ctx* ctx, Dev* d, hipStream_t st, size_t n, std::vector<uint8_t>& pub) {
+  std::vector<uint32_t> slots(n);
+  for (size_t i = 0; i < n; ++i) slots[i] = (uint32_t)i;
+  std::vector<uint8_t> xy(n * 64), ok(n);
+  uint8_t* buf = nullptr;
+  const size_t sb = round_up(n * 4, 256), xb = round_up(n * 64, 256);
+  if (hipMalloc(&buf, sb + xb + n) != hipSuccess) return GV_ENOMEM;
+  int rc = GV_OK;
+  if (hipMemcpyAsync(buf, slots.data(), n * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+      gvk_keys_point((uint32_t)n, (const uint32_t*)buf, d->kqt, d->kzq, (uint32_t)d->kcap, d->kok, (uint32_t)n,
+                     buf + sb, buf + sb + xb, st) != hipSuccess ||
+      hipMemcpyAsync(xy.data(), buf + sb, n * 64, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(ok.data(), buf + sb + xb, n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    rc = GV_EHIP;
+  (void)hipFree(buf);
+  if (rc) return rc;
+  pub.assign(n * 33, 0);
+  for (size_t i = 0; i < n; ++i) {
+    uint8_t* p = &pub[i * 33];
+    memcpy(p + 1, &xy[i * 64], 32);
+    p[0] = ok[i] ? (uint8_t)(0x02 | (xy[i * 64 + 63] & 1)) : 0x00;
+  }
+  return GV_OK;
+}
+}  // namespace
+
 int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out) {
   if (!ctx) return GV_EINVAL;
   if (n == 0) return GV_OK;
@@ -2250,32 +2327,31 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
       CK(hipStreamSynchronize(st));            // the caller's pub33 chunk is read by then
     }
     if (k6) d->keys6 = base + n;
-    // the wide-window tables: while every earlier slot has them and memory holds
-    // the grown arena (a refusal stops them until gv_keys_reset: batches
-    // then take the k6 tables)
+    // the wide-window tables: while every earlier slot has them and memory
+    // holds the grown arena (a refusal stops them until gv_keys_reset:
+    // batches then take the k6 tables).  An arena started from slot 0 takes
+    // the option's layout; one window per group (15 tables per key) moves the
+    // whole arena to two per group (8 tables) when it no longer fits: the
+    // loaded slots' keys are read back from the k4 tables and rebuilt.
     if (ctx->keys_wide && d->gtab6 && d->keysw == base && !d->kw_full) {
-      if (!ensure_keys_wide(d, base + n, base, st, ctx->key_cap, ctx->hbm_budget)) {
+      const int want = ctx->keys_wide == 2 ? GV_KW_NG1 : GV_KW_NG2;
+      if ((base == 0 || !d->kw_ng) && d->kw_ng != want) {
+        free_keys_wide(d);
+        d->kw_ng = want;
+      }
+      bool ok = ensure_keys_wide(d, base + n, base, st, ctx->key_cap, ctx->hbm_budget, ctx->keys_wide1_cap);
+      if (!ok && d->kw_ng == GV_KW_NG1) {
+        std::vector<uint8_t> old_pub;
+        if (base && (rc = read_back_pub33(ctx, d, st, base, old_pub))) return rc;
+        free_keys_wide(d);
+        d->kw_ng = GV_KW_NG2;
+        ok = ensure_keys_wide(d, base + n, 0, st, ctx->key_cap, ctx->hbm_budget);
+        if (ok && base && (rc = build_wide(ctx, d, s, st, old_pub.data(), base, 0))) return rc;
+      }
+      if (!ok) {
         d->kw_full = true;
       } else {
-        // GV_KW_ARENA_NG groups of GV_KW_NT entries: scratch rows per key ~6x
-        // the k6 build's (QW 9), so the chunks are smaller (scratch within
-        // what the k6 build's chunks take)
-        const size_t stepw = std::min<size_t>(ctx->max_batch, GV_KW_QW >= 9 ? 4096 : 8192);
-        for (size_t c0 = 0; c0 < n; c0 += stepw) {
-          const size_t cn = std::min(stepw, n - c0);
-          const size_t C = round_up(cn, 256);
-          const int qew = ctx->keys_scratch ? 1 : 0;
-          const size_t ww = gvk_keys_scratch_words((uint32_t)cn, GV_KW_ARENA_NG, GV_KW_NT, qew);
-          const size_t Cs = std::max(C, round_up(ww / GV_QTAB_WORDS + 1, 256));
-          if ((rc = ensure_cap(s, Cs))) return rc;
-          if ((rc = set_acquire(s, st))) return rc;
-          CK(hipMemcpyAsync(s->d_in, pub33 + c0 * 33, cn * 33, hipMemcpyHostToDevice, st));
-          CK(gvk_keys_build_wide(s->d_in, (uint32_t)cn, (uint32_t)C, s->in_x, s->in_pfx, s->in_r, s->in_s, s->in_e,
-                                 s->qtab, qew, (uint32_t)(base + c0), d->kqtw, d->kzqw, (uint32_t)d->kcapw, d->kok,
-                                 d->kqtw2, d->kzqw2, st));
-          if ((rc = set_release(s, st))) return rc;
-          CK(hipStreamSynchronize(st));
-        }
+        if ((rc = build_wide(ctx, d, s, st, pub33, n, base))) return rc;
         d->keysw = base + n;
       }
     }
@@ -2733,8 +2809,23 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "ed_keyed")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->ed_keyed = val != 0;
+  } else if (!strcmp(key, "keys_wide")) {
+    // the layout of an arena started from slot 0 from now on (a running arena
+    // keeps its layout until gv_keys_reset); 0 stops its use at once
+    if (val < 0 || val > 2) return GV_EINVAL;
+    std::vector<std::unique_lock<std::mutex>> held;
+    for (Dev* d : ctx->devs) held.emplace_back(d->mu);
+    for (Dev* d : ctx->devs) {
+      CK(hipSetDevice(d->id));
+      for (hipStream_t t : d->hi_st) CK(hipStreamSynchronize(t));
+      d->bits_used = false;
+    }
+    ctx->keys_wide = (int)val;
+  } else if (!strcmp(key, "keys_wide1_cap")) {
+    if (val < 0) return GV_EINVAL;
+    ctx->keys_wide1_cap = val == 0 ? SIZE_MAX : (size_t)val;
   } else if (!strcmp(key, "two_ladders") || !strcmp(key, "gfull") || !strcmp(key, "k6") ||
-             !strcmp(key, "keys_k6") || !strcmp(key, "keys_wide")) {
+             !strcmp(key, "keys_k6")) {
     // schedule switches: every device lock held across the drain and the
     // write, so no pipelined call launches on a mix of old and new state
     if (val != 0 && val != 1) return GV_EINVAL;
@@ -2746,7 +2837,7 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
       d->bits_used = false;
     }
     bool& flag = !strcmp(key, "two_ladders") ? ctx->two_ladders : !strcmp(key, "gfull") ? ctx->gfull
-                 : !strcmp(key, "k6") ? ctx->k6 : !strcmp(key, "keys_wide") ? ctx->keys_wide : ctx->keys_k6;
+                 : !strcmp(key, "k6") ? ctx->k6 : ctx->keys_k6;
     flag = val != 0;
   } else if (!strcmp(key, "async_chunk")) {
     if (val < 256 || (unsigned long long)val > kMaxItems) return GV_EINVAL;

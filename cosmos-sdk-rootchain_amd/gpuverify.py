@@ -510,7 +510,7 @@ class Verifier:
         _check(self._L.gv_group_stats(self._ctx, slot, ctypes.byref(b), ctypes.byref(k)), "gv_group_stats")
         return b.value, k.value
 
-    ROUTES = ("pub33", "keyed125", "k4", "k6", "lat", "lat_keyed", "k4f", "item_f", "kn", "ed_lat", "kw")
+    ROUTES = ("pub33", "keyed125", "k4", "k6", "lat", "lat_keyed", "k4f", "item_f", "kn", "ed_lat", "kw", "kw2")
 
     def route_stats(self, slot: int = 0) -> dict:
         """Batches per secp256k1 schedule on device slot since open (gv_route_stats)."""

@@ -298,13 +298,17 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * tables -- and keyed throughput batches whose slots all have them run the
  * 6-doubling ladder; small keyed batches keep the k4 tables; same verdicts;
  * default 1, env GV_KEYS_K6; route counter GV_ROUTE_KN),
- * "keys_wide" (0/1: gv_keys_load also builds each key's 9-bit-window
- * tables -- 8 groups of 256 entries on one Z, 160 KB per key, in an arena of
- * their own that grows by doubling while the HBM budget holds it and the
- * device keeps room for the k4 / k6 arena to reach key_cap -- and keyed
- * throughput batches whose slots all have them run the 9-doubling,
- * 30-addition ladder (else the k6 one); same verdicts; default 1, env
- * GV_KEYS_WIDE; route counter GV_ROUTE_KW),
+ * "keys_wide" (0/1/2: gv_keys_load also builds each key's 9-bit-window
+ * tables of 256 entries on one Z -- 2 (default): one window per group, 15
+ * tables (300 KB per key), no doublings and 30 Q additions per verify; 1: two
+ * windows per group, 8 tables (160 KB), 9 doublings -- in an arena of their
+ * own that grows by doubling while the HBM budget holds it and the device
+ * keeps room for the k4 / k6 arena to reach key_cap; with 2, an arena that no
+ * longer fits moves to the two-window layout (the loaded keys are read back
+ * from the k4 tables and rebuilt); keyed throughput batches whose slots all
+ * have them run that ladder (else the k6 one); same verdicts; the layout of
+ * an arena is chosen when it starts from slot 0; env GV_KEYS_WIDE; route
+ * counters GV_ROUTE_KW / GV_ROUTE_KW2),
  * "key_cap" / "ed_key_cap" (the callers' reset points of the secp256k1 /
  * ed25519 key arenas: an arena grows by doubling up to it and exactly past it;
  * defaults GV_KEY_CAP / GV_ED_KEY_CAP, env of the same names; the Go shim sets
@@ -386,8 +390,9 @@ int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys)
  * batches on the resident arena's k6 tables: 11 groups of 6-bit windows, 6
  * doublings, option "keys_k6"), GV_ROUTE_ED_LAT (small uncached ed25519
  * host batches on k_ed_lat_unc, option "ed_unc_lat_max"), GV_ROUTE_KW (keyed
- * batches on the resident arena's wide-window tables: 8 groups of 9-bit
- * windows, 9 doublings, option "keys_wide").  Instrumentation only (bench route
+ * batches on the resident arena's wide-window tables, one 9-bit window per
+ * group: 15 groups, no doublings, option "keys_wide"), GV_ROUTE_KW2 (the same
+ * with two windows per group: 8 groups, 9 doublings).  Instrumentation only (bench route
  * attribution, node metrics). */
 #define GV_ROUTE_PUB33 0
 #define GV_ROUTE_KEYED125 1
@@ -400,7 +405,8 @@ int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys)
 #define GV_ROUTE_KN 8
 #define GV_ROUTE_ED_LAT 9
 #define GV_ROUTE_KW 10
-#define GV_ROUTES 11
+#define GV_ROUTE_KW2 11
+#define GV_ROUTES 12
 int gv_route_stats(gv_ctx* ctx, int dev_slot, uint64_t out[GV_ROUTES]);
 
 const char* gv_strerror(int code);

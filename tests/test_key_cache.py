@@ -23,8 +23,9 @@ def ver():
 # (lat_max, sliced, keys_k6, keys_wide): the PATHS schedules (rows: pub33 only)
 # with the resident arena's kn tables (throughput: the wide-window tables), plus the
 # sliced kernel on the k4 tables and the throughput ladder on the k6 tables
-KEYED_PATHS = {**{p: (v[0], v[1], 1, 1) for p, v in PATHS.items() if p != "latency_rows"},
-               "latency_k4_arena": (1 << 30, 1, 0, 0), "throughput_k6_arena": (0, 1, 1, 0)}
+KEYED_PATHS = {**{p: (v[0], v[1], 1, 2) for p, v in PATHS.items() if p != "latency_rows"},
+               "latency_k4_arena": (1 << 30, 1, 0, 0), "throughput_k6_arena": (0, 1, 1, 0),
+               "throughput_wide_two": (0, 1, 1, 1)}
 
 
 @pytest.fixture(params=sorted(KEYED_PATHS))
@@ -43,7 +44,7 @@ def path(request, ver):
     ver.reset_schedule()
     ver.set_option("lat_sliced", 1)
     ver.set_option("keys_k6", 1)
-    ver.set_option("keys_wide", 1)
+    ver.set_option("keys_wide", 2)
 
 
 def keyed_inputs(ver, pub):

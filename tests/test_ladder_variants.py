@@ -25,16 +25,18 @@ pytestmark = pytest.mark.gpu
 
 SCHEDULES = {"k4f": {"gfull": 1, "k6": 0}, "k4": {"gfull": 0, "k6": 0}, "k6": {"gfull": 1, "k6": 1},
              "item_gf": {"group_keys": 0, "gfull_item": 1}, "item_glv": {"group_keys": 0, "gfull_item": 0}}
-ROUTE = {"k4f": "k4f", "k4": "k4", "k6": "k6", "wide": "k6", "item_gf": "item_f", "item_glv": "pub33"}
-DEFAULTS = {"gfull": 1, "k6": 0, "group_keys": 1, "gfull_item": 1, "keys_k6": 1, "keys_wide": 1}
+ROUTE = {"k4f": "k4f", "k4": "k4", "k6": "k6", "wide": "k6", "wide2": "k6", "item_gf": "item_f",
+         "item_glv": "pub33"}
+DEFAULTS = {"gfull": 1, "k6": 0, "group_keys": 1, "gfull_item": 1, "keys_k6": 1, "keys_wide": 2, "keys_wide1_cap": 0}
 # the cached-key route (gv_keys_load slots): k6 / wide-window tables are built
 # at load time when "keys_k6" / "keys_wide" are on; the message part of the test runs
 # the grouped route
 CACHED = {"k4f": {"gfull": 1, "keys_k6": 0, "keys_wide": 0, "k6": 0},
           "k4": {"gfull": 0, "keys_k6": 0, "keys_wide": 0, "k6": 0},
           "k6": {"gfull": 1, "keys_k6": 1, "keys_wide": 0, "k6": 1},
-          "wide": {"gfull": 1, "keys_k6": 1, "keys_wide": 1, "k6": 1}}
-ARENA_ROUTE = {"k6": "kn", "wide": "kw"}                          # schedule -> the arena's route counter
+          "wide": {"gfull": 1, "keys_k6": 1, "keys_wide": 2, "k6": 1},
+          "wide2": {"gfull": 1, "keys_k6": 1, "keys_wide": 1, "k6": 1}}
+ARENA_ROUTE = {"k6": "kn", "wide": "kw", "wide2": "kw2"}          # schedule -> the arena's route counter
 
 
 @pytest.fixture(scope="module")
@@ -209,34 +211,48 @@ def test_cached_keys_k6_goldens_and_slots(ver):
     ver.keys_reset()
 
 
-def test_wide_arena_growth_keeps_the_loaded_slots(ver):
-    """The wide-window tables live in an arena of their own that grows by doubling from
-    4,096 slots: a second load past it copies the first load's tables into the
-    grown arena (Z rows re-strided) and builds the rest; every slot then
-    verifies on the wide-window ladder exactly as on the k6 one, and a load after
-    gv_keys_reset rebuilds from slot 0."""
+@pytest.mark.parametrize("layout", ["one", "two", "relayout"])
+def test_wide_arena_growth_keeps_the_loaded_slots(ver, layout):
+    """The wide-window tables live in an arena of their own that grows by
+    doubling from 4,096 slots: a second load past it copies the first load's
+    tables into the grown arena (Z rows re-strided) and builds the rest; every
+    slot then verifies on the wide-window ladder exactly as on the k6 one, and
+    a load after gv_keys_reset rebuilds from slot 0.  Layouts: one window per
+    group (keys_wide 2), two (keys_wide 1), and one window per group whose
+    growth is refused (keys_wide1_cap 4,096): the whole arena moves to two
+    windows per group, the first load's keys read back from the k4 tables."""
     pub, sig, dig, exp = bench.make_digest_workload(30_000, 0x98, 6000, 0.25, 16)
     want = O.verify_digests(pub, sig, dig, threads=16)
+    route = "kw" if layout == "one" else "kw2"
+    sched = "wide" if layout != "two" else "wide2"
     ver.keys_reset()
-    uniq, first, inv = np.unique(pub, axis=0, return_index=True, return_inverse=True)
-    order = np.argsort(first)
-    a = ver.keys_load(uniq[order][:3000])
-    b = ver.keys_load(uniq[order][3000:])                          # past 4,096 slots: the wide arena grows
-    slots_u = np.concatenate([a, b]).astype(np.uint32)
-    rank = np.empty_like(order)
-    rank[order] = np.arange(len(order))
-    slots = slots_u[rank[inv.reshape(-1)]]
-    gotw, rw = run(ver, "wide", lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
-    assert rw["kw"] >= 1, rw
-    assert np.array_equal(gotw, want)
-    got6, r6 = run(ver, "k6", lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
-    assert r6["kn"] >= 1, r6
-    assert np.array_equal(got6, want)
-    ver.keys_reset()                                               # slots rewritten from 0
-    c = ver.keys_load(uniq[order][3000:]).astype(np.uint32)
-    sub = rank[inv.reshape(-1)] >= 3000
-    s2 = c[rank[inv.reshape(-1)][sub] - 3000]
-    got, r = run(ver, "wide", lambda: ver.verify_batch_digests_keyed(s2, sig[sub], dig[sub]), CACHED)
-    assert r["kw"] >= 1, r
-    assert np.array_equal(got, want[sub])
-    ver.keys_reset()
+    ver.set_option("keys_wide", 1 if layout == "two" else 2)
+    ver.set_option("keys_wide1_cap", 4096 if layout == "relayout" else 0)
+    try:
+        uniq, first, inv = np.unique(pub, axis=0, return_index=True, return_inverse=True)
+        order = np.argsort(first)
+        a = ver.keys_load(uniq[order][:3000])
+        b = ver.keys_load(uniq[order][3000:])                      # past 4,096 slots: the wide arena grows
+        slots_u = np.concatenate([a, b]).astype(np.uint32)
+        rank = np.empty_like(order)
+        rank[order] = np.arange(len(order))
+        slots = slots_u[rank[inv.reshape(-1)]]
+        gotw, rw = run(ver, sched, lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
+        assert rw[route] >= 1, rw
+        assert np.array_equal(gotw, want)
+        got6, r6 = run(ver, "k6", lambda: ver.verify_batch_digests_keyed(slots, sig, dig), CACHED)
+        assert r6["kn"] >= 1, r6
+        assert np.array_equal(got6, want)
+        ver.set_option("keys_wide", 1 if layout == "two" else 2)
+        ver.set_option("keys_wide1_cap", 4096 if layout == "relayout" else 0)
+        ver.keys_reset()                                           # slots rewritten from 0
+        c = ver.keys_load(uniq[order][3000:]).astype(np.uint32)
+        sub = rank[inv.reshape(-1)] >= 3000
+        s2 = c[rank[inv.reshape(-1)][sub] - 3000]
+        got, r = run(ver, sched, lambda: ver.verify_batch_digests_keyed(s2, sig[sub], dig[sub]), CACHED)
+        assert r["kw" if layout == "one" else "kw2"] >= 1 or (layout == "relayout" and r["kw"] >= 1), r
+        assert np.array_equal(got, want[sub])
+    finally:
+        ver.set_option("keys_wide", 2)
+        ver.set_option("keys_wide1_cap", 0)
+        ver.keys_reset()

@@ -19,7 +19,7 @@ def main():
     pub, sig, dig, exp = B.make_digest_workload(n, 0xC2, 65536, 0.0, B.host_cores()["effective"])
     ver = gvm.Verifier([0])
     for _ in range(reps):
-        for kw in (1, 0):
+        for kw in (2, 1, 0):
             ver.set_option("keys_wide", kw)
             r = X.c2_key_cache(ver, pub, sig, dig, exp, 65536, steps=20)
             print(json.dumps({"keys_wide": kw, "value": r["value"], "route": r["route"], "mismatches": r["mismatches"],
