@@ -34,6 +34,11 @@ struct ge_pre { fe29 ypx, ymx, xy2d; };           // (y+x, y-x, 2dxy), affine, m
 #define ED_BTAB_WINDOWS 32
 #define ED_BTAB_ENTRIES 129                       // j = 0..128
 #define ED_BTAB_WORDS (ED_BTAB_WINDOWS * ED_BTAB_ENTRIES * ED_PRE_WORDS)
+// The radix-2^16 comb table of B (k_ed_keyed): j * 65536^w * B, w < 16,
+// j = 0..2^15 -- 16 additions for [s]B instead of 32, 56.6 MB per device.
+#define ED_BTAB16_WINDOWS 16
+#define ED_BTAB16_ENTRIES 32769
+#define ED_BTAB16_WORDS ((size_t)ED_BTAB16_WINDOWS * ED_BTAB16_ENTRIES * ED_PRE_WORDS)
 
 GV_DEV void fe_const(fe29& r, const u32* c) {
 #pragma unroll
@@ -432,6 +437,47 @@ GV_DEV void ed_btab_entry(u32 out[ED_PRE_WORDS], int w, int j) {
     out[k] = p.ypx.n[k];
     out[9 + k] = p.ymx.n[k];
     out[18 + k] = p.xy2d.n[k];
+  }
+}
+
+// Radix-2^16 comb table entry j * 65536^w * B (affine precomputed form).
+GV_DEV void ed_btab16_entry(u32 out[ED_PRE_WORDS], int w, int j) {
+  ge_ext b;
+  fe_const(b.X, kEdBx);
+  fe_const(b.Y, kEdBy);
+  e29_set(b.Z, 1);
+  e29_mul(b.T, b.X, b.Y);
+  for (int k = 0; k < 16 * w; ++k) ge_dbl(b, b);
+  ge_cached cb;
+  ge_to_cached(cb, b);
+  ge_ext acc;
+  ge_identity(acc);
+  for (int bit = 15; bit >= 0; --bit) {
+    ge_dbl(acc, acc);
+    if ((j >> bit) & 1) ge_add_cached(acc, acc, cb, false);
+  }
+  ge_pre p;
+  ge_to_pre(p, acc);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    out[k] = p.ypx.n[k];
+    out[9 + k] = p.ymx.n[k];
+    out[18 + k] = p.xy2d.n[k];
+  }
+}
+
+// acc += [s]B from the radix-2^16 table: signed digits, LSB-first, digit w in
+// (-2^15, 2^15] (a digit above 2^15 borrows 2^16 and carries one into the
+// next window; s < 2^253 leaves no carry out of window 15).
+GV_DEV void ed_add_sb16(ge_ext& acc, const u32 s[8], const u32* btab16) {
+  int carry = 0;
+#pragma unroll 1
+  for (int w = 0; w < ED_BTAB16_WINDOWS; ++w) {
+    int dgt = (int)((s[w >> 1] >> (16 * (w & 1))) & 0xFFFFu) + carry;
+    carry = dgt > 32768 ? 1 : 0;
+    dgt -= 65536 * carry;
+    const int mag = dgt < 0 ? -dgt : dgt;
+    ge_add_pretab(acc, acc, btab16 + (size_t)(w * ED_BTAB16_ENTRIES + mag) * ED_PRE_WORDS, dgt < 0);
   }
 }
 

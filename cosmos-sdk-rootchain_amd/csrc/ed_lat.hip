@@ -714,21 +714,26 @@ __global__ __launch_bounds__(256) void k_ed_keyed(const gvk_edk b) {
       ge_add_tab<true>(acc, acc, kt + (size_t)(w * 8 + mag - 1) * ED_CACHED_WORDS, 1, 0, dg < 0);
     }
   }
-  // + [s]B: signed radix-256 digits, LSB-first (ed_ladder_check's recoding)
-  u32 ss[8];
+  // + [s]B: 16 signed radix-2^16 digits from btab16, or (null) 32 radix-256
+  // digits, LSB-first (ed_ladder_check's recoding)
+  if (b.btab16) {
+    ed_add_sb16(acc, sw + 8, b.btab16);
+  } else {
+    u32 ss[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) ss[i] = sw[8 + i];
-  int carry = 0;
+    for (int i = 0; i < 8; ++i) ss[i] = sw[8 + i];
+    int carry = 0;
 #pragma unroll 1
-  for (int w = 0; w < ED_BTAB_WINDOWS; ++w) {
-    int dgt = (int)(ss[0] & 0xFFu) + carry;
+    for (int w = 0; w < ED_BTAB_WINDOWS; ++w) {
+      int dgt = (int)(ss[0] & 0xFFu) + carry;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) ss[k] = (ss[k] >> 8) | (ss[k + 1] << 24);
-    ss[7] >>= 8;
-    carry = dgt > 128 ? 1 : 0;
-    dgt -= 256 * carry;
-    const int mag = dgt < 0 ? -dgt : dgt;
-    ge_add_pretab(acc, acc, b.btab + (size_t)(w * ED_BTAB_ENTRIES + mag) * ED_PRE_WORDS, dgt < 0);
+      for (int k = 0; k < 7; ++k) ss[k] = (ss[k] >> 8) | (ss[k + 1] << 24);
+      ss[7] >>= 8;
+      carry = dgt > 128 ? 1 : 0;
+      dgt -= 256 * carry;
+      const int mag = dgt < 0 ? -dgt : dgt;
+      ge_add_pretab(acc, acc, b.btab + (size_t)(w * ED_BTAB_ENTRIES + mag) * ED_PRE_WORDS, dgt < 0);
+    }
   }
   u32 ew[8];
   ge_tobytes(ew, acc);

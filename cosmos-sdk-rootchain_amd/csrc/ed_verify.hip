@@ -33,6 +33,7 @@ namespace ed {
 static_assert(ED_ATAB_WORDS == GV_ED_ATAB_WORDS, "per-lane table size");
 static_assert(GV_ED_ROWS == ED_ATAB_WORDS + 9, "scratch rows");
 static_assert(ED_BTAB_WORDS == GV_ED_BTAB_WORDS, "comb table size");
+static_assert(ED_BTAB16_WORDS == GV_ED_BTAB16_WORDS, "radix-2^16 comb table size");
 
 __global__ __launch_bounds__(256) void k_ed_btab(u32* btab) {
   const int t = blockIdx.x * 256 + threadIdx.x;
@@ -41,6 +42,15 @@ __global__ __launch_bounds__(256) void k_ed_btab(u32* btab) {
   ed_btab_entry(out, t / ED_BTAB_ENTRIES, t % ED_BTAB_ENTRIES);
 #pragma unroll
   for (int k = 0; k < ED_PRE_WORDS; ++k) btab[(size_t)t * ED_PRE_WORDS + k] = out[k];
+}
+
+__global__ __launch_bounds__(256) void k_ed_btab16(u32* btab16) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= ED_BTAB16_WINDOWS * ED_BTAB16_ENTRIES) return;
+  u32 out[ED_PRE_WORDS];
+  ed_btab16_entry(out, t / ED_BTAB16_ENTRIES, t % ED_BTAB16_ENTRIES);
+#pragma unroll
+  for (int k = 0; k < ED_PRE_WORDS; ++k) btab16[(size_t)t * ED_PRE_WORDS + k] = out[k];
 }
 
 // Stage 1 (register-heavy hash / decode / table build; ~11 % of the work).
@@ -99,6 +109,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 extern "C" hipError_t gvk_ed_btab(uint32_t* btab, hipStream_t st) {
   const int n = ED_BTAB_WINDOWS * ED_BTAB_ENTRIES;
   hipLaunchKernelGGL(gv::ed::k_ed_btab, dim3((n + 255) / 256), dim3(256), 0, st, btab);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t gvk_ed_btab16(uint32_t* btab16, hipStream_t st) {
+  const int n = ED_BTAB16_WINDOWS * ED_BTAB16_ENTRIES;
+  hipLaunchKernelGGL(gv::ed::k_ed_btab16, dim3((n + 255) / 256), dim3(256), 0, st, btab16);
   return hipGetLastError();
 }
 

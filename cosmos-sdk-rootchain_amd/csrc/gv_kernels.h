@@ -244,6 +244,9 @@ typedef struct gvk_ed {
   uint64_t* bits;               // C/64 words
 } gvk_ed;
 hipError_t gvk_ed_btab(uint32_t* btab, hipStream_t st);
+// The radix-2^16 comb table j * 65536^w * B, w < 16, j <= 2^15 (k_ed_keyed's [s]B).
+#define GV_ED_BTAB16_WORDS ((size_t)16 * 32769 * 27)
+hipError_t gvk_ed_btab16(uint32_t* btab16, hipStream_t st);
 hipError_t gvk_ed_verify(const gvk_ed* b, hipStream_t st);
 // ed25519 key arena (gv_ed_keys_load): per slot the comb table of -A,
 // j * 16^w * (-A), w < 64, j = 1..8, cached form (36 words each), the raw key
@@ -287,6 +290,7 @@ typedef struct gvk_edk {
   const uint32_t* kok;
   uint32_t kcount;
   const uint32_t* btab;
+  const uint32_t* btab16;       // GV_ED_BTAB16_WORDS, or null: [s]B from btab (32 additions instead of 16)
   uint8_t* out8;                // n verdict bytes (device)
 } gvk_edk;
 hipError_t gvk_ed_keyed(const gvk_edk* b, hipStream_t st);

@@ -166,6 +166,8 @@ struct Dev {
   int ring_next = 0, ring_count = 0, last = -1;
   // ed25519: the resident comb table and one scratch set
   uint32_t* edtab = nullptr;
+  uint32_t* edtab16 = nullptr;                    // the radix-2^16 comb table of B (k_ed_keyed), built on first use
+  bool edtab16_failed = false;
   struct Ed {
     size_t cap = 0;                               // lanes
     uint8_t* d_in = nullptr;                      // pub32 | sig64 | off u64 | len u32 (ed_layout)
@@ -466,7 +468,29 @@ struct EdGroupCfg {
   size_t cap;
   bool sorted;
   bool split_keys;   // k_ed_keys_chain + k_ed_keys_tab (the table adds off the serial chain)
+  bool btab16;       // k_ed_keyed takes [s]B from the radix-2^16 table
 };
+
+// The radix-2^16 comb table of B, built on the device on first use (56.6 MB);
+// null when the option is off or its allocation failed (k_ed_keyed then adds
+// [s]B from the radix-256 table: same verdicts).
+const uint32_t* ed_btab16(Dev* d, bool on, hipStream_t st) {
+  if (!on) return nullptr;
+  if (!d->edtab16 && !d->edtab16_failed) {
+    uint32_t* t = nullptr;
+    if (hipMalloc(&t, GV_ED_BTAB16_WORDS * 4) != hipSuccess) {
+      (void)hipGetLastError();
+      d->edtab16_failed = true;
+    } else if (gvk_ed_btab16(t, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+      (void)hipFree(t);
+      (void)hipGetLastError();
+      d->edtab16_failed = true;
+    } else {
+      d->edtab16 = t;
+    }
+  }
+  return d->edtab16;
+}
 
 int ensure_edg(Dev* d, size_t need) {
   if (need <= d->edg_cap) return GV_OK;
@@ -536,6 +560,7 @@ int ed_grouped(Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig, const u
   b.kok = d->edg_kok;
   b.kcount = (uint32_t)U;
   b.btab = d->edtab;
+  b.btab16 = ed_btab16(d, gc.btab16, st);
   b.out8 = (uint8_t*)o8;
   CK(gvk_ed_keyed(&b, st));
   CK(gvk_ed_pack_bits((uint32_t)n, (const uint8_t*)o8, bits, st));
@@ -669,6 +694,7 @@ struct gv_ctx {
   int ed_group_div = 16;         // ... with at most items / ed_group_div distinct keys
   size_t ed_group_cap = 16384;   // ... and at most this many (72 KB of comb table per key)
   bool ed_keys_split = true;     // ed25519 key tables: serial chain and table adds in two launches (GV_ED_KEYS_SPLIT=0: A/B)
+  bool ed_btab16 = true;         // k_ed_keyed's [s]B from the radix-2^16 table: 16 additions instead of 32 (GV_ED_BTAB16)
   bool ed_keyed = true;          // keyed ed25519 batches past ed_lat_max on k_ed_keyed (GV_ED_KEYED=0: the throughput kernels)
   size_t ed_lat_max = 2048;      // keyed ed25519 batches up to this size take k_ed_lat_sl (one signature per block)
   size_t ed_unc_lat_max = 2048;  // uncached ed25519 host batches up to this size take k_ed_lat_unc (one signature per block)
@@ -678,7 +704,7 @@ namespace {
 
 EdGroupCfg ed_group_cfg(const gv_ctx* ctx) {
   return EdGroupCfg{ctx->ed_group, ctx->ed_group_min, ctx->ed_group_div, ctx->ed_group_cap, ctx->sort_keys,
-                    ctx->ed_keys_split};
+                    ctx->ed_keys_split, ctx->ed_btab16};
 }
 
 // Optional device tables (the G tables past the 64 MiB GLV pair, the key
@@ -1879,6 +1905,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* ek = getenv("GV_ED_KEYED")) ctx->ed_keyed = strcmp(ek, "0") != 0;
   if (const char* eg = getenv("GV_ED_GROUP")) ctx->ed_group = strcmp(eg, "0") != 0;
   if (const char* es = getenv("GV_ED_KEYS_SPLIT")) ctx->ed_keys_split = strcmp(es, "0") != 0;
+  if (const char* eb = getenv("GV_ED_BTAB16")) ctx->ed_btab16 = strcmp(eb, "0") != 0;
   if (const char* ls = getenv("GV_LAT_SLICED")) ctx->lat_sliced = strcmp(ls, "0") != 0;
   if (const char* lr = getenv("GV_LAT_ROWS_MAX")) ctx->lat_rows_max = (size_t)strtoull(lr, nullptr, 10);
   if (const char* zc = getenv("GV_LAT_ZC")) ctx->lat_zero_copy = strcmp(zc, "0") != 0;
@@ -2007,6 +2034,7 @@ void gv_close(gv_ctx* ctx) {
                         d->kzqw, d->kqtw2, d->kzqw2})
       if (p) (void)hipFree(p);
     if (d->edtab) (void)hipFree(d->edtab);
+    if (d->edtab16) (void)hipFree(d->edtab16);
     if (d->ed.d_in) (void)hipFree(d->ed.d_in);
     if (d->ed.atab) (void)hipFree(d->ed.atab);
     if (d->ed.bits) (void)hipFree(d->ed.bits);
@@ -2538,6 +2566,7 @@ int ed_keyed_slice(gv_ctx* ctx, Dev* d, size_t lo, size_t hi, const EdKeyedHost&
     b.kok = d->ekok;
     b.kcount = (uint32_t)kcount;
     b.btab = d->edtab;
+    b.btab16 = ed_btab16(d, ctx->ed_btab16, st);
     b.out8 = dd + o_out;
     CK(gvk_ed_keyed(&b, st));
     CK(hipMemcpyAsync(h + o_out, dd + o_out, cn, hipMemcpyDeviceToHost, st));
@@ -2797,6 +2826,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "group_div")) {
     if (val < 2 || val > 1024) return GV_EINVAL;
     ctx->group_div = (int)val;
+  } else if (!strcmp(key, "ed_btab16")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->ed_btab16 = val != 0;
   } else if (!strcmp(key, "ed_keys_split")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->ed_keys_split = val != 0;

@@ -272,6 +272,10 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * table adds for [h](-A), no doublings, lanes in slot order; 0 = the
  * throughput kernels over the slots' raw keys; same verdicts; default 1, env
  * GV_ED_KEYED),
+ * "ed_btab16" (0/1: k_ed_keyed -- cached keys past "ed_lat_max" and grouped
+ * keys -- adds [s]B from a radix-2^16 comb table of B, j * 65536^w * B for
+ * w < 16 and j <= 2^15 (56.6 MB per device, built on first use): 16
+ * additions instead of 32; same verdicts; default 1, env GV_ED_BTAB16),
  * "sort_keys" (0/1: keyed throughput batches on the 4-group ladder -- cached
  * slots, grouped keys -- run their lanes in slot order: a counting sort by
  * slot, the signature rows read in that order, the accept bits gathered back

@@ -166,7 +166,8 @@ def test_small_batch_latency(ver):
 
 def test_large_keyed_batches_schedules_agree(ver):
     """Past ed_lat_max the cached-key throughput kernel (k_ed_keyed, lanes in
-    slot order) must give the throughput kernels' verdicts: goldens tiled and
+    slot order, [s]B from either comb table) must give the throughput kernels'
+    verdicts: goldens tiled and
     shuffled (every rejection class, keys that FromBytes rejects included),
     never-loaded slots interleaved, both lane orders."""
     gv = golden()
@@ -180,13 +181,17 @@ def test_large_keyed_batches_schedules_agree(ver):
     sg, msgs = sigs([s for *_, s, _ in items]), [m for _, _, m, _, _ in items]
     runs = {}
     try:
-        for keyed, srt in ((1, 1), (1, 0), (0, 1)):
+        # (ed_keyed, sort_keys, ed_btab16): [s]B from the radix-2^16 table
+        # (16 additions, the default) and from the radix-256 one (32)
+        for keyed, srt, b16 in ((1, 1, 1), (1, 0, 1), (1, 1, 0), (0, 1, 1)):
             ver.set_option("ed_keyed", keyed)
             ver.set_option("sort_keys", srt)
-            runs[(keyed, srt)] = ver.verify_batch_ed25519_keyed(slots, sg, msgs)
+            ver.set_option("ed_btab16", b16)
+            runs[(keyed, srt, b16)] = ver.verify_batch_ed25519_keyed(slots, sg, msgs)
     finally:
         ver.set_option("ed_keyed", 1)
         ver.set_option("sort_keys", 1)
+        ver.set_option("ed_btab16", 1)
     for k, got in runs.items():
         bad = np.nonzero(got.astype(bool) != exp)[0]
         assert bad.size == 0, (k, [(items[i][0], bool(exp[i])) for i in bad[:10]])
