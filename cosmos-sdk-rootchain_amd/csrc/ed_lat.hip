@@ -91,6 +91,18 @@ GV_DEV void ext_load(ge_ext& a, const u32* p) {
 #pragma unroll
   for (int i = 0; i < 9; ++i) { a.X.n[i] = p[i]; a.Y.n[i] = p[9 + i]; a.Z.n[i] = p[18 + i]; a.T.n[i] = p[27 + i]; }
 }
+// RB: the comb's radix bits -- 4 (the key arena's tables, 64 windows of 8
+// entries, read by k_ed_lat_sl too) or 6 (the grouped route's per-batch
+// tables: 43 windows of 32 entries, 43 additions per [h](-A) instead of 64).
+template <int RB>
+struct EdComb {
+  static constexpr int NW = RB == 4 ? 64 : 43;              // windows over h < 2^253
+  static constexpr int NE = 1 << (RB - 1);                  // entries j = 1..NE per window
+  static constexpr size_t WORDS = (size_t)NW * NE * ED_CACHED_WORDS;
+};
+static_assert(EdComb<4>::WORDS == GV_EDK_WORDS && EdComb<6>::WORDS == GV_EDK64_WORDS, "comb table sizes");
+
+template <int RB>
 __global__ __launch_bounds__(64) void k_ed_keys_chain(const uint8_t* pub32, uint32_t n, uint32_t base, uint32_t* kpub,
                                                       uint32_t* kok, uint32_t* wbase) {
   const uint32_t g = blockIdx.x * 64 + threadIdx.x;
@@ -106,34 +118,36 @@ __global__ __launch_bounds__(64) void k_ed_keys_chain(const uint8_t* pub32, uint
   const bool ok = ge_frombytes(a, pw);
   kok[base + g] = ok ? 1u : 0u;
   ge_neg(P, a);
-  u32* wb = wbase + (size_t)g * 64 * ED_CACHED_WORDS;
+  using L = EdComb<RB>;
+  u32* wb = wbase + (size_t)g * L::NW * ED_CACHED_WORDS;
 #pragma unroll 1
-  for (int w = 0; w < 64; ++w) {
+  for (int w = 0; w < L::NW; ++w) {
     if (w) {
-      ge_dbl_t<false>(P, P);
-      ge_dbl_t<false>(P, P);
-      ge_dbl_t<false>(P, P);
+#pragma unroll 1
+      for (int k = 0; k < RB - 1; ++k) ge_dbl_t<false>(P, P);
       ge_dbl_t<true>(P, P);
     }
     ext_store(wb + (size_t)w * ED_CACHED_WORDS, P);
   }
 }
+template <int RB>
 __global__ __launch_bounds__(256) void k_ed_keys_tab(uint32_t n, uint32_t base, uint32_t* ktab, const uint32_t* wbase) {
+  using L = EdComb<RB>;
   const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= n * 64u) return;
-  const uint32_t g = t >> 6, w = t & 63u;
+  if (t >= n * (uint32_t)L::NW) return;
+  const uint32_t g = t / (uint32_t)L::NW, w = t % (uint32_t)L::NW;
   ge_ext P;
   ext_load(P, wbase + (size_t)t * ED_CACHED_WORDS);
-  u32* tab = ktab + (size_t)(base + g) * GV_EDK_WORDS;
+  u32* tab = ktab + (size_t)(base + g) * L::WORDS;
   ge_cached c1, c;
   ge_to_cached(c1, P);
-  atab_store(tab + (size_t)(w * 8) * ED_CACHED_WORDS, 1, 0, c1);
+  atab_store(tab + (size_t)(w * L::NE) * ED_CACHED_WORDS, 1, 0, c1);
   ge_ext acc = P;
 #pragma unroll 1
-  for (int j = 2; j <= 8; ++j) {
+  for (int j = 2; j <= L::NE; ++j) {
     ge_add_cached(acc, acc, c1, false);
     ge_to_cached(c, acc);
-    atab_store(tab + (size_t)(w * 8 + j - 1) * ED_CACHED_WORDS, 1, 0, c);
+    atab_store(tab + (size_t)(w * L::NE + j - 1) * ED_CACHED_WORDS, 1, 0, c);
   }
 }
 
@@ -673,7 +687,9 @@ __global__ __launch_bounds__(256) void k_ed_lat_unc(const gvk_edl b) {
 // ed_ladder_check.  Lanes run in slot order (perm from gv_sort.hip's counting
 // sort): a validator set's commits name their keys in the same order every
 // block, so item order would put 64 different 73 KB tables under one wave.
+template <int RB>
 __global__ __launch_bounds__(256) void k_ed_keyed(const gvk_edk b) {
+  using L = EdComb<RB>;
   const uint32_t g = blockIdx.x * 256 + threadIdx.x;
   if (g >= b.n) return;
   const uint32_t it = b.perm ? b.perm[g] : g;
@@ -698,20 +714,22 @@ __global__ __launch_bounds__(256) void k_ed_keyed(const gvk_edk b) {
   sha512_pre64(dig, pre, [=](u32 i) { return (u32)m[i]; }, b.msg_len[it]);
   sc_reduce512(h, dig);                     // ScReduce
   ok = ok && (sw[15] >> 29) == 0 && sc_minimal(sw + 8);   // sig[63] & 224 == 0, ScMinimal
-  // [h](-A) = sum_w digit_w * 16^w (-A): one cached-table add per nonzero digit
-  const uint64_t car = sc_radix16_carries(h);
-  const u32* kt = b.ktab + (size_t)sl * GV_EDK_WORDS;
+  // [h](-A) = sum_w digit_w * 2^(RB w) (-A): one cached-table add per nonzero
+  // signed digit in [-2^(RB-1), 2^(RB-1)), LSB-first (no doublings: any order)
+  const u32* kt = b.ktab + (size_t)sl * L::WORDS;
   ge_ext acc;
   ge_identity(acc);
+  int cin = 0;
 #pragma unroll 1
-  for (int w = 0; w < 64; ++w) {
-    const int nib = (int)((h[w >> 3] >> (4 * (w & 7))) & 15u);
-    const int cin = w > 0 ? (int)((car >> (w - 1)) & 1u) : 0;
-    const int cout = w < 63 ? (int)((car >> w) & 1u) : 0;
-    const int dg = nib + cin - 16 * cout;
+  for (int w = 0; w < L::NW; ++w) {
+    const int pos = RB * w, wi = pos >> 5;
+    const uint64_t pair = (uint64_t)h[wi] | (wi < 7 ? (uint64_t)h[wi + 1] << 32 : 0ull);
+    int dg = (int)((pair >> (pos & 31)) & (uint64_t)((1u << RB) - 1u)) + cin;
+    cin = 0;
+    if (w < L::NW - 1 && dg >= L::NE) { dg -= 1 << RB; cin = 1; }   // h < 2^253: no carry out of the top window
     if (dg != 0) {
       const int mag = dg < 0 ? -dg : dg;
-      ge_add_tab<true>(acc, acc, kt + (size_t)(w * 8 + mag - 1) * ED_CACHED_WORDS, 1, 0, dg < 0);
+      ge_add_tab<true>(acc, acc, kt + (size_t)(w * L::NE + mag - 1) * ED_CACHED_WORDS, 1, 0, dg < 0);
     }
   }
   // + [s]B: 16 signed radix-2^16 digits from btab16, or (null) 32 radix-256
@@ -832,16 +850,24 @@ extern "C" hipError_t gvk_ed_pack_bits(uint32_t n, const uint8_t* out8, uint64_t
 
 extern "C" hipError_t gvk_ed_keyed(const gvk_edk* b, hipStream_t st) {
   if (b->n == 0) return hipSuccess;
-  hipLaunchKernelGGL(gv::ed::k_ed_keyed, dim3((b->n + 255) / 256), dim3(256), 0, st, *b);
+  if (b->rb == 6) hipLaunchKernelGGL(gv::ed::k_ed_keyed<6>, dim3((b->n + 255) / 256), dim3(256), 0, st, *b);
+  else hipLaunchKernelGGL(gv::ed::k_ed_keyed<4>, dim3((b->n + 255) / 256), dim3(256), 0, st, *b);
   return hipGetLastError();
 }
 
 extern "C" hipError_t gvk_ed_keys(const uint8_t* pub32, uint32_t n, uint32_t base, uint32_t* ktab, uint32_t* kpub,
-                                  uint32_t* kok, uint32_t* wbase, hipStream_t st) {
+                                  uint32_t* kok, uint32_t* wbase, int rb, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (wbase) {                              // chain + table launches (scratch: n * 64 * 36 words)
-    hipLaunchKernelGGL(gv::ed::k_ed_keys_chain, dim3((n + 63) / 64), dim3(64), 0, st, pub32, n, base, kpub, kok, wbase);
-    hipLaunchKernelGGL(gv::ed::k_ed_keys_tab, dim3((n * 64 + 255) / 256), dim3(256), 0, st, n, base, ktab,
+  if (rb == 6 && !wbase) return hipErrorInvalidValue;     // the radix-64 tables: the split build only
+  if (wbase && rb == 6) {                   // chain + table launches (scratch: n * 64 * 36 words)
+    hipLaunchKernelGGL(gv::ed::k_ed_keys_chain<6>, dim3((n + 63) / 64), dim3(64), 0, st, pub32, n, base, kpub, kok,
+                       wbase);
+    hipLaunchKernelGGL(gv::ed::k_ed_keys_tab<6>, dim3((n * gv::ed::EdComb<6>::NW + 255) / 256), dim3(256), 0, st, n,
+                       base, ktab, (const uint32_t*)wbase);
+  } else if (wbase) {
+    hipLaunchKernelGGL(gv::ed::k_ed_keys_chain<4>, dim3((n + 63) / 64), dim3(64), 0, st, pub32, n, base, kpub, kok,
+                       wbase);
+    hipLaunchKernelGGL(gv::ed::k_ed_keys_tab<4>, dim3((n * 64 + 255) / 256), dim3(256), 0, st, n, base, ktab,
                        (const uint32_t*)wbase);
   } else {
     hipLaunchKernelGGL(gv::ed::k_ed_keys, dim3((n + 63) / 64), dim3(64), 0, st, pub32, n, base, ktab, kpub, kok);

@@ -252,6 +252,8 @@ hipError_t gvk_ed_verify(const gvk_ed* b, hipStream_t st);
 // j * 16^w * (-A), w < 64, j = 1..8, cached form (36 words each), the raw key
 // words (8) and the FromBytes verdict.
 #define GV_EDK_WORDS (64 * 8 * 36)
+// The grouped route's radix-64 comb tables: 43 windows of 32 entries per key.
+#define GV_EDK64_WORDS (43 * 32 * 36)
 typedef struct gvk_edl {
   uint32_t n;
   const uint32_t* slot;         // n key slots
@@ -269,9 +271,10 @@ typedef struct gvk_edl {
 } gvk_edl;
 // wbase (may be null: one lane per key does everything): n * 64 * 36 words of
 // scratch for the window bases -- the chain and the table adds then run as
-// two launches (k_ed_keys_chain, k_ed_keys_tab), same table words.
+// two launches (k_ed_keys_chain, k_ed_keys_tab), same table words.  rb: the
+// comb radix bits, 4 (GV_EDK_WORDS per key) or 6 (GV_EDK64_WORDS; needs wbase).
 hipError_t gvk_ed_keys(const uint8_t* pub32, uint32_t n, uint32_t base, uint32_t* ktab, uint32_t* kpub, uint32_t* kok,
-                       uint32_t* wbase, hipStream_t st);
+                       uint32_t* wbase, int rb, hipStream_t st);
 hipError_t gvk_ed_lat(const gvk_edl* b, hipStream_t st);
 // Small ed25519 batches against uncached keys (k_ed_lat_unc): b->pub32 per item.
 hipError_t gvk_ed_lat_unc(const gvk_edl* b, hipStream_t st);
@@ -291,6 +294,7 @@ typedef struct gvk_edk {
   uint32_t kcount;
   const uint32_t* btab;
   const uint32_t* btab16;       // GV_ED_BTAB16_WORDS, or null: [s]B from btab (32 additions instead of 16)
+  int rb;                       // ktab's comb radix bits: 4 (GV_EDK_WORDS per key; 0 = 4) or 6 (GV_EDK64_WORDS)
   uint8_t* out8;                // n verdict bytes (device)
 } gvk_edk;
 hipError_t gvk_ed_keyed(const gvk_edk* b, hipStream_t st);

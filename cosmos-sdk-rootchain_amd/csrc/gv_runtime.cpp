@@ -193,6 +193,7 @@ struct Dev {
   // ed25519 in-batch key grouping: per-batch key arena (comb tables of -A), pinned count, stats
   uint32_t *edg_ktab = nullptr, *edg_kpub = nullptr, *edg_kok = nullptr;
   size_t edg_cap = 0;
+  size_t edg_words = 0;                           // table words per key of edg_ktab (the comb radix in use)
   uint32_t* ed_h_count = nullptr;
   uint64_t ed_grouped_batches = 0, ed_grouped_keys = 0;
   // large keyed ed25519 batches, two buffers (chunk i on set[i % 2]'s stream):
@@ -469,6 +470,7 @@ struct EdGroupCfg {
   bool sorted;
   bool split_keys;   // k_ed_keys_chain + k_ed_keys_tab (the table adds off the serial chain)
   bool btab16;       // k_ed_keyed takes [s]B from the radix-2^16 table
+  bool r64;          // the per-batch key tables are radix-64 combs (43 windows of 32 entries)
 };
 
 // The radix-2^16 comb table of B, built on the device on first use (56.6 MB);
@@ -492,13 +494,14 @@ const uint32_t* ed_btab16(Dev* d, bool on, hipStream_t st) {
   return d->edtab16;
 }
 
-int ensure_edg(Dev* d, size_t need) {
-  if (need <= d->edg_cap) return GV_OK;
+int ensure_edg(Dev* d, size_t need, size_t words) {
+  if (need <= d->edg_cap && words == d->edg_words) return GV_OK;
   for (uint32_t** q : {&d->edg_ktab, &d->edg_kpub, &d->edg_kok})
     if (*q) { (void)hipFree(*q); *q = nullptr; }
   d->edg_cap = 0;
+  d->edg_words = words;
   const size_t cap = round_up(std::max<size_t>(need, 1024), 1024);
-  if (hipMalloc(&d->edg_ktab, cap * (size_t)GV_EDK_WORDS * 4) != hipSuccess ||
+  if (hipMalloc(&d->edg_ktab, cap * words * 4) != hipSuccess ||
       hipMalloc(&d->edg_kpub, cap * 8 * 4) != hipSuccess || hipMalloc(&d->edg_kok, cap * 4) != hipSuccess)
     return GV_ENOMEM;
   d->edg_cap = cap;
@@ -540,11 +543,14 @@ int ed_grouped(Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig, const u
   CK(hipStreamSynchronize(st));
   const size_t U = *d->ed_h_count;
   if (U == 0 || U > capU || U * (size_t)gc.div > n) return GV_OK;
-  int rc = ensure_edg(d, U);
-  if (rc) return rc == GV_ENOMEM ? GV_OK : rc;
   uint32_t* wb = o8 + round_up(C / 4, 64);        // window-base scratch of the split key build
   if (!gc.split_keys || (size_t)(wb + U * 64 * 36 - q) > C * (size_t)GV_ED_ROWS) wb = nullptr;
-  CK(gvk_ed_keys(kpub32, (uint32_t)U, 0u, d->edg_ktab, d->edg_kpub, d->edg_kok, wb, st));
+  // radix-64 comb tables (43 additions per [h](-A) instead of 64) on the
+  // split build; the one-lane build writes the radix-16 ones
+  const int rb = gc.r64 && wb ? 6 : 4;
+  int rc = ensure_edg(d, U, rb == 6 ? (size_t)GV_EDK64_WORDS : (size_t)GV_EDK_WORDS);
+  if (rc) return rc == GV_ENOMEM ? GV_OK : rc;
+  CK(gvk_ed_keys(kpub32, (uint32_t)U, 0u, d->edg_ktab, d->edg_kpub, d->edg_kok, wb, rb, st));
   if (gc.sorted) CK(gvk_sort_slots(&so, (uint32_t)n, slot, (uint32_t)U, st));
   gvk_edk b;
   memset(&b, 0, sizeof b);
@@ -561,6 +567,7 @@ int ed_grouped(Dev* d, size_t n, const uint8_t* pub, const uint8_t* sig, const u
   b.kcount = (uint32_t)U;
   b.btab = d->edtab;
   b.btab16 = ed_btab16(d, gc.btab16, st);
+  b.rb = rb;
   b.out8 = (uint8_t*)o8;
   CK(gvk_ed_keyed(&b, st));
   CK(gvk_ed_pack_bits((uint32_t)n, (const uint8_t*)o8, bits, st));
@@ -695,6 +702,7 @@ struct gv_ctx {
   size_t ed_group_cap = 16384;   // ... and at most this many (72 KB of comb table per key)
   bool ed_keys_split = true;     // ed25519 key tables: serial chain and table adds in two launches (GV_ED_KEYS_SPLIT=0: A/B)
   bool ed_btab16 = true;         // k_ed_keyed's [s]B from the radix-2^16 table: 16 additions instead of 32 (GV_ED_BTAB16)
+  bool ed_group_r64 = true;      // grouped ed25519 key tables as radix-64 combs: 43 [h](-A) additions, not 64 (GV_ED_GROUP_R64)
   bool ed_keyed = true;          // keyed ed25519 batches past ed_lat_max on k_ed_keyed (GV_ED_KEYED=0: the throughput kernels)
   size_t ed_lat_max = 2048;      // keyed ed25519 batches up to this size take k_ed_lat_sl (one signature per block)
   size_t ed_unc_lat_max = 2048;  // uncached ed25519 host batches up to this size take k_ed_lat_unc (one signature per block)
@@ -704,7 +712,7 @@ namespace {
 
 EdGroupCfg ed_group_cfg(const gv_ctx* ctx) {
   return EdGroupCfg{ctx->ed_group, ctx->ed_group_min, ctx->ed_group_div, ctx->ed_group_cap, ctx->sort_keys,
-                    ctx->ed_keys_split, ctx->ed_btab16};
+                    ctx->ed_keys_split, ctx->ed_btab16, ctx->ed_group_r64};
 }
 
 // Optional device tables (the G tables past the 64 MiB GLV pair, the key
@@ -1906,6 +1914,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* eg = getenv("GV_ED_GROUP")) ctx->ed_group = strcmp(eg, "0") != 0;
   if (const char* es = getenv("GV_ED_KEYS_SPLIT")) ctx->ed_keys_split = strcmp(es, "0") != 0;
   if (const char* eb = getenv("GV_ED_BTAB16")) ctx->ed_btab16 = strcmp(eb, "0") != 0;
+  if (const char* er = getenv("GV_ED_GROUP_R64")) ctx->ed_group_r64 = strcmp(er, "0") != 0;
   if (const char* ls = getenv("GV_LAT_SLICED")) ctx->lat_sliced = strcmp(ls, "0") != 0;
   if (const char* lr = getenv("GV_LAT_ROWS_MAX")) ctx->lat_rows_max = (size_t)strtoull(lr, nullptr, 10);
   if (const char* zc = getenv("GV_LAT_ZC")) ctx->lat_zero_copy = strcmp(zc, "0") != 0;
@@ -2450,7 +2459,7 @@ int gv_ed_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub32, uint32_t* slot_
     if (hipMalloc(&dp, o_wb + (split ? wb_bytes : 0)) != hipSuccess) return GV_ENOMEM;
     if (hipMemcpyAsync(dp, pub32, n * 32, hipMemcpyHostToDevice, st) != hipSuccess ||
         gvk_ed_keys(dp, (uint32_t)n, (uint32_t)base, d->ektab, d->ekpub, d->ekok,
-                    split ? (uint32_t*)(dp + o_wb) : nullptr, st) != hipSuccess ||
+                    split ? (uint32_t*)(dp + o_wb) : nullptr, 4, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess) {
       (void)hipFree(dp);
       return GV_EHIP;
@@ -2829,6 +2838,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "ed_btab16")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->ed_btab16 = val != 0;
+  } else if (!strcmp(key, "ed_group_r64")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->ed_group_r64 = val != 0;
   } else if (!strcmp(key, "ed_keys_split")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->ed_keys_split = val != 0;

@@ -272,6 +272,9 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * table adds for [h](-A), no doublings, lanes in slot order; 0 = the
  * throughput kernels over the slots' raw keys; same verdicts; default 1, env
  * GV_ED_KEYED),
+ * "ed_group_r64" (0/1: the grouped route's per-batch ed25519 key tables are
+ * radix-64 combs -- 43 windows of 32 entries, 43 additions per [h](-A)
+ * instead of 64; same verdicts; default 1, env GV_ED_GROUP_R64),
  * "ed_btab16" (0/1: k_ed_keyed -- cached keys past "ed_lat_max" and grouped
  * keys -- adds [s]B from a radix-2^16 comb table of B, j * 65536^w * B for
  * w < 16 and j <= 2^15 (56.6 MB per device, built on first use): 16

@@ -181,7 +181,8 @@ def test_in_batch_key_grouping_matches_throughput_kernels(ver):
     (k_ed_keys) and verifies on k_ed_keyed; every golden vector (keys that
     FromBytes rejects, small-order keys, S >= L, non-canonical R ...) tiled
     and shuffled with random OpenSSL items must give the throughput kernels'
-    verdicts, host and device-resident, both lane orders."""
+    verdicts, host and device-resident, both lane orders, radix-64 and
+    radix-16 key combs."""
     gv = golden()
     rng = random.Random(0x6E)
     seeds = [rng.randbytes(32) for _ in range(24)]
@@ -206,9 +207,12 @@ def test_in_batch_key_grouping_matches_throughput_kernels(ver):
     ver.set_option("ed_group_min", 4096)
     try:
         runs = {}
-        for grp, srt in ((1, 1), (1, 0), (0, 1)):
+        # (ed_group, sort_keys, ed_group_r64): radix-64 grouped key tables (the
+        # default) and radix-16 ones
+        for grp, srt, r64 in ((1, 1, 1), (1, 0, 1), (1, 1, 0), (0, 1, 1)):
             ver.set_option("ed_group", grp)
             ver.set_option("sort_keys", srt)
+            ver.set_option("ed_group_r64", r64)
             b0, _ = ver.group_stats()
             host = ver.verify_batch_ed25519(pub, sig, (blob, off, ln))
             d = [ver.dev_alloc(a.nbytes) for a in (pub, sig, blob, off, ln)]
@@ -222,10 +226,11 @@ def test_in_batch_key_grouping_matches_throughput_kernels(ver):
             for ptr in d + [d_bits]:
                 ver.dev_free(ptr)
             dev = np.unpackbits(bits.view(np.uint8), bitorder="little")[:n].astype(bool)
-            runs[(grp, srt)] = (host.astype(bool), dev, ver.group_stats()[0] - b0)
+            runs[(grp, srt, r64)] = (host.astype(bool), dev, ver.group_stats()[0] - b0)
     finally:
         ver.set_option("ed_group", 1)
         ver.set_option("sort_keys", 1)
+        ver.set_option("ed_group_r64", 1)
         ver.set_option("ed_group_min", 196608)
     for k, (host, dev, grouped) in runs.items():
         assert grouped == (2 if k[0] else 0), (k, grouped)
