@@ -2378,11 +2378,12 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
       }
       bool ok = ensure_keys_wide(d, base + n, base, st, ctx->key_cap, ctx->hbm_budget, ctx->keys_wide1_cap);
       if (!ok && d->kw_ng == GV_KW_NG1) {
+        // (a failed read-back only stops the wide tables: the k6 ones serve)
         std::vector<uint8_t> old_pub;
-        if (base && (rc = read_back_pub33(ctx, d, st, base, old_pub))) return rc;
+        const bool back = !base || read_back_pub33(ctx, d, st, base, old_pub) == GV_OK;
         free_keys_wide(d);
         d->kw_ng = GV_KW_NG2;
-        ok = ensure_keys_wide(d, base + n, 0, st, ctx->key_cap, ctx->hbm_budget);
+        ok = back && ensure_keys_wide(d, base + n, 0, st, ctx->key_cap, ctx->hbm_budget);
         if (ok && base && (rc = build_wide(ctx, d, s, st, old_pub.data(), base, 0))) return rc;
       }
       if (!ok) {
