@@ -12,7 +12,9 @@ so the million-scale mix covers every acceptance and rejection rule.
 
 Every chunk runs the throughput schedule (the headline path); one more 1M
 chunk runs through the limb-sliced small-batch kernels (k_verify_lat_sl and
-k_verify_lat_sl4 by pub33, k_verify_lat16_sl keyed) with the small-batch bounds lifted.  The GPU
+k_verify_lat_sl4 by pub33, k_verify_lat16_sl keyed) with the small-batch
+bounds lifted, and through the resident key arena's throughput ladders (its
+one-window wide tables and its k6 tables) with every key of the chunk loaded.  The GPU
 bitmaps are compared in full with the verdicts known by construction, and
 all special cases plus a random 20k sample per chunk with the C oracle.  A
 JSON summary goes to GV_PARITY_OUT when set.  GV_PARITY_MILLIONS=0 skips.
@@ -85,13 +87,31 @@ def test_parity_millions():
                 slots = ver.keys_load(np.ascontiguousarray(uniq))[inv.reshape(-1)]
                 gk = ver.verify_batch_digests_keyed(np.ascontiguousarray(slots, np.uint32), sig, dig)
                 ver.keys_reset()
+                ver.reset_schedule()
+                # the resident arena's throughput ladders on the same 1M items
+                # (the node's default route): the one-window wide tables (kw)
+                # and the k6 tables (kn), every key of the chunk loaded
+                arena = {}
+                try:
+                    for wide, route in ((2, "kw"), (0, "kn")):
+                        ver.set_option("keys_wide", wide)
+                        sl = ver.keys_load(np.ascontiguousarray(uniq))[inv.reshape(-1)]
+                        r0 = ver.route_stats()
+                        arena[route] = ver.verify_batch_digests_keyed(np.ascontiguousarray(sl, np.uint32), sig, dig)
+                        assert ver.route_stats()[route] > r0[route], route
+                        ver.keys_reset()
+                finally:
+                    ver.set_option("keys_wide", 2)
                 m1, o1, checked = check_chunk(ver, O, rng, pub, sig, dig, exp, pos, threads, got)
                 m2, o2, _ = check_chunk(ver, O, rng, pub, sig, dig, exp, pos, threads, gk)
                 m3, o3, _ = check_chunk(ver, O, rng, pub, sig, dig, exp, pos, threads, gr)
-                rec.update({"schedule": "sliced pub33 (lat_sl, lat_sl4) + sliced keyed", "mismatch": m1 + m2 + m3,
-                            "oracle_mismatch": o1 + o2 + o3, "mismatch_pub33": m1, "mismatch_keyed": m2,
-                            "mismatch_pub33_rows": m3})
-                n_items = 3 * n
+                m4, o4, _ = check_chunk(ver, O, rng, pub, sig, dig, exp, pos, threads, arena["kw"])
+                m5, o5, _ = check_chunk(ver, O, rng, pub, sig, dig, exp, pos, threads, arena["kn"])
+                rec.update({"schedule": "sliced pub33 (lat_sl, lat_sl4) + sliced keyed + arena kw / kn",
+                            "mismatch": m1 + m2 + m3 + m4 + m5, "oracle_mismatch": o1 + o2 + o3 + o4 + o5,
+                            "mismatch_pub33": m1, "mismatch_keyed": m2, "mismatch_pub33_rows": m3,
+                            "mismatch_arena_kw": m4, "mismatch_arena_kn": m5})
+                n_items = 5 * n
             summary["chunks"].append(rec)
             summary["items"] += n if not sliced else n_items
             summary["mismatch_vs_construction"] += rec["mismatch"]
