@@ -355,10 +355,27 @@ GV_DEV uint64_t sc_radix16_carries(const u32 h[8]) {
   return k;
 }
 
+// acc += [s]B from the radix-2^16 table: signed digits, LSB-first, digit w in
+// (-2^15, 2^15] (a digit above 2^15 borrows 2^16 and carries one into the
+// next window; s < 2^253 leaves no carry out of window 15).
+GV_DEV void ed_add_sb16(ge_ext& acc, const u32 s[8], const u32* btab16) {
+  int carry = 0;
+#pragma unroll 1
+  for (int w = 0; w < ED_BTAB16_WINDOWS; ++w) {
+    int dgt = (int)((s[w >> 1] >> (16 * (w & 1))) & 0xFFFFu) + carry;
+    carry = dgt > 32768 ? 1 : 0;
+    dgt -= 65536 * carry;
+    const int mag = dgt < 0 ? -dgt : dgt;
+    ge_add_pretab(acc, acc, btab16 + (size_t)(w * ED_BTAB16_ENTRIES + mag) * ED_PRE_WORDS, dgt < 0);
+  }
+}
+
 // R' = [h](-A) + [s]B and compare its encoding with rw (sig[:32] words).
-// tab/stride: this lane's j(-A) table (already built); btab: the comb table.
+// tab/stride: this lane's j(-A) table (already built); btab: the comb table;
+// btab16 (may be null): the radix-2^16 comb table, then [s]B takes 16
+// additions from it instead of 32 from btab.
 GV_DEV bool ed_ladder_check(const u32 h[8], const u32 s[8], const u32* tab, size_t stride, const u32* btab,
-                            const u32 rw[8]) {
+                            const u32 rw[8], const u32* btab16 = nullptr) {
   // [h](-A): MSB-first, 4 doublings then one table add per digit
   uint64_t carries = sc_radix16_carries(h);
   u32 hs[8];
@@ -386,19 +403,24 @@ GV_DEV bool ed_ladder_check(const u32 h[8], const u32 s[8], const u32* tab, size
     else ge_add_tab<true>(acc, acc, tab, stride, mag, dgt < 0);      // the comb adds follow
   }
   // + [s]B: signed radix-256 digits, LSB-first, one precomputed add each
-  u32 ss[8];
+  // (or 16 radix-2^16 digits from btab16)
+  if (btab16) {
+    ed_add_sb16(acc, s, btab16);
+  } else {
+    u32 ss[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) ss[i] = s[i];
-  int carry = 0;
-  for (int w = 0; w < ED_BTAB_WINDOWS; ++w) {
-    int dgt = (int)(ss[0] & 0xFFu) + carry;
+    for (int i = 0; i < 8; ++i) ss[i] = s[i];
+    int carry = 0;
+    for (int w = 0; w < ED_BTAB_WINDOWS; ++w) {
+      int dgt = (int)(ss[0] & 0xFFu) + carry;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) ss[k] = (ss[k] >> 8) | (ss[k + 1] << 24);
-    ss[7] >>= 8;
-    carry = dgt > 128 ? 1 : 0;
-    dgt -= 256 * carry;
-    const int mag = dgt < 0 ? -dgt : dgt;
-    ge_add_pretab(acc, acc, btab + (size_t)(w * ED_BTAB_ENTRIES + mag) * ED_PRE_WORDS, dgt < 0);
+      for (int k = 0; k < 7; ++k) ss[k] = (ss[k] >> 8) | (ss[k + 1] << 24);
+      ss[7] >>= 8;
+      carry = dgt > 128 ? 1 : 0;
+      dgt -= 256 * carry;
+      const int mag = dgt < 0 ? -dgt : dgt;
+      ge_add_pretab(acc, acc, btab + (size_t)(w * ED_BTAB_ENTRIES + mag) * ED_PRE_WORDS, dgt < 0);
+    }
   }
   u32 ew[8];
   ge_tobytes(ew, acc);
@@ -466,20 +488,6 @@ GV_DEV void ed_btab16_entry(u32 out[ED_PRE_WORDS], int w, int j) {
   }
 }
 
-// acc += [s]B from the radix-2^16 table: signed digits, LSB-first, digit w in
-// (-2^15, 2^15] (a digit above 2^15 borrows 2^16 and carries one into the
-// next window; s < 2^253 leaves no carry out of window 15).
-GV_DEV void ed_add_sb16(ge_ext& acc, const u32 s[8], const u32* btab16) {
-  int carry = 0;
-#pragma unroll 1
-  for (int w = 0; w < ED_BTAB16_WINDOWS; ++w) {
-    int dgt = (int)((s[w >> 1] >> (16 * (w & 1))) & 0xFFFFu) + carry;
-    carry = dgt > 32768 ? 1 : 0;
-    dgt -= 65536 * carry;
-    const int mag = dgt < 0 ? -dgt : dgt;
-    ge_add_pretab(acc, acc, btab16 + (size_t)(w * ED_BTAB16_ENTRIES + mag) * ED_PRE_WORDS, dgt < 0);
-  }
-}
 
 // The per-item work before the ladder: h = SHA-512(R || A || M) mod L, the
 // S checks (sig[63] & 224 == 0, ScMinimal), FromBytes(A) and the table

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       sw[4 * k] = v.x; sw[4 * k + 1] = v.y; sw[4 * k + 2] = v.z; sw[4 * k + 3] = v.w;
     }
     const bool pre_ok = hrow[(size_t)8 * b.C] != 0;
-    ok = ed_ladder_check(h, sw + 8, tab, 1, b.btab, sw) && pre_ok;
+    ok = ed_ladder_check(h, sw + 8, tab, 1, b.btab, sw, b.btab16) && pre_ok;
   }
   const uint64_t mask = __ballot(ok);
   if ((threadIdx.x & 63) == 0 && g < b.n) b.bits[g >> 6] = mask;   // words up to ceil(n / 64) only

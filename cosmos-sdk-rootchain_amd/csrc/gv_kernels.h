@@ -241,6 +241,7 @@ typedef struct gvk_ed {
   const uint32_t* msg_len;
   uint32_t* atab;               // scratch: C x GV_ED_ATAB_WORDS lane-major table, then h (8) + verdict SoA rows
   const uint32_t* btab;         // GV_ED_BTAB_WORDS
+  const uint32_t* btab16;       // GV_ED_BTAB16_WORDS or null ([s]B in 16 additions instead of 32)
   uint64_t* bits;               // C/64 words
 } gvk_ed;
 hipError_t gvk_ed_btab(uint32_t* btab, hipStream_t st);

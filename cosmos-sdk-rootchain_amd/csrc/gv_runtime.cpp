@@ -591,6 +591,7 @@ int ed_launch(bool timed, Dev* d, size_t n, const uint8_t* pub, const uint8_t* s
   b.msg_blob = blob; b.msg_off = off; b.msg_len = len;
   b.atab = d->ed.atab;
   b.btab = d->edtab;
+  b.btab16 = ed_btab16(d, gc.btab16, st);
   b.bits = bits;
   hipEvent_t* rs = nullptr;
   if (timed) {                                    // stages: (none) x 3 | the ed25519 kernel

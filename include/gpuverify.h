@@ -276,7 +276,7 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * radix-64 combs -- 43 windows of 32 entries, 43 additions per [h](-A)
  * instead of 64; same verdicts; default 1, env GV_ED_GROUP_R64),
  * "ed_btab16" (0/1: k_ed_keyed -- cached keys past "ed_lat_max" and grouped
- * keys -- adds [s]B from a radix-2^16 comb table of B, j * 65536^w * B for
+ * keys -- and the per-item throughput kernels add [s]B from a radix-2^16 comb table of B, j * 65536^w * B for
  * w < 16 and j <= 2^15 (56.6 MB per device, built on first use): 16
  * additions instead of 32; same verdicts; default 1, env GV_ED_BTAB16),
  * "sort_keys" (0/1: keyed throughput batches on the 4-group ladder -- cached
