@@ -13,6 +13,7 @@ rocprofv3 -L > "$ROOT/$OUT/counters_list.txt" 2>&1 || true
 BENCH=("$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-latency --no-extras --items "$N")
 if [ "${MODE:-secp}" = ed ]; then BENCH=("$ROOT/tools/ed_probe.py" "$N" 16); fi   # ed25519 kernels
 if [ "${MODE:-secp}" = item ]; then BENCH+=(--keys "$N"); fi                           # per-item route: every key distinct
+if [ "${MODE:-secp}" = kw ]; then BENCH=("$ROOT/tools/kw_pmc_probe.py"); fi          # the resident arena's wide-window ladder
 if [ "${MODE:-secp}" = lat ]; then BENCH=("$ROOT/tools/lat_pmc_probe.py"); fi        # sliced small-batch kernels
 pass() {
   local name=$1; shift
