@@ -170,7 +170,10 @@ static_assert(GV_K6_QW * GV_K6_QWIN >= 130 && GV_K6_GW * GV_K6_GWIN >= 257, "k6 
 #endif
 #define GV_KW_NT (1 << (GV_KW_QW - 1))                    // 256 table entries per group
 #define GV_KW_QWIN ((130 + GV_KW_QW - 1) / GV_KW_QW)      // 15 windows per GLV half
-#define GV_KW_KEY_WORDS (GV_KW_NT * GV_QENT_WORDS)       // one group table (20,480 B)
+#ifndef GV_KW_ENT_WORDS
+#define GV_KW_ENT_WORDS GV_QENT_WORDS                     // entry stride (80 B; an A/B build may pad to 32 = 128 B)
+#endif
+#define GV_KW_KEY_WORDS (GV_KW_NT * GV_KW_ENT_WORDS)     // one group table (20,480 B)
 #define GV_KW_NG1 GV_KW_QWIN                              // one window per group: 15 groups
 #define GV_KW_NG2 ((GV_KW_QWIN + 1) / 2)                  // two windows per group (the last one): 8 groups
 static_assert(GV_KW_QW >= 7 && GV_KW_QW <= 9 && GV_KW_NG1 <= 19, "wide arena layout");

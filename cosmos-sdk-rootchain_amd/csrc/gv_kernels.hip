@@ -323,18 +323,19 @@ GV_DEV void load_qent(fe& x, fe& y, const u32* qt, u32 g, u32 j) {
 // limbs: x[9], y[9], 2 pad words = 80 bytes, five 16-byte accesses per lane;
 // no word conversion on either side.  G-table entries stay 8 x 32 words.
 // NT: entries per table row (GV_QTAB_N; GV_K6_NT for the k6 group tables).
-template <int NT = GV_QTAB_N>
+// EW: words per entry (GV_QENT_WORDS; the wide arena may pad to a cache line).
+template <int NT = GV_QTAB_N, int EW = GV_QENT_WORDS>
 GV_DEV void store_qent29(u32* qt, u32 g, int j, const fe29& x, const fe29& y) {
-  uint4* p = (uint4*)(qt + ((size_t)g * NT + j) * GV_QENT_WORDS);
+  uint4* p = (uint4*)(qt + ((size_t)g * NT + j) * EW);
   p[0] = make_uint4(x.n[0], x.n[1], x.n[2], x.n[3]);
   p[1] = make_uint4(x.n[4], x.n[5], x.n[6], x.n[7]);
   p[2] = make_uint4(x.n[8], y.n[0], y.n[1], y.n[2]);
   p[3] = make_uint4(y.n[3], y.n[4], y.n[5], y.n[6]);
   p[4] = make_uint4(y.n[7], y.n[8], 0u, 0u);
 }
-template <int NT = GV_QTAB_N>
+template <int NT = GV_QTAB_N, int EW = GV_QENT_WORDS>
 GV_DEV void load_qent29(fe29& x, fe29& y, const u32* qt, u32 g, u32 j) {
-  const uint4* p = (const uint4*)(qt + ((size_t)g * NT + j) * GV_QENT_WORDS);
+  const uint4* p = (const uint4*)(qt + ((size_t)g * NT + j) * EW);
   const uint4 a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
   x.n[0] = a.x; x.n[1] = a.y; x.n[2] = a.z; x.n[3] = a.w;
   x.n[4] = b.x; x.n[5] = b.y; x.n[6] = b.z; x.n[7] = b.w;
@@ -761,6 +762,7 @@ template <int QW, int NG>
 struct KLayout {
   static constexpr int QWIN = QW == GV_QW ? GV_QWIN : QW == GV_KW_QW ? GV_KW_QWIN : GV_K6_QWIN;
   static constexpr int NT = 1 << (QW - 1);                  // table entries per group
+  static constexpr int EW = QW == GV_KW_QW ? GV_KW_ENT_WORDS : GV_QENT_WORDS;   // words per entry
   static constexpr int P = (QWIN + NG - 1) / NG;            // ladder positions
   static constexpr int R = QWIN - (P - 1) * NG;             // groups with P windows
   static constexpr int nw(int k) { return k < R ? P : P - 1; }
@@ -813,7 +815,7 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_chain(u32 n, u32 C, 
   }
   kok[base + g] = ok ? 1u : 0u;
   auto park = [](u32* tab, u32 row, const u32* xw, const u32* yw) {
-    u32* p = tab + (size_t)row * L::NT * GV_QENT_WORDS;
+    u32* p = tab + (size_t)row * L::NT * L::EW;
 #pragma unroll
     for (int i = 0; i < 8; ++i) { p[i] = xw[i]; p[8 + i] = yw[i]; }
   };
@@ -1005,7 +1007,7 @@ GV_DEV void keys_put(u32* qe, u32 CL, u32 L, u32* tab, u32 row, int e, const fe2
       qe[((size_t)e * 18 + 9 + i) * CL + L] = y.n[i];
     }
   } else {
-    store_qent29<KLayout<QW, NG>::NT>(tab, row, e, x, y);
+    store_qent29<KLayout<QW, NG>::NT, KLayout<QW, NG>::EW>(tab, row, e, x, y);
   }
 }
 template <int QW, int NG>
@@ -1017,7 +1019,7 @@ GV_DEV void keys_get(const u32* qe, u32 CL, u32 L, const u32* tab, u32 row, int 
       y.n[i] = qe[((size_t)e * 18 + 9 + i) * CL + L];
     }
   } else {
-    load_qent29<KLayout<QW, NG>::NT>(x, y, tab, row, (u32)e);
+    load_qent29<KLayout<QW, NG>::NT, KLayout<QW, NG>::EW>(x, y, tab, row, (u32)e);
   }
 }
 
@@ -1032,7 +1034,7 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_fwd(u32 n, u32 CL, u
   const u32 row = grp == 0u ? base + key : (base + key) * (NG - 1) + (grp - 1u);
   fe29 qx, qy, X1, Y1, X2, Y2, t, u, prod;
   {
-    const u32* p = tab + (size_t)row * NT * GV_QENT_WORDS;
+    const u32* p = tab + (size_t)row * NT * KLayout<QW, NG>::EW;
     u32 w[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = p[i];
@@ -1138,7 +1140,7 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_back(u32 n, u32 CL, 
     keys_get<QW, NG>(qe, CL, L, tab, row, m - 1, x, y);
     f29x_mul(x, x, a2);
     f29x_mul(y, y, a3);
-    store_qent29<NT>(tab, row, m - 1, x, y);
+    store_qent29<NT, KLayout<QW, NG>::EW>(tab, row, m - 1, x, y);
   }
   store_f29(zrow, kC, base + key, zc);
 }
@@ -1691,7 +1693,7 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_kn(const u32* gta
       if (d == 0) continue;
       const u32 e = (u32)((d < 0 ? -d : d) - 1);
       fe29 x, y;
-      if (!isg) load_qent29<L::NT>(x, y, tab, row, e);
+      if (!isg) load_qent29<L::NT, L::EW>(x, y, tab, row, e);
       else load_gent29(x, y, tab, e);
       if (d < 0) f29_neg<1>(y, y);                         // 2
       add_entry(acc, inf, x, y, isg ? &zq : nullptr);
