@@ -1641,8 +1641,15 @@ __constant__ const int kKnNW[4][19] = {
 #undef GV_KN_ROW
 static_assert(GV_KN_ARENA_NG <= 16 && GV_KW_NG1 <= 19, "layout table rows");
 
+// GV_KN_WAVES: the same bound for k_ecmult_kn alone (A/B: its gathers from the
+// resident arena's large tables wait longer than k_ecmult_k4's)
+#ifndef GV_KN_WAVES
+#define GV_KN_ATTR GV_ECMULT_ATTR
+#else
+#define GV_KN_ATTR __attribute__((amdgpu_waves_per_eu(GV_KN_WAVES)))
+#endif
 template <int QW, int NG>
-__global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_kn(const u32* gtab6, u32 n, u32 C, const u32* digits,
+__global__ __launch_bounds__(256) GV_KN_ATTR void k_ecmult_kn(const u32* gtab6, u32 n, u32 C, const u32* digits,
                                                         const u32* kqt, const u32* kqt2, const u32* kzq,
                                                         const u32* flags, const u32* in_r, uint64_t* bits,
                                                         const u32* qidx, u32 kC) {
