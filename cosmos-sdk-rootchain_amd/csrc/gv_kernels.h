@@ -161,7 +161,7 @@ static_assert(GV_K6_QW * GV_K6_QWIN >= 130 && GV_K6_GW * GV_K6_GWIN >= 257, "k6 
 // (default): 256 entries, 15 windows, 30 Q additions; 15 groups and no
 // doublings, or 8 groups and 9 doublings (k6 arena: 6 doublings and 44
 // additions; QW 8: 8 and 34; QW 7: 7 and 38 with two windows per group).  G as on the k6 ladders (11 24-bit windows after the last
-// doubling, gtab6).  15 (8) x 20 KiB of tables per key, built at gv_keys_load
+// doubling, gtab6).  15 (8) x 16 KiB of tables per key, built at gv_keys_load
 // beside the k6 tables while the key set fits (kn on the k6 tables otherwise).
 // A/B on one box (profiles/r05/kw/): c2_key_cache QW 7 / 8 / 9 = 329-344 /
 // 366 / 380-381M/s, k6 arena 312-317M/s.
@@ -170,10 +170,13 @@ static_assert(GV_K6_QW * GV_K6_QWIN >= 130 && GV_K6_GW * GV_K6_GWIN >= 257, "k6 
 #endif
 #define GV_KW_NT (1 << (GV_KW_QW - 1))                    // 256 table entries per group
 #define GV_KW_QWIN ((130 + GV_KW_QW - 1) / GV_KW_QW)      // 15 windows per GLV half
+// Entry format: 16 = canonical words x[8] y[8] (64 B: a gather never
+// straddles two cache lines, and 20 % less memory than the 80-B raw-limb
+// entries, 20; 32 pads those to a line -- A/B builds).
 #ifndef GV_KW_ENT_WORDS
-#define GV_KW_ENT_WORDS GV_QENT_WORDS                     // entry stride (80 B; an A/B build may pad to 32 = 128 B)
+#define GV_KW_ENT_WORDS 16
 #endif
-#define GV_KW_KEY_WORDS (GV_KW_NT * GV_KW_ENT_WORDS)     // one group table (20,480 B)
+#define GV_KW_KEY_WORDS (GV_KW_NT * GV_KW_ENT_WORDS)     // one group table (16,384 B)
 #define GV_KW_NG1 GV_KW_QWIN                              // one window per group: 15 groups
 #define GV_KW_NG2 ((GV_KW_QWIN + 1) / 2)                  // two windows per group (the last one): 8 groups
 static_assert(GV_KW_QW >= 7 && GV_KW_QW <= 9 && GV_KW_NG1 <= 19, "wide arena layout");

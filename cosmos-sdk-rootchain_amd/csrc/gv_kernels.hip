@@ -324,9 +324,21 @@ GV_DEV void load_qent(fe& x, fe& y, const u32* qt, u32 g, u32 j) {
 // no word conversion on either side.  G-table entries stay 8 x 32 words.
 // NT: entries per table row (GV_QTAB_N; GV_K6_NT for the k6 group tables).
 // EW: words per entry (GV_QENT_WORDS; the wide arena may pad to a cache line).
+// EW == 16: the entry as canonical words x[8] y[8] (64 B, one half line),
+// converted on both sides.
 template <int NT = GV_QTAB_N, int EW = GV_QENT_WORDS>
 GV_DEV void store_qent29(u32* qt, u32 g, int j, const fe29& x, const fe29& y) {
   uint4* p = (uint4*)(qt + ((size_t)g * NT + j) * EW);
+  if constexpr (EW == 16) {
+    u32 xw[8], yw[8];
+    f29_to_words(xw, x);
+    f29_to_words(yw, y);
+    p[0] = make_uint4(xw[0], xw[1], xw[2], xw[3]);
+    p[1] = make_uint4(xw[4], xw[5], xw[6], xw[7]);
+    p[2] = make_uint4(yw[0], yw[1], yw[2], yw[3]);
+    p[3] = make_uint4(yw[4], yw[5], yw[6], yw[7]);
+    return;
+  }
   p[0] = make_uint4(x.n[0], x.n[1], x.n[2], x.n[3]);
   p[1] = make_uint4(x.n[4], x.n[5], x.n[6], x.n[7]);
   p[2] = make_uint4(x.n[8], y.n[0], y.n[1], y.n[2]);
@@ -336,6 +348,14 @@ GV_DEV void store_qent29(u32* qt, u32 g, int j, const fe29& x, const fe29& y) {
 template <int NT = GV_QTAB_N, int EW = GV_QENT_WORDS>
 GV_DEV void load_qent29(fe29& x, fe29& y, const u32* qt, u32 g, u32 j) {
   const uint4* p = (const uint4*)(qt + ((size_t)g * NT + j) * EW);
+  if constexpr (EW == 16) {
+    const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+    const u32 xw[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const u32 yw[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+    f29_from_words(x, xw);
+    f29_from_words(y, yw);
+    return;
+  }
   const uint4 a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
   x.n[0] = a.x; x.n[1] = a.y; x.n[2] = a.z; x.n[3] = a.w;
   x.n[4] = b.x; x.n[5] = b.y; x.n[6] = b.z; x.n[7] = b.w;

@@ -307,8 +307,8 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * default 1, env GV_KEYS_K6; route counter GV_ROUTE_KN),
  * "keys_wide" (0/1/2: gv_keys_load also builds each key's 9-bit-window
  * tables of 256 entries on one Z -- 2 (default): one window per group, 15
- * tables (300 KB per key), no doublings and 30 Q additions per verify; 1: two
- * windows per group, 8 tables (160 KB), 9 doublings -- in an arena of their
+ * tables (240 KB per key), no doublings and 30 Q additions per verify; 1: two
+ * windows per group, 8 tables (128 KB), 9 doublings -- in an arena of their
  * own that grows by doubling while the HBM budget holds it and the device
  * keeps room for the k4 / k6 arena to reach key_cap; with 2, an arena that no
  * longer fits moves to the two-window layout (the loaded keys are read back
