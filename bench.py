@@ -50,14 +50,18 @@ FM, FS, NM = 72, 44, 136
 DBL, MADD, LIFT, BETA, FINISH = 3 * FM + 4 * FS, 8 * FM + 3 * FS, FM, FM, 2 * FM + FS
 
 
-def w_ladder(ndbl: int, nq: int, ng: int, qw: int, nbeta: float | None = None) -> float:
+def w_ladder(ndbl: int, nq: int, ng: int, qw: int, nbeta: float | None = None, gframe: bool = False) -> float:
     """Expected products of one ladder: ndbl doublings, nq Q-type additions (half
     of them lambda-Q; a qw-bit Booth digit is zero with probability 2 /
     2^(qw+1)), ng lifted G additions, the final check.  Beta products: one per
     lambda-Q addition, or nbeta (the k4 ladders' lambda frame, GV_LAMFRAME:
-    two per ladder position)."""
+    two per ladder position).  gframe (k_ecmult_kn, GV_KN_GFRAME, round 6): the
+    accumulator moves onto the real curve once before the G additions (1M), so
+    they take no lift and the final check no Z zq product."""
     q = nq * (1 - 2.0 / 2 ** (qw + 1))
     nb = q / 2 if nbeta is None else nbeta
+    if gframe:
+        return ndbl * DBL + (q - 1) * MADD + nb * BETA + FM + ng * MADD + FINISH - FM
     return ndbl * DBL + (q - 1) * MADD + nb * BETA + ng * (MADD + LIFT) + FINISH
 
 
@@ -93,29 +97,50 @@ W_MUL = sum(W_KERNEL.values())
 # three parked group Zs 1M each) and the items run the keyed pipeline.
 
 
-def w_keybuild(nt: int, last_offset: int) -> float:
-    grp = (1 + (nt - 2) * 6 + 6 + (nt - 1) * 3 + (nt - 2)) * FM + (5 + (nt - 2) * 2 + 1 + (nt - 1)) * FS
-    return W_DECOMP + last_offset * DBL + 4 * grp + 3 * FM
+def w_keybuild(nt: int, last_offset: int, ng: int = 4) -> float:
+    # per group: rho over the other ng - 1 groups' E and the common Z (ng - 1 products; 3 for the quad)
+    grp = (1 + (nt - 2) * 6 + (ng + 2) + (nt - 1) * 3 + (nt - 2)) * FM + (5 + (nt - 2) * 2 + 1 + (nt - 1)) * FS
+    return W_DECOMP + last_offset * DBL + ng * grp + (ng - 1) * FM
 
 
 W_KEYBUILD_K4 = w_keybuild(16, 100)        # 4 groups of 16 entries, offsets 0/35/70/100
 W_KEYBUILD_K6 = w_keybuild(32, 102)        # 4 groups of 32 entries, offsets 0/36/72/102
+
+
+def kg_layout(ng: int) -> tuple[int, int]:
+    """(ladder positions P, last group's bit offset) of the kg layout KLayout<5, ng>
+    (gv_kernels.hip): 26 five-bit windows, the first R groups with P windows."""
+    p = -(-26 // ng)
+    r = 26 - (p - 1) * ng
+    k = ng - 1
+    return p, 5 * (k * p - (k - r if k > r else 0))
+
+
+def w_keybuild_kg(ng: int) -> float:
+    return w_keybuild(16, kg_layout(ng)[1], ng)
+
+
+def w_ladder_kg(ng: int) -> float:
+    """k_ecmult_kn<5, ng>: 5 (P - 1) doublings, 52 Q additions (2 beta products per position), 11 G
+    additions after the last doubling on the real curve"""
+    p = kg_layout(ng)[0]
+    return w_ladder(5 * (p - 1), 52, 11, 5, nbeta=2 * p, gframe=True)
 W_PREP_KEYED = W_SCALAR
 W_PREP_KEYED_F = 2 * NM + (2 * 64 + 68)   # k4f: u2's GLV split only (u1 is recoded unsplit)
 # k_ecmult_k4: 30 doublings, 52 Q (26 lambda, on the lambda frame: 2 beta products at each of 7 positions), 14 G additions
 W_LADDER_K4 = w_ladder(30, 52, 14, 5, nbeta=14)
 # k_ecmult_k6: 30 doublings, 44 Q (22 lambda, on the lambda frame: 2 beta products at each of 6 positions),
 # 11 G additions (G on the unsplit u1, 24-bit windows)
-W_LADDER_K6 = w_ladder(30, 44, 11, 6, nbeta=12)
+W_LADDER_K6 = w_ladder(30, 44, 11, 6, nbeta=12, gframe=True)
 # k_ecmult_kn<11> (the resident arena's k6 tables, option keys_k6): 11 groups of two 6-bit windows, 2 positions:
 # 6 doublings, 44 Q (22 lambda, 2 beta products per position), 11 G additions
-W_LADDER_KN = w_ladder(6, 44, 11, 6, nbeta=4)
+W_LADDER_KN = w_ladder(6, 44, 11, 6, nbeta=4, gframe=True)
 # k_ecmult_kn<9, 15> (the resident arena's wide-window tables, option keys_wide 2): 15 groups of one 9-bit window,
 # one position: no doublings, 30 Q (15 lambda, 2 beta products), 11 G additions
-W_LADDER_KW = w_ladder(0, 30, 11, 9, nbeta=2)
+W_LADDER_KW = w_ladder(0, 30, 11, 9, nbeta=2, gframe=True)
 # k_ecmult_kn<9, 8> (keys_wide 1, or an arena past the one-window layout's room): 8 groups of two 9-bit windows
 # (7 of two, one of one), 2 positions: 9 doublings, 30 Q (2 beta products per position), 11 G additions
-W_LADDER_KW2 = w_ladder(9, 30, 11, 9, nbeta=4)
+W_LADDER_KW2 = w_ladder(9, 30, 11, 9, nbeta=4, gframe=True)
 W_LADDER_K4F = w_ladder(30, 52, 11, 5, nbeta=14)   # k_ecmult_k4<true>: G on the unsplit u1, 11 25-bit windows
 # Peak: the highest v_mad_u64_u32 issue rate measured on MI355X
 # (tools/microbench/alu_rate.hip; profiles/r01/alu_rate_v3.jsonl, dependent
@@ -505,15 +530,17 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
     u_keys = (gk - grp0[1]) / max(1, gb - grp0[0]) if grouped else 0.0
     routes1 = ver.route_stats() if hasattr(ver, "route_stats") else {}
     k6 = grouped and routes1.get("k6", 0) - routes0.get("k6", 0) >= calib
+    kg = ver.get_option("kg") if grouped and routes1.get("kg", 0) - routes0.get("kg", 0) >= calib else 0
     k4f = grouped and routes1.get("k4f", 0) - routes0.get("k4f", 0) >= calib
     itemf = not grouped and routes1.get("item_f", 0) - routes0.get("item_f", 0) >= calib
     if grouped:
         # the key tables (k_keys_chain, k_keys_tables) run on a side stream
         # beside k_scalar_inv: that stage's time covers both
-        lad = "k_ecmult_k6" if k6 else "k_ecmult_k4"
-        wkb = W_KEYBUILD_K6 if k6 else W_KEYBUILD_K4
+        lad = f"k_ecmult_kn<5, {kg}>" if kg else "k_ecmult_k6" if k6 else "k_ecmult_k4"
+        wkb = w_keybuild_kg(kg) if kg else W_KEYBUILD_K6 if k6 else W_KEYBUILD_K4
         w = {"k_unpack+k_dedupe": 0.0, "k_scalar_inv|k_keys_chain+k_keys_tables": W_INV + wkb * u_keys / n,
-             "k_prep<keyed>": W_PREP_KEYED_F if (k4f or k6) else W_PREP_KEYED, lad: W_LADDER_K6 if k6 else W_LADDER_K4F if k4f else W_LADDER_K4}
+             "k_prep<keyed>": W_PREP_KEYED_F if (k4f or k6 or kg) else W_PREP_KEYED,
+             lad: w_ladder_kg(kg) if kg else W_LADDER_K6 if k6 else W_LADDER_K4F if k4f else W_LADDER_K4}
         kms = dict(zip(w, (unpack_ms, inv_ms, prep_ms, ecmult_ms)))
         ladder, w_route = lad, sum(w.values())
     else:
@@ -549,8 +576,11 @@ def main(argv=None, verifier_factory=None, workload_fn=None):
                    "items_per_gpu": n, "keys": args.keys, "adversarial_fraction": args.adversarial,
                    "global_batch": n * world, "parallelism": f"shard{world} (independent per-GPU shards, no collective)",
                    "route": ("in-batch key grouping: each distinct key parsed and tabulated once (k_dedupe, "
-                             "k_keys_chain + k_keys_tables), items on the keyed 30-doubling ladder "
-                             + ("k_ecmult_k6 (6-bit Q windows on 32-entry key tables, G on the unsplit "
+                             "k_keys_chain + k_keys_tables), items on the keyed "
+                             + (f"{5 * (kg_layout(kg)[0] - 1)}-doubling ladder k_ecmult_kn<5, {kg}> ({kg} groups of "
+                                "16-entry 5-bit tables, G after the last doubling from 11 24-bit windows on the real "
+                                "curve)" if kg else "30-doubling ladder ")
+                             + ("" if kg else "k_ecmult_k6 (6-bit Q windows on 32-entry key tables, G on the unsplit "
                                 "scalar: 11 24-bit windows)" if k6
                                 else "k_ecmult_k4 (G on the unsplit scalar: 11 25-bit windows)" if k4f
                                 else "k_ecmult_k4 (GLV G: 14 20-bit windows)")

@@ -82,9 +82,11 @@ typedef struct gvk_batch {
   // (GV_K6_GTAB_WORDS: the full-scalar 24-bit-window G tables); gtab4 unused
   const uint32_t* gtab6;
   int k6;
-  // kqw set (with k6 == GV_KW_NG1 or GV_KW_NG2): kqt / kqt2 / kzq are the
+  // kqw == 1 (with k6 == GV_KW_NG1 or GV_KW_NG2): kqt / kqt2 / kzq are the
   // resident arena's wide-window tables (GV_KW_NT entries per group) and the
-  // ladder is k_ecmult_kn<GV_KW_QW, k6>
+  // ladder is k_ecmult_kn<GV_KW_QW, k6>.  kqw == 2: the grouped route's
+  // 5-bit many-group tables (GV_QTAB_N entries, k6 groups, one of GV_KG_NGS):
+  // k_ecmult_kn<GV_QW, k6>
   int kqw;
   // k4 batches with gtabf set: the G half on the unsplit scalar (GV_GF_*),
   // k_prep<.., GF> digits and k_ecmult_k4<true> over gtabf (GV_GF_WORDS)
@@ -182,6 +184,18 @@ static_assert(GV_K6_QW * GV_K6_QWIN >= 130 && GV_K6_GW * GV_K6_GWIN >= 257, "k6 
 static_assert(GV_KW_QW >= 7 && GV_KW_QW <= 9 && GV_KW_NG1 <= 19, "wide arena layout");
 static_assert(GV_KW_QWIN + GV_K6_GWIN <= GV_DIGIT_ROWS, "wide-window digits fit the digit rows");
 static_assert(GV_KW_QW * GV_KW_QWIN >= 130, "wide windows cover the GLV halves");
+
+// The grouped route's many-group ladder (option "kg", k_ecmult_kn<GV_QW, NG>,
+// round 6): the in-batch key tables keep k4's 16-entry 5-bit windows (26 per
+// GLV half) but split them over NG groups instead of 4, so the ladder runs
+// ceil(26 / NG) positions -- NG = 7: 15 doublings instead of 30, NG = 9: 10 --
+// for NG x 16 table entries per key (k4: 64).  G as on the k6 ladders: 11
+// signed 24-bit windows of the unsplit u1 after the last doubling from gtab6,
+// on the real curve (one frame change, no per-entry lift).  NG must be one of
+// GV_KG_NGS (the instantiated layouts).
+#define GV_KG_NGS 6, 7, 9
+#define GV_KG_MAXNG 9
+static_assert(GV_QWIN + GV_K6_GWIN <= GV_DIGIT_ROWS, "kg digits fit the digit rows");
 
 // The k4 ladder's G half on the unsplit scalar (k_ecmult_k4<true>): u1 = e/s
 // is not GLV-split; its 11 signed 25-bit windows (window j at bit 25 j) are
@@ -348,6 +362,12 @@ size_t gvk_keys_scratch_words(uint32_t n, int ng, int nt, int with_qe);
 hipError_t gvk_keys_build_rows6(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx,
                                 uint32_t* scratch, int with_qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC,
                                 uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2, hipStream_t st);
+// kg key tables (ng groups of 16 entries, ng one of GV_KG_NGS) of n keys
+// already unpacked, slots 0..n-1.  kqt: n x GV_KEY_WORDS, kqt2: (ng - 1) n x
+// GV_KEY_WORDS, kzq2: (ng - 1) x 8 rows of stride kC.
+hipError_t gvk_keys_build_rows_kg(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx,
+                                  uint32_t* scratch, int with_qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC,
+                                  uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2, int ng, hipStream_t st);
 hipError_t gvk_verify_lat(const gvk_lat* b, hipStream_t st);
 hipError_t gvk_verify_lat16(const gvk_lat* b, hipStream_t st);
 hipError_t gvk_verify_lat_sl(const gvk_lat* b, hipStream_t st);

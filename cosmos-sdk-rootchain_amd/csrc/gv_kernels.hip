@@ -652,7 +652,9 @@ GV_DEV bool parse_pubkey(u32 pre, const fe& x, fe& y) {
 // GV_GF_W-bit windows, one int32 row each: digits[(GV_QWIN + j)*C + g]).
 // KW (with K6, GF): GV_KW_QW-bit Q windows (the resident arena's wide-window
 // tables), G as K6.
-template <bool KEYED, bool K6 = false, bool GF = false, bool KW = false>
+// KG (with K6, GF): GV_QW-bit Q windows (the grouped route's many-group
+// tables, option "kg"), G as K6.
+template <bool KEYED, bool K6 = false, bool GF = false, bool KW = false, bool KG = false>
 __global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u32* in_x, const u32* in_pfx,
                                                const u32* in_r, const u32* in_s, const u32* in_e,
                                                const u32* in_w, u32* digits, u32* qt, u32* zq_out,
@@ -729,7 +731,9 @@ __global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u
   // digits[(GV_QWIN + 2j + 1)*C + g] = dG2, j = 0..GV_GWIN-1.
   static_assert(GF || !K6, "the k6 ladder takes G on the unsplit scalar");
   static_assert(!KW || K6, "wide-window digits: the k6 ladder's G windows");
-  constexpr int QW = KW ? GV_KW_QW : K6 ? GV_K6_QW : GV_QW, QWIN = KW ? GV_KW_QWIN : K6 ? GV_K6_QWIN : GV_QWIN;
+  static_assert(!KG || (K6 && !KW), "kg digits: 5-bit Q windows, the k6 ladder's G windows");
+  constexpr int QW = KW ? GV_KW_QW : KG ? GV_QW : K6 ? GV_K6_QW : GV_QW;
+  constexpr int QWIN = KW ? GV_KW_QWIN : KG ? GV_QWIN : K6 ? GV_K6_QWIN : GV_QWIN;
   constexpr int GW = GV_GW, GWIN = GV_GWIN;
   constexpr int GFW = K6 ? GV_K6_GW : GV_GF_W, GFWIN = K6 ? GV_K6_GWIN : GV_GF_WIN;
 #pragma unroll
@@ -1343,12 +1347,14 @@ GV_DEV void add_entry(gej29& acc, bool& inf, const fe29& x, const fe29& y, const
 // Final check of a ladder: R = (X, Y, Z*zq) on the real curve; x(R) mod n ==
 // r, inversion-free (X == r Z^2, or (r + n) Z^2 when r < p - n); accept
 // bitmap by ballot.
+// framed: acc is already on the real curve (Z as is; zq unused).
 GV_DEV void ecmult_finish(const gej29& acc, bool inf, const fe29& zq, const u32* flags, const u32* in_r,
-                          uint64_t* bits, u32 n, u32 C, u32 g) {
+                          uint64_t* bits, u32 n, u32 C, u32 g, bool framed = false) {
   const u32 fl = flags[g];
   bool ok = (fl & 1u) && !inf;
   fe29 zr, zz, rf, t;
-  f29_mul(zr, acc.z, zq);
+  if (framed) zr = acc.z;
+  else f29_mul(zr, acc.z, zq);
   f29_sqr(zz, zr);
   u32 rw[8], X[8], tw[8];
 #pragma unroll
@@ -1638,28 +1644,45 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gta
     KLayout<QW, NG>::F(7), KLayout<QW, NG>::F(8), KLayout<QW, NG>::F(9), KLayout<QW, NG>::F(10), \
     KLayout<QW, NG>::F(11), KLayout<QW, NG>::F(12), KLayout<QW, NG>::F(13), KLayout<QW, NG>::F(14), \
     KLayout<QW, NG>::F(15), KLayout<QW, NG>::F(16), KLayout<QW, NG>::F(17), KLayout<QW, NG>::F(18)
-__constant__ const int kKnW0[4][19] = {
-    {KLayout<6, 4>::w0(0), KLayout<6, 4>::w0(1), KLayout<6, 4>::w0(2), KLayout<6, 4>::w0(3)},
-    {KLayout<6, GV_KN_ARENA_NG>::w0(0), KLayout<6, GV_KN_ARENA_NG>::w0(1), KLayout<6, GV_KN_ARENA_NG>::w0(2),
-     KLayout<6, GV_KN_ARENA_NG>::w0(3), KLayout<6, GV_KN_ARENA_NG>::w0(4), KLayout<6, GV_KN_ARENA_NG>::w0(5),
-     KLayout<6, GV_KN_ARENA_NG>::w0(6), KLayout<6, GV_KN_ARENA_NG>::w0(7), KLayout<6, GV_KN_ARENA_NG>::w0(8),
-     KLayout<6, GV_KN_ARENA_NG>::w0(9), KLayout<6, GV_KN_ARENA_NG>::w0(10), KLayout<6, GV_KN_ARENA_NG>::w0(11),
-     KLayout<6, GV_KN_ARENA_NG>::w0(12), KLayout<6, GV_KN_ARENA_NG>::w0(13), KLayout<6, GV_KN_ARENA_NG>::w0(14),
-     KLayout<6, GV_KN_ARENA_NG>::w0(15)},
+// rows 4.. : the grouped route's 5-bit many-group layouts (GV_KG_NGS)
+__constant__ const int kKnW0[7][19] = {
+    {GV_KN_ROW(6, 4, w0)},
+    {GV_KN_ROW(6, GV_KN_ARENA_NG, w0)},
     {GV_KN_ROW(GV_KW_QW, GV_KW_NG2, w0)},
-    {GV_KN_ROW(GV_KW_QW, GV_KW_NG1, w0)}};
-__constant__ const int kKnNW[4][19] = {
-    {KLayout<6, 4>::nw(0), KLayout<6, 4>::nw(1), KLayout<6, 4>::nw(2), KLayout<6, 4>::nw(3)},
-    {KLayout<6, GV_KN_ARENA_NG>::nw(0), KLayout<6, GV_KN_ARENA_NG>::nw(1), KLayout<6, GV_KN_ARENA_NG>::nw(2),
-     KLayout<6, GV_KN_ARENA_NG>::nw(3), KLayout<6, GV_KN_ARENA_NG>::nw(4), KLayout<6, GV_KN_ARENA_NG>::nw(5),
-     KLayout<6, GV_KN_ARENA_NG>::nw(6), KLayout<6, GV_KN_ARENA_NG>::nw(7), KLayout<6, GV_KN_ARENA_NG>::nw(8),
-     KLayout<6, GV_KN_ARENA_NG>::nw(9), KLayout<6, GV_KN_ARENA_NG>::nw(10), KLayout<6, GV_KN_ARENA_NG>::nw(11),
-     KLayout<6, GV_KN_ARENA_NG>::nw(12), KLayout<6, GV_KN_ARENA_NG>::nw(13), KLayout<6, GV_KN_ARENA_NG>::nw(14),
-     KLayout<6, GV_KN_ARENA_NG>::nw(15)},
+    {GV_KN_ROW(GV_KW_QW, GV_KW_NG1, w0)},
+    {GV_KN_ROW(GV_QW, 6, w0)},
+    {GV_KN_ROW(GV_QW, 7, w0)},
+    {GV_KN_ROW(GV_QW, 9, w0)}};
+__constant__ const int kKnNW[7][19] = {
+    {GV_KN_ROW(6, 4, nw)},
+    {GV_KN_ROW(6, GV_KN_ARENA_NG, nw)},
     {GV_KN_ROW(GV_KW_QW, GV_KW_NG2, nw)},
-    {GV_KN_ROW(GV_KW_QW, GV_KW_NG1, nw)}};
+    {GV_KN_ROW(GV_KW_QW, GV_KW_NG1, nw)},
+    {GV_KN_ROW(GV_QW, 6, nw)},
+    {GV_KN_ROW(GV_QW, 7, nw)},
+    {GV_KN_ROW(GV_QW, 9, nw)}};
 #undef GV_KN_ROW
 static_assert(GV_KN_ARENA_NG <= 16 && GV_KW_NG1 <= 19, "layout table rows");
+
+constexpr int kn_row(int qw, int ng) {
+  return qw == 6 && ng == 4                    ? 0
+         : qw == 6 && ng == GV_KN_ARENA_NG     ? 1
+         : qw == GV_KW_QW && ng == GV_KW_NG2   ? 2
+         : qw == GV_KW_QW && ng == GV_KW_NG1   ? 3
+         : qw == GV_QW && ng == 6              ? 4
+         : qw == GV_QW && ng == 7              ? 5
+         : qw == GV_QW && ng == 9              ? 6
+                                               : -1;
+}
+// GV_KN_GFRAME (default 1, round 6): after the last Q entry the accumulator
+// moves from the key tables' Z onto the real curve (Z <- Z zq, one product),
+// so the 11 G entries are added without the per-entry lift az = Z zq and the
+// final check skips its Z zq: 11 products fewer per verify.  The same point
+// and the same exceptional cases (the lift only rescaled the Jacobian
+// representative).  0: every G entry lifted (rounds 4-5).
+#ifndef GV_KN_GFRAME
+#define GV_KN_GFRAME 1
+#endif
 
 // GV_KN_WAVES: the same bound for k_ecmult_kn alone (A/B: its gathers from the
 // resident arena's large tables wait longer than k_ecmult_k4's)
@@ -1674,8 +1697,8 @@ __global__ __launch_bounds__(256) GV_KN_ATTR void k_ecmult_kn(const u32* gtab6, 
                                                         const u32* flags, const u32* in_r, uint64_t* bits,
                                                         const u32* qidx, u32 kC) {
   using L = KLayout<QW, NG>;
-  static_assert(QW == GV_KW_QW ? NG == GV_KW_NG1 || NG == GV_KW_NG2 : QW == GV_K6_QW && (NG == 4 || NG == GV_KN_ARENA_NG),
-                "a layout row of kKnW0 / kKnNW");
+  constexpr int T = kn_row(QW, NG);
+  static_assert(T >= 0, "a layout row of kKnW0 / kKnNW");
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   const u32 qi = qidx[g];
   fe29 zq;
@@ -1699,6 +1722,14 @@ __global__ __launch_bounds__(256) GV_KN_ATTR void k_ecmult_kn(const u32* gtab6, 
         f29x_mul(acc.x, acc.x, c);
       }
       if (slot >= 2 * NG && pos != 0) break;               // wave-uniform: G after the last doubling
+      if (GV_KN_GFRAME && slot == 2 * NG && !inf) {
+        // onto the real curve: acc (X, Y, Z) on the tables' Z is the point
+        // (X, Y, Z zq), so the G entries are added unlifted (az = Z) and the
+        // final check reads Z as is
+        fe29 z;
+        f29x_mul(z, acc.z, zq);
+        acc.z = z;
+      }
       int d;
       const u32* tab;
       u32 row = 0;
@@ -1706,7 +1737,6 @@ __global__ __launch_bounds__(256) GV_KN_ATTR void k_ecmult_kn(const u32* gtab6, 
       if (!isg) {
         const bool lam = slot >= NG;
         const int grp = lam ? 2 * NG - 1 - slot : slot;
-        constexpr int T = QW == GV_KW_QW ? (NG == GV_KW_NG1 ? 3 : 2) : NG == 4 ? 0 : 1;
         if (pos >= kKnNW[T][grp]) continue;                // wave-uniform
         const u32 dq = digits[(size_t)(kKnW0[T][grp] + pos) * C + g];
         d = lam ? ((int)dq >> 16) : ((int)(dq << 16) >> 16);
@@ -1723,10 +1753,11 @@ __global__ __launch_bounds__(256) GV_KN_ATTR void k_ecmult_kn(const u32* gtab6, 
       if (!isg) load_qent29<L::NT, L::EW>(x, y, tab, row, e);
       else load_gent29(x, y, tab, e);
       if (d < 0) f29_neg<1>(y, y);                         // 2
-      add_entry(acc, inf, x, y, isg ? &zq : nullptr);
+      add_entry(acc, inf, x, y, isg && !GV_KN_GFRAME ? &zq : nullptr);
     }
   }
-  ecmult_finish(acc, inf, zq, flags, in_r, bits, n, C, g);
+  // GV_KN_GFRAME: acc is on the real curve (or infinite: rejected either way)
+  ecmult_finish(acc, inf, zq, flags, in_r, bits, n, C, g, GV_KN_GFRAME != 0);
 }
 
 // ------------------------------------------------------------------- k_debug
@@ -1869,7 +1900,8 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   const dim3 blk(256), grd(C / 256);
   // key-ordered lanes (gv_sort.hip): keyed k4 batches with sort scratch
   const bool k6 = b->kslot && b->k6 && b->gtab6;
-  const bool kw = k6 && b->kqw && (b->k6 == GV_KW_NG1 || b->k6 == GV_KW_NG2);   // the arena's wide-window tables
+  const bool kw = k6 && b->kqw == 1 && (b->k6 == GV_KW_NG1 || b->k6 == GV_KW_NG2);   // the arena's wide-window tables
+  const bool kg = k6 && b->kqw == 2;             // the grouped route's 5-bit many-group tables
   const bool gf = b->kslot && b->gtab4 && b->gtabf && !k6;   // k_ecmult_k4<true>
   const bool gfp = !b->kslot && b->gtabf;                     // per-item pub33: k_ecmult<false, true>
   const bool sorted = b->kslot && (b->gtab4 || k6) && b->srt.perm;
@@ -1897,7 +1929,12 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
     hipLaunchKernelGGL(gv::k_scalar_inv, dim3((waves + 3) / 4), blk, 0, st, C, b->in_s, w, pre, M);
     if (b->keys_ready) (void)hipStreamWaitEvent(st, b->keys_ready, 0);   // grouped keys built beside s^-1
     if (b->ev[1]) (void)hipEventRecord(b->ev[1], st);
-    if (kw)
+    if (kg)
+      hipLaunchKernelGGL((gv::k_prep<true, true, true, false, true>), grd, blk, 0, st, C, b->n, (const uint32_t*)nullptr,
+                         (const uint32_t*)nullptr, b->in_r, b->in_s, b->in_e, (const uint32_t*)w, b->digits,
+                         (uint32_t*)nullptr, (uint32_t*)nullptr, b->flags, sorted ? b->srt.kslot : b->kslot,
+                         b->kok, b->kcount, b->in_pfx);
+    else if (kw)
       hipLaunchKernelGGL((gv::k_prep<true, true, true, true>), grd, blk, 0, st, C, b->n, (const uint32_t*)nullptr,
                          (const uint32_t*)nullptr, b->in_r, b->in_s, b->in_e, (const uint32_t*)w, b->digits,
                          (uint32_t*)nullptr, (uint32_t*)nullptr, b->flags, sorted ? b->srt.kslot : b->kslot,
@@ -1935,7 +1972,19 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
   }
   if (b->ev_ecm_start) (void)hipEventRecord(b->ev_ecm_start, se);
   if (b->bits_wait && !sorted) (void)hipStreamWaitEvent(se, b->bits_wait, 0);   // the ladder writes the bits
-  if (kw && b->k6 == GV_KW_NG1)
+#define GV_KG_LAUNCH(NG)                                                                                      \
+  hipLaunchKernelGGL((gv::k_ecmult_kn<GV_QW, NG>), grd, blk, 0, se, b->gtab6, b->n, C, b->digits, b->kqt, b->kqt2, \
+                     b->kzq, b->flags, b->in_r, sorted ? b->srt.bits : b->bits, (const uint32_t*)b->in_pfx, b->kC)
+  if (kg && b->k6 == 6)
+    GV_KG_LAUNCH(6);
+  else if (kg && b->k6 == 7)
+    GV_KG_LAUNCH(7);
+  else if (kg && b->k6 == 9)
+    GV_KG_LAUNCH(9);
+#undef GV_KG_LAUNCH
+  else if (kg)
+    return hipErrorInvalidValue;
+  else if (kw && b->k6 == GV_KW_NG1)
     hipLaunchKernelGGL((gv::k_ecmult_kn<GV_KW_QW, GV_KW_NG1>), grd, blk, 0, se, b->gtab6, b->n, C, b->digits,
                        b->kqt, b->kqt2, b->kzq, b->flags, b->in_r, sorted ? b->srt.bits : b->bits,
                        (const uint32_t*)b->in_pfx, b->kC);
@@ -2024,6 +2073,17 @@ hipError_t gvk_keys_build_rows6(uint32_t n, uint32_t C, const uint32_t* in_x, co
                                 uint32_t* scratch, int with_qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC,
                                 uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2, hipStream_t st) {
   return keys_tables_launch<GV_K6_QW, 4>(n, C, in_x, in_pfx, scratch, with_qe, 0u, kqt, kzq, kC, kok, kqt2, kzq2, st);
+}
+
+hipError_t gvk_keys_build_rows_kg(uint32_t n, uint32_t C, const uint32_t* in_x, const uint32_t* in_pfx,
+                                  uint32_t* scratch, int with_qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC,
+                                  uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2, int ng, hipStream_t st) {
+  switch (ng) {
+    case 6: return keys_tables_launch<GV_QW, 6>(n, C, in_x, in_pfx, scratch, with_qe, 0u, kqt, kzq, kC, kok, kqt2, kzq2, st);
+    case 7: return keys_tables_launch<GV_QW, 7>(n, C, in_x, in_pfx, scratch, with_qe, 0u, kqt, kzq, kC, kok, kqt2, kzq2, st);
+    case 9: return keys_tables_launch<GV_QW, 9>(n, C, in_x, in_pfx, scratch, with_qe, 0u, kqt, kzq, kC, kok, kqt2, kzq2, st);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t gvk_keys_build_wide(const uint8_t* pub33, uint32_t n, uint32_t C, uint32_t* in_x, uint32_t* in_pfx,

@@ -62,6 +62,15 @@ using gvstage::par_copy;
 using gvstage::par_copy_segs;
 using gvstage::run_sliced;
 
+// The grouped route's kg layouts (gv_kernels.h GV_KG_NGS), or 0 (off).
+bool kg_layout_ok(int ng) {
+  static const int kNGs[] = {GV_KG_NGS};
+  if (ng == 0) return true;
+  for (int v : kNGs)
+    if (v == ng) return true;
+  return false;
+}
+
 // ------------------------------------------------------------ device state
 // Device scratch of one batch chunk of C lanes (C % 256 == 0): the staged
 // inputs (one contiguous region so a host chunk is ONE H2D copy), the SoA
@@ -91,7 +100,7 @@ struct Set {
   // distinct keys, key-arena layout) for up to gcap keys, and the count
   uint32_t *g_kqt = nullptr, *g_kzq = nullptr, *g_kok = nullptr, *g_kqt2 = nullptr, *g_kzq2 = nullptr;
   size_t gcap = 0;
-  bool gk6 = false;                               // the arena's group tables are k6 (32 entries)
+  int g_ent = 0, g_ng = 0;                        // the arena's layout: words per group table, groups per key
   uint32_t* h_count = nullptr;                    // pinned: the distinct-key count read back
   // pinned host staging
   uint8_t* h_in = nullptr;
@@ -666,6 +675,9 @@ struct gv_ctx {
                                 // GLV windows (k_ecmult_k4<true>, 6 GiB of tables; GV_GFULL=0: A/B)
   bool k6 = false;              // grouped batches on k_ecmult_k6: 6-bit Q windows on 32-entry key tables, the lambda
                                 // frame, G on the unsplit u1 in 24-bit windows (GV_K6=1)
+  int kg = 0;                   // grouped batches on k_ecmult_kn<5, kg>: k4's 16-entry 5-bit tables over kg groups
+                                // (one of GV_KG_NGS; 0 = off), G after the last doubling from the 24-bit tables
+                                // (GV_KG, "kg"; takes precedence over k6)
   int keys_wide = 2;            // ... and wide-window tables while device memory holds them (GV_KEYS_WIDE): 2 = one
                                 // 9-bit window per group (15 groups of 256 entries, no doublings, 30 Q additions),
                                 // moving to two per group (8 groups, 9 doublings) when that no longer fits;
@@ -801,30 +813,32 @@ int ensure_gtab6(gv_ctx* ctx, Dev* d, Set* s, hipStream_t st, bool want, bool sy
 
 // The set's per-batch key arena for in-batch grouping (cap keys; k6: 32-entry
 // group tables), charged to the HBM budget like the other optional tables.
-size_t group_arena_bytes(size_t cap, bool k6) {
-  const size_t ent = (size_t)(k6 ? GV_K6_KEY_WORDS : GV_KEY_WORDS) * 4;
-  return cap * (ent * (1 + GV_KEY2_TABLES) + 8 * 4 * (1 + GV_KEY2_TABLES) + 4);
+// ent: words per group table (GV_KEY_WORDS: 16 entries; GV_K6_KEY_WORDS: 32),
+// ng: groups per key (4; the kg layouts GV_KG_NGS).
+size_t group_arena_bytes(size_t cap, int ent, int ng) {
+  return cap * ((size_t)ent * 4 * ng + 8 * 4 * ng + 4);
 }
-int ensure_group_arena(gv_ctx* ctx, Dev* d, Set* s, size_t cap, bool k6) {
-  if (cap <= s->gcap && k6 == s->gk6) return GV_OK;
+int ensure_group_arena(gv_ctx* ctx, Dev* d, Set* s, size_t cap, int ent, int ng) {
+  if (cap <= s->gcap && ent == s->g_ent && ng == s->g_ng) return GV_OK;
   for (uint32_t** p : {&s->g_kqt, &s->g_kzq, &s->g_kok, &s->g_kqt2, &s->g_kzq2})
     if (*p) { (void)hipFree(*p); *p = nullptr; }
-  d->opt_bytes -= std::min(d->opt_bytes, group_arena_bytes(s->gcap, s->gk6));
+  if (s->gcap) d->opt_bytes -= std::min(d->opt_bytes, group_arena_bytes(s->gcap, s->g_ent, s->g_ng));
   s->gcap = 0;
-  s->gk6 = k6;
-  const size_t ent = (size_t)(k6 ? GV_K6_KEY_WORDS : GV_KEY_WORDS) * 4;
-  if (d->opt_bytes + group_arena_bytes(cap, k6) > ctx->hbm_budget) return GV_ENOMEM;
-  if (hipMalloc(&s->g_kqt, cap * ent) != hipSuccess || hipMalloc(&s->g_kzq, cap * 8 * 4) != hipSuccess ||
+  s->g_ent = ent;
+  s->g_ng = ng;
+  const size_t eb = (size_t)ent * 4;
+  if (d->opt_bytes + group_arena_bytes(cap, ent, ng) > ctx->hbm_budget) return GV_ENOMEM;
+  if (hipMalloc(&s->g_kqt, cap * eb) != hipSuccess || hipMalloc(&s->g_kzq, cap * 8 * 4) != hipSuccess ||
       hipMalloc(&s->g_kok, cap * 4) != hipSuccess ||
-      hipMalloc(&s->g_kqt2, cap * GV_KEY2_TABLES * ent) != hipSuccess ||
-      hipMalloc(&s->g_kzq2, cap * GV_KEY2_TABLES * 8 * 4) != hipSuccess) {
+      hipMalloc(&s->g_kqt2, cap * (ng - 1) * eb) != hipSuccess ||
+      hipMalloc(&s->g_kzq2, cap * (ng - 1) * 8 * 4) != hipSuccess) {
     (void)hipGetLastError();
     for (uint32_t** p : {&s->g_kqt, &s->g_kzq, &s->g_kok, &s->g_kqt2, &s->g_kzq2})
       if (*p) { (void)hipFree(*p); *p = nullptr; }
     return GV_ENOMEM;
   }
   s->gcap = cap;
-  d->opt_bytes += group_arena_bytes(cap, k6);
+  d->opt_bytes += group_arena_bytes(cap, ent, ng);
   return GV_OK;
 }
 
@@ -850,6 +864,8 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   const size_t room = used < total ? total - used : 0;
   if (gvk_keys_scratch_words((uint32_t)capU, GV_LGRP, GV_QTAB_N, 0) > room) return GV_OK;   // no room: pub33
   const bool k6_room = gvk_keys_scratch_words((uint32_t)capU, 4, GV_K6_NT, 0) <= room;
+  const int kgng = ctx->kg;                     // 0 or one of GV_KG_NGS
+  const bool kg_room = kgng && gvk_keys_scratch_words((uint32_t)capU, kgng, GV_QTAB_N, 0) <= room;
   if (!s->h_count && hipHostMalloc((void**)&s->h_count, 64, hipHostMallocDefault) != hipSuccess) {
     s->h_count = nullptr;
     return GV_ENOMEM;
@@ -865,29 +881,40 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   CK(hipStreamSynchronize(st));
   const size_t U = *s->h_count;
   if (U == 0 || U * ctx->group_div > n || U > capU) return GV_OK;   // many distinct keys: the pub33 pipeline
-  if (ctx->k6 && k6_room && (rc = ensure_gtab6(ctx, d, s, st, true))) return rc;
-  bool k6 = ctx->k6 && k6_room && d->gtab6;
-  if (k6 && (rc = ensure_group_arena(ctx, d, s, capU, true))) {
+  // the layout: kg (5-bit windows over kgng groups) > k6 (6-bit, 4 groups) > k4,
+  // each needing gtab6 (kg, k6) and its arena within the HBM budget
+  if (((ctx->k6 && k6_room) || kg_room) && (rc = ensure_gtab6(ctx, d, s, st, true))) return rc;
+  bool kg = kg_room && d->gtab6;
+  if (kg && (rc = ensure_group_arena(ctx, d, s, capU, GV_KEY_WORDS, kgng))) {
+    if (rc != GV_ENOMEM) return rc;
+    kg = false;                                 // no room for kgng groups
+  }
+  bool k6 = !kg && ctx->k6 && k6_room && d->gtab6;
+  if (k6 && (rc = ensure_group_arena(ctx, d, s, capU, GV_K6_KEY_WORDS, GV_LGRP))) {
     if (rc != GV_ENOMEM) return rc;
     k6 = false;                                 // no room for the 32-entry tables: k4
   }
-  if (!k6 && (rc = ensure_gtab4(ctx, d, s, st))) return rc;
-  if (!k6 && (rc = ensure_group_arena(ctx, d, s, capU, false))) return rc == GV_ENOMEM ? GV_OK : rc;
+  if (!kg && !k6 && (rc = ensure_gtab4(ctx, d, s, st))) return rc;
+  if (!kg && !k6 && (rc = ensure_group_arena(ctx, d, s, capU, GV_KEY_WORDS, GV_LGRP)))
+    return rc == GV_ENOMEM ? GV_OK : rc;
   // the tables are built on the set's side stream while k_scalar_inv (which
   // does not read keys) runs on st: both are one wave per SIMD or so
   CK(hipEventRecord(s->fork, st));
   CK(hipStreamWaitEvent(s->side, s->fork, 0));
   // the forward pass's entries in coalesced scratch rows after the ratio and
   // E rows, when they fit (else through the tables themselves)
-  const int nt = k6 ? GV_K6_NT : GV_QTAB_N;
-  const int with_qe = ctx->keys_scratch && gvk_keys_scratch_words((uint32_t)U, 4, nt, 1) <= room ? 1 : 0;
-  if (k6)
+  const int nt = k6 ? GV_K6_NT : GV_QTAB_N, ng = kg ? kgng : GV_LGRP;
+  const int with_qe = ctx->keys_scratch && gvk_keys_scratch_words((uint32_t)U, ng, nt, 1) <= room ? 1 : 0;
+  if (kg)
+    CK(gvk_keys_build_rows_kg((uint32_t)U, (uint32_t)capU, kx, kpfx, sc, with_qe, s->g_kqt, s->g_kzq,
+                              (uint32_t)capU, s->g_kok, s->g_kqt2, s->g_kzq2, kgng, s->side));
+  else if (k6)
     CK(gvk_keys_build_rows6((uint32_t)U, (uint32_t)capU, kx, kpfx, sc, with_qe, s->g_kqt, s->g_kzq, (uint32_t)capU,
                             s->g_kok, s->g_kqt2, s->g_kzq2, s->side));
   else
     CK(gvk_keys_build_rows((uint32_t)U, (uint32_t)capU, kx, kpfx, sc, with_qe, s->g_kqt, s->g_kzq, (uint32_t)capU,
                            s->g_kok, s->g_kqt2, s->g_kzq2, s->side));
-  if (used_end) *used_end = sc + gvk_keys_scratch_words((uint32_t)U, 4, nt, with_qe);
+  if (used_end) *used_end = sc + gvk_keys_scratch_words((uint32_t)U, ng, nt, with_qe);
   CK(hipEventRecord(s->keys_done, s->side));
   b.keys_ready = s->keys_done;
   b.pub33 = nullptr;
@@ -895,7 +922,8 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   b.kC = (uint32_t)capU; b.kcount = (uint32_t)U;
   b.kqt2 = s->g_kqt2; b.gtab4 = d->gtab4;       // null gtab4: the 125-doubling keyed ladder
   b.gtabf = ctx->gfull ? d->gtabf : nullptr;    // built by ensure_gtab4 above on first use
-  b.k6 = k6 ? 4 : 0; b.gtab6 = d->gtab6;
+  b.k6 = kg ? kgng : k6 ? 4 : 0; b.gtab6 = d->gtab6;
+  b.kqw = kg ? 2 : 0;
   d->grouped_batches++;
   d->grouped_keys += U;
   return GV_OK;
@@ -929,7 +957,8 @@ struct KeyArena {
   uint32_t kC, kcount;
   const uint32_t* gtab4;
   const uint32_t* gtab6;
-  int k6;                                       // k6 group tables: the throughput pipeline only
+  int k6;                                       // k6 / kg group tables: the throughput pipeline only
+  int kqw;                                      // 2: the kg layout (gvk_batch kqw)
   hipEvent_t ready;
 };
 
@@ -968,7 +997,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     b.kslot = kslot; b.kqt = ka->kqt; b.kzq = ka->kzq; b.kok = ka->kok;
     b.kC = ka->kC; b.kcount = ka->kcount;
     b.kqt2 = ka->kqt2; b.gtab4 = ka->gtab4;
-    b.k6 = ka->k6; b.gtab6 = ka->gtab6;
+    b.k6 = ka->k6; b.kqw = ka->kqw; b.gtab6 = ka->gtab6;
     kzq2 = ka->kzq2;
     // the slots are on the device already (slice_group read the key count
     // back after k_dedupe_map); only k_prep on reads the tables, so the
@@ -1060,7 +1089,8 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
       b.gtabf = ctx->gfull && ctx->gfull_item ? d->gtabf : nullptr;
     }
     plan_sort(ctx, s, b, sort_base);
-    d->routes[b.kqw && b.gtab6 && b.k6 == GV_KW_NG2 ? GV_ROUTE_KW2
+    d->routes[b.kqw == 2 && b.gtab6               ? GV_ROUTE_KG
+              : b.kqw && b.gtab6 && b.k6 == GV_KW_NG2 ? GV_ROUTE_KW2
               : b.kqw && b.gtab6                ? GV_ROUTE_KW
               : b.k6 == GV_KN_ARENA_NG && b.gtab6 ? GV_ROUTE_KN
               : b.k6 && b.gtab6                ? GV_ROUTE_K6
@@ -1439,7 +1469,7 @@ int slice_group(gv_ctx* ctx, Dev* d, size_t lo, size_t n, const HostBatch& hb, K
   CK(hipEventRecord(g->grp_ready, g->st));
   ka->kqt = b.kqt; ka->kzq = b.kzq; ka->kok = b.kok; ka->kqt2 = b.kqt2; ka->kzq2 = g->g_kzq2;
   ka->kC = b.kC; ka->kcount = b.kcount; ka->gtab4 = b.gtab4;
-  ka->gtab6 = b.gtab6; ka->k6 = b.k6;
+  ka->gtab6 = b.gtab6; ka->k6 = b.k6; ka->kqw = b.kqw;
   ka->ready = g->grp_ready;
   *d_slots = b.kslot;
   return GV_OK;   // the set stays acquired until run_slice releases it after the last chunk
@@ -1907,6 +1937,10 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   parse_size_env("GV_MAX_BATCH", &ctx->max_batch);
   if (const char* k4 = getenv("GV_KEYED_K4")) ctx->keyed_k4 = strcmp(k4, "0") != 0;
   if (const char* k6 = getenv("GV_K6")) ctx->k6 = strcmp(k6, "0") != 0;
+  if (const char* kg = getenv("GV_KG")) {
+    const int v = atoi(kg);
+    if (kg_layout_ok(v)) ctx->kg = v;
+  }
   if (const char* gf = getenv("GV_GFULL")) ctx->gfull = strcmp(gf, "0") != 0;
   if (const char* tl = getenv("GV_TWO_LADDERS")) ctx->two_ladders = strcmp(tl, "0") != 0;
   if (const char* ks = getenv("GV_KEYS_SCRATCH")) ctx->keys_scratch = strcmp(ks, "0") != 0;
@@ -2770,6 +2804,30 @@ int gv_dev_verify_digests_keyed(gv_ctx* ctx, int dev_slot, size_t n, const void*
   });
 }
 
+int gv_get_option(gv_ctx* ctx, const char* key, long long* val) {
+  if (!ctx || !key || !val) return GV_EINVAL;
+  const struct {
+    const char* k;
+    long long v;
+  } opts[] = {{"kg", ctx->kg},
+              {"k6", ctx->k6},
+              {"gfull", ctx->gfull},
+              {"keys_k6", ctx->keys_k6},
+              {"keys_wide", ctx->keys_wide},
+              {"group_keys", ctx->group_keys},
+              {"sort_keys", ctx->sort_keys},
+              {"pipeline_dev", ctx->pipeline_dev},
+              {"two_ladders", ctx->two_ladders},
+              {"key_cap", (long long)ctx->key_cap},
+              {"max_batch", (long long)ctx->max_batch}};
+  for (const auto& o : opts)
+    if (!strcmp(key, o.k)) {
+      *val = o.v;
+      return GV_OK;
+    }
+  return GV_EINVAL;
+}
+
 int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   if (!ctx || !key) return GV_EINVAL;
   if (!strcmp(key, "lat_max") || !strcmp(key, "lat_max_keyed")) {
@@ -2867,6 +2925,16 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
       d->bits_used = false;
     }
     ctx->keys_wide = (int)val;
+  } else if (!strcmp(key, "kg")) {
+    if (!kg_layout_ok((int)val)) return GV_EINVAL;
+    std::vector<std::unique_lock<std::mutex>> held;
+    for (Dev* d : ctx->devs) held.emplace_back(d->mu);
+    for (Dev* d : ctx->devs) {
+      CK(hipSetDevice(d->id));
+      for (hipStream_t t : d->hi_st) CK(hipStreamSynchronize(t));
+      d->bits_used = false;
+    }
+    ctx->kg = (int)val;
   } else if (!strcmp(key, "keys_wide1_cap")) {
     if (val < 0) return GV_EINVAL;
     ctx->keys_wide1_cap = val == 0 ? SIZE_MAX : (size_t)val;

@@ -39,7 +39,7 @@ GV_OK, GV_EINVAL, GV_ENODEV, GV_EHIP, GV_ENOMEM, GV_EFAULT = 0, -1, -2, -3, -4, 
 EXPORTED_SYMBOLS = (
     "gv_open", "gv_close", "gv_num_devices", "gv_verify_msgs", "gv_verify_digests",
     "gv_verify_digests_bits", "gv_verify_msgs_bits", "gv_dev_verify_digests", "gv_dev_verify_msgs",
-    "gv_set_option", "gv_last_stage_ms", "gv_strerror", "gv_debug_op", "gv_dev_alloc", "gv_dev_free",
+    "gv_set_option", "gv_get_option", "gv_last_stage_ms", "gv_strerror", "gv_debug_op", "gv_dev_alloc", "gv_dev_free",
     "gv_dev_copy", "gv_dev_sync", "gv_stage_stats", "gv_keys_load", "gv_keys_reset", "gv_keys_count", "gv_keys_generation",
     "gv_verify_digests_keyed", "gv_verify_msgs_keyed", "gv_dev_verify_digests_keyed", "gv_stage_stats4",
     "gv_keys_point", "gv_dev_stream_create", "gv_dev_stream_sync", "gv_dev_stream_destroy",
@@ -107,6 +107,8 @@ def load(path: str = LIB_PATH):
     L.gv_verify_ed25519_msgs_keyed.restype = i32
     L.gv_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_longlong]
     L.gv_set_option.restype = i32
+    L.gv_get_option.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_longlong)]
+    L.gv_get_option.restype = i32
     L.gv_last_stage_ms.argtypes = [vp, i32] + [ctypes.POINTER(ctypes.c_float)] * 3
     L.gv_last_stage_ms.restype = i32
     L.gv_strerror.argtypes = [i32]
@@ -238,6 +240,11 @@ class Verifier:
 
     def set_option(self, key: str, val: int):
         _check(self._L.gv_set_option(self._ctx, key.encode(), int(val)), f"gv_set_option({key})")
+
+    def get_option(self, key: str) -> int:
+        v = ctypes.c_longlong(0)
+        _check(self._L.gv_get_option(self._ctx, key.encode(), ctypes.byref(v)), f"gv_get_option({key})")
+        return int(v.value)
 
     def verify_batch_digests(self, pub33: np.ndarray, sig64: np.ndarray, dig32: np.ndarray) -> np.ndarray:
         pub33, sig64, dig32 = (np.ascontiguousarray(a, dtype=np.uint8) for a in (pub33, sig64, dig32))
@@ -510,7 +517,8 @@ class Verifier:
         _check(self._L.gv_group_stats(self._ctx, slot, ctypes.byref(b), ctypes.byref(k)), "gv_group_stats")
         return b.value, k.value
 
-    ROUTES = ("pub33", "keyed125", "k4", "k6", "lat", "lat_keyed", "k4f", "item_f", "kn", "ed_lat", "kw", "kw2")
+    KG_DEFAULT = 0         # gv_runtime.cpp gv_ctx::kg (the grouped route's default layout)
+    ROUTES = ("pub33", "keyed125", "k4", "k6", "lat", "lat_keyed", "k4f", "item_f", "kn", "ed_lat", "kw", "kw2", "kg")
 
     def route_stats(self, slot: int = 0) -> dict:
         """Batches per secp256k1 schedule on device slot since open (gv_route_stats)."""

@@ -300,6 +300,13 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * 32-entry key tables, 30 doublings, G from 11 24-bit windows of the unsplit
  * u1 (5.5 GiB of tables, built by gv_open); same verdicts; default 0, env
  * GV_K6; route counter GV_ROUTE_K6),
+ * "kg" (0 or 6 / 7 / 9: in-batch grouped keys on the many-group 5-bit
+ * ladder -- k4's 16-entry tables of 5-bit windows split over kg groups
+ * instead of 4, so the ladder runs ceil(26 / kg) positions (kg 7: 15
+ * doublings, 9: 10) for kg x 16 table entries per key; G from 11 24-bit
+ * windows of the unsplit u1 after the last doubling, on the real curve; same
+ * verdicts; takes precedence over "k6"; env GV_KG; route counter
+ * GV_ROUTE_KG),
  * "keys_k6" (0/1: gv_keys_load also builds each key's 6-bit-window tables --
  * 11 groups of 32 entries on one Z, 28 KB per key beside the 5.4 KB of k4
  * tables -- and keyed throughput batches whose slots all have them run the
@@ -331,6 +338,12 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * ladder's time is its own start to end),
  * "fault_inject" (0/1: every verify call fails with GV_EFAULT; test hook). */
 int gv_set_option(gv_ctx* ctx, const char* key, long long val);
+/* The current value of a schedule option set by gv_set_option or its
+ * environment variable: "kg", "k6", "gfull", "keys_k6", "keys_wide",
+ * "group_keys", "sort_keys", "pipeline_dev", "two_ladders", "key_cap",
+ * "max_batch".  GV_EINVAL for any other key.  Instrumentation (bench route
+ * attribution). */
+int gv_get_option(gv_ctx* ctx, const char* key, long long* val);
 
 /* Asynchronous host batches.  gv_submit_* queue a batch with the arguments
  * of the matching gv_verify_* entry point and return at once with a ticket;
@@ -399,7 +412,8 @@ int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys)
  * host batches on k_ed_lat_unc, option "ed_unc_lat_max"), GV_ROUTE_KW (keyed
  * batches on the resident arena's wide-window tables, one 9-bit window per
  * group: 15 groups, no doublings, option "keys_wide"), GV_ROUTE_KW2 (the same
- * with two windows per group: 8 groups, 9 doublings).  Instrumentation only (bench route
+ * with two windows per group: 8 groups, 9 doublings), GV_ROUTE_KG (in-batch
+ * key grouping on the many-group 5-bit ladder, option "kg").  Instrumentation only (bench route
  * attribution, node metrics). */
 #define GV_ROUTE_PUB33 0
 #define GV_ROUTE_KEYED125 1
@@ -413,7 +427,8 @@ int gv_group_stats(gv_ctx* ctx, int dev_slot, uint64_t* batches, uint64_t* keys)
 #define GV_ROUTE_ED_LAT 9
 #define GV_ROUTE_KW 10
 #define GV_ROUTE_KW2 11
-#define GV_ROUTES 12
+#define GV_ROUTE_KG 12
+#define GV_ROUTES 13
 int gv_route_stats(gv_ctx* ctx, int dev_slot, uint64_t out[GV_ROUTES]);
 
 const char* gv_strerror(int code);

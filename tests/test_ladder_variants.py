@@ -1,4 +1,7 @@
-"""The keyed ladder's schedules must agree bit for bit: k_ecmult_k4 with the G
+"""The keyed ladder's schedules must agree bit for bit: the grouped route's
+many-group 5-bit ladders (gv_set_option "kg" 6 / 7 / 9: k4's 16-entry tables
+over 6, 7 or 9 groups, 20 / 15 / 10 doublings, G after the last doubling on the
+real curve), k_ecmult_k4 with the G
 half on the unsplit scalar (gv_set_option "gfull" 1, the default: 11 signed
 25-bit windows of u1 from the 2^o G tables), k_ecmult_k4 on the GLV-split G
 half (gfull 0: 14 20-bit windows) and k_ecmult_k6 (6-bit Q windows on 32-entry
@@ -23,19 +26,23 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-SCHEDULES = {"k4f": {"gfull": 1, "k6": 0}, "k4": {"gfull": 0, "k6": 0}, "k6": {"gfull": 1, "k6": 1},
+KG_DEFAULT = gvm.Verifier.KG_DEFAULT            # the library's default "kg" layout (0: k4 on the grouped route)
+SCHEDULES = {"k4f": {"gfull": 1, "k6": 0, "kg": 0}, "k4": {"gfull": 0, "k6": 0, "kg": 0},
+             "k6": {"gfull": 1, "k6": 1, "kg": 0},
+             "kg6": {"kg": 6}, "kg7": {"kg": 7}, "kg9": {"kg": 9},
              "item_gf": {"group_keys": 0, "gfull_item": 1}, "item_glv": {"group_keys": 0, "gfull_item": 0}}
-ROUTE = {"k4f": "k4f", "k4": "k4", "k6": "k6", "wide": "k6", "wide2": "k6", "item_gf": "item_f",
-         "item_glv": "pub33"}
-DEFAULTS = {"gfull": 1, "k6": 0, "group_keys": 1, "gfull_item": 1, "keys_k6": 1, "keys_wide": 2, "keys_wide1_cap": 0}
+ROUTE = {"k4f": "k4f", "k4": "k4", "k6": "k6", "kg6": "kg", "kg7": "kg", "kg9": "kg", "wide": "k6", "wide2": "k6",
+         "item_gf": "item_f", "item_glv": "pub33"}
+DEFAULTS = {"gfull": 1, "k6": 0, "kg": KG_DEFAULT, "group_keys": 1, "gfull_item": 1, "keys_k6": 1, "keys_wide": 2,
+            "keys_wide1_cap": 0}
 # the cached-key route (gv_keys_load slots): k6 / wide-window tables are built
 # at load time when "keys_k6" / "keys_wide" are on; the message part of the test runs
 # the grouped route
-CACHED = {"k4f": {"gfull": 1, "keys_k6": 0, "keys_wide": 0, "k6": 0},
-          "k4": {"gfull": 0, "keys_k6": 0, "keys_wide": 0, "k6": 0},
-          "k6": {"gfull": 1, "keys_k6": 1, "keys_wide": 0, "k6": 1},
-          "wide": {"gfull": 1, "keys_k6": 1, "keys_wide": 2, "k6": 1},
-          "wide2": {"gfull": 1, "keys_k6": 1, "keys_wide": 1, "k6": 1}}
+CACHED = {"k4f": {"gfull": 1, "keys_k6": 0, "keys_wide": 0, "k6": 0, "kg": 0},
+          "k4": {"gfull": 0, "keys_k6": 0, "keys_wide": 0, "k6": 0, "kg": 0},
+          "k6": {"gfull": 1, "keys_k6": 1, "keys_wide": 0, "k6": 1, "kg": 0},
+          "wide": {"gfull": 1, "keys_k6": 1, "keys_wide": 2, "k6": 1, "kg": 0},
+          "wide2": {"gfull": 1, "keys_k6": 1, "keys_wide": 1, "k6": 1, "kg": 0}}
 ARENA_ROUTE = {"k6": "kn", "wide": "kw", "wide2": "kw2"}          # schedule -> the arena's route counter
 
 
