@@ -378,9 +378,10 @@ constexpr size_t key_wide_slot_bytes(int ng) { return ((size_t)GV_KW_KEY_WORDS *
 // make a later gv_keys_load or batch fail), or when an allocation fails: the
 // arena is left as it was and batches keep the k6 tables.
 // The layout is d->kw_ng's; cap1 bounds the one-window layout's capacity (a
-// test hook, option "keys_wide1_cap").
+// test hook, option "keys_wide1_cap").  ed_room: device memory the ed25519
+// key arena still needs to reach its own cap (reserved the same way).
 bool ensure_keys_wide(Dev* d, size_t need, size_t used, hipStream_t st, size_t key_cap, size_t budget,
-                      size_t cap1 = SIZE_MAX) {
+                      size_t ed_room, size_t cap1 = SIZE_MAX) {
   if (need <= d->kcapw) return true;
   const size_t grow = d->kcapw >= key_cap ? need : std::min<size_t>(2 * d->kcapw, std::max<size_t>(need, key_cap));
   const size_t cap = round_up(std::max<size_t>({need, grow, 4096}), 256);
@@ -389,7 +390,8 @@ bool ensure_keys_wide(Dev* d, size_t need, size_t used, hipStream_t st, size_t k
   if (d->opt_bytes + cap * slot_b > budget) return false;
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return false;
-  const size_t reserve = (key_cap > d->kcap ? key_cap - d->kcap : 0) * key_slot_bytes(true) + (size_t(8) << 30);
+  const size_t reserve =
+      (key_cap > d->kcap ? key_cap - d->kcap : 0) * key_slot_bytes(true) + ed_room + (size_t(8) << 30);
   if (free_b < cap * slot_b + reserve) return false;
   const size_t ng1 = (size_t)d->kw_ng - 1;
   uint32_t *qt = nullptr, *zq = nullptr, *qt2 = nullptr, *zq2 = nullptr;
@@ -1702,6 +1704,7 @@ struct AsyncState {
   std::unordered_map<uint64_t, std::shared_ptr<AsyncJob>> jobs;
   uint64_t next_ticket = 1;
   size_t pending = 0;                             // jobs submitted, not done
+  int quiescing = 0;                              // gv_keys_load / gv_keys_reset in progress: submissions wait
   bool quit = false;
 };
 
@@ -1839,14 +1842,27 @@ AsyncState* async_state(gv_ctx* ctx) {
   return ctx->async;
 }
 
-// Wait until no submitted batch is pending (the key arenas change meaning
-// under a keyed batch otherwise).
-void async_quiesce(gv_ctx* ctx) {
-  AsyncState* as = ctx->async;
-  if (!as) return;
-  std::unique_lock<std::mutex> lk(as->m);
-  as->cv.wait(lk, [&] { return as->pending == 0; });
-}
+// Held by gv_keys_load / gv_keys_reset: waits until no submitted batch is
+// pending (the key arenas change meaning under a keyed batch otherwise), and
+// new submissions wait until it is released -- a caller that keeps queueing
+// batches can neither starve the load nor slip a batch in under it.
+struct AsyncQuiesce {
+  AsyncState* as;
+  explicit AsyncQuiesce(gv_ctx* ctx) : as(ctx->async) {
+    if (!as) return;
+    std::unique_lock<std::mutex> lk(as->m);
+    ++as->quiescing;
+    as->cv.wait(lk, [&] { return as->pending == 0; });
+  }
+  ~AsyncQuiesce() {
+    if (!as) return;
+    std::lock_guard<std::mutex> lk(as->m);
+    --as->quiescing;
+    as->cv.notify_all();
+  }
+  AsyncQuiesce(const AsyncQuiesce&) = delete;
+  AsyncQuiesce& operator=(const AsyncQuiesce&) = delete;
+};
 
 int submit_host(gv_ctx* ctx, size_t n, const HostBatch& hb_in, uint64_t* ticket) {
   if (!ctx || !ticket) return GV_EINVAL;
@@ -1862,7 +1878,8 @@ int submit_host(gv_ctx* ctx, size_t n, const HostBatch& hb_in, uint64_t* ticket)
                    is_pinned(hb_in.sig64) && is_pinned(hb_in.dig32);
   AsyncState* as = async_state(ctx);
   const size_t nd = ctx->devs.size(), per = round_up((n + nd - 1) / std::max<size_t>(nd, 1), 256);
-  std::lock_guard<std::mutex> lk(as->m);
+  std::unique_lock<std::mutex> lk(as->m);
+  as->cv.wait(lk, [&] { return as->quiescing == 0; });   // a key load / reset in progress
   for (size_t k = 0; k < nd; ++k) {
     const size_t lo = std::min(n, k * per), hi = std::min(n, (k + 1) * per);
     if (lo >= hi) continue;
@@ -2350,7 +2367,7 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
   if (!ctx) return GV_EINVAL;
   if (n == 0) return GV_OK;
   if (!pub33 || !slot_out) return GV_EINVAL;
-  async_quiesce(ctx);                           // no submitted keyed batch reads slots that move
+  AsyncQuiesce q(ctx);                          // no submitted keyed batch reads slots that move
   std::lock_guard<std::mutex> kl(ctx->keys_mu);
   const size_t base = ctx->keys;
   if (base + n > kMaxItems) return GV_EINVAL;
@@ -2411,20 +2428,28 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
         free_keys_wide(d);
         d->kw_ng = want;
       }
-      bool ok = ensure_keys_wide(d, base + n, base, st, ctx->key_cap, ctx->hbm_budget, ctx->keys_wide1_cap);
+      // the ed25519 arena's growth to ed_key_cap is reserved too (72 KB per key)
+      const size_t ed_room = (ctx->ed_key_cap > d->ekcap ? ctx->ed_key_cap - d->ekcap : 0) *
+                             ((size_t)GV_EDK_WORDS + 8 + 1) * 4;
+      bool ok = ensure_keys_wide(d, base + n, base, st, ctx->key_cap, ctx->hbm_budget, ed_room,
+                                 ctx->keys_wide1_cap);
       if (!ok && d->kw_ng == GV_KW_NG1) {
         // (a failed read-back only stops the wide tables: the k6 ones serve)
         std::vector<uint8_t> old_pub;
         const bool back = !base || read_back_pub33(ctx, d, st, base, old_pub) == GV_OK;
         free_keys_wide(d);
         d->kw_ng = GV_KW_NG2;
-        ok = back && ensure_keys_wide(d, base + n, 0, st, ctx->key_cap, ctx->hbm_budget);
-        if (ok && base && (rc = build_wide(ctx, d, s, st, old_pub.data(), base, 0))) return rc;
+        ok = back && ensure_keys_wide(d, base + n, 0, st, ctx->key_cap, ctx->hbm_budget, ed_room);
+        // a failed rebuild only stops the wide tables (the k6 / k4 ones serve
+        // every slot): never a gv_keys_load error
+        if (ok && base && build_wide(ctx, d, s, st, old_pub.data(), base, 0) != GV_OK) ok = false;
       }
+      if (ok && build_wide(ctx, d, s, st, pub33, n, base) != GV_OK) ok = false;
       if (!ok) {
+        (void)hipGetLastError();
+        d->keysw = 0;                             // no slot's wide tables are trusted past a failed build
         d->kw_full = true;
       } else {
-        if ((rc = build_wide(ctx, d, s, st, pub33, n, base))) return rc;
         d->keysw = base + n;
       }
     }
@@ -2436,7 +2461,7 @@ int gv_keys_load(gv_ctx* ctx, size_t n, const uint8_t* pub33, uint32_t* slot_out
 
 int gv_keys_reset(gv_ctx* ctx) {
   if (!ctx) return GV_EINVAL;
-  async_quiesce(ctx);
+  AsyncQuiesce q(ctx);
   std::lock_guard<std::mutex> kl(ctx->keys_mu);
   ctx->keys = 0;
   ctx->keys_gen.fetch_add(1);

@@ -17,6 +17,7 @@ from __future__ import annotations
 import ctypes
 import os
 import subprocess
+import weakref
 
 import numpy as np
 
@@ -208,11 +209,25 @@ class Verifier:
         _check(rc, "gv_open")
         self._ctx = ctx
         self._L = L
+        # submitted batches not yet waited for: ticket -> (input arrays, verdicts).
+        # The library reads the inputs and writes the verdicts until gv_wait, so
+        # they live here, not only in the Pending the caller may drop.
+        self._inflight = {}
 
     def close(self):
         if self._ctx:
+            for t in list(self._inflight):        # the lanes use these buffers until each batch is done
+                self._release(t)
             self._L.gv_close(self._ctx)
             self._ctx = None
+
+    def _release(self, ticket) -> int:
+        """gv_wait on a ticket still in flight (a dropped Pending, close()); 0 if already waited."""
+        if ticket not in self._inflight or not self._ctx:
+            return 0
+        rc = self._L.gv_wait(self._ctx, ticket)
+        self._inflight.pop(ticket, None)
+        return rc
 
     def __enter__(self):
         return self
@@ -278,16 +293,21 @@ class Verifier:
 
     # ---- asynchronous host batches (gv_submit_* / gv_wait)
     class Pending:
-        """A submitted batch: holds its input arrays (the library reads them
-        until gv_wait) and its verdict array."""
-        def __init__(self, ticket, out, keep):
-            self.ticket, self.out, self._keep = ticket, out, keep
+        """A submitted batch: its ticket and verdict array.  The Verifier keeps
+        the input arrays (and the verdicts) alive until the batch is waited for;
+        a Pending dropped without wait() is waited for when it is collected, so
+        the library never touches freed memory."""
+        def __init__(self, ticket, out):
+            self.ticket, self.out = ticket, out
 
     def _submit(self, fn, name, n, args, keep):
         out = np.zeros(n, dtype=np.uint8)
         t = ctypes.c_uint64(0)
         _check(fn(self._ctx, n, *[_ptr(a) for a in args], _ptr(out), ctypes.byref(t)), name)
-        return Verifier.Pending(t.value, out, keep)
+        self._inflight[t.value] = (keep, out)
+        p = Verifier.Pending(t.value, out)
+        weakref.finalize(p, self._release, t.value)
+        return p
 
     def submit_digests(self, pub33, sig64, dig32) -> "Verifier.Pending":
         a = [np.ascontiguousarray(x, dtype=np.uint8) for x in (pub33, sig64, dig32)]
@@ -311,8 +331,11 @@ class Verifier:
         return self._submit(self._L.gv_submit_msgs, "gv_submit_msgs", p.shape[0], a, a)
 
     def wait(self, pending: "Verifier.Pending") -> np.ndarray:
-        _check(self._L.gv_wait(self._ctx, pending.ticket), "gv_wait")
-        pending._keep = None
+        if pending.ticket not in self._inflight:
+            raise GpuVerifyError(GV_EINVAL, "gv_wait: ticket already waited for")
+        rc = self._L.gv_wait(self._ctx, pending.ticket)
+        self._inflight.pop(pending.ticket, None)
+        _check(rc, "gv_wait")
         return pending.out
 
     # ---- account pubkey cache (gv_keys_*)

@@ -55,7 +55,10 @@ type EdVerifier interface {
 }
 
 // AsyncVerifier queues a batch and returns at once: wait returns the
-// verdicts (VerifyBatch's), called exactly once.  The GPU implements it with
+// verdicts (VerifyBatch's).  wait is idempotent -- later calls return the
+// first call's verdicts -- so a caller can defer it as a guard: a batch that
+// is never waited keeps its pinned buffers out of the pool (GPU.Close would
+// block on them) and its ticket in the library.  The GPU implements it with
 // gv_submit_msgs[_keyed] / gv_wait, so the batch runs while the caller does
 // other work -- the same block's ed25519 leaves, the next block's state stage
 // -- and consecutive batches run as one stream of chunks on the device.
@@ -631,7 +634,9 @@ func (g *GPU) SubmitBatch(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]byte)
 		qs = append(qs, submit(idx, nil))
 	}
 	t0 := time.Now()
-	return func() []bool {
+	var once sync.Once
+	var verdicts []bool
+	waitAll := func() []bool {
 		ok := make([]bool, n)
 		for _, q := range qs {
 			rc := q.rc
@@ -652,6 +657,10 @@ func (g *GPU) SubmitBatch(pubs []secp256k1.PubKeySecp256k1, msgs, sigs [][]byte)
 			q.out.free()
 		}
 		return ok
+	}
+	return func() []bool {
+		once.Do(func() { verdicts = waitAll() })
+		return verdicts
 	}
 }
 

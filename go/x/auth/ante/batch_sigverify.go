@@ -292,6 +292,10 @@ func (b *batch) resolve(v gv.Verifier, cache *gv.VerdictCache) {
 	var res []bool
 	if async {
 		wait := av.SubmitBatch(pubs, msgs, sigs)
+		// wait is idempotent: if resolveEd panics (the ante chain runs under
+		// baseapp's recover) the queued batch is still waited for, so its
+		// pinned buffers go back to the pool and GPU.Close does not block
+		defer wait()
 		b.resolveEd(v, cache) // beside the queued secp256k1 batch
 		res = wait()
 	} else {

@@ -356,8 +356,13 @@ int gv_get_option(gv_ctx* ctx, const char* key, long long* val);
  * device-resident pipeline's overlap from host buffers.  Unlike gv_verify_*,
  * the library keeps the caller's pointers until gv_wait returns: the buffers
  * (ideally gv_host_alloc memory, read in place) must stay valid and unchanged
- * until then.  gv_keys_load / gv_keys_reset wait for every submitted batch
- * first; gv_close finishes the queued batches.  Replaces nothing in the
+ * until then.  gv_wait is also a ticket's release: a caller that abandons a
+ * batch (an error of its own between submit and wait) still waits for it,
+ * since the library reads and writes its buffers until the batch is done; a
+ * ticket never waited keeps a few hundred bytes of bookkeeping until gv_close,
+ * which finishes the queued batches and frees it.  gv_keys_load /
+ * gv_keys_reset wait for every submitted batch first, and submissions made
+ * while one of them runs wait until it returns.  Replaces nothing in the
  * reference (its ante handler verifies synchronously, x/auth/ante/
  * sigverify.go:210); it is how baseapp's pre-verification hook keeps the
  * GPU busy across blocks (baseapp/abci.go:203-221). */

@@ -5,6 +5,8 @@ last chunks -- and must give exactly the synchronous entry points' verdicts,
 whatever the mix of routes in the queue (grouped pub33, per-item pub33, keyed
 slots, messages, small batches on the zero-copy kernels, pinned and pageable
 buffers) and whatever the order of the waits."""
+import gc
+
 import numpy as np
 import pytest
 
@@ -79,7 +81,7 @@ def test_tickets(ver, c2):
     with pytest.raises(gvm.GpuVerifyError):                 # a ticket is waited for once
         ver.wait(p)
     with pytest.raises(gvm.GpuVerifyError):
-        ver.wait(gvm.Verifier.Pending(123456789, None, None))
+        ver.wait(gvm.Verifier.Pending(123456789, None))
 
 
 def test_keys_load_waits_for_submitted_keyed_batches(ver, c2):
@@ -103,3 +105,25 @@ def test_sync_calls_interleave_with_the_queue(ver, c2):
     assert np.array_equal(got, exp[:70_000])
     assert np.array_equal(ver.wait(p2), exp)
     assert np.array_equal(ver.wait(p1), exp)
+
+
+def test_dropped_pending_is_waited_before_its_buffers_go(ver, c2):
+    """the library reads a batch's inputs and writes its verdicts
+    until gv_wait.  A Pending dropped without wait() must not free them under
+    the lane: the Verifier keeps them and waits for the ticket when the
+    Pending is collected."""
+    pub, sig, dig, exp = c2
+    for k in range(3):                                        # fresh copies: nothing else holds them
+        ver.submit_digests(pub.copy(), sig.copy(), dig.copy())
+    gc.collect()
+    assert not ver._inflight                                  # every dropped ticket was waited for
+    p = ver.submit_digests(pub, sig, dig)
+    assert np.array_equal(ver.wait(p), exp)
+
+
+def test_close_waits_for_outstanding_batches(c2):
+    pub, sig, dig, exp = c2
+    v = gvm.Verifier([0])
+    p = v.submit_digests(pub, sig, dig)
+    v.close()                                                 # waits for the ticket, then gv_close
+    assert np.array_equal(p.out, exp)
