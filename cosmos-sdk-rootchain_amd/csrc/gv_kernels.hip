@@ -818,40 +818,85 @@ GV_DEV void gej29_to_affine_words(fe& x8, fe& y8, const gej29& p) {
 // The keyed ladders' tables are built in three launches so that the long
 // serial part runs one lane per key and the rest one lane per (key, group):
 //
-// k_keys_chain (lane = key): ParsePubKey (a rejected key gets G's tables,
-// never used: every item against it is false), then the doublings to each
-// group's base 2^bit(k) Q (100 for k4).  Each group's base point is parked, as
-// canonical words x[8] y[8], in entry 0 of its own table row (group 0 in kqt,
-// groups 1.. in kqt2 rows slot * (NG - 1) + k - 1); the Jacobian Z of groups
-// 1.. in their Z rows (kzq2, (NG - 1) x 8 rows of stride kC), group 0 is affine.
+// k_keys_chain: ParsePubKey and the doublings to each group's base 2^bit(k) Q
+// (100 for k4), on two waves per key set so the square root is off the
+// doubling chain (round 6).  With c = x^3 + 7 the point Q' = (c x, c^2) lies
+// on E': Y^2 = X^3 + 7 c^3, the image of Q = (x, y) under (x, y) -> (u^2 x,
+// u^3 y) with u = y (u^2 = c): a = 0 doubling and addition formulas never read
+// the curve constant, so the chain and the tables run on Q' as soon as c is
+// known, and a Jacobian (X, Y, Z) of E' is the point (X, Y, u Z) of E.
+// Blocks of 128 keys: waves 0-1 (the root role) run ParsePubKey's checks and
+// square root -- the verdict to kok, u (the root with the prefix's parity) to
+// the key's Z row kzq, which k_keys_fwd / k_keys_tables fold into every
+// group's table Z; waves 2-3 (the chain role) park Q' and its doublings.  For
+// a key ParsePubKey rejects c may be a non-square (Q' on the twist): its tables
+// are computed all the same and never used -- every item against it is false.
+// Each group's base point is parked, as canonical words x[8] y[8], in entry 0
+// of its own table row (group 0 in kqt, groups 1.. in kqt2 rows slot * (NG -
+// 1) + k - 1); the Jacobian Z of groups 1.. in their Z rows (kzq2, (NG - 1) x
+// 8 rows of stride kC), group 0 is affine (on E').
 template <int QW, int NG>
 __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_chain(u32 n, u32 C, const u32* in_x, const u32* in_pfx, u32 base,
-                                                     u32* kqt, u32 kC, u32* kok, u32* kqt2, u32* kzq2) {
+                                                     u32* kqt, u32 kC, u32* kok, u32* kqt2, u32* kzq2, u32* kzq) {
   using L = KLayout<QW, NG>;
-  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool root = threadIdx.x < 128u;                 // wave-uniform role
+  const u32 g = blockIdx.x * 128u + (threadIdx.x & 127u);
   if (g >= n) return;                       // no cross-lane work
-  fe x, y;
+  fe x;
   load_fe(x, in_x, C, g);
-  const bool ok = parse_pubkey(in_pfx[g], x, y);
-  if (!ok) {
-    fe_from_const(x, kGx);
-    fe_from_const(y, kGy);
+  fe29 x29, c;
+  {
+    fe29 seven;
+    f29_from_words(x29, x.v);
+    f29x_sqr(c, x29);
+    f29x_mul(c, c, x29);
+    f29_set_u32(seven, 7);
+    f29_add(c, c, seven);                   // c = x^3 + 7 (magnitude 2)
   }
-  kok[base + g] = ok ? 1u : 0u;
+  if (root) {
+    const u32 pre = in_pfx[g];
+    bool ok = (pre & 0xFEu) == 0x02u;
+    {                                       // x < p  (btcec: "pubkey X parameter is >= to P")
+      u32 br = 0, d;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d = __builtin_subc(x.v[i], kP[i], br, &br);
+      (void)d;
+      ok &= (br != 0);
+    }
+    fe29 y29, y2;
+    f29x_sqrt_candidate(y29, c);            // y = c^((p+1)/4)
+    f29x_sqr(y2, y29);
+    ok &= f29_equal(y2, c);                 // "invalid square root"
+    fe y;
+    f29_to_words(y.v, y29);                 // canonical
+    if ((y.v[0] & 1u) != (pre & 1u)) fe_neg(y, y);   // the prefix's parity (y != 0 always)
+    fe_normalize(y);
+    kok[base + g] = ok ? 1u : 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kzq[(size_t)i * kC + base + g] = y.v[i];   // u, read by the table build
+    return;
+  }
   auto park = [](u32* tab, u32 row, const u32* xw, const u32* yw) {
     u32* p = tab + (size_t)row * L::NT * L::EW;
 #pragma unroll
     for (int i = 0; i < 8; ++i) { p[i] = xw[i]; p[8 + i] = yw[i]; }
   };
-  park(kqt, base + g, x.v, y.v);
   gej29 q;
-  f29_from_words(q.x, x.v);
-  f29_from_words(q.y, y.v);
+  f29x_mul(q.x, c, x29);                    // Q' = (c x, c^2)
+  f29x_sqr(q.y, c);
   f29_set_u32(q.z, 1);
+  {
+    u32 xw[8], yw[8];
+    f29_to_words(xw, q.x);
+    f29_to_words(yw, q.y);
+    f29_from_words(q.x, xw);
+    f29_from_words(q.y, yw);
+    park(kqt, base + g, xw, yw);
+  }
 #pragma unroll 1
   for (int grp = 1; grp < NG; ++grp) {
 #pragma unroll 1
-    for (int k = L::bit(grp - 1); k < L::bit(grp); ++k) gej29x_double(q, q);  // never infinite: odd order
+    for (int k = L::bit(grp - 1); k < L::bit(grp); ++k) gej29x_double(q, q);  // Y never 0: no 2-torsion on E' or its twist
     u32 xw[8], yw[8];
     f29_to_words(xw, q.x);
     f29_to_words(yw, q.y);
@@ -965,11 +1010,17 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_tables(u32 n, u32 C4
     Y1 = a1;
     if (m + 1 < NT) put(m, X2, Y2);         // the last entry waits for rho
   }
-  // E = Z_15 (times the parked Jacobian Z for groups 1..3); the quad's others
+  // E = Z_15 (times the parked Jacobian Z for groups 1..3, and u: the chain
+  // ran on E', k_keys_chain); the quad's others
   if (grp) {
     fe29 z;
     load_f29(z, zrow, kC, base + key);
     f29x_mul(prod, prod, z);
+  }
+  {
+    fe29 u;
+    load_f29(u, kzq, kC, base + key);       // read by all four lanes before lane 0 writes zc there
+    f29x_mul(prod, prod, u);
   }
   fe29 e1, e2, e3;
 #pragma unroll
@@ -1049,7 +1100,7 @@ GV_DEV void keys_get(const u32* qe, u32 CL, u32 L, const u32* tab, u32 row, int 
 
 template <int QW, int NG>
 __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_fwd(u32 n, u32 CL, u32 base, u32* kqt, u32 kC, u32* kqt2,
-                                                   const u32* kzq2, u32* qr, u32* qe, u32* er) {
+                                                   const u32* kzq2, u32* qr, u32* qe, u32* er, const u32* kzq) {
   constexpr int NT = KLayout<QW, NG>::NT;
   const u32 L = blockIdx.x * blockDim.x + threadIdx.x;
   const u32 key = L / NG, grp = L % NG;
@@ -1113,11 +1164,17 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_fwd(u32 n, u32 CL, u
     Y1 = a1;
     keys_put<QW, NG>(qe, CL, L, tab, row, m, X2, Y2);    // (m+1)*Q on Z_m
   }
-  // E = Z_last (times the parked Jacobian Z for groups 1..)
+  // E = Z_last (times the parked Jacobian Z for groups 1.., and u: the chain
+  // ran on E', k_keys_chain; k_keys_back overwrites kzq only in a later launch)
   if (grp) {
     fe29 z;
     load_f29(z, kzq2 + (size_t)(grp - 1u) * 8 * kC, kC, base + key);
     f29x_mul(prod, prod, z);
+  }
+  {
+    fe29 u;
+    load_f29(u, kzq, kC, base + key);
+    f29x_mul(prod, prod, u);
   }
   store_ratio29(er, CL, L, 0, prod);
 }
@@ -2047,8 +2104,8 @@ static hipError_t keys_tables_launch(uint32_t n, uint32_t C, const uint32_t* in_
   uint32_t* qr = scratch;
   uint32_t* er = qr + (size_t)(NT - 2) * 9 * CL;
   uint32_t* qe = with_qe ? er + (size_t)9 * CL : nullptr;
-  hipLaunchKernelGGL((gv::k_keys_chain<QW, NG>), dim3((n + 255) / 256), dim3(256), 0, st, n, C, in_x, in_pfx, base,
-                     kqt, kC, kok, kqt2, kzq2);
+  hipLaunchKernelGGL((gv::k_keys_chain<QW, NG>), dim3((n + 127) / 128), dim3(256), 0, st, n, C, in_x, in_pfx, base,
+                     kqt, kC, kok, kqt2, kzq2, kzq);
   if (NG == 4) {
     // four groups: one launch, the quad trades its Zs by lane shuffles (the
     // last entry stays in registers; the E rows are unused)
@@ -2057,7 +2114,7 @@ static hipError_t keys_tables_launch(uint32_t n, uint32_t C, const uint32_t* in_
     return hipGetLastError();
   }
   hipLaunchKernelGGL((gv::k_keys_fwd<QW, NG>), dim3(CL / 256), dim3(256), 0, st, n, CL, base, kqt, kC, kqt2,
-                     (const uint32_t*)kzq2, qr, qe, er);
+                     (const uint32_t*)kzq2, qr, qe, er, (const uint32_t*)kzq);
   hipLaunchKernelGGL((gv::k_keys_back<QW, NG>), dim3(CL / 256), dim3(256), 0, st, n, CL, base, kqt, kzq, kC, kqt2,
                      kzq2, (const uint32_t*)qr, (const uint32_t*)qe, (const uint32_t*)er);
   return hipGetLastError();

@@ -5,7 +5,8 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "cosmos-sdk-rootchain_amd")
-for p in (REPO, PKG):
+WORKLOAD = os.path.join(REPO, "tools", "workload")      # txkit: test / bench signing tooling, not the product
+for p in (REPO, PKG, WORKLOAD):
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -36,6 +36,7 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "cosmos-sdk-rootchain_amd"))
+sys.path.insert(0, os.path.join(REPO, "tools", "workload"))          # txkit
 
 
 def _unpack_bits(bits: np.ndarray, n: int) -> np.ndarray:

@@ -15,7 +15,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FAKE = os.path.join(REPO, "tests", "sanitize", "build", "libgvhost_fake.so")
 os.environ["GVH_LIB"] = FAKE
 os.environ["GVFAKE_TRUST"] = "1"
-for p in (REPO, os.path.join(REPO, "cosmos-sdk-rootchain_amd"), os.path.join(REPO, "tools")):
+for p in (REPO, os.path.join(REPO, "cosmos-sdk-rootchain_amd"), os.path.join(REPO, "tools"),
+          os.path.join(REPO, "tools", "workload")):
     sys.path.insert(0, p)
 import numpy as np  # noqa: E402
 

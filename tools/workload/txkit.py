@@ -26,8 +26,7 @@ import os
 import struct
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-REPO = os.path.dirname(HERE)
-_WORK = os.path.join(REPO, "tools", "workload", "libgvwork.so")
+_WORK = os.path.join(HERE, "libgvwork.so")
 
 PREFIX_SECP = bytes.fromhex("eb5ae987")
 PREFIX_ED = bytes.fromhex("1624de64")
