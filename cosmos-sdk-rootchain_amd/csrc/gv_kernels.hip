@@ -767,6 +767,9 @@ __global__ __launch_bounds__(256) GV_PREP_ATTR void k_prep(u32 C, u32 n, const u
 }
 
 // ------------------------------------------------------------ key tables
+#ifndef GV_KEYS_PREFETCH
+#define GV_KEYS_PREFETCH 1
+#endif
 // Key arena (gv_keys_load): lane g parses key g of the load batch once and
 // writes its Q table to arena row base + g, the table's Z to kzq (8 rows of
 // stride kC) and the ParsePubKey verdict to kok.  A rejected key gets G's
@@ -825,10 +828,13 @@ GV_DEV void gej29_to_affine_words(fe& x8, fe& y8, const gej29& p) {
 // u^3 y) with u = y (u^2 = c): a = 0 doubling and addition formulas never read
 // the curve constant, so the chain and the tables run on Q' as soon as c is
 // known, and a Jacobian (X, Y, Z) of E' is the point (X, Y, u Z) of E.
-// Blocks of 128 keys: waves 0-1 (the root role) run ParsePubKey's checks and
-// square root -- the verdict to kok, u (the root with the prefix's parity) to
-// the key's Z row kzq, which k_keys_fwd / k_keys_tables fold into every
-// group's table Z; waves 2-3 (the chain role) park Q' and its doublings.  For
+// Blocks of 256 keys in 512 threads: waves 0-3 (the root role) run
+// ParsePubKey's checks and square root -- the verdict to kok, u (the root with
+// the prefix's parity) to the key's Z row kzq, which k_keys_fwd /
+// k_keys_tables fold into every group's table Z; waves 4-7 (the chain role)
+// park Q' and its doublings.  A block's wave w runs on SIMD w % 4, so every
+// SIMD holds one root wave beside one chain wave: the chain's dependent
+// products interleave with the root's instead of waiting on themselves.  For
 // a key ParsePubKey rejects c may be a non-square (Q' on the twist): its tables
 // are computed all the same and never used -- every item against it is false.
 // Each group's base point is parked, as canonical words x[8] y[8], in entry 0
@@ -836,11 +842,11 @@ GV_DEV void gej29_to_affine_words(fe& x8, fe& y8, const gej29& p) {
 // 1) + k - 1); the Jacobian Z of groups 1.. in their Z rows (kzq2, (NG - 1) x
 // 8 rows of stride kC), group 0 is affine (on E').
 template <int QW, int NG>
-__global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_chain(u32 n, u32 C, const u32* in_x, const u32* in_pfx, u32 base,
+__global__ __launch_bounds__(512) GV_FRONT_ATTR void k_keys_chain(u32 n, u32 C, const u32* in_x, const u32* in_pfx, u32 base,
                                                      u32* kqt, u32 kC, u32* kok, u32* kqt2, u32* kzq2, u32* kzq) {
   using L = KLayout<QW, NG>;
-  const bool root = threadIdx.x < 128u;                 // wave-uniform role
-  const u32 g = blockIdx.x * 128u + (threadIdx.x & 127u);
+  const bool root = threadIdx.x < 256u;                 // wave-uniform role
+  const u32 g = blockIdx.x * 256u + (threadIdx.x & 255u);
   if (g >= n) return;                       // no cross-lane work
   fe x;
   load_fe(x, in_x, C, g);
@@ -921,8 +927,18 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_chain(u32 n, u32 C, 
 // (null: the entries go through the table itself: lanes 1,280 B apart write
 // 80 B each, twice, and read them back in between).
 // QW: 5 (k4, 16 entries per table) or 6 (the grouped route's k6, 32 entries).
+// (four waves per SIMD: the launch is 4 waves per SIMD for 65,536 keys, so a
+// fifth VGPR bank's worth would leave a third of a round as tail)
+#ifndef GV_KEYS_TABLES_W4
+#define GV_KEYS_TABLES_W4 1
+#endif
+#if GV_KEYS_TABLES_W4
+#define GV_KEYS_TABLES_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+#else
+#define GV_KEYS_TABLES_ATTR GV_FRONT_ATTR
+#endif
 template <int QW>
-__global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_tables(u32 n, u32 C4, u32 base, u32* kqt, u32* kzq, u32 kC, u32* kqt2,
+__global__ __launch_bounds__(256) GV_KEYS_TABLES_ATTR void k_keys_tables(u32 n, u32 C4, u32 base, u32* kqt, u32* kzq, u32 kC, u32* kqt2,
                                                       u32* kzq2, u32* qr, u32* qe) {
   constexpr int NT = KLayout<QW, 4>::NT;
   const u32 L = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1042,7 +1058,29 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_tables(u32 n, u32 C4
     store_qent29<NT>(tab, row, NT - 1, X2, Y2);
   }
   // entry m (index m-1) on Z_{m-1} (m >= 2; entries 1, 2 on Z_1): times
-  // rho * Z_15 / Z_{m-1}
+  // rho * Z_15 / Z_{m-1}.  GV_KEYS_PREFETCH: the next iteration's ratio and
+  // entry are loaded at the top of this one, so their latency hides under
+  // this iteration's products (the loop is otherwise load-latency bound).
+#if GV_KEYS_PREFETCH
+  fe29 nr, nx, ny;
+  if (NT - 1 >= 2) load_ratio29(nr, qr, C4, L, NT - 3);
+  get(NT - 2, nx, ny);
+#pragma unroll 1
+  for (int m = NT - 1; m >= 1; --m) {
+    fe29 x = nx, y = ny, ratio = nr;
+    if (m >= 2) {                             // prefetch for m - 1
+      if (m - 1 >= 2) load_ratio29(nr, qr, C4, L, m - 3);
+      get(m - 2, nx, ny);
+    }
+    if (m >= 2) f29x_mul(acc, acc, ratio);
+    fe29 a2, a3;
+    f29x_sqr(a2, acc);
+    f29x_mul(a3, a2, acc);
+    f29x_mul(x, x, a2);
+    f29x_mul(y, y, a3);
+    store_qent29<NT>(tab, row, m - 1, x, y);
+  }
+#else
 #pragma unroll 1
   for (int m = NT - 1; m >= 1; --m) {
     if (m >= 2) {
@@ -1058,6 +1096,7 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_tables(u32 n, u32 C4
     f29x_mul(y, y, a3);
     store_qent29<NT>(tab, row, m - 1, x, y);
   }
+#endif
   store_f29(zrow, kC, base + key, zc);
 }
 
@@ -1208,6 +1247,26 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_back(u32 n, u32 CL, 
   }
   f29x_mul(zc, acc, own);                                // the common Z
   // entry m - 1 on Z_{m-1} (m >= 2; entries 1, 2 on Z_1): times rho Z_last / Z_{m-1}
+  // (GV_KEYS_PREFETCH: the next iteration's loads issued at the top, as k_keys_tables)
+#if GV_KEYS_PREFETCH
+  fe29 nr, nx, ny;
+  keys_get<QW, NG>(qe, CL, L, tab, row, NT - 1, nx, ny);
+#pragma unroll 1
+  for (int m = NT; m >= 1; --m) {
+    fe29 x = nx, y = ny, ratio = nr;
+    if (m >= 2) {                                        // prefetch for m - 1
+      if (m - 1 >= 2) load_ratio29(nr, qr, CL, L, m - 3);
+      keys_get<QW, NG>(qe, CL, L, tab, row, m - 2, nx, ny);
+    }
+    if (m >= 2 && m < NT) f29x_mul(acc, acc, ratio);
+    fe29 a2, a3;
+    f29x_sqr(a2, acc);
+    f29x_mul(a3, a2, acc);
+    f29x_mul(x, x, a2);
+    f29x_mul(y, y, a3);
+    store_qent29<NT, KLayout<QW, NG>::EW>(tab, row, m - 1, x, y);
+  }
+#else
 #pragma unroll 1
   for (int m = NT; m >= 1; --m) {
     if (m >= 2 && m < NT) {
@@ -1223,6 +1282,7 @@ __global__ __launch_bounds__(256) GV_FRONT_ATTR void k_keys_back(u32 n, u32 CL, 
     f29x_mul(y, y, a3);
     store_qent29<NT, KLayout<QW, NG>::EW>(tab, row, m - 1, x, y);
   }
+#endif
   store_f29(zrow, kC, base + key, zc);
 }
 
@@ -2104,7 +2164,7 @@ static hipError_t keys_tables_launch(uint32_t n, uint32_t C, const uint32_t* in_
   uint32_t* qr = scratch;
   uint32_t* er = qr + (size_t)(NT - 2) * 9 * CL;
   uint32_t* qe = with_qe ? er + (size_t)9 * CL : nullptr;
-  hipLaunchKernelGGL((gv::k_keys_chain<QW, NG>), dim3((n + 127) / 128), dim3(256), 0, st, n, C, in_x, in_pfx, base,
+  hipLaunchKernelGGL((gv::k_keys_chain<QW, NG>), dim3((n + 255) / 256), dim3(512), 0, st, n, C, in_x, in_pfx, base,
                      kqt, kC, kok, kqt2, kzq2, kzq);
   if (NG == 4) {
     // four groups: one launch, the quad trades its Zs by lane shuffles (the

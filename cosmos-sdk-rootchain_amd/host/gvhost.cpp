@@ -29,6 +29,7 @@
 #include <future>
 #include <memory>
 #include <mutex>
+#include <time.h>
 #include <random>
 #include <shared_mutex>
 #include <stdexcept>
@@ -961,55 +962,63 @@ struct Node {
 };
 
 // Build the node for pk.VerifyBytes(msg, sig) (secp256k1_nocgo.go / ed25519 /
-// multisig threshold_pubkey.go).  Multisig leaves are AND-ed in bit order; since
-// every leaf is a pure function, the AND equals the reference's short-circuit.
-Node build_node(const PubKey& pk, const H32& dig, Span sig, std::vector<Leaf>& leaves) {
-  Node n;
+// multisig threshold_pubkey.go) into n (its kids' capacity is reused: a plan
+// keeps its node across pooled Memo reuse).  Multisig leaves are AND-ed in bit
+// order; since every leaf is a pure function, the AND equals the reference's
+// short-circuit.  pre: sig already decoded as a Multisignature (make_plan
+// decodes it once for the gas charge and the node).
+void build_node(Node& n, const PubKey& pk, const H32& dig, Span sig, std::vector<Leaf>& leaves,
+                const Multisignature* pre = nullptr) {
+  n.op = Node::Const;
+  n.value = false;
+  n.leaf = -1;
+  n.kids.clear();
   switch (pk.kind) {
     case PubKey::Nil:
       n.op = Node::PanicNode;                         // method call on a nil interface
-      return n;
+      return;
     case PubKey::Secp256k1:
     case PubKey::Ed25519: {
-      if (sig.n != 64) { n.op = Node::Const; n.value = false; return n; }
-      Leaf L;
+      if (sig.n != 64) return;                        // false
+      leaves.emplace_back();
+      Leaf& L = leaves.back();
       L.kind = pk.kind == PubKey::Ed25519;
       if (L.kind) memcpy(L.pub.data(), pk.ed.data(), 32);
       else L.pub = pk.secp;
       memcpy(L.sig.data(), sig.p, 64);
       L.dig = dig;                                    // key: leaf_key() on first cache use
       n.op = Node::LeafRef;
-      n.leaf = (int)leaves.size();
-      leaves.push_back(L);
-      return n;
+      n.leaf = (int)leaves.size() - 1;
+      return;
     }
     case PubKey::Multisig: {
-      Multisignature ms;
-      try {
-        ms = decode_multisig(sig);
-      } catch (const AminoErr&) {
-        n.op = Node::Const; n.value = false;     // UnmarshalBinaryBare error -> false
-        return n;
+      Multisignature local;
+      const Multisignature* ms = pre;
+      if (!ms) {
+        try {
+          local = decode_multisig(sig);
+        } catch (const AminoErr&) {
+          return;                                     // UnmarshalBinaryBare error -> false
+        }
+        ms = &local;
       }
-      const int size = ms.bits.size();
-      if ((int)pk.subs.size() != size || ms.sigs.size() < pk.k || (int)ms.sigs.size() > size ||
-          ms.bits.true_bits_before(size) < (int)pk.k) {
-        n.op = Node::Const; n.value = false;
-        return n;
-      }
+      const int size = ms->bits.size();
+      if ((int)pk.subs.size() != size || ms->sigs.size() < pk.k || (int)ms->sigs.size() > size ||
+          ms->bits.true_bits_before(size) < (int)pk.k)
+        return;                                       // false
       n.op = Node::And;
-      n.kids.reserve(ms.sigs.size());
+      n.kids.reserve(ms->sigs.size());
       size_t si = 0;
       for (int i = 0; i < size; ++i) {
-        if (!ms.bits.get(i)) continue;
-        if (si >= ms.sigs.size()) throw Panic("runtime error: index out of range");
-        n.kids.push_back(build_node(pk.subs[i], dig, ms.sigs[si], leaves));
+        if (!ms->bits.get(i)) continue;
+        if (si >= ms->sigs.size()) throw Panic("runtime error: index out of range");
+        n.kids.emplace_back();
+        build_node(n.kids.back(), pk.subs[i], dig, ms->sigs[si], leaves);
         ++si;
       }
-      return n;
+      return;
     }
   }
-  return n;
 }
 
 bool eval(const Node& n, const std::vector<Leaf>& leaves) {
@@ -1159,6 +1168,110 @@ uint64_t fast_hash(const uint8_t* p, size_t n) {
   return h ^ (h >> 29);
 }
 
+// GVH_PROFILE laps: wall time, or (GVH_PROFILE=cpu) the calling thread's CPU
+// time -- with one host thread every stage runs on the caller, so the CPU
+// clock gives the front's cost without the scheduler's noise
+// (tools/front_cost.py).
+double prof_ms() {
+  static const bool cpu = [] {
+    const char* e = getenv("GVH_PROFILE");
+    return e && !strcmp(e, "cpu");
+  }();
+  timespec ts;
+  clock_gettime(cpu ? CLOCK_THREAD_CPUTIME_ID : CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec * 1e-6;
+}
+
+// Open-addressing map from a K-byte public key to a key-arena slot (the
+// account key caches below): one flat array probed linearly, so a lookup costs
+// about one cache miss -- the node-based unordered_map it replaces took ~20 %
+// of a single-threaded C4 block's host front in its bucket walks
+// (tools/front_cost, profiles/r06/front_cost).  The hash mixes 16 key bytes
+// with a per-process random seed: keys are attacker-chosen (a mempool tx
+// names any pubkey), so probe sequences must not be predictable.  Load factor
+// <= 1/2; erase shifts the run back (no tombstones).  Not thread-safe: the
+// callers' key_mu / gpu_mu rules apply as before (concurrent finds only).
+template <size_t K>
+class FlatSlotMap {
+ public:
+  FlatSlotMap() { grow(1024); }
+  const uint32_t* find(const uint8_t* key) const {
+    for (size_t i = hash(key) & mask_;; i = (i + 1) & mask_) {
+      const Ent& e = t_[i];
+      if (!e.full) return nullptr;
+      if (!memcmp(e.key, key, K)) return &e.val;
+    }
+  }
+  // (slot of the key, inserted?) -- an existing key keeps its value
+  std::pair<uint32_t*, bool> emplace(const uint8_t* key, uint32_t val) {
+    if (2 * (n_ + 1) > t_.size()) grow(2 * t_.size());
+    for (size_t i = hash(key) & mask_;; i = (i + 1) & mask_) {
+      Ent& e = t_[i];
+      if (!e.full) {
+        e.full = 1;
+        memcpy(e.key, key, K);
+        e.val = val;
+        ++n_;
+        return {&e.val, true};
+      }
+      if (!memcmp(e.key, key, K)) return {&e.val, false};
+    }
+  }
+  void set(const uint8_t* key, uint32_t val) { *emplace(key, val).first = val; }
+  void erase(const uint8_t* key) {
+    size_t i = hash(key) & mask_;
+    for (;; i = (i + 1) & mask_) {
+      if (!t_[i].full) return;
+      if (!memcmp(t_[i].key, key, K)) break;
+    }
+    // backward-shift deletion: move later members of the run into the hole
+    // when their home slot does not lie cyclically in (hole, j]
+    for (size_t j = (i + 1) & mask_;; j = (j + 1) & mask_) {
+      if (!t_[j].full) break;
+      const size_t home = hash(t_[j].key) & mask_;
+      const bool stays = i <= j ? (home > i && home <= j) : (home > i || home <= j);
+      if (stays) continue;
+      t_[i] = t_[j];
+      i = j;
+    }
+    t_[i].full = 0;
+    --n_;
+  }
+  void clear() {
+    for (Ent& e : t_) e.full = 0;
+    n_ = 0;
+  }
+  size_t size() const { return n_; }
+
+ private:
+  struct Ent {
+    uint32_t val;
+    uint8_t full;
+    uint8_t key[K];
+  };
+  uint64_t hash(const uint8_t* key) const {
+    constexpr size_t o = K == 33 ? 1 : 0;                 // skip a compressed key's prefix byte
+    uint64_t w0, w1;
+    memcpy(&w0, key + o, 8);
+    memcpy(&w1, key + o + 8, 8);
+    uint64_t h = (w0 ^ seed_) * 0x87C37B91114253D5ull;
+    h = (h ^ (h >> 31) ^ w1) * 0x4CF5AD432745937Full;
+    return h ^ (h >> 29);
+  }
+  void grow(size_t cap) {
+    std::vector<Ent> old;
+    old.swap(t_);
+    t_.assign(cap, Ent{});
+    mask_ = cap - 1;
+    n_ = 0;
+    for (const Ent& e : old)
+      if (e.full) emplace(e.key, e.val);
+  }
+  std::vector<Ent> t_;
+  size_t n_ = 0, mask_ = 0;
+  const uint64_t seed_ = ((uint64_t)std::random_device{}() << 32) ^ std::random_device{}();
+};
+
 // A decoded amino pubkey with its canonical bytes (pk.Bytes()), address and
 // CountSubKeys -- pure functions of the amino bytes, shared by every tx and
 // account that carries the same key.
@@ -1301,7 +1414,8 @@ struct Memo {
       p.gas_status = 0;
       p.resolved = false;
       p.owner = 0;
-      p.node = Node{};
+      p.node.op = Node::Const;                       // the kids' capacity is kept (build_node)
+      p.node.kids.clear();
       p.leaves.clear();
     }
     sacc.clear();
@@ -1393,24 +1507,10 @@ struct gvh_app {
   std::mutex gpu_mu;                           // one GPU batch at a time per app
   // account key cache: pub33 -> key-arena slot of the GPU
   // context (gv_keys_load); guarded by gpu_mu.  keyed = 0: pub33 batches.
-  struct Key33Hash {
-    size_t operator()(const std::array<uint8_t, 33>& k) const {
-      uint64_t h;
-      memcpy(&h, k.data() + 1, 8);                // x-coordinate bytes
-      return (size_t)h;
-    }
-  };
-  std::unordered_map<std::array<uint8_t, 33>, uint32_t, Key33Hash> key_slots;
+  FlatSlotMap<33> key_slots;
   // ed25519 keys (IBC validator sets, multisig ed25519 sub-keys): pub32 ->
   // slot of the context's ed25519 key arena (gv_ed_keys_load); gpu_mu
-  struct Key32Hash {
-    size_t operator()(const std::array<uint8_t, 32>& k) const {
-      uint64_t h;
-      memcpy(&h, k.data(), 8);
-      return (size_t)(h * 0x9E3779B97F4A7C15ull);
-    }
-  };
-  std::unordered_map<std::array<uint8_t, 32>, uint32_t, Key32Hash> ed_slots;
+  FlatSlotMap<32> ed_slots;
   uint64_t ed_key_gen = 0;
   uint64_t key_gen = 0;                        // gv_keys_generation the map belongs to
   bool keyed = true;
@@ -1578,7 +1678,8 @@ void parallel_parts(gvh_app* app, int parts, F fn) {
 // DefaultSigVerificationGasConsumer (sigverify.go:299-322) incl. the multisig
 // recursion (ConsumeMultisignatureVerificationGas :325-338, whose nested errors
 // are ignored).  Returns false + err for the top level only.
-bool consume_sig_gas(GasMeter& gm, Span sig, const PubKey& pk, const gvh_app* app, SdkError* err) {
+bool consume_sig_gas(GasMeter& gm, Span sig, const PubKey& pk, const gvh_app* app, SdkError* err,
+                     const Multisignature* pre = nullptr) {
   switch (pk.kind) {
     case PubKey::Ed25519:
       gm.consume(app->cost_ed, "ante verify: ed25519");
@@ -1588,18 +1689,22 @@ bool consume_sig_gas(GasMeter& gm, Span sig, const PubKey& pk, const gvh_app* ap
       gm.consume(app->cost_secp, "ante verify: secp256k1");
       return true;
     case PubKey::Multisig: {
-      Multisignature ms;
-      try {
-        ms = decode_multisig(sig);                   // MustUnmarshalBinaryBare: panics on error
-      } catch (const AminoErr& e) {
-        throw Panic(e.what());
+      Multisignature local;
+      const Multisignature* ms = pre;
+      if (!ms) {
+        try {
+          local = decode_multisig(sig);              // MustUnmarshalBinaryBare: panics on error
+        } catch (const AminoErr& e) {
+          throw Panic(e.what());
+        }
+        ms = &local;
       }
-      const int size = ms.bits.size();
+      const int size = ms->bits.size();
       size_t si = 0;
       for (int i = 0; i < size; ++i) {
-        if (!ms.bits.get(i)) continue;
-        if (si >= ms.sigs.size() || i >= (int)pk.subs.size()) throw Panic("runtime error: index out of range");
-        consume_sig_gas(gm, ms.sigs[si], pk.subs[i], app, nullptr);
+        if (!ms->bits.get(i)) continue;
+        if (si >= ms->sigs.size() || i >= (int)pk.subs.size()) throw Panic("runtime error: index out of range");
+        consume_sig_gas(gm, ms->sigs[si], pk.subs[i], app, nullptr);
         ++si;
       }
       return true;
@@ -1671,16 +1776,28 @@ void make_plan(SignerPlan& p, gvh_app* app, const Tx& tx, size_t signer, std::sh
   p.pub = std::move(pub);
   p.leaves.clear();
   p.resolved = false;
+  // a multisig's signature decoded once, for the gas charge and the node (a
+  // decode error: both decode again and fail as the reference does)
+  Multisignature pre;
+  bool have_pre = false;
+  if (p.pub->pk.kind == PubKey::Multisig) {
+    try {
+      pre = decode_multisig(tx.sigs[signer].sig);
+      have_pre = true;
+    } catch (const AminoErr&) {
+    }
+  }
   try {
     GasMeter g{true, 0};
-    p.gas_status = consume_sig_gas(g, tx.sigs[signer].sig, p.pub->pk, app, nullptr) ? 0 : 1;
+    p.gas_status =
+        consume_sig_gas(g, tx.sigs[signer].sig, p.pub->pk, app, nullptr, have_pre ? &pre : nullptr) ? 0 : 1;
     p.gas = g.used;
   } catch (const Panic&) {
     p.gas_status = 2;
   }
   const H32 dig = gpu_hash ? H32{} : sign_digest(tx, chain_json, accnum, seq);
   p.leaves.reserve((size_t)std::max(1, p.pub->subkeys));
-  p.node = build_node(p.pub->pk, dig, tx.sigs[signer].sig, p.leaves);
+  build_node(p.node, p.pub->pk, dig, tx.sigs[signer].sig, p.leaves, have_pre ? &pre : nullptr);
   bool need_msg = false;
   for (const Leaf& L : p.leaves) need_msg = need_msg || L.kind || gpu_hash;
   if (need_msg) {
@@ -1850,10 +1967,8 @@ void batch_pack(gvh_app* app, GpuBatch& b) {
         memcpy(&b.dig[k * 32], L.dig.data(), 32);
       }
       if (look) {
-        std::array<uint8_t, 33> key;
-        memcpy(key.data(), L.pub.data(), 33);
-        auto it = map.find(key);
-        b.slots[k] = it == map.end() ? UINT32_MAX : it->second;
+        const uint32_t* v = map.find(L.pub.data());
+        b.slots[k] = v ? *v : UINT32_MAX;
       }
     });
   }
@@ -1906,10 +2021,8 @@ int verify_secp(gvh_app* app, GpuBatch& b, uint64_t* ticket = nullptr) {
   }
   if (!b.looked_up || b.gen != gen)               // packed against another arena: look up again
     for (size_t k = 0; k < m; ++k) {
-      std::array<uint8_t, 33> key;
-      memcpy(key.data(), b.pub + 33 * k, 33);
-      auto it = map.find(key);
-      b.slots[k] = it == map.end() ? UINT32_MAX : it->second;
+      const uint32_t* v = map.find(b.pub + 33 * k);
+      b.slots[k] = v ? *v : UINT32_MAX;
     }
   if (m < app->key_load_min) {                    // small batch (CheckTx window, per-tx ante)
     bool all = true;
@@ -1922,12 +2035,12 @@ int verify_secp(gvh_app* app, GpuBatch& b, uint64_t* ticket = nullptr) {
     if (b.slots[k] != UINT32_MAX) continue;
     std::array<uint8_t, 33> key;
     memcpy(key.data(), b.pub + 33 * k, 33);
-    auto ins = map.emplace(key, kPending + (uint32_t)fresh_keys.size());
+    auto ins = map.emplace(key.data(), kPending + (uint32_t)fresh_keys.size());
     if (ins.second) {
       fresh.insert(fresh.end(), key.begin(), key.end());
       fresh_keys.push_back(key);
     }
-    b.slots[k] = ins.first->second;
+    b.slots[k] = *ins.first;
   }
   if (!fresh_keys.empty()) {
     const size_t nf = fresh_keys.size();
@@ -1939,11 +2052,11 @@ int verify_secp(gvh_app* app, GpuBatch& b, uint64_t* ticket = nullptr) {
         map.clear();
         app->key_gen = gv_keys_generation(app->gpu);
       } else {
-        for (auto& key : fresh_keys) map.erase(key);
+        for (auto& key : fresh_keys) map.erase(key.data());
       }
       return plain();
     }
-    for (size_t i = 0; i < nf; ++i) map[fresh_keys[i]] = got[i];
+    for (size_t i = 0; i < nf; ++i) map.set(fresh_keys[i].data(), got[i]);
     for (size_t k = 0; k < m; ++k)
       if (b.slots[k] >= kPending) b.slots[k] = got[b.slots[k] - kPending];
   }
@@ -1975,15 +2088,14 @@ int verify_ed(gvh_app* app, size_t m, const uint8_t* pub, const uint8_t* sig, co
   for (size_t k = 0; k < m; ++k) {
     std::array<uint8_t, 32> key;
     memcpy(key.data(), pub + 32 * k, 32);
-    auto it = map.find(key);
-    if (it != map.end()) { slots[k] = it->second; continue; }
+    if (const uint32_t* v = map.find(key.data())) { slots[k] = *v; continue; }
     if (!load) return gv_verify_ed25519_msgs(app->gpu, m, pub, sig, blob, off, len, ok);
-    auto ins = map.emplace(key, kPending + (uint32_t)fresh_keys.size());
+    auto ins = map.emplace(key.data(), kPending + (uint32_t)fresh_keys.size());
     if (ins.second) {
       fresh.insert(fresh.end(), key.begin(), key.end());
       fresh_keys.push_back(key);
     }
-    slots[k] = ins.first->second;
+    slots[k] = *ins.first;
   }
   if (!fresh_keys.empty()) {
     const size_t nf = fresh_keys.size();
@@ -1995,11 +2107,11 @@ int verify_ed(gvh_app* app, size_t m, const uint8_t* pub, const uint8_t* sig, co
         map.clear();
         app->ed_key_gen = gv_ed_keys_generation(app->gpu);
       } else {
-        for (auto& key : fresh_keys) map.erase(key);
+        for (auto& key : fresh_keys) map.erase(key.data());
       }
       return gv_verify_ed25519_msgs(app->gpu, m, pub, sig, blob, off, len, ok);
     }
-    for (size_t i = 0; i < nf; ++i) map[fresh_keys[i]] = got[i];
+    for (size_t i = 0; i < nf; ++i) map.set(fresh_keys[i].data(), got[i]);
     for (size_t k = 0; k < m; ++k)
       if (slots[k] >= kPending) slots[k] = got[slots[k] - kPending];
   }
@@ -2077,11 +2189,11 @@ int resolve(gvh_app* app, std::vector<Leaf*>& leaves, uint32_t* gpu_leaves, uint
   if (miss.empty()) return GVH_OK;
   if (!app->gpu) return GVH_ENOVERIFIER;
   const bool prof = getenv("GVH_PROFILE") != nullptr;
-  auto tr = std::chrono::steady_clock::now();
+  double tr = prof ? prof_ms() : 0.0;
   auto rlap = [&](const char* what) {
     if (!prof) return;
-    auto t = std::chrono::steady_clock::now();
-    fprintf(stderr, "resolve %s %.3f ms\n", what, std::chrono::duration<double, std::milli>(t - tr).count());
+    const double t = prof_ms();
+    fprintf(stderr, "resolve %s %.3f ms\n", what, t - tr);
     tr = t;
   };
   GpuBatch b;
@@ -2420,12 +2532,12 @@ struct PreState {
 
 void pre_front(gvh_app* app, size_t ntx, const uint8_t* const* txs, const size_t* lens, bool keep,
                uint64_t carry_from, PreState& ps) {
-  auto T0 = std::chrono::steady_clock::now();
   const bool prof = getenv("GVH_PROFILE") != nullptr;
+  double T0 = prof ? prof_ms() : 0.0;
   auto lap = [&](const char* what) {
     if (!prof) return;
-    auto t = std::chrono::steady_clock::now();
-    fprintf(stderr, "preverify %s %.3f ms\n", what, std::chrono::duration<double, std::milli>(t - T0).count());
+    const double t = prof_ms();
+    fprintf(stderr, "preverify %s %.3f ms\n", what, t - T0);
     T0 = t;
   };
   ps.keep = keep;
@@ -2780,6 +2892,8 @@ int deliver_block(gvh_app* app, size_t ntx, const uint8_t* const* txs, const siz
     std::lock_guard<std::mutex> g(app->deferred_mu);
     stale.swap(app->deferred);
   }
+  const bool prof = getenv("GVH_PROFILE") != nullptr;
+  const double p0 = prof ? prof_ms() : 0.0;
   const auto t0 = std::chrono::steady_clock::now();
   int rc;
   {
@@ -2804,6 +2918,7 @@ int deliver_block(gvh_app* app, size_t ntx, const uint8_t* const* txs, const siz
     pre_back(app, ps, rc, nullptr, &memos);
   }
   const auto t1 = std::chrono::steady_clock::now();
+  const double p1 = prof ? prof_ms() : 0.0;
   app->st_pre_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
   if (rc != GVH_OK) {
     release_memos(app, memos);
@@ -2811,17 +2926,15 @@ int deliver_block(gvh_app* app, size_t ntx, const uint8_t* const* txs, const siz
   }
   rc = deliver_memos(app, memos, out, codes);
   const auto t2 = std::chrono::steady_clock::now();
+  const double p2 = prof ? prof_ms() : 0.0;
   app->st_loop_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
   if (app->defer_release) {
     std::lock_guard<std::mutex> g(app->deferred_mu);
     if (app->deferred.empty()) app->deferred.swap(memos);
   }
   release_memos(app, memos);                        // not deferred (option off, or another call's memos wait)
-  if (getenv("GVH_PROFILE"))
-    fprintf(stderr, "deliver preverify %.3f ms loop %.3f ms release %.3f ms\n",
-            std::chrono::duration<double, std::milli>(t1 - t0).count(),
-            std::chrono::duration<double, std::milli>(t2 - t1).count(),
-            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count());
+  if (prof)
+    fprintf(stderr, "deliver preverify %.3f ms loop %.3f ms release %.3f ms\n", p1 - p0, p2 - p1, prof_ms() - p2);
   return rc;
 }
 
