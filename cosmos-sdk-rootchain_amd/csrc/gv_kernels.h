@@ -192,8 +192,9 @@ static_assert(GV_KW_QW * GV_KW_QWIN >= 130, "wide windows cover the GLV halves")
 // for NG x 16 table entries per key (k4: 64).  G as on the k6 ladders: 11
 // signed 24-bit windows of the unsplit u1 after the last doubling from gtab6,
 // on the real curve (one frame change, no per-entry lift).  NG must be one of
-// GV_KG_NGS (the instantiated layouts).
-#define GV_KG_NGS 6, 7, 9
+// GV_KG_NGS (the instantiated layouts); NG = 4 is k4's layout and tables
+// (k_keys_tables) with G after the last doubling.
+#define GV_KG_NGS 4, 6, 7, 9
 #define GV_KG_MAXNG 9
 static_assert(GV_QWIN + GV_K6_GWIN <= GV_DIGIT_ROWS, "kg digits fit the digit rows");
 

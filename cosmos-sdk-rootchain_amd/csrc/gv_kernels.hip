@@ -841,13 +841,56 @@ GV_DEV void gej29_to_affine_words(fe& x8, fe& y8, const gej29& p) {
 // of its own table row (group 0 in kqt, groups 1.. in kqt2 rows slot * (NG -
 // 1) + k - 1); the Jacobian Z of groups 1.. in their Z rows (kzq2, (NG - 1) x
 // 8 rows of stride kC), group 0 is affine (on E').
+// GV_CHAIN_SPLIT 0 (A/B): one lane per key runs ParsePubKey, then the
+// doublings on E itself (u = 1 in kzq), as in rounds 3-5.
+#ifndef GV_CHAIN_SPLIT
+#define GV_CHAIN_SPLIT 1
+#endif
 template <int QW, int NG>
 __global__ __launch_bounds__(512) GV_FRONT_ATTR void k_keys_chain(u32 n, u32 C, const u32* in_x, const u32* in_pfx, u32 base,
                                                      u32* kqt, u32 kC, u32* kok, u32* kqt2, u32* kzq2, u32* kzq) {
   using L = KLayout<QW, NG>;
+#if GV_CHAIN_SPLIT
   const bool root = threadIdx.x < 256u;                 // wave-uniform role
   const u32 g = blockIdx.x * 256u + (threadIdx.x & 255u);
+#else
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+#endif
   if (g >= n) return;                       // no cross-lane work
+#if !GV_CHAIN_SPLIT
+  {
+    fe x, y;
+    load_fe(x, in_x, C, g);
+    const bool ok = parse_pubkey(in_pfx[g], x, y);
+    if (!ok) {
+      fe_from_const(x, kGx);
+      fe_from_const(y, kGy);
+    }
+    kok[base + g] = ok ? 1u : 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kzq[(size_t)i * kC + base + g] = i == 0 ? 1u : 0u;   // u = 1: the chain runs on E
+    u32* p = kqt + (size_t)(base + g) * L::NT * L::EW;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { p[i] = x.v[i]; p[8 + i] = y.v[i]; }
+    gej29 q;
+    f29_from_words(q.x, x.v);
+    f29_from_words(q.y, y.v);
+    f29_set_u32(q.z, 1);
+#pragma unroll 1
+    for (int grp = 1; grp < NG; ++grp) {
+#pragma unroll 1
+      for (int k = L::bit(grp - 1); k < L::bit(grp); ++k) gej29x_double(q, q);
+      u32 xw[8], yw[8];
+      f29_to_words(xw, q.x);
+      f29_to_words(yw, q.y);
+      u32* t = kqt2 + (size_t)((base + g) * (NG - 1) + (grp - 1)) * L::NT * L::EW;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { t[i] = xw[i]; t[8 + i] = yw[i]; }
+      store_f29(kzq2 + (size_t)(grp - 1) * 8 * kC, kC, base + g, q.z);
+    }
+    return;
+  }
+#else
   fe x;
   load_fe(x, in_x, C, g);
   fe29 x29, c;
@@ -909,6 +952,7 @@ __global__ __launch_bounds__(512) GV_FRONT_ATTR void k_keys_chain(u32 n, u32 C, 
     park(kqt2, (base + g) * (NG - 1) + (grp - 1), xw, yw);
     store_f29(kzq2 + (size_t)(grp - 1) * 8 * kC, kC, base + g, q.z);
   }
+#endif
 }
 
 // k_keys_tables (lane L = 4 key + group, the four groups of a key in adjacent
@@ -1762,22 +1806,24 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gta
     KLayout<QW, NG>::F(11), KLayout<QW, NG>::F(12), KLayout<QW, NG>::F(13), KLayout<QW, NG>::F(14), \
     KLayout<QW, NG>::F(15), KLayout<QW, NG>::F(16), KLayout<QW, NG>::F(17), KLayout<QW, NG>::F(18)
 // rows 4.. : the grouped route's 5-bit many-group layouts (GV_KG_NGS)
-__constant__ const int kKnW0[7][19] = {
+__constant__ const int kKnW0[8][19] = {
     {GV_KN_ROW(6, 4, w0)},
     {GV_KN_ROW(6, GV_KN_ARENA_NG, w0)},
     {GV_KN_ROW(GV_KW_QW, GV_KW_NG2, w0)},
     {GV_KN_ROW(GV_KW_QW, GV_KW_NG1, w0)},
     {GV_KN_ROW(GV_QW, 6, w0)},
     {GV_KN_ROW(GV_QW, 7, w0)},
-    {GV_KN_ROW(GV_QW, 9, w0)}};
-__constant__ const int kKnNW[7][19] = {
+    {GV_KN_ROW(GV_QW, 9, w0)},
+    {GV_KN_ROW(GV_QW, 4, w0)}};
+__constant__ const int kKnNW[8][19] = {
     {GV_KN_ROW(6, 4, nw)},
     {GV_KN_ROW(6, GV_KN_ARENA_NG, nw)},
     {GV_KN_ROW(GV_KW_QW, GV_KW_NG2, nw)},
     {GV_KN_ROW(GV_KW_QW, GV_KW_NG1, nw)},
     {GV_KN_ROW(GV_QW, 6, nw)},
     {GV_KN_ROW(GV_QW, 7, nw)},
-    {GV_KN_ROW(GV_QW, 9, nw)}};
+    {GV_KN_ROW(GV_QW, 9, nw)},
+    {GV_KN_ROW(GV_QW, 4, nw)}};
 #undef GV_KN_ROW
 static_assert(GV_KN_ARENA_NG <= 16 && GV_KW_NG1 <= 19, "layout table rows");
 
@@ -1789,6 +1835,7 @@ constexpr int kn_row(int qw, int ng) {
          : qw == GV_QW && ng == 6              ? 4
          : qw == GV_QW && ng == 7              ? 5
          : qw == GV_QW && ng == 9              ? 6
+         : qw == GV_QW && ng == 4              ? 7
                                                : -1;
 }
 // GV_KN_GFRAME (default 1, round 6): after the last Q entry the accumulator
@@ -2092,7 +2139,9 @@ hipError_t gvk_verify(const gvk_batch* b, hipStream_t st) {
 #define GV_KG_LAUNCH(NG)                                                                                      \
   hipLaunchKernelGGL((gv::k_ecmult_kn<GV_QW, NG>), grd, blk, 0, se, b->gtab6, b->n, C, b->digits, b->kqt, b->kqt2, \
                      b->kzq, b->flags, b->in_r, sorted ? b->srt.bits : b->bits, (const uint32_t*)b->in_pfx, b->kC)
-  if (kg && b->k6 == 6)
+  if (kg && b->k6 == 4)
+    GV_KG_LAUNCH(4);
+  else if (kg && b->k6 == 6)
     GV_KG_LAUNCH(6);
   else if (kg && b->k6 == 7)
     GV_KG_LAUNCH(7);
@@ -2164,8 +2213,8 @@ static hipError_t keys_tables_launch(uint32_t n, uint32_t C, const uint32_t* in_
   uint32_t* qr = scratch;
   uint32_t* er = qr + (size_t)(NT - 2) * 9 * CL;
   uint32_t* qe = with_qe ? er + (size_t)9 * CL : nullptr;
-  hipLaunchKernelGGL((gv::k_keys_chain<QW, NG>), dim3((n + 255) / 256), dim3(512), 0, st, n, C, in_x, in_pfx, base,
-                     kqt, kC, kok, kqt2, kzq2, kzq);
+  hipLaunchKernelGGL((gv::k_keys_chain<QW, NG>), dim3((n + 255) / 256), dim3(GV_CHAIN_SPLIT ? 512 : 256), 0, st, n, C,
+                     in_x, in_pfx, base, kqt, kC, kok, kqt2, kzq2, kzq);
   if (NG == 4) {
     // four groups: one launch, the quad trades its Zs by lane shuffles (the
     // last entry stays in registers; the E rows are unused)
@@ -2196,6 +2245,7 @@ hipError_t gvk_keys_build_rows_kg(uint32_t n, uint32_t C, const uint32_t* in_x, 
                                   uint32_t* scratch, int with_qe, uint32_t* kqt, uint32_t* kzq, uint32_t kC,
                                   uint32_t* kok, uint32_t* kqt2, uint32_t* kzq2, int ng, hipStream_t st) {
   switch (ng) {
+    case 4: return keys_tables_launch<GV_QW, 4>(n, C, in_x, in_pfx, scratch, with_qe, 0u, kqt, kzq, kC, kok, kqt2, kzq2, st);
     case 6: return keys_tables_launch<GV_QW, 6>(n, C, in_x, in_pfx, scratch, with_qe, 0u, kqt, kzq, kC, kok, kqt2, kzq2, st);
     case 7: return keys_tables_launch<GV_QW, 7>(n, C, in_x, in_pfx, scratch, with_qe, 0u, kqt, kzq, kC, kok, kqt2, kzq2, st);
     case 9: return keys_tables_launch<GV_QW, 9>(n, C, in_x, in_pfx, scratch, with_qe, 0u, kqt, kzq, kC, kok, kqt2, kzq2, st);

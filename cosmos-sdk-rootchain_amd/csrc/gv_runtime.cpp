@@ -38,6 +38,7 @@
 #include "../../include/gpuverify.h"
 #include "gv_kernels.h"
 #include "gv_stage.h"
+#include "gv_async.h"
 
 namespace {
 
@@ -1686,27 +1687,12 @@ int run_host(gv_ctx* ctx, size_t n, const HostBatch& hb_in) {
 // before they return.  A batch is done when every device's slice has been
 // harvested; gv_wait returns its result.  The lane holds the device lock from
 // its first queued slice until its queue is empty and every chunk harvested.
-struct AsyncJob {
-  HostBatch hb;
-  int left = 0;                                   // device slices not finished (AsyncState::m)
-  int rc = GV_OK;
-  bool done = false;
+// The queue, tickets and quiesce are gv_async.h (also driven by the CPU
+// harness with fake devices); the lane body is lane_stream below.
+struct AsyncState : gvasync::Lanes<HostBatch> {
+  using gvasync::Lanes<HostBatch>::Lanes;
 };
-struct AsyncSlice {
-  std::shared_ptr<AsyncJob> job;
-  size_t lo = 0, hi = 0;
-};
-struct AsyncState {
-  std::mutex m;
-  std::condition_variable cv;                     // lanes: work or quit; waiters: a job done
-  std::vector<std::deque<AsyncSlice>> q;          // per device
-  std::vector<std::thread> lanes;
-  std::unordered_map<uint64_t, std::shared_ptr<AsyncJob>> jobs;
-  uint64_t next_ticket = 1;
-  size_t pending = 0;                             // jobs submitted, not done
-  int quiescing = 0;                              // gv_keys_load / gv_keys_reset in progress: submissions wait
-  bool quit = false;
-};
+using AsyncSlice = gvasync::Slice<HostBatch>;
 
 namespace {
 
@@ -1725,14 +1711,7 @@ void finish_slice(AsyncState* as, ActiveSlice& a) {
     const int rc = set_release(a.g, a.g->st);
     if (rc && !a.rc) a.rc = rc;
   }
-  std::lock_guard<std::mutex> lk(as->m);
-  AsyncJob& j = *a.sl.job;
-  if (a.rc && !j.rc) j.rc = a.rc;
-  if (--j.left == 0) {
-    j.done = true;
-    --as->pending;
-  }
-  as->cv.notify_all();
+  as->finish(a.sl, a.rc);
 }
 
 // Runs device k's queued slices (d->mu held) until the queue is empty, then
@@ -1762,12 +1741,7 @@ void lane_stream(gv_ctx* ctx, AsyncState* as, size_t k, Dev* d) {
   };
   for (;;) {
     AsyncSlice sl;
-    {
-      std::lock_guard<std::mutex> lk(as->m);
-      if (as->q[k].empty()) break;
-      sl = as->q[k].front();
-      as->q[k].pop_front();
-    }
+    if (!as->pop(k, sl)) break;
     act.emplace_back();
     ActiveSlice& a = act.back();
     a.sl = sl;
@@ -1807,61 +1781,31 @@ void lane_stream(gv_ctx* ctx, AsyncState* as, size_t k, Dev* d) {
   drain();
 }
 
-void lane_main(gv_ctx* ctx, AsyncState* as, size_t k) {
+// Device k's lane body (gvasync::Lanes calls it when k's queue holds a slice).
+void lane_run(gv_ctx* ctx, AsyncState* as, size_t k) {
   Dev* d = ctx->devs[k];
-  for (;;) {
-    {
-      std::unique_lock<std::mutex> lk(as->m);
-      as->cv.wait(lk, [&] { return as->quit || !as->q[k].empty(); });
-      if (as->q[k].empty()) return;               // quit, nothing left
-    }
-    std::lock_guard<std::mutex> dl(d->mu);
-    if (hipSetDevice(d->id) != hipSuccess) {      // fail every queued slice of this device
-      std::lock_guard<std::mutex> lk(as->m);
-      for (AsyncSlice& sl : as->q[k]) {
-        if (!sl.job->rc) sl.job->rc = GV_EHIP;
-        if (--sl.job->left == 0) { sl.job->done = true; --as->pending; }
-      }
-      as->q[k].clear();
-      as->cv.notify_all();
-      continue;
-    }
-    lane_stream(ctx, as, k, d);
+  std::lock_guard<std::mutex> dl(d->mu);
+  if (hipSetDevice(d->id) != hipSuccess) {        // fail every queued slice of this device
+    as->fail_queued(k, GV_EHIP);
+    return;
   }
+  lane_stream(ctx, as, k, d);
 }
 
 AsyncState* async_state(gv_ctx* ctx) {
   static std::mutex create_mu;
   std::lock_guard<std::mutex> lk(create_mu);
   if (!ctx->async) {
-    AsyncState* as = new AsyncState();
-    as->q.resize(ctx->devs.size());
-    for (size_t k = 0; k < ctx->devs.size(); ++k) as->lanes.emplace_back(lane_main, ctx, as, k);
-    ctx->async = as;
+    // (a lane runs only for a submitted slice, i.e. after ctx->async is set)
+    ctx->async = new AsyncState(ctx->devs.size(), [ctx](size_t k) { lane_run(ctx, ctx->async, k); });
   }
   return ctx->async;
 }
 
-// Held by gv_keys_load / gv_keys_reset: waits until no submitted batch is
-// pending (the key arenas change meaning under a keyed batch otherwise), and
-// new submissions wait until it is released -- a caller that keeps queueing
-// batches can neither starve the load nor slip a batch in under it.
-struct AsyncQuiesce {
-  AsyncState* as;
-  explicit AsyncQuiesce(gv_ctx* ctx) : as(ctx->async) {
-    if (!as) return;
-    std::unique_lock<std::mutex> lk(as->m);
-    ++as->quiescing;
-    as->cv.wait(lk, [&] { return as->pending == 0; });
-  }
-  ~AsyncQuiesce() {
-    if (!as) return;
-    std::lock_guard<std::mutex> lk(as->m);
-    --as->quiescing;
-    as->cv.notify_all();
-  }
-  AsyncQuiesce(const AsyncQuiesce&) = delete;
-  AsyncQuiesce& operator=(const AsyncQuiesce&) = delete;
+// Held by gv_keys_load / gv_keys_reset (gvasync::Lanes::Quiesce): no
+// submitted keyed batch reads a slot that moves, and no submission slips in.
+struct AsyncQuiesce : gvasync::Lanes<HostBatch>::Quiesce {
+  explicit AsyncQuiesce(gv_ctx* ctx) : Quiesce(ctx->async) {}
 };
 
 int submit_host(gv_ctx* ctx, size_t n, const HostBatch& hb_in, uint64_t* ticket) {
@@ -1872,26 +1816,10 @@ int submit_host(gv_ctx* ctx, size_t n, const HostBatch& hb_in, uint64_t* ticket)
     if ((!hb_in.pub33 && !hb_in.slots) || !hb_in.sig64 || (!hb_in.out_ok && !hb_in.out_bits)) return GV_EINVAL;
     if (!hb_in.dig32 && (!hb_in.blob || !hb_in.off || !hb_in.len)) return GV_EINVAL;
   }
-  auto job = std::make_shared<AsyncJob>();
-  job->hb = hb_in;
-  job->hb.pinned = hb_in.dig32 && is_pinned(hb_in.slots ? (const void*)hb_in.slots : hb_in.pub33) &&
-                   is_pinned(hb_in.sig64) && is_pinned(hb_in.dig32);
-  AsyncState* as = async_state(ctx);
-  const size_t nd = ctx->devs.size(), per = round_up((n + nd - 1) / std::max<size_t>(nd, 1), 256);
-  std::unique_lock<std::mutex> lk(as->m);
-  as->cv.wait(lk, [&] { return as->quiescing == 0; });   // a key load / reset in progress
-  for (size_t k = 0; k < nd; ++k) {
-    const size_t lo = std::min(n, k * per), hi = std::min(n, (k + 1) * per);
-    if (lo >= hi) continue;
-    as->q[k].push_back(AsyncSlice{job, lo, hi});
-    ++job->left;
-  }
-  if (job->left == 0) job->done = true;
-  else ++as->pending;
-  const uint64_t t = as->next_ticket++;
-  as->jobs.emplace(t, job);
-  *ticket = t;
-  as->cv.notify_all();
+  HostBatch hb = hb_in;
+  hb.pinned = hb_in.dig32 && is_pinned(hb_in.slots ? (const void*)hb_in.slots : hb_in.pub33) &&
+              is_pinned(hb_in.sig64) && is_pinned(hb_in.dig32);
+  *ticket = async_state(ctx)->submit(hb, n);
   return GV_OK;
 }
 
@@ -2072,12 +2000,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
 void gv_close(gv_ctx* ctx) {
   if (!ctx) return;
   if (AsyncState* as = ctx->async) {              // the lanes finish what is queued, then quit
-    {
-      std::lock_guard<std::mutex> lk(as->m);
-      as->quit = true;
-    }
-    as->cv.notify_all();
-    for (std::thread& t : as->lanes) t.join();
+    as->close();
     delete as;
     ctx->async = nullptr;
   }
@@ -2194,14 +2117,7 @@ int gv_submit_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, const uint
 
 int gv_wait(gv_ctx* ctx, uint64_t ticket) {
   if (!ctx || !ctx->async) return GV_EINVAL;
-  AsyncState* as = ctx->async;
-  std::unique_lock<std::mutex> lk(as->m);
-  auto it = as->jobs.find(ticket);
-  if (it == as->jobs.end()) return GV_EINVAL;
-  std::shared_ptr<AsyncJob> j = it->second;
-  as->cv.wait(lk, [&] { return j->done; });
-  as->jobs.erase(ticket);
-  return j->rc;
+  return ctx->async->wait(ticket, GV_EINVAL);
 }
 
 int gv_dev_verify_digests(gv_ctx* ctx, int dev_slot, size_t n, const void* d_pub33,

@@ -29,9 +29,9 @@ pytestmark = pytest.mark.gpu
 KG_DEFAULT = gvm.Verifier.KG_DEFAULT            # the library's default "kg" layout (0: k4 on the grouped route)
 SCHEDULES = {"k4f": {"gfull": 1, "k6": 0, "kg": 0}, "k4": {"gfull": 0, "k6": 0, "kg": 0},
              "k6": {"gfull": 1, "k6": 1, "kg": 0},
-             "kg6": {"kg": 6}, "kg7": {"kg": 7}, "kg9": {"kg": 9},
+             "kg4": {"kg": 4}, "kg6": {"kg": 6}, "kg7": {"kg": 7}, "kg9": {"kg": 9},
              "item_gf": {"group_keys": 0, "gfull_item": 1}, "item_glv": {"group_keys": 0, "gfull_item": 0}}
-ROUTE = {"k4f": "k4f", "k4": "k4", "k6": "k6", "kg6": "kg", "kg7": "kg", "kg9": "kg", "wide": "k6", "wide2": "k6",
+ROUTE = {"k4f": "k4f", "k4": "k4", "k6": "k6", "kg4": "kg", "kg6": "kg", "kg7": "kg", "kg9": "kg", "wide": "k6", "wide2": "k6",
          "item_gf": "item_f", "item_glv": "pub33"}
 DEFAULTS = {"gfull": 1, "k6": 0, "kg": KG_DEFAULT, "group_keys": 1, "gfull_item": 1, "keys_k6": 1, "keys_wide": 2,
             "keys_wide1_cap": 0}

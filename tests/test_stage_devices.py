@@ -4,7 +4,9 @@ harness tests/stage/stage_harness.cpp with fake devices (a sleep stands in
 for H2D + kernels).  A host batch's slices must all be in flight at once
 (each slice waits at a barrier for the others), every device must stage
 through its own pool (no thread shared between devices), every staged byte
-must match the caller's, and the ThreadSanitizer build must be clean."""
+must match the caller's, and the ThreadSanitizer build must be clean.  The
+asynchronous host-batch queue (csrc/gv_async.h) runs over the same fake
+devices (tests/stage/async_harness.cpp)."""
 import json
 import os
 import subprocess
@@ -18,6 +20,22 @@ HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "stage")
 def harness():
     subprocess.run(["make", "-s", "-C", HERE], check=True)
     return os.path.join(HERE, "stage_harness"), os.path.join(HERE, "stage_harness_tsan")
+
+
+@pytest.mark.parametrize("nd,subs,per,tsan", [(4, 3, 12, False), (8, 4, 8, False), (4, 3, 6, True)])
+def test_async_queue_over_fake_devices(harness, nd, subs, per, tsan):
+    """gv_submit_* / gv_wait's queue (csrc/gv_async.h) over >= 4
+    fake devices: the first batch's slices all in flight at once, ragged
+    batches from several submitter threads waited out of order with every
+    verdict byte right, tickets waited once, a quiescing key loader that never
+    sees a pending batch or a running slice, a failing device failing only the
+    batches it holds -- and, built with ThreadSanitizer, no data race."""
+    exe = os.path.join(HERE, "async_harness_tsan" if tsan else "async_harness")
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:exitcode=66") if tsan else None
+    out = run(exe, nd, subs, per, 100 if tsan else 200, env=env)
+    assert out["ok"] and out["concurrent"] and out["bad_bytes"] == 0, out
+    assert out["waited"] == subs * per and out["quiesces"] > 0 and out["quiesce_violations"] == 0, out
+    assert out["failed_device_rc"] != 0 and out["other_devices_rc"] == 0 and out["tickets_left"] == 0, out
 
 
 def run(exe, *args, env=None):
