@@ -1855,6 +1855,44 @@ constexpr int kn_row(int qw, int ng) {
 #else
 #define GV_KN_ATTR __attribute__((amdgpu_waves_per_eu(GV_KN_WAVES)))
 #endif
+// GV_KN_ZQ_LDS (round 6): with the G frame change zq is read once, at the
+// end; held in registers across the ladder it takes the kn ladders to 160
+// VGPRs (3 waves per SIMD, 32 VGPRs left for a front kernel's wave), parked in
+// LDS (9 KB per block) they compile to 122-126 VGPRs: 4 waves per SIMD.
+#ifndef GV_KN_ZQ_LDS
+#define GV_KN_ZQ_LDS 0
+#endif
+// GV_KN_PREFETCH (A/B, round 6): the slot loop runs one slot ahead -- slot
+// s + 1's digit is read and its table entry's loads issued before slot s's
+// addition, so the gather's latency hides under ~1.5k VALU of the addition
+// instead of stalling the wave (the resident arena's wide tables are read
+// from HBM: VALU busy 0.83 at round 5).  Same additions in the same order.
+#ifndef GV_KN_PREFETCH
+#define GV_KN_PREFETCH 0
+#endif
+// raw table-entry words in flight: Q entries (EW words), G entries (16 words)
+template <int NT, int EW>
+GV_DEV void fetch_qent(uint4* r, const u32* qt, u32 g, u32 j) {
+  const uint4* p = (const uint4*)(qt + ((size_t)g * NT + j) * EW);
+  r[0] = p[0]; r[1] = p[1]; r[2] = p[2]; r[3] = p[3];
+  if constexpr (EW != 16) r[4] = p[4];
+}
+template <int EW>
+GV_DEV void unpack_qent(fe29& x, fe29& y, const uint4* r) {
+  if constexpr (EW == 16) {
+    const u32 xw[8] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w};
+    const u32 yw[8] = {r[2].x, r[2].y, r[2].z, r[2].w, r[3].x, r[3].y, r[3].z, r[3].w};
+    f29_from_words(x, xw);
+    f29_from_words(y, yw);
+  } else {
+    x.n[0] = r[0].x; x.n[1] = r[0].y; x.n[2] = r[0].z; x.n[3] = r[0].w;
+    x.n[4] = r[1].x; x.n[5] = r[1].y; x.n[6] = r[1].z; x.n[7] = r[1].w;
+    x.n[8] = r[2].x; y.n[0] = r[2].y; y.n[1] = r[2].z; y.n[2] = r[2].w;
+    y.n[3] = r[3].x; y.n[4] = r[3].y; y.n[5] = r[3].z; y.n[6] = r[3].w;
+    y.n[7] = r[4].x; y.n[8] = r[4].y;
+  }
+}
+
 template <int QW, int NG>
 __global__ __launch_bounds__(256) GV_KN_ATTR void k_ecmult_kn(const u32* gtab6, u32 n, u32 C, const u32* digits,
                                                         const u32* kqt, const u32* kqt2, const u32* kzq,
@@ -1867,6 +1905,11 @@ __global__ __launch_bounds__(256) GV_KN_ATTR void k_ecmult_kn(const u32* gtab6, 
   const u32 qi = qidx[g];
   fe29 zq;
   load_f29(zq, kzq, kC, qi);
+#if GV_KN_ZQ_LDS
+  __shared__ u32 zq_lds[9][256];                 // zq parked in LDS until the frame change
+#pragma unroll
+  for (int i = 0; i < 9; ++i) zq_lds[i][threadIdx.x] = zq.n[i];
+#endif
   gej29 acc;
   f29_set_zero(acc.x); f29_set_zero(acc.y); f29_set_zero(acc.z);
   bool inf = true;
@@ -1878,6 +1921,68 @@ __global__ __launch_bounds__(256) GV_KN_ATTR void k_ecmult_kn(const u32* gtab6, 
     }
     // slots 0..NG-1: Q of groups 0..NG-1; NG..2NG-1: lambda Q of groups
     // NG-1..0 on the lambda^2 frame; then (position 0) the 11 G windows
+    // (the wide-window ladders only: the others would pass 168 VGPRs, 2 waves)
+    if constexpr (GV_KN_PREFETCH && QW == GV_KW_QW) {
+    constexpr int NSLOT = 2 * NG + GV_K6_GWIN;
+    // slot s's digit (0: nothing to add -- a window past the group's, or G
+    // off position 0) and the issue of its entry's loads into r
+    auto fetch = [&](int slot, uint4* r) -> int {
+      if (slot >= 2 * NG) {
+        if (pos != 0) return 0;
+        const int j = slot - 2 * NG;
+        const int d = (int)digits[(size_t)(L::QWIN + j) * C + g];
+        if (d) {
+          const uint4* p = (const uint4*)(gtab6 + (size_t)j * GV_K6_GTAB_N * 16 + (size_t)((d < 0 ? -d : d) - 1) * 16);
+          r[0] = p[0]; r[1] = p[1]; r[2] = p[2]; r[3] = p[3];
+        }
+        return d;
+      }
+      const bool lam = slot >= NG;
+      const int grp = lam ? 2 * NG - 1 - slot : slot;
+      if (pos >= kKnNW[T][grp]) return 0;
+      const u32 dq = digits[(size_t)(kKnW0[T][grp] + pos) * C + g];
+      const int d = lam ? ((int)dq >> 16) : ((int)(dq << 16) >> 16);
+      if (d) fetch_qent<L::NT, L::EW>(r, grp == 0 ? kqt : kqt2, grp == 0 ? qi : qi * (NG - 1) + (grp - 1),
+                                        (u32)((d < 0 ? -d : d) - 1));
+      return d;
+    };
+    uint4 rn[5];
+    int dn = fetch(0, rn);
+#pragma unroll 1
+    for (int slot = 0; slot < NSLOT; ++slot) {
+      uint4 rc[5] = {rn[0], rn[1], rn[2], rn[3], rn[4]};
+      const int d = dn;
+      if (slot + 1 < NSLOT) dn = fetch(slot + 1, rn);
+      if ((slot == NG || slot == 2 * NG) && !inf) {
+        fe29 c;                                            // into lambda^2 (acc) / back to acc
+        f29_from_const(c, slot == NG ? kBeta2 : kBeta);
+        f29x_mul(acc.x, acc.x, c);
+      }
+      if (slot >= 2 * NG && pos != 0) break;               // wave-uniform: G after the last doubling
+      if (GV_KN_GFRAME && slot == 2 * NG && !inf) {
+        fe29 z;
+#if GV_KN_ZQ_LDS
+#pragma unroll
+        for (int i = 0; i < 9; ++i) zq.n[i] = zq_lds[i][threadIdx.x];
+#endif
+        f29x_mul(z, acc.z, zq);
+        acc.z = z;
+      }
+      if (d == 0) continue;
+      const bool isg = slot >= 2 * NG;
+      fe29 x, y;
+      if (!isg) {
+        unpack_qent<L::EW>(x, y, rc);
+      } else {
+        const u32 xw[8] = {rc[0].x, rc[0].y, rc[0].z, rc[0].w, rc[1].x, rc[1].y, rc[1].z, rc[1].w};
+        const u32 yw[8] = {rc[2].x, rc[2].y, rc[2].z, rc[2].w, rc[3].x, rc[3].y, rc[3].z, rc[3].w};
+        f29_from_words(x, xw);
+        f29_from_words(y, yw);
+      }
+      if (d < 0) f29_neg<1>(y, y);                         // 2
+      add_entry(acc, inf, x, y, isg && !GV_KN_GFRAME ? &zq : nullptr);
+    }
+    } else {
 #pragma unroll 1
     for (int slot = 0; slot < 2 * NG + GV_K6_GWIN; ++slot) {
       if ((slot == NG || slot == 2 * NG) && !inf) {
@@ -1891,6 +1996,10 @@ __global__ __launch_bounds__(256) GV_KN_ATTR void k_ecmult_kn(const u32* gtab6, 
         // (X, Y, Z zq), so the G entries are added unlifted (az = Z) and the
         // final check reads Z as is
         fe29 z;
+#if GV_KN_ZQ_LDS
+#pragma unroll
+        for (int i = 0; i < 9; ++i) zq.n[i] = zq_lds[i][threadIdx.x];
+#endif
         f29x_mul(z, acc.z, zq);
         acc.z = z;
       }
@@ -1918,6 +2027,7 @@ __global__ __launch_bounds__(256) GV_KN_ATTR void k_ecmult_kn(const u32* gtab6, 
       else load_gent29(x, y, tab, e);
       if (d < 0) f29_neg<1>(y, y);                         // 2
       add_entry(acc, inf, x, y, isg && !GV_KN_GFRAME ? &zq : nullptr);
+    }
     }
   }
   // GV_KN_GFRAME: acc is on the real curve (or infinite: rejected either way)
