@@ -841,10 +841,14 @@ GV_DEV void gej29_to_affine_words(fe& x8, fe& y8, const gej29& p) {
 // of its own table row (group 0 in kqt, groups 1.. in kqt2 rows slot * (NG -
 // 1) + k - 1); the Jacobian Z of groups 1.. in their Z rows (kzq2, (NG - 1) x
 // 8 rows of stride kC), group 0 is affine (on E').
-// GV_CHAIN_SPLIT 0 (A/B): one lane per key runs ParsePubKey, then the
-// doublings on E itself (u = 1 in kzq), as in rounds 3-5.
+// GV_CHAIN_SPLIT 0 (the default): one lane per key runs ParsePubKey, then
+// the doublings on E itself (u = 1 in kzq), as in rounds 3-5.  1: the root
+// and chain roles above -- the serialized key stage is ~10 % shorter, but the
+// pipelined C2 step loses 4-5 % (216 vs 226M/s alternated on one box,
+// profiles/r06/ab3): the 512-thread blocks wait for two free wave slots on
+// every SIMD of a CU, which the previous call's ladder holds.
 #ifndef GV_CHAIN_SPLIT
-#define GV_CHAIN_SPLIT 1
+#define GV_CHAIN_SPLIT 0
 #endif
 template <int QW, int NG>
 __global__ __launch_bounds__(512) GV_FRONT_ATTR void k_keys_chain(u32 n, u32 C, const u32* in_x, const u32* in_pfx, u32 base,
@@ -1855,12 +1859,14 @@ constexpr int kn_row(int qw, int ng) {
 #else
 #define GV_KN_ATTR __attribute__((amdgpu_waves_per_eu(GV_KN_WAVES)))
 #endif
-// GV_KN_ZQ_LDS (round 6): with the G frame change zq is read once, at the
-// end; held in registers across the ladder it takes the kn ladders to 160
-// VGPRs (3 waves per SIMD, 32 VGPRs left for a front kernel's wave), parked in
-// LDS (9 KB per block) they compile to 122-126 VGPRs: 4 waves per SIMD.
+// GV_KN_ZQ_LDS (round 6, the 5-bit kg ladders only): with the G frame
+// change zq is read once, at the end; held in registers across the ladder it
+// takes k_ecmult_kn<5, NG> to 160 VGPRs (3 waves per SIMD, 32 VGPRs left for a
+// front kernel's wave), parked in LDS (9 KB per block) to 126: 4 waves per
+// SIMD (kg4: C2 216 -> 222M/s alternated, profiles/r06/ab3).  The arena's
+// ladders keep zq in registers (kw at 133 VGPRs: 440 vs 428M/s with LDS).
 #ifndef GV_KN_ZQ_LDS
-#define GV_KN_ZQ_LDS 0
+#define GV_KN_ZQ_LDS 1
 #endif
 // GV_KN_PREFETCH (A/B, round 6): the slot loop runs one slot ahead -- slot
 // s + 1's digit is read and its table entry's loads issued before slot s's
@@ -1905,11 +1911,12 @@ __global__ __launch_bounds__(256) GV_KN_ATTR void k_ecmult_kn(const u32* gtab6, 
   const u32 qi = qidx[g];
   fe29 zq;
   load_f29(zq, kzq, kC, qi);
-#if GV_KN_ZQ_LDS
-  __shared__ u32 zq_lds[9][256];                 // zq parked in LDS until the frame change
+  constexpr bool ZL = GV_KN_ZQ_LDS && GV_KN_GFRAME && QW == GV_QW;
+  __shared__ u32 zq_lds[ZL ? 9 : 1][256];        // ZL: zq parked in LDS until the frame change
+  if constexpr (ZL) {
 #pragma unroll
-  for (int i = 0; i < 9; ++i) zq_lds[i][threadIdx.x] = zq.n[i];
-#endif
+    for (int i = 0; i < 9; ++i) zq_lds[i][threadIdx.x] = zq.n[i];
+  }
   gej29 acc;
   f29_set_zero(acc.x); f29_set_zero(acc.y); f29_set_zero(acc.z);
   bool inf = true;
@@ -1961,10 +1968,10 @@ __global__ __launch_bounds__(256) GV_KN_ATTR void k_ecmult_kn(const u32* gtab6, 
       if (slot >= 2 * NG && pos != 0) break;               // wave-uniform: G after the last doubling
       if (GV_KN_GFRAME && slot == 2 * NG && !inf) {
         fe29 z;
-#if GV_KN_ZQ_LDS
+        if constexpr (ZL) {
 #pragma unroll
-        for (int i = 0; i < 9; ++i) zq.n[i] = zq_lds[i][threadIdx.x];
-#endif
+          for (int i = 0; i < 9; ++i) zq.n[i] = zq_lds[i][threadIdx.x];
+        }
         f29x_mul(z, acc.z, zq);
         acc.z = z;
       }
@@ -1996,10 +2003,10 @@ __global__ __launch_bounds__(256) GV_KN_ATTR void k_ecmult_kn(const u32* gtab6, 
         // (X, Y, Z zq), so the G entries are added unlifted (az = Z) and the
         // final check reads Z as is
         fe29 z;
-#if GV_KN_ZQ_LDS
+        if constexpr (ZL) {
 #pragma unroll
-        for (int i = 0; i < 9; ++i) zq.n[i] = zq_lds[i][threadIdx.x];
-#endif
+          for (int i = 0; i < 9; ++i) zq.n[i] = zq_lds[i][threadIdx.x];
+        }
         f29x_mul(z, acc.z, zq);
         acc.z = z;
       }

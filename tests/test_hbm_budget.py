@@ -13,7 +13,8 @@ the device:
   1 MiB      nothing optional                  per-item pub33       keys_load -> GV_ENOMEM
   1 GiB      k4 group G tables, small arenas   k4 (GLV G windows)   k4
   8 GiB      + full-scalar G tables            k4f                  k4f (no k6 tables)
-  default    everything                        k4f / k6             kn (the arena's k6 tables)
+  default    everything                        kg (k4 tables, G     kw (the arena's wide tables),
+                                               on the 24-bit ones)  kn (its k6 tables)
 """
 import os
 
@@ -98,6 +99,9 @@ def test_default_budget_takes_the_arena_wide_then_k6_tables(batch):
     pub, sig, dig, exp = batch
     ver = gvm.Verifier([0])
     try:
+        got, routes = routes_of(ver, lambda: ver.verify_batch_digests(pub, sig, dig))
+        assert np.array_equal(got, exp)
+        assert routes.get("kg", 0) >= 1, routes            # the grouped route's default layout (kg 4)
         uniq, inv = np.unique(pub, axis=0, return_inverse=True)
         slots = ver.keys_load(uniq)[inv.reshape(-1)].astype(np.uint32)
         got, routes = routes_of(ver, lambda: ver.verify_batch_digests_keyed(slots, sig, dig))
