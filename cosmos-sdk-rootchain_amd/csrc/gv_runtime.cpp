@@ -678,11 +678,13 @@ struct gv_ctx {
                                 // GLV windows (k_ecmult_k4<true>, 6 GiB of tables; GV_GFULL=0: A/B)
   bool k6 = false;              // grouped batches on k_ecmult_k6: 6-bit Q windows on 32-entry key tables, the lambda
                                 // frame, G on the unsplit u1 in 24-bit windows (GV_K6=1)
-  int kg = 4;                   // grouped batches on k_ecmult_kn<5, kg>: k4's 16-entry 5-bit tables over kg groups
+  int kg = 0;                   // grouped batches on k_ecmult_kn<5, kg>: k4's 16-entry 5-bit tables over kg groups
                                 // (one of GV_KG_NGS; 0 = k_ecmult_k4), G after the last doubling from the 24-bit
-                                // tables on the real curve (GV_KG, "kg"; takes precedence over k6).  4 (k4's
-                                // tables and schedule): 222 vs 216M/s; 7 / 9 groups cut the ladder 10-17 % but
-                                // their tables cost more in the front (217 / 210M/s, profiles/r06/ab3)
+                                // tables on the real curve (GV_KG, "kg"; takes precedence over k6).  Off: with
+                                // the unsplit key chain k4 stays ahead -- 223 vs 215-218M/s for kg 4 (its
+                                // ladder 2-3 % shorter, but at 126 VGPRs x 4 waves the next call's front kernels
+                                // no longer co-reside), 7 / 9 groups cut the ladder 10-17 % and cost more in the
+                                // front (217 / 210M/s; profiles/r06/ab3, ab4)
   int keys_wide = 2;            // ... and wide-window tables while device memory holds them (GV_KEYS_WIDE): 2 = one
                                 // 9-bit window per group (15 groups of 256 entries, no doublings, 30 Q additions),
                                 // moving to two per group (8 groups, 9 doublings) when that no longer fits;

@@ -540,7 +540,7 @@ class Verifier:
         _check(self._L.gv_group_stats(self._ctx, slot, ctypes.byref(b), ctypes.byref(k)), "gv_group_stats")
         return b.value, k.value
 
-    KG_DEFAULT = 4         # gv_runtime.cpp gv_ctx::kg (the grouped route's default layout)
+    KG_DEFAULT = 0         # gv_runtime.cpp gv_ctx::kg (the grouped route's default layout)
     ROUTES = ("pub33", "keyed125", "k4", "k6", "lat", "lat_keyed", "k4f", "item_f", "kn", "ed_lat", "kw", "kw2", "kg")
 
     def route_stats(self, slot: int = 0) -> dict:
