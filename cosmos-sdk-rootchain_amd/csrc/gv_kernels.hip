@@ -845,7 +845,7 @@ GV_DEV void gej29_to_affine_words(fe& x8, fe& y8, const gej29& p) {
 // the doublings on E itself (u = 1 in kzq), as in rounds 3-5.  1: the root
 // and chain roles above -- the serialized key stage is ~10 % shorter, but the
 // pipelined C2 step loses 4-5 % (216 vs 226M/s alternated on one box,
-// profiles/r06/ab3): the 512-thread blocks wait for two free wave slots on
+// profiles/r06/ab/ab3): the 512-thread blocks wait for two free wave slots on
 // every SIMD of a CU, which the previous call's ladder holds.
 #ifndef GV_CHAIN_SPLIT
 #define GV_CHAIN_SPLIT 0
@@ -1863,7 +1863,7 @@ constexpr int kn_row(int qw, int ng) {
 // change zq is read once, at the end; held in registers across the ladder it
 // takes k_ecmult_kn<5, NG> to 160 VGPRs (3 waves per SIMD, 32 VGPRs left for a
 // front kernel's wave), parked in LDS (9 KB per block) to 126: 4 waves per
-// SIMD (kg4: C2 216 -> 222M/s alternated, profiles/r06/ab3).  The arena's
+// SIMD (kg4: C2 216 -> 222M/s alternated, profiles/r06/ab/ab3).  The arena's
 // ladders keep zq in registers (kw at 133 VGPRs: 440 vs 428M/s with LDS).
 #ifndef GV_KN_ZQ_LDS
 #define GV_KN_ZQ_LDS 1

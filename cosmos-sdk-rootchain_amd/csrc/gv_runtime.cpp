@@ -684,7 +684,7 @@ struct gv_ctx {
                                 // the unsplit key chain k4 stays ahead -- 223 vs 215-218M/s for kg 4 (its
                                 // ladder 2-3 % shorter, but at 126 VGPRs x 4 waves the next call's front kernels
                                 // no longer co-reside), 7 / 9 groups cut the ladder 10-17 % and cost more in the
-                                // front (217 / 210M/s; profiles/r06/ab3, ab4)
+                                // front (217 / 210M/s; profiles/r06/ab/ab3, ab4)
   int keys_wide = 2;            // ... and wide-window tables while device memory holds them (GV_KEYS_WIDE): 2 = one
                                 // 9-bit window per group (15 groups of 256 entries, no doublings, 30 Q additions),
                                 // moving to two per group (8 groups, 9 doublings) when that no longer fits;
