@@ -3,7 +3,7 @@
 // completion over its device slices, and the quiesce a key load holds.  No
 // HIP in here: the device part of a lane (staging, key grouping, the chunks
 // on the device) is a callback, so the CPU harness
-// (tests/stage/stage_harness.cpp --async) drives this same queue with fake
+// (tests/stage/async_harness.cpp) drives this same queue with fake
 // devices, under ThreadSanitizer too.
 #pragma once
 #include <condition_variable>
