@@ -649,8 +649,14 @@ struct gv_ctx {
   int stage_pieces = 2;         // host path, pageable chunks of >= 65,536 items: staged in this many pieces, each
                                 // piece's H2D behind its copy (1 = one copy then one H2D; GV_STAGE_PIECES):
                                 // 121.4 / 129.4 / 126.2 / 126.8M/s at 1 / 2 / 4 / 8 (profiles/r04/hostpath/stage_pieces_ab.jsonl)
-  size_t async_chunk = 262144;  // submitted batches: chunk size (the stream of chunks is steady, no ramp needed;
-  int async_growth = 1;         // GV_ASYNC_CHUNK, GV_ASYNC_GROWTH; "async_chunk" / "async_growth")
+  size_t async_chunk = 0;       // submitted batches: 0 = a slice behind one still in flight is ONE chunk (its H2D
+                                // and front run under the previous ladder) and a slice on an idle device takes
+                                // the synchronous ramp; else fixed chunks of this size growing by async_growth
+                                // (GV_ASYNC_CHUNK, GV_ASYNC_GROWTH; "async_chunk" / "async_growth").  1M pinned
+                                // batches: 4.6 ms each steady at 0 vs 5.2 ms at 262,144 (a 262,144-item ladder is
+                                // 1,024 blocks = 1.33 rounds of the chip's 768 resident ones, and the next one
+                                // only starts as it drains; profiles/r06/async/)
+  int async_growth = 1;
   bool host_ladder_stream = false;  // host chunks' ladders on the set's low-priority ladder stream (chunk_ladder;
                                     // GV_HOST_LADDER_STREAM=1).  Measured off: async pinned 185 vs 157-167M/s,
                                     // sync pinned 158-160 vs 150-152M/s (profiles/r05/async_ab.jsonl)
@@ -891,18 +897,28 @@ int group_keys(gv_ctx* ctx, Dev* d, Set* s, gvk_batch& b, size_t n, hipStream_t 
   // the layout: kg (5-bit windows over kgng groups) > k6 (6-bit, 4 groups) > k4,
   // each needing gtab6 (kg, k6) and its arena within the HBM budget
   if (((ctx->k6 && k6_room) || kg_room) && (rc = ensure_gtab6(ctx, d, s, st, true))) return rc;
+  // the arena for the set's whole capacity when the budget holds it: a later,
+  // larger chunk on this set does not regrow it (hipFree waits for the device)
+  auto arena = [&](int ent, int ng) {
+    const size_t capA = round_up(std::max<size_t>(s->cap / ctx->group_div, 256), 256);
+    if (capA > capU && !(capA <= s->gcap && ent == s->g_ent && ng == s->g_ng)) {
+      const int r = ensure_group_arena(ctx, d, s, capA, ent, ng);
+      if (r != GV_ENOMEM) return r;
+    }
+    return ensure_group_arena(ctx, d, s, capU, ent, ng);
+  };
   bool kg = kg_room && d->gtab6;
-  if (kg && (rc = ensure_group_arena(ctx, d, s, capU, GV_KEY_WORDS, kgng))) {
+  if (kg && (rc = arena(GV_KEY_WORDS, kgng))) {
     if (rc != GV_ENOMEM) return rc;
     kg = false;                                 // no room for kgng groups
   }
   bool k6 = !kg && ctx->k6 && k6_room && d->gtab6;
-  if (k6 && (rc = ensure_group_arena(ctx, d, s, capU, GV_K6_KEY_WORDS, GV_LGRP))) {
+  if (k6 && (rc = arena(GV_K6_KEY_WORDS, GV_LGRP))) {
     if (rc != GV_ENOMEM) return rc;
     k6 = false;                                 // no room for the 32-entry tables: k4
   }
   if (!kg && !k6 && (rc = ensure_gtab4(ctx, d, s, st))) return rc;
-  if (!kg && !k6 && (rc = ensure_group_arena(ctx, d, s, capU, GV_KEY_WORDS, GV_LGRP)))
+  if (!kg && !k6 && (rc = arena(GV_KEY_WORDS, GV_LGRP)))
     return rc == GV_ENOMEM ? GV_OK : rc;
   // the tables are built on the set's side stream while k_scalar_inv (which
   // does not read keys) runs on st: both are one wave per SIMD or so
@@ -1265,13 +1281,17 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
   const bool dslots = hb.d_slots != nullptr;    // slice grouping: slots already on the device
   const bool keyed = hb.slots != nullptr || dslots, msgs = hb.dig32 == nullptr;
   const uint32_t* dsl = dslots ? hb.d_slots + (c0 - hb.d_slots_lo) : nullptr;
-  int rc = ensure_cap(s, C);
+  // a chunk past the ramp's first size grows the set straight to a whole
+  // max_batch chunk (device scratch and pinned staging): a regrowth costs
+  // tens of ms (hipFree waits for the device, pinning pages), so it happens
+  // once, not again for each larger chunk the ramp or a queued slice brings
+  const size_t grow_c = ctx->pipe_chunk && C > ctx->pipe_chunk ? std::max(C, round_up(ctx->max_batch, 256)) : C;
+  int rc = ensure_cap(s, grow_c);
   if (rc) return rc;
   const InLayout L = in_layout(C, keyed, msgs);
-  if ((rc = ensure_pinned(&s->h_in, &s->h_in_cap, L.total))) return rc;
   size_t hb_bytes = 0;
   if ((rc = ensure_pinned((uint8_t**)&s->h_bits, &s->h_bits_cap, (C / 64) * 8))) return rc;
-  uint8_t* h = s->h_in;
+  uint8_t* h = nullptr;                           // the staging buffer (not for the caller's pinned buffers)
   uint64_t bmin = 0;
   // h2d_serial: this chunk's copies start after the previous chunk's
   auto h2d_begin = [&]() -> int {
@@ -1320,6 +1340,11 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
     s->cn = cn;
     return GV_OK;
   }
+  // (grown: room for the largest layout, pub33 + digests, so a plain chunk
+  // after keyed ones does not regrow it either)
+  const size_t stage_bytes = grow_c > C ? in_layout(grow_c, false, false).total : L.total;
+  if ((rc = ensure_pinned(&s->h_in, &s->h_in_cap, stage_bytes))) return rc;
+  h = s->h_in;
   const size_t lmax0 = keyed ? ctx->lat_max_keyed : ctx->lat_max;
   const size_t slmax0 = keyed ? ctx->lat_sl_max_keyed : ctx->lat_sl_max;
   const bool zc_path = ctx->lat_zero_copy && ctx->lat_sliced && cn <= slmax0 && cn <= lmax0 && !dslots;
@@ -1746,6 +1771,7 @@ void lane_stream(gv_ctx* ctx, AsyncState* as, size_t k, Dev* d) {
   for (;;) {
     AsyncSlice sl;
     if (!as->pop(k, sl)) break;
+    const bool behind = !act.empty();             // an earlier slice's chunks still in flight
     act.emplace_back();
     ActiveSlice& a = act.back();
     a.sl = sl;
@@ -1753,7 +1779,8 @@ void lane_stream(gv_ctx* ctx, AsyncState* as, size_t k, Dev* d) {
     const size_t lo = sl.lo, n = sl.hi - sl.lo;
     const HostBatch& hb = sl.job->hb;
     const bool pipelined = n > (hb.slots ? ctx->lat_max_keyed : ctx->lat_max) && ctx->pipe_chunk;
-    const std::vector<size_t> sizes = chunk_ramp(ctx, n, pipelined, true);
+    const std::vector<size_t> sizes = ctx->async_chunk ? chunk_ramp(ctx, n, pipelined, true)
+                                      : chunk_ramp(ctx, n, pipelined && !behind);
     const bool try_group = hb.pub33 && !hb.slots && ctx->group_keys && n >= ctx->group_min && sizes.size() > 1;
     if (try_group) {
       Set* g = &d->gset[gflip];
@@ -2899,7 +2926,7 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
                  : !strcmp(key, "k6") ? ctx->k6 : ctx->keys_k6;
     flag = val != 0;
   } else if (!strcmp(key, "async_chunk")) {
-    if (val < 256 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
+    if ((val != 0 && val < 256) || (unsigned long long)val > kMaxItems) return GV_EINVAL;
     ctx->async_chunk = round_up((size_t)val, 256);
   } else if (!strcmp(key, "async_growth")) {
     if (val < 1 || val > 64) return GV_EINVAL;
