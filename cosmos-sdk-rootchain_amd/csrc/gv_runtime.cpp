@@ -1894,6 +1894,42 @@ bool parse_size_env(const char* name, size_t* out) {
 
 extern "C" {
 
+
+// gv_open's pre-sizing (GV_PRESIZE=1, off by default): both scratch sets of
+// every device at a whole max_batch chunk, and their grouping arenas when the
+// HBM budget holds them, allocated and written once, so a node's first large
+// calls neither allocate nor first-touch them.  First 1M call 1.30 -> 1.26x
+// steady (profiles/r06/first_call/presize_ab.jsonl): the rest is the first
+// ladders themselves (4.51, 4.30, 4.17 then 4.0 ms), not allocation; off by
+// default because the ~6 GB it holds per device would come out of the HBM
+// budget that the resident key arena sizes itself from.
+static int presize_devices(gv_ctx* ctx) {
+  const size_t C = round_up(ctx->max_batch, 256);
+  const size_t capU = round_up(std::max<size_t>(C / ctx->group_div, 256), 256);
+  for (Dev* d : ctx->devs) {
+    if (hipSetDevice(d->id) != hipSuccess) return GV_EHIP;
+    for (Set& s : d->set) {
+      int rc = ensure_cap(&s, C);
+      if (rc) return rc;
+      if (hipMemsetAsync(s.scratch, 0, s.d_in ? (size_t)((uint8_t*)(s.bits + C / 64) - s.scratch) : 0, s.st) !=
+          hipSuccess)
+        return GV_EHIP;
+      rc = ensure_group_arena(ctx, d, &s, capU, GV_KEY_WORDS, GV_LGRP);
+      if (rc == GV_OK) {
+        for (uint32_t* p : {s.g_kqt, s.g_kqt2})
+          if (hipMemsetAsync(p, 0, (size_t)capU * GV_KEY_WORDS * 4 * (p == s.g_kqt ? 1 : GV_LGRP - 1), s.st) !=
+              hipSuccess)
+            return GV_EHIP;
+      } else if (rc != GV_ENOMEM) {
+        return rc;
+      }
+    }
+    for (Set& s : d->set)
+      if (hipStreamSynchronize(s.st) != hipSuccess) return GV_EHIP;
+  }
+  return GV_OK;
+}
+
 int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (!out || n_dev < 0 || (n_dev > 0 && !dev_ids)) return GV_EINVAL;
   *out = nullptr;
@@ -2023,6 +2059,11 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
         gv_close(ctx);
         return GV_EHIP;
       }
+  }
+  const char* presize = getenv("GV_PRESIZE");
+  if (presize && strcmp(presize, "0") != 0) {
+    const int rc = presize_devices(ctx);
+    if (rc) { gv_close(ctx); return rc; }
   }
   *out = ctx;
   return GV_OK;
