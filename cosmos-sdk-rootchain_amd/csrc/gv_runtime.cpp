@@ -649,14 +649,16 @@ struct gv_ctx {
   int stage_pieces = 2;         // host path, pageable chunks of >= 65,536 items: staged in this many pieces, each
                                 // piece's H2D behind its copy (1 = one copy then one H2D; GV_STAGE_PIECES):
                                 // 121.4 / 129.4 / 126.2 / 126.8M/s at 1 / 2 / 4 / 8 (profiles/r04/hostpath/stage_pieces_ab.jsonl)
-  size_t async_chunk = 0;       // submitted batches: 0 = a slice behind one still in flight is ONE chunk (its H2D
-                                // and front run under the previous ladder) and a slice on an idle device takes
-                                // the synchronous ramp; else fixed chunks of this size growing by async_growth
-                                // (GV_ASYNC_CHUNK, GV_ASYNC_GROWTH; "async_chunk" / "async_growth").  1M pinned
-                                // batches: 4.6 ms each steady at 0 vs 5.2 ms at 262,144 (a 262,144-item ladder is
-                                // 1,024 blocks = 1.33 rounds of the chip's 768 resident ones, and the next one
-                                // only starts as it drains; profiles/r06/async/)
-  int async_growth = 1;
+  size_t async_chunk = 262144;  // submitted batches staged through the library (pageable, messages): fixed chunks
+  int async_growth = 1;         // of this size growing by async_growth (GV_ASYNC_CHUNK, GV_ASYNC_GROWTH;
+                                // "async_chunk" / "async_growth"): the copy of one chunk overlaps the others
+  bool async_whole = true;      // submitted batches read in place (the caller's pinned buffers): a slice behind
+                                // one still in flight is ONE chunk (its H2D and front run under the previous
+                                // ladder), a slice on an idle device takes the synchronous ramp (GV_ASYNC_WHOLE,
+                                // "async_whole").  1M pinned batches: 4.6 ms each steady vs 5.2 ms in 262,144-item
+                                // chunks (a 262,144-item ladder is 1,024 blocks = 1.33 rounds of the chip's 768
+                                // resident ones, and the next one only starts as it drains); pageable batches in
+                                // one chunk lose the copy overlap (143 vs 177M/s): profiles/r06/async/
   bool host_ladder_stream = false;  // host chunks' ladders on the set's low-priority ladder stream (chunk_ladder;
                                     // GV_HOST_LADDER_STREAM=1).  Measured off: async pinned 185 vs 157-167M/s,
                                     // sync pinned 158-160 vs 150-152M/s (profiles/r05/async_ab.jsonl)
@@ -1779,8 +1781,9 @@ void lane_stream(gv_ctx* ctx, AsyncState* as, size_t k, Dev* d) {
     const size_t lo = sl.lo, n = sl.hi - sl.lo;
     const HostBatch& hb = sl.job->hb;
     const bool pipelined = n > (hb.slots ? ctx->lat_max_keyed : ctx->lat_max) && ctx->pipe_chunk;
-    const std::vector<size_t> sizes = ctx->async_chunk ? chunk_ramp(ctx, n, pipelined, true)
-                                      : chunk_ramp(ctx, n, pipelined && !behind);
+    const bool in_place = hb.pinned;               // read from the caller's pinned buffers, no staging
+    const std::vector<size_t> sizes = ctx->async_whole && in_place ? chunk_ramp(ctx, n, pipelined && !behind)
+                                                                   : chunk_ramp(ctx, n, pipelined, true);
     const bool try_group = hb.pub33 && !hb.slots && ctx->group_keys && n >= ctx->group_min && sizes.size() > 1;
     if (try_group) {
       Set* g = &d->gset[gflip];
@@ -1980,6 +1983,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* hl = getenv("GV_HOST_LADDER_STREAM")) ctx->host_ladder_stream = strcmp(hl, "0") != 0;
   parse_size_env("GV_ASYNC_CHUNK", &ctx->async_chunk);
   if (const char* ag = getenv("GV_ASYNC_GROWTH")) ctx->async_growth = std::max(1, std::min(64, atoi(ag)));
+  if (const char* aw = getenv("GV_ASYNC_WHOLE")) ctx->async_whole = strcmp(aw, "0") != 0;
   if (const char* kc = getenv("GV_KEY_CAP")) {
     const long long v = atoll(kc);
     if (v >= 256 && (unsigned long long)v <= kMaxItems) ctx->key_cap = (size_t)v;
@@ -2967,8 +2971,11 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
                  : !strcmp(key, "k6") ? ctx->k6 : ctx->keys_k6;
     flag = val != 0;
   } else if (!strcmp(key, "async_chunk")) {
-    if ((val != 0 && val < 256) || (unsigned long long)val > kMaxItems) return GV_EINVAL;
+    if (val < 256 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
     ctx->async_chunk = round_up((size_t)val, 256);
+  } else if (!strcmp(key, "async_whole")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->async_whole = val != 0;
   } else if (!strcmp(key, "async_growth")) {
     if (val < 1 || val > 64) return GV_EINVAL;
     ctx->async_growth = (int)val;
