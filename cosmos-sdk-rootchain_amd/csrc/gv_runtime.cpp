@@ -2836,7 +2836,10 @@ int gv_get_option(gv_ctx* ctx, const char* key, long long* val) {
               {"pipeline_dev", ctx->pipeline_dev},
               {"two_ladders", ctx->two_ladders},
               {"key_cap", (long long)ctx->key_cap},
-              {"max_batch", (long long)ctx->max_batch}};
+              {"max_batch", (long long)ctx->max_batch},
+              {"async_chunk", (long long)ctx->async_chunk},
+              {"async_growth", ctx->async_growth},
+              {"async_whole", ctx->async_whole}};
   for (const auto& o : opts)
     if (!strcmp(key, o.k)) {
       *val = o.v;

@@ -244,6 +244,14 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * "stage_pieces" (pageable host chunks of at least 65,536 items are staged
  * into pinned memory in this many pieces, each piece's H2D right behind its
  * copy; default 2, env GV_STAGE_PIECES),
+ * "async_chunk" / "async_growth" (submitted batches staged through the
+ * library -- pageable buffers, messages: fixed chunks of async_chunk items,
+ * each later one at most async_growth times the one before; default 262144
+ * and 1, env GV_ASYNC_CHUNK / GV_ASYNC_GROWTH), "async_whole" (0/1:
+ * submitted digest batches read in place from gv_host_alloc memory run as
+ * ONE chunk when they queue behind a batch still in flight -- their copies
+ * and front kernels then run under the previous batch's ladder -- and take
+ * the pipe_chunk ramp on an idle device; default 1, env GV_ASYNC_WHOLE),
  * "h2d_serial" (0/1: a host slice's chunks send their inputs one after the
  * other -- each chunk's H2D waits for the previous chunk's -- so the chunk
  * the GPU needs first is not slowed by the next one's transfer; default 1,
@@ -341,7 +349,8 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val);
 /* The current value of a schedule option set by gv_set_option or its
  * environment variable: "kg", "k6", "gfull", "keys_k6", "keys_wide",
  * "group_keys", "sort_keys", "pipeline_dev", "two_ladders", "key_cap",
- * "max_batch".  GV_EINVAL for any other key.  Instrumentation (bench route
+ * "max_batch", "async_chunk", "async_growth", "async_whole".  GV_EINVAL for
+ * any other key.  Instrumentation (bench route
  * attribution). */
 int gv_get_option(gv_ctx* ctx, const char* key, long long* val);
 

@@ -127,3 +127,39 @@ def test_close_waits_for_outstanding_batches(c2):
     p = v.submit_digests(pub, sig, dig)
     v.close()                                                 # waits for the ticket, then gv_close
     assert np.array_equal(p.out, exp)
+
+
+def test_pinned_batches_whole_or_chunked(c2):
+    """Pinned batches queued behind one in flight run as one chunk
+    ("async_whole", default), as fixed chunks (off), or -- past max_batch --
+    as several max_batch chunks sharing one slice grouping; keyed pinned
+    batches the same.  Same verdicts every way."""
+    pub, sig, dig, exp = c2
+    v = gvm.Verifier([0])
+    hp = [v.host_array(a.shape, a.dtype) for a in (pub, sig, dig)]
+    try:
+        assert v.get_option("async_whole") == 1
+        assert v.get_option("async_chunk") == 262144 and v.get_option("async_growth") == 1
+        for h, a in zip(hp, (pub, sig, dig)):
+            h[...] = a
+        for whole, mb in ((1, None), (0, None), (1, 131072)):
+            v.set_option("async_whole", whole)
+            if mb:
+                v.set_option("max_batch", mb)
+            assert v.get_option("async_whole") == whole
+            pend = [v.submit_digests(*hp) for _ in range(4)]
+            for p in pend:
+                assert np.array_equal(v.wait(p), exp)
+        uniq, inv = np.unique(pub, axis=0, return_inverse=True)
+        hs = v.host_array((len(pub),), np.uint32)
+        try:
+            hs[...] = v.keys_load(uniq)[inv.reshape(-1)].astype(np.uint32)
+            pend = [v.submit_digests_keyed(hs, hp[1], hp[2]) for _ in range(3)]
+            for p in pend:
+                assert np.array_equal(v.wait(p), exp)
+        finally:
+            v.host_free(hs)
+    finally:
+        for h in hp:
+            v.host_free(h)
+        v.close()
