@@ -135,12 +135,17 @@ W_LADDER_K6 = w_ladder(30, 44, 11, 6, nbeta=12, gframe=True)
 # k_ecmult_kn<11> (the resident arena's k6 tables, option keys_k6): 11 groups of two 6-bit windows, 2 positions:
 # 6 doublings, 44 Q (22 lambda, 2 beta products per position), 11 G additions
 W_LADDER_KN = w_ladder(6, 44, 11, 6, nbeta=4, gframe=True)
-# k_ecmult_kn<9, 15> (the resident arena's wide-window tables, option keys_wide 2): 15 groups of one 9-bit window,
-# one position: no doublings, 30 Q (15 lambda, 2 beta products), 11 G additions
-W_LADDER_KW = w_ladder(0, 30, 11, 9, nbeta=2, gframe=True)
-# k_ecmult_kn<9, 8> (keys_wide 1, or an arena past the one-window layout's room): 8 groups of two 9-bit windows
-# (7 of two, one of one), 2 positions: 9 doublings, 30 Q (2 beta products per position), 11 G additions
-W_LADDER_KW2 = w_ladder(9, 30, 11, 9, nbeta=4, gframe=True)
+# k_ecmult_kn<qw, ceil(130 / qw)> (the resident arena's wide-window tables, option keys_wide 2; qw = the
+# library's gv_get_option("kw_qw"), 11 by default): one qw-bit window per group, one position: no doublings,
+# 2 ceil(130 / qw) Q (half lambda, 2 beta products), 11 G additions.  keys_wide 1 (or an arena past the
+# one-window layout's room): two windows per group, 2 positions: qw doublings, 4 beta products.
+def w_ladder_kw(qw: int = 11, two_windows: bool = False) -> float:
+    nq = 2 * ((130 + qw - 1) // qw)
+    return w_ladder(qw if two_windows else 0, nq, 11, qw, nbeta=4 if two_windows else 2, gframe=True)
+
+
+W_LADDER_KW = w_ladder_kw(11)
+W_LADDER_KW2 = w_ladder_kw(11, True)
 W_LADDER_K4F = w_ladder(30, 52, 11, 5, nbeta=14)   # k_ecmult_k4<true>: G on the unsplit u1, 11 25-bit windows
 # Peak: the highest v_mad_u64_u32 issue rate measured on MI355X
 # (tools/microbench/alu_rate.hip; profiles/r01/alu_rate_v3.jsonl, dependent

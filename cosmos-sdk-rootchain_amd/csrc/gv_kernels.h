@@ -159,29 +159,33 @@ static_assert(GV_K6_QW * GV_K6_QWIN >= 130 && GV_K6_GW * GV_K6_GWIN >= 257, "k6 
 // The resident arena's wide-window tables (option "keys_wide",
 // k_ecmult_kn<GV_KW_QW, NG>): 2^(QW-1) multiples per group, the signed QW-bit
 // windows of each 128-bit GLV half one per group (NG = GV_KW_NG1: one ladder
-// position, no doublings) or two per group (GV_KW_NG2: 2 positions).  QW = 9
-// (default): 256 entries, 15 windows, 30 Q additions; 15 groups and no
-// doublings, or 8 groups and 9 doublings (k6 arena: 6 doublings and 44
-// additions; QW 8: 8 and 34; QW 7: 7 and 38 with two windows per group).  G as on the k6 ladders (11 24-bit windows after the last
-// doubling, gtab6).  15 (8) x 16 KiB of tables per key, built at gv_keys_load
-// beside the k6 tables while the key set fits (kn on the k6 tables otherwise).
-// A/B on one box (profiles/r05/kw/): c2_key_cache QW 7 / 8 / 9 = 329-344 /
-// 366 / 380-381M/s, k6 arena 312-317M/s.
+// position, no doublings) or two per group (GV_KW_NG2: 2 positions).  QW = 11
+// (default, round 6): 1,024 entries, 12 windows, 24 Q additions; 12 groups
+// and no doublings (768 KiB of tables per key), or 6 groups and 11 doublings
+// (384 KiB).  G as on the k6 ladders (11 24-bit windows after the last
+// doubling, gtab6).  Built at gv_keys_load beside the k6 tables while the key
+// set fits (kw2, then kn on the k6 tables otherwise).  A/B on one box,
+// c2_key_cache (65,536 keys), one window per group: QW 7 / 8 / 9 =
+// 329-344 / 366 / 380-381M/s (round 5, profiles/r05/kw/); round 6
+// (profiles/r06/ab/kqw/): QW 9 / 10 / 11 / 12 = 421-430 / 452-467 / 482-488 /
+// 500-505M/s, serialized ladder 2.12-2.16 / 1.90-1.95 / 1.82-1.84 /
+// 1.71-1.74 ms; 12 doubles the tables again (1.5 MiB per key, 96 GiB for
+// 65,536 keys) for +3.5 %, so 11 is the default and 12 an A/B build.
 #ifndef GV_KW_QW
-#define GV_KW_QW 9                                        // (an A/B build may set 7 or 8)
+#define GV_KW_QW 11
 #endif
-#define GV_KW_NT (1 << (GV_KW_QW - 1))                    // 256 table entries per group
-#define GV_KW_QWIN ((130 + GV_KW_QW - 1) / GV_KW_QW)      // 15 windows per GLV half
+#define GV_KW_NT (1 << (GV_KW_QW - 1))                    // 1,024 table entries per group
+#define GV_KW_QWIN ((130 + GV_KW_QW - 1) / GV_KW_QW)      // 12 windows per GLV half
 // Entry format: 16 = canonical words x[8] y[8] (64 B: a gather never
 // straddles two cache lines, and 20 % less memory than the 80-B raw-limb
 // entries, 20; 32 pads those to a line -- A/B builds).
 #ifndef GV_KW_ENT_WORDS
 #define GV_KW_ENT_WORDS 16
 #endif
-#define GV_KW_KEY_WORDS (GV_KW_NT * GV_KW_ENT_WORDS)     // one group table (16,384 B)
-#define GV_KW_NG1 GV_KW_QWIN                              // one window per group: 15 groups
-#define GV_KW_NG2 ((GV_KW_QWIN + 1) / 2)                  // two windows per group (the last one): 8 groups
-static_assert(GV_KW_QW >= 7 && GV_KW_QW <= 9 && GV_KW_NG1 <= 19, "wide arena layout");
+#define GV_KW_KEY_WORDS (GV_KW_NT * GV_KW_ENT_WORDS)     // one group table (65,536 B)
+#define GV_KW_NG1 GV_KW_QWIN                              // one window per group: 12 groups
+#define GV_KW_NG2 ((GV_KW_QWIN + 1) / 2)                  // two windows per group: 6 groups
+static_assert(GV_KW_QW >= 7 && GV_KW_QW <= 12 && GV_KW_NG1 <= 19, "wide arena layout");
 static_assert(GV_KW_QWIN + GV_K6_GWIN <= GV_DIGIT_ROWS, "wide-window digits fit the digit rows");
 static_assert(GV_KW_QW * GV_KW_QWIN >= 130, "wide windows cover the GLV halves");
 

@@ -1798,9 +1798,9 @@ __global__ __launch_bounds__(256) GV_ECMULT_ATTR void k_ecmult_k4(const u32* gta
 // 2^23-entry tables of 2^(24 j) G.  Same additions, final check and semantics
 // as k_ecmult_k4 otherwise (lambda is a group automorphism, so every
 // exceptional case -- H == 0 -- meets the same points).
-// QW = GV_KW_QW (the arena's wide-window tables, GV_KW_*: 9 by default): 15
-// nine-bit windows per half in 8 groups, 256-entry tables, 9 doublings and 30
-// Q additions.
+// QW = GV_KW_QW (the arena's wide-window tables, GV_KW_*: 11 by default): 12
+// eleven-bit windows per GLV half, in 12 groups (one position, no doublings)
+// or 6 (two positions, 11 doublings), 1,024-entry tables, 24 Q additions.
 // The group layout as constant tables (row 0: NG = 4, row 1: the arena's NG,
 // row 2: the wide arena's NG) -- indexing them keeps the ladder's register
 // allocation at that of k4

@@ -2839,7 +2839,8 @@ int gv_get_option(gv_ctx* ctx, const char* key, long long* val) {
               {"max_batch", (long long)ctx->max_batch},
               {"async_chunk", (long long)ctx->async_chunk},
               {"async_growth", ctx->async_growth},
-              {"async_whole", ctx->async_whole}};
+              {"async_whole", ctx->async_whole},
+              {"kw_qw", GV_KW_QW}};                  // read-only: the wide arena's window width (build)
   for (const auto& o : opts)
     if (!strcmp(key, o.k)) {
       *val = o.v;

@@ -349,8 +349,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val);
 /* The current value of a schedule option set by gv_set_option or its
  * environment variable: "kg", "k6", "gfull", "keys_k6", "keys_wide",
  * "group_keys", "sort_keys", "pipeline_dev", "two_ladders", "key_cap",
- * "max_batch", "async_chunk", "async_growth", "async_whole".  GV_EINVAL for
- * any other key.  Instrumentation (bench route
+ * "max_batch", "async_chunk", "async_growth", "async_whole", and (read
+ * only) "kw_qw", the resident arena's wide-window width this library was
+ * built with.  GV_EINVAL for any other key.  Instrumentation (bench route
  * attribution). */
 int gv_get_option(gv_ctx* ctx, const char* key, long long* val);
 

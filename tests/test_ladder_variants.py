@@ -8,7 +8,8 @@ half (gfull 0: 14 20-bit windows) and k_ecmult_k6 (6-bit Q windows on 32-entry
 key tables, the lambda frame, G on the unsplit u1 in 11 signed 24-bit windows
 from the 2^(36 t) G tables: "k6" 1 on the grouped route, "keys_k6" 1 -- the
 default -- on the resident key arena), and the arena's wide-window tables
-("keys_wide", the default: 9-bit Q windows on 256-entry tables, 9 doublings).  Each is run on the grouped route (pub33
+("keys_wide", the default: 11-bit Q windows on 1,024-entry tables, one window per
+group and no doublings, or two per group and 11 doublings).  Each is run on the grouped route (pub33
 batches with repeated keys), the cached-key route (gv_keys_load slots) and the
 message path, against the oracle's expected verdicts, and the route counters
 must show the schedule that ran.  The per-item route (group_keys 0: each item parses its

@@ -266,15 +266,17 @@ def c2_key_cache(ver, pub, sig, dig, exp, nkeys: int, steps: int = 20):
     # the ladder's work, counted from the kernel's operations (bench.w_ladder),
     # over its serialized launch duration
     import bench as B
-    w_l = round(B.W_LADDER_KW if kwide else B.W_LADDER_KW2 if kwide2 else B.W_LADDER_KN if kn else B.W_LADDER_K6 if k6 else B.W_LADDER_K4F if k4f
-                else B.W_LADDER_K4)
+    qw = ver.get_option("kw_qw")
+    ng1 = (130 + qw - 1) // qw
+    w_l = round(B.w_ladder_kw(qw) if kwide else B.w_ladder_kw(qw, True) if kwide2 else B.W_LADDER_KN if kn
+                else B.W_LADDER_K6 if k6 else B.W_LADDER_K4F if k4f else B.W_LADDER_K4)
     ems = stages["serialized"]["ecmult_ms"] or 0.0
     ach = n * w_l / (ems * 1e-3) / 1e12 if ems else 0.0
     return {"items": n, "keys": nkeys, "value": round(n * steps / el, 1), "unit": "verifies/s",
             "keys_load_ms": round(t_load * 1e3, 2), "mismatches": int(np.count_nonzero(got != exp)),
             "route": "kw" if kwide else "kw2" if kwide2 else "kn" if kn else "k6" if k6 else "k4f" if k4f else "k4",
             "stages": stages,
-            "roofline": {"kernel": "k_ecmult_kn<9, 15>" if kwide else "k_ecmult_kn<9, 8>" if kwide2
+            "roofline": {"kernel": f"k_ecmult_kn<{qw}, {ng1}>" if kwide else f"k_ecmult_kn<{qw}, {(ng1 + 1) // 2}>" if kwide2
                          else "k_ecmult_kn<6, 11>" if kn
                          else "k_ecmult_kn<6, 4>" if k6 else "k_ecmult_k4",
                          "work_per_verify": w_l, "kernel_ms": ems,
@@ -283,10 +285,11 @@ def c2_key_cache(ver, pub, sig, dig, exp, nkeys: int, steps: int = 20):
                          "frac": round(ach * 1e12 / B.P_MUL_COMMITTED, 4)},
             "note": "keys parsed once into the HBM key arena (k4: Q, 2^35 Q, 2^70 Q, 2^100 Q tables of 16 entries on "
                     "one Z, 5.4 KB per key, read by the small-batch kernels; k6 (option keys_k6): 11 tables of 32 "
-                    "entries, 2^(12 k) Q for k < 11, on one Z, 28 KB per key; wide (option keys_wide 2): 15 tables of "
-                    "256 entries, 2^(9 k) Q for k < 15, 300 KB per key); items verified by slot (k_ecmult_kn<9, 15>: no "
-                    "doublings, 30 Q + 11 G additions; k_ecmult_kn<9, 8>: 9 doublings, 30 + 11; k_ecmult_kn<6, 11>: 6 doublings, 44 + 11; k_ecmult_k4: 30 "
-                    "doublings, 52 + 11)"}
+                    "entries, 2^(12 k) Q for k < 11, on one Z, 28 KB per key; wide (option keys_wide 2, qw = kw_qw, 11 "
+                    "by default): ceil(130 / qw) tables of 2^(qw - 1) entries, 2^(qw k) Q, 64 B entries (768 KiB per "
+                    "key at 11); items verified by slot (k_ecmult_kn<qw, ceil(130 / qw)>: no doublings, 2 ceil(130 / "
+                    "qw) Q + 11 G additions; two windows per group: qw doublings; k_ecmult_kn<6, 11>: 6 doublings, "
+                    "44 + 11; k_ecmult_k4: 30 doublings, 52 + 11)"}
 
 
 def c1_items(wl, n: int, threads: int, nkeys: int = 10000):
