@@ -158,8 +158,8 @@ struct Dev {
   uint32_t *kqt6 = nullptr, *kzq6 = nullptr, *kqt62 = nullptr, *kzq62 = nullptr;
   size_t keys6 = 0;                               // leading slots whose k6 tables are built
   // the resident arena's wide-window tables (option "keys_wide"): per slot
-  // kw_ng (GV_KW_NG1 = 15: one 9-bit window per group, or GV_KW_NG2 = 8: two)
-  // 256-entry group tables on one Z (kqtw: group 0, kqtw2:
+  // kw_ng (GV_KW_NG1 = 12: one 11-bit window per group, or GV_KW_NG2 = 6: two;
+  // GV_KW_QW, gv_kernels.h) 1,024-entry group tables on one Z (kqtw: group 0, kqtw2:
   // groups 1.., kzqw: the Z, 8 rows of stride kcapw; kzqw2: the chain's parked
   // Zs), in an arena of their own (capacity kcapw) grown by doubling while the
   // HBM budget holds it; keysw leading slots built.  kw_full: the budget
@@ -694,8 +694,8 @@ struct gv_ctx {
                                 // no longer co-reside), 7 / 9 groups cut the ladder 10-17 % and cost more in the
                                 // front (217 / 210M/s; profiles/r06/ab/ab3, ab4)
   int keys_wide = 2;            // ... and wide-window tables while device memory holds them (GV_KEYS_WIDE): 2 = one
-                                // 9-bit window per group (15 groups of 256 entries, no doublings, 30 Q additions),
-                                // moving to two per group (8 groups, 9 doublings) when that no longer fits;
+                                // GV_KW_QW-bit window per group (11: 12 groups of 1,024 entries, no doublings, 24 Q
+                                // additions), moving to two per group (6 groups, 11 doublings) when that no longer fits;
                                 // 1 = two per group; 0 = none
   size_t keys_wide1_cap = SIZE_MAX;   // test hook: the one-window layout's slot capacity ("keys_wide1_cap")
   bool keys_k6 = true;          // the resident arena (gv_keys_load) also holds k6 tables and its throughput batches
