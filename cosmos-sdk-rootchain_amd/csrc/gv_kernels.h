@@ -144,8 +144,10 @@ hipError_t gvk_unsort_bits(uint32_t n, const uint32_t* pos, const uint64_t* sbit
 #define GV_K6_QW 6
 #define GV_K6_NT 32                                       // table entries per group
 #define GV_K6_QWIN 22
+#ifndef GV_K6_GW
 #define GV_K6_GW 24
-#define GV_K6_GWIN 11
+#endif
+#define GV_K6_GWIN ((257 + GV_K6_GW - 1) / GV_K6_GW)    // 11 windows at 24 bits
 #define GV_K6_GNTAB GV_K6_GWIN                            // one G table per window
 #define GV_K6_GTAB_N (1u << (GV_K6_GW - 1))
 #define GV_K6_KEY_WORDS (GV_K6_NT * GV_QENT_WORDS)       // one group table (2,560 B)
