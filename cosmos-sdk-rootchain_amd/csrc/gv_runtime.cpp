@@ -987,6 +987,15 @@ struct KeyArena {
   hipEvent_t ready;
 };
 
+// A chunk past the ramp's first size grows its set straight to a whole
+// max_batch chunk (device scratch, pinned staging, the grouping arena): a
+// regrowth costs tens of ms (hipFree waits for the device, pinning pages), so
+// it happens once -- not again when a larger chunk, a queued whole slice or a
+// host-buffer call follows device-resident calls of another size.
+size_t grow_items(const gv_ctx* ctx, size_t C) {
+  return ctx->pipe_chunk && C > ctx->pipe_chunk ? std::max(C, round_up(ctx->max_batch, 256)) : C;
+}
+
 // Launch the pipeline for n items whose inputs already sit on the device, on
 // set s's scratch, stream st.  The caller holds d->mu.
 // st_ecm (pipelined device-resident calls): the ladder runs there, after the
@@ -997,7 +1006,7 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
            const KeyArena* ka = nullptr, bool no_group = false) {
   if (n == 0 || n > kMaxItems) return GV_EINVAL;
   const size_t C = round_up(n, 256);
-  int rc = ensure_cap(s, C);
+  int rc = ensure_cap(s, grow_items(ctx, C));
   if (rc) return rc;
   if (kslot && !ka) {                           // the arena always exists for a keyed batch
     rc = ensure_keys(d, 1, ctx->keys, st, ctx->key_cap, ctx->hbm_budget, nullptr);
@@ -1283,11 +1292,7 @@ int submit(gv_ctx* ctx, Dev* d, Set* s, size_t c0, size_t cn, const HostBatch& h
   const bool dslots = hb.d_slots != nullptr;    // slice grouping: slots already on the device
   const bool keyed = hb.slots != nullptr || dslots, msgs = hb.dig32 == nullptr;
   const uint32_t* dsl = dslots ? hb.d_slots + (c0 - hb.d_slots_lo) : nullptr;
-  // a chunk past the ramp's first size grows the set straight to a whole
-  // max_batch chunk (device scratch and pinned staging): a regrowth costs
-  // tens of ms (hipFree waits for the device, pinning pages), so it happens
-  // once, not again for each larger chunk the ramp or a queued slice brings
-  const size_t grow_c = ctx->pipe_chunk && C > ctx->pipe_chunk ? std::max(C, round_up(ctx->max_batch, 256)) : C;
+  const size_t grow_c = grow_items(ctx, C);   // (device scratch and pinned staging)
   int rc = ensure_cap(s, grow_c);
   if (rc) return rc;
   const InLayout L = in_layout(C, keyed, msgs);
@@ -1477,7 +1482,7 @@ int slice_group(gv_ctx* ctx, Dev* d, size_t lo, size_t n, const HostBatch& hb, K
   *d_slots = nullptr;
   if (!worth_grouping(hb.pub33 + lo * 33, n, ctx->group_div)) return GV_OK;
   const size_t C = round_up(n, 256);
-  int rc = ensure_cap(g, C);
+  int rc = ensure_cap(g, grow_items(ctx, C));
   if (rc) return rc;
   if ((rc = set_acquire(g, g->st))) return rc;
   const uint8_t* src = hb.pub33 + lo * 33;
