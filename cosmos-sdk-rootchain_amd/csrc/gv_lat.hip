@@ -25,6 +25,7 @@
 // mode).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include "secp_field.cuh"
 #include "secp_scalar.cuh"
 #include "secp_group29.cuh"
@@ -34,6 +35,7 @@
 #include "secp_fsl.cuh"
 #include "secp_modinv_sl.cuh"
 #include "secp_sha256.cuh"
+
 #include "gv_kernels.h"
 
 static_assert(F29_NCH == 2, "gv_lat.hip is built with -DF29_NCH=2");
@@ -42,6 +44,19 @@ static_assert(F29_NCH == 2, "gv_lat.hip is built with -DF29_NCH=2");
 #endif
 
 namespace gv {
+
+// Q digit width of a shared-state type: kQ6 (the kn arena's 6-bit windows),
+// kKW (the wide arena's GV_KW_QW-bit windows), else k4's 5-bit ones.
+template <class SH, class = void>
+struct lat_q_width {
+  static constexpr int qw = SH::kQ6 ? GV_K6_QW : GV_QW;
+  static constexpr int qwin = SH::kQ6 ? GV_K6_QWIN : GV_QWIN;
+};
+template <class SH>
+struct lat_q_width<SH, std::void_t<decltype(SH::kKW)>> {
+  static constexpr int qw = GV_KW_QW;
+  static constexpr int qwin = GV_KW_QWIN;
+};
 
 // GV_LAT_TRACE (A/B builds only): per block, wall-clock stamps (100 MHz) of
 // the phases -- start, wave 0 prep done, wave 1 scalars done, after the
@@ -406,7 +421,7 @@ GV_DEV void lat_scalars_e(SH& sh, int sig, bool live, const uint8_t* sig64, GetE
 #pragma unroll
     for (int i = 0; i < 4; ++i) { k1g[i] = k2g[i] = k1q[i] = k2q[i] = 0u; }
   }
-  constexpr int QW = SH::kQ6 ? GV_K6_QW : GV_QW, QWIN = SH::kQ6 ? GV_K6_QWIN : GV_QWIN;
+  constexpr int QW = lat_q_width<SH>::qw, QWIN = lat_q_width<SH>::qwin;
 #pragma unroll
   for (int win = 0; win < QWIN; ++win) {
     int d0 = booth_digit<QW>(k1q, win), d1 = booth_digit<QW>(k2q, win);
@@ -1702,6 +1717,174 @@ __global__ __launch_bounds__(256) void k_verify_lat16_kn(const gvk_lat b) {
   }
 }
 
+// Keyed small batches on the resident arena's wide-window tables
+// (k_verify_lat16_kw, round 6): the slot's GV_KW_NG1 group tables of
+// 2^(QW-1) entries (one QW-bit Booth window per group and GLV half, 64-B
+// canonical entries on one Z) need no doubling at all.  One signature per
+// 256-thread block, 16 rows: row g < GV_KW_NG1 adds group g's Q and lambda*Q
+// entries and lifts its sum by the tables' Z; rows 12..15 (wave 3) add the G
+// windows j == row - 12 (mod 4) from the 24-bit tables.  The 16 sums are
+// joined as in k_verify_lat16_kn.  Same verdicts as k_verify_lat16_sl.
+struct Lat16KwShared {
+  static constexpr bool kG5 = false;
+  static constexpr bool kG24 = true;
+  static constexpr bool kQ6 = false;
+  static constexpr bool kKW = true;         // Q digits: GV_KW_QW-bit windows (lat_q_width)
+  u32 eh[8];
+  u32 dq[1][GV_QWIN];                       // GV_KW_QWIN used
+  int dg24[1][GV_K6_GWIN];
+  u32 r[1][8];
+  u32 oks[1];
+  u32 pt[16][3][16];
+  u32 pinf[16];
+  u32 pw[4][3][16];
+  u32 pwinf[4];
+};
+static_assert(GV_KW_NG1 == GV_KW_QWIN && GV_KW_NG1 <= 12 && GV_KW_QWIN <= GV_QWIN && GV_K6_GWIN <= 12 &&
+                  GV_KW_ENT_WORDS == 16,
+              "kw rows: one window per group in rows 0..11, 64-B canonical entries");
+
+__global__ __launch_bounds__(256) void k_verify_lat16_kw(const gvk_lat b) {
+  __shared__ Lat16KwShared sh;
+  const u32 gi = blockIdx.x;                            // grid = n: every block is live
+  u32 sl = b.kslot[gi];
+  bool kok = sl < b.kcount;
+  if (!kok) sl = 0;                                     // the arena always holds slot 0's memory
+  kok = kok && b.kok[sl] != 0u;
+  if (b.msg_len) {
+    if (threadIdx.x < 64) {
+      lat_scalars_e<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, [&](u32 e[8]) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = sh.eh[7 - i];
+      });
+    } else {
+      if (threadIdx.x < 128) {
+        u32 eh[8];
+        sha256_msg_wave(eh, b.msg_blob + b.msg_off[gi], b.msg_len[gi]);
+        if (threadIdx.x == 64) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) sh.eh[i] = eh[i];
+        }
+      }
+      __syncthreads();
+    }
+  } else if (threadIdx.x < 64) {
+    lat_scalars<true>(sh, 0, true, b.sig64 + (size_t)gi * 64u, b.dig32 + (size_t)gi * 32u, nullptr, b.C, gi);
+  }
+  __syncthreads();
+  const fslk k = fsl_consts();
+  const u32 L = k.L, r16 = threadIdx.x >> 4, wave = threadIdx.x >> 6, row = r16 & 3u;
+  const bool lo = L < 9u;
+  gjsl A;
+  A.x = 0u; A.y = 0u; A.z = 0u;
+  bool inf = true;
+  if (wave < 3u) {                                      // rows 0..11: Q groups
+    const u32 g = r16;
+    if (g < (u32)GV_KW_NG1) {
+      u32 beta;
+      {
+        u32 w[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = kLBeta[i];
+        beta = fsl_from_words(w, k);
+      }
+      const u32* tab = g == 0u ? b.kqt + (size_t)sl * GV_KW_KEY_WORDS
+                               : b.kqt2 + ((size_t)sl * (GV_KW_NG1 - 1) + (g - 1u)) * GV_KW_KEY_WORDS;
+      const u32 dq = sh.dq[0][g];
+#pragma unroll 1
+      for (int t = 0; t < 2; ++t) {
+        const int d = t == 0 ? ((int)(dq << 16) >> 16) : ((int)dq >> 16);
+        if (d == 0) continue;
+        const u32* pe = tab + (size_t)((d < 0 ? -d : d) - 1) * GV_KW_ENT_WORDS;
+        u32 x = fsl_load_words(pe, k);
+        u32 y = fsl_load_words(pe + 8, k);
+        if (t == 1) x = fsl_mul(x, beta, k);            // lambda Q = (beta x, y), same Z
+        if (d < 0) y = k.bias - y;
+        if (inf) {
+          A.x = x; A.y = fsl_norm(y, k); A.z = L == 0u ? 1u : 0u;
+          inf = false;
+        } else {
+          gjsl_add_scaled(A, inf, x, y, A.z, k);
+        }
+      }
+      {                                                 // back to the real curve: Z * (the tables' Z)
+        u32 w[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = b.kzq[(size_t)i * b.kC + sl];
+        A.z = fsl_mul(A.z, fsl_from_words(w, k), k);
+      }
+    }
+  } else {                                              // rows 12..15: G windows j = row (mod 4)
+#pragma unroll 1
+    for (u32 j = row; j < GV_K6_GWIN; j += 4u) {
+      const int d = sh.dg24[0][j];
+      if (d == 0) continue;
+      const u32* pe = b.gtab6 + ((size_t)j * GV_K6_GTAB_N + (u32)((d < 0 ? -d : d) - 1)) * 16u;
+      const u32 x = fsl_load_words(pe, k);
+      u32 y = fsl_load_words(pe + 8, k);
+      if (d < 0) y = k.bias - y;
+      if (inf) {
+        A.x = x; A.y = fsl_norm(y, k); A.z = L == 0u ? 1u : 0u;
+        inf = false;
+      } else {
+        gjsl_add_scaled(A, inf, x, y, A.z, k);
+      }
+    }
+  }
+  if (lo) { sh.pt[r16][0][L] = A.x; sh.pt[r16][1][L] = A.y; sh.pt[r16][2][L] = A.z; }
+  if (L == 0u) sh.pinf[r16] = inf ? 1u : 0u;
+  __syncthreads();
+  {
+    const u32 r0 = wave * 4u;
+    A.x = lo ? sh.pt[r0][0][L] : 0u; A.y = lo ? sh.pt[r0][1][L] : 0u; A.z = lo ? sh.pt[r0][2][L] : 0u;
+    inf = sh.pinf[r0] != 0u;
+#pragma unroll 1
+    for (u32 j = 1; j < 4u; ++j) {
+      gjsl O;
+      O.x = lo ? sh.pt[r0 + j][0][L] : 0u; O.y = lo ? sh.pt[r0 + j][1][L] : 0u; O.z = lo ? sh.pt[r0 + j][2][L] : 0u;
+      gj4_add_gej(A, inf, O, sh.pinf[r0 + j] != 0u, row, k);
+    }
+    if (row == 0u) {
+      if (lo) { sh.pw[wave][0][L] = A.x; sh.pw[wave][1][L] = A.y; sh.pw[wave][2][L] = A.z; }
+      if (L == 0u) sh.pwinf[wave] = inf ? 1u : 0u;
+    }
+  }
+  __syncthreads();
+  if (wave != 0u) return;
+#pragma unroll 1
+  for (u32 j = 1; j < 4u; ++j) {
+    gjsl O;
+    O.x = lo ? sh.pw[j][0][L] : 0u; O.y = lo ? sh.pw[j][1][L] : 0u; O.z = lo ? sh.pw[j][2][L] : 0u;
+    gj4_add_gej(A, inf, O, sh.pwinf[j] != 0u, row, k);
+  }
+  const u32 fl = sh.oks[0];
+  bool okv = (fl & 1u) && kok && !inf;
+  u32 rw[8], X[8], T[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rw[i] = sh.r[0][i];
+  const u32 zz = fsl_sqr(A.z, k);
+  fsl_to_words(X, A.x);
+  fsl_to_words(T, fsl_mul(fsl_from_words(rw, k), zz, k));
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) eq &= (X[i] == T[i]);
+  if (!eq && (fl & 2u)) {
+    u32 rn[8], c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rn[i] = __builtin_addc(rw[i], kN[i], c, &c);
+    fsl_to_words(T, fsl_mul(fsl_from_words(rn, k), zz, k));
+    eq = true;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) eq &= (X[i] == T[i]);
+  }
+  okv &= eq;
+  if (threadIdx.x == 0) {
+    if (b.out8) b.out8[gi] = okv ? 1u : 0u;
+    else if (okv) atomicOr((unsigned long long*)&b.bits[gi >> 6], 1ull << (gi & 63u));
+  }
+}
+
 }  // namespace gv
 
 extern "C" hipError_t gvk_verify_lat16(const gvk_lat* b, hipStream_t st) {
@@ -1738,7 +1921,8 @@ extern "C" hipError_t gvk_verify_lat16_sl(const gvk_lat* b, hipStream_t st) {
     if (e != hipSuccess) return e;
   }
   if (b->ev[0]) (void)hipEventRecord(b->ev[0], st);
-  if (b->kn && b->gtab6) hipLaunchKernelGGL(gv::k_verify_lat16_kn, dim3(b->n), dim3(256), 0, st, *b);
+  if (b->kn == 2 && b->gtab6) hipLaunchKernelGGL(gv::k_verify_lat16_kw, dim3(b->n), dim3(256), 0, st, *b);
+  else if (b->kn && b->gtab6) hipLaunchKernelGGL(gv::k_verify_lat16_kn, dim3(b->n), dim3(256), 0, st, *b);
   else hipLaunchKernelGGL(gv::k_verify_lat16_sl, dim3(b->n), dim3(256), 0, st, *b);
   return hipGetLastError();
 }

@@ -662,6 +662,8 @@ struct gv_ctx {
   bool host_ladder_stream = false;  // host chunks' ladders on the set's low-priority ladder stream (chunk_ladder;
                                     // GV_HOST_LADDER_STREAM=1).  Measured off: async pinned 185 vs 157-167M/s,
                                     // sync pinned 158-160 vs 150-152M/s (profiles/r05/async_ab.jsonl)
+  bool lat_kw = true;           // keyed small batches on the wide arena's one-window tables (k_verify_lat16_kw)
+                                // when every slot has them, else the kn tables (GV_LAT_KW, "lat_kw")
   bool h2d_serial = true;       // host slices: a chunk's H2D waits for the previous chunk's, so concurrent
                                 // transfers do not share the link and delay the chunk the GPU needs first
                                 // (GV_H2D_SERIAL)
@@ -1094,7 +1096,13 @@ int launch(gv_ctx* ctx, Dev* d, Set* s, size_t n, const uint8_t* pub, const uint
     d->routes[kslot ? GV_ROUTE_LAT_KEYED : GV_ROUTE_LAT]++;
     if (kslot) {                                // keyed: 16 lanes per signature (group tables)
       lb.kqt2 = b.kqt2; lb.kzq2 = kzq2; lb.glat = d->glat;
-      if (sliced && !ka && ctx->keys_k6 && d->kqt6 && d->gtab6 && d->keys6 >= ctx->keys) {
+      if (sliced && !ka && ctx->keys_wide && ctx->lat_kw && d->kqtw && d->kw_ng == GV_KW_NG1 && d->gtab6 &&
+          d->keysw >= ctx->keys) {
+        // every slot has its one-window wide tables: k_verify_lat16_kw (no
+        // doublings; their own arena: Z rows of stride kcapw)
+        lb.kqt = d->kqtw; lb.kzq = d->kzqw; lb.kqt2 = d->kqtw2; lb.kzq2 = nullptr; lb.kC = (uint32_t)d->kcapw;
+        lb.gtab6 = d->gtab6; lb.kn = 2;
+      } else if (sliced && !ka && ctx->keys_k6 && d->kqt6 && d->gtab6 && d->keys6 >= ctx->keys) {
         // every slot has its kn tables: k_verify_lat16_kn (6 doublings, G from the 24-bit tables)
         lb.kqt = d->kqt6; lb.kzq = d->kzq6; lb.kqt2 = d->kqt62; lb.kzq2 = nullptr;
         lb.gtab6 = d->gtab6; lb.kn = 1;
@@ -1980,6 +1988,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* is = getenv("GV_INV_SMALL")) ctx->inv_small = strcmp(is, "0") != 0;
   if (const char* gi = getenv("GV_GFULL_ITEM")) ctx->gfull_item = strcmp(gi, "0") != 0;
   if (const char* hs = getenv("GV_H2D_SERIAL")) ctx->h2d_serial = strcmp(hs, "0") != 0;
+  if (const char* lk = getenv("GV_LAT_KW")) ctx->lat_kw = strcmp(lk, "0") != 0;
   if (const char* kk = getenv("GV_KEYS_K6")) ctx->keys_k6 = strcmp(kk, "0") != 0;
   if (const char* kk = getenv("GV_KEYS_WIDE")) {
     const int v = atoi(kk);
@@ -2845,6 +2854,7 @@ int gv_get_option(gv_ctx* ctx, const char* key, long long* val) {
               {"async_chunk", (long long)ctx->async_chunk},
               {"async_growth", ctx->async_growth},
               {"async_whole", ctx->async_whole},
+              {"lat_kw", ctx->lat_kw},
               {"kw_qw", GV_KW_QW}};                  // read-only: the wide arena's window width (build)
   for (const auto& o : opts)
     if (!strcmp(key, o.k)) {
@@ -2982,6 +2992,9 @@ int gv_set_option(gv_ctx* ctx, const char* key, long long val) {
   } else if (!strcmp(key, "async_chunk")) {
     if (val < 256 || (unsigned long long)val > kMaxItems) return GV_EINVAL;
     ctx->async_chunk = round_up((size_t)val, 256);
+  } else if (!strcmp(key, "lat_kw")) {
+    if (val != 0 && val != 1) return GV_EINVAL;
+    ctx->lat_kw = val != 0;
   } else if (!strcmp(key, "async_whole")) {
     if (val != 0 && val != 1) return GV_EINVAL;
     ctx->async_whole = val != 0;

@@ -244,6 +244,10 @@ int gv_verify_ed25519_msgs_keyed(gv_ctx* ctx, size_t n, const uint32_t* slot, co
  * "stage_pieces" (pageable host chunks of at least 65,536 items are staged
  * into pinned memory in this many pieces, each piece's H2D right behind its
  * copy; default 2, env GV_STAGE_PIECES),
+ * "lat_kw" (0/1: keyed sliced small batches whose slots all have the
+ * resident arena's one-window wide tables take k_verify_lat16_kw -- no
+ * doublings -- instead of the kn tables' k_verify_lat16_kn; default 1, env
+ * GV_LAT_KW),
  * "async_chunk" / "async_growth" (submitted batches staged through the
  * library -- pageable buffers, messages: fixed chunks of async_chunk items,
  * each later one at most async_growth times the one before; default 262144

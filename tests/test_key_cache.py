@@ -20,21 +20,25 @@ def ver():
     v.close()
 
 
-# (lat_max, sliced, keys_k6, keys_wide): the PATHS schedules (rows: pub33 only)
-# with the resident arena's kn tables (throughput: the wide-window tables), plus the
-# sliced kernel on the k4 tables and the throughput ladder on the k6 tables
-KEYED_PATHS = {**{p: (v[0], v[1], 1, 2) for p, v in PATHS.items() if p != "latency_rows"},
-               "latency_k4_arena": (1 << 30, 1, 0, 0), "throughput_k6_arena": (0, 1, 1, 0),
-               "throughput_wide_two": (0, 1, 1, 1)}
+# (lat_max, sliced, keys_k6, keys_wide, lat_kw): the PATHS schedules (rows: pub33
+# only) with the resident arena's wide-window tables (small batches:
+# k_verify_lat16_kw), plus the sliced kernel on the kn tables (lat_kw 0) and on
+# the k4 tables, and the throughput ladders on the k6 tables and the two-window layout
+KEYED_PATHS = {**{p: (v[0], v[1], 1, 2, 1) for p, v in PATHS.items() if p != "latency_rows"},
+               "latency_kn_arena": (1 << 30, 1, 1, 2, 0),
+               "latency_k4_arena": (1 << 30, 1, 0, 0, 1), "throughput_k6_arena": (0, 1, 1, 0, 1),
+               "throughput_wide_two": (0, 1, 1, 1, 1)}
 
 
 @pytest.fixture(params=sorted(KEYED_PATHS))
 def path(request, ver):
     """Keyed batches take the fused small-batch kernel up to lat_max
-    (k_verify_lat16_kn on the arena's kn tables, k_verify_lat16_sl on its k4
-    tables with keys_k6 0, or k_verify_lat16 with lat_sliced 0), the
+    (k_verify_lat16_kw on the arena's one-window wide tables,
+    k_verify_lat16_kn on its kn tables with lat_kw 0, k_verify_lat16_sl on its
+    k4 tables with keys_k6 0, or k_verify_lat16 with lat_sliced 0), the
     throughput pipeline above it: every schedule is checked."""
-    lat_max, sliced, keys_k6, keys_wide = KEYED_PATHS[request.param]
+    lat_max, sliced, keys_k6, keys_wide, lat_kw = KEYED_PATHS[request.param]
+    ver.set_option("lat_kw", lat_kw)
     ver.set_option("lat_max", lat_max)
     ver.set_option("lat_sliced", sliced)
     ver.set_option("lat_sl_max", 1 << 30)
@@ -45,6 +49,7 @@ def path(request, ver):
     ver.set_option("lat_sliced", 1)
     ver.set_option("keys_k6", 1)
     ver.set_option("keys_wide", 2)
+    ver.set_option("lat_kw", 1)
 
 
 def keyed_inputs(ver, pub):
