@@ -41,9 +41,10 @@ class Lanes {
  public:
   using SliceT = Slice<Batch>;
   // run(k): device k's lane body, called by device k's lane thread whenever
-  // its queue holds a slice.  It takes slices with pop(k, ..) until that
-  // returns false and reports each one with finish(); it returns once every
-  // slice it popped is finished.
+  // its queue holds a slice.  It takes slices with pop(k, ..) -- until that
+  // returns false, or fewer if it chooses (it is called again while the
+  // queue holds slices) -- and reports each one with finish(); it returns
+  // once every slice it popped is finished.
   Lanes(size_t ndev, std::function<void(size_t)> run) : q_(ndev), run_(std::move(run)) {
     for (size_t k = 0; k < ndev; ++k) lanes_.emplace_back([this, k] { lane(k); });
   }

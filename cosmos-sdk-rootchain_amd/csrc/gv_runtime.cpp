@@ -662,6 +662,8 @@ struct gv_ctx {
   bool host_ladder_stream = false;  // host chunks' ladders on the set's low-priority ladder stream (chunk_ladder;
                                     // GV_HOST_LADDER_STREAM=1).  Measured off: async pinned 185 vs 157-167M/s,
                                     // sync pinned 158-160 vs 150-152M/s (profiles/r05/async_ab.jsonl)
+  size_t lane_burst = 16;       // submitted batches: slices an async lane runs before it drains and releases the
+                                // device lock (GV_LANE_BURST)
   bool lat_kw = true;           // keyed small batches on the wide arena's one-window tables (k_verify_lat16_kw)
                                 // when every slot has them, else the kn tables (GV_LAT_KW, "lat_kw")
   bool h2d_serial = true;       // host slices: a chunk's H2D waits for the previous chunk's, so concurrent
@@ -1758,8 +1760,8 @@ void finish_slice(AsyncState* as, ActiveSlice& a) {
   as->finish(a.sl, a.rc);
 }
 
-// Runs device k's queued slices (d->mu held) until the queue is empty, then
-// drains.
+// Runs device k's queued slices (d->mu held) until the queue is empty or
+// lane_burst slices have run, then drains.
 void lane_stream(gv_ctx* ctx, AsyncState* as, size_t k, Dev* d) {
   std::list<ActiveSlice> act;
   ActiveSlice* owner[2] = {nullptr, nullptr};
@@ -1783,9 +1785,12 @@ void lane_stream(gv_ctx* ctx, AsyncState* as, size_t k, Dev* d) {
     harvest_set(sk);
     harvest_set(sk ^ 1);
   };
-  for (;;) {
+  for (size_t taken = 0;; ++taken) {
     AsyncSlice sl;
-    if (!as->pop(k, sl)) break;
+    // after lane_burst slices the lane drains and lets go of d->mu (the
+    // Lanes loop calls it again while the queue holds slices): a caller that
+    // keeps the queue full cannot starve synchronous calls on this device
+    if (taken >= ctx->lane_burst || !as->pop(k, sl)) break;
     const bool behind = !act.empty();             // an earlier slice's chunks still in flight
     act.emplace_back();
     ActiveSlice& a = act.back();
@@ -1989,6 +1994,7 @@ int gv_open(const int* dev_ids, int n_dev, gv_ctx** out) {
   if (const char* gi = getenv("GV_GFULL_ITEM")) ctx->gfull_item = strcmp(gi, "0") != 0;
   if (const char* hs = getenv("GV_H2D_SERIAL")) ctx->h2d_serial = strcmp(hs, "0") != 0;
   if (const char* lk = getenv("GV_LAT_KW")) ctx->lat_kw = strcmp(lk, "0") != 0;
+  if (const char* lb = getenv("GV_LANE_BURST")) ctx->lane_burst = (size_t)std::max(1, atoi(lb));
   if (const char* kk = getenv("GV_KEYS_K6")) ctx->keys_k6 = strcmp(kk, "0") != 0;
   if (const char* kk = getenv("GV_KEYS_WIDE")) {
     const int v = atoi(kk);
